@@ -1,0 +1,94 @@
+"""In-tree build driver for the native engine (hipcc for gfx950 + torch CppExtension).
+
+The built extension lands at cylon_amd/_C*.so so that it travels with the repo
+snapshot to the GPU box (no JIT cache under ~/.cache).
+"""
+import glob
+import hashlib
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+KERNELS = os.path.join(CSRC, "cylon", "kernels")
+OBJ_DIR = os.path.join(ROOT, "build", "hip_objs")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ROCM_INCLUDE = os.path.join(ROCM, "include")
+ROCM_LIB = os.path.join(ROCM, "lib")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+OFFLOAD_ARCH = os.environ.get("CYLON_OFFLOAD_ARCH", "gfx950")
+
+HIP_FLAGS = [
+    f"--offload-arch={OFFLOAD_ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-munsafe-fp-atomics",
+    "-Wno-unused-result",
+]
+
+
+def hip_sources():
+    return sorted(glob.glob(os.path.join(KERNELS, "*.hip")))
+
+
+def cpp_sources():
+    srcs = [os.path.join(CSRC, "bindings.cpp"), os.path.join(CSRC, "bindings_ops.cpp")]
+    for sub in ("cylon", "cylon/net", "cylon/ops", "cylon/ctx", "cylon/io", "cylon/kernels"):
+        srcs += sorted(glob.glob(os.path.join(CSRC, sub, "*.cpp")))
+    return [os.path.relpath(s, ROOT) for s in srcs]
+
+
+def _headers_digest():
+    h = hashlib.sha1()
+    for p in sorted(glob.glob(os.path.join(CSRC, "**", "*.hpp"), recursive=True) +
+                    glob.glob(os.path.join(CSRC, "**", "*.inc"), recursive=True)):
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _compile_one(src, digest):
+    name = os.path.splitext(os.path.basename(src))[0]
+    obj = os.path.join(OBJ_DIR, name + ".o")
+    stamp = obj + ".stamp"
+    with open(src, "rb") as f:
+        key = hashlib.sha1(f.read() + digest.encode() + " ".join(HIP_FLAGS).encode()).hexdigest()
+    if os.path.exists(obj) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == key:
+                return obj
+    cmd = [HIPCC] + HIP_FLAGS + ["-I", CSRC, "-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
+    with open(stamp, "w") as f:
+        f.write(key)
+    return obj
+
+
+def compile_hip_objects(jobs=None):
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    digest = _headers_digest()
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        return list(ex.map(lambda s: _compile_one(s, digest), hip_sources()))
+
+
+def build(verbose=False):
+    """Compile every HIP kernel for gfx950 and the extension, in-tree."""
+    env = dict(os.environ)
+    env.setdefault("MAX_JOBS", str(min(8, os.cpu_count() or 4)))
+    env.setdefault("PYTORCH_ROCM_ARCH", OFFLOAD_ARCH)
+    cmd = [sys.executable, "setup.py", "build_ext", "--inplace"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=not verbose, text=True)
+    if r.returncode != 0:
+        out = (r.stdout or "")[-4000:] + (r.stderr or "")[-8000:]
+        raise RuntimeError(f"native build failed:\n{out}")
+
+
+if __name__ == "__main__":
+    build(verbose=True)

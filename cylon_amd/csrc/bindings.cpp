@@ -1,0 +1,208 @@
+// Python binding of the native engine (module cylon_amd._C).
+// Reference: python/pycylon/*.pyx (Cython binding of libcylon) and
+// python/pycylon/api/lib.pyx (C-API wrap/unwrap).  Here pybind11 over the
+// C++ core; the pandas-like frontends (Table, DataFrame) are Python on top.
+#include <torch/extension.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+#include <torch/csrc/utils/pybind.h>
+
+#include "cylon/ctx/cylon_context.hpp"
+#include "cylon/net/communicator.hpp"
+#include "cylon/ops/api_ext.hpp"
+#include "cylon/table.hpp"
+
+namespace py = pybind11;
+using namespace cylon;
+
+namespace {
+
+at::Device parse_device(const std::string &s) { return at::Device(s); }
+
+join::config::JoinType parse_join_type(const std::string &t) {
+  if (t == "inner") return join::config::INNER;
+  if (t == "left") return join::config::LEFT;
+  if (t == "right") return join::config::RIGHT;
+  if (t == "outer" || t == "full_outer" || t == "fullouter") return join::config::FULL_OUTER;
+  CYLON_THROW(Code::Invalid, "unsupported join type '" << t << "'");
+}
+
+join::config::JoinAlgorithm parse_join_algo(const std::string &a) {
+  if (a == "hash") return join::config::HASH;
+  if (a == "sort") return join::config::SORT;
+  CYLON_THROW(Code::Invalid, "unsupported join algorithm '" << a << "'");
+}
+
+join::config::JoinConfig make_jc(const std::string &type, const std::string &algo, const std::vector<int> &l,
+                                 const std::vector<int> &r, const std::string &lp, const std::string &rp) {
+  return join::config::JoinConfig(parse_join_type(type), l, r, parse_join_algo(algo), lp, rp);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "cylon_amd native engine: MI355X HIP kernels + RCCL shuffle";
+
+  static py::exception<CylonError> exc(m, "CylonError", PyExc_RuntimeError);
+  py::register_exception_translator([](std::exception_ptr p) {
+    try {
+      if (p) std::rethrow_exception(p);
+    } catch (const CylonError &e) {
+      PyErr_SetObject(exc.ptr(), Py_BuildValue("(si)", e.what(), e.code()));
+    }
+  });
+
+  py::enum_<Type>(m, "Type")
+      .value("BOOL", Type::BOOL).value("UINT8", Type::UINT8).value("INT8", Type::INT8)
+      .value("UINT16", Type::UINT16).value("INT16", Type::INT16).value("UINT32", Type::UINT32)
+      .value("INT32", Type::INT32).value("UINT64", Type::UINT64).value("INT64", Type::INT64)
+      .value("HALF_FLOAT", Type::HALF_FLOAT).value("FLOAT", Type::FLOAT).value("DOUBLE", Type::DOUBLE)
+      .value("STRING", Type::STRING).value("BINARY", Type::BINARY)
+      .value("FIXED_SIZE_BINARY", Type::FIXED_SIZE_BINARY).value("DATE32", Type::DATE32)
+      .value("DATE64", Type::DATE64).value("TIMESTAMP", Type::TIMESTAMP).value("TIME32", Type::TIME32)
+      .value("TIME64", Type::TIME64).value("INTERVAL", Type::INTERVAL).value("DECIMAL", Type::DECIMAL)
+      .value("LIST", Type::LIST).value("EXTENSION", Type::EXTENSION)
+      .value("FIXED_SIZE_LIST", Type::FIXED_SIZE_LIST).value("DURATION", Type::DURATION);
+
+  py::enum_<Layout>(m, "Layout").value("FIXED_WIDTH", Layout::FIXED_WIDTH).value("VARIABLE_WIDTH", Layout::VARIABLE_WIDTH);
+
+  py::class_<DataType>(m, "DataType")
+      .def(py::init<>())
+      .def(py::init<Type>())
+      .def(py::init<Type, int32_t>())
+      .def_readwrite("type", &DataType::type)
+      .def_readwrite("byte_width", &DataType::byte_width)
+      .def_property("unit", [](const DataType &d) { return static_cast<int>(d.unit); },
+                    [](DataType &d, int u) { d.unit = static_cast<TimeUnit>(u); })
+      .def_readwrite("timezone", &DataType::timezone)
+      .def("width", &DataType::width)
+      .def("layout", &DataType::layout)
+      .def("is_numeric", &DataType::is_numeric)
+      .def("__eq__", [](const DataType &a, const DataType &b) { return a == b; })
+      .def("__repr__", &DataType::ToString)
+      .def("__str__", &DataType::ToString);
+
+  py::class_<Column>(m, "Column")
+      .def(py::init([](const std::string &name, const DataType &t, int64_t length, at::Tensor data,
+                       c10::optional<at::Tensor> offsets, c10::optional<at::Tensor> validity) {
+             return Column(name, t, length, data, offsets ? *offsets : at::Tensor(), validity ? *validity : at::Tensor());
+           }),
+           py::arg("name"), py::arg("type"), py::arg("length"), py::arg("data"), py::arg("offsets") = py::none(),
+           py::arg("validity") = py::none())
+      .def_readwrite("name", &Column::name)
+      .def_readonly("type", &Column::type)
+      .def_readonly("length", &Column::length)
+      .def_property_readonly("data", [](const Column &c) { return c.data; })
+      .def_property_readonly("offsets", [](const Column &c) -> py::object {
+        return c.offsets.defined() ? py::cast(c.offsets) : py::none();
+      })
+      .def_property_readonly("validity", [](const Column &c) -> py::object {
+        return c.validity.defined() ? py::cast(c.validity) : py::none();
+      })
+      .def("null_count", &Column::null_count)
+      .def("nbytes", &Column::nbytes)
+      .def("to", [](const Column &c, const std::string &d) { return c.to(parse_device(d)); })
+      .def("slice", &Column::slice)
+      .def("with_name", &Column::with_name);
+
+  py::enum_<net::CommType>(m, "CommType")
+      .value("LOCAL", net::CommType::LOCAL).value("MPI", net::CommType::MPI).value("TCP", net::CommType::TCP)
+      .value("UCX", net::CommType::UCX).value("RCCL", net::CommType::RCCL).value("GLOO", net::CommType::GLOO);
+
+  py::class_<CylonContext, std::shared_ptr<CylonContext>>(m, "Context")
+      .def_static("init_local", [](const std::string &dev) { return CylonContext::Init(parse_device(dev)); },
+                  py::arg("device") = "cpu")
+      .def_static("init_distributed",
+                  [](c10::intrusive_ptr<c10d::ProcessGroup> pg, const std::string &backend, const std::string &dev) {
+                    const auto ct = backend == "nccl" || backend == "rccl" ? net::CommType::RCCL : net::CommType::GLOO;
+                    const at::Device device = parse_device(dev);
+                    const at::Device comm_device = ct == net::CommType::RCCL ? device : at::Device(at::kCPU);
+                    auto comm = std::make_shared<net::ProcessGroupCommunicator>(pg, ct, comm_device);
+                    return CylonContext::InitDistributed(comm, device);
+                  })
+      .def("get_rank", &CylonContext::GetRank)
+      .def("get_world_size", &CylonContext::GetWorldSize)
+      .def("get_neighbours", &CylonContext::GetNeighbours)
+      .def("get_next_sequence", &CylonContext::GetNextSequence)
+      .def("is_distributed", &CylonContext::IsDistributed)
+      .def("get_comm_type", &CylonContext::GetCommType)
+      .def("barrier", &CylonContext::Barrier, py::call_guard<py::gil_scoped_release>())
+      .def("finalize", &CylonContext::Finalize)
+      .def("add_config", &CylonContext::AddConfig)
+      .def("get_config", &CylonContext::GetConfig, py::arg("key"), py::arg("default") = "")
+      .def("get_configs", &CylonContext::GetConfigs)
+      .def("device", [](const CylonContext &c) { return c.GetDevice().str(); })
+      .def("bytes_allocated", &CylonContext::BytesAllocated)
+      .def("max_memory", &CylonContext::MaxMemory)
+      .def("allreduce", [](CylonContext &c, at::Tensor t, int op) {
+        c.GetCommunicator()->AllReduce(t, static_cast<net::ReduceOp>(op));
+        return t;
+      })
+      .def("allgather", [](CylonContext &c, at::Tensor t) { return c.GetCommunicator()->AllGather(t); })
+      .def("allgatherv", [](CylonContext &c, at::Tensor t) { return c.GetCommunicator()->AllGatherV(t); })
+      .def("broadcast", [](CylonContext &c, at::Tensor t, int root) {
+        c.GetCommunicator()->Broadcast(t, root);
+        return t;
+      })
+      .def("alltoallv", [](CylonContext &c, at::Tensor t, std::vector<int64_t> sc) {
+        auto comm = c.GetCommunicator();
+        auto rc = comm->ExchangeCounts(sc);
+        return comm->AllToAllV(t, sc, rc);
+      });
+
+  py::class_<Table, std::shared_ptr<Table>>(m, "Table")
+      .def(py::init([](std::shared_ptr<CylonContext> ctx, std::vector<Column> cols) {
+        return std::make_shared<Table>(std::move(ctx), std::move(cols));
+      }))
+      .def("rows", &Table::Rows)
+      .def("num_columns", &Table::Columns)
+      .def("column_names", &Table::ColumnNames)
+      .def("column", &Table::column)
+      .def("columns", &Table::columns)
+      .def("column_index", &Table::ColumnIndex)
+      .def("context", &Table::GetContext)
+      .def("device", [](const Table &t) { return t.device().str(); })
+      .def("retain_memory", &Table::retainMemory)
+      .def("is_retain", &Table::IsRetain)
+      .def("clear", &Table::Clear)
+      .def("nbytes", &Table::nbytes)
+      .def("to", [](const Table &t, const std::string &d) { return t.to(parse_device(d)); });
+
+  // ---- operators (GIL released: kernels + collectives) -----------------------
+  auto rel = py::call_guard<py::gil_scoped_release>();
+  m.def("gather", &ops::Gather, rel);
+  m.def("gather_nullable", &ops::GatherNullable, rel);
+  m.def("project", &ops::Project, rel);
+  m.def("merge", &ops::Merge, rel);
+  m.def("slice", &ops::Slice, rel);
+  m.def("filter_by_mask", &ops::FilterByMask, rel);
+  m.def("mask_to_indices", &ops::MaskToIndices, py::arg("mask"), py::arg("invert") = false, rel);
+  m.def("map_to_hash_partitions", &ops::MapToHashPartitions, rel);
+  m.def("split", &ops::Split, rel);
+  m.def("hash_partition", &ops::HashPartition, rel);
+  m.def("shuffle", &ops::Shuffle, rel);
+  m.def("sort_indices", &ops::SortIndices, rel);
+  m.def("sort", &ops::Sort, rel);
+  m.def(
+      "join",
+      [](const TablePtr &l, const TablePtr &r, const std::string &type, const std::string &algo,
+         const std::vector<int> &lc, const std::vector<int> &rc, const std::string &lp, const std::string &rp) {
+        return ops::Join(l, r, make_jc(type, algo, lc, rc, lp, rp));
+      },
+      rel);
+  m.def(
+      "distributed_join",
+      [](const TablePtr &l, const TablePtr &r, const std::string &type, const std::string &algo,
+         const std::vector<int> &lc, const std::vector<int> &rc, const std::string &lp, const std::string &rp) {
+        return ops::DistributedJoin(l, r, make_jc(type, algo, lc, rc, lp, rp));
+      },
+      rel);
+  m.def(
+      "join_indices",
+      [](const TablePtr &l, const TablePtr &r, const std::string &type, const std::string &algo,
+         const std::vector<int> &lc, const std::vector<int> &rc) {
+        return ops::JoinIndices(l, r, make_jc(type, algo, lc, rc, "", ""));
+      },
+      rel);
+
+  register_extended_ops(m);
+}

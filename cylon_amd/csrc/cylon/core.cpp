@@ -1,0 +1,260 @@
+// L0/L2 core objects: DataType, Column, Table, CylonContext.
+// Reference: cpp/src/cylon/data_types.hpp, column.cpp, table.cpp:1-61 (ctor),
+// ctx/cylon_context.cpp:25-108.
+#include <c10/hip/HIPCachingAllocator.h>
+
+#include "column.hpp"
+#include "ctx/cylon_context.hpp"
+#include "table.hpp"
+
+namespace cylon {
+
+// ---------------------------------------------------------------------------
+// DataType
+// ---------------------------------------------------------------------------
+const char *TypeName(Type t) {
+  switch (t) {
+    case Type::BOOL: return "bool";
+    case Type::UINT8: return "uint8";
+    case Type::INT8: return "int8";
+    case Type::UINT16: return "uint16";
+    case Type::INT16: return "int16";
+    case Type::UINT32: return "uint32";
+    case Type::INT32: return "int32";
+    case Type::UINT64: return "uint64";
+    case Type::INT64: return "int64";
+    case Type::HALF_FLOAT: return "halffloat";
+    case Type::FLOAT: return "float";
+    case Type::DOUBLE: return "double";
+    case Type::STRING: return "string";
+    case Type::BINARY: return "binary";
+    case Type::FIXED_SIZE_BINARY: return "fixed_size_binary";
+    case Type::DATE32: return "date32";
+    case Type::DATE64: return "date64";
+    case Type::TIMESTAMP: return "timestamp";
+    case Type::TIME32: return "time32";
+    case Type::TIME64: return "time64";
+    case Type::INTERVAL: return "interval";
+    case Type::DECIMAL: return "decimal";
+    case Type::LIST: return "list";
+    case Type::EXTENSION: return "extension";
+    case Type::FIXED_SIZE_LIST: return "fixed_size_list";
+    case Type::DURATION: return "duration";
+  }
+  return "unknown";
+}
+
+std::string DataType::ToString() const {
+  std::string s = TypeName(type);
+  if (type == Type::FIXED_SIZE_BINARY || type == Type::DECIMAL) s += "[" + std::to_string(byte_width) + "]";
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// Column
+// ---------------------------------------------------------------------------
+at::ScalarType storage_dtype(const DataType &t) {
+  switch (t.type) {
+    case Type::BOOL:
+    case Type::UINT8: return at::kByte;
+    case Type::INT8: return at::kChar;
+    case Type::UINT16: return at::kUInt16;
+    case Type::INT16: return at::kShort;
+    case Type::UINT32: return at::kUInt32;
+    case Type::INT32:
+    case Type::DATE32:
+    case Type::TIME32: return at::kInt;
+    case Type::UINT64: return at::kUInt64;
+    case Type::INT64:
+    case Type::DATE64:
+    case Type::TIMESTAMP:
+    case Type::TIME64:
+    case Type::DURATION: return at::kLong;
+    case Type::HALF_FLOAT: return at::kHalf;
+    case Type::FLOAT: return at::kFloat;
+    case Type::DOUBLE: return at::kDouble;
+    case Type::FIXED_SIZE_BINARY:
+    case Type::DECIMAL:
+    case Type::STRING:
+    case Type::BINARY: return at::kByte;
+    default: CYLON_THROW(Code::NotImplemented, "no storage for type " << t.ToString());
+  }
+}
+
+Column make_fixed_column(const std::string &name, const DataType &t, int64_t n, at::Device dev, bool nullable) {
+  CYLON_CHECK(!t.is_variable_width(), Code::Invalid, "make_fixed_column on var width type");
+  const int64_t elems = (t.kind() == ValueKind::FIXED_BYTES) ? n * t.width() : n;
+  at::Tensor d = at::empty({elems}, at::TensorOptions().dtype(storage_dtype(t)).device(dev));
+  at::Tensor v;
+  if (nullable) v = at::empty({n}, at::TensorOptions().dtype(at::kByte).device(dev));
+  return Column(name, t, n, d, at::Tensor(), v);
+}
+
+int64_t Column::null_count() const {
+  if (!validity.defined() || length == 0) return 0;
+  return length - validity.sum().item<int64_t>();
+}
+
+int64_t Column::nbytes() const {
+  int64_t b = 0;
+  if (data.defined()) b += data.numel() * data.element_size();
+  if (offsets.defined()) b += offsets.numel() * offsets.element_size();
+  if (validity.defined()) b += validity.numel();
+  return b;
+}
+
+Column Column::to(at::Device dev, bool non_blocking) const {
+  Column c = *this;
+  if (data.defined()) c.data = data.to(dev, non_blocking);
+  if (offsets.defined()) c.offsets = offsets.to(dev, non_blocking);
+  if (validity.defined()) c.validity = validity.to(dev, non_blocking);
+  return c;
+}
+
+Column Column::slice(int64_t offset, int64_t len) const {
+  CYLON_CHECK(offset >= 0 && len >= 0 && offset + len <= length, Code::IndexError,
+              "slice [" << offset << ", " << offset + len << ") out of range for column of " << length);
+  Column c = *this;
+  c.length = len;
+  if (is_var()) {
+    at::Tensor off = offsets.slice(0, offset, offset + len + 1);
+    const int64_t b = off[0].item<int64_t>();
+    const int64_t e = off[len].item<int64_t>();
+    c.offsets = off - b;
+    c.data = data.slice(0, b, e);
+  } else if (type.kind() == ValueKind::FIXED_BYTES) {
+    c.data = data.slice(0, offset * type.width(), (offset + len) * type.width());
+  } else {
+    c.data = data.slice(0, offset, offset + len);
+  }
+  if (validity.defined()) c.validity = validity.slice(0, offset, offset + len);
+  return c;
+}
+
+// ---------------------------------------------------------------------------
+// Table
+// ---------------------------------------------------------------------------
+Table::Table(std::shared_ptr<CylonContext> ctx, std::vector<Column> columns)
+    : ctx_(std::move(ctx)), columns_(std::move(columns)) {
+  rows_ = columns_.empty() ? 0 : columns_[0].length;
+  for (const auto &c : columns_)
+    CYLON_CHECK(c.length == rows_, Code::Invalid,
+                "column '" << c.name << "' has " << c.length << " rows, expected " << rows_);
+}
+
+std::vector<std::string> Table::ColumnNames() const {
+  std::vector<std::string> names;
+  names.reserve(columns_.size());
+  for (const auto &c : columns_) names.push_back(c.name);
+  return names;
+}
+
+const Column &Table::column(int i) const {
+  CYLON_CHECK(i >= 0 && i < Columns(), Code::IndexError, "column index " << i << " out of range [0, " << Columns() << ")");
+  return columns_[i];
+}
+
+int Table::ColumnIndex(const std::string &name) const {
+  for (size_t i = 0; i < columns_.size(); ++i)
+    if (columns_[i].name == name) return static_cast<int>(i);
+  return -1;
+}
+
+at::Device Table::device() const {
+  if (!columns_.empty() && columns_[0].data.defined()) return columns_[0].device();
+  return ctx_ ? ctx_->GetDevice() : at::Device(at::kCPU);
+}
+
+int64_t Table::nbytes() const {
+  int64_t b = 0;
+  for (const auto &c : columns_) b += c.nbytes();
+  return b;
+}
+
+TablePtr Table::to(at::Device dev) const {
+  std::vector<Column> cols;
+  cols.reserve(columns_.size());
+  for (const auto &c : columns_) cols.push_back(c.to(dev));
+  auto t = Table::Make(ctx_, std::move(cols));
+  t->retainMemory(retain_);
+  return t;
+}
+
+// ---------------------------------------------------------------------------
+// CylonContext
+// ---------------------------------------------------------------------------
+CylonContext::CylonContext(bool distributed) : distributed_(distributed) {}
+
+std::shared_ptr<CylonContext> CylonContext::Init(at::Device device) {
+  auto ctx = std::make_shared<CylonContext>(false);
+  ctx->communicator_ = std::make_shared<net::LocalCommunicator>();
+  ctx->device_ = device;
+  return ctx;
+}
+
+std::shared_ptr<CylonContext> CylonContext::InitDistributed(std::shared_ptr<net::Communicator> comm,
+                                                            at::Device device) {
+  CYLON_CHECK(comm != nullptr, Code::Invalid, "InitDistributed needs a communicator");
+  auto ctx = std::make_shared<CylonContext>(true);
+  ctx->communicator_ = std::move(comm);
+  ctx->device_ = device;
+  return ctx;
+}
+
+void CylonContext::Finalize() {
+  if (communicator_) communicator_->Finalize();
+}
+
+void CylonContext::AddConfig(const std::string &key, const std::string &value) {
+  std::lock_guard<std::mutex> lk(mu_);
+  config_[key] = value;
+}
+
+std::string CylonContext::GetConfig(const std::string &key, const std::string &def) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = config_.find(key);
+  return it == config_.end() ? def : it->second;
+}
+
+std::shared_ptr<net::Communicator> CylonContext::GetCommunicator() const {
+  CYLON_CHECK(communicator_ != nullptr, Code::Invalid, "context has no communicator");
+  return communicator_;
+}
+
+int CylonContext::GetRank() const { return distributed_ ? communicator_->GetRank() : 0; }
+int CylonContext::GetWorldSize() const { return distributed_ ? communicator_->GetWorldSize() : 1; }
+
+std::vector<int> CylonContext::GetNeighbours(bool include_self) const {
+  std::vector<int> n;
+  const int w = GetWorldSize(), r = GetRank();
+  for (int i = 0; i < w; ++i)
+    if (i != r || include_self) n.push_back(i);
+  return n;
+}
+
+int CylonContext::GetNextSequence() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return sequence_no_++;
+}
+
+net::CommType CylonContext::GetCommType() const {
+  return communicator_ ? communicator_->GetCommType() : net::CommType::LOCAL;
+}
+
+void CylonContext::Barrier() {
+  if (communicator_) communicator_->Barrier();
+}
+
+int64_t CylonContext::BytesAllocated() const {
+  if (!device_.is_cuda()) return 0;
+  auto stats = c10::hip::HIPCachingAllocator::getDeviceStats(device_.index());
+  return stats.allocated_bytes[static_cast<size_t>(c10::CachingAllocator::StatType::AGGREGATE)].current;
+}
+
+int64_t CylonContext::MaxMemory() const {
+  if (!device_.is_cuda()) return 0;
+  auto stats = c10::hip::HIPCachingAllocator::getDeviceStats(device_.index());
+  return stats.allocated_bytes[static_cast<size_t>(c10::CachingAllocator::StatType::AGGREGATE)].peak;
+}
+
+}  // namespace cylon

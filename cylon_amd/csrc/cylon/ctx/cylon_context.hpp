@@ -1,0 +1,63 @@
+// L0 runtime context.
+//
+// Reference: cpp/src/cylon/ctx/cylon_context.hpp:29-146 (rank/world, config map,
+// communicator, memory pool, sequence numbers used as all-to-all edge tags).
+// Additions for MI355X: the context owns the device its tables live on
+// (cuda:<local_rank> under one-process-per-GPU) and exposes HBM pool stats from
+// the HIP caching allocator.
+#pragma once
+#include <ATen/ATen.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../net/communicator.hpp"
+
+namespace cylon {
+
+class CylonContext {
+ public:
+  explicit CylonContext(bool distributed);
+
+  // Local (rank 0 of 1) context on `device` (default: cpu).
+  static std::shared_ptr<CylonContext> Init(at::Device device = at::Device(at::kCPU));
+  static std::shared_ptr<CylonContext> InitDistributed(std::shared_ptr<net::Communicator> comm, at::Device device);
+
+  void Finalize();
+  void AddConfig(const std::string &key, const std::string &value);
+  std::string GetConfig(const std::string &key, const std::string &def = "") const;
+  const std::map<std::string, std::string> &GetConfigs() const { return config_; }
+
+  std::shared_ptr<net::Communicator> GetCommunicator() const;
+  void setCommunicator(std::shared_ptr<net::Communicator> comm) { communicator_ = std::move(comm); }
+  void setDistributed(bool d) { distributed_ = d; }
+
+  int GetRank() const;
+  int GetWorldSize() const;
+  std::vector<int> GetNeighbours(bool include_self) const;
+  int GetNextSequence();
+  bool IsDistributed() const { return distributed_; }
+  net::CommType GetCommType() const;
+  void Barrier();
+
+  at::Device GetDevice() const { return device_; }
+  void SetDevice(at::Device d) { device_ = d; }
+  bool on_gpu() const { return device_.is_cuda(); }
+
+  // HBM pool statistics (bytes) from the HIP caching allocator; 0 on CPU.
+  int64_t BytesAllocated() const;
+  int64_t MaxMemory() const;
+
+ private:
+  bool distributed_;
+  int sequence_no_ = 0;
+  std::shared_ptr<net::Communicator> communicator_;
+  std::map<std::string, std::string> config_;
+  at::Device device_{at::kCPU};
+  mutable std::mutex mu_;
+};
+
+}  // namespace cylon

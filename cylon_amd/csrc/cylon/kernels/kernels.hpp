@@ -1,0 +1,73 @@
+// Kernel-layer API (L3): raw-pointer primitives with identical signatures for
+// the MI355X HIP implementation (namespace cylon::hip, *.hip files) and the CPU
+// twin (namespace cylon::cpu, cpu_kernels.cpp).  The operator layer (ops/*.cpp)
+// allocates every buffer through torch's stream-ordered caching allocator and
+// dispatches on the tensor's device; kernels never allocate.
+//
+// Kernel inventory:
+//   K1/K2 partition hash        -> row_partition_hash / hash_to_partition
+//   K3    split / scatter       -> partition_positions + scatter_columns / scatter_var
+//   K4    gather (-1 -> null)   -> gather_columns / gather_var
+//   K5    hash join             -> hash_build / hash_probe_count / hash_probe_write
+//   K6    radix sort            -> radix_sort_pairs (sort.hip)
+//   K7    sort-merge join       -> merge_join_count / merge_join_write
+//   K8/K9 group-by              -> groupby_* (groupby.hip)
+//   K10   distinct / set ops    -> distinct_first / hash_set_*
+//   K11   compaction            -> mask_to_indices
+//   K12   reductions            -> reduce_column
+//   K13   range partition       -> range_bins
+//   K15   elementwise           -> elementwise.hip
+#pragma once
+#include "../common.hpp"
+
+namespace cylon {
+
+// Read-only column view handed to kernels.
+struct ColView {
+  const uint8_t *data = nullptr;     // fixed width values or var-width bytes
+  const int64_t *offsets = nullptr;  // var width only (n + 1 entries)
+  const uint8_t *valid = nullptr;    // optional byte mask, 1 = valid
+  int32_t width = 0;                 // bytes per element, 0 for var width
+  int32_t kind = 0;                  // ValueKind
+};
+
+struct MutColView {
+  uint8_t *data = nullptr;
+  int64_t *offsets = nullptr;
+  uint8_t *valid = nullptr;
+  int32_t width = 0;
+  int32_t kind = 0;
+};
+
+// Hash-table slot for the join / group-by / distinct tables: 16 bytes, one
+// global_load_dwordx4 per probe step.
+struct alignas(16) HashSlot {
+  int64_t key;
+  int64_t row;  // -1 = empty
+};
+
+constexpr int kMaxFusedCols = 16;  // columns handled by one multi-column launch
+
+// Aggregation op ids, numerically identical to the reference
+// (cpp/src/cylon/compute/aggregate_kernels.hpp:40-50).
+enum AggOp : int {
+  AGG_SUM = 0,
+  AGG_MIN = 1,
+  AGG_MAX = 2,
+  AGG_COUNT = 3,
+  AGG_MEAN = 4,
+  AGG_VAR = 5,
+  AGG_NUNIQUE = 6,
+  AGG_QUANTILE = 7,
+  AGG_STDDEV = 8,
+};
+
+namespace hip {
+#include "kernel_decls.inc"
+}  // namespace hip
+
+namespace cpu {
+#include "kernel_decls.inc"
+}  // namespace cpu
+
+}  // namespace cylon

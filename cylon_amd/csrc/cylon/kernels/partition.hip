@@ -1,0 +1,315 @@
+// K1/K2 partition hashing and K3 stable radix-partition scatter (gfx950).
+//
+// Reference semantics: cpp/src/cylon/arrow/arrow_partition_kernels.cpp:67-305
+// (hash chain h = 31*h + f(v)), cpp/src/cylon/partition/partition.cpp:27-90
+// (split into per-partition tables, order preserved inside a partition).
+//
+// MI355X design:
+//   * row_partition_hash: one pass per key column over coalesced loads;
+//     the chain stays in a uint32 per row.
+//   * partition_positions: two kernels.  (1) per-block LDS histogram of pid;
+//     (2) an exclusive scan of the partition-major block histogram (scan.hip);
+//     (3) a stable rank kernel: inside a wave, lanes holding the same pid are
+//     found with ceil(log2 P) 64-bit ballots (wave64 match), giving the
+//     in-wave rank by one popcount; per-wave running counters live in LDS and
+//     the cross-wave prefix is formed once per 2048-row sub-tile.  The result
+//     is the destination of each row in partition-major order, so every
+//     partition (and therefore every peer's slice in the RCCL shuffle) is one
+//     contiguous range: no pack step before the all-to-all.
+//   * scatter_columns: all fixed-width columns of a table in one launch,
+//     destination read once per row.
+#include "stable_rank.hpp"
+
+namespace cylon {
+namespace hip {
+
+struct ColSet {
+  ColView c[kMaxFusedCols];
+};
+struct MutColSet {
+  MutColView c[kMaxFusedCols];
+};
+
+// ---------------------------------------------------------------------------
+// K1 / K2
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t partition_f(const ColView &c, int64_t i) {
+  if (c.valid != nullptr && c.valid[i] == 0) return 0u;
+  const int kind = c.kind;
+  if (kind == static_cast<int>(ValueKind::VAR_BYTES)) {
+    const int64_t b = c.offsets[i], e = c.offsets[i + 1];
+    return hashing::murmur3_32(c.data + b, e - b, 0u);
+  }
+  if (kind == static_cast<int>(ValueKind::FIXED_BYTES)) {
+    return hashing::murmur3_32(c.data + i * (int64_t)c.width, c.width, 0u);
+  }
+  const uint64_t bits = load_bits(c.data, i, c.width);
+  if (kind == static_cast<int>(ValueKind::FLOAT)) {
+    switch (c.width) {
+      case 2: return hashing::murmur3_32_u16((uint16_t)bits);
+      case 4: return hashing::murmur3_32_u32((uint32_t)bits);
+      default: return hashing::murmur3_32_u64(bits);
+    }
+  }
+  // ModuloPartitionKernel: static_cast<uint32_t>(value)
+  return (uint32_t)extend_bits(bits, c.width, kind);
+}
+
+__global__ void k_row_partition_hash(ColSet cols, int ncols, int64_t n, uint32_t *__restrict__ h) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint32_t acc = 0;
+    for (int c = 0; c < ncols; ++c) acc = 31u * acc + partition_f(cols.c[c], i);
+    h[i] = acc;
+  }
+}
+
+void row_partition_hash(const ColView *cols, int ncols, int64_t n, uint32_t *h, void *stream) {
+  if (n == 0) return;
+  CYLON_CHECK(ncols <= kMaxFusedCols, Code::Invalid, "too many key columns " << ncols);
+  ColSet s;
+  for (int c = 0; c < ncols; ++c) s.c[c] = cols[c];
+  hipLaunchKernelGGL(k_row_partition_hash, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), s,
+                     ncols, n, h);
+  HIP_LAUNCH_CHECK();
+}
+
+// pid + global histogram.  LDS histogram per block, one global atomic per
+// (block, partition).
+__global__ void k_hash_to_partition(const uint32_t *__restrict__ h, int64_t n, uint32_t nparts,
+                                    uint32_t *__restrict__ pid, unsigned long long *counts) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned int *hist = reinterpret_cast<unsigned int *>(smem);
+  const bool use_lds = nparts <= 8192;
+  if (use_lds)
+    for (uint32_t p = threadIdx.x; p < nparts; p += blockDim.x) hist[p] = 0;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t p = hashing::partitioner(h[i], nparts);
+    pid[i] = p;
+    if (use_lds)
+      atomicAdd(&hist[p], 1u);
+    else
+      atomicAdd(&counts[p], 1ull);
+  }
+  __syncthreads();
+  if (use_lds)
+    for (uint32_t p = threadIdx.x; p < nparts; p += blockDim.x)
+      if (hist[p]) atomicAdd(&counts[p], (unsigned long long)hist[p]);
+}
+
+void hash_to_partition(const uint32_t *h, int64_t n, uint32_t nparts, uint32_t *pid, int64_t *counts,
+                       void *stream) {
+  HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int64_t) * nparts, as_stream(stream)));
+  if (n == 0) return;
+  size_t lds = nparts <= 8192 ? nparts * sizeof(unsigned int) : 0;
+  hipLaunchKernelGGL(k_hash_to_partition, dim3(grid_for(n)), dim3(kBlock), lds, as_stream(stream), h,
+                     n, nparts, pid, reinterpret_cast<unsigned long long *>(counts));
+  HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------
+// K3: stable partition positions (stable_rank.hpp core, bucket = pid)
+// ---------------------------------------------------------------------------
+constexpr uint32_t kMaxPosParts = 4096;
+
+struct PidDigit {
+  const uint32_t *pid;
+  __device__ __forceinline__ uint32_t operator()(int64_t i) const { return pid[i]; }
+};
+struct PosSink {
+  int64_t *pos;
+  __device__ __forceinline__ void operator()(int64_t i, int64_t d) const { pos[i] = d; }
+};
+
+int64_t partition_positions_workspace(int64_t n, uint32_t nparts) { return stable_rank_workspace(n, nparts); }
+
+__global__ void k_counts_from_scan(const int64_t *bh_scan, int64_t nblocks, uint32_t nparts, int64_t *counts) {
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < nparts; p += gridDim.x * blockDim.x)
+    counts[p] = bh_scan[(int64_t)(p + 1) * nblocks] - bh_scan[(int64_t)p * nblocks];
+}
+
+void partition_positions(const uint32_t *pid, int64_t n, uint32_t nparts, int64_t *ws, int64_t *pos,
+                         int64_t *counts, void *stream) {
+  CYLON_CHECK(nparts >= 1 && nparts <= kMaxPosParts, Code::Invalid,
+              "partition_positions supports 1.." << kMaxPosParts << " partitions, got " << nparts);
+  hipStream_t s = as_stream(stream);
+  if (n == 0) {
+    HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int64_t) * nparts, s));
+    return;
+  }
+  int64_t *bh_scan = nullptr;
+  int64_t nblocks = 0;
+  stable_rank_launch(PidDigit{pid}, PosSink{pos}, n, nparts, ws, s, &bh_scan, &nblocks);
+  hipLaunchKernelGGL(k_counts_from_scan, dim3(grid_for(nparts)), dim3(kBlock), 0, s, (const int64_t *)bh_scan,
+                     nblocks, nparts, counts);
+  HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------
+// K3: scatter fixed-width columns (all columns of the table in one launch)
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void move_elem(const uint8_t *src, int64_t si, uint8_t *dst, int64_t di) {
+  reinterpret_cast<T *>(dst)[di] = reinterpret_cast<const T *>(src)[si];
+}
+
+__device__ __forceinline__ void move_any(const uint8_t *src, int64_t si, uint8_t *dst, int64_t di, int w) {
+  switch (w) {
+    case 1: move_elem<uint8_t>(src, si, dst, di); break;
+    case 2: move_elem<uint16_t>(src, si, dst, di); break;
+    case 4: move_elem<uint32_t>(src, si, dst, di); break;
+    case 8: move_elem<uint64_t>(src, si, dst, di); break;
+    case 16: move_elem<uint4>(src, si, dst, di); break;
+    default:
+      for (int b = 0; b < w; ++b) dst[di * w + b] = src[si * w + b];
+  }
+}
+
+__global__ void k_scatter_columns(ColSet in, MutColSet out, int ncols, const int64_t *__restrict__ pos,
+                                  int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t d = pos[i];
+    for (int c = 0; c < ncols; ++c) {
+      move_any(in.c[c].data, i, out.c[c].data, d, in.c[c].width);
+      if (out.c[c].valid) out.c[c].valid[d] = in.c[c].valid ? in.c[c].valid[i] : (uint8_t)1;
+    }
+  }
+}
+
+void scatter_columns(const ColView *in, const MutColView *out, int ncols, const int64_t *pos, int64_t n,
+                     void *stream) {
+  if (n == 0 || ncols == 0) return;
+  for (int c0 = 0; c0 < ncols; c0 += kMaxFusedCols) {
+    const int nc = (ncols - c0) < kMaxFusedCols ? (ncols - c0) : kMaxFusedCols;
+    ColSet a;
+    MutColSet b;
+    for (int c = 0; c < nc; ++c) {
+      a.c[c] = in[c0 + c];
+      b.c[c] = out[c0 + c];
+    }
+    hipLaunchKernelGGL(k_scatter_columns, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), a, b, nc,
+                       pos, n);
+    HIP_LAUNCH_CHECK();
+  }
+}
+
+__global__ void k_scatter_var_lengths(ColView in, const int64_t *__restrict__ pos, int64_t n,
+                                      int64_t *__restrict__ out_lens) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    out_lens[pos[i]] = in.offsets[i + 1] - in.offsets[i];
+}
+
+void scatter_var_lengths(const ColView &in, const int64_t *pos, int64_t n, int64_t *out_lens, void *stream) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_scatter_var_lengths, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), in, pos, n,
+                     out_lens);
+  HIP_LAUNCH_CHECK();
+}
+
+// one wave per row: lanes copy the string bytes cooperatively
+__global__ void k_scatter_var_bytes(ColView in, const int64_t *__restrict__ pos, int64_t n,
+                                    const int64_t *__restrict__ out_off, uint8_t *__restrict__ out_bytes,
+                                    uint8_t *__restrict__ out_valid) {
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
+  const int lane = lane_id();
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; i < n; i += waves) {
+    const int64_t d = pos[i];
+    const int64_t sb = in.offsets[i], len = in.offsets[i + 1] - sb;
+    const int64_t db = out_off[d];
+    for (int64_t k = lane; k < len; k += kWave) out_bytes[db + k] = in.data[sb + k];
+    if (lane == 0 && out_valid) out_valid[d] = in.valid ? in.valid[i] : (uint8_t)1;
+  }
+}
+
+void scatter_var_bytes(const ColView &in, const int64_t *pos, int64_t n, const int64_t *out_offsets,
+                       uint8_t *out_bytes, uint8_t *out_valid, void *stream) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_scatter_var_bytes, dim3(grid_for(n, kBlock / kWave)), dim3(kBlock), 0,
+                     as_stream(stream), in, pos, n, out_offsets, out_bytes, out_valid);
+  HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------
+// K4: gather with -1 -> null
+// ---------------------------------------------------------------------------
+__global__ void k_gather_columns(ColSet in, MutColSet out, int ncols, const int64_t *__restrict__ idx,
+                                 int64_t m) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) {
+    const int64_t s = idx[j];
+    for (int c = 0; c < ncols; ++c) {
+      const int w = in.c[c].width;
+      if (s >= 0) {
+        move_any(in.c[c].data, s, out.c[c].data, j, w);
+      } else {
+        for (int b = 0; b < w; ++b) out.c[c].data[j * w + b] = 0;
+      }
+      if (out.c[c].valid)
+        out.c[c].valid[j] = (s < 0) ? (uint8_t)0 : (in.c[c].valid ? in.c[c].valid[s] : (uint8_t)1);
+    }
+  }
+}
+
+void gather_columns(const ColView *in, const MutColView *out, int ncols, const int64_t *idx, int64_t m,
+                    void *stream) {
+  if (m == 0 || ncols == 0) return;
+  for (int c0 = 0; c0 < ncols; c0 += kMaxFusedCols) {
+    const int nc = (ncols - c0) < kMaxFusedCols ? (ncols - c0) : kMaxFusedCols;
+    ColSet a;
+    MutColSet b;
+    for (int c = 0; c < nc; ++c) {
+      a.c[c] = in[c0 + c];
+      b.c[c] = out[c0 + c];
+    }
+    hipLaunchKernelGGL(k_gather_columns, dim3(grid_for(m)), dim3(kBlock), 0, as_stream(stream), a, b, nc, idx,
+                       m);
+    HIP_LAUNCH_CHECK();
+  }
+}
+
+__global__ void k_gather_var_lengths(ColView in, const int64_t *__restrict__ idx, int64_t m,
+                                     int64_t *__restrict__ out_lens) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) {
+    const int64_t s = idx[j];
+    out_lens[j] = s < 0 ? 0 : in.offsets[s + 1] - in.offsets[s];
+  }
+}
+
+void gather_var_lengths(const ColView &in, const int64_t *idx, int64_t m, int64_t *out_lens, void *stream) {
+  if (m == 0) return;
+  hipLaunchKernelGGL(k_gather_var_lengths, dim3(grid_for(m)), dim3(kBlock), 0, as_stream(stream), in, idx, m,
+                     out_lens);
+  HIP_LAUNCH_CHECK();
+}
+
+__global__ void k_gather_var_bytes(ColView in, const int64_t *__restrict__ idx, int64_t m,
+                                   const int64_t *__restrict__ out_off, uint8_t *__restrict__ out_bytes,
+                                   uint8_t *__restrict__ out_valid) {
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
+  const int lane = lane_id();
+  for (int64_t j = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; j < m; j += waves) {
+    const int64_t s = idx[j];
+    if (s >= 0) {
+      const int64_t sb = in.offsets[s], len = in.offsets[s + 1] - sb;
+      const int64_t db = out_off[j];
+      for (int64_t k = lane; k < len; k += kWave) out_bytes[db + k] = in.data[sb + k];
+    }
+    if (lane == 0 && out_valid) out_valid[j] = (s < 0) ? (uint8_t)0 : (in.valid ? in.valid[s] : (uint8_t)1);
+  }
+}
+
+void gather_var_bytes(const ColView &in, const int64_t *idx, int64_t m, const int64_t *out_offsets,
+                      uint8_t *out_bytes, uint8_t *out_valid, void *stream) {
+  if (m == 0) return;
+  hipLaunchKernelGGL(k_gather_var_bytes, dim3(grid_for(m, kBlock / kWave)), dim3(kBlock), 0, as_stream(stream),
+                     in, idx, m, out_offsets, out_bytes, out_valid);
+  HIP_LAUNCH_CHECK();
+}
+
+}  // namespace hip
+}  // namespace cylon

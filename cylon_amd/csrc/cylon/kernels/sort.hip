@@ -1,0 +1,231 @@
+// K6 LSD radix sort of (uint64 key, int64 value) pairs and K7 sort-merge join
+// expansion (gfx950).
+//
+// Reference: cpp/src/cylon/arrow/arrow_kernels.cpp:199-465 (IndexSortKernel,
+// InplaceIndexSortKernel = introsort, multi-column comparator chains) and
+// cpp/src/cylon/join/sort_join.cpp:110-370 (advance equal runs, cross product).
+//
+// MI355X design:
+//   * keys are first mapped to order-preserving unsigned 64-bit images
+//     (sign flip for ints, IEEE flip for floats, bitwise NOT for descending),
+//     so every column type sorts with the same unsigned radix passes;
+//   * one OR/AND reduction over the keys finds the byte positions that are
+//     constant across all keys; those passes are skipped (an int64 key column
+//     holding values < 2^32 needs 4 passes, not 8);
+//   * each 8-bit pass = block histogram (LDS) -> scan -> stable rank kernel
+//     (stable_rank.hpp: wave64 ballot-match ranking, 256 buckets) that
+//     scatters key and value directly (no intermediate position array);
+//   * merge join: per left key a lower/upper bound search in the sorted right
+//     keys (count pass stores the lower bound), scan, and a write pass that
+//     expands the equal range into (left row, right row) pairs.
+#include "stable_rank.hpp"
+
+namespace cylon {
+namespace hip {
+
+// ---------------------------------------------------------------------------
+// key images
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t order_image(uint64_t bits, int w, int kind) {
+  const int nb = 8 * w;
+  const uint64_t mask = (nb == 64) ? ~0ull : ((1ull << nb) - 1);
+  const uint64_t sign = 1ull << (nb - 1);
+  bits &= mask;
+  if (kind == static_cast<int>(ValueKind::SIGNED_INT)) return bits ^ sign;
+  if (kind == static_cast<int>(ValueKind::FLOAT)) {
+    // canonicalise -0.0 to +0.0 and every NaN to the positive quiet NaN (sorts last)
+    if (bits == sign) bits = 0;
+    const uint64_t exp_mask = (w == 8) ? 0x7ff0000000000000ull : (w == 4 ? 0x7f800000ull : 0x7c00ull);
+    const uint64_t man_mask = (w == 8) ? 0x000fffffffffffffull : (w == 4 ? 0x007fffffull : 0x03ffull);
+    if ((bits & exp_mask) == exp_mask && (bits & man_mask) != 0) bits = exp_mask | ((man_mask + 1) >> 1);
+    return (bits & sign) ? (~bits & mask) : (bits | sign);
+  }
+  return bits;
+}
+
+__global__ void k_sort_keys(ColView c, const int64_t *__restrict__ perm, int64_t n, bool desc,
+                            uint64_t *__restrict__ out) {
+  const int nb = 8 * c.width;
+  const uint64_t mask = (nb == 64) ? ~0ull : ((1ull << nb) - 1);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t s = perm ? perm[i] : i;
+    uint64_t k = order_image(load_bits(c.data, s, c.width), c.width, c.kind);
+    if (desc) k = ~k & mask;
+    out[i] = k;
+  }
+}
+
+void sort_keys_from_column(const ColView &col, const int64_t *perm, int64_t n, bool desc, uint64_t *out,
+                           void *stream) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_sort_keys, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), col, perm, n, desc, out);
+  HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------
+// radix sort
+// ---------------------------------------------------------------------------
+__global__ void k_or_and(const uint64_t *__restrict__ k, int64_t n, unsigned long long *acc) {
+  uint64_t o = 0, a = ~0ull;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t v = k[i];
+    o |= v;
+    a &= v;
+  }
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    o |= __shfl_xor(o, d, kWave);
+    a &= __shfl_xor(a, d, kWave);
+  }
+  if (lane_id() == 0) {
+    atomicOr(&acc[0], (unsigned long long)o);
+    atomicAnd(&acc[1], (unsigned long long)a);
+  }
+}
+
+struct RadixDigit {
+  const uint64_t *keys;
+  int shift;
+  __device__ __forceinline__ uint32_t operator()(int64_t i) const { return (uint32_t)(keys[i] >> shift) & 0xffu; }
+};
+
+struct RadixSink {
+  const uint64_t *kin;
+  const int64_t *vin;
+  uint64_t *kout;
+  int64_t *vout;
+  __device__ __forceinline__ void operator()(int64_t i, int64_t d) const {
+    kout[d] = kin[i];
+    vout[d] = vin[i];
+  }
+};
+
+int64_t radix_sort_workspace(int64_t n) { return stable_rank_workspace(n, 256) + 2; }
+
+int radix_sort_pairs(uint64_t *keys, int64_t *vals, int64_t n, uint64_t *keys_alt, int64_t *vals_alt, int begin_bit,
+                     int end_bit, int64_t *ws, void *stream) {
+  if (n <= 1) return 0;
+  hipStream_t s = as_stream(stream);
+  unsigned long long *acc = reinterpret_cast<unsigned long long *>(ws);
+  unsigned long long init[2] = {0ull, ~0ull};
+  HIP_CHECK(hipMemcpyAsync(acc, init, sizeof(init), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_or_and, dim3(grid_for(n, kBlock, 1024)), dim3(kBlock), 0, s, keys, n, acc);
+  HIP_LAUNCH_CHECK();
+  unsigned long long oa[2];
+  HIP_CHECK(hipMemcpyAsync(oa, acc, sizeof(oa), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  const uint64_t diff = oa[0] ^ oa[1];
+  int cur = 0;
+  uint64_t *kb[2] = {keys, keys_alt};
+  int64_t *vb[2] = {vals, vals_alt};
+  for (int shift = begin_bit; shift < end_bit; shift += 8) {
+    if (((diff >> shift) & 0xffull) == 0) continue;  // constant digit: pass is the identity
+    RadixDigit dg{kb[cur], shift};
+    RadixSink sk{kb[cur], vb[cur], kb[cur ^ 1], vb[cur ^ 1]};
+    stable_rank_launch(dg, sk, n, 256, ws + 2, s);
+    cur ^= 1;
+  }
+  return cur;
+}
+
+// ---------------------------------------------------------------------------
+// K7 merge join on sorted key arrays
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t lower_bound_u64(const uint64_t *a, int64_t n, uint64_t v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int64_t upper_bound_u64(const uint64_t *a, int64_t n, uint64_t v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] <= v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void k_merge_count(const uint64_t *__restrict__ lk, int64_t nl, const uint64_t *__restrict__ rk,
+                              int64_t nr, int64_t *__restrict__ lo_out, int64_t *__restrict__ counts) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) {
+    const uint64_t v = lk[i];
+    const int64_t lo = lower_bound_u64(rk, nr, v);
+    const int64_t hi = (lo < nr && rk[lo] == v) ? upper_bound_u64(rk + lo, nr - lo, v) + lo : lo;
+    lo_out[i] = lo;
+    counts[i] = hi - lo;
+  }
+}
+
+__global__ void k_merge_write(const int64_t *__restrict__ lperm, int64_t nl, const int64_t *__restrict__ rperm,
+                              const int64_t *__restrict__ lo, const int64_t *__restrict__ offs,
+                              int64_t *__restrict__ out_l, int64_t *__restrict__ out_r) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) {
+    const int64_t o = offs[i], c = offs[i + 1] - o;
+    const int64_t l = lperm[i], b = lo[i];
+    for (int64_t k = 0; k < c; ++k) {
+      out_l[o + k] = l;
+      out_r[o + k] = rperm[b + k];
+    }
+  }
+}
+
+void merge_join_count(const uint64_t *lk, int64_t nl, const uint64_t *rk, int64_t nr, int64_t *lo, int64_t *counts,
+                      void *stream) {
+  if (nl == 0) return;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(k_merge_count, dim3(grid_for(nl)), dim3(kBlock), 0, s, lk, nl, rk, nr, lo, counts);
+  HIP_LAUNCH_CHECK();
+}
+
+void merge_join_write(const int64_t *lperm, int64_t nl, const int64_t *rperm, const int64_t *lo, const int64_t *offs,
+                      int64_t *out_l, int64_t *out_r, void *stream) {
+  if (nl == 0) return;
+  hipLaunchKernelGGL(k_merge_write, dim3(grid_for(nl)), dim3(kBlock), 0, as_stream(stream), lperm, nl, rperm, lo,
+                     offs, out_l, out_r);
+  HIP_LAUNCH_CHECK();
+}
+
+}  // namespace hip
+}  // namespace cylon
+
+namespace cylon {
+namespace hip {
+
+__global__ void k_string_chunk_keys(ColView c, const int64_t *__restrict__ perm, int64_t n, int64_t chunk, bool desc,
+                                    uint64_t *__restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t s = perm ? perm[i] : i;
+    const int64_t b = c.offsets[s], len = c.offsets[s + 1] - b;
+    uint64_t k = 0;
+    if (chunk < 0) {
+      k = (uint64_t)len;
+    } else {
+      const int64_t st = chunk * 8;
+      for (int j = 0; j < 8; ++j) {
+        const int64_t p = st + j;
+        k = (k << 8) | (p < len ? (uint64_t)c.data[b + p] : 0ull);
+      }
+    }
+    out[i] = desc ? ~k : k;
+  }
+}
+
+void sort_string_chunk_keys(const ColView &col, const int64_t *perm, int64_t n, int64_t chunk, bool desc,
+                            uint64_t *out, void *stream) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_string_chunk_keys, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), col, perm, n, chunk,
+                     desc, out);
+  HIP_LAUNCH_CHECK();
+}
+
+}  // namespace hip
+}  // namespace cylon

@@ -1,0 +1,138 @@
+// ProcessGroup-backed communicator (RCCL over xGMI on MI355X, gloo on CPU).
+// Reference call sites replaced here: SURVEY.md §2.5 M1-M8
+// (MPI_Init/Barrier/Finalize, MPI_Isend/Irecv header+payload, MPI_Allreduce).
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+#include <torch/csrc/distributed/c10d/Types.hpp>
+
+#include "communicator.hpp"
+
+namespace cylon {
+namespace net {
+
+const char *CommTypeName(CommType t) {
+  switch (t) {
+    case CommType::LOCAL: return "local";
+    case CommType::MPI: return "mpi";
+    case CommType::TCP: return "tcp";
+    case CommType::UCX: return "ucx";
+    case CommType::RCCL: return "rccl";
+    case CommType::GLOO: return "gloo";
+  }
+  return "unknown";
+}
+
+std::vector<at::Tensor> Communicator::AllGatherV(const at::Tensor &in) {
+  const int w = GetWorldSize();
+  at::Tensor n = at::full({1}, in.size(0), at::TensorOptions().dtype(at::kLong).device(in.device()));
+  at::Tensor ns = AllGather(n).to(at::kCPU);
+  int64_t mx = 0;
+  std::vector<int64_t> lens(w);
+  for (int i = 0; i < w; ++i) {
+    lens[i] = ns[i].item<int64_t>();
+    mx = std::max(mx, lens[i]);
+  }
+  std::vector<int64_t> shape(in.sizes().begin(), in.sizes().end());
+  shape[0] = mx;
+  at::Tensor padded = at::zeros(shape, in.options());
+  if (in.size(0)) padded.slice(0, 0, in.size(0)).copy_(in);
+  at::Tensor all = AllGather(padded);
+  std::vector<at::Tensor> out;
+  for (int i = 0; i < w; ++i) out.push_back(all.slice(0, i * mx, i * mx + lens[i]));
+  return out;
+}
+
+ProcessGroupCommunicator::ProcessGroupCommunicator(c10::intrusive_ptr<c10d::ProcessGroup> pg, CommType type,
+                                                   at::Device comm_device)
+    : pg_(std::move(pg)), type_(type), device_(comm_device) {
+  rank_ = pg_->getRank();
+  world_ = pg_->getSize();
+}
+
+ProcessGroupCommunicator::~ProcessGroupCommunicator() = default;
+
+at::Tensor ProcessGroupCommunicator::to_comm(const at::Tensor &t) const {
+  at::Tensor c = t.device() == device_ ? t : t.to(device_);
+  // bool is not a collective dtype on every backend; move it as bytes
+  if (c.scalar_type() == at::kBool) c = c.view(at::kByte);
+  return c.contiguous();
+}
+
+void ProcessGroupCommunicator::Barrier() {
+  // an all-reduce of one element on the comm device is a barrier that works
+  // identically for RCCL and gloo and orders with the current stream.
+  at::Tensor t = at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(device_));
+  std::vector<at::Tensor> v{t};
+  pg_->allreduce(v)->wait();
+  if (device_.is_cuda()) t.cpu();
+}
+
+at::Tensor ProcessGroupCommunicator::AllToAllV(const at::Tensor &send, const std::vector<int64_t> &send_counts,
+                                               const std::vector<int64_t> &recv_counts) {
+  CYLON_CHECK((int)send_counts.size() == world_ && (int)recv_counts.size() == world_, Code::Invalid,
+              "all-to-all counts must have world-size entries");
+  int64_t total = 0;
+  for (auto c : recv_counts) total += c;
+  at::Tensor in = to_comm(send);
+  std::vector<int64_t> shape(in.sizes().begin(), in.sizes().end());
+  if (shape.empty()) shape.push_back(0);
+  shape[0] = total;
+  at::Tensor out = at::empty(shape, in.options());
+  std::vector<int64_t> sc(send_counts), rc(recv_counts);
+  pg_->alltoall_base(out, in, rc, sc)->wait();
+  if (send.scalar_type() == at::kBool) out = out.view(at::kBool);
+  return out.device() == send.device() ? out : out.to(send.device());
+}
+
+std::vector<int64_t> ProcessGroupCommunicator::ExchangeCounts(const std::vector<int64_t> &send_counts) {
+  CYLON_CHECK((int)send_counts.size() == world_, Code::Invalid, "counts must have world-size entries");
+  at::Tensor s = at::tensor(send_counts, at::TensorOptions().dtype(at::kLong)).to(device_);
+  at::Tensor r = at::empty({world_}, s.options());
+  std::vector<int64_t> ones(world_, 1);
+  pg_->alltoall_base(r, s, ones, ones)->wait();
+  at::Tensor h = r.to(at::kCPU);
+  return std::vector<int64_t>(h.data_ptr<int64_t>(), h.data_ptr<int64_t>() + world_);
+}
+
+static c10d::ReduceOp to_c10d(ReduceOp op) {
+  switch (op) {
+    case ReduceOp::SUM: return c10d::ReduceOp::SUM;
+    case ReduceOp::MIN: return c10d::ReduceOp::MIN;
+    case ReduceOp::MAX: return c10d::ReduceOp::MAX;
+    case ReduceOp::PROD: return c10d::ReduceOp::PRODUCT;
+  }
+  return c10d::ReduceOp::SUM;
+}
+
+void ProcessGroupCommunicator::AllReduce(at::Tensor &t, ReduceOp op) {
+  at::Tensor c = to_comm(t);
+  std::vector<at::Tensor> v{c};
+  c10d::AllreduceOptions o;
+  o.reduceOp = to_c10d(op);
+  pg_->allreduce(v, o)->wait();
+  if (!c.is_same(t)) t.copy_(c.view(t.scalar_type()));
+}
+
+at::Tensor ProcessGroupCommunicator::AllGather(const at::Tensor &in) {
+  at::Tensor c = to_comm(in);
+  std::vector<int64_t> shape(c.sizes().begin(), c.sizes().end());
+  if (shape.empty()) shape.push_back(1);
+  const int64_t n0 = shape[0];
+  shape[0] = n0 * world_;
+  at::Tensor out = at::empty(shape, c.options());
+  at::Tensor src = c.dim() == 0 ? c.reshape({1}) : c;
+  pg_->_allgather_base(out, src)->wait();
+  if (in.scalar_type() == at::kBool) out = out.view(at::kBool);
+  return out.device() == in.device() ? out : out.to(in.device());
+}
+
+void ProcessGroupCommunicator::Broadcast(at::Tensor &t, int root) {
+  at::Tensor c = to_comm(t);
+  std::vector<at::Tensor> v{c};
+  c10d::BroadcastOptions o;
+  o.rootRank = root;
+  pg_->broadcast(v, o)->wait();
+  if (!c.is_same(t)) t.copy_(c.view(t.scalar_type()));
+}
+
+}  // namespace net
+}  // namespace cylon

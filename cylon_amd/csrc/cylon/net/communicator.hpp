@@ -1,0 +1,104 @@
+// L1 communication layer.
+//
+// Reference: cpp/src/cylon/net/communicator.hpp:24-37 (Communicator),
+// comm_type.hpp:20-22 (CommType), comm_operations.hpp:26-30 (ReduceOp),
+// mpi/mpi_communicator.cpp (MPI backend), net/ops/all_to_all.* and
+// arrow/arrow_all_to_all.* (header+payload point-to-point shuffle protocol).
+//
+// MI355X design: one process per GPU; the transport is a torch.distributed
+// c10d ProcessGroup.  With backend "nccl" that is RCCL over xGMI (grouped
+// ncclSend/ncclRecv all-to-all, ring/tree all-reduce); with "gloo" the same
+// code runs on CPU for the multi-process tests.  Instead of the reference's
+// per-buffer header/payload messages and polling progress engine, a shuffle is
+// ONE size exchange (all_to_all of P int64 counts) followed by one
+// all_to_all_v per column buffer on data already laid out partition-major
+// by the K3 scatter kernel (no packing, no host progress loop).
+#pragma once
+#include <ATen/ATen.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../common.hpp"
+
+namespace c10d {
+class ProcessGroup;
+}
+
+namespace cylon {
+namespace net {
+
+// Numbering follows the reference: LOCAL=0, MPI=1, TCP=2, UCX=3; RCCL and GLOO
+// are the torch.distributed-backed transports of this engine.
+enum class CommType : int { LOCAL = 0, MPI = 1, TCP = 2, UCX = 3, RCCL = 4, GLOO = 5 };
+
+enum class ReduceOp : int { SUM = 0, MIN = 1, MAX = 2, PROD = 3 };
+
+const char *CommTypeName(CommType t);
+
+class Communicator {
+ public:
+  virtual ~Communicator() = default;
+  virtual int GetRank() const = 0;
+  virtual int GetWorldSize() const = 0;
+  virtual CommType GetCommType() const = 0;
+  virtual void Barrier() = 0;
+  virtual void Finalize() {}
+
+  // Variable all-to-all along dim 0: send[ sum(send_counts) ] -> recv[ sum(recv_counts) ].
+  virtual at::Tensor AllToAllV(const at::Tensor &send, const std::vector<int64_t> &send_counts,
+                               const std::vector<int64_t> &recv_counts) = 0;
+  // Exchange per-peer element counts (the size matrix row of this rank).
+  virtual std::vector<int64_t> ExchangeCounts(const std::vector<int64_t> &send_counts) = 0;
+  virtual void AllReduce(at::Tensor &t, ReduceOp op) = 0;
+  // out = concat over ranks of `in` (same shape on every rank)
+  virtual at::Tensor AllGather(const at::Tensor &in) = 0;
+  // Gather tensors of different lengths from every rank (dim 0).
+  virtual std::vector<at::Tensor> AllGatherV(const at::Tensor &in);
+  virtual void Broadcast(at::Tensor &t, int root) = 0;
+};
+
+class LocalCommunicator : public Communicator {
+ public:
+  int GetRank() const override { return 0; }
+  int GetWorldSize() const override { return 1; }
+  CommType GetCommType() const override { return CommType::LOCAL; }
+  void Barrier() override {}
+  at::Tensor AllToAllV(const at::Tensor &send, const std::vector<int64_t> &, const std::vector<int64_t> &) override {
+    return send;
+  }
+  std::vector<int64_t> ExchangeCounts(const std::vector<int64_t> &c) override { return c; }
+  void AllReduce(at::Tensor &, ReduceOp) override {}
+  at::Tensor AllGather(const at::Tensor &in) override { return in; }
+  void Broadcast(at::Tensor &, int) override {}
+};
+
+// Communicator over a c10d ProcessGroup (RCCL on MI355X, gloo on CPU).
+class ProcessGroupCommunicator : public Communicator {
+ public:
+  ProcessGroupCommunicator(c10::intrusive_ptr<c10d::ProcessGroup> pg, CommType type, at::Device comm_device);
+  ~ProcessGroupCommunicator() override;
+  int GetRank() const override { return rank_; }
+  int GetWorldSize() const override { return world_; }
+  CommType GetCommType() const override { return type_; }
+  void Barrier() override;
+  at::Tensor AllToAllV(const at::Tensor &send, const std::vector<int64_t> &send_counts,
+                       const std::vector<int64_t> &recv_counts) override;
+  std::vector<int64_t> ExchangeCounts(const std::vector<int64_t> &send_counts) override;
+  void AllReduce(at::Tensor &t, ReduceOp op) override;
+  at::Tensor AllGather(const at::Tensor &in) override;
+  void Broadcast(at::Tensor &t, int root) override;
+  at::Device comm_device() const { return device_; }
+
+ private:
+  at::Tensor to_comm(const at::Tensor &t) const;
+  c10::intrusive_ptr<c10d::ProcessGroup> pg_;
+  CommType type_;
+  at::Device device_;
+  int rank_;
+  int world_;
+};
+
+}  // namespace net
+}  // namespace cylon

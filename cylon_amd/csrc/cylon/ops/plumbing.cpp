@@ -1,0 +1,161 @@
+// Table plumbing operators: gather (K4), compaction (K11), project, merge,
+// slice.  Reference: cylon/util/copy_arrray.cpp:24-142 (copy_array_by_indices,
+// -1 -> null), table.cpp:267-289 (Merge), :831-850 (Project), arrow Filter.
+#include "util.hpp"
+
+namespace cylon {
+namespace ops {
+
+std::vector<ColView> views(const TablePtr &t, const std::vector<int> &cols) {
+  std::vector<ColView> v;
+  v.reserve(cols.size());
+  for (int c : cols) v.push_back(t->column(c).view());
+  return v;
+}
+
+static Column gather_var(const Exec &ex, const Column &c, const at::Tensor &idx, bool may_null) {
+  const int64_t m = idx.numel();
+  ColView in = c.view();
+  at::Tensor lens = ex.empty_i64(m);
+  KCALL(ex, gather_var_lengths, in, ptr<int64_t>(idx), m, ptr<int64_t>(lens));
+  at::Tensor offs = exclusive_scan(ex, lens);
+  const int64_t total = read_i64(offs, m);
+  at::Tensor bytes = ex.empty_bytes(total);
+  at::Tensor valid;
+  if (c.nullable() || may_null) valid = ex.empty_u8(m);
+  KCALL(ex, gather_var_bytes, in, ptr<int64_t>(idx), m, ptr<int64_t>(offs), ptr<uint8_t>(bytes),
+        valid.defined() ? ptr<uint8_t>(valid) : nullptr);
+  return Column(c.name, c.type, m, bytes, offs, valid);
+}
+
+// Gather every column of a table with one fused launch per 16 fixed-width
+// columns; var-width columns take the two-pass path.
+static std::vector<Column> gather_columns(const std::vector<Column> &cols, const at::Tensor &idx, bool may_null) {
+  CYLON_CHECK(idx.scalar_type() == at::kLong, Code::TypeError, "gather index must be int64");
+  std::vector<Column> out(cols.size());
+  if (cols.empty()) return out;
+  Exec ex(cols[0].device());
+  at::Tensor ix = idx.device() == ex.device ? idx.contiguous() : idx.to(ex.device).contiguous();
+  const int64_t m = ix.numel();
+  std::vector<ColView> ins;
+  std::vector<MutColView> outs;
+  std::vector<size_t> fixed_pos;
+  for (size_t i = 0; i < cols.size(); ++i) {
+    const Column &c = cols[i];
+    if (c.is_var()) {
+      out[i] = gather_var(ex, c, ix, may_null);
+      continue;
+    }
+    Column o = make_fixed_column(c.name, c.type, m, ex.device, c.nullable() || may_null);
+    ColView v = c.view();
+    MutColView mv;
+    mv.data = m ? reinterpret_cast<uint8_t *>(o.data.data_ptr()) : nullptr;
+    mv.valid = o.validity.defined() ? ptr<uint8_t>(o.validity) : nullptr;
+    mv.width = v.width;
+    mv.kind = v.kind;
+    ins.push_back(v);
+    outs.push_back(mv);
+    fixed_pos.push_back(i);
+    out[i] = std::move(o);
+  }
+  if (!ins.empty() && m > 0)
+    KCALL(ex, gather_columns, ins.data(), outs.data(), (int)ins.size(), ptr<int64_t>(ix), m);
+  return out;
+}
+
+Column GatherColumn(const Column &c, const at::Tensor &idx) { return gather_columns({c}, idx, true)[0]; }
+
+TablePtr Gather(const TablePtr &t, const at::Tensor &idx) {
+  // -1 entries make the output nullable only if the caller may pass them; we
+  // check cheaply: int64 min over the index is one reduction.
+  bool may_null = false;
+  if (idx.numel() > 0) may_null = idx.min().item<int64_t>() < 0;
+  return Table::Make(t->GetContext(), gather_columns(t->columns(), idx, may_null));
+}
+
+TablePtr GatherNullable(const TablePtr &t, const at::Tensor &idx, bool may_null) {
+  return Table::Make(t->GetContext(), gather_columns(t->columns(), idx, may_null));
+}
+
+at::Tensor MaskToIndices(const at::Tensor &mask, bool invert) {
+  Exec ex(mask.device());
+  at::Tensor mk = mask.scalar_type() == at::kBool ? mask.view(at::kByte) : mask;
+  CYLON_CHECK(mk.scalar_type() == at::kByte, Code::TypeError, "mask must be bool or uint8");
+  mk = mk.contiguous();
+  const int64_t n = mk.numel();
+  at::Tensor ws = ex.empty_i64(KSIZE(ex, mask_to_indices_workspace, n));
+  at::Tensor out = ex.empty_i64(n);
+  at::Tensor cnt = ex.empty_i64(1);
+  KCALL(ex, mask_to_indices, ptr<uint8_t>(mk), n, invert, ptr<int64_t>(ws), ptr<int64_t>(out), ptr<int64_t>(cnt));
+  const int64_t k = read_i64(cnt, 0);
+  return out.slice(0, 0, k);
+}
+
+TablePtr FilterByMask(const TablePtr &t, const at::Tensor &mask) {
+  CYLON_CHECK(mask.numel() == t->Rows(), Code::Invalid,
+              "mask length " << mask.numel() << " != table rows " << t->Rows());
+  at::Tensor idx = MaskToIndices(mask.device() == t->device() ? mask : mask.to(t->device()));
+  return GatherNullable(t, idx, false);
+}
+
+TablePtr Project(const TablePtr &t, const std::vector<int> &cols) {
+  std::vector<Column> out;
+  for (int c : cols) out.push_back(t->column(c));
+  return Table::Make(t->GetContext(), std::move(out));
+}
+
+TablePtr Slice(const TablePtr &t, int64_t offset, int64_t length) {
+  std::vector<Column> out;
+  for (const auto &c : t->columns()) out.push_back(c.slice(offset, length));
+  return Table::Make(t->GetContext(), std::move(out));
+}
+
+static Column concat_columns(const std::vector<const Column *> &parts) {
+  const Column &f = *parts[0];
+  int64_t n = 0;
+  bool nullable = false;
+  for (auto *p : parts) {
+    n += p->length;
+    nullable |= p->nullable();
+  }
+  at::Tensor valid;
+  if (nullable) {
+    std::vector<at::Tensor> vs;
+    for (auto *p : parts)
+      vs.push_back(p->nullable() ? p->validity : at::ones({p->length}, p->data.options().dtype(at::kByte)));
+    valid = at::cat(vs);
+  }
+  if (!f.is_var()) {
+    std::vector<at::Tensor> ds;
+    for (auto *p : parts) ds.push_back(p->data);
+    return Column(f.name, f.type, n, at::cat(ds), at::Tensor(), valid);
+  }
+  std::vector<at::Tensor> bs, os;
+  int64_t base = 0;
+  for (size_t i = 0; i < parts.size(); ++i) {
+    const Column *p = parts[i];
+    bs.push_back(p->data);
+    at::Tensor o = p->offsets.slice(0, i == 0 ? 0 : 1, p->length + 1) + base;
+    os.push_back(o);
+    base += p->data.numel();
+  }
+  return Column(f.name, f.type, n, at::cat(bs), at::cat(os), valid);
+}
+
+TablePtr Merge(const std::vector<TablePtr> &tables) {
+  CYLON_CHECK(!tables.empty(), Code::Invalid, "merge of zero tables");
+  const TablePtr &f = tables[0];
+  for (const auto &t : tables)
+    CYLON_CHECK(same_schema(f, t), Code::Invalid, "merge: tables must have identical schemas");
+  if (tables.size() == 1) return f;
+  std::vector<Column> out;
+  for (int c = 0; c < f->Columns(); ++c) {
+    std::vector<const Column *> parts;
+    for (const auto &t : tables) parts.push_back(&t->column(c));
+    out.push_back(concat_columns(parts));
+  }
+  return Table::Make(f->GetContext(), std::move(out));
+}
+
+}  // namespace ops
+}  // namespace cylon

@@ -1,0 +1,101 @@
+// Sorting (K6) and the sort-merge join pair generator (K7).
+// Reference: cpp/src/cylon/table.cpp:291-328 (Sort), util/arrow_utils.cpp:30-108
+// (SortTable / SortTableMultiColumns), join/sort_join.cpp:576-722.
+//
+// Multi-column order = LSD over columns: the permutation is refined by stable
+// radix sorts from the least significant sort column to the most significant
+// one.  Nulls sort last within each column (pandas na_position='last').
+// Strings sort by stable passes over their length and then their 8-byte
+// big-endian chunks from the last chunk to the first, which yields byte-wise
+// lexicographic order.
+#include "util.hpp"
+
+namespace cylon {
+namespace ops {
+
+std::pair<at::Tensor, at::Tensor> RadixSortPairs(const Exec &ex, at::Tensor keys, at::Tensor vals, int end_bit) {
+  const int64_t n = keys.numel();
+  at::Tensor ka = at::empty_like(keys), va = at::empty_like(vals);
+  at::Tensor ws = ex.empty_i64(KSIZE(ex, radix_sort_workspace, n));
+  const int which = KCALL(ex, radix_sort_pairs, reinterpret_cast<uint64_t *>(ptr<int64_t>(keys)), ptr<int64_t>(vals), n,
+                          reinterpret_cast<uint64_t *>(ptr<int64_t>(ka)), ptr<int64_t>(va), 0, end_bit,
+                          ptr<int64_t>(ws));
+  return which ? std::make_pair(ka, va) : std::make_pair(keys, vals);
+}
+
+static at::Tensor iota(const Exec &ex, int64_t n) {
+  at::Tensor p = ex.empty_i64(n);
+  KCALL(ex, iota, ptr<int64_t>(p), n, 0);
+  return p;
+}
+
+// stable: rows whose column value is null move to the end, order otherwise kept
+static at::Tensor nulls_last(const Exec &ex, const Column &c, const at::Tensor &perm) {
+  if (!c.nullable()) return perm;
+  at::Tensor v = c.validity.index_select(0, perm);
+  at::Tensor valid_pos = MaskToIndices(v, false);
+  if (valid_pos.numel() == perm.numel()) return perm;
+  at::Tensor null_pos = MaskToIndices(v, true);
+  return at::cat({perm.index_select(0, valid_pos), perm.index_select(0, null_pos)});
+}
+
+static at::Tensor refine_by_column(const Exec &ex, const Column &c, at::Tensor perm, bool asc) {
+  const int64_t n = perm.numel();
+  if (!c.is_var()) {
+    CYLON_CHECK(c.type.kind() != ValueKind::FIXED_BYTES, Code::NotImplemented,
+                "sorting fixed-size binary columns is not supported");
+    at::Tensor keys = ex.empty_i64(n);
+    KCALL(ex, sort_keys_from_column, c.view(), ptr<int64_t>(perm), n, !asc,
+          reinterpret_cast<uint64_t *>(ptr<int64_t>(keys)));
+    perm = RadixSortPairs(ex, keys, perm, 8 * c.type.width()).second;
+    return nulls_last(ex, c, perm);
+  }
+  // strings: length pass, then chunks from last to first
+  at::Tensor lens = c.offsets.slice(0, 1, c.length + 1) - c.offsets.slice(0, 0, c.length);
+  const int64_t maxlen = c.length ? lens.max().item<int64_t>() : 0;
+  const int64_t nchunks = (maxlen + 7) / 8;
+  for (int64_t ch = -1; ch < nchunks; ++ch) {
+    const int64_t chunk = ch < 0 ? -1 : nchunks - 1 - ch;
+    at::Tensor keys = ex.empty_i64(n);
+    KCALL(ex, sort_string_chunk_keys, c.view(), ptr<int64_t>(perm), n, chunk, !asc,
+          reinterpret_cast<uint64_t *>(ptr<int64_t>(keys)));
+    perm = RadixSortPairs(ex, keys, perm, 64).second;
+  }
+  return nulls_last(ex, c, perm);
+}
+
+at::Tensor SortIndices(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending) {
+  CYLON_CHECK(!cols.empty(), Code::Invalid, "sort needs at least one column");
+  CYLON_CHECK(ascending.size() == cols.size() || ascending.size() == 1, Code::Invalid,
+              "ascending flags must match sort columns");
+  Exec ex(t->device());
+  at::Tensor perm = iota(ex, t->Rows());
+  for (int k = (int)cols.size() - 1; k >= 0; --k) {
+    const bool asc = ascending.size() == 1 ? ascending[0] : ascending[k];
+    perm = refine_by_column(ex, t->column(cols[k]), perm, asc);
+  }
+  return perm;
+}
+
+TablePtr Sort(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending) {
+  if (t->Rows() <= 1) return t;
+  return GatherNullable(t, SortIndices(t, cols, ascending), false);
+}
+
+std::pair<at::Tensor, at::Tensor> SortJoinPairs(const Exec &ex, const at::Tensor &lkeys, const at::Tensor &rkeys) {
+  const int64_t nl = lkeys.numel(), nr = rkeys.numel();
+  auto ls = RadixSortPairs(ex, lkeys.clone(), iota(ex, nl), 64);
+  auto rs = RadixSortPairs(ex, rkeys.clone(), iota(ex, nr), 64);
+  at::Tensor lo = ex.empty_i64(nl), counts = ex.empty_i64(nl);
+  KCALL(ex, merge_join_count, reinterpret_cast<const uint64_t *>(ptr<int64_t>(ls.first)), nl,
+        reinterpret_cast<const uint64_t *>(ptr<int64_t>(rs.first)), nr, ptr<int64_t>(lo), ptr<int64_t>(counts));
+  at::Tensor offs = exclusive_scan(ex, counts);
+  const int64_t m = read_i64(offs, nl);
+  at::Tensor ol = ex.empty_i64(m), orr = ex.empty_i64(m);
+  KCALL(ex, merge_join_write, ptr<int64_t>(ls.second), nl, ptr<int64_t>(rs.second), ptr<int64_t>(lo),
+        ptr<int64_t>(offs), ptr<int64_t>(ol), ptr<int64_t>(orr));
+  return {ol, orr};
+}
+
+}  // namespace ops
+}  // namespace cylon

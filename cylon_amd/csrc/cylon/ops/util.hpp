@@ -1,0 +1,77 @@
+// Operator-layer helpers: device dispatch between the HIP kernels and their CPU
+// twins, stream lookup and scratch allocation through torch's caching
+// allocator (stream ordered, so scratch tensors may be released as soon as the
+// launches that use them are enqueued).
+#pragma once
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <vector>
+
+#include "../column.hpp"
+#include "../kernels/kernels.hpp"
+#include "../table.hpp"
+
+namespace cylon {
+namespace ops {
+
+struct Exec {
+  at::Device device{at::kCPU};
+  bool gpu = false;
+  void *stream = nullptr;
+
+  explicit Exec(at::Device d) : device(d), gpu(d.is_cuda()) {
+    if (gpu) stream = reinterpret_cast<void *>(c10::hip::getCurrentHIPStream(d.index()).stream());
+  }
+
+  at::TensorOptions opts(at::ScalarType t) const { return at::TensorOptions().dtype(t).device(device); }
+  at::Tensor empty_i64(int64_t n) const { return at::empty({n}, opts(at::kLong)); }
+  at::Tensor empty_u32(int64_t n) const { return at::empty({n}, opts(at::kInt)); }
+  at::Tensor empty_u8(int64_t n) const { return at::empty({n}, opts(at::kByte)); }
+  at::Tensor zeros_u8(int64_t n) const { return at::zeros({n}, opts(at::kByte)); }
+  at::Tensor empty_bytes(int64_t n) const { return at::empty({n}, opts(at::kByte)); }
+};
+
+// Call the same primitive on the device the Exec targets.
+#define KCALL(ex, fn, ...) \
+  ((ex).gpu ? ::cylon::hip::fn(__VA_ARGS__, (ex).stream) : ::cylon::cpu::fn(__VA_ARGS__, nullptr))
+
+#define KSIZE(ex, fn, ...) ((ex).gpu ? ::cylon::hip::fn(__VA_ARGS__) : ::cylon::cpu::fn(__VA_ARGS__))
+
+template <typename T>
+inline T *ptr(const at::Tensor &t) {
+  return t.numel() ? reinterpret_cast<T *>(t.data_ptr()) : nullptr;
+}
+
+// Read a single int64 element to the host (synchronises the stream).
+inline int64_t read_i64(const at::Tensor &t, int64_t index) { return t[index].item<int64_t>(); }
+
+inline std::vector<int64_t> to_host_vec(const at::Tensor &t) {
+  at::Tensor h = t.to(at::kCPU).contiguous();
+  return std::vector<int64_t>(h.data_ptr<int64_t>(), h.data_ptr<int64_t>() + h.numel());
+}
+
+// exclusive scan of int64 counts -> offsets[n+1]
+inline at::Tensor exclusive_scan(const Exec &ex, const at::Tensor &counts) {
+  const int64_t n = counts.numel();
+  at::Tensor out = ex.empty_i64(n + 1);
+  at::Tensor ws = ex.empty_i64(KSIZE(ex, scan_workspace, n));
+  KCALL(ex, exclusive_scan, ptr<int64_t>(counts), n, ptr<int64_t>(out), ptr<int64_t>(ws));
+  return out;
+}
+
+inline bool same_schema(const TablePtr &a, const TablePtr &b) {
+  if (a->Columns() != b->Columns()) return false;
+  for (int i = 0; i < a->Columns(); ++i)
+    if (a->column(i).type != b->column(i).type) return false;
+  return true;
+}
+
+std::vector<ColView> views(const TablePtr &t, const std::vector<int> &cols);
+
+// stable LSD radix sort of (uint64 keys stored in an int64 tensor, int64 values); consumes its inputs
+std::pair<at::Tensor, at::Tensor> RadixSortPairs(const Exec &ex, at::Tensor keys, at::Tensor vals, int end_bit);
+
+}  // namespace ops
+}  // namespace cylon

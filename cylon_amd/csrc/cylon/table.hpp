@@ -1,0 +1,103 @@
+// Table: the core data structure (L2), and the engine's operator API (L4/L5).
+//
+// Reference: cpp/src/cylon/table.hpp:46-468 (Table wraps arrow::Table; all
+// relational operators are free functions over shared_ptr<Table>).
+// Here a Table is a vector of device-resident Columns on the context's device
+// (an MI355X under one-process-per-GPU), plus the reference's retain flag.
+// Operators in namespace cylon::ops throw CylonError; the Status-returning
+// reference-shaped API lives in api.hpp.
+#pragma once
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "column.hpp"
+#include "ctx/cylon_context.hpp"
+#include "join/join_config.hpp"
+
+namespace cylon {
+
+class Table;
+using TablePtr = std::shared_ptr<Table>;
+
+class Table {
+ public:
+  Table(std::shared_ptr<CylonContext> ctx, std::vector<Column> columns);
+
+  static TablePtr Make(std::shared_ptr<CylonContext> ctx, std::vector<Column> columns) {
+    return std::make_shared<Table>(std::move(ctx), std::move(columns));
+  }
+
+  int64_t Rows() const { return rows_; }
+  int32_t Columns() const { return static_cast<int32_t>(columns_.size()); }
+  std::vector<std::string> ColumnNames() const;
+  const std::vector<Column> &columns() const { return columns_; }
+  const Column &column(int i) const;
+  int ColumnIndex(const std::string &name) const;  // -1 if absent
+  const std::shared_ptr<CylonContext> &GetContext() const { return ctx_; }
+  at::Device device() const;
+
+  void retainMemory(bool retain) { retain_ = retain; }
+  bool IsRetain() const { return retain_; }
+  void Clear() {
+    columns_.clear();
+    rows_ = 0;
+  }
+
+  // total bytes of all buffers
+  int64_t nbytes() const;
+  TablePtr to(at::Device dev) const;
+
+ private:
+  std::shared_ptr<CylonContext> ctx_;
+  std::vector<Column> columns_;
+  int64_t rows_ = 0;
+  bool retain_ = true;
+};
+
+// Sort options for DistributedSort (reference table.hpp:388-393).
+struct SortOptions {
+  uint32_t num_bins = 0;     // 0 -> 16 * world
+  uint64_t num_samples = 0;  // 0 -> 1% of rows
+  static SortOptions Defaults() { return SortOptions(); }
+};
+
+namespace ops {
+
+// ---- plumbing -------------------------------------------------------------
+TablePtr Gather(const TablePtr &t, const at::Tensor &idx);  // idx int64, -1 -> null row
+TablePtr GatherNullable(const TablePtr &t, const at::Tensor &idx, bool may_null);
+Column GatherColumn(const Column &c, const at::Tensor &idx);
+TablePtr Project(const TablePtr &t, const std::vector<int> &cols);
+TablePtr Merge(const std::vector<TablePtr> &tables);  // vertical concat
+TablePtr Slice(const TablePtr &t, int64_t offset, int64_t length);
+TablePtr FilterByMask(const TablePtr &t, const at::Tensor &mask);  // uint8/bool mask
+at::Tensor MaskToIndices(const at::Tensor &mask, bool invert = false);
+
+// ---- partitioning (K1/K2/K3) --------------------------------------------
+// pid[i] in [0, nparts) and per-partition row counts (host vector).
+std::pair<at::Tensor, std::vector<int64_t>> MapToHashPartitions(const TablePtr &t, const std::vector<int> &cols,
+                                                                uint32_t nparts);
+// Reorders rows partition-major (stable); returns reordered table + counts.
+std::pair<TablePtr, std::vector<int64_t>> PartitionReorder(const TablePtr &t, const at::Tensor &pid,
+                                                           uint32_t nparts);
+std::vector<TablePtr> Split(const TablePtr &t, const at::Tensor &pid, uint32_t nparts);
+std::vector<TablePtr> HashPartition(const TablePtr &t, const std::vector<int> &cols, uint32_t nparts);
+
+// ---- communication --------------------------------------------------------
+// partition-major table + per-partition counts -> received table
+TablePtr AllToAllTable(const TablePtr &partitioned, const std::vector<int64_t> &counts);
+TablePtr Shuffle(const TablePtr &t, const std::vector<int> &hash_cols);
+
+// ---- relational -----------------------------------------------------------
+TablePtr Join(const TablePtr &left, const TablePtr &right, const join::config::JoinConfig &cfg);
+TablePtr DistributedJoin(const TablePtr &left, const TablePtr &right, const join::config::JoinConfig &cfg);
+// index pairs of a local join (li, ri; -1 for the unmatched side)
+std::pair<at::Tensor, at::Tensor> JoinIndices(const TablePtr &left, const TablePtr &right,
+                                              const join::config::JoinConfig &cfg);
+
+at::Tensor SortIndices(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending);
+TablePtr Sort(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending);
+
+}  // namespace ops
+}  // namespace cylon

@@ -1,0 +1,201 @@
+"""Arrow <-> device column bridge (reference: cpp/src/cylon/arrow/arrow_types.cpp,
+arrow_builder.cpp; python/pycylon/data/table.pyx from_arrow/to_arrow).
+
+Host Arrow buffers are viewed zero-copy through numpy, moved to the context
+device in one H2D copy per buffer, and kept in the engine's layout:
+fixed width values, int64 string offsets, uint8 validity byte-mask.
+"""
+from typing import Optional
+
+import numpy as np
+import pyarrow as pa
+import torch
+
+from .._lib import C
+
+T = C.Type
+
+_UNIT = {"s": 0, "ms": 1, "us": 2, "ns": 3}
+_UNIT_INV = {v: k for k, v in _UNIT.items()}
+
+_SIMPLE = {
+    pa.bool_(): T.BOOL, pa.uint8(): T.UINT8, pa.int8(): T.INT8, pa.uint16(): T.UINT16, pa.int16(): T.INT16,
+    pa.uint32(): T.UINT32, pa.int32(): T.INT32, pa.uint64(): T.UINT64, pa.int64(): T.INT64,
+    pa.float16(): T.HALF_FLOAT, pa.float32(): T.FLOAT, pa.float64(): T.DOUBLE, pa.date32(): T.DATE32,
+    pa.date64(): T.DATE64,
+}
+
+_NP = {
+    T.BOOL: np.uint8, T.UINT8: np.uint8, T.INT8: np.int8, T.UINT16: np.uint16, T.INT16: np.int16,
+    T.UINT32: np.uint32, T.INT32: np.int32, T.UINT64: np.uint64, T.INT64: np.int64, T.HALF_FLOAT: np.float16,
+    T.FLOAT: np.float32, T.DOUBLE: np.float64, T.DATE32: np.int32, T.DATE64: np.int64, T.TIMESTAMP: np.int64,
+    T.TIME32: np.int32, T.TIME64: np.int64, T.DURATION: np.int64,
+}
+
+_TORCH = {
+    T.BOOL: torch.uint8, T.UINT8: torch.uint8, T.INT8: torch.int8, T.UINT16: torch.uint16, T.INT16: torch.int16,
+    T.UINT32: torch.uint32, T.INT32: torch.int32, T.UINT64: torch.uint64, T.INT64: torch.int64,
+    T.HALF_FLOAT: torch.float16, T.FLOAT: torch.float32, T.DOUBLE: torch.float64, T.DATE32: torch.int32,
+    T.DATE64: torch.int64, T.TIMESTAMP: torch.int64, T.TIME32: torch.int32, T.TIME64: torch.int64,
+    T.DURATION: torch.int64,
+}
+
+
+def to_cylon_type(at: pa.DataType) -> "C.DataType":
+    if at in _SIMPLE:
+        return C.DataType(_SIMPLE[at])
+    if pa.types.is_string(at) or pa.types.is_large_string(at):
+        return C.DataType(T.STRING)
+    if pa.types.is_binary(at) or pa.types.is_large_binary(at):
+        return C.DataType(T.BINARY)
+    if pa.types.is_fixed_size_binary(at):
+        return C.DataType(T.FIXED_SIZE_BINARY, at.byte_width)
+    if pa.types.is_decimal(at):
+        return C.DataType(T.DECIMAL, at.byte_width)
+    if pa.types.is_timestamp(at):
+        d = C.DataType(T.TIMESTAMP)
+        d.unit = _UNIT[at.unit]
+        d.timezone = at.tz or ""
+        return d
+    if pa.types.is_time32(at) or pa.types.is_time64(at):
+        d = C.DataType(T.TIME32 if pa.types.is_time32(at) else T.TIME64)
+        d.unit = _UNIT[at.unit]
+        return d
+    if pa.types.is_duration(at):
+        d = C.DataType(T.DURATION)
+        d.unit = _UNIT[at.unit]
+        return d
+    if pa.types.is_dictionary(at):
+        return to_cylon_type(at.value_type)
+    raise TypeError(f"arrow type {at} is not supported by cylon_amd")
+
+
+def to_arrow_type(dt: "C.DataType") -> pa.DataType:
+    t = dt.type
+    inv = {v: k for k, v in _SIMPLE.items()}
+    if t in inv:
+        return inv[t]
+    if t == T.STRING:
+        return pa.string()
+    if t == T.BINARY:
+        return pa.binary()
+    if t == T.FIXED_SIZE_BINARY:
+        return pa.binary(dt.byte_width)
+    if t == T.DECIMAL:
+        return pa.decimal128(38, 0)
+    if t == T.TIMESTAMP:
+        return pa.timestamp(_UNIT_INV[dt.unit], tz=dt.timezone or None)
+    if t == T.TIME32:
+        return pa.time32(_UNIT_INV[dt.unit])
+    if t == T.TIME64:
+        return pa.time64(_UNIT_INV[dt.unit])
+    if t == T.DURATION:
+        return pa.duration(_UNIT_INV[dt.unit])
+    raise TypeError(f"cylon type {dt} has no arrow mapping")
+
+
+def torch_dtype(dt: "C.DataType"):
+    return _TORCH.get(dt.type, torch.uint8)
+
+
+def _unpack_bits(buf, offset: int, n: int) -> np.ndarray:
+    raw = np.frombuffer(buf, dtype=np.uint8)
+    bits = np.unpackbits(raw, bitorder="little")
+    return np.ascontiguousarray(bits[offset:offset + n])
+
+
+def _to_dev(a: np.ndarray, device: str) -> torch.Tensor:
+    t = torch.from_numpy(np.ascontiguousarray(a).copy() if not a.flags.writeable else np.ascontiguousarray(a))
+    return t.to(device, non_blocking=False) if device != "cpu" else t
+
+
+def column_from_arrow(name: str, arr, device: str) -> "C.Column":
+    if isinstance(arr, pa.ChunkedArray):
+        arr = arr.combine_chunks() if arr.num_chunks != 1 else arr.chunk(0)
+    if pa.types.is_dictionary(arr.type):
+        arr = arr.dictionary_decode()
+    dt = to_cylon_type(arr.type)
+    n = len(arr)
+    off = arr.offset
+    bufs = arr.buffers()
+    validity = None
+    if arr.null_count > 0 and bufs[0] is not None:
+        validity = _to_dev(_unpack_bits(bufs[0], off, n), device)
+    t = dt.type
+    if t in (T.STRING, T.BINARY):
+        large = pa.types.is_large_string(arr.type) or pa.types.is_large_binary(arr.type)
+        otype = np.int64 if large else np.int32
+        offsets = np.frombuffer(bufs[1], dtype=otype)[off:off + n + 1].astype(np.int64) if n else np.zeros(1, np.int64)
+        base = int(offsets[0]) if n else 0
+        end = int(offsets[-1]) if n else 0
+        data = np.frombuffer(bufs[2], dtype=np.uint8)[base:end] if (bufs[2] is not None and end > base) else \
+            np.zeros(0, np.uint8)
+        offsets = offsets - base
+        return C.Column(name, dt, n, _to_dev(data, device), _to_dev(offsets, device), validity)
+    if t == T.BOOL:
+        data = _unpack_bits(bufs[1], off, n) if n else np.zeros(0, np.uint8)
+        return C.Column(name, dt, n, _to_dev(data, device), None, validity)
+    if t in (T.FIXED_SIZE_BINARY, T.DECIMAL):
+        w = dt.byte_width
+        data = np.frombuffer(bufs[1], dtype=np.uint8)[off * w:(off + n) * w]
+        return C.Column(name, dt, n, _to_dev(data, device), None, validity)
+    npt = _NP[t]
+    data = np.frombuffer(bufs[1], dtype=npt)[off:off + n] if n else np.zeros(0, npt)
+    return C.Column(name, dt, n, _to_dev(data, device), None, validity)
+
+
+def column_to_arrow(col: "C.Column") -> pa.Array:
+    dt = col.type
+    n = col.length
+    at = to_arrow_type(dt)
+    vbuf = None
+    null_count = 0
+    if col.validity is not None and n:
+        v = col.validity.cpu().numpy().astype(np.uint8)
+        null_count = int(n - v.sum())
+        if null_count:
+            vbuf = pa.py_buffer(np.packbits(v, bitorder="little"))
+    t = dt.type
+    data = col.data.cpu()
+    if t in (T.STRING, T.BINARY):
+        offsets = col.offsets.cpu().numpy()
+        nbytes = int(offsets[-1]) if n else 0
+        if nbytes >= 2 ** 31 - 1:
+            at = pa.large_string() if t == T.STRING else pa.large_binary()
+            obuf = pa.py_buffer(offsets.astype(np.int64))
+        else:
+            obuf = pa.py_buffer(offsets.astype(np.int32))
+        dbuf = pa.py_buffer(data.numpy().tobytes())
+        return pa.Array.from_buffers(at, n, [vbuf, obuf, dbuf], null_count=null_count)
+    if t == T.BOOL:
+        bits = np.packbits(data.numpy().astype(np.uint8) != 0, bitorder="little")
+        return pa.Array.from_buffers(at, n, [vbuf, pa.py_buffer(bits)], null_count=null_count)
+    if t == T.DECIMAL:
+        return pa.Array.from_buffers(at, n, [vbuf, pa.py_buffer(data.numpy().tobytes())], null_count=null_count)
+    arr = data.numpy()
+    return pa.Array.from_buffers(at, n, [vbuf, pa.py_buffer(arr.tobytes())], null_count=null_count)
+
+
+def table_from_arrow(ctx_native, table: pa.Table, device: str) -> "C.Table":
+    cols = [column_from_arrow(name, table.column(i), device) for i, name in enumerate(table.column_names)]
+    return C.Table(ctx_native, cols)
+
+
+def table_to_arrow(ctable: "C.Table") -> pa.Table:
+    cols = ctable.columns()
+    return pa.Table.from_arrays([column_to_arrow(c) for c in cols], names=[c.name for c in cols])
+
+
+def column_from_tensor(name: str, t: torch.Tensor, validity: Optional[torch.Tensor] = None) -> "C.Column":
+    """Zero-copy column over a 1-D torch tensor (device tensors stay on device)."""
+    m = {torch.bool: T.BOOL, torch.uint8: T.UINT8, torch.int8: T.INT8, torch.int16: T.INT16, torch.int32: T.INT32,
+         torch.int64: T.INT64, torch.float16: T.HALF_FLOAT, torch.float32: T.FLOAT, torch.float64: T.DOUBLE,
+         torch.uint16: T.UINT16, torch.uint32: T.UINT32, torch.uint64: T.UINT64}
+    if t.dtype not in m:
+        raise TypeError(f"unsupported tensor dtype {t.dtype}")
+    if t.dtype == torch.bool:
+        t = t.to(torch.uint8)
+    t = t.contiguous().reshape(-1)
+    if validity is not None:
+        validity = validity.to(torch.uint8).contiguous().reshape(-1)
+    return C.Column(name, C.DataType(m[t.dtype] if t.dtype in m else T.UINT8), t.numel(), t, None, validity)

@@ -1,0 +1,263 @@
+"""Table I/O (reference: cpp/src/cylon/io/arrow_io.cpp:33-116, csv_read_config.hpp,
+csv_write_config.hpp, parquet_config.hpp; python/pycylon/io/*.pyx, data/csv.pyx).
+
+Parsing stays on the host in Arrow's multi-threaded C++ readers (as in the
+reference); the parsed columns are then moved to the context's device in one
+H2D copy per buffer.  Several files are read concurrently, one thread each
+(reference table.cpp:799-829).
+"""
+from concurrent.futures import ThreadPoolExecutor
+from typing import Dict, List, Optional, Sequence, Union
+
+import pyarrow as pa
+import pyarrow.csv as pacsv
+
+from ..ctx.context import CylonContext
+from ..data.table import Table, _ensure_ctx
+
+
+def _arrow_type(t):
+    if isinstance(t, pa.DataType):
+        return t
+    from .. import types as cytypes
+    return cytypes.to_arrow(t)
+
+
+class CSVReadOptions:
+    """Builder with both pycylon (snake_case) and C++ (CamelCase) spellings."""
+
+    def __init__(self):
+        self._use_threads = True
+        self._block_size = 1 << 20
+        self._delimiter = ","
+        self._ignore_empty_lines = True
+        self._autogenerate_column_names = False
+        self._column_names: Optional[List[str]] = None
+        self._skip_rows = 0
+        self._column_types: Dict[str, pa.DataType] = {}
+        self._null_values: Optional[List[str]] = None
+        self._true_values: Optional[List[str]] = None
+        self._false_values: Optional[List[str]] = None
+        self._strings_can_be_null = False
+        self._include_columns: Optional[List[str]] = None
+        self._include_missing_columns = False
+        self._quoting = True
+        self._quote_char = '"'
+        self._double_quote = True
+        self._escaping = False
+        self._escape_char = "\\"
+        self._newlines_in_values = False
+
+    # pycylon spellings
+    def use_threads(self, v: bool = True):
+        self._use_threads = bool(v)
+        return self
+
+    def block_size(self, b: int):
+        self._block_size = int(b)
+        return self
+
+    def with_delimiter(self, d: str):
+        self._delimiter = d[0]
+        return self
+
+    def ignore_emptylines(self, v: bool = True):
+        self._ignore_empty_lines = v
+        return self
+
+    def use_cols(self, cols: List):
+        self._include_columns = [str(c) for c in cols]
+        return self
+
+    def skip_rows(self, rows: int = 0):
+        self._skip_rows = int(rows)
+        return self
+
+    def na_values(self, vals: List[str]):
+        self._null_values = list(vals)
+        return self
+
+    def with_column_types(self, types: Dict[str, object]):
+        self._column_types = {str(k): _arrow_type(v) for k, v in types.items()}
+        return self
+
+    def column_names(self, names: List[str]):
+        self._column_names = list(names)
+        return self
+
+    def autogenerate_column_names(self, v: bool = True):
+        self._autogenerate_column_names = v
+        return self
+
+    def true_values(self, vals):
+        self._true_values = list(vals)
+        return self
+
+    def false_values(self, vals):
+        self._false_values = list(vals)
+        return self
+
+    def strings_can_be_null(self, v: bool = True):
+        self._strings_can_be_null = v
+        return self
+
+    def include_missing_columns(self, v: bool = True):
+        self._include_missing_columns = v
+        return self
+
+    def use_quoting(self, v: bool = True):
+        self._quoting = v
+        return self
+
+    def with_quote_char(self, c: str):
+        self._quote_char = c
+        return self
+
+    def double_quote(self, v: bool = True):
+        self._double_quote = v
+        return self
+
+    def use_escaping(self, v: bool = True):
+        self._escaping = v
+        return self
+
+    def escaping_character(self, c: str):
+        self._escape_char = c
+        self._escaping = True
+        return self
+
+    def has_new_lines_in_values(self, v: bool = True):
+        self._newlines_in_values = v
+        return self
+
+    # C++ spellings (cylon/io/csv_read_config.hpp)
+    UseThreads = use_threads
+    BlockSize = block_size
+    WithDelimiter = with_delimiter
+    IgnoreEmptyLines = ignore_emptylines
+    SkipRows = skip_rows
+    NullValues = na_values
+    WithColumnTypes = with_column_types
+    ColumnNames = column_names
+    AutoGenerateColumnNames = autogenerate_column_names
+    TrueValues = true_values
+    FalseValues = false_values
+    StringsCanBeNull = strings_can_be_null
+    IncludeColumns = use_cols
+    IncludeMissingColumns = include_missing_columns
+    UseQuoting = use_quoting
+    WithQuoteChar = with_quote_char
+    DoubleQuote = double_quote
+    UseEscaping = use_escaping
+    EscapingCharacter = escaping_character
+    HasNewLinesInValues = has_new_lines_in_values
+
+    def _arrow(self):
+        ro = pacsv.ReadOptions(use_threads=self._use_threads, block_size=self._block_size,
+                               skip_rows=self._skip_rows, column_names=self._column_names,
+                               autogenerate_column_names=self._autogenerate_column_names)
+        po = pacsv.ParseOptions(delimiter=self._delimiter, quote_char=self._quote_char if self._quoting else False,
+                                double_quote=self._double_quote,
+                                escape_char=self._escape_char if self._escaping else False,
+                                newlines_in_values=self._newlines_in_values,
+                                ignore_empty_lines=self._ignore_empty_lines)
+        kw = dict(column_types=self._column_types or None, strings_can_be_null=self._strings_can_be_null,
+                  include_columns=self._include_columns,
+                  include_missing_columns=self._include_missing_columns)
+        if self._null_values is not None:
+            kw["null_values"] = self._null_values
+        if self._true_values is not None:
+            kw["true_values"] = self._true_values
+        if self._false_values is not None:
+            kw["false_values"] = self._false_values
+        co = pacsv.ConvertOptions(**kw)
+        return ro, po, co
+
+
+class CSVWriteOptions:
+    def __init__(self):
+        self._delimiter = ","
+        self._column_names: Optional[List[str]] = None
+
+    def with_delimiter(self, d: str):
+        self._delimiter = d
+        return self
+
+    def with_column_names(self, names=None):
+        self._column_names = list(names or [])
+        return self
+
+    def delimiter(self) -> str:
+        return self._delimiter
+
+    def column_names(self) -> List[str]:
+        return self._column_names or []
+
+    WithDelimiter = with_delimiter
+    ColumnNames = with_column_names
+
+
+def _read_one_csv(path: str, options: CSVReadOptions) -> pa.Table:
+    ro, po, co = options._arrow()
+    return pacsv.read_csv(path, read_options=ro, parse_options=po, convert_options=co)
+
+
+def read_csv(context: CylonContext, path: Union[str, Sequence[str]], csv_read_options: CSVReadOptions = None):
+    """Read one CSV file into a Table, or several concurrently into a list of Tables."""
+    ctx = _ensure_ctx(context)
+    opts = csv_read_options or CSVReadOptions()
+    if isinstance(path, (list, tuple)):
+        with ThreadPoolExecutor(max_workers=max(1, len(path))) as ex:
+            tabs = list(ex.map(lambda p: _read_one_csv(p, opts), path))
+        return [Table(t, ctx) for t in tabs]
+    return Table(_read_one_csv(path, opts), ctx)
+
+
+def write_csv(table: Table, path: str, csv_write_options: CSVWriteOptions = None):
+    opts = csv_write_options or CSVWriteOptions()
+    at = table.to_arrow()
+    if opts.column_names():
+        at = at.rename_columns(opts.column_names())
+    pacsv.write_csv(at, path, write_options=pacsv.WriteOptions(delimiter=opts.delimiter()))
+
+
+class ParquetOptions:
+    """reference: cpp/src/cylon/io/parquet_config.hpp:34"""
+
+    def __init__(self, concurrent_file_reads: bool = True, chunk_size: int = 64 * 1024 * 1024,
+                 compression: str = "snappy"):
+        self.concurrent_file_reads = concurrent_file_reads
+        self.chunk_size = chunk_size
+        self.compression = compression
+
+
+def read_parquet(context: CylonContext, path: Union[str, Sequence[str]], options: ParquetOptions = None):
+    import pyarrow.parquet as pq
+    ctx = _ensure_ctx(context)
+    if isinstance(path, (list, tuple)):
+        with ThreadPoolExecutor(max_workers=max(1, len(path))) as ex:
+            tabs = list(ex.map(pq.read_table, path))
+        return [Table(t, ctx) for t in tabs]
+    return Table(pq.read_table(path), ctx)
+
+
+def write_parquet(table: Table, path: str, options: ParquetOptions = None):
+    import pyarrow.parquet as pq
+    opts = options or ParquetOptions()
+    pq.write_table(table.to_arrow(), path, row_group_size=max(1, opts.chunk_size // 64),
+                   compression=opts.compression)
+
+
+def write_arrow_ipc(table: Table, path: str):
+    """Arrow IPC (Feather v2) serialisation of a device table."""
+    import pyarrow.feather as feather
+    feather.write_feather(table.to_arrow(), path)
+
+
+def read_arrow_ipc(context: CylonContext, path: str) -> Table:
+    import pyarrow.feather as feather
+    return Table(feather.read_table(path), _ensure_ctx(context))
+
+
+__all__ = ["CSVReadOptions", "CSVWriteOptions", "ParquetOptions", "read_csv", "write_csv", "read_parquet",
+           "write_parquet", "write_arrow_ipc", "read_arrow_ipc"]

@@ -1,0 +1,53 @@
+"""Communication configs (reference: python/pycylon/net/*.pyx).
+
+`MPIConfig` is kept as a name for source compatibility with pycylon programs,
+but on MI355X the transport is torch.distributed: RCCL (backend "nccl" on ROCm)
+over xGMI when the ranks own GPUs, gloo on CPU.  Rendezvous uses the torchrun
+environment (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, MASTER_PORT).
+"""
+from dataclasses import dataclass, field
+from typing import Optional
+
+from .._lib import C
+
+CommType = C.CommType
+
+
+@dataclass
+class CommConfig:
+    """Base distributed configuration."""
+    backend: Optional[str] = None          # "nccl"(=RCCL) | "gloo" | None -> auto
+    init_method: Optional[str] = None      # torch.distributed init_method (default env://)
+    rank: Optional[int] = None
+    world_size: Optional[int] = None
+    device: Optional[str] = None           # "cuda:<i>" | "cpu" | None -> auto
+    timeout_s: float = 600.0
+    options: dict = field(default_factory=dict)
+
+    def comm_type(self):
+        return CommType.RCCL if self.resolved_backend() == "nccl" else CommType.GLOO
+
+    def resolved_backend(self) -> str:
+        if self.backend:
+            return "nccl" if self.backend in ("nccl", "rccl") else self.backend
+        import torch
+        return "nccl" if torch.cuda.is_available() else "gloo"
+
+
+@dataclass
+class RCCLConfig(CommConfig):
+    """RCCL over xGMI (one process per MI355X)."""
+    backend: Optional[str] = "nccl"
+
+
+@dataclass
+class GlooConfig(CommConfig):
+    """gloo over TCP (CPU tables / tests)."""
+    backend: Optional[str] = "gloo"
+
+
+class MPIConfig(CommConfig):
+    """pycylon compatibility alias: selects the default torch.distributed backend."""
+
+
+__all__ = ["CommConfig", "RCCLConfig", "GlooConfig", "MPIConfig", "CommType"]

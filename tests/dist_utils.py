@@ -1,0 +1,57 @@
+"""Multi-process test harness: N ranks as N local processes over gloo (the
+analogue of the reference's `mpirun --oversubscribe -np N`, cpp/test/CMakeLists.txt:45-49)."""
+import os
+import socket
+import sys
+import traceback
+
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, fn, args, q):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    try:
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        if root not in sys.path:
+            sys.path.insert(0, root)
+        from cylon_amd import CylonContext, GlooConfig
+        ctx = CylonContext(config=GlooConfig(), distributed=True, device="cpu")
+        try:
+            res = fn(ctx, *args)
+        finally:
+            ctx.finalize()
+        q.put((rank, True, res))
+    except Exception:  # pragma: no cover - reported to the parent
+        q.put((rank, False, traceback.format_exc()))
+
+
+def run_distributed(fn, world: int, *args, timeout: float = 240.0):
+    """Run fn(ctx, *args) on `world` gloo ranks; returns the list of per-rank results."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            rank, ok, res = q.get(timeout=timeout)
+            if not ok:
+                raise AssertionError(f"rank {rank} failed:\n{res}")
+            results[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    return [results[r] for r in range(world)]

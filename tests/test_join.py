@@ -1,0 +1,129 @@
+"""Join tests: local joins vs a pandas oracle, and the reference's distributed
+golden files (cpp/test/join_test.cpp, data/output/join_inner_{world}_{rank}.csv)."""
+import os
+
+import numpy as np
+import pandas as pd
+import pyarrow as pa
+import pytest
+
+from cylon_amd import Table
+from cylon_amd.io import CSVReadOptions, read_csv
+
+from dist_utils import run_distributed
+
+JOIN_TYPES = ["inner", "left", "right", "outer"]
+
+
+def _canon(df: pd.DataFrame):
+    rows = [tuple(None if (isinstance(v, float) and np.isnan(v)) or v is None or v is pd.NA else v
+                  for v in r) for r in df.itertuples(index=False)]
+    return sorted(rows, key=lambda r: tuple((x is None, str(type(x)), x if x is not None else 0) for x in r))
+
+
+def _oracle(a: pd.DataFrame, b: pd.DataFrame, how, lk, rk, lp="l_", rp="r_"):
+    a2 = a.add_prefix(lp)
+    b2 = b.add_prefix(rp)
+    return a2.merge(b2, left_on=[lp + k for k in lk], right_on=[rp + k for k in rk], how=how)
+
+
+@pytest.mark.parametrize("algorithm", ["hash", "sort"])
+@pytest.mark.parametrize("how", JOIN_TYPES)
+def test_single_key_int(ctx, algorithm, how):
+    rng = np.random.default_rng(1)
+    a = pd.DataFrame({"k": rng.integers(-20, 60, 500), "v": rng.random(500)})
+    b = pd.DataFrame({"k": rng.integers(0, 80, 300), "w": rng.integers(0, 9, 300)})
+    out = Table.from_pandas(ctx, a).join(Table.from_pandas(ctx, b), how, algorithm, on=["k"], left_prefix="l_",
+                                         right_prefix="r_").to_pandas()
+    ref = _oracle(a, b, how, ["k"], ["k"])
+    assert list(out.columns) == ["l_k", "l_v", "r_k", "r_w"]
+    assert _canon(out) == _canon(ref[out.columns])
+
+
+@pytest.mark.parametrize("algorithm", ["hash", "sort"])
+@pytest.mark.parametrize("how", JOIN_TYPES)
+def test_multi_key_and_strings(ctx, algorithm, how):
+    rng = np.random.default_rng(2)
+    n, m = 400, 250
+    a = pd.DataFrame({"k1": rng.integers(0, 6, n), "k2": [f"s{x}" for x in rng.integers(0, 7, n)],
+                      "v": rng.random(n)})
+    b = pd.DataFrame({"k1": rng.integers(0, 6, m), "k2": [f"s{x}" for x in rng.integers(0, 7, m)],
+                      "w": [f"p{x}" for x in range(m)]})
+    out = Table.from_pandas(ctx, a).join(Table.from_pandas(ctx, b), how, algorithm, on=["k1", "k2"],
+                                         left_prefix="l_", right_prefix="r_").to_pandas()
+    ref = _oracle(a, b, how, ["k1", "k2"], ["k1", "k2"])
+    assert _canon(out) == _canon(ref[out.columns])
+
+
+def test_float_and_mixed_width_keys(ctx):
+    a = pa.table({"k": pa.array([1, 2, 3, -4], pa.int32()), "x": [1.5, 2.5, 3.5, 4.5]})
+    b = pa.table({"k": pa.array([3, 1, -4, 9, 1], pa.int64()), "y": [0.25, -0.0, 0.0, 1.0, 2.0]})
+    out = Table(a, ctx).join(Table(b, ctx), "inner", "hash", left_on=[0], right_on=[0]).to_pandas()
+    assert sorted(out["k"].iloc[:, 0].tolist()) == [-4, 1, 1, 3]
+    fa = pa.table({"f": [0.0, 1.5, float("nan")]})
+    fb = pa.table({"f": [-0.0, 1.5, 2.0]})
+    out = Table(fa, ctx).join(Table(fb, ctx), "inner", "hash", on=[0], left_prefix="a", right_prefix="b")
+    assert out.row_count == 2
+
+
+def test_null_keys_match_each_other(ctx):
+    a = pa.table({"k": pa.array([1, None, 3]), "v": [1, 2, 3]})
+    b = pa.table({"k": pa.array([None, 3, 4]), "w": [7, 8, 9]})
+    out = Table(a, ctx).join(Table(b, ctx), "inner", "hash", on=["k"], left_prefix="l_", right_prefix="r_")
+    d = out.to_pandas()
+    assert sorted(d["l_v"].tolist()) == [2, 3]
+
+
+def test_empty_tables(ctx):
+    a = pa.table({"k": pa.array([], pa.int64()), "v": pa.array([], pa.float64())})
+    b = pa.table({"k": pa.array([1, 2], pa.int64()), "w": pa.array([1.0, 2.0])})
+    for how in JOIN_TYPES:
+        out = Table(a, ctx).join(Table(b, ctx), how, "hash", on=[0], left_prefix="l_", right_prefix="r_")
+        expect = 2 if how in ("right", "outer") else 0
+        assert out.row_count == expect
+
+
+# --------------------------------------------------------------------------
+# distributed golden files (partition-sensitive: validates bit-exact K1 hashing)
+# --------------------------------------------------------------------------
+def _golden_join(ctx, data_dir, algorithm):
+    rank, world = ctx.get_rank(), ctx.get_world_size()
+    opts = CSVReadOptions().use_threads(False).with_column_types({"0": pa.int64(), "1": pa.float64()})
+    t1 = read_csv(ctx, os.path.join(data_dir, "input", f"csv1_{rank}.csv"), opts)
+    t2 = read_csv(ctx, os.path.join(data_dir, "input", f"csv2_{rank}.csv"), opts)
+    exp_opts = CSVReadOptions().use_threads(False)
+    exp = pa.csv.read_csv(os.path.join(data_dir, "output", f"join_inner_{world}_{rank}.csv"))
+    res = t1.distributed_join(t2, "inner", algorithm, on=[0])
+    got = res.to_pandas()
+    got_rows = sorted(tuple(round(float(x), 6) for x in r) for r in got.itertuples(index=False))
+    exp_rows = sorted(tuple(round(float(x), 6) for x in r) for r in exp.to_pandas().itertuples(index=False))
+    return got_rows == exp_rows, len(got_rows), len(exp_rows)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+@pytest.mark.parametrize("algorithm", ["hash", "sort"])
+def test_distributed_join_golden(data_dir, world, algorithm):
+    import pyarrow.csv  # noqa: F401
+    res = run_distributed(_golden_join, world, data_dir, algorithm)
+    for ok, got, exp in res:
+        assert ok, f"rows got={got} expected={exp}"
+
+
+def _dist_vs_oracle(ctx, how, algorithm):
+    rank, world = ctx.get_rank(), ctx.get_world_size()
+    rng = np.random.default_rng(100 + rank)
+    a = pd.DataFrame({"k": rng.integers(0, 40, 150), "s": [f"x{v}" for v in rng.integers(0, 5, 150)]})
+    b = pd.DataFrame({"k": rng.integers(0, 40, 120), "v": rng.random(120)})
+    out = Table.from_pandas(ctx, a).distributed_join(Table.from_pandas(ctx, b), how, algorithm, on=["k"],
+                                                     left_prefix="l_", right_prefix="r_")
+    return out.to_pandas(), a, b
+
+
+@pytest.mark.parametrize("how", JOIN_TYPES)
+def test_distributed_join_all_types(how):
+    res = run_distributed(_dist_vs_oracle, 2, how, "hash")
+    got = pd.concat([r[0] for r in res])
+    a = pd.concat([r[1] for r in res])
+    b = pd.concat([r[2] for r in res])
+    ref = _oracle(a, b, how, ["k"], ["k"])
+    assert _canon(got) == _canon(ref[got.columns])
