@@ -47,7 +47,8 @@ def test_partition_ids_and_split_match_cpu(gpu_ctx, ctx, nparts):
 @pytest.mark.parametrize("n", [0, 1, 63, 64, 4097, 1_000_000])
 def test_mask_compaction_and_gather(gpu_ctx, ctx, n):
     rng = np.random.default_rng(n)
-    at = pa.table({"x": rng.integers(0, 10, n), "y": pa.array([None if v < 0.1 else v for v in rng.random(n)])
+    at = pa.table({"x": rng.integers(0, 10, n),
+                   "y": pa.array([None if v < 0.1 else v for v in rng.random(n)], pa.float64())
                    if n < 5000 else rng.random(n)})
     g, c = _pair(gpu_ctx, ctx, at)
     mask = torch.from_numpy(rng.random(n) < 0.3)
