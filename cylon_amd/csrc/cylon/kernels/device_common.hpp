@@ -1,6 +1,7 @@
 // Device-side helpers shared by the HIP kernel translation units (gfx950).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
 #include "../common.hpp"
 #include "../hash.hpp"
 #include "../types.hpp"

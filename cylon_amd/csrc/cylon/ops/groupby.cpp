@@ -1,0 +1,480 @@
+// Group-by (hash and pipeline), two-phase distributed group-by and scalar
+// aggregates.
+//
+// Reference: cpp/src/cylon/groupby/groupby.cpp:24-137 (DistributedHashGroupBy:
+// local combine only when every op is SUM/MIN/MAX, then shuffle + final),
+// hash_groupby.cpp:92-320, pipeline_groupby.cpp:131-256,
+// compute/aggregates.cpp:26-152 (Sum/Count/Min/Max + MPI_Allreduce).
+//
+// Differences by design (documented in docs/semantics.md):
+//   * every decomposable op (SUM, COUNT, MIN, MAX, MEAN, VAR, STDDEV) is
+//     combined locally before the shuffle through partial states
+//     (count, sum, M2, sum^2/count), so only #local-groups rows cross xGMI;
+//   * output names carry a single prefix (the reference double-prefixes in
+//     its two-phase path);
+//   * COUNT counts non-null values (identical to the reference on non-null data).
+#include <limits>
+
+#include "relational.hpp"
+#include "util.hpp"
+
+namespace cylon {
+namespace ops {
+
+static int64_t next_pow2(int64_t v) {
+  int64_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+static bool simple_key(const Column &c) {
+  return !c.nullable() && !c.is_var() && c.type.kind() != ValueKind::FIXED_BYTES && c.type.width() <= 8;
+}
+
+static at::Tensor iota_t(const Exec &ex, int64_t n) {
+  at::Tensor p = ex.empty_i64(n);
+  KCALL(ex, iota, ptr<int64_t>(p), n, 0);
+  return p;
+}
+
+const char *AggPrefix(int op) {
+  switch (op) {
+    case AGG_SUM: return "sum_";
+    case AGG_MIN: return "min_";
+    case AGG_MAX: return "max_";
+    case AGG_COUNT: return "count_";
+    case AGG_MEAN: return "mean_";
+    case AGG_VAR: return "var_";
+    case AGG_NUNIQUE: return "nunique_";
+    case AGG_QUANTILE: return "quantile_";
+    case AGG_STDDEV: return "std_";
+  }
+  return "agg_";
+}
+
+GroupInfo GroupIds(const TablePtr &t, const std::vector<int> &cols, bool presorted) {
+  Exec ex(t->device());
+  const int64_t n = t->Rows();
+  GroupInfo gi;
+  if (n == 0) {
+    gi.gid = ex.empty_i64(0);
+    gi.first_rows = ex.empty_i64(0);
+    return gi;
+  }
+  if (!presorted && cols.size() == 1 && simple_key(t->column(cols[0]))) {
+    const Column &c = t->column(cols[0]);
+    at::Tensor keys;
+    if (c.type.width() == 8 && c.type.kind() == ValueKind::SIGNED_INT) {
+      keys = c.data.view(at::kLong);
+    } else {
+      keys = ex.empty_i64(n);
+      KCALL(ex, key64_from_column, c.view(), n, ptr<int64_t>(keys));
+    }
+    const int64_t cap = next_pow2(std::max<int64_t>(2 * n, 64));
+    at::Tensor slot_keys = at::full({cap}, std::numeric_limits<int64_t>::min(), ex.opts(at::kLong));
+    at::Tensor slot_first = at::full({cap + 1}, std::numeric_limits<int64_t>::max(), ex.opts(at::kLong));
+    at::Tensor slot_of_row = ex.empty_i64(n);
+    KCALL(ex, group_insert, ptr<int64_t>(keys), n, ptr<int64_t>(slot_keys), cap, ptr<int64_t>(slot_of_row),
+          ptr<int64_t>(slot_first));
+    at::Tensor flags = ex.zeros_u8(n);
+    KCALL(ex, mark_firsts, ptr<int64_t>(slot_first), cap + 1, ptr<uint8_t>(flags));
+    gi.first_rows = MaskToIndices(flags);
+    gi.ngroups = gi.first_rows.numel();
+    at::Tensor gid_at_row = ex.empty_i64(n);
+    KCALL(ex, scatter_iota, ptr<int64_t>(gi.first_rows), gi.ngroups, ptr<int64_t>(gid_at_row));
+    gi.gid = ex.empty_i64(n);
+    KCALL(ex, gather_chain2, ptr<int64_t>(slot_of_row), ptr<int64_t>(slot_first), ptr<int64_t>(gid_at_row), n,
+          ptr<int64_t>(gi.gid));
+    return gi;
+  }
+  // exact sort-based path (multi-column, strings, nullable keys, presorted input)
+  at::Tensor perm = presorted ? iota_t(ex, n) : SortIndices(t, cols, {true});
+  std::vector<ColView> v = views(t, cols);
+  at::Tensor heads = ex.empty_u8(n);
+  KCALL(ex, segment_heads, v.data(), (int)v.size(), ptr<int64_t>(perm), n, ptr<uint8_t>(heads));
+  at::Tensor head_pos = MaskToIndices(heads);
+  const int64_t nruns = head_pos.numel();
+  at::Tensor incl = exclusive_scan(ex, heads.to(at::kLong)).slice(0, 1, n + 1) - 1;  // run of each sorted position
+  at::Tensor first_unsorted = perm.index_select(0, head_pos);
+  at::Tensor gid_of_run;
+  if (presorted) {
+    gid_of_run = iota_t(ex, nruns);
+    gi.first_rows = first_unsorted;
+  } else {
+    auto s = RadixSortPairs(ex, first_unsorted.clone(), iota_t(ex, nruns), 64);
+    gi.first_rows = s.first;
+    gid_of_run = ex.empty_i64(nruns);
+    KCALL(ex, scatter_iota, ptr<int64_t>(s.second), nruns, ptr<int64_t>(gid_of_run));
+  }
+  gi.ngroups = nruns;
+  gi.gid = ex.empty_i64(n);
+  KCALL(ex, permute_assign, ptr<int64_t>(perm), ptr<int64_t>(incl.contiguous()), ptr<int64_t>(gid_of_run), n,
+        ptr<int64_t>(gi.gid));
+  return gi;
+}
+
+// ---------------------------------------------------------------------------
+// per-group accumulators
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr int kSumF = 0, kSumI = 1, kMin = 2, kMax = 3, kCount = 4, kM2 = 5;
+
+struct Acc {
+  const Exec &ex;
+  const at::Tensor &gid;  // may be undefined for a single group
+  int64_t n, ng;
+
+  const int64_t *g() const { return gid.defined() ? ptr<int64_t>(gid) : nullptr; }
+
+  at::Tensor run(const Column &c, int kind, const at::Tensor &mean = at::Tensor()) const {
+    at::Tensor acc;
+    if (kind == kSumF || kind == kM2) acc = at::zeros({ng}, ex.opts(at::kDouble));
+    else if (kind == kMin) acc = at::full({ng}, -1, ex.opts(at::kLong));
+    else acc = at::zeros({ng}, ex.opts(at::kLong));
+    KCALL(ex, agg_accumulate, g(), n, ng, c.view(), kind, acc.data_ptr(),
+          mean.defined() ? ptr<double>(mean) : nullptr);
+    return acc;
+  }
+};
+
+Column double_col(const std::string &name, at::Tensor v, at::Tensor valid = at::Tensor()) {
+  return Column(name, DataType(Type::DOUBLE), v.numel(), v.contiguous(),
+                at::Tensor(), valid.defined() ? valid.to(at::kByte).contiguous() : at::Tensor());
+}
+
+Column long_col(const std::string &name, at::Tensor v, Type t = Type::INT64) {
+  return Column(name, DataType(t), v.numel(), v.contiguous());
+}
+
+Column minmax_col(const Exec &ex, const std::string &name, const Column &c, const at::Tensor &img,
+                  const at::Tensor &count) {
+  const int64_t ng = img.numel();
+  Column out = make_fixed_column(name, c.type, ng, ex.device, c.nullable());
+  KCALL(ex, agg_unimage, reinterpret_cast<const uint64_t *>(ptr<int64_t>(img)), ng, c.type.width(),
+        static_cast<int>(c.type.kind()), reinterpret_cast<uint8_t *>(out.data.data_ptr()));
+  if (c.nullable()) out.validity = (count > 0).to(at::kByte);
+  return out;
+}
+
+Column column_from(const std::string &name, const at::Tensor &t) {
+  return Column(name, DataType(Type::INT64), t.numel(), t);
+}
+
+TablePtr values_by_group(const TablePtr &t, const at::Tensor &gid, const Column &val) {
+  std::vector<Column> cols{column_from("g", gid), val};
+  return Table::Make(t->GetContext(), std::move(cols));
+}
+
+}  // namespace
+
+static Column agg_column(const Exec &ex, const TablePtr &t, const GroupInfo &gi, const AggSpec &a) {
+  const Column &c = t->column(a.col);
+  const std::string name = std::string(AggPrefix(a.op)) + c.name;
+  Acc acc{ex, gi.gid, t->Rows(), gi.ngroups};
+  const bool is_float = c.type.kind() == ValueKind::FLOAT;
+  const bool numeric = c.type.is_numeric();
+  if (a.op != AGG_COUNT && a.op != AGG_NUNIQUE)
+    CYLON_CHECK(numeric, Code::TypeError, "aggregation " << AggPrefix(a.op) << " needs a numeric column, got "
+                                                         << c.type.ToString());
+  switch (a.op) {
+    case AGG_SUM:
+      if (is_float) return double_col(name, acc.run(c, kSumF));
+      return long_col(name, acc.run(c, kSumI),
+                      c.type.kind() == ValueKind::UNSIGNED_INT ? Type::UINT64 : Type::INT64);
+    case AGG_COUNT: return long_col(name, acc.run(c, kCount));
+    case AGG_MIN:
+    case AGG_MAX: {
+      at::Tensor img = acc.run(c, a.op == AGG_MIN ? kMin : kMax);
+      at::Tensor cnt = c.nullable() ? acc.run(c, kCount) : at::Tensor();
+      return minmax_col(ex, name, c, img, cnt);
+    }
+    case AGG_MEAN: {
+      at::Tensor s = acc.run(c, kSumF), n = acc.run(c, kCount);
+      return double_col(name, s / n.to(at::kDouble), n > 0);
+    }
+    case AGG_VAR:
+    case AGG_STDDEV: {
+      at::Tensor s = acc.run(c, kSumF), n = acc.run(c, kCount).to(at::kDouble);
+      at::Tensor mean = (s / n).contiguous();
+      at::Tensor m2 = acc.run(c, kM2, mean);
+      at::Tensor var = m2 / (n - a.ddof);
+      at::Tensor valid = (n - a.ddof) > 0;
+      return double_col(name, a.op == AGG_VAR ? var : var.sqrt(), valid);
+    }
+    case AGG_NUNIQUE:
+    case AGG_QUANTILE: {
+      at::Tensor gsub = gi.gid;
+      Column vsub = c;
+      if (c.nullable()) {  // both exclude nulls (pandas defaults)
+        at::Tensor keep = MaskToIndices(c.validity);
+        gsub = gi.gid.index_select(0, keep);
+        vsub = GatherColumn(c, keep);
+        vsub.validity = at::Tensor();
+      }
+      TablePtr tmp = values_by_group(t, gsub, vsub);
+      Acc sub{ex, gsub, tmp->Rows(), gi.ngroups};
+      if (a.op == AGG_NUNIQUE) {
+        GroupInfo pairs = GroupIds(tmp, {0, 1});
+        at::Tensor pg = gsub.index_select(0, pairs.first_rows);
+        Acc pacc{ex, pg, pg.numel(), gi.ngroups};
+        return long_col(name, pacc.run(column_from("g", pg), kCount));
+      }
+      at::Tensor perm = SortIndices(tmp, {0, 1}, {true});
+      at::Tensor counts = sub.run(column_from("g", gsub), kCount);
+      at::Tensor offs = exclusive_scan(ex, counts);
+      at::Tensor out = ex.opts(at::kDouble).device().is_cuda() ? at::empty({gi.ngroups}, ex.opts(at::kDouble))
+                                                               : at::empty({gi.ngroups}, ex.opts(at::kDouble));
+      at::Tensor valid = ex.empty_u8(gi.ngroups);
+      KCALL(ex, group_quantile, tmp->column(1).view(), ptr<int64_t>(perm), ptr<int64_t>(offs), gi.ngroups,
+            a.quantile, ptr<double>(out), ptr<uint8_t>(valid));
+      return double_col(name, out, valid);
+    }
+  }
+  CYLON_THROW(Code::NotImplemented, "aggregation op " << a.op << " not supported");
+}
+
+static TablePtr groupby_with(const TablePtr &t, const std::vector<int> &keys, const std::vector<AggSpec> &aggs,
+                             bool presorted) {
+  CYLON_CHECK(!keys.empty(), Code::Invalid, "group-by needs at least one key column");
+  Exec ex(t->device());
+  GroupInfo gi = GroupIds(t, keys, presorted);
+  TablePtr kt = GatherNullable(Project(t, keys), gi.first_rows, false);
+  std::vector<Column> cols = kt->columns();
+  for (const auto &a : aggs) cols.push_back(agg_column(ex, t, gi, a));
+  return Table::Make(t->GetContext(), std::move(cols));
+}
+
+TablePtr HashGroupBy(const TablePtr &t, const std::vector<int> &keys, const std::vector<AggSpec> &aggs) {
+  return groupby_with(t, keys, aggs, false);
+}
+
+TablePtr PipelineGroupBy(const TablePtr &t, const std::vector<int> &keys, const std::vector<AggSpec> &aggs) {
+  return groupby_with(t, keys, aggs, true);
+}
+
+// ---------------------------------------------------------------------------
+// distributed (two-phase with partial states)
+// ---------------------------------------------------------------------------
+static bool decomposable(int op) {
+  return op == AGG_SUM || op == AGG_COUNT || op == AGG_MIN || op == AGG_MAX || op == AGG_MEAN || op == AGG_VAR ||
+         op == AGG_STDDEV;
+}
+
+TablePtr DistributedHashGroupBy(const TablePtr &t, const std::vector<int> &keys, const std::vector<AggSpec> &aggs) {
+  auto ctx = t->GetContext();
+  if (ctx->GetWorldSize() == 1) return HashGroupBy(t, keys, aggs);
+  bool all_dec = true;
+  for (const auto &a : aggs) all_dec &= decomposable(a.op);
+  const int nk = (int)keys.size();
+  std::vector<int> key_pos(nk);
+  for (int i = 0; i < nk; ++i) key_pos[i] = i;
+
+  if (!all_dec) {  // shuffle raw rows, aggregate once
+    std::vector<int> cols = keys;
+    std::vector<AggSpec> remapped;
+    for (const auto &a : aggs) {
+      AggSpec b = a;
+      b.col = (int)cols.size();
+      cols.push_back(a.col);
+      remapped.push_back(b);
+    }
+    TablePtr sh = Shuffle(Project(t, cols), key_pos);
+    return HashGroupBy(sh, key_pos, remapped);
+  }
+
+  // phase 1: local partial states
+  Exec ex(t->device());
+  GroupInfo gi = GroupIds(t, keys, false);
+  TablePtr kt = GatherNullable(Project(t, keys), gi.first_rows, false);
+  std::vector<Column> pcols = kt->columns();
+  struct Plan {
+    int op;
+    int ddof;
+    std::string name;
+    std::vector<int> state_cols;  // positions in the partial table
+  };
+  std::vector<Plan> plans;
+  std::vector<AggSpec> combine;  // phase-2 aggregations over the state columns
+  Acc acc{ex, gi.gid, t->Rows(), gi.ngroups};
+  auto add_state = [&](Plan &p, Column c, int combine_op) {
+    const int pos = (int)pcols.size();
+    c.name = "__s" + std::to_string(pos);
+    pcols.push_back(std::move(c));
+    p.state_cols.push_back(pos);
+    combine.push_back(AggSpec{pos, combine_op});
+  };
+  for (const auto &a : aggs) {
+    const Column &c = t->column(a.col);
+    Plan p{a.op, a.ddof, std::string(AggPrefix(a.op)) + c.name, {}};
+    switch (a.op) {
+      case AGG_SUM:
+      case AGG_MIN:
+      case AGG_MAX:
+      case AGG_COUNT:
+        add_state(p, agg_column(ex, t, gi, a), a.op == AGG_COUNT ? AGG_SUM : a.op);
+        break;
+      case AGG_MEAN:
+        add_state(p, double_col("", acc.run(c, kSumF)), AGG_SUM);
+        add_state(p, long_col("", acc.run(c, kCount)), AGG_SUM);
+        break;
+      default: {  // VAR / STDDEV: (count, sum, M2, sum^2/count)
+        at::Tensor s = acc.run(c, kSumF), n = acc.run(c, kCount);
+        at::Tensor nd = n.to(at::kDouble);
+        at::Tensor mean = (s / nd).contiguous();
+        at::Tensor m2 = at::nan_to_num(acc.run(c, kM2, mean), 0.0);
+        at::Tensor q = at::nan_to_num(s * s / nd, 0.0);
+        add_state(p, long_col("", n), AGG_SUM);
+        add_state(p, double_col("", s), AGG_SUM);
+        add_state(p, double_col("", m2), AGG_SUM);
+        add_state(p, double_col("", q), AGG_SUM);
+      }
+    }
+    plans.push_back(std::move(p));
+  }
+  TablePtr partial = Table::Make(t->GetContext(), std::move(pcols));
+  // phase 2: shuffle partial rows by key, combine
+  TablePtr sh = Shuffle(partial, key_pos);
+  TablePtr comb = HashGroupBy(sh, key_pos, combine);
+  std::vector<Column> out;
+  for (int i = 0; i < nk; ++i) out.push_back(comb->column(i));
+  int ci = nk;
+  for (const auto &p : plans) {
+    switch (p.op) {
+      case AGG_SUM:
+      case AGG_MIN:
+      case AGG_MAX:
+      case AGG_COUNT:
+        out.push_back(comb->column(ci++).with_name(p.name));
+        break;
+      case AGG_MEAN: {
+        at::Tensor s = comb->column(ci++).data, n = comb->column(ci++).data.to(at::kDouble);
+        out.push_back(double_col(p.name, s / n, n > 0));
+        break;
+      }
+      default: {
+        at::Tensor n = comb->column(ci++).data.to(at::kDouble);
+        at::Tensor s = comb->column(ci++).data;
+        at::Tensor m2 = comb->column(ci++).data;
+        at::Tensor q = comb->column(ci++).data;
+        at::Tensor mean = s / n;
+        at::Tensor M2 = at::clamp_min(m2 + q - n * mean * mean, 0.0);
+        at::Tensor var = M2 / (n - p.ddof);
+        out.push_back(double_col(p.name, p.op == AGG_VAR ? var : var.sqrt(), (n - p.ddof) > 0));
+      }
+    }
+  }
+  return Table::Make(t->GetContext(), std::move(out));
+}
+
+TablePtr DistributedPipelineGroupBy(const TablePtr &t, const std::vector<int> &keys,
+                                    const std::vector<AggSpec> &aggs) {
+  auto ctx = t->GetContext();
+  std::vector<int> cols = keys;
+  std::vector<AggSpec> remapped;
+  for (const auto &a : aggs) {
+    AggSpec b = a;
+    b.col = (int)cols.size();
+    cols.push_back(a.col);
+    remapped.push_back(b);
+  }
+  std::vector<int> key_pos(keys.size());
+  for (size_t i = 0; i < keys.size(); ++i) key_pos[i] = (int)i;
+  TablePtr p = Project(t, cols);
+  if (ctx->GetWorldSize() > 1) p = Shuffle(p, key_pos);
+  TablePtr sorted = Sort(p, key_pos, {true});
+  return PipelineGroupBy(sorted, key_pos, remapped);
+}
+
+// ---------------------------------------------------------------------------
+// scalar aggregates (K12 + allreduce)
+// ---------------------------------------------------------------------------
+TablePtr Aggregate(const TablePtr &t, int col, int op, double quantile, int ddof, bool distributed) {
+  auto ctx = t->GetContext();
+  const bool dist = distributed && ctx->GetWorldSize() > 1;
+  auto comm = ctx->GetCommunicator();
+  Exec ex(t->device());
+  const Column &c = t->column(col);
+  at::Tensor none;
+  Acc acc{ex, none, t->Rows(), 1};
+  auto allreduce = [&](at::Tensor x, net::ReduceOp o) {
+    if (dist) comm->AllReduce(x, o);
+    return x;
+  };
+  const bool is_float = c.type.kind() == ValueKind::FLOAT;
+  std::vector<Column> out;
+  switch (op) {
+    case AGG_SUM:
+      if (is_float) out.push_back(double_col(c.name, allreduce(acc.run(c, kSumF), net::ReduceOp::SUM)));
+      else out.push_back(long_col(c.name, allreduce(acc.run(c, kSumI), net::ReduceOp::SUM)));
+      break;
+    case AGG_COUNT:
+      out.push_back(long_col(c.name, allreduce(acc.run(c, kCount), net::ReduceOp::SUM)));
+      break;
+    case AGG_MIN:
+    case AGG_MAX: {
+      CYLON_CHECK(c.type.is_numeric(), Code::TypeError, "min/max need a numeric column");
+      at::Tensor img = acc.run(c, op == AGG_MIN ? kMin : kMax);
+      // unsigned image -> signed order for the collective
+      at::Tensor flip = at::full({1}, std::numeric_limits<int64_t>::min(), img.options());
+      at::Tensor s = at::bitwise_xor(img, flip);
+      s = allreduce(s, op == AGG_MIN ? net::ReduceOp::MIN : net::ReduceOp::MAX);
+      img = at::bitwise_xor(s, flip).contiguous();
+      at::Tensor cnt = allreduce(acc.run(c, kCount), net::ReduceOp::SUM);
+      Column mc = minmax_col(ex, c.name, c, img, cnt);
+      if (!c.nullable()) mc.validity = (cnt > 0).to(at::kByte);
+      out.push_back(mc);
+      break;
+    }
+    case AGG_MEAN: {
+      at::Tensor s = allreduce(acc.run(c, kSumF), net::ReduceOp::SUM);
+      at::Tensor n = allreduce(acc.run(c, kCount), net::ReduceOp::SUM);
+      out.push_back(double_col(c.name, s / n.to(at::kDouble), n > 0));
+      break;
+    }
+    case AGG_VAR:
+    case AGG_STDDEV: {
+      at::Tensor s = allreduce(acc.run(c, kSumF), net::ReduceOp::SUM);
+      at::Tensor n = allreduce(acc.run(c, kCount), net::ReduceOp::SUM).to(at::kDouble);
+      at::Tensor mean = (s / n).contiguous();
+      at::Tensor m2 = allreduce(acc.run(c, kM2, mean), net::ReduceOp::SUM);
+      at::Tensor var = m2 / (n - ddof);
+      out.push_back(double_col(c.name, op == AGG_VAR ? var : var.sqrt(), (n - ddof) > 0));
+      break;
+    }
+    case AGG_NUNIQUE: {
+      TablePtr one = Project(t, {col});
+      if (c.nullable()) one = FilterByMask(one, c.validity);
+      TablePtr u = dist ? DistributedUnique(one, {0}, true) : Unique(one, {0}, true);
+      at::Tensor cnt = at::full({1}, u->Rows(), ex.opts(at::kLong));
+      out.push_back(long_col(c.name, allreduce(cnt, net::ReduceOp::SUM)));
+      break;
+    }
+    case AGG_QUANTILE: {
+      TablePtr one = Project(t, {col});
+      if (dist) {
+        std::vector<Column> gathered;
+        CYLON_CHECK(!c.is_var(), Code::TypeError, "quantile needs a numeric column");
+        auto parts = comm->AllGatherV(c.data);
+        at::Tensor all = at::cat(parts);
+        at::Tensor valid;
+        if (c.nullable()) valid = at::cat(comm->AllGatherV(c.validity));
+        one = Table::Make(ctx, {Column(c.name, c.type, all.numel(), all, at::Tensor(), valid)});
+      }
+      at::Tensor zero = at::zeros({one->Rows()}, ex.opts(at::kLong));
+      GroupInfo gi{zero, one->Rows() ? 1 : 0, at::Tensor()};
+      if (one->Rows() == 0) {
+        out.push_back(double_col(c.name, at::zeros({1}, ex.opts(at::kDouble)), at::zeros({1}, ex.opts(at::kByte))));
+        break;
+      }
+      Column q = agg_column(ex, one, gi, AggSpec{0, AGG_QUANTILE, quantile, ddof});
+      out.push_back(q.with_name(c.name));
+      break;
+    }
+    default: CYLON_THROW(Code::NotImplemented, "aggregate op " << op);
+  }
+  return Table::Make(ctx, std::move(out));
+}
+
+}  // namespace ops
+}  // namespace cylon

@@ -207,6 +207,100 @@ class Table:
         return self._wrap(C.distributed_join(self._t, table._t, jt, algorithm.lower(), lc, rc,
                                              kwargs.get("left_prefix", ""), kwargs.get("right_prefix", "")))
 
+    # set operations (distinct semantics over all columns; reference table.pyx:383-430)
+    def union(self, table: "Table") -> "Table":
+        return self._wrap(C.union(self._t, table._t))
+
+    def distributed_union(self, table: "Table") -> "Table":
+        return self._wrap(C.distributed_union(self._t, table._t))
+
+    def subtract(self, table: "Table") -> "Table":
+        return self._wrap(C.subtract(self._t, table._t))
+
+    def distributed_subtract(self, table: "Table") -> "Table":
+        return self._wrap(C.distributed_subtract(self._t, table._t))
+
+    def intersect(self, table: "Table") -> "Table":
+        return self._wrap(C.intersect(self._t, table._t))
+
+    def distributed_intersect(self, table: "Table") -> "Table":
+        return self._wrap(C.distributed_intersect(self._t, table._t))
+
+    def unique(self, columns: List = None, keep: str = "first", inplace=False) -> Optional["Table"]:
+        out = self._wrap(C.unique(self._t, self._resolve_columns(columns), keep == "first"))
+        if inplace:
+            self._t = out._t
+            return None
+        return out
+
+    def distributed_unique(self, columns: List = None, keep: str = "first", inplace=False):
+        out = self._wrap(C.distributed_unique(self._t, self._resolve_columns(columns), keep == "first"))
+        if inplace:
+            self._t = out._t
+            return None
+        return out
+
+    # aggregates (global across ranks, reference table.pyx:548-586)
+    def _agg_op(self, column, op, quantile=0.5, ddof=1) -> "Table":
+        from .aggregates import resolve_op
+        return self._wrap(C.aggregate(self._t, self._resolve_column(column), int(resolve_op(op)), quantile, ddof,
+                                      True))
+
+    def sum(self, column):
+        return self._agg_op(column, "sum")
+
+    def count(self, column):
+        return self._agg_op(column, "count")
+
+    def min(self, column):
+        return self._agg_op(column, "min")
+
+    def max(self, column):
+        return self._agg_op(column, "max")
+
+    def mean(self, column):
+        return self._agg_op(column, "mean")
+
+    def var(self, column, ddof=1):
+        return self._agg_op(column, "var", ddof=ddof)
+
+    def std(self, column, ddof=1):
+        return self._agg_op(column, "std", ddof=ddof)
+
+    def nunique(self, column):
+        return self._agg_op(column, "nunique")
+
+    def quantile(self, column, q=0.5):
+        return self._agg_op(column, "quantile", quantile=q)
+
+    def groupby(self, index, agg: dict, algorithm: str = "hash") -> "Table":
+        """Distributed group-by (reference table.pyx:587-647 -> DistributedHashGroupBy).
+
+        agg: {column: op | [ops]} with ops as names ('sum','cnt'/'count','min','max','mean','var','std',
+        'nunique','quantile'/'median') or AggregationOp values.
+        """
+        from .aggregates import parse_agg
+        if not agg or not isinstance(agg, dict):
+            raise ValueError("agg should be non-empty and dict type")
+        keys = self._resolve_columns(index)
+        cols, ops, qs, ddofs = parse_agg(self, agg)
+        fn = C.distributed_hash_groupby if algorithm == "hash" else C.distributed_pipeline_groupby
+        return self._wrap(fn(self._t, keys, cols, ops, qs, ddofs))
+
+    def local_groupby(self, index, agg: dict, algorithm: str = "hash") -> "Table":
+        from .aggregates import parse_agg
+        keys = self._resolve_columns(index)
+        cols, ops, qs, ddofs = parse_agg(self, agg)
+        fn = C.hash_groupby if algorithm == "hash" else C.pipeline_groupby
+        return self._wrap(fn(self._t, keys, cols, ops, qs, ddofs))
+
+    def distributed_sort(self, order_by=None, ascending: Union[bool, List[bool]] = True,
+                         sort_options: SortOptions = None) -> "Table":
+        cols = self._resolve_columns(order_by if order_by is not None else 0)
+        asc = [bool(a) for a in ascending] if isinstance(ascending, (list, tuple)) else [bool(ascending)] * len(cols)
+        so = sort_options or SortOptions()
+        return self._wrap(C.distributed_sort(self._t, cols, asc, so.num_bins, so.num_samples))
+
     def project(self, columns: List) -> "Table":
         return self._wrap(C.project(self._t, self._resolve_columns(columns)))
 

@@ -1,0 +1,139 @@
+"""Sorting and partitioning tests (reference: cpp/test/partition_test.cpp,
+sorting_test.cpp, quick_sort_test.cpp)."""
+import struct
+
+import numpy as np
+import pandas as pd
+import pyarrow as pa
+import pytest
+import torch
+
+from cylon_amd import C, SortOptions, Table
+
+from dist_utils import run_distributed
+
+
+def murmur3_32(data: bytes, seed: int = 0) -> int:
+    """Plain-python MurmurHash3_x86_32 oracle."""
+    c1, c2 = 0xCC9E2D51, 0x1B873593
+    h = seed
+    n = len(data)
+    for i in range(0, n - n % 4, 4):
+        k = struct.unpack_from("<I", data, i)[0]
+        k = (k * c1) & 0xFFFFFFFF
+        k = ((k << 15) | (k >> 17)) & 0xFFFFFFFF
+        k = (k * c2) & 0xFFFFFFFF
+        h ^= k
+        h = ((h << 13) | (h >> 19)) & 0xFFFFFFFF
+        h = (h * 5 + 0xE6546B64) & 0xFFFFFFFF
+    tail = data[n - n % 4:]
+    k = 0
+    if len(tail) >= 3:
+        k ^= tail[2] << 16
+    if len(tail) >= 2:
+        k ^= tail[1] << 8
+    if len(tail) >= 1:
+        k ^= tail[0]
+        k = (k * c1) & 0xFFFFFFFF
+        k = ((k << 15) | (k >> 17)) & 0xFFFFFFFF
+        k = (k * c2) & 0xFFFFFFFF
+        h ^= k
+    h ^= n
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    h ^= h >> 16
+    return h
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 3, 4, 7, 8, 16])
+def test_modulo_partition_spec(ctx, nparts):
+    # partition_test.cpp:32-53: int keys -> (uint32)v % P
+    vals = np.arange(-50, 200, dtype=np.int64)
+    t = Table(pa.table({"v": vals}), ctx)
+    pid, counts = C.map_to_hash_partitions(t.native, [0], nparts)
+    exp = (vals.astype(np.uint32) % nparts)
+    assert np.array_equal(pid.numpy().astype(np.uint32), exp)
+    assert counts == np.bincount(exp, minlength=nparts).tolist()
+
+
+@pytest.mark.parametrize("nparts", [2, 5, 8])
+def test_murmur_partition_spec(ctx, nparts):
+    # partition_test.cpp:55-79: doubles -> MurmurHash3_x86_32(&v, 8, 0) % P
+    vals = np.random.default_rng(3).normal(size=300)
+    t = Table(pa.table({"d": vals, "s": [f"str{i}" for i in range(300)]}), ctx)
+    pid, _ = C.map_to_hash_partitions(t.native, [0], nparts)
+    exp = [murmur3_32(struct.pack("<d", v)) % nparts for v in vals]
+    assert pid.numpy().astype(np.uint32).tolist() == exp
+    pid, _ = C.map_to_hash_partitions(t.native, [1], nparts)
+    exp = [murmur3_32(f"str{i}".encode()) % nparts for i in range(300)]
+    assert pid.numpy().astype(np.uint32).tolist() == exp
+    # multi-column chain: h = 31 * h + f(v)
+    pid, _ = C.map_to_hash_partitions(t.native, [0, 1], nparts)
+    exp = [((31 * murmur3_32(struct.pack("<d", v))) + murmur3_32(f"str{i}".encode())) % (1 << 32) % nparts
+           for i, v in enumerate(vals)]
+    assert pid.numpy().astype(np.uint32).tolist() == exp
+
+
+def test_split_is_stable(ctx):
+    t = Table(pa.table({"k": np.arange(1000) % 7, "i": np.arange(1000)}), ctx)
+    parts = t.hash_partition(["k"], 4)
+    for p in parts:
+        assert np.all(np.diff(p.to_pandas()["i"].to_numpy()) > 0)
+    assert sum(p.row_count for p in parts) == 1000
+
+
+@pytest.mark.parametrize("asc", [True, False])
+def test_local_sort_vs_pandas(ctx, asc):
+    rng = np.random.default_rng(0)
+    n = 3000
+    df = pd.DataFrame({"a": rng.integers(-5, 5, n), "b": rng.normal(size=n), "s": [f"s{x % 13}" for x in range(n)],
+                       "i": np.arange(n)})
+    t = Table.from_pandas(ctx, df)
+    for cols in (["a"], ["a", "b"], ["s", "a"], ["b"]):
+        got = t.sort(cols, ascending=asc).to_pandas()
+        exp = df.sort_values(cols, ascending=asc, kind="stable").reset_index(drop=True)
+        pd.testing.assert_frame_equal(got, exp)
+    got = t.sort(["a", "s"], ascending=[True, False]).to_pandas()
+    exp = df.sort_values(["a", "s"], ascending=[True, False], kind="stable").reset_index(drop=True)
+    pd.testing.assert_frame_equal(got, exp)
+
+
+def test_sort_nulls_last(ctx):
+    t = Table(pa.table({"a": pa.array([3, None, 1, None, 2])}), ctx)
+    assert t.sort("a").to_pydict()["a"] == [1, 2, 3, None, None]
+    assert t.sort("a", ascending=False).to_pydict()["a"] == [3, 2, 1, None, None]
+
+
+def _dist_sort(ctx, asc):
+    rng = np.random.default_rng(ctx.get_rank())
+    n = 2000
+    df = pd.DataFrame({"a": rng.integers(0, 10000, n), "b": rng.random(n)})
+    t = Table.from_pandas(ctx, df)
+    s = t.distributed_sort(["a", "b"], ascending=asc, sort_options=SortOptions(num_bins=0, num_samples=0))
+    total = s.count("a").to_pydict()["a"][0]
+    return s.to_pandas(), df, total
+
+
+@pytest.mark.parametrize("asc", [True, False])
+def test_distributed_sort_global_order(asc):
+    world = 4
+    res = run_distributed(_dist_sort, world, asc)
+    parts = [r[0] for r in res]
+    allin = pd.concat([r[1] for r in res])
+    for r in res:
+        assert r[2] == len(allin)  # row count preserved (distributed Count)
+    got = pd.concat(parts).reset_index(drop=True)
+    exp = allin.sort_values(["a", "b"], ascending=asc).reset_index(drop=True)
+    pd.testing.assert_frame_equal(got, exp)
+
+
+def test_range_partition_monotonic(ctx):
+    vals = np.random.default_rng(1).integers(0, 1 << 40, 5000)
+    t = Table(pa.table({"v": vals}), ctx)
+    pid, counts = C.map_to_sort_partitions(t.native, 0, 4, True, 0, 0)
+    pid = pid.numpy().astype(np.int64)
+    order = np.argsort(vals, kind="stable")
+    assert np.all(np.diff(pid[order]) >= 0)
+    assert sum(counts) == 5000
