@@ -95,6 +95,15 @@ CYLON_HD uint32_t murmur3_32_u16(uint16_t v) {
   return fmix32(h1);
 }
 
+// Slot of a 64-bit key in a power-of-two table of 2^(64-shift) slots: the TOP
+// bits of the mixed key.  The join radix-partitions its inputs by the top
+// bits of the same hash, so partition-major probe/build order walks the table
+// front to back and the active window of the table stays cache resident.
+CYLON_HD uint64_t slot_of(uint64_t k, int shift) { return fmix64(k) >> shift; }
+
+// radix partition id of a key for 2^bits partitions (consistent with slot_of)
+CYLON_HD uint32_t radix_part_of(uint64_t k, int bits) { return (uint32_t)(fmix64(k) >> (64 - bits)); }
+
 CYLON_HD uint32_t partitioner(uint32_t h, uint32_t nparts) {
   return (nparts & (nparts - 1)) == 0 ? (h & (nparts - 1)) : (h % nparts);
 }

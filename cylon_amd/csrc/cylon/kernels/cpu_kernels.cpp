@@ -225,8 +225,9 @@ void hash_table_init(HashSlot *table, int64_t cap, void *) {
 
 void hash_build(const int64_t *keys, int64_t n, HashSlot *table, int64_t cap, void *) {
   const uint64_t mask = (uint64_t)cap - 1;
+  const int shift = 64 - __builtin_ctzll((unsigned long long)cap);
   for (int64_t i = 0; i < n; ++i) {
-    uint64_t slot = hashing::fmix64((uint64_t)keys[i]) & mask;
+    uint64_t slot = hashing::slot_of((uint64_t)keys[i], shift);
     while (table[slot].row >= 0) slot = (slot + 1) & mask;
     table[slot].row = i;
     table[slot].key = keys[i];
@@ -235,9 +236,10 @@ void hash_build(const int64_t *keys, int64_t n, HashSlot *table, int64_t cap, vo
 
 void hash_probe_count(const int64_t *keys, int64_t n, const HashSlot *table, int64_t cap, int64_t *counts, void *) {
   const uint64_t mask = (uint64_t)cap - 1;
+  const int shift = 64 - __builtin_ctzll((unsigned long long)cap);
   for (int64_t i = 0; i < n; ++i) {
     const int64_t k = keys[i];
-    uint64_t slot = hashing::fmix64((uint64_t)k) & mask;
+    uint64_t slot = hashing::slot_of((uint64_t)k, shift);
     int64_t c = 0;
     while (table[slot].row >= 0) {
       c += table[slot].key == k;
@@ -250,12 +252,13 @@ void hash_probe_count(const int64_t *keys, int64_t n, const HashSlot *table, int
 void hash_probe_write(const int64_t *keys, int64_t n, const HashSlot *table, int64_t cap, const int64_t *offsets,
                       int64_t *out_p, int64_t *out_b, void *) {
   const uint64_t mask = (uint64_t)cap - 1;
+  const int shift = 64 - __builtin_ctzll((unsigned long long)cap);
   for (int64_t i = 0; i < n; ++i) {
     int64_t o = offsets[i];
     const int64_t end = offsets[i + 1];
     if (o == end) continue;
     const int64_t k = keys[i];
-    uint64_t slot = hashing::fmix64((uint64_t)k) & mask;
+    uint64_t slot = hashing::slot_of((uint64_t)k, shift);
     while (o < end && table[slot].row >= 0) {
       if (table[slot].key == k) {
         out_p[o] = i;
@@ -274,6 +277,10 @@ void rows_equal(const ColView *l, const ColView *r, int ncols, const int64_t *li
     for (int c = 0; c < ncols && e; ++c) e = value_equal(l[c], li[j], r[c], ri[j]);
     eq[j] = e ? 1 : 0;
   }
+}
+
+void radix_partition_ids(const int64_t *keys, int64_t n, int bits, uint32_t *pid, void *) {
+  for (int64_t i = 0; i < n; ++i) pid[i] = hashing::radix_part_of((uint64_t)keys[i], bits);
 }
 
 void mark_indices(const int64_t *idx, int64_t m, uint8_t *flags, void *) {

@@ -39,10 +39,11 @@ void hash_table_init(HashSlot *table, int64_t cap, void *stream) {
 
 __global__ void k_hash_build(const int64_t *__restrict__ keys, int64_t n, HashSlot *table, int64_t cap) {
   const uint64_t mask = (uint64_t)cap - 1;
+  const int shift = 64 - __builtin_ctzll((unsigned long long)cap);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const int64_t k = keys[i];
-    uint64_t slot = hashing::fmix64((uint64_t)k) & mask;
+    uint64_t slot = hashing::slot_of((uint64_t)k, shift);
     while (true) {
       unsigned long long *rowp = reinterpret_cast<unsigned long long *>(&table[slot].row);
       const unsigned long long prev = atomicCAS(rowp, ~0ull, (unsigned long long)i);
@@ -64,10 +65,11 @@ void hash_build(const int64_t *keys, int64_t n, HashSlot *table, int64_t cap, vo
 __global__ void k_hash_probe_count(const int64_t *__restrict__ keys, int64_t n, const HashSlot *__restrict__ table,
                                    int64_t cap, int64_t *__restrict__ counts) {
   const uint64_t mask = (uint64_t)cap - 1;
+  const int shift = 64 - __builtin_ctzll((unsigned long long)cap);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const int64_t k = keys[i];
-    uint64_t slot = hashing::fmix64((uint64_t)k) & mask;
+    uint64_t slot = hashing::slot_of((uint64_t)k, shift);
     int64_t c = 0;
     while (true) {
       const HashSlot s = table[slot];
@@ -91,13 +93,14 @@ __global__ void k_hash_probe_write(const int64_t *__restrict__ keys, int64_t n, 
                                    int64_t cap, const int64_t *__restrict__ offsets, int64_t *__restrict__ out_p,
                                    int64_t *__restrict__ out_b) {
   const uint64_t mask = (uint64_t)cap - 1;
+  const int shift = 64 - __builtin_ctzll((unsigned long long)cap);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     int64_t o = offsets[i];
     const int64_t end = offsets[i + 1];
     if (o == end) continue;
     const int64_t k = keys[i];
-    uint64_t slot = hashing::fmix64((uint64_t)k) & mask;
+    uint64_t slot = hashing::slot_of((uint64_t)k, shift);
     while (o < end) {
       const HashSlot s = table[slot];
       if (s.row < 0) break;
@@ -223,6 +226,18 @@ void rows_equal(const ColView *l, const ColView *r, int ncols, const int64_t *li
   }
   hipLaunchKernelGGL(k_rows_equal, dim3(grid_for(m)), dim3(kBlock), 0, as_stream(stream), a, b, ncols, li, ri, m,
                      eq);
+  HIP_LAUNCH_CHECK();
+}
+
+__global__ void k_radix_part_ids(const int64_t *__restrict__ keys, int64_t n, int bits, uint32_t *__restrict__ pid) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    pid[i] = hashing::radix_part_of((uint64_t)keys[i], bits);
+}
+
+void radix_partition_ids(const int64_t *keys, int64_t n, int bits, uint32_t *pid, void *stream) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_radix_part_ids, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), keys, n, bits, pid);
   HIP_LAUNCH_CHECK();
 }
 

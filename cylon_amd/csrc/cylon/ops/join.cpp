@@ -78,7 +78,32 @@ static std::pair<at::Tensor, at::Tensor> hash_join_pairs(const Exec &ex, const a
   return build_left ? std::make_pair(bo, po) : std::make_pair(po, bo);
 }
 
+// Build side rows above which both inputs are radix-partitioned (all columns)
+// by the top bits of the key hash before the hash join, so the build atomics,
+// the probes and the payload gathers all walk a cache-resident window.
+static constexpr int64_t kPartitionJoinRows = int64_t(1) << 23;
+
+static int partition_bits(int64_t rows) {
+  int b = 0;
+  while (b < 12 && (rows >> (b + 1)) >= (int64_t(1) << 16)) ++b;  // >= 64K rows per partition
+  return b;
+}
+
+static TablePtr radix_reorder(const Exec &ex, const TablePtr &t, const at::Tensor &keys, int bits) {
+  at::Tensor pid = ex.empty_u32(t->Rows());
+  KCALL(ex, radix_partition_ids, ptr<int64_t>(keys), t->Rows(), bits, ptr<uint32_t>(pid));
+  return PartitionReorder(t, pid, 1u << bits).first;
+}
+
+static std::pair<at::Tensor, at::Tensor> join_impl(TablePtr left, TablePtr right, const JoinConfig &cfg,
+                                                   bool allow_reorder, TablePtr *lout, TablePtr *rout);
+
 std::pair<at::Tensor, at::Tensor> JoinIndices(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
+  return join_impl(left, right, cfg, false, nullptr, nullptr);
+}
+
+static std::pair<at::Tensor, at::Tensor> join_impl(TablePtr left, TablePtr right, const JoinConfig &cfg,
+                                                   bool allow_reorder, TablePtr *lout, TablePtr *rout) {
   const auto &lc = cfg.GetLeftColumnIdx();
   const auto &rc = cfg.GetRightColumnIdx();
   CYLON_CHECK(lc.size() == rc.size(), Code::Invalid, "left/right key counts differ");
@@ -97,6 +122,16 @@ std::pair<at::Tensor, at::Tensor> JoinIndices(const TablePtr &left, const TableP
                      left->column(lc[0]).type == right->column(rc[0]).type;
   KeyEncoding lk = encode_keys(ex, left, lc, exact);
   KeyEncoding rk = encode_keys(ex, right, rc, exact);
+  if (allow_reorder && exact && ex.gpu && cfg.GetAlgorithm() == JoinAlgorithm::HASH &&
+      std::min(left->Rows(), right->Rows()) >= kPartitionJoinRows) {
+    const int bits = partition_bits(std::min(left->Rows(), right->Rows()));
+    left = radix_reorder(ex, left, lk.keys, bits);
+    right = radix_reorder(ex, right, rk.keys, bits);
+    lk = encode_keys(ex, left, lc, exact);
+    rk = encode_keys(ex, right, rc, exact);
+  }
+  if (lout) *lout = left;
+  if (rout) *rout = right;
 
   std::pair<at::Tensor, at::Tensor> pr;
   if (cfg.GetAlgorithm() == JoinAlgorithm::SORT)
@@ -141,12 +176,13 @@ std::pair<at::Tensor, at::Tensor> JoinIndices(const TablePtr &left, const TableP
 }
 
 TablePtr Join(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
-  auto idx = JoinIndices(left, right, cfg);
+  TablePtr l = left, r = right;
+  auto idx = join_impl(left, right, cfg, true, &l, &r);
   const JoinType jt = cfg.GetType();
   const bool lnull = jt == JoinType::RIGHT || jt == JoinType::FULL_OUTER;
   const bool rnull = jt == JoinType::LEFT || jt == JoinType::FULL_OUTER;
-  TablePtr lo = GatherNullable(left, idx.first, lnull);
-  TablePtr ro = GatherNullable(right, idx.second, rnull);
+  TablePtr lo = GatherNullable(l, idx.first, lnull);
+  TablePtr ro = GatherNullable(r, idx.second, rnull);
   std::vector<Column> cols;
   cols.reserve(lo->Columns() + ro->Columns());
   for (const auto &c : lo->columns()) cols.push_back(c.with_name(cfg.GetLeftTablePrefix() + c.name));
