@@ -216,57 +216,113 @@ void key64_from_column(const ColView &col, int64_t n, int64_t *out, void *) {
   for (int64_t i = 0; i < n; ++i) out[i] = extend_bits(load_bits(col.data, i, col.width), col.width, col.kind);
 }
 
-void hash_table_init(HashSlot *table, int64_t cap, void *) {
-  for (int64_t i = 0; i < cap; ++i) {
+void hash_table_init(HashSlot *table, int64_t tsize, void *) {
+  for (int64_t i = 0; i < tsize; ++i) {
     table[i].key = 0;
     table[i].row = -1;
   }
 }
 
-void hash_build(const int64_t *keys, int64_t n, HashSlot *table, int64_t cap, void *) {
-  const uint64_t mask = (uint64_t)cap - 1;
-  const int shift = 64 - __builtin_ctzll((unsigned long long)cap);
+static inline int64_t next_slot(int64_t s, int64_t tsize) { return (s + 1 == tsize) ? 0 : s + 1; }
+
+void hash_build(const int64_t *keys, int64_t n, HashTableRef t, void *) {
   for (int64_t i = 0; i < n; ++i) {
-    uint64_t slot = hashing::slot_of((uint64_t)keys[i], shift);
-    while (table[slot].row >= 0) slot = (slot + 1) & mask;
-    table[slot].row = i;
-    table[slot].key = keys[i];
+    int64_t slot = (int64_t)hashing::slot_of((uint64_t)keys[i], t.shift);
+    while (t.slots[slot].row >= 0) slot = next_slot(slot, t.tsize);
+    t.slots[slot].row = i;
+    t.slots[slot].key = keys[i];
   }
 }
 
-void hash_probe_count(const int64_t *keys, int64_t n, const HashSlot *table, int64_t cap, int64_t *counts, void *) {
-  const uint64_t mask = (uint64_t)cap - 1;
-  const int shift = 64 - __builtin_ctzll((unsigned long long)cap);
+int64_t hash_build_sorted_workspace(int64_t) { return 1; }
+
+int hash_build_sorted(const int64_t *keys, int64_t n, int shift, int64_t *, uint64_t *ka, int64_t *va, uint64_t *kb,
+                      int64_t *vb, int64_t *maxpos, void *) {
+  std::vector<int64_t> idx(n);
+  for (int64_t i = 0; i < n; ++i) idx[i] = i;
+  std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) {
+    return hashing::slot_of((uint64_t)keys[x], shift) < hashing::slot_of((uint64_t)keys[y], shift);
+  });
+  int64_t run = INT64_MIN;
+  for (int64_t i = 0; i < n; ++i) {
+    ka[i] = (uint64_t)keys[idx[i]];
+    va[i] = idx[i];
+    const int64_t t = (int64_t)hashing::slot_of(ka[i], shift) - i;
+    run = t > run ? t : run;
+    reinterpret_cast<int64_t *>(kb)[i] = run;
+  }
+  *maxpos = n ? reinterpret_cast<int64_t *>(kb)[n - 1] : 0;
+  (void)vb;
+  return 0;
+}
+
+void hash_table_place(const uint64_t *skeys, const int64_t *srows, const int64_t *pmax, int64_t n, HashTableRef t,
+                      void *) {
+  for (int64_t i = 0; i < n; ++i) {
+    t.slots[pmax[i] + i].key = (int64_t)skeys[i];
+    t.slots[pmax[i] + i].row = srows[i];
+  }
+}
+
+void hash_probe_count(const int64_t *keys, int64_t n, HashTableRef t, int64_t *counts, void *) {
   for (int64_t i = 0; i < n; ++i) {
     const int64_t k = keys[i];
-    uint64_t slot = hashing::slot_of((uint64_t)k, shift);
+    int64_t slot = (int64_t)hashing::slot_of((uint64_t)k, t.shift);
     int64_t c = 0;
-    while (table[slot].row >= 0) {
-      c += table[slot].key == k;
-      slot = (slot + 1) & mask;
+    while (t.slots[slot].row >= 0) {
+      c += t.slots[slot].key == k;
+      slot = next_slot(slot, t.tsize);
     }
     counts[i] = c;
   }
 }
 
-void hash_probe_write(const int64_t *keys, int64_t n, const HashSlot *table, int64_t cap, const int64_t *offsets,
-                      int64_t *out_p, int64_t *out_b, void *) {
-  const uint64_t mask = (uint64_t)cap - 1;
-  const int shift = 64 - __builtin_ctzll((unsigned long long)cap);
+void hash_probe_write(const int64_t *keys, int64_t n, HashTableRef t, const int64_t *offsets, int64_t *out_p,
+                      int64_t *out_b, void *) {
   for (int64_t i = 0; i < n; ++i) {
     int64_t o = offsets[i];
     const int64_t end = offsets[i + 1];
     if (o == end) continue;
     const int64_t k = keys[i];
-    uint64_t slot = hashing::slot_of((uint64_t)k, shift);
-    while (o < end && table[slot].row >= 0) {
-      if (table[slot].key == k) {
+    int64_t slot = (int64_t)hashing::slot_of((uint64_t)k, t.shift);
+    while (o < end && t.slots[slot].row >= 0) {
+      if (t.slots[slot].key == k) {
         out_p[o] = i;
-        out_b[o] = table[slot].row;
+        out_b[o] = t.slots[slot].row;
         ++o;
       }
-      slot = (slot + 1) & mask;
+      slot = next_slot(slot, t.tsize);
     }
+  }
+}
+
+void hash_probe_emit(const int64_t *keys, int64_t n, HashTableRef t, int64_t capacity, int64_t *counter,
+                     int64_t *out_p, int64_t *out_b, void *) {
+  int64_t o = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t k = keys[i];
+    int64_t slot = (int64_t)hashing::slot_of((uint64_t)k, t.shift);
+    while (t.slots[slot].row >= 0) {
+      if (t.slots[slot].key == k) {
+        if (o < capacity) {
+          out_p[o] = i;
+          out_b[o] = t.slots[slot].row;
+        }
+        ++o;
+      }
+      slot = next_slot(slot, t.tsize);
+    }
+  }
+  *counter = o;
+}
+
+int64_t max_scan_workspace(int64_t) { return 1; }
+
+void inclusive_max_scan(const int64_t *in, int64_t n, int64_t *out, int64_t *, void *) {
+  int64_t run = INT64_MIN;
+  for (int64_t i = 0; i < n; ++i) {
+    run = in[i] > run ? in[i] : run;
+    out[i] = run;
   }
 }
 
@@ -335,8 +391,17 @@ void sort_keys_from_column(const ColView &c, const int64_t *perm, int64_t n, boo
   const uint64_t mask = (nb == 64) ? ~0ull : ((1ull << nb) - 1);
   for (int64_t i = 0; i < n; ++i) {
     const int64_t s = perm ? perm[i] : i;
-    uint64_t k = order_image(load_bits(c.data, s, c.width), c.width, c.kind);
-    out[i] = desc ? (~k & mask) : k;
+    const uint64_t bits = load_bits(c.data, s, c.width);
+    uint64_t k = order_image(bits, c.width, c.kind);
+    k = desc ? (~k & mask) : k;
+    if (c.kind == static_cast<int>(ValueKind::FLOAT)) {  // NaN sorts last in both directions
+      const bool nan = c.width == 8 ? ((bits & 0x7ff0000000000000ull) == 0x7ff0000000000000ull &&
+                                       (bits & 0x000fffffffffffffull))
+                       : c.width == 4 ? ((bits & 0x7f800000ull) == 0x7f800000ull && (bits & 0x007fffffull))
+                                      : ((bits & 0x7c00ull) == 0x7c00ull && (bits & 0x03ffull));
+      if (nan) k = mask;
+    }
+    out[i] = k;
   }
 }
 

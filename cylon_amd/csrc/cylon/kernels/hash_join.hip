@@ -13,7 +13,7 @@
 // order (deterministic output).  Multi-column, nullable and var-width keys are
 // reduced to a 64-bit row hash first; candidate pairs are then confirmed by
 // rows_equal (null == null, pandas semantics).
-#include "device_common.hpp"
+#include "radix_pass.hpp"
 
 namespace cylon {
 namespace hip {
@@ -22,9 +22,9 @@ struct ColSet2 {
   ColView c[kMaxFusedCols];
 };
 
-__global__ void k_table_init(HashSlot *table, int64_t cap) {
+__global__ void k_table_init(HashSlot *table, int64_t tsize) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tsize; i += stride) {
     HashSlot s;
     s.key = 0;
     s.row = -1;
@@ -32,93 +32,213 @@ __global__ void k_table_init(HashSlot *table, int64_t cap) {
   }
 }
 
-void hash_table_init(HashSlot *table, int64_t cap, void *stream) {
-  hipLaunchKernelGGL(k_table_init, dim3(grid_for(cap)), dim3(kBlock), 0, as_stream(stream), table, cap);
+void hash_table_init(HashSlot *table, int64_t tsize, void *stream) {
+  hipLaunchKernelGGL(k_table_init, dim3(grid_for(tsize)), dim3(kBlock), 0, as_stream(stream), table, tsize);
   HIP_LAUNCH_CHECK();
 }
 
-__global__ void k_hash_build(const int64_t *__restrict__ keys, int64_t n, HashSlot *table, int64_t cap) {
-  const uint64_t mask = (uint64_t)cap - 1;
-  const int shift = 64 - __builtin_ctzll((unsigned long long)cap);
+__device__ __forceinline__ int64_t next_slot(int64_t s, int64_t tsize) { return (s + 1 == tsize) ? 0 : s + 1; }
+
+// atomic build (small build sides): CAS on the row word claims a slot
+__global__ void k_hash_build(const int64_t *__restrict__ keys, int64_t n, HashTableRef t) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const int64_t k = keys[i];
-    uint64_t slot = hashing::slot_of((uint64_t)k, shift);
+    int64_t slot = (int64_t)hashing::slot_of((uint64_t)k, t.shift);
     while (true) {
-      unsigned long long *rowp = reinterpret_cast<unsigned long long *>(&table[slot].row);
+      unsigned long long *rowp = reinterpret_cast<unsigned long long *>(&t.slots[slot].row);
       const unsigned long long prev = atomicCAS(rowp, ~0ull, (unsigned long long)i);
       if (prev == ~0ull) {
-        table[slot].key = k;
+        t.slots[slot].key = k;
         break;
       }
-      slot = (slot + 1) & mask;
+      slot = next_slot(slot, t.tsize);
     }
   }
 }
 
-void hash_build(const int64_t *keys, int64_t n, HashSlot *table, int64_t cap, void *stream) {
+void hash_build(const int64_t *keys, int64_t n, HashTableRef t, void *stream) {
   if (n == 0) return;
-  hipLaunchKernelGGL(k_hash_build, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), keys, n, table, cap);
+  hipLaunchKernelGGL(k_hash_build, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), keys, n, t);
   HIP_LAUNCH_CHECK();
 }
 
-__global__ void k_hash_probe_count(const int64_t *__restrict__ keys, int64_t n, const HashSlot *__restrict__ table,
-                                   int64_t cap, int64_t *__restrict__ counts) {
-  const uint64_t mask = (uint64_t)cap - 1;
-  const int shift = 64 - __builtin_ctzll((unsigned long long)cap);
+// ---- atomic-free build (large build sides) --------------------------------
+// (1) LSD radix sort of (key, row) by the key's slot (SlotDigit, 8-bit staged
+//     passes); (2) linear-probing placement of keys inserted in slot order is
+//     pos_i = i + max_{j<=i}(slot_j - j): one inclusive max-scan; (3) plain,
+//     sequential stores of the slots.  No atomics, no random writes.
+__global__ void k_slot_minus_index(const uint64_t *__restrict__ skeys, int64_t n, int shift,
+                                   int64_t *__restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    out[i] = (int64_t)hashing::slot_of(skeys[i], shift) - i;
+}
+
+int64_t hash_build_sorted_workspace(int64_t n) {
+  return std::max(stable_rank_workspace(n, kRadixBuckets), max_scan_workspace(n));
+}
+
+int hash_build_sorted(const int64_t *keys, int64_t n, int shift, int64_t *ws, uint64_t *ka, int64_t *va,
+                      uint64_t *kb, int64_t *vb, int64_t *maxpos, void *stream) {
+  hipStream_t s = as_stream(stream);
+  const int lg = 64 - shift;
+  uint64_t *kbuf[2] = {ka, kb};
+  int64_t *vbuf[2] = {va, vb};
+  int cur = -1;
+  for (int sh = 0; sh < lg; sh += kRadixBits) {
+    const uint64_t *kin = cur < 0 ? reinterpret_cast<const uint64_t *>(keys) : kbuf[cur];
+    const int64_t *vin = cur < 0 ? nullptr : vbuf[cur];
+    const int nxt = cur < 0 ? 0 : cur ^ 1;
+    radix_pass(SlotDigit{shift, sh}, kin, vin, kbuf[nxt], vbuf[nxt], n, ws, s);
+    cur = nxt;
+  }
+  // pos_i = i + max_{j<=i}(slot_j - j), written into the other buffer's value array
+  int64_t *t = vbuf[cur ^ 1];
+  hipLaunchKernelGGL(k_slot_minus_index, dim3(grid_for(n)), dim3(kBlock), 0, s, kbuf[cur], n, shift, t);
+  HIP_LAUNCH_CHECK();
+  int64_t *pm = reinterpret_cast<int64_t *>(kbuf[cur ^ 1]);
+  inclusive_max_scan(t, n, pm, ws, stream);
+  HIP_CHECK(hipMemcpyAsync(maxpos, pm + n - 1, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+  return cur;
+}
+
+__global__ void k_place(const uint64_t *__restrict__ skeys, const int64_t *__restrict__ srows,
+                        const int64_t *__restrict__ pmax, int64_t n, HashSlot *__restrict__ slots) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    HashSlot v;
+    v.key = (int64_t)skeys[i];
+    v.row = srows[i];
+    slots[pmax[i] + i] = v;
+  }
+}
+
+void hash_table_place(const uint64_t *skeys, const int64_t *srows, const int64_t *pmax, int64_t n, HashTableRef t,
+                      void *stream) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_place, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), skeys, srows, pmax, n, t.slots);
+  HIP_LAUNCH_CHECK();
+}
+
+// ---- probes ---------------------------------------------------------------
+__global__ void k_hash_probe_count(const int64_t *__restrict__ keys, int64_t n, HashTableRef t,
+                                   int64_t *__restrict__ counts) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const int64_t k = keys[i];
-    uint64_t slot = hashing::slot_of((uint64_t)k, shift);
+    int64_t slot = (int64_t)hashing::slot_of((uint64_t)k, t.shift);
     int64_t c = 0;
     while (true) {
-      const HashSlot s = table[slot];
+      const HashSlot s = t.slots[slot];
       if (s.row < 0) break;
       c += (s.key == k);
-      slot = (slot + 1) & mask;
+      slot = next_slot(slot, t.tsize);
     }
     counts[i] = c;
   }
 }
 
-void hash_probe_count(const int64_t *keys, int64_t n, const HashSlot *table, int64_t cap, int64_t *counts,
-                      void *stream) {
+void hash_probe_count(const int64_t *keys, int64_t n, HashTableRef t, int64_t *counts, void *stream) {
   if (n == 0) return;
-  hipLaunchKernelGGL(k_hash_probe_count, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), keys, n, table,
-                     cap, counts);
+  hipLaunchKernelGGL(k_hash_probe_count, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), keys, n, t, counts);
   HIP_LAUNCH_CHECK();
 }
 
-__global__ void k_hash_probe_write(const int64_t *__restrict__ keys, int64_t n, const HashSlot *__restrict__ table,
-                                   int64_t cap, const int64_t *__restrict__ offsets, int64_t *__restrict__ out_p,
+__global__ void k_hash_probe_write(const int64_t *__restrict__ keys, int64_t n, HashTableRef t,
+                                   const int64_t *__restrict__ offsets, int64_t *__restrict__ out_p,
                                    int64_t *__restrict__ out_b) {
-  const uint64_t mask = (uint64_t)cap - 1;
-  const int shift = 64 - __builtin_ctzll((unsigned long long)cap);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     int64_t o = offsets[i];
     const int64_t end = offsets[i + 1];
     if (o == end) continue;
     const int64_t k = keys[i];
-    uint64_t slot = hashing::slot_of((uint64_t)k, shift);
+    int64_t slot = (int64_t)hashing::slot_of((uint64_t)k, t.shift);
     while (o < end) {
-      const HashSlot s = table[slot];
+      const HashSlot s = t.slots[slot];
       if (s.row < 0) break;
       if (s.key == k) {
         out_p[o] = i;
         out_b[o] = s.row;
         ++o;
       }
-      slot = (slot + 1) & mask;
+      slot = next_slot(slot, t.tsize);
     }
   }
 }
 
-void hash_probe_write(const int64_t *keys, int64_t n, const HashSlot *table, int64_t cap, const int64_t *offsets,
-                      int64_t *out_probe, int64_t *out_build, void *stream) {
+void hash_probe_write(const int64_t *keys, int64_t n, HashTableRef t, const int64_t *offsets, int64_t *out_probe,
+                      int64_t *out_build, void *stream) {
   if (n == 0) return;
-  hipLaunchKernelGGL(k_hash_probe_write, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), keys, n, table,
-                     cap, offsets, out_probe, out_build);
+  hipLaunchKernelGGL(k_hash_probe_write, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), keys, n, t, offsets,
+                     out_probe, out_build);
+  HIP_LAUNCH_CHECK();
+}
+
+// Single-pass probe: each wave counts its matches, reserves output space with
+// ONE atomic add (wave64 shuffle scan of the per-lane counts) and re-walks the
+// chains (now L1/L2 hot) to write its pairs.  Output order across waves is not
+// deterministic.  If the reservation exceeds `capacity` nothing more is
+// written and the caller falls back to the exact two-pass probe.
+__global__ __launch_bounds__(kBlock) void k_hash_probe_emit(const int64_t *__restrict__ keys, int64_t n,
+                                                            HashTableRef t, int64_t capacity,
+                                                            unsigned long long *counter, int64_t *__restrict__ out_p,
+                                                            int64_t *__restrict__ out_b) {
+  const int lane = lane_id();
+  const int64_t wstride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~(kWave - 1)); base < n; base += wstride) {
+    const int64_t i = base + lane;
+    const bool active = i < n;
+    int64_t k = 0, slot0 = 0, c = 0;
+    if (active) {
+      k = keys[i];
+      slot0 = (int64_t)hashing::slot_of((uint64_t)k, t.shift);
+      int64_t slot = slot0;
+      while (true) {
+        const HashSlot s = t.slots[slot];
+        if (s.row < 0) break;
+        c += (s.key == k);
+        slot = next_slot(slot, t.tsize);
+      }
+    }
+    int64_t inc = c;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const int64_t x = __shfl_up(inc, d, kWave);
+      if (lane >= d) inc += x;
+    }
+    const int64_t total = __shfl(inc, kWave - 1, kWave);
+    if (total == 0) continue;
+    unsigned long long wbase = 0;
+    if (lane == 0) wbase = atomicAdd(counter, (unsigned long long)total);
+    wbase = __shfl(wbase, 0, kWave);
+    if ((int64_t)wbase + total > capacity) continue;  // overflow: counted, not written
+    int64_t o = (int64_t)wbase + inc - c;
+    if (c > 0) {
+      int64_t slot = slot0;
+      int64_t left = c;
+      while (left > 0) {
+        const HashSlot s = t.slots[slot];
+        if (s.key == k && s.row >= 0) {
+          out_p[o] = i;
+          out_b[o] = s.row;
+          ++o;
+          --left;
+        }
+        slot = next_slot(slot, t.tsize);
+      }
+    }
+  }
+}
+
+void hash_probe_emit(const int64_t *keys, int64_t n, HashTableRef t, int64_t capacity, int64_t *counter,
+                     int64_t *out_probe, int64_t *out_build, void *stream) {
+  hipStream_t s = as_stream(stream);
+  HIP_CHECK(hipMemsetAsync(counter, 0, sizeof(int64_t), s));
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_hash_probe_emit, dim3(grid_for(n)), dim3(kBlock), 0, s, keys, n, t, capacity,
+                     reinterpret_cast<unsigned long long *>(counter), out_probe, out_build);
   HIP_LAUNCH_CHECK();
 }
 

@@ -46,6 +46,13 @@ struct alignas(16) HashSlot {
   int64_t row;  // -1 = empty
 };
 
+// A hash table: tsize slots; a key's home slot is slot_of(key, shift) < 2^(64-shift) <= tsize.
+struct HashTableRef {
+  HashSlot *slots;
+  int64_t tsize;
+  int shift;
+};
+
 constexpr int kMaxFusedCols = 16;  // columns handled by one multi-column launch
 
 // Aggregation op ids, numerically identical to the reference

@@ -114,6 +114,107 @@ void exclusive_scan(const int64_t *in, int64_t n, int64_t *out, int64_t *ws, voi
 }
 
 // ---------------------------------------------------------------------------
+// inclusive max scan (hash-join placement: pos_i = i + max_{j<=i}(slot_j - j))
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t wave_inclusive_max(int64_t v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const int64_t t = __shfl_up(v, d, kWave);
+    if (lane >= d) v = t > v ? t : v;
+  }
+  return v;
+}
+
+// block-wide exclusive max (INT64_MIN identity) of one value per thread
+__device__ __forceinline__ int64_t block_exclusive_max(int64_t v, int64_t *lds_waves, int64_t *total) {
+  const int lane = lane_id();
+  const int wave = threadIdx.x / kWave;
+  const int64_t inc = wave_inclusive_max(v);
+  if (lane == kWave - 1) lds_waves[wave] = inc;
+  __syncthreads();
+  int64_t wave_off = INT64_MIN, tot = INT64_MIN;
+#pragma unroll
+  for (int w = 0; w < kBlock / kWave; ++w) {
+    const int64_t x = lds_waves[w];
+    if (w < wave) wave_off = x > wave_off ? x : wave_off;
+    tot = x > tot ? x : tot;
+  }
+  __syncthreads();
+  *total = tot;
+  int64_t prev = __shfl_up(inc, 1, kWave);
+  if (lane == 0) prev = INT64_MIN;
+  return prev > wave_off ? prev : wave_off;
+}
+
+__global__ __launch_bounds__(kBlock) void k_block_max(const int64_t *__restrict__ in, int64_t n,
+                                                      int64_t *__restrict__ out) {
+  __shared__ int64_t lds[kBlock / kWave];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int64_t m = INT64_MIN;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int64_t i = base + k;
+    if (i < n) m = in[i] > m ? in[i] : m;
+  }
+  int64_t tot;
+  block_exclusive_max(m, lds, &tot);
+  if (threadIdx.x == 0) out[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kBlock) void k_block_max_scan(const int64_t *__restrict__ in, int64_t n,
+                                                           const int64_t *__restrict__ carry_incl,
+                                                           int64_t *__restrict__ out) {
+  __shared__ int64_t lds[kBlock / kWave];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int64_t v[kScanItems];
+  int64_t m = INT64_MIN;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int64_t i = base + k;
+    v[k] = (i < n) ? in[i] : INT64_MIN;
+    m = v[k] > m ? v[k] : m;
+  }
+  int64_t tot;
+  int64_t run = block_exclusive_max(m, lds, &tot);
+  if (carry_incl && blockIdx.x > 0) {
+    const int64_t c = carry_incl[blockIdx.x - 1];
+    run = c > run ? c : run;
+  }
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int64_t i = base + k;
+    run = v[k] > run ? v[k] : run;
+    if (i < n) out[i] = run;
+  }
+}
+
+int64_t max_scan_workspace(int64_t n) {
+  const int64_t nb = (n + kScanTile - 1) / kScanTile;
+  if (nb <= 1) return 1;
+  return nb + nb + max_scan_workspace(nb);
+}
+
+void inclusive_max_scan(const int64_t *in, int64_t n, int64_t *out, int64_t *ws, void *stream) {
+  hipStream_t s = as_stream(stream);
+  if (n == 0) return;
+  const int64_t nb = (n + kScanTile - 1) / kScanTile;
+  if (nb == 1) {
+    hipLaunchKernelGGL(k_block_max_scan, dim3(1), dim3(kBlock), 0, s, in, n, (const int64_t *)nullptr, out);
+    HIP_LAUNCH_CHECK();
+    return;
+  }
+  int64_t *bmax = ws;
+  int64_t *bscan = ws + nb;
+  int64_t *sub = bscan + nb;
+  hipLaunchKernelGGL(k_block_max, dim3((unsigned)nb), dim3(kBlock), 0, s, in, n, bmax);
+  HIP_LAUNCH_CHECK();
+  inclusive_max_scan(bmax, nb, bscan, sub, stream);
+  hipLaunchKernelGGL(k_block_max_scan, dim3((unsigned)nb), dim3(kBlock), 0, s, in, n, (const int64_t *)bscan, out);
+  HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------
 // K11 compaction
 // ---------------------------------------------------------------------------
 constexpr int kCompactRounds = 16;                    // rounds of 256 rows per block

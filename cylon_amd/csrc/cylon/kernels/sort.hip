@@ -18,7 +18,7 @@
 //   * merge join: per left key a lower/upper bound search in the sorted right
 //     keys (count pass stores the lower bound), scan, and a write pass that
 //     expands the equal range into (left row, right row) pairs.
-#include "stable_rank.hpp"
+#include "radix_pass.hpp"
 
 namespace cylon {
 namespace hip {
@@ -43,6 +43,12 @@ __device__ __forceinline__ uint64_t order_image(uint64_t bits, int w, int kind) 
   return bits;
 }
 
+__device__ __forceinline__ bool is_nan_bits(uint64_t bits, int w) {
+  if (w == 8) return (bits & 0x7ff0000000000000ull) == 0x7ff0000000000000ull && (bits & 0x000fffffffffffffull);
+  if (w == 4) return (bits & 0x7f800000ull) == 0x7f800000ull && (bits & 0x007fffffull);
+  return (bits & 0x7c00ull) == 0x7c00ull && (bits & 0x03ffull);
+}
+
 __global__ void k_sort_keys(ColView c, const int64_t *__restrict__ perm, int64_t n, bool desc,
                             uint64_t *__restrict__ out) {
   const int nb = 8 * c.width;
@@ -50,8 +56,10 @@ __global__ void k_sort_keys(ColView c, const int64_t *__restrict__ perm, int64_t
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const int64_t s = perm ? perm[i] : i;
-    uint64_t k = order_image(load_bits(c.data, s, c.width), c.width, c.kind);
+    const uint64_t bits = load_bits(c.data, s, c.width);
+    uint64_t k = order_image(bits, c.width, c.kind);
     if (desc) k = ~k & mask;
+    if (c.kind == static_cast<int>(ValueKind::FLOAT) && is_nan_bits(bits, c.width)) k = mask;  // NaN last
     out[i] = k;
   }
 }
@@ -122,9 +130,7 @@ int radix_sort_pairs(uint64_t *keys, int64_t *vals, int64_t n, uint64_t *keys_al
   int64_t *vb[2] = {vals, vals_alt};
   for (int shift = begin_bit; shift < end_bit; shift += 8) {
     if (((diff >> shift) & 0xffull) == 0) continue;  // constant digit: pass is the identity
-    RadixDigit dg{kb[cur], shift};
-    RadixSink sk{kb[cur], vb[cur], kb[cur ^ 1], vb[cur ^ 1]};
-    stable_rank_launch(dg, sk, n, 256, ws + 2, s);
+    radix_pass(PlainDigit{shift}, kb[cur], vb[cur], kb[cur ^ 1], vb[cur ^ 1], n, ws + 2, s);
     cur ^= 1;
   }
   return cur;

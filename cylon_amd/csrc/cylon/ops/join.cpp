@@ -58,6 +58,13 @@ static KeyEncoding encode_keys(const Exec &ex, const TablePtr &t, const std::vec
   return {k, false};
 }
 
+// Build sides at least this large use the atomic-free sorted build (random
+// 64-bit CAS into a table far beyond the caches runs at the memory-side atomic
+// rate: 213 ms for 1B keys, profiles/); probe sides this large use the
+// single-pass probe.
+static constexpr int64_t kSortedBuildRows = int64_t(1) << 20;
+static constexpr int64_t kEmitProbeRows = int64_t(1) << 22;
+
 // inner-join index pairs on int64 keys via the K5 hash table (build = smaller side)
 static std::pair<at::Tensor, at::Tensor> hash_join_pairs(const Exec &ex, const at::Tensor &lk, const at::Tensor &rk) {
   const bool build_left = lk.numel() < rk.numel();
@@ -65,34 +72,55 @@ static std::pair<at::Tensor, at::Tensor> hash_join_pairs(const Exec &ex, const a
   const at::Tensor &pk = build_left ? rk : lk;
   const int64_t nb = bk.numel(), np = pk.numel();
   const int64_t cap = next_pow2(std::max<int64_t>(2 * nb, 64));
-  at::Tensor table = at::empty({cap * 2}, ex.opts(at::kLong));  // HashSlot = 2 x int64
-  HashSlot *tp = reinterpret_cast<HashSlot *>(table.data_ptr());
-  KCALL(ex, hash_table_init, tp, cap);
-  KCALL(ex, hash_build, ptr<int64_t>(bk), nb, tp, cap);
+  const int shift = 64 - __builtin_ctzll((unsigned long long)cap);
+  at::Tensor table;
+  HashTableRef t{nullptr, cap, shift};
+  if (ex.gpu && nb >= kSortedBuildRows) {
+    // atomic-free build: radix sort (key,row) by slot, prefix-max placement, sequential stores
+    at::Tensor ka = ex.empty_i64(nb), va = ex.empty_i64(nb), kb = ex.empty_i64(nb), vb = ex.empty_i64(nb);
+    at::Tensor mp = ex.empty_i64(1);
+    at::Tensor ws = ex.empty_i64(KSIZE(ex, hash_build_sorted_workspace, nb));
+    const int which = KCALL(ex, hash_build_sorted, ptr<int64_t>(bk), nb, shift, ptr<int64_t>(ws),
+                            reinterpret_cast<uint64_t *>(ptr<int64_t>(ka)), ptr<int64_t>(va),
+                            reinterpret_cast<uint64_t *>(ptr<int64_t>(kb)), ptr<int64_t>(vb), ptr<int64_t>(mp));
+    ws = at::Tensor();
+    const int64_t maxpos = read_i64(mp, 0) + nb - 1;
+    t.tsize = std::max<int64_t>(cap, maxpos + 2);
+    table = at::empty({t.tsize * 2}, ex.opts(at::kLong));  // HashSlot = 2 x int64
+    t.slots = reinterpret_cast<HashSlot *>(table.data_ptr());
+    KCALL(ex, hash_table_init, t.slots, t.tsize);
+    const at::Tensor &sk = which ? kb : ka;
+    const at::Tensor &sr = which ? vb : va;
+    const at::Tensor &pm = which ? ka : kb;
+    KCALL(ex, hash_table_place, reinterpret_cast<const uint64_t *>(ptr<int64_t>(sk)), ptr<int64_t>(sr),
+          ptr<int64_t>(pm), nb, t);
+  } else {
+    table = at::empty({cap * 2}, ex.opts(at::kLong));
+    t.slots = reinterpret_cast<HashSlot *>(table.data_ptr());
+    KCALL(ex, hash_table_init, t.slots, cap);
+    KCALL(ex, hash_build, ptr<int64_t>(bk), nb, t);
+  }
+  if (ex.gpu && np >= kEmitProbeRows) {
+    // single-pass probe into an over-allocated pair buffer; exact two-pass fallback on overflow
+    const int64_t capacity = np + np / 4 + 4096;
+    at::Tensor po = ex.empty_i64(capacity), bo = ex.empty_i64(capacity), cnt = ex.empty_i64(1);
+    KCALL(ex, hash_probe_emit, ptr<int64_t>(pk), np, t, capacity, ptr<int64_t>(cnt), ptr<int64_t>(po),
+          ptr<int64_t>(bo));
+    const int64_t m = read_i64(cnt, 0);
+    if (m <= capacity) {
+      po = po.slice(0, 0, m);
+      bo = bo.slice(0, 0, m);
+      return build_left ? std::make_pair(bo, po) : std::make_pair(po, bo);
+    }
+  }
   at::Tensor counts = ex.empty_i64(np);
-  KCALL(ex, hash_probe_count, ptr<int64_t>(pk), np, tp, cap, ptr<int64_t>(counts));
+  KCALL(ex, hash_probe_count, ptr<int64_t>(pk), np, t, ptr<int64_t>(counts));
   at::Tensor offs = exclusive_scan(ex, counts);
+  counts = at::Tensor();
   const int64_t m = read_i64(offs, np);
   at::Tensor po = ex.empty_i64(m), bo = ex.empty_i64(m);
-  KCALL(ex, hash_probe_write, ptr<int64_t>(pk), np, tp, cap, ptr<int64_t>(offs), ptr<int64_t>(po), ptr<int64_t>(bo));
+  KCALL(ex, hash_probe_write, ptr<int64_t>(pk), np, t, ptr<int64_t>(offs), ptr<int64_t>(po), ptr<int64_t>(bo));
   return build_left ? std::make_pair(bo, po) : std::make_pair(po, bo);
-}
-
-// Build side rows above which both inputs are radix-partitioned (all columns)
-// by the top bits of the key hash before the hash join, so the build atomics,
-// the probes and the payload gathers all walk a cache-resident window.
-static constexpr int64_t kPartitionJoinRows = int64_t(1) << 23;
-
-static int partition_bits(int64_t rows) {
-  int b = 0;
-  while (b < 12 && (rows >> (b + 1)) >= (int64_t(1) << 16)) ++b;  // >= 64K rows per partition
-  return b;
-}
-
-static TablePtr radix_reorder(const Exec &ex, const TablePtr &t, const at::Tensor &keys, int bits) {
-  at::Tensor pid = ex.empty_u32(t->Rows());
-  KCALL(ex, radix_partition_ids, ptr<int64_t>(keys), t->Rows(), bits, ptr<uint32_t>(pid));
-  return PartitionReorder(t, pid, 1u << bits).first;
 }
 
 static std::pair<at::Tensor, at::Tensor> join_impl(TablePtr left, TablePtr right, const JoinConfig &cfg,
@@ -122,14 +150,7 @@ static std::pair<at::Tensor, at::Tensor> join_impl(TablePtr left, TablePtr right
                      left->column(lc[0]).type == right->column(rc[0]).type;
   KeyEncoding lk = encode_keys(ex, left, lc, exact);
   KeyEncoding rk = encode_keys(ex, right, rc, exact);
-  if (allow_reorder && exact && ex.gpu && cfg.GetAlgorithm() == JoinAlgorithm::HASH &&
-      std::min(left->Rows(), right->Rows()) >= kPartitionJoinRows) {
-    const int bits = partition_bits(std::min(left->Rows(), right->Rows()));
-    left = radix_reorder(ex, left, lk.keys, bits);
-    right = radix_reorder(ex, right, rk.keys, bits);
-    lk = encode_keys(ex, left, lc, exact);
-    rk = encode_keys(ex, right, rc, exact);
-  }
+  (void)allow_reorder;  // hook for input reordering strategies (none profitable so far, see docs)
   if (lout) *lout = left;
   if (rout) *rout = right;
 

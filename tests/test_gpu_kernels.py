@@ -74,8 +74,9 @@ def test_join_gpu_vs_cpu(gpu_ctx, ctx, algorithm, how):
         assert _rows(res[0]) == _rows(res[1])
 
 
-def test_large_join_count_matches_pandas(gpu_ctx):
-    n = 2_000_000
+@pytest.mark.parametrize("n", [2_000_000, 6_000_000])
+def test_large_join_count_matches_pandas(gpu_ctx, n):
+    # 2M: sorted (atomic-free) build + two-pass probe; 6M: sorted build + single-pass emit probe
     g = torch.Generator(device="cuda").manual_seed(3)
     k1 = torch.randint(0, int(0.99 * n), (n,), generator=g, device="cuda")
     k2 = torch.randint(0, int(0.99 * n), (n,), generator=g, device="cuda")
