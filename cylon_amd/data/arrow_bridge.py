@@ -193,9 +193,10 @@ def column_from_tensor(name: str, t: torch.Tensor, validity: Optional[torch.Tens
          torch.uint16: T.UINT16, torch.uint32: T.UINT32, torch.uint64: T.UINT64}
     if t.dtype not in m:
         raise TypeError(f"unsupported tensor dtype {t.dtype}")
+    typ = m[t.dtype]
     if t.dtype == torch.bool:
         t = t.to(torch.uint8)
     t = t.contiguous().reshape(-1)
     if validity is not None:
         validity = validity.to(torch.uint8).contiguous().reshape(-1)
-    return C.Column(name, C.DataType(m[t.dtype] if t.dtype in m else T.UINT8), t.numel(), t, None, validity)
+    return C.Column(name, C.DataType(typ), t.numel(), t, None, validity)

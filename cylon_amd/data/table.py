@@ -13,6 +13,7 @@ import torch
 from .._lib import C
 from ..ctx.context import CylonContext
 from . import arrow_bridge as ab
+from .table_pandas import PandasOpsMixin
 
 _JOIN_TYPES = {"inner": "inner", "left": "left", "right": "right", "outer": "outer", "full_outer": "outer",
                "fullouter": "outer"}
@@ -42,7 +43,7 @@ class SortOptions:
         self.num_samples = int(num_samples)
 
 
-class Table:
+class Table(PandasOpsMixin):
     def __init__(self, pyarrow_table=None, context: Optional[CylonContext] = None, _native=None):
         self._ctx = _ensure_ctx(context)
         if _native is not None:

@@ -1,0 +1,226 @@
+"""Table indexing (reference: cpp/src/cylon/indexing/index.hpp:22-700,
+indexer.hpp:76-260, python/pycylon/indexing/index.pyx, python/pycylon/index.py).
+
+Index values live on the table's device as a tensor (numeric) or as an Arrow
+array (strings).  Lookups are device tensor searches (Linear), a lazily built
+value -> positions map (Hash) or arithmetic (Range).  Range-of-values `loc`
+selects from the first position of the start value to the last position of the
+end value, as the reference's LocIndexer does.
+"""
+from enum import IntEnum
+from typing import Any, List, Sequence
+
+import numpy as np
+import pyarrow as pa
+import torch
+
+
+class IndexingSchema(IntEnum):
+    RANGE = 0
+    LINEAR = 1
+    HASH = 2
+    BINARYTREE = 3
+    BTREE = 4
+
+
+class BaseIndex:
+    schema = IndexingSchema.LINEAR
+
+    def __init__(self, values, device: str = "cpu"):
+        if isinstance(values, (pa.Array, pa.ChunkedArray)):
+            arr = values.combine_chunks() if isinstance(values, pa.ChunkedArray) else values
+            if pa.types.is_integer(arr.type) or pa.types.is_floating(arr.type):
+                self._values = torch.from_numpy(arr.to_numpy(zero_copy_only=False).copy()).to(device)
+                self._arrow = None
+            else:
+                self._values = None
+                self._arrow = arr
+        elif torch.is_tensor(values):
+            self._values = values.to(device)
+            self._arrow = None
+        else:
+            arr = pa.array(list(values))
+            self.__init__(arr, device)
+            return
+        self.device = device
+
+    def __len__(self):
+        return len(self._values) if self._values is not None else len(self._arrow)
+
+    # ---- reference API ----------------------------------------------------
+    def get_index_array(self) -> pa.Array:
+        if self._values is not None:
+            return pa.array(self._values.cpu().numpy())
+        return self._arrow
+
+    def get_schema(self) -> IndexingSchema:
+        return self.schema
+
+    @property
+    def index_values(self) -> List[Any]:
+        return self.get_index_array().to_pylist()
+
+    @property
+    def values(self) -> np.ndarray:
+        return self.get_index_array().to_numpy(zero_copy_only=False)
+
+    def to(self, device: str) -> "BaseIndex":
+        return type(self)(self._values if self._values is not None else self._arrow, device)
+
+    def take(self, positions: torch.Tensor) -> "BaseIndex":
+        if self._values is not None:
+            return type(self)(self._values[positions.to(self._values.device)], self.device)
+        return type(self)(self._arrow.take(pa.array(positions.cpu().numpy())), self.device)
+
+    # ---- lookups ------------------------------------------------------------
+    def positions_of(self, value) -> torch.Tensor:
+        if self._values is not None:
+            return torch.nonzero(self._values == value, as_tuple=False).reshape(-1)
+        mask = np.asarray(self._arrow.to_numpy(zero_copy_only=False) == value)
+        return torch.from_numpy(np.nonzero(mask)[0].astype(np.int64))
+
+    def positions_of_list(self, values: Sequence) -> torch.Tensor:
+        parts = [self.positions_of(v) for v in values]
+        if not parts:
+            return torch.empty(0, dtype=torch.int64)
+        return torch.cat([p.to("cpu") for p in parts])
+
+    def range_positions(self, start, end) -> torch.Tensor:
+        s = self.positions_of(start)
+        e = self.positions_of(end)
+        if s.numel() == 0 or e.numel() == 0:
+            raise KeyError(f"index values {start!r}..{end!r} not found")
+        lo, hi = int(s.min()), int(e.max())
+        return torch.arange(lo, hi + 1, dtype=torch.int64)
+
+
+class LinearIndex(BaseIndex):
+    schema = IndexingSchema.LINEAR
+
+
+class HashIndex(BaseIndex):
+    schema = IndexingSchema.HASH
+
+    def __init__(self, values, device: str = "cpu"):
+        super().__init__(values, device)
+        self._map = None
+
+    def _build(self):
+        if self._map is None:
+            self._map = {}
+            for i, v in enumerate(self.index_values):
+                self._map.setdefault(v, []).append(i)
+
+    def positions_of(self, value) -> torch.Tensor:
+        self._build()
+        return torch.tensor(self._map.get(value, []), dtype=torch.int64)
+
+
+class RangeIndex(BaseIndex):
+    schema = IndexingSchema.RANGE
+
+    def __init__(self, start: int = 0, stop: int = 0, step: int = 1, device: str = "cpu"):
+        self.start, self.stop, self.step = int(start), int(stop), int(step)
+        self.device = device
+        self._values = None
+        self._arrow = None
+
+    @classmethod
+    def of_length(cls, n: int, device: str = "cpu"):
+        return cls(0, n, 1, device)
+
+    def __len__(self):
+        return max(0, (self.stop - self.start + self.step - 1) // self.step)
+
+    def get_index_array(self) -> pa.Array:
+        return pa.array(np.arange(self.start, self.stop, self.step, dtype=np.int64))
+
+    def to(self, device):
+        return RangeIndex(self.start, self.stop, self.step, device)
+
+    def take(self, positions: torch.Tensor) -> "BaseIndex":
+        vals = torch.arange(self.start, self.stop, self.step, dtype=torch.int64)[positions.cpu()]
+        return LinearIndex(vals, self.device)
+
+    def positions_of(self, value) -> torch.Tensor:
+        v = int(value)
+        if v < self.start or v >= self.stop or (v - self.start) % self.step:
+            return torch.empty(0, dtype=torch.int64)
+        return torch.tensor([(v - self.start) // self.step], dtype=torch.int64)
+
+
+def build_index(values, schema: IndexingSchema, device: str = "cpu") -> BaseIndex:
+    if schema == IndexingSchema.RANGE:
+        return RangeIndex.of_length(len(values), device)
+    if schema == IndexingSchema.HASH:
+        return HashIndex(values, device)
+    if schema in (IndexingSchema.LINEAR, IndexingSchema.BINARYTREE, IndexingSchema.BTREE):
+        return LinearIndex(values, device)
+    raise ValueError(f"unsupported indexing schema {schema}")
+
+
+class _Indexer:
+    def __init__(self, table):
+        self._t = table
+
+    def _cols(self, cols) -> List[int]:
+        t = self._t
+        if cols is None or (isinstance(cols, slice) and cols == slice(None)):
+            return list(range(t.column_count))
+        if isinstance(cols, slice):
+            a = 0 if cols.start is None else t._resolve_column(cols.start)
+            b = t.column_count - 1 if cols.stop is None else t._resolve_column(cols.stop)
+            return list(range(a, b + 1))
+        if isinstance(cols, (list, tuple)):
+            return [t._resolve_column(c) for c in cols]
+        return [t._resolve_column(cols)]
+
+    def _select(self, rows: torch.Tensor, cols):
+        t = self._t
+        sub = t.project(self._cols(cols))
+        out = sub.take(rows)
+        out._index = t.index.take(rows)
+        return out
+
+
+class LocIndexer(_Indexer):
+    """table.loc[rows, cols]: rows by index value / list of values / value range (inclusive)."""
+
+    def __getitem__(self, key):
+        rows, cols = (key if isinstance(key, tuple) else (key, None))
+        idx = self._t.index
+        if isinstance(rows, slice):
+            if rows.start is None and rows.stop is None:
+                pos = torch.arange(len(idx), dtype=torch.int64)
+            else:
+                start = rows.start if rows.start is not None else idx.index_values[0]
+                stop = rows.stop if rows.stop is not None else idx.index_values[-1]
+                pos = idx.range_positions(start, stop)
+        elif isinstance(rows, (list, tuple)):
+            pos = idx.positions_of_list(rows)
+        else:
+            pos = idx.positions_of(rows).cpu()
+        return self._select(pos, cols)
+
+
+class ILocIndexer(_Indexer):
+    """table.iloc[rows, cols]: positional rows (int / list / slice, exclusive stop) and columns."""
+
+    def __getitem__(self, key):
+        rows, cols = (key if isinstance(key, tuple) else (key, None))
+        n = self._t.row_count
+        if isinstance(rows, slice):
+            pos = torch.arange(n, dtype=torch.int64)[rows]
+        elif isinstance(rows, (list, tuple)):
+            pos = torch.tensor([r if r >= 0 else n + r for r in rows], dtype=torch.int64)
+        else:
+            r = int(rows)
+            pos = torch.tensor([r if r >= 0 else n + r], dtype=torch.int64)
+        if isinstance(cols, slice) and (cols.start is None or isinstance(cols.start, int)) and \
+                (cols.stop is None or isinstance(cols.stop, int)):
+            cols = list(range(self._t.column_count))[cols]
+        return self._select(pos, cols)
+
+
+__all__ = ["IndexingSchema", "BaseIndex", "LinearIndex", "HashIndex", "RangeIndex", "build_index", "LocIndexer",
+           "ILocIndexer"]

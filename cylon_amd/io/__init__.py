@@ -250,13 +250,15 @@ def write_parquet(table: Table, path: str, options: ParquetOptions = None):
 
 def write_arrow_ipc(table: Table, path: str):
     """Arrow IPC (Feather v2) serialisation of a device table."""
-    import pyarrow.feather as feather
-    feather.write_feather(table.to_arrow(), path)
+    at = table.to_arrow()
+    with pa.OSFile(path, "wb") as sink, pa.ipc.new_file(sink, at.schema) as writer:
+        writer.write_table(at)
 
 
 def read_arrow_ipc(context: CylonContext, path: str) -> Table:
-    import pyarrow.feather as feather
-    return Table(feather.read_table(path), _ensure_ctx(context))
+    with pa.memory_map(path, "r") as src:
+        at = pa.ipc.open_file(src).read_all()
+    return Table(at, _ensure_ctx(context))
 
 
 __all__ = ["CSVReadOptions", "CSVWriteOptions", "ParquetOptions", "read_csv", "write_csv", "read_parquet",

@@ -1,0 +1,117 @@
+"""DataFrame / CylonEnv frontend (reference: python/test/test_frame.py) and the indexing
+golden files (cpp/test/indexing_test.cpp, data/output/indexing_loc_{hl,r}_{1..9}.csv)."""
+import os
+
+import numpy as np
+import pandas as pd
+import pyarrow as pa
+import pyarrow.csv as pacsv
+import pytest
+
+from cylon_amd import CylonEnv, DataFrame, GlooConfig, IndexingSchema, Table
+
+from dist_utils import run_distributed
+
+
+def _rows(at):
+    return sorted(tuple(r.values()) for r in at.to_pylist())
+
+
+# indexing_test.cpp: index built on column 'a' (hash/linear) or a range index; data = b, c, d
+LOC_CASES = {
+    1: lambda t: t.loc[0:5, 0],
+    2: lambda t: t.loc[0:5, 0:1],
+    3: lambda t: t.loc[0:5, [0, 2]],
+    4: lambda t: t.loc[10, 1],
+    5: lambda t: t.loc[[4, 10], 1:2],
+    6: lambda t: t.loc[[4, 10], [0, 2]],
+    7: lambda t: t.loc[4, [0, 1]],
+    8: lambda t: t.loc[4, 1:2],
+    9: lambda t: t.loc[[4, 10], 0],
+}
+
+
+@pytest.mark.parametrize("schema", [IndexingSchema.HASH, IndexingSchema.LINEAR, IndexingSchema.RANGE])
+@pytest.mark.parametrize("case", sorted(LOC_CASES))
+def test_loc_golden(ctx, data_dir, schema, case):
+    at = pacsv.read_csv(os.path.join(data_dir, "input", "indexing_data.csv"))
+    t = Table(at, ctx)
+    if schema == IndexingSchema.RANGE:
+        t = t.drop(["a"])
+        t.set_index(list(range(t.row_count)), IndexingSchema.RANGE)
+        tag = "r"
+    else:
+        t.set_index("a", schema, drop=True)
+        tag = "hl"
+    got = LOC_CASES[case](t).to_arrow()
+    exp = pacsv.read_csv(os.path.join(data_dir, "output", f"indexing_loc_{tag}_{case}.csv"))
+    assert _rows(got.rename_columns(exp.column_names)) == _rows(exp)
+
+
+def test_indexing_schema_switch(ctx):
+    t = Table(pa.table({"k": [5, 6, 7], "v": [1, 2, 3]}), ctx)
+    t.set_index("k", IndexingSchema.HASH, drop=True)
+    assert t.indexing_schema == IndexingSchema.HASH
+    t.indexing_schema = IndexingSchema.LINEAR
+    assert t.loc[6].to_pydict() == {"v": [2]}
+
+
+def test_dataframe_basics(ctx):
+    df = DataFrame({"a": [3, 1, 2, 1], "b": [0.5, 1.5, None, 2.5]}, context=ctx)
+    assert df.shape == (4, 2) and df.columns == ["a", "b"]
+    assert df.sort_values(by="a").to_dict()["a"] == [1, 1, 2, 3]
+    assert df.drop_duplicates(subset=["a"]).to_dict()["a"] == [3, 1, 2]
+    assert df.drop_duplicates(subset=["a"], keep="last").to_dict()["b"] == [0.5, None, 2.5]
+    assert df.fillna(0).to_dict()["b"] == [0.5, 1.5, 0.0, 2.5]
+    assert df[df["a"] > 1].shape == (2, 2)
+    assert (df + 1).to_dict()["a"] == [4, 2, 3, 2]
+    df["c"] = 1
+    assert df.columns == ["a", "b", "c"]
+    assert df.isnull().to_dict()["b"][2] is True
+    cpu = df.to_cpu()
+    assert cpu.is_cpu() and cpu.device == "cpu"
+    assert df.groupby("a", {"c": "sum"}).sort_values(by="a").to_dict() == {"a": [1, 2, 3], "sum_c": [2, 1, 1]}
+
+
+def test_dataframe_merge_join_concat(ctx):
+    l = DataFrame({"k": [1, 2, 3], "x": ["a", "b", "c"]}, context=ctx)
+    r = DataFrame({"k": [2, 3, 4], "y": [20, 30, 40]}, context=ctx)
+    m = l.merge(r, how="inner", on=["k"], suffixes=("l_", "r_")).to_pandas()
+    assert sorted(m["l_k"].tolist()) == [2, 3]
+    m = l.merge(r, how="outer", algorithm="hash", left_on=["k"], right_on=["k"]).to_pandas()
+    assert len(m) == 4
+    r2 = r.set_index("k", drop=False)
+    j = l.join(r2, on="k", how="left").to_pandas()
+    assert len(j) == 3
+    c = DataFrame.concat([l, l], axis=0)
+    assert c.shape == (3, 2)  # reference concat(axis=0) is a set union
+    c1 = DataFrame.concat([l, r], axis=1)
+    assert c1.shape[0] == 3
+
+
+def _dist_frame(ctx):
+    env = CylonEnv.__new__(CylonEnv)
+    env._context, env._distributed, env._finalized = ctx, True, True
+    rank = ctx.get_rank()
+    l = DataFrame({"k": np.arange(rank * 10, rank * 10 + 10) % 7, "x": np.arange(10) + rank * 100})
+    r = DataFrame({"k": np.arange(7), "y": np.arange(7) * 10})
+    j = l.merge(r, on=["k"], env=env).to_pandas()
+    s = l.sort_values(by=["k", "x"], env=env).to_pandas()
+    u = l.drop_duplicates(subset=["k"], env=env).to_pandas()
+    g = l.groupby("k", {"x": "sum"}, env=env).to_pandas()
+    return j, s, u, g, l.to_pandas(), r.to_pandas()
+
+
+def test_dataframe_distributed_env():
+    res = run_distributed(_dist_frame, 2)
+    j = pd.concat([r[0] for r in res])
+    l = pd.concat([r[4] for r in res])
+    r = res[0][5]
+    exp = l.merge(r, on="k")
+    assert len(j) == 2 * len(exp)  # r is replicated on both ranks
+    s = pd.concat([x[1] for x in res]).reset_index(drop=True)
+    assert s["k"].is_monotonic_increasing
+    u = pd.concat([x[2] for x in res])
+    assert sorted(u["k"].tolist()) == sorted(l["k"].unique().tolist())
+    g = pd.concat([x[3] for x in res]).sort_values("k")
+    assert g["sum_x"].tolist() == l.groupby("k")["x"].sum().sort_index().tolist()
