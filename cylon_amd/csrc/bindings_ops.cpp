@@ -3,7 +3,11 @@
 #include <torch/extension.h>
 
 #include "cylon/kernels/kernels.hpp"
+#include <tuple>
+
+#include "cylon/api.hpp"
 #include "cylon/ops/api_ext.hpp"
+#include "cylon/ops/graph.hpp"
 #include "cylon/ops/relational.hpp"
 #include "cylon/table.hpp"
 
@@ -70,6 +74,83 @@ void register_extended_ops(py::module &m) {
         return ops::DistributedSort(t, cols, asc, o);
       },
       rel);
+  // ---- streaming op graph (C24) ------------------------------------------
+  m.def(
+      "dis_join_op",
+      [](std::shared_ptr<CylonContext> ctx, const std::vector<TablePtr> &lefts, const std::vector<TablePtr> &rights,
+         const std::string &type, const std::string &algo, const std::vector<int> &lc, const std::vector<int> &rc,
+         const std::string &lp, const std::string &rp, int num_splits) {
+        using namespace join::config;
+        const JoinType jt = type == "left" ? LEFT : type == "right" ? RIGHT : type == "outer" ? FULL_OUTER : INNER;
+        const JoinAlgorithm ja = algo == "hash" ? HASH : SORT;
+        graph::DisJoinOpConfig cfg{num_splits, JoinConfig(jt, lc, rc, ja, lp, rp)};
+        std::vector<TablePtr> out;
+        graph::DisJoinOP op(ctx, 0, [&out](int, const TablePtr &t) { out.push_back(t); }, cfg);
+        for (const auto &t : lefts) op.InsertTable(graph::DisJoinOP::kLeftTag, t);
+        for (const auto &t : rights) op.InsertTable(graph::DisJoinOP::kRightTag, t);
+        op.WaitForCompletion();
+        return out;
+      },
+      rel);
+  m.def(
+      "dis_union_op",
+      [](std::shared_ptr<CylonContext> ctx, const std::vector<TablePtr> &tables) {
+        std::vector<TablePtr> out;
+        graph::DisUnionOp op(ctx, 0, [&out](int, const TablePtr &t) { out.push_back(t); });
+        for (const auto &t : tables) op.InsertTable(0, t);
+        op.WaitForCompletion();
+        return out;
+      },
+      rel);
+
+  // ---- string-ID registry (reference table_api.hpp) ----------------------------
+  m.def("registry_put", &PutTable);
+  m.def("registry_get", &GetTable);
+  m.def("registry_remove", &RemoveTable);
+  m.def("registry_list", &ListTables);
+  m.def("registry_row_count", &RowCount);
+  m.def("registry_column_count", &ColumnCount);
+  m.def(
+      "registry_join",
+      [](const std::string &l, const std::string &r, const std::string &type, const std::string &algo,
+         const std::vector<int> &lc, const std::vector<int> &rc, const std::string &dest, bool distributed) {
+        using namespace join::config;
+        const JoinType jt = type == "left" ? LEFT : type == "right" ? RIGHT : type == "outer" ? FULL_OUTER : INNER;
+        JoinConfig cfg(jt, lc, rc, algo == "hash" ? HASH : SORT);
+        Status s = distributed ? DistributedJoinTables(l, r, cfg, dest) : JoinTables(l, r, cfg, dest);
+        return std::make_pair(s.get_code(), s.get_msg());  // converted after the GIL is re-acquired
+      },
+      rel);
+  m.def(
+      "registry_union",
+      [](const std::string &a, const std::string &b, const std::string &dest, bool distributed) {
+        Status s = UnionTables(a, b, dest, distributed);
+        return std::make_pair(s.get_code(), s.get_msg());  // converted after the GIL is re-acquired
+      },
+      rel);
+
+  // ---- all-to-all with the reference's insert/finish/isComplete protocol ----------
+  struct A2AHandle {
+    std::vector<std::tuple<int, TablePtr, int>> received;
+    std::unique_ptr<TableAllToAll> impl;
+  };
+  py::class_<A2AHandle, std::shared_ptr<A2AHandle>>(m, "TableAllToAll")
+      .def(py::init([](std::shared_ptr<CylonContext> ctx) {
+        auto h = std::make_shared<A2AHandle>();
+        A2AHandle *raw = h.get();
+        h->impl = std::make_unique<TableAllToAll>(ctx, [raw](int src, const TablePtr &t, int ref) {
+          raw->received.emplace_back(src, t, ref);
+          return true;
+        });
+        return h;
+      }))
+      .def("insert", [](A2AHandle &h, const TablePtr &t, int target, int ref) { return h.impl->insert(t, target, ref); },
+           py::arg("table"), py::arg("target"), py::arg("reference") = 0)
+      .def("finish", [](A2AHandle &h) { h.impl->finish(); })
+      .def("is_complete", [](A2AHandle &h) { return h.impl->isComplete(); }, rel)
+      .def("close", [](A2AHandle &h) { h.impl->close(); })
+      .def("received", [](A2AHandle &h) { return h.received; });
+
   m.def("map_to_sort_partitions", &ops::MapToSortPartitions, rel);
   m.def("partition_reorder", &ops::PartitionReorder, rel);
   m.def("all_to_all_table", &ops::AllToAllTable, rel);

@@ -1,0 +1,89 @@
+"""Op-graph runtime, table all-to-all, task all-to-all and the registry
+(reference: cpp/src/examples/ops/join_op_example.cpp, task_test.cpp, table_api)."""
+import numpy as np
+import pandas as pd
+import pyarrow as pa
+import pytest
+
+from cylon_amd import Table
+from cylon_amd.parallel import DisJoinOp, DisUnionOp, TableAllToAll, TableRegistry, TaskAllToAll
+
+from dist_utils import run_distributed
+
+
+def _rows(df):
+    return sorted(map(tuple, df.itertuples(index=False)))
+
+
+def _op_graph(ctx, nbatches):
+    rank = ctx.get_rank()
+    rng = np.random.default_rng(rank)
+    lefts = [pd.DataFrame({"k": rng.integers(0, 50, 40), "v": rng.random(40)}) for _ in range(nbatches)]
+    rights = [pd.DataFrame({"k": rng.integers(0, 50, 30), "w": rng.random(30)}) for _ in range(nbatches + rank)]
+    op = DisJoinOp(ctx, "inner", "hash", [0], [0], "l_", "r_", num_splits=8)
+    for d in lefts:
+        op.insert_table(DisJoinOp.LEFT, Table.from_pandas(ctx, d))
+    for d in rights:
+        op.insert_table(DisJoinOp.RIGHT, Table.from_pandas(ctx, d))
+    res = op.execute()
+    got = pd.concat([r.to_pandas() for r in res]) if res else pd.DataFrame()
+    u = DisUnionOp(ctx)
+    for d in lefts:
+        u.insert_table(0, Table.from_pandas(ctx, d))
+    un = pd.concat([r.to_pandas() for r in u.execute()])
+    return got, pd.concat(lefts), pd.concat(rights), un
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_dis_join_op_graph(world):
+    res = run_distributed(_op_graph, world, 2)
+    got = pd.concat([r[0] for r in res])
+    a = pd.concat([r[1] for r in res])
+    b = pd.concat([r[2] for r in res])
+    exp = a.add_prefix("l_").merge(b.add_prefix("r_"), left_on="l_k", right_on="r_k")
+    assert _rows(got) == _rows(exp[got.columns])
+    un = pd.concat([r[3] for r in res])
+    assert _rows(un) == _rows(a.drop_duplicates())
+
+
+def _a2a(ctx):
+    rank, world = ctx.get_rank(), ctx.get_world_size()
+    seen = []
+    a2a = TableAllToAll(ctx, lambda src, t, ref: seen.append((src, ref, t.to_pydict()["x"])) or True)
+    for target in range(world):
+        a2a.insert(Table(pa.table({"x": [rank * 10 + target]}), ctx), target, reference=rank * 100 + target)
+        a2a.insert(Table(pa.table({"x": [rank * 10 + target, -1]}), ctx), target, reference=7)
+    a2a.finish()
+    while not a2a.is_complete():
+        pass
+    tasks = TaskAllToAll(ctx, [t % world for t in range(2 * world)])
+    for task in range(2 * world):
+        tasks.insert(Table(pa.table({"x": [task]}), ctx), task)
+    got = [(s, r, t.to_pydict()["x"]) for s, t, r in tasks.wait_for_completion()]
+    return seen, got
+
+
+def test_table_all_to_all_protocol():
+    world = 3
+    res = run_distributed(_a2a, world)
+    for rank, (seen, tasks) in enumerate(res):
+        exp = []
+        for src in range(world):
+            exp.append((src, src * 100 + rank, [src * 10 + rank]))
+            exp.append((src, 7, [src * 10 + rank, -1]))
+        assert sorted(seen) == sorted(exp)
+        mine = sorted(t for t in range(2 * world) if t % world == rank)
+        assert sorted(r for _, r, _ in tasks) == sorted(mine * world)
+
+
+def test_registry(ctx):
+    reg = TableRegistry(ctx)
+    reg.put("a", Table(pa.table({"k": [1, 2, 3], "v": [1, 2, 3]}), ctx))
+    reg.put("b", Table(pa.table({"k": [2, 3, 4], "w": [5, 6, 7]}), ctx))
+    reg.join("a", "b", "j", "inner", "hash")
+    assert reg.row_count("j") == 2 and reg.column_count("j") == 4
+    reg.union("a", "a", "u")
+    assert reg.get("u").row_count == 3
+    assert set(reg.ids()) >= {"a", "b", "j", "u"}
+    reg.remove("j")
+    assert "j" not in reg.ids()
