@@ -10,6 +10,7 @@
 #include "cylon/net/communicator.hpp"
 #include "cylon/ops/api_ext.hpp"
 #include "cylon/table.hpp"
+#include "cylon/trace.hpp"
 
 namespace py = pybind11;
 using namespace cylon;
@@ -131,6 +132,10 @@ PYBIND11_MODULE(_C, m) {
       .def("get_config", &CylonContext::GetConfig, py::arg("key"), py::arg("default") = "")
       .def("get_configs", &CylonContext::GetConfigs)
       .def("device", [](const CylonContext &c) { return c.GetDevice().str(); })
+      .def("inject_faults",
+           [](CylonContext &c, int64_t fail_at_call) {
+             c.setCommunicator(std::make_shared<net::FaultInjectionCommunicator>(c.GetCommunicator(), fail_at_call));
+           })
       .def("bytes_allocated", &CylonContext::BytesAllocated)
       .def("max_memory", &CylonContext::MaxMemory)
       .def("allreduce", [](CylonContext &c, at::Tensor t, int op) {
@@ -203,6 +208,18 @@ PYBIND11_MODULE(_C, m) {
         return ops::JoinIndices(l, r, make_jc(type, algo, lc, rc, "", ""));
       },
       rel);
+
+  // ---- tracing / metrics -----------------------------------------------------
+  m.def("trace_enable", &trace::set_enabled);
+  m.def("trace_enabled", &trace::enabled);
+  m.def("trace_phases", [] {
+    std::map<std::string, std::pair<double, int64_t>> out;
+    for (auto &kv : trace::phases()) out[kv.first] = {kv.second.total_ms, kv.second.calls};
+    return out;
+  });
+  m.def("trace_counters", &trace::counters);
+  m.def("trace_reset", &trace::reset);
+  m.def("log", &trace::log);
 
   register_extended_ops(m);
 }

@@ -74,6 +74,53 @@ class LocalCommunicator : public Communicator {
   void Broadcast(at::Tensor &, int) override {}
 };
 
+// Fault injection for tests (SURVEY.md §5 failure detection): forwards to an inner
+// communicator and raises CylonError(ExecutionError) on the N-th collective, so the
+// failure path of every distributed operator can be exercised without a real
+// failing rank.  (The reference has no failure handling: errors abort or hang.)
+class FaultInjectionCommunicator : public Communicator {
+ public:
+  FaultInjectionCommunicator(std::shared_ptr<Communicator> inner, int64_t fail_at_call)
+      : inner_(std::move(inner)), fail_at_(fail_at_call) {}
+  int GetRank() const override { return inner_->GetRank(); }
+  int GetWorldSize() const override { return inner_->GetWorldSize(); }
+  CommType GetCommType() const override { return inner_->GetCommType(); }
+  void Barrier() override {
+    tick("Barrier");
+    inner_->Barrier();
+  }
+  at::Tensor AllToAllV(const at::Tensor &s, const std::vector<int64_t> &sc, const std::vector<int64_t> &rc) override {
+    tick("AllToAllV");
+    return inner_->AllToAllV(s, sc, rc);
+  }
+  std::vector<int64_t> ExchangeCounts(const std::vector<int64_t> &c) override {
+    tick("ExchangeCounts");
+    return inner_->ExchangeCounts(c);
+  }
+  void AllReduce(at::Tensor &t, ReduceOp op) override {
+    tick("AllReduce");
+    inner_->AllReduce(t, op);
+  }
+  at::Tensor AllGather(const at::Tensor &in) override {
+    tick("AllGather");
+    return inner_->AllGather(in);
+  }
+  void Broadcast(at::Tensor &t, int root) override {
+    tick("Broadcast");
+    inner_->Broadcast(t, root);
+  }
+  int64_t calls() const { return calls_; }
+
+ private:
+  void tick(const char *what) {
+    if (++calls_ == fail_at_) CYLON_THROW(Code::ExecutionError, "injected communication fault at call " << calls_
+                                                                    << " (" << what << ")");
+  }
+  std::shared_ptr<Communicator> inner_;
+  int64_t fail_at_;
+  int64_t calls_ = 0;
+};
+
 // Communicator over a c10d ProcessGroup (RCCL on MI355X, gloo on CPU).
 class ProcessGroupCommunicator : public Communicator {
  public:

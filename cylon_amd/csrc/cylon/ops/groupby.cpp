@@ -17,6 +17,7 @@
 
 #include "relational.hpp"
 #include "util.hpp"
+#include "../trace.hpp"
 
 namespace cylon {
 namespace ops {
@@ -238,7 +239,12 @@ static TablePtr groupby_with(const TablePtr &t, const std::vector<int> &keys, co
                              bool presorted) {
   CYLON_CHECK(!keys.empty(), Code::Invalid, "group-by needs at least one key column");
   Exec ex(t->device());
-  GroupInfo gi = GroupIds(t, keys, presorted);
+  GroupInfo gi;
+  {
+    CYLON_PHASE("groupby.group_ids", ex.device);
+    gi = GroupIds(t, keys, presorted);
+  }
+  CYLON_PHASE("groupby.aggregate", ex.device);
   TablePtr kt = GatherNullable(Project(t, keys), gi.first_rows, false);
   std::vector<Column> cols = kt->columns();
   for (const auto &a : aggs) cols.push_back(agg_column(ex, t, gi, a));

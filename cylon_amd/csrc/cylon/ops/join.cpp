@@ -17,6 +17,7 @@
 //      unmatched rows of the preserved side(s), appended with -1 partners.
 //   4. materialisation: one fused gather launch per side (K4).
 #include "util.hpp"
+#include "../trace.hpp"
 
 namespace cylon {
 namespace ops {
@@ -76,6 +77,7 @@ static std::pair<at::Tensor, at::Tensor> hash_join_pairs(const Exec &ex, const a
   at::Tensor table;
   HashTableRef t{nullptr, cap, shift};
   if (ex.gpu && nb >= kSortedBuildRows) {
+    CYLON_PHASE("join.build.sorted", ex.device);
     // atomic-free build: radix sort (key,row) by slot, prefix-max placement, sequential stores
     at::Tensor ka = ex.empty_i64(nb), va = ex.empty_i64(nb), kb = ex.empty_i64(nb), vb = ex.empty_i64(nb);
     at::Tensor mp = ex.empty_i64(1);
@@ -101,6 +103,7 @@ static std::pair<at::Tensor, at::Tensor> hash_join_pairs(const Exec &ex, const a
     KCALL(ex, hash_build, ptr<int64_t>(bk), nb, t);
   }
   if (ex.gpu && np >= kEmitProbeRows) {
+    CYLON_PHASE("join.probe.emit", ex.device);
     // single-pass probe into an over-allocated pair buffer; exact two-pass fallback on overflow
     const int64_t capacity = np + np / 4 + 4096;
     at::Tensor po = ex.empty_i64(capacity), bo = ex.empty_i64(capacity), cnt = ex.empty_i64(1);
@@ -113,6 +116,7 @@ static std::pair<at::Tensor, at::Tensor> hash_join_pairs(const Exec &ex, const a
       return build_left ? std::make_pair(bo, po) : std::make_pair(po, bo);
     }
   }
+  CYLON_PHASE("join.probe.twopass", ex.device);
   at::Tensor counts = ex.empty_i64(np);
   KCALL(ex, hash_probe_count, ptr<int64_t>(pk), np, t, ptr<int64_t>(counts));
   at::Tensor offs = exclusive_scan(ex, counts);
@@ -202,6 +206,7 @@ TablePtr Join(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg
   const JoinType jt = cfg.GetType();
   const bool lnull = jt == JoinType::RIGHT || jt == JoinType::FULL_OUTER;
   const bool rnull = jt == JoinType::LEFT || jt == JoinType::FULL_OUTER;
+  CYLON_PHASE("join.materialize", l->device());
   TablePtr lo = GatherNullable(l, idx.first, lnull);
   TablePtr ro = GatherNullable(r, idx.second, rnull);
   std::vector<Column> cols;

@@ -6,6 +6,7 @@
 // payload protocol).  Partition -> rank mapping is identical: partition i goes
 // to rank i when P == world, else to rank i*world/P (table.cpp:89-106).
 #include "util.hpp"
+#include "../trace.hpp"
 
 namespace cylon {
 namespace ops {
@@ -90,9 +91,18 @@ TablePtr Shuffle(const TablePtr &t, const std::vector<int> &hash_cols) {
   auto ctx = t->GetContext();
   const int world = ctx->GetWorldSize();
   if (world == 1) return t;
-  at::Tensor pid = hash_pids(t, hash_cols, (uint32_t)world);
-  auto r = PartitionReorder(t, pid, (uint32_t)world);
-  return AllToAllTable(r.first, r.second);
+  std::pair<TablePtr, std::vector<int64_t>> r;
+  {
+    CYLON_PHASE("shuffle.partition", t->device());
+    at::Tensor pid = hash_pids(t, hash_cols, (uint32_t)world);
+    r = PartitionReorder(t, pid, (uint32_t)world);
+  }
+  CYLON_PHASE("shuffle.exchange", t->device());
+  trace::add_counter("shuffle.rows_in", t->Rows());
+  trace::add_counter("shuffle.bytes_in", t->nbytes());
+  TablePtr out = AllToAllTable(r.first, r.second);
+  trace::add_counter("shuffle.rows_out", out->Rows());
+  return out;
 }
 
 }  // namespace ops

@@ -9,6 +9,7 @@
 // big-endian chunks from the last chunk to the first, which yields byte-wise
 // lexicographic order.
 #include "util.hpp"
+#include "../trace.hpp"
 
 namespace cylon {
 namespace ops {
@@ -69,6 +70,7 @@ at::Tensor SortIndices(const TablePtr &t, const std::vector<int> &cols, const st
   CYLON_CHECK(ascending.size() == cols.size() || ascending.size() == 1, Code::Invalid,
               "ascending flags must match sort columns");
   Exec ex(t->device());
+  CYLON_PHASE("sort.indices", ex.device);
   at::Tensor perm = iota(ex, t->Rows());
   for (int k = (int)cols.size() - 1; k >= 0; --k) {
     const bool asc = ascending.size() == 1 ? ascending[0] : ascending[k];

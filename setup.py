@@ -32,7 +32,7 @@ ext = CppExtension(
     extra_compile_args=["-O3", "-std=c++17", "-Wno-unused-function"],
     extra_objects=hip_objects,
     library_dirs=[_build.ROCM_LIB],
-    libraries=["amdhip64"],
+    libraries=["amdhip64", "rocprofiler-sdk-roctx"],
     extra_link_args=[f"-Wl,-rpath,{_build.ROCM_LIB}"],
 )
 

@@ -1,0 +1,87 @@
+"""Aux subsystems: tracing, fault injection, checkpointing, utils, interop, determinism."""
+import os
+
+import numpy as np
+import pandas as pd
+import pyarrow as pa
+import pytest
+import torch
+
+from cylon_amd import CylonError, Table
+from cylon_amd.utils import (MiniBatcher, benchmark_with_repitions, generate_numeric_csv, random_table, traced)
+from cylon_amd.utils import trace as tr
+from cylon_amd.utils.checkpoint import load_table, save_table
+from cylon_amd.utils.interop import from_dlpack, to_dlpack, to_tensor
+
+from dist_utils import run_distributed
+
+
+def test_tracing_phases(ctx):
+    t = random_table(ctx, 5000, 2, seed=1)
+    with traced():
+        t.join(t, "inner", "hash", on=[0])
+        t.sort("v0")
+        t.local_groupby("k", {"v1": "sum"})
+        ph = tr.phases()
+    assert "join.materialize" in ph and "sort.indices" in ph and "groupby.group_ids" in ph
+    assert all(v[0] >= 0 and v[1] >= 1 for v in ph.values())
+    assert "phase" in tr.report()
+
+
+def _fault(ctx):
+    t = Table(pa.table({"k": np.arange(100), "v": np.arange(100)}), ctx)
+    ctx._ctx.inject_faults(2)  # fail on the 2nd collective of the shuffle
+    try:
+        t.shuffle(["k"])
+    except CylonError as e:
+        return ("injected" in str(e), e.args[1] if len(e.args) > 1 else None)
+    return (False, None)
+
+
+def test_fault_injection_surfaces_as_error():
+    for ok, code in run_distributed(_fault, 2):
+        assert ok and code == 42  # Code::ExecutionError
+
+
+def _ckpt(ctx, d):
+    t = Table(pa.table({"k": np.arange(10) + 100 * ctx.get_rank()}), ctx)
+    save_table(t, d, "tbl")
+    ctx.barrier()
+    back = load_table(ctx, d, "tbl")
+    return back.to_pydict() == t.to_pydict()
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    assert all(run_distributed(_ckpt, 2, str(tmp_path)))
+
+
+def test_benchutils_datagen_minibatch(ctx, tmp_path):
+    @benchmark_with_repitions(repititions=3, time_type="ms")
+    def f(x):
+        return x + 1
+
+    t, r = f(1)
+    assert r == 2 and t >= 0
+    p = generate_numeric_csv(100, 4, str(tmp_path / "g.csv"), seed=0)
+    df = pd.read_csv(p)
+    assert df.shape == (100, 4) and df["0"].max() < 99
+    mb = MiniBatcher.generate_minibatches(np.arange(15000), 32)
+    assert mb.shape == (469, 32)
+    mt = MiniBatcher.generate_minibatches(torch.arange(10), 4)
+    assert mt.shape == (3, 4)
+
+
+def test_dlpack_interop(ctx):
+    t = random_table(ctx, 100, 2)
+    back = from_dlpack(ctx, to_dlpack(t))
+    assert back.to_arrow().equals(t.to_arrow())
+    x = to_tensor(t, ["v0", "v1"])
+    assert x.shape == (100, 2)
+
+
+def test_join_is_deterministic(ctx):
+    rng = np.random.default_rng(0)
+    a = Table(pa.table({"k": rng.integers(0, 100, 3000), "v": rng.random(3000)}), ctx)
+    r1 = a.join(a, "inner", "hash", on=[0]).to_arrow()
+    r2 = a.join(a, "inner", "hash", on=[0]).to_arrow()
+    assert r1.equals(r2)
