@@ -1,0 +1,493 @@
+// LDS radix hash join for large inner joins on a single exact int key (K3 + K5, gfx950).
+//
+// Measured on MI355X (tools/membench.hip, profiles/membench.txt): streaming
+// copies run at 5.7 TB/s, but 8-byte accesses scattered over anything larger
+// than an XCD's L2 (4 MB) run at ~50 G accesses/s whatever the window (1 MB
+// ... 64 GB), i.e. < 0.5 TB/s of useful data.  A join built on random probes
+// or gathers over the inputs is therefore bound by that rate (the global-table
+// path: probe 200 ms + gathers 110 ms for 1B x 1B).  This path touches HBM
+// only with coalesced streams:
+//   1. radix-partition BOTH relations, all fixed-width columns (validity bytes
+//      included), by the top `bits` bits of fmix64(key), with LSD passes of
+//      <= 10 bits.  A pass ranks an 8192-row tile per digit (wave64 ballot
+//      match, 16 waves), then moves each column through a 64 KB LDS stage:
+//      coalesced loads are written to LDS at their sorted slot, and the
+//      sorted tile is stored so that each digit's run (8192/512 = 16 rows =
+//      128 B per 8-byte column on average) is one contiguous segment.
+//   2. join bucket p of both sides in one workgroup: the build side's rows
+//      (key + payload) are copied into LDS with coalesced loads and indexed by
+//      an LDS open-addressing table (4096 slots, CAS insert).  A count kernel
+//      gives per-partition output sizes, a device scan the offsets, and the
+//      write kernel streams the probe rows, emitting every output column
+//      directly (probe payload from HBM, build payload from LDS).  Each wave
+//      owns a contiguous slice of the probe rows (wave-level scans only).
+// Partitions whose build side exceeds the LDS capacity are reported; the
+// caller then falls back to the global-table join.
+#include "stable_rank.hpp"
+
+namespace cylon {
+namespace hip {
+
+constexpr int kRPThreads = 1024;                 // partition pass block (16 waves)
+constexpr int kRPWaves = kRPThreads / kWave;
+constexpr int kRPItems = 8;                      // rows per thread per tile
+constexpr int kRPTile = kRPThreads * kRPItems;   // 8192 rows
+constexpr int kRPMaxBuckets = 1024;
+constexpr int kRJMaxDigitBits = 10;
+constexpr int kRJSlots = 4096;                   // LDS hash slots (uint32 = build row + 1)
+constexpr int kRJRowArea = 60 * 1024;            // LDS bytes for the staged build rows
+constexpr int kRJMaxRows = kRJSlots / 2;         // load factor <= 0.5
+constexpr int kRJThreads = 512;
+constexpr int kRJWaves = kRJThreads / kWave;
+
+struct ColSet {
+  const uint8_t *in[kMaxFusedCols];
+  uint8_t *out[kMaxFusedCols];
+  int width[kMaxFusedCols];
+  int n;
+};
+
+__device__ __forceinline__ uint32_t part_of(int64_t key, int bits) {
+  return bits == 0 ? 0u : (uint32_t)(hashing::fmix64((uint64_t)key) >> (64 - bits));
+}
+
+__device__ __forceinline__ uint64_t ld_elem(const uint8_t *src, int64_t i, int w) {
+  switch (w) {
+    case 1: return src[i];
+    case 2: return reinterpret_cast<const uint16_t *>(src)[i];
+    case 4: return reinterpret_cast<const uint32_t *>(src)[i];
+    default: return reinterpret_cast<const uint64_t *>(src)[i];
+  }
+}
+
+__device__ __forceinline__ void st_elem(uint8_t *dst, int64_t i, int w, uint64_t v) {
+  switch (w) {
+    case 1: dst[i] = (uint8_t)v; break;
+    case 2: reinterpret_cast<uint16_t *>(dst)[i] = (uint16_t)v; break;
+    case 4: reinterpret_cast<uint32_t *>(dst)[i] = (uint32_t)v; break;
+    default: reinterpret_cast<uint64_t *>(dst)[i] = v;
+  }
+}
+
+// --------------------------------------------------------------------------
+// partition pass
+// --------------------------------------------------------------------------
+struct PartDigit {
+  const int64_t *keys;
+  int bits;   // total partition bits
+  int shift;  // digit = (part >> shift) & mask
+  uint32_t mask;
+  __device__ __forceinline__ uint32_t operator()(int64_t i) const {
+    return (part_of(keys[i], bits) >> shift) & mask;
+  }
+};
+
+__global__ __launch_bounds__(kRPThreads) void k_rp_hist(PartDigit digit, int64_t n, uint32_t nbuckets,
+                                                        int64_t rows_per_block, int64_t nblocks,
+                                                        int64_t *__restrict__ bh) {
+  __shared__ unsigned int hist[kRPMaxBuckets];
+  for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) hist[p] = 0;
+  __syncthreads();
+  const int64_t begin = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t end = (begin + rows_per_block < n) ? begin + rows_per_block : n;
+  for (int64_t i0 = begin; i0 < end; i0 += 4 * kRPThreads) {
+    uint32_t d[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * kRPThreads + threadIdx.x;
+      d[u] = i < end ? digit(i) : 0xffffffffu;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (d[u] != 0xffffffffu) atomicAdd(&hist[d[u]], 1u);
+  }
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) bh[(int64_t)p * nblocks + blockIdx.x] = hist[p];
+}
+
+// block-wide exclusive scan of one uint32 per thread (kRPThreads threads)
+__device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) {
+  const int lane = lane_id(), wave = threadIdx.x / kWave;
+  uint32_t inc = c;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t t = __shfl_up(inc, d, kWave);
+    if (lane >= d) inc += t;
+  }
+  if (lane == kWave - 1) wsum[wave] = inc;
+  __syncthreads();
+  uint32_t off = 0;
+#pragma unroll
+  for (int w = 0; w < kRPWaves; ++w) off += (w < wave) ? wsum[w] : 0u;
+  return off + inc - c;
+}
+
+__global__ __launch_bounds__(kRPThreads) void k_rows_pass(PartDigit digit, int nbits, uint32_t nbuckets, ColSet cols,
+                                                          int64_t n, int64_t rows_per_block, int64_t nblocks,
+                                                          const int64_t *__restrict__ bh_scan) {
+  __shared__ int64_t running[kRPMaxBuckets];
+  __shared__ uint32_t toff[kRPMaxBuckets], ttot[kRPMaxBuckets];
+  __shared__ uint16_t wcnt[kRPWaves * kRPMaxBuckets];  // per-wave counts, then per-wave prefixes
+  __shared__ uint16_t sdig[kRPTile];                   // digit of each sorted slot
+  __shared__ uint64_t stage[kRPTile];                  // one column of the tile, in sorted order
+  __shared__ uint32_t wsum[kRPWaves];
+
+  const int64_t b = blockIdx.x;
+  for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] = bh_scan[(int64_t)p * nblocks + b];
+  for (uint32_t q = threadIdx.x; q < kRPWaves * nbuckets; q += blockDim.x) wcnt[q] = 0;
+  __syncthreads();
+  const int wave = threadIdx.x / kWave;
+  const int lane = lane_id();
+  const uint64_t lt = lanemask_lt();
+  const int64_t begin = b * rows_per_block;
+  const int64_t end = (begin + rows_per_block < n) ? begin + rows_per_block : n;
+  uint16_t *mycnt = wcnt + wave * nbuckets;
+  const int wrow = wave * kWave * kRPItems;
+
+  for (int64_t tile = begin; tile < end; tile += kRPTile) {
+    uint32_t pl[kRPItems];  // digit, then (in-wave rank << 16) | digit, then sorted slot; ~0 = inactive
+#pragma unroll
+    for (int k = 0; k < kRPItems; ++k) {  // 8 independent key loads in flight
+      const int64_t i = tile + wrow + k * kWave + lane;
+      pl[k] = i < end ? digit(i) : 0xffffffffu;
+    }
+#pragma unroll
+    for (int k = 0; k < kRPItems; ++k) {
+      const bool active = pl[k] != 0xffffffffu;
+      const uint32_t p = active ? pl[k] : 0u;
+      uint64_t m = __ballot(active);
+      for (int bit = 0; bit < nbits; ++bit) {
+        const uint32_t x = (p >> bit) & 1u;
+        const uint64_t bb = __ballot(x);
+        m &= x ? bb : ~bb;
+      }
+      const uint32_t rank = (uint32_t)__popcll(m & lt);
+      uint32_t base = 0;
+      if (active) base = mycnt[p];
+      __builtin_amdgcn_wave_barrier();
+      if (active && (m & lt) == 0) mycnt[p] = (uint16_t)(base + (uint32_t)__popcll(m));
+      __builtin_amdgcn_wave_barrier();
+      pl[k] = active ? (((base + rank) << 16) | p) : 0xffffffffu;
+    }
+    __syncthreads();
+    // per bucket: exclusive prefix over waves (in place) and the tile total
+    for (uint32_t p = threadIdx.x; p < nbuckets; p += kRPThreads) {
+      uint32_t run = 0;
+#pragma unroll
+      for (int w = 0; w < kRPWaves; ++w) {
+        const uint32_t c = wcnt[w * nbuckets + p];
+        wcnt[w * nbuckets + p] = (uint16_t)run;
+        run += c;
+      }
+      ttot[p] = run;
+    }
+    __syncthreads();
+    {
+      const uint32_t p = threadIdx.x;
+      const uint32_t ex = rp_block_exscan(p < nbuckets ? ttot[p] : 0u, wsum);
+      if (p < nbuckets) toff[p] = ex;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kRPItems; ++k) {
+      if (pl[k] == 0xffffffffu) continue;
+      const uint32_t p = pl[k] & 0xffffu;
+      const uint32_t pos = toff[p] + wcnt[wave * nbuckets + p] + (pl[k] >> 16);
+      sdig[pos] = (uint16_t)p;
+      pl[k] = pos;
+    }
+    const int cnt = (int)((end - tile) < kRPTile ? (end - tile) : kRPTile);
+    for (int c = 0; c < cols.n; ++c) {
+      const int w = cols.width[c];
+      const uint8_t *in = cols.in[c];
+      uint8_t *out = cols.out[c];
+      uint8_t *st = reinterpret_cast<uint8_t *>(stage);
+#pragma unroll
+      for (int k = 0; k < kRPItems; ++k)
+        if (pl[k] != 0xffffffffu) st_elem(st, pl[k], w, ld_elem(in, tile + wrow + k * kWave + lane, w));
+      __syncthreads();
+      for (int j = threadIdx.x; j < cnt; j += kRPThreads) {
+        const uint32_t p = sdig[j];
+        st_elem(out, running[p] + (j - (int64_t)toff[p]), w, ld_elem(st, j, w));
+      }
+      __syncthreads();
+    }
+    for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] += ttot[p];
+    for (uint32_t q = threadIdx.x; q < kRPWaves * nbuckets; q += blockDim.x) wcnt[q] = 0;
+    __syncthreads();
+  }
+}
+
+struct RPGeometry {
+  int64_t nblocks, rows_per_block;
+};
+
+static RPGeometry rp_geometry(int64_t n) {
+  const int64_t tiles = std::max<int64_t>(1, (n + kRPTile - 1) / kRPTile);
+  const int64_t want = 2 * kNumCUs;
+  const int64_t nb = tiles < want ? tiles : want;
+  RPGeometry g;
+  g.rows_per_block = ((tiles + nb - 1) / nb) * kRPTile;
+  g.nblocks = std::max<int64_t>(1, (n + g.rows_per_block - 1) / g.rows_per_block);
+  return g;
+}
+
+int64_t radix_rows_pass_workspace(int64_t n, int digit_bits) {
+  const RPGeometry g = rp_geometry(n);
+  const int64_t m = g.nblocks * (int64_t(1) << digit_bits);
+  return m + (m + 1) + scan_workspace(m);
+}
+
+void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, int digit_bits, const uint8_t *const *in,
+                     uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream) {
+  if (n == 0) return;
+  CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
+  CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
+  hipStream_t s = as_stream(stream);
+  const uint32_t nb = 1u << digit_bits;
+  const RPGeometry g = rp_geometry(n);
+  const int64_t m = g.nblocks * (int64_t)nb;
+  int64_t *bh = ws, *bh_scan = ws + m, *scan_ws = bh_scan + m + 1;
+  PartDigit dg{keys, total_bits, shift, nb - 1};
+  hipLaunchKernelGGL(k_rp_hist, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, n, nb, g.rows_per_block,
+                     g.nblocks, bh);
+  HIP_LAUNCH_CHECK();
+  exclusive_scan(bh, m, bh_scan, scan_ws, stream);
+  ColSet cs;
+  cs.n = ncols;
+  for (int c = 0; c < kMaxFusedCols; ++c) {
+    cs.in[c] = c < ncols ? in[c] : nullptr;
+    cs.out[c] = c < ncols ? out[c] : nullptr;
+    cs.width[c] = c < ncols ? widths[c] : 8;
+  }
+  hipLaunchKernelGGL(k_rows_pass, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, digit_bits, nb, cs, n,
+                     g.rows_per_block, g.nblocks, (const int64_t *)bh_scan);
+  HIP_LAUNCH_CHECK();
+}
+
+// offsets[p] = first row of partition p in partition-sorted keys (binary search), offsets[P] = n
+__global__ void k_part_offsets(const int64_t *__restrict__ keys, int64_t n, int bits, int64_t nparts,
+                               int64_t *__restrict__ offs) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= nparts; p += stride) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)part_of(keys[mid], bits) < p) lo = mid + 1; else hi = mid;
+    }
+    offs[p] = lo;
+  }
+}
+
+void radix_part_offsets(const int64_t *keys, int64_t n, int bits, int64_t *offs, void *stream) {
+  const int64_t np = int64_t(1) << bits;
+  hipLaunchKernelGGL(k_part_offsets, dim3(grid_for(np + 1)), dim3(kBlock), 0, as_stream(stream), keys, n, bits, np,
+                     offs);
+  HIP_LAUNCH_CHECK();
+}
+
+// --------------------------------------------------------------------------
+// per-partition LDS join
+// --------------------------------------------------------------------------
+// Build rows per partition that fit the LDS row area: keys (8 B) + the staged
+// build columns (widths w[q]; in[q] == nullptr marks the key column itself).
+int64_t radix_join_capacity(const int *widths, const uint8_t *const *in, int n) {
+  int64_t row = 8;
+  for (int q = 0; q < n; ++q)
+    if (in[q]) row += widths[q];
+  int64_t cap = kRJRowArea / row;
+  cap = std::min<int64_t>(cap, kRJMaxRows);
+  return cap & ~int64_t(7);  // multiple of 8: every column region stays 8-byte aligned
+}
+
+__device__ __forceinline__ uint32_t lds_slot(int64_t k) {
+  return (uint32_t)hashing::fmix64((uint64_t)k) & (kRJSlots - 1);
+}
+
+// Stage partition rows [rb, rb+nr) of the build side into LDS and index them.
+// Caller guarantees no thread still reads tab/area (barrier before the call).
+__device__ __forceinline__ void rj_stage(uint32_t *tab, uint8_t *area, const int64_t *__restrict__ bkeys, int64_t rb,
+                                         int nr, int cap, const ColSet *bc) {
+  int64_t *skeys = reinterpret_cast<int64_t *>(area);
+  for (int s = threadIdx.x; s < kRJSlots; s += blockDim.x) tab[s] = 0;
+  for (int r = threadIdx.x; r < nr; r += blockDim.x) skeys[r] = bkeys[rb + r];
+  if (bc) {
+    int64_t off = 8 * (int64_t)cap;
+    for (int q = 0; q < bc->n; ++q) {
+      if (!bc->in[q]) continue;
+      const int w = bc->width[q];
+      for (int r = threadIdx.x; r < nr; r += blockDim.x) st_elem(area + off, r, w, ld_elem(bc->in[q], rb + r, w));
+      off += (int64_t)cap * w;
+    }
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+    uint32_t s = lds_slot(skeys[r]);
+    while (atomicCAS(&tab[s], 0u, (uint32_t)(r + 1)) != 0u) s = (s + 1) & (kRJSlots - 1);
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t rj_count(const uint32_t *tab, const int64_t *skeys, int64_t k) {
+  uint32_t s = lds_slot(k), c = 0, v;
+  while ((v = tab[s]) != 0u) {
+    c += (skeys[v - 1] == k);
+    s = (s + 1) & (kRJSlots - 1);
+  }
+  return c;
+}
+
+__global__ __launch_bounds__(kRJThreads) void k_rj_count(const int64_t *__restrict__ pkeys,
+                                                         const int64_t *__restrict__ poffs,
+                                                         const int64_t *__restrict__ bkeys,
+                                                         const int64_t *__restrict__ boffs, int64_t nparts, int cap,
+                                                         int64_t *__restrict__ counts, int *overflow) {
+  __shared__ uint32_t tab[kRJSlots];
+  __shared__ __attribute__((aligned(16))) uint8_t area[kRJMaxRows * 8];
+  __shared__ unsigned long long wsum[kRJWaves];
+  const int64_t *skeys = reinterpret_cast<const int64_t *>(area);
+  for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
+    const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
+    const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
+    if (nr > cap) {  // uniform branch: whole block
+      if (threadIdx.x == 0) {
+        atomicOr(overflow, 1);
+        counts[p] = 0;
+      }
+      continue;
+    }
+    if (nr == 0 || nl == 0) {
+      if (threadIdx.x == 0) counts[p] = 0;
+      continue;
+    }
+    rj_stage(tab, area, bkeys, rb, (int)nr, cap, nullptr);
+    unsigned long long c = 0;
+    for (int64_t l = threadIdx.x; l < nl; l += blockDim.x) c += rj_count(tab, skeys, pkeys[lb + l]);
+    for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
+    if (lane_id() == 0) wsum[threadIdx.x / kWave] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long tot = 0;
+      for (int w = 0; w < kRJWaves; ++w) tot += wsum[w];
+      counts[p] = (int64_t)tot;
+    }
+    __syncthreads();
+  }
+}
+
+template <int MAXP>
+__global__ __launch_bounds__(kRJThreads) void k_rj_write(const int64_t *__restrict__ pkeys,
+                                                         const int64_t *__restrict__ poffs,
+                                                         const int64_t *__restrict__ bkeys,
+                                                         const int64_t *__restrict__ boffs, int64_t nparts, int cap,
+                                                         const int64_t *__restrict__ out_offs, ColSet pc, ColSet bc) {
+  __shared__ uint32_t tab[kRJSlots];
+  __shared__ __attribute__((aligned(16))) uint8_t area[kRJRowArea];
+  __shared__ uint32_t wtot[kRJWaves];
+  const int64_t *skeys = reinterpret_cast<const int64_t *>(area);
+  const int lane = lane_id();
+  const int wave = threadIdx.x / kWave;
+  for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
+    const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
+    const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
+    if (nr == 0 || nl == 0 || nr > cap) continue;
+    __syncthreads();  // previous partition fully done with tab / area / wtot
+    rj_stage(tab, area, bkeys, rb, (int)nr, cap, &bc);
+    // each wave owns a contiguous slice of the probe rows
+    const int64_t per = (nl + kRJWaves - 1) / kRJWaves;
+    const int64_t s0 = lb + std::min<int64_t>(nl, wave * per);
+    const int64_t s1 = lb + std::min<int64_t>(nl, (wave + 1) * per);
+    uint32_t c = 0;
+    for (int64_t l = s0 + lane; l < s1; l += kWave) c += rj_count(tab, skeys, pkeys[l]);
+    for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
+    if (lane == 0) wtot[wave] = c;
+    __syncthreads();
+    int64_t base = out_offs[p];
+    for (int w = 0; w < wave; ++w) base += wtot[w];
+    for (int64_t l0 = s0; l0 < s1; l0 += kWave) {
+      const int64_t l = l0 + lane;
+      const bool active = l < s1;
+      const int64_t k = active ? pkeys[l] : 0;
+      const uint32_t mc = active ? rj_count(tab, skeys, k) : 0u;
+      uint32_t inc = mc;  // wave inclusive scan of match counts
+#pragma unroll
+      for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t x = __shfl_up(inc, d, kWave);
+        if (lane >= d) inc += x;
+      }
+      const uint32_t wsum = __shfl(inc, kWave - 1, kWave);
+      int64_t o = base + (inc - mc);
+      if (mc) {
+        uint64_t pv[MAXP];  // probe row payload: all loads before any store
+#pragma unroll
+        for (int q = 0; q < MAXP; ++q)
+          if (q < pc.n) pv[q] = ld_elem(pc.in[q], l, pc.width[q]);
+        uint32_t s = lds_slot(k), left = mc, v;
+        while (left && (v = tab[s]) != 0u) {
+          const int r = (int)v - 1;
+          if (skeys[r] == k) {
+#pragma unroll
+            for (int q = 0; q < MAXP; ++q)
+              if (q < pc.n) st_elem(pc.out[q], o, pc.width[q], pv[q]);
+            int64_t off = 8 * (int64_t)cap;
+            for (int q = 0; q < bc.n; ++q) {
+              const int w = bc.width[q];
+              if (bc.in[q]) {
+                st_elem(bc.out[q], o, w, ld_elem(area + off, r, w));
+                off += (int64_t)cap * w;
+              } else {
+                st_elem(bc.out[q], o, w, (uint64_t)k);
+              }
+            }
+            ++o;
+            --left;
+          }
+          s = (s + 1) & (kRJSlots - 1);
+        }
+      }
+      base += wsum;
+    }
+  }
+}
+
+static int rj_grid(int64_t nparts) { return (int)std::min<int64_t>(nparts, kNumCUs * 8); }
+
+void radix_join_count(const int64_t *pkeys, const int64_t *poffs, const int64_t *bkeys, const int64_t *boffs,
+                      int64_t nparts, int64_t cap, int64_t *counts, int *overflow, void *stream) {
+  CYLON_CHECK(cap > 0 && cap <= kRJMaxRows, Code::Invalid, "radix join capacity " << cap);
+  hipStream_t s = as_stream(stream);
+  HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
+  hipLaunchKernelGGL(k_rj_count, dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts,
+                     (int)cap, counts, overflow);
+  HIP_LAUNCH_CHECK();
+}
+
+void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t *bkeys, const int64_t *boffs,
+                      int64_t nparts, int64_t cap, const int64_t *out_offs, const uint8_t *const *pin,
+                      uint8_t *const *pout, const int *pw, int npc, const uint8_t *const *bin, uint8_t *const *bout,
+                      const int *bw, int nbc, void *stream) {
+  CYLON_CHECK(npc <= kMaxFusedCols && nbc <= kMaxFusedCols, Code::Invalid, "too many columns");
+  CYLON_CHECK(cap > 0 && cap <= radix_join_capacity(bw, bin, nbc), Code::Invalid, "radix join capacity " << cap);
+  ColSet pc, bc;
+  pc.n = npc;
+  bc.n = nbc;
+  for (int q = 0; q < kMaxFusedCols; ++q) {
+    pc.in[q] = q < npc ? pin[q] : nullptr;
+    pc.out[q] = q < npc ? pout[q] : nullptr;
+    pc.width[q] = q < npc ? pw[q] : 8;
+    bc.in[q] = q < nbc ? bin[q] : nullptr;
+    bc.out[q] = q < nbc ? bout[q] : nullptr;
+    bc.width[q] = q < nbc ? bw[q] : 8;
+  }
+  hipStream_t s = as_stream(stream);
+  if (npc <= 4)
+    hipLaunchKernelGGL(k_rj_write<4>, dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys, boffs,
+                       nparts, (int)cap, out_offs, pc, bc);
+  else
+    hipLaunchKernelGGL(k_rj_write<kMaxFusedCols>, dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys,
+                       boffs, nparts, (int)cap, out_offs, pc, bc);
+  HIP_LAUNCH_CHECK();
+}
+
+}  // namespace hip
+}  // namespace cylon

@@ -127,6 +127,180 @@ static std::pair<at::Tensor, at::Tensor> hash_join_pairs(const Exec &ex, const a
   return build_left ? std::make_pair(bo, po) : std::make_pair(po, bo);
 }
 
+// ---------------------------------------------------------------------------
+// K5 LDS radix join (radix_join.hip): partition both sides, all columns, into
+// LDS-sized buckets and join bucket pairs inside one workgroup each, emitting
+// the output columns directly.  Used on the GPU for large inner joins on one
+// exact key where every column is fixed width <= 8 bytes.
+// ---------------------------------------------------------------------------
+static int64_t radix_join_min_rows() {
+  const char *e = std::getenv("CYLON_RADIX_JOIN_MIN_ROWS");  // tuning / test knob
+  return e ? std::atoll(e) : (int64_t(1) << 22);
+}
+
+static constexpr int64_t kRadixRowsPerPart = 4096;  // avg build rows per partition (LDS table: 6144 max)
+
+static bool radix_eligible(const TablePtr &t) {
+  int slots = 1;
+  for (const auto &c : t->columns()) {
+    const int w = c.type.width();
+    if (c.is_var() || c.type.kind() == ValueKind::FIXED_BYTES || !(w == 1 || w == 2 || w == 4 || w == 8) ||
+        c.data.element_size() != w)
+      return false;
+    slots += 1 + (c.nullable() ? 1 : 0);
+  }
+  return slots <= kMaxFusedCols;
+}
+
+struct RadixSide {
+  at::Tensor keys, offs;
+  std::vector<at::Tensor> data, valid;  // per table column (valid undefined if not nullable)
+  std::vector<bool> is_key;             // data[c] is the (partitioned) key array itself
+};
+
+// Partition every column of t (+ validity bytes) by the top `bits` bits of fmix64(key).
+static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Tensor &keys, int bits) {
+  const int64_t n = t->Rows();
+  std::vector<at::Tensor> cur{keys};
+  std::vector<int> widths{8};
+  std::vector<int> dslot(t->Columns(), -1), vslot(t->Columns(), -1);
+  for (int c = 0; c < t->Columns(); ++c) {
+    const Column &col = t->column(c);
+    if (col.type.width() == 8 && col.data.data_ptr() == keys.data_ptr()) {
+      dslot[c] = 0;  // the key column itself
+    } else {
+      dslot[c] = (int)cur.size();
+      cur.push_back(col.data);
+      widths.push_back(col.type.width());
+    }
+    if (col.nullable()) {
+      vslot[c] = (int)cur.size();
+      cur.push_back(col.validity);
+      widths.push_back(1);
+    }
+  }
+  static const int max_db = [] {  // digit bits per pass (<= 10, radix_join.hip); tuning knob
+    const char *e = std::getenv("CYLON_RADIX_DIGIT_BITS");
+    return e ? std::max(1, std::min(10, std::atoi(e))) : 10;
+  }();
+  const int npass = (bits + max_db - 1) / max_db;
+  int shift = 0;
+  at::Tensor ws;
+  for (int ps = 0; ps < npass; ++ps) {
+    const int db = (bits - shift + (npass - ps) - 1) / (npass - ps);
+    const int64_t wsn = hip::radix_rows_pass_workspace(n, db);
+    if (!ws.defined() || ws.numel() < wsn) ws = ex.empty_i64(wsn);
+    std::vector<at::Tensor> nxt;
+    std::vector<const uint8_t *> in;
+    std::vector<uint8_t *> out;
+    for (auto &x : cur) {
+      nxt.push_back(at::empty_like(x));
+      in.push_back(reinterpret_cast<const uint8_t *>(x.data_ptr()));
+      out.push_back(reinterpret_cast<uint8_t *>(nxt.back().data_ptr()));
+    }
+    hip::radix_rows_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, bits, shift, db, in.data(),
+                         out.data(), widths.data(), (int)cur.size(), ptr<int64_t>(ws), ex.stream);
+    cur = std::move(nxt);
+    shift += db;
+  }
+  RadixSide s;
+  s.keys = cur[0];
+  s.offs = ex.empty_i64((int64_t(1) << bits) + 1);
+  hip::radix_part_offsets(ptr<int64_t>(s.keys), n, bits, ptr<int64_t>(s.offs), ex.stream);
+  for (int c = 0; c < t->Columns(); ++c) {
+    s.data.push_back(cur[dslot[c]]);
+    s.valid.push_back(vslot[c] >= 0 ? cur[vslot[c]] : at::Tensor());
+    s.is_key.push_back(dslot[c] == 0);
+  }
+  return s;
+}
+
+// Column pointer lists of one side for the write kernel (nullptr input = key column).
+struct RadixCols {
+  std::vector<const uint8_t *> in;
+  std::vector<uint8_t *> out;
+  std::vector<int> w;
+};
+
+static RadixCols radix_cols(const TablePtr &t, const RadixSide *s, const std::vector<Column> *outs) {
+  RadixCols rc;
+  for (int c = 0; c < t->Columns(); ++c) {
+    const Column &col = t->column(c);
+    rc.in.push_back(s && !s->is_key[c] ? reinterpret_cast<const uint8_t *>(s->data[c].data_ptr())
+                                       : (s ? nullptr : reinterpret_cast<const uint8_t *>(1)));
+    rc.out.push_back(outs ? reinterpret_cast<uint8_t *>((*outs)[c].data.data_ptr()) : nullptr);
+    rc.w.push_back(col.type.width());
+    if (col.nullable()) {
+      rc.in.push_back(s ? s->valid[c].data_ptr<uint8_t>() : reinterpret_cast<const uint8_t *>(1));
+      rc.out.push_back(outs ? (*outs)[c].validity.data_ptr<uint8_t>() : nullptr);
+      rc.w.push_back(1);
+    }
+  }
+  return rc;
+}
+
+// Returns nullptr when a build partition overflows the LDS capacity (heavy key
+// skew / duplicates); the caller then runs the global-table join.
+static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr &right, const at::Tensor &lk,
+                           const at::Tensor &rk, const JoinConfig &cfg) {
+  const int64_t nl = left->Rows(), nr = right->Rows();
+  const bool build_left = nl < nr;
+  const TablePtr &bt = build_left ? left : right;
+  const int64_t nb = std::min(nl, nr);
+  // LDS capacity from the build side's staged row width (key column counted once)
+  RadixCols shape = radix_cols(bt, nullptr, nullptr);
+  for (int c = 0, q = 0; c < bt->Columns(); ++c, ++q) {
+    const Column &col = bt->column(c);
+    if (col.type.width() == 8 && col.data.data_ptr() == (build_left ? lk : rk).data_ptr()) shape.in[q] = nullptr;
+    if (col.nullable()) ++q;
+  }
+  const int64_t cap = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size());
+  const int64_t target = std::max<int64_t>(1, cap * 2 / 3);  // mean build rows per partition
+  int bits = 0;
+  while ((nb >> bits) > target) ++bits;
+  const int64_t nparts = int64_t(1) << bits;
+  RadixSide L, R;
+  {
+    CYLON_PHASE("join.radix.partition", ex.device);
+    L = radix_partition(ex, left, lk, bits);
+    R = radix_partition(ex, right, rk, bits);
+  }
+  RadixSide &B = build_left ? L : R;
+  RadixSide &P = build_left ? R : L;
+  at::Tensor counts = ex.empty_i64(nparts);
+  at::Tensor overflow = at::empty({1}, ex.opts(at::kInt));
+  {
+    CYLON_PHASE("join.radix.count", ex.device);
+    hip::radix_join_count(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
+                          nparts, cap, ptr<int64_t>(counts), overflow.data_ptr<int>(), ex.stream);
+  }
+  if (overflow.item<int>() != 0) {
+    trace::add_counter("join.radix.overflow_fallback", 1);
+    return nullptr;
+  }
+  at::Tensor out_offs = exclusive_scan(ex, counts);
+  const int64_t m = read_i64(out_offs, nparts);
+  CYLON_PHASE("join.radix.write", ex.device);
+  std::vector<Column> lcols, rcols;
+  for (const auto &col : left->columns())
+    lcols.push_back(make_fixed_column(cfg.GetLeftTablePrefix() + col.name, col.type, m, ex.device, col.nullable()));
+  for (const auto &col : right->columns())
+    rcols.push_back(make_fixed_column(cfg.GetRightTablePrefix() + col.name, col.type, m, ex.device, col.nullable()));
+  if (m > 0) {
+    RadixCols pc = build_left ? radix_cols(right, &R, &rcols) : radix_cols(left, &L, &lcols);
+    RadixCols bc = build_left ? radix_cols(left, &L, &lcols) : radix_cols(right, &R, &rcols);
+    // probe-side columns are streamed from HBM: the key column is read from its partitioned array
+    for (size_t q = 0; q < pc.in.size(); ++q)
+      if (!pc.in[q]) pc.in[q] = reinterpret_cast<const uint8_t *>(P.keys.data_ptr());
+    hip::radix_join_write(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
+                          nparts, cap, ptr<int64_t>(out_offs), pc.in.data(), pc.out.data(), pc.w.data(),
+                          (int)pc.in.size(), bc.in.data(), bc.out.data(), bc.w.data(), (int)bc.in.size(), ex.stream);
+  }
+  trace::add_counter("join.radix.rows_out", m);
+  for (auto &c : rcols) lcols.push_back(std::move(c));
+  return Table::Make(left->GetContext(), std::move(lcols));
+}
+
 static std::pair<at::Tensor, at::Tensor> join_impl(TablePtr left, TablePtr right, const JoinConfig &cfg,
                                                    bool allow_reorder, TablePtr *lout, TablePtr *rout);
 
@@ -201,6 +375,18 @@ static std::pair<at::Tensor, at::Tensor> join_impl(TablePtr left, TablePtr right
 }
 
 TablePtr Join(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
+  if (left->device().is_cuda() && cfg.GetType() == JoinType::INNER && cfg.GetAlgorithm() == JoinAlgorithm::HASH &&
+      cfg.GetLeftColumnIdx().size() == 1 && std::min(left->Rows(), right->Rows()) >= radix_join_min_rows() &&
+      radix_eligible(left) && radix_eligible(right)) {
+    const Column &a = left->column(cfg.GetLeftColumnIdx()[0]);
+    const Column &b = right->column(cfg.GetRightColumnIdx()[0]);
+    if (simple_key(a) && simple_key(b) && a.type == b.type) {
+      Exec ex(left->device());
+      KeyEncoding lk = encode_keys(ex, left, cfg.GetLeftColumnIdx(), true);
+      KeyEncoding rk = encode_keys(ex, right, cfg.GetRightColumnIdx(), true);
+      if (TablePtr out = radix_join(ex, left, right, lk.keys, rk.keys, cfg)) return out;
+    }
+  }
   TablePtr l = left, r = right;
   auto idx = join_impl(left, right, cfg, true, &l, &r);
   const JoinType jt = cfg.GetType();

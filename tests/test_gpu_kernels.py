@@ -130,3 +130,36 @@ def test_radix_sort_large_int64(gpu_ctx):
     t = Table.from_torch(gpu_ctx, {"k": k})
     s = t.sort("k").to_torch()["k"]
     assert torch.equal(s, torch.sort(k).values)
+
+
+def _sorted_df(t):
+    df = t.to_pandas()
+    return df.sort_values(list(df.columns), kind="stable").reset_index(drop=True)
+
+
+@pytest.mark.parametrize("case", ["int64", "int32_nullable", "dups", "skew_fallback", "left_smaller"])
+def test_radix_join_matches_global_table_join(gpu_ctx, monkeypatch, case):
+    """K5 LDS radix join (partitioned, fused materialisation) vs the global-table join."""
+    rng = np.random.default_rng(11)
+    nl, nr = 300_000, 200_000
+    if case == "left_smaller":
+        nl, nr = nr, nl
+    hi = 20000 if case == "dups" else int(0.9 * max(nl, nr))
+    kl, kr = rng.integers(0, hi, nl), rng.integers(0, hi, nr)
+    if case == "skew_fallback":
+        kr[:10_000] = 7  # one build partition > LDS table capacity -> global fallback
+    kt = pa.int32() if case == "int32_nullable" else pa.int64()
+    mask_u = rng.random(nl) < 0.1 if case == "int32_nullable" else None
+    mask_b = rng.random(nr) < 0.2 if case == "int32_nullable" else None
+    a = pa.table({"k": pa.array(kl, kt), "v": rng.random(nl),
+                  "u": pa.array(rng.integers(-300, 300, nl), pa.int16(), mask=mask_u)})
+    b = pa.table({"w": pa.array(rng.random(nr), pa.float32()), "k": pa.array(kr, kt),
+                  "b": pa.array(rng.random(nr) < 0.5, mask=mask_b)})
+    L, R = Table(a, gpu_ctx), Table(b, gpu_ctx)
+    on = dict(left_on=["k"], right_on=["k"], left_prefix="l_", right_prefix="r_")
+    monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", "1")
+    got = L.join(R, "inner", "hash", **on)
+    monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", str(1 << 62))
+    ref = L.join(R, "inner", "hash", **on)
+    assert got.column_names == ref.column_names
+    pd.testing.assert_frame_equal(_sorted_df(got), _sorted_df(ref))
