@@ -69,6 +69,19 @@ __device__ __forceinline__ void st_elem(uint8_t *dst, int64_t i, int w, uint64_t
   }
 }
 
+// Column loops below are unrolled to compile-time bounds with `q < n` guards, so
+// every ColSet field is a statically indexed kernel argument (SGPRs, loaded
+// once); a runtime-indexed field would be re-fetched with a dependent scalar
+// load per element.  W8 = every column 8 bytes wide (no width dispatch).
+template <bool W8>
+__device__ __forceinline__ uint64_t ldw(const uint8_t *p, int64_t i, int w) {
+  return W8 ? reinterpret_cast<const uint64_t *>(p)[i] : ld_elem(p, i, w);
+}
+template <bool W8>
+__device__ __forceinline__ void stw(uint8_t *p, int64_t i, int w, uint64_t v) {
+  if (W8) reinterpret_cast<uint64_t *>(p)[i] = v; else st_elem(p, i, w, v);
+}
+
 // --------------------------------------------------------------------------
 // partition pass
 // --------------------------------------------------------------------------
@@ -77,10 +90,11 @@ struct PartDigit {
   int bits;   // total partition bits
   int shift;  // digit = (part >> shift) & mask
   uint32_t mask;
-  __device__ __forceinline__ uint32_t operator()(int64_t i) const {
-    return (part_of(keys[i], bits) >> shift) & mask;
-  }
+  __device__ __forceinline__ uint32_t of_key(int64_t k) const { return (part_of(k, bits) >> shift) & mask; }
+  __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key(keys[i]); }
 };
+
+constexpr int kRPPrefetch = 4;  // columns (0 = key) loaded with the keys at tile start, held in VGPRs
 
 __global__ __launch_bounds__(kRPThreads) void k_rp_hist(PartDigit digit, int64_t n, uint32_t nbuckets,
                                                         int64_t rows_per_block, int64_t nblocks,
@@ -122,6 +136,7 @@ __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) 
   return off + inc - c;
 }
 
+template <bool W8>
 __global__ __launch_bounds__(kRPThreads) void k_rows_pass(PartDigit digit, int nbits, uint32_t nbuckets, ColSet cols,
                                                           int64_t n, int64_t rows_per_block, int64_t nblocks,
                                                           const int64_t *__restrict__ bh_scan) {
@@ -146,10 +161,21 @@ __global__ __launch_bounds__(kRPThreads) void k_rows_pass(PartDigit digit, int n
 
   for (int64_t tile = begin; tile < end; tile += kRPTile) {
     uint32_t pl[kRPItems];  // digit, then (in-wave rank << 16) | digit, then sorted slot; ~0 = inactive
+    uint64_t pv[kRPItems][kRPPrefetch];  // the tile's first columns: one exposed load latency per tile
 #pragma unroll
-    for (int k = 0; k < kRPItems; ++k) {  // 8 independent key loads in flight
+    for (int k = 0; k < kRPItems; ++k) {
       const int64_t i = tile + wrow + k * kWave + lane;
-      pl[k] = i < end ? digit(i) : 0xffffffffu;
+      if (i < end) {
+        pv[k][0] = (uint64_t)digit.keys[i];
+#pragma unroll
+        for (int q = 1; q < kRPPrefetch; ++q)
+          if (q < cols.n) pv[k][q] = ldw<W8>(cols.in[q], i, cols.width[q]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kRPItems; ++k) {
+      const int64_t i = tile + wrow + k * kWave + lane;
+      pl[k] = i < end ? digit.of_key((int64_t)pv[k][0]) : 0xffffffffu;
     }
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k) {
@@ -197,11 +223,26 @@ __global__ __launch_bounds__(kRPThreads) void k_rows_pass(PartDigit digit, int n
       pl[k] = pos;
     }
     const int cnt = (int)((end - tile) < kRPTile ? (end - tile) : kRPTile);
-    for (int c = 0; c < cols.n; ++c) {
+    uint8_t *st = reinterpret_cast<uint8_t *>(stage);
+#pragma unroll
+    for (int c = 0; c < kRPPrefetch; ++c) {  // prefetched columns: LDS stage -> sorted runs
+      if (c >= cols.n) break;
+      const int w = cols.width[c];
+#pragma unroll
+      for (int k = 0; k < kRPItems; ++k)
+        if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, pv[k][c]);
+      __syncthreads();
+      uint8_t *out = cols.out[c];
+      for (int j = threadIdx.x; j < cnt; j += kRPThreads) {
+        const uint32_t p = sdig[j];
+        stw<W8>(out, running[p] + (j - (int64_t)toff[p]), w, ldw<W8>(st, j, w));
+      }
+      __syncthreads();
+    }
+    for (int c = kRPPrefetch; c < cols.n; ++c) {  // remaining columns: load, stage, store
       const int w = cols.width[c];
       const uint8_t *in = cols.in[c];
       uint8_t *out = cols.out[c];
-      uint8_t *st = reinterpret_cast<uint8_t *>(stage);
 #pragma unroll
       for (int k = 0; k < kRPItems; ++k)
         if (pl[k] != 0xffffffffu) st_elem(st, pl[k], w, ld_elem(in, tile + wrow + k * kWave + lane, w));
@@ -260,8 +301,14 @@ void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, 
     cs.out[c] = c < ncols ? out[c] : nullptr;
     cs.width[c] = c < ncols ? widths[c] : 8;
   }
-  hipLaunchKernelGGL(k_rows_pass, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, digit_bits, nb, cs, n,
-                     g.rows_per_block, g.nblocks, (const int64_t *)bh_scan);
+  bool w8 = true;
+  for (int c = 0; c < ncols; ++c) w8 &= widths[c] == 8;
+  if (w8)
+    hipLaunchKernelGGL(k_rows_pass<true>, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, digit_bits, nb, cs,
+                       n, g.rows_per_block, g.nblocks, (const int64_t *)bh_scan);
+  else
+    hipLaunchKernelGGL(k_rows_pass<false>, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, digit_bits, nb, cs,
+                       n, g.rows_per_block, g.nblocks, (const int64_t *)bh_scan);
   HIP_LAUNCH_CHECK();
 }
 
@@ -304,30 +351,6 @@ __device__ __forceinline__ uint32_t lds_slot(int64_t k) {
   return (uint32_t)hashing::fmix64((uint64_t)k) & (kRJSlots - 1);
 }
 
-// Stage partition rows [rb, rb+nr) of the build side into LDS and index them.
-// Caller guarantees no thread still reads tab/area (barrier before the call).
-__device__ __forceinline__ void rj_stage(uint32_t *tab, uint8_t *area, const int64_t *__restrict__ bkeys, int64_t rb,
-                                         int nr, int cap, const ColSet *bc) {
-  int64_t *skeys = reinterpret_cast<int64_t *>(area);
-  for (int s = threadIdx.x; s < kRJSlots; s += blockDim.x) tab[s] = 0;
-  for (int r = threadIdx.x; r < nr; r += blockDim.x) skeys[r] = bkeys[rb + r];
-  if (bc) {
-    int64_t off = 8 * (int64_t)cap;
-    for (int q = 0; q < bc->n; ++q) {
-      if (!bc->in[q]) continue;
-      const int w = bc->width[q];
-      for (int r = threadIdx.x; r < nr; r += blockDim.x) st_elem(area + off, r, w, ld_elem(bc->in[q], rb + r, w));
-      off += (int64_t)cap * w;
-    }
-  }
-  __syncthreads();
-  for (int r = threadIdx.x; r < nr; r += blockDim.x) {
-    uint32_t s = lds_slot(skeys[r]);
-    while (atomicCAS(&tab[s], 0u, (uint32_t)(r + 1)) != 0u) s = (s + 1) & (kRJSlots - 1);
-  }
-  __syncthreads();
-}
-
 __device__ __forceinline__ uint32_t rj_count(const uint32_t *tab, const int64_t *skeys, int64_t k) {
   uint32_t s = lds_slot(k), c = 0, v;
   while ((v = tab[s]) != 0u) {
@@ -337,15 +360,28 @@ __device__ __forceinline__ uint32_t rj_count(const uint32_t *tab, const int64_t 
   return c;
 }
 
+// Build side of one partition held in VGPRs: thread t owns rows t + i * kRJThreads
+// (cap <= kRJMaxRows = 4 * kRJThreads).  Loaded together with the probe rows so
+// a partition exposes one global-memory latency, not one per phase.
+constexpr int kRJRowsPerThread = kRJMaxRows / kRJThreads;
+static_assert(kRJRowsPerThread * kRJThreads == kRJMaxRows, "build rows per thread");
+constexpr int kRJProbeRounds = 2;  // probe rounds of 64 rows per wave held in VGPRs
+
+__device__ __forceinline__ void rj_insert(uint32_t *tab, const int64_t *skeys, int nr) {
+  for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+    uint32_t s = lds_slot(skeys[r]);
+    while (atomicCAS(&tab[s], 0u, (uint32_t)(r + 1)) != 0u) s = (s + 1) & (kRJSlots - 1);
+  }
+}
+
 __global__ __launch_bounds__(kRJThreads) void k_rj_count(const int64_t *__restrict__ pkeys,
                                                          const int64_t *__restrict__ poffs,
                                                          const int64_t *__restrict__ bkeys,
                                                          const int64_t *__restrict__ boffs, int64_t nparts, int cap,
                                                          int64_t *__restrict__ counts, int *overflow) {
   __shared__ uint32_t tab[kRJSlots];
-  __shared__ __attribute__((aligned(16))) uint8_t area[kRJMaxRows * 8];
+  __shared__ int64_t skeys[kRJMaxRows];
   __shared__ unsigned long long wsum[kRJWaves];
-  const int64_t *skeys = reinterpret_cast<const int64_t *>(area);
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
     const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
     const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
@@ -360,9 +396,28 @@ __global__ __launch_bounds__(kRJThreads) void k_rj_count(const int64_t *__restri
       if (threadIdx.x == 0) counts[p] = 0;
       continue;
     }
-    rj_stage(tab, area, bkeys, rb, (int)nr, cap, nullptr);
+    int64_t bk[kRJRowsPerThread], pk[kRJRowsPerThread];
+#pragma unroll
+    for (int i = 0; i < kRJRowsPerThread; ++i) {
+      const int r = threadIdx.x + i * kRJThreads;
+      if (r < nr) bk[i] = bkeys[rb + r];
+      if (r < nl) pk[i] = pkeys[lb + r];
+    }
+    __syncthreads();  // previous partition done with tab / skeys / wsum
+    for (int s = threadIdx.x; s < kRJSlots; s += blockDim.x) tab[s] = 0;
+#pragma unroll
+    for (int i = 0; i < kRJRowsPerThread; ++i) {
+      const int r = threadIdx.x + i * kRJThreads;
+      if (r < nr) skeys[r] = bk[i];
+    }
+    __syncthreads();
+    rj_insert(tab, skeys, (int)nr);
+    __syncthreads();
     unsigned long long c = 0;
-    for (int64_t l = threadIdx.x; l < nl; l += blockDim.x) c += rj_count(tab, skeys, pkeys[lb + l]);
+#pragma unroll
+    for (int i = 0; i < kRJRowsPerThread; ++i)
+      if (threadIdx.x + i * kRJThreads < nl) c += rj_count(tab, skeys, pk[i]);
+    for (int64_t l = threadIdx.x + kRJMaxRows; l < nl; l += blockDim.x) c += rj_count(tab, skeys, pkeys[lb + l]);
     for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
     if (lane_id() == 0) wsum[threadIdx.x / kWave] = c;
     __syncthreads();
@@ -371,43 +426,120 @@ __global__ __launch_bounds__(kRJThreads) void k_rj_count(const int64_t *__restri
       for (int w = 0; w < kRJWaves; ++w) tot += wsum[w];
       counts[p] = (int64_t)tot;
     }
-    __syncthreads();
   }
 }
 
-template <int MAXP>
-__global__ __launch_bounds__(kRJThreads) void k_rj_write(const int64_t *__restrict__ pkeys,
-                                                         const int64_t *__restrict__ poffs,
-                                                         const int64_t *__restrict__ bkeys,
-                                                         const int64_t *__restrict__ boffs, int64_t nparts, int cap,
-                                                         const int64_t *__restrict__ out_offs, ColSet pc, ColSet bc) {
+struct BuildOut {               // build-side output columns
+  uint8_t *out[kMaxFusedCols];
+  int width[kMaxFusedCols];
+  int lds_off[kMaxFusedCols];   // byte offset of the staged column in the LDS row area, -1 = key
+  int n;
+};
+
+template <int MAXP, int MAXB, bool W8>
+__global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__restrict__ pkeys,
+                                                            const int64_t *__restrict__ poffs,
+                                                            const int64_t *__restrict__ bkeys,
+                                                            const int64_t *__restrict__ boffs, int64_t nparts,
+                                                            int cap, const int64_t *__restrict__ out_offs, ColSet pc,
+                                                            ColSet bs, BuildOut bo) {
+  // pc: probe columns (in -> out); bs: staged build columns (in, width), LDS
+  // region j at 8*cap + sum of cap*width of the earlier ones; bo: build outputs.
+  // The first MAXP probe / MAXB staged columns travel through VGPRs.
   __shared__ uint32_t tab[kRJSlots];
   __shared__ __attribute__((aligned(16))) uint8_t area[kRJRowArea];
   __shared__ uint32_t wtot[kRJWaves];
-  const int64_t *skeys = reinterpret_cast<const int64_t *>(area);
+  int64_t *skeys = reinterpret_cast<int64_t *>(area);
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
     const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
     const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
     if (nr == 0 || nl == 0 || nr > cap) continue;
-    __syncthreads();  // previous partition fully done with tab / area / wtot
-    rj_stage(tab, area, bkeys, rb, (int)nr, cap, &bc);
-    // each wave owns a contiguous slice of the probe rows
-    const int64_t per = (nl + kRJWaves - 1) / kRJWaves;
+    const int64_t obase = out_offs[p];
+    // ---- phase A: every global load of the partition in flight at once
+    int64_t bk[kRJRowsPerThread];
+    uint64_t bv[kRJRowsPerThread][MAXB];
+#pragma unroll
+    for (int i = 0; i < kRJRowsPerThread; ++i) {
+      const int r = threadIdx.x + i * kRJThreads;
+      if (r < nr) {
+        bk[i] = bkeys[rb + r];
+#pragma unroll
+        for (int j = 0; j < MAXB; ++j)
+          if (j < bs.n) bv[i][j] = ldw<W8>(bs.in[j], rb + r, bs.width[j]);
+      }
+    }
+    const int64_t per = (nl + kRJWaves - 1) / kRJWaves;  // each wave owns a contiguous probe slice
     const int64_t s0 = lb + std::min<int64_t>(nl, wave * per);
     const int64_t s1 = lb + std::min<int64_t>(nl, (wave + 1) * per);
+    int64_t pk[kRJProbeRounds];
+    uint64_t pv[kRJProbeRounds][MAXP];
+#pragma unroll
+    for (int u = 0; u < kRJProbeRounds; ++u) {
+      const int64_t l = s0 + u * kWave + lane;
+      if (l < s1) {
+        pk[u] = pkeys[l];
+#pragma unroll
+        for (int q = 0; q < MAXP; ++q)
+          if (q < pc.n) pv[u][q] = ldw<W8>(pc.in[q], l, pc.width[q]);
+      }
+    }
+    // ---- phase B: stage + index the build rows
+    __syncthreads();  // previous partition fully done with tab / area / wtot
+    for (int s = threadIdx.x; s < kRJSlots; s += blockDim.x) tab[s] = 0;
+#pragma unroll
+    for (int i = 0; i < kRJRowsPerThread; ++i) {
+      const int r = threadIdx.x + i * kRJThreads;
+      if (r < nr) {
+        skeys[r] = bk[i];
+        int64_t off = 8 * (int64_t)cap;
+#pragma unroll
+        for (int j = 0; j < MAXB; ++j)
+          if (j < bs.n) {
+            stw<W8>(area + off, r, bs.width[j], bv[i][j]);
+            off += (int64_t)cap * bs.width[j];
+          }
+        for (int j = MAXB; j < bs.n; ++j) {  // rare: wide build rows
+          stw<W8>(area + off, r, bs.width[j], ldw<W8>(bs.in[j], rb + r, bs.width[j]));
+          off += (int64_t)cap * bs.width[j];
+        }
+      }
+    }
+    __syncthreads();
+    rj_insert(tab, skeys, (int)nr);
+    __syncthreads();
+    // ---- phase C: count this wave's matches, slice offsets
     uint32_t c = 0;
-    for (int64_t l = s0 + lane; l < s1; l += kWave) c += rj_count(tab, skeys, pkeys[l]);
+#pragma unroll
+    for (int u = 0; u < kRJProbeRounds; ++u)
+      if (s0 + u * kWave + lane < s1) c += rj_count(tab, skeys, pk[u]);
+    for (int64_t l = s0 + kRJProbeRounds * kWave + lane; l < s1; l += kWave) c += rj_count(tab, skeys, pkeys[l]);
     for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
     if (lane == 0) wtot[wave] = c;
     __syncthreads();
-    int64_t base = out_offs[p];
+    int64_t base = obase;
     for (int w = 0; w < wave; ++w) base += wtot[w];
-    for (int64_t l0 = s0; l0 < s1; l0 += kWave) {
-      const int64_t l = l0 + lane;
+    // ---- phase D: emit
+    for (int u = 0; s0 + (int64_t)u * kWave < s1; ++u) {
+      const int64_t l = s0 + (int64_t)u * kWave + lane;
       const bool active = l < s1;
-      const int64_t k = active ? pkeys[l] : 0;
+      int64_t k = 0;
+      uint64_t v[MAXP];
+      if (u < kRJProbeRounds) {
+#pragma unroll
+        for (int uu = 0; uu < kRJProbeRounds; ++uu)
+          if (uu == u) {
+            k = pk[uu];
+#pragma unroll
+            for (int q = 0; q < MAXP; ++q) v[q] = pv[uu][q];
+          }
+      } else if (active) {
+        k = pkeys[l];
+#pragma unroll
+        for (int q = 0; q < MAXP; ++q)
+          if (q < pc.n) v[q] = ldw<W8>(pc.in[q], l, pc.width[q]);
+      }
       const uint32_t mc = active ? rj_count(tab, skeys, k) : 0u;
       uint32_t inc = mc;  // wave inclusive scan of match counts
 #pragma unroll
@@ -417,33 +549,27 @@ __global__ __launch_bounds__(kRJThreads) void k_rj_write(const int64_t *__restri
       }
       const uint32_t wsum = __shfl(inc, kWave - 1, kWave);
       int64_t o = base + (inc - mc);
-      if (mc) {
-        uint64_t pv[MAXP];  // probe row payload: all loads before any store
+      uint32_t s = lds_slot(k), left = mc, e;
+      while (left && (e = tab[s]) != 0u) {
+        const int r = (int)e - 1;
+        if (skeys[r] == k) {
 #pragma unroll
-        for (int q = 0; q < MAXP; ++q)
-          if (q < pc.n) pv[q] = ld_elem(pc.in[q], l, pc.width[q]);
-        uint32_t s = lds_slot(k), left = mc, v;
-        while (left && (v = tab[s]) != 0u) {
-          const int r = (int)v - 1;
-          if (skeys[r] == k) {
+          for (int q = 0; q < MAXP; ++q)
+            if (q < pc.n) stw<W8>(pc.out[q], o, pc.width[q], v[q]);
+          for (int q = MAXP; q < pc.n; ++q)
+            stw<W8>(pc.out[q], o, pc.width[q], ldw<W8>(pc.in[q], l, pc.width[q]));
 #pragma unroll
-            for (int q = 0; q < MAXP; ++q)
-              if (q < pc.n) st_elem(pc.out[q], o, pc.width[q], pv[q]);
-            int64_t off = 8 * (int64_t)cap;
-            for (int q = 0; q < bc.n; ++q) {
-              const int w = bc.width[q];
-              if (bc.in[q]) {
-                st_elem(bc.out[q], o, w, ld_elem(area + off, r, w));
-                off += (int64_t)cap * w;
-              } else {
-                st_elem(bc.out[q], o, w, (uint64_t)k);
-              }
-            }
-            ++o;
-            --left;
-          }
-          s = (s + 1) & (kRJSlots - 1);
+          for (int q = 0; q < MAXB + 1; ++q)
+            if (q < bo.n)
+              stw<W8>(bo.out[q], o, bo.width[q],
+                      bo.lds_off[q] < 0 ? (uint64_t)k : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
+          for (int q = MAXB + 1; q < bo.n; ++q)
+            stw<W8>(bo.out[q], o, bo.width[q],
+                    bo.lds_off[q] < 0 ? (uint64_t)k : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
+          ++o;
+          --left;
         }
+        s = (s + 1) & (kRJSlots - 1);
       }
       base += wsum;
     }
@@ -468,24 +594,42 @@ void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t 
                       const int *bw, int nbc, void *stream) {
   CYLON_CHECK(npc <= kMaxFusedCols && nbc <= kMaxFusedCols, Code::Invalid, "too many columns");
   CYLON_CHECK(cap > 0 && cap <= radix_join_capacity(bw, bin, nbc), Code::Invalid, "radix join capacity " << cap);
-  ColSet pc, bc;
+  ColSet pc, bs;
+  BuildOut bo;
   pc.n = npc;
-  bc.n = nbc;
+  bs.n = 0;
+  bo.n = nbc;
+  bool w8 = true;
   for (int q = 0; q < kMaxFusedCols; ++q) {
     pc.in[q] = q < npc ? pin[q] : nullptr;
     pc.out[q] = q < npc ? pout[q] : nullptr;
     pc.width[q] = q < npc ? pw[q] : 8;
-    bc.in[q] = q < nbc ? bin[q] : nullptr;
-    bc.out[q] = q < nbc ? bout[q] : nullptr;
-    bc.width[q] = q < nbc ? bw[q] : 8;
+    bs.in[q] = nullptr;
+    bs.out[q] = nullptr;
+    bs.width[q] = 8;
+    bo.out[q] = q < nbc ? bout[q] : nullptr;
+    bo.width[q] = q < nbc ? bw[q] : 8;
+    bo.lds_off[q] = -1;
+    if (q < npc) w8 &= pw[q] == 8;
+    if (q < nbc) w8 &= bw[q] == 8;
   }
+  int64_t off = 8 * cap;
+  for (int q = 0; q < nbc; ++q)
+    if (bin[q]) {
+      bo.lds_off[q] = (int)off;
+      off += cap * bw[q];
+      bs.in[bs.n] = bin[q];
+      bs.width[bs.n++] = bw[q];
+    }
+  CYLON_CHECK(off <= kRJRowArea, Code::Invalid, "radix join LDS rows " << off);
   hipStream_t s = as_stream(stream);
-  if (npc <= 4)
-    hipLaunchKernelGGL(k_rj_write<4>, dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys, boffs,
-                       nparts, (int)cap, out_offs, pc, bc);
+  // probe columns beyond 4 and staged build columns beyond 3 are loaded in place (slower, correct)
+  if (w8)
+    hipLaunchKernelGGL((k_rj_write<4, 3, true>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys,
+                       boffs, nparts, (int)cap, out_offs, pc, bs, bo);
   else
-    hipLaunchKernelGGL(k_rj_write<kMaxFusedCols>, dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys,
-                       boffs, nparts, (int)cap, out_offs, pc, bc);
+    hipLaunchKernelGGL((k_rj_write<4, 3, false>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys,
+                       boffs, nparts, (int)cap, out_offs, pc, bs, bo);
   HIP_LAUNCH_CHECK();
 }
 
