@@ -34,9 +34,8 @@ constexpr int kRPItems = 8;                      // rows per thread per tile
 constexpr int kRPTile = kRPThreads * kRPItems;   // 8192 rows
 constexpr int kRPMaxBuckets = 1024;
 constexpr int kRJMaxDigitBits = 10;
-constexpr int kRJSlots = 4096;                   // LDS hash slots (uint32 = build row + 1)
-constexpr int kRJRowArea = 60 * 1024;            // LDS bytes for the staged build rows
-constexpr int kRJMaxRows = kRJSlots / 2;         // load factor <= 0.5
+constexpr int kRJRowArea = 77568;                // LDS bytes for the staged build rows (2 blocks per CU)
+constexpr int kRJMaxRows = 2560;                 // build rows per partition (5 per thread)
 constexpr int kRJThreads = 512;
 constexpr int kRJWaves = kRJThreads / kWave;
 
@@ -94,7 +93,6 @@ struct PartDigit {
   __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key(keys[i]); }
 };
 
-constexpr int kRPPrefetch = 4;  // columns (0 = key) loaded with the keys at tile start, held in VGPRs
 
 __global__ __launch_bounds__(kRPThreads) void k_rp_hist(PartDigit digit, int64_t n, uint32_t nbuckets,
                                                         int64_t rows_per_block, int64_t nblocks,
@@ -136,21 +134,26 @@ __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) 
   return off + inc - c;
 }
 
+// LDS: running (8 KB) + toff (4 KB) + one 64 KB union that holds the per-wave
+// digit counters and the sorted-slot digits while ranking, then the column
+// stage (76 KB).  One 1024-thread block per CU (the ranking needs ~120 VGPRs);
+// global latency is hidden by software pipelining in registers instead: the
+// loads of column c+1 (and, during the last column, the next tile's keys) are
+// in flight while column c streams out of the stage.  Column 0 is the key.
 template <bool W8>
 __global__ __launch_bounds__(kRPThreads) void k_rows_pass(PartDigit digit, int nbits, uint32_t nbuckets, ColSet cols,
                                                           int64_t n, int64_t rows_per_block, int64_t nblocks,
                                                           const int64_t *__restrict__ bh_scan) {
   __shared__ int64_t running[kRPMaxBuckets];
-  __shared__ uint32_t toff[kRPMaxBuckets], ttot[kRPMaxBuckets];
-  __shared__ uint16_t wcnt[kRPWaves * kRPMaxBuckets];  // per-wave counts, then per-wave prefixes
-  __shared__ uint16_t sdig[kRPTile];                   // digit of each sorted slot
-  __shared__ uint64_t stage[kRPTile];                  // one column of the tile, in sorted order
+  __shared__ uint32_t toff[kRPMaxBuckets + 1];
+  __shared__ uint64_t ustage[kRPTile];  // column stage | {wcnt[16][nb] u16, sdig[tile] u16 at +32 KB}
   __shared__ uint32_t wsum[kRPWaves];
+  uint16_t *wcnt = reinterpret_cast<uint16_t *>(ustage);
+  uint16_t *sdig = wcnt + kRPWaves * kRPMaxBuckets;
+  uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
 
   const int64_t b = blockIdx.x;
   for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] = bh_scan[(int64_t)p * nblocks + b];
-  for (uint32_t q = threadIdx.x; q < kRPWaves * nbuckets; q += blockDim.x) wcnt[q] = 0;
-  __syncthreads();
   const int wave = threadIdx.x / kWave;
   const int lane = lane_id();
   const uint64_t lt = lanemask_lt();
@@ -159,24 +162,20 @@ __global__ __launch_bounds__(kRPThreads) void k_rows_pass(PartDigit digit, int n
   uint16_t *mycnt = wcnt + wave * nbuckets;
   const int wrow = wave * kWave * kRPItems;
 
+  uint64_t kv[kRPItems];  // keys of the current tile (column 0)
+#pragma unroll
+  for (int k = 0; k < kRPItems; ++k) {
+    const int64_t i = begin + wrow + k * kWave + lane;
+    if (i < end) kv[k] = (uint64_t)digit.keys[i];
+  }
   for (int64_t tile = begin; tile < end; tile += kRPTile) {
+    const int cnt = (int)((end - tile) < kRPTile ? (end - tile) : kRPTile);
     uint32_t pl[kRPItems];  // digit, then (in-wave rank << 16) | digit, then sorted slot; ~0 = inactive
-    uint64_t pv[kRPItems][kRPPrefetch];  // the tile's first columns: one exposed load latency per tile
 #pragma unroll
-    for (int k = 0; k < kRPItems; ++k) {
-      const int64_t i = tile + wrow + k * kWave + lane;
-      if (i < end) {
-        pv[k][0] = (uint64_t)digit.keys[i];
-#pragma unroll
-        for (int q = 1; q < kRPPrefetch; ++q)
-          if (q < cols.n) pv[k][q] = ldw<W8>(cols.in[q], i, cols.width[q]);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kRPItems; ++k) {
-      const int64_t i = tile + wrow + k * kWave + lane;
-      pl[k] = i < end ? digit.of_key((int64_t)pv[k][0]) : 0xffffffffu;
-    }
+    for (int k = 0; k < kRPItems; ++k)
+      pl[k] = (wrow + k * kWave + lane < cnt) ? digit.of_key((int64_t)kv[k]) : 0xffffffffu;
+    for (uint32_t q = threadIdx.x; q < kRPWaves * nbuckets; q += blockDim.x) wcnt[q] = 0;
+    __syncthreads();  // also orders the previous tile's stage reads before the counters reuse it
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k) {
       const bool active = pl[k] != 0xffffffffu;
@@ -196,22 +195,20 @@ __global__ __launch_bounds__(kRPThreads) void k_rows_pass(PartDigit digit, int n
       pl[k] = active ? (((base + rank) << 16) | p) : 0xffffffffu;
     }
     __syncthreads();
-    // per bucket: exclusive prefix over waves (in place) and the tile total
-    for (uint32_t p = threadIdx.x; p < nbuckets; p += kRPThreads) {
-      uint32_t run = 0;
-#pragma unroll
-      for (int w = 0; w < kRPWaves; ++w) {
-        const uint32_t c = wcnt[w * nbuckets + p];
-        wcnt[w * nbuckets + p] = (uint16_t)run;
-        run += c;
-      }
-      ttot[p] = run;
-    }
-    __syncthreads();
-    {
+    {  // bucket p = thread: exclusive prefix over waves (in place), then block scan of the totals
       const uint32_t p = threadIdx.x;
-      const uint32_t ex = rp_block_exscan(p < nbuckets ? ttot[p] : 0u, wsum);
+      uint32_t run = 0;
+      if (p < nbuckets) {
+#pragma unroll
+        for (int w = 0; w < kRPWaves; ++w) {
+          const uint32_t c = wcnt[w * nbuckets + p];
+          wcnt[w * nbuckets + p] = (uint16_t)run;
+          run += c;
+        }
+      }
+      const uint32_t ex = rp_block_exscan(run, wsum);
       if (p < nbuckets) toff[p] = ex;
+      if (p == nbuckets - 1) toff[nbuckets] = ex + run;
     }
     __syncthreads();
 #pragma unroll
@@ -222,40 +219,50 @@ __global__ __launch_bounds__(kRPThreads) void k_rows_pass(PartDigit digit, int n
       sdig[pos] = (uint16_t)p;
       pl[k] = pos;
     }
-    const int cnt = (int)((end - tile) < kRPTile ? (end - tile) : kRPTile);
-    uint8_t *st = reinterpret_cast<uint8_t *>(stage);
-#pragma unroll
-    for (int c = 0; c < kRPPrefetch; ++c) {  // prefetched columns: LDS stage -> sorted runs
-      if (c >= cols.n) break;
-      const int w = cols.width[c];
-#pragma unroll
-      for (int k = 0; k < kRPItems; ++k)
-        if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, pv[k][c]);
-      __syncthreads();
-      uint8_t *out = cols.out[c];
-      for (int j = threadIdx.x; j < cnt; j += kRPThreads) {
-        const uint32_t p = sdig[j];
-        stw<W8>(out, running[p] + (j - (int64_t)toff[p]), w, ldw<W8>(st, j, w));
-      }
-      __syncthreads();
-    }
-    for (int c = kRPPrefetch; c < cols.n; ++c) {  // remaining columns: load, stage, store
-      const int w = cols.width[c];
-      const uint8_t *in = cols.in[c];
-      uint8_t *out = cols.out[c];
-#pragma unroll
-      for (int k = 0; k < kRPItems; ++k)
-        if (pl[k] != 0xffffffffu) st_elem(st, pl[k], w, ld_elem(in, tile + wrow + k * kWave + lane, w));
-      __syncthreads();
-      for (int j = threadIdx.x; j < cnt; j += kRPThreads) {
-        const uint32_t p = sdig[j];
-        st_elem(out, running[p] + (j - (int64_t)toff[p]), w, ld_elem(st, j, w));
-      }
-      __syncthreads();
-    }
-    for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] += ttot[p];
-    for (uint32_t q = threadIdx.x; q < kRPWaves * nbuckets; q += blockDim.x) wcnt[q] = 0;
     __syncthreads();
+    int64_t dst[kRPItems];  // destination of sorted slot j = threadIdx.x + q * kRPThreads
+#pragma unroll
+    for (int q = 0; q < kRPItems; ++q) {
+      const int j = threadIdx.x + q * kRPThreads;
+      if (j < cnt) {
+        const uint32_t p = sdig[j];
+        dst[q] = running[p] + (j - (int64_t)toff[p]);
+      }
+    }
+    __syncthreads();  // counters / digits dead: the union becomes the column stage
+    uint64_t v[kRPItems];
+#pragma unroll
+    for (int k = 0; k < kRPItems; ++k) v[k] = kv[k];
+    const int64_t next = tile + kRPTile;
+#pragma unroll 1
+    for (int c = 0; c < cols.n; ++c) {  // column fields fetched once per column (scalar loads)
+      const int w = cols.width[c];
+      uint8_t *out = cols.out[c];
+#pragma unroll
+      for (int k = 0; k < kRPItems; ++k)
+        if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k]);
+      __syncthreads();
+      if (c + 1 < cols.n) {  // prefetch column c+1 of this tile
+        const uint8_t *in = cols.in[c + 1];
+        const int w1 = cols.width[c + 1];
+#pragma unroll
+        for (int k = 0; k < kRPItems; ++k)
+          if (pl[k] != 0xffffffffu) v[k] = ldw<W8>(in, tile + wrow + k * kWave + lane, w1);
+      } else {  // prefetch the next tile's keys
+#pragma unroll
+        for (int k = 0; k < kRPItems; ++k) {
+          const int64_t i = next + wrow + k * kWave + lane;
+          if (i < end) kv[k] = (uint64_t)digit.keys[i];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kRPItems; ++q) {
+        const int j = threadIdx.x + q * kRPThreads;
+        if (j < cnt) stw<W8>(out, dst[q], w, ldw<W8>(st, j, w));
+      }
+      __syncthreads();
+    }
+    for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] += toff[p + 1] - toff[p];
   }
 }
 
@@ -284,6 +291,8 @@ void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, 
   if (n == 0) return;
   CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
   CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
+  CYLON_CHECK(in[0] == reinterpret_cast<const uint8_t *>(keys) && widths[0] == 8, Code::Invalid,
+              "radix pass: column 0 must be the key");
   hipStream_t s = as_stream(stream);
   const uint32_t nb = 1u << digit_bits;
   const RPGeometry g = rp_geometry(n);
@@ -336,10 +345,20 @@ void radix_part_offsets(const int64_t *keys, int64_t n, int bits, int64_t *offs,
 // --------------------------------------------------------------------------
 // per-partition LDS join
 // --------------------------------------------------------------------------
-// Build rows per partition that fit the LDS row area: keys (8 B) + the staged
-// build columns (widths w[q]; in[q] == nullptr marks the key column itself).
+// The build rows of a partition are indexed by a bucketed (CSR) hash in LDS:
+// 2048 buckets by the low bits of fmix64(key) (independent of the partition
+// bits, which are the top bits), bucket starts as uint16, the keys stored in
+// bucket order and a uint16 permutation back to the staged row.  A probe scans
+// exactly its bucket (mean occupancy < 1): no clustering, no tombstones, and a
+// lane's loop length is its bucket's size.  Built with one LDS atomic per row
+// (16-bit counters packed in pairs), a block scan and one scatter.
+constexpr int kRJBuckets = 2048;
+
+// Build rows per partition that fit the LDS row area: key (8 B) + permutation
+// (2 B) + the staged build columns (widths w[q]; in[q] == nullptr marks the key
+// column itself, which is not staged twice).
 int64_t radix_join_capacity(const int *widths, const uint8_t *const *in, int n) {
-  int64_t row = 8;
+  int64_t row = 8 + 2;
   for (int q = 0; q < n; ++q)
     if (in[q]) row += widths[q];
   int64_t cap = kRJRowArea / row;
@@ -347,41 +366,66 @@ int64_t radix_join_capacity(const int *widths, const uint8_t *const *in, int n) 
   return cap & ~int64_t(7);  // multiple of 8: every column region stays 8-byte aligned
 }
 
-__device__ __forceinline__ uint32_t lds_slot(int64_t k) {
-  return (uint32_t)hashing::fmix64((uint64_t)k) & (kRJSlots - 1);
+__device__ __forceinline__ uint32_t rj_bucket(int64_t k) {
+  return (uint32_t)hashing::fmix64((uint64_t)k) & (kRJBuckets - 1);
 }
 
-__device__ __forceinline__ uint32_t rj_count(const uint32_t *tab, const int64_t *skeys, int64_t k) {
-  uint32_t s = lds_slot(k), c = 0, v;
-  while ((v = tab[s]) != 0u) {
-    c += (skeys[v - 1] == k);
-    s = (s + 1) & (kRJSlots - 1);
+// Build rows of one partition: thread t owns rows t + i * kRJThreads (cap <= kRJMaxRows).
+constexpr int kRJRowsPerThread = kRJMaxRows / kRJThreads;
+static_assert(kRJRowsPerThread * kRJThreads == kRJMaxRows, "build rows per thread");
+constexpr int kRJProbeRounds = 1;  // probe rounds of 64 rows per wave prefetched into VGPRs
+constexpr int kRJBucketsPerThread = kRJBuckets / kRJThreads;
+
+// bst[0..kRJBuckets) holds per-bucket counts on entry (exclusive starts on exit), bst[kRJBuckets] = total
+__device__ __forceinline__ void rj_scan_buckets(uint16_t *bst, uint32_t *wsum) {
+  const int lane = lane_id(), wave = threadIdx.x / kWave;
+  uint32_t c[kRJBucketsPerThread], t = 0;
+#pragma unroll
+  for (int j = 0; j < kRJBucketsPerThread; ++j) {
+    c[j] = bst[threadIdx.x * kRJBucketsPerThread + j];
+    t += c[j];
   }
+  uint32_t inc = t;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t x = __shfl_up(inc, d, kWave);
+    if (lane >= d) inc += x;
+  }
+  if (lane == kWave - 1) wsum[wave] = inc;
+  __syncthreads();
+  uint32_t off = inc - t;
+  for (int w = 0; w < wave; ++w) off += wsum[w];
+#pragma unroll
+  for (int j = 0; j < kRJBucketsPerThread; ++j) {
+    bst[threadIdx.x * kRJBucketsPerThread + j] = (uint16_t)off;
+    off += c[j];
+  }
+  if (threadIdx.x == kRJThreads - 1) bst[kRJBuckets] = (uint16_t)off;
+}
+
+// count one bucket's rank for a new row: 16-bit counters packed in pairs
+__device__ __forceinline__ uint32_t rj_claim(uint16_t *bst, uint32_t b) {
+  const uint32_t sh = (b & 1u) * 16u;
+  const uint32_t old = atomicAdd(reinterpret_cast<uint32_t *>(bst) + (b >> 1), 1u << sh);
+  return (old >> sh) & 0xffffu;
+}
+
+__device__ __forceinline__ uint32_t rj_count(const uint16_t *bst, const int64_t *skeys, int64_t k) {
+  const uint32_t b = rj_bucket(k);
+  uint32_t c = 0;
+  for (uint32_t i = bst[b], e = bst[b + 1]; i < e; ++i) c += (skeys[i] == k);
   return c;
 }
 
-// Build side of one partition held in VGPRs: thread t owns rows t + i * kRJThreads
-// (cap <= kRJMaxRows = 4 * kRJThreads).  Loaded together with the probe rows so
-// a partition exposes one global-memory latency, not one per phase.
-constexpr int kRJRowsPerThread = kRJMaxRows / kRJThreads;
-static_assert(kRJRowsPerThread * kRJThreads == kRJMaxRows, "build rows per thread");
-constexpr int kRJProbeRounds = 2;  // probe rounds of 64 rows per wave held in VGPRs
-
-__device__ __forceinline__ void rj_insert(uint32_t *tab, const int64_t *skeys, int nr) {
-  for (int r = threadIdx.x; r < nr; r += blockDim.x) {
-    uint32_t s = lds_slot(skeys[r]);
-    while (atomicCAS(&tab[s], 0u, (uint32_t)(r + 1)) != 0u) s = (s + 1) & (kRJSlots - 1);
-  }
-}
-
-__global__ __launch_bounds__(kRJThreads) void k_rj_count(const int64_t *__restrict__ pkeys,
+__global__ __launch_bounds__(kRJThreads, 4) void k_rj_count(const int64_t *__restrict__ pkeys,
                                                          const int64_t *__restrict__ poffs,
                                                          const int64_t *__restrict__ bkeys,
                                                          const int64_t *__restrict__ boffs, int64_t nparts, int cap,
                                                          int64_t *__restrict__ counts, int *overflow) {
-  __shared__ uint32_t tab[kRJSlots];
+  __shared__ __attribute__((aligned(16))) uint16_t bst[kRJBuckets + 8];
   __shared__ int64_t skeys[kRJMaxRows];
-  __shared__ unsigned long long wsum[kRJWaves];
+  __shared__ uint32_t wsum[kRJWaves];
+  __shared__ unsigned long long csum[kRJWaves];
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
     const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
     const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
@@ -403,27 +447,31 @@ __global__ __launch_bounds__(kRJThreads) void k_rj_count(const int64_t *__restri
       if (r < nr) bk[i] = bkeys[rb + r];
       if (r < nl) pk[i] = pkeys[lb + r];
     }
-    __syncthreads();  // previous partition done with tab / skeys / wsum
-    for (int s = threadIdx.x; s < kRJSlots; s += blockDim.x) tab[s] = 0;
-#pragma unroll
-    for (int i = 0; i < kRJRowsPerThread; ++i) {
-      const int r = threadIdx.x + i * kRJThreads;
-      if (r < nr) skeys[r] = bk[i];
-    }
+    __syncthreads();  // previous partition done with bst / skeys / csum
+    for (int s = threadIdx.x; s < kRJBuckets / 2; s += blockDim.x) reinterpret_cast<uint32_t *>(bst)[s] = 0;
     __syncthreads();
-    rj_insert(tab, skeys, (int)nr);
+    uint32_t rk[kRJRowsPerThread];
+#pragma unroll
+    for (int i = 0; i < kRJRowsPerThread; ++i)
+      if (threadIdx.x + i * kRJThreads < nr) rk[i] = rj_claim(bst, rj_bucket(bk[i]));
+    __syncthreads();
+    rj_scan_buckets(bst, wsum);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kRJRowsPerThread; ++i)
+      if (threadIdx.x + i * kRJThreads < nr) skeys[bst[rj_bucket(bk[i])] + rk[i]] = bk[i];
     __syncthreads();
     unsigned long long c = 0;
 #pragma unroll
     for (int i = 0; i < kRJRowsPerThread; ++i)
-      if (threadIdx.x + i * kRJThreads < nl) c += rj_count(tab, skeys, pk[i]);
-    for (int64_t l = threadIdx.x + kRJMaxRows; l < nl; l += blockDim.x) c += rj_count(tab, skeys, pkeys[lb + l]);
+      if (threadIdx.x + i * kRJThreads < nl) c += rj_count(bst, skeys, pk[i]);
+    for (int64_t l = threadIdx.x + kRJMaxRows; l < nl; l += blockDim.x) c += rj_count(bst, skeys, pkeys[lb + l]);
     for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
-    if (lane_id() == 0) wsum[threadIdx.x / kWave] = c;
+    if (lane_id() == 0) csum[threadIdx.x / kWave] = c;
     __syncthreads();
     if (threadIdx.x == 0) {
       unsigned long long tot = 0;
-      for (int w = 0; w < kRJWaves; ++w) tot += wsum[w];
+      for (int w = 0; w < kRJWaves; ++w) tot += csum[w];
       counts[p] = (int64_t)tot;
     }
   }
@@ -444,12 +492,14 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
                                                             int cap, const int64_t *__restrict__ out_offs, ColSet pc,
                                                             ColSet bs, BuildOut bo) {
   // pc: probe columns (in -> out); bs: staged build columns (in, width), LDS
-  // region j at 8*cap + sum of cap*width of the earlier ones; bo: build outputs.
-  // The first MAXP probe / MAXB staged columns travel through VGPRs.
-  __shared__ uint32_t tab[kRJSlots];
+  // region j at 10*cap + sum of cap*width of the earlier ones; bo: build outputs.
+  // Row area: keys in bucket order [0, 8 cap), permutation to the staged row
+  // [8 cap, 10 cap), payload columns in staged (original) row order.
+  __shared__ __attribute__((aligned(16))) uint16_t bst[kRJBuckets + 8];
   __shared__ __attribute__((aligned(16))) uint8_t area[kRJRowArea];
   __shared__ uint32_t wtot[kRJWaves];
   int64_t *skeys = reinterpret_cast<int64_t *>(area);
+  uint16_t *perm = reinterpret_cast<uint16_t *>(area + 8 * (int64_t)cap);
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
@@ -457,19 +507,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
     const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
     if (nr == 0 || nl == 0 || nr > cap) continue;
     const int64_t obase = out_offs[p];
-    // ---- phase A: every global load of the partition in flight at once
-    int64_t bk[kRJRowsPerThread];
-    uint64_t bv[kRJRowsPerThread][MAXB];
-#pragma unroll
-    for (int i = 0; i < kRJRowsPerThread; ++i) {
-      const int r = threadIdx.x + i * kRJThreads;
-      if (r < nr) {
-        bk[i] = bkeys[rb + r];
-#pragma unroll
-        for (int j = 0; j < MAXB; ++j)
-          if (j < bs.n) bv[i][j] = ldw<W8>(bs.in[j], rb + r, bs.width[j]);
-      }
-    }
+    // ---- phase A: probe rows of this wave's slice into VGPRs (in flight during the build)
     const int64_t per = (nl + kRJWaves - 1) / kRJWaves;  // each wave owns a contiguous probe slice
     const int64_t s0 = lb + std::min<int64_t>(nl, wave * per);
     const int64_t s1 = lb + std::min<int64_t>(nl, (wave + 1) * per);
@@ -485,36 +523,61 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
           if (q < pc.n) pv[u][q] = ldw<W8>(pc.in[q], l, pc.width[q]);
       }
     }
+    int64_t bk[kRJRowsPerThread];
+#pragma unroll
+    for (int i = 0; i < kRJRowsPerThread; ++i) {
+      const int r = threadIdx.x + i * kRJThreads;
+      if (r < nr) bk[i] = bkeys[rb + r];
+    }
     // ---- phase B: stage + index the build rows
-    __syncthreads();  // previous partition fully done with tab / area / wtot
-    for (int s = threadIdx.x; s < kRJSlots; s += blockDim.x) tab[s] = 0;
+    __syncthreads();  // previous partition fully done with bst / area / wtot
+    for (int s = threadIdx.x; s < kRJBuckets / 2; s += blockDim.x) reinterpret_cast<uint32_t *>(bst)[s] = 0;
+    {  // payload columns, column by column (5 loads in flight per column)
+      int64_t off = 10 * (int64_t)cap;
+#pragma unroll
+      for (int j = 0; j < MAXB; ++j) {
+        if (j < bs.n) {
+          uint64_t x[kRJRowsPerThread];
+#pragma unroll
+          for (int i = 0; i < kRJRowsPerThread; ++i)
+            if (threadIdx.x + i * kRJThreads < nr) x[i] = ldw<W8>(bs.in[j], rb + threadIdx.x + i * kRJThreads, bs.width[j]);
+#pragma unroll
+          for (int i = 0; i < kRJRowsPerThread; ++i)
+            if (threadIdx.x + i * kRJThreads < nr) stw<W8>(area + off, threadIdx.x + i * kRJThreads, bs.width[j], x[i]);
+          off += (int64_t)cap * bs.width[j];
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      for (int j = MAXB; j < bs.n; ++j) {  // rare: wide build rows
+        for (int r = threadIdx.x; r < nr; r += kRJThreads)
+          stw<W8>(area + off, r, bs.width[j], ldw<W8>(bs.in[j], rb + r, bs.width[j]));
+        off += (int64_t)cap * bs.width[j];
+      }
+    }
+    __syncthreads();
+    uint32_t rk[kRJRowsPerThread];
+#pragma unroll
+    for (int i = 0; i < kRJRowsPerThread; ++i)
+      if (threadIdx.x + i * kRJThreads < nr) rk[i] = rj_claim(bst, rj_bucket(bk[i]));
+    __syncthreads();
+    rj_scan_buckets(bst, wtot);
+    __syncthreads();
 #pragma unroll
     for (int i = 0; i < kRJRowsPerThread; ++i) {
       const int r = threadIdx.x + i * kRJThreads;
       if (r < nr) {
-        skeys[r] = bk[i];
-        int64_t off = 8 * (int64_t)cap;
-#pragma unroll
-        for (int j = 0; j < MAXB; ++j)
-          if (j < bs.n) {
-            stw<W8>(area + off, r, bs.width[j], bv[i][j]);
-            off += (int64_t)cap * bs.width[j];
-          }
-        for (int j = MAXB; j < bs.n; ++j) {  // rare: wide build rows
-          stw<W8>(area + off, r, bs.width[j], ldw<W8>(bs.in[j], rb + r, bs.width[j]));
-          off += (int64_t)cap * bs.width[j];
-        }
+        const uint32_t pos = bst[rj_bucket(bk[i])] + rk[i];
+        skeys[pos] = bk[i];
+        perm[pos] = (uint16_t)r;
       }
     }
-    __syncthreads();
-    rj_insert(tab, skeys, (int)nr);
     __syncthreads();
     // ---- phase C: count this wave's matches, slice offsets
     uint32_t c = 0;
 #pragma unroll
     for (int u = 0; u < kRJProbeRounds; ++u)
-      if (s0 + u * kWave + lane < s1) c += rj_count(tab, skeys, pk[u]);
-    for (int64_t l = s0 + kRJProbeRounds * kWave + lane; l < s1; l += kWave) c += rj_count(tab, skeys, pkeys[l]);
+      if (s0 + u * kWave + lane < s1) c += rj_count(bst, skeys, pk[u]);
+    for (int64_t l = s0 + kRJProbeRounds * kWave + lane; l < s1; l += kWave) c += rj_count(bst, skeys, pkeys[l]);
     for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
     if (lane == 0) wtot[wave] = c;
     __syncthreads();
@@ -540,7 +603,13 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
         for (int q = 0; q < MAXP; ++q)
           if (q < pc.n) v[q] = ldw<W8>(pc.in[q], l, pc.width[q]);
       }
-      const uint32_t mc = active ? rj_count(tab, skeys, k) : 0u;
+      uint32_t i0 = 0, i1 = 0, mc = 0;
+      if (active) {
+        const uint32_t b = rj_bucket(k);
+        i0 = bst[b];
+        i1 = bst[b + 1];
+        for (uint32_t i = i0; i < i1; ++i) mc += (skeys[i] == k);
+      }
       uint32_t inc = mc;  // wave inclusive scan of match counts
 #pragma unroll
       for (int d = 1; d < kWave; d <<= 1) {
@@ -549,10 +618,10 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
       }
       const uint32_t wsum = __shfl(inc, kWave - 1, kWave);
       int64_t o = base + (inc - mc);
-      uint32_t s = lds_slot(k), left = mc, e;
-      while (left && (e = tab[s]) != 0u) {
-        const int r = (int)e - 1;
-        if (skeys[r] == k) {
+      if (mc) {
+        for (uint32_t i = i0; i < i1; ++i) {
+          if (skeys[i] != k) continue;
+          const int r = perm[i];
 #pragma unroll
           for (int q = 0; q < MAXP; ++q)
             if (q < pc.n) stw<W8>(pc.out[q], o, pc.width[q], v[q]);
@@ -567,9 +636,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
             stw<W8>(bo.out[q], o, bo.width[q],
                     bo.lds_off[q] < 0 ? (uint64_t)k : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
           ++o;
-          --left;
         }
-        s = (s + 1) & (kRJSlots - 1);
       }
       base += wsum;
     }
@@ -613,7 +680,7 @@ void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t 
     if (q < npc) w8 &= pw[q] == 8;
     if (q < nbc) w8 &= bw[q] == 8;
   }
-  int64_t off = 8 * cap;
+  int64_t off = 10 * cap;
   for (int q = 0; q < nbc; ++q)
     if (bin[q]) {
       bo.lds_off[q] = (int)off;

@@ -36,6 +36,29 @@ __global__ void k_copy4(Cols c, long n, int perm) {
   }
 }
 
+// radix-pass write pattern: every 8192-row tile sends one run of R rows to each of 8192/R buckets
+template <bool NT>
+__global__ void k_scatter_runs(Cols c, long n, int R) {
+  const long nb = 8192 / R, bsize = n / nb;
+  long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const long tile = i >> 13, j = i & 8191;
+    const long d = (j / R) * bsize + tile * R + (j % R);
+    long v0 = c.in[0][i], v1 = c.in[1][i], v2 = c.in[2][i], v3 = c.in[3][i];
+    if (NT) {
+      __builtin_nontemporal_store(v0, &c.out[0][d]);
+      __builtin_nontemporal_store(v1, &c.out[1][d]);
+      __builtin_nontemporal_store(v2, &c.out[2][d]);
+      __builtin_nontemporal_store(v3, &c.out[3][d]);
+    } else {
+      c.out[0][d] = v0;
+      c.out[1][d] = v1;
+      c.out[2][d] = v2;
+      c.out[3][d] = v3;
+    }
+  }
+}
+
 __global__ void k_copy1(const long *in, long *out, long n) {
   long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = in[i];
@@ -77,6 +100,19 @@ struct CopyArg {
 static void run_copy(void *p) {
   CopyArg *a = (CopyArg *)p;
   hipLaunchKernelGGL(k_copy4, dim3(4096), dim3(256), 0, 0, a->c, a->n, a->perm);
+}
+struct ScatArg {
+  Cols c;
+  long n;
+  int R;
+  bool nt;
+};
+static void run_scat(void *p) {
+  ScatArg *a = (ScatArg *)p;
+  if (a->nt)
+    hipLaunchKernelGGL(k_scatter_runs<true>, dim3(4096), dim3(256), 0, 0, a->c, a->n, a->R);
+  else
+    hipLaunchKernelGGL(k_scatter_runs<false>, dim3(4096), dim3(256), 0, 0, a->c, a->n, a->R);
 }
 struct Copy1Arg {
   const long *in;
@@ -134,6 +170,21 @@ int main(int argc, char **argv) {
       fflush(stdout);
     }
   }
+  for (int nt = 0; nt < 2; ++nt)
+    for (int R = 2; R <= 128; R *= 2) {
+      ScatArg a;
+      for (int c = 0; c < 4; ++c) {
+        a.c.in[c] = sep[c];
+        a.c.out[c] = sep[4 + c];
+      }
+      a.n = n;
+      a.R = R;
+      a.nt = nt;
+      ms = timeit(run_scat, &a, 3);
+      printf("scatter runs of %3d rows (%4d buckets) %s: %.3f ms  %.2f TB/s\n", R, 8192 / R, nt ? "nt   " : "plain", ms,
+             8.0 * bytes / ms / 1e9);
+      fflush(stdout);
+    }
   long *sink;
   CK(hipMalloc(&sink, 8));
   for (long w = 1L << 20; w <= (long)bytes * 8; w <<= 2) {
