@@ -57,6 +57,14 @@ constexpr int kMaxFusedCols = 16;  // columns handled by one multi-column launch
 
 // Aggregation op ids, numerically identical to the reference
 // (cpp/src/cylon/compute/aggregate_kernels.hpp:40-50).
+// one accumulator of the LDS radix group-by (radix_groupby.hip)
+struct RGAccDesc {
+  const uint8_t *src;    // partitioned value column (nullptr: plain row count)
+  const uint8_t *valid;  // partitioned validity bytes (nullptr: all valid)
+  int kind;              // 0 SUM_F64, 1 SUM_I64, 2 MIN (order image), 3 MAX (order image), 4 COUNT
+  int width, vkind;      // value width / ValueKind
+};
+
 enum AggOp : int {
   AGG_SUM = 0,
   AGG_MIN = 1,

@@ -1,0 +1,284 @@
+// LDS radix hash group-by for large single-integer-key aggregations (K8, gfx950).
+//
+// Reference behaviour: cpp/src/cylon/groupby/hash_groupby.cpp:30-190 (one
+// pass over rows into a std::unordered_map of per-group aggregation states).
+// On MI355X a group table far beyond the 4 MB per-XCD L2 turns every row into
+// a random global atomic (~50 G accesses/s, tools/membench.hip), so this path
+//   1. estimates the number of distinct keys with a HyperLogLog sketch
+//      (2^14 registers, LDS-privatised per block, one pass over the keys);
+//   2. radix-partitions key + value columns by the top bits of fmix64(key)
+//      (radix_join.hip passes) so each partition holds ~0.6 x 4096 distinct
+//      keys;
+//   3. aggregates one partition per workgroup in an LDS open-addressing table
+//      (64-bit LDS CAS on the key, LDS atomics for the states: f64 add, i64
+//      add, u64 min/max on order-preserving images, counts), then compacts
+//      the partition's groups with a block scan into a slab at the
+//      partition's row offset (groups <= rows), with the group count per
+//      partition;
+//   4. a copy kernel packs the slabs after a device scan of the counts.
+// A partition whose distinct keys overflow the table is reported and the
+// caller falls back to the global path.
+#include "device_common.hpp"
+
+namespace cylon {
+namespace hip {
+
+constexpr int kHllBits = 14;
+constexpr int kHllRegs = 1 << kHllBits;
+constexpr int kRGThreads = 512;
+constexpr int kRGWaves = kRGThreads / kWave;
+constexpr int64_t kRGEmpty = INT64_MIN;  // empty-slot sentinel; the key INT64_MIN itself gets slot S
+
+__global__ __launch_bounds__(kBlock) void k_hll(const int64_t *__restrict__ keys, int64_t n,
+                                                uint32_t *__restrict__ regs) {
+  __shared__ uint32_t r[kHllRegs];
+  for (int i = threadIdx.x; i < kHllRegs; i += blockDim.x) r[i] = 0;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t h = hashing::fmix64((uint64_t)keys[i]);
+    const uint32_t idx = (uint32_t)(h >> (64 - kHllBits));
+    const uint32_t rho = (uint32_t)__clzll((h << kHllBits) | (1ull << (kHllBits - 1))) + 1;
+    atomicMax(&r[idx], rho);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kHllRegs; i += blockDim.x)
+    if (r[i]) atomicMax(&regs[i], r[i]);
+}
+
+double distinct_estimate(const int64_t *keys, int64_t n, uint32_t *regs, void *stream) {
+  hipStream_t s = as_stream(stream);
+  HIP_CHECK(hipMemsetAsync(regs, 0, sizeof(uint32_t) * kHllRegs, s));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_hll, dim3(grid_for(n, kBlock, kNumCUs * 2)), dim3(kBlock), 0, s, keys, n, regs);
+    HIP_LAUNCH_CHECK();
+  }
+  std::vector<uint32_t> h(kHllRegs);
+  HIP_CHECK(hipMemcpyAsync(h.data(), regs, sizeof(uint32_t) * kHllRegs, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  double z = 0.0;
+  int zeros = 0;
+  for (uint32_t x : h) {
+    z += std::ldexp(1.0, -(int)x);
+    zeros += x == 0;
+  }
+  const double m = kHllRegs;
+  double est = (0.7213 / (1.0 + 1.079 / m)) * m * m / z;
+  if (est <= 2.5 * m && zeros > 0) est = m * std::log(m / zeros);  // linear counting
+  return est;
+}
+
+// accumulator kinds
+enum RGKind : int { RG_SUMF = 0, RG_SUMI = 1, RG_MIN = 2, RG_MAX = 3, RG_CNT = 4 };
+
+struct RGArgs {
+  RGAccDesc acc[4];
+  int nacc;
+};
+
+__device__ __forceinline__ uint64_t rg_img(uint64_t bits, int w, int kind) {
+  const int nb = 8 * w;
+  const uint64_t mask = (nb == 64) ? ~0ull : ((1ull << nb) - 1);
+  const uint64_t sign = 1ull << (nb - 1);
+  bits &= mask;
+  if (kind == static_cast<int>(ValueKind::SIGNED_INT)) return bits ^ sign;
+  if (kind == static_cast<int>(ValueKind::FLOAT)) {
+    if (bits == sign) bits = 0;
+    return (bits & sign) ? (~bits & mask) : (bits | sign);
+  }
+  return bits;
+}
+
+__device__ __forceinline__ double rg_double(uint64_t b, int w, int kind) {
+  if (kind == static_cast<int>(ValueKind::FLOAT)) {
+    if (w == 8) return __longlong_as_double((long long)b);
+    if (w == 4) return (double)__int_as_float((int)b);
+    return (double)__half2float(__ushort_as_half((unsigned short)b));
+  }
+  if (kind == static_cast<int>(ValueKind::SIGNED_INT)) return (double)extend_bits(b, w, kind);
+  return (double)b;
+}
+
+__device__ __forceinline__ uint64_t rg_init(int kind) { return kind == RG_MIN ? ~0ull : 0ull; }
+
+template <int A, int S>
+__global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict__ keys,
+                                                       const int64_t *__restrict__ offs, int64_t nparts, RGArgs a,
+                                                       int64_t *__restrict__ okeys, uint64_t *__restrict__ oacc,
+                                                       int64_t n, int64_t *__restrict__ gcount, int *overflow) {
+  __shared__ int64_t tk[S + 1];
+  __shared__ unsigned long long ta[A][S + 1];
+  __shared__ uint32_t wsum[kRGWaves];
+  __shared__ int bad;
+  const int lane = lane_id(), wave = threadIdx.x / kWave;
+  for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
+    const int64_t rb = offs[p], re = offs[p + 1];
+    if (rb == re) {
+      if (threadIdx.x == 0) gcount[p] = 0;
+      continue;
+    }
+    __syncthreads();  // previous partition done with the table
+    for (int s = threadIdx.x; s <= S; s += blockDim.x) {
+      tk[s] = kRGEmpty;
+#pragma unroll
+      for (int j = 0; j < A; ++j)
+        if (j < a.nacc) ta[j][s] = rg_init(a.acc[j].kind);
+    }
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    for (int64_t r = rb + threadIdx.x; r < re; r += blockDim.x) {
+      const int64_t k = keys[r];
+      uint64_t vb[A];
+#pragma unroll
+      for (int j = 0; j < A; ++j)
+        if (j < a.nacc && a.acc[j].src) vb[j] = load_bits(a.acc[j].src, r, a.acc[j].width);
+      int slot = S;
+      if (k != kRGEmpty) {
+        uint32_t s = (uint32_t)hashing::fmix64((uint64_t)k) & (S - 1);
+        int probes = 0;
+        while (true) {
+          const int64_t cur = tk[s];
+          if (cur == k) break;
+          if (cur == kRGEmpty) {
+            const unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long *>(&tk[s]),
+                                                      (unsigned long long)kRGEmpty, (unsigned long long)k);
+            if (prev == (unsigned long long)kRGEmpty || prev == (unsigned long long)k) break;
+            continue;  // lost the race to another key: re-read this slot
+          }
+          s = (s + 1) & (S - 1);
+          if (++probes >= S) {
+            s = S + 1;  // table full
+            break;
+          }
+        }
+        if (s > S) {
+          atomicOr(&bad, 1);
+          continue;
+        }
+        slot = (int)s;
+      }  // else: the INT64_MIN key accumulates into slot S
+#pragma unroll
+      for (int j = 0; j < A; ++j) {
+        if (j >= a.nacc) continue;
+        const RGAccDesc &c = a.acc[j];
+        if (c.valid && !c.valid[r]) continue;
+        unsigned long long *t = &ta[j][slot];
+        switch (c.kind) {
+          case RG_SUMF: atomicAdd(reinterpret_cast<double *>(t), rg_double(vb[j], c.width, c.vkind)); break;
+          case RG_SUMI: atomicAdd(t, (unsigned long long)extend_bits(vb[j], c.width, c.vkind)); break;
+          case RG_MIN: atomicMin(t, (unsigned long long)rg_img(vb[j], c.width, c.vkind)); break;
+          case RG_MAX: atomicMax(t, (unsigned long long)rg_img(vb[j], c.width, c.vkind)); break;
+          default: atomicAdd(t, 1ull);
+        }
+      }
+      if (slot == S) atomicOr(&bad, 2);  // INT64_MIN present
+    }
+    __syncthreads();
+    if (bad & 1) {
+      if (threadIdx.x == 0) {
+        atomicOr(overflow, 1);
+        gcount[p] = 0;
+      }
+      continue;
+    }
+    // compact occupied slots (+ slot S when the INT64_MIN key occurred) into the slab at rb
+    constexpr int kPer = (S + kRGThreads - 1) / kRGThreads;
+    uint32_t occ = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int s = threadIdx.x * kPer + q;
+      if (s < S && tk[s] != kRGEmpty) occ |= 1u << q;
+    }
+    const uint32_t c = __popc(occ);
+    uint32_t inc = c;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t x = __shfl_up(inc, d, kWave);
+      if (lane >= d) inc += x;
+    }
+    if (lane == kWave - 1) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t pos = inc - c, tot = 0;
+    for (int w = 0; w < kRGWaves; ++w) {
+      pos += (w < wave) ? wsum[w] : 0u;
+      tot += wsum[w];
+    }
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      if (!(occ >> q & 1u)) continue;
+      const int s = threadIdx.x * kPer + q;
+      const int64_t o = rb + pos++;
+      okeys[o] = tk[s];
+#pragma unroll
+      for (int j = 0; j < A; ++j)
+        if (j < a.nacc) oacc[(int64_t)j * n + o] = ta[j][s];
+    }
+    if (threadIdx.x == 0) {
+      const bool has_min = (bad & 2) != 0;
+      if (has_min) {
+        const int64_t o = rb + tot;
+        okeys[o] = kRGEmpty;
+        for (int j = 0; j < A; ++j)
+          if (j < a.nacc) oacc[(int64_t)j * n + o] = ta[j][S];
+      }
+      gcount[p] = tot + (has_min ? 1 : 0);
+    }
+  }
+}
+
+// out[goff[p] + i] = slab[offs[p] + i] for i < count[p] (keys + nacc accumulator planes)
+__global__ void k_rg_pack(const int64_t *__restrict__ offs, const int64_t *__restrict__ goff, int64_t nparts,
+                          const int64_t *__restrict__ okeys, const uint64_t *__restrict__ oacc, int64_t n, int nacc,
+                          int64_t *__restrict__ keys_out, uint64_t *__restrict__ acc_out, int64_t ngroups) {
+  for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
+    const int64_t src = offs[p], dst = goff[p], cnt = goff[p + 1] - dst;
+    for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+      keys_out[dst + i] = okeys[src + i];
+      for (int j = 0; j < nacc; ++j) acc_out[(int64_t)j * ngroups + dst + i] = oacc[(int64_t)j * n + src + i];
+    }
+  }
+}
+
+int64_t distinct_estimate_workspace() { return kHllRegs; }
+
+void radix_groupby_agg(const int64_t *keys, const int64_t *offs, int64_t nparts, const RGAccDesc *acc, int nacc,
+                       int64_t *okeys, uint64_t *oacc, int64_t n, int64_t *gcount, int *overflow, void *stream) {
+  CYLON_CHECK(nacc >= 0 && nacc <= 4, Code::Invalid, "radix group-by: at most 4 accumulators");
+  RGArgs a;
+  a.nacc = nacc;
+  for (int j = 0; j < 4; ++j) {
+    a.acc[j].src = j < nacc ? acc[j].src : nullptr;
+    a.acc[j].valid = j < nacc ? acc[j].valid : nullptr;
+    a.acc[j].kind = j < nacc ? acc[j].kind : RG_CNT;
+    a.acc[j].width = j < nacc ? acc[j].width : 8;
+    a.acc[j].vkind = j < nacc ? acc[j].vkind : 0;
+  }
+  hipStream_t s = as_stream(stream);
+  HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
+  const int grid = (int)std::min<int64_t>(nparts, kNumCUs * 4);
+  // LDS (keys + states) <= 64 KB: two or more blocks per CU
+  if (nacc <= 1)
+    hipLaunchKernelGGL((k_rg_agg<1, 4096>), dim3(grid), dim3(kRGThreads), 0, s, keys, offs, nparts, a, okeys, oacc,
+                       n, gcount, overflow);
+  else if (nacc <= 3)
+    hipLaunchKernelGGL((k_rg_agg<3, 2048>), dim3(grid), dim3(kRGThreads), 0, s, keys, offs, nparts, a, okeys, oacc,
+                       n, gcount, overflow);
+  else
+    hipLaunchKernelGGL((k_rg_agg<4, 1024>), dim3(grid), dim3(kRGThreads), 0, s, keys, offs, nparts, a, okeys, oacc,
+                       n, gcount, overflow);
+  HIP_LAUNCH_CHECK();
+}
+
+int64_t radix_groupby_slots(int nacc) { return nacc <= 1 ? 4096 : (nacc <= 3 ? 2048 : 1024); }
+
+void radix_groupby_pack(const int64_t *offs, const int64_t *goff, int64_t nparts, const int64_t *okeys,
+                        const uint64_t *oacc, int64_t n, int nacc, int64_t *keys_out, uint64_t *acc_out,
+                        int64_t ngroups, void *stream) {
+  const int grid = (int)std::min<int64_t>(nparts, kNumCUs * 8);
+  hipLaunchKernelGGL(k_rg_pack, dim3(grid), dim3(kBlock), 0, as_stream(stream), offs, goff, nparts, okeys, oacc, n,
+                     nacc, keys_out, acc_out, ngroups);
+  HIP_LAUNCH_CHECK();
+}
+
+}  // namespace hip
+}  // namespace cylon

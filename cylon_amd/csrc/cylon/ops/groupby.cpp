@@ -13,6 +13,7 @@
 //   * output names carry a single prefix (the reference double-prefixes in
 //     its two-phase path);
 //   * COUNT counts non-null values (identical to the reference on non-null data).
+#include <cstdlib>
 #include <limits>
 
 #include "relational.hpp"
@@ -235,9 +236,167 @@ static Column agg_column(const Exec &ex, const TablePtr &t, const GroupInfo &gi,
   CYLON_THROW(Code::NotImplemented, "aggregation op " << a.op << " not supported");
 }
 
+// ---------------------------------------------------------------------------
+// K8 LDS radix group-by (radix_groupby.hip): large inputs, one integer key,
+// SUM / COUNT / MIN / MAX / MEAN.  Groups come out in partition order (the
+// hash path's first-occurrence order is not kept; the reference's hash
+// group-by order is unspecified as well).  Returns nullptr when not eligible
+// or when a partition overflows its LDS table.
+// ---------------------------------------------------------------------------
+static int64_t radix_groupby_min_rows() {
+  const char *e = std::getenv("CYLON_RADIX_GROUPBY_MIN_ROWS");  // tuning / test knob
+  return e ? std::atoll(e) : (int64_t(1) << 22);
+}
+
+static TablePtr radix_groupby(const TablePtr &t, int key, const std::vector<AggSpec> &aggs) {
+  const int64_t n = t->Rows();
+  if (!t->device().is_cuda() || n < radix_groupby_min_rows()) return nullptr;
+  const Column &kc = t->column(key);
+  if (!simple_key(kc) || (kc.type.kind() != ValueKind::SIGNED_INT && kc.type.kind() != ValueKind::UNSIGNED_INT))
+    return nullptr;
+  struct Plan {
+    int col, kind;  // kind: 0 SUMF 1 SUMI 2 MIN 3 MAX 4 CNT
+  };
+  std::vector<Plan> plan;
+  auto need = [&](int col, int kind) {
+    for (size_t j = 0; j < plan.size(); ++j)
+      if (plan[j].col == col && plan[j].kind == kind) return (int)j;
+    plan.push_back({col, kind});
+    return (int)plan.size() - 1;
+  };
+  struct Out {
+    int op, col, a, b;  // accumulator indices (b: count for MEAN / nullable MIN,MAX)
+  };
+  std::vector<Out> outs;
+  for (const auto &a : aggs) {
+    const Column &c = t->column(a.col);
+    const int w = c.type.width();
+    if (c.is_var() || c.type.kind() == ValueKind::FIXED_BYTES || !c.type.is_numeric() ||
+        !(w == 1 || w == 2 || w == 4 || w == 8))
+      return nullptr;
+    const bool fl = c.type.kind() == ValueKind::FLOAT;
+    switch (a.op) {
+      case AGG_SUM: outs.push_back({a.op, a.col, need(a.col, fl ? 0 : 1), -1}); break;
+      case AGG_COUNT: outs.push_back({a.op, a.col, need(a.col, 4), -1}); break;
+      case AGG_MIN:
+      case AGG_MAX:
+        outs.push_back({a.op, a.col, need(a.col, a.op == AGG_MIN ? 2 : 3), c.nullable() ? need(a.col, 4) : -1});
+        break;
+      case AGG_MEAN: outs.push_back({a.op, a.col, need(a.col, 0), need(a.col, 4)}); break;
+      default: return nullptr;
+    }
+  }
+  if (plan.size() > 4) return nullptr;
+  Exec ex(t->device());
+  const int nacc = (int)plan.size();
+  at::Tensor keys;
+  if (kc.type.width() == 8) {
+    keys = kc.data.view(at::kLong);
+  } else {
+    keys = ex.empty_i64(n);
+    hip::key64_from_column(kc.view(), n, ptr<int64_t>(keys), ex.stream);
+  }
+  double est;
+  {
+    CYLON_PHASE("groupby.radix.estimate", ex.device);
+    at::Tensor regs = at::empty({hip::distinct_estimate_workspace()}, ex.opts(at::kInt));
+    est = hip::distinct_estimate(ptr<int64_t>(keys), n, reinterpret_cast<uint32_t *>(ptr<int32_t>(regs)), ex.stream);
+  }
+  const double target = 0.6 * (double)hip::radix_groupby_slots(nacc);  // mean distinct keys per partition
+  int bits = 0;
+  while (bits < 24 && est * 1.05 / (double)(int64_t(1) << bits) > target) ++bits;
+  // partition set: key, each used value column, its validity
+  std::vector<at::Tensor> cols{keys};
+  std::vector<int> widths{8};
+  std::vector<int> dslot(t->Columns(), -1), vslot(t->Columns(), -1);
+  for (const auto &pl : plan) {
+    const Column &c = t->column(pl.col);
+    if (dslot[pl.col] < 0) {
+      dslot[pl.col] = (int)cols.size();
+      cols.push_back(c.data);
+      widths.push_back(c.type.width());
+      if (c.nullable()) {
+        vslot[pl.col] = (int)cols.size();
+        cols.push_back(c.validity);
+        widths.push_back(1);
+      }
+    }
+  }
+  at::Tensor offs;
+  if (bits > 0) {
+    CYLON_PHASE("groupby.radix.partition", ex.device);
+    cols = RadixPartition(ex, std::move(cols), widths, bits, &offs);
+  } else {
+    offs = at::tensor({int64_t(0), n}, at::TensorOptions().dtype(at::kLong)).to(ex.device);
+  }
+  const int64_t nparts = int64_t(1) << bits;
+  std::vector<RGAccDesc> desc(nacc);
+  for (int j = 0; j < nacc; ++j) {
+    const Column &c = t->column(plan[j].col);
+    desc[j].src = plan[j].kind == 4 ? nullptr : reinterpret_cast<const uint8_t *>(cols[dslot[plan[j].col]].data_ptr());
+    desc[j].valid = vslot[plan[j].col] >= 0 ? cols[vslot[plan[j].col]].data_ptr<uint8_t>() : nullptr;
+    desc[j].kind = plan[j].kind;
+    desc[j].width = c.type.width();
+    desc[j].vkind = static_cast<int>(c.type.kind());
+  }
+  at::Tensor okeys = ex.empty_i64(n), oacc = ex.empty_i64(std::max(1, nacc) * n), gcount = ex.empty_i64(nparts);
+  at::Tensor overflow = at::empty({1}, ex.opts(at::kInt));
+  {
+    CYLON_PHASE("groupby.radix.aggregate", ex.device);
+    hip::radix_groupby_agg(ptr<int64_t>(cols[0]), ptr<int64_t>(offs), nparts, desc.data(), nacc, ptr<int64_t>(okeys),
+                           reinterpret_cast<uint64_t *>(ptr<int64_t>(oacc)), n, ptr<int64_t>(gcount),
+                           overflow.data_ptr<int>(), ex.stream);
+  }
+  if (overflow.item<int>() != 0) {
+    trace::add_counter("groupby.radix.overflow_fallback", 1);
+    return nullptr;
+  }
+  at::Tensor goff = exclusive_scan(ex, gcount);
+  const int64_t ng = read_i64(goff, nparts);
+  at::Tensor gkeys = ex.empty_i64(ng), gacc = ex.empty_i64(std::max(1, nacc) * ng);
+  if (ng > 0)
+    hip::radix_groupby_pack(ptr<int64_t>(offs), ptr<int64_t>(goff), nparts, ptr<int64_t>(okeys),
+                            reinterpret_cast<const uint64_t *>(ptr<int64_t>(oacc)), n, nacc, ptr<int64_t>(gkeys),
+                            reinterpret_cast<uint64_t *>(ptr<int64_t>(gacc)), ng, ex.stream);
+  trace::add_counter("groupby.radix.groups", ng);
+  auto plane = [&](int j) { return gacc.slice(0, j * ng, (j + 1) * ng); };
+  std::vector<Column> out;
+  {
+    at::Tensor kd = kc.type.width() == 8 ? gkeys : gkeys.to(kc.data.scalar_type());
+    out.emplace_back(kc.name, kc.type, ng, kd.contiguous());
+  }
+  for (const auto &o : outs) {
+    const Column &c = t->column(o.col);
+    const std::string name = std::string(AggPrefix(o.op)) + c.name;
+    switch (o.op) {
+      case AGG_SUM:
+        if (c.type.kind() == ValueKind::FLOAT) out.push_back(double_col(name, plane(o.a).view(at::kDouble)));
+        else
+          out.push_back(long_col(name, plane(o.a),
+                                 c.type.kind() == ValueKind::UNSIGNED_INT ? Type::UINT64 : Type::INT64));
+        break;
+      case AGG_COUNT: out.push_back(long_col(name, plane(o.a))); break;
+      case AGG_MIN:
+      case AGG_MAX: {
+        at::Tensor cnt = o.b >= 0 ? plane(o.b) : at::Tensor();
+        out.push_back(minmax_col(ex, name, c, plane(o.a).contiguous(), cnt));
+        break;
+      }
+      case AGG_MEAN: {
+        at::Tensor s = plane(o.a).view(at::kDouble), cnt = plane(o.b);
+        out.push_back(double_col(name, s / cnt.to(at::kDouble), cnt > 0));
+        break;
+      }
+    }
+  }
+  return Table::Make(t->GetContext(), std::move(out));
+}
+
 static TablePtr groupby_with(const TablePtr &t, const std::vector<int> &keys, const std::vector<AggSpec> &aggs,
                              bool presorted) {
   CYLON_CHECK(!keys.empty(), Code::Invalid, "group-by needs at least one key column");
+  if (!presorted && keys.size() == 1)
+    if (TablePtr r = radix_groupby(t, keys[0], aggs)) return r;
   Exec ex(t->device());
   GroupInfo gi;
   {

@@ -160,7 +160,6 @@ struct RadixSide {
 
 // Partition every column of t (+ validity bytes) by the top `bits` bits of fmix64(key).
 static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Tensor &keys, int bits) {
-  const int64_t n = t->Rows();
   std::vector<at::Tensor> cur{keys};
   std::vector<int> widths{8};
   std::vector<int> dslot(t->Columns(), -1), vslot(t->Columns(), -1);
@@ -179,34 +178,11 @@ static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Te
       widths.push_back(1);
     }
   }
-  static const int max_db = [] {  // digit bits per pass (<= 10, radix_join.hip); tuning knob
-    const char *e = std::getenv("CYLON_RADIX_DIGIT_BITS");
-    return e ? std::max(1, std::min(10, std::atoi(e))) : 10;
-  }();
-  const int npass = (bits + max_db - 1) / max_db;
-  int shift = 0;
-  at::Tensor ws;
-  for (int ps = 0; ps < npass; ++ps) {
-    const int db = (bits - shift + (npass - ps) - 1) / (npass - ps);
-    const int64_t wsn = hip::radix_rows_pass_workspace(n, db);
-    if (!ws.defined() || ws.numel() < wsn) ws = ex.empty_i64(wsn);
-    std::vector<at::Tensor> nxt;
-    std::vector<const uint8_t *> in;
-    std::vector<uint8_t *> out;
-    for (auto &x : cur) {
-      nxt.push_back(at::empty_like(x));
-      in.push_back(reinterpret_cast<const uint8_t *>(x.data_ptr()));
-      out.push_back(reinterpret_cast<uint8_t *>(nxt.back().data_ptr()));
-    }
-    hip::radix_rows_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, bits, shift, db, in.data(),
-                         out.data(), widths.data(), (int)cur.size(), ptr<int64_t>(ws), ex.stream);
-    cur = std::move(nxt);
-    shift += db;
-  }
+  at::Tensor offs;
+  cur = RadixPartition(ex, std::move(cur), widths, bits, &offs);
   RadixSide s;
   s.keys = cur[0];
-  s.offs = ex.empty_i64((int64_t(1) << bits) + 1);
-  hip::radix_part_offsets(ptr<int64_t>(s.keys), n, bits, ptr<int64_t>(s.offs), ex.stream);
+  s.offs = offs;
   for (int c = 0; c < t->Columns(); ++c) {
     s.data.push_back(cur[dslot[c]]);
     s.valid.push_back(vslot[c] >= 0 ? cur[vslot[c]] : at::Tensor());

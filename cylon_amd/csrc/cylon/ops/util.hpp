@@ -52,6 +52,13 @@ inline std::vector<int64_t> to_host_vec(const at::Tensor &t) {
   return std::vector<int64_t>(h.data_ptr<int64_t>(), h.data_ptr<int64_t>() + h.numel());
 }
 
+// Radix-partition tensors by the top `bits` bits of fmix64(cols[0]) (cols[0] =
+// int64 keys, widths 1/2/4/8 bytes) with LSD passes of <= 10 bits
+// (radix_join.hip).  Returns the permuted tensors; *offs = partition offsets
+// [2^bits + 1].  GPU only.
+std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> cols, const std::vector<int> &widths,
+                                       int bits, at::Tensor *offs);
+
 // exclusive scan of int64 counts -> offsets[n+1]
 inline at::Tensor exclusive_scan(const Exec &ex, const at::Tensor &counts) {
   const int64_t n = counts.numel();

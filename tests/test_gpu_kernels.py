@@ -163,3 +163,28 @@ def test_radix_join_matches_global_table_join(gpu_ctx, monkeypatch, case):
     ref = L.join(R, "inner", "hash", **on)
     assert got.column_names == ref.column_names
     pd.testing.assert_frame_equal(_sorted_df(got), _sorted_df(ref))
+
+
+@pytest.mark.parametrize("case", ["int64_many_groups", "int32_nullable", "few_groups", "min_key", "wide_aggs"])
+def test_radix_groupby_matches_global(gpu_ctx, monkeypatch, case):
+    """K8 LDS radix group-by (HLL sizing, partitioned LDS aggregation) vs the global-table path."""
+    rng = np.random.default_rng(5)
+    n = 400_000
+    groups = {"int64_many_groups": 150_000, "int32_nullable": 20_000, "few_groups": 7, "min_key": 5000,
+              "wide_aggs": 3000}[case]
+    k = rng.integers(-groups, groups, n)
+    if case == "min_key":
+        k[::97] = np.iinfo(np.int64).min
+    kt = pa.int32() if case == "int32_nullable" else pa.int64()
+    fmask = rng.random(n) < 0.1 if case == "int32_nullable" else None
+    t = pa.table({"k": pa.array(k, kt), "f": pa.array(rng.standard_normal(n), mask=fmask),
+                  "i": pa.array(rng.integers(-1000, 1000, n), pa.int32())})
+    T = Table(t, gpu_ctx)
+    aggs = {"f": ["sum", "count", "min", "max", "mean"], "i": ["sum", "min"]} if case == "wide_aggs" else \
+        {"f": ["sum", "mean"], "i": ["max", "count"]}
+    res = []
+    for thr in ("1", str(1 << 62)):
+        monkeypatch.setenv("CYLON_RADIX_GROUPBY_MIN_ROWS", thr)
+        df = T.local_groupby("k", aggs).to_pandas()
+        res.append(df.sort_values("k").reset_index(drop=True))
+    pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-9, atol=1e-9)
