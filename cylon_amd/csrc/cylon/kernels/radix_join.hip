@@ -94,7 +94,17 @@ struct PartDigit {
 };
 
 
-__global__ __launch_bounds__(kRPThreads) void k_rp_hist(PartDigit digit, int64_t n, uint32_t nbuckets,
+// Sort digit: bits [shift, shift + log2(mask+1)) of an order-preserving uint64 image (K6).
+struct ImageDigit {
+  const int64_t *keys;
+  int shift;
+  uint32_t mask;
+  __device__ __forceinline__ uint32_t of_key(int64_t k) const { return (uint32_t)((uint64_t)k >> shift) & mask; }
+  __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key(keys[i]); }
+};
+
+template <class Digit>
+__global__ __launch_bounds__(kRPThreads) void k_rp_hist(Digit digit, int64_t n, uint32_t nbuckets,
                                                         int64_t rows_per_block, int64_t nblocks,
                                                         int64_t *__restrict__ bh) {
   __shared__ unsigned int hist[kRPMaxBuckets];
@@ -140,8 +150,8 @@ __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) 
 // global latency is hidden by software pipelining in registers instead: the
 // loads of column c+1 (and, during the last column, the next tile's keys) are
 // in flight while column c streams out of the stage.  Column 0 is the key.
-template <bool W8>
-__global__ __launch_bounds__(kRPThreads) void k_rows_pass(PartDigit digit, int nbits, uint32_t nbuckets, ColSet cols,
+template <class Digit, bool W8>
+__global__ __launch_bounds__(kRPThreads) void k_rows_pass(Digit digit, int nbits, uint32_t nbuckets, ColSet cols,
                                                           int64_t n, int64_t rows_per_block, int64_t nblocks,
                                                           const int64_t *__restrict__ bh_scan) {
   __shared__ int64_t running[kRPMaxBuckets];
@@ -286,21 +296,21 @@ int64_t radix_rows_pass_workspace(int64_t n, int digit_bits) {
   return m + (m + 1) + scan_workspace(m);
 }
 
-void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, int digit_bits, const uint8_t *const *in,
-                     uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream) {
+template <class Digit>
+static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const uint8_t *const *in, uint8_t *const *out,
+                             const int *widths, int ncols, int64_t *ws, void *stream) {
   if (n == 0) return;
   CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
   CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
-  CYLON_CHECK(in[0] == reinterpret_cast<const uint8_t *>(keys) && widths[0] == 8, Code::Invalid,
+  CYLON_CHECK(in[0] == reinterpret_cast<const uint8_t *>(dg.keys) && widths[0] == 8, Code::Invalid,
               "radix pass: column 0 must be the key");
   hipStream_t s = as_stream(stream);
   const uint32_t nb = 1u << digit_bits;
   const RPGeometry g = rp_geometry(n);
   const int64_t m = g.nblocks * (int64_t)nb;
   int64_t *bh = ws, *bh_scan = ws + m, *scan_ws = bh_scan + m + 1;
-  PartDigit dg{keys, total_bits, shift, nb - 1};
-  hipLaunchKernelGGL(k_rp_hist, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, n, nb, g.rows_per_block,
-                     g.nblocks, bh);
+  hipLaunchKernelGGL(k_rp_hist<Digit>, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, n, nb,
+                     g.rows_per_block, g.nblocks, bh);
   HIP_LAUNCH_CHECK();
   exclusive_scan(bh, m, bh_scan, scan_ws, stream);
   ColSet cs;
@@ -313,12 +323,24 @@ void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, 
   bool w8 = true;
   for (int c = 0; c < ncols; ++c) w8 &= widths[c] == 8;
   if (w8)
-    hipLaunchKernelGGL(k_rows_pass<true>, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, digit_bits, nb, cs,
-                       n, g.rows_per_block, g.nblocks, (const int64_t *)bh_scan);
+    hipLaunchKernelGGL((k_rows_pass<Digit, true>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, digit_bits,
+                       nb, cs, n, g.rows_per_block, g.nblocks, (const int64_t *)bh_scan);
   else
-    hipLaunchKernelGGL(k_rows_pass<false>, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, digit_bits, nb, cs,
-                       n, g.rows_per_block, g.nblocks, (const int64_t *)bh_scan);
+    hipLaunchKernelGGL((k_rows_pass<Digit, false>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg,
+                       digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, (const int64_t *)bh_scan);
   HIP_LAUNCH_CHECK();
+}
+
+void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, int digit_bits, const uint8_t *const *in,
+                     uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream) {
+  const uint32_t nb = 1u << digit_bits;
+  rows_pass_launch(PartDigit{keys, total_bits, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws, stream);
+}
+
+void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_bits, const uint8_t *const *in,
+                          uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream) {
+  const uint32_t nb = 1u << digit_bits;
+  rows_pass_launch(ImageDigit{keys, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws, stream);
 }
 
 // offsets[p] = first row of partition p in partition-sorted keys (binary search), offsets[P] = n

@@ -112,6 +112,20 @@ struct RadixSink {
 
 int64_t radix_sort_workspace(int64_t n) { return stable_rank_workspace(n, 256) + 2; }
 
+uint64_t varying_bits(const uint64_t *keys, int64_t n, int64_t *ws2, void *stream) {
+  if (n <= 1) return 0;
+  hipStream_t s = as_stream(stream);
+  unsigned long long *acc = reinterpret_cast<unsigned long long *>(ws2);
+  unsigned long long init[2] = {0ull, ~0ull};
+  HIP_CHECK(hipMemcpyAsync(acc, init, sizeof(init), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_or_and, dim3(grid_for(n, kBlock, 1024)), dim3(kBlock), 0, s, keys, n, acc);
+  HIP_LAUNCH_CHECK();
+  unsigned long long oa[2];
+  HIP_CHECK(hipMemcpyAsync(oa, acc, sizeof(oa), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return oa[0] ^ oa[1];
+}
+
 int radix_sort_pairs(uint64_t *keys, int64_t *vals, int64_t n, uint64_t *keys_alt, int64_t *vals_alt, int begin_bit,
                      int end_bit, int64_t *ws, void *stream) {
   if (n <= 1) return 0;

@@ -8,6 +8,8 @@
 // Strings sort by stable passes over their length and then their 8-byte
 // big-endian chunks from the last chunk to the first, which yields byte-wise
 // lexicographic order.
+#include <cstdlib>
+
 #include "util.hpp"
 #include "../trace.hpp"
 
@@ -79,8 +81,103 @@ at::Tensor SortIndices(const TablePtr &t, const std::vector<int> &cols, const st
   return perm;
 }
 
+// Large single-key sorts on the GPU: LSD passes over the key's order image
+// that move every column (radix_join.hip k_rows_pass with an image digit)
+// instead of sorting (image, row) pairs and gathering each column at random
+// afterwards (~50 G random accesses/s, profiles/membench.txt).  Constant
+// leading/trailing bits of the image are skipped (OR ^ AND reduction).
+static int64_t radix_sort_min_rows() {
+  const char *e = std::getenv("CYLON_RADIX_SORT_MIN_ROWS");  // tuning / test knob
+  return e ? std::atoll(e) : (int64_t(1) << 22);
+}
+
+static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
+  const int64_t n = t->Rows();
+  if (!t->device().is_cuda() || n < radix_sort_min_rows()) return nullptr;
+  const Column &kc = t->column(col);
+  if (kc.nullable() || kc.is_var() || kc.type.kind() == ValueKind::FIXED_BYTES) return nullptr;
+  int slots = 1;
+  for (const auto &c : t->columns()) {
+    const int w = c.type.width();
+    if (c.is_var() || c.type.kind() == ValueKind::FIXED_BYTES || !(w == 1 || w == 2 || w == 4 || w == 8) ||
+        c.data.element_size() != w)
+      return nullptr;
+    slots += 1 + (c.nullable() ? 1 : 0);
+  }
+  if (slots > kMaxFusedCols) return nullptr;
+  Exec ex(t->device());
+  CYLON_PHASE("sort.radix_rows", ex.device);
+  at::Tensor img = ex.empty_i64(n);
+  hip::sort_keys_from_column(kc.view(), nullptr, n, !asc, reinterpret_cast<uint64_t *>(ptr<int64_t>(img)), ex.stream);
+  at::Tensor ws2 = ex.empty_i64(2);
+  const uint64_t diff = hip::varying_bits(reinterpret_cast<const uint64_t *>(ptr<int64_t>(img)), n,
+                                          ptr<int64_t>(ws2), ex.stream);
+  // an integer key is rebuilt from its image at the end instead of travelling too
+  const bool key_from_image = kc.type.kind() == ValueKind::SIGNED_INT || kc.type.kind() == ValueKind::UNSIGNED_INT;
+  std::vector<at::Tensor> cur{img};
+  std::vector<int> widths{8};
+  for (int ci = 0; ci < t->Columns(); ++ci) {
+    const Column &c = t->column(ci);
+    if (!(key_from_image && ci == col)) {
+      cur.push_back(c.data);
+      widths.push_back(c.type.width());
+    }
+    if (c.nullable()) {
+      cur.push_back(c.validity);
+      widths.push_back(1);
+    }
+  }
+  if (diff != 0) {
+    const int lo = __builtin_ctzll(diff), hi = 64 - __builtin_clzll(diff);
+    const int npass = (hi - lo + 9) / 10;
+    at::Tensor ws;
+    int shift = lo;
+    for (int ps = 0; ps < npass; ++ps) {
+      const int db = (hi - shift + (npass - ps) - 1) / (npass - ps);
+      const int64_t wsn = hip::radix_rows_pass_workspace(n, db);
+      if (!ws.defined() || ws.numel() < wsn) ws = ex.empty_i64(wsn);
+      std::vector<at::Tensor> nxt;
+      std::vector<const uint8_t *> in;
+      std::vector<uint8_t *> out;
+      for (auto &x : cur) {
+        nxt.push_back(at::empty_like(x));
+        in.push_back(reinterpret_cast<const uint8_t *>(x.data_ptr()));
+        out.push_back(reinterpret_cast<uint8_t *>(nxt.back().data_ptr()));
+      }
+      hip::radix_sort_rows_pass(ptr<int64_t>(cur[0]), n, shift, db, in.data(), out.data(), widths.data(),
+                                (int)cur.size(), ptr<int64_t>(ws), ex.stream);
+      cur = std::move(nxt);
+      shift += db;
+    }
+  }
+  std::vector<Column> cols;
+  size_t q = 1;
+  for (int ci = 0; ci < t->Columns(); ++ci) {
+    const Column &c = t->column(ci);
+    at::Tensor d;
+    if (key_from_image && ci == col) {
+      at::Tensor im = cur[0];
+      if (!asc) {
+        const int nb = 8 * c.type.width();
+        const int64_t mask = nb == 64 ? -1 : (int64_t)((1ull << nb) - 1);
+        im = at::bitwise_and(at::bitwise_not(im), mask);
+      }
+      d = at::empty_like(c.data);
+      hip::agg_unimage(reinterpret_cast<const uint64_t *>(ptr<int64_t>(im)), n, c.type.width(),
+                       static_cast<int>(c.type.kind()), reinterpret_cast<uint8_t *>(d.data_ptr()), ex.stream);
+    } else {
+      d = cur[q++];
+    }
+    at::Tensor v = c.nullable() ? cur[q++] : at::Tensor();
+    cols.emplace_back(c.name, c.type, n, d, at::Tensor(), v);
+  }
+  return Table::Make(t->GetContext(), std::move(cols));
+}
+
 TablePtr Sort(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending) {
   if (t->Rows() <= 1) return t;
+  if (cols.size() == 1)
+    if (TablePtr r = radix_sort_table(t, cols[0], ascending.empty() ? true : ascending[0])) return r;
   return GatherNullable(t, SortIndices(t, cols, ascending), false);
 }
 
