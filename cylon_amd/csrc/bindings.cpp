@@ -109,7 +109,31 @@ PYBIND11_MODULE(_C, m) {
       .value("LOCAL", net::CommType::LOCAL).value("MPI", net::CommType::MPI).value("TCP", net::CommType::TCP)
       .value("UCX", net::CommType::UCX).value("RCCL", net::CommType::RCCL).value("GLOO", net::CommType::GLOO);
 
+  py::class_<MemoryPool, std::shared_ptr<MemoryPool>>(m, "MemoryPool")
+      .def("bytes_allocated", &MemoryPool::bytes_allocated)
+      .def("max_memory", &MemoryPool::max_memory)
+      .def("backend_name", &MemoryPool::backend_name)
+      .def("device", [](const MemoryPool &p) { return p.device().str(); })
+      .def(
+          "empty",
+          [](const std::shared_ptr<MemoryPool> &p, std::vector<int64_t> shape, const std::string &dtype) {
+            static const std::map<std::string, at::ScalarType> m{
+                {"int8", at::kChar},  {"uint8", at::kByte},   {"int16", at::kShort},   {"int32", at::kInt},
+                {"int64", at::kLong}, {"float16", at::kHalf}, {"float32", at::kFloat}, {"float64", at::kDouble},
+                {"bool", at::kBool}};
+            auto it = m.find(dtype);
+            CYLON_CHECK(it != m.end(), Code::Invalid, "unsupported dtype " << dtype);
+            return EmptyFromPool(p, shape, it->second);
+          },
+          py::arg("shape"), py::arg("dtype"), "tensor whose storage is allocated from this pool");
+  m.def("host_memory_pool", []() { return std::shared_ptr<MemoryPool>(std::make_shared<HostMemoryPool>()); });
+  m.def("device_memory_pool", [](const std::string &dev) {
+    return std::shared_ptr<MemoryPool>(std::make_shared<DeviceMemoryPool>(parse_device(dev)));
+  });
+
   py::class_<CylonContext, std::shared_ptr<CylonContext>>(m, "Context")
+      .def("memory_pool", &CylonContext::GetMemoryPool)
+      .def("set_memory_pool", &CylonContext::SetMemoryPool)
       .def_static("init_local", [](const std::string &dev) { return CylonContext::Init(parse_device(dev)); },
                   py::arg("device") = "cpu")
       .def_static("init_distributed",

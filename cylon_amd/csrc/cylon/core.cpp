@@ -251,6 +251,12 @@ int64_t CylonContext::BytesAllocated() const {
   return stats.allocated_bytes[static_cast<size_t>(c10::CachingAllocator::StatType::AGGREGATE)].current;
 }
 
+std::shared_ptr<MemoryPool> CylonContext::GetMemoryPool() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!pool_ || pool_->device() != device_) pool_ = DefaultMemoryPool(device_);
+  return pool_;
+}
+
 int64_t CylonContext::MaxMemory() const {
   if (!device_.is_cuda()) return 0;
   auto stats = c10::hip::HIPCachingAllocator::getDeviceStats(device_.index());

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../net/communicator.hpp"
+#include "memory_pool.hpp"
 
 namespace cylon {
 
@@ -51,12 +52,18 @@ class CylonContext {
   int64_t BytesAllocated() const;
   int64_t MaxMemory() const;
 
+  // C2: the context's memory pool (default: DeviceMemoryPool / HostMemoryPool
+  // for the context device; reference ctx/cylon_context.hpp GetMemoryPool).
+  std::shared_ptr<MemoryPool> GetMemoryPool();
+  void SetMemoryPool(std::shared_ptr<MemoryPool> pool) { pool_ = std::move(pool); }
+
  private:
   bool distributed_;
   int sequence_no_ = 0;
   std::shared_ptr<net::Communicator> communicator_;
   std::map<std::string, std::string> config_;
   at::Device device_{at::kCPU};
+  std::shared_ptr<MemoryPool> pool_;
   mutable std::mutex mu_;
 };
 

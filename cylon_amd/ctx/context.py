@@ -116,7 +116,18 @@ class CylonContext:
         return self.device.startswith("cuda")
 
     def memory_stats(self) -> dict:
-        return {"bytes_allocated": self._ctx.bytes_allocated(), "max_memory": self._ctx.max_memory()}
+        pool = self.memory_pool()
+        return {"bytes_allocated": self._ctx.bytes_allocated(), "max_memory": self._ctx.max_memory(),
+                "pool_backend": pool.backend_name(), "pool_bytes_allocated": pool.bytes_allocated(),
+                "pool_max_memory": pool.max_memory()}
+
+    def memory_pool(self):
+        """The context's MemoryPool (C2; reference ctx/memory_pool.hpp): HBM via the HIP caching
+        allocator on a GPU context, aligned host memory otherwise."""
+        return self._ctx.memory_pool()
+
+    def set_memory_pool(self, pool) -> None:
+        self._ctx.set_memory_pool(pool)
 
     def allreduce(self, tensor: torch.Tensor, op: str = "sum") -> torch.Tensor:
         ops = {"sum": 0, "min": 1, "max": 2, "prod": 3}

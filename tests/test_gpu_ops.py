@@ -107,3 +107,15 @@ def test_rccl_communicator_world1():
         ctx.finalize()
         if dist.is_initialized():
             dist.destroy_process_group()
+
+
+def test_device_memory_pool(gpu_ctx):
+    pool = gpu_ctx.memory_pool()
+    assert pool.backend_name() == "hip_caching_allocator" and pool.device().startswith("cuda")
+    before = pool.bytes_allocated()
+    x = pool.empty([1 << 20], "int64")
+    assert x.is_cuda and pool.bytes_allocated() == before + 8 * (1 << 20)
+    x.fill_(3)
+    assert int(x.sum()) == 3 * (1 << 20)
+    del x
+    assert pool.bytes_allocated() == before

@@ -85,3 +85,18 @@ def test_join_is_deterministic(ctx):
     r1 = a.join(a, "inner", "hash", on=[0]).to_arrow()
     r2 = a.join(a, "inner", "hash", on=[0]).to_arrow()
     assert r1.equals(r2)
+
+
+def test_memory_pool_accounting(ctx):
+    from cylon_amd.ctx import host_memory_pool
+    pool = ctx.memory_pool()
+    assert pool.backend_name() == "host" and pool.device() == "cpu"
+    p = host_memory_pool()
+    x = p.empty([1000, 4], "float64")
+    assert tuple(x.shape) == (1000, 4) and p.bytes_allocated() == 32000
+    x.fill_(1.5)
+    assert float(x.sum()) == 6000.0
+    del x
+    assert p.bytes_allocated() == 0 and p.max_memory() == 32000
+    ctx.set_memory_pool(p)
+    assert ctx.memory_stats()["pool_max_memory"] == 32000
