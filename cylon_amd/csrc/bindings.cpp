@@ -7,6 +7,7 @@
 #include <torch/csrc/utils/pybind.h>
 
 #include "cylon/ctx/cylon_context.hpp"
+#include "cylon/net/channel.hpp"
 #include "cylon/net/communicator.hpp"
 #include "cylon/ops/api_ext.hpp"
 #include "cylon/table.hpp"
@@ -16,6 +17,28 @@ namespace py = pybind11;
 using namespace cylon;
 
 namespace {
+
+// Python subclasses of the channel callbacks (reference net/channel.hpp callbacks)
+class PyRecvCb : public net::ChannelReceiveCallback {
+ public:
+  void receivedHeader(int source, int finished, const std::vector<int32_t> &header) override {
+    PYBIND11_OVERRIDE_PURE_NAME(void, net::ChannelReceiveCallback, "received_header", receivedHeader, source,
+                                finished, header);
+  }
+  void receivedData(int source, const at::Tensor &buffer) override {
+    PYBIND11_OVERRIDE_PURE_NAME(void, net::ChannelReceiveCallback, "received_data", receivedData, source, buffer);
+  }
+};
+
+class PySendCb : public net::ChannelSendCallback {
+ public:
+  void sendComplete(const std::shared_ptr<net::TxRequest> &req) override {
+    PYBIND11_OVERRIDE_PURE_NAME(void, net::ChannelSendCallback, "send_complete", sendComplete, req);
+  }
+  void sendFinishComplete(const std::shared_ptr<net::TxRequest> &req) override {
+    PYBIND11_OVERRIDE_PURE_NAME(void, net::ChannelSendCallback, "send_finish_complete", sendFinishComplete, req);
+  }
+};
 
 at::Device parse_device(const std::string &s) { return at::Device(s); }
 
@@ -108,6 +131,35 @@ PYBIND11_MODULE(_C, m) {
   py::enum_<net::CommType>(m, "CommType")
       .value("LOCAL", net::CommType::LOCAL).value("MPI", net::CommType::MPI).value("TCP", net::CommType::TCP)
       .value("UCX", net::CommType::UCX).value("RCCL", net::CommType::RCCL).value("GLOO", net::CommType::GLOO);
+
+  py::class_<net::TxRequest, std::shared_ptr<net::TxRequest>>(m, "TxRequest")
+      .def(py::init<>())
+      .def(py::init([](int target, py::object buffer, std::vector<int32_t> header) {
+             at::Tensor b = buffer.is_none() ? at::Tensor() : buffer.cast<at::Tensor>();
+             return std::make_shared<net::TxRequest>(target, b, header);
+           }),
+           py::arg("target"), py::arg("buffer") = py::none(), py::arg("header") = std::vector<int32_t>{})
+      .def_readwrite("target", &net::TxRequest::target)
+      .def_readwrite("header", &net::TxRequest::header)
+      .def_property(
+          "buffer", [](const net::TxRequest &r) -> py::object {
+            return r.buffer.defined() ? py::cast(r.buffer) : py::none();
+          },
+          [](net::TxRequest &r, at::Tensor b) { r.buffer = b; });
+  py::class_<net::ChannelReceiveCallback, PyRecvCb>(m, "ChannelReceiveCallback").def(py::init<>());
+  py::class_<net::ChannelSendCallback, PySendCb>(m, "ChannelSendCallback").def(py::init<>());
+  py::class_<net::Channel, std::shared_ptr<net::Channel>>(m, "Channel")
+      .def(py::init([](const std::shared_ptr<CylonContext> &ctx) {
+        return std::make_shared<net::Channel>(ctx->GetCommunicator(), ctx->GetDevice());
+      }))
+      .def("init", &net::Channel::init, py::arg("edge"), py::arg("receives"), py::arg("send_ids"),
+           py::arg("receive_callback"), py::arg("send_callback"), py::keep_alive<1, 5>(), py::keep_alive<1, 6>())
+      .def("send", &net::Channel::send)
+      .def("send_fin", &net::Channel::sendFin)
+      .def("progress_sends", &net::Channel::progressSends)
+      .def("progress_receives", &net::Channel::progressReceives)
+      .def("is_complete", &net::Channel::isComplete)
+      .def("close", &net::Channel::close);
 
   py::class_<MemoryPool, std::shared_ptr<MemoryPool>>(m, "MemoryPool")
       .def("bytes_allocated", &MemoryPool::bytes_allocated)

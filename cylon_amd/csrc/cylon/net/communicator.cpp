@@ -1,6 +1,9 @@
 // ProcessGroup-backed communicator (RCCL over xGMI on MI355X, gloo on CPU).
 // Reference call sites replaced here: SURVEY.md §2.5 M1-M8
 // (MPI_Init/Barrier/Finalize, MPI_Isend/Irecv header+payload, MPI_Allreduce).
+#include <atomic>
+#include <chrono>
+#include <thread>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/distributed/c10d/Types.hpp>
 
@@ -132,6 +135,92 @@ void ProcessGroupCommunicator::Broadcast(at::Tensor &t, int root) {
   o.rootRank = root;
   pg_->broadcast(v, o)->wait();
   if (!c.is_same(t)) t.copy_(c.view(t.scalar_type()));
+}
+
+}  // namespace net
+}  // namespace cylon
+
+namespace cylon {
+namespace net {
+
+std::shared_ptr<P2PRequest> Communicator::ISend(const at::Tensor &, int, int) {
+  CYLON_THROW(Code::NotImplemented, "point-to-point send needs a distributed communicator");
+}
+
+std::shared_ptr<P2PRequest> Communicator::IRecv(at::Tensor &, int, int) {
+  CYLON_THROW(Code::NotImplemented, "point-to-point receive needs a distributed communicator");
+}
+
+namespace {
+// A c10d work plus the staging buffers a transfer needs when the caller's tensor
+// is not on the communication device (copied back once the receive completes).
+// RCCL works report completion through isCompleted() (event query); gloo's
+// point-to-point works only complete inside wait(), so for gloo a helper
+// thread waits and Test() reads its flag.
+class PGRequest : public P2PRequest {
+ public:
+  PGRequest(c10::intrusive_ptr<c10d::Work> w, at::Tensor staged, at::Tensor user, bool threaded)
+      : work_(std::move(w)), staged_(std::move(staged)), user_(std::move(user)) {
+    if (threaded) {
+      st_ = std::make_shared<State>();
+      auto st = st_;
+      auto w2 = work_;
+      std::thread([st, w2]() {
+        try {
+          w2->wait();
+        } catch (...) {
+          st->err = std::current_exception();
+        }
+        st->done.store(true);
+      }).detach();
+    }
+  }
+  bool Test() override {
+    if (done_) return true;
+    if (st_ ? !st_->done.load() : !work_->isCompleted()) return false;
+    finish();
+    return true;
+  }
+  void Wait() override {
+    if (done_) return;
+    if (st_) {
+      while (!st_->done.load()) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    } else {
+      work_->wait();
+    }
+    finish();
+  }
+
+ private:
+  struct State {
+    std::atomic<bool> done{false};
+    std::exception_ptr err;
+  };
+  void finish() {
+    done_ = true;
+    if (st_ && st_->err) std::rethrow_exception(st_->err);
+    if (user_.defined() && !staged_.is_same(user_)) user_.copy_(staged_.view(user_.scalar_type()));
+  }
+  c10::intrusive_ptr<c10d::Work> work_;
+  at::Tensor staged_, user_;
+  std::shared_ptr<State> st_;
+  bool done_ = false;
+};
+}  // namespace
+
+std::shared_ptr<P2PRequest> ProcessGroupCommunicator::ISend(const at::Tensor &t, int dst, int tag) {
+  CYLON_CHECK(dst >= 0 && dst < world_ && dst != rank_, Code::Invalid, "bad send target " << dst);
+  at::Tensor c = to_comm(t);
+  std::vector<at::Tensor> v{c};
+  return std::make_shared<PGRequest>(pg_->send(v, dst, tag), c, at::Tensor(), type_ != CommType::RCCL);
+}
+
+std::shared_ptr<P2PRequest> ProcessGroupCommunicator::IRecv(at::Tensor &t, int src, int tag) {
+  CYLON_CHECK(src >= 0 && src < world_ && src != rank_, Code::Invalid, "bad receive source " << src);
+  at::Tensor c = to_comm(t);
+  const bool staged = !(c.is_same(t));
+  std::vector<at::Tensor> v{c};
+  return std::make_shared<PGRequest>(pg_->recv(v, src, tag), c, staged ? t : at::Tensor(), type_ != CommType::RCCL);
 }
 
 }  // namespace net

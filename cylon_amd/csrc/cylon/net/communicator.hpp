@@ -37,6 +37,14 @@ enum class ReduceOp : int { SUM = 0, MIN = 1, MAX = 2, PROD = 3 };
 
 const char *CommTypeName(CommType t);
 
+// An outstanding point-to-point transfer (ISend / IRecv).
+class P2PRequest {
+ public:
+  virtual ~P2PRequest() = default;
+  virtual bool Test() = 0;  // non-blocking completion check
+  virtual void Wait() = 0;
+};
+
 class Communicator {
  public:
   virtual ~Communicator() = default;
@@ -57,6 +65,10 @@ class Communicator {
   // Gather tensors of different lengths from every rank (dim 0).
   virtual std::vector<at::Tensor> AllGatherV(const at::Tensor &in);
   virtual void Broadcast(at::Tensor &t, int root) = 0;
+  // Point-to-point (C4 Channel transport; reference mpi_channel.cpp Isend/Irecv).
+  // Messages between a pair with the same tag are matched in posting order.
+  virtual std::shared_ptr<P2PRequest> ISend(const at::Tensor &t, int dst, int tag);
+  virtual std::shared_ptr<P2PRequest> IRecv(at::Tensor &t, int src, int tag);
 };
 
 class LocalCommunicator : public Communicator {
@@ -109,6 +121,14 @@ class FaultInjectionCommunicator : public Communicator {
     tick("Broadcast");
     inner_->Broadcast(t, root);
   }
+  std::shared_ptr<P2PRequest> ISend(const at::Tensor &t, int dst, int tag) override {
+    tick("ISend");
+    return inner_->ISend(t, dst, tag);
+  }
+  std::shared_ptr<P2PRequest> IRecv(at::Tensor &t, int src, int tag) override {
+    tick("IRecv");
+    return inner_->IRecv(t, src, tag);
+  }
   int64_t calls() const { return calls_; }
 
  private:
@@ -136,6 +156,8 @@ class ProcessGroupCommunicator : public Communicator {
   void AllReduce(at::Tensor &t, ReduceOp op) override;
   at::Tensor AllGather(const at::Tensor &in) override;
   void Broadcast(at::Tensor &t, int root) override;
+  std::shared_ptr<P2PRequest> ISend(const at::Tensor &t, int dst, int tag) override;
+  std::shared_ptr<P2PRequest> IRecv(at::Tensor &t, int src, int tag) override;
   at::Device comm_device() const { return device_; }
 
  private:

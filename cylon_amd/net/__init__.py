@@ -51,3 +51,43 @@ class MPIConfig(CommConfig):
 
 
 __all__ = ["CommConfig", "RCCLConfig", "GlooConfig", "MPIConfig", "CommType"]
+
+
+# ---- point-to-point channel (C4 / P6; reference net/channel.hpp, pycylon/net/txrequest.pyx)
+TxRequest = C.TxRequest
+ChannelReceiveCallback = C.ChannelReceiveCallback
+ChannelSendCallback = C.ChannelSendCallback
+
+
+class Channel:
+    """Polled header+payload message channel between ranks over the context's
+    communicator (c10d send/recv: RCCL p2p over xGMI, gloo on CPU).
+
+    channel = Channel(ctx); channel.init(edge, receives, send_ids, rcv_cb, snd_cb)
+    channel.send(TxRequest(target, tensor, [h0..h5])); channel.send_fin(TxRequest(target))
+    while not channel.is_complete(): channel.progress_sends(); channel.progress_receives()
+    """
+
+    def __init__(self, ctx):
+        self._ch = C.Channel(ctx._ctx if hasattr(ctx, "_ctx") else ctx)
+
+    def init(self, edge: int, receives, send_ids, receive_callback, send_callback):
+        self._ch.init(int(edge), list(receives), list(send_ids), receive_callback, send_callback)
+
+    def send(self, req) -> int:
+        return self._ch.send(req)
+
+    def send_fin(self, req) -> int:
+        return self._ch.send_fin(req)
+
+    def progress_sends(self):
+        self._ch.progress_sends()
+
+    def progress_receives(self):
+        self._ch.progress_receives()
+
+    def is_complete(self) -> bool:
+        return self._ch.is_complete()
+
+    def close(self):
+        self._ch.close()

@@ -87,3 +87,52 @@ def test_registry(ctx):
     assert set(reg.ids()) >= {"a", "b", "j", "u"}
     reg.remove("j")
     assert "j" not in reg.ids()
+
+
+def _channel(ctx):
+    import torch
+    from cylon_amd.net import Channel, ChannelReceiveCallback, ChannelSendCallback, TxRequest
+    rank, world = ctx.get_rank(), ctx.get_world_size()
+    got, sent = [], []
+
+    class R(ChannelReceiveCallback):
+        def received_header(self, source, finished, header):
+            got.append(("h", source, finished, list(header[:2])))
+
+        def received_data(self, source, buffer):
+            got.append(("d", source, buffer.view(torch.int64).tolist()))
+
+    class S(ChannelSendCallback):
+        def send_complete(self, req):
+            sent.append(req.header[0])
+
+        def send_finish_complete(self, req):
+            sent.append("fin")
+
+    rcb, scb = R(), S()
+    peers = [r for r in range(world) if r != rank]
+    ch = Channel(ctx)
+    ch.init(7, peers, peers, rcb, scb)
+    for p in peers:
+        for m in range(3):
+            ch.send(TxRequest(p, torch.arange(m + 1, dtype=torch.int64) + 100 * rank, [m, rank]))
+        ch.send(TxRequest(p, None, [9, 9]))  # header-only message
+        ch.send_fin(TxRequest(p))
+    import time
+    t0 = time.time()
+    while not ch.is_complete() and time.time() - t0 < 60:
+        ch.progress_sends()
+        ch.progress_receives()
+    ch.close()
+    return got, sent
+
+
+def test_channel_point_to_point():
+    res = run_distributed(_channel, 2)
+    for rank, (got, sent) in enumerate(res):
+        other = 1 - rank
+        assert sent == [0, 1, 2, 9, "fin"]
+        datas = [g[2] for g in got if g[0] == "d"]
+        assert datas[:3] == [[100 * other + i for i in range(m + 1)] for m in range(3)]
+        heads = [g for g in got if g[0] == "h"]
+        assert heads[0][3] == [0, other] and heads[-1][2] == 1 and len(heads) == 5
