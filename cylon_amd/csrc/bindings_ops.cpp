@@ -6,6 +6,7 @@
 #include <tuple>
 
 #include "cylon/api.hpp"
+#include "cylon/io/csv.hpp"
 #include "cylon/ops/api_ext.hpp"
 #include "cylon/ops/graph.hpp"
 #include "cylon/ops/relational.hpp"
@@ -29,6 +30,52 @@ static std::vector<ops::AggSpec> make_specs(const std::vector<int> &cols, const 
 
 void register_extended_ops(py::module &m) {
   auto rel = py::call_guard<py::gil_scoped_release>();
+
+  // ---- C25 native CSV I/O
+  m.def(
+      "read_csv",
+      [](const std::shared_ptr<CylonContext> &ctx, const std::vector<std::string> &paths, const std::string &delimiter,
+         bool header, bool autogen, const std::vector<std::string> &column_names, int64_t skip_rows,
+         bool ignore_empty_lines, const std::vector<std::string> &include_columns,
+         const std::vector<std::string> &null_values, const std::vector<std::string> &true_values,
+         const std::vector<std::string> &false_values, bool strings_can_be_null, bool quoting,
+         const std::string &quote_char, bool double_quote, int threads) {
+        io::CSVReadOptions o;
+        o.delimiter = delimiter.empty() ? ',' : delimiter[0];
+        o.header = header;
+        o.autogenerate_column_names = autogen;
+        o.column_names = column_names;
+        o.skip_rows = skip_rows;
+        o.ignore_empty_lines = ignore_empty_lines;
+        o.include_columns = include_columns;
+        o.null_values = null_values;
+        if (!true_values.empty()) o.true_values = true_values;
+        if (!false_values.empty()) o.false_values = false_values;
+        o.strings_can_be_null = strings_can_be_null;
+        o.quoting = quoting;
+        o.quote_char = quote_char.empty() ? '"' : quote_char[0];
+        o.double_quote = double_quote;
+        o.threads = threads;
+        return io::ReadCSVs(ctx, paths, o);
+      },
+      py::arg("ctx"), py::arg("paths"), py::arg("delimiter") = ",", py::arg("header") = true,
+      py::arg("autogenerate_column_names") = false, py::arg("column_names") = std::vector<std::string>{},
+      py::arg("skip_rows") = 0, py::arg("ignore_empty_lines") = true,
+      py::arg("include_columns") = std::vector<std::string>{}, py::arg("null_values") = std::vector<std::string>{},
+      py::arg("true_values") = std::vector<std::string>{}, py::arg("false_values") = std::vector<std::string>{},
+      py::arg("strings_can_be_null") = false, py::arg("quoting") = true, py::arg("quote_char") = "\"",
+      py::arg("double_quote") = true, py::arg("threads") = 0, rel);
+  m.def(
+      "write_csv",
+      [](const TablePtr &t, const std::string &path, const std::string &delimiter,
+         const std::vector<std::string> &names) {
+        io::CSVWriteOptions o;
+        o.delimiter = delimiter.empty() ? ',' : delimiter[0];
+        o.column_names = names;
+        io::WriteCSV(t, path, o);
+      },
+      py::arg("table"), py::arg("path"), py::arg("delimiter") = ",",
+      py::arg("column_names") = std::vector<std::string>{}, rel);
 
   py::enum_<AggOp>(m, "AggregationOp")
       .value("SUM", AGG_SUM).value("MIN", AGG_MIN).value("MAX", AGG_MAX).value("COUNT", AGG_COUNT)

@@ -1,0 +1,469 @@
+// Native CSV reader / writer (C25): see csv.hpp.
+#include "csv.hpp"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <charconv>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <string_view>
+#include <thread>
+#include <unordered_set>
+
+namespace cylon {
+namespace io {
+
+namespace {
+
+class MappedFile {
+ public:
+  explicit MappedFile(const std::string &path) {
+    fd_ = ::open(path.c_str(), O_RDONLY);
+    CYLON_CHECK(fd_ >= 0, Code::IOError, "cannot open " << path);
+    struct stat st;
+    CYLON_CHECK(::fstat(fd_, &st) == 0, Code::IOError, "cannot stat " << path);
+    size_ = (size_t)st.st_size;
+    if (size_ > 0) {
+      void *p = ::mmap(nullptr, size_, PROT_READ, MAP_PRIVATE, fd_, 0);
+      CYLON_CHECK(p != MAP_FAILED, Code::IOError, "cannot mmap " << path);
+      data_ = static_cast<const char *>(p);
+      ::madvise(p, size_, MADV_SEQUENTIAL);
+    }
+  }
+  ~MappedFile() {
+    if (data_) ::munmap(const_cast<char *>(data_), size_);
+    if (fd_ >= 0) ::close(fd_);
+  }
+  const char *data() const { return data_; }
+  size_t size() const { return size_; }
+
+ private:
+  int fd_ = -1;
+  const char *data_ = nullptr;
+  size_t size_ = 0;
+};
+
+struct Field {
+  const char *p;
+  uint32_t len;
+  bool quoted;    // enclosed in quotes
+  bool escaped;   // contains doubled quotes (needs unescaping)
+};
+
+// Split [b, e) (one line, no newline) into fields.
+void split_line(const char *b, const char *e, const CSVReadOptions &o, std::vector<Field> &out) {
+  out.clear();
+  const char *p = b;
+  while (true) {
+    Field f{p, 0, false, false};
+    if (o.quoting && p < e && *p == o.quote_char) {
+      const char *s = ++p;
+      while (p < e) {
+        if (*p == o.quote_char) {
+          if (o.double_quote && p + 1 < e && p[1] == o.quote_char) {
+            f.escaped = true;
+            p += 2;
+            continue;
+          }
+          break;
+        }
+        ++p;
+      }
+      f.p = s;
+      f.len = (uint32_t)(p - s);
+      f.quoted = true;
+      if (p < e) ++p;  // closing quote
+      while (p < e && *p != o.delimiter) ++p;
+    } else {
+      while (p < e && *p != o.delimiter) ++p;
+      f.len = (uint32_t)(p - f.p);
+    }
+    out.push_back(f);
+    if (p >= e) break;
+    ++p;  // delimiter
+    if (p == e) {  // trailing delimiter: one more empty field
+      out.push_back(Field{p, 0, false, false});
+      break;
+    }
+  }
+}
+
+std::string field_string(const Field &f, char quote) {
+  if (!f.escaped) return std::string(f.p, f.len);
+  std::string s;
+  s.reserve(f.len);
+  for (uint32_t i = 0; i < f.len; ++i) {
+    s.push_back(f.p[i]);
+    if (f.p[i] == quote && i + 1 < f.len && f.p[i + 1] == quote) ++i;
+  }
+  return s;
+}
+
+enum Seen : uint8_t { S_NULL = 1, S_INT = 2, S_BOOL = 4, S_DBL = 8, S_STR = 16 };
+
+struct Sets {
+  std::unordered_set<std::string_view> nulls, trues, falses;
+};
+
+bool parse_i64(std::string_view s, int64_t *v) {
+  if (s.empty()) return false;
+  const char *b = s.data(), *e = b + s.size();
+  if (*b == '+') ++b;
+  auto r = std::from_chars(b, e, *v);
+  return r.ec == std::errc() && r.ptr == e;
+}
+
+bool parse_f64(std::string_view s, double *v) {
+  if (s.empty() || s.size() > 120) return false;
+  char buf[128];
+  std::memcpy(buf, s.data(), s.size());
+  buf[s.size()] = 0;
+  char *end = nullptr;
+  *v = std::strtod(buf, &end);
+  return end == buf + s.size();
+}
+
+uint8_t classify(const Field &f, const Sets &sets) {
+  std::string_view s(f.p, f.len);
+  if (!f.quoted && sets.nulls.count(s)) return S_NULL;
+  if (f.escaped) return S_STR;
+  int64_t i;
+  if (parse_i64(s, &i)) return S_INT;
+  if (sets.trues.count(s) || sets.falses.count(s)) return S_BOOL;
+  double d;
+  if (parse_f64(s, &d)) return S_DBL;
+  return S_STR;
+}
+
+enum class Kind { I64, F64, BOOL, STR };
+
+Kind resolve(uint8_t seen) {
+  if (seen & S_STR) return Kind::STR;
+  if ((seen & S_BOOL) && (seen & (S_INT | S_DBL))) return Kind::STR;
+  if (seen & S_BOOL) return Kind::BOOL;
+  if (seen & S_DBL) return Kind::F64;
+  if (seen & S_INT) return Kind::I64;
+  return Kind::STR;  // only nulls
+}
+
+// line starts of [b, e): positions just after '\n' (quotes spanning lines are not supported)
+void find_lines(const char *base, size_t b, size_t e, bool skip_empty, std::vector<std::pair<size_t, size_t>> &out) {
+  size_t s = b;
+  while (s < e) {
+    const void *nl = std::memchr(base + s, '\n', e - s);
+    size_t t = nl ? (size_t)(static_cast<const char *>(nl) - base) : e;
+    size_t te = t;
+    if (te > s && base[te - 1] == '\r') --te;
+    if (!(skip_empty && te == s)) out.emplace_back(s, te);
+    s = t + 1;
+  }
+}
+
+template <class F>
+void parallel_for(int T, F &&fn) {
+  if (T <= 1) {
+    fn(0);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(T);
+  std::vector<std::exception_ptr> errs(T);
+  for (int t = 0; t < T; ++t)
+    th.emplace_back([&, t]() {
+      try {
+        fn(t);
+      } catch (...) {
+        errs[t] = std::current_exception();
+      }
+    });
+  for (auto &x : th) x.join();
+  for (auto &e : errs)
+    if (e) std::rethrow_exception(e);
+}
+
+}  // namespace
+
+TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &path, const CSVReadOptions &o) {
+  MappedFile mf(path);
+  const char *base = mf.data();
+  const size_t size = mf.size();
+  Sets sets;
+  static const std::vector<std::string> kArrowNulls{"",     "#N/A", "#N/A N/A", "#NA", "-1.#IND", "-1.#QNAN",
+                                                    "-NaN", "-nan", "1.#IND",   "1.#QNAN", "N/A", "NA",
+                                                    "NULL", "NaN",  "n/a",      "nan",     "null"};
+  const std::vector<std::string> &nulls = o.null_values.empty() ? kArrowNulls : o.null_values;
+  for (const auto &s : nulls) sets.nulls.insert(s);
+  for (const auto &s : o.true_values) sets.trues.insert(s);
+  for (const auto &s : o.false_values) sets.falses.insert(s);
+
+  // skip rows, then the header
+  size_t pos = 0;
+  for (int64_t i = 0; i < o.skip_rows && pos < size; ++i) {
+    const void *nl = std::memchr(base + pos, '\n', size - pos);
+    pos = nl ? (size_t)(static_cast<const char *>(nl) - base) + 1 : size;
+  }
+  std::vector<std::string> names = o.column_names;
+  std::vector<Field> fields;
+  const bool header_row = names.empty() && !o.autogenerate_column_names && o.header;
+  if (header_row) {
+    while (pos < size) {  // first non-empty line
+      const void *nl = std::memchr(base + pos, '\n', size - pos);
+      size_t t = nl ? (size_t)(static_cast<const char *>(nl) - base) : size;
+      size_t te = (t > pos && base[t - 1] == '\r') ? t - 1 : t;
+      const size_t ls = pos;
+      pos = t + 1;
+      if (te == ls && o.ignore_empty_lines) continue;
+      split_line(base + ls, base + te, o, fields);
+      for (const auto &f : fields) names.push_back(field_string(f, o.quote_char));
+      break;
+    }
+  }
+  // line-aligned chunks
+  int T = o.threads > 0 ? o.threads : (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+  const size_t data_bytes = pos < size ? size - pos : 0;
+  T = (int)std::max<size_t>(1, std::min<size_t>((size_t)T, data_bytes / (1 << 16) + 1));
+  std::vector<size_t> cut(T + 1, size);
+  cut[0] = std::min(pos, size);
+  for (int t = 1; t < T; ++t) {
+    size_t c = cut[0] + data_bytes * t / T;
+    const void *nl = c < size ? std::memchr(base + c, '\n', size - c) : nullptr;
+    cut[t] = nl ? (size_t)(static_cast<const char *>(nl) - base) + 1 : size;
+    cut[t] = std::max(cut[t], cut[t - 1]);
+  }
+  std::vector<std::vector<std::pair<size_t, size_t>>> lines(T);
+  parallel_for(T, [&](int t) { find_lines(base, cut[t], cut[t + 1], o.ignore_empty_lines, lines[t]); });
+
+  // column count
+  int ncols = (int)names.size();
+  if (ncols == 0) {
+    for (auto &lv : lines)
+      if (!lv.empty()) {
+        split_line(base + lv[0].first, base + lv[0].second, o, fields);
+        ncols = (int)fields.size();
+        break;
+      }
+    for (int i = 0; i < ncols; ++i) names.push_back("f" + std::to_string(i));
+  }
+  // selected columns (output order)
+  std::vector<int> sel;
+  if (o.include_columns.empty()) {
+    for (int i = 0; i < ncols; ++i) sel.push_back(i);
+  } else {
+    for (const auto &c : o.include_columns) {
+      auto it = std::find(names.begin(), names.end(), c);
+      CYLON_CHECK(it != names.end(), Code::KeyError, "CSV column '" << c << "' not found in " << path);
+      sel.push_back((int)(it - names.begin()));
+    }
+  }
+  const int nsel = (int)sel.size();
+
+  // pass A: type inference
+  std::vector<std::vector<uint8_t>> seen(T, std::vector<uint8_t>(nsel, 0));
+  parallel_for(T, [&](int t) {
+    std::vector<Field> fs;
+    for (const auto &ln : lines[t]) {
+      split_line(base + ln.first, base + ln.second, o, fs);
+      CYLON_CHECK((int)fs.size() == ncols, Code::Invalid,
+                  "CSV parse error in " << path << ": expected " << ncols << " columns, got " << fs.size());
+      for (int j = 0; j < nsel; ++j) seen[t][j] |= classify(fs[sel[j]], sets);
+    }
+  });
+  std::vector<Kind> kinds(nsel);
+  for (int j = 0; j < nsel; ++j) {
+    uint8_t s = 0;
+    for (int t = 0; t < T; ++t) s |= seen[t][j];
+    kinds[j] = resolve(s);
+  }
+  std::vector<int64_t> row0(T + 1, 0);
+  for (int t = 0; t < T; ++t) row0[t + 1] = row0[t] + (int64_t)lines[t].size();
+  const int64_t n = row0[T];
+
+  // pass B: convert
+  std::vector<at::Tensor> data(nsel), valid(nsel);
+  std::vector<std::vector<std::string>> sbytes(nsel, std::vector<std::string>(T));
+  std::vector<std::vector<std::vector<int64_t>>> slens(nsel, std::vector<std::vector<int64_t>>(T));
+  auto cpu = [](at::ScalarType st) { return at::TensorOptions().dtype(st).device(at::kCPU); };
+  for (int j = 0; j < nsel; ++j) {
+    valid[j] = at::ones({n}, cpu(at::kByte));
+    if (kinds[j] == Kind::I64) data[j] = at::empty({n}, cpu(at::kLong));
+    if (kinds[j] == Kind::F64) data[j] = at::empty({n}, cpu(at::kDouble));
+    if (kinds[j] == Kind::BOOL) data[j] = at::empty({n}, cpu(storage_dtype(DataType(Type::BOOL))));
+  }
+  parallel_for(T, [&](int t) {
+    std::vector<Field> fs;
+    int64_t r = row0[t];
+    for (const auto &ln : lines[t]) {
+      split_line(base + ln.first, base + ln.second, o, fs);
+      for (int j = 0; j < nsel; ++j) {
+        const Field &f = fs[sel[j]];
+        std::string_view s(f.p, f.len);
+        const bool is_null = !f.quoted && sets.nulls.count(s);
+        uint8_t *v = valid[j].data_ptr<uint8_t>();
+        switch (kinds[j]) {
+          case Kind::I64: {
+            int64_t x = 0;
+            if (is_null) v[r] = 0; else parse_i64(s, &x);
+            data[j].data_ptr<int64_t>()[r] = x;
+            break;
+          }
+          case Kind::F64: {
+            double x = 0;
+            if (is_null) v[r] = 0; else parse_f64(s, &x);
+            data[j].data_ptr<double>()[r] = x;
+            break;
+          }
+          case Kind::BOOL: {
+            uint8_t x = 0;
+            if (is_null) v[r] = 0; else x = sets.trues.count(s) ? 1 : 0;
+            static_cast<uint8_t *>(data[j].data_ptr())[r] = x;
+            break;
+          }
+          case Kind::STR: {
+            if (is_null && o.strings_can_be_null) {
+              v[r] = 0;
+              slens[j][t].push_back(0);
+            } else {
+              const std::string x = field_string(f, o.quote_char);
+              sbytes[j][t] += x;
+              slens[j][t].push_back((int64_t)x.size());
+            }
+            break;
+          }
+        }
+      }
+      ++r;
+    }
+  });
+  std::vector<Column> cols;
+  for (int j = 0; j < nsel; ++j) {
+    const std::string &name = names[sel[j]];
+    const bool any_null = n > 0 && valid[j].min().item<uint8_t>() == 0;
+    at::Tensor vd = any_null ? valid[j] : at::Tensor();
+    if (kinds[j] == Kind::STR) {
+      int64_t total = 0;
+      for (int t = 0; t < T; ++t) total += (int64_t)sbytes[j][t].size();
+      at::Tensor bytes = at::empty({total}, cpu(at::kByte));
+      at::Tensor offs = at::empty({n + 1}, cpu(at::kLong));
+      int64_t *op = offs.data_ptr<int64_t>();
+      uint8_t *bp = bytes.data_ptr<uint8_t>();
+      int64_t acc = 0, r = 0;
+      op[0] = 0;
+      for (int t = 0; t < T; ++t) {
+        std::memcpy(bp + acc, sbytes[j][t].data(), sbytes[j][t].size());
+        for (int64_t len : slens[j][t]) {
+          acc += len;
+          op[++r] = acc;
+        }
+      }
+      cols.emplace_back(name, DataType(Type::STRING), n, bytes, offs, vd);
+    } else {
+      const Type ty = kinds[j] == Kind::I64 ? Type::INT64 : kinds[j] == Kind::F64 ? Type::DOUBLE : Type::BOOL;
+      cols.emplace_back(name, DataType(ty), n, data[j], at::Tensor(), vd);
+    }
+  }
+  TablePtr t = Table::Make(ctx, std::move(cols));
+  return ctx->GetDevice().is_cuda() ? t->to(ctx->GetDevice()) : t;
+}
+
+std::vector<TablePtr> ReadCSVs(const std::shared_ptr<CylonContext> &ctx, const std::vector<std::string> &paths,
+                               const CSVReadOptions &opts) {
+  std::vector<TablePtr> out(paths.size());
+  CSVReadOptions o = opts;
+  if (o.threads == 0)
+    o.threads = std::max(1, (int)std::min<size_t>(16, std::thread::hardware_concurrency()) / (int)std::max<size_t>(1, paths.size()));
+  parallel_for((int)paths.size(), [&](int i) { out[i] = ReadCSV(ctx, paths[i], o); });
+  return out;
+}
+
+namespace {
+void put_escaped(std::string &out, const char *p, size_t len, char delim) {
+  bool q = false;
+  for (size_t i = 0; i < len; ++i)
+    if (p[i] == delim || p[i] == '"' || p[i] == '\n' || p[i] == '\r') q = true;
+  if (!q) {
+    out.append(p, len);
+    return;
+  }
+  out.push_back('"');
+  for (size_t i = 0; i < len; ++i) {
+    if (p[i] == '"') out.push_back('"');
+    out.push_back(p[i]);
+  }
+  out.push_back('"');
+}
+}  // namespace
+
+void WriteCSV(const TablePtr &table, const std::string &path, const CSVWriteOptions &opts) {
+  TablePtr t = table->device().is_cuda() ? table->to(at::Device(at::kCPU)) : table;
+  std::ofstream f(path, std::ios::binary);
+  CYLON_CHECK(f.good(), Code::IOError, "cannot open " << path << " for writing");
+  std::vector<std::string> names = opts.column_names.empty() ? t->ColumnNames() : opts.column_names;
+  CYLON_CHECK((int)names.size() == t->Columns(), Code::Invalid, "CSV header has " << names.size() << " names for "
+                                                                                   << t->Columns() << " columns");
+  std::string out;
+  for (size_t i = 0; i < names.size(); ++i) {
+    if (i) out.push_back(opts.delimiter);
+    out.push_back('"');
+    out += names[i];
+    out.push_back('"');
+  }
+  out.push_back('\n');
+  char buf[64];
+  for (int64_t r = 0; r < t->Rows(); ++r) {
+    for (int c = 0; c < t->Columns(); ++c) {
+      if (c) out.push_back(opts.delimiter);
+      const Column &col = t->column(c);
+      if (col.nullable() && col.validity.data_ptr<uint8_t>()[r] == 0) continue;
+      const uint8_t *d = static_cast<const uint8_t *>(col.data.data_ptr());
+      if (col.is_var()) {
+        const int64_t *o = col.offsets.data_ptr<int64_t>();
+        put_escaped(out, reinterpret_cast<const char *>(d) + o[r], (size_t)(o[r + 1] - o[r]), opts.delimiter);
+        continue;
+      }
+      const int w = col.type.width();
+      const ValueKind k = col.type.kind();
+      std::to_chars_result res{buf, std::errc()};
+      if (col.type.type == Type::BOOL) {
+        out += d[r] ? "true" : "false";
+        continue;
+      }
+      if (k == ValueKind::FLOAT) {
+        const double x = w == 8 ? reinterpret_cast<const double *>(d)[r]
+                                : w == 4 ? (double)reinterpret_cast<const float *>(d)[r] : 0.0;
+        res = w == 4 ? std::to_chars(buf, buf + sizeof(buf), reinterpret_cast<const float *>(d)[r])
+                     : std::to_chars(buf, buf + sizeof(buf), x);
+      } else if (k == ValueKind::SIGNED_INT) {
+        int64_t x = w == 1 ? (int64_t)reinterpret_cast<const int8_t *>(d)[r]
+                    : w == 2 ? (int64_t)reinterpret_cast<const int16_t *>(d)[r]
+                    : w == 4 ? (int64_t)reinterpret_cast<const int32_t *>(d)[r]
+                             : reinterpret_cast<const int64_t *>(d)[r];
+        res = std::to_chars(buf, buf + sizeof(buf), x);
+      } else if (k == ValueKind::UNSIGNED_INT) {
+        uint64_t x = w == 1 ? d[r]
+                     : w == 2 ? reinterpret_cast<const uint16_t *>(d)[r]
+                     : w == 4 ? reinterpret_cast<const uint32_t *>(d)[r]
+                              : reinterpret_cast<const uint64_t *>(d)[r];
+        res = std::to_chars(buf, buf + sizeof(buf), x);
+      } else {
+        CYLON_THROW(Code::NotImplemented, "WriteCSV: unsupported column type " << col.type.ToString());
+      }
+      out.append(buf, res.ptr);
+    }
+    out.push_back('\n');
+    if (out.size() > (1 << 22)) {
+      f.write(out.data(), (std::streamsize)out.size());
+      out.clear();
+    }
+  }
+  f.write(out.data(), (std::streamsize)out.size());
+  CYLON_CHECK(f.good(), Code::IOError, "write failed: " << path);
+}
+
+}  // namespace io
+}  // namespace cylon

@@ -13,6 +13,7 @@ from typing import Dict, List, Optional, Sequence, Union
 import pyarrow as pa
 import pyarrow.csv as pacsv
 
+from .._lib import C
 from ..ctx.context import CylonContext
 from ..data.table import Table, _ensure_ctx
 
@@ -198,6 +199,26 @@ class CSVWriteOptions:
     ColumnNames = with_column_names
 
 
+def _native_ok(o: CSVReadOptions) -> bool:
+    """Options the native C++ reader (cylon/io/csv.cpp) implements; others go through Arrow."""
+    return not (o._column_types or o._escaping or o._newlines_in_values or o._include_missing_columns)
+
+
+def _read_native(ctx: CylonContext, paths: Sequence[str], o: CSVReadOptions) -> List[Table]:
+    nulls = o._null_values
+    if nulls is not None and len(nulls) == 0:
+        nulls = ["\x00"]  # explicit empty list: nothing is null
+    tabs = C.read_csv(ctx._ctx, list(paths), delimiter=o._delimiter, header=True,
+                      autogenerate_column_names=o._autogenerate_column_names,
+                      column_names=o._column_names or [], skip_rows=o._skip_rows,
+                      ignore_empty_lines=o._ignore_empty_lines, include_columns=o._include_columns or [],
+                      null_values=nulls or [], true_values=o._true_values or [],
+                      false_values=o._false_values or [], strings_can_be_null=o._strings_can_be_null,
+                      quoting=o._quoting, quote_char=o._quote_char, double_quote=o._double_quote,
+                      threads=0 if o._use_threads else 1)
+    return [Table(context=ctx, _native=t) for t in tabs]
+
+
 def _read_one_csv(path: str, options: CSVReadOptions) -> pa.Table:
     ro, po, co = options._arrow()
     try:
@@ -216,6 +237,9 @@ def read_csv(context: CylonContext, path: Union[str, Sequence[str]], csv_read_op
     """Read one CSV file into a Table, or several concurrently into a list of Tables."""
     ctx = _ensure_ctx(context)
     opts = csv_read_options or CSVReadOptions()
+    if _native_ok(opts) and os.environ.get("CYLON_CSV_READER", "native") == "native":
+        tabs = _read_native(ctx, list(path) if isinstance(path, (list, tuple)) else [path], opts)
+        return tabs if isinstance(path, (list, tuple)) else tabs[0]
     if isinstance(path, (list, tuple)):
         with ThreadPoolExecutor(max_workers=max(1, len(path))) as ex:
             tabs = list(ex.map(lambda p: _read_one_csv(p, opts), path))
