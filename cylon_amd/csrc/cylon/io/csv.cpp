@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <charconv>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -109,6 +110,28 @@ enum Seen : uint8_t { S_NULL = 1, S_INT = 2, S_BOOL = 4, S_DBL = 8, S_STR = 16 }
 
 struct Sets {
   std::unordered_set<std::string_view> nulls, trues, falses;
+  // cheap pre-filter for the null lookup: (first byte, length) of any null spelling
+  bool first[256] = {};
+  bool len[64] = {};
+  bool empty_is_null = false;
+  void index() {
+    for (auto s : trues)
+      if (!s.empty()) bfirst[(unsigned char)s[0]] = true;
+    for (auto s : falses)
+      if (!s.empty()) bfirst[(unsigned char)s[0]] = true;
+    for (auto s : nulls) {
+      if (s.empty()) empty_is_null = true;
+      else first[(unsigned char)s[0]] = true;
+      if (s.size() < 64) len[s.size()] = true;
+    }
+  }
+  bool bfirst[256] = {};
+  bool is_null(std::string_view s) const {
+    if (s.empty()) return empty_is_null;
+    if (s.size() >= 64 || !len[s.size()] || !first[(unsigned char)s[0]]) return false;
+    return nulls.count(s) > 0;
+  }
+  bool maybe_bool(std::string_view s) const { return !s.empty() && bfirst[(unsigned char)s[0]]; }
 };
 
 bool parse_i64(std::string_view s, int64_t *v) {
@@ -120,7 +143,12 @@ bool parse_i64(std::string_view s, int64_t *v) {
 }
 
 bool parse_f64(std::string_view s, double *v) {
-  if (s.empty() || s.size() > 120) return false;
+  if (s.empty()) return false;
+  const char *b = s.data(), *e = b + s.size();
+  if (*b == '+') ++b;
+  auto r = std::from_chars(b, e, *v);
+  if (r.ec == std::errc() && r.ptr == e) return true;
+  if (s.size() > 120) return false;  // inf / nan spellings etc.: strtod
   char buf[128];
   std::memcpy(buf, s.data(), s.size());
   buf[s.size()] = 0;
@@ -131,12 +159,23 @@ bool parse_f64(std::string_view s, double *v) {
 
 uint8_t classify(const Field &f, const Sets &sets) {
   std::string_view s(f.p, f.len);
-  if (!f.quoted && sets.nulls.count(s)) return S_NULL;
+  if (!f.quoted && sets.is_null(s)) return S_NULL;
   if (f.escaped) return S_STR;
+  // character-class fast path: plain integers and decimal numbers
+  size_t k = (!s.empty() && (s[0] == '-' || s[0] == '+')) ? 1 : 0;
+  bool digits = k < s.size(), numeric = k < s.size();
+  for (size_t q = k; q < s.size(); ++q) {
+    const char c = s[q];
+    const bool dg = c >= '0' && c <= '9';
+    digits &= dg;
+    numeric &= dg || c == '.' || c == 'e' || c == 'E' || c == '-' || c == '+';
+  }
+  if (digits && s.size() - k <= 18 && !sets.maybe_bool(s)) return S_INT;
+  double d;
+  if (numeric && !digits && parse_f64(s, &d)) return S_DBL;
   int64_t i;
   if (parse_i64(s, &i)) return S_INT;
-  if (sets.trues.count(s) || sets.falses.count(s)) return S_BOOL;
-  double d;
+  if (sets.maybe_bool(s) && (sets.trues.count(s) || sets.falses.count(s))) return S_BOOL;
   if (parse_f64(s, &d)) return S_DBL;
   return S_STR;
 }
@@ -201,6 +240,7 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
   for (const auto &s : nulls) sets.nulls.insert(s);
   for (const auto &s : o.true_values) sets.trues.insert(s);
   for (const auto &s : o.false_values) sets.falses.insert(s);
+  sets.index();
 
   // skip rows, then the header
   size_t pos = 0;
@@ -227,7 +267,7 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
   // line-aligned chunks
   int T = o.threads > 0 ? o.threads : (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
   const size_t data_bytes = pos < size ? size - pos : 0;
-  T = (int)std::max<size_t>(1, std::min<size_t>((size_t)T, data_bytes / (1 << 16) + 1));
+  T = (int)std::max<size_t>(1, std::min<size_t>((size_t)T, data_bytes / (1 << 20)));  // >= 1 MB per thread
   std::vector<size_t> cut(T + 1, size);
   cut[0] = std::min(pos, size);
   for (int t = 1; t < T; ++t) {
@@ -237,7 +277,15 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
     cut[t] = std::max(cut[t], cut[t - 1]);
   }
   std::vector<std::vector<std::pair<size_t, size_t>>> lines(T);
+  auto tick = [t0 = std::chrono::steady_clock::now()](const char *what) {
+    static const bool on = std::getenv("CYLON_CSV_TIMING") != nullptr;
+    if (on)
+      std::fprintf(stderr, "[csv] %-10s %.3f ms\n", what,
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  };
+  tick("open");
   parallel_for(T, [&](int t) { find_lines(base, cut[t], cut[t + 1], o.ignore_empty_lines, lines[t]); });
+  tick("lines");
 
   // column count
   int ncols = (int)names.size();
@@ -274,6 +322,7 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
       for (int j = 0; j < nsel; ++j) seen[t][j] |= classify(fs[sel[j]], sets);
     }
   });
+  tick("infer");
   std::vector<Kind> kinds(nsel);
   for (int j = 0; j < nsel; ++j) {
     uint8_t s = 0;
@@ -295,6 +344,14 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
     if (kinds[j] == Kind::F64) data[j] = at::empty({n}, cpu(at::kDouble));
     if (kinds[j] == Kind::BOOL) data[j] = at::empty({n}, cpu(storage_dtype(DataType(Type::BOOL))));
   }
+  std::vector<uint8_t *> vptr(nsel);
+  std::vector<void *> dptr(nsel, nullptr);
+  for (int j = 0; j < nsel; ++j) {
+    vptr[j] = valid[j].data_ptr<uint8_t>();
+    if (data[j].defined()) dptr[j] = data[j].data_ptr();
+  }
+  std::vector<std::vector<uint8_t>> anynull(T, std::vector<uint8_t>(nsel, 0));
+  tick("alloc");
   parallel_for(T, [&](int t) {
     std::vector<Field> fs;
     int64_t r = row0[t];
@@ -303,30 +360,31 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
       for (int j = 0; j < nsel; ++j) {
         const Field &f = fs[sel[j]];
         std::string_view s(f.p, f.len);
-        const bool is_null = !f.quoted && sets.nulls.count(s);
-        uint8_t *v = valid[j].data_ptr<uint8_t>();
+        const bool is_null = !f.quoted && sets.is_null(s);
+        uint8_t *v = vptr[j];
         switch (kinds[j]) {
           case Kind::I64: {
             int64_t x = 0;
-            if (is_null) v[r] = 0; else parse_i64(s, &x);
-            data[j].data_ptr<int64_t>()[r] = x;
+            if (is_null) v[r] = 0, anynull[t][j] = 1; else parse_i64(s, &x);
+            static_cast<int64_t *>(dptr[j])[r] = x;
             break;
           }
           case Kind::F64: {
             double x = 0;
-            if (is_null) v[r] = 0; else parse_f64(s, &x);
-            data[j].data_ptr<double>()[r] = x;
+            if (is_null) v[r] = 0, anynull[t][j] = 1; else parse_f64(s, &x);
+            static_cast<double *>(dptr[j])[r] = x;
             break;
           }
           case Kind::BOOL: {
             uint8_t x = 0;
-            if (is_null) v[r] = 0; else x = sets.trues.count(s) ? 1 : 0;
-            static_cast<uint8_t *>(data[j].data_ptr())[r] = x;
+            if (is_null) v[r] = 0, anynull[t][j] = 1; else x = sets.trues.count(s) ? 1 : 0;
+            static_cast<uint8_t *>(dptr[j])[r] = x;
             break;
           }
           case Kind::STR: {
             if (is_null && o.strings_can_be_null) {
               v[r] = 0;
+              anynull[t][j] = 1;
               slens[j][t].push_back(0);
             } else {
               const std::string x = field_string(f, o.quote_char);
@@ -340,10 +398,12 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
       ++r;
     }
   });
+  tick("convert");
   std::vector<Column> cols;
   for (int j = 0; j < nsel; ++j) {
     const std::string &name = names[sel[j]];
-    const bool any_null = n > 0 && valid[j].min().item<uint8_t>() == 0;
+    bool any_null = false;
+    for (int t = 0; t < T; ++t) any_null |= anynull[t][j] != 0;
     at::Tensor vd = any_null ? valid[j] : at::Tensor();
     if (kinds[j] == Kind::STR) {
       int64_t total = 0;
@@ -367,6 +427,7 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
       cols.emplace_back(name, DataType(ty), n, data[j], at::Tensor(), vd);
     }
   }
+  tick("columns");
   TablePtr t = Table::Make(ctx, std::move(cols));
   return ctx->GetDevice().is_cuda() ? t->to(ctx->GetDevice()) : t;
 }
