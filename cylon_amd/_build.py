@@ -36,7 +36,7 @@ def hip_sources():
 
 
 def cpp_sources():
-    srcs = [os.path.join(CSRC, "bindings.cpp"), os.path.join(CSRC, "bindings_ops.cpp")]
+    srcs = [os.path.join(CSRC, "bindings.cpp"), os.path.join(CSRC, "bindings_ops.cpp"), os.path.join(CSRC, "capi.cpp")]
     for sub in ("cylon", "cylon/net", "cylon/ops", "cylon/ctx", "cylon/io", "cylon/kernels"):
         srcs += sorted(glob.glob(os.path.join(CSRC, sub, "*.cpp")))
     return [os.path.relpath(s, ROOT) for s in srcs]

@@ -132,6 +132,26 @@ PYBIND11_MODULE(_C, m) {
       .value("LOCAL", net::CommType::LOCAL).value("MPI", net::CommType::MPI).value("TCP", net::CommType::TCP)
       .value("UCX", net::CommType::UCX).value("RCCL", net::CommType::RCCL).value("GLOO", net::CommType::GLOO);
 
+  // ---- P8 C-API: opaque capsules for third-party native code (reference python/pycylon/api/lib.pyx)
+  m.def("table_to_capsule", [](const TablePtr &t) {
+    return py::capsule(new TablePtr(t), "cylon_amd.Table", [](PyObject *o) {
+      delete static_cast<TablePtr *>(PyCapsule_GetPointer(o, "cylon_amd.Table"));
+    });
+  });
+  m.def("table_from_capsule", [](py::capsule c) {
+    CYLON_CHECK(std::string(c.name()) == "cylon_amd.Table", Code::Invalid, "not a cylon_amd.Table capsule");
+    return *static_cast<TablePtr *>(c.get_pointer());
+  });
+  m.def("context_to_capsule", [](const std::shared_ptr<CylonContext> &ctx) {
+    return py::capsule(new std::shared_ptr<CylonContext>(ctx), "cylon_amd.Context", [](PyObject *o) {
+      delete static_cast<std::shared_ptr<CylonContext> *>(PyCapsule_GetPointer(o, "cylon_amd.Context"));
+    });
+  });
+  m.def("context_from_capsule", [](py::capsule c) {
+    CYLON_CHECK(std::string(c.name()) == "cylon_amd.Context", Code::Invalid, "not a cylon_amd.Context capsule");
+    return *static_cast<std::shared_ptr<CylonContext> *>(c.get_pointer());
+  });
+
   py::class_<net::TxRequest, std::shared_ptr<net::TxRequest>>(m, "TxRequest")
       .def(py::init<>())
       .def(py::init([](int target, py::object buffer, std::vector<int32_t> header) {

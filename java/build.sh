@@ -1,0 +1,14 @@
+#!/usr/bin/env bash
+# Build the Java API (J1) and its JNI layer (J2).  Needs a JDK (javac, jni.h) and a built
+# cylon_amd extension (python -c "import cylon_amd").  Not part of the CI image (no JDK).
+set -euo pipefail
+HERE=$(cd "$(dirname "$0")" && pwd)
+ROOT=$(cd "$HERE/.." && pwd)
+: "${JAVA_HOME:?set JAVA_HOME to a JDK}"
+SO=$(python -c "import cylon_amd._C as c; print(c.__file__)")
+mkdir -p "$HERE/build/classes"
+javac -d "$HERE/build/classes" $(find "$HERE/src/main/java" -name '*.java')
+g++ -O2 -shared -fPIC -std=c++17 -I"$JAVA_HOME/include" -I"$JAVA_HOME/include/linux" \
+    "$HERE/src/main/native/cylon_jni.cpp" "$SO" -Wl,-rpath,"$(dirname "$SO")" -o "$HERE/build/libcylon_jni.so"
+jar cf "$HERE/build/cylon_amd.jar" -C "$HERE/build/classes" .
+echo "built $HERE/build/cylon_amd.jar and $HERE/build/libcylon_jni.so"
