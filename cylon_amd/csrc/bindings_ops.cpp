@@ -31,6 +31,8 @@ static std::vector<ops::AggSpec> make_specs(const std::vector<int> &cols, const 
 void register_extended_ops(py::module &m) {
   auto rel = py::call_guard<py::gil_scoped_release>();
 
+  m.def("index_lookup", &ops::IndexLookup, py::arg("ctx"), py::arg("index"), py::arg("labels"), rel);
+
   // ---- C25 native CSV I/O
   m.def(
       "read_csv",

@@ -95,6 +95,8 @@ TablePtr DistributedJoin(const TablePtr &left, const TablePtr &right, const join
 // index pairs of a local join (li, ri; -1 for the unmatched side)
 std::pair<at::Tensor, at::Tensor> JoinIndices(const TablePtr &left, const TablePtr &right,
                                               const join::config::JoinConfig &cfg);
+// C27/K16: index row positions matching each label, grouped by label order then row order
+at::Tensor IndexLookup(const std::shared_ptr<CylonContext> &ctx, const Column &index, const Column &labels);
 
 at::Tensor SortIndices(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending);
 TablePtr Sort(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending);

@@ -2,10 +2,11 @@
 indexer.hpp:76-260, python/pycylon/indexing/index.pyx, python/pycylon/index.py).
 
 Index values live on the table's device as a tensor (numeric) or as an Arrow
-array (strings).  Lookups are device tensor searches (Linear), a lazily built
-value -> positions map (Hash) or arithmetic (Range).  Range-of-values `loc`
-selects from the first position of the start value to the last position of the
-end value, as the reference's LocIndexer does.
+array (strings).  Label lookups (Linear and Hash schemas) run natively: one
+device hash join of the label column against the index column plus a
+(label, row) ordering (C.index_lookup, cylon/ops/index.cpp); Range indexes are
+arithmetic.  Range-of-values `loc` selects from the first position of the start
+value to the last position of the end value, as the reference's LocIndexer does.
 """
 from enum import IntEnum
 from typing import Any, List, Sequence
@@ -13,6 +14,17 @@ from typing import Any, List, Sequence
 import numpy as np
 import pyarrow as pa
 import torch
+
+from .._lib import C
+from ..data import arrow_bridge as ab
+
+_CTXS = {}
+
+
+def _native_ctx(device: str):
+    if device not in _CTXS:
+        _CTXS[device] = C.Context.init_local(device)
+    return _CTXS[device]
 
 
 class IndexingSchema(IntEnum):
@@ -43,6 +55,7 @@ class BaseIndex:
             self.__init__(arr, device)
             return
         self.device = device
+        self._col = None
 
     def __len__(self):
         return len(self._values) if self._values is not None else len(self._arrow)
@@ -73,17 +86,31 @@ class BaseIndex:
         return type(self)(self._arrow.take(pa.array(positions.cpu().numpy())), self.device)
 
     # ---- lookups ------------------------------------------------------------
+    def _native_column(self):
+        if getattr(self, "_col", None) is None:
+            if self._values is not None:
+                self._col = ab.column_from_tensor("i", self._values.contiguous())
+            else:
+                self._col = ab.column_from_arrow("i", self._arrow, self.device)
+        return self._col
+
     def positions_of(self, value) -> torch.Tensor:
-        if self._values is not None:
-            return torch.nonzero(self._values == value, as_tuple=False).reshape(-1)
-        mask = np.asarray(self._arrow.to_numpy(zero_copy_only=False) == value)
-        return torch.from_numpy(np.nonzero(mask)[0].astype(np.int64))
+        return self.positions_of_list([value])
 
     def positions_of_list(self, values: Sequence) -> torch.Tensor:
-        parts = [self.positions_of(v) for v in values]
-        if not parts:
+        values = list(values)
+        if not values or len(self) == 0:
             return torch.empty(0, dtype=torch.int64)
-        return torch.cat([p.to("cpu") for p in parts])
+        try:
+            labels = pa.array(values, type=self.get_index_array().type)
+        except (pa.ArrowInvalid, pa.ArrowTypeError, TypeError, OverflowError):
+            return self._positions_slow(values)
+        col = ab.column_from_arrow("l", labels, self.device)
+        return C.index_lookup(_native_ctx(self.device), self._native_column(), col).cpu()
+
+    def _positions_slow(self, values) -> torch.Tensor:
+        vals = self.index_values
+        return torch.tensor([i for v in values for i, x in enumerate(vals) if x == v], dtype=torch.int64)
 
     def range_positions(self, start, end) -> torch.Tensor:
         s = self.positions_of(start)
@@ -99,21 +126,9 @@ class LinearIndex(BaseIndex):
 
 
 class HashIndex(BaseIndex):
+    """Hash schema: same native lookup (the device hash table is built per lookup on the
+    smaller side, which for label lookups is the label list)."""
     schema = IndexingSchema.HASH
-
-    def __init__(self, values, device: str = "cpu"):
-        super().__init__(values, device)
-        self._map = None
-
-    def _build(self):
-        if self._map is None:
-            self._map = {}
-            for i, v in enumerate(self.index_values):
-                self._map.setdefault(v, []).append(i)
-
-    def positions_of(self, value) -> torch.Tensor:
-        self._build()
-        return torch.tensor(self._map.get(value, []), dtype=torch.int64)
 
 
 class RangeIndex(BaseIndex):
@@ -141,6 +156,10 @@ class RangeIndex(BaseIndex):
     def take(self, positions: torch.Tensor) -> "BaseIndex":
         vals = torch.arange(self.start, self.stop, self.step, dtype=torch.int64)[positions.cpu()]
         return LinearIndex(vals, self.device)
+
+    def positions_of_list(self, values: Sequence) -> torch.Tensor:
+        parts = [self.positions_of(v) for v in values]
+        return torch.cat(parts) if parts else torch.empty(0, dtype=torch.int64)
 
     def positions_of(self, value) -> torch.Tensor:
         v = int(value)

@@ -119,3 +119,16 @@ def test_device_memory_pool(gpu_ctx):
     assert int(x.sum()) == 3 * (1 << 20)
     del x
     assert pool.bytes_allocated() == before
+
+
+def test_native_index_lookup_on_gpu(gpu_ctx, ctx):
+    import numpy as np
+    from cylon_amd.indexing.index import IndexingSchema
+    rng = np.random.default_rng(3)
+    keys = rng.integers(0, 500, 20000)
+    res = []
+    for cx in (gpu_ctx, ctx):
+        t = Table(pa.table({"k": keys, "v": np.arange(20000)}), cx)
+        t.set_index("k", IndexingSchema.HASH, drop=True)
+        res.append(t.loc[[7, 3, 499, 1000], "v"].to_pandas()["v"].tolist())
+    assert res[0] == res[1] and len(res[0]) == int(np.isin(keys, [7, 3, 499]).sum())
