@@ -136,3 +136,27 @@ def test_channel_point_to_point():
         assert datas[:3] == [[100 * other + i for i in range(m + 1)] for m in range(3)]
         heads = [g for g in got if g[0] == "h"]
         assert heads[0][3] == [0, other] and heads[-1][2] == 1 and len(heads) == 5
+
+
+def _etl(ctx, data_dir):
+    import os
+    import torch
+    from cylon_amd.io import read_csv
+    from cylon_amd.models import join_features, train_ddp
+    r = ctx.get_rank() + 1
+    dev = read_csv(ctx, os.path.join(data_dir, f"user_device_tm_{r}.csv"))
+    use = read_csv(ctx, os.path.join(data_dir, f"user_usage_tm_{r}.csv"))
+    x, y = join_features(dev, use)
+    model, loss = train_ddp(x, y, epochs=2, train_rows=50)
+    # DDP keeps replicas identical
+    w = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    return x.shape[0], x.shape[1], loss, w.tolist()
+
+
+def test_etl_to_ddp_pipeline():
+    import os
+    d = os.path.join(os.path.dirname(__file__), "data", "tutorial")
+    res = run_distributed(_etl, 2, d)
+    for rows, feats, loss, _ in res:
+        assert rows > 50 and feats == 4 and loss == loss
+    assert np.allclose(res[0][3], res[1][3])

@@ -192,3 +192,16 @@ def test_context_config(ctx):
     ctx.add_config("compute_engine", "device")
     assert ctx.get_rank() == 0 and ctx.get_world_size() == 1 and not ctx.is_distributed()
     assert ctx.get_next_sequence() + 1 == ctx.get_next_sequence()
+
+
+def test_functional_ops_api(ctx):
+    from cylon_amd import ops
+    a = Table.from_pydict(ctx, {"k": [3, 1, 2, 2], "v": [1.0, 2.0, 3.0, 4.0]})
+    b = Table.from_pydict(ctx, {"k": [2, 3, 9], "w": [5, 6, 7]})
+    assert ops.join(a, b, "inner", "hash", on=["k"]).row_count == 3
+    assert ops.sort(a, "k").to_pydict()["k"] == [1, 2, 2, 3]
+    assert ops.unique(a, ["k"]).row_count == 3
+    assert ops.local_groupby(a, "k", {"v": "sum"}).row_count == 3
+    assert ops.merge([a, a]).row_count == 8
+    assert ops.project(a, ["v"]).column_names == ["v"]
+    assert ops.union(ops.project(a, ["k"]), ops.project(b, ["k"])).row_count == 4
