@@ -48,6 +48,11 @@ def make_relation(ctx, rows_local, key_range, ncols, seed, device):
     return Table.from_torch(ctx, cols)
 
 
+def sync():
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -55,19 +60,21 @@ def main():
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from cylon_amd import CylonContext, RCCLConfig
+    from cylon_amd import CylonContext, GlooConfig, RCCLConfig
 
+    # CYLON_BENCH_BACKEND=gloo rehearses the multi-rank path on CPUs (tests only)
+    cpu_rehearsal = os.environ.get("CYLON_BENCH_BACKEND", "") == "gloo"
     if world > 1:
-        ctx = CylonContext(config=RCCLConfig(), distributed=True)
+        ctx = CylonContext(config=GlooConfig() if cpu_rehearsal else RCCLConfig(), distributed=True)
     else:
-        ctx = CylonContext(config=None, distributed=False, device="cuda:0")
+        ctx = CylonContext(config=None, distributed=False, device="cpu" if cpu_rehearsal else "cuda:0")
     device = ctx.device
     n = world
     rows_local = args.rows // n
     key_range = max(1, int(args.key_ratio * args.rows))
     left = make_relation(ctx, rows_local, key_range, args.payload_cols, 1000 + rank, device)
     right = make_relation(ctx, rows_local, key_range, args.payload_cols, 2000 + rank, device)
-    torch.cuda.synchronize()
+    sync()
 
     def step():
         out = left.distributed_join(right, "inner", args.algorithm, on=[0], left_prefix="l_", right_prefix="r_")
@@ -77,11 +84,11 @@ def main():
     for _ in range(args.warmup):
         out_rows = step()
     ctx.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out_rows = step()
-    torch.cuda.synchronize()
+    sync()
     ctx.barrier()
     elapsed = time.perf_counter() - t0
 

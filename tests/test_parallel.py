@@ -160,3 +160,28 @@ def test_etl_to_ddp_pipeline():
     for rows, feats, loss, _ in res:
         assert rows > 50 and feats == 4 and loss == loss
     assert np.allclose(res[0][3], res[1][3])
+
+
+def test_bench_contract_multirank_cpu_rehearsal():
+    """bench.py under torch.distributed.run (2 ranks, gloo): one JSON line with the driver's fields."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, CYLON_BENCH_BACKEND="gloo")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+                          "--gpus", "2", "--steps", "2", "--warmup", "1", "--rows", "100000"],
+                         capture_output=True, text=True, timeout=240, env=env, cwd="/tmp")
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert out.returncode == 0 and len(lines) == 1, out.stderr[-2000:]
+    rec = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in rec
+    assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["config"]["output_rows"] > 0
