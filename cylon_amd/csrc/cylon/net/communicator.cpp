@@ -143,6 +143,20 @@ void ProcessGroupCommunicator::Broadcast(at::Tensor &t, int root) {
 namespace cylon {
 namespace net {
 
+namespace {
+class DoneRequest : public P2PRequest {
+ public:
+  bool Test() override { return true; }
+  void Wait() override {}
+};
+}  // namespace
+
+std::pair<at::Tensor, std::shared_ptr<P2PRequest>> Communicator::AllToAllVAsync(const at::Tensor &send,
+                                                                                const std::vector<int64_t> &sc,
+                                                                                const std::vector<int64_t> &rc) {
+  return {AllToAllV(send, sc, rc), std::make_shared<DoneRequest>()};
+}
+
 std::shared_ptr<P2PRequest> Communicator::ISend(const at::Tensor &, int, int) {
   CYLON_THROW(Code::NotImplemented, "point-to-point send needs a distributed communicator");
 }
@@ -207,6 +221,31 @@ class PGRequest : public P2PRequest {
   bool done_ = false;
 };
 }  // namespace
+
+std::pair<at::Tensor, std::shared_ptr<P2PRequest>> ProcessGroupCommunicator::AllToAllVAsync(
+    const at::Tensor &send, const std::vector<int64_t> &send_counts, const std::vector<int64_t> &recv_counts) {
+  CYLON_CHECK((int)send_counts.size() == world_ && (int)recv_counts.size() == world_, Code::Invalid,
+              "all-to-all counts must have world-size entries");
+  int64_t total = 0;
+  for (auto c : recv_counts) total += c;
+  at::Tensor in = to_comm(send);
+  std::vector<int64_t> shape(in.sizes().begin(), in.sizes().end());
+  if (shape.empty()) shape.push_back(0);
+  shape[0] = total;
+  at::Tensor out = at::empty(shape, in.options());
+  std::vector<int64_t> sc(send_counts), rc(recv_counts);
+  auto work = pg_->alltoall_base(out, in, rc, sc);
+  // the receive buffer is handed out in the caller's dtype/device once waited on
+  at::Tensor user = out;
+  if (send.scalar_type() == at::kBool) user = out.view(at::kBool);
+  if (user.device() != send.device()) {
+    auto req = std::make_shared<PGRequest>(work, out, at::Tensor(), type_ != CommType::RCCL);
+    req->Wait();
+    return {user.to(send.device()), std::make_shared<DoneRequest>()};
+  }
+  // keep `in` alive until completion: c10d works hold their tensors
+  return {user, std::make_shared<PGRequest>(work, out, at::Tensor(), type_ != CommType::RCCL)};
+}
 
 std::shared_ptr<P2PRequest> ProcessGroupCommunicator::ISend(const at::Tensor &t, int dst, int tag) {
   CYLON_CHECK(dst >= 0 && dst < world_ && dst != rank_, Code::Invalid, "bad send target " << dst);

@@ -57,6 +57,12 @@ class Communicator {
   // Variable all-to-all along dim 0: send[ sum(send_counts) ] -> recv[ sum(recv_counts) ].
   virtual at::Tensor AllToAllV(const at::Tensor &send, const std::vector<int64_t> &send_counts,
                                const std::vector<int64_t> &recv_counts) = 0;
+  // Posted all-to-all: returns the receive tensor and a request to Wait() on before
+  // using it.  RCCL works run on the communicator's stream; kernels enqueued on the
+  // compute stream between posting and waiting overlap with the transfer.
+  // Default: the blocking AllToAllV with an already completed request.
+  virtual std::pair<at::Tensor, std::shared_ptr<P2PRequest>> AllToAllVAsync(
+      const at::Tensor &send, const std::vector<int64_t> &send_counts, const std::vector<int64_t> &recv_counts);
   // Exchange per-peer element counts (the size matrix row of this rank).
   virtual std::vector<int64_t> ExchangeCounts(const std::vector<int64_t> &send_counts) = 0;
   virtual void AllReduce(at::Tensor &t, ReduceOp op) = 0;
@@ -105,6 +111,12 @@ class FaultInjectionCommunicator : public Communicator {
     tick("AllToAllV");
     return inner_->AllToAllV(s, sc, rc);
   }
+  std::pair<at::Tensor, std::shared_ptr<P2PRequest>> AllToAllVAsync(const at::Tensor &s,
+                                                                    const std::vector<int64_t> &sc,
+                                                                    const std::vector<int64_t> &rc) override {
+    tick("AllToAllV");
+    return inner_->AllToAllVAsync(s, sc, rc);
+  }
   std::vector<int64_t> ExchangeCounts(const std::vector<int64_t> &c) override {
     tick("ExchangeCounts");
     return inner_->ExchangeCounts(c);
@@ -152,6 +164,9 @@ class ProcessGroupCommunicator : public Communicator {
   void Barrier() override;
   at::Tensor AllToAllV(const at::Tensor &send, const std::vector<int64_t> &send_counts,
                        const std::vector<int64_t> &recv_counts) override;
+  std::pair<at::Tensor, std::shared_ptr<P2PRequest>> AllToAllVAsync(
+      const at::Tensor &send, const std::vector<int64_t> &send_counts,
+      const std::vector<int64_t> &recv_counts) override;
   std::vector<int64_t> ExchangeCounts(const std::vector<int64_t> &send_counts) override;
   void AllReduce(at::Tensor &t, ReduceOp op) override;
   at::Tensor AllGather(const at::Tensor &in) override;

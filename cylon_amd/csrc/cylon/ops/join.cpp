@@ -384,9 +384,8 @@ TablePtr Join(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg
 TablePtr DistributedJoin(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
   auto ctx = left->GetContext();
   if (ctx->GetWorldSize() == 1) return Join(left, right, cfg);
-  TablePtr l = Shuffle(left, cfg.GetLeftColumnIdx());
-  TablePtr r = Shuffle(right, cfg.GetRightColumnIdx());
-  return Join(l, r, cfg);
+  auto lr = ShufflePair(left, cfg.GetLeftColumnIdx(), right, cfg.GetRightColumnIdx());
+  return Join(lr.first, lr.second, cfg);
 }
 
 }  // namespace ops

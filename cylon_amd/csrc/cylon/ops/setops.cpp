@@ -82,7 +82,8 @@ static TablePtr dist_set_op(const TablePtr &l, const TablePtr &r, SetOp op) {
   auto ctx = l->GetContext();
   if (ctx->GetWorldSize() == 1) return set_op(l, r, op);
   const auto cols = all_cols(l);
-  return set_op(Shuffle(l, cols), Shuffle(r, cols), op);
+  auto lr = ShufflePair(l, cols, r, cols);
+  return set_op(lr.first, lr.second, op);
 }
 
 TablePtr DistributedUnion(const TablePtr &l, const TablePtr &r) { return dist_set_op(l, r, SetOp::UNION); }

@@ -23,11 +23,29 @@ static at::Tensor hash_pids(const TablePtr &t, const std::vector<int> &cols, uin
   return pid;
 }
 
-TablePtr AllToAllTable(const TablePtr &part, const std::vector<int64_t> &counts) {
+// A table whose column buffers are in flight (posted all-to-alls).
+struct PendingTable {
+  std::shared_ptr<CylonContext> ctx;
+  int64_t total = 0;
+  struct Col {
+    const Column *src;
+    at::Tensor data, valid, rlens;  // receive buffers (rlens: var-width lengths)
+  };
+  std::vector<Col> cols;
+  std::vector<std::shared_ptr<net::P2PRequest>> reqs;
+  TablePtr passthrough;  // world 1
+};
+
+static PendingTable AllToAllBegin(const TablePtr &part, const std::vector<int64_t> &counts) {
+  PendingTable pt;
   auto ctx = part->GetContext();
+  pt.ctx = ctx;
   auto comm = ctx->GetCommunicator();
   const int world = ctx->GetWorldSize();
-  if (world == 1 || !ctx->IsDistributed()) return part;
+  if (world == 1 || !ctx->IsDistributed()) {
+    pt.passthrough = part;
+    return pt;
+  }
   const size_t P = counts.size();
 
   // rows per destination rank (partition-major order keeps each rank contiguous)
@@ -37,8 +55,7 @@ TablePtr AllToAllTable(const TablePtr &part, const std::vector<int64_t> &counts)
     send_rows[target] += counts[i];
   }
   std::vector<int64_t> recv_rows = comm->ExchangeCounts(send_rows);
-  int64_t total = 0;
-  for (auto r : recv_rows) total += r;
+  for (auto r : recv_rows) pt.total += r;
 
   // schema-level nullability must agree across ranks
   const int ncols = part->Columns();
@@ -49,60 +66,113 @@ TablePtr AllToAllTable(const TablePtr &part, const std::vector<int64_t> &counts)
   std::vector<int64_t> nullable = to_host_vec(gflags.to(at::kLong));
 
   Exec ex(part->device());
-  std::vector<Column> out;
+  auto post = [&](const at::Tensor &t, const std::vector<int64_t> &sc, const std::vector<int64_t> &rc) {
+    auto r = comm->AllToAllVAsync(t, sc, rc);
+    pt.reqs.push_back(r.second);
+    return r.first;
+  };
   for (int c = 0; c < ncols; ++c) {
     const Column &col = part->column(c);
-    at::Tensor valid;
+    PendingTable::Col pc;
+    pc.src = &col;
     if (nullable[c]) {
       at::Tensor v = col.nullable() ? col.validity : at::ones({col.length}, ex.opts(at::kByte));
-      valid = comm->AllToAllV(v, send_rows, recv_rows);
+      pc.valid = post(v, send_rows, recv_rows);
     }
     if (!col.is_var()) {
       const int64_t per = col.type.kind() == ValueKind::FIXED_BYTES ? col.type.width() : 1;
       std::vector<int64_t> sc(send_rows), rc(recv_rows);
       for (auto &x : sc) x *= per;
       for (auto &x : rc) x *= per;
-      at::Tensor d = comm->AllToAllV(col.data, sc, rc);
-      out.emplace_back(col.name, col.type, total, d, at::Tensor(), valid);
-      continue;
-    }
-    // var width: lengths, then bytes
-    at::Tensor lens = col.offsets.slice(0, 1, col.length + 1) - col.offsets.slice(0, 0, col.length);
-    at::Tensor rlens = comm->AllToAllV(lens.contiguous(), send_rows, recv_rows);
-    std::vector<int64_t> send_bytes(world, 0);
-    {
-      at::Tensor ho = col.offsets.to(at::kCPU);
-      const int64_t *o = ho.data_ptr<int64_t>();
-      int64_t row = 0;
-      for (int r = 0; r < world; ++r) {
-        send_bytes[r] = o[row + send_rows[r]] - o[row];
-        row += send_rows[r];
+      pc.data = post(col.data, sc, rc);
+    } else {  // var width: lengths, then bytes
+      at::Tensor lens = col.offsets.slice(0, 1, col.length + 1) - col.offsets.slice(0, 0, col.length);
+      pc.rlens = post(lens.contiguous(), send_rows, recv_rows);
+      std::vector<int64_t> send_bytes(world, 0);
+      {
+        at::Tensor ho = col.offsets.to(at::kCPU);
+        const int64_t *o = ho.data_ptr<int64_t>();
+        int64_t row = 0;
+        for (int r = 0; r < world; ++r) {
+          send_bytes[r] = o[row + send_rows[r]] - o[row];
+          row += send_rows[r];
+        }
       }
+      std::vector<int64_t> recv_bytes = comm->ExchangeCounts(send_bytes);
+      pc.data = post(col.data, send_bytes, recv_bytes);
     }
-    std::vector<int64_t> recv_bytes = comm->ExchangeCounts(send_bytes);
-    at::Tensor bytes = comm->AllToAllV(col.data, send_bytes, recv_bytes);
-    at::Tensor offs = exclusive_scan(ex, rlens.contiguous());
-    out.emplace_back(col.name, col.type, total, bytes, offs, valid);
+    pt.cols.push_back(pc);
   }
-  return Table::Make(ctx, std::move(out));
+  return pt;
+}
+
+static TablePtr AllToAllFinish(PendingTable &pt) {
+  if (pt.passthrough) return pt.passthrough;
+  for (auto &r : pt.reqs) r->Wait();
+  std::vector<Column> out;
+  for (auto &pc : pt.cols) {
+    const Column &col = *pc.src;
+    if (!col.is_var()) {
+      out.emplace_back(col.name, col.type, pt.total, pc.data, at::Tensor(), pc.valid);
+    } else {
+      Exec ex(pc.rlens.device());
+      at::Tensor offs = exclusive_scan(ex, pc.rlens.contiguous());
+      out.emplace_back(col.name, col.type, pt.total, pc.data, offs, pc.valid);
+    }
+  }
+  return Table::Make(pt.ctx, std::move(out));
+}
+
+TablePtr AllToAllTable(const TablePtr &part, const std::vector<int64_t> &counts) {
+  PendingTable pt = AllToAllBegin(part, counts);
+  return AllToAllFinish(pt);
+}
+
+static std::pair<TablePtr, std::vector<int64_t>> shuffle_partition(const TablePtr &t,
+                                                                   const std::vector<int> &hash_cols, int world) {
+  CYLON_PHASE("shuffle.partition", t->device());
+  at::Tensor pid = hash_pids(t, hash_cols, (uint32_t)world);
+  return PartitionReorder(t, pid, (uint32_t)world);
 }
 
 TablePtr Shuffle(const TablePtr &t, const std::vector<int> &hash_cols) {
   auto ctx = t->GetContext();
   const int world = ctx->GetWorldSize();
   if (world == 1) return t;
-  std::pair<TablePtr, std::vector<int64_t>> r;
-  {
-    CYLON_PHASE("shuffle.partition", t->device());
-    at::Tensor pid = hash_pids(t, hash_cols, (uint32_t)world);
-    r = PartitionReorder(t, pid, (uint32_t)world);
-  }
+  auto r = shuffle_partition(t, hash_cols, world);
   CYLON_PHASE("shuffle.exchange", t->device());
   trace::add_counter("shuffle.rows_in", t->Rows());
   trace::add_counter("shuffle.bytes_in", t->nbytes());
   TablePtr out = AllToAllTable(r.first, r.second);
   trace::add_counter("shuffle.rows_out", out->Rows());
   return out;
+}
+
+// Both relations of a distributed binary operator: the second table's partitioning
+// kernels are enqueued while the first table's all-to-alls are in flight on the
+// communicator's stream, and the two transfers are waited for only at the end.
+std::pair<TablePtr, TablePtr> ShufflePair(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,
+                                          const std::vector<int> &bcols) {
+  auto ctx = a->GetContext();
+  const int world = ctx->GetWorldSize();
+  if (world == 1) return {a, b};
+  auto ra = shuffle_partition(a, acols, world);
+  PendingTable pa;
+  {
+    CYLON_PHASE("shuffle.exchange", a->device());
+    pa = AllToAllBegin(ra.first, ra.second);
+  }
+  auto rb = shuffle_partition(b, bcols, world);
+  PendingTable pb;
+  {
+    CYLON_PHASE("shuffle.exchange", b->device());
+    pb = AllToAllBegin(rb.first, rb.second);
+  }
+  trace::add_counter("shuffle.rows_in", a->Rows() + b->Rows());
+  trace::add_counter("shuffle.bytes_in", a->nbytes() + b->nbytes());
+  TablePtr oa = AllToAllFinish(pa), ob = AllToAllFinish(pb);
+  trace::add_counter("shuffle.rows_out", oa->Rows() + ob->Rows());
+  return {oa, ob};
 }
 
 }  // namespace ops

@@ -88,6 +88,9 @@ std::vector<TablePtr> HashPartition(const TablePtr &t, const std::vector<int> &c
 // partition-major table + per-partition counts -> received table
 TablePtr AllToAllTable(const TablePtr &partitioned, const std::vector<int64_t> &counts);
 TablePtr Shuffle(const TablePtr &t, const std::vector<int> &hash_cols);
+// shuffle two tables with the second one's partitioning overlapped with the first's transfer
+std::pair<TablePtr, TablePtr> ShufflePair(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,
+                                          const std::vector<int> &bcols);
 
 // ---- relational -----------------------------------------------------------
 TablePtr Join(const TablePtr &left, const TablePtr &right, const join::config::JoinConfig &cfg);
