@@ -62,9 +62,15 @@ def main():
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from cylon_amd import CylonContext, GlooConfig, RCCLConfig
 
-    # CYLON_BENCH_BACKEND=gloo rehearses the multi-rank path on CPUs (tests only)
-    cpu_rehearsal = os.environ.get("CYLON_BENCH_BACKEND", "") == "gloo"
-    if world > 1:
+    # CYLON_BENCH_BACKEND=gloo rehearses the multi-rank path on CPUs (tests only);
+    # gloo-gpu keeps the tables in HBM (ranks may share one GPU) with gloo collectives
+    backend = os.environ.get("CYLON_BENCH_BACKEND", "")
+    cpu_rehearsal = backend == "gloo"
+    if world > 1 and backend == "gloo-gpu":
+        ndev = max(torch.cuda.device_count(), 1)
+        ctx = CylonContext(config=GlooConfig(device=f"cuda:{int(os.environ.get('LOCAL_RANK', '0')) % ndev}"),
+                           distributed=True)
+    elif world > 1:
         ctx = CylonContext(config=GlooConfig() if cpu_rehearsal else RCCLConfig(), distributed=True)
     else:
         ctx = CylonContext(config=None, distributed=False, device="cpu" if cpu_rehearsal else "cuda:0")

@@ -198,27 +198,77 @@ struct RadixCols {
   std::vector<int> w;
 };
 
-static RadixCols radix_cols(const TablePtr &t, const RadixSide *s, const std::vector<Column> *outs) {
+static RadixCols radix_cols(const TablePtr &t, const RadixSide *s, const std::vector<Column> *outs,
+                            int64_t out_off = 0) {
   RadixCols rc;
   for (int c = 0; c < t->Columns(); ++c) {
     const Column &col = t->column(c);
     rc.in.push_back(s && !s->is_key[c] ? reinterpret_cast<const uint8_t *>(s->data[c].data_ptr())
                                        : (s ? nullptr : reinterpret_cast<const uint8_t *>(1)));
-    rc.out.push_back(outs ? reinterpret_cast<uint8_t *>((*outs)[c].data.data_ptr()) : nullptr);
+    rc.out.push_back(outs ? reinterpret_cast<uint8_t *>((*outs)[c].data.data_ptr()) + out_off * col.type.width()
+                          : nullptr);
     rc.w.push_back(col.type.width());
     if (col.nullable()) {
       rc.in.push_back(s ? s->valid[c].data_ptr<uint8_t>() : reinterpret_cast<const uint8_t *>(1));
-      rc.out.push_back(outs ? (*outs)[c].validity.data_ptr<uint8_t>() : nullptr);
+      rc.out.push_back(outs ? (*outs)[c].validity.data_ptr<uint8_t>() + out_off : nullptr);
       rc.w.push_back(1);
     }
   }
   return rc;
 }
 
+// Output accumulator of a chunked (pipelined) distributed join.  The radix join
+// writes every chunk's rows straight into one set of output columns at the
+// running row offset (capacity sized from the first chunk's output for all
+// chunks, grown geometrically if a later chunk needs more), so the chunked join
+// costs no concatenation pass; chunks that take another join path hand over
+// whole tables, concatenated once at the end.
+struct JoinSink {
+  std::vector<Column> cols;  // left columns ++ right columns, `cap` rows each
+  int64_t size = 0, cap = 0;
+  int chunks_total = 1, chunks_done = 0;
+  std::vector<TablePtr> tables;
+
+  // room for m more rows; returns the row offset to write at
+  int64_t reserve(const Exec &ex, int64_t m, const std::vector<Column> &proto) {
+    if (size + m > cap) {
+      const int64_t left_chunks = std::max(1, chunks_total - chunks_done);
+      const int64_t want = std::max(size + m + (m * (left_chunks - 1)) * 103 / 100 + 4096, 2 * cap);
+      std::vector<Column> fresh;
+      for (size_t c = 0; c < proto.size(); ++c) {
+        Column n = make_fixed_column(proto[c].name, proto[c].type, want, ex.device, proto[c].nullable());
+        if (size > 0) {
+          n.data.slice(0, 0, size).copy_(cols[c].data.slice(0, 0, size));
+          if (n.nullable()) n.validity.slice(0, 0, size).copy_(cols[c].validity.slice(0, 0, size));
+        }
+        fresh.push_back(std::move(n));
+      }
+      cols = std::move(fresh);
+      cap = want;
+    }
+    const int64_t off = size;
+    size += m;
+    return off;
+  }
+
+  TablePtr finish(const std::shared_ptr<CylonContext> &ctx) {
+    std::vector<TablePtr> parts;
+    if (!cols.empty()) {
+      std::vector<Column> out;
+      for (const auto &c : cols) out.push_back(c.slice(0, size));
+      parts.push_back(Table::Make(ctx, std::move(out)));
+    }
+    for (auto &t : tables) parts.push_back(t);
+    if (parts.size() == 1) return parts[0];
+    return Merge(parts);
+  }
+};
+
 // Returns nullptr when a build partition overflows the LDS capacity (heavy key
-// skew / duplicates); the caller then runs the global-table join.
+// skew / duplicates); the caller then runs the global-table join.  With a sink
+// the rows are written into the sink's columns and the sink's table is returned.
 static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr &right, const at::Tensor &lk,
-                           const at::Tensor &rk, const JoinConfig &cfg) {
+                           const at::Tensor &rk, const JoinConfig &cfg, JoinSink *sink = nullptr) {
   const int64_t nl = left->Rows(), nr = right->Rows();
   const bool build_left = nl < nr;
   const TablePtr &bt = build_left ? left : right;
@@ -261,13 +311,25 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   const int64_t m = read_i64(out_offs, nparts);
   CYLON_PHASE("join.radix.write", ex.device);
   std::vector<Column> lcols, rcols;
-  for (const auto &col : left->columns())
-    lcols.push_back(make_fixed_column(cfg.GetLeftTablePrefix() + col.name, col.type, m, ex.device, col.nullable()));
-  for (const auto &col : right->columns())
-    rcols.push_back(make_fixed_column(cfg.GetRightTablePrefix() + col.name, col.type, m, ex.device, col.nullable()));
+  int64_t off = 0;
+  if (sink) {
+    std::vector<Column> proto;
+    for (const auto &col : left->columns())
+      proto.emplace_back(cfg.GetLeftTablePrefix() + col.name, col.type, 0, col.data, at::Tensor(), col.validity);
+    for (const auto &col : right->columns())
+      proto.emplace_back(cfg.GetRightTablePrefix() + col.name, col.type, 0, col.data, at::Tensor(), col.validity);
+    off = sink->reserve(ex, m, proto);
+    lcols.assign(sink->cols.begin(), sink->cols.begin() + left->Columns());
+    rcols.assign(sink->cols.begin() + left->Columns(), sink->cols.end());
+  } else {
+    for (const auto &col : left->columns())
+      lcols.push_back(make_fixed_column(cfg.GetLeftTablePrefix() + col.name, col.type, m, ex.device, col.nullable()));
+    for (const auto &col : right->columns())
+      rcols.push_back(make_fixed_column(cfg.GetRightTablePrefix() + col.name, col.type, m, ex.device, col.nullable()));
+  }
   if (m > 0) {
-    RadixCols pc = build_left ? radix_cols(right, &R, &rcols) : radix_cols(left, &L, &lcols);
-    RadixCols bc = build_left ? radix_cols(left, &L, &lcols) : radix_cols(right, &R, &rcols);
+    RadixCols pc = build_left ? radix_cols(right, &R, &rcols, off) : radix_cols(left, &L, &lcols, off);
+    RadixCols bc = build_left ? radix_cols(left, &L, &lcols, off) : radix_cols(right, &R, &rcols, off);
     // probe-side columns are streamed from HBM: the key column is read from its partitioned array
     for (size_t q = 0; q < pc.in.size(); ++q)
       if (!pc.in[q]) pc.in[q] = reinterpret_cast<const uint8_t *>(P.keys.data_ptr());
@@ -276,6 +338,7 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
                           (int)pc.in.size(), bc.in.data(), bc.out.data(), bc.w.data(), (int)bc.in.size(), ex.stream);
   }
   trace::add_counter("join.radix.rows_out", m);
+  if (sink) return Table::Make(left->GetContext(), sink->cols);
   for (auto &c : rcols) lcols.push_back(std::move(c));
   return Table::Make(left->GetContext(), std::move(lcols));
 }
@@ -353,7 +416,9 @@ static std::pair<at::Tensor, at::Tensor> join_impl(TablePtr left, TablePtr right
   return {li, ri};
 }
 
-TablePtr Join(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
+// Local join.  With a sink (chunked distributed join) the radix path writes into
+// the sink and nullptr is returned; other paths return their table.
+static TablePtr join_local(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg, JoinSink *sink) {
   if (left->device().is_cuda() && cfg.GetType() == JoinType::INNER && cfg.GetAlgorithm() == JoinAlgorithm::HASH &&
       cfg.GetLeftColumnIdx().size() == 1 && std::min(left->Rows(), right->Rows()) >= radix_join_min_rows() &&
       radix_eligible(left) && radix_eligible(right)) {
@@ -363,7 +428,7 @@ TablePtr Join(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg
       Exec ex(left->device());
       KeyEncoding lk = encode_keys(ex, left, cfg.GetLeftColumnIdx(), true);
       KeyEncoding rk = encode_keys(ex, right, cfg.GetRightColumnIdx(), true);
-      if (TablePtr out = radix_join(ex, left, right, lk.keys, rk.keys, cfg)) return out;
+      if (TablePtr out = radix_join(ex, left, right, lk.keys, rk.keys, cfg, sink)) return sink ? nullptr : out;
     }
   }
   TablePtr l = left, r = right;
@@ -381,9 +446,45 @@ TablePtr Join(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg
   return Table::Make(left->GetContext(), std::move(cols));
 }
 
+TablePtr Join(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
+  return join_local(left, right, cfg, nullptr);
+}
+
+// Number of hash chunks of the pipelined distributed join (identical on every
+// rank: config / environment, or the global row count).  Context config
+// "shuffle_chunks" (or CYLON_SHUFFLE_CHUNKS) forces a value; by default device
+// tables with >= 2^24 rows per rank per relation are shuffled in 4 chunks, so
+// that three quarters of the local join overlap the RCCL transfer.
+static int join_shuffle_chunks(const TablePtr &left, const TablePtr &right) {
+  auto ctx = left->GetContext();
+  for (const TablePtr &t : {left, right})
+    for (const auto &c : t->columns())
+      if (c.is_var()) return 1;
+  std::string v = ctx->GetConfig("shuffle_chunks", "");
+  if (v.empty())
+    if (const char *e = std::getenv("CYLON_SHUFFLE_CHUNKS")) v = e;
+  if (!v.empty()) return std::max(1, std::min(64, std::atoi(v.c_str())));
+  if (!left->device().is_cuda()) return 1;
+  at::Tensor rows = at::tensor({std::min(left->Rows(), right->Rows())},
+                               at::TensorOptions().dtype(at::kLong)).to(left->device());
+  ctx->GetCommunicator()->AllReduce(rows, net::ReduceOp::MIN);
+  return rows.item<int64_t>() >= (int64_t(1) << 24) ? 4 : 1;
+}
+
 TablePtr DistributedJoin(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
   auto ctx = left->GetContext();
   if (ctx->GetWorldSize() == 1) return Join(left, right, cfg);
+  const int K = join_shuffle_chunks(left, right);
+  if (K > 1) {
+    JoinSink sink;
+    sink.chunks_total = K;
+    ShufflePairChunked(left, cfg.GetLeftColumnIdx(), right, cfg.GetRightColumnIdx(), K,
+                       [&](int, const TablePtr &l, const TablePtr &r) {
+                         if (TablePtr t = join_local(l, r, cfg, &sink)) sink.tables.push_back(t);
+                         ++sink.chunks_done;
+                       });
+    return sink.finish(ctx);
+  }
   auto lr = ShufflePair(left, cfg.GetLeftColumnIdx(), right, cfg.GetRightColumnIdx());
   return Join(lr.first, lr.second, cfg);
 }

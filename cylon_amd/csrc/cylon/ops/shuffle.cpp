@@ -33,45 +33,46 @@ struct PendingTable {
   };
   std::vector<Col> cols;
   std::vector<std::shared_ptr<net::P2PRequest>> reqs;
+  TablePtr keep;         // the sent table (its buffers must outlive the posted transfers)
   TablePtr passthrough;  // world 1
 };
 
-static PendingTable AllToAllBegin(const TablePtr &part, const std::vector<int64_t> &counts) {
+// schema-level nullability of every column, agreed across ranks (one all-reduce
+// for any number of tables with the same column count)
+static std::vector<int64_t> agree_nullability(const std::vector<TablePtr> &ts) {
+  auto ctx = ts[0]->GetContext();
+  std::vector<int> off;
+  int total = 0;
+  for (auto &t : ts) {
+    off.push_back(total);
+    total += t->Columns();
+  }
+  at::Tensor flags = at::zeros({std::max(total, 1)}, at::TensorOptions().dtype(at::kInt));
+  for (size_t i = 0; i < ts.size(); ++i)
+    for (int c = 0; c < ts[i]->Columns(); ++c) flags[off[i] + c] = ts[i]->column(c).nullable() ? 1 : 0;
+  at::Tensor g = flags.to(ts[0]->device());
+  ctx->GetCommunicator()->AllReduce(g, net::ReduceOp::MAX);
+  return to_host_vec(g.to(at::kLong));
+}
+
+// Posts one all-to-all per column buffer of `part` (rows already grouped by
+// destination rank, send_rows[r] rows for rank r) and returns without waiting.
+// nullable[c] is the cross-rank agreed nullability of column c.
+static PendingTable AllToAllPost(const TablePtr &part, const std::vector<int64_t> &send_rows,
+                                 const std::vector<int64_t> &recv_rows, const std::vector<int64_t> &nullable) {
   PendingTable pt;
   auto ctx = part->GetContext();
   pt.ctx = ctx;
   auto comm = ctx->GetCommunicator();
   const int world = ctx->GetWorldSize();
-  if (world == 1 || !ctx->IsDistributed()) {
-    pt.passthrough = part;
-    return pt;
-  }
-  const size_t P = counts.size();
-
-  // rows per destination rank (partition-major order keeps each rank contiguous)
-  std::vector<int64_t> send_rows(world, 0);
-  for (size_t i = 0; i < P; ++i) {
-    const size_t target = (P == (size_t)world) ? i : i * world / P;
-    send_rows[target] += counts[i];
-  }
-  std::vector<int64_t> recv_rows = comm->ExchangeCounts(send_rows);
   for (auto r : recv_rows) pt.total += r;
-
-  // schema-level nullability must agree across ranks
-  const int ncols = part->Columns();
-  at::Tensor flags = at::zeros({std::max(ncols, 1)}, at::TensorOptions().dtype(at::kInt));
-  for (int c = 0; c < ncols; ++c) flags[c] = part->column(c).nullable() ? 1 : 0;
-  at::Tensor gflags = flags.to(part->device());
-  comm->AllReduce(gflags, net::ReduceOp::MAX);
-  std::vector<int64_t> nullable = to_host_vec(gflags.to(at::kLong));
-
   Exec ex(part->device());
   auto post = [&](const at::Tensor &t, const std::vector<int64_t> &sc, const std::vector<int64_t> &rc) {
     auto r = comm->AllToAllVAsync(t, sc, rc);
     pt.reqs.push_back(r.second);
     return r.first;
   };
-  for (int c = 0; c < ncols; ++c) {
+  for (int c = 0; c < part->Columns(); ++c) {
     const Column &col = part->column(c);
     PendingTable::Col pc;
     pc.src = &col;
@@ -103,7 +104,27 @@ static PendingTable AllToAllBegin(const TablePtr &part, const std::vector<int64_
     }
     pt.cols.push_back(pc);
   }
+  pt.keep = part;
   return pt;
+}
+
+static PendingTable AllToAllBegin(const TablePtr &part, const std::vector<int64_t> &counts) {
+  auto ctx = part->GetContext();
+  const int world = ctx->GetWorldSize();
+  if (world == 1 || !ctx->IsDistributed()) {
+    PendingTable pt;
+    pt.passthrough = part;
+    return pt;
+  }
+  const size_t P = counts.size();
+  // rows per destination rank (partition-major order keeps each rank contiguous)
+  std::vector<int64_t> send_rows(world, 0);
+  for (size_t i = 0; i < P; ++i) {
+    const size_t target = (P == (size_t)world) ? i : i * world / P;
+    send_rows[target] += counts[i];
+  }
+  std::vector<int64_t> recv_rows = ctx->GetCommunicator()->ExchangeCounts(send_rows);
+  return AllToAllPost(part, send_rows, recv_rows, agree_nullability({part}));
 }
 
 static TablePtr AllToAllFinish(PendingTable &pt) {
@@ -173,6 +194,108 @@ std::pair<TablePtr, TablePtr> ShufflePair(const TablePtr &a, const std::vector<i
   TablePtr oa = AllToAllFinish(pa), ob = AllToAllFinish(pb);
   trace::add_counter("shuffle.rows_out", oa->Rows() + ob->Rows());
   return {oa, ob};
+}
+
+}  // namespace ops
+}  // namespace cylon
+
+namespace cylon {
+namespace ops {
+
+// Pipelined shuffle of two relations in K hash-disjoint chunks.
+//
+// Rows are partitioned once into W*K partitions with the reference's partition
+// hash h (pid = h % (W*K) = W*chunk + rank, chunk = (h / W) % K), so the rank
+// a row goes to is h % W exactly as in the unchunked shuffle, and a chunk is a
+// contiguous, rank-grouped row range of the reordered table.  The counts of
+// every chunk and both tables are exchanged in one all-to-all, then every
+// chunk's column all-to-alls are posted at once: RCCL runs them back to back on
+// its own stream while `consume(k, a_k, b_k)` processes chunk k on the compute
+// stream as soon as chunk k has landed (the request waits are stream waits on
+// RCCL, not host blocks), so the local work on chunk k overlaps the xGMI
+// transfer of chunks k+1..K-1.  Equal keys hash to the same chunk, which makes
+// any per-key operator (join of every type, set ops) chunk-separable.
+// Fixed-width columns only (var-width columns would need a synchronous byte
+// count exchange per chunk).
+void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,
+                        const std::vector<int> &bcols, int chunks,
+                        const std::function<void(int, const TablePtr &, const TablePtr &)> &consume) {
+  auto ctx = a->GetContext();
+  const int W = ctx->GetWorldSize();
+  const int K = std::max(1, chunks);
+  for (const TablePtr &t : {a, b})
+    for (const auto &c : t->columns())
+      CYLON_CHECK(!c.is_var(), Code::Invalid, "chunked shuffle supports fixed-width columns only");
+  const uint32_t P = (uint32_t)W * (uint32_t)K;
+  std::pair<TablePtr, std::vector<int64_t>> ra, rb;
+  {
+    CYLON_PHASE("shuffle.partition", a->device());
+    ra = PartitionReorder(a, hash_pids(a, acols, P), P);
+    rb = PartitionReorder(b, hash_pids(b, bcols, P), P);
+  }
+  if (W == 1 || !ctx->IsDistributed()) {
+    int64_t oa = 0, ob = 0;
+    for (int k = 0; k < K; ++k) {
+      const int64_t na = ra.second[k], nb = rb.second[k];
+      consume(k, Slice(ra.first, oa, na), Slice(rb.first, ob, nb));
+      oa += na;
+      ob += nb;
+    }
+    return;
+  }
+  auto comm = ctx->GetCommunicator();
+  // one count exchange for all chunks of both tables: block r = [a chunks 0..K-1, b chunks 0..K-1]
+  std::vector<int64_t> sendc((size_t)W * 2 * K), recvc;
+  for (int r = 0; r < W; ++r)
+    for (int k = 0; k < K; ++k) {
+      sendc[(size_t)r * 2 * K + k] = ra.second[(size_t)k * W + r];
+      sendc[(size_t)r * 2 * K + K + k] = rb.second[(size_t)k * W + r];
+    }
+  {
+    at::Tensor s = at::tensor(sendc, at::TensorOptions().dtype(at::kLong)).to(a->device());
+    std::vector<int64_t> per(W, 2 * K);
+    recvc = to_host_vec(comm->AllToAllV(s, per, per));
+  }
+  const std::vector<int64_t> nullable = agree_nullability({ra.first, rb.first});
+  const std::vector<int64_t> na_flags(nullable.begin(), nullable.begin() + a->Columns());
+  const std::vector<int64_t> nb_flags(nullable.begin() + a->Columns(), nullable.end());
+
+  std::vector<PendingTable> pa(K), pb(K);
+  {
+    CYLON_PHASE("shuffle.post", a->device());
+    int64_t oa = 0, ob = 0;
+    for (int k = 0; k < K; ++k) {
+      std::vector<int64_t> sa(W), sb(W), qa(W), qb(W);
+      int64_t ta = 0, tb = 0;
+      for (int r = 0; r < W; ++r) {
+        sa[r] = ra.second[(size_t)k * W + r];
+        sb[r] = rb.second[(size_t)k * W + r];
+        qa[r] = recvc[(size_t)r * 2 * K + k];
+        qb[r] = recvc[(size_t)r * 2 * K + K + k];
+        ta += sa[r];
+        tb += sb[r];
+      }
+      pa[k] = AllToAllPost(Slice(ra.first, oa, ta), sa, qa, na_flags);
+      pb[k] = AllToAllPost(Slice(rb.first, ob, tb), sb, qb, nb_flags);
+      oa += ta;
+      ob += tb;
+    }
+  }
+  trace::add_counter("shuffle.rows_in", a->Rows() + b->Rows());
+  trace::add_counter("shuffle.bytes_in", a->nbytes() + b->nbytes());
+  trace::add_counter("shuffle.chunks", K);
+  for (int k = 0; k < K; ++k) {
+    TablePtr ta, tb;
+    {
+      CYLON_PHASE("shuffle.wait", a->device());
+      ta = AllToAllFinish(pa[k]);
+      tb = AllToAllFinish(pb[k]);
+    }
+    pa[k] = PendingTable();
+    pb[k] = PendingTable();
+    trace::add_counter("shuffle.rows_out", ta->Rows() + tb->Rows());
+    consume(k, ta, tb);
+  }
 }
 
 }  // namespace ops

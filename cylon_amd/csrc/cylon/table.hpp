@@ -7,6 +7,7 @@
 // Operators in namespace cylon::ops throw CylonError; the Status-returning
 // reference-shaped API lives in api.hpp.
 #pragma once
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -91,6 +92,11 @@ TablePtr Shuffle(const TablePtr &t, const std::vector<int> &hash_cols);
 // shuffle two tables with the second one's partitioning overlapped with the first's transfer
 std::pair<TablePtr, TablePtr> ShufflePair(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,
                                           const std::vector<int> &bcols);
+// pipelined shuffle of two tables in `chunks` hash-disjoint chunks: consume(k, a_k, b_k) runs
+// on chunk k while the transfers of the later chunks are still in flight (fixed-width columns)
+void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,
+                        const std::vector<int> &bcols, int chunks,
+                        const std::function<void(int, const TablePtr &, const TablePtr &)> &consume);
 
 // ---- relational -----------------------------------------------------------
 TablePtr Join(const TablePtr &left, const TablePtr &right, const join::config::JoinConfig &cfg);

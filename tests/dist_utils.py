@@ -16,15 +16,16 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, fn, args, q):
+def _worker(rank, world, port, fn, args, q, device="cpu", env=None):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
                        "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    os.environ.update(env or {})
     try:
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         if root not in sys.path:
             sys.path.insert(0, root)
         from cylon_amd import CylonContext, GlooConfig
-        ctx = CylonContext(config=GlooConfig(), distributed=True, device="cpu")
+        ctx = CylonContext(config=GlooConfig(), distributed=True, device=device)
         try:
             res = fn(ctx, *args)
         finally:
@@ -34,12 +35,15 @@ def _worker(rank, world, port, fn, args, q):
         q.put((rank, False, traceback.format_exc()))
 
 
-def run_distributed(fn, world: int, *args, timeout: float = 240.0):
-    """Run fn(ctx, *args) on `world` gloo ranks; returns the list of per-rank results."""
+def run_distributed(fn, world: int, *args, timeout: float = 240.0, device: str = "cpu", env=None):
+    """Run fn(ctx, *args) on `world` gloo ranks; returns the list of per-rank results.
+
+    device="cuda:0" puts every rank's tables on the (single) GPU of the box while the
+    collectives go over gloo: the device kernels of the multi-rank paths run for real."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, q, device, env)) for r in range(world)]
     for p in procs:
         p.start()
     results = {}

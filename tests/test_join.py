@@ -127,3 +127,45 @@ def test_distributed_join_all_types(how):
     b = pd.concat([r[2] for r in res])
     ref = _oracle(a, b, how, ["k"], ["k"])
     assert _canon(got) == _canon(ref[got.columns])
+
+
+def _golden_join_chunked(ctx, data_dir, algorithm, chunks):
+    ctx.add_config("shuffle_chunks", str(chunks))
+    return _golden_join(ctx, data_dir, algorithm)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("chunks", [2, 3])
+def test_distributed_join_chunked_golden(data_dir, world, chunks):
+    """Pipelined (chunked) shuffle: every rank ends with exactly the reference's per-rank join rows."""
+    res = run_distributed(_golden_join_chunked, world, data_dir, "hash", chunks)
+    for ok, got, exp in res:
+        assert ok, f"rows got={got} expected={exp}"
+
+
+def _dist_chunked_vs_oracle(ctx, how, algorithm, chunks):
+    ctx.add_config("shuffle_chunks", str(chunks))
+    rank = ctx.get_rank()
+    rng = np.random.default_rng(300 + rank)
+    a = pd.DataFrame({"k": rng.integers(0, 60, 400), "x": rng.integers(0, 9, 400).astype(np.int32),
+                      "f": rng.random(400)})
+    a.loc[a.index % 7 == 0, "f"] = np.nan  # nullable payload
+    b = pd.DataFrame({"k": rng.integers(0, 60, 300), "v": rng.random(300)})
+    from cylon_amd._lib import C
+    C.trace_enable(True)
+    out = Table.from_pandas(ctx, a).distributed_join(Table.from_pandas(ctx, b), how, algorithm, on=["k"],
+                                                     left_prefix="l_", right_prefix="r_")
+    assert C.trace_counters().get("shuffle.chunks") == chunks
+    C.trace_enable(False)
+    return out.to_pandas(), a, b
+
+
+@pytest.mark.parametrize("how", JOIN_TYPES)
+@pytest.mark.parametrize("algorithm", ["hash", "sort"])
+def test_distributed_join_chunked_all_types(how, algorithm):
+    res = run_distributed(_dist_chunked_vs_oracle, 2, how, algorithm, 4)
+    got = pd.concat([r[0] for r in res])
+    a = pd.concat([r[1] for r in res])
+    b = pd.concat([r[2] for r in res])
+    ref = _oracle(a, b, how, ["k"], ["k"])
+    assert _canon(got) == _canon(ref[got.columns])

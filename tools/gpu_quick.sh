@@ -1,0 +1,12 @@
+# Quick GPU validation: pytest -m gpu, smoke, default bench.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest exit $rc" >> gpurun_out/pytest_gpu.log; tail -8 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
+tail -2 gpurun_out/smoke.log
+timeout -k 10 600 python bench.py > gpurun_out/bench_default.log 2>&1 || exit 1
+grep '^{' gpurun_out/bench_default.log

@@ -1,0 +1,61 @@
+"""Per-rank compute of the N-GPU headline join, simulated on one GPU.
+
+For world W each rank holds rows/W rows per relation.  This times, on one
+MI355X, what one rank does outside the RCCL transfer: the shuffle's hash
+partition + partition-major reorder of both relations, and the local join of
+the received rows (≈ rows/W per relation).  Usage: python tools/rank_sim.py [rows] [W ...]
+"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cylon_amd import CylonContext, Table  # noqa: E402
+from cylon_amd._lib import C  # noqa: E402
+
+rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000_000
+worlds = [int(x) for x in sys.argv[2:]] or [2, 4, 8]
+ctx = CylonContext(device="cuda:0")
+hi = int(0.99 * rows)
+
+
+def rel(n, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return Table.from_torch(ctx, {"k": torch.randint(0, hi, (n,), generator=g, device="cuda"),
+                                  **{f"v{i}": torch.rand(n, generator=g, device="cuda", dtype=torch.float64)
+                                     for i in range(3)}})
+
+
+def timed(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    best = 1e9
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        r = fn()
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+        del r
+    return best * 1e3
+
+
+for W in worlds:
+    n = rows // W
+    L, R = rel(n, 1), rel(n, 2)
+
+    def part():
+        outs = []
+        for t in (L, R):
+            pid, counts = C.map_to_hash_partitions(t.native, [0], W)
+            outs.append(C.partition_reorder(t.native, pid, W))
+        return outs
+
+    tp = timed(part)
+    tj = timed(lambda: L.join(R, "inner", "hash", on=[0]))
+    nbytes = 2 * n * 32 * (W - 1) / W
+    print(f"W={W} rows/rank={n}: partition+reorder(both) {tp:.1f} ms, local join {tj:.1f} ms, "
+          f"bytes sent/rank {nbytes / 1e9:.2f} GB", flush=True)
+    del L, R
+    torch.cuda.empty_cache()
