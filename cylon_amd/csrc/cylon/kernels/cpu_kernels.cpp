@@ -401,6 +401,7 @@ void sort_keys_from_column(const ColView &c, const int64_t *perm, int64_t n, boo
                                       : ((bits & 0x7c00ull) == 0x7c00ull && (bits & 0x03ffull));
       if (nan) k = mask;
     }
+    if (c.valid != nullptr && c.valid[s] == 0) k = mask;  // nulls: constant image (see sort.hip)
     out[i] = k;
   }
 }
@@ -481,7 +482,7 @@ void sort_string_chunk_keys(const ColView &c, const int64_t *perm, int64_t n, in
         k = (k << 8) | (p < len ? (uint64_t)c.data[b + p] : 0ull);
       }
     }
-    out[i] = desc ? ~k : k;
+    out[i] = (c.valid != nullptr && c.valid[s] == 0) ? ~0ull : (desc ? ~k : k);  // nulls: constant image
   }
 }
 

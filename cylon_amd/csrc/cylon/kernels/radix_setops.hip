@@ -1,0 +1,246 @@
+// LDS radix distinct for set operations and unique (K10, gfx950).
+//
+// Reference behaviour: cpp/src/cylon/table.cpp:531-721 (Union / Subtract /
+// Intersect insert row indices into a row-hash set with full-row equality;
+// output = first occurrences in input order, left rows before right rows) and
+// :923-999 (Unique keep first / last over a column subset).
+//
+// MI355X design (no sort, no global hash table):
+//   1. k_so_hash: one pass per table writes a 64-bit row hash (NaN / -0.0 /
+//      null canonicalised so that equal rows hash equal) and the global row id
+//      (left rows 0..nl-1, right rows nl..n-1).
+//   2. the (hash, row id) pairs are radix-partitioned by the top bits of
+//      fmix64(hash) with the LDS-staged passes of radix_join.hip (16 bytes per
+//      row move, not the table), so a partition's distinct hashes fit one LDS
+//      table.  The passes are stable: inside a partition row ids ascend.
+//   3. k_so_dedup, one partition per workgroup: phase 1 inserts every hash into
+//      an LDS open-addressing table (64-bit LDS CAS) and folds the partition-local
+//      position into the slot's representative (LDS atomicMin = first
+//      occurrence, atomicMax = last) and the side flags (left / right row seen);
+//      phase 2 revisits the rows: a row that is not its slot's representative is
+//      compared column by column with the representative (random reads, one per
+//      duplicate row); an unequal pair is a 64-bit hash collision and flags the
+//      whole call for the exact fallback.  Each row's keep decision is written
+//      to a byte mask indexed by row id only where it differs from the mask's
+//      initial value (union: drop duplicates; subtract: drop left rows that
+//      repeat or occur on the right; intersect: keep first left rows that occur
+//      on the right), so mostly-distinct unions cost no scattered writes.
+//      The count of such exceptions lets the host skip the compaction.
+//   4. the host compacts the mask (ascending row ids = the reference's output
+//      order) and gathers the surviving rows.
+#include "device_common.hpp"
+
+namespace cylon {
+namespace hip {
+
+constexpr int kSOThreads = 512;
+constexpr int kSOSlots = 4096;      // LDS table: 16 B per slot -> 64 KB, two workgroups per CU
+constexpr int64_t kSORowsPerPart = 1750;
+
+struct SOColSet {
+  ColView c[kMaxFusedCols];
+};
+
+// value hash with the equality semantics of value_equal (hash_join.hip): null ==
+// null, NaN == NaN (any payload), -0.0 == 0.0
+__device__ __forceinline__ uint64_t so_value_hash(const ColView &c, int64_t i) {
+  if (c.valid != nullptr && c.valid[i] == 0) return 0x5bd1e9955bd1e995ULL;
+  if (c.kind == static_cast<int>(ValueKind::VAR_BYTES)) {
+    const int64_t b = c.offsets[i], e = c.offsets[i + 1];
+    const uint32_t h1 = hashing::murmur3_32(c.data + b, e - b, 0u);
+    const uint32_t h2 = hashing::murmur3_32(c.data + b, e - b, 0x9747b28cu);
+    return ((uint64_t)h1 << 32) ^ h2 ^ (uint64_t)(e - b);
+  }
+  if (c.kind == static_cast<int>(ValueKind::FIXED_BYTES)) {
+    const uint32_t h1 = hashing::murmur3_32(c.data + i * (int64_t)c.width, c.width, 0u);
+    const uint32_t h2 = hashing::murmur3_32(c.data + i * (int64_t)c.width, c.width, 0x9747b28cu);
+    return ((uint64_t)h1 << 32) ^ h2;
+  }
+  uint64_t bits = (uint64_t)extend_bits(load_bits(c.data, i, c.width), c.width, c.kind);
+  if (c.kind == static_cast<int>(ValueKind::FLOAT)) {
+    bool nan = false;
+    if (c.width == 8) nan = __longlong_as_double((long long)bits) != __longlong_as_double((long long)bits);
+    else if (c.width == 4) nan = __int_as_float((int)bits) != __int_as_float((int)bits);
+    else if (c.width == 2) nan = ((bits & 0x7c00u) == 0x7c00u) && (bits & 0x3ffu);
+    if (nan) bits = 0x7ff8000000000000ull;
+  }
+  return hashing::fmix64(bits);
+}
+
+__global__ void k_so_hash(SOColSet cols, int ncols, int64_t n, int64_t base, uint64_t *__restrict__ h,
+                          int64_t *__restrict__ rowid) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint64_t x = 0x84222325cbf29ce4ULL;
+    for (int c = 0; c < ncols; ++c) x = hashing::combine64(x, so_value_hash(cols.c[c], i));
+    h[base + i] = x | 1ull;  // 0 marks an empty LDS slot
+    rowid[base + i] = base + i;
+  }
+}
+
+void setop_row_hash(const ColView *cols, int ncols, int64_t n, int64_t base, uint64_t *h, int64_t *rowid,
+                    void *stream) {
+  if (n == 0) return;
+  CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "set operation over " << ncols << " columns");
+  SOColSet s;
+  for (int c = 0; c < ncols; ++c) s.c[c] = cols[c];
+  hipLaunchKernelGGL(k_so_hash, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), s, ncols, n, base, h, rowid);
+  HIP_LAUNCH_CHECK();
+}
+
+int64_t setop_rows_per_part() { return kSORowsPerPart; }
+
+__device__ __forceinline__ bool so_value_equal(const ColView &a, int64_t i, const ColView &b, int64_t j) {
+  const bool va = a.valid == nullptr || a.valid[i] != 0;
+  const bool vb = b.valid == nullptr || b.valid[j] != 0;
+  if (!va || !vb) return va == vb;
+  if (a.kind == static_cast<int>(ValueKind::VAR_BYTES)) {
+    const int64_t ab = a.offsets[i], al = a.offsets[i + 1] - ab;
+    const int64_t bb = b.offsets[j], bl = b.offsets[j + 1] - bb;
+    if (al != bl) return false;
+    for (int64_t k = 0; k < al; ++k)
+      if (a.data[ab + k] != b.data[bb + k]) return false;
+    return true;
+  }
+  if (a.kind == static_cast<int>(ValueKind::FIXED_BYTES)) {
+    for (int k = 0; k < a.width; ++k)
+      if (a.data[i * a.width + k] != b.data[j * a.width + k]) return false;
+    return true;
+  }
+  const int64_t x = extend_bits(load_bits(a.data, i, a.width), a.width, a.kind);
+  const int64_t y = extend_bits(load_bits(b.data, j, b.width), b.width, b.kind);
+  if (a.kind == static_cast<int>(ValueKind::FLOAT)) {
+    if (a.width == 8) {
+      const double dx = __longlong_as_double(x), dy = __longlong_as_double(y);
+      return dx == dy || (dx != dx && dy != dy);
+    }
+    if (a.width == 4) {
+      const float fx = __int_as_float((int)x), fy = __int_as_float((int)y);
+      return fx == fy || (fx != fx && fy != fy);
+    }
+    if (a.width == 2) {
+      const bool nx = ((x & 0x7c00) == 0x7c00) && (x & 0x3ff), ny = ((y & 0x7c00) == 0x7c00) && (y & 0x3ff);
+      return nx ? ny : (!ny && x == y);
+    }
+  }
+  return x == y;
+}
+
+__device__ __forceinline__ bool so_rows_equal(const SOColSet &L, const SOColSet &R, int ncols, int64_t nl,
+                                              int64_t a, int64_t b) {
+  const SOColSet &A = a < nl ? L : R;
+  const SOColSet &B = b < nl ? L : R;
+  const int64_t ia = a < nl ? a : a - nl, ib = b < nl ? b : b - nl;
+  for (int c = 0; c < ncols; ++c)
+    if (!so_value_equal(A.c[c], ia, B.c[c], ib)) return false;
+  return true;
+}
+
+enum SOOp : int { SO_DISTINCT = 0, SO_SUBTRACT = 1, SO_INTERSECT = 2 };
+
+// slot of hash h (claims one in phase 1); -1 if the table is full
+template <bool kInsert>
+__device__ __forceinline__ int so_slot(unsigned long long *keys, uint64_t h) {
+  uint32_t s = (uint32_t)h & (kSOSlots - 1);
+  for (int probes = 0; probes < kSOSlots; ++probes) {
+    const unsigned long long cur = keys[s];
+    if (cur == h) return (int)s;
+    if (cur == 0ull) {
+      if (!kInsert) return -1;
+      const unsigned long long prev = atomicCAS(&keys[s], 0ull, (unsigned long long)h);
+      if (prev == 0ull || prev == h) return (int)s;
+    }
+    s = (s + 1) & (kSOSlots - 1);
+  }
+  return -1;
+}
+
+__global__ __launch_bounds__(kSOThreads) void k_so_dedup(const uint64_t *__restrict__ ph,
+                                                         const int64_t *__restrict__ prow,
+                                                         const int64_t *__restrict__ offs, int64_t nparts,
+                                                         int64_t nl, int op, int keep_last, SOColSet L, SOColSet R,
+                                                         int ncols, uint8_t *__restrict__ mask,
+                                                         unsigned long long *exc, int *bad) {
+  __shared__ unsigned long long keys[kSOSlots];
+  __shared__ uint32_t rep[kSOSlots];
+  __shared__ uint32_t side[kSOSlots];
+  __shared__ int sbad;
+  const uint32_t rep_init = keep_last ? 0u : 0xffffffffu;
+  for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
+    const int64_t rb = offs[p], re = offs[p + 1];
+    if (rb == re) continue;
+    __syncthreads();  // previous partition done with the table
+    for (int s = threadIdx.x; s < kSOSlots; s += blockDim.x) {
+      keys[s] = 0ull;
+      rep[s] = rep_init;
+      side[s] = 0u;
+    }
+    if (threadIdx.x == 0) sbad = 0;
+    __syncthreads();
+    // phase 1: insert, fold representative position and side flags
+    for (int64_t r = rb + threadIdx.x; r < re; r += blockDim.x) {
+      const uint64_t h = ph[r];
+      const int s = so_slot<true>(keys, h);
+      if (s < 0) {
+        sbad = 1;
+        continue;
+      }
+      const uint32_t local = (uint32_t)(r - rb);
+      if (keep_last) atomicMax(&rep[s], local);
+      else atomicMin(&rep[s], local);
+      atomicOr(&side[s], prow[r] < nl ? 1u : 2u);
+    }
+    __syncthreads();
+    if (sbad) {
+      if (threadIdx.x == 0) atomicExch(bad, 1);
+      continue;
+    }
+    // phase 2: verify duplicates against their representative, write mask exceptions
+    for (int64_t r = rb + threadIdx.x; r < re; r += blockDim.x) {
+      const uint64_t h = ph[r];
+      const int s = so_slot<false>(keys, h);
+      const uint32_t local = (uint32_t)(r - rb);
+      const int64_t row = prow[r];
+      const bool first = rep[s] == local;
+      if (!first && !so_rows_equal(L, R, ncols, nl, row, prow[rb + rep[s]])) atomicExch(bad, 1);  // collision
+      bool flip = false;
+      if (op == SO_DISTINCT) {
+        flip = !first;  // default keep
+        if (flip) mask[row] = 0;
+      } else if (row < nl) {
+        const bool on_right = (side[s] & 2u) != 0;
+        if (op == SO_SUBTRACT) {
+          flip = !(first && !on_right);  // default keep
+          if (flip) mask[row] = 0;
+        } else {
+          flip = first && on_right;  // default drop
+          if (flip) mask[row] = 1;
+        }
+      }
+      const uint64_t b = __ballot(flip);
+      if (lane_id() == 0 && b) atomicAdd(exc, (unsigned long long)__popcll(b));
+    }
+  }
+}
+
+void setop_dedup(const uint64_t *ph, const int64_t *prow, const int64_t *offs, int64_t nparts, int64_t nl, int op,
+                 bool keep_last, const ColView *lcols, const ColView *rcols, int ncols, uint8_t *mask, int64_t *exc,
+                 int *bad, void *stream) {
+  hipStream_t s = as_stream(stream);
+  HIP_CHECK(hipMemsetAsync(exc, 0, sizeof(int64_t), s));
+  HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(int), s));
+  if (nparts == 0) return;
+  CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "set operation over " << ncols << " columns");
+  SOColSet L, R;
+  for (int c = 0; c < ncols; ++c) {
+    L.c[c] = lcols[c];
+    R.c[c] = rcols ? rcols[c] : lcols[c];
+  }
+  const int grid = (int)std::min<int64_t>(nparts, (int64_t)kNumCUs * 2 * 8);
+  hipLaunchKernelGGL(k_so_dedup, dim3(grid), dim3(kSOThreads), 0, s, ph, prow, offs, nparts, nl, op,
+                     keep_last ? 1 : 0, L, R, ncols, mask, reinterpret_cast<unsigned long long *>(exc), bad);
+  HIP_LAUNCH_CHECK();
+}
+
+}  // namespace hip
+}  // namespace cylon

@@ -60,6 +60,9 @@ __global__ void k_sort_keys(ColView c, const int64_t *__restrict__ perm, int64_t
     uint64_t k = order_image(bits, c.width, c.kind);
     if (desc) k = ~k & mask;
     if (c.kind == static_cast<int>(ValueKind::FLOAT) && is_nan_bits(bits, c.width)) k = mask;  // NaN last
+    // a null's image is a constant: null rows keep their order from the previous (less
+    // significant) sort columns, so equal rows stay adjacent in multi-column sorts
+    if (c.valid != nullptr && c.valid[s] == 0) k = mask;
     out[i] = k;
   }
 }
@@ -235,7 +238,7 @@ __global__ void k_string_chunk_keys(ColView c, const int64_t *__restrict__ perm,
         k = (k << 8) | (p < len ? (uint64_t)c.data[b + p] : 0ull);
       }
     }
-    out[i] = desc ? ~k : k;
+    out[i] = (c.valid != nullptr && c.valid[s] == 0) ? ~0ull : (desc ? ~k : k);  // nulls: constant image
   }
 }
 

@@ -15,6 +15,7 @@
 #include <limits>
 
 #include "relational.hpp"
+#include "../trace.hpp"
 #include "util.hpp"
 
 namespace cylon {
@@ -30,8 +31,96 @@ static void verify_schema(const TablePtr &l, const TablePtr &r) {
   CYLON_CHECK(same_schema(l, r), Code::Invalid, "set operation: tables must have the same schema");
 }
 
+// ---------------------------------------------------------------------------
+// K10 LDS radix distinct (radix_setops.hip): device path of union / subtract /
+// intersect / unique for large inputs.  The surviving rows keep the reference's
+// order (ascending row ids, left before right).  Returns nullptr when not
+// eligible or when the kernel reports an LDS overflow / hash collision (the
+// exact sort-based path then runs).
+// ---------------------------------------------------------------------------
+enum class SetOp { UNION, SUBTRACT, INTERSECT };
+
+static int64_t radix_setop_min_rows() {
+  const char *e = std::getenv("CYLON_RADIX_SETOP_MIN_ROWS");  // tuning / test knob
+  return e ? std::atoll(e) : (int64_t(1) << 20);
+}
+
+// rows il of l followed by rows ir of r in one table (fixed-width columns: one
+// output allocation, two gather launches)
+static TablePtr gather_two(const TablePtr &l, const at::Tensor &il, const TablePtr &r, const at::Tensor &ir) {
+  bool fixed = true;
+  for (const auto &c : l->columns()) fixed &= !c.is_var();
+  if (!fixed) return Merge({GatherNullable(l, il, false), GatherNullable(r, ir, false)});
+  Exec ex(l->device());
+  const int64_t kl = il.numel(), kr = ir.numel();
+  std::vector<Column> out;
+  std::vector<ColView> lin, rin;
+  std::vector<MutColView> lo, ro;
+  for (int c = 0; c < l->Columns(); ++c) {
+    const Column &a = l->column(c), &b = r->column(c);
+    Column o = make_fixed_column(a.name, a.type, kl + kr, ex.device, a.nullable() || b.nullable());
+    MutColView m;
+    m.data = kl + kr ? reinterpret_cast<uint8_t *>(o.data.data_ptr()) : nullptr;
+    m.valid = o.validity.defined() ? ptr<uint8_t>(o.validity) : nullptr;
+    m.width = a.type.width();
+    m.kind = static_cast<int>(a.type.kind());
+    lo.push_back(m);
+    if (m.data) m.data += kl * m.width;
+    if (m.valid) m.valid += kl;
+    ro.push_back(m);
+    lin.push_back(a.view());
+    rin.push_back(b.view());
+    out.push_back(std::move(o));
+  }
+  if (kl) KCALL(ex, gather_columns, lin.data(), lo.data(), (int)lin.size(), ptr<int64_t>(il), kl);
+  if (kr) KCALL(ex, gather_columns, rin.data(), ro.data(), (int)rin.size(), ptr<int64_t>(ir), kr);
+  return Table::Make(l->GetContext(), std::move(out));
+}
+
+static TablePtr radix_distinct(const TablePtr &l, const TablePtr &r, const std::vector<int> &cols, SetOp op,
+                               bool keep_last) {
+  if (!l->device().is_cuda()) return nullptr;
+  const int64_t nl = l->Rows(), nr = r ? r->Rows() : 0, n = nl + nr;
+  const int ncols = (int)cols.size();
+  if (n < radix_setop_min_rows() || ncols < 1 || ncols > kMaxFusedCols) return nullptr;
+  Exec ex(l->device());
+  CYLON_PHASE("setop.radix", ex.device);
+  std::vector<ColView> lv = views(l, cols), rv = r ? views(r, cols) : lv;
+  at::Tensor h = ex.empty_i64(n), rid = ex.empty_i64(n);
+  hip::setop_row_hash(lv.data(), ncols, nl, 0, reinterpret_cast<uint64_t *>(ptr<int64_t>(h)), ptr<int64_t>(rid),
+                      ex.stream);
+  if (nr) hip::setop_row_hash(rv.data(), ncols, nr, nl, reinterpret_cast<uint64_t *>(ptr<int64_t>(h)),
+                              ptr<int64_t>(rid), ex.stream);
+  int bits = 0;
+  while ((n >> bits) > hip::setop_rows_per_part()) ++bits;
+  at::Tensor offs;
+  std::vector<at::Tensor> pr = RadixPartition(ex, {h, rid}, {8, 8}, bits, &offs);
+  h = rid = at::Tensor();
+  const int opi = op == SetOp::UNION ? 0 : (op == SetOp::SUBTRACT ? 1 : 2);
+  const int64_t mlen = op == SetOp::UNION ? n : nl;
+  at::Tensor mask = op == SetOp::INTERSECT ? ex.zeros_u8(mlen) : at::ones({mlen}, ex.opts(at::kByte));
+  at::Tensor exc = ex.empty_i64(1);
+  at::Tensor bad = at::empty({1}, ex.opts(at::kInt));
+  hip::setop_dedup(reinterpret_cast<const uint64_t *>(ptr<int64_t>(pr[0])), ptr<int64_t>(pr[1]), ptr<int64_t>(offs),
+                   int64_t(1) << bits, nl, opi, keep_last, lv.data(), r ? rv.data() : nullptr, ncols,
+                   ptr<uint8_t>(mask), ptr<int64_t>(exc), bad.data_ptr<int>(), ex.stream);
+  pr.clear();
+  if (bad.item<int>() != 0) {
+    trace::add_counter("setop.radix.fallback", 1);
+    return nullptr;
+  }
+  const int64_t e = exc.item<int64_t>();
+  trace::add_counter("setop.radix.exceptions", e);
+  if (op == SetOp::UNION && e == 0) return r ? Merge({l, r}) : Slice(l, 0, nl);  // every row distinct
+  if (op == SetOp::SUBTRACT && e == 0) return Slice(l, 0, nl);
+  if (!r || op != SetOp::UNION) return GatherNullable(l, MaskToIndices(mask), false);
+  return gather_two(l, MaskToIndices(mask.slice(0, 0, nl)), r, MaskToIndices(mask.slice(0, nl, n)));
+}
+
 TablePtr Unique(const TablePtr &t, const std::vector<int> &cols, bool keep_first) {
   if (t->Rows() == 0) return t;
+  if (TablePtr out = radix_distinct(t, nullptr, cols.empty() ? all_cols(t) : cols, SetOp::UNION, !keep_first))
+    return out;
   Exec ex(t->device());
   GroupInfo gi = GroupIds(t, cols.empty() ? all_cols(t) : cols);
   at::Tensor keep = gi.first_rows;
@@ -54,10 +143,9 @@ TablePtr DistributedUnique(const TablePtr &t, const std::vector<int> &cols, bool
   return Unique(Shuffle(t, c), c, keep_first);
 }
 
-enum class SetOp { UNION, SUBTRACT, INTERSECT };
-
 static TablePtr set_op(const TablePtr &l, const TablePtr &r, SetOp op) {
   verify_schema(l, r);
+  if (TablePtr out = radix_distinct(l, r, all_cols(l), op, false)) return out;
   TablePtr m = Merge({l, r});
   if (m->Rows() == 0) return m;
   Exec ex(m->device());

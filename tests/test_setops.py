@@ -99,3 +99,19 @@ def test_distributed_set_ops_vs_sets():
     assert _set(s) == _set(a) - _set(b) and len(s) == len(_set(s))
     assert _set(i) == _set(a) & _set(b) and len(i) == len(_set(i))
     assert sorted(q["x"].tolist()) == sorted(a["x"].unique().tolist())
+
+
+def test_unique_and_sort_with_nulls_over_varying_payload(ctx):
+    """Null entries whose underlying buffer values differ are still equal (and adjacent in
+    multi-column sorts): nulls get a constant sort image."""
+    import numpy as np
+    import pyarrow as pa
+    from cylon_amd import Table
+    f = pa.array([0.5, 1.25, 0.5, 7.0, 2.0], mask=np.array([True, False, False, True, False]))
+    t = Table(pa.table({"f": f, "i": pa.array([1, 2, 1, 1, 2], pa.int32())}), ctx)
+    assert t.unique(None).to_pydict() == {"f": [None, 1.25, 0.5, 2.0], "i": [1, 2, 1, 2]}
+    s = t.sort(["f", "i"]).to_pydict()
+    assert s == {"f": [0.5, 1.25, 2.0, None, None], "i": [1, 2, 2, 1, 1]}
+    u = Table(pa.table({"f": pa.array([3.0], type=pa.float64(), mask=np.array([True])), "i": pa.array([1], pa.int32())}), ctx)
+    assert t.union(u).row_count == 4
+    assert t.subtract(u).to_pydict() == {"f": [1.25, 0.5, 2.0], "i": [2, 1, 2]}

@@ -5,6 +5,8 @@
   4. hash groupby + sum, 1B rows / 10M int64 groups (whole problem on one GPU, and
      the 125M-row per-GPU share of the 8-GPU config)
   5. radix sort of 2B int64 rows (whole problem on one GPU, and the 250M per-GPU share)
+  6. union of two join-shaped relations (the reference's second headline chart)
+  7. the headline join with the sort algorithm
 
 Prints one JSON line per config.  Synthetic data generated in HBM (CSV files for 1).
 Usage: python tools/bench_suite.py [--configs 1,2,4,5] [--reps 3] [--scale 1.0]
@@ -122,6 +124,45 @@ def cfg5(reps, scale):
         del t
 
 
+def cfg6(reps, scale):
+    """Reference headline #2 (docs/src/pages/index.js:118-134): union of two relations of the
+    join benchmark's shape (int64 key + 3 float64), distinct rows, on one GPU."""
+    ctx = CylonContext(device="cuda:0")
+    for n in (int(200_000_000 * scale), int(1_000_000_000 * scale)):
+        hi = int(0.99 * n)
+        L = Table.from_torch(ctx, rel(n, hi, 1, ["float64"] * 3))
+        R = Table.from_torch(ctx, rel(n, hi, 2, ["float64"] * 3))
+        out = {}
+
+        def run():
+            out["rows"] = L.distributed_union(R).row_count
+
+        med, ts = timed(run, reps)
+        emit(config="6: union (distinct rows), int64 key + 3 float64, one GPU", n=n, ms=med * 1e3,
+             rows_per_s=2 * n / med, rows_out=out["rows"], all_ms=[x * 1e3 for x in ts])
+        del L, R
+        torch.cuda.empty_cache()
+
+
+def cfg7(reps, scale):
+    """The join benchmark with the reference's sort algorithm (arch.md reports sort times for w >= 2)."""
+    ctx = CylonContext(device="cuda:0")
+    for n in (int(200_000_000 * scale), int(1_000_000_000 * scale)):
+        hi = int(0.99 * n)
+        L = Table.from_torch(ctx, rel(n, hi, 1, ["float64"] * 3))
+        R = Table.from_torch(ctx, rel(n, hi, 2, ["float64"] * 3))
+        out = {}
+
+        def run():
+            out["rows"] = L.distributed_join(R, "inner", "sort", on=[0]).row_count
+
+        med, ts = timed(run, reps)
+        emit(config="7: sort-algorithm inner join, int64 key + 3 float64, one GPU", n=n, ms=med * 1e3,
+             rows_per_s=2 * n / med, rows_out=out["rows"], all_ms=[x * 1e3 for x in ts])
+        del L, R
+        torch.cuda.empty_cache()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="1,2,4,5")
@@ -130,7 +171,8 @@ def main():
     a = ap.parse_args()
     for c in a.configs.split(","):
         {"1": lambda: cfg1(a.reps), "2": lambda: cfg2(a.reps, a.scale), "4": lambda: cfg4(a.reps, a.scale),
-         "5": lambda: cfg5(a.reps, a.scale)}[c.strip()]()
+         "5": lambda: cfg5(a.reps, a.scale), "6": lambda: cfg6(a.reps, a.scale),
+         "7": lambda: cfg7(a.reps, a.scale)}[c.strip()]()
         torch.cuda.empty_cache() if torch.cuda.is_available() else None
 
 
