@@ -450,31 +450,10 @@ TablePtr Join(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg
   return join_local(left, right, cfg, nullptr);
 }
 
-// Number of hash chunks of the pipelined distributed join (identical on every
-// rank: config / environment, or the global row count).  Context config
-// "shuffle_chunks" (or CYLON_SHUFFLE_CHUNKS) forces a value; by default device
-// tables with >= 2^24 rows per rank per relation are shuffled in 4 chunks, so
-// that three quarters of the local join overlap the RCCL transfer.
-static int join_shuffle_chunks(const TablePtr &left, const TablePtr &right) {
-  auto ctx = left->GetContext();
-  for (const TablePtr &t : {left, right})
-    for (const auto &c : t->columns())
-      if (c.is_var()) return 1;
-  std::string v = ctx->GetConfig("shuffle_chunks", "");
-  if (v.empty())
-    if (const char *e = std::getenv("CYLON_SHUFFLE_CHUNKS")) v = e;
-  if (!v.empty()) return std::max(1, std::min(64, std::atoi(v.c_str())));
-  if (!left->device().is_cuda()) return 1;
-  at::Tensor rows = at::tensor({std::min(left->Rows(), right->Rows())},
-                               at::TensorOptions().dtype(at::kLong)).to(left->device());
-  ctx->GetCommunicator()->AllReduce(rows, net::ReduceOp::MIN);
-  return rows.item<int64_t>() >= (int64_t(1) << 24) ? 4 : 1;
-}
-
 TablePtr DistributedJoin(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
   auto ctx = left->GetContext();
   if (ctx->GetWorldSize() == 1) return Join(left, right, cfg);
-  const int K = join_shuffle_chunks(left, right);
+  const int K = ShuffleChunks(left, right);
   if (K > 1) {
     JoinSink sink;
     sink.chunks_total = K;

@@ -170,6 +170,13 @@ static TablePtr dist_set_op(const TablePtr &l, const TablePtr &r, SetOp op) {
   auto ctx = l->GetContext();
   if (ctx->GetWorldSize() == 1) return set_op(l, r, op);
   const auto cols = all_cols(l);
+  const int K = ShuffleChunks(l, r);
+  if (K > 1) {  // chunk k's local set operation overlaps the transfer of the later chunks
+    std::vector<TablePtr> parts;
+    ShufflePairChunked(l, cols, r, cols, K,
+                       [&](int, const TablePtr &a, const TablePtr &b) { parts.push_back(set_op(a, b, op)); });
+    return Merge(parts);
+  }
   auto lr = ShufflePair(l, cols, r, cols);
   return set_op(lr.first, lr.second, op);
 }

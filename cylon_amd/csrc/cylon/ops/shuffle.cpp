@@ -11,6 +11,20 @@
 namespace cylon {
 namespace ops {
 
+// partition ids + per-partition row counts (device tensor)
+static std::pair<at::Tensor, at::Tensor> hash_pids_counts(const TablePtr &t, const std::vector<int> &cols,
+                                                          uint32_t nparts) {
+  Exec ex(t->device());
+  const int64_t n = t->Rows();
+  std::vector<ColView> v = views(t, cols);
+  at::Tensor h = ex.empty_u32(n);
+  at::Tensor pid = ex.empty_u32(n);
+  at::Tensor counts = ex.empty_i64(nparts);
+  KCALL(ex, row_partition_hash, v.data(), (int)v.size(), n, ptr<uint32_t>(h));
+  KCALL(ex, hash_to_partition, ptr<uint32_t>(h), n, nparts, ptr<uint32_t>(pid), ptr<int64_t>(counts));
+  return {pid, counts};
+}
+
 static at::Tensor hash_pids(const TablePtr &t, const std::vector<int> &cols, uint32_t nparts) {
   Exec ex(t->device());
   const int64_t n = t->Rows();
@@ -202,6 +216,26 @@ std::pair<TablePtr, TablePtr> ShufflePair(const TablePtr &a, const std::vector<i
 namespace cylon {
 namespace ops {
 
+// Number of hash chunks for a pipelined binary operator (identical on every
+// rank: config / environment, or the global row count).  Context config
+// "shuffle_chunks" (or CYLON_SHUFFLE_CHUNKS) forces a value; by default device
+// tables with >= 2^24 rows per rank per relation are shuffled in 4 chunks, so
+// that three quarters of the local operator overlap the RCCL transfer.
+int ShuffleChunks(const TablePtr &a, const TablePtr &b) {
+  auto ctx = a->GetContext();
+  for (const TablePtr &t : {a, b})
+    for (const auto &c : t->columns())
+      if (c.is_var()) return 1;
+  std::string v = ctx->GetConfig("shuffle_chunks", "");
+  if (v.empty())
+    if (const char *e = std::getenv("CYLON_SHUFFLE_CHUNKS")) v = e;
+  if (!v.empty()) return std::max(1, std::min(64, std::atoi(v.c_str())));
+  if (!a->device().is_cuda() || ctx->GetWorldSize() == 1) return 1;
+  at::Tensor rows = at::tensor({std::min(a->Rows(), b->Rows())}, at::TensorOptions().dtype(at::kLong)).to(a->device());
+  ctx->GetCommunicator()->AllReduce(rows, net::ReduceOp::MIN);
+  return rows.item<int64_t>() >= (int64_t(1) << 24) ? 4 : 1;
+}
+
 // Pipelined shuffle of two relations in K hash-disjoint chunks.
 //
 // Rows are partitioned once into W*K partitions with the reference's partition
@@ -227,13 +261,9 @@ void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const 
     for (const auto &c : t->columns())
       CYLON_CHECK(!c.is_var(), Code::Invalid, "chunked shuffle supports fixed-width columns only");
   const uint32_t P = (uint32_t)W * (uint32_t)K;
-  std::pair<TablePtr, std::vector<int64_t>> ra, rb;
-  {
-    CYLON_PHASE("shuffle.partition", a->device());
-    ra = PartitionReorder(a, hash_pids(a, acols, P), P);
-    rb = PartitionReorder(b, hash_pids(b, bcols, P), P);
-  }
   if (W == 1 || !ctx->IsDistributed()) {
+    auto ra = PartitionReorder(a, hash_pids(a, acols, P), P);
+    auto rb = PartitionReorder(b, hash_pids(b, bcols, P), P);
     int64_t oa = 0, ob = 0;
     for (int k = 0; k < K; ++k) {
       const int64_t na = ra.second[k], nb = rb.second[k];
@@ -244,41 +274,57 @@ void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const 
     return;
   }
   auto comm = ctx->GetCommunicator();
-  // one count exchange for all chunks of both tables: block r = [a chunks 0..K-1, b chunks 0..K-1]
+  // partition ids and counts of both tables first (cheap), so that one count exchange
+  // serves every chunk and b's reorder can run while a's first chunk is on the wire
+  std::pair<at::Tensor, at::Tensor> ha, hb;
+  {
+    CYLON_PHASE("shuffle.partition", a->device());
+    ha = hash_pids_counts(a, acols, P);
+    hb = hash_pids_counts(b, bcols, P);
+  }
+  const std::vector<int64_t> ca = to_host_vec(ha.second), cb = to_host_vec(hb.second);
+  // block r of the exchange = [a chunks 0..K-1, b chunks 0..K-1] for rank r
   std::vector<int64_t> sendc((size_t)W * 2 * K), recvc;
   for (int r = 0; r < W; ++r)
     for (int k = 0; k < K; ++k) {
-      sendc[(size_t)r * 2 * K + k] = ra.second[(size_t)k * W + r];
-      sendc[(size_t)r * 2 * K + K + k] = rb.second[(size_t)k * W + r];
+      sendc[(size_t)r * 2 * K + k] = ca[(size_t)k * W + r];
+      sendc[(size_t)r * 2 * K + K + k] = cb[(size_t)k * W + r];
     }
   {
     at::Tensor s = at::tensor(sendc, at::TensorOptions().dtype(at::kLong)).to(a->device());
     std::vector<int64_t> per(W, 2 * K);
     recvc = to_host_vec(comm->AllToAllV(s, per, per));
   }
-  const std::vector<int64_t> nullable = agree_nullability({ra.first, rb.first});
+  const std::vector<int64_t> nullable = agree_nullability({a, b});
   const std::vector<int64_t> na_flags(nullable.begin(), nullable.begin() + a->Columns());
   const std::vector<int64_t> nb_flags(nullable.begin() + a->Columns(), nullable.end());
 
   std::vector<PendingTable> pa(K), pb(K);
+  std::vector<int64_t> offa(K + 1, 0), offb(K + 1, 0);
+  auto post = [&](const TablePtr &part, const std::vector<int64_t> &cnt, int side, int k,
+                  const std::vector<int64_t> &flags, std::vector<int64_t> &off) -> PendingTable {
+    std::vector<int64_t> sc(W), rc(W);
+    int64_t tot = 0;
+    for (int r = 0; r < W; ++r) {
+      sc[r] = cnt[(size_t)k * W + r];
+      rc[r] = recvc[(size_t)r * 2 * K + side * K + k];
+      tot += sc[r];
+    }
+    off[k + 1] = off[k] + tot;
+    return AllToAllPost(Slice(part, off[k], tot), sc, rc, flags);
+  };
+  TablePtr pta, ptb;
   {
-    CYLON_PHASE("shuffle.post", a->device());
-    int64_t oa = 0, ob = 0;
-    for (int k = 0; k < K; ++k) {
-      std::vector<int64_t> sa(W), sb(W), qa(W), qb(W);
-      int64_t ta = 0, tb = 0;
-      for (int r = 0; r < W; ++r) {
-        sa[r] = ra.second[(size_t)k * W + r];
-        sb[r] = rb.second[(size_t)k * W + r];
-        qa[r] = recvc[(size_t)r * 2 * K + k];
-        qb[r] = recvc[(size_t)r * 2 * K + K + k];
-        ta += sa[r];
-        tb += sb[r];
-      }
-      pa[k] = AllToAllPost(Slice(ra.first, oa, ta), sa, qa, na_flags);
-      pb[k] = AllToAllPost(Slice(rb.first, ob, tb), sb, qb, nb_flags);
-      oa += ta;
-      ob += tb;
+    CYLON_PHASE("shuffle.reorder+post", a->device());
+    pta = PartitionReorder(a, ha.first, P).first;
+    ha = {};
+    pa[0] = post(pta, ca, 0, 0, na_flags, offa);  // a's chunk 0 transfers while b is reordered
+    ptb = PartitionReorder(b, hb.first, P).first;
+    hb = {};
+    pb[0] = post(ptb, cb, 1, 0, nb_flags, offb);
+    for (int k = 1; k < K; ++k) {
+      pa[k] = post(pta, ca, 0, k, na_flags, offa);
+      pb[k] = post(ptb, cb, 1, k, nb_flags, offb);
     }
   }
   trace::add_counter("shuffle.rows_in", a->Rows() + b->Rows());

@@ -94,6 +94,8 @@ std::pair<TablePtr, TablePtr> ShufflePair(const TablePtr &a, const std::vector<i
                                           const std::vector<int> &bcols);
 // pipelined shuffle of two tables in `chunks` hash-disjoint chunks: consume(k, a_k, b_k) runs
 // on chunk k while the transfers of the later chunks are still in flight (fixed-width columns)
+// chunk count for ShufflePairChunked (same on every rank; 1 = unchunked)
+int ShuffleChunks(const TablePtr &a, const TablePtr &b);
 void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,
                         const std::vector<int> &bcols, int chunks,
                         const std::function<void(int, const TablePtr &, const TablePtr &)> &consume);

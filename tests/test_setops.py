@@ -78,8 +78,14 @@ def test_unique_with_nulls_and_strings(ctx):
     assert len(got) == 3
 
 
-def _dist_set_ops(ctx):
+def _numeric(df):
+    return df.assign(s=df["s"].str[1:].astype(np.int64))
+
+
+def _dist_set_ops(ctx, numeric=False):
     a, b = _frames()
+    if numeric:
+        a, b = _numeric(a), _numeric(b)
     r = ctx.get_rank()
     a = a.iloc[r::ctx.get_world_size()]
     b = b.iloc[r::ctx.get_world_size()]
@@ -88,9 +94,22 @@ def _dist_set_ops(ctx):
             ta.distributed_intersect(tb).to_pandas(), ta.distributed_unique(["x"]).to_pandas())
 
 
-def test_distributed_set_ops_vs_sets():
+def _dist_set_ops_chunked(ctx):
+    from cylon_amd._lib import C
+    ctx.add_config("shuffle_chunks", "3")
+    C.trace_enable(True)
+    out = _dist_set_ops(ctx, numeric=True)
+    assert C.trace_counters().get("shuffle.chunks", 0) >= 3
+    C.trace_enable(False)
+    return out
+
+
+@pytest.mark.parametrize("chunked", [False, True])
+def test_distributed_set_ops_vs_sets(chunked):
     a, b = _frames()
-    res = run_distributed(_dist_set_ops, 3)
+    if chunked:
+        a, b = _numeric(a), _numeric(b)
+    res = run_distributed(_dist_set_ops_chunked if chunked else _dist_set_ops, 3)
     u = pd.concat([r[0] for r in res])
     s = pd.concat([r[1] for r in res])
     i = pd.concat([r[2] for r in res])
