@@ -486,5 +486,13 @@ void sort_string_chunk_keys(const ColView &c, const int64_t *perm, int64_t n, in
   }
 }
 
+void narrow_i64(const int64_t *in, int64_t n, int64_t base, uint32_t *out, void *) {
+  for (int64_t i = 0; i < n; ++i) out[i] = (uint32_t)((uint64_t)in[i] - (uint64_t)base);
+}
+
+void widen_u32(const uint32_t *in, int64_t n, int64_t base, int64_t *out, void *) {
+  for (int64_t i = 0; i < n; ++i) out[i] = (int64_t)((uint64_t)base + in[i]);
+}
+
 }  // namespace cpu
 }  // namespace cylon

@@ -311,5 +311,65 @@ void gather_var_bytes(const ColView &in, const int64_t *idx, int64_t m, const in
   HIP_LAUNCH_CHECK();
 }
 
+// ---------------------------------------------------------------------------
+// shuffle wire narrowing (int64 <-> uint32 offsets from a global base): two
+// rows per thread with 16-byte accesses of the wide side when aligned
+// ---------------------------------------------------------------------------
+template <bool kVec>
+__global__ void k_narrow_i64(const int64_t *__restrict__ in, int64_t n, int64_t base, uint32_t *__restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (kVec) {
+    for (int64_t i = t0; i < (n >> 1); i += stride) {
+      const longlong2 v = reinterpret_cast<const longlong2 *>(in)[i];
+      reinterpret_cast<uint2 *>(out)[i] =
+          make_uint2((uint32_t)((uint64_t)v.x - (uint64_t)base), (uint32_t)((uint64_t)v.y - (uint64_t)base));
+    }
+    if ((n & 1) && t0 == 0) out[n - 1] = (uint32_t)((uint64_t)in[n - 1] - (uint64_t)base);
+  } else {
+    for (int64_t i = t0; i < n; i += stride) out[i] = (uint32_t)((uint64_t)in[i] - (uint64_t)base);
+  }
+}
+
+template <bool kVec>
+__global__ void k_widen_u32(const uint32_t *__restrict__ in, int64_t n, int64_t base, int64_t *__restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (kVec) {
+    for (int64_t i = t0; i < (n >> 1); i += stride) {
+      const uint2 v = reinterpret_cast<const uint2 *>(in)[i];
+      longlong2 o;
+      o.x = (long long)((uint64_t)base + v.x);
+      o.y = (long long)((uint64_t)base + v.y);
+      reinterpret_cast<longlong2 *>(out)[i] = o;
+    }
+    if ((n & 1) && t0 == 0) out[n - 1] = (int64_t)((uint64_t)base + in[n - 1]);
+  } else {
+    for (int64_t i = t0; i < n; i += stride) out[i] = (int64_t)((uint64_t)base + in[i]);
+  }
+}
+
+void narrow_i64(const int64_t *in, int64_t n, int64_t base, uint32_t *out, void *stream) {
+  if (n == 0) return;
+  const bool vec = reinterpret_cast<uintptr_t>(in) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 8 == 0;
+  if (vec)
+    hipLaunchKernelGGL(k_narrow_i64<true>, dim3(grid_for((n + 1) / 2)), dim3(kBlock), 0, as_stream(stream), in, n,
+                       base, out);
+  else
+    hipLaunchKernelGGL(k_narrow_i64<false>, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), in, n, base, out);
+  HIP_LAUNCH_CHECK();
+}
+
+void widen_u32(const uint32_t *in, int64_t n, int64_t base, int64_t *out, void *stream) {
+  if (n == 0) return;
+  const bool vec = reinterpret_cast<uintptr_t>(in) % 8 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0;
+  if (vec)
+    hipLaunchKernelGGL(k_widen_u32<true>, dim3(grid_for((n + 1) / 2)), dim3(kBlock), 0, as_stream(stream), in, n,
+                       base, out);
+  else
+    hipLaunchKernelGGL(k_widen_u32<false>, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), in, n, base, out);
+  HIP_LAUNCH_CHECK();
+}
+
 }  // namespace hip
 }  // namespace cylon

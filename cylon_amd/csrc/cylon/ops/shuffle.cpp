@@ -5,6 +5,8 @@
 // shuffle_table_by_hashing), arrow/arrow_all_to_all.cpp (per-buffer header +
 // payload protocol).  Partition -> rank mapping is identical: partition i goes
 // to rank i when P == world, else to rank i*world/P (table.cpp:89-106).
+#include <limits>
+
 #include "util.hpp"
 #include "../trace.hpp"
 
@@ -49,7 +51,99 @@ struct PendingTable {
   std::vector<std::shared_ptr<net::P2PRequest>> reqs;
   TablePtr keep;         // the sent table (its buffers must outlive the posted transfers)
   TablePtr passthrough;  // world 1
+  std::vector<int64_t> wire_base;  // per column: narrowed on the wire (see WirePlan) -> base, else unset
+  std::vector<bool> wire_narrow;
+  std::vector<DataType> wire_type;  // original column types
 };
+
+// Wire format of a shuffled table: 8-byte signed integer columns whose global
+// value range fits 32 bits travel as uint32 offsets from the global minimum
+// (frame of reference), so e.g. the headline join's int64 key costs 4 of the
+// 32 bytes a row puts on xGMI instead of 8; the receiver widens them back.
+// Config "shuffle_narrow" = "0" (or CYLON_SHUFFLE_NARROW=0) turns it off.
+struct WirePlan {
+  std::vector<bool> narrow;
+  std::vector<int64_t> base;
+  bool any() const {
+    for (bool b : narrow)
+      if (b) return true;
+    return false;
+  }
+};
+
+static bool narrow_candidate(const Column &c) {
+  return !c.is_var() && c.type.kind() == ValueKind::SIGNED_INT && c.type.width() == 8 &&
+         c.data.scalar_type() == at::kLong;
+}
+
+static std::vector<WirePlan> plan_wire(const std::vector<TablePtr> &ts) {
+  std::vector<WirePlan> plans(ts.size());
+  for (size_t i = 0; i < ts.size(); ++i) {
+    plans[i].narrow.assign(ts[i]->Columns(), false);
+    plans[i].base.assign(ts[i]->Columns(), 0);
+  }
+  auto ctx = ts[0]->GetContext();
+  std::string v = ctx->GetConfig("shuffle_narrow", "");
+  if (v.empty())
+    if (const char *e = std::getenv("CYLON_SHUFFLE_NARROW")) v = e;
+  if (v == "0") return plans;
+  std::vector<std::pair<size_t, int>> cand;
+  for (size_t i = 0; i < ts.size(); ++i)
+    for (int c = 0; c < ts[i]->Columns(); ++c)
+      if (narrow_candidate(ts[i]->column(c))) cand.push_back({i, c});
+  if (cand.empty()) return plans;
+  const at::Device dev = ts[0]->device();
+  std::vector<at::Tensor> lo, hi;
+  for (auto &ic : cand) {
+    const Column &c = ts[ic.first]->column(ic.second);
+    if (c.length == 0) {
+      lo.push_back(at::full({1}, std::numeric_limits<int64_t>::max(), at::TensorOptions().dtype(at::kLong).device(dev)));
+      hi.push_back(at::full({1}, std::numeric_limits<int64_t>::min(), at::TensorOptions().dtype(at::kLong).device(dev)));
+    } else {
+      auto mm = at::aminmax(c.data.slice(0, 0, c.length));
+      lo.push_back(std::get<0>(mm).reshape({1}));
+      hi.push_back(std::get<1>(mm).reshape({1}));
+    }
+  }
+  at::Tensor mins = at::cat(lo), maxs = at::cat(hi);
+  auto comm = ctx->GetCommunicator();
+  comm->AllReduce(mins, net::ReduceOp::MIN);
+  comm->AllReduce(maxs, net::ReduceOp::MAX);
+  const std::vector<int64_t> hmin = to_host_vec(mins), hmax = to_host_vec(maxs);
+  for (size_t j = 0; j < cand.size(); ++j) {
+    if (hmax[j] < hmin[j]) continue;  // no rows anywhere
+    if ((uint64_t)hmax[j] - (uint64_t)hmin[j] > 0xffffffffull) continue;
+    plans[cand[j].first].narrow[cand[j].second] = true;
+    plans[cand[j].first].base[cand[j].second] = hmin[j];
+    trace::add_counter("shuffle.narrowed_columns", 1);
+  }
+  return plans;
+}
+
+// narrowed columns replaced by int32-stored offsets (same names)
+static TablePtr to_wire(const TablePtr &t, const WirePlan &p) {
+  if (!p.any()) return t;
+  Exec ex(t->device());
+  std::vector<Column> cols;
+  for (int c = 0; c < t->Columns(); ++c) {
+    const Column &col = t->column(c);
+    if (!p.narrow[c]) {
+      cols.push_back(col);
+      continue;
+    }
+    at::Tensor w = at::empty({col.length}, ex.opts(at::kInt));
+    KCALL(ex, narrow_i64, ptr<int64_t>(col.data), col.length, p.base[c], reinterpret_cast<uint32_t *>(ptr<int32_t>(w)));
+    cols.emplace_back(col.name, DataType(Type::UINT32), col.length, w, at::Tensor(), col.validity);
+  }
+  return Table::Make(t->GetContext(), std::move(cols));
+}
+
+static void attach_plan(PendingTable &pt, const TablePtr &orig, const WirePlan &p) {
+  if (!p.any()) return;
+  pt.wire_narrow = p.narrow;
+  pt.wire_base = p.base;
+  for (const auto &c : orig->columns()) pt.wire_type.push_back(c.type);
+}
 
 // schema-level nullability of every column, agreed across ranks (one all-reduce
 // for any number of tables with the same column count)
@@ -138,16 +232,27 @@ static PendingTable AllToAllBegin(const TablePtr &part, const std::vector<int64_
     send_rows[target] += counts[i];
   }
   std::vector<int64_t> recv_rows = ctx->GetCommunicator()->ExchangeCounts(send_rows);
-  return AllToAllPost(part, send_rows, recv_rows, agree_nullability({part}));
+  const std::vector<int64_t> nullable = agree_nullability({part});
+  const WirePlan plan = plan_wire({part})[0];
+  PendingTable pt = AllToAllPost(to_wire(part, plan), send_rows, recv_rows, nullable);
+  attach_plan(pt, part, plan);
+  return pt;
 }
 
 static TablePtr AllToAllFinish(PendingTable &pt) {
   if (pt.passthrough) return pt.passthrough;
   for (auto &r : pt.reqs) r->Wait();
   std::vector<Column> out;
-  for (auto &pc : pt.cols) {
+  for (size_t c = 0; c < pt.cols.size(); ++c) {
+    auto &pc = pt.cols[c];
     const Column &col = *pc.src;
-    if (!col.is_var()) {
+    if (!pt.wire_narrow.empty() && pt.wire_narrow[c]) {  // widen back to int64
+      Exec ex(pc.data.device());
+      at::Tensor w = ex.empty_i64(pt.total);
+      KCALL(ex, widen_u32, reinterpret_cast<const uint32_t *>(ptr<int32_t>(pc.data)), pt.total, pt.wire_base[c],
+            ptr<int64_t>(w));
+      out.emplace_back(col.name, pt.wire_type[c], pt.total, w, at::Tensor(), pc.valid);
+    } else if (!col.is_var()) {
       out.emplace_back(col.name, col.type, pt.total, pc.data, at::Tensor(), pc.valid);
     } else {
       Exec ex(pc.rlens.device());
@@ -296,6 +401,7 @@ void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const 
     recvc = to_host_vec(comm->AllToAllV(s, per, per));
   }
   const std::vector<int64_t> nullable = agree_nullability({a, b});
+  const std::vector<WirePlan> plans = plan_wire({a, b});
   const std::vector<int64_t> na_flags(nullable.begin(), nullable.begin() + a->Columns());
   const std::vector<int64_t> nb_flags(nullable.begin() + a->Columns(), nullable.end());
 
@@ -311,15 +417,17 @@ void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const 
       tot += sc[r];
     }
     off[k + 1] = off[k] + tot;
-    return AllToAllPost(Slice(part, off[k], tot), sc, rc, flags);
+    PendingTable pt = AllToAllPost(Slice(part, off[k], tot), sc, rc, flags);
+    attach_plan(pt, side == 0 ? a : b, plans[side]);
+    return pt;
   };
   TablePtr pta, ptb;
   {
     CYLON_PHASE("shuffle.reorder+post", a->device());
-    pta = PartitionReorder(a, ha.first, P).first;
+    pta = to_wire(PartitionReorder(a, ha.first, P).first, plans[0]);
     ha = {};
     pa[0] = post(pta, ca, 0, 0, na_flags, offa);  // a's chunk 0 transfers while b is reordered
-    ptb = PartitionReorder(b, hb.first, P).first;
+    ptb = to_wire(PartitionReorder(b, hb.first, P).first, plans[1]);
     hb = {};
     pb[0] = post(ptb, cb, 1, 0, nb_flags, offb);
     for (int k = 1; k < K; ++k) {

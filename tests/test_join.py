@@ -169,3 +169,40 @@ def test_distributed_join_chunked_all_types(how, algorithm):
     b = pd.concat([r[2] for r in res])
     ref = _oracle(a, b, how, ["k"], ["k"])
     assert _canon(got) == _canon(ref[got.columns])
+
+
+def _narrow_join(ctx, chunks):
+    from cylon_amd._lib import C
+    ctx.add_config("shuffle_chunks", str(chunks))
+    rank = ctx.get_rank()
+    rng = np.random.default_rng(40 + rank)
+    n = 500
+    # key: negative, range < 2^32 (narrowed); w: range > 2^32 (not narrowed); z: nullable, narrowed
+    a = pd.DataFrame({"k": rng.integers(-2_000_000_000, -1_999_999_900, n),
+                      "w": rng.integers(-(1 << 60), 1 << 60, n),
+                      "z": pd.array(rng.integers(5, 50, n), dtype="Int64")})
+    a.loc[a.index % 5 == 0, "z"] = pd.NA
+    b = pd.DataFrame({"k": rng.integers(-2_000_000_000, -1_999_999_900, n // 2), "v": rng.random(n // 2)})
+    if rank == 1:
+        b = b.iloc[:0]  # an empty relation on one rank
+    C.trace_enable(True)
+    C.trace_reset()
+    out = Table.from_pandas(ctx, a).distributed_join(Table.from_pandas(ctx, b), "inner", "hash", on=["k"],
+                                                     left_prefix="l_", right_prefix="r_")
+    narrowed = C.trace_counters().get("shuffle.narrowed_columns", 0)
+    C.trace_enable(False)
+    return out.to_pandas(), a, b, narrowed
+
+
+@pytest.mark.parametrize("chunks", [1, 2])
+def test_distributed_join_narrowed_wire(chunks):
+    """int64 columns with a global range < 2^32 travel as uint32 offsets (negative values, nulls, an empty
+    rank); wider columns travel as is; the result is exact."""
+    res = run_distributed(_narrow_join, 2, chunks)
+    got = pd.concat([r[0] for r in res])
+    a = pd.concat([r[1] for r in res])
+    b = pd.concat([r[2] for r in res])
+    ref = _oracle(a, b, "inner", ["k"], ["k"])
+    assert len(got) == len(ref) > 0
+    assert _canon(got) == _canon(ref[got.columns])
+    assert all(r[3] == 3 for r in res)  # l.k, l.z, r.k (l.w spans > 2^32)
