@@ -35,7 +35,7 @@ namespace hip {
 
 constexpr int kSOThreads = 512;
 constexpr int kSOSlots = 4096;      // LDS table: 16 B per slot -> 64 KB, two workgroups per CU
-constexpr int64_t kSORowsPerPart = 1750;
+constexpr int64_t kSORowsPerPart = 2048;  // 2^20 partitions (two 10-bit passes) up to 2^31 rows
 
 struct SOColSet {
   ColView c[kMaxFusedCols];
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(kSOThreads) void k_so_dedup(const uint64_t *__restr
       const uint32_t local = (uint32_t)(r - rb);
       if (keep_last) atomicMax(&rep[s], local);
       else atomicMin(&rep[s], local);
-      atomicOr(&side[s], prow[r] < nl ? 1u : 2u);
+      if (op != SO_DISTINCT) atomicOr(&side[s], prow[r] < nl ? 1u : 2u);
     }
     __syncthreads();
     if (sbad) {
