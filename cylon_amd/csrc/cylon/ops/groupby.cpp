@@ -448,11 +448,6 @@ TablePtr DistributedHashGroupBy(const TablePtr &t, const std::vector<int> &keys,
     return HashGroupBy(sh, key_pos, remapped);
   }
 
-  // phase 1: local partial states
-  Exec ex(t->device());
-  GroupInfo gi = GroupIds(t, keys, false);
-  TablePtr kt = GatherNullable(Project(t, keys), gi.first_rows, false);
-  std::vector<Column> pcols = kt->columns();
   struct Plan {
     int op;
     int ddof;
@@ -461,6 +456,42 @@ TablePtr DistributedHashGroupBy(const TablePtr &t, const std::vector<int> &keys,
   };
   std::vector<Plan> plans;
   std::vector<AggSpec> combine;  // phase-2 aggregations over the state columns
+  TablePtr partial;
+
+  // phase 1, fast form: SUM / COUNT / MIN / MAX / MEAN over non-null value columns
+  // are their own partial states, so the local hash group-by produces them directly
+  // (the LDS radix group-by on device tables, radix_groupby.hip) instead of the
+  // global group-id path below.
+  bool simple_states = true;
+  for (const auto &a : aggs)
+    simple_states &= (a.op == AGG_SUM || a.op == AGG_COUNT || a.op == AGG_MIN || a.op == AGG_MAX ||
+                      a.op == AGG_MEAN) &&
+                     !t->column(a.col).nullable();
+  if (simple_states) {
+    std::vector<AggSpec> st;
+    for (const auto &a : aggs) {
+      Plan p{a.op, a.ddof, std::string(AggPrefix(a.op)) + t->column(a.col).name, {}};
+      auto add = [&](int op, int combine_op) {
+        const int pos = nk + (int)st.size();
+        st.push_back(AggSpec{a.col, op});
+        p.state_cols.push_back(pos);
+        combine.push_back(AggSpec{pos, combine_op});
+      };
+      if (a.op == AGG_MEAN) {
+        add(AGG_SUM, AGG_SUM);
+        add(AGG_COUNT, AGG_SUM);
+      } else {
+        add(a.op, a.op == AGG_COUNT ? AGG_SUM : a.op);
+      }
+      plans.push_back(std::move(p));
+    }
+    partial = HashGroupBy(t, keys, st);
+  } else {
+  // phase 1: local partial states
+  Exec ex(t->device());
+  GroupInfo gi = GroupIds(t, keys, false);
+  TablePtr kt = GatherNullable(Project(t, keys), gi.first_rows, false);
+  std::vector<Column> pcols = kt->columns();
   Acc acc{ex, gi.gid, t->Rows(), gi.ngroups};
   auto add_state = [&](Plan &p, Column c, int combine_op) {
     const int pos = (int)pcols.size();
@@ -497,7 +528,8 @@ TablePtr DistributedHashGroupBy(const TablePtr &t, const std::vector<int> &keys,
     }
     plans.push_back(std::move(p));
   }
-  TablePtr partial = Table::Make(t->GetContext(), std::move(pcols));
+  partial = Table::Make(t->GetContext(), std::move(pcols));
+  }  // generic phase 1
   // phase 2: shuffle partial rows by key, combine
   TablePtr sh = Shuffle(partial, key_pos);
   TablePtr comb = HashGroupBy(sh, key_pos, combine);
@@ -513,7 +545,7 @@ TablePtr DistributedHashGroupBy(const TablePtr &t, const std::vector<int> &keys,
         out.push_back(comb->column(ci++).with_name(p.name));
         break;
       case AGG_MEAN: {
-        at::Tensor s = comb->column(ci++).data, n = comb->column(ci++).data.to(at::kDouble);
+        at::Tensor s = comb->column(ci++).data.to(at::kDouble), n = comb->column(ci++).data.to(at::kDouble);
         out.push_back(double_col(p.name, s / n, n > 0));
         break;
       }

@@ -105,6 +105,28 @@ def test_distributed_groupby_vs_pandas(ops):
         _check(got, df, keys, "v", ops)
 
 
+def _dist_groupby_simple(ctx, keys):
+    df = _frame(20 + ctx.get_rank(), n=900, nulls=False)
+    t = Table.from_pandas(ctx, df)
+    ops = ["sum", "count", "min", "max", "mean"]
+    return t.groupby(keys, {"v": ops, "i": ["sum", "mean", "max"]}).to_pandas(), df
+
+
+@pytest.mark.parametrize("keys", [["k"], ["k", "s"]])
+def test_distributed_groupby_partial_states_fast_form(keys):
+    """SUM / COUNT / MIN / MAX / MEAN over non-null columns: the local group-by emits the
+    partial states directly (phase 1 fast form)."""
+    res = run_distributed(_dist_groupby_simple, 3, keys)
+    got = pd.concat([r[0] for r in res])
+    df = pd.concat([r[1] for r in res])
+    _check(got, df, keys, "v", ["sum", "count", "min", "max", "mean"])
+    exp = df.groupby(keys)["i"].agg(["sum", "mean", "max"]).reset_index()
+    m = got.merge(exp, on=keys)
+    assert len(m) == len(exp) == len(got)
+    assert (m["sum_i"] == m["sum"]).all() and (m["max_i"] == m["max"]).all()
+    np.testing.assert_allclose(m["mean_i"], m["mean"], rtol=1e-12)
+
+
 def _dist_aggs(ctx):
     rng = np.random.default_rng(ctx.get_rank())
     df = pd.DataFrame({"a": rng.integers(-50, 50, 100), "f": rng.random(100)})
