@@ -16,8 +16,12 @@ from .data.aggregates import AggregationOp
 from .data.table import SortOptions, Table
 from .frame import CylonEnv, DataFrame
 from .indexing.index import IndexingSchema
+from .io import CSVReadOptions, CSVWriteOptions, read_csv
 from .net import CommConfig, GlooConfig, MPIConfig, RCCLConfig
 from .series import Series
+
+Column = C.Column      # pycylon.data.column.Column
+DataType = C.DataType  # pycylon.data.data_type.DataType
 from .types import (binary, bool, date32, date64, decimal, double, duration, extension, fixed_sized_binary,  # noqa
                     fixed_sized_list, float, half_float, int8, int16, int32, int64, interval, list, string, time32,
                     time64, timestamp, uint8, uint16, uint32, uint64)
@@ -26,4 +30,5 @@ __version__ = "0.1.0"
 
 __all__ = ["C", "CylonError", "CylonContext", "Table", "DataFrame", "CylonEnv", "Series", "SortOptions",
            "JoinConfig", "JoinType", "JoinAlgorithm", "Status", "Code", "AggregationOp", "IndexingSchema",
-           "CommConfig", "GlooConfig", "MPIConfig", "RCCLConfig"]
+           "CommConfig", "GlooConfig", "MPIConfig", "RCCLConfig", "Column", "DataType", "read_csv",
+           "CSVReadOptions", "CSVWriteOptions"]

@@ -237,3 +237,94 @@ def unique_values(table, column=0) -> List[Any]:
 
 def nunique(table, column=0) -> int:
     return len(unique_values(table, column))
+
+
+# ---------------------------------------------------------------------------
+# Reference entry points (python/pycylon/data/compute.pyx), mapped onto the
+# device engine above.  Same names and argument order as pycylon.
+# ---------------------------------------------------------------------------
+def comparison_compute_op_iter(array, other, op):
+    """compute.pyx:78 — elementwise comparison of a 1-D array with a scalar."""
+    return np.asarray([op(x, other) for x in np.asarray(array)], dtype=bool)
+
+
+def comparison_compute_np_op(array, other, op):
+    """compute.pyx:108 — vectorised comparison of a numpy array with a scalar."""
+    return op(np.asarray(array), other)
+
+
+def table_compare_ar_op(table, other, op):
+    """compute.pyx:127 — comparison through the Arrow (host) engine."""
+    return binary_op(table, other, op, engine="arrow")
+
+
+def table_compare_np_op(table, other, op):
+    """compute.pyx:164 — the reference's numpy engine; here the device engine."""
+    return binary_op(table, other, op, engine="device")
+
+
+def table_compare_op(table, other, op, engine="arrow"):
+    """compute.pyx:198."""
+    return binary_op(table, other, op, engine=engine)
+
+
+def invert(table):
+    """compute.pyx:226 — logical not of bool columns (other types raise, as in the reference)."""
+    for c in table.native.columns():
+        if c.type.type != T.BOOL:
+            raise ValueError(f"Invert only support for bool types, but found {c.type}")
+    return unary_op(table, torch.logical_not, "invert")
+
+
+def neg(table):
+    """compute.pyx:246 — negation of numeric columns."""
+    return unary_op(table, torch.neg, "neg")
+
+
+def division_op(table, op, value):
+    """compute.pyx:267 — table / scalar (op: operator.truediv or operator.floordiv)."""
+    return binary_op(table, value, op)
+
+
+def math_op(table, op, value, engine="device"):
+    """compute.pyx:441 — table (+ - * /) scalar or table."""
+    return binary_op(table, value, op, engine="arrow" if engine == "arrow" else "device")
+
+
+def math_op_numpy(table, op, value):
+    """compute.pyx:299."""
+    return math_op(table, op, value, "numpy")
+
+
+def math_op_arrow(table, op, value):
+    """compute.pyx:347."""
+    return math_op(table, op, value, "arrow")
+
+
+def math_op_c_numpy(table, op, value):
+    """compute.pyx:373."""
+    return math_op(table, op, value, "numpy")
+
+
+def unique(table):
+    """compute.pyx:454 — per column, the number of distinct values (a one-row table)."""
+    from .table import Table
+    return Table.from_pydict(table.context, {name: [nunique(table, i)] for i, name in enumerate(table.column_names)})
+
+
+def compare_array_like_values(l_org_ar, l_cmp_ar, skip_null=True):
+    """compute.pyx:509 — membership of each value of l_org_ar in l_cmp_ar (pyarrow arrays)."""
+    return pc.is_in(l_org_ar, options=pc.SetLookupOptions(value_set=pa.array(l_cmp_ar), skip_nulls=skip_null))
+
+
+def drop_na(table, how: str, axis=0):
+    """compute.pyx:714."""
+    return table.dropna(axis=axis, how=how)
+
+
+def infer_map(table, func):
+    """compute.pyx:792 — func applied to every column as a numpy array; one output column each."""
+    from .table import Table
+    arrays = [pa.array(np.asarray(func(col.to_numpy(zero_copy_only=False))))
+              for col in table.to_arrow().combine_chunks().itercolumns()]
+    return Table.from_arrow(table.context, pa.Table.from_arrays(arrays, names=table.column_names))

@@ -179,8 +179,25 @@ def build_index(values, schema: IndexingSchema, device: str = "cpu") -> BaseInde
 
 
 class _Indexer:
-    def __init__(self, table):
-        self._t = table
+    """Row/column selector bound to a table.  Constructed with a table (``table.loc``) or,
+    like the reference's ``LocIndexer(indexing_schema)``, with a schema, in which case the
+    ``loc_with_*`` calls name the table explicitly."""
+
+    def __init__(self, table=None):
+        self._t = table if not isinstance(table, (IndexingSchema, int)) else None
+
+    def _on(self, table):
+        return type(self)(table) if table is not None else self
+
+    # reference API (python/pycylon/indexing/index.pyx LocIndexer / ILocIndexer)
+    def loc_with_single_column(self, indices, column_index, table=None):
+        return self._on(table)[indices, column_index]
+
+    def loc_with_multi_column(self, indices, column_list, table=None):
+        return self._on(table)[indices, list(column_list)]
+
+    def loc_with_range_column(self, indices, column_range, table=None):
+        return self._on(table)[indices, column_range]
 
     def _cols(self, cols) -> List[int]:
         t = self._t
@@ -241,5 +258,17 @@ class ILocIndexer(_Indexer):
         return self._select(pos, cols)
 
 
+class PyLocIndexer:
+    """Reference python/pycylon/indexing/index.pyx PyLocIndexer: ``PyLocIndexer(table, "loc" | "iloc")[rows, cols]``."""
+
+    def __init__(self, cn_table, mode):
+        if mode not in ("loc", "iloc"):
+            raise ValueError(f"unsupported indexing mode {mode}")
+        self._indexer = (LocIndexer if mode == "loc" else ILocIndexer)(cn_table)
+
+    def __getitem__(self, item):
+        return self._indexer[item]
+
+
 __all__ = ["IndexingSchema", "BaseIndex", "LinearIndex", "HashIndex", "RangeIndex", "build_index", "LocIndexer",
-           "ILocIndexer"]
+           "ILocIndexer", "PyLocIndexer"]

@@ -115,3 +115,19 @@ def test_dataframe_distributed_env():
     assert sorted(u["k"].tolist()) == sorted(l["k"].unique().tolist())
     g = pd.concat([x[3] for x in res]).sort_values("k")
     assert g["sum_x"].tolist() == l.groupby("k")["x"].sum().sort_index().tolist()
+
+
+def test_reference_indexer_entry_points(ctx):
+    """pycylon's LocIndexer.loc_with_* and PyLocIndexer entry points."""
+    import pyarrow as pa
+    from cylon_amd import Table
+    from cylon_amd.indexing import ILocIndexer, IndexingSchema, LocIndexer, PyLocIndexer
+    t = Table(pa.table({"a": [10, 20, 30, 40], "b": [1.0, 2.0, 3.0, 4.0], "c": ["w", "x", "y", "z"]}), ctx)
+    li = LocIndexer(IndexingSchema.LINEAR)
+    assert li.loc_with_single_column(slice(1, 2), "b", t).to_pydict() == {"b": [2.0, 3.0]}
+    assert li.loc_with_multi_column([0, 3], ["a", "c"], t).to_pydict() == {"a": [10, 40], "c": ["w", "z"]}
+    assert li.loc_with_range_column(slice(2, 3), slice("b", "c"), t).to_pydict() == {"b": [3.0, 4.0],
+                                                                                     "c": ["y", "z"]}
+    assert ILocIndexer(t).loc_with_single_column(slice(0, 2), 0).to_pydict() == {"a": [10, 20]}
+    assert PyLocIndexer(t, "iloc")[1:3, ["a"]].to_pydict() == {"a": [20, 30]}
+    assert PyLocIndexer(t, "loc")[2, "c"].to_pydict() == {"c": ["y"]}
