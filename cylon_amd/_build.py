@@ -35,11 +35,43 @@ def hip_sources():
     return sorted(glob.glob(os.path.join(KERNELS, "*.hip")))
 
 
+# sources compiled on their own as C++20 (the Arrow 25 C++ headers need it) and
+# linked as objects into the extension
+CXX20_SOURCES = [os.path.join(CSRC, "cylon", "io", "arrow_io.cpp")]
+
+
 def cpp_sources():
     srcs = [os.path.join(CSRC, "bindings.cpp"), os.path.join(CSRC, "bindings_ops.cpp"), os.path.join(CSRC, "capi.cpp")]
     for sub in ("cylon", "cylon/net", "cylon/ops", "cylon/ctx", "cylon/io", "cylon/kernels"):
         srcs += sorted(glob.glob(os.path.join(CSRC, sub, "*.cpp")))
-    return [os.path.relpath(s, ROOT) for s in srcs]
+    return [os.path.relpath(s, ROOT) for s in srcs if s not in CXX20_SOURCES]
+
+
+def compile_cxx20_objects(extra_includes):
+    """Compile CXX20_SOURCES with the host compiler against torch's and Arrow's headers."""
+    import torch
+    from torch.utils.cpp_extension import include_paths
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    digest = _headers_digest()
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    flags = ["-std=c++20", "-O2", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1",
+             "-DUSE_ROCM=1", "-Wno-unused-function"]
+    incs = [CSRC, ROCM_INCLUDE] + include_paths() + list(extra_includes)
+    objs = []
+    for src in CXX20_SOURCES:
+        obj = os.path.join(OBJ_DIR, os.path.splitext(os.path.basename(src))[0] + ".cxx20.o")
+        stamp = obj + ".stamp"
+        with open(src, "rb") as f:
+            key = hashlib.sha1(f.read() + digest.encode() + " ".join(flags + incs).encode()).hexdigest()
+        if not (os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read().strip() == key):
+            cmd = ["g++"] + flags + [x for i in incs for x in ("-I", i)] + ["-c", src, "-o", obj]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"g++ failed for {src}:\n{r.stderr[-6000:]}")
+            with open(stamp, "w") as f:
+                f.write(key)
+        objs.append(obj)
+    return objs
 
 
 def _headers_digest():

@@ -6,6 +6,7 @@
 #include <tuple>
 
 #include "cylon/api.hpp"
+#include "cylon/io/arrow_io.hpp"
 #include "cylon/io/csv.hpp"
 #include "cylon/ops/api_ext.hpp"
 #include "cylon/ops/graph.hpp"
@@ -78,6 +79,29 @@ void register_extended_ops(py::module &m) {
       },
       py::arg("table"), py::arg("path"), py::arg("delimiter") = ",",
       py::arg("column_names") = std::vector<std::string>{}, rel);
+
+  // ---- C25 native Parquet I/O (Arrow / Parquet C++ from pyarrow's libraries)
+  m.def(
+      "read_parquet",
+      [](const std::shared_ptr<CylonContext> &ctx, const std::vector<std::string> &paths,
+         const std::vector<std::string> &columns, bool use_threads, bool concurrent_file_reads) {
+        io::ParquetOptions o;
+        o.columns = columns;
+        o.use_threads = use_threads;
+        o.concurrent_file_reads = concurrent_file_reads;
+        return io::ReadParquets(ctx, paths, o);
+      },
+      py::arg("ctx"), py::arg("paths"), py::arg("columns") = std::vector<std::string>{},
+      py::arg("use_threads") = true, py::arg("concurrent_file_reads") = true, rel);
+  m.def(
+      "write_parquet",
+      [](const TablePtr &t, const std::string &path, const std::string &compression, int64_t chunk_size) {
+        io::ParquetOptions o;
+        o.compression = compression;
+        o.chunk_size = chunk_size;
+        io::WriteParquet(t, path, o);
+      },
+      py::arg("table"), py::arg("path"), py::arg("compression") = "snappy", py::arg("chunk_size") = 1 << 20, rel);
 
   py::enum_<AggOp>(m, "AggregationOp")
       .value("SUM", AGG_SUM).value("MIN", AGG_MIN).value("MAX", AGG_MAX).value("COUNT", AGG_COUNT)

@@ -21,6 +21,29 @@ Status guard(F &&f) {
 }
 }  // namespace
 
+Status FromCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &path, TablePtr &out,
+               const io::CSVReadOptions &options) {
+  return guard([&] { out = io::ReadCSV(ctx, path, options); });
+}
+Status FromCSV(const std::shared_ptr<CylonContext> &ctx, const std::vector<std::string> &paths,
+               std::vector<TablePtr> &out, const io::CSVReadOptions &options) {
+  return guard([&] { out = io::ReadCSVs(ctx, paths, options); });
+}
+Status WriteCSV(const TablePtr &t, const std::string &path, const io::CSVWriteOptions &options) {
+  return guard([&] { io::WriteCSV(t, path, options); });
+}
+Status FromParquet(const std::shared_ptr<CylonContext> &ctx, const std::string &path, TablePtr &out,
+                   const io::ParquetOptions &options) {
+  return guard([&] { out = io::ReadParquet(ctx, path, options); });
+}
+Status FromParquet(const std::shared_ptr<CylonContext> &ctx, const std::vector<std::string> &paths,
+                   std::vector<TablePtr> &out, const io::ParquetOptions &options) {
+  return guard([&] { out = io::ReadParquets(ctx, paths, options); });
+}
+Status WriteParquet(const TablePtr &t, const std::string &path, const io::ParquetOptions &options) {
+  return guard([&] { io::WriteParquet(t, path, options); });
+}
+
 Status Join(const TablePtr &l, const TablePtr &r, const join::config::JoinConfig &cfg, TablePtr &out) {
   return guard([&] { out = ops::Join(l, r, cfg); });
 }

@@ -13,6 +13,8 @@
 #include <string>
 #include <vector>
 
+#include "io/arrow_io.hpp"
+#include "io/csv.hpp"
 #include "ops/relational.hpp"
 #include "table.hpp"
 
@@ -54,6 +56,21 @@ Status HashPartition(const TablePtr &t, const std::vector<int> &hash_cols, int n
                      std::map<int, TablePtr> *out);
 Status Unique(const TablePtr &t, const std::vector<int> &cols, TablePtr &out, bool first = true);
 Status DistributedUnique(const TablePtr &t, const std::vector<int> &cols, TablePtr &out);
+
+// ---- I/O (reference table.hpp FromCSV / WriteCSV / FromParquet / WriteParquet) --------
+Status FromCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &path, TablePtr &out,
+               const io::CSVReadOptions &options = io::CSVReadOptions());
+// several files concurrently (one thread per file); out[i] <- paths[i]
+Status FromCSV(const std::shared_ptr<CylonContext> &ctx, const std::vector<std::string> &paths,
+               std::vector<TablePtr> &out, const io::CSVReadOptions &options = io::CSVReadOptions());
+Status WriteCSV(const TablePtr &t, const std::string &path,
+                const io::CSVWriteOptions &options = io::CSVWriteOptions());
+Status FromParquet(const std::shared_ptr<CylonContext> &ctx, const std::string &path, TablePtr &out,
+                   const io::ParquetOptions &options = io::ParquetOptions());
+Status FromParquet(const std::shared_ptr<CylonContext> &ctx, const std::vector<std::string> &paths,
+                   std::vector<TablePtr> &out, const io::ParquetOptions &options = io::ParquetOptions());
+Status WriteParquet(const TablePtr &t, const std::string &path,
+                    const io::ParquetOptions &options = io::ParquetOptions());
 
 // Row-predicate selection (reference table.cpp:504-529): the predicate sees a host Row view.
 class Row {

@@ -256,30 +256,41 @@ def write_csv(table: Table, path: str, csv_write_options: CSVWriteOptions = None
 
 
 class ParquetOptions:
-    """reference: cpp/src/cylon/io/parquet_config.hpp:34"""
+    """reference: cpp/src/cylon/io/parquet_config.hpp:24-53 (concurrent file reads, chunk size,
+    writer properties -> compression here); `columns` selects / orders the columns to read."""
 
-    def __init__(self, concurrent_file_reads: bool = True, chunk_size: int = 64 * 1024 * 1024,
-                 compression: str = "snappy"):
+    def __init__(self, concurrent_file_reads: bool = True, chunk_size: int = 1 << 20,
+                 compression: str = "snappy", columns: Sequence[str] = (), use_threads: bool = True):
         self.concurrent_file_reads = concurrent_file_reads
         self.chunk_size = chunk_size
         self.compression = compression
+        self.columns = list(columns)
+        self.use_threads = use_threads
+
+    def ConcurrentFileReads(self, v: bool) -> "ParquetOptions":
+        self.concurrent_file_reads = v
+        return self
+
+    def ChunkSize(self, rows: int) -> "ParquetOptions":
+        self.chunk_size = rows
+        return self
 
 
 def read_parquet(context: CylonContext, path: Union[str, Sequence[str]], options: ParquetOptions = None):
-    import pyarrow.parquet as pq
+    """Native Parquet reader (io/arrow_io.cpp, Arrow / Parquet C++): a Table, or a list of Tables
+    for a list of paths (read concurrently, one thread per file)."""
     ctx = _ensure_ctx(context)
-    if isinstance(path, (list, tuple)):
-        with ThreadPoolExecutor(max_workers=max(1, len(path))) as ex:
-            tabs = list(ex.map(pq.read_table, path))
-        return [Table(t, ctx) for t in tabs]
-    return Table(pq.read_table(path), ctx)
+    opts = options or ParquetOptions()
+    paths = list(path) if isinstance(path, (list, tuple)) else [path]
+    natives = C.read_parquet(ctx._ctx, [str(p) for p in paths], opts.columns, opts.use_threads,
+                             opts.concurrent_file_reads)
+    tables = [Table(None, ctx, _native=n) for n in natives]
+    return tables if isinstance(path, (list, tuple)) else tables[0]
 
 
 def write_parquet(table: Table, path: str, options: ParquetOptions = None):
-    import pyarrow.parquet as pq
     opts = options or ParquetOptions()
-    pq.write_table(table.to_arrow(), path, row_group_size=max(1, opts.chunk_size // 64),
-                   compression=opts.compression)
+    C.write_parquet(table.native, str(path), opts.compression or "none", max(1, int(opts.chunk_size)))
 
 
 def write_arrow_ipc(table: Table, path: str):

@@ -24,16 +24,25 @@ hip_objects = _build.compile_hip_objects()
 
 from torch.utils.cpp_extension import BuildExtension, CppExtension  # noqa: E402
 
+# Arrow / Parquet C++ (native Parquet I/O and the Arrow bridge, io/arrow_io.cpp):
+# the libraries and headers that ship inside pyarrow, linked by path (the wheel
+# has no unversioned .so symlinks) with an rpath to pyarrow's directory.
+import pyarrow  # noqa: E402
+
+_PA_DIR = pyarrow.get_library_dirs()[0]
+_PA_LIBS = [os.path.join(_PA_DIR, f) for f in sorted(os.listdir(_PA_DIR))
+            if f.startswith(("libarrow.so.", "libparquet.so.")) and f.count(".") == 2]
+
 ext = CppExtension(
     name="cylon_amd._C",
     sources=_build.cpp_sources(),
     include_dirs=[_build.CSRC, _build.ROCM_INCLUDE],
     define_macros=[("__HIP_PLATFORM_AMD__", "1"), ("USE_ROCM", "1")],
     extra_compile_args=["-O3", "-std=c++17", "-Wno-unused-function"],
-    extra_objects=hip_objects,
+    extra_objects=hip_objects + _build.compile_cxx20_objects([pyarrow.get_include()]) + _PA_LIBS,
     library_dirs=[_build.ROCM_LIB],
     libraries=["amdhip64", "rocprofiler-sdk-roctx"],
-    extra_link_args=[f"-Wl,-rpath,{_build.ROCM_LIB}"],
+    extra_link_args=[f"-Wl,-rpath,{_build.ROCM_LIB}", f"-Wl,-rpath,{_PA_DIR}"],
 )
 
 setup(

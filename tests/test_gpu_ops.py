@@ -207,3 +207,15 @@ def test_radix_union_all_distinct_fast_path(gpu_ctx, monkeypatch):
     assert both.row_count == n
     assert torch.equal(both.to_torch()["k"], L.to_torch()["k"])
     assert L.intersect(L).row_count == n and L.subtract(L).row_count == 0
+
+
+def test_native_parquet_to_and_from_hbm(gpu_ctx, tmp_path):
+    import pyarrow.parquet as pq
+    from cylon_amd.io import read_parquet, write_parquet
+    at = pa.table({"k": [3, None, 1], "s": ["x", "yy", None], "f": [0.5, None, 2.0]})
+    p = str(tmp_path / "g.parquet")
+    pq.write_table(at, p)
+    t = read_parquet(gpu_ctx, p)
+    assert t.device.startswith("cuda") and t.to_arrow().equals(at)
+    write_parquet(t.sort("k"), str(tmp_path / "o.parquet"))
+    assert pq.read_table(str(tmp_path / "o.parquet")).column("k").to_pylist() == [1, 3, None]
