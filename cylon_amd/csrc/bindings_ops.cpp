@@ -226,5 +226,6 @@ void register_extended_ops(py::module &m) {
 
   m.def("map_to_sort_partitions", &ops::MapToSortPartitions, rel);
   m.def("partition_reorder", &ops::PartitionReorder, rel);
+  m.def("shuffle_partition", &ops::ShufflePartition, rel);
   m.def("all_to_all_table", &ops::AllToAllTable, rel);
 }

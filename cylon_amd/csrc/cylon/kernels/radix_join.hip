@@ -94,6 +94,19 @@ struct PartDigit {
 };
 
 
+// Shuffle digit: the reference's partition of a single 8-byte integer key
+// (ModuloPartitionKernel: h = (uint32)key, pid = h % P, or h & (P-1) for powers
+// of two; partition.hip partition_f + hashing::partitioner), so one LDS-staged
+// pass produces the partition-major order of the whole table.
+struct ModDigit {
+  const int64_t *keys;
+  uint32_t nparts;
+  __device__ __forceinline__ uint32_t of_key(int64_t k) const {
+    return hashing::partitioner((uint32_t)(uint64_t)k, nparts);
+  }
+  __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key(keys[i]); }
+};
+
 // Sort digit: bits [shift, shift + log2(mask+1)) of an order-preserving uint64 image (K6).
 struct ImageDigit {
   const int64_t *keys;
@@ -341,6 +354,44 @@ void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_b
                           uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream) {
   const uint32_t nb = 1u << digit_bits;
   rows_pass_launch(ImageDigit{keys, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws, stream);
+}
+
+static int bits_for(uint32_t nparts) {
+  int b = 1;
+  while ((1u << b) < nparts) ++b;
+  return b;
+}
+
+int64_t radix_mod_rows_pass_workspace(int64_t n, uint32_t nparts) {
+  return radix_rows_pass_workspace(n, bits_for(nparts));
+}
+
+void radix_mod_rows_pass(const int64_t *keys, int64_t n, uint32_t nparts, const uint8_t *const *in, uint8_t *const *out,
+                         const int *widths, int ncols, int64_t *ws, void *stream) {
+  CYLON_CHECK(nparts >= 1 && nparts <= (uint32_t)kRPMaxBuckets, Code::Invalid, "partition count " << nparts);
+  rows_pass_launch(ModDigit{keys, nparts}, n, bits_for(nparts), in, out, widths, ncols, ws, stream);
+}
+
+__global__ __launch_bounds__(kRPThreads) void k_mod_counts(ModDigit digit, int64_t n,
+                                                           unsigned long long *__restrict__ counts) {
+  __shared__ unsigned int hist[kRPMaxBuckets];
+  for (uint32_t p = threadIdx.x; p < digit.nparts; p += blockDim.x) hist[p] = 0;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) atomicAdd(&hist[digit(i)], 1u);
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < digit.nparts; p += blockDim.x)
+    if (hist[p]) atomicAdd(&counts[p], (unsigned long long)hist[p]);
+}
+
+void mod_partition_counts(const int64_t *keys, int64_t n, uint32_t nparts, int64_t *counts, void *stream) {
+  CYLON_CHECK(nparts >= 1 && nparts <= (uint32_t)kRPMaxBuckets, Code::Invalid, "partition count " << nparts);
+  hipStream_t s = as_stream(stream);
+  HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int64_t) * nparts, s));
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_mod_counts, dim3(grid_for(n, kRPThreads, kNumCUs * 2)), dim3(kRPThreads), 0, s,
+                     ModDigit{keys, nparts}, n, reinterpret_cast<unsigned long long *>(counts));
+  HIP_LAUNCH_CHECK();
 }
 
 // offsets[p] = first row of partition p in partition-sorted keys (binary search), offsets[P] = n

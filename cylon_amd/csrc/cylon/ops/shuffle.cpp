@@ -39,6 +39,72 @@ static at::Tensor hash_pids(const TablePtr &t, const std::vector<int> &cols, uin
   return pid;
 }
 
+// ---------------------------------------------------------------------------
+// Fast shuffle partition (radix_join.hip ModDigit pass): when the partition key
+// is one non-null 8-byte integer column of a device table whose columns are all
+// 1/2/4/8 bytes wide, the reference partition id is (uint32)key % P and a single
+// LDS-staged pass moves the whole table into partition-major order (one read and
+// one write per buffer, long write runs for P <= 1024) instead of pid + hash
+// arrays, a ballot ranking and a per-row scatter.
+// ---------------------------------------------------------------------------
+static bool mod_pass_eligible(const TablePtr &t, const std::vector<int> &cols, uint32_t P) {
+  if (!t->device().is_cuda() || cols.size() != 1 || P > 1024 || t->Rows() == 0) return false;
+  const Column &k = t->column(cols[0]);
+  if (k.nullable() || k.is_var() || k.type.width() != 8 || k.data.element_size() != 8 ||
+      (k.type.kind() != ValueKind::SIGNED_INT && k.type.kind() != ValueKind::UNSIGNED_INT))
+    return false;
+  int slots = 1;
+  for (int c = 0; c < t->Columns(); ++c) {
+    const Column &col = t->column(c);
+    const int w = col.type.width();
+    if (col.is_var() || col.type.kind() == ValueKind::FIXED_BYTES || !(w == 1 || w == 2 || w == 4 || w == 8) ||
+        col.data.element_size() != w)
+      return false;
+    slots += (c == cols[0] ? 0 : 1) + (col.nullable() ? 1 : 0);
+  }
+  return slots <= kMaxFusedCols;
+}
+
+static std::vector<int64_t> mod_counts(const TablePtr &t, int key, uint32_t P) {
+  Exec ex(t->device());
+  at::Tensor counts = ex.empty_i64(P);
+  hip::mod_partition_counts(reinterpret_cast<const int64_t *>(t->column(key).data.data_ptr()), t->Rows(), P,
+                            ptr<int64_t>(counts), ex.stream);
+  return to_host_vec(counts);
+}
+
+static TablePtr mod_reorder(const TablePtr &t, int key, uint32_t P) {
+  Exec ex(t->device());
+  const int64_t n = t->Rows();
+  const Column &kc = t->column(key);
+  std::vector<const uint8_t *> in{reinterpret_cast<const uint8_t *>(kc.data.data_ptr())};
+  std::vector<at::Tensor> out{at::empty_like(kc.data)};
+  std::vector<int> widths{8};
+  std::vector<int> dslot(t->Columns(), 0), vslot(t->Columns(), -1);
+  auto add = [&](const at::Tensor &x, int w) {
+    in.push_back(reinterpret_cast<const uint8_t *>(x.data_ptr()));
+    out.push_back(at::empty_like(x));
+    widths.push_back(w);
+    return (int)out.size() - 1;
+  };
+  for (int c = 0; c < t->Columns(); ++c) {
+    const Column &col = t->column(c);
+    if (c != key) dslot[c] = add(col.data, col.type.width());
+    if (col.nullable()) vslot[c] = add(col.validity, 1);
+  }
+  std::vector<uint8_t *> outp;
+  for (auto &o : out) outp.push_back(reinterpret_cast<uint8_t *>(o.data_ptr()));
+  at::Tensor ws = ex.empty_i64(hip::radix_mod_rows_pass_workspace(n, P));
+  hip::radix_mod_rows_pass(reinterpret_cast<const int64_t *>(in[0]), n, P, in.data(), outp.data(), widths.data(),
+                           (int)in.size(), ptr<int64_t>(ws), ex.stream);
+  std::vector<Column> cols;
+  for (int c = 0; c < t->Columns(); ++c) {
+    const Column &col = t->column(c);
+    cols.emplace_back(col.name, col.type, n, out[dslot[c]], at::Tensor(), vslot[c] >= 0 ? out[vslot[c]] : at::Tensor());
+  }
+  return Table::Make(t->GetContext(), std::move(cols));
+}
+
 // A table whose column buffers are in flight (posted all-to-alls).
 struct PendingTable {
   std::shared_ptr<CylonContext> ctx;
@@ -268,9 +334,19 @@ TablePtr AllToAllTable(const TablePtr &part, const std::vector<int64_t> &counts)
   return AllToAllFinish(pt);
 }
 
+std::pair<TablePtr, std::vector<int64_t>> ShufflePartition(const TablePtr &t, const std::vector<int> &hash_cols,
+                                                           uint32_t nparts) {
+  if (mod_pass_eligible(t, hash_cols, nparts)) return {mod_reorder(t, hash_cols[0], nparts), mod_counts(t, hash_cols[0], nparts)};
+  return PartitionReorder(t, hash_pids(t, hash_cols, nparts), nparts);
+}
+
 static std::pair<TablePtr, std::vector<int64_t>> shuffle_partition(const TablePtr &t,
                                                                    const std::vector<int> &hash_cols, int world) {
   CYLON_PHASE("shuffle.partition", t->device());
+  if (mod_pass_eligible(t, hash_cols, (uint32_t)world)) {
+    std::vector<int64_t> counts = mod_counts(t, hash_cols[0], (uint32_t)world);
+    return {mod_reorder(t, hash_cols[0], (uint32_t)world), counts};
+  }
   at::Tensor pid = hash_pids(t, hash_cols, (uint32_t)world);
   return PartitionReorder(t, pid, (uint32_t)world);
 }
@@ -382,12 +458,18 @@ void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const 
   // partition ids and counts of both tables first (cheap), so that one count exchange
   // serves every chunk and b's reorder can run while a's first chunk is on the wire
   std::pair<at::Tensor, at::Tensor> ha, hb;
+  const bool fast_a = mod_pass_eligible(a, acols, P), fast_b = mod_pass_eligible(b, bcols, P);
+  std::vector<int64_t> ca, cb;
   {
     CYLON_PHASE("shuffle.partition", a->device());
-    ha = hash_pids_counts(a, acols, P);
-    hb = hash_pids_counts(b, bcols, P);
+    if (fast_a) ca = mod_counts(a, acols[0], P);
+    else ha = hash_pids_counts(a, acols, P);
+    if (fast_b) cb = mod_counts(b, bcols[0], P);
+    else hb = hash_pids_counts(b, bcols, P);
   }
-  const std::vector<int64_t> ca = to_host_vec(ha.second), cb = to_host_vec(hb.second);
+  if (!fast_a) ca = to_host_vec(ha.second);
+  if (!fast_b) cb = to_host_vec(hb.second);
+  trace::add_counter("shuffle.fast_partition", (fast_a ? 1 : 0) + (fast_b ? 1 : 0));
   // block r of the exchange = [a chunks 0..K-1, b chunks 0..K-1] for rank r
   std::vector<int64_t> sendc((size_t)W * 2 * K), recvc;
   for (int r = 0; r < W; ++r)
@@ -424,10 +506,10 @@ void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const 
   TablePtr pta, ptb;
   {
     CYLON_PHASE("shuffle.reorder+post", a->device());
-    pta = to_wire(PartitionReorder(a, ha.first, P).first, plans[0]);
+    pta = to_wire(fast_a ? mod_reorder(a, acols[0], P) : PartitionReorder(a, ha.first, P).first, plans[0]);
     ha = {};
     pa[0] = post(pta, ca, 0, 0, na_flags, offa);  // a's chunk 0 transfers while b is reordered
-    ptb = to_wire(PartitionReorder(b, hb.first, P).first, plans[1]);
+    ptb = to_wire(fast_b ? mod_reorder(b, bcols[0], P) : PartitionReorder(b, hb.first, P).first, plans[1]);
     hb = {};
     pb[0] = post(ptb, cb, 1, 0, nb_flags, offb);
     for (int k = 1; k < K; ++k) {

@@ -83,6 +83,10 @@ std::pair<at::Tensor, std::vector<int64_t>> MapToHashPartitions(const TablePtr &
 std::pair<TablePtr, std::vector<int64_t>> PartitionReorder(const TablePtr &t, const at::Tensor &pid,
                                                            uint32_t nparts);
 std::vector<TablePtr> Split(const TablePtr &t, const at::Tensor &pid, uint32_t nparts);
+// the shuffle's partitioning: reference hash partition ids -> partition-major table + counts
+// (one LDS-staged pass for a single non-null 8-byte integer key on the device)
+std::pair<TablePtr, std::vector<int64_t>> ShufflePartition(const TablePtr &t, const std::vector<int> &hash_cols,
+                                                           uint32_t nparts);
 std::vector<TablePtr> HashPartition(const TablePtr &t, const std::vector<int> &cols, uint32_t nparts);
 
 // ---- communication --------------------------------------------------------

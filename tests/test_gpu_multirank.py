@@ -54,6 +54,7 @@ def test_chunked_distributed_join_on_device(chunks):
         assert c.get("join.radix.rows_out", 0) > 0, c  # the LDS radix join ran (into the sink when chunked)
         if chunks > 1:
             assert c.get("shuffle.chunks") == chunks
+            assert c.get("shuffle.fast_partition") == 2  # one LDS-staged pass per relation
 
 
 def _dist_ops(ctx):
@@ -70,6 +71,27 @@ def _dist_ops(ctx):
     tu1, tu2 = Table.from_pandas(ctx, u1), Table.from_pandas(ctx, u2)
     sets = {op: getattr(tu1, f"distributed_{op}")(tu2).to_pandas() for op in ("union", "intersect", "subtract")}
     return df, g, s, u1, u2, sets
+
+
+def test_shuffle_partition_fast_pass_matches_generic():
+    """The shuffle's one-pass partition of an int64-keyed table equals the generic
+    pid + stable scatter path (rows, order within partitions, counts)."""
+    import torch
+    from cylon_amd import CylonContext, Table
+    from cylon_amd._lib import C
+    ctx = CylonContext(device=DEV)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    n = 300_000
+    t = Table.from_torch(ctx, {"k": torch.randint(-2**40, 2**40, (n,), generator=g, device="cuda"),
+                               "x": torch.randint(0, 100, (n,), generator=g, device="cuda", dtype=torch.int32),
+                               "f": torch.rand(n, generator=g, device="cuda", dtype=torch.float64)})
+    for P in (2, 8, 24, 1024):
+        fast, cf = C.shuffle_partition(t.native, [0], P)
+        pid, _ = C.map_to_hash_partitions(t.native, [0], P)
+        slow, cs = C.partition_reorder(t.native, pid, P)
+        assert list(cf) == list(cs)
+        a, b = Table(None, ctx, _native=fast).to_arrow(), Table(None, ctx, _native=slow).to_arrow()
+        assert a.equals(b), P
 
 
 def test_distributed_ops_on_device():

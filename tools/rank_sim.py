@@ -52,10 +52,15 @@ for W in worlds:
             outs.append(C.partition_reorder(t.native, pid, W))
         return outs
 
+    def part_fast():  # what the shuffle runs for an int64 key: one LDS-staged pass (W * 4 chunk partitions)
+        return [C.shuffle_partition(t.native, [0], W * 4) for t in (L, R)]
+
     tp = timed(part)
+    tpf = timed(part_fast)
     tj = timed(lambda: L.join(R, "inner", "hash", on=[0]))
     nbytes = 2 * n * 32 * (W - 1) / W
-    print(f"W={W} rows/rank={n}: partition+reorder(both) {tp:.1f} ms, local join {tj:.1f} ms, "
+    print(f"W={W} rows/rank={n}: partition+reorder(both) generic {tp:.1f} ms, fast {tpf:.1f} ms, "
+          f"local join {tj:.1f} ms, "
           f"bytes sent/rank {nbytes / 1e9:.2f} GB", flush=True)
     del L, R
     torch.cuda.empty_cache()
