@@ -550,6 +550,12 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_count(const int64_t *__res
   }
 }
 
+__device__ __forceinline__ int64_t rj_shfl64(int64_t x, int src) {
+  const uint32_t lo = __shfl((uint32_t)(uint64_t)x, src, kWave);
+  const uint32_t hi = __shfl((uint32_t)((uint64_t)x >> 32), src, kWave);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 struct BuildOut {               // build-side output columns
   uint8_t *out[kMaxFusedCols];
   int width[kMaxFusedCols];
@@ -661,7 +667,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
       const int64_t l = s0 + (int64_t)u * kWave + lane;
       const bool active = l < s1;
       int64_t k = 0;
-      uint64_t v[MAXP];
+      uint64_t v[MAXP] = {};
       if (u < kRJProbeRounds) {
 #pragma unroll
         for (int uu = 0; uu < kRJProbeRounds; ++uu)
@@ -690,25 +696,54 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
         if (lane >= d) inc += x;
       }
       const uint32_t wsum = __shfl(inc, kWave - 1, kWave);
-      int64_t o = base + (inc - mc);
-      if (mc) {
-        for (uint32_t i = i0; i < i1; ++i) {
-          if (skeys[i] != k) continue;
-          const int r = perm[i];
+      const uint32_t excl = inc - mc;
+      // Load-balanced expansion: lane t writes output rows base + t, base + 64 + t, ...
+      // of this round, so every store covers a contiguous, fully active run of the
+      // output column (a lane-per-probe-row loop over bucket entries would issue
+      // sparse partial-line stores).  The producing probe lane ("owner") of row
+      // s is found by a binary search over the wave's inclusive match counts and
+      // its key / bucket / payload are read with cross-lane permutes.
+      for (uint32_t t0 = 0; t0 < wsum; t0 += kWave) {
+        const uint32_t so = t0 + lane;
+        const bool act = so < wsum;
+        int owner = 0;
+#pragma unroll
+        for (int step = kWave / 2; step >= 1; step >>= 1) {
+          const uint32_t ic = __shfl(inc, owner + step - 1, kWave);
+          if (ic <= so) owner += step;
+        }
+        const uint32_t j = so - __shfl(excl, owner, kWave);  // match rank inside the owner's bucket
+        const int64_t ko = rj_shfl64(k, owner);
+        const uint32_t b0 = __shfl(i0, owner, kWave), b1 = __shfl(i1, owner, kWave);
+        uint64_t vo[MAXP];
+#pragma unroll
+        for (int q = 0; q < MAXP; ++q) vo[q] = (uint64_t)rj_shfl64((int64_t)v[q], owner);
+        if (act) {
+          int r = 0;
+          for (uint32_t i = b0, c = 0; i < b1; ++i) {
+            if (skeys[i] != ko) continue;
+            if (c == j) {
+              r = perm[i];
+              break;
+            }
+            ++c;
+          }
+          const int64_t o = base + so;
 #pragma unroll
           for (int q = 0; q < MAXP; ++q)
-            if (q < pc.n) stw<W8>(pc.out[q], o, pc.width[q], v[q]);
-          for (int q = MAXP; q < pc.n; ++q)
-            stw<W8>(pc.out[q], o, pc.width[q], ldw<W8>(pc.in[q], l, pc.width[q]));
+            if (q < pc.n) stw<W8>(pc.out[q], o, pc.width[q], vo[q]);
+          if (pc.n > MAXP) {
+            const int64_t lo = s0 + (int64_t)u * kWave + owner;
+            for (int q = MAXP; q < pc.n; ++q) stw<W8>(pc.out[q], o, pc.width[q], ldw<W8>(pc.in[q], lo, pc.width[q]));
+          }
 #pragma unroll
           for (int q = 0; q < MAXB + 1; ++q)
             if (q < bo.n)
               stw<W8>(bo.out[q], o, bo.width[q],
-                      bo.lds_off[q] < 0 ? (uint64_t)k : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
+                      bo.lds_off[q] < 0 ? (uint64_t)ko : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
           for (int q = MAXB + 1; q < bo.n; ++q)
             stw<W8>(bo.out[q], o, bo.width[q],
-                    bo.lds_off[q] < 0 ? (uint64_t)k : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
-          ++o;
+                    bo.lds_off[q] < 0 ? (uint64_t)ko : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
         }
       }
       base += wsum;
