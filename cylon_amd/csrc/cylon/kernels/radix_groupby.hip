@@ -23,23 +23,37 @@
 namespace cylon {
 namespace hip {
 
-constexpr int kHllBits = 14;
+constexpr int kHllBits = 12;  // 4096 registers: 1.6% standard error, 16 KB of LDS per block
 constexpr int kHllRegs = 1 << kHllBits;
 constexpr int kRGThreads = 512;
 constexpr int kRGWaves = kRGThreads / kWave;
 constexpr int64_t kRGEmpty = INT64_MIN;  // empty-slot sentinel; the key INT64_MIN itself gets slot S
 
+__device__ __forceinline__ void hll_add(uint32_t *r, int64_t key) {
+  const uint64_t h = hashing::fmix64((uint64_t)key);
+  const uint32_t idx = (uint32_t)(h >> (64 - kHllBits));
+  const uint32_t rho = (uint32_t)__clzll((h << kHllBits) | (1ull << (kHllBits - 1))) + 1;
+  atomicMax(&r[idx], rho);
+}
+
+// two keys per thread per step (16-byte loads); LDS-privatised registers
 __global__ __launch_bounds__(kBlock) void k_hll(const int64_t *__restrict__ keys, int64_t n,
                                                 uint32_t *__restrict__ regs) {
   __shared__ uint32_t r[kHllRegs];
   for (int i = threadIdx.x; i < kHllRegs; i += blockDim.x) r[i] = 0;
   __syncthreads();
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint64_t h = hashing::fmix64((uint64_t)keys[i]);
-    const uint32_t idx = (uint32_t)(h >> (64 - kHllBits));
-    const uint32_t rho = (uint32_t)__clzll((h << kHllBits) | (1ull << (kHllBits - 1))) + 1;
-    atomicMax(&r[idx], rho);
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool vec = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
+  if (vec) {
+    for (int64_t i = t0; i < (n >> 1); i += stride) {
+      const longlong2 k2 = reinterpret_cast<const longlong2 *>(keys)[i];
+      hll_add(r, k2.x);
+      hll_add(r, k2.y);
+    }
+    if ((n & 1) && t0 == 0) hll_add(r, keys[n - 1]);
+  } else {
+    for (int64_t i = t0; i < n; i += stride) hll_add(r, keys[i]);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < kHllRegs; i += blockDim.x)
@@ -50,7 +64,7 @@ double distinct_estimate(const int64_t *keys, int64_t n, uint32_t *regs, void *s
   hipStream_t s = as_stream(stream);
   HIP_CHECK(hipMemsetAsync(regs, 0, sizeof(uint32_t) * kHllRegs, s));
   if (n > 0) {
-    hipLaunchKernelGGL(k_hll, dim3(grid_for(n, kBlock, kNumCUs * 2)), dim3(kBlock), 0, s, keys, n, regs);
+    hipLaunchKernelGGL(k_hll, dim3(grid_for((n + 1) / 2, kBlock, kNumCUs * 8)), dim3(kBlock), 0, s, keys, n, regs);
     HIP_LAUNCH_CHECK();
   }
   std::vector<uint32_t> h(kHllRegs);
