@@ -35,43 +35,89 @@ def hip_sources():
     return sorted(glob.glob(os.path.join(KERNELS, "*.hip")))
 
 
-# sources compiled on their own as C++20 (the Arrow 25 C++ headers need it) and
-# linked as objects into the extension
+# sources that need C++20 (the Arrow 25 C++ headers)
 CXX20_SOURCES = [os.path.join(CSRC, "cylon", "io", "arrow_io.cpp")]
+# the Python extension (pybind11 bindings) - everything else is the native core library
+BINDING_SOURCES = [os.path.join(CSRC, "bindings.cpp"), os.path.join(CSRC, "bindings_ops.cpp")]
+CORE_LIB = os.path.join(PKG, "libcylon_amd.so")
 
 
-def cpp_sources():
-    srcs = [os.path.join(CSRC, "bindings.cpp"), os.path.join(CSRC, "bindings_ops.cpp"), os.path.join(CSRC, "capi.cpp")]
+def core_sources():
+    srcs = [os.path.join(CSRC, "capi.cpp")]
     for sub in ("cylon", "cylon/net", "cylon/ops", "cylon/ctx", "cylon/io", "cylon/kernels"):
         srcs += sorted(glob.glob(os.path.join(CSRC, sub, "*.cpp")))
-    return [os.path.relpath(s, ROOT) for s in srcs if s not in CXX20_SOURCES]
+    return srcs
 
 
-def compile_cxx20_objects(extra_includes):
-    """Compile CXX20_SOURCES with the host compiler against torch's and Arrow's headers."""
+def binding_sources():
+    return [os.path.relpath(s, ROOT) for s in BINDING_SOURCES]
+
+
+def _torch_flags():
     import torch
-    from torch.utils.cpp_extension import include_paths
-    os.makedirs(OBJ_DIR, exist_ok=True)
-    digest = _headers_digest()
+    from torch.utils.cpp_extension import include_paths, library_paths
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
-    flags = ["-std=c++20", "-O2", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1",
-             "-DUSE_ROCM=1", "-Wno-unused-function"]
-    incs = [CSRC, ROCM_INCLUDE] + include_paths() + list(extra_includes)
-    objs = []
-    for src in CXX20_SOURCES:
-        obj = os.path.join(OBJ_DIR, os.path.splitext(os.path.basename(src))[0] + ".cxx20.o")
-        stamp = obj + ".stamp"
-        with open(src, "rb") as f:
-            key = hashlib.sha1(f.read() + digest.encode() + " ".join(flags + incs).encode()).hexdigest()
-        if not (os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read().strip() == key):
-            cmd = ["g++"] + flags + [x for i in incs for x in ("-I", i)] + ["-c", src, "-o", obj]
-            r = subprocess.run(cmd, capture_output=True, text=True)
-            if r.returncode != 0:
-                raise RuntimeError(f"g++ failed for {src}:\n{r.stderr[-6000:]}")
-            with open(stamp, "w") as f:
-                f.write(key)
-        objs.append(obj)
-    return objs
+    return include_paths(), library_paths()[0], [f"-D_GLIBCXX_USE_CXX11_ABI={abi}"]
+
+
+def _arrow_paths():
+    import pyarrow
+    d = pyarrow.get_library_dirs()[0]
+    libs = [os.path.join(d, f) for f in sorted(os.listdir(d))
+            if f.startswith(("libarrow.so.", "libparquet.so.")) and f.count(".") == 2]
+    return pyarrow.get_include(), d, libs
+
+
+def _compile_cxx(src, digest, incs, defs):
+    std = "-std=c++20" if src in CXX20_SOURCES else "-std=c++17"
+    flags = [std, "-O3", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-Wall", "-Wno-unused-function",
+             "-Wno-sign-compare"] + defs
+    rel = os.path.relpath(src, CSRC).replace(os.sep, "__")
+    obj = os.path.join(OBJ_DIR, "core", os.path.splitext(rel)[0] + ".o")
+    stamp = obj + ".stamp"
+    with open(src, "rb") as f:
+        key = hashlib.sha1(f.read() + digest.encode() + " ".join(flags + incs).encode()).hexdigest()
+    if os.path.exists(obj) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == key:
+                return obj, False
+    cmd = ["g++"] + flags + [x for i in incs for x in ("-I", i)] + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"g++ failed for {src}:\n{r.stderr[-6000:]}")
+    with open(stamp, "w") as f:
+        f.write(key)
+    return obj, True
+
+
+def build_core(jobs=None):
+    """Native core library cylon_amd/libcylon_amd.so: C++ engine + C ABI + HIP kernels.
+
+    Links libtorch / c10 (tensors, allocator, c10d process groups), the HIP
+    runtime and the Arrow / Parquet C++ libraries shipped with pyarrow; no
+    Python.  C++ programs (examples/cpp) and the Python extension link it."""
+    hip_objs = compile_hip_objects(jobs)
+    os.makedirs(os.path.join(OBJ_DIR, "core"), exist_ok=True)
+    digest = _headers_digest()
+    tinc, tlib, tdefs = _torch_flags()
+    ainc, adir, alibs = _arrow_paths()
+    incs = [CSRC, ROCM_INCLUDE] + tinc + [ainc]
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        res = list(ex.map(lambda s: _compile_cxx(s, digest, incs, tdefs), core_sources()))
+    objs = [o for o, _ in res]
+    inputs = objs + hip_objs
+    if os.path.exists(CORE_LIB) and not any(c for _, c in res) and \
+            all(os.path.getmtime(o) <= os.path.getmtime(CORE_LIB) for o in inputs):
+        return CORE_LIB
+    cmd = (["g++", "-shared", "-o", CORE_LIB, "-Wl,-soname,libcylon_amd.so"] + inputs +
+           ["-L", tlib, "-Wl,--no-as-needed", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lc10", "-lc10_hip",
+            "-Wl,--as-needed", "-L", ROCM_LIB, "-lamdhip64", "-lrocprofiler-sdk-roctx"] + alibs +
+           [f"-Wl,-rpath,{tlib}", f"-Wl,-rpath,{ROCM_LIB}", f"-Wl,-rpath,{adir}"])
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"linking {CORE_LIB} failed:\n{r.stderr[-6000:]}")
+    return CORE_LIB
 
 
 def _headers_digest():

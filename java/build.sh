@@ -1,11 +1,12 @@
 #!/usr/bin/env bash
-# Build the Java API (J1) and its JNI layer (J2).  Needs a JDK (javac, jni.h) and a built
-# cylon_amd extension (python -c "import cylon_amd").  Not part of the CI image (no JDK).
+# Build the Java API (J1) and its JNI layer (J2).  Needs a JDK (javac, jni.h) and the built
+# native core library cylon_amd/libcylon_amd.so (python setup.py build_ext --inplace); the JNI
+# layer links only that library (C ABI), no Python.  Not part of the CI image (no JDK).
 set -euo pipefail
 HERE=$(cd "$(dirname "$0")" && pwd)
 ROOT=$(cd "$HERE/.." && pwd)
 : "${JAVA_HOME:?set JAVA_HOME to a JDK}"
-SO=$(python -c "import cylon_amd._C as c; print(c.__file__)")
+SO="$ROOT/cylon_amd/libcylon_amd.so"
 mkdir -p "$HERE/build/classes"
 javac -d "$HERE/build/classes" $(find "$HERE/src/main/java" -name '*.java')
 g++ -O2 -shared -fPIC -std=c++17 -I"$JAVA_HOME/include" -I"$JAVA_HOME/include/linux" \

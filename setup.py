@@ -1,12 +1,13 @@
 """Build the cylon_amd native engine in-tree.
 
-Two stages:
-  1. every HIP kernel file (cylon_amd/csrc/cylon/kernels/*.hip) is compiled by
-     hipcc for gfx950 (MI355X) into an object file (no torch headers, no
-     hipify: the sources are HIP);
-  2. the host C++ core + pybind11 bindings are compiled as a torch
-     CppExtension and linked with those objects and libamdhip64 into
-     cylon_amd/_C*.so.
+Two artefacts:
+  1. cylon_amd/libcylon_amd.so - the native core library (C++ engine, C ABI,
+     every HIP kernel compiled by hipcc for gfx950 / MI355X; links libtorch /
+     c10, the HIP runtime and the Arrow / Parquet C++ libraries from pyarrow;
+     no Python).  Built by cylon_amd/_build.py with hipcc + g++.  C++ programs
+     link it directly (examples/cpp).
+  2. cylon_amd/_C*.so - the pybind11 bindings (torch CppExtension) over the
+     core library (rpath $ORIGIN).
 
 Usage: python setup.py build_ext --inplace   (or cylon_amd._build.build())
 """
@@ -20,29 +21,20 @@ _spec = importlib.util.spec_from_file_location(
 _build = importlib.util.module_from_spec(_spec)
 _spec.loader.exec_module(_build)
 
-hip_objects = _build.compile_hip_objects()
+core_lib = _build.build_core()
 
 from torch.utils.cpp_extension import BuildExtension, CppExtension  # noqa: E402
 
-# Arrow / Parquet C++ (native Parquet I/O and the Arrow bridge, io/arrow_io.cpp):
-# the libraries and headers that ship inside pyarrow, linked by path (the wheel
-# has no unversioned .so symlinks) with an rpath to pyarrow's directory.
-import pyarrow  # noqa: E402
-
-_PA_DIR = pyarrow.get_library_dirs()[0]
-_PA_LIBS = [os.path.join(_PA_DIR, f) for f in sorted(os.listdir(_PA_DIR))
-            if f.startswith(("libarrow.so.", "libparquet.so.")) and f.count(".") == 2]
-
 ext = CppExtension(
     name="cylon_amd._C",
-    sources=_build.cpp_sources(),
+    sources=_build.binding_sources(),
     include_dirs=[_build.CSRC, _build.ROCM_INCLUDE],
     define_macros=[("__HIP_PLATFORM_AMD__", "1"), ("USE_ROCM", "1")],
     extra_compile_args=["-O3", "-std=c++17", "-Wno-unused-function"],
-    extra_objects=hip_objects + _build.compile_cxx20_objects([pyarrow.get_include()]) + _PA_LIBS,
+    extra_objects=[core_lib],
     library_dirs=[_build.ROCM_LIB],
-    libraries=["amdhip64", "rocprofiler-sdk-roctx"],
-    extra_link_args=[f"-Wl,-rpath,{_build.ROCM_LIB}", f"-Wl,-rpath,{_PA_DIR}"],
+    libraries=["amdhip64"],
+    extra_link_args=["-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{_build.ROCM_LIB}"],
 )
 
 setup(

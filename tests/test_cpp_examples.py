@@ -1,0 +1,62 @@
+"""The native C++ API without Python: examples/cpp/relational_example.cpp links only
+cylon_amd/libcylon_amd.so (+ libtorch) and must agree with the Python API."""
+import os
+import subprocess
+
+import pyarrow as pa
+import pyarrow.csv  # noqa: F401
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "examples", "cpp", "bin", "relational_example")
+
+
+def _ensure_built():
+    src = os.path.join(ROOT, "examples", "cpp", "relational_example.cpp")
+    lib = os.path.join(ROOT, "cylon_amd", "libcylon_amd.so")
+    if not os.path.exists(EXE) or os.path.getmtime(EXE) < max(os.path.getmtime(src), os.path.getmtime(lib)):
+        subprocess.run(["bash", os.path.join(ROOT, "examples", "cpp", "build.sh")], check=True, capture_output=True)
+    return EXE
+
+
+def _run(device, tmp_path, data_dir):
+    exe = _ensure_built() if device == "cpu" else EXE
+    r = subprocess.run([exe, device, os.path.join(data_dir, "input", "csv1_0.csv"),
+                        os.path.join(data_dir, "input", "csv2_0.csv"), str(tmp_path)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return dict((k, int(v)) for k, v in (line.split() for line in r.stdout.splitlines()))
+
+
+def _python_counts(ctx, data_dir):
+    from cylon_amd import Table
+    from cylon_amd.io import read_csv
+    a = read_csv(ctx, os.path.join(data_dir, "input", "csv1_0.csv"))
+    b = read_csv(ctx, os.path.join(data_dir, "input", "csv2_0.csv"))
+    return {"left": a.row_count, "right": b.row_count,
+            "join_hash": a.join(b, "inner", "hash", on=[0]).row_count,
+            "join_sort": a.join(b, "inner", "sort", on=[0]).row_count,
+            "union": a.union(b).row_count, "intersect": a.intersect(b).row_count,
+            "subtract": a.subtract(b).row_count, "unique_col0": a.unique([a.column_names[0]]).row_count,
+            "sort": a.row_count, "sum_col1": 1}
+
+
+def test_cpp_example_on_cpu(ctx, tmp_path, data_dir):
+    got = _run("cpu", tmp_path, data_dir)
+    exp = _python_counts(ctx, data_dir)
+    for k, v in exp.items():
+        assert got[k] == v, (k, got, exp)
+    assert got["parquet_roundtrip"] == got["join_hash"]
+    assert got["groupby_sum"] == got["unique_col0"]
+    assert pa.csv.read_csv(str(tmp_path / "join.csv")).num_rows == got["join_hash"]
+
+
+@pytest.mark.gpu
+def test_cpp_example_on_gpu(tmp_path, data_dir):
+    if not os.path.exists(EXE):
+        pytest.fail("examples/cpp/bin/relational_example missing: run __graft_entry__.build()")
+    from cylon_amd import CylonContext
+    got = _run("cuda:0", tmp_path, data_dir)
+    exp = _python_counts(CylonContext(device="cpu"), data_dir)
+    for k, v in exp.items():
+        assert got[k] == v, (k, got, exp)
