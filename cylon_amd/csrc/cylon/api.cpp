@@ -1,6 +1,7 @@
 // Status-returning API, table registry, Row/Select and the all-to-all classes (see api.hpp).
 #include "api.hpp"
 
+#include <iostream>
 #include <mutex>
 
 #include "ops/util.hpp"
@@ -103,18 +104,57 @@ bool Row::IsNull(int col) const {
   return c.nullable() && c.validity.data_ptr<uint8_t>()[row_] == 0;
 }
 
-int64_t Row::GetInt64(int col) const {
+const uint8_t *Row::raw(int col, int *width) const {
   const Column &c = t_->column(col);
-  at::Tensor v = c.data.slice(0, row_, row_ + 1).to(at::kLong);
-  return v.item<int64_t>();
+  CYLON_CHECK(!c.is_var(), Code::TypeError, "column " << c.name << " is variable width");
+  CYLON_CHECK(row_ >= 0 && row_ < c.length, Code::IndexError, "row " << row_ << " out of range");
+  *width = c.type.width();
+  return static_cast<const uint8_t *>(c.data.data_ptr()) + row_ * (int64_t)(*width);
+}
+
+int64_t Row::GetInt64(int col) const {
+  int w = 0;
+  const uint8_t *p = raw(col, &w);
+  const ValueKind k = t_->column(col).type.kind();
+  CYLON_CHECK(k == ValueKind::SIGNED_INT || k == ValueKind::UNSIGNED_INT, Code::TypeError,
+              "column " << t_->column(col).name << " is not an integer column");
+  if (k == ValueKind::UNSIGNED_INT) return (int64_t)GetUInt64(col);
+  switch (w) {
+    case 1: return *reinterpret_cast<const int8_t *>(p);
+    case 2: return *reinterpret_cast<const int16_t *>(p);
+    case 4: return *reinterpret_cast<const int32_t *>(p);
+    default: return *reinterpret_cast<const int64_t *>(p);
+  }
+}
+
+uint64_t Row::GetUInt64(int col) const {
+  int w = 0;
+  const uint8_t *p = raw(col, &w);
+  switch (w) {
+    case 1: return *p;
+    case 2: return *reinterpret_cast<const uint16_t *>(p);
+    case 4: return *reinterpret_cast<const uint32_t *>(p);
+    default: return *reinterpret_cast<const uint64_t *>(p);
+  }
 }
 
 double Row::GetDouble(int col) const {
   const Column &c = t_->column(col);
-  return c.data.slice(0, row_, row_ + 1).to(at::kDouble).item<double>();
+  if (c.type.kind() != ValueKind::FLOAT) return c.type.kind() == ValueKind::UNSIGNED_INT ? (double)GetUInt64(col)
+                                                                                         : (double)GetInt64(col);
+  int w = 0;
+  const uint8_t *p = raw(col, &w);
+  if (w == 8) return *reinterpret_cast<const double *>(p);
+  if (w == 4) return *reinterpret_cast<const float *>(p);
+  return (double)c.data.slice(0, row_, row_ + 1).to(at::kDouble).item<double>();  // half
 }
 
-bool Row::GetBool(int col) const { return GetInt64(col) != 0; }
+bool Row::GetBool(int col) const { return GetUInt64(col) != 0; }
+
+const uint8_t *Row::GetFixedBinary(int col) const {
+  int w = 0;
+  return raw(col, &w);
+}
 
 std::string Row::GetString(int col) const {
   const Column &c = t_->column(col);
@@ -231,6 +271,97 @@ Status SortTable(const std::string &id, int col, const std::string &dest, bool a
 
 int64_t RowCount(const std::string &id) { return GetTable(id)->Rows(); }
 int32_t ColumnCount(const std::string &id) { return GetTable(id)->Columns(); }
+std::vector<std::string> ColumnNames(const std::string &id) { return GetTable(id)->ColumnNames(); }
+
+Status ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &path, const std::string &id,
+               const io::CSVReadOptions &options) {
+  return guard([&] { PutTable(id, io::ReadCSV(ctx, path, options)); });
+}
+Status ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::vector<std::string> &paths,
+               const std::vector<std::string> &ids, const io::CSVReadOptions &options) {
+  return guard([&] {
+    CYLON_CHECK(paths.size() == ids.size(), Code::Invalid, paths.size() << " paths for " << ids.size() << " ids");
+    auto ts = io::ReadCSVs(ctx, paths, options);
+    for (size_t i = 0; i < ts.size(); ++i) PutTable(ids[i], ts[i]);
+  });
+}
+Status WriteCSV(const std::string &id, const std::string &path, const io::CSVWriteOptions &options) {
+  return guard([&] { io::WriteCSV(GetTable(id), path, options); });
+}
+Status ReadParquet(const std::shared_ptr<CylonContext> &ctx, const std::string &path, const std::string &id,
+                   const io::ParquetOptions &options) {
+  return guard([&] { PutTable(id, io::ReadParquet(ctx, path, options)); });
+}
+Status ReadParquet(const std::shared_ptr<CylonContext> &ctx, const std::vector<std::string> &paths,
+                   const std::vector<std::string> &ids, const io::ParquetOptions &options) {
+  return guard([&] {
+    CYLON_CHECK(paths.size() == ids.size(), Code::Invalid, paths.size() << " paths for " << ids.size() << " ids");
+    auto ts = io::ReadParquets(ctx, paths, options);
+    for (size_t i = 0; i < ts.size(); ++i) PutTable(ids[i], ts[i]);
+  });
+}
+Status WriteParquet(const std::string &id, const std::string &path, const io::ParquetOptions &options) {
+  return guard([&] { io::WriteParquet(GetTable(id), path, options); });
+}
+Status SubtractTables(const std::string &a, const std::string &b, const std::string &dest, bool distributed) {
+  return guard([&] {
+    PutTable(dest, distributed ? ops::DistributedSubtract(GetTable(a), GetTable(b)) : ops::Subtract(GetTable(a), GetTable(b)));
+  });
+}
+Status IntersectTables(const std::string &a, const std::string &b, const std::string &dest, bool distributed) {
+  return guard([&] {
+    PutTable(dest, distributed ? ops::DistributedIntersect(GetTable(a), GetTable(b))
+                               : ops::Intersect(GetTable(a), GetTable(b)));
+  });
+}
+Status MergeTables(const std::vector<std::string> &ids, const std::string &dest) {
+  return guard([&] {
+    std::vector<TablePtr> ts;
+    for (const auto &id : ids) ts.push_back(GetTable(id));
+    PutTable(dest, ops::Merge(ts));
+  });
+}
+Status HashPartitionTable(const std::string &id, const std::vector<int> &hash_columns, int num_partitions,
+                          std::unordered_map<int, std::string> *out) {
+  return guard([&] {
+    auto parts = ops::HashPartition(GetTable(id), hash_columns, (uint32_t)num_partitions);
+    for (size_t p = 0; p < parts.size(); ++p) {
+      const std::string pid = id + "_" + std::to_string(p);
+      PutTable(pid, parts[p]);
+      if (out) (*out)[(int)p] = pid;
+    }
+  });
+}
+Status SelectTable(const std::string &id, const std::function<bool(const Row &)> &selector, const std::string &dest) {
+  TablePtr out;
+  Status s = guard([&] { GetTable(id); });
+  if (!s.is_ok()) return s;
+  s = Select(GetTable(id), selector, out);
+  if (s.is_ok()) PutTable(dest, out);
+  return s;
+}
+Status ProjectTable(const std::string &id, const std::vector<int64_t> &columns, const std::string &dest) {
+  return guard([&] {
+    std::vector<int> cols(columns.begin(), columns.end());
+    PutTable(dest, ops::Project(GetTable(id), cols));
+  });
+}
+Status PrintToOStream(const TablePtr &t, int col1, int col2, int64_t row1, int64_t row2, std::ostream &out,
+                      char delimiter, bool use_custom_header, const std::vector<std::string> &headers) {
+  return guard([&] { io::PrintToOStream(t, col1, col2, row1, row2, out, delimiter, use_custom_header, headers); });
+}
+Status Print(const TablePtr &t, int col1, int col2, int64_t row1, int64_t row2) {
+  return PrintToOStream(t, col1, col2, row1, row2, std::cout);
+}
+Status Print(const std::string &id, int col1, int col2, int64_t row1, int64_t row2) {
+  return guard([&] { io::PrintToOStream(GetTable(id), col1, col2, row1, row2, std::cout); });
+}
+Status PrintToOStream(const std::string &id, int col1, int col2, int64_t row1, int64_t row2, std::ostream &out,
+                      char delimiter, bool use_custom_header, const std::vector<std::string> &headers) {
+  return guard([&] {
+    io::PrintToOStream(GetTable(id), col1, col2, row1, row2, out, delimiter, use_custom_header, headers);
+  });
+}
 
 // ---- TableAllToAll --------------------------------------------------------------------
 TableAllToAll::TableAllToAll(std::shared_ptr<CylonContext> ctx, TableCallback callback)

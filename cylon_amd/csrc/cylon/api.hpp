@@ -10,7 +10,9 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <ostream>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "io/arrow_io.hpp"
@@ -72,18 +74,37 @@ Status FromParquet(const std::shared_ptr<CylonContext> &ctx, const std::vector<s
 Status WriteParquet(const TablePtr &t, const std::string &path,
                     const io::ParquetOptions &options = io::ParquetOptions());
 
-// Row-predicate selection (reference table.cpp:504-529): the predicate sees a host Row view.
+// Row-predicate selection (reference table.cpp:504-529, row.hpp:23-52): the predicate
+// sees a host Row view; accessors read the host buffers directly (no per-row allocation).
 class Row {
  public:
   Row(const TablePtr &host_table, int64_t row) : t_(host_table), row_(row) {}
+  void SetIndex(int64_t row) { row_ = row; }
   int64_t RowIndex() const { return row_; }
   bool IsNull(int col) const;
-  int64_t GetInt64(int col) const;  // any integer / temporal type, sign-extended
-  double GetDouble(int col) const;  // any numeric type
+  int8_t GetInt8(int col) const { return (int8_t)GetInt64(col); }
+  uint8_t GetUInt8(int col) const { return (uint8_t)GetUInt64(col); }
+  int16_t GetInt16(int col) const { return (int16_t)GetInt64(col); }
+  uint16_t GetUInt16(int col) const { return (uint16_t)GetUInt64(col); }
+  int32_t GetInt32(int col) const { return (int32_t)GetInt64(col); }
+  uint32_t GetUInt32(int col) const { return (uint32_t)GetUInt64(col); }
+  int64_t GetInt64(int col) const;    // any integer / temporal type, sign-extended
+  uint64_t GetUInt64(int col) const;  // any integer type, zero-extended
+  float GetHalfFloat(int col) const { return (float)GetDouble(col); }
+  float GetFloat(int col) const { return (float)GetDouble(col); }
+  double GetDouble(int col) const;    // any numeric type
   bool GetBool(int col) const;
   std::string GetString(int col) const;
+  const uint8_t *GetFixedBinary(int col) const;  // FIXED_SIZE_BINARY / DECIMAL bytes
+  int32_t GetDate32(int col) const { return (int32_t)GetInt64(col); }
+  int64_t GetDate64(int col) const { return GetInt64(col); }
+  int64_t GetTimestamp(int col) const { return GetInt64(col); }
+  int32_t Time32(int col) const { return (int32_t)GetInt64(col); }
+  int64_t Time64(int col) const { return GetInt64(col); }
+  const uint8_t *Decimal(int col) const { return GetFixedBinary(col); }
 
  private:
+  const uint8_t *raw(int col, int *width) const;
   TablePtr t_;
   int64_t row_;
 };
@@ -103,6 +124,13 @@ Status Max(const TablePtr &t, int32_t col, TablePtr &out);
 Status MinMax(const TablePtr &t, int32_t col, TablePtr &out);  // 1 row, columns min, max
 }  // namespace compute
 
+// ---- printing (reference table.hpp Print / PrintToOStream) -----------------------------
+// columns [col1, col2) x rows [row1, row2) as delimited text; negative ends = to the last one
+Status PrintToOStream(const TablePtr &t, int col1, int col2, int64_t row1, int64_t row2, std::ostream &out,
+                      char delimiter = ',', bool use_custom_header = false,
+                      const std::vector<std::string> &headers = {});
+Status Print(const TablePtr &t, int col1 = 0, int col2 = -1, int64_t row1 = 0, int64_t row2 = -1);
+
 // ---- string-ID table registry (reference table_api.cpp:34-61) --------------------
 void PutTable(const std::string &id, const TablePtr &table);
 TablePtr GetTable(const std::string &id);
@@ -116,6 +144,33 @@ Status UnionTables(const std::string &a, const std::string &b, const std::string
 Status SortTable(const std::string &id, int col, const std::string &dest, bool ascending);
 int64_t RowCount(const std::string &id);
 int32_t ColumnCount(const std::string &id);
+std::vector<std::string> ColumnNames(const std::string &id);
+// registry versions of the remaining table_api.hpp calls (reference table_api.hpp:40-195)
+Status ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &path, const std::string &id,
+               const io::CSVReadOptions &options = io::CSVReadOptions());
+Status ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::vector<std::string> &paths,
+               const std::vector<std::string> &ids, const io::CSVReadOptions &options = io::CSVReadOptions());
+Status WriteCSV(const std::string &id, const std::string &path,
+                const io::CSVWriteOptions &options = io::CSVWriteOptions());
+Status ReadParquet(const std::shared_ptr<CylonContext> &ctx, const std::string &path, const std::string &id,
+                   const io::ParquetOptions &options = io::ParquetOptions());
+Status ReadParquet(const std::shared_ptr<CylonContext> &ctx, const std::vector<std::string> &paths,
+                   const std::vector<std::string> &ids, const io::ParquetOptions &options = io::ParquetOptions());
+Status WriteParquet(const std::string &id, const std::string &path,
+                    const io::ParquetOptions &options = io::ParquetOptions());
+Status SubtractTables(const std::string &a, const std::string &b, const std::string &dest, bool distributed);
+Status IntersectTables(const std::string &a, const std::string &b, const std::string &dest, bool distributed);
+Status MergeTables(const std::vector<std::string> &ids, const std::string &dest);
+// partition p -> id "<id>_<p>" registered and returned in *out
+Status HashPartitionTable(const std::string &id, const std::vector<int> &hash_columns, int num_partitions,
+                          std::unordered_map<int, std::string> *out);
+Status SelectTable(const std::string &id, const std::function<bool(const Row &)> &selector,
+                   const std::string &dest);
+Status ProjectTable(const std::string &id, const std::vector<int64_t> &columns, const std::string &dest);
+Status Print(const std::string &id, int col1, int col2, int64_t row1, int64_t row2);
+Status PrintToOStream(const std::string &id, int col1, int col2, int64_t row1, int64_t row2, std::ostream &out,
+                      char delimiter = ',', bool use_custom_header = false,
+                      const std::vector<std::string> &headers = {});
 
 // ---- table all-to-all with the reference's insert/finish/isComplete protocol ----
 // (arrow/arrow_all_to_all.hpp:101-253).  Tables inserted per target are batched;

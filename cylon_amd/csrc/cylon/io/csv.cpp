@@ -460,31 +460,27 @@ void put_escaped(std::string &out, const char *p, size_t len, char delim) {
 }
 }  // namespace
 
-void WriteCSV(const TablePtr &table, const std::string &path, const CSVWriteOptions &opts) {
-  TablePtr t = table->device().is_cuda() ? table->to(at::Device(at::kCPU)) : table;
-  std::ofstream f(path, std::ios::binary);
-  CYLON_CHECK(f.good(), Code::IOError, "cannot open " << path << " for writing");
-  std::vector<std::string> names = opts.column_names.empty() ? t->ColumnNames() : opts.column_names;
-  CYLON_CHECK((int)names.size() == t->Columns(), Code::Invalid, "CSV header has " << names.size() << " names for "
-                                                                                   << t->Columns() << " columns");
+// CSV text of columns [col1, col2) and rows [row1, row2) of a host table
+static void write_csv_rows(const TablePtr &t, int col1, int col2, int64_t row1, int64_t row2, char delim,
+                           const std::vector<std::string> &names, std::ostream &f) {
   std::string out;
-  for (size_t i = 0; i < names.size(); ++i) {
-    if (i) out.push_back(opts.delimiter);
+  for (int i = col1; i < col2; ++i) {
+    if (i > col1) out.push_back(delim);
     out.push_back('"');
-    out += names[i];
+    out += names[i - col1];
     out.push_back('"');
   }
   out.push_back('\n');
   char buf[64];
-  for (int64_t r = 0; r < t->Rows(); ++r) {
-    for (int c = 0; c < t->Columns(); ++c) {
-      if (c) out.push_back(opts.delimiter);
+  for (int64_t r = row1; r < row2; ++r) {
+    for (int c = col1; c < col2; ++c) {
+      if (c > col1) out.push_back(delim);
       const Column &col = t->column(c);
       if (col.nullable() && col.validity.data_ptr<uint8_t>()[r] == 0) continue;
       const uint8_t *d = static_cast<const uint8_t *>(col.data.data_ptr());
       if (col.is_var()) {
         const int64_t *o = col.offsets.data_ptr<int64_t>();
-        put_escaped(out, reinterpret_cast<const char *>(d) + o[r], (size_t)(o[r + 1] - o[r]), opts.delimiter);
+        put_escaped(out, reinterpret_cast<const char *>(d) + o[r], (size_t)(o[r + 1] - o[r]), delim);
         continue;
       }
       const int w = col.type.width();
@@ -512,7 +508,7 @@ void WriteCSV(const TablePtr &table, const std::string &path, const CSVWriteOpti
                               : reinterpret_cast<const uint64_t *>(d)[r];
         res = std::to_chars(buf, buf + sizeof(buf), x);
       } else {
-        CYLON_THROW(Code::NotImplemented, "WriteCSV: unsupported column type " << col.type.ToString());
+        CYLON_THROW(Code::NotImplemented, "CSV text: unsupported column type " << col.type.ToString());
       }
       out.append(buf, res.ptr);
     }
@@ -523,7 +519,37 @@ void WriteCSV(const TablePtr &table, const std::string &path, const CSVWriteOpti
     }
   }
   f.write(out.data(), (std::streamsize)out.size());
+}
+
+void WriteCSV(const TablePtr &table, const std::string &path, const CSVWriteOptions &opts) {
+  TablePtr t = table->device().is_cuda() ? table->to(at::Device(at::kCPU)) : table;
+  std::ofstream f(path, std::ios::binary);
+  CYLON_CHECK(f.good(), Code::IOError, "cannot open " << path << " for writing");
+  std::vector<std::string> names = opts.column_names.empty() ? t->ColumnNames() : opts.column_names;
+  CYLON_CHECK((int)names.size() == t->Columns(), Code::Invalid, "CSV header has " << names.size() << " names for "
+                                                                                   << t->Columns() << " columns");
+  write_csv_rows(t, 0, t->Columns(), 0, t->Rows(), opts.delimiter, names, f);
   CYLON_CHECK(f.good(), Code::IOError, "write failed: " << path);
+}
+
+void PrintToOStream(const TablePtr &table, int col1, int col2, int64_t row1, int64_t row2, std::ostream &out,
+                    char delimiter, bool use_custom_header, const std::vector<std::string> &headers) {
+  col2 = col2 < 0 ? table->Columns() : std::min(col2, table->Columns());
+  row2 = row2 < 0 ? table->Rows() : std::min(row2, table->Rows());
+  col1 = std::max(0, std::min(col1, col2));
+  row1 = std::max<int64_t>(0, std::min(row1, row2));
+  // only the printed rows travel to the host
+  TablePtr t = table->device().is_cuda() ? ops::Slice(table, row1, row2 - row1)->to(at::Device(at::kCPU))
+                                         : ops::Slice(table, row1, row2 - row1);
+  std::vector<std::string> names;
+  if (use_custom_header) {
+    CYLON_CHECK((int)headers.size() == col2 - col1, Code::Invalid,
+                "custom header has " << headers.size() << " names for " << (col2 - col1) << " columns");
+    names = headers;
+  } else {
+    for (int c = col1; c < col2; ++c) names.push_back(t->column(c).name);
+  }
+  write_csv_rows(t, col1, col2, 0, t->Rows(), delimiter, names, out);
 }
 
 }  // namespace io

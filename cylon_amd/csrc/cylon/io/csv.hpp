@@ -13,6 +13,7 @@
 // spellings follow Arrow's and string columns are never null unless
 // strings_can_be_null is set.
 #pragma once
+#include <ostream>
 #include <string>
 #include <vector>
 
@@ -49,6 +50,11 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
 std::vector<TablePtr> ReadCSVs(const std::shared_ptr<CylonContext> &ctx, const std::vector<std::string> &paths,
                                const CSVReadOptions &opts);
 void WriteCSV(const TablePtr &table, const std::string &path, const CSVWriteOptions &opts);
+// columns [col1, col2) x rows [row1, row2) as CSV text (negative ends = to the last one);
+// reference table.hpp PrintToOStream / Print
+void PrintToOStream(const TablePtr &table, int col1, int col2, int64_t row1, int64_t row2, std::ostream &out,
+                    char delimiter = ',', bool use_custom_header = false,
+                    const std::vector<std::string> &headers = {});
 
 }  // namespace io
 }  // namespace cylon

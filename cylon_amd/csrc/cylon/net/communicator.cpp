@@ -2,6 +2,7 @@
 // Reference call sites replaced here: SURVEY.md §2.5 M1-M8
 // (MPI_Init/Barrier/Finalize, MPI_Isend/Irecv header+payload, MPI_Allreduce).
 #include <atomic>
+#include <cstdlib>
 #include <chrono>
 #include <thread>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
@@ -53,6 +54,13 @@ ProcessGroupCommunicator::ProcessGroupCommunicator(c10::intrusive_ptr<c10d::Proc
 
 ProcessGroupCommunicator::~ProcessGroupCommunicator() = default;
 
+void ProcessGroupCommunicator::Finalize() { pg_.reset(); }
+
+c10d::ProcessGroup &ProcessGroupCommunicator::pg() const {
+  CYLON_CHECK(pg_, Code::Invalid, "communicator used after finalize()");
+  return *pg_;
+}
+
 at::Tensor ProcessGroupCommunicator::to_comm(const at::Tensor &t) const {
   at::Tensor c = t.device() == device_ ? t : t.to(device_);
   // bool is not a collective dtype on every backend; move it as bytes
@@ -65,7 +73,7 @@ void ProcessGroupCommunicator::Barrier() {
   // identically for RCCL and gloo and orders with the current stream.
   at::Tensor t = at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(device_));
   std::vector<at::Tensor> v{t};
-  pg_->allreduce(v)->wait();
+  pg().allreduce(v)->wait();
   if (device_.is_cuda()) t.cpu();
 }
 
@@ -81,7 +89,7 @@ at::Tensor ProcessGroupCommunicator::AllToAllV(const at::Tensor &send, const std
   shape[0] = total;
   at::Tensor out = at::empty(shape, in.options());
   std::vector<int64_t> sc(send_counts), rc(recv_counts);
-  pg_->alltoall_base(out, in, rc, sc)->wait();
+  pg().alltoall_base(out, in, rc, sc)->wait();
   if (send.scalar_type() == at::kBool) out = out.view(at::kBool);
   return out.device() == send.device() ? out : out.to(send.device());
 }
@@ -91,7 +99,7 @@ std::vector<int64_t> ProcessGroupCommunicator::ExchangeCounts(const std::vector<
   at::Tensor s = at::tensor(send_counts, at::TensorOptions().dtype(at::kLong)).to(device_);
   at::Tensor r = at::empty({world_}, s.options());
   std::vector<int64_t> ones(world_, 1);
-  pg_->alltoall_base(r, s, ones, ones)->wait();
+  pg().alltoall_base(r, s, ones, ones)->wait();
   at::Tensor h = r.to(at::kCPU);
   return std::vector<int64_t>(h.data_ptr<int64_t>(), h.data_ptr<int64_t>() + world_);
 }
@@ -111,7 +119,7 @@ void ProcessGroupCommunicator::AllReduce(at::Tensor &t, ReduceOp op) {
   std::vector<at::Tensor> v{c};
   c10d::AllreduceOptions o;
   o.reduceOp = to_c10d(op);
-  pg_->allreduce(v, o)->wait();
+  pg().allreduce(v, o)->wait();
   if (!c.is_same(t)) t.copy_(c.view(t.scalar_type()));
 }
 
@@ -123,7 +131,7 @@ at::Tensor ProcessGroupCommunicator::AllGather(const at::Tensor &in) {
   shape[0] = n0 * world_;
   at::Tensor out = at::empty(shape, c.options());
   at::Tensor src = c.dim() == 0 ? c.reshape({1}) : c;
-  pg_->_allgather_base(out, src)->wait();
+  pg()._allgather_base(out, src)->wait();
   if (in.scalar_type() == at::kBool) out = out.view(at::kBool);
   return out.device() == in.device() ? out : out.to(in.device());
 }
@@ -133,7 +141,7 @@ void ProcessGroupCommunicator::Broadcast(at::Tensor &t, int root) {
   std::vector<at::Tensor> v{c};
   c10d::BroadcastOptions o;
   o.rootRank = root;
-  pg_->broadcast(v, o)->wait();
+  pg().broadcast(v, o)->wait();
   if (!c.is_same(t)) t.copy_(c.view(t.scalar_type()));
 }
 
@@ -234,7 +242,7 @@ std::pair<at::Tensor, std::shared_ptr<P2PRequest>> ProcessGroupCommunicator::All
   shape[0] = total;
   at::Tensor out = at::empty(shape, in.options());
   std::vector<int64_t> sc(send_counts), rc(recv_counts);
-  auto work = pg_->alltoall_base(out, in, rc, sc);
+  auto work = pg().alltoall_base(out, in, rc, sc);
   // the receive buffer is handed out in the caller's dtype/device once waited on
   at::Tensor user = out;
   if (send.scalar_type() == at::kBool) user = out.view(at::kBool);
@@ -242,6 +250,13 @@ std::pair<at::Tensor, std::shared_ptr<P2PRequest>> ProcessGroupCommunicator::All
     auto req = std::make_shared<PGRequest>(work, out, at::Tensor(), type_ != CommType::RCCL);
     req->Wait();
     return {user.to(send.device()), std::make_shared<DoneRequest>()};
+  }
+  if (type_ != CommType::RCCL) {
+    // gloo: complete the exchange before returning.  A gloo all-to-all left in flight
+    // while the caller issues further collectives deadlocked intermittently under CPU
+    // oversubscription (the CPU rehearsal path only needs the semantics, not overlap).
+    work->wait();
+    return {user, std::make_shared<DoneRequest>()};
   }
   // keep `in` alive until completion: c10d works hold their tensors
   return {user, std::make_shared<PGRequest>(work, out, at::Tensor(), type_ != CommType::RCCL)};
@@ -251,7 +266,7 @@ std::shared_ptr<P2PRequest> ProcessGroupCommunicator::ISend(const at::Tensor &t,
   CYLON_CHECK(dst >= 0 && dst < world_ && dst != rank_, Code::Invalid, "bad send target " << dst);
   at::Tensor c = to_comm(t);
   std::vector<at::Tensor> v{c};
-  return std::make_shared<PGRequest>(pg_->send(v, dst, tag), c, at::Tensor(), type_ != CommType::RCCL);
+  return std::make_shared<PGRequest>(pg().send(v, dst, tag), c, at::Tensor(), type_ != CommType::RCCL);
 }
 
 std::shared_ptr<P2PRequest> ProcessGroupCommunicator::IRecv(at::Tensor &t, int src, int tag) {
@@ -259,7 +274,7 @@ std::shared_ptr<P2PRequest> ProcessGroupCommunicator::IRecv(at::Tensor &t, int s
   at::Tensor c = to_comm(t);
   const bool staged = !(c.is_same(t));
   std::vector<at::Tensor> v{c};
-  return std::make_shared<PGRequest>(pg_->recv(v, src, tag), c, staged ? t : at::Tensor(), type_ != CommType::RCCL);
+  return std::make_shared<PGRequest>(pg().recv(v, src, tag), c, staged ? t : at::Tensor(), type_ != CommType::RCCL);
 }
 
 }  // namespace net

@@ -173,10 +173,14 @@ class ProcessGroupCommunicator : public Communicator {
   void Broadcast(at::Tensor &t, int root) override;
   std::shared_ptr<P2PRequest> ISend(const at::Tensor &t, int dst, int tag) override;
   std::shared_ptr<P2PRequest> IRecv(at::Tensor &t, int src, int tag) override;
+  // drops the ProcessGroup reference, so that torch.distributed.destroy_process_group()
+  // tears the group down deterministically (not at interpreter exit)
+  void Finalize() override;
   at::Device comm_device() const { return device_; }
 
  private:
   at::Tensor to_comm(const at::Tensor &t) const;
+  c10d::ProcessGroup &pg() const;
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;
   CommType type_;
   at::Device device_;

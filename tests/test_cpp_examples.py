@@ -12,9 +12,11 @@ EXE = os.path.join(ROOT, "examples", "cpp", "bin", "relational_example")
 
 
 def _ensure_built():
-    src = os.path.join(ROOT, "examples", "cpp", "relational_example.cpp")
-    lib = os.path.join(ROOT, "cylon_amd", "libcylon_amd.so")
-    if not os.path.exists(EXE) or os.path.getmtime(EXE) < max(os.path.getmtime(src), os.path.getmtime(lib)):
+    import glob
+    srcs = glob.glob(os.path.join(ROOT, "examples", "cpp", "*.cpp"))
+    exes = [os.path.join(ROOT, "examples", "cpp", "bin", os.path.basename(s)[:-4]) for s in srcs]
+    newest = max(os.path.getmtime(p) for p in srcs + [os.path.join(ROOT, "cylon_amd", "libcylon_amd.so")])
+    if any(not os.path.exists(e) or os.path.getmtime(e) < newest for e in exes):
         subprocess.run(["bash", os.path.join(ROOT, "examples", "cpp", "build.sh")], check=True, capture_output=True)
     return EXE
 
@@ -60,3 +62,44 @@ def test_cpp_example_on_gpu(tmp_path, data_dir):
     exp = _python_counts(CylonContext(device="cpu"), data_dir)
     for k, v in exp.items():
         assert got[k] == v, (k, got, exp)
+
+
+REG = os.path.join(ROOT, "examples", "cpp", "bin", "registry_example")
+
+
+def _run_registry(device, tmp_path, data_dir):
+    if device == "cpu":
+        _ensure_built()
+    r = subprocess.run([REG, device, os.path.join(data_dir, "input", "csv1_0.csv"),
+                        os.path.join(data_dir, "input", "csv2_0.csv"), str(tmp_path)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return dict((k, int(v)) for k, v in (line.split() for line in r.stdout.splitlines()))
+
+
+def _check_registry(got, ctx, data_dir):
+    from cylon_amd.io import read_csv
+    a = read_csv(ctx, os.path.join(data_dir, "input", "csv1_0.csv"))
+    b = read_csv(ctx, os.path.join(data_dir, "input", "csv2_0.csv"))
+    first = a.to_pandas().iloc[:, 0]
+    exp = {"a": a.row_count, "b": b.row_count, "j": a.join(b, "inner", "hash", on=[0]).row_count,
+           "s": a.subtract(b).row_count, "i": a.intersect(b).row_count, "m": a.row_count + b.row_count,
+           "sel": int((first % 2 == 0).sum()), "partitions": 3, "partition_rows": a.row_count, "p_columns": 2,
+           "printed_lines": 1 + min(3, a.join(b, "inner", "hash", on=[0]).row_count)}
+    for k, v in exp.items():
+        assert got[k] == v, (k, got, exp)
+    assert got["p"] == got["j"] == got["j2"]
+    if got["sel"]:
+        assert got["sel_first_even"] == 1
+
+
+def test_cpp_registry_example_on_cpu(ctx, tmp_path, data_dir):
+    _check_registry(_run_registry("cpu", tmp_path, data_dir), ctx, data_dir)
+
+
+@pytest.mark.gpu
+def test_cpp_registry_example_on_gpu(tmp_path, data_dir):
+    from cylon_amd import CylonContext
+    if not os.path.exists(REG):
+        pytest.fail("examples/cpp/bin/registry_example missing: run __graft_entry__.build()")
+    _check_registry(_run_registry("cuda:0", tmp_path, data_dir), CylonContext(device="cpu"), data_dir)
