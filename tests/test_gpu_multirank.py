@@ -17,7 +17,8 @@ SMALL_RADIX = {"CYLON_RADIX_JOIN_MIN_ROWS": "1024"}  # radix join (and its sink)
 
 
 def _canon(df):
-    return sorted(tuple("nan" if (isinstance(x, float) and np.isnan(x)) else x for x in r)
+    # nulls / NaN -> one sortable sentinel (the test data has no infinities)
+    return sorted(tuple(float("-inf") if (isinstance(x, float) and np.isnan(x)) else x for x in r)
                   for r in df.itertuples(index=False))
 
 
@@ -114,3 +115,47 @@ def test_distributed_ops_on_device():
     for op, rows in expect.items():
         got = [tuple(x) for r in res for x in r[5][op].to_numpy().tolist()]
         assert len(got) == len(set(got)) and set(got) == rows, op
+
+
+def _join_edge_cases(ctx, case):
+    import torch
+    from cylon_amd import Table
+    from cylon_amd._lib import C
+    rank = ctx.get_rank()
+    g = torch.Generator(device="cuda").manual_seed(50 + rank)
+    n = 40_000
+    if case == "skew":  # one hot key on the (smaller) build side overflows the LDS capacity -> fallback
+        k = torch.randint(0, 5000, (n,), generator=g, device="cuda")
+        m = n // 4
+        kb = torch.where(torch.rand(m, generator=g, device="cuda") < 0.3, torch.zeros(m, dtype=torch.int64, device="cuda"),
+                         torch.randint(1, 5000, (m,), generator=g, device="cuda"))
+    else:
+        k = torch.randint(0, 60_000, (n,), generator=g, device="cuda")
+        kb = torch.randint(0, 60_000, (n if rank == 0 else 0,), generator=g, device="cuda")  # rank 1: empty right
+    v = torch.rand(n, generator=g, device="cuda", dtype=torch.float64)
+    a = Table.from_torch(ctx, {"k": k, "v": v})
+    if case == "nulls":  # nullable payload through the radix sink
+        import pyarrow as pa
+        at = a.to_arrow()
+        mask = (at.column("v").to_numpy() < 0.2)
+        a = Table(pa.table({"k": at.column("k"), "v": pa.array(at.column("v").to_numpy(), mask=mask)}), ctx)
+    b = Table.from_torch(ctx, {"k": kb, "w": torch.rand(kb.numel(), generator=g, device="cuda", dtype=torch.float64)})
+    ctx.add_config("shuffle_chunks", "3")
+    C.trace_enable(True)
+    C.trace_reset()
+    out = a.distributed_join(b, "inner", "hash", on=["k"], left_prefix="l_", right_prefix="r_")
+    c = dict(C.trace_counters())
+    return out.to_pandas(), a.to_pandas(), b.to_pandas(), c
+
+
+@pytest.mark.parametrize("case", ["skew", "empty_rank", "nulls"])
+def test_chunked_join_edge_cases_on_device(case):
+    res = run_distributed(_join_edge_cases, 2, case, device=DEV, env=SMALL_RADIX)
+    got = pd.concat([r[0] for r in res])
+    a = pd.concat([r[1] for r in res])
+    b = pd.concat([r[2] for r in res])
+    ref = a.add_prefix("l_").merge(b.add_prefix("r_"), left_on="l_k", right_on="r_k")
+    assert len(got) == len(ref)
+    assert _canon(got[sorted(got.columns)]) == _canon(ref[sorted(got.columns)])
+    if case == "skew":
+        assert any(r[3].get("join.radix.overflow_fallback", 0) > 0 for r in res)
