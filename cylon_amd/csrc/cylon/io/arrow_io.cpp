@@ -269,7 +269,7 @@ TablePtr ReadParquet(const std::shared_ptr<CylonContext> &ctx, const std::string
   reader->set_use_threads(opts.use_threads);
   std::shared_ptr<arrow::Table> t;
   if (opts.columns.empty()) {
-    check(reader->ReadTable(&t), "read parquet");
+    t = ok_or_throw(reader->ReadTable(), "read parquet");
   } else {
     std::shared_ptr<arrow::Schema> schema;
     check(reader->GetSchema(&schema), "parquet schema");
@@ -279,7 +279,7 @@ TablePtr ReadParquet(const std::shared_ptr<CylonContext> &ctx, const std::string
       CYLON_CHECK(i >= 0, Code::KeyError, "parquet file " << path << " has no column " << name);
       idx.push_back(i);
     }
-    check(reader->ReadTable(idx, &t), "read parquet");
+    t = ok_or_throw(reader->ReadTable(idx), "read parquet");
   }
   return FromArrowTable(ctx, t);
 }

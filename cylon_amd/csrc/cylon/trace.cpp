@@ -77,12 +77,11 @@ Phase::Phase(const char *name, const at::Device &dev) : name_(name) {
     dev_ = dev.index();
     hipStream_t s = c10::hip::getCurrentHIPStream(dev.index()).stream();
     hipEvent_t a, b;
-    if (hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess) {
-      hipEventRecord(a, s);
+    if (hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess && hipEventRecord(a, s) == hipSuccess) {
       start_ = a;
       stop_ = b;
     } else {
-      gpu_ = false;
+      gpu_ = false;  // timing falls back to the host clock
     }
   }
   if (!gpu_) t0_ns_ = now_ns();
@@ -92,10 +91,13 @@ Phase::~Phase() {
   if (!active_) return;
   roctxRangePop();
   std::lock_guard<std::mutex> lk(g_mu);
-  if (gpu_) {
-    hipStream_t s = c10::hip::getCurrentHIPStream(dev_).stream();
-    hipEventRecord(static_cast<hipEvent_t>(stop_), s);
+  hipStream_t s = gpu_ ? c10::hip::getCurrentHIPStream(dev_).stream() : nullptr;
+  if (gpu_ && hipEventRecord(static_cast<hipEvent_t>(stop_), s) == hipSuccess) {
     pending().push_back({name_, static_cast<hipEvent_t>(start_), static_cast<hipEvent_t>(stop_)});
+  } else if (gpu_) {
+    (void)hipEventDestroy(static_cast<hipEvent_t>(start_));
+    (void)hipEventDestroy(static_cast<hipEvent_t>(stop_));
+    stats()[name_].calls++;  // counted, not timed
   } else {
     auto &st = stats()[name_];
     st.total_ms += (now_ns() - t0_ns_) / 1e6;
@@ -112,14 +114,14 @@ void add_counter(const std::string &name, int64_t value) {
 std::map<std::string, PhaseStat> phases() {
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto &p : pending()) {
-    hipEventSynchronize(p.stop);
     float ms = 0;
-    hipEventElapsedTime(&ms, p.start, p.stop);
+    if (hipEventSynchronize(p.stop) != hipSuccess || hipEventElapsedTime(&ms, p.start, p.stop) != hipSuccess)
+      ms = 0;  // a failed query leaves the phase counted but untimed
     auto &st = stats()[p.name];
     st.total_ms += ms;
     st.calls++;
-    hipEventDestroy(p.start);
-    hipEventDestroy(p.stop);
+    (void)hipEventDestroy(p.start);
+    (void)hipEventDestroy(p.stop);
   }
   pending().clear();
   return stats();
