@@ -16,6 +16,8 @@
 //   3. outer completion: matched flags (mark_indices) + compaction of the
 //      unmatched rows of the preserved side(s), appended with -1 partners.
 //   4. materialisation: one fused gather launch per side (K4).
+#include <limits>
+
 #include "util.hpp"
 #include "../trace.hpp"
 
@@ -416,9 +418,69 @@ static std::pair<at::Tensor, at::Tensor> join_impl(TablePtr left, TablePtr right
   return {li, ri};
 }
 
+// K7 sort-merge join on row-sorted tables (device, large inner joins on one exact
+// integer key, algorithm = SORT).  Both relations are first sorted by the key with
+// the row-moving LSD passes of ops::Sort (every column moves with the key, constant
+// key bits skipped), so the merge's index pairs are monotone in both tables and
+// the final gathers stream through HBM instead of touching it at random (the
+// pair-sort + gather form spends most of its time in those random gathers).  The
+// output comes out ordered by key, as the reference's sort join does.
+static TablePtr sorted_merge_join(const Exec &ex, const TablePtr &left, const TablePtr &right,
+                                  const JoinConfig &cfg) {
+  const int lc = cfg.GetLeftColumnIdx()[0], rc = cfg.GetRightColumnIdx()[0];
+  TablePtr ls, rs;
+  {
+    CYLON_PHASE("join.sortmerge.sort", ex.device);
+    ls = Sort(left, {lc}, {true});
+    rs = Sort(right, {rc}, {true});
+  }
+  // merge_join_* compare keys as uint64: the sign-flipped image of a signed key is
+  // ordered like the key itself
+  auto image = [&](const TablePtr &t, int c) {
+    KeyEncoding k = encode_keys(ex, t, {c}, true);
+    return t->column(c).type.kind() == ValueKind::SIGNED_INT
+               ? at::bitwise_xor(k.keys, at::full({1}, std::numeric_limits<int64_t>::min(), k.keys.options()))
+               : k.keys;
+  };
+  at::Tensor lk = image(ls, lc), rk = image(rs, rc);
+  const int64_t nl = ls->Rows(), nr = rs->Rows();
+  at::Tensor li, ri;
+  {
+    CYLON_PHASE("join.sortmerge.merge", ex.device);
+    at::Tensor lo = ex.empty_i64(nl), counts = ex.empty_i64(nl);
+    KCALL(ex, merge_join_count, reinterpret_cast<const uint64_t *>(ptr<int64_t>(lk)), nl,
+          reinterpret_cast<const uint64_t *>(ptr<int64_t>(rk)), nr, ptr<int64_t>(lo), ptr<int64_t>(counts));
+    at::Tensor offs = exclusive_scan(ex, counts);
+    const int64_t m = read_i64(offs, nl);
+    at::Tensor lperm = ex.empty_i64(nl), rperm = ex.empty_i64(nr);
+    KCALL(ex, iota, ptr<int64_t>(lperm), nl, 0);
+    KCALL(ex, iota, ptr<int64_t>(rperm), nr, 0);
+    li = ex.empty_i64(m);
+    ri = ex.empty_i64(m);
+    KCALL(ex, merge_join_write, ptr<int64_t>(lperm), nl, ptr<int64_t>(rperm), ptr<int64_t>(lo), ptr<int64_t>(offs),
+          ptr<int64_t>(li), ptr<int64_t>(ri));
+  }
+  CYLON_PHASE("join.sortmerge.materialize", ex.device);
+  TablePtr lo = GatherNullable(ls, li, false);
+  TablePtr ro = GatherNullable(rs, ri, false);
+  std::vector<Column> cols;
+  for (const auto &c : lo->columns()) cols.push_back(c.with_name(cfg.GetLeftTablePrefix() + c.name));
+  for (const auto &c : ro->columns()) cols.push_back(c.with_name(cfg.GetRightTablePrefix() + c.name));
+  trace::add_counter("join.sortmerge.rows_out", li.numel());
+  return Table::Make(left->GetContext(), std::move(cols));
+}
+
 // Local join.  With a sink (chunked distributed join) the radix path writes into
 // the sink and nullptr is returned; other paths return their table.
 static TablePtr join_local(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg, JoinSink *sink) {
+  if (left->device().is_cuda() && cfg.GetType() == JoinType::INNER && cfg.GetAlgorithm() == JoinAlgorithm::SORT &&
+      cfg.GetLeftColumnIdx().size() == 1 && std::min(left->Rows(), right->Rows()) >= radix_join_min_rows() &&
+      radix_eligible(left) && radix_eligible(right)) {
+    const Column &a = left->column(cfg.GetLeftColumnIdx()[0]);
+    const Column &b = right->column(cfg.GetRightColumnIdx()[0]);
+    if (simple_key(a) && simple_key(b) && a.type == b.type && a.type.kind() != ValueKind::FLOAT)
+      return sorted_merge_join(Exec(left->device()), left, right, cfg);
+  }
   if (left->device().is_cuda() && cfg.GetType() == JoinType::INNER && cfg.GetAlgorithm() == JoinAlgorithm::HASH &&
       cfg.GetLeftColumnIdx().size() == 1 && std::min(left->Rows(), right->Rows()) >= radix_join_min_rows() &&
       radix_eligible(left) && radix_eligible(right)) {

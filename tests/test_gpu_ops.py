@@ -219,3 +219,26 @@ def test_native_parquet_to_and_from_hbm(gpu_ctx, tmp_path):
     assert t.device.startswith("cuda") and t.to_arrow().equals(at)
     write_parquet(t.sort("k"), str(tmp_path / "o.parquet"))
     assert pq.read_table(str(tmp_path / "o.parquet")).column("k").to_pylist() == [1, 3, None]
+
+
+def test_sorted_merge_join_matches_cpu(gpu_ctx, ctx, monkeypatch):
+    """algorithm="sort" on the device: row-sorted tables + monotone merge (forced on small inputs);
+    same rows as the CPU twin, output ordered by key."""
+    from cylon_amd._lib import C
+    monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", "1")
+    monkeypatch.setenv("CYLON_RADIX_SORT_MIN_ROWS", "1")
+    rng = np.random.default_rng(12)
+    a = pa.table({"k": rng.integers(-3000, 3000, 40_000), "x": rng.random(40_000),
+                  "i": pa.array(rng.integers(0, 9, 40_000).astype(np.int32))})
+    b = pa.table({"k": rng.integers(-3000, 3000, 25_000), "y": rng.random(25_000)})
+    C.trace_enable(True)
+    C.trace_reset()
+    g = Table(a, gpu_ctx).join(Table(b, gpu_ctx), "inner", "sort", on=["k"], left_prefix="l_",
+                               right_prefix="r_").to_pandas()
+    assert C.trace_counters().get("join.sortmerge.rows_out", 0) == len(g)
+    C.trace_enable(False)
+    c = Table(a, ctx).join(Table(b, ctx), "inner", "sort", on=["k"], left_prefix="l_", right_prefix="r_").to_pandas()
+    assert len(g) == len(c) > 0
+    assert np.all(np.diff(g["l_k"].to_numpy()) >= 0)
+    key = lambda df: sorted(map(tuple, df[sorted(df.columns)].to_numpy().tolist()))
+    assert key(g) == key(c)
