@@ -174,16 +174,109 @@ __device__ __forceinline__ int64_t upper_bound_u64(const uint64_t *a, int64_t n,
   return lo;
 }
 
-__global__ void k_merge_count(const uint64_t *__restrict__ lk, int64_t nl, const uint64_t *__restrict__ rk,
-                              int64_t nr, int64_t *__restrict__ lo_out, int64_t *__restrict__ counts) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) {
-    const uint64_t v = lk[i];
-    const int64_t lo = lower_bound_u64(rk, nr, v);
-    const int64_t hi = (lo < nr && rk[lo] == v) ? upper_bound_u64(rk + lo, nr - lo, v) + lo : lo;
-    lo_out[i] = lo;
-    counts[i] = hi - lo;
+// Both key arrays are sorted, so a tile of 2048 consecutive left keys matches a
+// contiguous right window [lb(first), ub(last)). k_merge_bounds finds each tile's
+// window with two global binary searches (one thread per tile, all tiles in
+// parallel); k_merge_count stages the tile and, when it fits, the window in LDS,
+// and each thread walks its 8 consecutive left keys with a forward pointer
+// (galloping to a binary search after a few steps, so sparse/dense mixes stay
+// O(log) per key). This replaces one 30-step random-access global binary search
+// per left row (72 ms at 1B x 1B) with two streaming reads.
+constexpr int kMJThreads = 256;
+constexpr int kMJPerThread = 8;
+constexpr int kMJTile = kMJThreads * kMJPerThread;
+constexpr int kMJWindow = 4096;
+
+__device__ __forceinline__ int mj_pad(int i) { return i + i / kMJPerThread; }  // +1 slot per thread: no bank clash
+
+// the window bounds of tile b are parked in lo_out[b*T] / counts[b*T]: only block b
+// reads them, before it overwrites them
+__global__ void k_merge_bounds(const uint64_t *__restrict__ lk, int64_t nl, const uint64_t *__restrict__ rk,
+                               int64_t nr, int64_t *__restrict__ lo_out, int64_t *__restrict__ counts) {
+  const int64_t tiles = (nl + kMJTile - 1) / kMJTile;
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= tiles) return;
+  const int64_t base = b * kMJTile;
+  const int64_t last = (base + kMJTile < nl ? base + kMJTile : nl) - 1;
+  const uint64_t first_key = lk[base], last_key = lk[last];
+  lo_out[base] = lower_bound_u64(rk, nr, first_key);
+  counts[base] = upper_bound_u64(rk, nr, last_key);
+}
+
+template <typename RP>
+__device__ __forceinline__ void mj_walk(const uint64_t *lt, RP rw, int64_t wn, int r0, int rows, int64_t *lo_v,
+                                        int64_t *c_v) {
+  if (r0 >= rows) return;
+  int64_t p = 0;
+  {
+    int64_t hi = wn;
+    const uint64_t v = lt[mj_pad(r0)];
+    while (p < hi) {
+      const int64_t mid = (p + hi) >> 1;
+      if (rw[mid] < v) p = mid + 1; else hi = mid;
+    }
   }
+#pragma unroll
+  for (int j = 0; j < kMJPerThread; ++j) {
+    if (r0 + j < rows) {
+      const uint64_t v = lt[mj_pad(r0 + j)];
+      int step = 0;
+      while (p < wn && rw[p] < v && step < 4) { ++p; ++step; }
+      if (p < wn && rw[p] < v) {
+        int64_t hi = wn;
+        while (p < hi) {
+          const int64_t mid = (p + hi) >> 1;
+          if (rw[mid] < v) p = mid + 1; else hi = mid;
+        }
+      }
+      int64_t q = p;
+      step = 0;
+      while (q < wn && rw[q] == v && step < 4) { ++q; ++step; }
+      if (q < wn && rw[q] == v) {
+        int64_t hi = wn;
+        while (q < hi) {
+          const int64_t mid = (q + hi) >> 1;
+          if (rw[mid] <= v) q = mid + 1; else hi = mid;
+        }
+      }
+      lo_v[j] = p;
+      c_v[j] = q - p;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kMJThreads) void k_merge_count(const uint64_t *__restrict__ lk, int64_t nl,
+                                                            const uint64_t *__restrict__ rk, int64_t nr,
+                                                            int64_t *__restrict__ lo_out,
+                                                            int64_t *__restrict__ counts) {
+  __shared__ uint64_t lt[kMJTile + kMJThreads];
+  __shared__ uint64_t rw[kMJWindow];
+  const int64_t base = (int64_t)blockIdx.x * kMJTile;
+  const int rows = (int)(nl - base < kMJTile ? nl - base : kMJTile);
+  const int64_t rs = lo_out[base], wn = counts[base] - rs;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < rows; i += kMJThreads) lt[mj_pad(i)] = lk[base + i];
+  const bool in_lds = wn <= kMJWindow;
+  if (in_lds)
+    for (int i = tid; i < wn; i += kMJThreads) rw[i] = rk[rs + i];
+  __syncthreads();
+  const int r0 = tid * kMJPerThread;
+  int64_t lo_v[kMJPerThread], c_v[kMJPerThread];
+  if (in_lds) mj_walk(lt, (const uint64_t *)rw, wn, r0, rows, lo_v, c_v);
+  else mj_walk(lt, rk + rs, wn, r0, rows, lo_v, c_v);
+  // stage both outputs through the tile buffer so the global stores coalesce
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kMJPerThread; ++j)
+    if (r0 + j < rows) lt[mj_pad(r0 + j)] = (uint64_t)(rs + lo_v[j]);
+  __syncthreads();
+  for (int i = tid; i < rows; i += kMJThreads) lo_out[base + i] = (int64_t)lt[mj_pad(i)];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kMJPerThread; ++j)
+    if (r0 + j < rows) lt[mj_pad(r0 + j)] = (uint64_t)c_v[j];
+  __syncthreads();
+  for (int i = tid; i < rows; i += kMJThreads) counts[base + i] = (int64_t)lt[mj_pad(i)];
 }
 
 __global__ void k_merge_write(const int64_t *__restrict__ lperm, int64_t nl, const int64_t *__restrict__ rperm,
@@ -204,7 +297,11 @@ void merge_join_count(const uint64_t *lk, int64_t nl, const uint64_t *rk, int64_
                       void *stream) {
   if (nl == 0) return;
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(k_merge_count, dim3(grid_for(nl)), dim3(kBlock), 0, s, lk, nl, rk, nr, lo, counts);
+  const int64_t tiles = (nl + kMJTile - 1) / kMJTile;
+  hipLaunchKernelGGL(k_merge_bounds, dim3((unsigned)((tiles + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, lk, nl, rk,
+                     nr, lo, counts);
+  HIP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_merge_count, dim3((unsigned)tiles), dim3(kMJThreads), 0, s, lk, nl, rk, nr, lo, counts);
   HIP_LAUNCH_CHECK();
 }
 

@@ -242,3 +242,29 @@ def test_sorted_merge_join_matches_cpu(gpu_ctx, ctx, monkeypatch):
     assert np.all(np.diff(g["l_k"].to_numpy()) >= 0)
     key = lambda df: sorted(map(tuple, df[sorted(df.columns)].to_numpy().tolist()))
     assert key(g) == key(c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["hot_key", "sparse_left", "dense_left", "disjoint"])
+def test_sorted_merge_join_window_shapes(gpu_ctx, ctx, monkeypatch, shape):
+    """The tiled merge count stages a right-key window per 2048-row left tile in LDS; windows larger than
+    LDS (a hot key, a sparse left side over a dense right side) take the global-memory walk with galloping."""
+    monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", "1")
+    monkeypatch.setenv("CYLON_RADIX_SORT_MIN_ROWS", "1")
+    rng = np.random.default_rng(5)
+    if shape == "hot_key":
+        lk = np.concatenate([rng.integers(0, 50_000, 30_000), np.full(40, 777)])
+        rk = np.concatenate([rng.integers(0, 50_000, 30_000), np.full(9_000, 777)])
+    elif shape == "sparse_left":
+        lk, rk = rng.integers(0, 10**6, 3_000), rng.integers(0, 10**6, 300_000)
+    elif shape == "dense_left":
+        lk, rk = rng.integers(0, 10**6, 300_000), rng.integers(0, 10**6, 3_000)
+    else:
+        lk, rk = rng.integers(0, 10**5, 20_000), rng.integers(2 * 10**5, 3 * 10**5, 20_000)
+    a = pa.table({"k": lk, "x": np.arange(len(lk), dtype=np.float64)})
+    b = pa.table({"k": rk, "y": np.arange(len(rk), dtype=np.float64)})
+    g = Table(a, gpu_ctx).join(Table(b, gpu_ctx), "inner", "sort", on=["k"]).to_pandas()
+    c = Table(a, ctx).join(Table(b, ctx), "inner", "sort", on=["k"]).to_pandas()
+    assert len(g) == len(c)
+    key = lambda df: sorted(map(tuple, df[sorted(df.columns)].to_numpy().tolist()))
+    assert key(g) == key(c)
