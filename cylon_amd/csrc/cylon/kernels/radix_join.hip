@@ -34,9 +34,9 @@ constexpr int kRPItems = 8;                      // rows per thread per tile
 constexpr int kRPTile = kRPThreads * kRPItems;   // 8192 rows
 constexpr int kRPMaxBuckets = 1024;
 constexpr int kRJMaxDigitBits = 10;
-constexpr int kRJRowArea = 77568;                // LDS bytes for the staged build rows (2 blocks per CU)
-constexpr int kRJMaxRows = 2560;                 // build rows per partition (5 per thread)
-constexpr int kRJThreads = 512;
+constexpr int kRJRowArea = 155520;               // LDS bytes for the staged build rows (1 block per CU)
+constexpr int kRJMaxRows = 5120;                 // build rows per partition (5 per thread)
+constexpr int kRJThreads = 1024;
 constexpr int kRJWaves = kRJThreads / kWave;
 
 struct ColSet {
@@ -425,7 +425,7 @@ void radix_part_offsets(const int64_t *keys, int64_t n, int bits, int64_t *offs,
 // exactly its bucket (mean occupancy < 1): no clustering, no tombstones, and a
 // lane's loop length is its bucket's size.  Built with one LDS atomic per row
 // (16-bit counters packed in pairs), a block scan and one scatter.
-constexpr int kRJBuckets = 2048;
+constexpr int kRJBuckets = 4096;
 
 // Build rows per partition that fit the LDS row area: key (8 B) + permutation
 // (2 B) + the staged build columns (widths w[q]; in[q] == nullptr marks the key
