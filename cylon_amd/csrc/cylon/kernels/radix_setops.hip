@@ -34,8 +34,13 @@ namespace cylon {
 namespace hip {
 
 constexpr int kSOThreads = 512;
-constexpr int kSOSlots = 4096;      // LDS table: 16 B per slot -> 64 KB, two workgroups per CU
-constexpr int64_t kSORowsPerPart = 2048;  // 2^20 partitions (two 10-bit passes) up to 2^31 rows
+// LDS table: 8 B hash + 4 B representative + 2 side bits per slot, 4096 slots ->
+// 49 KB, several workgroups per CU.  Partitions of <= 2048 rows (load <= 0.5): 2^31
+// rows take 20 partition bits (two 10-bit passes).  Measured alternative: 8192-row
+// partitions in a 12288-slot table (one workgroup per CU) let 2^31 rows use two
+// 9-bit passes (-8 ms per 1B x 1B union) but the dedup lost more (+10 ms).
+constexpr int kSOSlots = 4096;
+constexpr int64_t kSORowsPerPart = 2048;
 
 struct SOColSet {
   ColView c[kMaxFusedCols];
@@ -141,7 +146,7 @@ enum SOOp : int { SO_DISTINCT = 0, SO_SUBTRACT = 1, SO_INTERSECT = 2 };
 // slot of hash h (claims one in phase 1); -1 if the table is full
 template <bool kInsert>
 __device__ __forceinline__ int so_slot(unsigned long long *keys, uint64_t h) {
-  uint32_t s = (uint32_t)h & (kSOSlots - 1);
+  uint32_t s = (uint32_t)(((uint64_t)(uint32_t)h * kSOSlots) >> 32);  // not a power of two: multiply-shift
   for (int probes = 0; probes < kSOSlots; ++probes) {
     const unsigned long long cur = keys[s];
     if (cur == h) return (int)s;
@@ -150,11 +155,33 @@ __device__ __forceinline__ int so_slot(unsigned long long *keys, uint64_t h) {
       const unsigned long long prev = atomicCAS(&keys[s], 0ull, (unsigned long long)h);
       if (prev == 0ull || prev == h) return (int)s;
     }
-    s = (s + 1) & (kSOSlots - 1);
+    s = s + 1 == (uint32_t)kSOSlots ? 0u : s + 1;
   }
   return -1;
 }
 
+static_assert(kSORowsPerPart % kSOThreads == 0, "rows per thread");
+constexpr int kSOItems = (int)(kSORowsPerPart / kSOThreads);  // rows per thread held in registers
+
+__device__ __forceinline__ void so_load(const uint64_t *__restrict__ ph, const int64_t *__restrict__ prow,
+                                        const int64_t *__restrict__ offs, int64_t p, int64_t &rb, int64_t &re,
+                                        uint64_t *hv, int64_t *rv) {
+  rb = offs[p];
+  re = offs[p + 1];
+#pragma unroll
+  for (int k = 0; k < kSOItems; ++k) {
+    const int64_t r = rb + threadIdx.x + k * kSOThreads;
+    if (r < re) {
+      hv[k] = ph[r];
+      rv[k] = prow[r];
+    }
+  }
+}
+
+// One workgroup per partition at a time.  The partition's (hash, row) pairs are
+// held in registers (8 per thread) and the next partition's are loaded while this
+// one is deduplicated, so the global latency hides behind the LDS work of the two
+// phases (rows beyond 8192 in a skewed partition are streamed from global).
 __global__ __launch_bounds__(kSOThreads) void k_so_dedup(const uint64_t *__restrict__ ph,
                                                          const int64_t *__restrict__ prow,
                                                          const int64_t *__restrict__ offs, int64_t nparts,
@@ -163,52 +190,32 @@ __global__ __launch_bounds__(kSOThreads) void k_so_dedup(const uint64_t *__restr
                                                          unsigned long long *exc, int *bad) {
   __shared__ unsigned long long keys[kSOSlots];
   __shared__ uint32_t rep[kSOSlots];
-  __shared__ uint32_t side[kSOSlots];
+  __shared__ uint32_t side[kSOSlots / 16];  // 2 bits per slot: 1 = on the left, 2 = on the right
   __shared__ int sbad;
   const uint32_t rep_init = keep_last ? 0u : 0xffffffffu;
-  for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
-    const int64_t rb = offs[p], re = offs[p + 1];
-    if (rb == re) continue;
-    __syncthreads();  // previous partition done with the table
-    for (int s = threadIdx.x; s < kSOSlots; s += blockDim.x) {
-      keys[s] = 0ull;
-      rep[s] = rep_init;
-      side[s] = 0u;
+  // phase 1: insert, fold representative position and side flags
+  auto insert = [&](uint64_t h, int64_t row, uint32_t local) {
+    const int s = so_slot<true>(keys, h);
+    if (s < 0) {
+      sbad = 1;
+      return;
     }
-    if (threadIdx.x == 0) sbad = 0;
-    __syncthreads();
-    // phase 1: insert, fold representative position and side flags
-    for (int64_t r = rb + threadIdx.x; r < re; r += blockDim.x) {
-      const uint64_t h = ph[r];
-      const int s = so_slot<true>(keys, h);
-      if (s < 0) {
-        sbad = 1;
-        continue;
-      }
-      const uint32_t local = (uint32_t)(r - rb);
-      if (keep_last) atomicMax(&rep[s], local);
-      else atomicMin(&rep[s], local);
-      if (op != SO_DISTINCT) atomicOr(&side[s], prow[r] < nl ? 1u : 2u);
-    }
-    __syncthreads();
-    if (sbad) {
-      if (threadIdx.x == 0) atomicExch(bad, 1);
-      continue;
-    }
-    // phase 2: verify duplicates against their representative, write mask exceptions
-    for (int64_t r = rb + threadIdx.x; r < re; r += blockDim.x) {
-      const uint64_t h = ph[r];
+    if (keep_last) atomicMax(&rep[s], local);
+    else atomicMin(&rep[s], local);
+    if (op != SO_DISTINCT) atomicOr(&side[s >> 4], (row < nl ? 1u : 2u) << ((s & 15) * 2));
+  };
+  // phase 2: verify duplicates against their representative, write mask exceptions
+  auto verify = [&](bool active, uint64_t h, int64_t row, uint32_t local, int64_t rb) {
+    bool flip = false;
+    if (active) {
       const int s = so_slot<false>(keys, h);
-      const uint32_t local = (uint32_t)(r - rb);
-      const int64_t row = prow[r];
       const bool first = rep[s] == local;
       if (!first && !so_rows_equal(L, R, ncols, nl, row, prow[rb + rep[s]])) atomicExch(bad, 1);  // collision
-      bool flip = false;
       if (op == SO_DISTINCT) {
         flip = !first;  // default keep
         if (flip) mask[row] = 0;
       } else if (row < nl) {
-        const bool on_right = (side[s] & 2u) != 0;
+        const bool on_right = ((side[s >> 4] >> ((s & 15) * 2)) & 2u) != 0;
         if (op == SO_SUBTRACT) {
           flip = !(first && !on_right);  // default keep
           if (flip) mask[row] = 0;
@@ -217,8 +224,54 @@ __global__ __launch_bounds__(kSOThreads) void k_so_dedup(const uint64_t *__restr
           if (flip) mask[row] = 1;
         }
       }
-      const uint64_t b = __ballot(flip);
-      if (lane_id() == 0 && b) atomicAdd(exc, (unsigned long long)__popcll(b));
+    }
+    const uint64_t b = __ballot(flip);
+    if (lane_id() == 0 && b) atomicAdd(exc, (unsigned long long)__popcll(b));
+  };
+  int64_t p = blockIdx.x, nb = 0, ne = 0;
+  uint64_t nh[kSOItems];
+  int64_t nr[kSOItems];
+  if (p < nparts) so_load(ph, prow, offs, p, nb, ne, nh, nr);
+  for (; p < nparts; p += gridDim.x) {
+    const int64_t rb = nb, re = ne;
+    uint64_t hv[kSOItems];
+    int64_t rv[kSOItems];
+#pragma unroll
+    for (int k = 0; k < kSOItems; ++k) {
+      hv[k] = nh[k];
+      rv[k] = nr[k];
+    }
+    if (p + gridDim.x < nparts) so_load(ph, prow, offs, p + gridDim.x, nb, ne, nh, nr);
+    if (rb == re) continue;
+    __syncthreads();  // previous partition done with the table
+    for (int s = threadIdx.x; s < kSOSlots; s += blockDim.x) {
+      keys[s] = 0ull;
+      rep[s] = rep_init;
+    }
+    for (int s = threadIdx.x; s < kSOSlots / 16; s += blockDim.x) side[s] = 0u;
+    if (threadIdx.x == 0) sbad = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSOItems; ++k) {
+      const int64_t r = rb + threadIdx.x + k * kSOThreads;
+      if (r < re) insert(hv[k], rv[k], (uint32_t)(r - rb));
+    }
+    for (int64_t r = rb + kSORowsPerPart + threadIdx.x; r < re; r += kSOThreads)
+      insert(ph[r], prow[r], (uint32_t)(r - rb));
+    __syncthreads();
+    if (sbad) {
+      if (threadIdx.x == 0) atomicExch(bad, 1);
+      continue;
+    }
+#pragma unroll
+    for (int k = 0; k < kSOItems; ++k) {
+      const int64_t r = rb + threadIdx.x + k * kSOThreads;
+      verify(r < re, hv[k], rv[k], (uint32_t)(r - rb), rb);
+    }
+    for (int64_t r0 = rb + kSORowsPerPart; r0 < re; r0 += kSOThreads) {  // wave-uniform trip count
+      const int64_t r = r0 + threadIdx.x;
+      const bool act = r < re;
+      verify(act, act ? ph[r] : 0, act ? prow[r] : 0, (uint32_t)(r - rb), rb);
     }
   }
 }
@@ -236,7 +289,7 @@ void setop_dedup(const uint64_t *ph, const int64_t *prow, const int64_t *offs, i
     L.c[c] = lcols[c];
     R.c[c] = rcols ? rcols[c] : lcols[c];
   }
-  const int grid = (int)std::min<int64_t>(nparts, (int64_t)kNumCUs * 2 * 8);
+  const int grid = (int)std::min<int64_t>(nparts, (int64_t)kNumCUs * 16);
   hipLaunchKernelGGL(k_so_dedup, dim3(grid), dim3(kSOThreads), 0, s, ph, prow, offs, nparts, nl, op,
                      keep_last ? 1 : 0, L, R, ncols, mask, reinterpret_cast<unsigned long long *>(exc), bad);
   HIP_LAUNCH_CHECK();
