@@ -1,5 +1,6 @@
 // Bindings for the extended relational operators (set ops, unique, group-by,
 // aggregates, range partition, distributed sort).
+#include <map>
 #include <torch/extension.h>
 
 #include "cylon/kernels/kernels.hpp"
@@ -42,8 +43,17 @@ void register_extended_ops(py::module &m) {
          bool ignore_empty_lines, const std::vector<std::string> &include_columns,
          const std::vector<std::string> &null_values, const std::vector<std::string> &true_values,
          const std::vector<std::string> &false_values, bool strings_can_be_null, bool quoting,
-         const std::string &quote_char, bool double_quote, int threads) {
+         const std::string &quote_char, bool double_quote, int threads, bool escaping, const std::string &escape_char,
+         bool newlines_in_values, const std::map<std::string, int> &column_types, bool include_missing_columns,
+         int64_t block_size, bool concurrent_file_reads) {
         io::CSVReadOptions o;
+        o.escaping = escaping;
+        if (!escape_char.empty()) o.escape_char = escape_char[0];
+        o.newlines_in_values = newlines_in_values;
+        for (const auto &kv : column_types) o.column_types.emplace(kv.first, DataType(static_cast<Type>(kv.second)));
+        o.include_missing_columns = include_missing_columns;
+        o.block_size = (int32_t)std::min<int64_t>(block_size, INT32_MAX);
+        o.concurrent_file_reads = concurrent_file_reads;
         o.delimiter = delimiter.empty() ? ',' : delimiter[0];
         o.header = header;
         o.autogenerate_column_names = autogen;
@@ -67,7 +77,10 @@ void register_extended_ops(py::module &m) {
       py::arg("include_columns") = std::vector<std::string>{}, py::arg("null_values") = std::vector<std::string>{},
       py::arg("true_values") = std::vector<std::string>{}, py::arg("false_values") = std::vector<std::string>{},
       py::arg("strings_can_be_null") = false, py::arg("quoting") = true, py::arg("quote_char") = "\"",
-      py::arg("double_quote") = true, py::arg("threads") = 0, rel);
+      py::arg("double_quote") = true, py::arg("threads") = 0, py::arg("escaping") = false,
+      py::arg("escape_char") = "\\", py::arg("newlines_in_values") = false,
+      py::arg("column_types") = std::map<std::string, int>{}, py::arg("include_missing_columns") = false,
+      py::arg("block_size") = int64_t(1) << 20, py::arg("concurrent_file_reads") = true, rel);
   m.def(
       "write_csv",
       [](const TablePtr &t, const std::string &path, const std::string &delimiter,

@@ -66,6 +66,11 @@ void split_line(const char *b, const char *e, const CSVReadOptions &o, std::vect
     if (o.quoting && p < e && *p == o.quote_char) {
       const char *s = ++p;
       while (p < e) {
+        if (o.escaping && *p == o.escape_char && p + 1 < e) {
+          f.escaped = true;
+          p += 2;
+          continue;
+        }
         if (*p == o.quote_char) {
           if (o.double_quote && p + 1 < e && p[1] == o.quote_char) {
             f.escaped = true;
@@ -82,7 +87,13 @@ void split_line(const char *b, const char *e, const CSVReadOptions &o, std::vect
       if (p < e) ++p;  // closing quote
       while (p < e && *p != o.delimiter) ++p;
     } else {
-      while (p < e && *p != o.delimiter) ++p;
+      while (p < e && *p != o.delimiter) {
+        if (o.escaping && *p == o.escape_char && p + 1 < e) {
+          f.escaped = true;
+          ++p;
+        }
+        ++p;
+      }
       f.len = (uint32_t)(p - f.p);
     }
     out.push_back(f);
@@ -95,13 +106,18 @@ void split_line(const char *b, const char *e, const CSVReadOptions &o, std::vect
   }
 }
 
-std::string field_string(const Field &f, char quote) {
+// field text with doubled quotes (inside quotes) and escape characters resolved
+std::string field_string(const Field &f, const CSVReadOptions &o) {
   if (!f.escaped) return std::string(f.p, f.len);
   std::string s;
   s.reserve(f.len);
   for (uint32_t i = 0; i < f.len; ++i) {
+    if (o.escaping && f.p[i] == o.escape_char && i + 1 < f.len) {
+      s.push_back(f.p[++i]);
+      continue;
+    }
     s.push_back(f.p[i]);
-    if (f.p[i] == quote && i + 1 < f.len && f.p[i + 1] == quote) ++i;
+    if (f.quoted && f.p[i] == o.quote_char && i + 1 < f.len && f.p[i + 1] == o.quote_char) ++i;
   }
   return s;
 }
@@ -204,6 +220,44 @@ void find_lines(const char *base, size_t b, size_t e, bool skip_empty, std::vect
   }
 }
 
+// newlines_in_values: a newline inside a quoted value does not end the record
+void find_records(const char *base, size_t b, size_t e, const CSVReadOptions &o,
+                  std::vector<std::pair<size_t, size_t>> &out) {
+  size_t s = b;
+  bool inq = false;
+  for (size_t i = b; i < e; ++i) {
+    const char c = base[i];
+    if (o.escaping && c == o.escape_char) {
+      ++i;
+      continue;
+    }
+    if (o.quoting && c == o.quote_char) inq = !inq;
+    else if (c == '\n' && !inq) {
+      size_t te = i;
+      if (te > s && base[te - 1] == '\r') --te;
+      if (!(o.ignore_empty_lines && te == s)) out.emplace_back(s, te);
+      s = i + 1;
+    }
+  }
+  if (s < e) {
+    size_t te = e;
+    if (base[te - 1] == '\r') --te;
+    if (!(o.ignore_empty_lines && te == s)) out.emplace_back(s, te);
+  }
+}
+
+Kind forced_kind(const DataType &t) {
+  switch (t.type) {
+    case Type::BOOL: return Kind::BOOL;
+    case Type::HALF_FLOAT: case Type::FLOAT: case Type::DOUBLE: return Kind::F64;
+    case Type::STRING: case Type::BINARY: return Kind::STR;
+    default: break;
+  }
+  CYLON_CHECK(t.layout() == Layout::FIXED_WIDTH && t.type != Type::FIXED_SIZE_BINARY && t.type != Type::DECIMAL, Code::NotImplemented,
+              "CSV column type " << t.ToString() << " is not supported");
+  return Kind::I64;  // integers and the integer-backed temporal types
+}
+
 template <class F>
 void parallel_for(int T, F &&fn) {
   if (T <= 1) {
@@ -260,14 +314,16 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
       pos = t + 1;
       if (te == ls && o.ignore_empty_lines) continue;
       split_line(base + ls, base + te, o, fields);
-      for (const auto &f : fields) names.push_back(field_string(f, o.quote_char));
+      for (const auto &f : fields) names.push_back(field_string(f, o));
       break;
     }
   }
   // line-aligned chunks
   int T = o.threads > 0 ? o.threads : (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
   const size_t data_bytes = pos < size ? size - pos : 0;
-  T = (int)std::max<size_t>(1, std::min<size_t>((size_t)T, data_bytes / (1 << 20)));  // >= 1 MB per thread
+  const size_t min_block = (size_t)std::max<int32_t>(1, o.block_size);
+  T = (int)std::max<size_t>(1, std::min<size_t>((size_t)T, data_bytes / min_block));  // >= block_size per thread
+  if (!o.use_threads || o.newlines_in_values) T = 1;
   std::vector<size_t> cut(T + 1, size);
   cut[0] = std::min(pos, size);
   for (int t = 1; t < T; ++t) {
@@ -284,7 +340,8 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   };
   tick("open");
-  parallel_for(T, [&](int t) { find_lines(base, cut[t], cut[t + 1], o.ignore_empty_lines, lines[t]); });
+  if (o.newlines_in_values) find_records(base, cut[0], cut[1], o, lines[0]);
+  else parallel_for(T, [&](int t) { find_lines(base, cut[t], cut[t + 1], o.ignore_empty_lines, lines[t]); });
   tick("lines");
 
   // column count
@@ -300,15 +357,23 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
   }
   // selected columns (output order)
   std::vector<int> sel;
+  std::vector<std::string> missing;  // output position -> name of an absent included column ("" = parsed)
   if (o.include_columns.empty()) {
     for (int i = 0; i < ncols; ++i) sel.push_back(i);
   } else {
     for (const auto &c : o.include_columns) {
       auto it = std::find(names.begin(), names.end(), c);
-      CYLON_CHECK(it != names.end(), Code::KeyError, "CSV column '" << c << "' not found in " << path);
+      if (it == names.end()) {
+        CYLON_CHECK(o.include_missing_columns, Code::KeyError, "CSV column '" << c << "' not found in " << path);
+        missing.resize(sel.size() + 1);
+        missing.back() = c;
+        sel.push_back(-1);
+        continue;
+      }
       sel.push_back((int)(it - names.begin()));
     }
   }
+  missing.resize(sel.size());
   const int nsel = (int)sel.size();
 
   // pass A: type inference
@@ -319,15 +384,22 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
       split_line(base + ln.first, base + ln.second, o, fs);
       CYLON_CHECK((int)fs.size() == ncols, Code::Invalid,
                   "CSV parse error in " << path << ": expected " << ncols << " columns, got " << fs.size());
-      for (int j = 0; j < nsel; ++j) seen[t][j] |= classify(fs[sel[j]], sets);
+      for (int j = 0; j < nsel; ++j)
+        if (sel[j] >= 0) seen[t][j] |= classify(fs[sel[j]], sets);
     }
   });
   tick("infer");
   std::vector<Kind> kinds(nsel);
+  std::vector<const DataType *> want(nsel, nullptr);  // explicit column_types entry
   for (int j = 0; j < nsel; ++j) {
     uint8_t s = 0;
     for (int t = 0; t < T; ++t) s |= seen[t][j];
     kinds[j] = resolve(s);
+    auto it = o.column_types.find(sel[j] >= 0 ? names[sel[j]] : missing[j]);
+    if (it != o.column_types.end()) {
+      want[j] = &it->second;
+      kinds[j] = forced_kind(it->second);
+    }
   }
   std::vector<int64_t> row0(T + 1, 0);
   for (int t = 0; t < T; ++t) row0[t + 1] = row0[t] + (int64_t)lines[t].size();
@@ -344,6 +416,8 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
     if (kinds[j] == Kind::F64) data[j] = at::empty({n}, cpu(at::kDouble));
     if (kinds[j] == Kind::BOOL) data[j] = at::empty({n}, cpu(storage_dtype(DataType(Type::BOOL))));
   }
+  for (int j = 0; j < nsel; ++j)
+    if (sel[j] < 0 && data[j].defined()) data[j].zero_();
   std::vector<uint8_t *> vptr(nsel);
   std::vector<void *> dptr(nsel, nullptr);
   for (int j = 0; j < nsel; ++j) {
@@ -358,26 +432,40 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
     for (const auto &ln : lines[t]) {
       split_line(base + ln.first, base + ln.second, o, fs);
       for (int j = 0; j < nsel; ++j) {
+        uint8_t *v = vptr[j];
+        if (sel[j] < 0) {  // absent included column: null
+          v[r] = 0;
+          anynull[t][j] = 1;
+          if (kinds[j] == Kind::STR) slens[j][t].push_back(0);
+          continue;
+        }
         const Field &f = fs[sel[j]];
         std::string_view s(f.p, f.len);
         const bool is_null = !f.quoted && sets.is_null(s);
-        uint8_t *v = vptr[j];
+        const bool strict = want[j] != nullptr;  // explicit types reject unparsable values
         switch (kinds[j]) {
           case Kind::I64: {
             int64_t x = 0;
-            if (is_null) v[r] = 0, anynull[t][j] = 1; else parse_i64(s, &x);
+            if (is_null) v[r] = 0, anynull[t][j] = 1;
+            else if (!parse_i64(s, &x) && strict)
+              CYLON_THROW(Code::Invalid, "CSV conversion error in " << path << ": '" << s << "' is not an integer");
             static_cast<int64_t *>(dptr[j])[r] = x;
             break;
           }
           case Kind::F64: {
             double x = 0;
-            if (is_null) v[r] = 0, anynull[t][j] = 1; else parse_f64(s, &x);
+            if (is_null) v[r] = 0, anynull[t][j] = 1;
+            else if (!parse_f64(s, &x) && strict)
+              CYLON_THROW(Code::Invalid, "CSV conversion error in " << path << ": '" << s << "' is not a number");
             static_cast<double *>(dptr[j])[r] = x;
             break;
           }
           case Kind::BOOL: {
             uint8_t x = 0;
-            if (is_null) v[r] = 0, anynull[t][j] = 1; else x = sets.trues.count(s) ? 1 : 0;
+            if (is_null) v[r] = 0, anynull[t][j] = 1;
+            else if (sets.trues.count(s)) x = 1;
+            else if (strict && !sets.falses.count(s))
+              CYLON_THROW(Code::Invalid, "CSV conversion error in " << path << ": '" << s << "' is not a boolean");
             static_cast<uint8_t *>(dptr[j])[r] = x;
             break;
           }
@@ -387,7 +475,7 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
               anynull[t][j] = 1;
               slens[j][t].push_back(0);
             } else {
-              const std::string x = field_string(f, o.quote_char);
+              const std::string x = field_string(f, o);
               sbytes[j][t] += x;
               slens[j][t].push_back((int64_t)x.size());
             }
@@ -401,7 +489,7 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
   tick("convert");
   std::vector<Column> cols;
   for (int j = 0; j < nsel; ++j) {
-    const std::string &name = names[sel[j]];
+    const std::string &name = sel[j] >= 0 ? names[sel[j]] : missing[j];
     bool any_null = false;
     for (int t = 0; t < T; ++t) any_null |= anynull[t][j] != 0;
     at::Tensor vd = any_null ? valid[j] : at::Tensor();
@@ -421,9 +509,13 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
           op[++r] = acc;
         }
       }
-      cols.emplace_back(name, DataType(Type::STRING), n, bytes, offs, vd);
+      cols.emplace_back(name, want[j] ? *want[j] : DataType(Type::STRING), n, bytes, offs, vd);
     } else {
       const Type ty = kinds[j] == Kind::I64 ? Type::INT64 : kinds[j] == Kind::F64 ? Type::DOUBLE : Type::BOOL;
+      if (want[j] && want[j]->type != ty) {  // narrow / reinterpret to the requested type
+        cols.emplace_back(name, *want[j], n, data[j].to(storage_dtype(*want[j])), at::Tensor(), vd);
+        continue;
+      }
       cols.emplace_back(name, DataType(ty), n, data[j], at::Tensor(), vd);
     }
   }
@@ -438,7 +530,9 @@ std::vector<TablePtr> ReadCSVs(const std::shared_ptr<CylonContext> &ctx, const s
   CSVReadOptions o = opts;
   if (o.threads == 0)
     o.threads = std::max(1, (int)std::min<size_t>(16, std::thread::hardware_concurrency()) / (int)std::max<size_t>(1, paths.size()));
-  parallel_for((int)paths.size(), [&](int i) { out[i] = ReadCSV(ctx, paths[i], o); });
+  if (o.concurrent_file_reads) parallel_for((int)paths.size(), [&](int i) { out[i] = ReadCSV(ctx, paths[i], o); });
+  else
+    for (size_t i = 0; i < paths.size(); ++i) out[i] = ReadCSV(ctx, paths[i], o);
   return out;
 }
 

@@ -15,6 +15,7 @@
 #pragma once
 #include <ostream>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../table.hpp"
@@ -30,6 +31,7 @@ struct CSVReadOptions {
   int64_t skip_rows = 0;
   bool ignore_empty_lines = true;
   std::vector<std::string> include_columns;  // subset / order of columns to keep
+  bool include_missing_columns = false;      // absent include_columns -> all-null columns
   std::vector<std::string> null_values;      // empty -> Arrow's defaults
   std::vector<std::string> true_values{"1", "True", "TRUE", "true"};
   std::vector<std::string> false_values{"0", "False", "FALSE", "false"};
@@ -37,7 +39,41 @@ struct CSVReadOptions {
   bool quoting = true;
   char quote_char = '"';
   bool double_quote = true;
-  int threads = 0;  // 0 -> hardware concurrency (capped at 16)
+  bool escaping = false;         // escape_char makes the next character literal
+  char escape_char = '\\';
+  bool newlines_in_values = false;  // quoted values may span lines (single-threaded line scan)
+  std::unordered_map<std::string, DataType> column_types;  // overrides inference per column
+  int threads = 0;               // 0 -> hardware concurrency (capped at 16)
+  bool use_threads = true;       // false -> one parser thread
+  bool concurrent_file_reads = true;  // ReadCSVs: one thread per file
+  int32_t block_size = 1 << 20;  // minimum bytes per parser thread
+
+  // Builder form of the reference's CSVReadOptions (csv_read_config.hpp:27-150).
+  CSVReadOptions &ConcurrentFileReads(bool v) { concurrent_file_reads = v; return *this; }
+  bool IsConcurrentFileReads() const { return concurrent_file_reads; }
+  CSVReadOptions &UseThreads(bool v) { use_threads = v; return *this; }
+  CSVReadOptions &WithDelimiter(char d) { delimiter = d; return *this; }
+  CSVReadOptions &IgnoreEmptyLines() { ignore_empty_lines = true; return *this; }
+  CSVReadOptions &AutoGenerateColumnNames() { autogenerate_column_names = true; return *this; }
+  CSVReadOptions &ColumnNames(const std::vector<std::string> &names) { column_names = names; return *this; }
+  CSVReadOptions &BlockSize(int32_t b) { block_size = b; return *this; }
+  CSVReadOptions &UseQuoting() { quoting = true; return *this; }
+  CSVReadOptions &WithQuoteChar(char q) { quote_char = q; quoting = true; return *this; }
+  CSVReadOptions &DoubleQuote() { double_quote = true; return *this; }
+  CSVReadOptions &UseEscaping() { escaping = true; return *this; }
+  CSVReadOptions &EscapingCharacter(char c) { escape_char = c; escaping = true; return *this; }
+  CSVReadOptions &HasNewLinesInValues() { newlines_in_values = true; return *this; }
+  CSVReadOptions &SkipRows(int32_t n) { skip_rows = n; return *this; }
+  CSVReadOptions &WithColumnTypes(const std::unordered_map<std::string, DataType> &t) {
+    column_types = t;
+    return *this;
+  }
+  CSVReadOptions &NullValues(const std::vector<std::string> &v) { null_values = v; return *this; }
+  CSVReadOptions &TrueValues(const std::vector<std::string> &v) { true_values = v; return *this; }
+  CSVReadOptions &FalseValues(const std::vector<std::string> &v) { false_values = v; return *this; }
+  CSVReadOptions &StringsCanBeNull() { strings_can_be_null = true; return *this; }
+  CSVReadOptions &IncludeColumns(const std::vector<std::string> &c) { include_columns = c; return *this; }
+  CSVReadOptions &IncludeMissingColumns() { include_missing_columns = true; return *this; }
 };
 
 struct CSVWriteOptions {

@@ -14,6 +14,8 @@ import pyarrow as pa
 import pyarrow.csv as pacsv
 
 from .._lib import C
+
+Type = C.Type
 from ..ctx.context import CylonContext
 from ..data.table import Table, _ensure_ctx
 
@@ -199,9 +201,18 @@ class CSVWriteOptions:
     ColumnNames = with_column_names
 
 
+_NATIVE_COLUMN_TYPES = {
+    pa.int8(): Type.INT8, pa.int16(): Type.INT16, pa.int32(): Type.INT32, pa.int64(): Type.INT64,
+    pa.uint8(): Type.UINT8, pa.uint16(): Type.UINT16, pa.uint32(): Type.UINT32, pa.uint64(): Type.UINT64,
+    pa.float16(): Type.HALF_FLOAT, pa.float32(): Type.FLOAT, pa.float64(): Type.DOUBLE, pa.bool_(): Type.BOOL,
+    pa.string(): Type.STRING, pa.binary(): Type.BINARY,
+}
+
+
 def _native_ok(o: CSVReadOptions) -> bool:
-    """Options the native C++ reader (cylon/io/csv.cpp) implements; others go through Arrow."""
-    return not (o._column_types or o._escaping or o._newlines_in_values or o._include_missing_columns)
+    """Options the native C++ reader (cylon/io/csv.cpp) implements; explicit column types
+    other than plain numeric / bool / string ones go through Arrow."""
+    return all(t in _NATIVE_COLUMN_TYPES for t in o._column_types.values())
 
 
 def _read_native(ctx: CylonContext, paths: Sequence[str], o: CSVReadOptions) -> List[Table]:
@@ -215,7 +226,10 @@ def _read_native(ctx: CylonContext, paths: Sequence[str], o: CSVReadOptions) -> 
                       null_values=nulls or [], true_values=o._true_values or [],
                       false_values=o._false_values or [], strings_can_be_null=o._strings_can_be_null,
                       quoting=o._quoting, quote_char=o._quote_char, double_quote=o._double_quote,
-                      threads=0 if o._use_threads else 1)
+                      threads=0 if o._use_threads else 1, escaping=o._escaping, escape_char=o._escape_char,
+                      newlines_in_values=o._newlines_in_values,
+                      column_types={k: int(_NATIVE_COLUMN_TYPES[t]) for k, t in o._column_types.items()},
+                      include_missing_columns=o._include_missing_columns, block_size=o._block_size)
     return [Table(context=ctx, _native=t) for t in tabs]
 
 

@@ -38,7 +38,7 @@ int main(int argc, char **argv) {
 
   TablePtr a, b, j, js, u, i, s, q, srt, g, sum, back;
   CHECK_OK(cylon::FromCSV(ctx, argv[2], a));
-  CHECK_OK(cylon::FromCSV(ctx, argv[3], b));
+  CHECK_OK(cylon::FromCSV(ctx, argv[3], b, cylon::io::CSVReadOptions().WithDelimiter(',').UseThreads(true).BlockSize(1 << 20)));
   report("left", a);
   report("right", b);
 

@@ -96,3 +96,38 @@ def test_native_parquet_large_strings(ctx, tmp_path):
     p = str(tmp_path / "l.parquet")
     pq.write_table(at, p)
     assert read_parquet(ctx, p).to_pydict() == {"s": ["xxxxx", "yy", None]}
+
+
+def test_native_reader_escaping_and_multiline_values(ctx, tmp_path, monkeypatch):
+    """Escape characters and quoted values spanning lines (HasNewLinesInValues) parse
+    natively the way Arrow's reader parses them."""
+    p = tmp_path / "m.csv"
+    p.write_bytes(b'id,text,v\n1,"line one\nline two",1.5\n2,plain\\,comma,2.5\n3,"say \\"hi\\"",3.0\n'
+                  b'4,"a\r\nb",4.0\n')
+    opts = lambda: CSVReadOptions().use_escaping().has_new_lines_in_values()  # noqa: E731
+    a, b = _both(ctx, str(p), opts, monkeypatch)
+    pd.testing.assert_frame_equal(a, b)
+    assert a["text"].tolist()[:3] == ["line one\nline two", "plain,comma", 'say "hi"']
+
+
+def test_native_reader_column_types_and_missing_columns(ctx, tmp_path, monkeypatch):
+    import pyarrow as pa
+    p = tmp_path / "t.csv"
+    p.write_text("a,b,c,d\n1,2.5,x,1\n-3,,y,0\n7,4.25,,1\n")
+    opts = lambda: (CSVReadOptions()  # noqa: E731
+                    .with_column_types({"a": pa.int32(), "b": pa.float32(), "d": pa.bool_(), "e": pa.int16()})
+                    .use_cols(["d", "a", "e", "b"]).include_missing_columns())
+    a, b = _both(ctx, str(p), opts, monkeypatch)
+    pd.testing.assert_frame_equal(a, b)
+    t = read_csv(ctx, str(p), opts())
+    assert [str(x) for x in t.to_arrow().schema.types] == ["bool", "int32", "int16", "float"]
+    assert t.to_pandas()["e"].isna().all()
+
+
+def test_native_reader_rejects_bad_typed_values(ctx, tmp_path, monkeypatch):
+    import pyarrow as pa
+    p = tmp_path / "bad.csv"
+    p.write_text("a,b\n1,2\nx,3\n")
+    monkeypatch.setenv("CYLON_CSV_READER", "native")
+    with pytest.raises(Exception, match="conversion"):
+        read_csv(ctx, str(p), CSVReadOptions().with_column_types({"a": pa.int64()}))
