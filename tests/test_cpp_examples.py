@@ -12,12 +12,18 @@ EXE = os.path.join(ROOT, "examples", "cpp", "bin", "relational_example")
 
 
 def _ensure_built():
+    import fcntl
     import glob
     srcs = glob.glob(os.path.join(ROOT, "examples", "cpp", "*.cpp"))
     exes = [os.path.join(ROOT, "examples", "cpp", "bin", os.path.basename(s)[:-4]) for s in srcs]
-    newest = max(os.path.getmtime(p) for p in srcs + [os.path.join(ROOT, "cylon_amd", "libcylon_amd.so")])
-    if any(not os.path.exists(e) or os.path.getmtime(e) < newest for e in exes):
-        subprocess.run(["bash", os.path.join(ROOT, "examples", "cpp", "build.sh")], check=True, capture_output=True)
+    os.makedirs(os.path.join(ROOT, "examples", "cpp", "bin"), exist_ok=True)
+    # one builder at a time: parallel test workers would otherwise rewrite an executable another runs
+    with open(os.path.join(ROOT, "examples", "cpp", "bin", ".build.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        newest = max(os.path.getmtime(p) for p in srcs + [os.path.join(ROOT, "cylon_amd", "libcylon_amd.so")])
+        if any(not os.path.exists(e) or os.path.getmtime(e) < newest for e in exes):
+            subprocess.run(["bash", os.path.join(ROOT, "examples", "cpp", "build.sh")], check=True,
+                           capture_output=True)
     return EXE
 
 
