@@ -116,6 +116,20 @@ struct ImageDigit {
   __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key(keys[i]); }
 };
 
+// Order-preserving range digit (K7 range join): the partition of key k is
+// ((k ^ flip) - mn) >> rshift -- key ranges in key order -- and a pass's digit is
+// bits [shift, shift + log2(mask + 1)) of that partition id.
+struct RangeDigit {
+  const int64_t *keys;
+  uint64_t flip, mn;
+  int rshift, shift;
+  uint32_t mask;
+  __device__ __forceinline__ uint32_t of_key(int64_t k) const {
+    return (uint32_t)((((uint64_t)k ^ flip) - mn) >> (rshift + shift)) & mask;
+  }
+  __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key(keys[i]); }
+};
+
 template <class Digit>
 __global__ __launch_bounds__(kRPThreads) void k_rp_hist(Digit digit, int64_t n, uint32_t nbuckets,
                                                         int64_t rows_per_block, int64_t nblocks,
@@ -356,6 +370,14 @@ void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_b
   rows_pass_launch(ImageDigit{keys, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws, stream);
 }
 
+void radix_range_rows_pass(const int64_t *keys, int64_t n, uint64_t flip, uint64_t mn, int rshift, int shift,
+                           int digit_bits, const uint8_t *const *in, uint8_t *const *out, const int *widths, int ncols,
+                           int64_t *ws, void *stream) {
+  const uint32_t nb = 1u << digit_bits;
+  rows_pass_launch(RangeDigit{keys, flip, mn, rshift, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws,
+                   stream);
+}
+
 static int bits_for(uint32_t nparts) {
   int b = 1;
   while ((1u << b) < nparts) ++b;
@@ -412,6 +434,27 @@ void radix_part_offsets(const int64_t *keys, int64_t n, int bits, int64_t *offs,
   const int64_t np = int64_t(1) << bits;
   hipLaunchKernelGGL(k_part_offsets, dim3(grid_for(np + 1)), dim3(kBlock), 0, as_stream(stream), keys, n, bits, np,
                      offs);
+  HIP_LAUNCH_CHECK();
+}
+
+__global__ void k_range_part_offsets(const int64_t *__restrict__ keys, int64_t n, uint64_t flip, uint64_t mn,
+                                     int rshift, int64_t nparts, int64_t *__restrict__ offs) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= nparts; p += stride) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)((((uint64_t)keys[mid] ^ flip) - mn) >> rshift) < p) lo = mid + 1; else hi = mid;
+    }
+    offs[p] = lo;
+  }
+}
+
+void radix_range_part_offsets(const int64_t *keys, int64_t n, uint64_t flip, uint64_t mn, int rshift, int bits,
+                              int64_t *offs, void *stream) {
+  const int64_t np = int64_t(1) << bits;
+  hipLaunchKernelGGL(k_range_part_offsets, dim3(grid_for(np + 1)), dim3(kBlock), 0, as_stream(stream), keys, n, flip,
+                     mn, rshift, np, offs);
   HIP_LAUNCH_CHECK();
 }
 
@@ -805,6 +848,213 @@ void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t 
   else
     hipLaunchKernelGGL((k_rj_write<4, 3, false>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys,
                        boffs, nparts, (int)cap, out_offs, pc, bs, bo);
+  HIP_LAUNCH_CHECK();
+}
+
+
+// --------------------------------------------------------------------------
+// K7 range join: sort-algorithm inner join on range partitions
+// --------------------------------------------------------------------------
+// Both relations are partitioned by RangeDigit into key ranges of 2^rshift
+// values (rshift <= 12), so inside a partition the low rshift bits of
+// (key ^ flip) - mn are an exact key offset.  Per partition one workgroup
+// counts both sides by key offset in LDS (4096 buckets), scans the counts into
+// CSR starts and output offsets, scatters each side's row numbers into key
+// order (uint16 permutations), and then emits output rows slot-major: output
+// row t of the partition finds its key by a binary search over the output
+// offsets and its (left, right) pair as (idx / |R_v|, idx % |R_v|).  The output
+// is therefore ordered by key (partitions are key ranges in order), with no key
+// comparisons at all and every output column written as contiguous runs.
+constexpr int kRGThreads = 1024;
+constexpr int kRGMaxRows = 8192;  // rows per side per partition (uint16 permutations)
+constexpr int kRGBuckets = 4096;
+constexpr int kRGBucketsPerThread = kRGBuckets / kRGThreads;
+
+int64_t range_join_max_rows() { return kRGMaxRows; }
+int range_join_max_shift() { return 12; }
+
+__device__ __forceinline__ uint32_t rg_bucket(int64_t k, uint64_t flip, uint64_t mn, uint32_t bmask) {
+  return (uint32_t)(((uint64_t)k ^ flip) - mn) & bmask;
+}
+
+__global__ __launch_bounds__(kRGThreads) void k_rg_count(const int64_t *__restrict__ lkeys,
+                                                         const int64_t *__restrict__ loffs,
+                                                         const int64_t *__restrict__ rkeys,
+                                                         const int64_t *__restrict__ roffs, int64_t nparts,
+                                                         uint64_t flip, uint64_t mn, uint32_t bmask,
+                                                         int64_t *__restrict__ counts, int *overflow) {
+  __shared__ uint32_t hl[kRGBuckets], hr[kRGBuckets];
+  __shared__ unsigned long long wsum[kRGThreads / kWave];
+  const uint32_t nb = bmask + 1;
+  for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
+    const int64_t lb = loffs[p], nl = loffs[p + 1] - lb;
+    const int64_t rb = roffs[p], nr = roffs[p + 1] - rb;
+    if (nl > kRGMaxRows || nr > kRGMaxRows) {  // uniform branch
+      if (threadIdx.x == 0) {
+        atomicOr(overflow, 1);
+        counts[p] = 0;
+      }
+      continue;
+    }
+    if (nl == 0 || nr == 0) {
+      if (threadIdx.x == 0) counts[p] = 0;
+      continue;
+    }
+    __syncthreads();  // previous partition done with hl / hr / wsum
+    for (uint32_t v = threadIdx.x; v < nb; v += kRGThreads) hl[v] = hr[v] = 0;
+    __syncthreads();
+    for (int64_t r = threadIdx.x; r < nl; r += kRGThreads) atomicAdd(&hl[rg_bucket(lkeys[lb + r], flip, mn, bmask)], 1u);
+    for (int64_t r = threadIdx.x; r < nr; r += kRGThreads) atomicAdd(&hr[rg_bucket(rkeys[rb + r], flip, mn, bmask)], 1u);
+    __syncthreads();
+    unsigned long long c = 0;
+    for (uint32_t v = threadIdx.x; v < nb; v += kRGThreads) c += (unsigned long long)hl[v] * hr[v];
+    for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
+    if (lane_id() == 0) wsum[threadIdx.x / kWave] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long t = 0;
+      for (int w = 0; w < kRGThreads / kWave; ++w) t += wsum[w];
+      counts[p] = (int64_t)t;
+    }
+  }
+}
+
+// exclusive scan of a[0..nb) in place (a[nb] = total), kRGBucketsPerThread values per thread
+template <class T>
+__device__ __forceinline__ void rg_scan(T *a, uint32_t nb, T *wtot) {
+  const int lane = lane_id(), wave = threadIdx.x / kWave;
+  T c[kRGBucketsPerThread], t = 0;
+#pragma unroll
+  for (int j = 0; j < kRGBucketsPerThread; ++j) {
+    const uint32_t v = threadIdx.x * kRGBucketsPerThread + j;
+    c[j] = v < nb ? a[v] : T(0);
+    t += c[j];
+  }
+  T inc = t;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const T x = __shfl_up(inc, d, kWave);
+    if (lane >= d) inc += x;
+  }
+  if (lane == kWave - 1) wtot[wave] = inc;
+  __syncthreads();
+  T off = inc - t;
+  for (int w = 0; w < wave; ++w) off += wtot[w];
+  T total = 0;
+  for (int w = 0; w < kRGThreads / kWave; ++w) total += wtot[w];
+#pragma unroll
+  for (int j = 0; j < kRGBucketsPerThread; ++j) {
+    const uint32_t v = threadIdx.x * kRGBucketsPerThread + j;
+    if (v < nb) a[v] = off;
+    off += c[j];
+  }
+  if (threadIdx.x == 0) a[nb] = total;
+}
+
+template <bool W8>
+__global__ __launch_bounds__(kRGThreads) void k_rg_write(const int64_t *__restrict__ lkeys,
+                                                         const int64_t *__restrict__ loffs,
+                                                         const int64_t *__restrict__ rkeys,
+                                                         const int64_t *__restrict__ roffs, int64_t nparts,
+                                                         uint64_t flip, uint64_t mn, uint32_t bmask,
+                                                         const int64_t *__restrict__ out_offs, ColSet lc, ColSet rc) {
+  __shared__ uint32_t ls[kRGBuckets + 1], rs[kRGBuckets + 1], oo[kRGBuckets + 1];
+  __shared__ uint32_t lcur[kRGBuckets], rcur[kRGBuckets];
+  __shared__ uint16_t pl[kRGMaxRows], pr[kRGMaxRows];
+  __shared__ uint32_t wtot[3][kRGThreads / kWave];
+  const uint32_t nb = bmask + 1;
+  for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
+    const int64_t lb = loffs[p], nl = loffs[p + 1] - lb;
+    const int64_t rb = roffs[p], nr = roffs[p + 1] - rb;
+    if (nl == 0 || nr == 0 || nl > kRGMaxRows || nr > kRGMaxRows) continue;
+    const int64_t obase = out_offs[p];
+    __syncthreads();  // previous partition fully done with the LDS arrays
+    for (uint32_t v = threadIdx.x; v < nb; v += kRGThreads) ls[v] = rs[v] = 0;
+    __syncthreads();
+    for (int64_t r = threadIdx.x; r < nl; r += kRGThreads) atomicAdd(&ls[rg_bucket(lkeys[lb + r], flip, mn, bmask)], 1u);
+    for (int64_t r = threadIdx.x; r < nr; r += kRGThreads) atomicAdd(&rs[rg_bucket(rkeys[rb + r], flip, mn, bmask)], 1u);
+    __syncthreads();
+    for (uint32_t v = threadIdx.x; v < nb; v += kRGThreads) oo[v] = ls[v] * rs[v];
+    __syncthreads();
+    rg_scan(ls, nb, wtot[0]);
+    rg_scan(rs, nb, wtot[1]);
+    rg_scan(oo, nb, wtot[2]);
+    __syncthreads();
+    for (uint32_t v = threadIdx.x; v < nb; v += kRGThreads) {
+      lcur[v] = ls[v];
+      rcur[v] = rs[v];
+    }
+    __syncthreads();
+    for (int64_t r = threadIdx.x; r < nl; r += kRGThreads)
+      pl[atomicAdd(&lcur[rg_bucket(lkeys[lb + r], flip, mn, bmask)], 1u)] = (uint16_t)r;
+    for (int64_t r = threadIdx.x; r < nr; r += kRGThreads)
+      pr[atomicAdd(&rcur[rg_bucket(rkeys[rb + r], flip, mn, bmask)], 1u)] = (uint16_t)r;
+    __syncthreads();
+    const uint32_t total = oo[nb];
+    for (uint32_t t = threadIdx.x; t < total; t += kRGThreads) {
+      uint32_t lo = 0, hi = nb;  // largest v with oo[v] <= t (always a non-empty key)
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (oo[mid] <= t) lo = mid; else hi = mid;
+      }
+      const uint32_t v = lo;
+      const uint32_t idx = t - oo[v], cr = rs[v + 1] - rs[v];
+      const uint32_t li = idx / cr, ri = idx - li * cr;
+      const int64_t lrow = lb + pl[ls[v] + li], rrow = rb + pr[rs[v] + ri];
+      const int64_t o = obase + t;
+#pragma unroll
+      for (int q = 0; q < kMaxFusedCols; ++q)
+        if (q < lc.n) stw<W8>(lc.out[q], o, lc.width[q], ldw<W8>(lc.in[q], lrow, lc.width[q]));
+#pragma unroll
+      for (int q = 0; q < kMaxFusedCols; ++q)
+        if (q < rc.n) stw<W8>(rc.out[q], o, rc.width[q], ldw<W8>(rc.in[q], rrow, rc.width[q]));
+    }
+  }
+}
+
+static int rg_grid(int64_t nparts) { return (int)std::min<int64_t>(nparts, kNumCUs * 4); }
+
+void range_join_count(const int64_t *lkeys, const int64_t *loffs, const int64_t *rkeys, const int64_t *roffs,
+                      int64_t nparts, uint64_t flip, uint64_t mn, int rshift, int64_t *counts, int *overflow,
+                      void *stream) {
+  CYLON_CHECK(rshift >= 0 && rshift <= 12, Code::Invalid, "range join key bits per partition " << rshift);
+  hipStream_t s = as_stream(stream);
+  HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
+  if (nparts == 0) return;
+  hipLaunchKernelGGL(k_rg_count, dim3(rg_grid(nparts)), dim3(kRGThreads), 0, s, lkeys, loffs, rkeys, roffs, nparts,
+                     flip, mn, (uint32_t)((1u << rshift) - 1), counts, overflow);
+  HIP_LAUNCH_CHECK();
+}
+
+void range_join_write(const int64_t *lkeys, const int64_t *loffs, const int64_t *rkeys, const int64_t *roffs,
+                      int64_t nparts, uint64_t flip, uint64_t mn, int rshift, const int64_t *out_offs,
+                      const uint8_t *const *lin, uint8_t *const *lout, const int *lw, int nlc,
+                      const uint8_t *const *rin, uint8_t *const *rout, const int *rw, int nrc, void *stream) {
+  CYLON_CHECK(rshift >= 0 && rshift <= 12, Code::Invalid, "range join key bits per partition " << rshift);
+  CYLON_CHECK(nlc <= kMaxFusedCols && nrc <= kMaxFusedCols, Code::Invalid, "too many columns");
+  if (nparts == 0) return;
+  ColSet lc, rc;
+  lc.n = nlc;
+  rc.n = nrc;
+  bool w8 = true;
+  for (int q = 0; q < kMaxFusedCols; ++q) {
+    lc.in[q] = q < nlc ? lin[q] : nullptr;
+    lc.out[q] = q < nlc ? lout[q] : nullptr;
+    lc.width[q] = q < nlc ? lw[q] : 8;
+    rc.in[q] = q < nrc ? rin[q] : nullptr;
+    rc.out[q] = q < nrc ? rout[q] : nullptr;
+    rc.width[q] = q < nrc ? rw[q] : 8;
+    if (q < nlc) w8 &= lw[q] == 8;
+    if (q < nrc) w8 &= rw[q] == 8;
+  }
+  const uint32_t bmask = (uint32_t)((1u << rshift) - 1);
+  hipStream_t s = as_stream(stream);
+  if (w8)
+    hipLaunchKernelGGL(k_rg_write<true>, dim3(rg_grid(nparts)), dim3(kRGThreads), 0, s, lkeys, loffs, rkeys, roffs,
+                       nparts, flip, mn, bmask, out_offs, lc, rc);
+  else
+    hipLaunchKernelGGL(k_rg_write<false>, dim3(rg_grid(nparts)), dim3(kRGThreads), 0, s, lkeys, loffs, rkeys, roffs,
+                       nparts, flip, mn, bmask, out_offs, lc, rc);
   HIP_LAUNCH_CHECK();
 }
 

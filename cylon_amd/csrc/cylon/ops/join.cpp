@@ -161,7 +161,8 @@ struct RadixSide {
 };
 
 // Partition every column of t (+ validity bytes) by the top `bits` bits of fmix64(key).
-static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Tensor &keys, int bits) {
+static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Tensor &keys, int bits,
+                                 const RangeSpec *range = nullptr) {
   std::vector<at::Tensor> cur{keys};
   std::vector<int> widths{8};
   std::vector<int> dslot(t->Columns(), -1), vslot(t->Columns(), -1);
@@ -181,7 +182,7 @@ static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Te
     }
   }
   at::Tensor offs;
-  cur = RadixPartition(ex, std::move(cur), widths, bits, &offs);
+  cur = RadixPartition(ex, std::move(cur), widths, bits, &offs, range);
   RadixSide s;
   s.keys = cur[0];
   s.offs = offs;
@@ -470,6 +471,90 @@ static TablePtr sorted_merge_join(const Exec &ex, const TablePtr &left, const Ta
   return Table::Make(left->GetContext(), std::move(cols));
 }
 
+// K7 range join (device, inner, one signed integer key, algorithm = SORT): both
+// relations are radix-partitioned into key ranges in key order (RangeSpec), each
+// partition holding 2^rshift consecutive key values (rshift <= 12), and each
+// partition is joined in LDS by exact key offset, emitting its rows in key order
+// (radix_join.hip k_rg_*).  Same passes as the hash radix join, no full sort.
+// Returns nullptr when the keys are too sparse for 12-bit partitions or a
+// partition overflows (skew): the caller then runs sorted_merge_join.
+static bool range_join_enabled() {
+  const char *e = std::getenv("CYLON_RANGE_JOIN");  // test / tuning knob: 0 = sort-merge path only
+  return !(e && e[0] == '0');
+}
+
+static TablePtr range_join(const Exec &ex, const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
+  const int lc = cfg.GetLeftColumnIdx()[0], rc = cfg.GetRightColumnIdx()[0];
+  if (left->column(lc).type.kind() != ValueKind::SIGNED_INT) return nullptr;
+  const int64_t nl = left->Rows(), nr = right->Rows();
+  KeyEncoding lk = encode_keys(ex, left, {lc}, true), rk = encode_keys(ex, right, {rc}, true);
+  at::Tensor mm = at::stack({lk.keys.min(), lk.keys.max(), rk.keys.min(), rk.keys.max()}).to(at::kCPU);
+  const int64_t *h = mm.data_ptr<int64_t>();
+  const int64_t kmin = std::min(h[0], h[2]), kmax = std::max(h[1], h[3]);
+  const uint64_t span = (uint64_t)kmax - (uint64_t)kmin;  // signed range as an unsigned count
+  int span_bits = 0;
+  while (span_bits < 64 && (span >> span_bits) != 0) ++span_bits;
+  // ~half the LDS capacity per side and partition on average: far below the cap for uniform keys
+  const int64_t target = hip::range_join_max_rows() / 2;
+  int bits = 0;
+  while ((std::max(nl, nr) >> bits) > target) ++bits;
+  // sparse keys: up to 16x more (smaller) partitions than the row count asks for keep
+  // each partition's key range within the 4096 exact-offset buckets
+  const int maxs = hip::range_join_max_shift();
+  if (span_bits - bits > maxs && span_bits - maxs <= bits + 4) bits = span_bits - maxs;
+  const int rshift = std::max(0, span_bits - bits);
+  if (rshift > maxs) {
+    trace::add_counter("join.range.sparse_fallback", 1);
+    return nullptr;
+  }
+  const int pbits = span_bits - rshift;
+  RangeSpec spec;
+  spec.flip = uint64_t(1) << 63;  // signed -> order-preserving unsigned image
+  spec.mn = (uint64_t)kmin ^ spec.flip;
+  spec.rshift = rshift;
+  const int64_t nparts = int64_t(1) << pbits;
+  RadixSide L, R;
+  {
+    CYLON_PHASE("join.range.partition", ex.device);
+    L = radix_partition(ex, left, lk.keys, pbits, &spec);
+    R = radix_partition(ex, right, rk.keys, pbits, &spec);
+  }
+  at::Tensor counts = ex.empty_i64(nparts);
+  at::Tensor overflow = at::empty({1}, ex.opts(at::kInt));
+  {
+    CYLON_PHASE("join.range.count", ex.device);
+    hip::range_join_count(ptr<int64_t>(L.keys), ptr<int64_t>(L.offs), ptr<int64_t>(R.keys), ptr<int64_t>(R.offs),
+                          nparts, spec.flip, spec.mn, rshift, ptr<int64_t>(counts), overflow.data_ptr<int>(),
+                          ex.stream);
+  }
+  if (overflow.item<int>() != 0) {
+    trace::add_counter("join.range.overflow_fallback", 1);
+    return nullptr;
+  }
+  at::Tensor out_offs = exclusive_scan(ex, counts);
+  const int64_t m = read_i64(out_offs, nparts);
+  CYLON_PHASE("join.range.write", ex.device);
+  std::vector<Column> lcols, rcols;
+  for (const auto &col : left->columns())
+    lcols.push_back(make_fixed_column(cfg.GetLeftTablePrefix() + col.name, col.type, m, ex.device, col.nullable()));
+  for (const auto &col : right->columns())
+    rcols.push_back(make_fixed_column(cfg.GetRightTablePrefix() + col.name, col.type, m, ex.device, col.nullable()));
+  if (m > 0) {
+    RadixCols a = radix_cols(left, &L, &lcols), b = radix_cols(right, &R, &rcols);
+    for (auto &q : a.in)
+      if (!q) q = reinterpret_cast<const uint8_t *>(L.keys.data_ptr());
+    for (auto &q : b.in)
+      if (!q) q = reinterpret_cast<const uint8_t *>(R.keys.data_ptr());
+    hip::range_join_write(ptr<int64_t>(L.keys), ptr<int64_t>(L.offs), ptr<int64_t>(R.keys), ptr<int64_t>(R.offs),
+                          nparts, spec.flip, spec.mn, rshift, ptr<int64_t>(out_offs), a.in.data(), a.out.data(),
+                          a.w.data(), (int)a.in.size(), b.in.data(), b.out.data(), b.w.data(), (int)b.in.size(),
+                          ex.stream);
+  }
+  trace::add_counter("join.range.rows_out", m);
+  for (auto &c : rcols) lcols.push_back(std::move(c));
+  return Table::Make(left->GetContext(), std::move(lcols));
+}
+
 // Local join.  With a sink (chunked distributed join) the radix path writes into
 // the sink and nullptr is returned; other paths return their table.
 static TablePtr join_local(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg, JoinSink *sink) {
@@ -478,8 +563,12 @@ static TablePtr join_local(const TablePtr &left, const TablePtr &right, const Jo
       radix_eligible(left) && radix_eligible(right)) {
     const Column &a = left->column(cfg.GetLeftColumnIdx()[0]);
     const Column &b = right->column(cfg.GetRightColumnIdx()[0]);
-    if (simple_key(a) && simple_key(b) && a.type == b.type && a.type.kind() != ValueKind::FLOAT)
-      return sorted_merge_join(Exec(left->device()), left, right, cfg);
+    if (simple_key(a) && simple_key(b) && a.type == b.type && a.type.kind() != ValueKind::FLOAT) {
+      Exec ex(left->device());
+      if (range_join_enabled())
+        if (TablePtr out = range_join(ex, left, right, cfg)) return out;
+      return sorted_merge_join(ex, left, right, cfg);
+    }
   }
   if (left->device().is_cuda() && cfg.GetType() == JoinType::INNER && cfg.GetAlgorithm() == JoinAlgorithm::HASH &&
       cfg.GetLeftColumnIdx().size() == 1 && std::min(left->Rows(), right->Rows()) >= radix_join_min_rows() &&

@@ -8,7 +8,7 @@ namespace cylon {
 namespace ops {
 
 std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> cur, const std::vector<int> &widths,
-                                       int bits, at::Tensor *offs) {
+                                       int bits, at::Tensor *offs, const RangeSpec *range) {
   CYLON_CHECK(ex.gpu, Code::Invalid, "RadixPartition is a device path");
   CYLON_CHECK(!cur.empty() && cur.size() == widths.size() && widths[0] == 8, Code::Invalid,
               "RadixPartition: column 0 must be the int64 key");
@@ -32,13 +32,22 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
       in.push_back(reinterpret_cast<const uint8_t *>(x.data_ptr()));
       out.push_back(reinterpret_cast<uint8_t *>(nxt.back().data_ptr()));
     }
-    hip::radix_rows_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, bits, shift, db, in.data(),
-                         out.data(), widths.data(), (int)cur.size(), ptr<int64_t>(ws), ex.stream);
+    if (range)
+      hip::radix_range_rows_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, range->flip, range->mn,
+                                 range->rshift, shift, db, in.data(), out.data(), widths.data(), (int)cur.size(),
+                                 ptr<int64_t>(ws), ex.stream);
+    else
+      hip::radix_rows_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, bits, shift, db, in.data(),
+                           out.data(), widths.data(), (int)cur.size(), ptr<int64_t>(ws), ex.stream);
     cur = std::move(nxt);
     shift += db;
   }
   *offs = ex.empty_i64((int64_t(1) << bits) + 1);
-  hip::radix_part_offsets(ptr<int64_t>(cur[0]), n, bits, ptr<int64_t>(*offs), ex.stream);
+  if (range)
+    hip::radix_range_part_offsets(ptr<int64_t>(cur[0]), n, range->flip, range->mn, range->rshift, bits,
+                                  ptr<int64_t>(*offs), ex.stream);
+  else
+    hip::radix_part_offsets(ptr<int64_t>(cur[0]), n, bits, ptr<int64_t>(*offs), ex.stream);
   return cur;
 }
 

@@ -55,9 +55,14 @@ inline std::vector<int64_t> to_host_vec(const at::Tensor &t) {
 // Radix-partition tensors by the top `bits` bits of fmix64(cols[0]) (cols[0] =
 // int64 keys, widths 1/2/4/8 bytes) with LSD passes of <= 10 bits
 // (radix_join.hip).  Returns the permuted tensors; *offs = partition offsets
-// [2^bits + 1].  GPU only.
+// [2^bits + 1].  GPU only.  With `range` the partition is instead the order-
+// preserving ((key ^ flip) - mn) >> rshift (key ranges in key order).
+struct RangeSpec {
+  uint64_t flip = 0, mn = 0;
+  int rshift = 0;
+};
 std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> cols, const std::vector<int> &widths,
-                                       int bits, at::Tensor *offs);
+                                       int bits, at::Tensor *offs, const RangeSpec *range = nullptr);
 
 // exclusive scan of int64 counts -> offsets[n+1]
 inline at::Tensor exclusive_scan(const Exec &ex, const at::Tensor &counts) {

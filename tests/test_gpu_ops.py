@@ -227,6 +227,7 @@ def test_sorted_merge_join_matches_cpu(gpu_ctx, ctx, monkeypatch):
     from cylon_amd._lib import C
     monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", "1")
     monkeypatch.setenv("CYLON_RADIX_SORT_MIN_ROWS", "1")
+    monkeypatch.setenv("CYLON_RANGE_JOIN", "0")
     rng = np.random.default_rng(12)
     a = pa.table({"k": rng.integers(-3000, 3000, 40_000), "x": rng.random(40_000),
                   "i": pa.array(rng.integers(0, 9, 40_000).astype(np.int32))})
@@ -267,4 +268,39 @@ def test_sorted_merge_join_window_shapes(gpu_ctx, ctx, monkeypatch, shape):
     c = Table(a, ctx).join(Table(b, ctx), "inner", "sort", on=["k"]).to_pandas()
     assert len(g) == len(c)
     key = lambda df: sorted(map(tuple, df[sorted(df.columns)].to_numpy().tolist()))
+    assert key(g) == key(c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["signed_wide", "int32_nullable", "dups"])
+def test_range_join_matches_cpu(gpu_ctx, ctx, monkeypatch, shape):
+    """algorithm="sort" through the range join (order-preserving range partitions + per-partition LDS join by
+    exact key offset): same rows as the CPU twin, ordered by key."""
+    from cylon_amd._lib import C
+    monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", "1")
+    rng = np.random.default_rng(21)
+    if shape == "signed_wide":
+        base = -(2 ** 40)
+        a = pa.table({"k": base + rng.integers(0, 100_000, 50_000), "x": rng.random(50_000)})
+        b = pa.table({"k": base + rng.integers(0, 100_000, 30_000), "y": rng.random(30_000)})
+    elif shape == "int32_nullable":
+        ka = rng.integers(-20_000, 30_000, 40_000).astype(np.int32)
+        kb = rng.integers(-20_000, 30_000, 35_000).astype(np.int32)
+        xa = pa.array(rng.random(40_000), mask=rng.random(40_000) < 0.1)
+        ib = pa.array(rng.integers(0, 100, 35_000).astype(np.int8), mask=rng.random(35_000) < 0.2)
+        a = pa.table({"k": pa.array(ka), "x": xa})
+        b = pa.table({"k": pa.array(kb), "i": ib, "z": rng.random(35_000)})
+    else:
+        a = pa.table({"k": rng.integers(0, 256, 20_000), "x": rng.random(20_000)})
+        b = pa.table({"k": rng.integers(0, 256, 20_000), "y": rng.random(20_000)})
+    C.trace_enable(True)
+    C.trace_reset()
+    g = Table(a, gpu_ctx).join(Table(b, gpu_ctx), "inner", "sort", on=["k"], left_prefix="l_",
+                               right_prefix="r_").to_pandas()
+    assert C.trace_counters().get("join.range.rows_out", -1) == len(g)
+    C.trace_enable(False)
+    c = Table(a, ctx).join(Table(b, ctx), "inner", "sort", on=["k"], left_prefix="l_", right_prefix="r_").to_pandas()
+    assert len(g) == len(c) > 0
+    assert np.all(np.diff(g["l_k"].to_numpy().astype(np.int64)) >= 0)
+    key = lambda df: sorted(map(tuple, df[sorted(df.columns)].fillna(-1).to_numpy().tolist()))
     assert key(g) == key(c)
