@@ -951,6 +951,39 @@ __device__ __forceinline__ void rg_scan(T *a, uint32_t nb, T *wtot) {
   if (threadIdx.x == 0) a[nb] = total;
 }
 
+constexpr int kRGEmit = 4;  // output rows per thread per emit chunk (4096 per chunk)
+
+// stream one column of a partition side into the LDS stage (coalesced), then write
+// the chunk's output rows from it: an output row's payload is a random row of the
+// partition, so gathering it straight from global memory would pull a whole cache
+// line through L2 -> L1 per 8-byte value (the first version of this kernel was
+// bound by exactly that).
+template <bool W8>
+__device__ __forceinline__ void rg_emit_column(uint8_t *stage, const uint8_t *in, int64_t base, int64_t rows,
+                                               uint8_t *out, int w, int64_t obase, uint32_t c0, uint32_t total,
+                                               const uint16_t *pos) {
+  __syncthreads();  // stage free
+  for (int64_t r0 = 0; r0 < rows; r0 += 4 * kRGThreads) {  // four loads in flight per thread
+    uint64_t x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t r = r0 + u * kRGThreads + threadIdx.x;
+      if (r < rows) x[u] = ldw<W8>(in, base + r, w);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t r = r0 + u * kRGThreads + threadIdx.x;
+      if (r < rows) stw<W8>(stage, r, w, x[u]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < kRGEmit; ++e) {
+    const uint32_t t = c0 + e * kRGThreads + threadIdx.x;
+    if (t < total) stw<W8>(out, obase + t, w, ldw<W8>(stage, pos[e], w));
+  }
+}
+
 template <bool W8>
 __global__ __launch_bounds__(kRGThreads) void k_rg_write(const int64_t *__restrict__ lkeys,
                                                          const int64_t *__restrict__ loffs,
@@ -959,9 +992,12 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_write(const int64_t *__restri
                                                          uint64_t flip, uint64_t mn, uint32_t bmask,
                                                          const int64_t *__restrict__ out_offs, ColSet lc, ColSet rc) {
   __shared__ uint32_t ls[kRGBuckets + 1], rs[kRGBuckets + 1], oo[kRGBuckets + 1];
-  __shared__ uint32_t lcur[kRGBuckets], rcur[kRGBuckets];
   __shared__ uint16_t pl[kRGMaxRows], pr[kRGMaxRows];
+  __shared__ uint64_t stage64[kRGMaxRows];  // scatter cursors, then one payload column at a time
   __shared__ uint32_t wtot[3][kRGThreads / kWave];
+  uint8_t *stage = reinterpret_cast<uint8_t *>(stage64);
+  uint32_t *lcur = reinterpret_cast<uint32_t *>(stage64), *rcur = lcur + kRGBuckets;
+  static_assert(2 * kRGBuckets * sizeof(uint32_t) <= kRGMaxRows * sizeof(uint64_t), "cursors fit the stage");
   const uint32_t nb = bmask + 1;
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
     const int64_t lb = loffs[p], nl = loffs[p + 1] - lb;
@@ -991,23 +1027,30 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_write(const int64_t *__restri
       pr[atomicAdd(&rcur[rg_bucket(rkeys[rb + r], flip, mn, bmask)], 1u)] = (uint16_t)r;
     __syncthreads();
     const uint32_t total = oo[nb];
-    for (uint32_t t = threadIdx.x; t < total; t += kRGThreads) {
-      uint32_t lo = 0, hi = nb;  // largest v with oo[v] <= t (always a non-empty key)
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (oo[mid] <= t) lo = mid; else hi = mid;
+    for (uint32_t c0 = 0; c0 < total; c0 += kRGEmit * kRGThreads) {
+      uint16_t lp[kRGEmit], rp[kRGEmit];  // partition rows of this thread's output rows
+#pragma unroll
+      for (int e = 0; e < kRGEmit; ++e) {
+        const uint32_t t = c0 + e * kRGThreads + threadIdx.x;
+        lp[e] = rp[e] = 0;
+        if (t < total) {
+          uint32_t lo = 0, hi = nb;  // largest v with oo[v] <= t (always a non-empty key)
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (oo[mid] <= t) lo = mid; else hi = mid;
+          }
+          const uint32_t idx = t - oo[lo], cr = rs[lo + 1] - rs[lo];
+          const uint32_t li = idx / cr, ri = idx - li * cr;
+          lp[e] = pl[ls[lo] + li];
+          rp[e] = pr[rs[lo] + ri];
+        }
       }
-      const uint32_t v = lo;
-      const uint32_t idx = t - oo[v], cr = rs[v + 1] - rs[v];
-      const uint32_t li = idx / cr, ri = idx - li * cr;
-      const int64_t lrow = lb + pl[ls[v] + li], rrow = rb + pr[rs[v] + ri];
-      const int64_t o = obase + t;
-#pragma unroll
-      for (int q = 0; q < kMaxFusedCols; ++q)
-        if (q < lc.n) stw<W8>(lc.out[q], o, lc.width[q], ldw<W8>(lc.in[q], lrow, lc.width[q]));
-#pragma unroll
-      for (int q = 0; q < kMaxFusedCols; ++q)
-        if (q < rc.n) stw<W8>(rc.out[q], o, rc.width[q], ldw<W8>(rc.in[q], rrow, rc.width[q]));
+#pragma unroll 1
+      for (int q = 0; q < lc.n; ++q)
+        rg_emit_column<W8>(stage, lc.in[q], lb, nl, lc.out[q], lc.width[q], obase, c0, total, lp);
+#pragma unroll 1
+      for (int q = 0; q < rc.n; ++q)
+        rg_emit_column<W8>(stage, rc.in[q], rb, nr, rc.out[q], rc.width[q], obase, c0, total, rp);
     }
   }
 }

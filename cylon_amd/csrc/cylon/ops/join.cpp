@@ -495,7 +495,10 @@ static TablePtr range_join(const Exec &ex, const TablePtr &left, const TablePtr 
   int span_bits = 0;
   while (span_bits < 64 && (span >> span_bits) != 0) ++span_bits;
   // ~half the LDS capacity per side and partition on average: far below the cap for uniform keys
-  const int64_t target = hip::range_join_max_rows() / 2;
+  static const int64_t target = [] {  // tuning knob
+    const char *e = std::getenv("CYLON_RANGE_JOIN_TARGET");
+    return e ? std::max<int64_t>(1, std::atoll(e)) : hip::range_join_max_rows() / 2;
+  }();
   int bits = 0;
   while ((std::max(nl, nr) >> bits) > target) ++bits;
   // sparse keys: up to 16x more (smaller) partitions than the row count asks for keep
