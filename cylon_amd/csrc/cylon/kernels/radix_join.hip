@@ -873,8 +873,30 @@ constexpr int kRGBucketsPerThread = kRGBuckets / kRGThreads;
 int64_t range_join_max_rows() { return kRGMaxRows; }
 int range_join_max_shift() { return 12; }
 
-__device__ __forceinline__ uint32_t rg_bucket(int64_t k, uint64_t flip, uint64_t mn, uint32_t bmask) {
-  return (uint32_t)(((uint64_t)k ^ flip) - mn) & bmask;
+constexpr int kRGRowsPerThread = kRGMaxRows / kRGThreads;
+
+// Low 32 bits of a partition's keys (all the bucket needs: the offset is taken
+// mod 2^rshift) held in registers, kRGRowsPerThread per thread; loaded for the
+// next partition while the current one is processed.
+struct RGKeys {
+  int64_t b = 0, n = 0;
+  uint32_t k[kRGRowsPerThread];
+};
+
+__device__ __forceinline__ void rg_load(const int64_t *__restrict__ keys, const int64_t *__restrict__ offs, int64_t p,
+                                        RGKeys &s) {
+  s.b = offs[p];
+  s.n = offs[p + 1] - s.b;
+  const uint32_t *k32 = reinterpret_cast<const uint32_t *>(keys);
+#pragma unroll
+  for (int i = 0; i < kRGRowsPerThread; ++i) {
+    const int64_t r = threadIdx.x + i * kRGThreads;
+    if (r < s.n && r < kRGMaxRows) s.k[i] = k32[2 * (s.b + r)];  // little endian: low half
+  }
+}
+
+__device__ __forceinline__ uint32_t rg_bucket32(uint32_t k, uint32_t flip, uint32_t mn, uint32_t bmask) {
+  return ((k ^ flip) - mn) & bmask;
 }
 
 __global__ __launch_bounds__(kRGThreads) void k_rg_count(const int64_t *__restrict__ lkeys,
@@ -885,26 +907,38 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_count(const int64_t *__restri
                                                          int64_t *__restrict__ counts, int *overflow) {
   __shared__ uint32_t hl[kRGBuckets], hr[kRGBuckets];
   __shared__ unsigned long long wsum[kRGThreads / kWave];
-  const uint32_t nb = bmask + 1;
+  const uint32_t nb = bmask + 1, f32 = (uint32_t)flip, m32 = (uint32_t)mn;
+  RGKeys nl_, nr_;
+  if ((int64_t)blockIdx.x < nparts) {
+    rg_load(lkeys, loffs, blockIdx.x, nl_);
+    rg_load(rkeys, roffs, blockIdx.x, nr_);
+  }
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
-    const int64_t lb = loffs[p], nl = loffs[p + 1] - lb;
-    const int64_t rb = roffs[p], nr = roffs[p + 1] - rb;
-    if (nl > kRGMaxRows || nr > kRGMaxRows) {  // uniform branch
+    const RGKeys L = nl_, R = nr_;
+    if (p + gridDim.x < nparts) {  // next partition's keys in flight during this one
+      rg_load(lkeys, loffs, p + gridDim.x, nl_);
+      rg_load(rkeys, roffs, p + gridDim.x, nr_);
+    }
+    if (L.n > kRGMaxRows || R.n > kRGMaxRows) {  // uniform branch
       if (threadIdx.x == 0) {
         atomicOr(overflow, 1);
         counts[p] = 0;
       }
       continue;
     }
-    if (nl == 0 || nr == 0) {
+    if (L.n == 0 || R.n == 0) {
       if (threadIdx.x == 0) counts[p] = 0;
       continue;
     }
     __syncthreads();  // previous partition done with hl / hr / wsum
     for (uint32_t v = threadIdx.x; v < nb; v += kRGThreads) hl[v] = hr[v] = 0;
     __syncthreads();
-    for (int64_t r = threadIdx.x; r < nl; r += kRGThreads) atomicAdd(&hl[rg_bucket(lkeys[lb + r], flip, mn, bmask)], 1u);
-    for (int64_t r = threadIdx.x; r < nr; r += kRGThreads) atomicAdd(&hr[rg_bucket(rkeys[rb + r], flip, mn, bmask)], 1u);
+#pragma unroll
+    for (int i = 0; i < kRGRowsPerThread; ++i) {
+      const int64_t r = threadIdx.x + i * kRGThreads;
+      if (r < L.n) atomicAdd(&hl[rg_bucket32(L.k[i], f32, m32, bmask)], 1u);
+      if (r < R.n) atomicAdd(&hr[rg_bucket32(R.k[i], f32, m32, bmask)], 1u);
+    }
     __syncthreads();
     unsigned long long c = 0;
     for (uint32_t v = threadIdx.x; v < nb; v += kRGThreads) c += (unsigned long long)hl[v] * hr[v];
@@ -998,17 +1032,30 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_write(const int64_t *__restri
   uint8_t *stage = reinterpret_cast<uint8_t *>(stage64);
   uint32_t *lcur = reinterpret_cast<uint32_t *>(stage64), *rcur = lcur + kRGBuckets;
   static_assert(2 * kRGBuckets * sizeof(uint32_t) <= kRGMaxRows * sizeof(uint64_t), "cursors fit the stage");
-  const uint32_t nb = bmask + 1;
+  const uint32_t nb = bmask + 1, f32 = (uint32_t)flip, m32 = (uint32_t)mn;
+  RGKeys nl_, nr_;
+  if ((int64_t)blockIdx.x < nparts) {
+    rg_load(lkeys, loffs, blockIdx.x, nl_);
+    rg_load(rkeys, roffs, blockIdx.x, nr_);
+  }
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
-    const int64_t lb = loffs[p], nl = loffs[p + 1] - lb;
-    const int64_t rb = roffs[p], nr = roffs[p + 1] - rb;
+    const RGKeys L = nl_, R = nr_;
+    if (p + gridDim.x < nparts) {  // next partition's keys in flight during this one
+      rg_load(lkeys, loffs, p + gridDim.x, nl_);
+      rg_load(rkeys, roffs, p + gridDim.x, nr_);
+    }
+    const int64_t lb = L.b, nl = L.n, rb = R.b, nr = R.n;
     if (nl == 0 || nr == 0 || nl > kRGMaxRows || nr > kRGMaxRows) continue;
     const int64_t obase = out_offs[p];
     __syncthreads();  // previous partition fully done with the LDS arrays
     for (uint32_t v = threadIdx.x; v < nb; v += kRGThreads) ls[v] = rs[v] = 0;
     __syncthreads();
-    for (int64_t r = threadIdx.x; r < nl; r += kRGThreads) atomicAdd(&ls[rg_bucket(lkeys[lb + r], flip, mn, bmask)], 1u);
-    for (int64_t r = threadIdx.x; r < nr; r += kRGThreads) atomicAdd(&rs[rg_bucket(rkeys[rb + r], flip, mn, bmask)], 1u);
+#pragma unroll
+    for (int i = 0; i < kRGRowsPerThread; ++i) {
+      const int64_t r = threadIdx.x + i * kRGThreads;
+      if (r < nl) atomicAdd(&ls[rg_bucket32(L.k[i], f32, m32, bmask)], 1u);
+      if (r < nr) atomicAdd(&rs[rg_bucket32(R.k[i], f32, m32, bmask)], 1u);
+    }
     __syncthreads();
     for (uint32_t v = threadIdx.x; v < nb; v += kRGThreads) oo[v] = ls[v] * rs[v];
     __syncthreads();
@@ -1021,10 +1068,12 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_write(const int64_t *__restri
       rcur[v] = rs[v];
     }
     __syncthreads();
-    for (int64_t r = threadIdx.x; r < nl; r += kRGThreads)
-      pl[atomicAdd(&lcur[rg_bucket(lkeys[lb + r], flip, mn, bmask)], 1u)] = (uint16_t)r;
-    for (int64_t r = threadIdx.x; r < nr; r += kRGThreads)
-      pr[atomicAdd(&rcur[rg_bucket(rkeys[rb + r], flip, mn, bmask)], 1u)] = (uint16_t)r;
+#pragma unroll
+    for (int i = 0; i < kRGRowsPerThread; ++i) {
+      const int64_t r = threadIdx.x + i * kRGThreads;
+      if (r < nl) pl[atomicAdd(&lcur[rg_bucket32(L.k[i], f32, m32, bmask)], 1u)] = (uint16_t)r;
+      if (r < nr) pr[atomicAdd(&rcur[rg_bucket32(R.k[i], f32, m32, bmask)], 1u)] = (uint16_t)r;
+    }
     __syncthreads();
     const uint32_t total = oo[nb];
     for (uint32_t c0 = 0; c0 < total; c0 += kRGEmit * kRGThreads) {
