@@ -49,9 +49,12 @@ __device__ __forceinline__ bool is_nan_bits(uint64_t bits, int w) {
   return (bits & 0x7c00ull) == 0x7c00ull && (bits & 0x03ffull);
 }
 
+// acc != nullptr: also OR / AND-reduce the images into acc[0] / acc[1] (the bits
+// that vary, for the radix pass count) so the sort needs no second read of them
 __global__ void k_sort_keys(ColView c, const int64_t *__restrict__ perm, int64_t n, bool desc,
-                            uint64_t *__restrict__ out) {
+                            uint64_t *__restrict__ out, unsigned long long *acc) {
   const int nb = 8 * c.width;
+  uint64_t o = 0, a = ~0ull;
   const uint64_t mask = (nb == 64) ? ~0ull : ((1ull << nb) - 1);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -64,14 +67,42 @@ __global__ void k_sort_keys(ColView c, const int64_t *__restrict__ perm, int64_t
     // significant) sort columns, so equal rows stay adjacent in multi-column sorts
     if (c.valid != nullptr && c.valid[s] == 0) k = mask;
     out[i] = k;
+    o |= k;
+    a &= k;
+  }
+  if (acc == nullptr) return;
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    o |= __shfl_xor(o, d, kWave);
+    a &= __shfl_xor(a, d, kWave);
+  }
+  if (lane_id() == 0) {
+    atomicOr(&acc[0], (unsigned long long)o);
+    atomicAnd(&acc[1], (unsigned long long)a);
   }
 }
 
 void sort_keys_from_column(const ColView &col, const int64_t *perm, int64_t n, bool desc, uint64_t *out,
                            void *stream) {
   if (n == 0) return;
-  hipLaunchKernelGGL(k_sort_keys, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), col, perm, n, desc, out);
+  hipLaunchKernelGGL(k_sort_keys, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), col, perm, n, desc, out,
+                     nullptr);
   HIP_LAUNCH_CHECK();
+}
+
+uint64_t sort_keys_varying_bits(const ColView &col, int64_t n, bool desc, uint64_t *out, int64_t *ws2,
+                                void *stream) {
+  if (n == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  unsigned long long *acc = reinterpret_cast<unsigned long long *>(ws2);
+  unsigned long long init[2] = {0ull, ~0ull};
+  HIP_CHECK(hipMemcpyAsync(acc, init, sizeof(init), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_sort_keys, dim3(grid_for(n)), dim3(kBlock), 0, s, col, nullptr, n, desc, out, acc);
+  HIP_LAUNCH_CHECK();
+  unsigned long long oa[2];
+  HIP_CHECK(hipMemcpyAsync(oa, acc, sizeof(oa), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return n <= 1 ? 0 : (oa[0] ^ oa[1]);
 }
 
 // ---------------------------------------------------------------------------

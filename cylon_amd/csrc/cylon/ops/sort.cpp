@@ -108,10 +108,9 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
   Exec ex(t->device());
   CYLON_PHASE("sort.radix_rows", ex.device);
   at::Tensor img = ex.empty_i64(n);
-  hip::sort_keys_from_column(kc.view(), nullptr, n, !asc, reinterpret_cast<uint64_t *>(ptr<int64_t>(img)), ex.stream);
   at::Tensor ws2 = ex.empty_i64(2);
-  const uint64_t diff = hip::varying_bits(reinterpret_cast<const uint64_t *>(ptr<int64_t>(img)), n,
-                                          ptr<int64_t>(ws2), ex.stream);
+  const uint64_t diff = hip::sort_keys_varying_bits(kc.view(), n, !asc, reinterpret_cast<uint64_t *>(ptr<int64_t>(img)),
+                                                    ptr<int64_t>(ws2), ex.stream);
   // an integer key is rebuilt from its image at the end instead of travelling too
   const bool key_from_image = kc.type.kind() == ValueKind::SIGNED_INT || kc.type.kind() == ValueKind::UNSIGNED_INT;
   std::vector<at::Tensor> cur{img};
