@@ -44,6 +44,7 @@ struct ColSet {
   uint8_t *out[kMaxFusedCols];
   int width[kMaxFusedCols];
   int n;
+  uint64_t key_xor;  // XORed into column 0 as it is stored (a sort's last pass rebuilds int64 keys from images)
 };
 
 __device__ __forceinline__ uint32_t part_of(int64_t key, int bits) {
@@ -275,9 +276,10 @@ __global__ __launch_bounds__(kRPThreads) void k_rows_pass(Digit digit, int nbits
     for (int c = 0; c < cols.n; ++c) {  // column fields fetched once per column (scalar loads)
       const int w = cols.width[c];
       uint8_t *out = cols.out[c];
+      const uint64_t x = c == 0 ? cols.key_xor : 0ull;
 #pragma unroll
       for (int k = 0; k < kRPItems; ++k)
-        if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k]);
+        if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
       __syncthreads();
       if (c + 1 < cols.n) {  // prefetch column c+1 of this tile
         const uint8_t *in = cols.in[c + 1];
@@ -325,7 +327,7 @@ int64_t radix_rows_pass_workspace(int64_t n, int digit_bits) {
 
 template <class Digit>
 static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const uint8_t *const *in, uint8_t *const *out,
-                             const int *widths, int ncols, int64_t *ws, void *stream) {
+                             const int *widths, int ncols, int64_t *ws, void *stream, uint64_t key_xor = 0) {
   if (n == 0) return;
   CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
   CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
@@ -342,6 +344,7 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   exclusive_scan(bh, m, bh_scan, scan_ws, stream);
   ColSet cs;
   cs.n = ncols;
+  cs.key_xor = key_xor;
   for (int c = 0; c < kMaxFusedCols; ++c) {
     cs.in[c] = c < ncols ? in[c] : nullptr;
     cs.out[c] = c < ncols ? out[c] : nullptr;
@@ -365,9 +368,10 @@ void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, 
 }
 
 void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_bits, const uint8_t *const *in,
-                          uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream) {
+                          uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream,
+                          uint64_t key_xor) {
   const uint32_t nb = 1u << digit_bits;
-  rows_pass_launch(ImageDigit{keys, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws, stream);
+  rows_pass_launch(ImageDigit{keys, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws, stream, key_xor);
 }
 
 void radix_range_rows_pass(const int64_t *keys, int64_t n, uint64_t flip, uint64_t mn, int rshift, int shift,

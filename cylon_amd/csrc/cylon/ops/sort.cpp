@@ -126,6 +126,10 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
       widths.push_back(1);
     }
   }
+  // an 8-byte integer key comes back from its image by one XOR, applied by the last
+  // pass as it stores column 0 (no separate un-image read + write of the key)
+  const bool key_in_last_pass = key_from_image && kc.type.width() == 8 && diff != 0;
+  const uint64_t key_xor = (kc.type.kind() == ValueKind::SIGNED_INT ? (1ull << 63) : 0ull) ^ (asc ? 0ull : ~0ull);
   if (diff != 0) {
     const int lo = __builtin_ctzll(diff), hi = 64 - __builtin_clzll(diff);
     const int npass = (hi - lo + 9) / 10;
@@ -144,7 +148,8 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
         out.push_back(reinterpret_cast<uint8_t *>(nxt.back().data_ptr()));
       }
       hip::radix_sort_rows_pass(ptr<int64_t>(cur[0]), n, shift, db, in.data(), out.data(), widths.data(),
-                                (int)cur.size(), ptr<int64_t>(ws), ex.stream);
+                                (int)cur.size(), ptr<int64_t>(ws), ex.stream,
+                                ps + 1 == npass && key_in_last_pass ? key_xor : 0ull);
       cur = std::move(nxt);
       shift += db;
     }
@@ -154,7 +159,9 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
   for (int ci = 0; ci < t->Columns(); ++ci) {
     const Column &c = t->column(ci);
     at::Tensor d;
-    if (key_from_image && ci == col) {
+    if (key_in_last_pass && ci == col) {
+      d = cur[0].view(c.data.scalar_type());
+    } else if (key_from_image && ci == col) {
       at::Tensor im = cur[0];
       if (!asc) {
         const int nb = 8 * c.type.width();
