@@ -11,18 +11,31 @@ RCCL + local device hash join + materialisation of all 8 output columns).
 metric value = (|L| + |R|) / step time, whole job.
 
 Usage:
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--algorithm hash|sort]
-  N > 1 is launched by torch.distributed.run (one process per GPU).
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--algorithm hash|sort] [--verify]
+
+With --gpus N > 1 and no torchrun environment, bench.py starts
+`torch.distributed.run --nproc-per-node N` on itself as a child process (one
+rank per GPU, RCCL), the way the reference's run_dist_scaling.py:115-154 starts
+`mpirun -np w`; the parent never touches the GPU.  Under an outer torchrun,
+WORLD_SIZE must equal --gpus (a mismatch exits non-zero).
+
+After the timed region one extra traced step reports per-phase milliseconds
+(max over ranks; not part of the metric), and --verify checks the last timed
+step's output against an independent torch computation of the same join
+(key-count and payload-sum identities, see verify_join).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import torch
 
 REFERENCE_ROWS_PER_S = 4.0e8 / 2.3  # BASELINE.md: 2 x 200M rows in 2.3 s on 160 CPU cores (provisional row count)
+ROOT = os.path.dirname(os.path.abspath(__file__))
 
 
 def parse():
@@ -34,8 +47,54 @@ def parse():
     p.add_argument("--payload-cols", type=int, default=3)
     p.add_argument("--algorithm", default="hash", choices=["hash", "sort"])
     p.add_argument("--key-ratio", type=float, default=0.99)
-    p.add_argument("--profile-phases", action="store_true", help="print per-phase timings (extra syncs)")
+    p.add_argument("--no-phases", action="store_true", help="skip the traced per-phase step after the timed region")
+    p.add_argument("--verify", action="store_true", help="check the last output against torch (outside the timing)")
     return p.parse_args()
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(script: str, nproc: int, argv) -> int:
+    """Run `script argv` as nproc torchrun ranks in a child process and return its exit code.
+    Called before anything in this process initialises HIP (exec after a GPU touch is forbidden)."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), script, *argv]
+    return subprocess.call(cmd, env=env)
+
+
+def resolve_world(gpus: int, script: str, argv):
+    """(world, rank) for this process, or exits: spawns the ranks when --gpus > 1 is asked for
+    without a torchrun environment; refuses a WORLD_SIZE that disagrees with --gpus."""
+    if "WORLD_SIZE" not in os.environ:
+        if gpus > 1:
+            sys.exit(spawn_ranks(script, gpus, argv))
+        return 1, 0
+    world = int(os.environ["WORLD_SIZE"])
+    if world != gpus:
+        print(f"error: --gpus {gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    return world, int(os.environ.get("RANK", "0"))
+
+
+def make_context(world: int):
+    """CYLON_BENCH_BACKEND=gloo rehearses the multi-rank path on CPUs (tests only); gloo-gpu keeps
+    the tables in HBM (ranks may share one GPU) with gloo collectives; default = RCCL."""
+    from cylon_amd import CylonContext, GlooConfig, RCCLConfig
+    backend = os.environ.get("CYLON_BENCH_BACKEND", "")
+    if world > 1 and backend == "gloo-gpu":
+        ndev = max(torch.cuda.device_count(), 1)
+        return CylonContext(config=GlooConfig(device=f"cuda:{int(os.environ.get('LOCAL_RANK', '0')) % ndev}"),
+                            distributed=True)
+    if world > 1:
+        return CylonContext(config=GlooConfig() if backend == "gloo" else RCCLConfig(), distributed=True)
+    return CylonContext(config=None, distributed=False, device="cpu" if backend == "gloo" else "cuda:0")
 
 
 def make_relation(ctx, rows_local, key_range, ncols, seed, device):
@@ -53,27 +112,56 @@ def sync():
         torch.cuda.synchronize()
 
 
+def max_over_ranks(ctx, d: dict) -> dict:
+    """{name: value} -> {name: max over ranks} (names missing on a rank count as 0)."""
+    if ctx.get_world_size() == 1:
+        return d
+    import torch.distributed as dist
+    allv = [None] * ctx.get_world_size()
+    dist.all_gather_object(allv, d)
+    out = {}
+    for part in allv:
+        for k, v in part.items():
+            out[k] = max(out.get(k, 0.0), v)
+    return out
+
+
+def verify_join(ctx, left, right, out, key_range) -> dict:
+    """Independent check of an inner join output by per-key identities (torch bincount over the
+    global key range, all-reduced over ranks):
+      rows        = sum_k cL(k) cR(k)
+      sum l_k     = sum_k k cL(k) cR(k)      (and l_k == r_k row by row)
+      sum l_v0    = sum_k SL(k) cR(k)         SL = per-key sum of left v0
+      sum r_v0    = sum_k cL(k) SR(k)"""
+    lt, rt, ot = left.to_torch(), right.to_torch(), out.to_torch()
+    dev = lt["k"].device
+    cL = torch.bincount(lt["k"], minlength=key_range).to(torch.float64)
+    cR = torch.bincount(rt["k"], minlength=key_range).to(torch.float64)
+    SL = torch.bincount(lt["k"], weights=lt["v0"], minlength=key_range)
+    SR = torch.bincount(rt["k"], weights=rt["v0"], minlength=key_range)
+    for t in (cL, cR, SL, SR):
+        if ctx.get_world_size() > 1:
+            t.copy_(ctx.allreduce(t, "sum"))
+    keys = torch.arange(key_range, device=dev, dtype=torch.float64)
+    expect = torch.stack([(cL * cR).sum(), (keys * cL * cR).sum(), (SL * cR).sum(), (cL * SR).sum()])
+    del cL, cR, SL, SR, keys
+    mism = (ot["l_k"] != ot["r_k"]).sum().to(torch.float64)
+    got = torch.stack([torch.tensor(float(out.row_count), dtype=torch.float64, device=dev),
+                       ot["l_k"].to(torch.float64).sum(), ot["l_v0"].sum(), ot["r_v0"].sum(), mism])
+    if ctx.get_world_size() > 1:
+        got = ctx.allreduce(got, "sum")
+    e, g = expect.cpu().tolist(), got.cpu().tolist()
+    rel = [abs(a - b) / max(abs(a), 1.0) for a, b in zip(e, g[:4])]
+    ok = g[0] == e[0] and g[4] == 0 and rel[1] < 1e-12 and rel[2] < 1e-9 and rel[3] < 1e-9
+    return {"ok": bool(ok), "rows": int(g[0]), "expected_rows": int(e[0]), "key_mismatch_rows": int(g[4]),
+            "rel_err_sum_k": rel[1], "rel_err_sum_l_v0": rel[2], "rel_err_sum_r_v0": rel[3]}
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from cylon_amd import CylonContext, GlooConfig, RCCLConfig
-
-    # CYLON_BENCH_BACKEND=gloo rehearses the multi-rank path on CPUs (tests only);
-    # gloo-gpu keeps the tables in HBM (ranks may share one GPU) with gloo collectives
-    backend = os.environ.get("CYLON_BENCH_BACKEND", "")
-    cpu_rehearsal = backend == "gloo"
-    if world > 1 and backend == "gloo-gpu":
-        ndev = max(torch.cuda.device_count(), 1)
-        ctx = CylonContext(config=GlooConfig(device=f"cuda:{int(os.environ.get('LOCAL_RANK', '0')) % ndev}"),
-                           distributed=True)
-    elif world > 1:
-        ctx = CylonContext(config=GlooConfig() if cpu_rehearsal else RCCLConfig(), distributed=True)
-    else:
-        ctx = CylonContext(config=None, distributed=False, device="cpu" if cpu_rehearsal else "cuda:0")
+    world, rank = resolve_world(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    sys.path.insert(0, ROOT)
+    ctx = make_context(world)
     device = ctx.device
     n = world
     rows_local = args.rows // n
@@ -83,20 +171,22 @@ def main():
     sync()
 
     def step():
-        out = left.distributed_join(right, "inner", args.algorithm, on=[0], left_prefix="l_", right_prefix="r_")
-        return out.row_count
+        return left.distributed_join(right, "inner", args.algorithm, on=[0], left_prefix="l_", right_prefix="r_")
 
-    out_rows = 0
+    out = None
     for _ in range(args.warmup):
-        out_rows = step()
+        out = step()
+        out = None
     ctx.barrier()
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out_rows = step()
+        out = None  # the previous output is released before the next join allocates
+        out = step()
     sync()
     ctx.barrier()
     elapsed = time.perf_counter() - t0
+    out_rows = out.row_count if out is not None else 0
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
@@ -105,6 +195,28 @@ def main():
         rows_t = ctx.allreduce(rows_t, "sum")
         out_rows = int(rows_t.item())
     elapsed = float(t.item())
+
+    verify = None
+    if args.verify and out is not None:
+        verify = verify_join(ctx, left, right, out, key_range)
+    out = None
+
+    phases = None
+    if not args.no_phases:
+        from cylon_amd.utils import trace
+        trace.enable_tracing(True)
+        trace.reset_tracing()
+        ctx.barrier()
+        sync()
+        t1 = time.perf_counter()
+        step()
+        sync()
+        traced_ms = 1000.0 * (time.perf_counter() - t1)
+        ph = {k: v[0] for k, v in trace.phases().items()}
+        ph["step_total"] = traced_ms
+        trace.enable_tracing(False)
+        phases = {k: round(v, 3) for k, v in sorted(max_over_ranks(ctx, ph).items())}
+
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
     rows_in = 2 * rows_local * n
     value = rows_in / (ms_per_step / 1000.0)
@@ -126,14 +238,20 @@ def main():
                 "model": f"distributed inner join ({args.algorithm}), int64 key + {args.payload_cols} float64 cols",
                 "global_batch": args.rows,
                 "seq_len": 1 + args.payload_cols,
-                "parallelism": f"dp{n} (hash shuffle over RCCL)" if n > 1 else "dp1 (local join)",
+                "parallelism": f"dp{n} (hash shuffle over {'RCCL' if os.environ.get('CYLON_BENCH_BACKEND', '') == '' else os.environ['CYLON_BENCH_BACKEND']})" if n > 1 else "dp1 (local join)",
                 "rows_per_relation": args.rows,
                 "output_rows": out_rows,
                 "key_range": key_range,
             },
         }
+        if phases is not None:
+            rec["phases_ms_max_over_ranks"] = phases
+        if verify is not None:
+            rec["verify"] = verify
         print(json.dumps(rec), flush=True)
     ctx.finalize()
+    if verify is not None and not verify["ok"]:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -185,3 +185,29 @@ def test_bench_contract_multirank_cpu_rehearsal():
               "vs_baseline", "dtype", "data", "config"):
         assert k in rec
     assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["config"]["output_rows"] > 0
+
+
+def test_bench_self_launch_four_ranks_cpu():
+    """bench.py --gpus 4 with no torchrun environment starts 4 ranks itself (child torchrun) and
+    reports n_gpus == 4, per-phase timings and a passing --verify; a WORLD_SIZE that disagrees
+    with --gpus exits non-zero (reference launch: cpp/src/experiments/run_dist_scaling.py:115-154)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["CYLON_BENCH_BACKEND"] = "gloo"
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4", "--steps", "2",
+                          "--warmup", "1", "--rows", "80000", "--verify"],
+                         capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert out.returncode == 0 and len(lines) == 1, out.stderr[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 4 and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["verify"]["ok"] and rec["verify"]["rows"] == rec["config"]["output_rows"]
+    assert "shuffle.exchange" in rec["phases_ms_max_over_ranks"]
+    bad = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4", "--rows", "1000"],
+                         capture_output=True, text=True, timeout=120, cwd="/tmp",
+                         env=dict(env, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
+    assert bad.returncode == 2 and "WORLD_SIZE" in bad.stderr

@@ -5,8 +5,9 @@
   union   : distributed union of two join-shaped relations (reference headline #2)
 
 Strong scaling: --rows is the global row count, split over the ranks; data is
-generated in HBM on each rank.  Launch like bench.py:
-  python -m torch.distributed.run --nproc-per-node N tools/bench_dist.py --config groupby
+generated in HBM on each rank.  Launch like bench.py: `--gpus N` without a torchrun
+environment starts N ranks itself (bench.spawn_ranks, a child torchrun); under an
+outer torchrun WORLD_SIZE must equal --gpus.
 CYLON_BENCH_BACKEND=gloo-gpu runs the ranks over gloo (ranks may share one GPU:
 rehearsal of the device code paths, not a timing of xGMI).
 Prints one JSON line per config on rank 0 (max over ranks of the timed region).
@@ -21,31 +22,25 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from cylon_amd import CylonContext, GlooConfig, RCCLConfig, Table  # noqa: E402
+from bench import make_context, resolve_world  # noqa: E402  (imports no GPU code)
 
 DEFAULT_ROWS = {"groupby": 1_000_000_000, "sort": 2_000_000_000, "union": 1_000_000_000}
 
 
-def make_ctx():
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world == 1:
-        return CylonContext(config=None, distributed=False, device="cuda:0")
-    if os.environ.get("CYLON_BENCH_BACKEND", "") == "gloo-gpu":
-        ndev = max(torch.cuda.device_count(), 1)
-        return CylonContext(config=GlooConfig(device=f"cuda:{int(os.environ.get('LOCAL_RANK', '0')) % ndev}"),
-                            distributed=True)
-    return CylonContext(config=RCCLConfig(), distributed=True)
+def sync():
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
 
 
 def timed(ctx, fn, steps, warmup):
     for _ in range(warmup):
         fn()
     ctx.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         out = fn()
-    torch.cuda.synchronize()
+    sync()
     ctx.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=ctx.device)
     if ctx.get_world_size() > 1:
@@ -55,13 +50,16 @@ def timed(ctx, fn, steps, warmup):
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--config", default="groupby", choices=["groupby", "sort", "union"])
     ap.add_argument("--rows", type=int, default=0)
     ap.add_argument("--groups", type=int, default=10_000_000)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     a = ap.parse_args()
-    ctx = make_ctx()
+    world, _ = resolve_world(a.gpus, os.path.abspath(__file__), sys.argv[1:])
+    from cylon_amd import Table
+    ctx = make_context(world)
     rank, world = ctx.get_rank(), ctx.get_world_size()
     rows = a.rows or DEFAULT_ROWS[a.config]
     n = rows // world
