@@ -7,6 +7,8 @@
 // Internally every call forwards to the throwing operators in cylon::ops and
 // converts CylonError into a Status.
 #pragma once
+#include <chrono>
+#include <thread>
 #include <functional>
 #include <map>
 #include <memory>
@@ -210,9 +212,17 @@ class TaskAllToAll {
   }
   void finish() { inner_.finish(); }
   bool isComplete() { return inner_.isComplete(); }
-  void WaitForCompletion() {
+  // Bounded wait (the reference busy-spins forever, arrow_task_all_to_all.cpp): a peer
+  // that never delivers surfaces as ExecutionError after `timeout_s` seconds instead of
+  // hanging the rank; polling backs off to 50 us sleeps after the first sweeps.
+  void WaitForCompletion(double timeout_s = 600.0) {
     finish();
-    while (!isComplete()) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int64_t sweep = 0; !isComplete(); ++sweep) {
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      CYLON_CHECK(el < timeout_s, Code::ExecutionError,
+                  "task all-to-all incomplete after " << timeout_s << " s (" << sweep << " progress sweeps)");
+      if (sweep > 1024) std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
   }
 

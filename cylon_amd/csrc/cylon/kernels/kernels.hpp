@@ -69,6 +69,11 @@ enum AggOp : int {
   AGG_SUM = 0,
   AGG_MIN = 1,
   AGG_MAX = 2,
+  // COUNT = non-null values of the aggregated column, in the group-by and the scalar
+  // aggregate alike.  The reference's scalar Count is the same (Arrow COUNT_NON_NULL,
+  // compute/aggregates.cpp:55); its group-by CountKernel counts rows, nulls included
+  // (compute/aggregate_kernels.hpp:438-440).  Deliberate pandas choice; identical on
+  // non-null data (docs/semantics.md).
   AGG_COUNT = 3,
   AGG_MEAN = 4,
   AGG_VAR = 5,

@@ -333,6 +333,10 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
   CYLON_CHECK(in[0] == reinterpret_cast<const uint8_t *>(dg.keys) && widths[0] == 8, Code::Invalid,
               "radix pass: column 0 must be the key");
+  // key_xor rebuilds int64 keys from order images: only a sort's image digit may set it
+  // (partition / mod / range digits store column 0 as read)
+  CYLON_CHECK(key_xor == 0 || std::is_same<Digit, ImageDigit>::value, Code::Invalid,
+              "radix pass: key_xor is only valid for order-image digits");
   hipStream_t s = as_stream(stream);
   const uint32_t nb = 1u << digit_bits;
   const RPGeometry g = rp_geometry(n);

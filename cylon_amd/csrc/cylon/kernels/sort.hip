@@ -90,19 +90,32 @@ void sort_keys_from_column(const ColView &col, const int64_t *perm, int64_t n, b
   HIP_LAUNCH_CHECK();
 }
 
+
+// OR / AND accumulators of a key scan (varying bits = OR ^ AND): acc[0] = 0, acc[1] = ~0
+// are set on the stream (no host staging), the readback is the only synchronisation.
+static unsigned long long *or_and_init(int64_t *ws2, hipStream_t s) {
+  unsigned long long *acc = reinterpret_cast<unsigned long long *>(ws2);
+  HIP_CHECK(hipMemsetAsync(acc, 0, sizeof(unsigned long long), s));
+  HIP_CHECK(hipMemsetAsync(acc + 1, 0xff, sizeof(unsigned long long), s));
+  return acc;
+}
+
+static uint64_t or_and_diff(const unsigned long long *acc, hipStream_t s) {
+  unsigned long long oa[2];
+  HIP_CHECK(hipMemcpyAsync(oa, acc, sizeof(oa), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return oa[0] ^ oa[1];
+}
+
 uint64_t sort_keys_varying_bits(const ColView &col, int64_t n, bool desc, uint64_t *out, int64_t *ws2,
                                 void *stream) {
   if (n == 0) return 0;
   hipStream_t s = as_stream(stream);
-  unsigned long long *acc = reinterpret_cast<unsigned long long *>(ws2);
-  unsigned long long init[2] = {0ull, ~0ull};
-  HIP_CHECK(hipMemcpyAsync(acc, init, sizeof(init), hipMemcpyHostToDevice, s));
+  unsigned long long *acc = or_and_init(ws2, s);
   hipLaunchKernelGGL(k_sort_keys, dim3(grid_for(n)), dim3(kBlock), 0, s, col, nullptr, n, desc, out, acc);
   HIP_LAUNCH_CHECK();
-  unsigned long long oa[2];
-  HIP_CHECK(hipMemcpyAsync(oa, acc, sizeof(oa), hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-  return n <= 1 ? 0 : (oa[0] ^ oa[1]);
+  const uint64_t diff = or_and_diff(acc, s);
+  return n <= 1 ? 0 : diff;
 }
 
 // ---------------------------------------------------------------------------
@@ -149,30 +162,20 @@ int64_t radix_sort_workspace(int64_t n) { return stable_rank_workspace(n, 256) +
 uint64_t varying_bits(const uint64_t *keys, int64_t n, int64_t *ws2, void *stream) {
   if (n <= 1) return 0;
   hipStream_t s = as_stream(stream);
-  unsigned long long *acc = reinterpret_cast<unsigned long long *>(ws2);
-  unsigned long long init[2] = {0ull, ~0ull};
-  HIP_CHECK(hipMemcpyAsync(acc, init, sizeof(init), hipMemcpyHostToDevice, s));
+  unsigned long long *acc = or_and_init(ws2, s);
   hipLaunchKernelGGL(k_or_and, dim3(grid_for(n, kBlock, 1024)), dim3(kBlock), 0, s, keys, n, acc);
   HIP_LAUNCH_CHECK();
-  unsigned long long oa[2];
-  HIP_CHECK(hipMemcpyAsync(oa, acc, sizeof(oa), hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-  return oa[0] ^ oa[1];
+  return or_and_diff(acc, s);
 }
 
 int radix_sort_pairs(uint64_t *keys, int64_t *vals, int64_t n, uint64_t *keys_alt, int64_t *vals_alt, int begin_bit,
                      int end_bit, int64_t *ws, void *stream) {
   if (n <= 1) return 0;
   hipStream_t s = as_stream(stream);
-  unsigned long long *acc = reinterpret_cast<unsigned long long *>(ws);
-  unsigned long long init[2] = {0ull, ~0ull};
-  HIP_CHECK(hipMemcpyAsync(acc, init, sizeof(init), hipMemcpyHostToDevice, s));
+  unsigned long long *acc = or_and_init(ws, s);
   hipLaunchKernelGGL(k_or_and, dim3(grid_for(n, kBlock, 1024)), dim3(kBlock), 0, s, keys, n, acc);
   HIP_LAUNCH_CHECK();
-  unsigned long long oa[2];
-  HIP_CHECK(hipMemcpyAsync(oa, acc, sizeof(oa), hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-  const uint64_t diff = oa[0] ^ oa[1];
+  const uint64_t diff = or_and_diff(acc, s);
   int cur = 0;
   uint64_t *kb[2] = {keys, keys_alt};
   int64_t *vb[2] = {vals, vals_alt};

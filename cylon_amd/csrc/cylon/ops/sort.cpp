@@ -147,6 +147,8 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
         in.push_back(reinterpret_cast<const uint8_t *>(x.data_ptr()));
         out.push_back(reinterpret_cast<uint8_t *>(nxt.back().data_ptr()));
       }
+      // the XOR goes on the FINAL pass only: a pass reads column 0 as the order image it
+      // ranks by, so an un-imaged key column must never be the input of another pass
       hip::radix_sort_rows_pass(ptr<int64_t>(cur[0]), n, shift, db, in.data(), out.data(), widths.data(),
                                 (int)cur.size(), ptr<int64_t>(ws), ex.stream,
                                 ps + 1 == npass && key_in_last_pass ? key_xor : 0ull);

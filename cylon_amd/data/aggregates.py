@@ -1,5 +1,10 @@
 """Aggregation op enum and helpers (reference: python/pycylon/data/aggregates.pyx:17-40,
-cpp/src/cylon/compute/aggregate_kernels.hpp:40-50)."""
+cpp/src/cylon/compute/aggregate_kernels.hpp:40-50).
+
+COUNT counts the non-null values of the aggregated column (pandas ``count``), in
+``groupby`` and in the scalar ``Table.count`` alike.  The reference's scalar Count
+is the same (Arrow COUNT_NON_NULL); its group-by COUNT counts rows, nulls included.
+Results are identical on columns without nulls."""
 from .._lib import C
 
 AggregationOp = C.AggregationOp

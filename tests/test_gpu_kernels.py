@@ -190,13 +190,25 @@ def test_radix_groupby_matches_global(gpu_ctx, monkeypatch, case):
     pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-9, atol=1e-9)
 
 
-@pytest.mark.parametrize("dtype", ["int64", "float64", "int32", "uint16", "float32"])
+@pytest.mark.parametrize("dtype", ["int64", "float64", "int32", "uint16", "float32", "uint64", "int64_full",
+                                   "int64_equal"])
 @pytest.mark.parametrize("asc", [True, False])
 def test_radix_row_sort_matches_index_sort(gpu_ctx, monkeypatch, dtype, asc):
-    """Row-moving LSD sort (all columns through LDS-staged passes) vs index sort + gather; stable on ties."""
+    """Row-moving LSD sort (all columns through LDS-staged passes) vs index sort + gather; stable on ties.
+    uint64 keys >= 2^63 and full-range int64 keys (INT64_MIN / INT64_MAX present) take the last pass's
+    XOR-on-store path; all-equal keys take the zero-varying-bits branch."""
     rng = np.random.default_rng(9)
     n = 300_000
-    if dtype.startswith("float"):
+    if dtype == "uint64":
+        k = rng.integers(0, 1 << 63, n, dtype=np.uint64) | (rng.integers(0, 2, n, dtype=np.uint64) << np.uint64(63))
+        k[:5] = [0, (1 << 64) - 1, 1 << 63, (1 << 63) - 1, 1]
+    elif dtype == "int64_full":
+        k = rng.integers(np.iinfo(np.int64).min, np.iinfo(np.int64).max, n, dtype=np.int64)
+        k[:4] = [np.iinfo(np.int64).min, np.iinfo(np.int64).max, 0, -1]
+        k[4:2000] = k[2000:3996]  # ties
+    elif dtype == "int64_equal":
+        k = np.full(n, -77, dtype=np.int64)
+    elif dtype.startswith("float"):
         k = rng.standard_normal(n).astype(dtype)
         k[::101] = np.nan
         k[::103] = -0.0

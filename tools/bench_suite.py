@@ -43,6 +43,28 @@ def timed(fn, reps, warmup=1, sync=True):
     return statistics.median(ts), ts
 
 
+def verify_sorted(orig, k):
+    """Non-decreasing and the same multiset as the input (count, wrapping sum and sum of squares)."""
+    if orig.numel() != k.numel():
+        return False
+    mono = bool((k[1:] >= k[:-1]).all().item())
+    same = all(int(a.item()) == int(b.item()) for a, b in ((orig.sum(), k.sum()), ((orig * orig).sum(), (k * k).sum())))
+    return mono and same
+
+
+def verify_groupby(t, res, groups):
+    """Group sums against torch index_add over the group ids (outside the timed region)."""
+    c = t.to_torch()
+    g, x = c["g"], c["x"]
+    ref = torch.zeros(groups, dtype=torch.float64, device=g.device).index_add_(0, g, x)
+    present = torch.bincount(g, minlength=groups) > 0
+    cols = list(res.to_torch().values())
+    keys, sums = cols[0], cols[1]
+    if keys.numel() != int(present.sum().item()):
+        return False
+    return bool(torch.allclose(sums, ref[keys], rtol=1e-9, atol=1e-9).item())
+
+
 def emit(**kw):
     print(json.dumps(kw), flush=True)
 
@@ -99,11 +121,14 @@ def cfg4(reps, scale):
         out = {}
 
         def run():
-            out["groups"] = t.local_groupby("g", {"x": "sum"}).row_count
+            out["res"] = t.local_groupby("g", {"x": "sum"})
+            out["groups"] = out["res"].row_count
 
         med, ts = timed(run, reps)
+        ok = verify_groupby(t, out.pop("res"), groups)
         emit(config="4: hash groupby+sum, 10M int64 groups, one GPU", n=n, ms=med * 1e3, rows_per_s=n / med,
-             groups_out=out["groups"], all_ms=[x * 1e3 for x in ts])
+             groups_out=out["groups"], verified=ok, all_ms=[x * 1e3 for x in ts])
+        assert ok, "config 4 output differs from the torch index_add reference"
         del t
 
 
@@ -115,12 +140,13 @@ def cfg5(reps, scale):
         out = {}
 
         def run():
-            s = t.sort("k")
-            out["rows"] = s.row_count
+            out["sorted"] = t.sort("k")
 
         med, ts = timed(run, reps)
+        ok = verify_sorted(t.to_torch()["k"], out.pop("sorted").to_torch()["k"])
         emit(config="5: radix sort of int64 rows (table sort, one GPU)", n=n, ms=med * 1e3, rows_per_s=n / med,
-             all_ms=[x * 1e3 for x in ts])
+             verified=ok, all_ms=[x * 1e3 for x in ts])
+        assert ok, "config 5 output is not a sorted permutation of the input"
         del t
 
 
