@@ -17,7 +17,7 @@ from .data.table import SortOptions, Table
 from .frame import CylonEnv, DataFrame
 from .indexing.index import IndexingSchema
 from .io import CSVReadOptions, CSVWriteOptions, read_csv
-from .net import CommConfig, GlooConfig, MPIConfig, RCCLConfig
+from .net import CommConfig, GlooConfig, MPIConfig, RCCLConfig, TCPConfig
 from .series import Series
 
 Column = C.Column      # pycylon.data.column.Column
@@ -30,5 +30,5 @@ __version__ = "0.1.0"
 
 __all__ = ["C", "CylonError", "CylonContext", "Table", "DataFrame", "CylonEnv", "Series", "SortOptions",
            "JoinConfig", "JoinType", "JoinAlgorithm", "Status", "Code", "AggregationOp", "IndexingSchema",
-           "CommConfig", "GlooConfig", "MPIConfig", "RCCLConfig", "Column", "DataType", "read_csv",
+           "CommConfig", "GlooConfig", "MPIConfig", "RCCLConfig", "TCPConfig", "Column", "DataType", "read_csv",
            "CSVReadOptions", "CSVWriteOptions"]

@@ -6,6 +6,7 @@
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/utils/pybind.h>
 
+#include "cylon/net/async_delay_communicator.hpp"
 #include "cylon/ctx/cylon_context.hpp"
 #include "cylon/net/channel.hpp"
 #include "cylon/net/communicator.hpp"
@@ -64,6 +65,22 @@ join::config::JoinConfig make_jc(const std::string &type, const std::string &alg
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
+  // release the GIL inside every blocking transport wait (net::EnterBlocking)
+  net::SetBlockingHook([]() -> std::unique_ptr<net::BlockingRegion> {
+    struct GilRelease : net::BlockingRegion {
+      PyThreadState *st = nullptr;
+      GilRelease() {
+        // holds the GIL iff it has a current thread state (PyGILState_Check is not reliable
+        // after pybind11's gil_scoped_release)
+        if (Py_IsInitialized() && _PyThreadState_UncheckedGet() != nullptr) st = PyEval_SaveThread();
+      }
+      ~GilRelease() override {
+        if (st) PyEval_RestoreThread(st);
+      }
+    };
+    return std::make_unique<GilRelease>();
+  });
+
   m.doc() = "cylon_amd native engine: MI355X HIP kernels + RCCL shuffle";
 
   static py::exception<CylonError> exc(m, "CylonError", PyExc_RuntimeError);
@@ -90,20 +107,20 @@ PYBIND11_MODULE(_C, m) {
   py::enum_<Layout>(m, "Layout").value("FIXED_WIDTH", Layout::FIXED_WIDTH).value("VARIABLE_WIDTH", Layout::VARIABLE_WIDTH);
 
   py::class_<DataType>(m, "DataType")
-      .def(py::init<>())
-      .def(py::init<Type>())
-      .def(py::init<Type, int32_t>())
+      .def(py::init<>(), py::call_guard<py::gil_scoped_release>())
+      .def(py::init<Type>(), py::call_guard<py::gil_scoped_release>())
+      .def(py::init<Type, int32_t>(), py::call_guard<py::gil_scoped_release>())
       .def_readwrite("type", &DataType::type)
       .def_readwrite("byte_width", &DataType::byte_width)
       .def_property("unit", [](const DataType &d) { return static_cast<int>(d.unit); },
                     [](DataType &d, int u) { d.unit = static_cast<TimeUnit>(u); })
       .def_readwrite("timezone", &DataType::timezone)
-      .def("width", &DataType::width)
-      .def("layout", &DataType::layout)
-      .def("is_numeric", &DataType::is_numeric)
-      .def("__eq__", [](const DataType &a, const DataType &b) { return a == b; })
-      .def("__repr__", &DataType::ToString)
-      .def("__str__", &DataType::ToString);
+      .def("width", &DataType::width, py::call_guard<py::gil_scoped_release>())
+      .def("layout", &DataType::layout, py::call_guard<py::gil_scoped_release>())
+      .def("is_numeric", &DataType::is_numeric, py::call_guard<py::gil_scoped_release>())
+      .def("__eq__", [](const DataType &a, const DataType &b) { return a == b; }, py::call_guard<py::gil_scoped_release>())
+      .def("__repr__", &DataType::ToString, py::call_guard<py::gil_scoped_release>())
+      .def("__str__", &DataType::ToString, py::call_guard<py::gil_scoped_release>());
 
   py::class_<Column>(m, "Column")
       .def(py::init([](const std::string &name, const DataType &t, int64_t length, at::Tensor data,
@@ -122,11 +139,11 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("validity", [](const Column &c) -> py::object {
         return c.validity.defined() ? py::cast(c.validity) : py::none();
       })
-      .def("null_count", &Column::null_count)
-      .def("nbytes", &Column::nbytes)
-      .def("to", [](const Column &c, const std::string &d) { return c.to(parse_device(d)); })
-      .def("slice", &Column::slice)
-      .def("with_name", &Column::with_name);
+      .def("null_count", &Column::null_count, py::call_guard<py::gil_scoped_release>())
+      .def("nbytes", &Column::nbytes, py::call_guard<py::gil_scoped_release>())
+      .def("to", [](const Column &c, const std::string &d) { return c.to(parse_device(d)); }, py::call_guard<py::gil_scoped_release>())
+      .def("slice", &Column::slice, py::call_guard<py::gil_scoped_release>())
+      .def("with_name", &Column::with_name, py::call_guard<py::gil_scoped_release>());
 
   py::enum_<net::CommType>(m, "CommType")
       .value("LOCAL", net::CommType::LOCAL).value("MPI", net::CommType::MPI).value("TCP", net::CommType::TCP)
@@ -153,7 +170,7 @@ PYBIND11_MODULE(_C, m) {
   });
 
   py::class_<net::TxRequest, std::shared_ptr<net::TxRequest>>(m, "TxRequest")
-      .def(py::init<>())
+      .def(py::init<>(), py::call_guard<py::gil_scoped_release>())
       .def(py::init([](int target, py::object buffer, std::vector<int32_t> header) {
              at::Tensor b = buffer.is_none() ? at::Tensor() : buffer.cast<at::Tensor>();
              return std::make_shared<net::TxRequest>(target, b, header);
@@ -166,26 +183,26 @@ PYBIND11_MODULE(_C, m) {
             return r.buffer.defined() ? py::cast(r.buffer) : py::none();
           },
           [](net::TxRequest &r, at::Tensor b) { r.buffer = b; });
-  py::class_<net::ChannelReceiveCallback, PyRecvCb>(m, "ChannelReceiveCallback").def(py::init<>());
-  py::class_<net::ChannelSendCallback, PySendCb>(m, "ChannelSendCallback").def(py::init<>());
+  py::class_<net::ChannelReceiveCallback, PyRecvCb>(m, "ChannelReceiveCallback").def(py::init<>(), py::call_guard<py::gil_scoped_release>());
+  py::class_<net::ChannelSendCallback, PySendCb>(m, "ChannelSendCallback").def(py::init<>(), py::call_guard<py::gil_scoped_release>());
   py::class_<net::Channel, std::shared_ptr<net::Channel>>(m, "Channel")
       .def(py::init([](const std::shared_ptr<CylonContext> &ctx) {
         return std::make_shared<net::Channel>(ctx->GetCommunicator(), ctx->GetDevice());
-      }))
+      }), py::call_guard<py::gil_scoped_release>())
       .def("init", &net::Channel::init, py::arg("edge"), py::arg("receives"), py::arg("send_ids"),
-           py::arg("receive_callback"), py::arg("send_callback"), py::keep_alive<1, 5>(), py::keep_alive<1, 6>())
-      .def("send", &net::Channel::send)
-      .def("send_fin", &net::Channel::sendFin)
-      .def("progress_sends", &net::Channel::progressSends)
-      .def("progress_receives", &net::Channel::progressReceives)
-      .def("is_complete", &net::Channel::isComplete)
-      .def("close", &net::Channel::close);
+           py::arg("receive_callback"), py::arg("send_callback"), py::keep_alive<1, 5>(), py::keep_alive<1, 6>(), py::call_guard<py::gil_scoped_release>())
+      .def("send", &net::Channel::send, py::call_guard<py::gil_scoped_release>())
+      .def("send_fin", &net::Channel::sendFin, py::call_guard<py::gil_scoped_release>())
+      .def("progress_sends", &net::Channel::progressSends, py::call_guard<py::gil_scoped_release>())
+      .def("progress_receives", &net::Channel::progressReceives, py::call_guard<py::gil_scoped_release>())
+      .def("is_complete", &net::Channel::isComplete, py::call_guard<py::gil_scoped_release>())
+      .def("close", &net::Channel::close, py::call_guard<py::gil_scoped_release>());
 
   py::class_<MemoryPool, std::shared_ptr<MemoryPool>>(m, "MemoryPool")
-      .def("bytes_allocated", &MemoryPool::bytes_allocated)
-      .def("max_memory", &MemoryPool::max_memory)
-      .def("backend_name", &MemoryPool::backend_name)
-      .def("device", [](const MemoryPool &p) { return p.device().str(); })
+      .def("bytes_allocated", &MemoryPool::bytes_allocated, py::call_guard<py::gil_scoped_release>())
+      .def("max_memory", &MemoryPool::max_memory, py::call_guard<py::gil_scoped_release>())
+      .def("backend_name", &MemoryPool::backend_name, py::call_guard<py::gil_scoped_release>())
+      .def("device", [](const MemoryPool &p) { return p.device().str(); }, py::call_guard<py::gil_scoped_release>())
       .def(
           "empty",
           [](const std::shared_ptr<MemoryPool> &p, std::vector<int64_t> shape, const std::string &dtype) {
@@ -197,17 +214,17 @@ PYBIND11_MODULE(_C, m) {
             CYLON_CHECK(it != m.end(), Code::Invalid, "unsupported dtype " << dtype);
             return EmptyFromPool(p, shape, it->second);
           },
-          py::arg("shape"), py::arg("dtype"), "tensor whose storage is allocated from this pool");
-  m.def("host_memory_pool", []() { return std::shared_ptr<MemoryPool>(std::make_shared<HostMemoryPool>()); });
+          py::arg("shape"), py::arg("dtype"), "tensor whose storage is allocated from this pool", py::call_guard<py::gil_scoped_release>());
+  m.def("host_memory_pool", []() { return std::shared_ptr<MemoryPool>(std::make_shared<HostMemoryPool>()); }, py::call_guard<py::gil_scoped_release>());
   m.def("device_memory_pool", [](const std::string &dev) {
     return std::shared_ptr<MemoryPool>(std::make_shared<DeviceMemoryPool>(parse_device(dev)));
-  });
+  }, py::call_guard<py::gil_scoped_release>());
 
   py::class_<CylonContext, std::shared_ptr<CylonContext>>(m, "Context")
-      .def("memory_pool", &CylonContext::GetMemoryPool)
-      .def("set_memory_pool", &CylonContext::SetMemoryPool)
+      .def("memory_pool", &CylonContext::GetMemoryPool, py::call_guard<py::gil_scoped_release>())
+      .def("set_memory_pool", &CylonContext::SetMemoryPool, py::call_guard<py::gil_scoped_release>())
       .def_static("init_local", [](const std::string &dev) { return CylonContext::Init(parse_device(dev)); },
-                  py::arg("device") = "cpu")
+                  py::arg("device") = "cpu", py::call_guard<py::gil_scoped_release>())
       .def_static("init_distributed",
                   [](c10::intrusive_ptr<c10d::ProcessGroup> pg, const std::string &backend, const std::string &dev) {
                     const auto ct = backend == "nccl" || backend == "rccl" ? net::CommType::RCCL : net::CommType::GLOO;
@@ -215,58 +232,82 @@ PYBIND11_MODULE(_C, m) {
                     const at::Device comm_device = ct == net::CommType::RCCL ? device : at::Device(at::kCPU);
                     auto comm = std::make_shared<net::ProcessGroupCommunicator>(pg, ct, comm_device);
                     return CylonContext::InitDistributed(comm, device);
-                  })
-      .def("get_rank", &CylonContext::GetRank)
-      .def("get_world_size", &CylonContext::GetWorldSize)
-      .def("get_neighbours", &CylonContext::GetNeighbours)
-      .def("get_next_sequence", &CylonContext::GetNextSequence)
-      .def("is_distributed", &CylonContext::IsDistributed)
-      .def("get_comm_type", &CylonContext::GetCommType)
+                  }, py::call_guard<py::gil_scoped_release>())
+      .def_static("init_native",
+                  [](const std::string &comm, int rank, int world, const std::string &dev, double timeout_s) {
+                    net::CommConfig cfg;
+                    cfg.type = comm == "tcp" || comm == "gloo" ? net::CommType::TCP
+                               : comm == "mpi"                 ? net::CommType::MPI
+                                                               : net::CommType::RCCL;
+                    cfg.rank = rank;
+                    cfg.world_size = world;
+                    cfg.device = dev;
+                    cfg.timeout_s = timeout_s;
+                    return CylonContext::InitDistributed(cfg);
+                  },
+                  py::arg("comm"), py::arg("rank") = -1, py::arg("world_size") = -1, py::arg("device") = "",
+                  py::arg("timeout_s") = 1800.0, py::call_guard<py::gil_scoped_release>())
+      .def("get_rank", &CylonContext::GetRank, py::call_guard<py::gil_scoped_release>())
+      .def("get_world_size", &CylonContext::GetWorldSize, py::call_guard<py::gil_scoped_release>())
+      .def("get_neighbours", &CylonContext::GetNeighbours, py::call_guard<py::gil_scoped_release>())
+      .def("get_next_sequence", &CylonContext::GetNextSequence, py::call_guard<py::gil_scoped_release>())
+      .def("is_distributed", &CylonContext::IsDistributed, py::call_guard<py::gil_scoped_release>())
+      .def("get_comm_type", &CylonContext::GetCommType, py::call_guard<py::gil_scoped_release>())
       .def("barrier", &CylonContext::Barrier, py::call_guard<py::gil_scoped_release>())
-      .def("finalize", &CylonContext::Finalize)
-      .def("add_config", &CylonContext::AddConfig)
-      .def("get_config", &CylonContext::GetConfig, py::arg("key"), py::arg("default") = "")
-      .def("get_configs", &CylonContext::GetConfigs)
-      .def("device", [](const CylonContext &c) { return c.GetDevice().str(); })
+      .def("finalize", &CylonContext::Finalize, py::call_guard<py::gil_scoped_release>())
+      .def("add_config", &CylonContext::AddConfig, py::call_guard<py::gil_scoped_release>())
+      .def("get_config", &CylonContext::GetConfig, py::arg("key"), py::arg("default") = "", py::call_guard<py::gil_scoped_release>())
+      .def("get_configs", &CylonContext::GetConfigs, py::call_guard<py::gil_scoped_release>())
+      .def("device", [](const CylonContext &c) { return c.GetDevice().str(); }, py::call_guard<py::gil_scoped_release>())
       .def("inject_faults",
            [](CylonContext &c, int64_t fail_at_call) {
              c.setCommunicator(std::make_shared<net::FaultInjectionCommunicator>(c.GetCommunicator(), fail_at_call));
-           })
-      .def("bytes_allocated", &CylonContext::BytesAllocated)
-      .def("max_memory", &CylonContext::MaxMemory)
+           }, py::call_guard<py::gil_scoped_release>())
+      .def("use_async_delay_transport",
+           [](CylonContext &c, double delay_us) {
+             c.setCommunicator(std::make_shared<net::AsyncDelayCommunicator>(c.GetCommunicator(), delay_us));
+           }, py::call_guard<py::gil_scoped_release>())
+      .def("async_transport_stats",
+           [](CylonContext &c) {
+             auto a = std::dynamic_pointer_cast<net::AsyncDelayCommunicator>(c.GetCommunicator());
+             CYLON_CHECK(a != nullptr, Code::Invalid, "context does not use the async delay transport");
+             return std::make_pair(a->posted(), a->observed_in_flight());
+           }, py::call_guard<py::gil_scoped_release>())
+      .def("bytes_allocated", &CylonContext::BytesAllocated, py::call_guard<py::gil_scoped_release>())
+      .def("max_memory", &CylonContext::MaxMemory, py::call_guard<py::gil_scoped_release>())
       .def("allreduce", [](CylonContext &c, at::Tensor t, int op) {
         c.GetCommunicator()->AllReduce(t, static_cast<net::ReduceOp>(op));
         return t;
-      })
-      .def("allgather", [](CylonContext &c, at::Tensor t) { return c.GetCommunicator()->AllGather(t); })
-      .def("allgatherv", [](CylonContext &c, at::Tensor t) { return c.GetCommunicator()->AllGatherV(t); })
+      }, py::call_guard<py::gil_scoped_release>())
+      .def("allgather", [](CylonContext &c, at::Tensor t) { return c.GetCommunicator()->AllGather(t); }, py::call_guard<py::gil_scoped_release>())
+      .def("allgatherv", [](CylonContext &c, at::Tensor t) { return c.GetCommunicator()->AllGatherV(t); }, py::call_guard<py::gil_scoped_release>())
       .def("broadcast", [](CylonContext &c, at::Tensor t, int root) {
         c.GetCommunicator()->Broadcast(t, root);
         return t;
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("alltoallv", [](CylonContext &c, at::Tensor t, std::vector<int64_t> sc) {
         auto comm = c.GetCommunicator();
         auto rc = comm->ExchangeCounts(sc);
         return comm->AllToAllV(t, sc, rc);
-      });
+      }, py::call_guard<py::gil_scoped_release>());
 
   py::class_<Table, std::shared_ptr<Table>>(m, "Table")
       .def(py::init([](std::shared_ptr<CylonContext> ctx, std::vector<Column> cols) {
         return std::make_shared<Table>(std::move(ctx), std::move(cols));
-      }))
-      .def("rows", &Table::Rows)
-      .def("num_columns", &Table::Columns)
-      .def("column_names", &Table::ColumnNames)
-      .def("column", &Table::column)
-      .def("columns", &Table::columns)
-      .def("column_index", &Table::ColumnIndex)
-      .def("context", &Table::GetContext)
-      .def("device", [](const Table &t) { return t.device().str(); })
-      .def("retain_memory", &Table::retainMemory)
-      .def("is_retain", &Table::IsRetain)
-      .def("clear", &Table::Clear)
-      .def("nbytes", &Table::nbytes)
-      .def("to", [](const Table &t, const std::string &d) { return t.to(parse_device(d)); });
+      }), py::call_guard<py::gil_scoped_release>())
+      .def("rows", &Table::Rows, py::call_guard<py::gil_scoped_release>())
+      .def("num_columns", &Table::Columns, py::call_guard<py::gil_scoped_release>())
+      .def("column_names", &Table::ColumnNames, py::call_guard<py::gil_scoped_release>())
+      .def("column", &Table::column, py::call_guard<py::gil_scoped_release>())
+      .def("columns", &Table::columns, py::call_guard<py::gil_scoped_release>())
+      .def("column_index", &Table::ColumnIndex, py::call_guard<py::gil_scoped_release>())
+      .def("context", &Table::GetContext, py::call_guard<py::gil_scoped_release>())
+      .def("device", [](const Table &t) { return t.device().str(); }, py::call_guard<py::gil_scoped_release>())
+      .def("retain_memory", &Table::retainMemory, py::call_guard<py::gil_scoped_release>())
+      .def("is_retain", &Table::IsRetain, py::call_guard<py::gil_scoped_release>())
+      .def("clear", &Table::Clear, py::call_guard<py::gil_scoped_release>())
+      .def("nbytes", &Table::nbytes, py::call_guard<py::gil_scoped_release>())
+      .def("to", [](const Table &t, const std::string &d) { return t.to(parse_device(d)); }, py::call_guard<py::gil_scoped_release>());
 
   // ---- operators (GIL released: kernels + collectives) -----------------------
   auto rel = py::call_guard<py::gil_scoped_release>();
@@ -306,16 +347,16 @@ PYBIND11_MODULE(_C, m) {
       rel);
 
   // ---- tracing / metrics -----------------------------------------------------
-  m.def("trace_enable", &trace::set_enabled);
-  m.def("trace_enabled", &trace::enabled);
+  m.def("trace_enable", &trace::set_enabled, py::call_guard<py::gil_scoped_release>());
+  m.def("trace_enabled", &trace::enabled, py::call_guard<py::gil_scoped_release>());
   m.def("trace_phases", [] {
     std::map<std::string, std::pair<double, int64_t>> out;
     for (auto &kv : trace::phases()) out[kv.first] = {kv.second.total_ms, kv.second.calls};
     return out;
-  });
-  m.def("trace_counters", &trace::counters);
-  m.def("trace_reset", &trace::reset);
-  m.def("log", &trace::log);
+  }, py::call_guard<py::gil_scoped_release>());
+  m.def("trace_counters", &trace::counters, py::call_guard<py::gil_scoped_release>());
+  m.def("trace_reset", &trace::reset, py::call_guard<py::gil_scoped_release>());
+  m.def("log", &trace::log, py::call_guard<py::gil_scoped_release>());
 
   register_extended_ops(m);
 }

@@ -132,20 +132,19 @@ void register_extended_ops(py::module &m) {
 
   m.def("group_ids", [](const TablePtr &t, const std::vector<int> &cols, bool presorted) {
     auto g = ops::GroupIds(t, cols, presorted);
-    return py::make_tuple(g.gid, g.ngroups, g.first_rows);
-  });
+    return std::make_tuple(g.gid, g.ngroups, g.first_rows);
+  }, py::call_guard<py::gil_scoped_release>());
 
   auto groupby_fn = [](TablePtr (*fn)(const TablePtr &, const std::vector<int> &, const std::vector<ops::AggSpec> &)) {
     return [fn](const TablePtr &t, const std::vector<int> &keys, const std::vector<int> &cols,
                 const std::vector<int> &op_ids, const std::vector<double> &qs, const std::vector<int> &ddofs) {
-      py::gil_scoped_release nogil;
       return fn(t, keys, make_specs(cols, op_ids, qs, ddofs));
     };
   };
-  m.def("hash_groupby", groupby_fn(&ops::HashGroupBy));
-  m.def("pipeline_groupby", groupby_fn(&ops::PipelineGroupBy));
-  m.def("distributed_hash_groupby", groupby_fn(&ops::DistributedHashGroupBy));
-  m.def("distributed_pipeline_groupby", groupby_fn(&ops::DistributedPipelineGroupBy));
+  m.def("hash_groupby", groupby_fn(&ops::HashGroupBy), py::call_guard<py::gil_scoped_release>());
+  m.def("pipeline_groupby", groupby_fn(&ops::PipelineGroupBy), py::call_guard<py::gil_scoped_release>());
+  m.def("distributed_hash_groupby", groupby_fn(&ops::DistributedHashGroupBy), py::call_guard<py::gil_scoped_release>());
+  m.def("distributed_pipeline_groupby", groupby_fn(&ops::DistributedPipelineGroupBy), py::call_guard<py::gil_scoped_release>());
 
   m.def("aggregate", &ops::Aggregate, py::arg("table"), py::arg("col"), py::arg("op"), py::arg("quantile") = 0.5,
         py::arg("ddof") = 1, py::arg("distributed") = true, rel);
@@ -190,12 +189,12 @@ void register_extended_ops(py::module &m) {
       rel);
 
   // ---- string-ID registry (reference table_api.hpp) ----------------------------
-  m.def("registry_put", &PutTable);
-  m.def("registry_get", &GetTable);
-  m.def("registry_remove", &RemoveTable);
-  m.def("registry_list", &ListTables);
-  m.def("registry_row_count", &RowCount);
-  m.def("registry_column_count", &ColumnCount);
+  m.def("registry_put", &PutTable, py::call_guard<py::gil_scoped_release>());
+  m.def("registry_get", &GetTable, py::call_guard<py::gil_scoped_release>());
+  m.def("registry_remove", &RemoveTable, py::call_guard<py::gil_scoped_release>());
+  m.def("registry_list", &ListTables, py::call_guard<py::gil_scoped_release>());
+  m.def("registry_row_count", &RowCount, py::call_guard<py::gil_scoped_release>());
+  m.def("registry_column_count", &ColumnCount, py::call_guard<py::gil_scoped_release>());
   m.def(
       "registry_join",
       [](const std::string &l, const std::string &r, const std::string &type, const std::string &algo,
@@ -229,13 +228,13 @@ void register_extended_ops(py::module &m) {
           return true;
         });
         return h;
-      }))
+      }), py::call_guard<py::gil_scoped_release>())
       .def("insert", [](A2AHandle &h, const TablePtr &t, int target, int ref) { return h.impl->insert(t, target, ref); },
-           py::arg("table"), py::arg("target"), py::arg("reference") = 0)
-      .def("finish", [](A2AHandle &h) { h.impl->finish(); })
+           py::arg("table"), py::arg("target"), py::arg("reference") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("finish", [](A2AHandle &h) { h.impl->finish(); }, py::call_guard<py::gil_scoped_release>())
       .def("is_complete", [](A2AHandle &h) { return h.impl->isComplete(); }, rel)
-      .def("close", [](A2AHandle &h) { h.impl->close(); })
-      .def("received", [](A2AHandle &h) { return h.received; });
+      .def("close", [](A2AHandle &h) { h.impl->close(); }, py::call_guard<py::gil_scoped_release>())
+      .def("received", [](A2AHandle &h) { return h.received; }, py::call_guard<py::gil_scoped_release>());
 
   m.def("map_to_sort_partitions", &ops::MapToSortPartitions, rel);
   m.def("partition_reorder", &ops::PartitionReorder, rel);

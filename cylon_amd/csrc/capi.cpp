@@ -65,6 +65,21 @@ CYLON_CAPI int cylon_init(const char *device) {
   });
 }
 
+CYLON_CAPI int cylon_init_distributed(const char *comm_type) {
+  return guard([&] {
+    const std::string t = comm_type ? comm_type : "rccl";
+    net::CommType ct = net::CommType::RCCL;
+    if (t == "tcp" || t == "gloo") ct = net::CommType::TCP;
+    else if (t == "mpi") ct = net::CommType::MPI;
+    else CYLON_CHECK(t == "rccl" || t == "nccl", Code::Invalid, "unknown comm type '" << t << "'");
+    std::lock_guard<std::mutex> lk(g_mu);
+    net::CommConfig cfg;
+    cfg.type = ct;
+    g_ctx = CylonContext::InitDistributed(cfg);
+    return 0;
+  });
+}
+
 CYLON_CAPI int cylon_get_rank(void) { return ctx()->GetRank(); }
 CYLON_CAPI int cylon_get_world_size(void) { return ctx()->GetWorldSize(); }
 CYLON_CAPI int cylon_barrier(void) {

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../net/communicator.hpp"
+#include "../net/tcp_communicator.hpp"
 #include "memory_pool.hpp"
 
 namespace cylon {
@@ -26,6 +27,10 @@ class CylonContext {
   // Local (rank 0 of 1) context on `device` (default: cpu).
   static std::shared_ptr<CylonContext> Init(at::Device device = at::Device(at::kCPU));
   static std::shared_ptr<CylonContext> InitDistributed(std::shared_ptr<net::Communicator> comm, at::Device device);
+  // Native bootstrap (no Python): TCPStore rendezvous from the torchrun environment, then
+  // RCCL (ProcessGroupNCCL, device cuda:<LOCAL_RANK>) or the TCP mesh (host tables).
+  // Reference: ctx/cylon_context.cpp:32-43 InitDistributed(MPIConfig).
+  static std::shared_ptr<CylonContext> InitDistributed(const net::CommConfig &cfg);
 
   void Finalize();
   void AddConfig(const std::string &key, const std::string &value);

@@ -335,7 +335,7 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
               "radix pass: column 0 must be the key");
   // key_xor rebuilds int64 keys from order images: only a sort's image digit may set it
   // (partition / mod / range digits store column 0 as read)
-  CYLON_CHECK(key_xor == 0 || std::is_same<Digit, ImageDigit>::value, Code::Invalid,
+  CYLON_CHECK((key_xor == 0 || std::is_same<Digit, ImageDigit>::value), Code::Invalid,
               "radix pass: key_xor is only valid for order-image digits");
   hipStream_t s = as_stream(stream);
   const uint32_t nb = 1u << digit_bits;

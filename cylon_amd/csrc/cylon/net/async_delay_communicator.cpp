@@ -1,0 +1,95 @@
+// Asynchronous loopback test transport (see async_delay_communicator.hpp).
+#include "async_delay_communicator.hpp"
+
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+
+#include "../kernels/kernels.hpp"
+
+namespace cylon {
+namespace net {
+
+#define ADC_HIP(expr)                                                                               \
+  do {                                                                                              \
+    hipError_t _e = (expr);                                                                         \
+    CYLON_CHECK(_e == hipSuccess, Code::ExecutionError, #expr << ": " << hipGetErrorString(_e));    \
+  } while (0)
+
+namespace {
+class DoneReq : public P2PRequest {
+ public:
+  bool Test() override { return true; }
+  void Wait() override {}
+};
+
+class EventRequest : public P2PRequest {
+ public:
+  EventRequest(hipEvent_t ev, at::Tensor staged, at::Tensor out, int dev, std::shared_ptr<int64_t> seen)
+      : ev_(ev), staged_(std::move(staged)), out_(std::move(out)), dev_(dev), seen_(std::move(seen)) {}
+  ~EventRequest() override {
+    // never let the staging / receive buffers return to the allocator under a live copy
+    if (!waited_) (void)hipEventSynchronize(ev_);
+    (void)hipEventDestroy(ev_);
+  }
+  bool Test() override {
+    const hipError_t q = hipEventQuery(ev_);
+    CYLON_CHECK(q == hipSuccess || q == hipErrorNotReady, Code::ExecutionError, "event query: " << hipGetErrorString(q));
+    if (!polled_) {
+      polled_ = true;
+      if (q == hipErrorNotReady) ++*seen_;
+    }
+    return q == hipSuccess;
+  }
+  void Wait() override {
+    if (waited_) return;
+    if (!polled_) Test();
+    hipStream_t cur = c10::hip::getCurrentHIPStream(dev_).stream();
+    ADC_HIP(hipStreamWaitEvent(cur, ev_, 0));  // stream-ordered, the host does not block
+    waited_ = true;
+  }
+
+ private:
+  hipEvent_t ev_;
+  at::Tensor staged_, out_;
+  int dev_;
+  std::shared_ptr<int64_t> seen_;
+  bool waited_ = false, polled_ = false;
+};
+}  // namespace
+
+AsyncDelayCommunicator::~AsyncDelayCommunicator() {
+  if (side_) (void)hipStreamDestroy(reinterpret_cast<hipStream_t>(side_));
+}
+
+std::pair<at::Tensor, std::shared_ptr<P2PRequest>> AsyncDelayCommunicator::AllToAllVAsync(
+    const at::Tensor &s, const std::vector<int64_t> &sc, const std::vector<int64_t> &rc) {
+  at::Tensor staged = inner_->AllToAllV(s, sc, rc);
+  if (!staged.is_cuda()) return {staged, std::make_shared<DoneReq>()};  // host tables: nothing to overlap
+  const int dev = staged.device().index();
+  if (!side_ || side_dev_ != dev) {
+    hipStream_t st;
+    ADC_HIP(hipSetDevice(dev));
+    ADC_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    side_ = st;
+    side_dev_ = dev;
+  }
+  hipStream_t side = reinterpret_cast<hipStream_t>(side_);
+  hipStream_t cur = c10::hip::getCurrentHIPStream(dev).stream();
+  at::Tensor out = at::empty_like(staged);
+  const size_t nb = (size_t)staged.numel() * staged.element_size();
+  if (nb) ADC_HIP(hipMemsetAsync(out.data_ptr(), 0xff, nb, cur));  // poison
+  hipEvent_t ready, done;
+  ADC_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+  ADC_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+  ADC_HIP(hipEventRecord(ready, cur));
+  ADC_HIP(hipStreamWaitEvent(side, ready, 0));
+  (void)hipEventDestroy(ready);
+  hip::spin_delay_us(delay_us_, side);
+  if (nb) ADC_HIP(hipMemcpyAsync(out.data_ptr(), staged.data_ptr(), nb, hipMemcpyDeviceToDevice, side));
+  ADC_HIP(hipEventRecord(done, side));
+  ++posted_;
+  return {out, std::make_shared<EventRequest>(done, staged, out, dev, in_flight_seen_)};
+}
+
+}  // namespace net
+}  // namespace cylon

@@ -13,6 +13,21 @@
 namespace cylon {
 namespace net {
 
+static std::atomic<BlockingHook> g_blocking_hook{nullptr};
+
+void SetBlockingHook(BlockingHook hook) { g_blocking_hook.store(hook); }
+
+std::unique_ptr<BlockingRegion> EnterBlocking() {
+  BlockingHook h = g_blocking_hook.load();
+  return h ? h() : nullptr;
+}
+
+// wait on a c10d work inside a blocking region
+static void wait_work(const c10::intrusive_ptr<c10d::Work> &w) {
+  auto region = EnterBlocking();
+  w->wait();
+}
+
 const char *CommTypeName(CommType t) {
   switch (t) {
     case CommType::LOCAL: return "local";
@@ -73,7 +88,7 @@ void ProcessGroupCommunicator::Barrier() {
   // identically for RCCL and gloo and orders with the current stream.
   at::Tensor t = at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(device_));
   std::vector<at::Tensor> v{t};
-  pg().allreduce(v)->wait();
+  wait_work(pg().allreduce(v));
   if (device_.is_cuda()) t.cpu();
 }
 
@@ -89,7 +104,7 @@ at::Tensor ProcessGroupCommunicator::AllToAllV(const at::Tensor &send, const std
   shape[0] = total;
   at::Tensor out = at::empty(shape, in.options());
   std::vector<int64_t> sc(send_counts), rc(recv_counts);
-  pg().alltoall_base(out, in, rc, sc)->wait();
+  wait_work(pg().alltoall_base(out, in, rc, sc));
   if (send.scalar_type() == at::kBool) out = out.view(at::kBool);
   return out.device() == send.device() ? out : out.to(send.device());
 }
@@ -99,7 +114,7 @@ std::vector<int64_t> ProcessGroupCommunicator::ExchangeCounts(const std::vector<
   at::Tensor s = at::tensor(send_counts, at::TensorOptions().dtype(at::kLong)).to(device_);
   at::Tensor r = at::empty({world_}, s.options());
   std::vector<int64_t> ones(world_, 1);
-  pg().alltoall_base(r, s, ones, ones)->wait();
+  wait_work(pg().alltoall_base(r, s, ones, ones));
   at::Tensor h = r.to(at::kCPU);
   return std::vector<int64_t>(h.data_ptr<int64_t>(), h.data_ptr<int64_t>() + world_);
 }
@@ -119,7 +134,7 @@ void ProcessGroupCommunicator::AllReduce(at::Tensor &t, ReduceOp op) {
   std::vector<at::Tensor> v{c};
   c10d::AllreduceOptions o;
   o.reduceOp = to_c10d(op);
-  pg().allreduce(v, o)->wait();
+  wait_work(pg().allreduce(v, o));
   if (!c.is_same(t)) t.copy_(c.view(t.scalar_type()));
 }
 
@@ -131,7 +146,7 @@ at::Tensor ProcessGroupCommunicator::AllGather(const at::Tensor &in) {
   shape[0] = n0 * world_;
   at::Tensor out = at::empty(shape, c.options());
   at::Tensor src = c.dim() == 0 ? c.reshape({1}) : c;
-  pg()._allgather_base(out, src)->wait();
+  wait_work(pg()._allgather_base(out, src));
   if (in.scalar_type() == at::kBool) out = out.view(at::kBool);
   return out.device() == in.device() ? out : out.to(in.device());
 }
@@ -141,7 +156,7 @@ void ProcessGroupCommunicator::Broadcast(at::Tensor &t, int root) {
   std::vector<at::Tensor> v{c};
   c10d::BroadcastOptions o;
   o.rootRank = root;
-  pg().broadcast(v, o)->wait();
+  wait_work(pg().broadcast(v, o));
   if (!c.is_same(t)) t.copy_(c.view(t.scalar_type()));
 }
 
@@ -189,7 +204,7 @@ class PGRequest : public P2PRequest {
       auto w2 = work_;
       std::thread([st, w2]() {
         try {
-          w2->wait();
+          w2->wait();  // helper thread: never holds the GIL
         } catch (...) {
           st->err = std::current_exception();
         }
@@ -206,9 +221,10 @@ class PGRequest : public P2PRequest {
   void Wait() override {
     if (done_) return;
     if (st_) {
+      auto region = EnterBlocking();
       while (!st_->done.load()) std::this_thread::sleep_for(std::chrono::microseconds(50));
     } else {
-      work_->wait();
+      wait_work(work_);
     }
     finish();
   }
@@ -255,7 +271,7 @@ std::pair<at::Tensor, std::shared_ptr<P2PRequest>> ProcessGroupCommunicator::All
     // gloo: complete the exchange before returning.  A gloo all-to-all left in flight
     // while the caller issues further collectives deadlocked intermittently under CPU
     // oversubscription (the CPU rehearsal path only needs the semantics, not overlap).
-    work->wait();
+    wait_work(work);
     return {user, std::make_shared<DoneRequest>()};
   }
   // keep `in` alive until completion: c10d works hold their tensors

@@ -37,6 +37,18 @@ enum class ReduceOp : int { SUM = 0, MIN = 1, MAX = 2, PROD = 3 };
 
 const char *CommTypeName(CommType t);
 
+// Scope around every blocking wait on a transport.  The core library has no Python
+// dependency; the Python extension installs a hook whose region releases the GIL when
+// the waiting thread holds it: c10d gloo works complete on worker threads that can
+// need the GIL (future callbacks), and a rank blocked in wait() while holding it
+// deadlocked the collective under CPU load.
+struct BlockingRegion {
+  virtual ~BlockingRegion() = default;
+};
+using BlockingHook = std::unique_ptr<BlockingRegion> (*)();
+void SetBlockingHook(BlockingHook hook);
+std::unique_ptr<BlockingRegion> EnterBlocking();
+
 // An outstanding point-to-point transfer (ISend / IRecv).
 class P2PRequest {
  public:

@@ -41,6 +41,12 @@ class CylonContext:
         if distributed:
             cfg = config if isinstance(config, CommConfig) else CommConfig()
             backend = cfg.resolved_backend()
+            if backend == "tcp":  # native bootstrap + TCP mesh, no torch.distributed
+                self._ctx = C.Context.init_native("tcp", -1 if cfg.rank is None else cfg.rank,
+                                                  -1 if cfg.world_size is None else cfg.world_size,
+                                                  device or cfg.device or "cpu", float(cfg.timeout_s))
+                self._finalized = False
+                return
             dev = device or cfg.device or (_default_device(True) if backend == "nccl" else "cpu")
             if dev.startswith("cuda"):
                 torch.cuda.set_device(torch.device(dev))

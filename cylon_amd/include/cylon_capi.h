@@ -21,6 +21,11 @@ const char *cylon_last_error(void);
 
 /* context: "cpu" or "cuda:<i>" (local, rank 0 of 1) */
 int cylon_init(const char *device);
+/* distributed context from the torchrun environment (RANK, WORLD_SIZE, MASTER_ADDR,
+   MASTER_PORT, LOCAL_RANK): comm_type "rccl" (one GPU per rank, cuda:<LOCAL_RANK>),
+   "tcp" / "gloo" (host tables over the native TCP mesh) or "mpi" (rccl if GPUs are
+   visible, else tcp).  Reference: CylonContext::InitDistributed(MPIConfig). */
+int cylon_init_distributed(const char *comm_type);
 int cylon_get_rank(void);
 int cylon_get_world_size(void);
 int cylon_barrier(void);

@@ -46,11 +46,26 @@ class GlooConfig(CommConfig):
     backend: Optional[str] = "gloo"
 
 
+@dataclass
+class TCPConfig(CommConfig):
+    """Native TCP mesh (CommType.TCP, no torch.distributed): the C++ bootstrap
+    (CylonContext::InitDistributed) rendezvouses through a c10d TCPStore at
+    MASTER_ADDR:MASTER_PORT and connects every rank pair by a socket.  Host tables;
+    the reference declares this comm type but never implements it."""
+    backend: Optional[str] = "tcp"
+
+    def comm_type(self):
+        return CommType.TCP
+
+    def resolved_backend(self) -> str:
+        return "tcp"
+
+
 class MPIConfig(CommConfig):
     """pycylon compatibility alias: selects the default torch.distributed backend."""
 
 
-__all__ = ["CommConfig", "RCCLConfig", "GlooConfig", "MPIConfig", "CommType"]
+__all__ = ["CommConfig", "RCCLConfig", "GlooConfig", "TCPConfig", "MPIConfig", "CommType"]
 
 
 # ---- point-to-point channel (C4 / P6; reference net/channel.hpp, pycylon/net/txrequest.pyx)

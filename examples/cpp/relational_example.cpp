@@ -2,7 +2,11 @@
 // groupby_example.cpp, sorting_example.cpp, parquet_join_example.cpp).
 //
 // Links only the native core library (cylon_amd/libcylon_amd.so) + libtorch; no Python.
-//   usage: relational_example <device: cpu | cuda:0> <csv1> <csv2> <out_dir>
+//   usage: relational_example <device: cpu | cuda:0 | tcp | rccl> <csv1> <csv2> <out_dir>
+// "tcp" / "rccl" bring up a distributed context natively from the torchrun
+// environment (RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT, LOCAL_RANK) -- the
+// reference's CylonContext::InitDistributed(MPIConfig) -- and "%r" in the paths
+// becomes the rank (per-rank input partitions, per-rank outputs).
 // Reads two CSV tables, then runs join (hash + sort), union / intersect / subtract,
 // unique, sort, a group-by and a scalar aggregate, writes the join result as CSV
 // and Parquet, reads the Parquet file back, and prints one "name rows" line per result.
@@ -34,11 +38,23 @@ int main(int argc, char **argv) {
     return 2;
   }
   const std::string dev = argv[1], out = argv[4];
-  auto ctx = cylon::CylonContext::Init(at::Device(dev));
+  std::shared_ptr<cylon::CylonContext> ctx;
+  if (dev == "tcp" || dev == "rccl") {
+    cylon::net::CommConfig cfg;
+    cfg.type = dev == "tcp" ? cylon::net::CommType::TCP : cylon::net::CommType::RCCL;
+    ctx = cylon::CylonContext::InitDistributed(cfg);
+  } else {
+    ctx = cylon::CylonContext::Init(at::Device(dev));
+  }
+  const std::string rank = std::to_string(ctx->GetRank());
+  auto path = [&](std::string p) {
+    for (size_t i = p.find("%r"); i != std::string::npos; i = p.find("%r")) p.replace(i, 2, rank);
+    return p;
+  };
 
   TablePtr a, b, j, js, u, i, s, q, srt, g, sum, back;
-  CHECK_OK(cylon::FromCSV(ctx, argv[2], a));
-  CHECK_OK(cylon::FromCSV(ctx, argv[3], b, cylon::io::CSVReadOptions().WithDelimiter(',').UseThreads(true).BlockSize(1 << 20)));
+  CHECK_OK(cylon::FromCSV(ctx, path(argv[2]), a));
+  CHECK_OK(cylon::FromCSV(ctx, path(argv[3]), b, cylon::io::CSVReadOptions().WithDelimiter(',').UseThreads(true).BlockSize(1 << 20)));
   report("left", a);
   report("right", b);
 
@@ -63,9 +79,12 @@ int main(int argc, char **argv) {
   CHECK_OK(cylon::compute::Sum(a, 1, sum));
   report("sum_col1", sum);
 
-  CHECK_OK(cylon::WriteCSV(j, out + "/join.csv"));
-  CHECK_OK(cylon::WriteParquet(j, out + "/join.parquet"));
-  CHECK_OK(cylon::FromParquet(ctx, out + "/join.parquet", back));
+  const std::string stem = out + (ctx->IsDistributed() ? "/join_" + rank : "/join");
+  CHECK_OK(cylon::WriteCSV(j, stem + ".csv"));
+  CHECK_OK(cylon::WriteParquet(j, stem + ".parquet"));
+  CHECK_OK(cylon::FromParquet(ctx, stem + ".parquet", back));
   report("parquet_roundtrip", back);
+  ctx->Barrier();
+  ctx->Finalize();
   return 0;
 }

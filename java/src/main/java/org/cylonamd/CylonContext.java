@@ -20,6 +20,16 @@ public final class CylonContext {
     return init("cpu");
   }
 
+  /**
+   * Distributed context from the torchrun environment (RANK, WORLD_SIZE, MASTER_ADDR,
+   * MASTER_PORT, LOCAL_RANK): "rccl" (one GPU per rank), "tcp" (host tables) or "mpi".
+   * Reference: CylonContext.init(MPIConfig) / InitDistributed.
+   */
+  public static CylonContext initDistributed(String commType) {
+    check(nativeInitDistributed(commType));
+    return new CylonContext();
+  }
+
   public int getRank() { return nativeRank(); }
 
   public int getWorldSize() { return nativeWorldSize(); }
@@ -33,6 +43,7 @@ public final class CylonContext {
   }
 
   private static native int nativeInit(String device);
+  private static native int nativeInitDistributed(String commType);
   private static native int nativeRank();
   private static native int nativeWorldSize();
   private static native int nativeBarrier();

@@ -45,6 +45,10 @@ JNIEXPORT jint JFN(CylonContext, nativeInit)(JNIEnv *env, jclass, jstring dev) {
   JStr d(env, dev);
   return cylon_init(d.c);
 }
+JNIEXPORT jint JFN(CylonContext, nativeInitDistributed)(JNIEnv *env, jclass, jstring comm) {
+  JStr c(env, comm);
+  return cylon_init_distributed(c.c);
+}
 JNIEXPORT jint JFN(CylonContext, nativeRank)(JNIEnv *, jclass) { return cylon_get_rank(); }
 JNIEXPORT jint JFN(CylonContext, nativeWorldSize)(JNIEnv *, jclass) { return cylon_get_world_size(); }
 JNIEXPORT jint JFN(CylonContext, nativeBarrier)(JNIEnv *, jclass) { return cylon_barrier(); }

@@ -24,8 +24,10 @@ def _worker(rank, world, port, fn, args, q, device="cpu", env=None):
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         if root not in sys.path:
             sys.path.insert(0, root)
-        from cylon_amd import CylonContext, GlooConfig
-        ctx = CylonContext(config=GlooConfig(), distributed=True, device=device)
+        from cylon_amd import CylonContext, GlooConfig, TCPConfig
+        # CYLON_TEST_COMM=tcp: the native bootstrap + TCP mesh instead of torch.distributed gloo
+        cfg = TCPConfig() if os.environ.get("CYLON_TEST_COMM") == "tcp" else GlooConfig()
+        ctx = CylonContext(config=cfg, distributed=True, device=device)
         try:
             res = fn(ctx, *args)
         finally:

@@ -159,3 +159,57 @@ def test_chunked_join_edge_cases_on_device(case):
     assert _canon(got[sorted(got.columns)]) == _canon(ref[sorted(got.columns)])
     if case == "skew":
         assert any(r[3].get("join.radix.overflow_fallback", 0) > 0 for r in res)
+
+
+# ---------------------------------------------------------------------------
+# Asynchronous exchange on the device (net/async_delay_communicator.hpp): every posted
+# all-to-all completes on a side HIP stream after a spin delay into a poisoned buffer,
+# with event-backed requests (Test = event query, Wait = stream wait) -- RCCL's completion
+# semantics, so the chunk-k-consumed-while-k+1-in-flight ordering runs for real.
+# ---------------------------------------------------------------------------
+def _async_join(ctx, chunks, n, delay_us):
+    from cylon_amd import Table
+    from cylon_amd._lib import C
+    rank = ctx.get_rank()
+    ctx._ctx.use_async_delay_transport(float(delay_us))
+    rng = np.random.default_rng(70 + rank)
+    a = pd.DataFrame({"k": rng.integers(0, int(0.99 * 2 * n), n), "x": rng.integers(-9, 9, n).astype(np.int32),
+                      "f": rng.random(n)})
+    b = pd.DataFrame({"k": rng.integers(0, int(0.99 * 2 * n), n), "v": rng.random(n)})
+    ta, tb = Table.from_pandas(ctx, a), Table.from_pandas(ctx, b)
+    ctx.add_config("shuffle_chunks", str(chunks))
+    C.trace_enable(True)
+    C.trace_reset()
+    out = ta.distributed_join(tb, "inner", "hash", on=["k"], left_prefix="l_", right_prefix="r_")
+    got = out.to_pandas()
+    join_counters = dict(C.trace_counters())
+    u1 = pd.DataFrame({"a": rng.integers(0, 500, 4000), "b": rng.integers(0, 3, 4000)})
+    u2 = pd.DataFrame({"a": rng.integers(0, 500, 3000), "b": rng.integers(0, 3, 3000)})
+    tu1, tu2 = Table.from_pandas(ctx, u1), Table.from_pandas(ctx, u2)
+    sets = {op: getattr(tu1, f"distributed_{op}")(tu2).to_pandas() for op in ("union", "intersect", "subtract")}
+    posted, in_flight = ctx._ctx.async_transport_stats()
+    return got, a, b, u1, u2, sets, posted, in_flight, join_counters
+
+
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_async_exchange_join_and_setops_on_device(chunks):
+    res = run_distributed(_async_join, 2, chunks, 60_000, 3000, device=DEV, env=SMALL_RADIX)
+    got = pd.concat([r[0] for r in res])
+    a = pd.concat([r[1] for r in res])
+    b = pd.concat([r[2] for r in res])
+    ref = a.add_prefix("l_").merge(b.add_prefix("r_"), left_on="l_k", right_on="r_k")
+    assert len(got) == len(ref) > 0
+    assert _canon(got[sorted(got.columns)]) == _canon(ref[sorted(got.columns)])
+    u1 = pd.concat([r[3] for r in res])
+    u2 = pd.concat([r[4] for r in res])
+    A = set(map(tuple, u1.to_numpy().tolist()))
+    B = set(map(tuple, u2.to_numpy().tolist()))
+    for op, rows in {"union": A | B, "intersect": A & B, "subtract": A - B}.items():
+        g = [tuple(x) for r in res for x in r[5][op].to_numpy().tolist()]
+        assert len(g) == len(set(g)) and set(g) == rows, op
+    for r in res:
+        posted, in_flight, c = r[6], r[7], r[8]
+        assert posted > 0
+        assert in_flight > 0, "no posted exchange was still in flight when its consumer reached it"
+        if chunks > 1:
+            assert c.get("shuffle.chunks") == chunks

@@ -109,6 +109,16 @@ def test_distributed_join_golden(data_dir, world, algorithm):
         assert ok, f"rows got={got} expected={exp}"
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_distributed_join_golden_native_tcp(data_dir, world):
+    """Same golden files with the context brought up natively (TCPConfig: C++ bootstrap over a
+    TCPStore, native TCP mesh transport; no torch.distributed process group)."""
+    import pyarrow.csv  # noqa: F401
+    res = run_distributed(_golden_join, world, data_dir, "hash", env={"CYLON_TEST_COMM": "tcp"})
+    for ok, got, exp in res:
+        assert ok, f"rows got={got} expected={exp}"
+
+
 def _dist_vs_oracle(ctx, how, algorithm):
     rank, world = ctx.get_rank(), ctx.get_world_size()
     rng = np.random.default_rng(100 + rank)
