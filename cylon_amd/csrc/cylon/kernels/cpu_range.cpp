@@ -2,6 +2,7 @@
 #include <cmath>
 #include <cstring>
 #include <limits>
+#include <vector>
 
 #include "kernels.hpp"
 #include "../types.hpp"
@@ -74,6 +75,36 @@ void range_partition(const ColView &c, int64_t n, double vmin, double vmax, int6
     if (desc) p = nparts - 1 - p;
     pid[i] = p;
     counts[p]++;
+  }
+}
+
+}  // namespace cpu
+}  // namespace cylon
+
+namespace cylon {
+namespace cpu {
+
+void splitter_partition(const uint64_t *const *images, const uint8_t *const *nulls, int nkeys, int64_t n,
+                        int64_t gid0, const uint64_t *splitters, uint32_t nparts, uint32_t *pid, int64_t *counts,
+                        void *) {
+  const int stride = 2 * nkeys + 1;
+  std::vector<uint64_t> k(stride);
+  for (int64_t i = 0; i < n; ++i) {
+    for (int c = 0; c < nkeys; ++c) {
+      k[2 * c] = nulls[c] ? (uint64_t)(nulls[c][i] != 0) : 0ull;
+      k[2 * c + 1] = images[c][i];
+    }
+    k[2 * nkeys] = (uint64_t)(gid0 + i);
+    uint32_t lo = 0, hi = nparts - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      const uint64_t *s = splitters + (int64_t)mid * stride;
+      int cmp = 0;
+      for (int w = 0; w < stride && cmp == 0; ++w) cmp = s[w] < k[w] ? -1 : (s[w] > k[w] ? 1 : 0);
+      if (cmp < 0) lo = mid + 1; else hi = mid;
+    }
+    pid[i] = lo;
+    ++counts[lo];
   }
 }
 

@@ -122,5 +122,75 @@ void range_partition(const ColView &c, int64_t n, double vmin, double vmax, int6
   HIP_LAUNCH_CHECK();
 }
 
+// ---------------------------------------------------------------------------
+// Sample-sort partition by exact composite splitters (see kernel_decls.inc).
+// The splitters (<= 1023 x (2 * kMaxSortKeys + 1) words) are staged in LDS;
+// every row binary-searches them, and a block histogram in LDS feeds one
+// atomic per partition per block.
+// ---------------------------------------------------------------------------
+constexpr int kMaxSortKeys = 4;
+constexpr int kMaxSplitParts = 1024;
+
+struct SplitKeys {
+  const uint64_t *img[kMaxSortKeys];
+  const uint8_t *nul[kMaxSortKeys];
+};
+
+__global__ __launch_bounds__(kBlock) void k_splitter_partition(SplitKeys keys, int nkeys, int64_t n, int64_t gid0,
+                                                               const uint64_t *__restrict__ spl, uint32_t nparts,
+                                                               uint32_t *__restrict__ pid,
+                                                               unsigned long long *__restrict__ counts) {
+  extern __shared__ uint64_t s_spl[];  // (nparts - 1) * stride words, then nparts u32 counters
+  const int stride = 2 * nkeys + 1;
+  const int nw = (int)(nparts - 1) * stride;
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) s_spl[i] = spl[i];
+  unsigned int *hist = reinterpret_cast<unsigned int *>(s_spl + nw);
+  for (uint32_t p = threadIdx.x; p < nparts; p += blockDim.x) hist[p] = 0;
+  __syncthreads();
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+    uint64_t k[2 * kMaxSortKeys + 1];
+#pragma unroll
+    for (int c = 0; c < kMaxSortKeys; ++c)
+      if (c < nkeys) {
+        k[2 * c] = keys.nul[c] ? (uint64_t)(keys.nul[c][i] != 0) : 0ull;
+        k[2 * c + 1] = keys.img[c][i];
+      }
+    k[2 * nkeys] = (uint64_t)(gid0 + i);
+    // lower bound: first splitter >= key; pid = number of splitters < key
+    uint32_t lo = 0, hi = nparts - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      const uint64_t *s = s_spl + (int64_t)mid * stride;
+      int cmp = 0;
+      for (int w = 0; w < stride && cmp == 0; ++w) cmp = s[w] < k[w] ? -1 : (s[w] > k[w] ? 1 : 0);
+      if (cmp < 0) lo = mid + 1; else hi = mid;
+    }
+    pid[i] = lo;
+    atomicAdd(&hist[lo], 1u);
+  }
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < nparts; p += blockDim.x)
+    if (hist[p]) atomicAdd(&counts[p], (unsigned long long)hist[p]);
+}
+
+void splitter_partition(const uint64_t *const *images, const uint8_t *const *nulls, int nkeys, int64_t n,
+                        int64_t gid0, const uint64_t *splitters, uint32_t nparts, uint32_t *pid, int64_t *counts,
+                        void *stream) {
+  CYLON_CHECK(nkeys >= 1 && nkeys <= kMaxSortKeys, Code::Invalid, "splitter partition over " << nkeys << " keys");
+  CYLON_CHECK(nparts >= 1 && nparts <= (uint32_t)kMaxSplitParts, Code::Invalid, "partition count " << nparts);
+  if (n == 0) return;
+  SplitKeys k{};
+  for (int c = 0; c < nkeys; ++c) {
+    k.img[c] = images[c];
+    k.nul[c] = nulls[c];
+  }
+  const size_t lds = (size_t)(nparts - 1) * (2 * nkeys + 1) * sizeof(uint64_t) + nparts * sizeof(unsigned int);
+  hipLaunchKernelGGL(k_splitter_partition, dim3(grid_for(n, kBlock, kNumCUs * 4)), dim3(kBlock), lds,
+                     as_stream(stream), k, nkeys, n, gid0, splitters, nparts, pid,
+                     reinterpret_cast<unsigned long long *>(counts));
+  HIP_LAUNCH_CHECK();
+}
+
 }  // namespace hip
 }  // namespace cylon

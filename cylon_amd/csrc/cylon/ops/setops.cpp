@@ -11,6 +11,7 @@
 // presence flags (mark_indices over the L and R slices of the group-id vector)
 // and one gather of the selected first-occurrence rows.  Output keeps the input
 // order of the surviving rows (first occurrences ascend).
+#include <algorithm>
 #include <cmath>
 #include <limits>
 
@@ -250,12 +251,111 @@ std::pair<at::Tensor, std::vector<int64_t>> MapToSortPartitions(const TablePtr &
   return {pid, to_host_vec(counts)};
 }
 
+// Exact sample-sort splitters (DistributedSort).  Every row gets the composite key
+// (null_0, image_0, ..., null_K-1, image_K-1, gid) over ALL sort columns -- order
+// images are the local sort's uint64 keys (direction applied, NaN last), nulls sort
+// last, gid = the row's global number -- so keys are distinct and totally ordered
+// exactly like the final order.  A random sample of each rank's keys is all-gathered,
+// sorted on the host and cut at W-1 equal-count positions; rows are then assigned by
+// binary search over these splitters.  Unlike the reference's equal-width bins over
+// a double [min, max] (table.cpp:338-382, arrow_partition_kernels.cpp:334-455), no
+// precision is lost for int64 keys, and equal keys may straddle ranks in gid order,
+// so heavy skew (even a single repeated key) still splits evenly.  The local sort
+// after the exchange is stable and receives pieces in rank order, which keeps equal
+// keys in gid order: the distributed sort is globally stable.
+static bool splitter_sort_eligible(const TablePtr &t, const std::vector<int> &cols, int world) {
+  if (cols.empty() || cols.size() > 4 || world > 1024) return false;
+  for (int c : cols) {
+    const Column &col = t->column(c);
+    if (col.is_var() || col.type.kind() == ValueKind::FIXED_BYTES || !col.type.is_numeric()) return false;
+  }
+  return true;
+}
+
+static TablePtr splitter_sort(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending,
+                              const SortOptions &opts) {
+  auto ctx = t->GetContext();
+  auto comm = ctx->GetCommunicator();
+  const int W = ctx->GetWorldSize();
+  const int K = (int)cols.size();
+  const int stride = 2 * K + 1;
+  Exec ex(t->device());
+  const int64_t n = t->Rows();
+  std::vector<at::Tensor> imgs(K), nuls(K);
+  std::vector<const uint64_t *> ip(K);
+  std::vector<const uint8_t *> np(K, nullptr);
+  {
+    CYLON_PHASE("sort.dist.images", ex.device);
+    for (int k = 0; k < K; ++k) {
+      const Column &c = t->column(cols[k]);
+      const bool asc = ascending.empty() ? true : (ascending.size() == 1 ? ascending[0] : ascending[k]);
+      imgs[k] = ex.empty_i64(std::max<int64_t>(n, 1));
+      if (n) KCALL(ex, sort_keys_from_column, c.view(), nullptr, n, !asc, reinterpret_cast<uint64_t *>(ptr<int64_t>(imgs[k])));
+      ip[k] = reinterpret_cast<const uint64_t *>(imgs[k].data_ptr());
+      if (c.nullable()) {
+        nuls[k] = c.validity.slice(0, 0, n).eq(0).to(at::kByte).contiguous();
+        np[k] = nuls[k].numel() ? nuls[k].data_ptr<uint8_t>() : nullptr;
+      }
+    }
+  }
+  // global row numbers: rank r's rows are gid0 .. gid0 + n - 1
+  at::Tensor ns = comm->AllGather(at::full({1}, n, ex.opts(at::kLong))).to(at::kCPU);
+  int64_t gid0 = 0;
+  for (int r = 0; r < ctx->GetRank(); ++r) gid0 += ns[r].item<int64_t>();
+  // sample -> all-gather -> host sort -> W-1 splitters
+  const int64_t per = std::min<int64_t>(n, opts.num_samples ? (int64_t)opts.num_samples : 256 * (int64_t)W);
+  at::Tensor idx = per == n ? at::arange(n, ex.opts(at::kLong))
+                            : at::randint(0, std::max<int64_t>(n, 1), {per}, ex.opts(at::kLong));
+  at::Tensor sample = at::empty({per, stride}, ex.opts(at::kLong));
+  for (int k = 0; k < K; ++k) {
+    sample.select(1, 2 * k).copy_(nuls[k].defined() ? nuls[k].index_select(0, idx).to(at::kLong)
+                                                    : at::zeros({per}, ex.opts(at::kLong)));
+    sample.select(1, 2 * k + 1).copy_(imgs[k].slice(0, 0, std::max<int64_t>(n, 1)).index_select(0, idx));
+  }
+  sample.select(1, 2 * K).copy_(idx + gid0);
+  std::vector<at::Tensor> parts = comm->AllGatherV(sample.reshape({-1}));
+  at::Tensor all = at::cat(parts).to(at::kCPU).contiguous();
+  const int64_t S = all.numel() / stride;
+  const uint64_t *sw = reinterpret_cast<const uint64_t *>(all.data_ptr<int64_t>());
+  std::vector<int64_t> order(S);
+  for (int64_t i = 0; i < S; ++i) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+    return std::lexicographical_compare(sw + a * stride, sw + (a + 1) * stride, sw + b * stride, sw + (b + 1) * stride);
+  });
+  std::vector<uint64_t> spl((size_t)(W - 1) * stride, ~0ull);
+  for (int i = 0; i + 1 < W && S > 0; ++i) {
+    const int64_t at_ = std::min<int64_t>(S - 1, (int64_t)(i + 1) * S / W);
+    std::copy(sw + order[at_] * stride, sw + (order[at_] + 1) * stride, spl.begin() + (size_t)i * stride);
+  }
+  at::Tensor spl_t = at::from_blob(spl.data(), {(int64_t)spl.size()}, at::TensorOptions().dtype(at::kLong))
+                         .to(ex.device)
+                         .contiguous();
+  at::Tensor pid = ex.empty_u32(std::max<int64_t>(n, 1));
+  at::Tensor counts = at::zeros({W}, ex.opts(at::kLong));
+  {
+    CYLON_PHASE("sort.dist.partition", ex.device);
+    KCALL(ex, splitter_partition, ip.data(), np.data(), K, n, gid0,
+          reinterpret_cast<const uint64_t *>(ptr<int64_t>(spl_t)), (uint32_t)W, ptr<uint32_t>(pid),
+          ptr<int64_t>(counts));
+  }
+  trace::add_counter("sort.dist.splitter_partitions", 1);
+  auto reordered = PartitionReorder(t, pid.slice(0, 0, n), (uint32_t)W);
+  TablePtr recv;
+  {
+    CYLON_PHASE("sort.dist.exchange", ex.device);
+    recv = AllToAllTable(reordered.first, reordered.second);
+  }
+  return Sort(recv, cols, ascending);
+}
+
 TablePtr DistributedSort(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending,
                          const SortOptions &opts) {
   auto ctx = t->GetContext();
   const int world = ctx->GetWorldSize();
   if (world == 1) return Sort(t, cols, ascending);
   CYLON_CHECK(!cols.empty(), Code::Invalid, "sort needs at least one column");
+  if (splitter_sort_eligible(t, cols, world)) return splitter_sort(t, cols, ascending, opts);
+  // string / binary first column etc.: the reference's histogram partition on the first column
   const bool asc0 = ascending.empty() ? true : ascending[0];
   auto pm = MapToSortPartitions(t, cols[0], (uint32_t)world, asc0, opts.num_samples, opts.num_bins);
   auto reordered = PartitionReorder(t, pm.first, (uint32_t)world);

@@ -58,8 +58,10 @@ class Table {
 
 // Sort options for DistributedSort (reference table.hpp:388-393).
 struct SortOptions {
+  // DistributedSort samples num_samples rows per rank (0 -> 256 x world) for its exact
+  // splitters; MapToSortPartitions (the reference's bin histogram) uses both fields.
   uint32_t num_bins = 0;     // 0 -> 16 * world
-  uint64_t num_samples = 0;  // 0 -> 1% of rows
+  uint64_t num_samples = 0;  // 0 -> DistributedSort: 256 x world per rank; MapToSortPartitions: 1% of rows
   static SortOptions Defaults() { return SortOptions(); }
 };
 

@@ -137,3 +137,46 @@ def test_range_partition_monotonic(ctx):
     order = np.argsort(vals, kind="stable")
     assert np.all(np.diff(pid[order]) >= 0)
     assert sum(counts) == 5000
+
+
+def _dist_sort_case(ctx, case):
+    rank = ctx.get_rank()
+    rng = np.random.default_rng(40 + rank)
+    n = 3000 + 500 * rank
+    if case == "wide_int64":  # keys spanning +-2^62 (beyond double precision)
+        a = rng.integers(-(1 << 62), 1 << 62, n, dtype=np.int64)
+        a[: n // 10] = (1 << 62) + np.arange(n // 10)  # neighbours 1 apart near 2^62
+        df = pd.DataFrame({"a": a, "i": np.arange(n) + 100000 * rank})
+        cols, asc = ["a"], True
+    elif case == "one_key":  # every row the same key: balance must come from the tie-break
+        df = pd.DataFrame({"a": np.full(n, 7, dtype=np.int64), "i": np.arange(n) + 100000 * rank})
+        cols, asc = ["a"], True
+    elif case == "skew_desc":  # 90% of the rows on one key, descending
+        a = np.where(rng.random(n) < 0.9, 123, rng.integers(0, 1000, n)).astype(np.int64)
+        df = pd.DataFrame({"a": a, "i": np.arange(n) + 100000 * rank})
+        cols, asc = ["a"], False
+    elif case == "multi_nulls":  # two sort columns, nulls in the first, float second
+        a = pd.array(rng.integers(0, 20, n), dtype="Int64")
+        a[rng.random(n) < 0.1] = pd.NA
+        df = pd.DataFrame({"a": a, "b": rng.standard_normal(n), "i": np.arange(n) + 100000 * rank})
+        cols, asc = ["a", "b"], [True, False]
+    t = Table.from_pandas(ctx, df)
+    s = t.distributed_sort(cols, ascending=asc)
+    return s.to_pandas(), df, cols, asc
+
+
+@pytest.mark.parametrize("case", ["wide_int64", "one_key", "skew_desc", "multi_nulls"])
+def test_distributed_sort_exact_splitters(case):
+    """Exact composite-key splitters: global order equals a stable sort of the rank-ordered
+    concatenation (ties keep input order across ranks), and per-rank loads stay within 1.5x
+    of the mean even when one key holds every row (reference: table.cpp:338-382)."""
+    world = 4
+    res = run_distributed(_dist_sort_case, world, case)
+    cols, asc = res[0][2], res[0][3]
+    allin = pd.concat([r[1] for r in res]).reset_index(drop=True)
+    got = pd.concat([r[0] for r in res]).reset_index(drop=True)
+    exp = allin.sort_values(cols, ascending=asc, kind="mergesort", na_position="last").reset_index(drop=True)
+    assert len(got) == len(exp)
+    pd.testing.assert_frame_equal(got.astype(exp.dtypes.to_dict()), exp, check_dtype=False)
+    loads = [len(r[0]) for r in res]
+    assert max(loads) <= 1.5 * len(allin) / world, loads
