@@ -3,6 +3,7 @@
 
 #include "relational.hpp"
 #include "util.hpp"
+#include "../trace.hpp"
 
 namespace cylon {
 namespace graph {
@@ -127,12 +128,12 @@ bool SequentialExecution::IsComplete() {
 }
 
 bool JoinExecution::IsComplete() {
-  auto run = [](std::vector<Op *> &ops, size_t &idx) {
-    while (idx < ops.size()) {
-      if (!ops[idx]->IsComplete()) return false;
-      ++idx;
-    }
-    return true;
+  // the ops of one subtree are progressed round-robin (a batch flows root -> partition ->
+  // exchange -> split while the next one follows), one subtree at a time
+  auto run = [](std::vector<Op *> &ops, size_t &) {
+    bool all = true;
+    for (Op *op : ops) all &= op->IsComplete();
+    return all;
   };
   if (stage_ == 0) {
     if (!run(l_, idx_)) return false;
@@ -179,24 +180,64 @@ AllToAllOp::AllToAllOp(std::shared_ptr<CylonContext> ctx, int id, ResultsCallbac
 bool AllToAllOp::Execute(int tag, const TablePtr &table) {
   CYLON_CHECK(tag >= 0 && tag < (int)per_target_.size(), Code::IndexError, "all-to-all target " << tag);
   per_target_[tag].push_back(table);
+  if (!tmpl_) tmpl_ = table;
+  bool whole = true;
+  for (auto &v : per_target_) whole &= !v.empty();
+  if (whole) Round(false);
+  Poll(false);
   return true;
 }
 
-void AllToAllOp::OnParentsFinalized() {
-  TablePtr tmpl;
-  for (auto &v : per_target_)
-    if (!v.empty()) tmpl = v[0];
-  CYLON_CHECK(tmpl != nullptr, Code::Invalid, "AllToAllOp on rank " << ctx_->GetRank() << " received no table");
+bool AllToAllOp::Round(bool done) {
+  at::Tensor flag = at::full({1}, done ? 1 : 0, at::TensorOptions().dtype(at::kInt).device(ctx_->GetDevice()));
+  if (ctx_->GetWorldSize() > 1) ctx_->GetCommunicator()->AllReduce(flag, net::ReduceOp::SUM);
+  if (flag.item<int>() == ctx_->GetWorldSize()) return true;
+  CYLON_CHECK(tmpl_ != nullptr, Code::Invalid, "AllToAllOp on rank " << ctx_->GetRank() << " received no table");
   std::vector<TablePtr> ordered;
   std::vector<int64_t> counts;
-  for (auto &v : per_target_) {
-    TablePtr m = v.empty() ? ops::Slice(tmpl, 0, 0) : ops::Merge(v);
+  for (auto &v : per_target_) {  // one batch = the oldest pending partition of every target
+    TablePtr m = v.empty() ? ops::Slice(tmpl_, 0, 0) : v.front();
+    if (!v.empty()) v.pop_front();
     counts.push_back(m->Rows());
     ordered.push_back(m);
   }
-  TablePtr out = ops::AllToAllTable(ops::Merge(ordered), counts);
-  per_target_.assign(per_target_.size(), {});
-  Emit(out_tag_, out);
+  posted_.push_back(ops::PostAllToAllTable(ops::Merge(ordered), counts));
+  ++rounds_;
+  trace::add_counter("graph.alltoall.rounds", 1);
+  return false;
+}
+
+void AllToAllOp::Poll(bool wait) {
+  while (!posted_.empty() && (wait || ops::PostedExchangeReady(*posted_.front()))) {
+    if (!wait) {
+      ++emitted_early_;
+      trace::add_counter("graph.alltoall.streamed_rounds", 1);  // emitted before the inputs ended
+    }
+    TablePtr out = ops::FinishPostedExchange(*posted_.front());
+    posted_.pop_front();
+    Emit(out_tag_, out);
+  }
+}
+
+bool AllToAllOp::IsComplete() {
+  Poll(false);
+  return Op::IsComplete();
+}
+
+bool AllToAllOp::Finalize() {
+  if (!all_done_) {
+    for (;;) {  // batches still pending (incomplete ones included)
+      bool pending = false;
+      for (auto &v : per_target_) pending |= !v.empty();
+      if (!pending) break;
+      Round(false);
+    }
+    while (!Round(true)) {                     // empty rounds until every rank is done
+    }
+    all_done_ = true;
+  }
+  Poll(true);
+  return true;
 }
 
 SplitOp::SplitOp(std::shared_ptr<CylonContext> ctx, int id, ResultsCallback cb, int num_splits, std::vector<int> cols,

@@ -8,13 +8,13 @@
 //
 // MI355X design: every op body is a device operator from this engine (hash
 // partition K1-K3, join K4-K7, union K10); the exchange edge (AllToAllOp)
-// performs ONE size exchange + per-buffer RCCL all-to-all when its parents
-// finalize, so every rank issues the same collectives in the same order
-// (the scheduler is deterministic) - no host progress engine is needed for
-// the transport.  Input batches stream through the partition/split ops as they
-// arrive; the sub-partition fan-out (SplitOp) bounds the size of each local
-// join like the reference's two-level partitioning.
+// streams: each input batch becomes one exchange round (size exchange + per-buffer
+// RCCL all-to-alls left in flight), polled without blocking, so batch k is split /
+// joined while batch k+1 is on xGMI.  Rounds are collective and identical on every
+// rank (see AllToAllOp).  The sub-partition fan-out (SplitOp) bounds the size of
+// each local join like the reference's two-level partitioning.
 #pragma once
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -158,18 +158,40 @@ class PartitionOp : public Op {
   std::vector<int> cols_;
 };
 
-// buffers partitions per target; on parents' completion performs the exchange
+// Streaming exchange edge (reference all_to_all_op.cpp:40-62 inserts every batch into
+// its ArrowAllToAll and progresses it inside IsComplete).  Here the exchange advances in
+// ROUNDS that every rank takes part in, so the collectives stay matched:
+//   * a round starts as soon as a whole batch has arrived (one partition per target,
+//     PartitionOp emits exactly that): one all-reduce of the "inputs finished" flag,
+//     then the batch's size exchange and its column all-to-alls are POSTED, not waited;
+//   * IsComplete polls the posted rounds in order and emits each received table as
+//     soon as its transfers have landed, while later batches are still partitioned
+//     and on the wire (RCCL: its own stream; requests tested without blocking);
+//   * after its own inputs end, a rank keeps joining rounds with empty sends until
+//     the all-reduced flag says every rank is done.
+// Only one exchange op may be progressing at a time in a schedule (JoinExecution runs
+// the left subtree, then the right), which keeps the round sequence identical on all
+// ranks.
 class AllToAllOp : public Op {
  public:
   AllToAllOp(std::shared_ptr<CylonContext> ctx, int id, ResultsCallback cb, int out_tag);
+  bool IsComplete() override;
+  int64_t rounds() const { return rounds_; }
+  int64_t emitted_early() const { return emitted_early_; }
 
  protected:
   bool Execute(int tag, const TablePtr &table) override;
-  void OnParentsFinalized() override;
+  bool Finalize() override;
 
  private:
-  std::vector<std::vector<TablePtr>> per_target_;
+  bool Round(bool done);  // returns true when every rank reported done (no exchange posted)
+  void Poll(bool wait);
+  std::vector<std::deque<TablePtr>> per_target_;
+  std::deque<std::shared_ptr<ops::PostedExchange>> posted_;
+  TablePtr tmpl_;
   int out_tag_;
+  bool all_done_ = false;
+  int64_t rounds_ = 0, emitted_early_ = 0;
 };
 
 // local hash split into `num_splits` sub-partitions (tag = base_tag + i)

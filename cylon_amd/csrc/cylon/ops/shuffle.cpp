@@ -334,6 +334,25 @@ TablePtr AllToAllTable(const TablePtr &part, const std::vector<int64_t> &counts)
   return AllToAllFinish(pt);
 }
 
+struct PostedExchange {
+  PendingTable pt;
+};
+
+std::shared_ptr<PostedExchange> PostAllToAllTable(const TablePtr &part, const std::vector<int64_t> &counts) {
+  auto x = std::make_shared<PostedExchange>();
+  x->pt = AllToAllBegin(part, counts);
+  return x;
+}
+
+bool PostedExchangeReady(PostedExchange &x) {
+  if (x.pt.passthrough) return true;
+  for (auto &r : x.pt.reqs)
+    if (!r->Test()) return false;
+  return true;
+}
+
+TablePtr FinishPostedExchange(PostedExchange &x) { return AllToAllFinish(x.pt); }
+
 std::pair<TablePtr, std::vector<int64_t>> ShufflePartition(const TablePtr &t, const std::vector<int> &hash_cols,
                                                            uint32_t nparts) {
   if (mod_pass_eligible(t, hash_cols, nparts)) return {mod_reorder(t, hash_cols[0], nparts), mod_counts(t, hash_cols[0], nparts)};

@@ -94,6 +94,14 @@ std::vector<TablePtr> HashPartition(const TablePtr &t, const std::vector<int> &c
 // ---- communication --------------------------------------------------------
 // partition-major table + per-partition counts -> received table
 TablePtr AllToAllTable(const TablePtr &partitioned, const std::vector<int64_t> &counts);
+// Posted (non-blocking) form of AllToAllTable: the size / schema agreement collectives
+// run now, the column all-to-alls are left in flight (RCCL: on its stream).
+// PostedExchangeReady tests the transfers without blocking; FinishPostedExchange waits
+// (stream-ordered on RCCL) and assembles the received table.
+struct PostedExchange;
+std::shared_ptr<PostedExchange> PostAllToAllTable(const TablePtr &partitioned, const std::vector<int64_t> &counts);
+bool PostedExchangeReady(PostedExchange &x);
+TablePtr FinishPostedExchange(PostedExchange &x);
 TablePtr Shuffle(const TablePtr &t, const std::vector<int> &hash_cols);
 // shuffle two tables with the second one's partitioning overlapped with the first's transfer
 std::pair<TablePtr, TablePtr> ShufflePair(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,

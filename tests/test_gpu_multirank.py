@@ -240,3 +240,35 @@ def test_distributed_sort_exact_splitters_on_device(case):
     assert got["k"].tolist() == exp["k"].tolist() and got["i"].tolist() == exp["i"].tolist()
     loads = [len(r[0]) for r in res]
     assert max(loads) <= 1.5 * len(allin) / 2, loads
+
+
+def _graph_async(ctx):
+    from cylon_amd import Table
+    from cylon_amd._lib import C
+    from cylon_amd.parallel import DisJoinOp
+    rank = ctx.get_rank()
+    ctx._ctx.use_async_delay_transport(500.0)
+    rng = np.random.default_rng(20 + rank)
+    lefts = [pd.DataFrame({"k": rng.integers(0, 5000, 20_000), "v": rng.random(20_000)}) for _ in range(4 - 2 * rank)]
+    rights = [pd.DataFrame({"k": rng.integers(0, 5000, 15_000), "w": rng.random(15_000)}) for _ in range(2)]
+    C.trace_enable(True)
+    C.trace_reset()
+    op = DisJoinOp(ctx, "inner", "hash", [0], [0], "l_", "r_", num_splits=4)
+    for d in lefts:
+        op.insert_table(DisJoinOp.LEFT, Table.from_pandas(ctx, d))
+    for d in rights:
+        op.insert_table(DisJoinOp.RIGHT, Table.from_pandas(ctx, d))
+    got = pd.concat([r.to_pandas() for r in op.execute()])
+    return got, pd.concat(lefts), pd.concat(rights), dict(C.trace_counters())
+
+
+def test_dis_join_op_streaming_on_device_async():
+    """Streaming op-graph exchange on HBM tables with event-backed asynchronous transfers."""
+    res = run_distributed(_graph_async, 2, device=DEV)
+    got = pd.concat([r[0] for r in res])
+    a = pd.concat([r[1] for r in res])
+    b = pd.concat([r[2] for r in res])
+    ref = a.add_prefix("l_").merge(b.add_prefix("r_"), left_on="l_k", right_on="r_k")
+    assert len(got) == len(ref) and _canon(got[sorted(got.columns)]) == _canon(ref[sorted(got.columns)])
+    for r in res:
+        assert r[3].get("graph.alltoall.rounds") == 6, r[3]  # 4 left rounds (rank 0's batches) + 2 right

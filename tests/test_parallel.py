@@ -211,3 +211,38 @@ def test_bench_self_launch_four_ranks_cpu():
                          capture_output=True, text=True, timeout=120, cwd="/tmp",
                          env=dict(env, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
     assert bad.returncode == 2 and "WORLD_SIZE" in bad.stderr
+
+
+def _op_graph_uneven(ctx):
+    """Ranks feed different numbers of batches; the streaming exchange keeps rounds matched."""
+    from cylon_amd._lib import C
+    rank = ctx.get_rank()
+    rng = np.random.default_rng(10 + rank)
+    nb_left = 5 if rank == 0 else 1
+    lefts = [pd.DataFrame({"k": rng.integers(0, 60, 50), "v": rng.random(50)}) for _ in range(nb_left)]
+    rights = [pd.DataFrame({"k": rng.integers(0, 60, 35), "w": rng.random(35)}) for _ in range(2 + rank)]
+    C.trace_enable(True)
+    C.trace_reset()
+    op = DisJoinOp(ctx, "inner", "hash", [0], [0], "l_", "r_", num_splits=4)
+    for d in lefts:
+        op.insert_table(DisJoinOp.LEFT, Table.from_pandas(ctx, d))
+    for d in rights:
+        op.insert_table(DisJoinOp.RIGHT, Table.from_pandas(ctx, d))
+    res = op.execute()
+    got = pd.concat([r.to_pandas() for r in res]) if res else pd.DataFrame()
+    return got, pd.concat(lefts), pd.concat(rights), dict(C.trace_counters())
+
+
+def test_dis_join_op_streaming_rounds():
+    """AllToAllOp streams (reference all_to_all_op.cpp:40-62): one collective round per batch,
+    empty rounds for ranks whose inputs ended, results equal to pandas."""
+    res = run_distributed(_op_graph_uneven, 2)
+    got = pd.concat([r[0] for r in res])
+    a = pd.concat([r[1] for r in res])
+    b = pd.concat([r[2] for r in res])
+    exp = a.add_prefix("l_").merge(b.add_prefix("r_"), left_on="l_k", right_on="r_k")
+    assert len(got) == len(exp) and _rows(got) == _rows(exp[got.columns])
+    for r in res:
+        c = r[3]
+        # left: 5 rounds (rank 0's batches), right: 3 rounds -- identical on both ranks
+        assert c.get("graph.alltoall.rounds") == 8, c
