@@ -44,7 +44,7 @@ CORE_LIB = os.path.join(PKG, "libcylon_amd.so")
 
 def core_sources():
     srcs = [os.path.join(CSRC, "capi.cpp")]
-    for sub in ("cylon", "cylon/net", "cylon/ops", "cylon/ctx", "cylon/io", "cylon/kernels"):
+    for sub in ("cylon", "cylon/net", "cylon/ops", "cylon/ctx", "cylon/io", "cylon/kernels", "cylon/indexing"):
         srcs += sorted(glob.glob(os.path.join(CSRC, sub, "*.cpp")))
     return srcs
 

@@ -9,6 +9,7 @@
 #include "cylon/api.hpp"
 #include "cylon/io/arrow_io.hpp"
 #include "cylon/io/csv.hpp"
+#include "cylon/indexing/index.hpp"
 #include "cylon/ops/api_ext.hpp"
 #include "cylon/ops/graph.hpp"
 #include "cylon/ops/relational.hpp"
@@ -34,6 +35,39 @@ void register_extended_ops(py::module &m) {
   auto rel = py::call_guard<py::gil_scoped_release>();
 
   m.def("index_lookup", &ops::IndexLookup, py::arg("ctx"), py::arg("index"), py::arg("labels"), rel);
+
+  // ---- C27 persistent indexes + loc / iloc indexers (cylon/indexing/index.hpp)
+  py::enum_<indexing::IndexingSchema>(m, "IndexingSchema")
+      .value("RANGE", indexing::IndexingSchema::Range)
+      .value("LINEAR", indexing::IndexingSchema::Linear)
+      .value("HASH", indexing::IndexingSchema::Hash)
+      .value("BINARYTREE", indexing::IndexingSchema::BinaryTree)
+      .value("BTREE", indexing::IndexingSchema::BTree);
+  py::class_<indexing::BaseIndex, std::shared_ptr<indexing::BaseIndex>>(m, "NativeIndex")
+      .def("locations_of", &indexing::BaseIndex::LocationsOf, rel)
+      .def("range_of", &indexing::BaseIndex::RangeOf, rel)
+      .def("schema", &indexing::BaseIndex::GetSchema)
+      .def("size", &indexing::BaseIndex::Size)
+      .def("persistent_rows", [](const indexing::BaseIndex &i) {
+        auto *s = dynamic_cast<const indexing::SortedIndex *>(&i);
+        return s ? s->BuiltRows() : int64_t(0);
+      });
+  m.def("build_index", &indexing::BuildIndex, py::arg("table"), py::arg("col"), py::arg("schema"), rel);
+  m.def("index_from_column", [](std::shared_ptr<CylonContext> ctx, const Column &c, indexing::IndexingSchema schema) {
+    return indexing::BuildIndex(Table::Make(ctx, {c}), 0, schema);
+  }, rel);
+  m.def("table_set_index", [](const TablePtr &t, std::shared_ptr<indexing::BaseIndex> i) { t->SetIndex(i); }, rel);
+  m.def("table_get_index", [](const TablePtr &t) { return t->GetIndex(); }, rel);
+  m.def("table_reset_index", [](const TablePtr &t) { t->ResetIndex(); }, rel);
+  m.def("loc", [](const TablePtr &t, const Column &values, const std::vector<int> &cols, indexing::IndexingSchema s) {
+    return indexing::LocIndexer(s).Loc(t, values, cols);
+  }, rel);
+  m.def("loc_range", [](const TablePtr &t, const Column &start, const Column &end, const std::vector<int> &cols,
+                        indexing::IndexingSchema s) { return indexing::LocIndexer(s).LocRange(t, start, end, cols); },
+        rel);
+  m.def("iloc", [](const TablePtr &t, at::Tensor pos, const std::vector<int> &cols) {
+    return indexing::ILocIndexer().ILoc(t, pos, cols);
+  }, rel);
 
   // ---- C25 native CSV I/O
   m.def(

@@ -18,6 +18,10 @@
 
 namespace cylon {
 
+namespace indexing {
+class BaseIndex;
+}
+
 class Table;
 using TablePtr = std::shared_ptr<Table>;
 
@@ -49,9 +53,16 @@ class Table {
   int64_t nbytes() const;
   TablePtr to(at::Device dev) const;
 
+  // C27: the table's index (reference table.cpp:1001-1055 Set_Index / GetIndex / ResetIndex);
+  // none = the implicit range index 0..rows-1
+  void SetIndex(std::shared_ptr<indexing::BaseIndex> index) { index_ = std::move(index); }
+  const std::shared_ptr<indexing::BaseIndex> &GetIndex() const { return index_; }
+  void ResetIndex() { index_.reset(); }
+
  private:
   std::shared_ptr<CylonContext> ctx_;
   std::vector<Column> columns_;
+  std::shared_ptr<indexing::BaseIndex> index_;
   int64_t rows_ = 0;
   bool retain_ = true;
 };

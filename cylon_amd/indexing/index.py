@@ -2,10 +2,11 @@
 indexer.hpp:76-260, python/pycylon/indexing/index.pyx, python/pycylon/index.py).
 
 Index values live on the table's device as a tensor (numeric) or as an Arrow
-array (strings).  Label lookups (Linear and Hash schemas) run natively: one
-device hash join of the label column against the index column plus a
-(label, row) ordering (C.index_lookup, cylon/ops/index.cpp); Range indexes are
-arithmetic.  Range-of-values `loc` selects from the first position of the start
+array (strings).  Hash, BinaryTree and BTree indexes build their native structure
+once (cylon/indexing/index.hpp: sorted order images, plus a device hash table for
+Hash) and every lookup is a probe / binary search per label; Linear keeps the
+reference's per-lookup semantics (one device join of the labels against the
+column, C.index_lookup); Range indexes are arithmetic.  Range-of-values `loc` selects from the first position of the start
 value to the last position of the end value, as the reference's LocIndexer does.
 """
 from enum import IntEnum
@@ -41,7 +42,7 @@ class BaseIndex:
     def __init__(self, values, device: str = "cpu"):
         if isinstance(values, (pa.Array, pa.ChunkedArray)):
             arr = values.combine_chunks() if isinstance(values, pa.ChunkedArray) else values
-            if pa.types.is_integer(arr.type) or pa.types.is_floating(arr.type):
+            if (pa.types.is_integer(arr.type) or pa.types.is_floating(arr.type)) and arr.null_count == 0:
                 self._values = torch.from_numpy(arr.to_numpy(zero_copy_only=False).copy()).to(device)
                 self._arrow = None
             else:
@@ -97,6 +98,10 @@ class BaseIndex:
     def positions_of(self, value) -> torch.Tensor:
         return self.positions_of_list([value])
 
+    def _persistent(self):
+        """The native index structure (hash / sorted schemas), built once per index."""
+        return None
+
     def positions_of_list(self, values: Sequence) -> torch.Tensor:
         values = list(values)
         if not values or len(self) == 0:
@@ -106,6 +111,9 @@ class BaseIndex:
         except (pa.ArrowInvalid, pa.ArrowTypeError, TypeError, OverflowError):
             return self._positions_slow(values)
         col = ab.column_from_arrow("l", labels, self.device)
+        nidx = self._persistent()
+        if nidx is not None:
+            return nidx.locations_of(col).cpu()
         return C.index_lookup(_native_ctx(self.device), self._native_column(), col).cpu()
 
     def _positions_slow(self, values) -> torch.Tensor:
@@ -125,10 +133,37 @@ class LinearIndex(BaseIndex):
     schema = IndexingSchema.LINEAR
 
 
-class HashIndex(BaseIndex):
-    """Hash schema: same native lookup (the device hash table is built per lookup on the
-    smaller side, which for label lookups is the label list)."""
+class _PersistentIndex(BaseIndex):
+    """An index whose native structure (cylon/indexing/index.hpp) is built once, at
+    construction (``set_index``), and reused by every lookup: Hash = sorted order images
+    + an open-addressing table of the distinct values (one probe per label);
+    BinaryTree / BTree = the sorted images (binary search per label).  String indexes
+    fall back to the per-lookup join inside the native index."""
+
+    def __init__(self, values, device: str = "cpu"):
+        super().__init__(values, device)
+        self._nidx = C.index_from_column(_native_ctx(self.device), self._native_column(),
+                                         getattr(C.IndexingSchema, self.schema.name))
+
+    def _persistent(self):
+        return self._nidx
+
+    @property
+    def persistent_rows(self) -> int:
+        """Rows held by the built structure (0 when the column type uses the join fallback)."""
+        return self._nidx.persistent_rows()
+
+
+class HashIndex(_PersistentIndex):
     schema = IndexingSchema.HASH
+
+
+class BinaryTreeIndex(_PersistentIndex):
+    schema = IndexingSchema.BINARYTREE
+
+
+class BTreeIndex(_PersistentIndex):
+    schema = IndexingSchema.BTREE
 
 
 class RangeIndex(BaseIndex):
@@ -173,7 +208,11 @@ def build_index(values, schema: IndexingSchema, device: str = "cpu") -> BaseInde
         return RangeIndex.of_length(len(values), device)
     if schema == IndexingSchema.HASH:
         return HashIndex(values, device)
-    if schema in (IndexingSchema.LINEAR, IndexingSchema.BINARYTREE, IndexingSchema.BTREE):
+    if schema == IndexingSchema.BINARYTREE:
+        return BinaryTreeIndex(values, device)
+    if schema == IndexingSchema.BTREE:
+        return BTreeIndex(values, device)
+    if schema == IndexingSchema.LINEAR:
         return LinearIndex(values, device)
     raise ValueError(f"unsupported indexing schema {schema}")
 

@@ -6,6 +6,7 @@ import numpy as np
 import pandas as pd
 import pyarrow as pa
 import pyarrow.csv as pacsv
+import torch
 import pytest
 
 from cylon_amd import CylonEnv, DataFrame, GlooConfig, IndexingSchema, Table
@@ -131,3 +132,63 @@ def test_reference_indexer_entry_points(ctx):
     assert ILocIndexer(t).loc_with_single_column(slice(0, 2), 0).to_pydict() == {"a": [10, 20]}
     assert PyLocIndexer(t, "iloc")[1:3, ["a"]].to_pydict() == {"a": [20, 30]}
     assert PyLocIndexer(t, "loc")[2, "c"].to_pydict() == {"c": ["y"]}
+
+
+# ---- persistent native indexes (cylon/indexing/index.hpp) -----------------------
+
+
+
+def _loc_oracle(vals, labels):
+    return [i for l in labels for i, v in enumerate(vals) if v == l]
+
+
+@pytest.mark.parametrize("schema", ["HASH", "BINARYTREE", "BTREE", "LINEAR"])
+@pytest.mark.parametrize("kind", ["int64", "int32", "float64", "nullable"])
+def test_persistent_index_lookups(ctx, schema, kind):
+    """Built once, then probed: label order then row order, duplicates, misses, nulls never match."""
+    from cylon_amd._lib import C
+    from cylon_amd.indexing import IndexingSchema, build_index
+    rng = np.random.default_rng(3)
+    vals = rng.integers(-50, 50, 3000)
+    if kind == "float64":
+        arr = pa.array(vals.astype(np.float64) / 4)
+    elif kind == "int32":
+        arr = pa.array(vals.astype(np.int32))
+    elif kind == "nullable":
+        arr = pa.array(vals, mask=rng.random(3000) < 0.1)
+    else:
+        arr = pa.array(vals)
+    C.trace_enable(True)
+    C.trace_reset()
+    idx = build_index(arr, IndexingSchema[schema], ctx.device)
+    pyvals = arr.to_pylist()
+    labels = [pyvals[5], 1000, pyvals[17], pyvals[5]]
+    for _ in range(3):  # repeated lookups reuse the built structure
+        got = idx.positions_of_list(labels).tolist()
+    assert got == _loc_oracle(pyvals, labels)
+    built = dict(C.trace_counters()).get("index.built_rows", 0)
+    if schema != "LINEAR":
+        assert idx.persistent_rows == sum(v is not None for v in pyvals)
+        assert built == idx.persistent_rows  # one build, not one per lookup
+    C.trace_enable(False)
+
+
+def test_native_loc_indexer_and_set_index(ctx):
+    """C++ LocIndexer / ILocIndexer over a table whose index was set once (Set_Index)."""
+    from cylon_amd._lib import C
+    from cylon_amd.data import arrow_bridge as ab
+    t = Table(pa.table({"k": [5, 3, 9, 3, 7, 1], "v": [0.5, 0.3, 0.9, 0.35, 0.7, 0.1]}), ctx)
+    nidx = C.build_index(t.native, 0, C.IndexingSchema.HASH)
+    C.table_set_index(t.native, nidx)
+    assert C.table_get_index(t.native) is not None
+    lab = ab.column_from_arrow("l", pa.array([3, 7]), ctx.device)
+    out = Table(None, ctx, _native=C.loc(t.native, lab, [1], C.IndexingSchema.HASH)).to_pydict()
+    assert out == {"v": [0.3, 0.35, 0.7]}
+    s = ab.column_from_arrow("s", pa.array([3]), ctx.device)
+    e = ab.column_from_arrow("e", pa.array([7]), ctx.device)
+    rng = Table(None, ctx, _native=C.loc_range(t.native, s, e, [], C.IndexingSchema.HASH)).to_pydict()
+    assert rng["k"] == [3, 9, 3, 7]
+    il = Table(None, ctx, _native=C.iloc(t.native, torch.tensor([5, 0]), [0])).to_pydict()
+    assert il == {"k": [1, 5]}
+    C.table_reset_index(t.native)
+    assert C.table_get_index(t.native) is None

@@ -304,3 +304,21 @@ def test_range_join_matches_cpu(gpu_ctx, ctx, monkeypatch, shape):
     assert np.all(np.diff(g["l_k"].to_numpy().astype(np.int64)) >= 0)
     key = lambda df: sorted(map(tuple, df[sorted(df.columns)].fillna(-1).to_numpy().tolist()))
     assert key(g) == key(c)
+
+
+@pytest.mark.parametrize("schema", ["HASH", "BTREE"])
+def test_persistent_index_on_device(schema):
+    """Device-built persistent index (sorted images + device hash table) vs a numpy oracle."""
+    import pyarrow as pa
+    from cylon_amd.indexing import IndexingSchema, build_index
+    rng = np.random.default_rng(8)
+    n = 1_000_000
+    vals = rng.integers(0, 200_000, n)
+    idx = build_index(pa.array(vals), IndexingSchema[schema], "cuda:0")
+    labels = rng.integers(0, 210_000, 500).tolist()
+    got = idx.positions_of_list(labels).numpy()
+    order = np.argsort(vals, kind="stable")
+    sv = vals[order]
+    exp = np.concatenate([order[np.searchsorted(sv, l, "left"):np.searchsorted(sv, l, "right")] for l in labels])
+    assert np.array_equal(got, exp)
+    assert idx.persistent_rows == n
