@@ -115,6 +115,11 @@ PYBIND11_MODULE(_C, m) {
       .def_property("unit", [](const DataType &d) { return static_cast<int>(d.unit); },
                     [](DataType &d, int u) { d.unit = static_cast<TimeUnit>(u); })
       .def_readwrite("timezone", &DataType::timezone)
+      .def_readwrite("value_type", &DataType::value_type)
+      .def_readwrite("list_size", &DataType::list_size)
+      .def("value_width", &DataType::value_width)
+      .def_static("list_of", &DataType::List)
+      .def_static("fixed_size_list_of", &DataType::FixedSizeList)
       .def("width", &DataType::width, py::call_guard<py::gil_scoped_release>())
       .def("layout", &DataType::layout, py::call_guard<py::gil_scoped_release>())
       .def("is_numeric", &DataType::is_numeric, py::call_guard<py::gil_scoped_release>())

@@ -47,6 +47,8 @@ const char *TypeName(Type t) {
 std::string DataType::ToString() const {
   std::string s = TypeName(type);
   if (type == Type::FIXED_SIZE_BINARY || type == Type::DECIMAL) s += "[" + std::to_string(byte_width) + "]";
+  if (type == Type::LIST) s += "<" + std::string(TypeName(value_type)) + ">";
+  if (type == Type::FIXED_SIZE_LIST) s += "<" + std::string(TypeName(value_type)) + ", " + std::to_string(list_size) + ">";
   return s;
 }
 
@@ -76,7 +78,9 @@ at::ScalarType storage_dtype(const DataType &t) {
     case Type::FIXED_SIZE_BINARY:
     case Type::DECIMAL:
     case Type::STRING:
-    case Type::BINARY: return at::kByte;
+    case Type::BINARY:
+    case Type::LIST:
+    case Type::FIXED_SIZE_LIST: return at::kByte;
     default: CYLON_THROW(Code::NotImplemented, "no storage for type " << t.ToString());
   }
 }

@@ -42,11 +42,21 @@ static at::Tensor nulls_last(const Exec &ex, const Column &c, const at::Tensor &
   return at::cat({perm.index_select(0, valid_pos), perm.index_select(0, null_pos)});
 }
 
+static at::Tensor refine_by_column(const Exec &ex, const Column &c, at::Tensor perm, bool asc);
+
+// fixed-size binary / decimal / fixed-size list: byte-wise order, through the
+// variable-width path over synthetic offsets i * width
+static at::Tensor refine_fixed_bytes(const Exec &ex, const Column &c, at::Tensor perm, bool asc) {
+  const int64_t w = c.type.width();
+  at::Tensor offs = at::arange(0, (c.length + 1) * w, w, ex.opts(at::kLong));
+  Column v(c.name, DataType(Type::BINARY), c.length, c.data, offs, c.validity);
+  return refine_by_column(ex, v, std::move(perm), asc);
+}
+
 static at::Tensor refine_by_column(const Exec &ex, const Column &c, at::Tensor perm, bool asc) {
   const int64_t n = perm.numel();
+  if (!c.is_var() && c.type.kind() == ValueKind::FIXED_BYTES) return refine_fixed_bytes(ex, c, std::move(perm), asc);
   if (!c.is_var()) {
-    CYLON_CHECK(c.type.kind() != ValueKind::FIXED_BYTES, Code::NotImplemented,
-                "sorting fixed-size binary columns is not supported");
     at::Tensor keys = ex.empty_i64(n);
     KCALL(ex, sort_keys_from_column, c.view(), ptr<int64_t>(perm), n, !asc,
           reinterpret_cast<uint64_t *>(ptr<int64_t>(keys)));

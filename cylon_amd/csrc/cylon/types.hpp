@@ -5,6 +5,12 @@
 // meaning.  Physical storage is device-resident and Arrow-like:
 //   * fixed width  -> one contiguous buffer of n * byte_width bytes
 //   * STRING/BINARY -> int64 offsets[n+1] + uint8 bytes   (always 64-bit offsets)
+//   * LIST<numeric> -> the same var-width layout: int64 BYTE offsets[n+1] + the child
+//                      values' bytes (Arrow's element offsets x element width), so every
+//                      gather / shuffle / join materialisation path moves lists as it
+//                      moves binary values (reference: arrow_types.cpp:83-111 accepts
+//                      list<numeric>, copy_arrray.cpp:113-139,222-281 gathers it)
+//   * FIXED_SIZE_LIST<numeric, k> -> fixed width k x element width bytes per row
 //   * validity      -> optional uint8 byte-mask (1 = valid)
 // Byte masks instead of bit-packed validity keep the scatter/gather kernels
 // free of read-modify-write bit updates; Arrow bitmaps are produced at the
@@ -61,12 +67,35 @@ struct DataType {
   int32_t byte_width = 0;  // only used by FIXED_SIZE_BINARY / DECIMAL
   TimeUnit unit = TimeUnit::MILLI;
   std::string timezone;
+  Type value_type = Type::INT64;  // LIST / FIXED_SIZE_LIST element type (numeric)
+  int32_t list_size = 0;          // FIXED_SIZE_LIST elements per row
 
   DataType() = default;
   explicit DataType(Type t) : type(t) {}
   DataType(Type t, int32_t bw) : type(t), byte_width(bw) {}
 
   static DataType FixedSizeBinary(int32_t w) { return DataType(Type::FIXED_SIZE_BINARY, w); }
+  static DataType List(Type elem) {
+    DataType d(Type::LIST);
+    d.value_type = elem;
+    d.check_list();
+    return d;
+  }
+  static DataType FixedSizeList(Type elem, int32_t size) {
+    DataType d(Type::FIXED_SIZE_LIST);
+    d.value_type = elem;
+    d.list_size = size;
+    d.check_list();
+    return d;
+  }
+  bool is_list() const { return type == Type::LIST || type == Type::FIXED_SIZE_LIST; }
+  // element width of a list type (numeric elements only)
+  int32_t value_width() const { return DataType(value_type).width(); }
+  void check_list() const {
+    CYLON_CHECK(DataType(value_type).is_numeric(), Code::NotImplemented,
+                "list columns support numeric elements only, not type " << static_cast<int>(value_type));
+    CYLON_CHECK(type != Type::FIXED_SIZE_LIST || list_size >= 0, Code::Invalid, "negative list size");
+  }
   static DataType Timestamp(TimeUnit u, std::string tz = "") {
     DataType d(Type::TIMESTAMP);
     d.unit = u;
@@ -75,13 +104,13 @@ struct DataType {
   }
 
   bool operator==(const DataType &o) const {
-    return type == o.type && width() == o.width() && unit == o.unit;
+    return type == o.type && width() == o.width() && unit == o.unit && (!is_list() || value_type == o.value_type);
   }
   bool operator!=(const DataType &o) const { return !(*this == o); }
 
   Layout layout() const { return is_variable_width() ? Layout::VARIABLE_WIDTH : Layout::FIXED_WIDTH; }
 
-  bool is_variable_width() const { return type == Type::STRING || type == Type::BINARY; }
+  bool is_variable_width() const { return type == Type::STRING || type == Type::BINARY || type == Type::LIST; }
 
   // physical bytes per element for fixed width types; 0 for var width
   int32_t width() const {
@@ -106,8 +135,10 @@ struct DataType {
       case Type::DURATION: return 8;
       case Type::FIXED_SIZE_BINARY:
       case Type::DECIMAL: return byte_width;
+      case Type::FIXED_SIZE_LIST: return list_size * value_width();
       case Type::STRING:
-      case Type::BINARY: return 0;
+      case Type::BINARY:
+      case Type::LIST: return 0;
       default: CYLON_THROW(Code::NotImplemented, "type " << static_cast<int>(type) << " is not supported");
     }
   }
@@ -133,9 +164,11 @@ struct DataType {
       case Type::FLOAT:
       case Type::DOUBLE: return ValueKind::FLOAT;
       case Type::FIXED_SIZE_BINARY:
-      case Type::DECIMAL: return ValueKind::FIXED_BYTES;
+      case Type::DECIMAL:
+      case Type::FIXED_SIZE_LIST: return ValueKind::FIXED_BYTES;
       case Type::STRING:
-      case Type::BINARY: return ValueKind::VAR_BYTES;
+      case Type::BINARY:
+      case Type::LIST: return ValueKind::VAR_BYTES;
       default: CYLON_THROW(Code::NotImplemented, "type " << static_cast<int>(type) << " is not supported");
     }
   }

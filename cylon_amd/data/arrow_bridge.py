@@ -67,6 +67,13 @@ def to_cylon_type(at: pa.DataType) -> "C.DataType":
         return d
     if pa.types.is_dictionary(at):
         return to_cylon_type(at.value_type)
+    if pa.types.is_list(at) or pa.types.is_large_list(at) or pa.types.is_fixed_size_list(at):
+        vt = at.value_type
+        if vt not in _SIMPLE or vt == pa.bool_() or not (pa.types.is_integer(vt) or pa.types.is_floating(vt)):
+            raise TypeError(f"arrow type {at} is not supported by cylon_amd (list elements must be numeric)")
+        if pa.types.is_fixed_size_list(at):
+            return C.DataType.fixed_size_list_of(_SIMPLE[vt], at.list_size)
+        return C.DataType.list_of(_SIMPLE[vt])
     raise TypeError(f"arrow type {at} is not supported by cylon_amd")
 
 
@@ -91,6 +98,10 @@ def to_arrow_type(dt: "C.DataType") -> pa.DataType:
         return pa.time64(_UNIT_INV[dt.unit])
     if t == T.DURATION:
         return pa.duration(_UNIT_INV[dt.unit])
+    if t == T.LIST:
+        return pa.list_(inv[dt.value_type])
+    if t == T.FIXED_SIZE_LIST:
+        return pa.list_(inv[dt.value_type], dt.list_size)
     raise TypeError(f"cylon type {dt} has no arrow mapping")
 
 
@@ -132,6 +143,30 @@ def column_from_arrow(name: str, arr, device: str) -> "C.Column":
             np.zeros(0, np.uint8)
         offsets = offsets - base
         return C.Column(name, dt, n, _to_dev(data, device), _to_dev(offsets, device), validity)
+    if t in (T.LIST, T.FIXED_SIZE_LIST):  # numeric lists: child values' bytes (+ byte offsets)
+        w = dt.value_width()
+        npt = _NP[dt.value_type]
+        if t == T.FIXED_SIZE_LIST:
+            k = dt.list_size
+            child = arr.values.slice(off * k, n * k)
+        else:
+            eoffs = np.asarray(arr.offsets).astype(np.int64) if n else np.zeros(1, np.int64)
+            child = arr.values.slice(int(eoffs[0]), int(eoffs[-1] - eoffs[0]))
+        if child.null_count:  # element nulls are only allowed under null rows (their values are unused)
+            cvalid = np.asarray(child.is_valid())
+            row_of = np.arange(len(child)) // k if t == T.FIXED_SIZE_LIST else \
+                np.searchsorted(eoffs - eoffs[0], np.arange(len(child)), side="right") - 1
+            rvalid = np.asarray(arr.is_valid())
+            if np.any(~cvalid & rvalid[row_of]):
+                raise NotImplementedError(f"column {name}: null list elements are not supported")
+            child = child.fill_null(0)
+        cb = child.buffers()
+        vals = np.frombuffer(cb[1], dtype=npt)[child.offset:child.offset + len(child)] if len(child) else \
+            np.zeros(0, npt)
+        data = vals.view(np.uint8)
+        if t == T.FIXED_SIZE_LIST:
+            return C.Column(name, dt, n, _to_dev(data, device), None, validity)
+        return C.Column(name, dt, n, _to_dev(data, device), _to_dev((eoffs - eoffs[0]) * w, device), validity)
     if t == T.BOOL:
         data = _unpack_bits(bufs[1], off, n) if n else np.zeros(0, np.uint8)
         return C.Column(name, dt, n, _to_dev(data, device), None, validity)
@@ -167,6 +202,20 @@ def column_to_arrow(col: "C.Column") -> pa.Array:
             obuf = pa.py_buffer(offsets.astype(np.int32))
         dbuf = pa.py_buffer(data.numpy().tobytes())
         return pa.Array.from_buffers(at, n, [vbuf, obuf, dbuf], null_count=null_count)
+    if t in (T.LIST, T.FIXED_SIZE_LIST):
+        et = to_arrow_type(C.DataType(dt.value_type))
+        w = dt.value_width()
+        raw = data.numpy().tobytes()
+        child = pa.Array.from_buffers(et, len(raw) // w, [None, pa.py_buffer(raw)])
+        if t == T.FIXED_SIZE_LIST:
+            return pa.Array.from_buffers(at, n, [vbuf], null_count=null_count, children=[child])
+        eoffs = col.offsets.cpu().numpy() // w
+        if len(child) >= 2 ** 31 - 1:
+            at = pa.large_list(et)
+            obuf = pa.py_buffer(eoffs.astype(np.int64))
+        else:
+            obuf = pa.py_buffer(eoffs.astype(np.int32))
+        return pa.Array.from_buffers(at, n, [vbuf, obuf], null_count=null_count, children=[child])
     if t == T.BOOL:
         bits = np.packbits(data.numpy().astype(np.uint8) != 0, bitorder="little")
         return pa.Array.from_buffers(at, n, [vbuf, pa.py_buffer(bits)], null_count=null_count)
