@@ -1,6 +1,9 @@
 // Native Arrow C++ bridge and Parquet I/O (see arrow_io.hpp).
 #include "arrow_io.hpp"
 
+#include <algorithm>
+#include <functional>
+
 #include <arrow/api.h>
 #include <arrow/io/file.h>
 #include <parquet/arrow/reader.h>
@@ -87,6 +90,13 @@ DataType to_cylon(const arrow::DataType &t) {
       d.unit = unit_of(static_cast<const arrow::DurationType &>(t).unit());
       return d;
     }
+    case Type::LIST:
+    case Type::LARGE_LIST:
+      return DataType::List(to_cylon(*static_cast<const arrow::BaseListType &>(t).value_type()).type);
+    case Type::FIXED_SIZE_LIST: {
+      const auto &fl = static_cast<const arrow::FixedSizeListType &>(t);
+      return DataType::FixedSizeList(to_cylon(*fl.value_type()).type, fl.list_size());
+    }
     default: CYLON_THROW(Code::NotImplemented, "arrow type " << t.ToString() << " is not supported");
   }
 }
@@ -115,6 +125,10 @@ std::shared_ptr<arrow::DataType> to_arrow(const DataType &t, bool large_var) {
     case cylon::Type::TIME64: return arrow::time64(arrow_unit(t.unit));
     case cylon::Type::DURATION: return arrow::duration(arrow_unit(t.unit));
     case cylon::Type::DECIMAL: return arrow::decimal128(38, 0);
+    case cylon::Type::LIST:
+      return large_var ? arrow::large_list(to_arrow(DataType(t.value_type), false))
+                       : arrow::list(to_arrow(DataType(t.value_type), false));
+    case cylon::Type::FIXED_SIZE_LIST: return arrow::fixed_size_list(to_arrow(DataType(t.value_type), false), t.list_size);
     default: CYLON_THROW(Code::NotImplemented, "type " << static_cast<int>(t.type) << " has no Arrow mapping");
   }
 }
@@ -131,11 +145,51 @@ at::Tensor validity_bytes(const arrow::ArrayData &d) {
   return v;
 }
 
+// element nulls are only representable under null rows (their bytes are never read)
+void check_list_children(const arrow::ArrayData &d, const arrow::ArrayData &child, int64_t first, int64_t count,
+                         const std::function<int64_t(int64_t)> &row_of, const std::string &name) {
+  if (child.GetNullCount() == 0 || !child.buffers[0]) return;
+  const uint8_t *cb = child.buffers[0]->data();
+  const uint8_t *pb = d.buffers[0] ? d.buffers[0]->data() : nullptr;
+  for (int64_t e = 0; e < count; ++e)
+    if (!arrow::bit_util::GetBit(cb, child.offset + first + e)) {
+      const int64_t r = row_of(e);
+      CYLON_CHECK(pb && !arrow::bit_util::GetBit(pb, d.offset + r), Code::NotImplemented,
+                  "column " << name << ": null list elements are not supported");
+    }
+}
+
+Column list_column_from_array(const std::string &name, const arrow::ArrayData &d, const DataType &t,
+                              at::Tensor valid, const at::Device &dev) {
+  const int64_t n = d.length, w = t.value_width();
+  const arrow::ArrayData &child = *d.child_data[0];
+  if (t.type == cylon::Type::FIXED_SIZE_LIST) {
+    const int64_t k = t.list_size;
+    check_list_children(d, child, d.offset * k, n * k, [k](int64_t e) { return e / k; }, name);
+    at::Tensor bytes = host_bytes(n * k * w);
+    if (n * k) std::memcpy(bytes.data_ptr<uint8_t>(), child.buffers[1]->data() + (child.offset + d.offset * k) * w, n * k * w);
+    return Column(name, t, n, bytes.to(dev), at::Tensor(), valid.defined() ? valid.to(dev) : valid);
+  }
+  const bool large = d.type->id() == arrow::Type::LARGE_LIST;
+  at::Tensor offs = at::empty({n + 1}, at::TensorOptions().dtype(at::kLong));
+  int64_t *o = offs.data_ptr<int64_t>();
+  for (int64_t i = 0; i <= n; ++i) o[i] = large ? d.GetValues<int64_t>(1)[i] : (int64_t)d.GetValues<int32_t>(1)[i];
+  const int64_t first = o[0], last = o[n];
+  check_list_children(d, child, first, last - first, [o, n](int64_t e) {
+    return (int64_t)(std::upper_bound(o, o + n + 1, o[0] + e) - o) - 1;
+  }, name);
+  for (int64_t i = 0; i <= n; ++i) o[i] = (o[i] - first) * w;  // element offsets -> byte offsets
+  at::Tensor bytes = host_bytes((last - first) * w);
+  if (last > first) std::memcpy(bytes.data_ptr<uint8_t>(), child.buffers[1]->data() + (child.offset + first) * w, (last - first) * w);
+  return Column(name, t, n, bytes.to(dev), offs.to(dev), valid.defined() ? valid.to(dev) : valid);
+}
+
 Column column_from_array(const std::string &name, const arrow::Array &arr, const at::Device &dev) {
   const arrow::ArrayData &d = *arr.data();
   const DataType t = to_cylon(*arr.type());
   const int64_t n = d.length;
   at::Tensor valid = validity_bytes(d);
+  if (t.is_list()) return list_column_from_array(name, d, t, valid, dev);
   if (t.is_variable_width()) {
     const bool large = arr.type_id() == arrow::Type::LARGE_STRING || arr.type_id() == arrow::Type::LARGE_BINARY;
     at::Tensor offs = at::empty({n + 1}, at::TensorOptions().dtype(at::kLong));
@@ -196,6 +250,23 @@ std::shared_ptr<arrow::Array> array_from_column(const Column &col) {
     at::Tensor v = col.validity.to(at::kCPU).contiguous();
     validity = pack_bits(v.data_ptr<uint8_t>(), n, &nulls);
     if (nulls == 0) validity = nullptr;
+  }
+  if (col.type.is_list()) {  // child values (numeric) + element offsets / fixed rows
+    const int64_t w = col.type.value_width();
+    auto elem = to_arrow(DataType(col.type.value_type), false);
+    at::Tensor bytes = col.data.to(at::kCPU).contiguous();
+    if (col.type.type == cylon::Type::FIXED_SIZE_LIST) {
+      const int64_t k = col.type.list_size;
+      auto child = arrow::ArrayData::Make(elem, n * k, {nullptr, to_buffer(bytes.slice(0, 0, n * k * w).contiguous())}, 0);
+      return arrow::MakeArray(arrow::ArrayData::Make(to_arrow(col.type, false), n, {validity}, {child}, nulls));
+    }
+    at::Tensor o = col.offsets.to(at::kCPU).contiguous();
+    const int64_t base = o[0].item<int64_t>(), total = o[n].item<int64_t>() - base;
+    const bool large = total / w > (int64_t)INT32_MAX;
+    at::Tensor eo = (o - base) / w;
+    std::shared_ptr<arrow::Buffer> obuf = large ? to_buffer(eo.contiguous()) : to_buffer(eo.to(at::kInt).contiguous());
+    auto child = arrow::ArrayData::Make(elem, total / w, {nullptr, to_buffer(bytes.slice(0, base, base + total).contiguous())}, 0);
+    return arrow::MakeArray(arrow::ArrayData::Make(to_arrow(col.type, large), n, {validity, obuf}, {child}, nulls));
   }
   if (col.is_var()) {
     at::Tensor o = col.offsets.to(at::kCPU).contiguous();

@@ -121,3 +121,20 @@ def test_list_columns_distributed_join_on_device():
     b = pa.concat_tables([r[2] for r in res])
     assert _rows(got.select(["l_k", "l_l", "l_f", "r_k", "r_w"])) == _oracle_join(a, b, "inner", ["k", "l", "f"],
                                                                                  ["k", "w"])
+
+
+def test_list_columns_native_parquet_roundtrip(ctx, tmp_path):
+    """The C++ Parquet writer / reader (io/arrow_io.cpp) map list and fixed-size-list columns.
+    (Fixed-size lists without null rows: Arrow's own Parquet round trip of a null fixed-size
+    list row fails, pyarrow 25 included.)"""
+    import pyarrow.parquet as pq
+    from cylon_amd.io import read_parquet, write_parquet
+    rng = np.random.default_rng(9)
+    f = pa.array([list(map(float, v)) for v in rng.standard_normal((80, 3))], pa.list_(pa.float64(), 3))
+    t = pa.table({"k": pa.array(rng.integers(0, 9, 80)), "l": _lists(rng, 80), "f": f})
+    p = tmp_path / "lists.parquet"
+    write_parquet(Table(t, ctx), str(p))
+    assert pq.read_table(p).column("l").to_pylist() == t.column("l").to_pylist()
+    back = read_parquet(ctx, str(p)).to_arrow()
+    assert back.column("l").to_pylist() == t.column("l").to_pylist()
+    assert back.column("f").to_pylist() == t.column("f").to_pylist()
