@@ -10,9 +10,11 @@
 #include "cylon/io/arrow_io.hpp"
 #include "cylon/io/csv.hpp"
 #include "cylon/indexing/index.hpp"
+#include "cylon/io/device_interop.hpp"
 #include "cylon/ops/api_ext.hpp"
 #include "cylon/ops/graph.hpp"
 #include "cylon/ops/relational.hpp"
+#include "cylon/ops/util.hpp"
 #include "cylon/table.hpp"
 
 namespace py = pybind11;
@@ -35,6 +37,54 @@ void register_extended_ops(py::module &m) {
   auto rel = py::call_guard<py::gil_scoped_release>();
 
   m.def("index_lookup", &ops::IndexLookup, py::arg("ctx"), py::arg("index"), py::arg("labels"), rel);
+
+  // ---- validity bitmaps <-> byte masks at the Arrow boundary (bitmap.hip)
+  m.def("pack_validity", [](at::Tensor bytes) {
+    ops::Exec ex(bytes.device());
+    bytes = bytes.contiguous().to(at::kByte);
+    const int64_t n = bytes.numel();
+    at::Tensor words = at::empty({std::max<int64_t>((n + 63) / 64, 1)}, ex.opts(at::kLong));
+    at::Tensor nulls = at::zeros({1}, ex.opts(at::kLong));
+    KCALL(ex, pack_validity, bytes.data_ptr<uint8_t>(), n, reinterpret_cast<uint64_t *>(words.data_ptr<int64_t>()),
+          nulls.data_ptr<int64_t>());
+    return std::make_pair(words.slice(0, 0, (n + 63) / 64), nulls.item<int64_t>());
+  }, py::call_guard<py::gil_scoped_release>());
+  m.def("unpack_validity", [](at::Tensor bits, int64_t bit_offset, int64_t n) {
+    ops::Exec ex(bits.device());
+    bits = bits.contiguous();
+    at::Tensor out = at::empty({n}, ex.opts(at::kByte));
+    if (n) KCALL(ex, unpack_validity, reinterpret_cast<const uint8_t *>(bits.data_ptr()), bit_offset, n,
+                 out.data_ptr<uint8_t>());
+    return out;
+  }, py::call_guard<py::gil_scoped_release>());
+
+  // ---- Arrow C Device Data Interface (PyCapsules "arrow_schema" / "arrow_device_array")
+  m.def("export_device_table", [](const TablePtr &t) {
+    auto *sch = new ArrowSchema();
+    auto *arr = new ArrowDeviceArray();
+    {
+      py::gil_scoped_release nogil;
+      io::ExportDeviceTable(t, sch, arr);
+    }
+    PyObject *cs = PyCapsule_New(sch, "arrow_schema", [](PyObject *o) {
+      auto *p = static_cast<ArrowSchema *>(PyCapsule_GetPointer(o, "arrow_schema"));
+      if (p && p->release) p->release(p);
+      delete p;
+    });
+    PyObject *ca = PyCapsule_New(arr, "arrow_device_array", [](PyObject *o) {
+      auto *p = static_cast<ArrowDeviceArray *>(PyCapsule_GetPointer(o, "arrow_device_array"));
+      if (p && p->array.release) p->array.release(&p->array);
+      delete p;
+    });
+    return py::make_tuple(py::reinterpret_steal<py::object>(cs), py::reinterpret_steal<py::object>(ca));
+  });
+  m.def("import_device_table", [](std::shared_ptr<CylonContext> ctx, py::object schema, py::object array) {
+    auto *sch = static_cast<ArrowSchema *>(PyCapsule_GetPointer(schema.ptr(), "arrow_schema"));
+    auto *arr = static_cast<ArrowDeviceArray *>(PyCapsule_GetPointer(array.ptr(), "arrow_device_array"));
+    CYLON_CHECK(sch && arr, Code::Invalid, "expected 'arrow_schema' and 'arrow_device_array' capsules");
+    py::gil_scoped_release nogil;
+    return io::ImportDeviceTable(ctx, sch, arr);  // moves the structs (the capsules then only free them)
+  });
 
   // ---- C27 persistent indexes + loc / iloc indexers (cylon/indexing/index.hpp)
   py::enum_<indexing::IndexingSchema>(m, "IndexingSchema")

@@ -263,7 +263,7 @@ std::shared_ptr<arrow::Array> array_from_column(const Column &col) {
     at::Tensor o = col.offsets.to(at::kCPU).contiguous();
     const int64_t base = o[0].item<int64_t>(), total = o[n].item<int64_t>() - base;
     const bool large = total / w > (int64_t)INT32_MAX;
-    at::Tensor eo = (o - base) / w;
+    at::Tensor eo = (o - base).div(w, "trunc");
     std::shared_ptr<arrow::Buffer> obuf = large ? to_buffer(eo.contiguous()) : to_buffer(eo.to(at::kInt).contiguous());
     auto child = arrow::ArrayData::Make(elem, total / w, {nullptr, to_buffer(bytes.slice(0, base, base + total).contiguous())}, 0);
     return arrow::MakeArray(arrow::ArrayData::Make(to_arrow(col.type, large), n, {validity, obuf}, {child}, nulls));

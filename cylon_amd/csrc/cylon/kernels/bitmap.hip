@@ -1,0 +1,56 @@
+// Arrow validity bitmaps <-> the engine's byte masks (the Arrow boundary: import,
+// export, C Device Data interface).  Reference: util/copy_arrray.cpp:24-110 builds
+// bitmaps row by row on the host.  Here a wave64 ballot IS one LSB-first bitmap
+// word: pack is one coalesced byte load and one 8-byte store per 64 rows; unpack is
+// one byte store per row.
+#include "device_common.hpp"
+
+namespace cylon {
+namespace hip {
+
+__global__ void k_pack_validity(const uint8_t *__restrict__ bytes, int64_t n, uint64_t *__restrict__ bitmap,
+                                unsigned long long *__restrict__ nulls) {
+  const int64_t words = (n + 63) / 64;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  const int lane = lane_id();
+  unsigned long long z = 0;
+  for (int64_t w = wave; w < words; w += nwaves) {
+    const int64_t i = w * 64 + lane;
+    const bool v = i < n && bytes[i] != 0;
+    const uint64_t word = __ballot(v);
+    if (lane == 0) {
+      bitmap[w] = word;
+      const int64_t valid_bits = (n - w * 64) < 64 ? (n - w * 64) : 64;
+      z += (unsigned long long)(valid_bits - __popcll(word));
+    }
+  }
+  if (lane == 0 && z) atomicAdd(nulls, z);
+}
+
+void pack_validity(const uint8_t *bytes, int64_t n, uint64_t *bitmap, int64_t *nulls, void *stream) {
+  if (n == 0) return;
+  const int64_t words = (n + 63) / 64;
+  hipLaunchKernelGGL(k_pack_validity, dim3(grid_for(words * kWave)), dim3(kBlock), 0, as_stream(stream), bytes, n,
+                     bitmap, reinterpret_cast<unsigned long long *>(nulls));
+  HIP_LAUNCH_CHECK();
+}
+
+__global__ void k_unpack_validity(const uint8_t *__restrict__ bits, int64_t bit_offset, int64_t n,
+                                  uint8_t *__restrict__ bytes) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+    const int64_t b = bit_offset + i;
+    bytes[i] = (bits[b >> 3] >> (b & 7)) & 1;
+  }
+}
+
+void unpack_validity(const uint8_t *bits, int64_t bit_offset, int64_t n, uint8_t *bytes, void *stream) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_unpack_validity, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), bits, bit_offset, n,
+                     bytes);
+  HIP_LAUNCH_CHECK();
+}
+
+}  // namespace hip
+}  // namespace cylon

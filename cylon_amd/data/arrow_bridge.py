@@ -131,7 +131,10 @@ def column_from_arrow(name: str, arr, device: str) -> "C.Column":
     bufs = arr.buffers()
     validity = None
     if arr.null_count > 0 and bufs[0] is not None:
-        validity = _to_dev(_unpack_bits(bufs[0], off, n), device)
+        # the packed bitmap crosses to the device (1/8 of the bytes) and is unpacked there
+        nb = (off + n + 7) // 8
+        bits = _to_dev(np.frombuffer(bufs[0], dtype=np.uint8)[:nb], device)
+        validity = C.unpack_validity(bits, off, n)
     t = dt.type
     if t in (T.STRING, T.BINARY):
         large = pa.types.is_large_string(arr.type) or pa.types.is_large_binary(arr.type)
@@ -186,10 +189,10 @@ def column_to_arrow(col: "C.Column") -> pa.Array:
     vbuf = None
     null_count = 0
     if col.validity is not None and n:
-        v = col.validity.cpu().numpy().astype(np.uint8)
-        null_count = int(n - v.sum())
+        # packed on the device by one ballot per 64 rows; only the bitmap crosses to the host
+        words, null_count = C.pack_validity(col.validity)
         if null_count:
-            vbuf = pa.py_buffer(np.packbits(v, bitorder="little"))
+            vbuf = pa.py_buffer(words.cpu().numpy().tobytes())
     t = dt.type
     data = col.data.cpu()
     if t in (T.STRING, T.BINARY):

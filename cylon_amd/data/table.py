@@ -112,6 +112,26 @@ class Table(PandasOpsMixin):
         cols = [c.to_numpy(zero_copy_only=False) for c in self.to_arrow().columns]
         return np.array(cols).T.copy(order=order) if cols else np.empty((0, 0))
 
+    # ---- Arrow PyCapsule interfaces ---------------------------------------------
+    def __arrow_c_stream__(self, requested_schema=None):
+        """Host Arrow C stream (pyarrow / polars / duckdb consumers)."""
+        return self.to_arrow().__arrow_c_stream__(requested_schema)
+
+    def __arrow_c_device_array__(self, requested_schema=None, **kwargs):
+        """Arrow C Device Data Interface: a struct array whose buffers stay where the table
+        lives (ARROW_DEVICE_ROCM in HBM, zero-copy for values / offsets / list children;
+        bitmaps and packed booleans produced on the device; sync_event = a hipEvent_t)."""
+        if requested_schema is not None:
+            raise NotImplementedError("schema requests are not supported")
+        return C.export_device_table(self._t)
+
+    @staticmethod
+    def from_arrow_device(context: CylonContext, obj) -> "Table":
+        """Zero-copy import of an object exposing __arrow_c_device_array__ (or the capsule pair)."""
+        ctx = _ensure_ctx(context)
+        caps = obj.__arrow_c_device_array__() if hasattr(obj, "__arrow_c_device_array__") else obj
+        return Table(context=ctx, _native=C.import_device_table(ctx._ctx, caps[0], caps[1]))
+
     def to_torch(self) -> Dict[str, torch.Tensor]:
         """Columns as device tensors (zero-copy, fixed width columns only)."""
         out = {}

@@ -28,7 +28,7 @@ from torch.utils.cpp_extension import BuildExtension, CppExtension  # noqa: E402
 ext = CppExtension(
     name="cylon_amd._C",
     sources=_build.binding_sources(),
-    include_dirs=[_build.CSRC, _build.ROCM_INCLUDE],
+    include_dirs=[_build.CSRC, _build.ROCM_INCLUDE, _build._arrow_paths()[0]],
     define_macros=[("__HIP_PLATFORM_AMD__", "1"), ("USE_ROCM", "1")],
     extra_compile_args=["-O3", "-std=c++17", "-Wno-unused-function"],
     extra_objects=[core_lib],

@@ -224,3 +224,62 @@ def test_radix_row_sort_matches_index_sort(gpu_ctx, monkeypatch, dtype, asc):
         monkeypatch.setenv("CYLON_RADIX_SORT_MIN_ROWS", thr)
         res.append(T.sort("k", ascending=asc).to_pandas())
     pd.testing.assert_frame_equal(res[0], res[1])
+
+
+# ---------------------------------------------------------------------------
+# correctness at bench scale, against independent torch computations
+# ---------------------------------------------------------------------------
+def _bench_module():
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("cylon_bench", os.path.join(os.path.dirname(__file__), "..",
+                                                                              "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+@pytest.mark.parametrize("algorithm", ["hash", "sort"])
+def test_join_100m_payload_identities(gpu_ctx, algorithm):
+    """100M x 100M join (the radix / range LDS paths at scale): row count, key sum and both payload
+    sums equal the per-key identities computed independently with torch.bincount (bench.verify_join)."""
+    n = 100_000_000
+    bm = _bench_module()
+    key_range = int(0.99 * n)
+    left = bm.make_relation(gpu_ctx, n, key_range, 3, 11, "cuda:0")
+    right = bm.make_relation(gpu_ctx, n, key_range, 3, 12, "cuda:0")
+    out = left.distributed_join(right, "inner", algorithm, on=[0], left_prefix="l_", right_prefix="r_")
+    v = bm.verify_join(gpu_ctx, left, right, out, key_range)
+    assert v["ok"], v
+    del out
+    torch.cuda.empty_cache()
+
+
+def test_groupby_1b_rows_sums_match_index_add(gpu_ctx):
+    """Config 4 shape (1B rows / 10M groups, the radix group-by): every group sum equals torch index_add."""
+    n, groups = 1_000_000_000, 10_000_000
+    g = torch.Generator(device="cuda").manual_seed(4)
+    keys = torch.randint(0, groups, (n,), generator=g, device="cuda")
+    x = torch.rand(n, generator=g, device="cuda", dtype=torch.float64)
+    t = Table.from_torch(gpu_ctx, {"g": keys, "x": x})
+    res = t.local_groupby("g", {"x": "sum"}).to_torch()
+    ks, sums = list(res.values())[:2]
+    ref = torch.zeros(groups, dtype=torch.float64, device="cuda").index_add_(0, keys, x)
+    assert ks.numel() == int((torch.bincount(keys, minlength=groups) > 0).sum())
+    assert torch.allclose(sums, ref[ks], rtol=1e-9, atol=1e-9)
+    del t, keys, x, res, ref
+    torch.cuda.empty_cache()
+
+
+def test_sort_2b_rows_sorted_permutation(gpu_ctx):
+    """Config 5 shape (2B int64 rows, the row-moving radix sort): output non-decreasing and the
+    same multiset as the input (count, wrapping sum, wrapping sum of squares)."""
+    n = 2_000_000_000
+    g = torch.Generator(device="cuda").manual_seed(5)
+    k = torch.randint(-(1 << 62), 1 << 62, (n,), generator=g, device="cuda")
+    s = Table.from_torch(gpu_ctx, {"k": k}).sort("k").to_torch()["k"]
+    assert s.numel() == n
+    assert bool((s[1:] >= s[:-1]).all())
+    assert int(s.sum()) == int(k.sum()) and int((s * s).sum()) == int((k * k).sum())
+    del s, k
+    torch.cuda.empty_cache()
