@@ -62,7 +62,7 @@ def verify_groupby(t, res, groups):
     keys, sums = cols[0], cols[1]
     if keys.numel() != int(present.sum().item()):
         return False
-    return bool(torch.allclose(sums, ref[keys], rtol=1e-9, atol=1e-9).item())
+    return bool(torch.allclose(sums, ref[keys], rtol=1e-9, atol=1e-9))
 
 
 def emit(**kw):
