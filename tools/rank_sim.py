@@ -15,8 +15,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cylon_amd import CylonContext, Table  # noqa: E402
 from cylon_amd._lib import C  # noqa: E402
 
-rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000_000
-worlds = [int(x) for x in sys.argv[2:]] or [2, 4, 8]
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+SORT = "--sort" in sys.argv  # config 5: distributed sample sort of 2B int64 keys
+rows = int(args[0]) if args else (2_000_000_000 if SORT else 1_000_000_000)
+worlds = [int(x) for x in args[1:]] or [2, 4, 8]
+XGMI_GBPS = 77.0  # per link per direction (MI355X: 7 links x ~153 GB/s bidirectional)
 ctx = CylonContext(device="cuda:0")
 hi = int(0.99 * rows)
 
@@ -40,6 +43,35 @@ def timed(fn, reps=3):
         del r
     return best * 1e3
 
+
+def sort_sim(W):
+    """Per-rank work of DistributedSort on W ranks: images + splitter partition + reorder (the
+    hash pid + partition-major reorder is the proxy: same scatter), the exchange of (W-1)/W of the
+    keys over W-1 links, then the local radix sort of the received rows (~rows/W)."""
+    n = rows // W
+    g = torch.Generator(device="cuda").manual_seed(5)
+    t = Table.from_torch(ctx, {"k": torch.randint(-(1 << 62), 1 << 62, (n,), generator=g, device="cuda")})
+
+    def part():
+        pid, _ = C.map_to_hash_partitions(t.native, [0], W)
+        return C.partition_reorder(t.native, pid, W)
+
+    tp = timed(part)
+    ts = timed(lambda: t.sort("k"))
+    nbytes = n * 8 * (W - 1) / W
+    txfer = nbytes / ((W - 1) * XGMI_GBPS * 1e9) * 1e3
+    est = tp + txfer + ts
+    print(f"SORT W={W} rows/rank={n}: partition {tp:.1f} ms, exchange {nbytes / 1e9:.2f} GB over {W - 1} links "
+          f"~{txfer:.1f} ms, local sort {ts:.1f} ms => estimate {est:.1f} ms ({rows / est / 1e6:.0f} M rows/s/job)",
+          flush=True)
+    del t
+    torch.cuda.empty_cache()
+
+
+if SORT:
+    for W in worlds:
+        sort_sim(W)
+    sys.exit(0)
 
 for W in worlds:
     n = rows // W
