@@ -496,3 +496,14 @@ void widen_u32(const uint32_t *in, int64_t n, int64_t base, int64_t *out, void *
 
 }  // namespace cpu
 }  // namespace cylon
+
+namespace cylon {
+namespace cpu {
+
+void batched_copy(const void *const *src, void *const *dst, const int64_t *bytes, int n, void *) {
+  for (int i = 0; i < n; ++i)
+    if (bytes[i] > 0) std::memcpy(dst[i], src[i], (size_t)bytes[i]);
+}
+
+}  // namespace cpu
+}  // namespace cylon

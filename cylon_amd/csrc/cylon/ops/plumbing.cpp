@@ -1,10 +1,6 @@
 // Table plumbing operators: gather (K4), compaction (K11), project, merge,
 // slice.  Reference: cylon/util/copy_arrray.cpp:24-142 (copy_array_by_indices,
 // -1 -> null), table.cpp:267-289 (Merge), :831-850 (Project), arrow Filter.
-#include <hip/hip_runtime.h>
-
-#include <cstring>
-
 #include "util.hpp"
 
 namespace cylon {
@@ -114,34 +110,37 @@ TablePtr Slice(const TablePtr &t, int64_t offset, int64_t length) {
   return Table::Make(t->GetContext(), std::move(out));
 }
 
-// Concatenation of contiguous buffers into one allocation: device parts are moved by
-// hipMemcpyAsync on the current stream (the runtime's blit path streams at HBM rate;
-// at::cat's batched-copy kernel measured ~2 TB/s on the 1B-row union,
-// profiles/suite_cfg6_1gpu_kernels.txt), host parts by memcpy.
-static at::Tensor concat_buffers(const std::vector<at::Tensor> &parts) {
+// Concatenation of contiguous buffers into one allocation: all parts of all columns
+// are moved by ONE batched copy launch (kernels/copy.hip: 16-byte vectors, every copy
+// in flight at once) -- at::cat's batched kernel and the runtime's blit copy both ran
+// the 1B-row union's concatenation at ~2-2.4 TB/s (profiles/suite_cfg6_*).
+struct CopyPlan {
+  std::vector<const void *> src;
+  std::vector<void *> dst;
+  std::vector<int64_t> bytes;
+  std::vector<at::Tensor> keep;  // contiguous copies of strided parts, alive until launch
+};
+
+static at::Tensor concat_buffers(const std::vector<at::Tensor> &parts, CopyPlan &plan) {
   int64_t n = 0;
   for (const auto &p : parts) n += p.numel();
   at::Tensor out = at::empty({n}, parts[0].options());
   const int64_t es = out.element_size();
   uint8_t *dst = n ? reinterpret_cast<uint8_t *>(out.data_ptr()) : nullptr;
-  Exec ex(out.device());
   for (const auto &p0 : parts) {
     const at::Tensor p = p0.contiguous();
     const int64_t nb = p.numel() * es;
     if (nb == 0) continue;
-    if (ex.gpu) {
-      const hipError_t e = hipMemcpyAsync(dst, p.data_ptr(), (size_t)nb, hipMemcpyDeviceToDevice,
-                                          reinterpret_cast<hipStream_t>(ex.stream));
-      CYLON_CHECK(e == hipSuccess, Code::ExecutionError, "concat copy: " << hipGetErrorString(e));
-    } else {
-      std::memcpy(dst, p.data_ptr(), (size_t)nb);
-    }
+    plan.keep.push_back(p);
+    plan.src.push_back(p.data_ptr());
+    plan.dst.push_back(dst);
+    plan.bytes.push_back(nb);
     dst += nb;
   }
   return out;
 }
 
-static Column concat_columns(const std::vector<const Column *> &parts) {
+static Column concat_columns(const std::vector<const Column *> &parts, CopyPlan &plan) {
   const Column &f = *parts[0];
   int64_t n = 0;
   bool nullable = false;
@@ -155,12 +154,12 @@ static Column concat_columns(const std::vector<const Column *> &parts) {
     for (auto *p : parts)
       vs.push_back(p->nullable() ? p->validity.slice(0, 0, p->length)
                                  : at::ones({p->length}, p->data.options().dtype(at::kByte)));
-    valid = concat_buffers(vs);
+    valid = concat_buffers(vs, plan);
   }
   if (!f.is_var()) {
     std::vector<at::Tensor> ds;
     for (auto *p : parts) ds.push_back(p->data);
-    return Column(f.name, f.type, n, concat_buffers(ds), at::Tensor(), valid);
+    return Column(f.name, f.type, n, concat_buffers(ds, plan), at::Tensor(), valid);
   }
   std::vector<at::Tensor> bs, os;
   int64_t base = 0;
@@ -181,10 +180,15 @@ TablePtr Merge(const std::vector<TablePtr> &tables) {
     CYLON_CHECK(same_schema(f, t), Code::Invalid, "merge: tables must have identical schemas");
   if (tables.size() == 1) return f;
   std::vector<Column> out;
+  CopyPlan plan;
   for (int c = 0; c < f->Columns(); ++c) {
     std::vector<const Column *> parts;
     for (const auto &t : tables) parts.push_back(&t->column(c));
-    out.push_back(concat_columns(parts));
+    out.push_back(concat_columns(parts, plan));
+  }
+  if (!plan.src.empty()) {
+    Exec ex(f->device());
+    KCALL(ex, batched_copy, plan.src.data(), plan.dst.data(), plan.bytes.data(), (int)plan.src.size());
   }
   return Table::Make(f->GetContext(), std::move(out));
 }

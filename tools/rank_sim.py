@@ -62,7 +62,7 @@ def sort_sim(W):
     txfer = nbytes / ((W - 1) * XGMI_GBPS * 1e9) * 1e3
     est = tp + txfer + ts
     print(f"SORT W={W} rows/rank={n}: partition {tp:.1f} ms, exchange {nbytes / 1e9:.2f} GB over {W - 1} links "
-          f"~{txfer:.1f} ms, local sort {ts:.1f} ms => estimate {est:.1f} ms ({rows / est / 1e6:.0f} M rows/s/job)",
+          f"~{txfer:.1f} ms, local sort {ts:.1f} ms => estimate {est:.1f} ms ({rows / est * 1e3:.3g} rows/s/job)",
           flush=True)
     del t
     torch.cuda.empty_cache()
