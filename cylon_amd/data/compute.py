@@ -195,10 +195,19 @@ def is_in(table, values, skip_null: bool = True):
             vals = [v for v in vals if isinstance(v, (str, bytes))]
         else:
             vals = [v for v in vals if not isinstance(v, (str, bytes))]
-        if is_var(c):
-            res = pc.is_in(_arrow_col(c), value_set=pa.array(vals, type=_arrow_col(c).type) if vals else
-                           pa.array([], type=_arrow_col(c).type), skip_nulls=skip_null)
-            out.append(_from_arrow(c.name, res, table.device))
+        if is_var(c):  # device hash join of the column against the distinct value set
+            n = c.length
+            res = torch.zeros(n, dtype=torch.bool, device=c.data.device)
+            if vals and n:
+                vs = pa.array(vals, type=ab.to_arrow_type(c.type)).unique()
+                vt = C.Table(table.native.context(), [ab.column_from_arrow("v", vs, table.device)])
+                lt = C.Table(table.native.context(), [c])
+                li, _ = C.join_indices(lt, vt, "inner", "hash", [0], [0])
+                res[li.to(res.device)] = True
+            valid = col_valid(c)
+            if valid is not None:
+                res = res & valid
+            out.append(make_col(c.name, res))
             continue
         v = col_values(c)
         vs = torch.tensor([x for x in vals if x is not None], dtype=v.dtype, device=v.device) if vals else \
@@ -211,9 +220,46 @@ def is_in(table, values, skip_null: bool = True):
     return table._wrap(C.Table(table.native.context(), out))
 
 
+def _device_cast(c, target: pa.DataType, safe: bool):
+    """Numeric -> numeric casts on the column's device (torch), with Arrow's safe-cast checks:
+    float -> int must be integral and in range, int -> narrower int must be in range."""
+    if is_var(c) or c.type.type == T.BOOL:
+        return None
+    src = ab.to_arrow_type(c.type)
+    num = lambda t: pa.types.is_integer(t) or pa.types.is_floating(t)  # noqa: E731
+    if not (num(src) and num(target)) or target == pa.float16() or src == pa.float16():
+        return None
+    ct = ab.to_cylon_type(target)
+    tdt = ab.torch_dtype(ct)
+    v = c.data
+    valid = col_valid(c)
+    if safe and pa.types.is_integer(target):
+        live = v if valid is None else v[valid]
+        if live.numel():
+            info = np.iinfo(target.to_pandas_dtype())
+            if pa.types.is_floating(src):
+                if not bool(torch.all(torch.isfinite(live)) and torch.all(live == torch.trunc(live))):
+                    raise pa.ArrowInvalid(f"column {c.name}: float values would be truncated")
+                lo, hi = float(live.min()), float(live.max())
+            else:
+                lo, hi = int(live.min()), int(live.max())
+            if lo < info.min or hi > info.max:
+                raise pa.ArrowInvalid(f"column {c.name}: integer value out of range for {target}")
+    out = v.to(tdt)
+    return C.Column(c.name, ct, c.length, out.contiguous(), None,
+                    None if c.validity is None else c.validity.contiguous())
+
+
 def cast(table, dtype, safe: bool = True):
-    """astype: dtype may be a single type or {column: type}."""
+    """astype: dtype may be a single type or {column: type}.  Numeric -> numeric casts run on the
+    table's device; everything else goes through Arrow's cast kernels on the host."""
     from ..types import to_arrow
+    cols = table.native.columns()
+    targets = [dtype.get(c.name) if isinstance(dtype, dict) else dtype for c in cols]
+    dev = [None if t is None else _device_cast(c, to_arrow(t), safe) for c, t in zip(cols, targets)]
+    if all(t is None or d is not None for t, d in zip(targets, dev)):
+        out = [c if d is None else d for c, d in zip(cols, dev)]
+        return table._wrap(C.Table(table.native.context(), out))
     at = table.to_arrow()
     arrays, names = [], []
     for name, col in zip(at.column_names, at.columns):

@@ -205,3 +205,24 @@ def test_functional_ops_api(ctx):
     assert ops.merge([a, a]).row_count == 8
     assert ops.project(a, ["v"]).column_names == ["v"]
     assert ops.union(ops.project(a, ["k"]), ops.project(b, ["k"])).row_count == 4
+
+
+def test_device_isin_strings_and_numeric_cast(ctx):
+    """isin on string columns (device hash join against the value set) and numeric astype on the
+    table's device with Arrow's safe-cast checks (reference: pycylon compute.pyx is_in / astype)."""
+    import pyarrow as pa
+    from cylon_amd import Table
+    t = Table(pa.table({"s": pa.array(["a", None, "bb", "c", "a"]), "x": pa.array([1.0, 2.0, None, 4.0, 5.0]),
+                        "i": pa.array([1, 2, 3, 300, 5])}), ctx)
+    got = t.isin({"s": ["a", "c", None], "x": [2.0, 5.0], "i": [3]}).to_pydict()
+    assert got["s"] == [True, False, False, True, True]
+    assert got["x"] == [False, True, False, False, True]
+    assert got["i"] == [False, False, True, False, False]
+    c = t.astype({"x": "int32", "i": "int16"}).to_arrow()
+    assert c.column("x").type == pa.int32() and c.column("x").to_pylist() == [1, 2, None, 4, 5]
+    assert c.column("i").type == pa.int16()
+    import pytest
+    with pytest.raises(Exception):
+        Table(pa.table({"x": [1.5]}), ctx).astype("int64")
+    with pytest.raises(Exception):
+        t.astype({"i": "int8"})  # 300 out of range
