@@ -52,5 +52,63 @@ void unpack_validity(const uint8_t *bits, int64_t bit_offset, int64_t n, uint8_t
   HIP_LAUNCH_CHECK();
 }
 
+
+// ---------------------------------------------------------------------------
+// byte columns <-> 8-byte words (radix passes: validity bytes ride in 8-byte rows)
+// ---------------------------------------------------------------------------
+constexpr int kMaxByteCols = 64;
+
+struct ByteCols {
+  const uint8_t *in[kMaxByteCols];
+  uint8_t *out[kMaxByteCols];
+  const uint64_t *win[kMaxByteCols / 8];
+  uint64_t *wout[kMaxByteCols / 8];
+};
+
+__global__ void k_pack_byte_columns(ByteCols c, int k, int64_t n) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  const int nw = (k + 7) / 8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+#pragma unroll 1
+    for (int w = 0; w < nw; ++w) {
+      uint64_t word = 0;
+      for (int j = 0; j < 8 && 8 * w + j < k; ++j) word |= (uint64_t)c.in[8 * w + j][i] << (8 * j);
+      c.wout[w][i] = word;
+    }
+  }
+}
+
+__global__ void k_unpack_byte_columns(ByteCols c, int k, int64_t n) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  const int nw = (k + 7) / 8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+#pragma unroll 1
+    for (int w = 0; w < nw; ++w) {
+      const uint64_t word = c.win[w][i];
+      for (int j = 0; j < 8 && 8 * w + j < k; ++j) c.out[8 * w + j][i] = (uint8_t)(word >> (8 * j));
+    }
+  }
+}
+
+void pack_byte_columns(const uint8_t *const *cols, int k, int64_t n, uint64_t *const *words, void *stream) {
+  CYLON_CHECK(k >= 1 && k <= kMaxByteCols, Code::Invalid, "byte column count " << k);
+  if (n == 0) return;
+  ByteCols c{};
+  for (int j = 0; j < k; ++j) c.in[j] = cols[j];
+  for (int w = 0; w < (k + 7) / 8; ++w) c.wout[w] = words[w];
+  hipLaunchKernelGGL(k_pack_byte_columns, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), c, k, n);
+  HIP_LAUNCH_CHECK();
+}
+
+void unpack_byte_columns(const uint64_t *const *words, int k, int64_t n, uint8_t *const *cols, void *stream) {
+  CYLON_CHECK(k >= 1 && k <= kMaxByteCols, Code::Invalid, "byte column count " << k);
+  if (n == 0) return;
+  ByteCols c{};
+  for (int j = 0; j < k; ++j) c.out[j] = cols[j];
+  for (int w = 0; w < (k + 7) / 8; ++w) c.win[w] = words[w];
+  hipLaunchKernelGGL(k_unpack_byte_columns, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), c, k, n);
+  HIP_LAUNCH_CHECK();
+}
+
 }  // namespace hip
 }  // namespace cylon
