@@ -12,7 +12,9 @@ from cylon_amd import CylonContext, Table  # noqa: E402
 from cylon_amd._lib import C  # noqa: E402
 from cylon_amd.data import arrow_bridge as ab  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 200_000_000
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+n = int(args[0]) if args else 200_000_000
+MODES = (True,) if "--only-nullable" in sys.argv else (False, True)
 ctx = CylonContext(device="cuda:0")
 hi = int(0.99 * n)
 
@@ -27,7 +29,7 @@ def rel(seed, nullable):
     return Table(context=ctx, _native=C.Table(ctx._ctx, cols))
 
 
-for nullable in (False, True):
+for nullable in MODES:
     L, R = rel(1, nullable), rel(2, nullable)
     L.join(R, "inner", "hash", on=[0])
     torch.cuda.synchronize()
