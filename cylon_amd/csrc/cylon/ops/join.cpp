@@ -156,9 +156,24 @@ static bool radix_eligible(const TablePtr &t) {
 
 struct RadixSide {
   at::Tensor keys, offs;
-  std::vector<at::Tensor> data, valid;  // per table column (valid undefined if not nullable)
+  std::vector<at::Tensor> data, valid;  // per table column (valid undefined if not nullable or packed)
   std::vector<bool> is_key;             // data[c] is the (partitioned) key array itself
+  // validity bytes kept packed 8 per 8-byte word (radix.cpp): vpos[c] = byte position of
+  // column c's validity in the words (-1: not packed); the write kernel moves the words
+  std::vector<int> vpos;
+  std::vector<at::Tensor> vwords;
 };
+
+// the partition / write kernels move validity packed when every data column is 8 bytes wide
+// (the all-8-byte kernel variants; byte runs of 1-byte validity columns cost 2x)
+static bool packs_validity(const TablePtr &t) {
+  bool any = false;
+  for (const auto &c : t->columns()) {
+    if (c.type.width() != 8) return false;
+    any |= c.nullable();
+  }
+  return any;
+}
 
 // Partition every column of t (+ validity bytes) by the top `bits` bits of fmix64(key).
 static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Tensor &keys, int bits,
@@ -182,13 +197,22 @@ static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Te
     }
   }
   at::Tensor offs;
-  cur = RadixPartition(ex, std::move(cur), widths, bits, &offs, range);
+  const size_t nslots = cur.size();
+  std::vector<int> packed;
+  cur = RadixPartition(ex, std::move(cur), widths, bits, &offs, range, packs_validity(t) ? &packed : nullptr);
   RadixSide s;
   s.keys = cur[0];
   s.offs = offs;
+  for (size_t w = nslots; w < cur.size(); ++w) s.vwords.push_back(cur[w]);
   for (int c = 0; c < t->Columns(); ++c) {
     s.data.push_back(cur[dslot[c]]);
-    s.valid.push_back(vslot[c] >= 0 ? cur[vslot[c]] : at::Tensor());
+    const bool pk = vslot[c] >= 0 && !s.vwords.empty();
+    s.valid.push_back(vslot[c] >= 0 && !pk ? cur[vslot[c]] : at::Tensor());
+    int pos = -1;
+    if (pk)
+      for (size_t j = 0; j < packed.size(); ++j)
+        if (packed[j] == vslot[c]) pos = (int)j;
+    s.vpos.push_back(pos);
     s.is_key.push_back(dslot[c] == 0);
   }
   return s;
@@ -202,8 +226,10 @@ struct RadixCols {
 };
 
 static RadixCols radix_cols(const TablePtr &t, const RadixSide *s, const std::vector<Column> *outs,
-                            int64_t out_off = 0) {
+                            int64_t out_off = 0, const std::vector<at::Tensor> *word_outs = nullptr) {
   RadixCols rc;
+  const bool packed = s ? !s->vwords.empty() : packs_validity(t);
+  int nnull = 0;
   for (int c = 0; c < t->Columns(); ++c) {
     const Column &col = t->column(c);
     rc.in.push_back(s && !s->is_key[c] ? reinterpret_cast<const uint8_t *>(s->data[c].data_ptr())
@@ -211,13 +237,36 @@ static RadixCols radix_cols(const TablePtr &t, const RadixSide *s, const std::ve
     rc.out.push_back(outs ? reinterpret_cast<uint8_t *>((*outs)[c].data.data_ptr()) + out_off * col.type.width()
                           : nullptr);
     rc.w.push_back(col.type.width());
-    if (col.nullable()) {
+    if (col.nullable() && packed) {
+      ++nnull;
+    } else if (col.nullable()) {
       rc.in.push_back(s ? s->valid[c].data_ptr<uint8_t>() : reinterpret_cast<const uint8_t *>(1));
       rc.out.push_back(outs ? (*outs)[c].validity.data_ptr<uint8_t>() + out_off : nullptr);
       rc.w.push_back(1);
     }
   }
+  if (packed) {  // the packed validity words, 8 bytes per row (outputs: temporary words)
+    const int nw = (nnull + 7) / 8;
+    for (int w = 0; w < nw; ++w) {
+      rc.in.push_back(s ? reinterpret_cast<const uint8_t *>(s->vwords[w].data_ptr()) : reinterpret_cast<const uint8_t *>(1));
+      rc.out.push_back(word_outs ? reinterpret_cast<uint8_t *>((*word_outs)[w].data_ptr()) : nullptr);
+      rc.w.push_back(8);
+    }
+  }
   return rc;
+}
+
+// output validity of the packed columns from the written words (at row offset out_off)
+static void unpack_validity_words(const Exec &ex, const TablePtr &t, const RadixSide &s,
+                                  const std::vector<at::Tensor> &words, std::vector<Column> &outs, int64_t out_off,
+                                  int64_t m) {
+  if (s.vwords.empty() || m == 0) return;
+  std::vector<uint8_t *> dst;
+  for (int c = 0; c < t->Columns(); ++c)
+    if (s.vpos[c] >= 0) dst.push_back(outs[c].validity.data_ptr<uint8_t>() + out_off);
+  std::vector<const uint64_t *> wp;
+  for (const auto &w : words) wp.push_back(reinterpret_cast<const uint64_t *>(w.data_ptr()));
+  hip::unpack_byte_columns(wp.data(), (int)dst.size(), m, dst.data(), ex.stream);
 }
 
 // Output accumulator of a chunked (pipelined) distributed join.  The radix join
@@ -281,7 +330,7 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   for (int c = 0, q = 0; c < bt->Columns(); ++c, ++q) {
     const Column &col = bt->column(c);
     if (col.type.width() == 8 && col.data.data_ptr() == (build_left ? lk : rk).data_ptr()) shape.in[q] = nullptr;
-    if (col.nullable()) ++q;
+    if (col.nullable() && !packs_validity(bt)) ++q;  // packed validity words sit after the columns
   }
   const int64_t cap = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size());
   // mean build rows per partition: 0.85 x capacity keeps the largest of ~1M uniform
@@ -331,14 +380,22 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
       rcols.push_back(make_fixed_column(cfg.GetRightTablePrefix() + col.name, col.type, m, ex.device, col.nullable()));
   }
   if (m > 0) {
-    RadixCols pc = build_left ? radix_cols(right, &R, &rcols, off) : radix_cols(left, &L, &lcols, off);
-    RadixCols bc = build_left ? radix_cols(left, &L, &lcols, off) : radix_cols(right, &R, &rcols, off);
+    auto word_outs = [&](const RadixSide &sd) {
+      std::vector<at::Tensor> w;
+      for (size_t i = 0; i < sd.vwords.size(); ++i) w.push_back(ex.empty_i64(m));
+      return w;
+    };
+    std::vector<at::Tensor> lwords = word_outs(L), rwords = word_outs(R);
+    RadixCols pc = build_left ? radix_cols(right, &R, &rcols, off, &rwords) : radix_cols(left, &L, &lcols, off, &lwords);
+    RadixCols bc = build_left ? radix_cols(left, &L, &lcols, off, &lwords) : radix_cols(right, &R, &rcols, off, &rwords);
     // probe-side columns are streamed from HBM: the key column is read from its partitioned array
     for (size_t q = 0; q < pc.in.size(); ++q)
       if (!pc.in[q]) pc.in[q] = reinterpret_cast<const uint8_t *>(P.keys.data_ptr());
     hip::radix_join_write(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
                           nparts, cap, ptr<int64_t>(out_offs), pc.in.data(), pc.out.data(), pc.w.data(),
                           (int)pc.in.size(), bc.in.data(), bc.out.data(), bc.w.data(), (int)bc.in.size(), ex.stream);
+    unpack_validity_words(ex, left, L, lwords, lcols, off, m);
+    unpack_validity_words(ex, right, R, rwords, rcols, off, m);
   }
   trace::add_counter("join.radix.rows_out", m);
   if (sink) return Table::Make(left->GetContext(), sink->cols);
@@ -543,7 +600,10 @@ static TablePtr range_join(const Exec &ex, const TablePtr &left, const TablePtr 
   for (const auto &col : right->columns())
     rcols.push_back(make_fixed_column(cfg.GetRightTablePrefix() + col.name, col.type, m, ex.device, col.nullable()));
   if (m > 0) {
-    RadixCols a = radix_cols(left, &L, &lcols), b = radix_cols(right, &R, &rcols);
+    std::vector<at::Tensor> lwords, rwords;
+    for (size_t i = 0; i < L.vwords.size(); ++i) lwords.push_back(ex.empty_i64(m));
+    for (size_t i = 0; i < R.vwords.size(); ++i) rwords.push_back(ex.empty_i64(m));
+    RadixCols a = radix_cols(left, &L, &lcols, 0, &lwords), b = radix_cols(right, &R, &rcols, 0, &rwords);
     for (auto &q : a.in)
       if (!q) q = reinterpret_cast<const uint8_t *>(L.keys.data_ptr());
     for (auto &q : b.in)
@@ -552,6 +612,8 @@ static TablePtr range_join(const Exec &ex, const TablePtr &left, const TablePtr 
                           nparts, spec.flip, spec.mn, rshift, ptr<int64_t>(out_offs), a.in.data(), a.out.data(),
                           a.w.data(), (int)a.in.size(), b.in.data(), b.out.data(), b.w.data(), (int)b.in.size(),
                           ex.stream);
+    unpack_validity_words(ex, left, L, lwords, lcols, 0, m);
+    unpack_validity_words(ex, right, R, rwords, rcols, 0, m);
   }
   trace::add_counter("join.range.rows_out", m);
   for (auto &c : rcols) lcols.push_back(std::move(c));

@@ -8,7 +8,8 @@ namespace cylon {
 namespace ops {
 
 std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> cur, const std::vector<int> &widths,
-                                       int bits, at::Tensor *offs, const RangeSpec *range) {
+                                       int bits, at::Tensor *offs, const RangeSpec *range,
+                                       std::vector<int> *keep_packed) {
   CYLON_CHECK(ex.gpu, Code::Invalid, "RadixPartition is a device path");
   CYLON_CHECK(!cur.empty() && cur.size() == widths.size() && widths[0] == 8, Code::Invalid,
               "RadixPartition: column 0 must be the int64 key");
@@ -79,7 +80,14 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
     cur = std::move(nxt);
     shift += db;
   }
-  if (pack) {  // unpack into 1-byte columns, original order
+  if (pack && keep_packed) {  // caller consumes the words: undefined byte slots + words appended
+    const int nw = ((int)byte_idx.size() + 7) / 8;
+    std::vector<at::Tensor> out(keep_idx.size() + byte_idx.size());
+    for (size_t j = 0; j < keep_idx.size(); ++j) out[keep_idx[j]] = cur[j];
+    for (int w = 0; w < nw; ++w) out.push_back(cur[keep_idx.size() + w]);
+    *keep_packed = byte_idx;
+    cur = std::move(out);
+  } else if (pack) {  // unpack into 1-byte columns, original order
     const int k = (int)byte_idx.size(), nw = (k + 7) / 8;
     std::vector<at::Tensor> out(keep_idx.size() + byte_idx.size());
     for (size_t j = 0; j < keep_idx.size(); ++j) out[keep_idx[j]] = cur[j];
@@ -94,6 +102,7 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
     cur = std::move(out);
   }
   *offs = ex.empty_i64((int64_t(1) << bits) + 1);
+  if (keep_packed && !pack) keep_packed->clear();
   if (range)
     hip::radix_range_part_offsets(ptr<int64_t>(cur[0]), n, range->flip, range->mn, range->rshift, bits,
                                   ptr<int64_t>(*offs), ex.stream);

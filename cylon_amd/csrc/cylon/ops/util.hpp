@@ -61,8 +61,12 @@ struct RangeSpec {
   uint64_t flip = 0, mn = 0;
   int rshift = 0;
 };
+// keep_packed != nullptr: validity-style 1-byte columns that were packed 8 per 8-byte word
+// for the passes stay packed -- their slots come back undefined, the words are appended
+// to the result and *keep_packed lists the packed column indices in byte order.
 std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> cols, const std::vector<int> &widths,
-                                       int bits, at::Tensor *offs, const RangeSpec *range = nullptr);
+                                       int bits, at::Tensor *offs, const RangeSpec *range = nullptr,
+                                       std::vector<int> *keep_packed = nullptr);
 
 // exclusive scan of int64 counts -> offsets[n+1]
 inline at::Tensor exclusive_scan(const Exec &ex, const at::Tensor &counts) {
