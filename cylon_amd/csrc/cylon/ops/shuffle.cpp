@@ -77,26 +77,33 @@ static TablePtr mod_reorder(const TablePtr &t, int key, uint32_t P) {
   Exec ex(t->device());
   const int64_t n = t->Rows();
   const Column &kc = t->column(key);
-  std::vector<const uint8_t *> in{reinterpret_cast<const uint8_t *>(kc.data.data_ptr())};
-  std::vector<at::Tensor> out{at::empty_like(kc.data)};
+  std::vector<at::Tensor> src{kc.data};
   std::vector<int> widths{8};
   std::vector<int> dslot(t->Columns(), 0), vslot(t->Columns(), -1);
   auto add = [&](const at::Tensor &x, int w) {
-    in.push_back(reinterpret_cast<const uint8_t *>(x.data_ptr()));
-    out.push_back(at::empty_like(x));
+    src.push_back(x);
     widths.push_back(w);
-    return (int)out.size() - 1;
+    return (int)src.size() - 1;
   };
   for (int c = 0; c < t->Columns(); ++c) {
     const Column &col = t->column(c);
     if (c != key) dslot[c] = add(col.data, col.type.width());
     if (col.nullable()) vslot[c] = add(col.validity, 1);
   }
+  // validity bytes travel packed so a nullable all-8-byte table keeps the 8-byte path
+  const BytePacking bp = PackByteColumns(ex, src, widths, n);
+  std::vector<at::Tensor> out;
+  std::vector<const uint8_t *> in;
   std::vector<uint8_t *> outp;
-  for (auto &o : out) outp.push_back(reinterpret_cast<uint8_t *>(o.data_ptr()));
+  for (auto &x : src) {
+    out.push_back(at::empty_like(x));
+    in.push_back(reinterpret_cast<const uint8_t *>(x.data_ptr()));
+    outp.push_back(reinterpret_cast<uint8_t *>(out.back().data_ptr()));
+  }
   at::Tensor ws = ex.empty_i64(hip::radix_mod_rows_pass_workspace(n, P));
   hip::radix_mod_rows_pass(reinterpret_cast<const int64_t *>(in[0]), n, P, in.data(), outp.data(), widths.data(),
                            (int)in.size(), ptr<int64_t>(ws), ex.stream);
+  out = UnpackByteColumns(ex, bp, std::move(out), n);
   std::vector<Column> cols;
   for (int c = 0; c < t->Columns(); ++c) {
     const Column &col = t->column(c);

@@ -140,6 +140,9 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
   // pass as it stores column 0 (no separate un-image read + write of the key)
   const bool key_in_last_pass = key_from_image && kc.type.width() == 8 && diff != 0;
   const uint64_t key_xor = (kc.type.kind() == ValueKind::SIGNED_INT ? (1ull << 63) : 0ull) ^ (asc ? 0ull : ~0ull);
+  // validity bytes of an otherwise all-8-byte table travel packed (8-byte pass path)
+  BytePacking bp;
+  if (diff != 0) bp = PackByteColumns(ex, cur, widths, n);
   if (diff != 0) {
     const int lo = __builtin_ctzll(diff), hi = 64 - __builtin_clzll(diff);
     const int npass = (hi - lo + 9) / 10;
@@ -165,6 +168,7 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
       cur = std::move(nxt);
       shift += db;
     }
+    cur = UnpackByteColumns(ex, bp, std::move(cur), n);
   }
   std::vector<Column> cols;
   size_t q = 1;

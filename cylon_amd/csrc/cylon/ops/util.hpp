@@ -68,6 +68,21 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
                                        int bits, at::Tensor *offs, const RangeSpec *range = nullptr,
                                        std::vector<int> *keep_packed = nullptr);
 
+// Row-moving passes (k_rows_pass) take their all-8-byte path only when every moved
+// column is 8 bytes wide; validity bytes beside 8-byte columns therefore travel packed
+// 8 per 8-byte word (bitmap.hip pack_byte_columns).  PackByteColumns rewrites
+// cols/widths in place (kept columns first, then the words) when that applies;
+// UnpackByteColumns restores the original column order.
+struct BytePacking {
+  std::vector<int> byte_idx, keep_idx;  // original positions
+  std::vector<at::ScalarType> byte_dtype;  // 1-byte dtypes (uint8 validity, bool/int8 data)
+  bool active = false;
+  int words() const { return ((int)byte_idx.size() + 7) / 8; }
+};
+BytePacking PackByteColumns(const Exec &ex, std::vector<at::Tensor> &cols, std::vector<int> &widths, int64_t n);
+std::vector<at::Tensor> UnpackByteColumns(const Exec &ex, const BytePacking &bp, std::vector<at::Tensor> cols,
+                                          int64_t n);
+
 // exclusive scan of int64 counts -> offsets[n+1]
 inline at::Tensor exclusive_scan(const Exec &ex, const at::Tensor &counts) {
   const int64_t n = counts.numel();

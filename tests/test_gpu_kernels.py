@@ -217,7 +217,8 @@ def test_radix_row_sort_matches_index_sort(gpu_ctx, monkeypatch, dtype, asc):
     else:
         k = rng.integers(-5000, 5000, n).astype(dtype)  # many ties: stability visible in the payload
     t = pa.table({"p": pa.array(np.arange(n)), "k": k,
-                  "q": pa.array(rng.random(n), mask=rng.random(n) < 0.2)})
+                  "q": pa.array(rng.random(n), mask=rng.random(n) < 0.2),
+                  "b": pa.array(rng.random(n) < 0.5, mask=rng.random(n) < 0.1)})  # packed bytes
     T = Table(t, gpu_ctx)
     res = []
     for thr in ("1", str(1 << 62)):

@@ -74,18 +74,30 @@ def _dist_ops(ctx):
     return df, g, s, u1, u2, sets
 
 
-def test_shuffle_partition_fast_pass_matches_generic():
+@pytest.mark.parametrize("shape", ["mixed_widths", "nullable_8byte"])
+def test_shuffle_partition_fast_pass_matches_generic(shape):
     """The shuffle's one-pass partition of an int64-keyed table equals the generic
-    pid + stable scatter path (rows, order within partitions, counts)."""
+    pid + stable scatter path (rows, order within partitions, counts).  nullable_8byte:
+    validity and bool bytes travel packed 8 per word through the pass (radix.cpp
+    PackByteColumns) and are unpacked back to their columns."""
+    import pyarrow as pa
     import torch
     from cylon_amd import CylonContext, Table
     from cylon_amd._lib import C
     ctx = CylonContext(device=DEV)
     g = torch.Generator(device="cuda").manual_seed(3)
     n = 300_000
-    t = Table.from_torch(ctx, {"k": torch.randint(-2**40, 2**40, (n,), generator=g, device="cuda"),
-                               "x": torch.randint(0, 100, (n,), generator=g, device="cuda", dtype=torch.int32),
-                               "f": torch.rand(n, generator=g, device="cuda", dtype=torch.float64)})
+    if shape == "mixed_widths":
+        t = Table.from_torch(ctx, {"k": torch.randint(-2**40, 2**40, (n,), generator=g, device="cuda"),
+                                   "x": torch.randint(0, 100, (n,), generator=g, device="cuda", dtype=torch.int32),
+                                   "f": torch.rand(n, generator=g, device="cuda", dtype=torch.float64)})
+    else:
+        rng = np.random.default_rng(4)
+        t = Table(pa.table({"k": rng.integers(-2**40, 2**40, n),
+                            "f": pa.array(rng.random(n), mask=rng.random(n) < 0.3),
+                            "i": pa.array(rng.integers(0, 9, n), mask=rng.random(n) < 0.1),
+                            "b": pa.array(rng.random(n) < 0.5, mask=rng.random(n) < 0.2)}), ctx)
+        assert t.device.startswith("cuda")
     for P in (2, 8, 24, 1024):
         fast, cf = C.shuffle_partition(t.native, [0], P)
         pid, _ = C.map_to_hash_partitions(t.native, [0], P)

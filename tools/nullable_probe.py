@@ -1,6 +1,7 @@
-"""Cost of nullability in the radix join: 200M x 200M, int64 key + 3 float64 payload, once with
-non-nullable payload and once with every payload column nullable (validity bytes travel through
-the LDS passes as one more 1-byte column each)."""
+"""Cost of nullability in the LDS row-moving passes: int64 key + 3 float64 payload (200M rows by
+default), once with non-nullable payload and once with every payload column nullable (validity
+bytes travel packed 8 per 8-byte word through the passes).  --op join (200M x 200M radix join,
+default), sort (radix table sort by the key) or shuffle (one-pass mod partition into 8 parts)."""
 import os
 import sys
 import time
@@ -15,6 +16,7 @@ from cylon_amd.data import arrow_bridge as ab  # noqa: E402
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 n = int(args[0]) if args else 200_000_000
 MODES = (True,) if "--only-nullable" in sys.argv else (False, True)
+OP = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--op=")), "join")
 ctx = CylonContext(device="cuda:0")
 hi = int(0.99 * n)
 
@@ -29,17 +31,26 @@ def rel(seed, nullable):
     return Table(context=ctx, _native=C.Table(ctx._ctx, cols))
 
 
+def run(L, R):
+    if OP == "sort":
+        return L.sort("k")
+    if OP == "shuffle":
+        return C.shuffle_partition(L.native, [0], 8)
+    return L.join(R, "inner", "hash", on=[0])
+
+
 for nullable in MODES:
-    L, R = rel(1, nullable), rel(2, nullable)
-    L.join(R, "inner", "hash", on=[0])
+    L = rel(1, nullable)
+    R = rel(2, nullable) if OP == "join" else None
+    run(L, R)
     torch.cuda.synchronize()
     ts = []
     for _ in range(5):
         t0 = time.perf_counter()
-        out = L.join(R, "inner", "hash", on=[0])
+        out = run(L, R)
         torch.cuda.synchronize()
         ts.append((time.perf_counter() - t0) * 1e3)
         del out
-    print(f"nullable={nullable}: median {sorted(ts)[2]:.2f} ms  all {[round(x, 2) for x in ts]}", flush=True)
+    print(f"{OP} nullable={nullable}: median {sorted(ts)[2]:.2f} ms  all {[round(x, 2) for x in ts]}", flush=True)
     del L, R
     torch.cuda.empty_cache()
