@@ -23,6 +23,8 @@
 //      owns a contiguous slice of the probe rows (wave-level scans only).
 // Partitions whose build side exceeds the LDS capacity are reported; the
 // caller then falls back to the global-table join.
+#include <cstdlib>
+
 #include "stable_rank.hpp"
 
 namespace cylon {
@@ -155,7 +157,8 @@ __global__ __launch_bounds__(kRPThreads) void k_rp_hist(Digit digit, int64_t n, 
   for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) bh[(int64_t)p * nblocks + blockIdx.x] = hist[p];
 }
 
-// block-wide exclusive scan of one uint32 per thread (kRPThreads threads)
+// block-wide exclusive scan of one uint32 per thread (WAVES waves)
+template <int WAVES = kRPWaves>
 __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) {
   const int lane = lane_id(), wave = threadIdx.x / kWave;
   uint32_t inc = c;
@@ -168,7 +171,7 @@ __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) 
   __syncthreads();
   uint32_t off = 0;
 #pragma unroll
-  for (int w = 0; w < kRPWaves; ++w) off += (w < wave) ? wsum[w] : 0u;
+  for (int w = 0; w < WAVES; ++w) off += (w < wave) ? wsum[w] : 0u;
   return off + inc - c;
 }
 
@@ -178,16 +181,26 @@ __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) 
 // global latency is hidden by software pipelining in registers instead: the
 // loads of column c+1 (and, during the last column, the next tile's keys) are
 // in flight while column c streams out of the stage.  Column 0 is the key.
-template <class Digit, bool W8>
-__global__ __launch_bounds__(kRPThreads) void k_rows_pass(Digit digit, int nbits, uint32_t nbuckets, ColSet cols,
-                                                          int64_t n, int64_t rows_per_block, int64_t nblocks,
-                                                          const int64_t *__restrict__ bh_scan) {
+//
+// THREADS = 512 runs two 4096-row blocks per CU instead of one 8192-row block, so
+// one block's ranking overlaps the other's memory traffic (every stage write waits
+// with vmcnt(0) for all outstanding loads AND stores: gfx9 counts both on one
+// counter).  Issuing several columns' loads per wait instead (more VGPRs, fewer
+// waves) measured slower -- profiles/rows_pass_experiments_r02.txt.
+template <class Digit, bool W8, int THREADS>
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_rows_pass(
+    Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
+    const int64_t *__restrict__ bh_scan) {
+  constexpr int WAVES = THREADS / kWave;
+  constexpr int TILE = THREADS * kRPItems;
+  constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;  // buckets per thread in the offset scan
+  static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 2 <= TILE * 8, "ranking scratch must fit the stage");
   __shared__ int64_t running[kRPMaxBuckets];
   __shared__ uint32_t toff[kRPMaxBuckets + 1];
-  __shared__ uint64_t ustage[kRPTile];  // column stage | {wcnt[16][nb] u16, sdig[tile] u16 at +32 KB}
-  __shared__ uint32_t wsum[kRPWaves];
+  __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16, sdig[TILE] u16}
+  __shared__ uint32_t wsum[WAVES];
   uint16_t *wcnt = reinterpret_cast<uint16_t *>(ustage);
-  uint16_t *sdig = wcnt + kRPWaves * kRPMaxBuckets;
+  uint16_t *sdig = wcnt + WAVES * kRPMaxBuckets;
   uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
 
   const int64_t b = blockIdx.x;
@@ -206,13 +219,13 @@ __global__ __launch_bounds__(kRPThreads) void k_rows_pass(Digit digit, int nbits
     const int64_t i = begin + wrow + k * kWave + lane;
     if (i < end) kv[k] = (uint64_t)digit.keys[i];
   }
-  for (int64_t tile = begin; tile < end; tile += kRPTile) {
-    const int cnt = (int)((end - tile) < kRPTile ? (end - tile) : kRPTile);
+  for (int64_t tile = begin; tile < end; tile += TILE) {
+    const int cnt = (int)((end - tile) < TILE ? (end - tile) : TILE);
     uint32_t pl[kRPItems];  // digit, then (in-wave rank << 16) | digit, then sorted slot; ~0 = inactive
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k)
       pl[k] = (wrow + k * kWave + lane < cnt) ? digit.of_key((int64_t)kv[k]) : 0xffffffffu;
-    for (uint32_t q = threadIdx.x; q < kRPWaves * nbuckets; q += blockDim.x) wcnt[q] = 0;
+    for (uint32_t q = threadIdx.x; q < WAVES * nbuckets; q += blockDim.x) wcnt[q] = 0;
     __syncthreads();  // also orders the previous tile's stage reads before the counters reuse it
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k) {
@@ -233,20 +246,32 @@ __global__ __launch_bounds__(kRPThreads) void k_rows_pass(Digit digit, int nbits
       pl[k] = active ? (((base + rank) << 16) | p) : 0xffffffffu;
     }
     __syncthreads();
-    {  // bucket p = thread: exclusive prefix over waves (in place), then block scan of the totals
-      const uint32_t p = threadIdx.x;
-      uint32_t run = 0;
-      if (p < nbuckets) {
+    {  // thread owns buckets [t*BPT, t*BPT+BPT): exclusive prefix over waves (in place), then a
+       // block scan of the thread totals
+      uint32_t loc[BPT];
+      uint32_t total = 0;
 #pragma unroll
-        for (int w = 0; w < kRPWaves; ++w) {
-          const uint32_t c = wcnt[w * nbuckets + p];
-          wcnt[w * nbuckets + p] = (uint16_t)run;
-          run += c;
+      for (int i = 0; i < BPT; ++i) {
+        const uint32_t p = threadIdx.x * BPT + i;
+        loc[i] = total;
+        uint32_t run = 0;
+        if (p < nbuckets) {
+#pragma unroll
+          for (int w = 0; w < WAVES; ++w) {
+            const uint32_t c = wcnt[w * nbuckets + p];
+            wcnt[w * nbuckets + p] = (uint16_t)run;
+            run += c;
+          }
         }
+        total += run;
       }
-      const uint32_t ex = rp_block_exscan(run, wsum);
-      if (p < nbuckets) toff[p] = ex;
-      if (p == nbuckets - 1) toff[nbuckets] = ex + run;
+      const uint32_t ex = rp_block_exscan<WAVES>(total, wsum);
+#pragma unroll
+      for (int i = 0; i < BPT; ++i) {
+        const uint32_t p = threadIdx.x * BPT + i;
+        if (p < nbuckets) toff[p] = ex + loc[i];
+      }
+      if (threadIdx.x == THREADS - 1) toff[nbuckets] = ex + total;
     }
     __syncthreads();
 #pragma unroll
@@ -258,20 +283,21 @@ __global__ __launch_bounds__(kRPThreads) void k_rows_pass(Digit digit, int nbits
       pl[k] = pos;
     }
     __syncthreads();
-    int64_t dst[kRPItems];  // destination of sorted slot j = threadIdx.x + q * kRPThreads
+    int64_t dst[kRPItems];  // destination of sorted slot j = threadIdx.x + q * THREADS
 #pragma unroll
     for (int q = 0; q < kRPItems; ++q) {
-      const int j = threadIdx.x + q * kRPThreads;
+      const int j = threadIdx.x + q * THREADS;
       if (j < cnt) {
         const uint32_t p = sdig[j];
         dst[q] = running[p] + (j - (int64_t)toff[p]);
       }
     }
     __syncthreads();  // counters / digits dead: the union becomes the column stage
+    const int64_t next = tile + TILE;
+    // load column c+1 while column c streams out of the stage
     uint64_t v[kRPItems];
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k) v[k] = kv[k];
-    const int64_t next = tile + kRPTile;
 #pragma unroll 1
     for (int c = 0; c < cols.n; ++c) {  // column fields fetched once per column (scalar loads)
       const int w = cols.width[c];
@@ -296,7 +322,7 @@ __global__ __launch_bounds__(kRPThreads) void k_rows_pass(Digit digit, int nbits
       }
 #pragma unroll
       for (int q = 0; q < kRPItems; ++q) {
-        const int j = threadIdx.x + q * kRPThreads;
+        const int j = threadIdx.x + q * THREADS;
         if (j < cnt) stw<W8>(out, dst[q], w, ldw<W8>(st, j, w));
       }
       __syncthreads();
@@ -309,20 +335,50 @@ struct RPGeometry {
   int64_t nblocks, rows_per_block;
 };
 
-static RPGeometry rp_geometry(int64_t n) {
-  const int64_t tiles = std::max<int64_t>(1, (n + kRPTile - 1) / kRPTile);
-  const int64_t want = 2 * kNumCUs;
+// Pass block size.  Two 512-thread blocks per CU (4096-row tiles) interleave one
+// block's ranking with the other's memory traffic: a 2B-row key-only sort runs 137 ->
+// 120 ms.  With several payload columns the halved tile shortens every bucket's write
+// run per tile (1B x 1B join: partition 82 -> 99 ms), so wide rows keep one 1024-thread
+// block (profiles/rows_pass_experiments_r02.txt).  CYLON_RP_THREADS=512|1024 forces one.
+static int rp_threads(int ncols) {
+  static const int forced = [] {
+    const char *e = std::getenv("CYLON_RP_THREADS");
+    const int t = e ? std::atoi(e) : 0;
+    return t == 512 || t == 1024 ? t : 0;
+  }();
+  return forced ? forced : (ncols <= 2 ? 512 : 1024);
+}
+
+static RPGeometry rp_geometry(int64_t n, int ncols) {
+  const int threads = rp_threads(ncols);
+  const int64_t tile = (int64_t)threads * kRPItems;
+  const int64_t tiles = std::max<int64_t>(1, (n + tile - 1) / tile);
+  const int64_t want = 2 * kNumCUs * (1024 / threads);  // two rounds of resident blocks (16 waves per CU)
   const int64_t nb = tiles < want ? tiles : want;
   RPGeometry g;
-  g.rows_per_block = ((tiles + nb - 1) / nb) * kRPTile;
+  g.rows_per_block = ((tiles + nb - 1) / nb) * tile;
   g.nblocks = std::max<int64_t>(1, (n + g.rows_per_block - 1) / g.rows_per_block);
   return g;
 }
 
-int64_t radix_rows_pass_workspace(int64_t n, int digit_bits) {
-  const RPGeometry g = rp_geometry(n);
-  const int64_t m = g.nblocks * (int64_t(1) << digit_bits);
-  return m + (m + 1) + scan_workspace(m);
+int64_t radix_rows_pass_workspace(int64_t n, int digit_bits) {  // covers both block sizes
+  int64_t ws = 0;
+  for (int ncols : {1, kMaxFusedCols}) {
+    const int64_t m = rp_geometry(n, ncols).nblocks * (int64_t(1) << digit_bits);
+    ws = std::max(ws, m + (m + 1) + scan_workspace(m));
+  }
+  return ws;
+}
+
+template <class Digit, int THREADS>
+static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit &dg, int digit_bits, uint32_t nb,
+                             const ColSet &cs, int64_t n, const int64_t *bh_scan) {
+  if (w8)
+    hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s,
+                       dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan);
+  else
+    hipLaunchKernelGGL((k_rows_pass<Digit, false, THREADS>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s,
+                       dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan);
 }
 
 template <class Digit>
@@ -339,7 +395,7 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
               "radix pass: key_xor is only valid for order-image digits");
   hipStream_t s = as_stream(stream);
   const uint32_t nb = 1u << digit_bits;
-  const RPGeometry g = rp_geometry(n);
+  const RPGeometry g = rp_geometry(n, ncols);
   const int64_t m = g.nblocks * (int64_t)nb;
   int64_t *bh = ws, *bh_scan = ws + m, *scan_ws = bh_scan + m + 1;
   hipLaunchKernelGGL(k_rp_hist<Digit>, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, n, nb,
@@ -356,12 +412,10 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   }
   bool w8 = true;
   for (int c = 0; c < ncols; ++c) w8 &= widths[c] == 8;
-  if (w8)
-    hipLaunchKernelGGL((k_rows_pass<Digit, true>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, digit_bits,
-                       nb, cs, n, g.rows_per_block, g.nblocks, (const int64_t *)bh_scan);
+  if (rp_threads(ncols) == 1024)
+    rows_pass_kernel<Digit, 1024>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
   else
-    hipLaunchKernelGGL((k_rows_pass<Digit, false>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg,
-                       digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, (const int64_t *)bh_scan);
+    rows_pass_kernel<Digit, 512>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
   HIP_LAUNCH_CHECK();
 }
 
