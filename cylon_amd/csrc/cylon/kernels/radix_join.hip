@@ -23,7 +23,9 @@
 //      owns a contiguous slice of the probe rows (wave-level scans only).
 // Partitions whose build side exceeds the LDS capacity are reported; the
 // caller then falls back to the global-table join.
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "stable_rank.hpp"
 
@@ -187,10 +189,24 @@ __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) 
 // with vmcnt(0) for all outstanding loads AND stores: gfx9 counts both on one
 // counter).  Issuing several columns' loads per wait instead (more VGPRs, fewer
 // waves) measured slower -- profiles/rows_pass_experiments_r02.txt.
+// Debug phase stamps (CYLON_RP_STAMPS=1, rows_pass_launch): wave 0 of block 0 records the
+// shader clock at each phase boundary of its first kRPStampTiles tiles; nullptr otherwise.
+constexpr int kRPStampTiles = 64, kRPStampSlots = 16;
+#define RP_STAMP(slot)                                                                               \
+  do {                                                                                               \
+    if (stamps != nullptr && blockIdx.x == 0 && tix < kRPStampTiles && (slot) < kRPStampSlots) {     \
+      unsigned long long t_;                                                                         \
+      __builtin_amdgcn_sched_barrier(0);                                                             \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                    \
+      __builtin_amdgcn_sched_barrier(0);                                                             \
+      if (threadIdx.x == 0) stamps[tix * kRPStampSlots + (slot)] = t_;                               \
+    }                                                                                                \
+  } while (0)
+
 template <class Digit, bool W8, int THREADS>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_rows_pass(
     Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
-    const int64_t *__restrict__ bh_scan) {
+    const int64_t *__restrict__ bh_scan, unsigned long long *__restrict__ stamps) {
   constexpr int WAVES = THREADS / kWave;
   constexpr int TILE = THREADS * kRPItems;
   constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;  // buckets per thread in the offset scan
@@ -220,11 +236,14 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     if (i < end) kv[k] = (uint64_t)digit.keys[i];
   }
   for (int64_t tile = begin; tile < end; tile += TILE) {
+    const int tix = (int)((tile - begin) / TILE);
+    RP_STAMP(0);
     const int cnt = (int)((end - tile) < TILE ? (end - tile) : TILE);
     uint32_t pl[kRPItems];  // digit, then (in-wave rank << 16) | digit, then sorted slot; ~0 = inactive
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k)
       pl[k] = (wrow + k * kWave + lane < cnt) ? digit.of_key((int64_t)kv[k]) : 0xffffffffu;
+    RP_STAMP(1);
     for (uint32_t q = threadIdx.x; q < WAVES * nbuckets; q += blockDim.x) wcnt[q] = 0;
     __syncthreads();  // also orders the previous tile's stage reads before the counters reuse it
 #pragma unroll
@@ -246,6 +265,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       pl[k] = active ? (((base + rank) << 16) | p) : 0xffffffffu;
     }
     __syncthreads();
+    RP_STAMP(2);
     {  // thread owns buckets [t*BPT, t*BPT+BPT): exclusive prefix over waves (in place), then a
        // block scan of the thread totals
       uint32_t loc[BPT];
@@ -274,6 +294,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       if (threadIdx.x == THREADS - 1) toff[nbuckets] = ex + total;
     }
     __syncthreads();
+    RP_STAMP(3);
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k) {
       if (pl[k] == 0xffffffffu) continue;
@@ -283,6 +304,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       pl[k] = pos;
     }
     __syncthreads();
+    RP_STAMP(4);
     int64_t dst[kRPItems];  // destination of sorted slot j = threadIdx.x + q * THREADS
 #pragma unroll
     for (int q = 0; q < kRPItems; ++q) {
@@ -293,6 +315,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       }
     }
     __syncthreads();  // counters / digits dead: the union becomes the column stage
+    RP_STAMP(5);
     const int64_t next = tile + TILE;
     // load column c+1 while column c streams out of the stage
     uint64_t v[kRPItems];
@@ -307,6 +330,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       for (int k = 0; k < kRPItems; ++k)
         if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
       __syncthreads();
+      RP_STAMP(6 + 2 * c);
       if (c + 1 < cols.n) {  // prefetch column c+1 of this tile
         const uint8_t *in = cols.in[c + 1];
         const int w1 = cols.width[c + 1];
@@ -326,6 +350,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         if (j < cnt) stw<W8>(out, dst[q], w, ldw<W8>(st, j, w));
       }
       __syncthreads();
+      RP_STAMP(7 + 2 * c);
     }
     for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] += toff[p + 1] - toff[p];
   }
@@ -373,12 +398,47 @@ int64_t radix_rows_pass_workspace(int64_t n, int digit_bits) {  // covers both b
 template <class Digit, int THREADS>
 static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit &dg, int digit_bits, uint32_t nb,
                              const ColSet &cs, int64_t n, const int64_t *bh_scan) {
+  static const bool stamp = std::getenv("CYLON_RP_STAMPS") != nullptr;  // debug: phase stamps to stderr
+  unsigned long long *st = nullptr;
+  if (stamp) {
+    HIP_CHECK(hipStreamSynchronize(s));
+    HIP_CHECK(hipMalloc(&st, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
+    HIP_CHECK(hipMemset(st, 0, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
+  }
   if (w8)
     hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s,
-                       dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan);
+                       dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, st);
   else
     hipLaunchKernelGGL((k_rows_pass<Digit, false, THREADS>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s,
-                       dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan);
+                       dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, st);
+  if (stamp) {
+    HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<unsigned long long> h(kRPStampTiles * kRPStampSlots);
+    HIP_CHECK(hipMemcpy(h.data(), st, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipFree(st));
+    // mean cycles of each phase over the full tiles after the first (tile i: slot j - slot j-1,
+    // slot 0 of tile i+1 closes the last column)
+    const int last = 7 + 2 * (cs.n - 1);
+    double sum[kRPStampSlots] = {0};
+    int tiles = 0;
+    for (int t = 1; t + 1 < kRPStampTiles; ++t) {
+      if (h[(t + 1) * kRPStampSlots] == 0) break;
+      for (int j = 1; j <= last && j < kRPStampSlots; ++j)
+        sum[j] += (double)(h[t * kRPStampSlots + j] - h[t * kRPStampSlots + j - 1]);
+      sum[0] += (double)(h[(t + 1) * kRPStampSlots] - h[t * kRPStampSlots]);
+      ++tiles;
+    }
+    if (tiles > 0) {
+      std::fprintf(stderr, "rp_stamps threads=%d ncols=%d bits=%d tiles=%d tile_total=%.0f |", THREADS, cs.n,
+                   digit_bits, tiles, sum[0] / tiles);
+      static const char *names[] = {"", "keys", "rank", "scan", "slot", "dst"};
+      for (int j = 1; j <= last && j < kRPStampSlots; ++j) {
+        if (j <= 5) std::fprintf(stderr, " %s=%.0f", names[j], sum[j] / tiles);
+        else std::fprintf(stderr, " c%d_%s=%.0f", (j - 6) / 2, (j % 2 == 0) ? "stage" : "scatter", sum[j] / tiles);
+      }
+      std::fprintf(stderr, "\n");
+    }
+  }
 }
 
 template <class Digit>
