@@ -38,6 +38,14 @@ void register_extended_ops(py::module &m) {
 
   m.def("index_lookup", &ops::IndexLookup, py::arg("ctx"), py::arg("index"), py::arg("labels"), rel);
 
+  // ---- device self-check behind the radix passes' wave-atomic stable ranking (radix_join.hip)
+  m.def("lds_lane_order_violations", [](const std::string &device, int blocks, int rounds) {
+    ops::Exec ex{at::Device(device)};
+    CYLON_CHECK(ex.gpu, Code::Invalid, "lds_lane_order_violations needs a GPU device");
+    return hip::lds_lane_order_violations(blocks, rounds, ex.stream);
+  }, py::arg("device") = "cuda:0", py::arg("blocks") = 256, py::arg("rounds") = 4096,
+     py::call_guard<py::gil_scoped_release>());
+
   // ---- validity bitmaps <-> byte masks at the Arrow boundary (bitmap.hip)
   m.def("pack_validity", [](at::Tensor bytes) {
     ops::Exec ex(bytes.device());

@@ -25,6 +25,8 @@
 // caller then falls back to the global-table join.
 #include <cstdio>
 #include <cstdlib>
+#include <string>
+#include <type_traits>
 #include <vector>
 
 #include "stable_rank.hpp"
@@ -41,6 +43,7 @@ constexpr int kRJMaxDigitBits = 10;
 constexpr int kRJRowArea = 155520;               // LDS bytes for the staged build rows (1 block per CU)
 constexpr int kRJMaxRows = 5120;                 // build rows per partition (5 per thread)
 constexpr int kRJThreads = 1024;
+constexpr int kRankBallot = 0, kRankBlockAtomic = 1, kRankWaveAtomic = 2;
 constexpr int kRJWaves = kRJThreads / kWave;
 
 struct ColSet {
@@ -203,7 +206,11 @@ constexpr int kRPStampTiles = 64, kRPStampSlots = 16;
     }                                                                                                \
   } while (0)
 
-template <class Digit, bool W8, int THREADS>
+// RANK: kRankBallot (stable wave64 ballot match), kRankBlockAtomic (one LDS atomic per row
+// on block-wide counters: unstable), kRankWaveAtomic (LDS atomics on the wave's own packed
+// 16-bit counters: stable exactly when one instruction's same-address atomics return in lane
+// order -- tools/lds_atomic_order.hip measures that on the device).
+template <class Digit, bool W8, int THREADS, int RANK>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_rows_pass(
     Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
     const int64_t *__restrict__ bh_scan, unsigned long long *__restrict__ stamps) {
@@ -216,6 +223,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16, sdig[TILE] u16}
   __shared__ uint32_t wsum[WAVES];
   uint16_t *wcnt = reinterpret_cast<uint16_t *>(ustage);
+  constexpr bool STABLE = RANK != kRankBlockAtomic;
+  uint32_t *bcnt = reinterpret_cast<uint32_t *>(ustage);  // block-atomic ranking: block-wide counters
+  static_assert(WAVES * kRPMaxBuckets * 2 >= kRPMaxBuckets * 4, "block counters must fit the wave counters");
   uint16_t *sdig = wcnt + WAVES * kRPMaxBuckets;
   uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
 
@@ -244,8 +254,27 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     for (int k = 0; k < kRPItems; ++k)
       pl[k] = (wrow + k * kWave + lane < cnt) ? digit.of_key((int64_t)kv[k]) : 0xffffffffu;
     RP_STAMP(1);
-    for (uint32_t q = threadIdx.x; q < WAVES * nbuckets; q += blockDim.x) wcnt[q] = 0;
+    if (STABLE) {
+      for (uint32_t q = threadIdx.x; q < WAVES * nbuckets; q += blockDim.x) wcnt[q] = 0;
+    } else {
+      for (uint32_t q = threadIdx.x; q < nbuckets; q += blockDim.x) bcnt[q] = 0;
+    }
     __syncthreads();  // also orders the previous tile's stage reads before the counters reuse it
+    if (!STABLE) {
+      // order inside a bucket's run is free (join partitions): one LDS atomic per row
+      // replaces the nbits ballots of the stable match
+#pragma unroll
+      for (int k = 0; k < kRPItems; ++k)
+        if (pl[k] != 0xffffffffu) pl[k] |= atomicAdd(&bcnt[pl[k]], 1u) << 16;
+    } else if (RANK == kRankWaveAtomic) {
+      uint32_t *myw = reinterpret_cast<uint32_t *>(mycnt);  // nbuckets is even: word-aligned rows
+#pragma unroll
+      for (int k = 0; k < kRPItems; ++k)
+        if (pl[k] != 0xffffffffu) {
+          const uint32_t p = pl[k], sh = (p & 1u) * 16u;
+          pl[k] |= ((atomicAdd(&myw[p >> 1], 1u << sh) >> sh) & 0xffffu) << 16;
+        }
+    } else
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k) {
       const bool active = pl[k] != 0xffffffffu;
@@ -276,11 +305,15 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         loc[i] = total;
         uint32_t run = 0;
         if (p < nbuckets) {
+          if (STABLE) {
 #pragma unroll
-          for (int w = 0; w < WAVES; ++w) {
-            const uint32_t c = wcnt[w * nbuckets + p];
-            wcnt[w * nbuckets + p] = (uint16_t)run;
-            run += c;
+            for (int w = 0; w < WAVES; ++w) {
+              const uint32_t c = wcnt[w * nbuckets + p];
+              wcnt[w * nbuckets + p] = (uint16_t)run;
+              run += c;
+            }
+          } else {
+            run = bcnt[p];
           }
         }
         total += run;
@@ -299,7 +332,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     for (int k = 0; k < kRPItems; ++k) {
       if (pl[k] == 0xffffffffu) continue;
       const uint32_t p = pl[k] & 0xffffu;
-      const uint32_t pos = toff[p] + wcnt[wave * nbuckets + p] + (pl[k] >> 16);
+      const uint32_t pos = toff[p] + (STABLE ? (uint32_t)wcnt[wave * nbuckets + p] : 0u) + (pl[k] >> 16);
       sdig[pos] = (uint16_t)p;
       pl[k] = pos;
     }
@@ -374,6 +407,70 @@ static int rp_threads(int ncols) {
   return forced ? forced : (ncols <= 2 ? 512 : 1024);
 }
 
+// Self-check of kRankWaveAtomic's precondition: every lane of a wave adds 1 to a
+// pseudo-random packed 16-bit counter of the wave's own row (bucket ranges of 2 ... 1024,
+// so many lanes share an address or a word) and compares the returned count with the
+// stable rank from ballots (count before + #lower lanes in the same bucket).  gfx950
+// returns same-address LDS atomics of one instruction in lane order: 0 violations in
+// 4.3e10 lane-ops (tools/lds_atomic_order.hip, profiles/rank_variants_r02.txt).
+constexpr int kLOThreads = 256;
+__global__ __launch_bounds__(kLOThreads) void k_lane_order_check(int rounds, unsigned long long *bad) {
+  __shared__ uint32_t cnt[(kLOThreads / kWave) * (kRPMaxBuckets / 2)];
+  const int wave = threadIdx.x / kWave, lane = lane_id();
+  const uint64_t lt = lanemask_lt();
+  uint32_t *mine = cnt + wave * (kRPMaxBuckets / 2);
+  unsigned long long nbad = 0;
+  for (int r0 = 0; r0 < rounds; r0 += 256) {  // 16-bit halves: restart every 256 rounds
+    for (int q = lane; q < kRPMaxBuckets / 2; q += kWave) mine[q] = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (int r = r0; r < r0 + 256 && r < rounds; ++r) {
+      const int nbits = 1 + (r % 10);
+      const uint32_t b = (uint32_t)hashing::fmix64(((uint64_t)blockIdx.x << 40) ^ ((uint64_t)r << 12) ^ threadIdx.x) &
+                         ((1u << nbits) - 1u);
+      uint64_t m = ~0ull;
+      for (int bit = 0; bit < nbits; ++bit) {
+        const uint32_t x = (b >> bit) & 1u;
+        const uint64_t bb = __ballot(x);
+        m &= x ? bb : ~bb;
+      }
+      const uint32_t sh = (b & 1u) * 16u;
+      const uint32_t before = (mine[b >> 1] >> sh) & 0xffffu;
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t got = (atomicAdd(&mine[b >> 1], 1u << sh) >> sh) & 0xffffu;
+      __builtin_amdgcn_wave_barrier();
+      nbad += got != before + (uint32_t)__popcll(m & lt);
+    }
+  }
+  for (int d = kWave / 2; d > 0; d >>= 1) nbad += __shfl_xor(nbad, d, kWave);
+  if (lane == 0 && nbad) atomicAdd(bad, nbad);
+}
+
+int64_t lds_lane_order_violations(int blocks, int rounds, void *stream) {
+  hipStream_t s = as_stream(stream);
+  unsigned long long *d = nullptr, h = 0;
+  HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&d), sizeof(h)));
+  HIP_CHECK(hipMemsetAsync(d, 0, sizeof(h), s));
+  hipLaunchKernelGGL(k_lane_order_check, dim3((unsigned)blocks), dim3(kLOThreads), 0, s, rounds, d);
+  HIP_LAUNCH_CHECK();
+  HIP_CHECK(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  HIP_CHECK(hipFree(d));
+  return (int64_t)h;
+}
+
+// Stable ranking method: wave-atomic when the device passes the lane-order self-check
+// (run once per process), else ballots.  CYLON_RP_RANK=wave|ballot forces one.
+static bool rp_wave_atomic(hipStream_t s) {
+  static const int forced = [] {
+    const char *e = std::getenv("CYLON_RP_RANK");
+    if (!e) return -1;
+    return std::string(e) == "wave" ? 1 : (std::string(e) == "ballot" ? 0 : -1);
+  }();
+  if (forced >= 0) return forced == 1;
+  static const bool ok = lds_lane_order_violations(64, 1024, s) == 0;
+  return ok;
+}
+
 static RPGeometry rp_geometry(int64_t n, int ncols) {
   const int threads = rp_threads(ncols);
   const int64_t tile = (int64_t)threads * kRPItems;
@@ -395,7 +492,7 @@ int64_t radix_rows_pass_workspace(int64_t n, int digit_bits) {  // covers both b
   return ws;
 }
 
-template <class Digit, int THREADS>
+template <class Digit, int THREADS, int RANK>
 static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit &dg, int digit_bits, uint32_t nb,
                              const ColSet &cs, int64_t n, const int64_t *bh_scan) {
   static const bool stamp = std::getenv("CYLON_RP_STAMPS") != nullptr;  // debug: phase stamps to stderr
@@ -406,10 +503,10 @@ static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const 
     HIP_CHECK(hipMemset(st, 0, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
   }
   if (w8)
-    hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s,
+    hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS, RANK>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s,
                        dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, st);
   else
-    hipLaunchKernelGGL((k_rows_pass<Digit, false, THREADS>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s,
+    hipLaunchKernelGGL((k_rows_pass<Digit, false, THREADS, RANK>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s,
                        dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, st);
   if (stamp) {
     HIP_CHECK(hipStreamSynchronize(s));
@@ -429,8 +526,8 @@ static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const 
       ++tiles;
     }
     if (tiles > 0) {
-      std::fprintf(stderr, "rp_stamps threads=%d ncols=%d bits=%d tiles=%d tile_total=%.0f |", THREADS, cs.n,
-                   digit_bits, tiles, sum[0] / tiles);
+      std::fprintf(stderr, "rp_stamps threads=%d stable=%d ncols=%d bits=%d tiles=%d tile_total=%.0f |", THREADS,
+                   RANK, cs.n, digit_bits, tiles, sum[0] / tiles);
       static const char *names[] = {"", "keys", "rank", "scan", "slot", "dst"};
       for (int j = 1; j <= last && j < kRPStampSlots; ++j) {
         if (j <= 5) std::fprintf(stderr, " %s=%.0f", names[j], sum[j] / tiles);
@@ -441,9 +538,13 @@ static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const 
   }
 }
 
-template <class Digit>
+// stable = false (join partitions only) ranks rows with LDS atomics: rows of one
+// bucket keep no particular order inside a tile's run.  Instantiated for PartDigit
+// only; every other digit (sort, shuffle, range join) needs the stable order.
+template <class Digit, bool CAN_UNSTABLE = std::is_same<Digit, PartDigit>::value>
 static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const uint8_t *const *in, uint8_t *const *out,
-                             const int *widths, int ncols, int64_t *ws, void *stream, uint64_t key_xor = 0) {
+                             const int *widths, int ncols, int64_t *ws, void *stream, uint64_t key_xor = 0,
+                             bool stable = true) {
   if (n == 0) return;
   CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
   CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
@@ -472,17 +573,27 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   }
   bool w8 = true;
   for (int c = 0; c < ncols; ++c) w8 &= widths[c] == 8;
-  if (rp_threads(ncols) == 1024)
-    rows_pass_kernel<Digit, 1024>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
-  else
-    rows_pass_kernel<Digit, 512>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
+  CYLON_CHECK(stable || CAN_UNSTABLE, Code::Invalid, "radix pass: only partition digits may rank unstably");
+  const bool big = rp_threads(ncols) == 1024;
+  if (CAN_UNSTABLE && !stable) {
+    constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankBallot;
+    if (big) rows_pass_kernel<Digit, 1024, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
+    else rows_pass_kernel<Digit, 512, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
+  } else if (rp_wave_atomic(s)) {
+    if (big) rows_pass_kernel<Digit, 1024, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
+    else rows_pass_kernel<Digit, 512, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
+  } else {
+    if (big) rows_pass_kernel<Digit, 1024, kRankBallot>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
+    else rows_pass_kernel<Digit, 512, kRankBallot>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
+  }
   HIP_LAUNCH_CHECK();
 }
 
 void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, int digit_bits, const uint8_t *const *in,
-                     uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream) {
+                     uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream, bool stable) {
   const uint32_t nb = 1u << digit_bits;
-  rows_pass_launch(PartDigit{keys, total_bits, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws, stream);
+  rows_pass_launch(PartDigit{keys, total_bits, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws, stream, 0,
+                   stable);
 }
 
 void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_bits, const uint8_t *const *in,

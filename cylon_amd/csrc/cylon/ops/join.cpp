@@ -16,6 +16,7 @@
 //   3. outer completion: matched flags (mark_indices) + compaction of the
 //      unmatched rows of the preserved side(s), appended with -1 partners.
 //   4. materialisation: one fused gather launch per side (K4).
+#include <cstdlib>
 #include <limits>
 
 #include "util.hpp"
@@ -199,7 +200,15 @@ static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Te
   at::Tensor offs;
   const size_t nslots = cur.size();
   std::vector<int> packed;
-  cur = RadixPartition(ex, std::move(cur), widths, bits, &offs, range, packs_validity(t) ? &packed : nullptr);
+  // hash partitions: the LDS join ignores row order inside a partition, so the first LSD pass
+  // ranks with LDS atomics (later passes must keep its order; CYLON_RP_STABLE=1 restores the
+  // stable ballot ranking everywhere for A/B runs)
+  static const bool force_stable = [] {
+    const char *e = std::getenv("CYLON_RP_STABLE");
+    return e && e[0] == '1';
+  }();
+  cur = RadixPartition(ex, std::move(cur), widths, bits, &offs, range, packs_validity(t) ? &packed : nullptr,
+                       range != nullptr || force_stable);
   RadixSide s;
   s.keys = cur[0];
   s.offs = offs;

@@ -67,7 +67,7 @@ std::vector<at::Tensor> UnpackByteColumns(const Exec &ex, const BytePacking &bp,
 
 std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> cur, const std::vector<int> &widths,
                                        int bits, at::Tensor *offs, const RangeSpec *range,
-                                       std::vector<int> *keep_packed) {
+                                       std::vector<int> *keep_packed, bool stable) {
   CYLON_CHECK(ex.gpu, Code::Invalid, "RadixPartition is a device path");
   CYLON_CHECK(!cur.empty() && cur.size() == widths.size() && widths[0] == 8, Code::Invalid,
               "RadixPartition: column 0 must be the int64 key");
@@ -101,7 +101,8 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
                                  ptr<int64_t>(ws), ex.stream);
     else
       hip::radix_rows_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, bits, shift, db, in.data(),
-                           out.data(), pw.data(), (int)cur.size(), ptr<int64_t>(ws), ex.stream);
+                           out.data(), pw.data(), (int)cur.size(), ptr<int64_t>(ws), ex.stream,
+                           stable || ps > 0);  // LSD: every pass after the first keeps the order it receives
     cur = std::move(nxt);
     shift += db;
   }

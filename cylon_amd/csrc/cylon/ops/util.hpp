@@ -61,12 +61,14 @@ struct RangeSpec {
   uint64_t flip = 0, mn = 0;
   int rshift = 0;
 };
+// stable = false lets the first LSD pass rank with LDS atomics (rows of one partition
+// come out in no particular order: the hash join only).
 // keep_packed != nullptr: validity-style 1-byte columns that were packed 8 per 8-byte word
 // for the passes stay packed -- their slots come back undefined, the words are appended
 // to the result and *keep_packed lists the packed column indices in byte order.
 std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> cols, const std::vector<int> &widths,
                                        int bits, at::Tensor *offs, const RangeSpec *range = nullptr,
-                                       std::vector<int> *keep_packed = nullptr);
+                                       std::vector<int> *keep_packed = nullptr, bool stable = true);
 
 // Row-moving passes (k_rows_pass) take their all-8-byte path only when every moved
 // column is 8 bytes wide; validity bytes beside 8-byte columns therefore travel packed

@@ -25,6 +25,37 @@ def test_extension_is_native_and_on_gpu(gpu_ctx):
     assert t.device.startswith("cuda")
 
 
+def test_lds_atomics_return_in_lane_order(gpu_ctx):
+    """Precondition of the radix passes' wave-atomic stable ranking: same-address LDS atomics of
+    one wave64 instruction return in lane order (the passes self-check this once per process and
+    fall back to ballot ranking otherwise; here 256 blocks x 4096 rounds = 6.7e7 lane-ops)."""
+    assert C.lds_lane_order_violations("cuda:0", 256, 4096) == 0
+
+
+@pytest.mark.parametrize("rank", ["wave", "ballot"])
+def test_radix_sort_stable_under_both_rankings(gpu_ctx, rank):
+    """The row-moving sort (stable LSD passes) under each stable ranking method, in a child
+    process (the choice is fixed per process): ties keep their input order."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import numpy as np, pyarrow as pa\n"
+        "from cylon_amd import CylonContext, Table\n"
+        "ctx = CylonContext(config=None, distributed=False, device='cuda:0')\n"
+        "rng = np.random.default_rng(3)\n"
+        "n = 400_000\n"
+        "k = rng.integers(-300, 300, n)\n"
+        "t = Table(pa.table({'k': k, 'p': np.arange(n)}), ctx)\n"
+        "s = t.sort('k').to_pandas()\n"
+        "ref = np.lexsort((np.arange(n), k))\n"
+        "assert np.array_equal(s['p'].to_numpy(), ref), 'unstable'\n"
+        "print('ok')\n")
+    env = dict(os.environ, CYLON_RP_RANK=rank, CYLON_RADIX_SORT_MIN_ROWS="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]
+
+
 @pytest.mark.parametrize("nparts", [1, 2, 3, 4, 7, 8, 64, 1000])
 def test_partition_ids_and_split_match_cpu(gpu_ctx, ctx, nparts):
     rng = np.random.default_rng(nparts)
