@@ -723,15 +723,16 @@ __device__ __forceinline__ uint32_t rj_bucket(int64_t k) {
 constexpr int kRJRowsPerThread = kRJMaxRows / kRJThreads;
 static_assert(kRJRowsPerThread * kRJThreads == kRJMaxRows, "build rows per thread");
 constexpr int kRJProbeRounds = 1;  // probe rounds of 64 rows per wave prefetched into VGPRs
-constexpr int kRJBucketsPerThread = kRJBuckets / kRJThreads;
 
 // bst[0..kRJBuckets) holds per-bucket counts on entry (exclusive starts on exit), bst[kRJBuckets] = total
+template <int THREADS = kRJThreads>
 __device__ __forceinline__ void rj_scan_buckets(uint16_t *bst, uint32_t *wsum) {
+  constexpr int BPT = kRJBuckets / THREADS;
   const int lane = lane_id(), wave = threadIdx.x / kWave;
-  uint32_t c[kRJBucketsPerThread], t = 0;
+  uint32_t c[BPT], t = 0;
 #pragma unroll
-  for (int j = 0; j < kRJBucketsPerThread; ++j) {
-    c[j] = bst[threadIdx.x * kRJBucketsPerThread + j];
+  for (int j = 0; j < BPT; ++j) {
+    c[j] = bst[threadIdx.x * BPT + j];
     t += c[j];
   }
   uint32_t inc = t;
@@ -745,11 +746,11 @@ __device__ __forceinline__ void rj_scan_buckets(uint16_t *bst, uint32_t *wsum) {
   uint32_t off = inc - t;
   for (int w = 0; w < wave; ++w) off += wsum[w];
 #pragma unroll
-  for (int j = 0; j < kRJBucketsPerThread; ++j) {
-    bst[threadIdx.x * kRJBucketsPerThread + j] = (uint16_t)off;
+  for (int j = 0; j < BPT; ++j) {
+    bst[threadIdx.x * BPT + j] = (uint16_t)off;
     off += c[j];
   }
-  if (threadIdx.x == kRJThreads - 1) bst[kRJBuckets] = (uint16_t)off;
+  if (threadIdx.x == THREADS - 1) bst[kRJBuckets] = (uint16_t)off;
 }
 
 // count one bucket's rank for a new row: 16-bit counters packed in pairs
@@ -766,15 +767,23 @@ __device__ __forceinline__ uint32_t rj_count(const uint16_t *bst, const int64_t 
   return c;
 }
 
-__global__ __launch_bounds__(kRJThreads, 4) void k_rj_count(const int64_t *__restrict__ pkeys,
-                                                         const int64_t *__restrict__ poffs,
-                                                         const int64_t *__restrict__ bkeys,
-                                                         const int64_t *__restrict__ boffs, int64_t nparts, int cap,
-                                                         int64_t *__restrict__ counts, int *overflow) {
+// Count kernel block: 512 threads (10 build + 10 probe keys per thread) so two or three
+// blocks share a CU (48 KB LDS each) and one block's key loads overlap another's probing;
+// the 1024-thread version ran one latency-bound block per CU (128 VGPRs).
+constexpr int kRCThreads = 512;
+constexpr int kRCWaves = kRCThreads / kWave;
+constexpr int kRCRowsPerThread = kRJMaxRows / kRCThreads;
+static_assert(kRCRowsPerThread * kRCThreads == kRJMaxRows, "count rows per thread");
+
+__global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_rj_count(const int64_t *__restrict__ pkeys,
+                                                      const int64_t *__restrict__ poffs,
+                                                      const int64_t *__restrict__ bkeys,
+                                                      const int64_t *__restrict__ boffs, int64_t nparts, int cap,
+                                                      int64_t *__restrict__ counts, int *overflow) {
   __shared__ __attribute__((aligned(16))) uint16_t bst[kRJBuckets + 8];
   __shared__ int64_t skeys[kRJMaxRows];
-  __shared__ uint32_t wsum[kRJWaves];
-  __shared__ unsigned long long csum[kRJWaves];
+  __shared__ uint32_t wsum[kRCWaves];
+  __shared__ unsigned long long csum[kRCWaves];
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
     const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
     const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
@@ -789,38 +798,45 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_count(const int64_t *__res
       if (threadIdx.x == 0) counts[p] = 0;
       continue;
     }
-    int64_t bk[kRJRowsPerThread], pk[kRJRowsPerThread];
-#pragma unroll
-    for (int i = 0; i < kRJRowsPerThread; ++i) {
-      const int r = threadIdx.x + i * kRJThreads;
-      if (r < nr) bk[i] = bkeys[rb + r];
-      if (r < nl) pk[i] = pkeys[lb + r];
-    }
+    // build keys are read twice (claim, then place): the second read hits L2 and the block
+    // keeps only 16-bit ranks in registers (two 512-thread blocks per CU without spills)
     __syncthreads();  // previous partition done with bst / skeys / csum
     for (int s = threadIdx.x; s < kRJBuckets / 2; s += blockDim.x) reinterpret_cast<uint32_t *>(bst)[s] = 0;
     __syncthreads();
-    uint32_t rk[kRJRowsPerThread];
+    uint32_t rk[kRCRowsPerThread];
 #pragma unroll
-    for (int i = 0; i < kRJRowsPerThread; ++i)
-      if (threadIdx.x + i * kRJThreads < nr) rk[i] = rj_claim(bst, rj_bucket(bk[i]));
+    for (int i = 0; i < kRCRowsPerThread; ++i) {
+      const int r = threadIdx.x + i * kRCThreads;
+      if (r < nr) rk[i] = rj_claim(bst, rj_bucket(bkeys[rb + r]));
+    }
     __syncthreads();
-    rj_scan_buckets(bst, wsum);
+    rj_scan_buckets<kRCThreads>(bst, wsum);
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < kRJRowsPerThread; ++i)
-      if (threadIdx.x + i * kRJThreads < nr) skeys[bst[rj_bucket(bk[i])] + rk[i]] = bk[i];
+    for (int i = 0; i < kRCRowsPerThread; ++i) {
+      const int r = threadIdx.x + i * kRCThreads;
+      if (r < nr) {
+        const int64_t k = bkeys[rb + r];
+        skeys[bst[rj_bucket(k)] + rk[i]] = k;
+      }
+    }
     __syncthreads();
     unsigned long long c = 0;
+    for (int64_t l0 = threadIdx.x; l0 < nl; l0 += 4 * kRCThreads) {  // 4 probe loads in flight
+      int64_t pk[4];
 #pragma unroll
-    for (int i = 0; i < kRJRowsPerThread; ++i)
-      if (threadIdx.x + i * kRJThreads < nl) c += rj_count(bst, skeys, pk[i]);
-    for (int64_t l = threadIdx.x + kRJMaxRows; l < nl; l += blockDim.x) c += rj_count(bst, skeys, pkeys[lb + l]);
+      for (int u = 0; u < 4; ++u)
+        if (l0 + u * kRCThreads < nl) pk[u] = pkeys[lb + l0 + u * kRCThreads];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (l0 + u * kRCThreads < nl) c += rj_count(bst, skeys, pk[u]);
+    }
     for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
     if (lane_id() == 0) csum[threadIdx.x / kWave] = c;
     __syncthreads();
     if (threadIdx.x == 0) {
       unsigned long long tot = 0;
-      for (int w = 0; w < kRJWaves; ++w) tot += csum[w];
+      for (int w = 0; w < kRCWaves; ++w) tot += csum[w];
       counts[p] = (int64_t)tot;
     }
   }
@@ -1034,8 +1050,8 @@ void radix_join_count(const int64_t *pkeys, const int64_t *poffs, const int64_t 
   CYLON_CHECK(cap > 0 && cap <= kRJMaxRows, Code::Invalid, "radix join capacity " << cap);
   hipStream_t s = as_stream(stream);
   HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
-  hipLaunchKernelGGL(k_rj_count, dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts,
-                     (int)cap, counts, overflow);
+  hipLaunchKernelGGL(k_rj_count, dim3((unsigned)std::min<int64_t>(nparts, kNumCUs * 12)), dim3(kRCThreads), 0, s,
+                     pkeys, poffs, bkeys, boffs, nparts, (int)cap, counts, overflow);
   HIP_LAUNCH_CHECK();
 }
 
