@@ -460,16 +460,17 @@ int64_t lds_lane_order_violations(int blocks, int rounds, void *stream) {
 
 // Stable ranking method: wave-atomic when the device passes the lane-order self-check
 // (run once per process), else ballots.  CYLON_RP_RANK=wave|ballot forces one.
-static bool rp_wave_atomic(hipStream_t s) {
+bool lds_lane_order_ok(void *stream) {
   static const int forced = [] {
     const char *e = std::getenv("CYLON_RP_RANK");
     if (!e) return -1;
     return std::string(e) == "wave" ? 1 : (std::string(e) == "ballot" ? 0 : -1);
   }();
   if (forced >= 0) return forced == 1;
-  static const bool ok = lds_lane_order_violations(64, 1024, s) == 0;
+  static const bool ok = lds_lane_order_violations(64, 1024, stream) == 0;
   return ok;
 }
+static bool rp_wave_atomic(hipStream_t s) { return lds_lane_order_ok(reinterpret_cast<void *>(s)); }
 
 static RPGeometry rp_geometry(int64_t n, int ncols) {
   const int threads = rp_threads(ncols);
@@ -878,7 +879,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
     const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
     if (nr == 0 || nl == 0 || nr > cap) continue;
     const int64_t obase = out_offs[p];
-    // ---- phase A: probe rows of this wave's slice into VGPRs (in flight during the build)
+    // ---- phase A: probe rows of this wave's slice into VGkRJProbeRoundss (in flight during the build)
     const int64_t per = (nl + kRJWaves - 1) / kRJWaves;  // each wave owns a contiguous probe slice
     const int64_t s0 = lb + std::min<int64_t>(nl, wave * per);
     const int64_t s1 = lb + std::min<int64_t>(nl, (wave + 1) * per);

@@ -56,7 +56,10 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(DigitFn digit, int64_t n
   for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) bh[(int64_t)p * nblocks + b] = hist[p];
 }
 
-template <class DigitFn, class SinkFn>
+// WAVE_ATOMIC: the wave's own LDS counters hand out ranks by atomicAdd (stable because gfx950
+// returns one instruction's same-address LDS atomics in lane order; radix_join.hip
+// lds_lane_order_ok checks that on the device), instead of nbits ballots per row.
+template <class DigitFn, class SinkFn, bool WAVE_ATOMIC>
 __global__ __launch_bounds__(kBlock) void k_stable_rank(DigitFn digit, SinkFn sink, int64_t n, uint32_t nbuckets,
                                                         int nbits, int64_t rows_per_block, int64_t nblocks,
                                                         const int64_t *__restrict__ bh_scan) {
@@ -86,6 +89,11 @@ __global__ __launch_bounds__(kBlock) void k_stable_rank(DigitFn digit, SinkFn si
       const int64_t i = wbase + (int64_t)k * kWave + lane;
       const bool active = i < end;
       const uint32_t p = active ? digit(i) : 0u;
+      if (WAVE_ATOMIC) {
+        pk[k] = active ? p : 0xffffffffu;
+        lk[k] = active ? atomicAdd(&mycnt[p], 1u) : 0u;
+        continue;
+      }
       uint64_t m = __ballot(active);
       for (int bit = 0; bit < nbits; ++bit) {
         const uint32_t x = (p >> bit) & 1u;
@@ -146,9 +154,14 @@ void stable_rank_launch(DigitFn digit, SinkFn sink, int64_t n, uint32_t nbuckets
   exclusive_scan(bh, m, bh_scan, scan_ws, reinterpret_cast<void *>(s));
   int nbits = 0;
   while ((1u << nbits) < nbuckets) ++nbits;
-  hipLaunchKernelGGL((k_stable_rank<DigitFn, SinkFn>), dim3((unsigned)g.nblocks), dim3(kBlock),
-                     rank_lds_bytes(nbuckets), s, digit, sink, n, nbuckets, nbits, g.rows_per_block, g.nblocks,
-                     bh_scan);
+  if (lds_lane_order_ok(reinterpret_cast<void *>(s)))
+    hipLaunchKernelGGL((k_stable_rank<DigitFn, SinkFn, true>), dim3((unsigned)g.nblocks), dim3(kBlock),
+                       rank_lds_bytes(nbuckets), s, digit, sink, n, nbuckets, nbits, g.rows_per_block, g.nblocks,
+                       bh_scan);
+  else
+    hipLaunchKernelGGL((k_stable_rank<DigitFn, SinkFn, false>), dim3((unsigned)g.nblocks), dim3(kBlock),
+                       rank_lds_bytes(nbuckets), s, digit, sink, n, nbuckets, nbits, g.rows_per_block, g.nblocks,
+                       bh_scan);
   HIP_LAUNCH_CHECK();
   if (bh_scan_out) *bh_scan_out = bh_scan;
   if (nblocks_out) *nblocks_out = g.nblocks;
