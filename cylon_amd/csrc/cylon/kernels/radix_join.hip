@@ -393,18 +393,20 @@ struct RPGeometry {
   int64_t nblocks, rows_per_block;
 };
 
-// Pass block size.  Two 512-thread blocks per CU (4096-row tiles) interleave one
-// block's ranking with the other's memory traffic: a 2B-row key-only sort runs 137 ->
-// 120 ms.  With several payload columns the halved tile shortens every bucket's write
-// run per tile (1B x 1B join: partition 82 -> 99 ms), so wide rows keep one 1024-thread
-// block (profiles/rows_pass_experiments_r02.txt).  CYLON_RP_THREADS=512|1024 forces one.
-static int rp_threads(int ncols) {
+// Pass block size.  With LDS-atomic ranking (cheap_rank) one 1024-thread block per CU
+// (8192-row tiles, 16-row write runs per bucket) wins for every width: 1B-row union
+// 130 -> 118 ms, 250M sort 16.4 -> 14.4 ms, group-by 27.9 -> 27.0 ms
+// (profiles/rank_variants_r02.txt).  With the ballot ranking, two 512-thread blocks per CU
+// (4096-row tiles) interleave one block's ranking with the other's memory traffic, which
+// pays for 1-2 column passes (2B sort 137 -> 120 ms) but not for wide rows
+// (profiles/rows_pass_experiments_r02.txt).  CYLON_RP_THREADS=512|1024 forces one.
+static int rp_threads(int ncols, bool cheap_rank) {
   static const int forced = [] {
     const char *e = std::getenv("CYLON_RP_THREADS");
     const int t = e ? std::atoi(e) : 0;
     return t == 512 || t == 1024 ? t : 0;
   }();
-  return forced ? forced : (ncols <= 2 ? 512 : 1024);
+  return forced ? forced : (ncols <= 2 && !cheap_rank ? 512 : 1024);
 }
 
 // Self-check of kRankWaveAtomic's precondition: every lane of a wave adds 1 to a
@@ -472,8 +474,7 @@ bool lds_lane_order_ok(void *stream) {
 }
 static bool rp_wave_atomic(hipStream_t s) { return lds_lane_order_ok(reinterpret_cast<void *>(s)); }
 
-static RPGeometry rp_geometry(int64_t n, int ncols) {
-  const int threads = rp_threads(ncols);
+static RPGeometry rp_geometry(int64_t n, int threads) {
   const int64_t tile = (int64_t)threads * kRPItems;
   const int64_t tiles = std::max<int64_t>(1, (n + tile - 1) / tile);
   const int64_t want = 2 * kNumCUs * (1024 / threads);  // two rounds of resident blocks (16 waves per CU)
@@ -486,8 +487,8 @@ static RPGeometry rp_geometry(int64_t n, int ncols) {
 
 int64_t radix_rows_pass_workspace(int64_t n, int digit_bits) {  // covers both block sizes
   int64_t ws = 0;
-  for (int ncols : {1, kMaxFusedCols}) {
-    const int64_t m = rp_geometry(n, ncols).nblocks * (int64_t(1) << digit_bits);
+  for (int threads : {512, 1024}) {
+    const int64_t m = rp_geometry(n, threads).nblocks * (int64_t(1) << digit_bits);
     ws = std::max(ws, m + (m + 1) + scan_workspace(m));
   }
   return ws;
@@ -557,7 +558,11 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
               "radix pass: key_xor is only valid for order-image digits");
   hipStream_t s = as_stream(stream);
   const uint32_t nb = 1u << digit_bits;
-  const RPGeometry g = rp_geometry(n, ncols);
+  CYLON_CHECK(stable || CAN_UNSTABLE, Code::Invalid, "radix pass: only partition digits may rank unstably");
+  const bool unstable = CAN_UNSTABLE && !stable;
+  const bool wave_atomic = !unstable && rp_wave_atomic(s);
+  const int threads = rp_threads(ncols, unstable || wave_atomic);
+  const RPGeometry g = rp_geometry(n, threads);
   const int64_t m = g.nblocks * (int64_t)nb;
   int64_t *bh = ws, *bh_scan = ws + m, *scan_ws = bh_scan + m + 1;
   hipLaunchKernelGGL(k_rp_hist<Digit>, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, n, nb,
@@ -574,13 +579,12 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   }
   bool w8 = true;
   for (int c = 0; c < ncols; ++c) w8 &= widths[c] == 8;
-  CYLON_CHECK(stable || CAN_UNSTABLE, Code::Invalid, "radix pass: only partition digits may rank unstably");
-  const bool big = rp_threads(ncols) == 1024;
-  if (CAN_UNSTABLE && !stable) {
+  const bool big = threads == 1024;
+  if (unstable) {
     constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankBallot;
     if (big) rows_pass_kernel<Digit, 1024, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
     else rows_pass_kernel<Digit, 512, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
-  } else if (rp_wave_atomic(s)) {
+  } else if (wave_atomic) {
     if (big) rows_pass_kernel<Digit, 1024, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
     else rows_pass_kernel<Digit, 512, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
   } else {
