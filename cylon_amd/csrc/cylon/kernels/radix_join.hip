@@ -120,7 +120,10 @@ struct ImageDigit {
   const int64_t *keys;
   int shift;
   uint32_t mask;
-  __device__ __forceinline__ uint32_t of_key(int64_t k) const { return (uint32_t)((uint64_t)k >> shift) & mask; }
+  uint64_t flip;  // image = key ^ flip (0 once column 0 holds images)
+  __device__ __forceinline__ uint32_t of_key(int64_t k) const {
+    return (uint32_t)(((uint64_t)k ^ flip) >> shift) & mask;
+  }
   __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key(keys[i]); }
 };
 
@@ -603,9 +606,10 @@ void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, 
 
 void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_bits, const uint8_t *const *in,
                           uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream,
-                          uint64_t key_xor) {
+                          uint64_t key_xor, uint64_t digit_flip) {
   const uint32_t nb = 1u << digit_bits;
-  rows_pass_launch(ImageDigit{keys, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws, stream, key_xor);
+  rows_pass_launch(ImageDigit{keys, shift, nb - 1, digit_flip}, n, digit_bits, in, out, widths, ncols, ws, stream,
+                   key_xor);
 }
 
 void radix_range_rows_pass(const int64_t *keys, int64_t n, uint64_t flip, uint64_t mn, int rshift, int shift,

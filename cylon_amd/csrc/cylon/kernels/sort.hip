@@ -66,7 +66,7 @@ __global__ void k_sort_keys(ColView c, const int64_t *__restrict__ perm, int64_t
     // a null's image is a constant: null rows keep their order from the previous (less
     // significant) sort columns, so equal rows stay adjacent in multi-column sorts
     if (c.valid != nullptr && c.valid[s] == 0) k = mask;
-    out[i] = k;
+    if (out != nullptr) out[i] = k;  // null: reduction only (8-byte integer keys imaged by the first pass)
     o |= k;
     a &= k;
   }

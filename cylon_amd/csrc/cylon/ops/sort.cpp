@@ -117,12 +117,18 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
   if (slots > kMaxFusedCols) return nullptr;
   Exec ex(t->device());
   CYLON_PHASE("sort.radix_rows", ex.device);
-  at::Tensor img = ex.empty_i64(n);
-  at::Tensor ws2 = ex.empty_i64(2);
-  const uint64_t diff = hip::sort_keys_varying_bits(kc.view(), n, !asc, reinterpret_cast<uint64_t *>(ptr<int64_t>(img)),
-                                                    ptr<int64_t>(ws2), ex.stream);
   // an integer key is rebuilt from its image at the end instead of travelling too
   const bool key_from_image = kc.type.kind() == ValueKind::SIGNED_INT || kc.type.kind() == ValueKind::UNSIGNED_INT;
+  // an 8-byte integer key's image is key ^ key_xor: the first pass reads the raw keys (its digit
+  // XORs them) and stores images, so the image kernel only reduces (no 8 B/row image write)
+  const uint64_t key_xor = (kc.type.kind() == ValueKind::SIGNED_INT ? (1ull << 63) : 0ull) ^ (asc ? 0ull : ~0ull);
+  const bool raw_in = key_from_image && kc.type.width() == 8 && kc.data.is_contiguous() &&
+                      kc.data.element_size() == 8;
+  at::Tensor img = raw_in ? kc.data : ex.empty_i64(n);
+  at::Tensor ws2 = ex.empty_i64(2);
+  const uint64_t diff = hip::sort_keys_varying_bits(
+      kc.view(), n, !asc, raw_in ? nullptr : reinterpret_cast<uint64_t *>(ptr<int64_t>(img)), ptr<int64_t>(ws2),
+      ex.stream);
   std::vector<at::Tensor> cur{img};
   std::vector<int> widths{8};
   for (int ci = 0; ci < t->Columns(); ++ci) {
@@ -139,7 +145,6 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
   // an 8-byte integer key comes back from its image by one XOR, applied by the last
   // pass as it stores column 0 (no separate un-image read + write of the key)
   const bool key_in_last_pass = key_from_image && kc.type.width() == 8 && diff != 0;
-  const uint64_t key_xor = (kc.type.kind() == ValueKind::SIGNED_INT ? (1ull << 63) : 0ull) ^ (asc ? 0ull : ~0ull);
   // validity bytes of an otherwise all-8-byte table travel packed (8-byte pass path)
   BytePacking bp;
   if (diff != 0) bp = PackByteColumns(ex, cur, widths, n);
@@ -162,9 +167,12 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
       }
       // the XOR goes on the FINAL pass only: a pass reads column 0 as the order image it
       // ranks by, so an un-imaged key column must never be the input of another pass
+      // raw_in: the first pass ranks key ^ key_xor and stores it (raw -> image); the last
+      // pass XORs again (image -> raw); one pass does both (stores the raw key)
+      const uint64_t flip = ps == 0 && raw_in ? key_xor : 0ull;
       hip::radix_sort_rows_pass(ptr<int64_t>(cur[0]), n, shift, db, in.data(), out.data(), widths.data(),
                                 (int)cur.size(), ptr<int64_t>(ws), ex.stream,
-                                ps + 1 == npass && key_in_last_pass ? key_xor : 0ull);
+                                flip ^ (ps + 1 == npass && key_in_last_pass ? key_xor : 0ull), flip);
       cur = std::move(nxt);
       shift += db;
     }
@@ -176,6 +184,8 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
     const Column &c = t->column(ci);
     at::Tensor d;
     if (key_in_last_pass && ci == col) {
+      d = cur[0].view(c.data.scalar_type());
+    } else if (raw_in && ci == col) {  // all keys equal (no pass ran): column 0 is still the raw key
       d = cur[0].view(c.data.scalar_type());
     } else if (key_from_image && ci == col) {
       at::Tensor im = cur[0];
