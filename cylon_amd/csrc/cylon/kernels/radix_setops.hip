@@ -194,21 +194,23 @@ __global__ __launch_bounds__(kSOThreads) void k_so_dedup(const uint64_t *__restr
   __shared__ int sbad;
   const uint32_t rep_init = keep_last ? 0u : 0xffffffffu;
   // phase 1: insert, fold representative position and side flags
-  auto insert = [&](uint64_t h, int64_t row, uint32_t local) {
+  auto insert = [&](uint64_t h, int64_t row, uint32_t local) -> int {
     const int s = so_slot<true>(keys, h);
     if (s < 0) {
       sbad = 1;
-      return;
+      return s;
     }
     if (keep_last) atomicMax(&rep[s], local);
     else atomicMin(&rep[s], local);
     if (op != SO_DISTINCT) atomicOr(&side[s >> 4], (row < nl ? 1u : 2u) << ((s & 15) * 2));
+    return s;
   };
   // phase 2: verify duplicates against their representative, write mask exceptions
-  auto verify = [&](bool active, uint64_t h, int64_t row, uint32_t local, int64_t rb) {
+  // slot: the slot phase 1 claimed for this row (-1: look it up again)
+  auto verify = [&](bool active, uint64_t h, int64_t row, uint32_t local, int64_t rb, int slot) {
     bool flip = false;
     if (active) {
-      const int s = so_slot<false>(keys, h);
+      const int s = slot >= 0 ? slot : so_slot<false>(keys, h);
       const bool first = rep[s] == local;
       if (!first && !so_rows_equal(L, R, ncols, nl, row, prow[rb + rep[s]])) atomicExch(bad, 1);  // collision
       if (op == SO_DISTINCT) {
@@ -251,10 +253,11 @@ __global__ __launch_bounds__(kSOThreads) void k_so_dedup(const uint64_t *__restr
     for (int s = threadIdx.x; s < kSOSlots / 16; s += blockDim.x) side[s] = 0u;
     if (threadIdx.x == 0) sbad = 0;
     __syncthreads();
+    int sl[kSOItems];  // claimed slots: phase 2 does not probe again
 #pragma unroll
     for (int k = 0; k < kSOItems; ++k) {
       const int64_t r = rb + threadIdx.x + k * kSOThreads;
-      if (r < re) insert(hv[k], rv[k], (uint32_t)(r - rb));
+      sl[k] = r < re ? insert(hv[k], rv[k], (uint32_t)(r - rb)) : -1;
     }
     for (int64_t r = rb + kSORowsPerPart + threadIdx.x; r < re; r += kSOThreads)
       insert(ph[r], prow[r], (uint32_t)(r - rb));
@@ -266,12 +269,12 @@ __global__ __launch_bounds__(kSOThreads) void k_so_dedup(const uint64_t *__restr
 #pragma unroll
     for (int k = 0; k < kSOItems; ++k) {
       const int64_t r = rb + threadIdx.x + k * kSOThreads;
-      verify(r < re, hv[k], rv[k], (uint32_t)(r - rb), rb);
+      verify(r < re, hv[k], rv[k], (uint32_t)(r - rb), rb, sl[k]);
     }
     for (int64_t r0 = rb + kSORowsPerPart; r0 < re; r0 += kSOThreads) {  // wave-uniform trip count
       const int64_t r = r0 + threadIdx.x;
       const bool act = r < re;
-      verify(act, act ? ph[r] : 0, act ? prow[r] : 0, (uint32_t)(r - rb), rb);
+      verify(act, act ? ph[r] : 0, act ? prow[r] : 0, (uint32_t)(r - rb), rb, -1);
     }
   }
 }
