@@ -370,9 +370,14 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       if (c + 1 < cols.n) {  // prefetch column c+1 of this tile
         const uint8_t *in = cols.in[c + 1];
         const int w1 = cols.width[c + 1];
+        if (in == nullptr) {  // row-id column: the pass generates it (no 8 B/row array to read)
 #pragma unroll
-        for (int k = 0; k < kRPItems; ++k)
-          if (pl[k] != 0xffffffffu) v[k] = ldw<W8>(in, tile + wrow + k * kWave + lane, w1);
+          for (int k = 0; k < kRPItems; ++k) v[k] = (uint64_t)(tile + wrow + k * kWave + lane);
+        } else {
+#pragma unroll
+          for (int k = 0; k < kRPItems; ++k)
+            if (pl[k] != 0xffffffffu) v[k] = ldw<W8>(in, tile + wrow + k * kWave + lane, w1);
+        }
       } else {  // prefetch the next tile's keys
 #pragma unroll
         for (int k = 0; k < kRPItems; ++k) {
@@ -581,7 +586,11 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
     cs.width[c] = c < ncols ? widths[c] : 8;
   }
   bool w8 = true;
-  for (int c = 0; c < ncols; ++c) w8 &= widths[c] == 8;
+  for (int c = 0; c < ncols; ++c) {
+    w8 &= widths[c] == 8;
+    CYLON_CHECK(in[c] != nullptr || (c > 0 && widths[c] == 8), Code::Invalid,
+                "radix pass: a generated row-id column must be an 8-byte payload column");
+  }
   const bool big = threads == 1024;
   if (unstable) {
     constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankBallot;

@@ -79,7 +79,7 @@ __global__ void k_so_hash(SOColSet cols, int ncols, int64_t n, int64_t base, uin
     uint64_t x = 0x84222325cbf29ce4ULL;
     for (int c = 0; c < ncols; ++c) x = hashing::combine64(x, so_value_hash(cols.c[c], i));
     h[base + i] = x | 1ull;  // 0 marks an empty LDS slot
-    rowid[base + i] = base + i;
+    if (rowid != nullptr) rowid[base + i] = base + i;  // null: the partition pass generates row ids
   }
 }
 
