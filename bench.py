@@ -49,6 +49,9 @@ def parse():
     p.add_argument("--key-ratio", type=float, default=0.99)
     p.add_argument("--no-phases", action="store_true", help="skip the traced per-phase step after the timed region")
     p.add_argument("--verify", action="store_true", help="check the last output against torch (outside the timing)")
+    p.add_argument("--force-shuffle", action="store_true",
+                   help="with --gpus 1: run a world-1 RCCL context through the full shuffle + exchange path "
+                        "(config force_shuffle=1) instead of the local join")
     return p.parse_args()
 
 
@@ -83,11 +86,20 @@ def resolve_world(gpus: int, script: str, argv):
     return world, int(os.environ.get("RANK", "0"))
 
 
-def make_context(world: int):
+def make_context(world: int, force_shuffle: bool = False):
     """CYLON_BENCH_BACKEND=gloo rehearses the multi-rank path on CPUs (tests only); gloo-gpu keeps
-    the tables in HBM (ranks may share one GPU) with gloo collectives; default = RCCL."""
+    the tables in HBM (ranks may share one GPU) with gloo collectives; default = RCCL.
+    force_shuffle at world 1: a distributed RCCL context of one rank whose operators take the
+    shuffle path (RCCL self all-to-all), so the 1-GPU run measures the exchange machinery."""
     from cylon_amd import CylonContext, GlooConfig, RCCLConfig
     backend = os.environ.get("CYLON_BENCH_BACKEND", "")
+    if world == 1 and force_shuffle:
+        for k, v in (("RANK", "0"), ("WORLD_SIZE", "1"), ("LOCAL_RANK", "0"), ("MASTER_ADDR", "127.0.0.1")):
+            os.environ.setdefault(k, v)
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        ctx = CylonContext(config=GlooConfig() if backend == "gloo" else RCCLConfig(), distributed=True)
+        ctx.add_config("force_shuffle", "1")
+        return ctx
     if world > 1 and backend == "gloo-gpu":
         ndev = max(torch.cuda.device_count(), 1)
         return CylonContext(config=GlooConfig(device=f"cuda:{int(os.environ.get('LOCAL_RANK', '0')) % ndev}"),
@@ -161,7 +173,7 @@ def main():
     args = parse()
     world, rank = resolve_world(args.gpus, os.path.abspath(__file__), sys.argv[1:])
     sys.path.insert(0, ROOT)
-    ctx = make_context(world)
+    ctx = make_context(world, args.force_shuffle)
     device = ctx.device
     n = world
     rows_local = args.rows // n
@@ -202,6 +214,7 @@ def main():
     out = None
 
     phases = None
+    counters = {}
     if not args.no_phases:
         from cylon_amd.utils import trace
         trace.enable_tracing(True)
@@ -214,6 +227,7 @@ def main():
         traced_ms = 1000.0 * (time.perf_counter() - t1)
         ph = {k: v[0] for k, v in trace.phases().items()}
         ph["step_total"] = traced_ms
+        counters = {k: v for k, v in trace.counters().items() if k.startswith("shuffle.")}
         trace.enable_tracing(False)
         phases = {k: round(v, 3) for k, v in sorted(max_over_ranks(ctx, ph).items())}
 
@@ -238,7 +252,8 @@ def main():
                 "model": f"distributed inner join ({args.algorithm}), int64 key + {args.payload_cols} float64 cols",
                 "global_batch": args.rows,
                 "seq_len": 1 + args.payload_cols,
-                "parallelism": f"dp{n} (hash shuffle over {'RCCL' if os.environ.get('CYLON_BENCH_BACKEND', '') == '' else os.environ['CYLON_BENCH_BACKEND']})" if n > 1 else "dp1 (local join)",
+                "parallelism": (f"dp{n} (hash shuffle over {'RCCL' if os.environ.get('CYLON_BENCH_BACKEND', '') == '' else os.environ['CYLON_BENCH_BACKEND']})"
+                                if n > 1 or args.force_shuffle else "dp1 (local join)"),
                 "rows_per_relation": args.rows,
                 "output_rows": out_rows,
                 "key_range": key_range,
@@ -248,6 +263,10 @@ def main():
             rec["phases_ms_max_over_ranks"] = phases
         if verify is not None:
             rec["verify"] = verify
+        if args.force_shuffle:
+            rec["force_shuffle"] = True
+        if counters:
+            rec["shuffle_counters_rank0"] = counters
         print(json.dumps(rec), flush=True)
     ctx.finalize()
     if verify is not None and not verify["ok"]:

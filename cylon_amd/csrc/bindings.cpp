@@ -117,6 +117,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("timezone", &DataType::timezone)
       .def_readwrite("value_type", &DataType::value_type)
       .def_readwrite("list_size", &DataType::list_size)
+      .def_readwrite("precision", &DataType::precision)
+      .def_readwrite("scale", &DataType::scale)
       .def("value_width", &DataType::value_width)
       .def_static("list_of", &DataType::List)
       .def_static("fixed_size_list_of", &DataType::FixedSizeList)

@@ -3,6 +3,8 @@
 // ctx/cylon_context.cpp:25-108.
 #include <c10/hip/HIPCachingAllocator.h>
 
+#include <cstdlib>
+
 #include "column.hpp"
 #include "ctx/cylon_context.hpp"
 #include "table.hpp"
@@ -227,6 +229,15 @@ std::shared_ptr<net::Communicator> CylonContext::GetCommunicator() const {
 
 int CylonContext::GetRank() const { return distributed_ ? communicator_->GetRank() : 0; }
 int CylonContext::GetWorldSize() const { return distributed_ ? communicator_->GetWorldSize() : 1; }
+
+bool CylonContext::ShuffleRequired() const {
+  if (!distributed_) return false;
+  if (GetWorldSize() > 1) return true;
+  std::string v = GetConfig("force_shuffle", "");
+  if (v.empty())
+    if (const char *e = std::getenv("CYLON_FORCE_SHUFFLE")) v = e;
+  return v == "1" || v == "true";
+}
 
 std::vector<int> CylonContext::GetNeighbours(bool include_self) const {
   std::vector<int> n;

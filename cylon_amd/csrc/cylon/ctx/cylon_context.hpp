@@ -46,6 +46,12 @@ class CylonContext {
   std::vector<int> GetNeighbours(bool include_self) const;
   int GetNextSequence();
   bool IsDistributed() const { return distributed_; }
+  // True when distributed operators must run their shuffle + exchange path: world > 1,
+  // or a distributed world-1 context with config "force_shuffle" = "1" (env
+  // CYLON_FORCE_SHUFFLE=1).  The forced form runs every exchange through the real
+  // transport (RCCL self all-to-all on one GPU) instead of the world-1 local shortcut,
+  // so the asynchronous exchange path can be tested and profiled on a single GPU.
+  bool ShuffleRequired() const;
   net::CommType GetCommType() const;
   void Barrier();
 

@@ -68,7 +68,14 @@ DataType to_cylon(const arrow::DataType &t) {
     case Type::LARGE_BINARY: return DataType(cylon::Type::BINARY);
     case Type::FIXED_SIZE_BINARY:
       return DataType::FixedSizeBinary(static_cast<const arrow::FixedSizeBinaryType &>(t).byte_width());
-    case Type::DECIMAL128: return DataType(cylon::Type::DECIMAL, 16);
+    case Type::DECIMAL128:
+    case Type::DECIMAL256: {
+      const auto &dt = static_cast<const arrow::DecimalType &>(t);
+      DataType d(cylon::Type::DECIMAL, dt.byte_width());
+      d.precision = dt.precision();
+      d.scale = dt.scale();
+      return d;
+    }
     case Type::DATE32: return DataType(cylon::Type::DATE32);
     case Type::DATE64: return DataType(cylon::Type::DATE64);
     case Type::TIMESTAMP: {
@@ -124,7 +131,9 @@ std::shared_ptr<arrow::DataType> to_arrow(const DataType &t, bool large_var) {
     case cylon::Type::TIME32: return arrow::time32(arrow_unit(t.unit));
     case cylon::Type::TIME64: return arrow::time64(arrow_unit(t.unit));
     case cylon::Type::DURATION: return arrow::duration(arrow_unit(t.unit));
-    case cylon::Type::DECIMAL: return arrow::decimal128(38, 0);
+    case cylon::Type::DECIMAL:
+      if (t.byte_width == 32) return arrow::decimal256(t.precision ? t.precision : 76, t.scale);
+      return arrow::decimal128(t.precision ? t.precision : 38, t.scale);
     case cylon::Type::LIST:
       return large_var ? arrow::large_list(to_arrow(DataType(t.value_type), false))
                        : arrow::list(to_arrow(DataType(t.value_type), false));

@@ -5,6 +5,7 @@
 
 #include <ATen/hip/HIPContext.h>
 #include <cstring>
+#include <cstdio>
 #include <map>
 
 #include "../ops/util.hpp"
@@ -59,7 +60,9 @@ std::string format_of(const DataType &t) {
     case Type::STRING: return "U";
     case Type::BINARY: return "Z";
     case Type::FIXED_SIZE_BINARY: return "w:" + std::to_string(t.byte_width);
-    case Type::DECIMAL: return "d:38,0";
+    case Type::DECIMAL:  // "d:precision,scale[,bitwidth]"
+      return "d:" + std::to_string(t.precision ? t.precision : (t.byte_width == 32 ? 76 : 38)) + "," +
+             std::to_string(t.scale) + (t.byte_width == 32 ? ",256" : "");
     case Type::DATE32: return "tdD";
     case Type::DATE64: return "tdm";
     case Type::TIMESTAMP: return std::string("ts") + unit_char(t.unit) + ":" + t.timezone;
@@ -81,7 +84,15 @@ DataType type_of_format(const std::string &f, const ArrowSchema *s) {
   auto it = simple.find(f);
   if (it != simple.end()) return DataType(it->second);
   if (f.rfind("w:", 0) == 0) return DataType::FixedSizeBinary(std::atoi(f.c_str() + 2));
-  if (f.rfind("d:", 0) == 0) return DataType(Type::DECIMAL, 16);
+  if (f.rfind("d:", 0) == 0) {
+    int p = 0, sc = 0, bits = 128;
+    std::sscanf(f.c_str() + 2, "%d,%d,%d", &p, &sc, &bits);
+    CYLON_CHECK(bits == 128 || bits == 256, Code::NotImplemented, "decimal bit width " << bits);
+    DataType d(Type::DECIMAL, bits / 8);
+    d.precision = p;
+    d.scale = sc;
+    return d;
+  }
   if (f.rfind("ts", 0) == 0 && f.size() >= 4) {
     DataType d = DataType::Timestamp(unit_of_char(f[2]), f.size() > 4 ? f.substr(4) : "");
     return d;

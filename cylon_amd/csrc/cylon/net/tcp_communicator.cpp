@@ -216,8 +216,13 @@ void TcpCommunicator::reader_loop(int peer) {
     for (;;) {
       int64_t hdr[2];
       if (!read_all(fd, hdr, sizeof(hdr))) break;
+      // a frame is never larger than one host buffer can be (64 GiB sanity cap)
+      CYLON_CHECK(hdr[1] >= 0 && hdr[1] <= (int64_t(1) << 36), Code::IOError,
+                  "tcp frame from rank " << peer << " has a bad length " << hdr[1]);
       std::vector<uint8_t> b((size_t)hdr[1]);
-      if (hdr[1]) read_all(fd, b.data(), hdr[1]);
+      // EOF between a header and its payload is a peer failure, never an empty frame
+      if (hdr[1]) CYLON_CHECK(read_all(fd, b.data(), hdr[1]), Code::IOError,
+                              "rank " << peer << " closed the connection inside a frame");
       {
         std::lock_guard<std::mutex> lk(q_mu_);
         queues_[{peer, hdr[0]}].push_back(std::move(b));

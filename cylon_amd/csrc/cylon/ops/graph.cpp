@@ -160,7 +160,7 @@ PartitionOp::PartitionOp(std::shared_ptr<CylonContext> ctx, int id, ResultsCallb
 
 bool PartitionOp::Execute(int, const TablePtr &table) {
   const int world = ctx_->GetWorldSize();
-  if (world == 1) {
+  if (!ctx_->ShuffleRequired()) {
     Emit(0, table);
     return true;
   }

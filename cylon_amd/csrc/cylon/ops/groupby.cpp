@@ -428,7 +428,7 @@ static bool decomposable(int op) {
 
 TablePtr DistributedHashGroupBy(const TablePtr &t, const std::vector<int> &keys, const std::vector<AggSpec> &aggs) {
   auto ctx = t->GetContext();
-  if (ctx->GetWorldSize() == 1) return HashGroupBy(t, keys, aggs);
+  if (!ctx->ShuffleRequired()) return HashGroupBy(t, keys, aggs);
   bool all_dec = true;
   for (const auto &a : aggs) all_dec &= decomposable(a.op);
   const int nk = (int)keys.size();

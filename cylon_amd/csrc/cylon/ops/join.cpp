@@ -677,7 +677,7 @@ TablePtr Join(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg
 
 TablePtr DistributedJoin(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
   auto ctx = left->GetContext();
-  if (ctx->GetWorldSize() == 1) return Join(left, right, cfg);
+  if (!ctx->ShuffleRequired()) return Join(left, right, cfg);
   const int K = ShuffleChunks(left, right);
   if (K > 1) {
     JoinSink sink;

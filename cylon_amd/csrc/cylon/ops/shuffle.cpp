@@ -292,7 +292,7 @@ static PendingTable AllToAllPost(const TablePtr &part, const std::vector<int64_t
 static PendingTable AllToAllBegin(const TablePtr &part, const std::vector<int64_t> &counts) {
   auto ctx = part->GetContext();
   const int world = ctx->GetWorldSize();
-  if (world == 1 || !ctx->IsDistributed()) {
+  if (!ctx->ShuffleRequired()) {
     PendingTable pt;
     pt.passthrough = part;
     return pt;
@@ -314,6 +314,12 @@ static PendingTable AllToAllBegin(const TablePtr &part, const std::vector<int64_
 
 static TablePtr AllToAllFinish(PendingTable &pt) {
   if (pt.passthrough) return pt.passthrough;
+  // a request still in flight when its consumer arrives means the transfer overlapped the
+  // work enqueued since it was posted (the wait below is a stream wait on RCCL, not a block)
+  int64_t in_flight = 0;
+  for (auto &r : pt.reqs) in_flight += r->Test() ? 0 : 1;
+  trace::add_counter("shuffle.requests_waited", (int64_t)pt.reqs.size());
+  trace::add_counter("shuffle.requests_in_flight_at_wait", in_flight);
   for (auto &r : pt.reqs) r->Wait();
   std::vector<Column> out;
   for (size_t c = 0; c < pt.cols.size(); ++c) {
@@ -380,7 +386,7 @@ static std::pair<TablePtr, std::vector<int64_t>> shuffle_partition(const TablePt
 TablePtr Shuffle(const TablePtr &t, const std::vector<int> &hash_cols) {
   auto ctx = t->GetContext();
   const int world = ctx->GetWorldSize();
-  if (world == 1) return t;
+  if (!ctx->ShuffleRequired()) return t;
   auto r = shuffle_partition(t, hash_cols, world);
   CYLON_PHASE("shuffle.exchange", t->device());
   trace::add_counter("shuffle.rows_in", t->Rows());
@@ -397,7 +403,7 @@ std::pair<TablePtr, TablePtr> ShufflePair(const TablePtr &a, const std::vector<i
                                           const std::vector<int> &bcols) {
   auto ctx = a->GetContext();
   const int world = ctx->GetWorldSize();
-  if (world == 1) return {a, b};
+  if (!ctx->ShuffleRequired()) return {a, b};
   auto ra = shuffle_partition(a, acols, world);
   PendingTable pa;
   {
@@ -437,7 +443,7 @@ int ShuffleChunks(const TablePtr &a, const TablePtr &b) {
   if (v.empty())
     if (const char *e = std::getenv("CYLON_SHUFFLE_CHUNKS")) v = e;
   if (!v.empty()) return std::max(1, std::min(64, std::atoi(v.c_str())));
-  if (!a->device().is_cuda() || ctx->GetWorldSize() == 1) return 1;
+  if (!a->device().is_cuda() || !ctx->ShuffleRequired()) return 1;
   at::Tensor rows = at::tensor({std::min(a->Rows(), b->Rows())}, at::TensorOptions().dtype(at::kLong)).to(a->device());
   ctx->GetCommunicator()->AllReduce(rows, net::ReduceOp::MIN);
   return rows.item<int64_t>() >= (int64_t(1) << 24) ? 4 : 1;
@@ -468,7 +474,7 @@ void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const 
     for (const auto &c : t->columns())
       CYLON_CHECK(!c.is_var(), Code::Invalid, "chunked shuffle supports fixed-width columns only");
   const uint32_t P = (uint32_t)W * (uint32_t)K;
-  if (W == 1 || !ctx->IsDistributed()) {
+  if (!ctx->ShuffleRequired()) {
     auto ra = PartitionReorder(a, hash_pids(a, acols, P), P);
     auto rb = PartitionReorder(b, hash_pids(b, bcols, P), P);
     int64_t oa = 0, ob = 0;

@@ -44,10 +44,35 @@ static at::Tensor nulls_last(const Exec &ex, const Column &c, const at::Tensor &
 
 static at::Tensor refine_by_column(const Exec &ex, const Column &c, at::Tensor perm, bool asc);
 
-// fixed-size binary / decimal / fixed-size list: byte-wise order, through the
-// variable-width path over synthetic offsets i * width
+// bytes [off, off + width of t) of every row of a fixed-width column as a contiguous
+// column of numeric type t (the validity of the source column)
+static Column fixed_slice(const Column &c, int64_t off, const DataType &t) {
+  const int64_t w = c.type.width(), n = c.length;
+  at::Tensor b = c.data.view(at::kByte).slice(0, 0, n * w).reshape({n, w}).slice(1, off, off + t.width());
+  return Column(c.name, t, n, b.contiguous().view(storage_dtype(t)).reshape({n}), at::Tensor(), c.validity);
+}
+
+// fixed-size binary: byte-wise (memcmp) order, through the variable-width path over
+// synthetic offsets i * width.  DECIMAL (little-endian two's complement, 16 or 32
+// bytes): numeric order -- LSD over 8-byte limbs, unsigned below the top limb, signed
+// top limb.  FIXED_SIZE_LIST<numeric>: lexicographic element-wise numeric order --
+// LSD over the elements.  (Byte order would put 256 before 1 and negatives last.)
 static at::Tensor refine_fixed_bytes(const Exec &ex, const Column &c, at::Tensor perm, bool asc) {
   const int64_t w = c.type.width();
+  if (c.type.type == Type::DECIMAL) {
+    CYLON_CHECK(w % 8 == 0 && w >= 8, Code::NotImplemented, "sort by a decimal of " << w << " bytes");
+    for (int64_t limb = 0; limb < w / 8; ++limb) {
+      const bool top = limb == w / 8 - 1;
+      perm = refine_by_column(ex, fixed_slice(c, 8 * limb, DataType(top ? Type::INT64 : Type::UINT64)), perm, asc);
+    }
+    return perm;
+  }
+  if (c.type.type == Type::FIXED_SIZE_LIST) {
+    const DataType et(c.type.value_type);
+    for (int64_t e = (int64_t)c.type.list_size - 1; e >= 0; --e)
+      perm = refine_by_column(ex, fixed_slice(c, e * et.width(), et), perm, asc);
+    return c.type.list_size > 0 ? perm : nulls_last(ex, c, perm);
+  }
   at::Tensor offs = at::arange(0, (c.length + 1) * w, w, ex.opts(at::kLong));
   Column v(c.name, DataType(Type::BINARY), c.length, c.data, offs, c.validity);
   return refine_by_column(ex, v, std::move(perm), asc);
@@ -55,6 +80,7 @@ static at::Tensor refine_fixed_bytes(const Exec &ex, const Column &c, at::Tensor
 
 static at::Tensor refine_by_column(const Exec &ex, const Column &c, at::Tensor perm, bool asc) {
   const int64_t n = perm.numel();
+  CYLON_CHECK(c.type.type != Type::LIST, Code::NotImplemented, "sort by a list column (" << c.name << ")");
   if (!c.is_var() && c.type.kind() == ValueKind::FIXED_BYTES) return refine_fixed_bytes(ex, c, std::move(perm), asc);
   if (!c.is_var()) {
     at::Tensor keys = ex.empty_i64(n);

@@ -69,6 +69,8 @@ struct DataType {
   std::string timezone;
   Type value_type = Type::INT64;  // LIST / FIXED_SIZE_LIST element type (numeric)
   int32_t list_size = 0;          // FIXED_SIZE_LIST elements per row
+  int32_t precision = 0;          // DECIMAL precision / scale (0, 0 = unknown: decimal(38, 0))
+  int32_t scale = 0;
 
   DataType() = default;
   explicit DataType(Type t) : type(t) {}

@@ -51,7 +51,9 @@ def to_cylon_type(at: pa.DataType) -> "C.DataType":
     if pa.types.is_fixed_size_binary(at):
         return C.DataType(T.FIXED_SIZE_BINARY, at.byte_width)
     if pa.types.is_decimal(at):
-        return C.DataType(T.DECIMAL, at.byte_width)
+        d = C.DataType(T.DECIMAL, at.byte_width)
+        d.precision, d.scale = at.precision, at.scale
+        return d
     if pa.types.is_timestamp(at):
         d = C.DataType(T.TIMESTAMP)
         d.unit = _UNIT[at.unit]
@@ -89,7 +91,9 @@ def to_arrow_type(dt: "C.DataType") -> pa.DataType:
     if t == T.FIXED_SIZE_BINARY:
         return pa.binary(dt.byte_width)
     if t == T.DECIMAL:
-        return pa.decimal128(38, 0)
+        if dt.byte_width == 32:
+            return pa.decimal256(dt.precision or 76, dt.scale)
+        return pa.decimal128(dt.precision or 38, dt.scale)
     if t == T.TIMESTAMP:
         return pa.timestamp(_UNIT_INV[dt.unit], tz=dt.timezone or None)
     if t == T.TIME32:

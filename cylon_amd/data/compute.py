@@ -222,12 +222,15 @@ def is_in(table, values, skip_null: bool = True):
 
 def _device_cast(c, target: pa.DataType, safe: bool):
     """Numeric -> numeric casts on the column's device (torch), with Arrow's safe-cast checks:
-    float -> int must be integral and in range, int -> narrower int must be in range."""
+    float -> int must be integral and in range, int -> narrower int must be in range, int -> float
+    must lie within the float's exact integer range (2^53 / 2^24).  uint64 sources go to Arrow."""
     if is_var(c) or c.type.type == T.BOOL:
         return None
     src = ab.to_arrow_type(c.type)
     num = lambda t: pa.types.is_integer(t) or pa.types.is_floating(t)  # noqa: E731
     if not (num(src) and num(target)) or target == pa.float16() or src == pa.float16():
+        return None
+    if src == pa.uint64():  # torch has no full uint64 min/max/compare support: Arrow's host kernels
         return None
     ct = ab.to_cylon_type(target)
     tdt = ab.torch_dtype(ct)
@@ -245,6 +248,12 @@ def _device_cast(c, target: pa.DataType, safe: bool):
                 lo, hi = int(live.min()), int(live.max())
             if lo < info.min or hi > info.max:
                 raise pa.ArrowInvalid(f"column {c.name}: integer value out of range for {target}")
+    if safe and pa.types.is_floating(target) and pa.types.is_integer(src):
+        # Arrow's safe int -> float cast refuses integers beyond the float's exact range
+        live = v if valid is None else v[valid]
+        lim = 2 ** 53 if target == pa.float64() else 2 ** 24
+        if live.numel() and (int(live.min()) < -lim or int(live.max()) > lim):
+            raise pa.ArrowInvalid(f"column {c.name}: integer value not in range: {-lim} to {lim}")
     out = v.to(tdt)
     return C.Column(c.name, ct, c.length, out.contiguous(), None,
                     None if c.validity is None else c.validity.contiguous())

@@ -24,9 +24,11 @@ def _worker(rank, world, port, fn, args, q, device="cpu", env=None):
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         if root not in sys.path:
             sys.path.insert(0, root)
-        from cylon_amd import CylonContext, GlooConfig, TCPConfig
-        # CYLON_TEST_COMM=tcp: the native bootstrap + TCP mesh instead of torch.distributed gloo
-        cfg = TCPConfig() if os.environ.get("CYLON_TEST_COMM") == "tcp" else GlooConfig()
+        from cylon_amd import CylonContext, GlooConfig, RCCLConfig, TCPConfig
+        # CYLON_TEST_COMM=tcp: the native bootstrap + TCP mesh instead of torch.distributed gloo;
+        # CYLON_TEST_COMM=rccl: torch.distributed nccl (RCCL), one rank per GPU
+        comm = os.environ.get("CYLON_TEST_COMM")
+        cfg = TCPConfig() if comm == "tcp" else (RCCLConfig() if comm == "rccl" else GlooConfig())
         ctx = CylonContext(config=cfg, distributed=True, device=device)
         try:
             res = fn(ctx, *args)

@@ -1,0 +1,65 @@
+"""force_shuffle on a distributed world-1 context (CPU, gloo): every distributed
+operator takes its shuffle + exchange path instead of the world-1 shortcut and must
+give the local operator's result.  The GPU twin over RCCL is
+tests/test_gpu_rccl_forced.py."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from dist_utils import run_distributed
+
+
+def _frame(df):
+    df = df[sorted(df.columns)]
+    return df.sort_values(list(df.columns), kind="mergesort").reset_index(drop=True)
+
+
+def _ops(ctx, chunks):
+    from cylon_amd import CylonContext, Table
+    from cylon_amd._lib import C
+    rng = np.random.default_rng(1)
+    n = 20_000
+    a = pd.DataFrame({"k": rng.integers(0, 15_000, n), "x": rng.integers(-5, 5, n), "f": rng.random(n)})
+    b = pd.DataFrame({"k": rng.integers(0, 15_000, n), "v": rng.random(n), "s": [f"s{i % 17}" for i in range(n)]})
+    local = CylonContext()
+    res = {}
+    for forced in (False, True):
+        ctx.add_config("force_shuffle", "1" if forced else "0")
+        ctx.add_config("shuffle_chunks", str(chunks))
+        C.trace_enable(True)
+        C.trace_reset()
+        ta, tb = Table.from_pandas(ctx, a), Table.from_pandas(ctx, b)
+        r = {"join": ta.distributed_join(tb, "inner", "hash", on=["k"], left_prefix="l_", right_prefix="r_"),
+             "ljoin": ta.distributed_join(tb, "left", "sort", on=["k"], left_prefix="l_", right_prefix="r_"),
+             "union": ta[["k"]].distributed_union(tb[["k"]]),
+             "subtract": ta[["k"]].distributed_subtract(tb[["k"]]),
+             "intersect": ta[["k"]].distributed_intersect(tb[["k"]]),
+             "unique": tb.distributed_unique(["s"]),
+             "groupby": ta.groupby("x", {"f": ["sum", "mean"], "k": "max"}),
+             "sort": ta.distributed_sort(["x", "k"], ascending=[False, True])}
+        res[forced] = ({k: v.to_pandas() for k, v in r.items()}, dict(C.trace_counters()))
+    la, lb = Table.from_pandas(local, a), Table.from_pandas(local, b)
+    ref = la.join(lb, "inner", "hash", on=["k"], left_prefix="l_", right_prefix="r_").to_pandas()
+    return res, ref
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_force_shuffle_world1_matches_local(chunks):
+    res, ref = run_distributed(_ops, 1, chunks)[0]
+    plain, pc = res[False]
+    forced, fc = res[True]
+    assert pc.get("shuffle.requests_waited", 0) == 0  # world-1 shortcut: no exchange
+    assert fc.get("shuffle.requests_waited", 0) > 0, fc  # forced: every op went through the exchange
+    if chunks > 1:
+        assert fc.get("shuffle.chunks", 0) >= chunks and fc["shuffle.chunks"] % chunks == 0  # summed over ops
+    pd.testing.assert_frame_equal(_frame(forced["join"]), _frame(ref), check_dtype=False)
+    for op in plain:
+        g, e = forced[op], plain[op]
+        if op == "sort":
+            assert g[["x", "k"]].equals(e[["x", "k"]])
+        if op == "groupby":
+            g, e = g.sort_values("x").reset_index(drop=True), e.sort_values("x").reset_index(drop=True)
+            np.testing.assert_allclose(g["sum_f"], e["sum_f"], rtol=1e-12)
+            np.testing.assert_allclose(g["mean_f"], e["mean_f"], rtol=1e-12)
+            g, e = g.drop(columns=["sum_f", "mean_f"]), e.drop(columns=["sum_f", "mean_f"])
+        pd.testing.assert_frame_equal(_frame(g), _frame(e), check_dtype=False, obj=op)
