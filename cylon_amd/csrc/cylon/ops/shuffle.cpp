@@ -289,6 +289,16 @@ static PendingTable AllToAllPost(const TablePtr &part, const std::vector<int64_t
   return pt;
 }
 
+// requests of a just-posted exchange that are still running (Test() == false): the
+// transfer is asynchronous to the host and to the kernels enqueued after it
+static void count_pending(const PendingTable &pt) {
+  if (!trace::enabled()) return;
+  int64_t pending = 0;
+  for (auto &r : pt.reqs) pending += r->Test() ? 0 : 1;
+  trace::add_counter("shuffle.requests_posted", (int64_t)pt.reqs.size());
+  trace::add_counter("shuffle.requests_pending_after_post", pending);
+}
+
 static PendingTable AllToAllBegin(const TablePtr &part, const std::vector<int64_t> &counts) {
   auto ctx = part->GetContext();
   const int world = ctx->GetWorldSize();
@@ -309,6 +319,7 @@ static PendingTable AllToAllBegin(const TablePtr &part, const std::vector<int64_
   const WirePlan plan = plan_wire({part})[0];
   PendingTable pt = AllToAllPost(to_wire(part, plan), send_rows, recv_rows, nullable);
   attach_plan(pt, part, plan);
+  count_pending(pt);
   return pt;
 }
 
@@ -547,6 +558,10 @@ void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const 
     for (int k = 1; k < K; ++k) {
       pa[k] = post(pta, ca, 0, k, na_flags, offa);
       pb[k] = post(ptb, cb, 1, k, nb_flags, offb);
+    }
+    for (int k = 0; k < K; ++k) {
+      count_pending(pa[k]);
+      count_pending(pb[k]);
     }
   }
   trace::add_counter("shuffle.rows_in", a->Rows() + b->Rows());

@@ -80,13 +80,14 @@ def test_forced_rccl_shuffle_matches_cpu_twin(chunks):
         else:
             got, exp = _sorted_frame(got), _sorted_frame(exp)
         pd.testing.assert_frame_equal(got, exp, check_dtype=False, obj=op)
-    # the exchange ran through RCCL work handles: requests were posted and waited on; with
-    # chunks, every chunk is posted before chunk 0 is consumed, so at least one request is
-    # still running on the RCCL stream when its consumer reaches it (unchunked, the blocking
-    # count exchange of the second relation usually lets the first transfer finish)
+    # the exchange ran through RCCL work handles: requests were posted, were still running on
+    # the RCCL stream after posting (PGRequest::Test() == false: asynchronous to the host), and
+    # were waited on by their consumers.  (Whether one is still running when its consumer
+    # arrives -- shuffle.requests_in_flight_at_wait -- depends on how fast the self-exchange
+    # is relative to the host's posting, so it is reported, not asserted.)
     assert jc.get("shuffle.requests_waited", 0) > 0, jc
+    assert jc.get("shuffle.requests_pending_after_post", 0) > 0, jc
     assert jc.get("join.radix.rows_out", 0) == len(out["join"][0]), jc
     if chunks > 1:
         assert jc.get("shuffle.chunks") == chunks, jc
-        assert jc.get("shuffle.requests_in_flight_at_wait", 0) > 0, jc
     assert oc.get("shuffle.requests_waited", 0) > 0, oc

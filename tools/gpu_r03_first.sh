@@ -12,4 +12,5 @@ for i in 1 2; do
 done
 timeout -k 10 200 python bench.py --steps 10 --warmup 3 --force-shuffle > $O/forced.json 2> $O/forced.err
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof_forced -o forced -- python3 bench.py --steps 1 --warmup 1 --force-shuffle --no-phases > $O/prof_forced.log 2>&1
-echo done
+
+bash tools/gpu_pmc_r03.sh base
