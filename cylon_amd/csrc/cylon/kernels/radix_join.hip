@@ -797,23 +797,27 @@ __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4)))
                                                       const int64_t *__restrict__ poffs,
                                                       const int64_t *__restrict__ bkeys,
                                                       const int64_t *__restrict__ boffs, int64_t nparts, int cap,
-                                                      int64_t *__restrict__ counts, int *overflow) {
+                                                      int64_t pstride, int64_t *__restrict__ counts, int *overflow) {
+  // pstride > 1: only partitions 0, pstride, 2 pstride, ... are counted, into counts[p / pstride]
+  // (the sampled output-size estimate of the fused write path)
   __shared__ __attribute__((aligned(16))) uint16_t bst[kRJBuckets + 8];
   __shared__ int64_t skeys[kRJMaxRows];
   __shared__ uint32_t wsum[kRCWaves];
   __shared__ unsigned long long csum[kRCWaves];
-  for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
+  const int64_t nsample = (nparts + pstride - 1) / pstride;
+  for (int64_t ci = blockIdx.x; ci < nsample; ci += gridDim.x) {
+    const int64_t p = ci * pstride;
     const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
     const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
     if (nr > cap) {  // uniform branch: whole block
       if (threadIdx.x == 0) {
         atomicOr(overflow, 1);
-        counts[p] = 0;
+        counts[ci] = 0;
       }
       continue;
     }
     if (nr == 0 || nl == 0) {
-      if (threadIdx.x == 0) counts[p] = 0;
+      if (threadIdx.x == 0) counts[ci] = 0;
       continue;
     }
     // build keys are read twice (claim, then place): the second read hits L2 and the block
@@ -855,7 +859,7 @@ __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4)))
     if (threadIdx.x == 0) {
       unsigned long long tot = 0;
       for (int w = 0; w < kRCWaves; ++w) tot += csum[w];
-      counts[p] = (int64_t)tot;
+      counts[ci] = (int64_t)tot;
     }
   }
 }
@@ -879,7 +883,14 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
                                                             const int64_t *__restrict__ bkeys,
                                                             const int64_t *__restrict__ boffs, int64_t nparts,
                                                             int cap, const int64_t *__restrict__ out_offs, ColSet pc,
-                                                            ColSet bs, BuildOut bo) {
+                                                            ColSet bs, BuildOut bo,
+                                                            unsigned long long *__restrict__ cursor, int64_t out_cap,
+                                                            int *__restrict__ overflow) {
+  // out_offs != nullptr: partition p's rows start at out_offs[p] (exact count kernel ran first).
+  // out_offs == nullptr: fused count -- each partition claims its rows from *cursor with one
+  // atomic after counting its matches (output partitions land in claim order); a claim past
+  // out_cap sets overflow bit 2 and writes nothing (the cursor still totals the rows needed),
+  // a build side beyond the LDS capacity sets bit 1.
   // pc: probe columns (in -> out); bs: staged build columns (in, width), LDS
   // region j at 10*cap + sum of cap*width of the earlier ones; bo: build outputs.
   // Row area: keys in bucket order [0, 8 cap), permutation to the staged row
@@ -887,6 +898,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
   __shared__ __attribute__((aligned(16))) uint16_t bst[kRJBuckets + 8];
   __shared__ __attribute__((aligned(16))) uint8_t area[kRJRowArea];
   __shared__ uint32_t wtot[kRJWaves];
+  __shared__ int64_t sclaim;
   int64_t *skeys = reinterpret_cast<int64_t *>(area);
   uint16_t *perm = reinterpret_cast<uint16_t *>(area + 8 * (int64_t)cap);
   const int lane = lane_id();
@@ -894,8 +906,9 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
     const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
     const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
+    if (nr > cap && out_offs == nullptr && threadIdx.x == 0) atomicOr(overflow, 1);
     if (nr == 0 || nl == 0 || nr > cap) continue;
-    const int64_t obase = out_offs[p];
+    const int64_t obase = out_offs ? out_offs[p] : 0;
     // ---- phase A: probe rows of this wave's slice into VGkRJProbeRoundss (in flight during the build)
     const int64_t per = (nl + kRJWaves - 1) / kRJWaves;  // each wave owns a contiguous probe slice
     const int64_t s0 = lb + std::min<int64_t>(nl, wave * per);
@@ -971,6 +984,19 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
     if (lane == 0) wtot[wave] = c;
     __syncthreads();
     int64_t base = obase;
+    if (out_offs == nullptr) {
+      if (threadIdx.x == 0) {
+        unsigned long long tot = 0;
+        for (int w = 0; w < kRJWaves; ++w) tot += wtot[w];
+        const unsigned long long at = tot ? atomicAdd(cursor, tot) : 0ull;
+        const bool fits = at + tot <= (unsigned long long)out_cap;
+        if (!fits) atomicOr(overflow, 2);
+        sclaim = fits ? (int64_t)at : -1;
+      }
+      __syncthreads();
+      base = sclaim;
+      if (base < 0) continue;  // uniform: the block's claim did not fit
+    }
     for (int w = 0; w < wave; ++w) base += wtot[w];
     // ---- phase D: emit
     for (int u = 0; s0 + (int64_t)u * kWave < s1; ++u) {
@@ -1064,20 +1090,24 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
 static int rj_grid(int64_t nparts) { return (int)std::min<int64_t>(nparts, kNumCUs * 8); }
 
 void radix_join_count(const int64_t *pkeys, const int64_t *poffs, const int64_t *bkeys, const int64_t *boffs,
-                      int64_t nparts, int64_t cap, int64_t *counts, int *overflow, void *stream) {
+                      int64_t nparts, int64_t cap, int64_t *counts, int *overflow, void *stream, int64_t pstride) {
   CYLON_CHECK(cap > 0 && cap <= kRJMaxRows, Code::Invalid, "radix join capacity " << cap);
+  CYLON_CHECK(pstride >= 1, Code::Invalid, "partition stride " << pstride);
   hipStream_t s = as_stream(stream);
   HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
-  hipLaunchKernelGGL(k_rj_count, dim3((unsigned)std::min<int64_t>(nparts, kNumCUs * 12)), dim3(kRCThreads), 0, s,
-                     pkeys, poffs, bkeys, boffs, nparts, (int)cap, counts, overflow);
+  const int64_t nsample = (nparts + pstride - 1) / pstride;
+  hipLaunchKernelGGL(k_rj_count, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(nsample, kNumCUs * 12))),
+                     dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap, pstride, counts, overflow);
   HIP_LAUNCH_CHECK();
 }
 
 void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t *bkeys, const int64_t *boffs,
                       int64_t nparts, int64_t cap, const int64_t *out_offs, const uint8_t *const *pin,
                       uint8_t *const *pout, const int *pw, int npc, const uint8_t *const *bin, uint8_t *const *bout,
-                      const int *bw, int nbc, void *stream) {
+                      const int *bw, int nbc, void *stream, int64_t *cursor, int64_t out_cap, int *overflow) {
   CYLON_CHECK(npc <= kMaxFusedCols && nbc <= kMaxFusedCols, Code::Invalid, "too many columns");
+  CYLON_CHECK(out_offs != nullptr || (cursor != nullptr && overflow != nullptr), Code::Invalid,
+              "radix join write: needs partition offsets or an output cursor");
   CYLON_CHECK(cap > 0 && cap <= radix_join_capacity(bw, bin, nbc), Code::Invalid, "radix join capacity " << cap);
   ColSet pc, bs;
   BuildOut bo;
@@ -1109,12 +1139,13 @@ void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t 
   CYLON_CHECK(off <= kRJRowArea, Code::Invalid, "radix join LDS rows " << off);
   hipStream_t s = as_stream(stream);
   // probe columns beyond 4 and staged build columns beyond 3 are loaded in place (slower, correct)
+  unsigned long long *cur = reinterpret_cast<unsigned long long *>(cursor);
   if (w8)
     hipLaunchKernelGGL((k_rj_write<4, 3, true>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys,
-                       boffs, nparts, (int)cap, out_offs, pc, bs, bo);
+                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow);
   else
     hipLaunchKernelGGL((k_rj_write<4, 3, false>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys,
-                       boffs, nparts, (int)cap, out_offs, pc, bs, bo);
+                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow);
   HIP_LAUNCH_CHECK();
 }
 

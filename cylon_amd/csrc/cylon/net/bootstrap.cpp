@@ -85,6 +85,10 @@ std::shared_ptr<Communicator> MakeCommunicator(const CommConfig &in, at::Device 
   c10::hip::set_device(dev.index());
   auto opts = c10d::ProcessGroupNCCL::Options::create();
   opts->timeout = std::chrono::milliseconds((int64_t)(cfg.timeout_s * 1000.0));
+  // RCCL's stream at high priority: HIP maps streams onto a few hardware queues, and a
+  // normal-priority comm stream can share the compute stream's queue, which serialises every
+  // all-to-all with the operator kernels (measured: 0 ms of overlap, profiles/rccl_queue_r03.txt)
+  opts->is_high_priority_stream = true;
   auto backend = c10::make_intrusive<c10d::ProcessGroupNCCL>(store, cfg.rank, cfg.world_size, opts);
   auto pg = c10::make_intrusive<c10d::ProcessGroup>(store, cfg.rank, cfg.world_size);
   backend->setSequenceNumberForGroup();

@@ -357,52 +357,128 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   }
   RadixSide &B = build_left ? L : R;
   RadixSide &P = build_left ? R : L;
-  at::Tensor counts = ex.empty_i64(nparts);
+  // Output size.  Exact mode: a count kernel over every partition, a scan, then the write
+  // kernel at the scanned offsets.  Fused mode (default): the count kernel runs on every
+  // 32nd partition only, the output is allocated for the extrapolated size + 2 % (partitions
+  // are hash-uniform: the estimate's standard error is ~0.03 % at 1B rows), and the write
+  // kernel counts each partition's matches itself and claims its output rows with one
+  // atomic.  A claim past the allocation makes the kernel report the exact total instead,
+  // and the write runs again into an exact allocation (skewed keys); the row order differs
+  // between runs either way (docs/semantics.md).
+  // test / A-B knobs: CYLON_RJ_EXACT_COUNT=1 (count kernel over every partition),
+  // CYLON_RJ_FUSED_MIN_PARTS (default 4096), CYLON_RJ_ESTIMATE_SCALE (scales the estimate: < 1
+  // forces the exact rerun)
+  const char *ec = std::getenv("CYLON_RJ_EXACT_COUNT");
+  const char *fm = std::getenv("CYLON_RJ_FUSED_MIN_PARTS");
+  const char *es = std::getenv("CYLON_RJ_ESTIMATE_SCALE");
+  const bool exact_count = ec && ec[0] == '1';
+  const int64_t fused_min = fm ? std::atoll(fm) : 4096;
+  const double est_scale = es ? std::atof(es) : 1.0;
+  const int64_t stride = exact_count || nparts < fused_min ? 1 : std::min<int64_t>(32, std::max<int64_t>(1, nparts / 64));
+  const int64_t nsample = (nparts + stride - 1) / stride;
+  at::Tensor counts = ex.empty_i64(nsample);
   at::Tensor overflow = at::empty({1}, ex.opts(at::kInt));
+  at::Tensor out_offs;
+  int64_t m = 0, alloc = 0;
   {
     CYLON_PHASE("join.radix.count", ex.device);
     hip::radix_join_count(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
-                          nparts, cap, ptr<int64_t>(counts), overflow.data_ptr<int>(), ex.stream);
+                          nparts, cap, ptr<int64_t>(counts), overflow.data_ptr<int>(), ex.stream, stride);
+    if (stride == 1) {
+      out_offs = exclusive_scan(ex, counts);
+      at::Tensor tail = at::cat({out_offs.slice(0, nparts, nparts + 1), overflow.to(at::kLong)}).cpu();
+      m = tail[0].item<int64_t>();
+      if (tail[1].item<int64_t>() != 0) {
+        trace::add_counter("join.radix.overflow_fallback", 1);
+        return nullptr;
+      }
+      alloc = m;
+    } else {
+      at::Tensor tail = at::stack({counts.sum(), overflow.to(at::kLong)[0]}).cpu();
+      if (tail[1].item<int64_t>() != 0) {  // a sampled partition already overflows the LDS
+        trace::add_counter("join.radix.overflow_fallback", 1);
+        return nullptr;
+      }
+      const double est = (double)tail[0].item<int64_t>() * (double)nparts / (double)nsample;
+      alloc = (int64_t)(est * 1.02 * est_scale) + (est_scale < 1.0 ? 0 : 65536);
+      trace::add_counter("join.radix.estimated_rows", (int64_t)est);
+    }
   }
-  if (overflow.item<int>() != 0) {
-    trace::add_counter("join.radix.overflow_fallback", 1);
-    return nullptr;
-  }
-  at::Tensor out_offs = exclusive_scan(ex, counts);
-  const int64_t m = read_i64(out_offs, nparts);
   CYLON_PHASE("join.radix.write", ex.device);
   std::vector<Column> lcols, rcols;
+  std::vector<at::Tensor> lwords, rwords;
   int64_t off = 0;
-  if (sink) {
-    std::vector<Column> proto;
-    for (const auto &col : left->columns())
-      proto.emplace_back(cfg.GetLeftTablePrefix() + col.name, col.type, 0, col.data, at::Tensor(), col.validity);
-    for (const auto &col : right->columns())
-      proto.emplace_back(cfg.GetRightTablePrefix() + col.name, col.type, 0, col.data, at::Tensor(), col.validity);
-    off = sink->reserve(ex, m, proto);
-    lcols.assign(sink->cols.begin(), sink->cols.begin() + left->Columns());
-    rcols.assign(sink->cols.begin() + left->Columns(), sink->cols.end());
-  } else {
-    for (const auto &col : left->columns())
-      lcols.push_back(make_fixed_column(cfg.GetLeftTablePrefix() + col.name, col.type, m, ex.device, col.nullable()));
-    for (const auto &col : right->columns())
-      rcols.push_back(make_fixed_column(cfg.GetRightTablePrefix() + col.name, col.type, m, ex.device, col.nullable()));
-  }
-  if (m > 0) {
+  auto allocate = [&](int64_t rows) {
+    lcols.clear();
+    rcols.clear();
+    if (sink) {
+      std::vector<Column> proto;
+      for (const auto &col : left->columns())
+        proto.emplace_back(cfg.GetLeftTablePrefix() + col.name, col.type, 0, col.data, at::Tensor(), col.validity);
+      for (const auto &col : right->columns())
+        proto.emplace_back(cfg.GetRightTablePrefix() + col.name, col.type, 0, col.data, at::Tensor(), col.validity);
+      off = sink->reserve(ex, rows, proto);
+      lcols.assign(sink->cols.begin(), sink->cols.begin() + left->Columns());
+      rcols.assign(sink->cols.begin() + left->Columns(), sink->cols.end());
+    } else {
+      for (const auto &col : left->columns())
+        lcols.push_back(make_fixed_column(cfg.GetLeftTablePrefix() + col.name, col.type, rows, ex.device, col.nullable()));
+      for (const auto &col : right->columns())
+        rcols.push_back(make_fixed_column(cfg.GetRightTablePrefix() + col.name, col.type, rows, ex.device, col.nullable()));
+    }
     auto word_outs = [&](const RadixSide &sd) {
       std::vector<at::Tensor> w;
-      for (size_t i = 0; i < sd.vwords.size(); ++i) w.push_back(ex.empty_i64(m));
+      for (size_t i = 0; i < sd.vwords.size(); ++i) w.push_back(ex.empty_i64(std::max<int64_t>(rows, 1)));
       return w;
     };
-    std::vector<at::Tensor> lwords = word_outs(L), rwords = word_outs(R);
+    lwords = word_outs(L);
+    rwords = word_outs(R);
+  };
+  auto write = [&](int64_t rows, const int64_t *offs, int64_t *cursor) {
     RadixCols pc = build_left ? radix_cols(right, &R, &rcols, off, &rwords) : radix_cols(left, &L, &lcols, off, &lwords);
     RadixCols bc = build_left ? radix_cols(left, &L, &lcols, off, &lwords) : radix_cols(right, &R, &rcols, off, &rwords);
     // probe-side columns are streamed from HBM: the key column is read from its partitioned array
     for (size_t q = 0; q < pc.in.size(); ++q)
       if (!pc.in[q]) pc.in[q] = reinterpret_cast<const uint8_t *>(P.keys.data_ptr());
     hip::radix_join_write(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
-                          nparts, cap, ptr<int64_t>(out_offs), pc.in.data(), pc.out.data(), pc.w.data(),
-                          (int)pc.in.size(), bc.in.data(), bc.out.data(), bc.w.data(), (int)bc.in.size(), ex.stream);
+                          nparts, cap, offs, pc.in.data(), pc.out.data(), pc.w.data(), (int)pc.in.size(),
+                          bc.in.data(), bc.out.data(), bc.w.data(), (int)bc.in.size(), ex.stream, cursor, rows,
+                          overflow.data_ptr<int>());
+  };
+  if (stride == 1) {
+    allocate(m);
+    if (m > 0) write(m, ptr<int64_t>(out_offs), nullptr);
+  } else {
+    at::Tensor cursor = at::zeros({1}, ex.opts(at::kLong));
+    overflow.zero_();
+    allocate(alloc);
+    write(alloc, nullptr, ptr<int64_t>(cursor));
+    at::Tensor res = at::cat({cursor, overflow.to(at::kLong)}).cpu();
+    m = res[0].item<int64_t>();
+    const int64_t flags = res[1].item<int64_t>();
+    if (flags & 1) {  // a build partition beyond the LDS capacity: global-table join instead
+      if (sink) sink->size = off;
+      trace::add_counter("join.radix.overflow_fallback", 1);
+      return nullptr;
+    }
+    if (flags & 2) {  // the estimate was short: write again into an exact allocation
+      trace::add_counter("join.radix.estimate_rerun", 1);
+      if (sink) sink->size = off;
+      cursor.zero_();
+      overflow.zero_();
+      allocate(m);
+      write(m, nullptr, ptr<int64_t>(cursor));
+      CYLON_CHECK(at::cat({cursor, overflow.to(at::kLong)}).cpu().equal(at::tensor({m, (int64_t)0})),
+                  Code::ExecutionError, "radix join: exact rerun did not match its own count");
+    } else if (sink) {
+      sink->size = off + m;  // give back the estimate's slack
+    }
+    if (!sink) {
+      for (auto &c : lcols) c = c.slice(0, m);
+      for (auto &c : rcols) c = c.slice(0, m);
+    }
+  }
+  if (m > 0) {
     unpack_validity_words(ex, left, L, lwords, lcols, off, m);
     unpack_validity_words(ex, right, R, rwords, rcols, off, m);
   }

@@ -544,6 +544,7 @@ void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const 
     off[k + 1] = off[k] + tot;
     PendingTable pt = AllToAllPost(Slice(part, off[k], tot), sc, rc, flags);
     attach_plan(pt, side == 0 ? a : b, plans[side]);
+    count_pending(pt);
     return pt;
   };
   TablePtr pta, ptb;
@@ -558,10 +559,6 @@ void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const 
     for (int k = 1; k < K; ++k) {
       pa[k] = post(pta, ca, 0, k, na_flags, offa);
       pb[k] = post(ptb, cb, 1, k, nb_flags, offb);
-    }
-    for (int k = 0; k < K; ++k) {
-      count_pending(pa[k]);
-      count_pending(pb[k]);
     }
   }
   trace::add_counter("shuffle.rows_in", a->Rows() + b->Rows());

@@ -338,3 +338,34 @@ def test_radix_join_packed_validity_matches_cpu(gpu_ctx, ctx, monkeypatch, algor
                                      right_prefix="r_").to_pandas())
     assert len(res[0]) == len(res[1]) > 0
     assert _rows(res[0]) == _rows(res[1])
+
+
+@pytest.mark.parametrize("mode", ["fused", "fused_rerun", "fused_nullable"])
+def test_radix_join_fused_count_matches_exact(gpu_ctx, monkeypatch, mode):
+    """Fused count (sampled output estimate + per-partition atomic claims in the write kernel) vs the
+    exact count kernel + scan; fused_rerun scales the estimate down so the write kernel overflows its
+    allocation, reports the exact total and runs again; nullable payloads use the packed words."""
+    rng = np.random.default_rng(21)
+    n = 3_000_000
+    kl, kr = rng.integers(0, int(0.9 * n), n), rng.integers(0, int(0.9 * n), n)
+    mask = rng.random(n) < 0.2 if mode == "fused_nullable" else None
+    a = pa.table({"k": kl, "v": pa.array(rng.random(n), mask=mask), "i": rng.integers(-9, 9, n)})
+    b = pa.table({"k": kr, "w": rng.random(n)})
+    L, R = Table(a, gpu_ctx), Table(b, gpu_ctx)
+    on = dict(left_on=["k"], right_on=["k"], left_prefix="l_", right_prefix="r_")
+    monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", "1024")
+    monkeypatch.setenv("CYLON_RJ_FUSED_MIN_PARTS", "64")
+    if mode == "fused_rerun":
+        monkeypatch.setenv("CYLON_RJ_ESTIMATE_SCALE", "0.5")
+    from cylon_amd._lib import C
+    C.trace_enable(True)
+    C.trace_reset()
+    got = L.join(R, "inner", "hash", **on)
+    c = dict(C.trace_counters())
+    C.trace_enable(False)
+    assert c.get("join.radix.estimated_rows", 0) > 0, c  # the fused path ran
+    assert (c.get("join.radix.estimate_rerun", 0) == 1) == (mode == "fused_rerun"), c
+    monkeypatch.setenv("CYLON_RJ_EXACT_COUNT", "1")
+    ref = L.join(R, "inner", "hash", **on)
+    assert got.row_count == ref.row_count == c["join.radix.rows_out"]
+    pd.testing.assert_frame_equal(_sorted_df(got), _sorted_df(ref))

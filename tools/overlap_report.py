@@ -1,30 +1,40 @@
-"""Overlap of the asynchronous transport's delay kernels with the join kernels in a
-rocprofv3 kernel trace (results.db): for every k_spin_delay interval, the compute
-kernels that ran while it was in flight.  Used for profiles/async_overlap_*.txt."""
+"""Overlap of transfer kernels with compute kernels in a rocprofv3 kernel trace (results.db):
+for every transfer-kernel interval, the compute kernels that ran while it was in flight.
+
+  python tools/overlap_report.py <results.db> [transfer substring, default k_spin_delay]
+
+k_spin_delay = the asynchronous delay transport (profiles/async_overlap_*.txt);
+rcclGenericKernel = the RCCL all-to-all kernels of a forced / multi-rank shuffle
+(profiles/rccl_forced_*.txt)."""
 import sqlite3
 import sys
 
 
-def report(db):
+def short(n):
+    return (n or "?").split("(")[0].replace("void ", "").replace("cylon::hip::", "")[:48]
+
+
+def report(db, pat="k_spin_delay"):
     c = sqlite3.connect(db)
     cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
     name = "kernel_name" if "kernel_name" in cols else "name"
     rows = c.execute(f"select {name}, start, end from kernels order by start").fetchall()
-    spins = [(s, e) for n, s, e in rows if "k_spin_delay" in (n or "")]
-    work = [(n, s, e) for n, s, e in rows if "k_spin_delay" not in (n or "") and "rocclr" not in (n or "")]
-    out = [f"{len(spins)} delay kernels, {len(work)} compute kernels"]
+    xfer = [(n, s, e) for n, s, e in rows if pat in (n or "")]
+    work = [(n, s, e) for n, s, e in rows if pat not in (n or "") and "rocclr" not in (n or "")]
+    out = [f"{len(xfer)} transfer kernels ({pat}), {len(work)} compute kernels"]
     total_ov = 0
-    for i, (s, e) in enumerate(spins):
-        ov = [(n, max(s, ws), min(e, we)) for n, ws, we in work if ws < e and we > s]
+    t0 = rows[0][1] if rows else 0
+    for i, (n, s, e) in enumerate(xfer):
+        ov = [(wn, max(s, ws), min(e, we)) for wn, ws, we in work if ws < e and we > s]
         t = sum(b - a for _, a, b in ov)
         total_ov += t
-        names = sorted({(n or "?").split("(")[0].split("<")[0].replace("void ", "")[-40:] for n, _, _ in ov})
-        out.append(f"delay {i:3d}: {(e - s) / 1e3:9.1f} us in flight, {len(ov):4d} compute kernels overlapping "
-                   f"for {t / 1e3:9.1f} us: {', '.join(names[:6])}")
-    span = sum(e - s for s, e in spins)
-    out.append(f"TOTAL delay-in-flight {span / 1e6:.3f} ms, compute overlapped with it {total_ov / 1e6:.3f} ms")
+        names = sorted({short(wn) for wn, _, _ in ov})
+        out.append(f"xfer {i:3d} @ {(s - t0) / 1e6:9.3f} ms: {(e - s) / 1e3:9.1f} us in flight, {len(ov):4d} compute "
+                   f"kernels overlapping for {t / 1e3:9.1f} us: {', '.join(names[:5])}")
+    span = sum(e - s for _, s, e in xfer)
+    out.append(f"TOTAL transfer-in-flight {span / 1e6:.3f} ms, compute overlapped with it {total_ov / 1e6:.3f} ms")
     return "\n".join(out)
 
 
 if __name__ == "__main__":
-    print(report(sys.argv[1]))
+    print(report(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "k_spin_delay"))
