@@ -397,6 +397,160 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   }
 }
 
+// Register-lean pass: the same tile algorithm (8192-row tiles, LDS-atomic ranking, one
+// 64 KB column stage), restructured so that TWO 1024-thread blocks fit a CU (<= 64 VGPRs,
+// 76 KB LDS each): one block's ranking / scans / barriers then run while the other block's
+// columns stream, instead of leaving the CU's share of HBM idle for a third of every tile
+// (profiles/rank_variants_r02.txt: 33 % of a join tile has no memory traffic).  What the
+// classic kernel held in registers across phases is dropped or packed:
+//   * no cross-column / cross-tile prefetch (the second block hides the load latency);
+//   * the destination of sorted slot j is packed as (digit << 16 | j - toff[digit]) and
+//     completed from running[] in LDS at store time (8 VGPRs instead of 16).
+template <class Digit, bool W8, int RANK>
+__global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_rows_pass_lean(
+    Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
+    const int64_t *__restrict__ bh_scan) {
+  constexpr int THREADS = kRPThreads, WAVES = THREADS / kWave, TILE = THREADS * kRPItems;
+  constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;
+  static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 2 <= TILE * 8, "ranking scratch must fit the stage");
+  __shared__ int64_t running[kRPMaxBuckets];
+  __shared__ uint32_t toff[kRPMaxBuckets + 1];
+  __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16 or bcnt[nb] u32, sdig[TILE] u16}
+  __shared__ uint32_t wsum[WAVES];
+  constexpr bool STABLE = RANK != kRankBlockAtomic;
+  uint16_t *wcnt = reinterpret_cast<uint16_t *>(ustage);
+  uint32_t *bcnt = reinterpret_cast<uint32_t *>(ustage);
+  uint16_t *sdig = wcnt + WAVES * kRPMaxBuckets;
+  uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
+  (void)nbits;
+
+  const int64_t b = blockIdx.x;
+  for (uint32_t p = threadIdx.x; p < nbuckets; p += THREADS) running[p] = bh_scan[(int64_t)p * nblocks + b];
+  // wave index made provably uniform: per-wave base pointers then live in SGPRs and every
+  // load / store addresses its row with a 32-bit lane offset plus an immediate
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t begin = b * rows_per_block;
+  const int64_t end = (begin + rows_per_block < n) ? begin + rows_per_block : n;
+  uint16_t *mycnt = wcnt + wave * nbuckets;
+  const int wrow = wave * kWave * kRPItems;
+
+  for (int64_t tile = begin; tile < end; tile += TILE) {
+    const int cnt = (int)((end - tile) < TILE ? (end - tile) : TILE);
+    // per-thread constants are recomputed every tile from an opaque copy of the thread id:
+    // hoisted out of the tile loop they outlive the 64-VGPR budget and spill
+    int tx = (int)threadIdx.x;
+    asm volatile("" : "+v"(tx));
+    const int lane = tx & (kWave - 1);
+    uint32_t pl[kRPItems];  // digit | in-tile rank << 16, then the sorted slot; ~0 = inactive
+    const int64_t *kbase = digit.keys + tile + wrow;  // wave-uniform
+    const int lim = cnt - wrow;                       // rows of this wave's slice that exist
+    {  // the keys are not held across the ranking: column 0 re-reads them (L2 hits) like any column
+      uint64_t kk[kRPItems];
+#pragma unroll
+      for (int k = 0; k < kRPItems; ++k) kk[k] = (k * kWave + lane < lim) ? (uint64_t)kbase[k * kWave + lane] : 0ull;
+#pragma unroll
+      for (int k = 0; k < kRPItems; ++k) pl[k] = (k * kWave + lane < lim) ? digit.of_key((int64_t)kk[k]) : 0xffffffffu;
+    }
+    if (STABLE) {
+      for (uint32_t q = tx; q < WAVES * nbuckets; q += THREADS) wcnt[q] = 0;
+    } else {
+      for (uint32_t q = tx; q < nbuckets; q += THREADS) bcnt[q] = 0;
+    }
+    __syncthreads();  // also: the previous tile's stage reads are done
+    if (!STABLE) {
+#pragma unroll
+      for (int k = 0; k < kRPItems; ++k)
+        if (pl[k] != 0xffffffffu) pl[k] |= atomicAdd(&bcnt[pl[k]], 1u) << 16;
+    } else {
+      uint32_t *myw = reinterpret_cast<uint32_t *>(mycnt);
+#pragma unroll
+      for (int k = 0; k < kRPItems; ++k)
+        if (pl[k] != 0xffffffffu) {
+          const uint32_t p = pl[k], sh = (p & 1u) * 16u;
+          pl[k] |= ((atomicAdd(&myw[p >> 1], 1u << sh) >> sh) & 0xffffu) << 16;
+        }
+    }
+    __syncthreads();
+    {
+      uint32_t loc[BPT];
+      uint32_t total = 0;
+#pragma unroll
+      for (int i = 0; i < BPT; ++i) {
+        const uint32_t p = tx * BPT + i;
+        loc[i] = total;
+        uint32_t run = 0;
+        if (p < nbuckets) {
+          if (STABLE) {
+#pragma unroll
+            for (int w = 0; w < WAVES; ++w) {
+              const uint32_t c = wcnt[w * nbuckets + p];
+              wcnt[w * nbuckets + p] = (uint16_t)run;
+              run += c;
+            }
+          } else {
+            run = bcnt[p];
+          }
+        }
+        total += run;
+      }
+      const uint32_t ex = rp_block_exscan<WAVES>(total, wsum);
+#pragma unroll
+      for (int i = 0; i < BPT; ++i) {
+        const uint32_t p = tx * BPT + i;
+        if (p < nbuckets) toff[p] = ex + loc[i];
+      }
+      if (tx == THREADS - 1) toff[nbuckets] = ex + total;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kRPItems; ++k) {
+      if (pl[k] == 0xffffffffu) continue;
+      const uint32_t p = pl[k] & 0xffffu;
+      const uint32_t pos = toff[p] + (STABLE ? (uint32_t)wcnt[wave * nbuckets + p] : 0u) + (pl[k] >> 16);
+      sdig[pos] = (uint16_t)p;
+      pl[k] = pos;
+    }
+    __syncthreads();
+    uint32_t dp[kRPItems];  // sorted slot j = tx + q * THREADS -> digit << 16 | offset in its run
+#pragma unroll
+    for (int q = 0; q < kRPItems; ++q) {
+      const int j = tx + q * THREADS;
+      const uint32_t p = j < cnt ? sdig[j] : 0u;
+      dp[q] = (p << 16) | (uint32_t)(j - (int)toff[p]);
+    }
+    __syncthreads();  // counters / digits dead: the union becomes the column stage
+#pragma unroll 1
+    for (int c = 0; c < cols.n; ++c) {
+      const int w = cols.width[c];
+      uint8_t *out = cols.out[c];
+      uint64_t v[kRPItems];
+      const uint8_t *in = cols.in[c];
+      if (in == nullptr) {  // generated row-id column (computed here, not hoisted: 16 VGPRs)
+        int64_t rbase = tile + wrow;
+        asm volatile("" : "+s"(rbase));
+#pragma unroll
+        for (int k = 0; k < kRPItems; ++k) v[k] = (uint64_t)(rbase + k * kWave + lane);
+      } else {
+        const uint8_t *ibase = in + (tile + wrow) * (int64_t)w;  // wave-uniform
+#pragma unroll
+        for (int k = 0; k < kRPItems; ++k) v[k] = (k * kWave + lane < lim) ? ldw<W8>(ibase, k * kWave + lane, w) : 0ull;
+      }
+      const uint64_t x = c == 0 ? cols.key_xor : 0ull;
+#pragma unroll
+      for (int k = 0; k < kRPItems; ++k)
+        if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < kRPItems; ++q) {
+        const int j = tx + q * THREADS;
+        if (j < cnt) stw<W8>(out, running[dp[q] >> 16] + (int64_t)(dp[q] & 0xffffu), w, ldw<W8>(st, j, w));
+      }
+      __syncthreads();
+    }
+    for (uint32_t p = tx; p < nbuckets; p += THREADS) running[p] += toff[p + 1] - toff[p];
+  }
+}
+
 struct RPGeometry {
   int64_t nblocks, rows_per_block;
 };
@@ -482,10 +636,24 @@ bool lds_lane_order_ok(void *stream) {
 }
 static bool rp_wave_atomic(hipStream_t s) { return lds_lane_order_ok(reinterpret_cast<void *>(s)); }
 
-static RPGeometry rp_geometry(int64_t n, int threads) {
+// Pass kernel: "lean" (two register-lean blocks per CU) or "classic" (one block per CU with
+// register software pipelining).  Measured on one box, same tree (profiles/r03/lean_pass_ab.txt):
+// lean wins for passes that move 1-2 columns (2B-row sort 107.5 -> 99.2 ms, 1B group-by 27.6 ->
+// 25.0 ms; its two blocks overlap each other's ranking and barriers) and loses for the 4-column
+// join passes (17.9 -> 20.0 ms per pass: without the classic kernel's next-column prefetch each
+// column's load latency is exposed).  CYLON_RP_KERNEL=lean|classic forces one (read per launch).
+static bool rp_lean(int ncols) {
+  const char *e = std::getenv("CYLON_RP_KERNEL");
+  if (e && std::string(e) == "lean") return true;
+  if (e && std::string(e) == "classic") return false;
+  return ncols <= 2;
+}
+
+// resident: blocks per CU that run at once (lean pass: 2 x 1024 threads)
+static RPGeometry rp_geometry(int64_t n, int threads, int resident = 1) {
   const int64_t tile = (int64_t)threads * kRPItems;
   const int64_t tiles = std::max<int64_t>(1, (n + tile - 1) / tile);
-  const int64_t want = 2 * kNumCUs * (1024 / threads);  // two rounds of resident blocks (16 waves per CU)
+  const int64_t want = 2 * kNumCUs * (1024 / threads) * resident;  // two rounds of resident blocks
   const int64_t nb = tiles < want ? tiles : want;
   RPGeometry g;
   g.rows_per_block = ((tiles + nb - 1) / nb) * tile;
@@ -493,10 +661,11 @@ static RPGeometry rp_geometry(int64_t n, int threads) {
   return g;
 }
 
-int64_t radix_rows_pass_workspace(int64_t n, int digit_bits) {  // covers both block sizes
+int64_t radix_rows_pass_workspace(int64_t n, int digit_bits) {  // covers both block sizes and the lean pass
   int64_t ws = 0;
-  for (int threads : {512, 1024}) {
-    const int64_t m = rp_geometry(n, threads).nblocks * (int64_t(1) << digit_bits);
+  for (int threads : {512, 1024, 2048}) {
+    const int64_t m = (threads == 2048 ? rp_geometry(n, 1024, 2) : rp_geometry(n, threads)).nblocks *
+                      (int64_t(1) << digit_bits);
     ws = std::max(ws, m + (m + 1) + scan_workspace(m));
   }
   return ws;
@@ -567,10 +736,15 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   hipStream_t s = as_stream(stream);
   const uint32_t nb = 1u << digit_bits;
   CYLON_CHECK(stable || CAN_UNSTABLE, Code::Invalid, "radix pass: only partition digits may rank unstably");
+  // test knob: every partition pass ranks unstably, so LSD passes after the first scramble the
+  // order they received -- rows end in wrong partitions and the join's ranking guard must fire
+  const char *dbg = std::getenv("CYLON_RP_DEBUG_UNSTABLE");
+  if (CAN_UNSTABLE && dbg && dbg[0] == '1') stable = false;
   const bool unstable = CAN_UNSTABLE && !stable;
   const bool wave_atomic = !unstable && rp_wave_atomic(s);
   const int threads = rp_threads(ncols, unstable || wave_atomic);
-  const RPGeometry g = rp_geometry(n, threads);
+  const bool lean = rp_lean(ncols) && (unstable || wave_atomic) && threads == 1024;
+  const RPGeometry g = rp_geometry(n, threads, lean ? 2 : 1);
   const int64_t m = g.nblocks * (int64_t)nb;
   int64_t *bh = ws, *bh_scan = ws + m, *scan_ws = bh_scan + m + 1;
   hipLaunchKernelGGL(k_rp_hist<Digit>, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, n, nb,
@@ -592,6 +766,23 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
                 "radix pass: a generated row-id column must be an 8-byte payload column");
   }
   const bool big = threads == 1024;
+  if (lean) {
+    constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankWaveAtomic;
+    if (unstable && w8)
+      hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, R>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg,
+                         digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan);
+    else if (unstable)
+      hipLaunchKernelGGL((k_rows_pass_lean<Digit, false, R>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg,
+                         digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan);
+    else if (w8)
+      hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, kRankWaveAtomic>), dim3((unsigned)g.nblocks),
+                         dim3(kRPThreads), 0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan);
+    else
+      hipLaunchKernelGGL((k_rows_pass_lean<Digit, false, kRankWaveAtomic>), dim3((unsigned)g.nblocks),
+                         dim3(kRPThreads), 0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan);
+    HIP_LAUNCH_CHECK();
+    return;
+  }
   if (unstable) {
     constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankBallot;
     if (big) rows_pass_kernel<Digit, 1024, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
@@ -805,6 +996,7 @@ __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4)))
   __shared__ uint32_t wsum[kRCWaves];
   __shared__ unsigned long long csum[kRCWaves];
   const int64_t nsample = (nparts + pstride - 1) / pstride;
+  const int pbits = __builtin_ctzll((unsigned long long)nparts);  // nparts = 2^bits
   for (int64_t ci = blockIdx.x; ci < nsample; ci += gridDim.x) {
     const int64_t p = ci * pstride;
     const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
@@ -826,10 +1018,15 @@ __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4)))
     for (int s = threadIdx.x; s < kRJBuckets / 2; s += blockDim.x) reinterpret_cast<uint32_t *>(bst)[s] = 0;
     __syncthreads();
     uint32_t rk[kRCRowsPerThread];
+    bool misplaced = false;  // ranking guard: a row whose key hashes to another partition
 #pragma unroll
     for (int i = 0; i < kRCRowsPerThread; ++i) {
       const int r = threadIdx.x + i * kRCThreads;
-      if (r < nr) rk[i] = rj_claim(bst, rj_bucket(bkeys[rb + r]));
+      if (r < nr) {
+        const int64_t k = bkeys[rb + r];
+        misplaced |= part_of(k, pbits) != (uint32_t)p;
+        rk[i] = rj_claim(bst, rj_bucket(k));
+      }
     }
     __syncthreads();
     rj_scan_buckets<kRCThreads>(bst, wsum);
@@ -851,8 +1048,12 @@ __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4)))
         if (l0 + u * kRCThreads < nl) pk[u] = pkeys[lb + l0 + u * kRCThreads];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (l0 + u * kRCThreads < nl) c += rj_count(bst, skeys, pk[u]);
+        if (l0 + u * kRCThreads < nl) {
+          misplaced |= part_of(pk[u], pbits) != (uint32_t)p;
+          c += rj_count(bst, skeys, pk[u]);
+        }
     }
+    if (misplaced) atomicOr(overflow, 4);
     for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
     if (lane_id() == 0) csum[threadIdx.x / kWave] = c;
     __syncthreads();
@@ -903,6 +1104,8 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
   uint16_t *perm = reinterpret_cast<uint16_t *>(area + 8 * (int64_t)cap);
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
+  const int pbits = __builtin_ctzll((unsigned long long)nparts);  // nparts = 2^bits
+  bool misplaced = false;  // ranking guard (overflow bit 4): a row whose key hashes elsewhere
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
     const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
     const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
@@ -929,7 +1132,10 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
 #pragma unroll
     for (int i = 0; i < kRJRowsPerThread; ++i) {
       const int r = threadIdx.x + i * kRJThreads;
-      if (r < nr) bk[i] = bkeys[rb + r];
+      if (r < nr) {
+        bk[i] = bkeys[rb + r];
+        misplaced |= part_of(bk[i], pbits) != (uint32_t)p;
+      }
     }
     // ---- phase B: stage + index the build rows
     __syncthreads();  // previous partition fully done with bst / area / wtot
@@ -1020,6 +1226,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
       }
       uint32_t i0 = 0, i1 = 0, mc = 0;
       if (active) {
+        misplaced |= part_of(k, pbits) != (uint32_t)p;
         const uint32_t b = rj_bucket(k);
         i0 = bst[b];
         i1 = bst[b + 1];
@@ -1085,6 +1292,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
       base += wsum;
     }
   }
+  if (misplaced && overflow != nullptr) atomicOr(overflow, 4);
 }
 
 static int rj_grid(int64_t nparts) { return (int)std::min<int64_t>(nparts, kNumCUs * 8); }

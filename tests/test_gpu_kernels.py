@@ -369,3 +369,33 @@ def test_radix_join_fused_count_matches_exact(gpu_ctx, monkeypatch, mode):
     ref = L.join(R, "inner", "hash", **on)
     assert got.row_count == ref.row_count == c["join.radix.rows_out"]
     pd.testing.assert_frame_equal(_sorted_df(got), _sorted_df(ref))
+
+
+@pytest.mark.parametrize("count_mode", ["fused", "exact"])
+def test_radix_join_ranking_guard_falls_back(gpu_ctx, monkeypatch, count_mode):
+    """The LSD partition passes after the first must keep the order they receive (wave-atomic
+    stable ranking).  CYLON_RP_DEBUG_UNSTABLE=1 breaks that on purpose: rows then sit in partitions
+    their keys do not hash to, the count / write kernels' per-row guard (part_of(key) == partition)
+    flags it, and the join falls back to the global-table path with a correct result."""
+    rng = np.random.default_rng(8)
+    n = 6_000_000  # 11 partition bits: two LSD passes
+    a = pa.table({"k": rng.integers(0, n, n), "v": rng.random(n)})
+    b = pa.table({"k": rng.integers(0, n, n), "w": rng.random(n)})
+    L, R = Table(a, gpu_ctx), Table(b, gpu_ctx)
+    on = dict(left_on=["k"], right_on=["k"], left_prefix="l_", right_prefix="r_")
+    monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", "1024")
+    if count_mode == "fused":
+        monkeypatch.setenv("CYLON_RJ_FUSED_MIN_PARTS", "64")
+    else:
+        monkeypatch.setenv("CYLON_RJ_EXACT_COUNT", "1")
+    from cylon_amd._lib import C
+    ref = L.join(R, "inner", "hash", **on)
+    monkeypatch.setenv("CYLON_RP_DEBUG_UNSTABLE", "1")
+    C.trace_enable(True)
+    C.trace_reset()
+    got = L.join(R, "inner", "hash", **on)
+    c = dict(C.trace_counters())
+    C.trace_enable(False)
+    assert c.get("join.radix.order_violation_fallback", 0) == 1, c
+    assert got.row_count == ref.row_count
+    pd.testing.assert_frame_equal(_sorted_df(got), _sorted_df(ref))
