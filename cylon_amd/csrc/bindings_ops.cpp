@@ -39,6 +39,12 @@ void register_extended_ops(py::module &m) {
   m.def("index_lookup", &ops::IndexLookup, py::arg("ctx"), py::arg("index"), py::arg("labels"), rel);
 
   // ---- device self-check behind the radix passes' wave-atomic stable ranking (radix_join.hip)
+  m.def("rp_reset_lane_order", []() { hip::rp_reset_lane_order(); });
+  m.def("rp_take_order_violation", [](const std::string &device) {
+    ops::Exec ex{at::Device(device)};
+    CYLON_CHECK(ex.gpu, Code::Invalid, "rp_take_order_violation needs a GPU device");
+    return hip::rp_take_order_violation(ex.stream);
+  });
   m.def("lds_lane_order_violations", [](const std::string &device, int blocks, int rounds) {
     ops::Exec ex{at::Device(device)};
     CYLON_CHECK(ex.gpu, Code::Invalid, "lds_lane_order_violations needs a GPU device");

@@ -2,11 +2,13 @@
 // Reference: cpp/src/cylon/data_types.hpp, column.cpp, table.cpp:1-61 (ctor),
 // ctx/cylon_context.cpp:25-108.
 #include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPGuard.h>
 
 #include <cstdlib>
 
 #include "column.hpp"
 #include "ctx/cylon_context.hpp"
+#include "kernels/kernels.hpp"
 #include "table.hpp"
 
 namespace cylon {
@@ -191,10 +193,19 @@ TablePtr Table::to(at::Device dev) const {
 // ---------------------------------------------------------------------------
 CylonContext::CylonContext(bool distributed) : distributed_(distributed) {}
 
+// GPU contexts run the radix passes' lane-order self-check once per device here, so that
+// no pass allocates or synchronises for it (and stream capture of a pass stays possible)
+static void warm_device(const at::Device &device) {
+  if (!device.is_cuda()) return;
+  c10::hip::HIPGuard guard(device.index());
+  hip::lds_lane_order_ok(reinterpret_cast<void *>(c10::hip::getCurrentHIPStream(device.index()).stream()));
+}
+
 std::shared_ptr<CylonContext> CylonContext::Init(at::Device device) {
   auto ctx = std::make_shared<CylonContext>(false);
   ctx->communicator_ = std::make_shared<net::LocalCommunicator>();
   ctx->device_ = device;
+  warm_device(device);
   return ctx;
 }
 
@@ -204,6 +215,7 @@ std::shared_ptr<CylonContext> CylonContext::InitDistributed(std::shared_ptr<net:
   auto ctx = std::make_shared<CylonContext>(true);
   ctx->communicator_ = std::move(comm);
   ctx->device_ = device;
+  warm_device(device);
   return ctx;
 }
 

@@ -23,6 +23,7 @@
 //      owns a contiguous slice of the probe rows (wave-level scans only).
 // Partitions whose build side exceeds the LDS capacity are reported; the
 // caller then falls back to the global-table join.
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -52,6 +53,11 @@ struct ColSet {
   int width[kMaxFusedCols];
   int n;
   uint64_t key_xor;  // XORed into column 0 as it is stored (a sort's last pass rebuilds int64 keys from images)
+  // Ranking guard (passes that must be stable): inside every bucket run of the sorted tile the
+  // input rows must ascend; a violation -- the wave-atomic ranking relies on gfx950 returning one
+  // instruction's same-address LDS atomics in lane order -- sets *order_bad.
+  int check_order;
+  int *order_bad;
 };
 
 __device__ __forceinline__ uint32_t part_of(int64_t key, int bits) {
@@ -220,17 +226,19 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   constexpr int WAVES = THREADS / kWave;
   constexpr int TILE = THREADS * kRPItems;
   constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;  // buckets per thread in the offset scan
-  static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 2 <= TILE * 8, "ranking scratch must fit the stage");
+  static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 2 * 2 <= TILE * 8, "ranking scratch must fit the stage");
   __shared__ int64_t running[kRPMaxBuckets];
   __shared__ uint32_t toff[kRPMaxBuckets + 1];
-  __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16, sdig[TILE] u16}
+  __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16, sdig[TILE] u16, srow[TILE] u16}
   __shared__ uint32_t wsum[WAVES];
   uint16_t *wcnt = reinterpret_cast<uint16_t *>(ustage);
   constexpr bool STABLE = RANK != kRankBlockAtomic;
   uint32_t *bcnt = reinterpret_cast<uint32_t *>(ustage);  // block-atomic ranking: block-wide counters
   static_assert(WAVES * kRPMaxBuckets * 2 >= kRPMaxBuckets * 4, "block counters must fit the wave counters");
   uint16_t *sdig = wcnt + WAVES * kRPMaxBuckets;
+  uint16_t *srow = sdig + TILE;  // input row (in the tile) of sorted slot j: the ranking guard
   uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
+  bool order_bad = false;
 
   const int64_t b = blockIdx.x;
   for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] = bh_scan[(int64_t)p * nblocks + b];
@@ -337,6 +345,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       const uint32_t p = pl[k] & 0xffffu;
       const uint32_t pos = toff[p] + (STABLE ? (uint32_t)wcnt[wave * nbuckets + p] : 0u) + (pl[k] >> 16);
       sdig[pos] = (uint16_t)p;
+      if (cols.check_order) srow[pos] = (uint16_t)(wrow + k * kWave + lane);
       pl[k] = pos;
     }
     __syncthreads();
@@ -348,6 +357,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       if (j < cnt) {
         const uint32_t p = sdig[j];
         dst[q] = running[p] + (j - (int64_t)toff[p]);
+        if (cols.check_order && j > 0 && sdig[j - 1] == p && srow[j - 1] > srow[j]) order_bad = true;
       }
     }
     __syncthreads();  // counters / digits dead: the union becomes the column stage
@@ -395,6 +405,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] += toff[p + 1] - toff[p];
   }
+  if (order_bad) atomicOr(cols.order_bad, 1);
 }
 
 // Register-lean pass: the same tile algorithm (8192-row tiles, LDS-atomic ranking, one
@@ -412,7 +423,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
     const int64_t *__restrict__ bh_scan) {
   constexpr int THREADS = kRPThreads, WAVES = THREADS / kWave, TILE = THREADS * kRPItems;
   constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;
-  static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 2 <= TILE * 8, "ranking scratch must fit the stage");
+  static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 2 * 2 <= TILE * 8, "ranking scratch must fit the stage");
   __shared__ int64_t running[kRPMaxBuckets];
   __shared__ uint32_t toff[kRPMaxBuckets + 1];
   __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16 or bcnt[nb] u32, sdig[TILE] u16}
@@ -421,7 +432,9 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
   uint16_t *wcnt = reinterpret_cast<uint16_t *>(ustage);
   uint32_t *bcnt = reinterpret_cast<uint32_t *>(ustage);
   uint16_t *sdig = wcnt + WAVES * kRPMaxBuckets;
+  uint16_t *srow = sdig + TILE;  // ranking guard (see ColSet::check_order)
   uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
+  bool order_bad = false;
   (void)nbits;
 
   const int64_t b = blockIdx.x;
@@ -508,6 +521,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
       const uint32_t p = pl[k] & 0xffffu;
       const uint32_t pos = toff[p] + (STABLE ? (uint32_t)wcnt[wave * nbuckets + p] : 0u) + (pl[k] >> 16);
       sdig[pos] = (uint16_t)p;
+      if (cols.check_order) srow[pos] = (uint16_t)(wrow + k * kWave + lane);
       pl[k] = pos;
     }
     __syncthreads();
@@ -517,6 +531,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
       const int j = tx + q * THREADS;
       const uint32_t p = j < cnt ? sdig[j] : 0u;
       dp[q] = (p << 16) | (uint32_t)(j - (int)toff[p]);
+      if (cols.check_order && j > 0 && j < cnt && sdig[j - 1] == p && srow[j - 1] > srow[j]) order_bad = true;
     }
     __syncthreads();  // counters / digits dead: the union becomes the column stage
 #pragma unroll 1
@@ -549,6 +564,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
     }
     for (uint32_t p = tx; p < nbuckets; p += THREADS) running[p] += toff[p + 1] - toff[p];
   }
+  if (order_bad) atomicOr(cols.order_bad, 1);
 }
 
 struct RPGeometry {
@@ -577,17 +593,22 @@ static int rp_threads(int ncols, bool cheap_rank) {
 // stable rank from ballots (count before + #lower lanes in the same bucket).  gfx950
 // returns same-address LDS atomics of one instruction in lane order: 0 violations in
 // 4.3e10 lane-ops (tools/lds_atomic_order.hip, profiles/rank_variants_r02.txt).
-constexpr int kLOThreads = 256;
-__global__ __launch_bounds__(kLOThreads) void k_lane_order_check(int rounds, unsigned long long *bad) {
-  __shared__ uint32_t cnt[(kLOThreads / kWave) * (kRPMaxBuckets / 2)];
+// The probe runs the shapes the ranking code launches: 1024-thread blocks with packed 16-bit
+// counters (k_rows_pass, k_rows_pass_lean) and 256-thread blocks with 32-bit counters
+// (stable_rank.hpp k_stable_rank).
+template <int THREADS, bool PACKED16>
+__global__ __launch_bounds__(THREADS) void k_lane_order_check(int rounds, unsigned long long *bad) {
+  constexpr int WORDS = PACKED16 ? kRPMaxBuckets / 2 : kRPMaxBuckets;
+  __shared__ uint32_t cnt[(THREADS / kWave) * WORDS];
   const int wave = threadIdx.x / kWave, lane = lane_id();
   const uint64_t lt = lanemask_lt();
-  uint32_t *mine = cnt + wave * (kRPMaxBuckets / 2);
+  uint32_t *mine = cnt + wave * WORDS;
   unsigned long long nbad = 0;
-  for (int r0 = 0; r0 < rounds; r0 += 256) {  // 16-bit halves: restart every 256 rounds
-    for (int q = lane; q < kRPMaxBuckets / 2; q += kWave) mine[q] = 0;
+  constexpr int RESTART = PACKED16 ? 256 : 1 << 20;  // 16-bit halves: restart every 256 rounds
+  for (int r0 = 0; r0 < rounds; r0 += RESTART) {
+    for (int q = lane; q < WORDS; q += kWave) mine[q] = 0;
     __builtin_amdgcn_wave_barrier();
-    for (int r = r0; r < r0 + 256 && r < rounds; ++r) {
+    for (int r = r0; r < r0 + RESTART && r < rounds; ++r) {
       const int nbits = 1 + (r % 10);
       const uint32_t b = (uint32_t)hashing::fmix64(((uint64_t)blockIdx.x << 40) ^ ((uint64_t)r << 12) ^ threadIdx.x) &
                          ((1u << nbits) - 1u);
@@ -597,10 +618,17 @@ __global__ __launch_bounds__(kLOThreads) void k_lane_order_check(int rounds, uns
         const uint64_t bb = __ballot(x);
         m &= x ? bb : ~bb;
       }
-      const uint32_t sh = (b & 1u) * 16u;
-      const uint32_t before = (mine[b >> 1] >> sh) & 0xffffu;
-      __builtin_amdgcn_wave_barrier();
-      const uint32_t got = (atomicAdd(&mine[b >> 1], 1u << sh) >> sh) & 0xffffu;
+      uint32_t before, got;
+      if (PACKED16) {
+        const uint32_t sh = (b & 1u) * 16u;
+        before = (mine[b >> 1] >> sh) & 0xffffu;
+        __builtin_amdgcn_wave_barrier();
+        got = (atomicAdd(&mine[b >> 1], 1u << sh) >> sh) & 0xffffu;
+      } else {
+        before = mine[b];
+        __builtin_amdgcn_wave_barrier();
+        got = atomicAdd(&mine[b], 1u);
+      }
       __builtin_amdgcn_wave_barrier();
       nbad += got != before + (uint32_t)__popcll(m & lt);
     }
@@ -614,7 +642,11 @@ int64_t lds_lane_order_violations(int blocks, int rounds, void *stream) {
   unsigned long long *d = nullptr, h = 0;
   HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&d), sizeof(h)));
   HIP_CHECK(hipMemsetAsync(d, 0, sizeof(h), s));
-  hipLaunchKernelGGL(k_lane_order_check, dim3((unsigned)blocks), dim3(kLOThreads), 0, s, rounds, d);
+  hipLaunchKernelGGL((k_lane_order_check<256, true>), dim3((unsigned)blocks), dim3(256), 0, s, rounds, d);
+  HIP_LAUNCH_CHECK();
+  hipLaunchKernelGGL((k_lane_order_check<1024, true>), dim3((unsigned)blocks), dim3(1024), 0, s, rounds / 4, d);
+  HIP_LAUNCH_CHECK();
+  hipLaunchKernelGGL((k_lane_order_check<256, false>), dim3((unsigned)blocks), dim3(256), 0, s, rounds, d);
   HIP_LAUNCH_CHECK();
   HIP_CHECK(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
@@ -622,8 +654,19 @@ int64_t lds_lane_order_violations(int blocks, int rounds, void *stream) {
   return (int64_t)h;
 }
 
-// Stable ranking method: wave-atomic when the device passes the lane-order self-check
-// (run once per process), else ballots.  CYLON_RP_RANK=wave|ballot forces one.
+// Stable ranking method per device: wave-atomic when the device passed the lane-order
+// self-check (run once per device, at context creation -- CylonContext::Init calls
+// lds_lane_order_ok -- not inside a pass), else ballots.  A stability violation seen by a
+// pass's ranking guard (rp_take_order_violation) switches the device to ballots for the rest
+// of the process.  CYLON_RP_RANK=wave|ballot forces one.
+static std::atomic<int> g_lane_ok[64];  // 0 unknown, 1 ok, 2 not ok
+
+static int current_device() {
+  int d = 0;
+  HIP_CHECK(hipGetDevice(&d));
+  return d & 63;
+}
+
 bool lds_lane_order_ok(void *stream) {
   static const int forced = [] {
     const char *e = std::getenv("CYLON_RP_RANK");
@@ -631,8 +674,49 @@ bool lds_lane_order_ok(void *stream) {
     return std::string(e) == "wave" ? 1 : (std::string(e) == "ballot" ? 0 : -1);
   }();
   if (forced >= 0) return forced == 1;
-  static const bool ok = lds_lane_order_violations(64, 1024, stream) == 0;
-  return ok;
+  std::atomic<int> &st = g_lane_ok[current_device()];
+  int v = st.load();
+  if (v == 0) {
+    v = lds_lane_order_violations(64, 1024, stream) == 0 ? 1 : 2;
+    int expect = 0;
+    st.compare_exchange_strong(expect, v);
+    v = st.load();
+  }
+  return v == 1;
+}
+
+// per-device flag the passes' ranking guard raises (allocated once per device)
+static int *order_flag() {
+  static std::atomic<int *> flags[64];
+  const int d = current_device();
+  int *f = flags[d].load();
+  if (!f) {
+    HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&f), sizeof(int)));
+    HIP_CHECK(hipMemset(f, 0, sizeof(int)));
+    int *expect = nullptr;
+    if (!flags[d].compare_exchange_strong(expect, f)) {
+      HIP_CHECK(hipFree(f));
+      f = expect;
+    }
+  }
+  return f;
+}
+
+void rp_reset_lane_order() {  // forget every device's ranking verdict (tests): re-probe on next use
+  for (auto &v : g_lane_ok) v.store(0);
+}
+
+bool rp_take_order_violation(void *stream) {
+  hipStream_t s = as_stream(stream);
+  int h = 0;
+  int *f = order_flag();
+  HIP_CHECK(hipMemcpyAsync(&h, f, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  if (h) {
+    HIP_CHECK(hipMemsetAsync(f, 0, sizeof(int), s));
+    g_lane_ok[current_device()].store(2);  // stable passes rank with ballots from now on
+  }
+  return h != 0;
 }
 static bool rp_wave_atomic(hipStream_t s) { return lds_lane_order_ok(reinterpret_cast<void *>(s)); }
 
@@ -738,6 +822,7 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   CYLON_CHECK(stable || CAN_UNSTABLE, Code::Invalid, "radix pass: only partition digits may rank unstably");
   // test knob: every partition pass ranks unstably, so LSD passes after the first scramble the
   // order they received -- rows end in wrong partitions and the join's ranking guard must fire
+  const bool want_stable = stable;  // the ranking guard checks what the caller asked for
   const char *dbg = std::getenv("CYLON_RP_DEBUG_UNSTABLE");
   if (CAN_UNSTABLE && dbg && dbg[0] == '1') stable = false;
   const bool unstable = CAN_UNSTABLE && !stable;
@@ -754,6 +839,8 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   ColSet cs;
   cs.n = ncols;
   cs.key_xor = key_xor;
+  cs.check_order = want_stable ? 1 : 0;
+  cs.order_bad = order_flag();
   for (int c = 0; c < kMaxFusedCols; ++c) {
     cs.in[c] = c < ncols ? in[c] : nullptr;
     cs.out[c] = c < ncols ? out[c] : nullptr;
@@ -996,7 +1083,6 @@ __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4)))
   __shared__ uint32_t wsum[kRCWaves];
   __shared__ unsigned long long csum[kRCWaves];
   const int64_t nsample = (nparts + pstride - 1) / pstride;
-  const int pbits = __builtin_ctzll((unsigned long long)nparts);  // nparts = 2^bits
   for (int64_t ci = blockIdx.x; ci < nsample; ci += gridDim.x) {
     const int64_t p = ci * pstride;
     const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
@@ -1018,15 +1104,10 @@ __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4)))
     for (int s = threadIdx.x; s < kRJBuckets / 2; s += blockDim.x) reinterpret_cast<uint32_t *>(bst)[s] = 0;
     __syncthreads();
     uint32_t rk[kRCRowsPerThread];
-    bool misplaced = false;  // ranking guard: a row whose key hashes to another partition
 #pragma unroll
     for (int i = 0; i < kRCRowsPerThread; ++i) {
       const int r = threadIdx.x + i * kRCThreads;
-      if (r < nr) {
-        const int64_t k = bkeys[rb + r];
-        misplaced |= part_of(k, pbits) != (uint32_t)p;
-        rk[i] = rj_claim(bst, rj_bucket(k));
-      }
+      if (r < nr) rk[i] = rj_claim(bst, rj_bucket(bkeys[rb + r]));
     }
     __syncthreads();
     rj_scan_buckets<kRCThreads>(bst, wsum);
@@ -1048,12 +1129,8 @@ __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4)))
         if (l0 + u * kRCThreads < nl) pk[u] = pkeys[lb + l0 + u * kRCThreads];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (l0 + u * kRCThreads < nl) {
-          misplaced |= part_of(pk[u], pbits) != (uint32_t)p;
-          c += rj_count(bst, skeys, pk[u]);
-        }
+        if (l0 + u * kRCThreads < nl) c += rj_count(bst, skeys, pk[u]);
     }
-    if (misplaced) atomicOr(overflow, 4);
     for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
     if (lane_id() == 0) csum[threadIdx.x / kWave] = c;
     __syncthreads();
@@ -1104,8 +1181,6 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
   uint16_t *perm = reinterpret_cast<uint16_t *>(area + 8 * (int64_t)cap);
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
-  const int pbits = __builtin_ctzll((unsigned long long)nparts);  // nparts = 2^bits
-  bool misplaced = false;  // ranking guard (overflow bit 4): a row whose key hashes elsewhere
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
     const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
     const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
@@ -1132,10 +1207,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
 #pragma unroll
     for (int i = 0; i < kRJRowsPerThread; ++i) {
       const int r = threadIdx.x + i * kRJThreads;
-      if (r < nr) {
-        bk[i] = bkeys[rb + r];
-        misplaced |= part_of(bk[i], pbits) != (uint32_t)p;
-      }
+      if (r < nr) bk[i] = bkeys[rb + r];
     }
     // ---- phase B: stage + index the build rows
     __syncthreads();  // previous partition fully done with bst / area / wtot
@@ -1226,7 +1298,6 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
       }
       uint32_t i0 = 0, i1 = 0, mc = 0;
       if (active) {
-        misplaced |= part_of(k, pbits) != (uint32_t)p;
         const uint32_t b = rj_bucket(k);
         i0 = bst[b];
         i1 = bst[b + 1];
@@ -1292,7 +1363,6 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
       base += wsum;
     }
   }
-  if (misplaced && overflow != nullptr) atomicOr(overflow, 4);
 }
 
 static int rj_grid(int64_t nparts) { return (int)std::min<int64_t>(nparts, kNumCUs * 8); }

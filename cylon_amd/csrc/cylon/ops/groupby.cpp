@@ -347,6 +347,10 @@ static TablePtr radix_groupby(const TablePtr &t, int key, const std::vector<AggS
                            reinterpret_cast<uint64_t *>(ptr<int64_t>(oacc)), n, ptr<int64_t>(gcount),
                            overflow.data_ptr<int>(), ex.stream);
   }
+  if (hip::rp_take_order_violation(ex.stream)) {  // ranking guard of a stable pass fired
+    trace::add_counter("groupby.radix.order_violation_fallback", 1);
+    return nullptr;
+  }
   if (overflow.item<int>() != 0) {
     trace::add_counter("groupby.radix.overflow_fallback", 1);
     return nullptr;

@@ -384,21 +384,24 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     CYLON_PHASE("join.radix.count", ex.device);
     hip::radix_join_count(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
                           nparts, cap, ptr<int64_t>(counts), overflow.data_ptr<int>(), ex.stream, stride);
+    // the ranking guard of the stable (second and later) partition passes
+    if (hip::rp_take_order_violation(ex.stream)) {
+      trace::add_counter("join.radix.order_violation_fallback", 1);
+      return nullptr;
+    }
     if (stride == 1) {
       out_offs = exclusive_scan(ex, counts);
       at::Tensor tail = at::cat({out_offs.slice(0, nparts, nparts + 1), overflow.to(at::kLong)}).cpu();
       m = tail[0].item<int64_t>();
       if (tail[1].item<int64_t>() != 0) {
-        trace::add_counter((tail[1].item<int64_t>() & 4) ? "join.radix.order_violation_fallback"
-                                                          : "join.radix.overflow_fallback", 1);
+        trace::add_counter("join.radix.overflow_fallback", 1);
         return nullptr;
       }
       alloc = m;
     } else {
       at::Tensor tail = at::stack({counts.sum(), overflow.to(at::kLong)[0]}).cpu();
       if (tail[1].item<int64_t>() != 0) {  // a sampled partition already overflows the LDS (or is misplaced)
-        trace::add_counter((tail[1].item<int64_t>() & 4) ? "join.radix.order_violation_fallback"
-                                                          : "join.radix.overflow_fallback", 1);
+        trace::add_counter("join.radix.overflow_fallback", 1);
         return nullptr;
       }
       const double est = (double)tail[0].item<int64_t>() * (double)nparts / (double)nsample;
@@ -458,11 +461,6 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     at::Tensor res = at::cat({cursor, overflow.to(at::kLong)}).cpu();
     m = res[0].item<int64_t>();
     const int64_t flags = res[1].item<int64_t>();
-    if (flags & 4) {  // ranking guard: a row sits in a partition its key does not hash to
-      if (sink) sink->size = off;
-      trace::add_counter("join.radix.order_violation_fallback", 1);
-      return nullptr;
-    }
     if (flags & 1) {  // a build partition beyond the LDS capacity: global-table join instead
       if (sink) sink->size = off;
       trace::add_counter("join.radix.overflow_fallback", 1);

@@ -8,6 +8,7 @@
 // Strings sort by stable passes over their length and then their 8-byte
 // big-endian chunks from the last chunk to the first, which yields byte-wise
 // lexicographic order.
+#include <limits>
 #include <cstdlib>
 
 #include "util.hpp"
@@ -203,6 +204,10 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
       shift += db;
     }
     cur = UnpackByteColumns(ex, bp, std::move(cur), n);
+    if (hip::rp_take_order_violation(ex.stream)) {  // ranking guard: index sort instead
+      trace::add_counter("sort.radix.order_violation_fallback", 1);
+      return nullptr;
+    }
   }
   std::vector<Column> cols;
   size_t q = 1;
@@ -232,11 +237,39 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
   return Table::Make(t->GetContext(), std::move(cols));
 }
 
+// config "verify_sort" = "1" (or CYLON_VERIFY_SORT=1): one read of the first sort column's
+// order images checks that the result is non-decreasing in the requested order
+static void verify_sorted(const TablePtr &out, int col, bool asc) {
+  auto ctx = out->GetContext();
+  std::string v = ctx->GetConfig("verify_sort", "");
+  if (v.empty())
+    if (const char *e = std::getenv("CYLON_VERIFY_SORT")) v = e;
+  if (v != "1" || out->Rows() < 2) return;
+  Exec ex(out->device());
+  const Column &c = out->column(col);
+  const int64_t n = out->Rows();
+  if (c.is_var() || c.type.kind() == ValueKind::FIXED_BYTES) return;
+  at::Tensor img = ex.empty_i64(n);
+  KCALL(ex, sort_keys_from_column, c.view(), nullptr, n, !asc, reinterpret_cast<uint64_t *>(ptr<int64_t>(img)));
+  // unsigned order of the images = signed order after flipping the top bit; nulls sort last
+  at::Tensor s = at::bitwise_xor(img, at::full({1}, std::numeric_limits<int64_t>::min(), img.options()));
+  at::Tensor bad = s.slice(0, 1, n).lt(s.slice(0, 0, n - 1));
+  if (c.nullable()) {
+    at::Tensor valid = c.validity.slice(0, 0, n).to(at::kBool);
+    bad = bad & valid.slice(0, 1, n) & valid.slice(0, 0, n - 1);
+    bad = bad | (valid.slice(0, 1, n) & valid.slice(0, 0, n - 1).logical_not());  // a value after a null
+  }
+  CYLON_CHECK(!bad.any().item<bool>(), Code::ExecutionError, "sort verification failed on column " << c.name);
+  trace::add_counter("sort.verified", 1);
+}
+
 TablePtr Sort(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending) {
   if (t->Rows() <= 1) return t;
-  if (cols.size() == 1)
-    if (TablePtr r = radix_sort_table(t, cols[0], ascending.empty() ? true : ascending[0])) return r;
-  return GatherNullable(t, SortIndices(t, cols, ascending), false);
+  TablePtr out;
+  if (cols.size() == 1) out = radix_sort_table(t, cols[0], ascending.empty() ? true : ascending[0]);
+  if (!out) out = GatherNullable(t, SortIndices(t, cols, ascending), false);
+  verify_sorted(out, cols[0], ascending.empty() ? true : ascending[0]);
+  return out;
 }
 
 std::pair<at::Tensor, at::Tensor> SortJoinPairs(const Exec &ex, const at::Tensor &lkeys, const at::Tensor &rkeys) {

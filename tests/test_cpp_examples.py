@@ -147,3 +147,103 @@ def test_cpp_example_native_distributed_tcp(tmp_path, data_dir, world):
             assert got[op] == len(_rows(os.path.join(gold, f"{op}_{world}_{r}.csv"))), (r, op)
         assert got["parquet_roundtrip"] == got["join_hash"]
     assert len({o["sum_col1"] for o in outs}) == 1
+
+
+# ---------------------------------------------------------------------------
+# the example programs mirroring the reference's cpp/src/examples (groupby, sorting, unique,
+# partition, select / project / table-from-vectors, indexing): every printed result checked
+# against the Python API on the same input
+# ---------------------------------------------------------------------------
+def _run_example(name, device, *args):
+    if device == "cpu":
+        _ensure_built()
+    exe = os.path.join(ROOT, "examples", "cpp", "bin", name)
+    if not os.path.exists(exe):
+        pytest.fail(f"examples/cpp/bin/{name} missing: run __graft_entry__.build()")
+    r = subprocess.run([exe, device, *args], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return dict((k, int(v)) for k, v in (line.split() for line in r.stdout.splitlines()))
+
+
+def _check_examples(device, data_dir):
+    import pandas as pd
+    from cylon_amd import CylonContext
+    from cylon_amd.io import read_csv
+    ctx = CylonContext(device="cpu")
+    csv = os.path.join(data_dir, "input", "csv1_0.csv")
+    t = read_csv(ctx, csv)
+    df = t.to_pandas()
+    c0 = df.columns[0]
+
+    got = _run_example("groupby_example", device, csv)
+    assert got["hash_groups"] == got["pipeline_groups"] == df[c0].nunique()
+    assert got["hash_columns"] == 9 and got["count_col1"] == len(df)
+    assert got["pipeline_matches_hash"] == got["group_sums_match_total"] == got["minmax_consistent"] == 1
+
+    got = _run_example("sorting_example", device, csv)
+    assert got["sort_asc_rows"] == got["dist_sort_rows"] == len(df)
+    assert all(got[k] == 1 for k in ("sort_asc_ok", "sort_desc_ok", "sort_multi_ok", "dist_sort_ok")), got
+
+    got = _run_example("unique_example", device, csv)
+    assert got["unique_first"] == got["unique_last"] == got["distributed_unique"] == df[c0].nunique()
+    assert got["unique_all_columns"] == len(df.drop_duplicates())
+    assert got["unique_first"] == t.unique([c0], keep="first").row_count
+    assert got["unique_last"] == t.unique([c0], keep="last").row_count
+
+    got = _run_example("partition_example", device, csv, "4")
+    assert got["partition_total"] == got["shuffled"] == len(df)
+    for p in range(4):  # reference modulo partition of an int64 key: (uint32)v % 4
+        assert got[f"partition_{p}"] == int(((df[c0].to_numpy().astype("uint32")) % 4 == p).sum()), p
+
+    got = _run_example("select_project_example", device, csv)
+    assert got["select_even_col0"] == int((df[c0] % 2 == 0).sum())
+    assert got["project_columns"] == 1 and got["merge_rows"] == len(df) + got["select_even_col0"]
+    assert got["vector_table_rows"] == 5 and got["vector_table_first_id"] == 1 and got["vector_table_sum_x10"] == 125
+
+    icsv = os.path.join(data_dir, "input", "indexing_data.csv")
+    idf = pd.read_csv(icsv)
+    got = _run_example("indexing_example", device, icsv)
+    labels = idf.iloc[:3, 0].tolist()
+    want = int(idf.iloc[:, 0].isin(labels).sum())
+    assert got["loc_hash"] == got["loc_sorted"] == got["loc_linear"] == want
+    assert got["iloc_range"] == 5
+    it = read_csv(ctx, icsv)
+    it.set_index(it.column_names[0])
+    assert got["loc_range"] == it.loc[labels[1]:labels[2]].row_count
+
+
+def test_cpp_reference_examples_on_cpu(data_dir):
+    _check_examples("cpu", data_dir)
+
+
+@pytest.mark.gpu
+def test_cpp_reference_examples_on_gpu(data_dir):
+    _check_examples("cuda:0", data_dir)
+
+
+def test_cpp_examples_distributed_tcp(data_dir):
+    """groupby / sorting examples as 2 native TCP ranks: the distributed sort leaves every rank
+    ordered and the group-by's pipeline and hash results agree on every rank."""
+    import socket
+    _ensure_built()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    for name in ("groupby_example", "sorting_example"):
+        exe = os.path.join(ROOT, "examples", "cpp", "bin", name)
+        procs = []
+        for r in range(2):
+            env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC")}
+            env.update(RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                       MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([exe, "tcp", os.path.join(data_dir, "input", f"csv1_{r}.csv")],
+                                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
+        res = [p.communicate(timeout=180) for p in procs]
+        assert all(p.returncode == 0 for p in procs), [e[-1500:] for _, e in res]
+        outs = [dict((k, int(v)) for k, v in (line.split() for line in o.splitlines())) for o, _ in res]
+        for o in outs:
+            if name == "sorting_example":
+                assert o["dist_sort_ok"] == 1 and o["sort_multi_ok"] == 1
+            else:
+                assert o["pipeline_matches_hash"] == 1 and o["group_sums_match_total"] == 1
+        port += 1

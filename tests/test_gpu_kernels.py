@@ -374,9 +374,9 @@ def test_radix_join_fused_count_matches_exact(gpu_ctx, monkeypatch, mode):
 @pytest.mark.parametrize("count_mode", ["fused", "exact"])
 def test_radix_join_ranking_guard_falls_back(gpu_ctx, monkeypatch, count_mode):
     """The LSD partition passes after the first must keep the order they receive (wave-atomic
-    stable ranking).  CYLON_RP_DEBUG_UNSTABLE=1 breaks that on purpose: rows then sit in partitions
-    their keys do not hash to, the count / write kernels' per-row guard (part_of(key) == partition)
-    flags it, and the join falls back to the global-table path with a correct result."""
+    stable ranking).  CYLON_RP_DEBUG_UNSTABLE=1 breaks that on purpose (block-atomic ranking in
+    every pass): the passes' ranking guard -- inside each bucket run of a sorted tile the input rows
+    must ascend -- flags it, and the join falls back to the global-table path with a correct result."""
     rng = np.random.default_rng(8)
     n = 6_000_000  # 11 partition bits: two LSD passes
     a = pa.table({"k": rng.integers(0, n, n), "v": rng.random(n)})
@@ -396,6 +396,29 @@ def test_radix_join_ranking_guard_falls_back(gpu_ctx, monkeypatch, count_mode):
     got = L.join(R, "inner", "hash", **on)
     c = dict(C.trace_counters())
     C.trace_enable(False)
+    monkeypatch.delenv("CYLON_RP_DEBUG_UNSTABLE")
+    C.rp_reset_lane_order()  # the guard switched the device to ballot ranking: probe again
     assert c.get("join.radix.order_violation_fallback", 0) == 1, c
     assert got.row_count == ref.row_count
     pd.testing.assert_frame_equal(_sorted_df(got), _sorted_df(ref))
+
+
+@pytest.mark.parametrize("dtype", ["int64", "float64"])
+def test_verify_sort_config(gpu_ctx, dtype):
+    """config verify_sort=1: the sorted result is checked in order-image space (nulls last)."""
+    from cylon_amd._lib import C
+    rng = np.random.default_rng(2)
+    n = 5_000_000
+    k = rng.integers(-10**9, 10**9, n).astype(dtype)
+    t = Table(pa.table({"k": pa.array(k, mask=rng.random(n) < 0.01), "p": np.arange(n)}), gpu_ctx)
+    gpu_ctx.add_config("verify_sort", "1")
+    C.trace_enable(True)
+    C.trace_reset()
+    try:
+        for asc in (True, False):
+            t.sort("k", ascending=asc)
+        c = dict(C.trace_counters())
+    finally:
+        gpu_ctx.add_config("verify_sort", "0")
+        C.trace_enable(False)
+    assert c.get("sort.verified", 0) == 2, c

@@ -180,3 +180,25 @@ def test_distributed_sort_exact_splitters(case):
     pd.testing.assert_frame_equal(got.astype(exp.dtypes.to_dict()), exp, check_dtype=False)
     loads = [len(r[0]) for r in res]
     assert max(loads) <= 1.5 * len(allin) / world, loads
+
+
+def test_verify_sort_config_cpu(ctx):
+    """config verify_sort=1 on the CPU engine: sorted results pass the order-image check."""
+    import numpy as np
+    import pyarrow as pa
+    from cylon_amd import Table
+    from cylon_amd._lib import C
+    rng = np.random.default_rng(3)
+    t = Table(pa.table({"k": pa.array(rng.standard_normal(5000), mask=rng.random(5000) < 0.05),
+                        "i": rng.integers(0, 9, 5000)}), ctx)
+    ctx.add_config("verify_sort", "1")
+    C.trace_enable(True)
+    C.trace_reset()
+    try:
+        t.sort("k")
+        t.sort(["i", "k"], ascending=[False, True])
+        c = dict(C.trace_counters())
+    finally:
+        ctx.add_config("verify_sort", "0")
+        C.trace_enable(False)
+    assert c.get("sort.verified", 0) == 2
