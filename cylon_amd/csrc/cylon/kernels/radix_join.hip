@@ -226,17 +226,17 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   constexpr int WAVES = THREADS / kWave;
   constexpr int TILE = THREADS * kRPItems;
   constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;  // buckets per thread in the offset scan
-  static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 2 * 2 <= TILE * 8, "ranking scratch must fit the stage");
+  static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 4 <= TILE * 8, "ranking scratch must fit the stage");
   __shared__ int64_t running[kRPMaxBuckets];
   __shared__ uint32_t toff[kRPMaxBuckets + 1];
-  __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16, sdig[TILE] u16, srow[TILE] u16}
+  __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16, sdig[TILE] u32}
   __shared__ uint32_t wsum[WAVES];
   uint16_t *wcnt = reinterpret_cast<uint16_t *>(ustage);
   constexpr bool STABLE = RANK != kRankBlockAtomic;
   uint32_t *bcnt = reinterpret_cast<uint32_t *>(ustage);  // block-atomic ranking: block-wide counters
   static_assert(WAVES * kRPMaxBuckets * 2 >= kRPMaxBuckets * 4, "block counters must fit the wave counters");
-  uint16_t *sdig = wcnt + WAVES * kRPMaxBuckets;
-  uint16_t *srow = sdig + TILE;  // input row (in the tile) of sorted slot j: the ranking guard
+  // sorted slot j -> digit << 16 | input row in the tile (the row feeds the ranking guard)
+  uint32_t *sdig = reinterpret_cast<uint32_t *>(wcnt + WAVES * kRPMaxBuckets);
   uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
   bool order_bad = false;
 
@@ -344,8 +344,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       if (pl[k] == 0xffffffffu) continue;
       const uint32_t p = pl[k] & 0xffffu;
       const uint32_t pos = toff[p] + (STABLE ? (uint32_t)wcnt[wave * nbuckets + p] : 0u) + (pl[k] >> 16);
-      sdig[pos] = (uint16_t)p;
-      if (cols.check_order) srow[pos] = (uint16_t)(wrow + k * kWave + lane);
+      sdig[pos] = (p << 16) | (uint32_t)(wrow + k * kWave + lane);
       pl[k] = pos;
     }
     __syncthreads();
@@ -355,9 +354,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     for (int q = 0; q < kRPItems; ++q) {
       const int j = threadIdx.x + q * THREADS;
       if (j < cnt) {
-        const uint32_t p = sdig[j];
+        const uint32_t e = sdig[j], p = e >> 16;
         dst[q] = running[p] + (j - (int64_t)toff[p]);
-        if (cols.check_order && j > 0 && sdig[j - 1] == p && srow[j - 1] > srow[j]) order_bad = true;
+        if (cols.check_order && j > 0) {  // same bucket as the previous slot: input order kept?
+          const uint32_t f = sdig[j - 1];
+          order_bad |= (f >> 16) == p && f > e;
+        }
       }
     }
     __syncthreads();  // counters / digits dead: the union becomes the column stage
@@ -423,7 +425,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
     const int64_t *__restrict__ bh_scan) {
   constexpr int THREADS = kRPThreads, WAVES = THREADS / kWave, TILE = THREADS * kRPItems;
   constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;
-  static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 2 * 2 <= TILE * 8, "ranking scratch must fit the stage");
+  static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 4 <= TILE * 8, "ranking scratch must fit the stage");
   __shared__ int64_t running[kRPMaxBuckets];
   __shared__ uint32_t toff[kRPMaxBuckets + 1];
   __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16 or bcnt[nb] u32, sdig[TILE] u16}
@@ -431,8 +433,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
   constexpr bool STABLE = RANK != kRankBlockAtomic;
   uint16_t *wcnt = reinterpret_cast<uint16_t *>(ustage);
   uint32_t *bcnt = reinterpret_cast<uint32_t *>(ustage);
-  uint16_t *sdig = wcnt + WAVES * kRPMaxBuckets;
-  uint16_t *srow = sdig + TILE;  // ranking guard (see ColSet::check_order)
+  uint32_t *sdig = reinterpret_cast<uint32_t *>(wcnt + WAVES * kRPMaxBuckets);  // digit << 16 | input row
   uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
   bool order_bad = false;
   (void)nbits;
@@ -520,8 +521,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
       if (pl[k] == 0xffffffffu) continue;
       const uint32_t p = pl[k] & 0xffffu;
       const uint32_t pos = toff[p] + (STABLE ? (uint32_t)wcnt[wave * nbuckets + p] : 0u) + (pl[k] >> 16);
-      sdig[pos] = (uint16_t)p;
-      if (cols.check_order) srow[pos] = (uint16_t)(wrow + k * kWave + lane);
+      sdig[pos] = (p << 16) | (uint32_t)(wrow + k * kWave + lane);
       pl[k] = pos;
     }
     __syncthreads();
@@ -529,9 +529,12 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
 #pragma unroll
     for (int q = 0; q < kRPItems; ++q) {
       const int j = tx + q * THREADS;
-      const uint32_t p = j < cnt ? sdig[j] : 0u;
+      const uint32_t e = j < cnt ? sdig[j] : 0u, p = e >> 16;
       dp[q] = (p << 16) | (uint32_t)(j - (int)toff[p]);
-      if (cols.check_order && j > 0 && j < cnt && sdig[j - 1] == p && srow[j - 1] > srow[j]) order_bad = true;
+      if (cols.check_order && j > 0 && j < cnt) {  // same bucket as the previous slot: input order kept?
+        const uint32_t f = sdig[j - 1];
+        order_bad |= (f >> 16) == p && f > e;
+      }
     }
     __syncthreads();  // counters / digits dead: the union becomes the column stage
 #pragma unroll 1
@@ -839,7 +842,8 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   ColSet cs;
   cs.n = ncols;
   cs.key_xor = key_xor;
-  cs.check_order = want_stable ? 1 : 0;
+  const char *gd = std::getenv("CYLON_RP_GUARD");  // A/B knob: 0 disables the ranking guard
+  cs.check_order = want_stable && !(gd && gd[0] == '0') ? 1 : 0;
   cs.order_bad = order_flag();
   for (int c = 0; c < kMaxFusedCols; ++c) {
     cs.in[c] = c < ncols ? in[c] : nullptr;

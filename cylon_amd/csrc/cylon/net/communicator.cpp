@@ -9,6 +9,7 @@
 #include <torch/csrc/distributed/c10d/Types.hpp>
 
 #include "communicator.hpp"
+#include "../trace.hpp"
 
 namespace cylon {
 namespace net {
@@ -84,6 +85,7 @@ at::Tensor ProcessGroupCommunicator::to_comm(const at::Tensor &t) const {
 }
 
 void ProcessGroupCommunicator::Barrier() {
+  trace::add_counter("comm.barrier", 1);
   // an all-reduce of one element on the comm device is a barrier that works
   // identically for RCCL and gloo and orders with the current stream.
   at::Tensor t = at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(device_));
@@ -94,6 +96,7 @@ void ProcessGroupCommunicator::Barrier() {
 
 at::Tensor ProcessGroupCommunicator::AllToAllV(const at::Tensor &send, const std::vector<int64_t> &send_counts,
                                                const std::vector<int64_t> &recv_counts) {
+  trace::add_counter("comm.alltoall_blocking", 1);
   CYLON_CHECK((int)send_counts.size() == world_ && (int)recv_counts.size() == world_, Code::Invalid,
               "all-to-all counts must have world-size entries");
   int64_t total = 0;
@@ -110,6 +113,7 @@ at::Tensor ProcessGroupCommunicator::AllToAllV(const at::Tensor &send, const std
 }
 
 std::vector<int64_t> ProcessGroupCommunicator::ExchangeCounts(const std::vector<int64_t> &send_counts) {
+  trace::add_counter("comm.alltoall_blocking", 1);
   CYLON_CHECK((int)send_counts.size() == world_, Code::Invalid, "counts must have world-size entries");
   at::Tensor s = at::tensor(send_counts, at::TensorOptions().dtype(at::kLong)).to(device_);
   at::Tensor r = at::empty({world_}, s.options());
@@ -130,6 +134,7 @@ static c10d::ReduceOp to_c10d(ReduceOp op) {
 }
 
 void ProcessGroupCommunicator::AllReduce(at::Tensor &t, ReduceOp op) {
+  trace::add_counter("comm.allreduce", 1);
   at::Tensor c = to_comm(t);
   std::vector<at::Tensor> v{c};
   c10d::AllreduceOptions o;
@@ -139,6 +144,7 @@ void ProcessGroupCommunicator::AllReduce(at::Tensor &t, ReduceOp op) {
 }
 
 at::Tensor ProcessGroupCommunicator::AllGather(const at::Tensor &in) {
+  trace::add_counter("comm.allgather", 1);
   at::Tensor c = to_comm(in);
   std::vector<int64_t> shape(c.sizes().begin(), c.sizes().end());
   if (shape.empty()) shape.push_back(1);
@@ -152,6 +158,7 @@ at::Tensor ProcessGroupCommunicator::AllGather(const at::Tensor &in) {
 }
 
 void ProcessGroupCommunicator::Broadcast(at::Tensor &t, int root) {
+  trace::add_counter("comm.broadcast", 1);
   at::Tensor c = to_comm(t);
   std::vector<at::Tensor> v{c};
   c10d::BroadcastOptions o;
@@ -250,6 +257,7 @@ std::pair<at::Tensor, std::shared_ptr<P2PRequest>> ProcessGroupCommunicator::All
     const at::Tensor &send, const std::vector<int64_t> &send_counts, const std::vector<int64_t> &recv_counts) {
   CYLON_CHECK((int)send_counts.size() == world_ && (int)recv_counts.size() == world_, Code::Invalid,
               "all-to-all counts must have world-size entries");
+  trace::add_counter("comm.alltoall_posted", 1);
   int64_t total = 0;
   for (auto c : recv_counts) total += c;
   at::Tensor in = to_comm(send);

@@ -90,7 +90,7 @@ GroupInfo GroupIds(const TablePtr &t, const std::vector<int> &cols, bool presort
     return gi;
   }
   // exact sort-based path (multi-column, strings, nullable keys, presorted input)
-  at::Tensor perm = presorted ? iota_t(ex, n) : SortIndices(t, cols, {true});
+  at::Tensor perm = presorted ? iota_t(ex, n) : SortIndices(t, cols, {true}, true);
   std::vector<ColView> v = views(t, cols);
   at::Tensor heads = ex.empty_u8(n);
   KCALL(ex, segment_heads, v.data(), (int)v.size(), ptr<int64_t>(perm), n, ptr<uint8_t>(heads));

@@ -759,19 +759,19 @@ TablePtr Join(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg
 TablePtr DistributedJoin(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
   auto ctx = left->GetContext();
   if (!ctx->ShuffleRequired()) return Join(left, right, cfg);
-  const int K = ShuffleChunks(left, right);
-  if (K > 1) {
-    JoinSink sink;
-    sink.chunks_total = K;
-    ShufflePairChunked(left, cfg.GetLeftColumnIdx(), right, cfg.GetRightColumnIdx(), K,
-                       [&](int, const TablePtr &l, const TablePtr &r) {
-                         if (TablePtr t = join_local(l, r, cfg, &sink)) sink.tables.push_back(t);
-                         ++sink.chunks_done;
-                       });
-    return sink.finish(ctx);
-  }
-  auto lr = ShufflePair(left, cfg.GetLeftColumnIdx(), right, cfg.GetRightColumnIdx());
-  return Join(lr.first, lr.second, cfg);
+  JoinSink sink;
+  TablePtr whole;
+  ShufflePairPlanned(left, cfg.GetLeftColumnIdx(), right, cfg.GetRightColumnIdx(),
+                     [&](int, int K, const TablePtr &l, const TablePtr &r) {
+                       if (K == 1) {  // unchunked: the shuffled pair is joined as a whole
+                         whole = Join(l, r, cfg);
+                         return;
+                       }
+                       sink.chunks_total = K;
+                       if (TablePtr t = join_local(l, r, cfg, &sink)) sink.tables.push_back(t);
+                       ++sink.chunks_done;
+                     });
+  return whole ? whole : sink.finish(ctx);
 }
 
 }  // namespace ops

@@ -578,5 +578,195 @@ void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const 
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// ShufflePairPlanned: one host-synchronous collective before the first payload post.
+//
+// The row counts are computed for P = W * Kc partitions (chunk-major pid = h % P, so the
+// destination rank is pid % W = h % W), which serves both outcomes: K = Kc chunks use them
+// directly, K = 1 sums a rank's Kc chunk counts.  Every rank's descriptor
+//   [rows_a, rows_b | nullable flags of a's and b's columns | min, max of every narrowable
+//    int64 column | counts_a[P] | counts_b[P]]
+// is all-gathered once; K (the reference-compatible default: 4 chunks when every rank holds
+// >= 2^24 rows per relation on a GPU, else 1; config shuffle_chunks forces it), the receive
+// counts, the agreed nullability and the wire narrowing are then derived identically on every
+// rank from the gathered matrix, with no further collective before the payload all-to-alls.
+// ---------------------------------------------------------------------------
+static at::Tensor counts_device(const TablePtr &t, const std::vector<int> &cols, uint32_t P, bool fast) {
+  Exec ex(t->device());
+  if (fast) {
+    at::Tensor c = ex.empty_i64(P);
+    hip::mod_partition_counts(reinterpret_cast<const int64_t *>(t->column(cols[0]).data.data_ptr()), t->Rows(), P,
+                              ptr<int64_t>(c), ex.stream);
+    return c;
+  }
+  return hash_pids_counts(t, cols, P).second;
+}
+
+void ShufflePairPlanned(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,
+                        const std::vector<int> &bcols,
+                        const std::function<void(int, int, const TablePtr &, const TablePtr &)> &consume) {
+  auto ctx = a->GetContext();
+  if (!ctx->ShuffleRequired()) {
+    consume(0, 1, a, b);
+    return;
+  }
+  bool var = false;
+  for (const TablePtr &t : {a, b})
+    for (const auto &c : t->columns()) var |= c.is_var();
+  if (var) {  // strings: byte counts per column need their own exchange (ShufflePair)
+    auto lr = ShufflePair(a, acols, b, bcols);
+    consume(0, 1, lr.first, lr.second);
+    return;
+  }
+  const int W = ctx->GetWorldSize(), me = ctx->GetRank();
+  std::string v = ctx->GetConfig("shuffle_chunks", "");
+  if (v.empty())
+    if (const char *e = std::getenv("CYLON_SHUFFLE_CHUNKS")) v = e;
+  const int forced = v.empty() ? 0 : std::max(1, std::min(64, std::atoi(v.c_str())));
+  const int Kc = forced ? forced : (a->device().is_cuda() ? 4 : 1);
+  const uint32_t P = (uint32_t)W * (uint32_t)Kc;
+  const at::Device dev = a->device();
+  const auto lopt = at::TensorOptions().dtype(at::kLong).device(dev);
+  // ---- the descriptor (assembled on the device: no sync before the all-gather)
+  std::vector<at::Tensor> parts;
+  parts.push_back(at::tensor({a->Rows(), b->Rows()}, at::TensorOptions().dtype(at::kLong)).to(dev));
+  std::vector<int64_t> nflags;
+  for (const TablePtr &t : {a, b})
+    for (const auto &c : t->columns()) nflags.push_back(c.nullable() ? 1 : 0);
+  parts.push_back(at::tensor(nflags, at::TensorOptions().dtype(at::kLong)).to(dev));
+  std::string nv = ctx->GetConfig("shuffle_narrow", "");
+  if (nv.empty())
+    if (const char *e = std::getenv("CYLON_SHUFFLE_NARROW")) nv = e;
+  std::vector<std::pair<int, int>> cand;  // (table, column) narrowable on the wire
+  if (nv != "0")
+    for (int side = 0; side < 2; ++side) {
+      const TablePtr &t = side == 0 ? a : b;
+      for (int c = 0; c < t->Columns(); ++c)
+        if (narrow_candidate(t->column(c))) cand.push_back({side, c});
+    }
+  for (auto &sc : cand) {
+    const Column &c = (sc.first == 0 ? a : b)->column(sc.second);
+    if (c.length == 0) {
+      parts.push_back(at::tensor({std::numeric_limits<int64_t>::max(), std::numeric_limits<int64_t>::min()}, lopt));
+    } else {
+      auto mm = at::aminmax(c.data.slice(0, 0, c.length));
+      parts.push_back(at::stack({std::get<0>(mm), std::get<1>(mm)}));
+    }
+  }
+  const bool fast_a = mod_pass_eligible(a, acols, P), fast_b = mod_pass_eligible(b, bcols, P);
+  {
+    CYLON_PHASE("shuffle.partition", dev);
+    parts.push_back(counts_device(a, acols, P, fast_a));
+    parts.push_back(counts_device(b, bcols, P, fast_b));
+  }
+  at::Tensor desc = at::cat(parts);
+  const int64_t D = desc.numel();
+  at::Tensor all;
+  {
+    CYLON_PHASE("shuffle.plan", dev);
+    all = ctx->GetCommunicator()->AllGather(desc).to(at::kCPU).contiguous();
+  }
+  trace::add_counter("shuffle.plan_collectives", 1);
+  const int64_t *g = all.data_ptr<int64_t>();  // W x D
+  const int na_cols = a->Columns(), nb_cols = b->Columns();
+  const int64_t off_null = 2, off_mm = off_null + na_cols + nb_cols, off_cnt = off_mm + 2 * (int64_t)cand.size();
+  CYLON_CHECK(off_cnt + 2 * (int64_t)P == D, Code::ExecutionError, "shuffle descriptor layout");
+  // chunk count
+  int K = Kc;
+  if (!forced) {
+    int64_t mn = std::numeric_limits<int64_t>::max();
+    for (int r = 0; r < W; ++r) mn = std::min(mn, std::min(g[r * D + 0], g[r * D + 1]));
+    K = mn >= (int64_t(1) << 24) ? Kc : 1;
+  }
+  // nullability (any rank) and the wire plan (global ranges)
+  std::vector<int64_t> nullable(na_cols + nb_cols, 0);
+  for (int r = 0; r < W; ++r)
+    for (int c = 0; c < na_cols + nb_cols; ++c) nullable[c] |= g[r * D + off_null + c];
+  std::vector<WirePlan> plans(2);
+  plans[0].narrow.assign(na_cols, false);
+  plans[0].base.assign(na_cols, 0);
+  plans[1].narrow.assign(nb_cols, false);
+  plans[1].base.assign(nb_cols, 0);
+  for (size_t j = 0; j < cand.size(); ++j) {
+    int64_t lo = std::numeric_limits<int64_t>::max(), hi = std::numeric_limits<int64_t>::min();
+    for (int r = 0; r < W; ++r) {
+      lo = std::min(lo, g[r * D + off_mm + 2 * j]);
+      hi = std::max(hi, g[r * D + off_mm + 2 * j + 1]);
+    }
+    if (hi < lo || (uint64_t)hi - (uint64_t)lo > 0xffffffffull) continue;
+    plans[cand[j].first].narrow[cand[j].second] = true;
+    plans[cand[j].first].base[cand[j].second] = lo;
+    trace::add_counter("shuffle.narrowed_columns", 1);
+  }
+  const std::vector<int64_t> na_flags(nullable.begin(), nullable.begin() + na_cols);
+  const std::vector<int64_t> nb_flags(nullable.begin() + na_cols, nullable.end());
+  // per chunk k: rows this rank sends to rank r (local counts) and receives from rank r
+  auto sendc = [&](int side, int k, int r) -> int64_t {
+    const int64_t *c = g + (int64_t)me * D + off_cnt + (int64_t)side * P;
+    if (K == Kc) return c[(int64_t)k * W + r];
+    int64_t s = 0;
+    for (int q = 0; q < Kc; ++q) s += c[(int64_t)q * W + r];
+    return s;
+  };
+  auto recvc = [&](int side, int k, int r) -> int64_t {
+    const int64_t *c = g + (int64_t)r * D + off_cnt + (int64_t)side * P;
+    if (K == Kc) return c[(int64_t)k * W + me];
+    int64_t s = 0;
+    for (int q = 0; q < Kc; ++q) s += c[(int64_t)q * W + me];
+    return s;
+  };
+  const uint32_t PK = (uint32_t)W * (uint32_t)K;
+  const bool fa = K == Kc ? fast_a : mod_pass_eligible(a, acols, PK), fb = K == Kc ? fast_b : mod_pass_eligible(b, bcols, PK);
+  trace::add_counter("shuffle.fast_partition", (fa ? 1 : 0) + (fb ? 1 : 0));
+  auto reorder = [&](const TablePtr &t, const std::vector<int> &cols, bool fast) -> TablePtr {
+    return fast ? mod_reorder(t, cols[0], PK) : PartitionReorder(t, hash_pids(t, cols, PK), PK).first;
+  };
+  std::vector<PendingTable> pa(K), pb(K);
+  std::vector<int64_t> offa(K + 1, 0), offb(K + 1, 0);
+  auto post = [&](const TablePtr &part, int side, int k, const std::vector<int64_t> &flags,
+                  std::vector<int64_t> &off) -> PendingTable {
+    std::vector<int64_t> sc(W), rc(W);
+    int64_t tot = 0;
+    for (int r = 0; r < W; ++r) {
+      sc[r] = sendc(side, k, r);
+      rc[r] = recvc(side, k, r);
+      tot += sc[r];
+    }
+    off[k + 1] = off[k] + tot;
+    PendingTable pt = AllToAllPost(Slice(part, off[k], tot), sc, rc, flags);
+    attach_plan(pt, side == 0 ? a : b, plans[side]);
+    count_pending(pt);
+    return pt;
+  };
+  TablePtr pta, ptb;
+  {
+    CYLON_PHASE("shuffle.reorder+post", dev);
+    pta = to_wire(reorder(a, acols, fa), plans[0]);
+    pa[0] = post(pta, 0, 0, na_flags, offa);  // a's chunk 0 transfers while b is reordered
+    ptb = to_wire(reorder(b, bcols, fb), plans[1]);
+    pb[0] = post(ptb, 1, 0, nb_flags, offb);
+    for (int k = 1; k < K; ++k) {
+      pa[k] = post(pta, 0, k, na_flags, offa);
+      pb[k] = post(ptb, 1, k, nb_flags, offb);
+    }
+  }
+  trace::add_counter("shuffle.rows_in", a->Rows() + b->Rows());
+  trace::add_counter("shuffle.bytes_in", a->nbytes() + b->nbytes());
+  trace::add_counter("shuffle.chunks", K);
+  for (int k = 0; k < K; ++k) {
+    TablePtr ta, tb;
+    {
+      CYLON_PHASE("shuffle.wait", dev);
+      ta = AllToAllFinish(pa[k]);
+      tb = AllToAllFinish(pb[k]);
+    }
+    pa[k] = PendingTable();
+    pb[k] = PendingTable();
+    trace::add_counter("shuffle.rows_out", ta->Rows() + tb->Rows());
+    consume(k, K, ta, tb);
+  }
+}
+
 }  // namespace ops
 }  // namespace cylon

@@ -43,7 +43,7 @@ static at::Tensor nulls_last(const Exec &ex, const Column &c, const at::Tensor &
   return at::cat({perm.index_select(0, valid_pos), perm.index_select(0, null_pos)});
 }
 
-static at::Tensor refine_by_column(const Exec &ex, const Column &c, at::Tensor perm, bool asc);
+static at::Tensor refine_by_column(const Exec &ex, const Column &c, at::Tensor perm, bool asc, bool grouping = false);
 
 // bytes [off, off + width of t) of every row of a fixed-width column as a contiguous
 // column of numeric type t (the validity of the source column)
@@ -79,9 +79,11 @@ static at::Tensor refine_fixed_bytes(const Exec &ex, const Column &c, at::Tensor
   return refine_by_column(ex, v, std::move(perm), asc);
 }
 
-static at::Tensor refine_by_column(const Exec &ex, const Column &c, at::Tensor perm, bool asc) {
+// grouping: the order only has to bring equal values together (group ids, distinct rows), so
+// list columns may use their byte order there; a user-visible sort by a list column is refused
+static at::Tensor refine_by_column(const Exec &ex, const Column &c, at::Tensor perm, bool asc, bool grouping) {
   const int64_t n = perm.numel();
-  CYLON_CHECK(c.type.type != Type::LIST, Code::NotImplemented, "sort by a list column (" << c.name << ")");
+  CYLON_CHECK(grouping || c.type.type != Type::LIST, Code::NotImplemented, "sort by a list column (" << c.name << ")");
   if (!c.is_var() && c.type.kind() == ValueKind::FIXED_BYTES) return refine_fixed_bytes(ex, c, std::move(perm), asc);
   if (!c.is_var()) {
     at::Tensor keys = ex.empty_i64(n);
@@ -104,7 +106,8 @@ static at::Tensor refine_by_column(const Exec &ex, const Column &c, at::Tensor p
   return nulls_last(ex, c, perm);
 }
 
-at::Tensor SortIndices(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending) {
+at::Tensor SortIndices(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending,
+                       bool grouping) {
   CYLON_CHECK(!cols.empty(), Code::Invalid, "sort needs at least one column");
   CYLON_CHECK(ascending.size() == cols.size() || ascending.size() == 1, Code::Invalid,
               "ascending flags must match sort columns");
@@ -113,7 +116,7 @@ at::Tensor SortIndices(const TablePtr &t, const std::vector<int> &cols, const st
   at::Tensor perm = iota(ex, t->Rows());
   for (int k = (int)cols.size() - 1; k >= 0; --k) {
     const bool asc = ascending.size() == 1 ? ascending[0] : ascending[k];
-    perm = refine_by_column(ex, t->column(cols[k]), perm, asc);
+    perm = refine_by_column(ex, t->column(cols[k]), perm, asc, grouping);
   }
   return perm;
 }

@@ -124,6 +124,14 @@ int ShuffleChunks(const TablePtr &a, const TablePtr &b);
 void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,
                         const std::vector<int> &bcols, int chunks,
                         const std::function<void(int, const TablePtr &, const TablePtr &)> &consume);
+// The binary operators' shuffle (DistributedJoin, distributed set operations): decides the chunk
+// count itself and agrees on everything the exchange needs -- chunk count, per-chunk row counts of
+// both tables, column nullability, narrowed wire columns -- in ONE all-gather of a per-rank
+// descriptor before the first payload all-to-all is posted.  consume(k, K, a_k, b_k) runs once per
+// chunk (K == 1: the whole shuffled pair).  Var-width tables take ShufflePair (K = 1).
+void ShufflePairPlanned(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,
+                        const std::vector<int> &bcols,
+                        const std::function<void(int, int, const TablePtr &, const TablePtr &)> &consume);
 
 // ---- relational -----------------------------------------------------------
 TablePtr Join(const TablePtr &left, const TablePtr &right, const join::config::JoinConfig &cfg);
@@ -134,7 +142,9 @@ std::pair<at::Tensor, at::Tensor> JoinIndices(const TablePtr &left, const TableP
 // C27/K16: index row positions matching each label, grouped by label order then row order
 at::Tensor IndexLookup(const std::shared_ptr<CylonContext> &ctx, const Column &index, const Column &labels);
 
-at::Tensor SortIndices(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending);
+// grouping = true: only equal values must end adjacent (list columns then sort by their bytes)
+at::Tensor SortIndices(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending,
+                       bool grouping = false);
 TablePtr Sort(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending);
 
 }  // namespace ops

@@ -63,3 +63,33 @@ def test_force_shuffle_world1_matches_local(chunks):
             np.testing.assert_allclose(g["mean_f"], e["mean_f"], rtol=1e-12)
             g, e = g.drop(columns=["sum_f", "mean_f"]), e.drop(columns=["sum_f", "mean_f"])
         pd.testing.assert_frame_equal(_frame(g), _frame(e), check_dtype=False, obj=op)
+
+
+def _prologue(ctx, chunks):
+    from cylon_amd import Table
+    from cylon_amd._lib import C
+    rng = np.random.default_rng(5 + ctx.get_rank())
+    n = 30_000
+    a = pd.DataFrame({"k": rng.integers(0, 40_000, n), "v": rng.random(n)})
+    b = pd.DataFrame({"k": rng.integers(0, 40_000, n), "w": rng.random(n), "i": rng.integers(0, 9, n)})
+    ta, tb = Table.from_pandas(ctx, a), Table.from_pandas(ctx, b)
+    ctx.add_config("shuffle_chunks", str(chunks))
+    C.trace_enable(True)
+    C.trace_reset()
+    out = ta.distributed_join(tb, "inner", "hash", on=["k"])
+    c = dict(C.trace_counters())
+    C.trace_enable(False)
+    return out.row_count, c, len(a.merge(b, on="k"))
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_exchange_prologue_is_one_collective(chunks):
+    """A distributed join agrees on chunk count, per-chunk counts of both tables, nullability and
+    the narrowed wire format with ONE all-gather; the only other collectives are the posted
+    payload all-to-alls (reference exchanged headers per buffer, table.cpp:67-131)."""
+    res = run_distributed(_prologue, 2, chunks)
+    for rows, c, _ in res:
+        assert c.get("comm.allgather") == 1, c
+        assert c.get("comm.allreduce", 0) == 0 and c.get("comm.alltoall_blocking", 0) == 0, c
+        assert c.get("comm.alltoall_posted", 0) == chunks * (2 + 3), c  # one per column buffer per chunk
+    assert sum(r[0] for r in res) > 0

@@ -206,7 +206,8 @@ def test_bench_self_launch_four_ranks_cpu():
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 4 and rec["steps"] == 2 and rec["warmup"] == 1
     assert rec["verify"]["ok"] and rec["verify"]["rows"] == rec["config"]["output_rows"]
-    assert "shuffle.exchange" in rec["phases_ms_max_over_ranks"]
+    ph = rec["phases_ms_max_over_ranks"]
+    assert "shuffle.plan" in ph and "shuffle.reorder+post" in ph, ph  # one planning collective, then posts
     bad = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4", "--rows", "1000"],
                          capture_output=True, text=True, timeout=120, cwd="/tmp",
                          env=dict(env, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
