@@ -448,8 +448,10 @@ TablePtr DistributedHashGroupBy(const TablePtr &t, const std::vector<int> &keys,
       cols.push_back(a.col);
       remapped.push_back(b);
     }
-    TablePtr sh = Shuffle(Project(t, cols), key_pos);
-    return HashGroupBy(sh, key_pos, remapped);
+    std::vector<TablePtr> parts;
+    ShufflePlanned(Project(t, cols), key_pos,
+                   [&](int, int, const TablePtr &sh) { parts.push_back(HashGroupBy(sh, key_pos, remapped)); });
+    return parts.size() == 1 ? parts[0] : Merge(parts);
   }
 
   struct Plan {
@@ -534,9 +536,13 @@ TablePtr DistributedHashGroupBy(const TablePtr &t, const std::vector<int> &keys,
   }
   partial = Table::Make(t->GetContext(), std::move(pcols));
   }  // generic phase 1
-  // phase 2: shuffle partial rows by key, combine
-  TablePtr sh = Shuffle(partial, key_pos);
-  TablePtr comb = HashGroupBy(sh, key_pos, combine);
+  // phase 2: shuffle partial rows by key and combine -- chunk by hash-disjoint chunk, so the
+  // combine of chunk k runs while the later chunks are still on the wire
+  std::vector<TablePtr> combined;
+  ShufflePlanned(partial, key_pos, [&](int, int, const TablePtr &sh) {
+    combined.push_back(HashGroupBy(sh, key_pos, combine));
+  });
+  TablePtr comb = combined.size() == 1 ? combined[0] : Merge(combined);
   std::vector<Column> out;
   for (int i = 0; i < nk; ++i) out.push_back(comb->column(i));
   int ci = nk;

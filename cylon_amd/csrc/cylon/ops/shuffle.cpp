@@ -394,10 +394,21 @@ static std::pair<TablePtr, std::vector<int64_t>> shuffle_partition(const TablePt
   return PartitionReorder(t, pid, (uint32_t)world);
 }
 
+static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<std::vector<int>> &tcols,
+                            bool allow_chunks,
+                            const std::function<void(int, int, const std::vector<TablePtr> &)> &consume);
+
 TablePtr Shuffle(const TablePtr &t, const std::vector<int> &hash_cols) {
   auto ctx = t->GetContext();
   const int world = ctx->GetWorldSize();
   if (!ctx->ShuffleRequired()) return t;
+  bool var = false;
+  for (const auto &c : t->columns()) var |= c.is_var();
+  if (!var) {  // fixed width: one planning collective (ShufflePairPlanned's descriptor), one post
+    TablePtr out;
+    planned_shuffle({t}, {hash_cols}, false, [&](int, int, const std::vector<TablePtr> &r) { out = r[0]; });
+    return out;
+  }
   auto r = shuffle_partition(t, hash_cols, world);
   CYLON_PHASE("shuffle.exchange", t->device());
   trace::add_counter("shuffle.rows_in", t->Rows());
@@ -603,50 +614,55 @@ static at::Tensor counts_device(const TablePtr &t, const std::vector<int> &cols,
   return hash_pids_counts(t, cols, P).second;
 }
 
-void ShufflePairPlanned(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,
-                        const std::vector<int> &bcols,
-                        const std::function<void(int, int, const TablePtr &, const TablePtr &)> &consume) {
-  auto ctx = a->GetContext();
+// ts: one or two tables (the binary operators shuffle both relations in one plan).
+static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<std::vector<int>> &tcols,
+                            bool allow_chunks,
+                            const std::function<void(int, int, const std::vector<TablePtr> &)> &consume) {
+  const int NT = (int)ts.size();
+  auto ctx = ts[0]->GetContext();
   if (!ctx->ShuffleRequired()) {
-    consume(0, 1, a, b);
+    consume(0, 1, ts);
     return;
   }
   bool var = false;
-  for (const TablePtr &t : {a, b})
+  for (const TablePtr &t : ts)
     for (const auto &c : t->columns()) var |= c.is_var();
-  if (var) {  // strings: byte counts per column need their own exchange (ShufflePair)
-    auto lr = ShufflePair(a, acols, b, bcols);
-    consume(0, 1, lr.first, lr.second);
+  if (var) {  // strings: byte counts per column need their own exchange
+    if (NT == 2) {
+      auto lr = ShufflePair(ts[0], tcols[0], ts[1], tcols[1]);
+      consume(0, 1, {lr.first, lr.second});
+    } else {
+      consume(0, 1, {Shuffle(ts[0], tcols[0])});
+    }
     return;
   }
   const int W = ctx->GetWorldSize(), me = ctx->GetRank();
   std::string v = ctx->GetConfig("shuffle_chunks", "");
   if (v.empty())
     if (const char *e = std::getenv("CYLON_SHUFFLE_CHUNKS")) v = e;
-  const int forced = v.empty() ? 0 : std::max(1, std::min(64, std::atoi(v.c_str())));
-  const int Kc = forced ? forced : (a->device().is_cuda() ? 4 : 1);
+  const int forced = !allow_chunks ? 1 : (v.empty() ? 0 : std::max(1, std::min(64, std::atoi(v.c_str()))));
+  const int Kc = forced ? forced : (ts[0]->device().is_cuda() ? 4 : 1);
   const uint32_t P = (uint32_t)W * (uint32_t)Kc;
-  const at::Device dev = a->device();
+  const at::Device dev = ts[0]->device();
   const auto lopt = at::TensorOptions().dtype(at::kLong).device(dev);
   // ---- the descriptor (assembled on the device: no sync before the all-gather)
   std::vector<at::Tensor> parts;
-  parts.push_back(at::tensor({a->Rows(), b->Rows()}, at::TensorOptions().dtype(at::kLong)).to(dev));
-  std::vector<int64_t> nflags;
-  for (const TablePtr &t : {a, b})
+  std::vector<int64_t> rows, nflags;
+  for (const TablePtr &t : ts) rows.push_back(t->Rows());
+  for (const TablePtr &t : ts)
     for (const auto &c : t->columns()) nflags.push_back(c.nullable() ? 1 : 0);
+  parts.push_back(at::tensor(rows, at::TensorOptions().dtype(at::kLong)).to(dev));
   parts.push_back(at::tensor(nflags, at::TensorOptions().dtype(at::kLong)).to(dev));
   std::string nv = ctx->GetConfig("shuffle_narrow", "");
   if (nv.empty())
     if (const char *e = std::getenv("CYLON_SHUFFLE_NARROW")) nv = e;
   std::vector<std::pair<int, int>> cand;  // (table, column) narrowable on the wire
   if (nv != "0")
-    for (int side = 0; side < 2; ++side) {
-      const TablePtr &t = side == 0 ? a : b;
-      for (int c = 0; c < t->Columns(); ++c)
-        if (narrow_candidate(t->column(c))) cand.push_back({side, c});
-    }
+    for (int side = 0; side < NT; ++side)
+      for (int c = 0; c < ts[side]->Columns(); ++c)
+        if (narrow_candidate(ts[side]->column(c))) cand.push_back({side, c});
   for (auto &sc : cand) {
-    const Column &c = (sc.first == 0 ? a : b)->column(sc.second);
+    const Column &c = ts[sc.first]->column(sc.second);
     if (c.length == 0) {
       parts.push_back(at::tensor({std::numeric_limits<int64_t>::max(), std::numeric_limits<int64_t>::min()}, lopt));
     } else {
@@ -654,11 +670,13 @@ void ShufflePairPlanned(const TablePtr &a, const std::vector<int> &acols, const 
       parts.push_back(at::stack({std::get<0>(mm), std::get<1>(mm)}));
     }
   }
-  const bool fast_a = mod_pass_eligible(a, acols, P), fast_b = mod_pass_eligible(b, bcols, P);
+  std::vector<bool> fast(NT);
   {
     CYLON_PHASE("shuffle.partition", dev);
-    parts.push_back(counts_device(a, acols, P, fast_a));
-    parts.push_back(counts_device(b, bcols, P, fast_b));
+    for (int i = 0; i < NT; ++i) {
+      fast[i] = mod_pass_eligible(ts[i], tcols[i], P);
+      parts.push_back(counts_device(ts[i], tcols[i], P, fast[i]));
+    }
   }
   at::Tensor desc = at::cat(parts);
   const int64_t D = desc.numel();
@@ -669,25 +687,28 @@ void ShufflePairPlanned(const TablePtr &a, const std::vector<int> &acols, const 
   }
   trace::add_counter("shuffle.plan_collectives", 1);
   const int64_t *g = all.data_ptr<int64_t>();  // W x D
-  const int na_cols = a->Columns(), nb_cols = b->Columns();
-  const int64_t off_null = 2, off_mm = off_null + na_cols + nb_cols, off_cnt = off_mm + 2 * (int64_t)cand.size();
-  CYLON_CHECK(off_cnt + 2 * (int64_t)P == D, Code::ExecutionError, "shuffle descriptor layout");
-  // chunk count
+  std::vector<int> ncols(NT), coff(NT + 1, 0);
+  for (int i = 0; i < NT; ++i) {
+    ncols[i] = ts[i]->Columns();
+    coff[i + 1] = coff[i] + ncols[i];
+  }
+  const int64_t off_null = NT, off_mm = off_null + coff[NT], off_cnt = off_mm + 2 * (int64_t)cand.size();
+  CYLON_CHECK(off_cnt + (int64_t)NT * P == D, Code::ExecutionError, "shuffle descriptor layout");
   int K = Kc;
-  if (!forced) {
+  if (!forced) {  // chunked when every rank holds >= 2^24 rows of every table
     int64_t mn = std::numeric_limits<int64_t>::max();
-    for (int r = 0; r < W; ++r) mn = std::min(mn, std::min(g[r * D + 0], g[r * D + 1]));
+    for (int r = 0; r < W; ++r)
+      for (int i = 0; i < NT; ++i) mn = std::min(mn, g[r * D + i]);
     K = mn >= (int64_t(1) << 24) ? Kc : 1;
   }
-  // nullability (any rank) and the wire plan (global ranges)
-  std::vector<int64_t> nullable(na_cols + nb_cols, 0);
+  std::vector<int64_t> nullable(coff[NT], 0);
   for (int r = 0; r < W; ++r)
-    for (int c = 0; c < na_cols + nb_cols; ++c) nullable[c] |= g[r * D + off_null + c];
-  std::vector<WirePlan> plans(2);
-  plans[0].narrow.assign(na_cols, false);
-  plans[0].base.assign(na_cols, 0);
-  plans[1].narrow.assign(nb_cols, false);
-  plans[1].base.assign(nb_cols, 0);
+    for (int c = 0; c < coff[NT]; ++c) nullable[c] |= g[r * D + off_null + c];
+  std::vector<WirePlan> plans(NT);
+  for (int i = 0; i < NT; ++i) {
+    plans[i].narrow.assign(ncols[i], false);
+    plans[i].base.assign(ncols[i], 0);
+  }
   for (size_t j = 0; j < cand.size(); ++j) {
     int64_t lo = std::numeric_limits<int64_t>::max(), hi = std::numeric_limits<int64_t>::min();
     for (int r = 0; r < W; ++r) {
@@ -699,73 +720,81 @@ void ShufflePairPlanned(const TablePtr &a, const std::vector<int> &acols, const 
     plans[cand[j].first].base[cand[j].second] = lo;
     trace::add_counter("shuffle.narrowed_columns", 1);
   }
-  const std::vector<int64_t> na_flags(nullable.begin(), nullable.begin() + na_cols);
-  const std::vector<int64_t> nb_flags(nullable.begin() + na_cols, nullable.end());
-  // per chunk k: rows this rank sends to rank r (local counts) and receives from rank r
-  auto sendc = [&](int side, int k, int r) -> int64_t {
-    const int64_t *c = g + (int64_t)me * D + off_cnt + (int64_t)side * P;
-    if (K == Kc) return c[(int64_t)k * W + r];
+  // rows this rank sends to / receives from rank r in chunk k (K = 1: a rank's Kc counts summed)
+  auto cnt = [&](int side, int k, int from, int to) -> int64_t {
+    const int64_t *c = g + (int64_t)from * D + off_cnt + (int64_t)side * P;
+    if (K == Kc) return c[(int64_t)k * W + to];
     int64_t s = 0;
-    for (int q = 0; q < Kc; ++q) s += c[(int64_t)q * W + r];
-    return s;
-  };
-  auto recvc = [&](int side, int k, int r) -> int64_t {
-    const int64_t *c = g + (int64_t)r * D + off_cnt + (int64_t)side * P;
-    if (K == Kc) return c[(int64_t)k * W + me];
-    int64_t s = 0;
-    for (int q = 0; q < Kc; ++q) s += c[(int64_t)q * W + me];
+    for (int q = 0; q < Kc; ++q) s += c[(int64_t)q * W + to];
     return s;
   };
   const uint32_t PK = (uint32_t)W * (uint32_t)K;
-  const bool fa = K == Kc ? fast_a : mod_pass_eligible(a, acols, PK), fb = K == Kc ? fast_b : mod_pass_eligible(b, bcols, PK);
-  trace::add_counter("shuffle.fast_partition", (fa ? 1 : 0) + (fb ? 1 : 0));
-  auto reorder = [&](const TablePtr &t, const std::vector<int> &cols, bool fast) -> TablePtr {
-    return fast ? mod_reorder(t, cols[0], PK) : PartitionReorder(t, hash_pids(t, cols, PK), PK).first;
-  };
-  std::vector<PendingTable> pa(K), pb(K);
-  std::vector<int64_t> offa(K + 1, 0), offb(K + 1, 0);
-  auto post = [&](const TablePtr &part, int side, int k, const std::vector<int64_t> &flags,
-                  std::vector<int64_t> &off) -> PendingTable {
+  std::vector<TablePtr> wired(NT);
+  std::vector<std::vector<PendingTable>> pend(NT, std::vector<PendingTable>(K));
+  std::vector<std::vector<int64_t>> off(NT, std::vector<int64_t>(K + 1, 0));
+  auto post = [&](int side, int k) {
     std::vector<int64_t> sc(W), rc(W);
     int64_t tot = 0;
     for (int r = 0; r < W; ++r) {
-      sc[r] = sendc(side, k, r);
-      rc[r] = recvc(side, k, r);
+      sc[r] = cnt(side, k, me, r);
+      rc[r] = cnt(side, k, r, me);
       tot += sc[r];
     }
-    off[k + 1] = off[k] + tot;
-    PendingTable pt = AllToAllPost(Slice(part, off[k], tot), sc, rc, flags);
-    attach_plan(pt, side == 0 ? a : b, plans[side]);
+    off[side][k + 1] = off[side][k] + tot;
+    const std::vector<int64_t> flags(nullable.begin() + coff[side], nullable.begin() + coff[side + 1]);
+    PendingTable pt = AllToAllPost(Slice(wired[side], off[side][k], tot), sc, rc, flags);
+    attach_plan(pt, ts[side], plans[side]);
     count_pending(pt);
-    return pt;
+    pend[side][k] = std::move(pt);
   };
-  TablePtr pta, ptb;
+  int nfast = 0;
   {
     CYLON_PHASE("shuffle.reorder+post", dev);
-    pta = to_wire(reorder(a, acols, fa), plans[0]);
-    pa[0] = post(pta, 0, 0, na_flags, offa);  // a's chunk 0 transfers while b is reordered
-    ptb = to_wire(reorder(b, bcols, fb), plans[1]);
-    pb[0] = post(ptb, 1, 0, nb_flags, offb);
-    for (int k = 1; k < K; ++k) {
-      pa[k] = post(pta, 0, k, na_flags, offa);
-      pb[k] = post(ptb, 1, k, nb_flags, offb);
+    for (int i = 0; i < NT; ++i) {  // table i's first chunk transfers while table i+1 is reordered
+      const bool f = K == Kc ? fast[i] : mod_pass_eligible(ts[i], tcols[i], PK);
+      nfast += f ? 1 : 0;
+      TablePtr ro = f ? mod_reorder(ts[i], tcols[i][0], PK) : PartitionReorder(ts[i], hash_pids(ts[i], tcols[i], PK), PK).first;
+      wired[i] = to_wire(ro, plans[i]);
+      post(i, 0);
     }
+    for (int k = 1; k < K; ++k)
+      for (int i = 0; i < NT; ++i) post(i, k);
   }
-  trace::add_counter("shuffle.rows_in", a->Rows() + b->Rows());
-  trace::add_counter("shuffle.bytes_in", a->nbytes() + b->nbytes());
+  int64_t rows_in = 0, bytes_in = 0;
+  for (const TablePtr &t : ts) {
+    rows_in += t->Rows();
+    bytes_in += t->nbytes();
+  }
+  trace::add_counter("shuffle.fast_partition", nfast);
+  trace::add_counter("shuffle.rows_in", rows_in);
+  trace::add_counter("shuffle.bytes_in", bytes_in);
   trace::add_counter("shuffle.chunks", K);
   for (int k = 0; k < K; ++k) {
-    TablePtr ta, tb;
+    std::vector<TablePtr> got(NT);
     {
       CYLON_PHASE("shuffle.wait", dev);
-      ta = AllToAllFinish(pa[k]);
-      tb = AllToAllFinish(pb[k]);
+      for (int i = 0; i < NT; ++i) got[i] = AllToAllFinish(pend[i][k]);
     }
-    pa[k] = PendingTable();
-    pb[k] = PendingTable();
-    trace::add_counter("shuffle.rows_out", ta->Rows() + tb->Rows());
-    consume(k, K, ta, tb);
+    int64_t rows_out = 0;
+    for (int i = 0; i < NT; ++i) {
+      pend[i][k] = PendingTable();
+      rows_out += got[i]->Rows();
+    }
+    trace::add_counter("shuffle.rows_out", rows_out);
+    consume(k, K, got);
   }
+}
+
+void ShufflePairPlanned(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,
+                        const std::vector<int> &bcols,
+                        const std::function<void(int, int, const TablePtr &, const TablePtr &)> &consume) {
+  planned_shuffle({a, b}, {acols, bcols}, true,
+                  [&](int k, int K, const std::vector<TablePtr> &t) { consume(k, K, t[0], t[1]); });
+}
+
+void ShufflePlanned(const TablePtr &t, const std::vector<int> &cols,
+                    const std::function<void(int, int, const TablePtr &)> &consume) {
+  planned_shuffle({t}, {cols}, true, [&](int k, int K, const std::vector<TablePtr> &r) { consume(k, K, r[0]); });
 }
 
 }  // namespace ops

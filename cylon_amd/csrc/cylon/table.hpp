@@ -132,6 +132,9 @@ void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const 
 void ShufflePairPlanned(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,
                         const std::vector<int> &bcols,
                         const std::function<void(int, int, const TablePtr &, const TablePtr &)> &consume);
+// single-table form (distributed group-by / unique): consume(k, K, t_k) per hash-disjoint chunk
+void ShufflePlanned(const TablePtr &t, const std::vector<int> &cols,
+                    const std::function<void(int, int, const TablePtr &)> &consume);
 
 // ---- relational -----------------------------------------------------------
 TablePtr Join(const TablePtr &left, const TablePtr &right, const join::config::JoinConfig &cfg);
