@@ -289,10 +289,24 @@ class DataFrame(object):
 
     def reset_index(self, level=None, drop: bool = False, inplace: bool = False, col_level=0, col_fill=""):
         target = self if inplace else DataFrame(self._table.project(list(range(self._table.column_count))))
+        names = list(self._index_columns)
         target._table._index = self._table.index
+        had_index = "index" in target.columns
         target._table.reset_index(drop_index=drop)
+        if not drop and not had_index and len(names) == 1 and isinstance(names[0], str) and \
+                names[0] not in target.columns and "index" in target.columns:
+            target._table.rename({"index": names[0]})  # pandas names the column after the index
         target._index_columns = []
         return None if inplace else target
+
+    def _with_index_columns(self) -> "DataFrame":
+        """This frame with its index columns present as ordinary columns (set_index(drop=True)
+        moved them into the index)."""
+        if all(isinstance(c, str) and c in self.columns for c in self._index_columns):
+            return self
+        out = self.reset_index()
+        out._index_columns = list(self._index_columns)
+        return out
 
     # ------------------------------------------------------------ relational
     def join(self, other: "DataFrame", on=None, how="left", lsuffix="l", rsuffix="r", sort=False,
@@ -303,7 +317,9 @@ class DataFrame(object):
         if not left_on or not right_on:
             return self._join_on_index(other, how, algorithm, env)
         left_on = left_on if isinstance(left_on, list) else [left_on]
-        return self._do_join(other, how, algorithm, left_on, right_on, lsuffix, rsuffix, env, sort)
+        left = self._with_index_columns() if on is None else self
+        return left._do_join(other._with_index_columns(), how, algorithm, left_on, right_on, lsuffix, rsuffix, env,
+                             sort)
 
     def _join_on_index(self, other, how, algorithm, env):
         tables = [self._change_context(env)._table if env else self._table,
@@ -334,8 +350,8 @@ class DataFrame(object):
         if right_index:
             right_on = right._index_columns
         if left_on is None or right_on is None:
-            raise ValueError("Columns to merge is not specified. Expected on or left_index/right_index."
-                             "Make sure dataframes has specified index columns if using left_index/right_index")
+            raise ValueError("merge needs join keys: pass on=, left_on=/right_on=, or left_index/right_index "
+                             "on frames that have index columns set")
         left_on = left_on if isinstance(left_on, list) else [left_on]
         right_on = right_on if isinstance(right_on, list) else [right_on]
         return self._do_join(right, how, algorithm, left_on, right_on, suffixes[0], suffixes[1], env, sort)

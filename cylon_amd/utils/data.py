@@ -66,7 +66,7 @@ class DataLoader(object):
         self._dataset = values
 
     def load(self):
-        raise NotImplementedError("Base class Not Implemented Method")
+        raise NotImplementedError(f"{type(self).__name__}.load: subclasses provide the loading strategy")
 
 
 class LocalDataLoader(DataLoader):
