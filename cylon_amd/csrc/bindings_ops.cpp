@@ -11,6 +11,7 @@
 #include "cylon/io/csv.hpp"
 #include "cylon/indexing/index.hpp"
 #include "cylon/io/device_interop.hpp"
+#include "cylon/io/h2d.hpp"
 #include "cylon/ops/api_ext.hpp"
 #include "cylon/ops/graph.hpp"
 #include "cylon/ops/relational.hpp"
@@ -71,6 +72,18 @@ void register_extended_ops(py::module &m) {
                  out.data_ptr<uint8_t>());
     return out;
   }, py::call_guard<py::gil_scoped_release>());
+
+  // ---- pinned, pipelined host -> device ingest (io/h2d.cpp); src = host address of nbytes
+  m.def("h2d_copy", [](uintptr_t src, int64_t nbytes, at::Tensor dst, int threads) {
+    CYLON_CHECK(dst.is_cuda() && dst.is_contiguous(), Code::Invalid, "h2d_copy: contiguous device tensor expected");
+    CYLON_CHECK(nbytes >= 0 && nbytes <= (int64_t)(dst.numel() * dst.element_size()), Code::Invalid,
+                "h2d_copy: " << nbytes << " bytes do not fit the destination");
+    io::H2DStats st;
+    io::StagedH2D(reinterpret_cast<const void *>(src), dst.data_ptr(), (size_t)nbytes, dst.device().index(), threads,
+                  &st);
+    return st.seconds;
+  }, py::arg("src"), py::arg("nbytes"), py::arg("dst"), py::arg("threads") = 0,
+     py::call_guard<py::gil_scoped_release>());
 
   // ---- Arrow C Device Data Interface (PyCapsules "arrow_schema" / "arrow_device_array")
   m.def("export_device_table", [](const TablePtr &t) {

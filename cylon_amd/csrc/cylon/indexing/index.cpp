@@ -27,10 +27,19 @@ at::Tensor RangeIndex::LocationsOf(const Column &labels) const {
 }
 
 // ---- linear (per-lookup join, the reference's scan index) ------------------------
+// Labels in the index column's type.  A label that the conversion does not carry exactly
+// (2.5 against an integer index, 300 against int8, 2^53 + 1 against float64) matches nothing:
+// it is marked null instead of matching the value it was rounded to.
 static Column as_index_type(const Column &labels, const Column &index) {
   if (labels.type == index.type || index.is_var() || labels.is_var()) return labels.to(index.data.device());
-  at::Tensor d = labels.data.slice(0, 0, labels.length).to(index.data.device()).to(storage_dtype(index.type));
-  at::Tensor v = labels.nullable() ? labels.validity.slice(0, 0, labels.length).to(index.data.device()) : at::Tensor();
+  const at::Device dev = index.data.device();
+  at::Tensor src = labels.data.slice(0, 0, labels.length).to(dev);
+  at::Tensor d = src.to(storage_dtype(index.type));
+  at::Tensor exact = d.to(src.scalar_type()).eq(src);
+  if (at::isFloatingType(src.scalar_type()) || at::isFloatingType(d.scalar_type()))  // and back, in double
+    exact &= d.to(at::kDouble).eq(src.to(at::kDouble));
+  at::Tensor v = exact.to(at::kByte);
+  if (labels.nullable()) v.mul_(labels.validity.slice(0, 0, labels.length).to(dev).ne(0).to(at::kByte));
   return Column(labels.name, index.type, labels.length, d, at::Tensor(), v);
 }
 
@@ -94,10 +103,28 @@ at::Tensor SortedIndex::LocationsOf(const Column &labels) const {
 }
 
 // ---- hash --------------------------------------------------------------------------
+// byte-keyed columns (strings, binary, fixed-size binary): the run keys are 64-bit hashes of the
+// values (row_hash64), sorted with their rows; a probe verifies the bytes of every candidate
+static bool bytes_keyed(const Column &c) { return c.is_var() || c.type.kind() == ValueKind::FIXED_BYTES; }
+
 HashIndex::HashIndex(std::shared_ptr<CylonContext> ctx, Column col)
     : SortedIndex(std::move(ctx), std::move(col), IndexingSchema::Hash) {
-  if (!persistent()) return;
   Exec ex(col_.data.device());
+  if (bytes_keyed(col_)) {
+    CYLON_PHASE("index.build", ex.device);
+    const int64_t n = col_.length;
+    at::Tensor h = ex.empty_i64(std::max<int64_t>(n, 1));
+    const ColView v = col_.view();
+    if (n) KCALL(ex, row_hash64, &v, 1, n, reinterpret_cast<uint64_t *>(ptr<int64_t>(h)));
+    at::Tensor rows = col_.nullable() ? ops::MaskToIndices(col_.validity.slice(0, 0, n))
+                                      : at::arange(n, ex.opts(at::kLong));
+    auto sorted = ops::RadixSortPairs(ex, h.slice(0, 0, n).index_select(0, rows).contiguous(), rows.contiguous(), 64);
+    sorted_img_ = sorted.first;
+    sorted_pos_ = sorted.second;
+    bytes_ = true;
+    trace::add_counter("index.built_rows", rows.numel());
+  }
+  if (!persistent()) return;
   const int64_t n = sorted_img_.numel();
   cap_ = 16;
   while (cap_ < 2 * std::max<int64_t>(n, 1)) cap_ <<= 1;  // >= 2 x distinct images
@@ -114,14 +141,35 @@ at::Tensor HashIndex::LocationsOf(const Column &labels) const {
   if (!persistent()) return LinearIndex::LocationsOf(labels);
   Exec ex(col_.data.device());
   CYLON_PHASE("index.lookup", ex.device);
-  at::Tensor img = LabelImages(labels);
+  const bool bytes = bytes_;
+  Column lab = bytes ? labels.to(col_.data.device()) : Column();
+  CYLON_CHECK(!bytes || bytes_keyed(lab), Code::TypeError, "a string / binary index needs string / binary labels");
+  at::Tensor img;
+  if (bytes) {
+    img = ex.empty_i64(std::max<int64_t>(lab.length, 1));
+    const ColView lv = lab.view();
+    if (lab.length) KCALL(ex, row_hash64, &lv, 1, lab.length, reinterpret_cast<uint64_t *>(ptr<int64_t>(img)));
+    img = img.slice(0, 0, lab.length);
+  } else {
+    img = LabelImages(labels);
+  }
   const int64_t m = img.numel();
   at::Tensor lo = ex.empty_i64(std::max<int64_t>(m, 1)).slice(0, 0, m), cnt = ex.empty_i64(std::max<int64_t>(m, 1)).slice(0, 0, m);
   KCALL(ex, hash_index_probe, reinterpret_cast<const uint64_t *>(ptr<int64_t>(tkeys_)), ptr<int32_t>(used_),
         ptr<int64_t>(tlo_), ptr<int64_t>(tcnt_), cap_, reinterpret_cast<const uint64_t *>(ptr<int64_t>(img)), m,
         ptr<int64_t>(lo), ptr<int64_t>(cnt));
   zero_null_labels(labels, cnt);
-  return GatherRuns(lo, cnt);
+  if (!bytes) return GatherRuns(lo, cnt);
+  // candidates share the label's 64-bit hash: keep those whose bytes equal the label's
+  at::Tensor cand = GatherRuns(lo, cnt);
+  at::Tensor offs = ops::exclusive_scan(ex, cnt);
+  at::Tensor keep = at::empty({std::max<int64_t>(cand.numel(), 1)}, ex.opts(at::kByte));
+  const ColView cv = col_.view(), lv = lab.view();
+  KCALL(ex, index_verify_bytes, cv, lv, ptr<int64_t>(sorted_pos_), ptr<int64_t>(lo), ptr<int64_t>(cnt),
+        ptr<int64_t>(offs), m, keep.data_ptr<uint8_t>());
+  const int64_t k = cand.numel();
+  if (k == 0) return cand;
+  return cand.index_select(0, ops::MaskToIndices(keep.slice(0, 0, k)));
 }
 
 std::shared_ptr<BaseIndex> BuildIndex(const TablePtr &t, int col, IndexingSchema schema) {

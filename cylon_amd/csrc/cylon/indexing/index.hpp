@@ -12,8 +12,10 @@
 // every lookup is a probe (or binary search) per label, a scan of the match counts and
 // a coalesced gather of positions (kernels/index.hip).  Linear keeps the reference's
 // per-lookup semantics (one device join of the labels against the column).  Results
-// are in label order, then row order (pandas `loc`).  Variable-width (string) index
-// columns use the per-lookup join for every schema.
+// are in label order, then row order (pandas `loc`).  String / binary index columns:
+// the Hash schema is persistent too (reference HashIndex<arrow::StringType>, index.hpp:222)
+// -- the runs are keyed by 64-bit hashes of the bytes and a probe verifies every candidate's
+// bytes against its label; the sorted schemas use the per-lookup join.
 #pragma once
 #include <memory>
 
@@ -85,8 +87,10 @@ class HashIndex : public SortedIndex {
   HashIndex(std::shared_ptr<CylonContext> ctx, Column col);
   at::Tensor LocationsOf(const Column &labels) const override;
   int64_t Capacity() const { return cap_; }
+  bool BytesKeyed() const { return bytes_; }
 
  private:
+  bool bytes_ = false;  // run keys are 64-bit hashes of string / binary values (verified on probe)
   int64_t cap_ = 0;
   at::Tensor tkeys_, used_, tlo_, tcnt_;
 };

@@ -53,5 +53,30 @@ void index_gather_positions(const int64_t *sorted_pos, const int64_t *lo, const 
     for (int64_t j = 0; j < cnt[i]; ++j) out[offs[i] + j] = sorted_pos[lo[i] + j];
 }
 
+static void bytes_of(const ColView &c, int64_t r, const uint8_t *&p, int64_t &len) {
+  if (c.offsets) {
+    p = c.data + c.offsets[r];
+    len = c.offsets[r + 1] - c.offsets[r];
+  } else {
+    p = c.data + r * (int64_t)c.width;
+    len = c.width;
+  }
+}
+
+void index_verify_bytes(const ColView &col, const ColView &labels, const int64_t *sorted_pos, const int64_t *lo,
+                        const int64_t *cnt, const int64_t *offs, int64_t m, uint8_t *keep, void *) {
+  for (int64_t i = 0; i < m; ++i) {
+    const uint8_t *lp;
+    int64_t ll;
+    bytes_of(labels, i, lp, ll);
+    for (int64_t j = 0; j < cnt[i]; ++j) {
+      const uint8_t *cp;
+      int64_t cl;
+      bytes_of(col, sorted_pos[lo[i] + j], cp, cl);
+      keep[offs[i] + j] = cl == ll && (ll == 0 || std::equal(cp, cp + ll, lp)) ? 1 : 0;
+    }
+  }
+}
+
 }  // namespace cpu
 }  // namespace cylon

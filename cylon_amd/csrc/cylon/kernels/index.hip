@@ -132,5 +132,46 @@ void index_gather_positions(const int64_t *sorted_pos, const int64_t *lo, const 
   HIP_LAUNCH_CHECK();
 }
 
+// the bytes of row r of a var-width (offsets) or fixed-width column
+__device__ __forceinline__ void idx_bytes(const ColView &c, int64_t r, const uint8_t *&p, int64_t &len) {
+  if (c.offsets) {
+    p = c.data + c.offsets[r];
+    len = c.offsets[r + 1] - c.offsets[r];
+  } else {
+    p = c.data + r * (int64_t)c.width;
+    len = c.width;
+  }
+}
+
+// one wave per label, one lane per candidate row of the label's hash run
+__global__ void k_index_verify_bytes(ColView col, ColView labels, const int64_t *__restrict__ sorted_pos,
+                                     const int64_t *__restrict__ lo, const int64_t *__restrict__ cnt,
+                                     const int64_t *__restrict__ offs, int64_t m, uint8_t *__restrict__ keep) {
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
+  const int lane = lane_id();
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; i < m; i += waves) {
+    const int64_t l = lo[i], c = cnt[i], o = offs[i];
+    const uint8_t *lp;
+    int64_t ll;
+    idx_bytes(labels, i, lp, ll);
+    for (int64_t j = lane; j < c; j += kWave) {
+      const uint8_t *cp;
+      int64_t cl;
+      idx_bytes(col, sorted_pos[l + j], cp, cl);
+      bool eq = cl == ll;
+      for (int64_t b = 0; eq && b < ll; ++b) eq = cp[b] == lp[b];
+      keep[o + j] = eq ? 1 : 0;
+    }
+  }
+}
+
+void index_verify_bytes(const ColView &col, const ColView &labels, const int64_t *sorted_pos, const int64_t *lo,
+                        const int64_t *cnt, const int64_t *offs, int64_t m, uint8_t *keep, void *stream) {
+  if (m == 0) return;
+  hipLaunchKernelGGL(k_index_verify_bytes, dim3(grid_for(m * kWave)), dim3(kBlock), 0, as_stream(stream), col, labels,
+                     sorted_pos, lo, cnt, offs, m, keep);
+  HIP_LAUNCH_CHECK();
+}
+
 }  // namespace hip
 }  // namespace cylon

@@ -171,6 +171,119 @@ __global__ __launch_bounds__(kRPThreads) void k_rp_hist(Digit digit, int64_t n, 
   for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) bh[(int64_t)p * nblocks + blockIdx.x] = hist[p];
 }
 
+// Chained-scan passes (decoupled lookback).  Histogram mode runs k_rp_hist before every pass:
+// it re-reads the keys (8 B/row, 15 % of a key-only sort) to give each block's contiguous chunk
+// its bucket offsets.  Lookback mode counts every pass's digits ONCE (k_lb_hist: the counts of a
+// digit do not depend on the row order) and lets the pass kernel find a tile's offsets itself:
+// tiles are claimed in row order from a ticket counter; a tile publishes its per-bucket count,
+// then sums its predecessors' published counts back to the nearest tile that already published
+// an inclusive prefix, and publishes its own.  Status words are 64-bit (flag | pass epoch | rows)
+// relaxed agent-scope atomics: the value travels with its flag, so no fence is needed, and a
+// word left by an earlier pass of the same session (other epoch) reads as "not ready".
+constexpr int kLbMaxPasses = 8;
+constexpr unsigned long long kLbAgg = 1ull << 62, kLbPrefix = 2ull << 62, kLbValue = (1ull << 56) - 1;
+
+struct Lookback {
+  const int64_t *gstart;         // exclusive global start of every bucket of this pass
+  unsigned long long *status;    // [tile][nbuckets]
+  unsigned int *ticket;          // next tile to claim
+  unsigned long long epoch;      // 1..63
+};
+
+// Windowed lookback in two steps: lb_publish stores tile t's count of bucket p right after the
+// scan (successors can sum it while this tile ranks its slots); lb_exclusive then reads its
+// predecessors' words kLbWin at a time (independent loads, one round trip per window),
+// consumes them in order (waiting for any tile not ranked yet) until it meets an inclusive
+// prefix, publishes t's own prefix and returns the rows of bucket p in tiles < t plus the
+// bucket's global start.  One dependent load per predecessor cost the key-only sort ~50 % per
+// pass: hundreds of tiles are in flight, and the walk back to the nearest prefix is long.  The
+// window is not held across the slot phase (the loads' registers spill there).
+constexpr int kLbWin = 8;
+
+__device__ __forceinline__ unsigned long long lb_load(const unsigned long long *w) {
+  return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(unsigned long long *w, unsigned long long v) {
+  __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void lb_publish(const Lookback &lb, uint32_t nb, int64_t t, uint32_t p, uint32_t cnt) {
+  const unsigned long long tag = lb.epoch << 56;
+  if (t == 0) lb_store(lb.status + p, kLbPrefix | tag | (unsigned long long)(lb.gstart[p] + cnt));
+  else lb_store(lb.status + t * nb + p, kLbAgg | tag | cnt);
+}
+
+__device__ __forceinline__ int64_t lb_exclusive(const Lookback &lb, uint32_t nb, int64_t t, uint32_t p, uint32_t cnt) {
+  if (t == 0) return lb.gstart[p];
+  int64_t excl = 0;
+  for (int64_t j = t - 1;; j -= kLbWin) {
+    unsigned long long v[kLbWin];
+#pragma unroll
+    for (int w = 0; w < kLbWin; ++w) v[w] = j - w >= 0 ? lb_load(lb.status + (j - w) * nb + p) : 0ull;
+    bool found = false;
+#pragma unroll
+    for (int w = 0; w < kLbWin; ++w) {
+      if (found || j - w < 0) continue;  // tile 0 always holds a prefix: the walk ends there at the latest
+      unsigned long long x = v[w];
+      while (((x >> 56) & 63ull) != lb.epoch) {  // tile j - w not ranked yet (its block is running)
+        __builtin_amdgcn_s_sleep(1);
+        x = lb_load(lb.status + (j - w) * nb + p);
+      }
+      excl += (int64_t)(x & kLbValue);
+      found = (x & kLbPrefix) != 0;
+    }
+    if (found) break;
+  }
+  lb_store(lb.status + t * nb + p, kLbPrefix | (lb.epoch << 56) | (unsigned long long)(excl + cnt));
+  return excl;
+}
+
+template <class Digit>
+struct DigitSet {
+  Digit d[kLbMaxPasses];
+  int n;
+};
+
+// every pass's digit histogram in one read of the keys: hist[s][p] (u64, accumulated)
+template <class Digit>
+__global__ __launch_bounds__(kRPThreads) void k_lb_hist(DigitSet<Digit> ds, int64_t n, uint32_t nb,
+                                                        unsigned long long *__restrict__ gh) {
+  __shared__ unsigned int hist[kLbMaxPasses * kRPMaxBuckets];
+  for (uint32_t q = threadIdx.x; q < (uint32_t)ds.n * nb; q += blockDim.x) hist[q] = 0;
+  __syncthreads();
+  const int64_t *keys = ds.d[0].keys;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t k = keys[i];
+#pragma unroll
+    for (int s = 0; s < kLbMaxPasses; ++s)
+      if (s < ds.n) atomicAdd(&hist[s * nb + ds.d[s].of_key(k)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q < (uint32_t)ds.n * nb; q += blockDim.x)
+    if (hist[q]) atomicAdd(&gh[q], (unsigned long long)hist[q]);
+}
+
+// gstart[s][p] = exclusive scan of hist[s][.] (one block per pass)
+__global__ __launch_bounds__(kRPThreads) void k_lb_scan(const unsigned long long *__restrict__ gh, uint32_t nb,
+                                                        int64_t *__restrict__ gstart) {
+  __shared__ int64_t wsum[kRPWaves];
+  const int s = blockIdx.x, lane = lane_id(), wave = threadIdx.x / kWave;
+  const uint32_t p = threadIdx.x;
+  const int64_t c = p < nb ? (int64_t)gh[s * nb + p] : 0;
+  int64_t inc = c;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const int64_t t = __shfl_up(inc, d, kWave);
+    if (lane >= d) inc += t;
+  }
+  if (lane == kWave - 1) wsum[wave] = inc;
+  __syncthreads();
+  int64_t off = 0;
+  for (int w = 0; w < wave; ++w) off += wsum[w];
+  if (p < nb) gstart[s * nb + p] = off + inc - c;
+}
+
 // block-wide exclusive scan of one uint32 per thread (WAVES waves)
 template <int WAVES = kRPWaves>
 __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) {
@@ -219,14 +332,16 @@ constexpr int kRPStampTiles = 64, kRPStampSlots = 16;
 // on block-wide counters: unstable), kRankWaveAtomic (LDS atomics on the wave's own packed
 // 16-bit counters: stable exactly when one instruction's same-address atomics return in lane
 // order -- tools/lds_atomic_order.hip measures that on the device).
-template <class Digit, bool W8, int THREADS, int RANK>
+// LB: lookback mode (tiles claimed from lb.ticket, offsets by decoupled lookback; bh_scan unused).
+template <class Digit, bool W8, int THREADS, int RANK, bool LB>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_rows_pass(
     Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
-    const int64_t *__restrict__ bh_scan, unsigned long long *__restrict__ stamps) {
+    const int64_t *__restrict__ bh_scan, Lookback lb, unsigned long long *__restrict__ stamps) {
   constexpr int WAVES = THREADS / kWave;
   constexpr int TILE = THREADS * kRPItems;
   constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;  // buckets per thread in the offset scan
   static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 4 <= TILE * 8, "ranking scratch must fit the stage");
+  static_assert(!LB || (THREADS >= kRPMaxBuckets && TILE == kRPTile), "lookback: one bucket a thread, 8192-row tiles");
   __shared__ int64_t running[kRPMaxBuckets];
   __shared__ uint32_t toff[kRPMaxBuckets + 1];
   __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16, sdig[TILE] u32}
@@ -238,15 +353,24 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   // sorted slot j -> digit << 16 | input row in the tile (the row feeds the ranking guard)
   uint32_t *sdig = reinterpret_cast<uint32_t *>(wcnt + WAVES * kRPMaxBuckets);
   uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
+  __shared__ int64_t s_next;  // LB: first row of the next claimed tile
   bool order_bad = false;
 
   const int64_t b = blockIdx.x;
-  for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] = bh_scan[(int64_t)p * nblocks + b];
+  int64_t begin, end;
+  if (LB) {
+    if (threadIdx.x == 0) s_next = (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
+    __syncthreads();
+    begin = s_next;
+    end = n;
+  } else {
+    for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] = bh_scan[(int64_t)p * nblocks + b];
+    begin = b * rows_per_block;
+    end = (begin + rows_per_block < n) ? begin + rows_per_block : n;
+  }
   const int wave = threadIdx.x / kWave;
   const int lane = lane_id();
   const uint64_t lt = lanemask_lt();
-  const int64_t begin = b * rows_per_block;
-  const int64_t end = (begin + rows_per_block < n) ? begin + rows_per_block : n;
   uint16_t *mycnt = wcnt + wave * nbuckets;
   const int wrow = wave * kWave * kRPItems;
 
@@ -256,7 +380,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     const int64_t i = begin + wrow + k * kWave + lane;
     if (i < end) kv[k] = (uint64_t)digit.keys[i];
   }
-  for (int64_t tile = begin; tile < end; tile += TILE) {
+  for (int64_t tile = begin, next = 0; tile < end; tile = next) {
+    next = tile + TILE;
     const int tix = (int)((tile - begin) / TILE);
     RP_STAMP(0);
     const int cnt = (int)((end - tile) < TILE ? (end - tile) : TILE);
@@ -339,6 +464,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     __syncthreads();
     RP_STAMP(3);
+    // LB: this tile's bucket offsets from its predecessors (read by the dst phase): count published
+    // before the slot phase, lookback after it.  nbuckets <= THREADS: one bucket a thread
+    const uint32_t lbc = LB && threadIdx.x < nbuckets ? toff[threadIdx.x + 1] - toff[threadIdx.x] : 0u;
+    if (LB && threadIdx.x < nbuckets) lb_publish(lb, nbuckets, tile / TILE, threadIdx.x, lbc);
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k) {
       if (pl[k] == 0xffffffffu) continue;
@@ -347,6 +476,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       sdig[pos] = (p << 16) | (uint32_t)(wrow + k * kWave + lane);
       pl[k] = pos;
     }
+    if (LB && threadIdx.x < nbuckets) running[threadIdx.x] = lb_exclusive(lb, nbuckets, tile / TILE, threadIdx.x, lbc);
     __syncthreads();
     RP_STAMP(4);
     int64_t dst[kRPItems];  // destination of sorted slot j = threadIdx.x + q * THREADS
@@ -364,7 +494,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     __syncthreads();  // counters / digits dead: the union becomes the column stage
     RP_STAMP(5);
-    const int64_t next = tile + TILE;
     // load column c+1 while column c streams out of the stage
     uint64_t v[kRPItems];
 #pragma unroll
@@ -374,10 +503,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       const int w = cols.width[c];
       uint8_t *out = cols.out[c];
       const uint64_t x = c == 0 ? cols.key_xor : 0ull;
+      if (LB && c + 1 == cols.n && threadIdx.x == 0) s_next = (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
 #pragma unroll
       for (int k = 0; k < kRPItems; ++k)
         if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
       __syncthreads();
+      if (LB && c + 1 == cols.n) next = s_next;
       RP_STAMP(6 + 2 * c);
       if (c + 1 < cols.n) {  // prefetch column c+1 of this tile
         const uint8_t *in = cols.in[c + 1];
@@ -405,7 +536,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       __syncthreads();
       RP_STAMP(7 + 2 * c);
     }
-    for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] += toff[p + 1] - toff[p];
+    if (!LB)
+      for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] += toff[p + 1] - toff[p];
   }
   if (order_bad) atomicOr(cols.order_bad, 1);
 }
@@ -419,10 +551,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 //   * no cross-column / cross-tile prefetch (the second block hides the load latency);
 //   * the destination of sorted slot j is packed as (digit << 16 | j - toff[digit]) and
 //     completed from running[] in LDS at store time (8 VGPRs instead of 16).
-template <class Digit, bool W8, int RANK>
+template <class Digit, bool W8, int RANK, bool LB>
 __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_rows_pass_lean(
     Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
-    const int64_t *__restrict__ bh_scan) {
+    const int64_t *__restrict__ bh_scan, Lookback lb) {
   constexpr int THREADS = kRPThreads, WAVES = THREADS / kWave, TILE = THREADS * kRPItems;
   constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;
   static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 4 <= TILE * 8, "ranking scratch must fit the stage");
@@ -435,20 +567,30 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
   uint32_t *bcnt = reinterpret_cast<uint32_t *>(ustage);
   uint32_t *sdig = reinterpret_cast<uint32_t *>(wcnt + WAVES * kRPMaxBuckets);  // digit << 16 | input row
   uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
+  __shared__ int64_t s_next;  // LB: first row of the next claimed tile
   bool order_bad = false;
   (void)nbits;
 
   const int64_t b = blockIdx.x;
-  for (uint32_t p = threadIdx.x; p < nbuckets; p += THREADS) running[p] = bh_scan[(int64_t)p * nblocks + b];
+  int64_t begin, end;
+  if (LB) {
+    if (threadIdx.x == 0) s_next = (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
+    __syncthreads();
+    begin = s_next;
+    end = n;
+  } else {
+    for (uint32_t p = threadIdx.x; p < nbuckets; p += THREADS) running[p] = bh_scan[(int64_t)p * nblocks + b];
+    begin = b * rows_per_block;
+    end = (begin + rows_per_block < n) ? begin + rows_per_block : n;
+  }
   // wave index made provably uniform: per-wave base pointers then live in SGPRs and every
   // load / store addresses its row with a 32-bit lane offset plus an immediate
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const int64_t begin = b * rows_per_block;
-  const int64_t end = (begin + rows_per_block < n) ? begin + rows_per_block : n;
   uint16_t *mycnt = wcnt + wave * nbuckets;
   const int wrow = wave * kWave * kRPItems;
 
-  for (int64_t tile = begin; tile < end; tile += TILE) {
+  for (int64_t tile = begin, next = 0; tile < end; tile = next) {
+    next = tile + TILE;
     const int cnt = (int)((end - tile) < TILE ? (end - tile) : TILE);
     // per-thread constants are recomputed every tile from an opaque copy of the thread id:
     // hoisted out of the tile loop they outlive the 64-VGPR budget and spill
@@ -516,6 +658,10 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
       if (tx == THREADS - 1) toff[nbuckets] = ex + total;
     }
     __syncthreads();
+    // LB: this tile's bucket offsets (read by the column stores): count published before the slot
+    // phase, lookback after it.  nbuckets <= THREADS: one bucket a thread
+    const uint32_t lbc = LB && (uint32_t)tx < nbuckets ? toff[tx + 1] - toff[tx] : 0u;
+    if (LB && (uint32_t)tx < nbuckets) lb_publish(lb, nbuckets, tile / TILE, tx, lbc);
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k) {
       if (pl[k] == 0xffffffffu) continue;
@@ -524,6 +670,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
       sdig[pos] = (p << 16) | (uint32_t)(wrow + k * kWave + lane);
       pl[k] = pos;
     }
+    if (LB && (uint32_t)tx < nbuckets) running[tx] = lb_exclusive(lb, nbuckets, tile / TILE, tx, lbc);
     __syncthreads();
     uint32_t dp[kRPItems];  // sorted slot j = tx + q * THREADS -> digit << 16 | offset in its run
 #pragma unroll
@@ -554,10 +701,12 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
         for (int k = 0; k < kRPItems; ++k) v[k] = (k * kWave + lane < lim) ? ldw<W8>(ibase, k * kWave + lane, w) : 0ull;
       }
       const uint64_t x = c == 0 ? cols.key_xor : 0ull;
+      if (LB && c + 1 == cols.n && tx == 0) s_next = (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
 #pragma unroll
       for (int k = 0; k < kRPItems; ++k)
         if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
       __syncthreads();
+      if (LB && c + 1 == cols.n) next = s_next;
 #pragma unroll
       for (int q = 0; q < kRPItems; ++q) {
         const int j = tx + q * THREADS;
@@ -565,7 +714,8 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
       }
       __syncthreads();
     }
-    for (uint32_t p = tx; p < nbuckets; p += THREADS) running[p] += toff[p + 1] - toff[p];
+    if (!LB)
+      for (uint32_t p = tx; p < nbuckets; p += THREADS) running[p] += toff[p + 1] - toff[p];
   }
   if (order_bad) atomicOr(cols.order_bad, 1);
 }
@@ -758,23 +908,23 @@ int64_t radix_rows_pass_workspace(int64_t n, int digit_bits) {  // covers both b
   return ws;
 }
 
-template <class Digit, int THREADS, int RANK>
+template <class Digit, int THREADS, int RANK, bool LB = false>
 static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit &dg, int digit_bits, uint32_t nb,
-                             const ColSet &cs, int64_t n, const int64_t *bh_scan) {
+                             const ColSet &cs, int64_t n, const int64_t *bh_scan, const Lookback &lb = Lookback{}) {
   static const bool stamp = std::getenv("CYLON_RP_STAMPS") != nullptr;  // debug: phase stamps to stderr
   unsigned long long *st = nullptr;
-  if (stamp) {
+  if (stamp && !LB) {
     HIP_CHECK(hipStreamSynchronize(s));
     HIP_CHECK(hipMalloc(&st, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
     HIP_CHECK(hipMemset(st, 0, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
   }
   if (w8)
-    hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS, RANK>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s,
-                       dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, st);
+    hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS, RANK, LB>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s,
+                       dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
   else
-    hipLaunchKernelGGL((k_rows_pass<Digit, false, THREADS, RANK>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s,
-                       dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, st);
-  if (stamp) {
+    hipLaunchKernelGGL((k_rows_pass<Digit, false, THREADS, RANK, LB>), dim3((unsigned)g.nblocks), dim3(THREADS), 0,
+                       s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
+  if (st) {
     HIP_CHECK(hipStreamSynchronize(s));
     std::vector<unsigned long long> h(kRPStampTiles * kRPStampSlots);
     HIP_CHECK(hipMemcpy(h.data(), st, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost));
@@ -804,13 +954,99 @@ static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const 
   }
 }
 
+template <class Digit, int RANK, bool LB>
+static void lean_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit &dg, int digit_bits, uint32_t nb,
+                        const ColSet &cs, int64_t n, const int64_t *bh_scan, const Lookback &lb) {
+  if (w8)
+    hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, RANK, LB>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s,
+                       dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
+  else
+    hipLaunchKernelGGL((k_rows_pass_lean<Digit, false, RANK, LB>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s,
+                       dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
+}
+
+// ---- lookback session workspace (int64 words):
+//   [hist u64: kLbMaxPasses x kRPMaxBuckets][gstart: same][tickets: kLbMaxPasses u32 (4 words)][status: tiles x 2^maxbits]
+constexpr int64_t kLbHistWords = (int64_t)kLbMaxPasses * kRPMaxBuckets;
+static int64_t lb_tiles(int64_t n) { return std::max<int64_t>(1, (n + kRPTile - 1) / kRPTile); }
+
+// Off by default: measured slower on MI355X (profiles/r03/lookback_ab.txt: 2B sort 99.3 -> 110.1 ms,
+// headline join 110.8 -> 118.6 ms).  Tiles claimed by ticket land in row order on whichever XCD
+// is free, so consecutive tiles' partial 128-B runs of one bucket are written from different
+// L2s instead of merging in one (the per-block chunks of histogram mode keep a bucket's
+// consecutive runs in one block, one L2), and every tile waits on agent-scope status words.
+// CYLON_RP_LOOKBACK=1 enables it.
+bool radix_lookback_enabled() {
+  const char *e = std::getenv("CYLON_RP_LOOKBACK");
+  return e && e[0] == '1';
+}
+
+int64_t radix_lb_workspace(int64_t n, int max_digit_bits) {
+  return 2 * kLbHistWords + kLbMaxPasses / 2 + lb_tiles(n) * (int64_t(1) << max_digit_bits);
+}
+
+template <class Digit>
+static void lb_prepare(const DigitSet<Digit> &ds, int64_t n, int max_digit_bits, int64_t *lbws, hipStream_t s) {
+  CYLON_CHECK(ds.n >= 1 && ds.n <= kLbMaxPasses, Code::Invalid, "lookback passes " << ds.n);
+  CYLON_CHECK(max_digit_bits >= 1 && max_digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << max_digit_bits);
+  const uint32_t nb = 1u << max_digit_bits;
+  // histograms, tickets and status words start at zero (epoch 0 is never a pass's tag)
+  HIP_CHECK(hipMemsetAsync(lbws, 0, sizeof(int64_t) * radix_lb_workspace(n, max_digit_bits), s));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_lb_hist<Digit>, dim3(grid_for(n, kRPThreads * 8, kNumCUs * 2)), dim3(kRPThreads), 0, s, ds, n,
+                       nb, reinterpret_cast<unsigned long long *>(lbws));
+    HIP_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(k_lb_scan, dim3(ds.n), dim3(kRPThreads), 0, s, reinterpret_cast<unsigned long long *>(lbws), nb,
+                     lbws + kLbHistWords);
+  HIP_LAUNCH_CHECK();
+}
+
+// Every pass of one session uses the same bucket count (2^max_digit_bits histogram rows; a pass
+// with fewer digit bits leaves the upper rows empty).
+void radix_lb_prepare_part(const int64_t *keys, int64_t n, int total_bits, const int *shifts, const int *dbits,
+                           int npass, int max_digit_bits, int64_t *lbws, void *stream) {
+  DigitSet<PartDigit> ds{};
+  ds.n = npass;
+  for (int s = 0; s < npass; ++s) ds.d[s] = PartDigit{keys, total_bits, shifts[s], (1u << dbits[s]) - 1};
+  lb_prepare(ds, n, max_digit_bits, lbws, as_stream(stream));
+}
+
+void radix_lb_prepare_sort(const int64_t *keys, int64_t n, uint64_t flip, const int *shifts, const int *dbits,
+                           int npass, int max_digit_bits, int64_t *lbws, void *stream) {
+  DigitSet<ImageDigit> ds{};
+  ds.n = npass;
+  for (int s = 0; s < npass; ++s) ds.d[s] = ImageDigit{keys, shifts[s], (1u << dbits[s]) - 1, flip};
+  lb_prepare(ds, n, max_digit_bits, lbws, as_stream(stream));
+}
+
+void radix_lb_prepare_range(const int64_t *keys, int64_t n, uint64_t flip, uint64_t mn, int rshift, const int *shifts,
+                            const int *dbits, int npass, int max_digit_bits, int64_t *lbws, void *stream) {
+  DigitSet<RangeDigit> ds{};
+  ds.n = npass;
+  for (int s = 0; s < npass; ++s) ds.d[s] = RangeDigit{keys, flip, mn, rshift, shifts[s], (1u << dbits[s]) - 1};
+  lb_prepare(ds, n, max_digit_bits, lbws, as_stream(stream));
+}
+
+// pass `pass` of a lookback session: its gstart row, ticket and epoch
+static Lookback lb_args(int64_t *lbws, int pass, int max_digit_bits) {
+  Lookback lb;
+  lb.gstart = lbws + kLbHistWords + (int64_t)pass * (int64_t(1) << max_digit_bits);
+  lb.ticket = reinterpret_cast<unsigned int *>(lbws + 2 * kLbHistWords) + pass;
+  lb.status = reinterpret_cast<unsigned long long *>(lbws + 2 * kLbHistWords + kLbMaxPasses / 2);
+  lb.epoch = (unsigned long long)(pass + 1);
+  return lb;
+}
+
 // stable = false (join partitions only) ranks rows with LDS atomics: rows of one
 // bucket keep no particular order inside a tile's run.  Instantiated for PartDigit
 // only; every other digit (sort, shuffle, range join) needs the stable order.
+// lbws != nullptr: lookback mode, pass `lb_pass` of the session radix_lb_prepare_* set up with
+// `lb_bits` histogram bits (digit_bits <= lb_bits); ws is not used.
 template <class Digit, bool CAN_UNSTABLE = std::is_same<Digit, PartDigit>::value>
 static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const uint8_t *const *in, uint8_t *const *out,
                              const int *widths, int ncols, int64_t *ws, void *stream, uint64_t key_xor = 0,
-                             bool stable = true) {
+                             bool stable = true, int64_t *lbws = nullptr, int lb_pass = 0, int lb_bits = 0) {
   if (n == 0) return;
   CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
   CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
@@ -820,6 +1056,9 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   // (partition / mod / range digits store column 0 as read)
   CYLON_CHECK((key_xor == 0 || std::is_same<Digit, ImageDigit>::value), Code::Invalid,
               "radix pass: key_xor is only valid for order-image digits");
+  const bool lbm = lbws != nullptr;
+  CYLON_CHECK(!lbm || (lb_pass >= 0 && lb_pass < kLbMaxPasses && digit_bits <= lb_bits), Code::Invalid,
+              "radix pass: bad lookback pass " << lb_pass);
   hipStream_t s = as_stream(stream);
   const uint32_t nb = 1u << digit_bits;
   CYLON_CHECK(stable || CAN_UNSTABLE, Code::Invalid, "radix pass: only partition digits may rank unstably");
@@ -830,15 +1069,28 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   if (CAN_UNSTABLE && dbg && dbg[0] == '1') stable = false;
   const bool unstable = CAN_UNSTABLE && !stable;
   const bool wave_atomic = !unstable && rp_wave_atomic(s);
-  const int threads = rp_threads(ncols, unstable || wave_atomic);
+  // lookback tiles are 8192 rows: 1024-thread kernels only
+  const int threads = lbm ? 1024 : rp_threads(ncols, unstable || wave_atomic);
   const bool lean = rp_lean(ncols) && (unstable || wave_atomic) && threads == 1024;
-  const RPGeometry g = rp_geometry(n, threads, lean ? 2 : 1);
-  const int64_t m = g.nblocks * (int64_t)nb;
-  int64_t *bh = ws, *bh_scan = ws + m, *scan_ws = bh_scan + m + 1;
-  hipLaunchKernelGGL(k_rp_hist<Digit>, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, n, nb,
-                     g.rows_per_block, g.nblocks, bh);
-  HIP_LAUNCH_CHECK();
-  exclusive_scan(bh, m, bh_scan, scan_ws, stream);
+  RPGeometry g;
+  const int64_t *bh_scan = nullptr;
+  Lookback lb{};
+  if (lbm) {
+    // status rows are 2^lb_bits wide; a pass with fewer bits indexes them with its own nb
+    lb = lb_args(lbws, lb_pass, lb_bits);
+    g.rows_per_block = kRPTile;
+    g.nblocks = std::min<int64_t>(lb_tiles(n), (int64_t)kNumCUs * (lean ? 2 : 1));  // persistent, tiles by ticket
+  } else {
+    g = rp_geometry(n, threads, lean ? 2 : 1);
+    const int64_t m = g.nblocks * (int64_t)nb;
+    int64_t *bh = ws;
+    int64_t *scan_out = ws + m, *scan_ws = scan_out + m + 1;
+    hipLaunchKernelGGL(k_rp_hist<Digit>, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, n, nb,
+                       g.rows_per_block, g.nblocks, bh);
+    HIP_LAUNCH_CHECK();
+    exclusive_scan(bh, m, scan_out, scan_ws, stream);
+    bh_scan = scan_out;
+  }
   ColSet cs;
   cs.n = ncols;
   cs.key_xor = key_xor;
@@ -859,22 +1111,22 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   const bool big = threads == 1024;
   if (lean) {
     constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankWaveAtomic;
-    if (unstable && w8)
-      hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, R>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg,
-                         digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan);
-    else if (unstable)
-      hipLaunchKernelGGL((k_rows_pass_lean<Digit, false, R>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg,
-                         digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan);
-    else if (w8)
-      hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, kRankWaveAtomic>), dim3((unsigned)g.nblocks),
-                         dim3(kRPThreads), 0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan);
-    else
-      hipLaunchKernelGGL((k_rows_pass_lean<Digit, false, kRankWaveAtomic>), dim3((unsigned)g.nblocks),
-                         dim3(kRPThreads), 0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan);
+    if (lbm) {
+      if (unstable) lean_kernel<Digit, R, true>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
+      else lean_kernel<Digit, kRankWaveAtomic, true>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
+    } else {
+      if (unstable) lean_kernel<Digit, R, false>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
+      else lean_kernel<Digit, kRankWaveAtomic, false>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
+    }
     HIP_LAUNCH_CHECK();
     return;
   }
-  if (unstable) {
+  if (lbm) {
+    constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankBallot;
+    if (unstable) rows_pass_kernel<Digit, 1024, R, true>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
+    else if (wave_atomic) rows_pass_kernel<Digit, 1024, kRankWaveAtomic, true>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
+    else rows_pass_kernel<Digit, 1024, kRankBallot, true>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
+  } else if (unstable) {
     constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankBallot;
     if (big) rows_pass_kernel<Digit, 1024, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
     else rows_pass_kernel<Digit, 512, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
@@ -889,26 +1141,27 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
 }
 
 void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, int digit_bits, const uint8_t *const *in,
-                     uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream, bool stable) {
+                     uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream, bool stable,
+                     int64_t *lbws, int lb_pass, int lb_bits) {
   const uint32_t nb = 1u << digit_bits;
   rows_pass_launch(PartDigit{keys, total_bits, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws, stream, 0,
-                   stable);
+                   stable, lbws, lb_pass, lb_bits);
 }
 
 void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_bits, const uint8_t *const *in,
                           uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream,
-                          uint64_t key_xor, uint64_t digit_flip) {
+                          uint64_t key_xor, uint64_t digit_flip, int64_t *lbws, int lb_pass, int lb_bits) {
   const uint32_t nb = 1u << digit_bits;
   rows_pass_launch(ImageDigit{keys, shift, nb - 1, digit_flip}, n, digit_bits, in, out, widths, ncols, ws, stream,
-                   key_xor);
+                   key_xor, true, lbws, lb_pass, lb_bits);
 }
 
 void radix_range_rows_pass(const int64_t *keys, int64_t n, uint64_t flip, uint64_t mn, int rshift, int shift,
                            int digit_bits, const uint8_t *const *in, uint8_t *const *out, const int *widths, int ncols,
-                           int64_t *ws, void *stream) {
+                           int64_t *ws, void *stream, int64_t *lbws, int lb_pass, int lb_bits) {
   const uint32_t nb = 1u << digit_bits;
   rows_pass_launch(RangeDigit{keys, flip, mn, rshift, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws,
-                   stream);
+                   stream, 0, true, lbws, lb_pass, lb_bits);
 }
 
 static int bits_for(uint32_t nparts) {

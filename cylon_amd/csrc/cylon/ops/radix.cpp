@@ -1,5 +1,6 @@
 // Shared radix partitioning driver for the LDS radix join and group-by
 // (kernels: radix_join.hip k_rp_hist / k_rows_pass / k_part_offsets).
+#include <algorithm>
 #include <cstdlib>
 
 #include "util.hpp"
@@ -84,11 +85,35 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
     return e ? std::max(1, std::min(10, std::atoi(e))) : 10;
   }();
   const int npass = (bits + max_db - 1) / max_db;
+  std::vector<int> shifts, dbits;
+  int lb_bits = 0;
+  for (int ps = 0, sh = 0; ps < npass; ++ps) {
+    const int db = (bits - sh + (npass - ps) - 1) / (npass - ps);
+    shifts.push_back(sh);
+    dbits.push_back(db);
+    lb_bits = std::max(lb_bits, db);
+    sh += db;
+  }
+  // chained-scan passes (kernels/radix_join.hip k_lb_hist): one read of the keys counts the
+  // digits of every pass instead of a histogram kernel before each pass
+  const bool lbm = npass >= 2 && n > 0 && hip::radix_lookback_enabled();
+  at::Tensor lbws;
+  if (lbm) {
+    lbws = ex.empty_i64(hip::radix_lb_workspace(n, lb_bits));
+    const int64_t *k0 = reinterpret_cast<const int64_t *>(cur[0].data_ptr());
+    if (range)
+      hip::radix_lb_prepare_range(k0, n, range->flip, range->mn, range->rshift, shifts.data(), dbits.data(), npass,
+                                  lb_bits, ptr<int64_t>(lbws), ex.stream);
+    else
+      hip::radix_lb_prepare_part(k0, n, bits, shifts.data(), dbits.data(), npass, lb_bits, ptr<int64_t>(lbws),
+                                 ex.stream);
+  }
+  int64_t *lbp = lbm ? ptr<int64_t>(lbws) : nullptr;
   int shift = 0;
   at::Tensor ws;
   for (int ps = 0; ps < npass; ++ps) {
-    const int db = (bits - shift + (npass - ps) - 1) / (npass - ps);
-    const int64_t wsn = hip::radix_rows_pass_workspace(n, db);
+    const int db = dbits[ps];
+    const int64_t wsn = lbm ? 1 : hip::radix_rows_pass_workspace(n, db);
     if (!ws.defined() || ws.numel() < wsn) ws = ex.empty_i64(wsn);
     std::vector<at::Tensor> nxt;
     std::vector<const uint8_t *> in;
@@ -102,11 +127,12 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
     if (range)
       hip::radix_range_rows_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, range->flip, range->mn,
                                  range->rshift, shift, db, in.data(), out.data(), pw.data(), (int)cur.size(),
-                                 ptr<int64_t>(ws), ex.stream);
+                                 ptr<int64_t>(ws), ex.stream, lbp, ps, lb_bits);
     else
       hip::radix_rows_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, bits, shift, db, in.data(),
                            out.data(), pw.data(), (int)cur.size(), ptr<int64_t>(ws), ex.stream,
-                           stable || ps > 0);  // LSD: every pass after the first keeps the order it receives
+                           stable || ps > 0,  // LSD: every pass after the first keeps the order it receives
+                           lbp, ps, lb_bits);
     cur = std::move(nxt);
     shift += db;
   }

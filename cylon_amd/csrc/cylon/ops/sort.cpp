@@ -181,11 +181,28 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
   if (diff != 0) {
     const int lo = __builtin_ctzll(diff), hi = 64 - __builtin_clzll(diff);
     const int npass = (hi - lo + 9) / 10;
-    at::Tensor ws;
+    std::vector<int> shifts, dbits;
+    int max_db = 0;
+    for (int ps = 0, sh = lo; ps < npass; ++ps) {
+      const int db = (hi - sh + (npass - ps) - 1) / (npass - ps);
+      shifts.push_back(sh);
+      dbits.push_back(db);
+      max_db = std::max(max_db, db);
+      sh += db;
+    }
+    // chained-scan passes: every pass's digit counts from one read of the keys (pass 0's input,
+    // imaged by the same flip as pass 0's digit) instead of a histogram kernel per pass
+    const bool lbm = npass >= 2 && hip::radix_lookback_enabled();
+    at::Tensor ws, lbws;
+    if (lbm) {
+      lbws = ex.empty_i64(hip::radix_lb_workspace(n, max_db));
+      hip::radix_lb_prepare_sort(ptr<int64_t>(cur[0]), n, raw_in ? key_xor : 0ull, shifts.data(), dbits.data(), npass,
+                                 max_db, ptr<int64_t>(lbws), ex.stream);
+    }
     int shift = lo;
     for (int ps = 0; ps < npass; ++ps) {
-      const int db = (hi - shift + (npass - ps) - 1) / (npass - ps);
-      const int64_t wsn = hip::radix_rows_pass_workspace(n, db);
+      const int db = dbits[ps];
+      const int64_t wsn = lbm ? 1 : hip::radix_rows_pass_workspace(n, db);
       if (!ws.defined() || ws.numel() < wsn) ws = ex.empty_i64(wsn);
       std::vector<at::Tensor> nxt;
       std::vector<const uint8_t *> in;
@@ -202,7 +219,8 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
       const uint64_t flip = ps == 0 && raw_in ? key_xor : 0ull;
       hip::radix_sort_rows_pass(ptr<int64_t>(cur[0]), n, shift, db, in.data(), out.data(), widths.data(),
                                 (int)cur.size(), ptr<int64_t>(ws), ex.stream,
-                                flip ^ (ps + 1 == npass && key_in_last_pass ? key_xor : 0ull), flip);
+                                flip ^ (ps + 1 == npass && key_in_last_pass ? key_xor : 0ull), flip,
+                                lbm ? ptr<int64_t>(lbws) : nullptr, ps, max_db);
       cur = std::move(nxt);
       shift += db;
     }

@@ -5,6 +5,7 @@ Host Arrow buffers are viewed zero-copy through numpy, moved to the context
 device in one H2D copy per buffer, and kept in the engine's layout:
 fixed width values, int64 string offsets, uint8 validity byte-mask.
 """
+import os
 from typing import Optional
 
 import numpy as np
@@ -113,14 +114,24 @@ def torch_dtype(dt: "C.DataType"):
     return _TORCH.get(dt.type, torch.uint8)
 
 
-def _unpack_bits(buf, offset: int, n: int) -> np.ndarray:
-    raw = np.frombuffer(buf, dtype=np.uint8)
-    bits = np.unpackbits(raw, bitorder="little")
-    return np.ascontiguousarray(bits[offset:offset + n])
+_STAGED_MIN_BYTES = 1 << 20
+
+
+def _staged_ingest() -> bool:
+    """CYLON_STAGED_INGEST=0 falls back to torch's pageable copy (A/B knob, tools/ingest_bench.py)."""
+    return os.environ.get("CYLON_STAGED_INGEST", "1") != "0"
 
 
 def _to_dev(a: np.ndarray, device: str) -> torch.Tensor:
-    t = torch.from_numpy(np.ascontiguousarray(a).copy() if not a.flags.writeable else np.ascontiguousarray(a))
+    """Host array -> tensor on `device`.  Device copies of >= 1 MiB go through the native pinned
+    staging ring (io/h2d.cpp: worker threads fill pinned chunks while the DMA engine drains
+    the previous ones; the device's current stream waits on the copy, the host does not)."""
+    a = np.ascontiguousarray(a)
+    if device != "cpu" and a.nbytes >= _STAGED_MIN_BYTES and _staged_ingest():
+        out = torch.empty(a.shape, dtype=torch.from_numpy(np.empty(0, a.dtype)).dtype, device=device)
+        C.h2d_copy(a.ctypes.data, a.nbytes, out)
+        return out
+    t = torch.from_numpy(a.copy() if not a.flags.writeable else a)
     return t.to(device, non_blocking=False) if device != "cpu" else t
 
 
@@ -174,9 +185,11 @@ def column_from_arrow(name: str, arr, device: str) -> "C.Column":
         if t == T.FIXED_SIZE_LIST:
             return C.Column(name, dt, n, _to_dev(data, device), None, validity)
         return C.Column(name, dt, n, _to_dev(data, device), _to_dev((eoffs - eoffs[0]) * w, device), validity)
-    if t == T.BOOL:
-        data = _unpack_bits(bufs[1], off, n) if n else np.zeros(0, np.uint8)
-        return C.Column(name, dt, n, _to_dev(data, device), None, validity)
+    if t == T.BOOL:  # the packed values cross (1/8 of the bytes) and are unpacked where they land
+        if not n:
+            return C.Column(name, dt, n, _to_dev(np.zeros(0, np.uint8), device), None, validity)
+        packed = _to_dev(np.frombuffer(bufs[1], dtype=np.uint8)[:(off + n + 7) // 8], device)
+        return C.Column(name, dt, n, C.unpack_validity(packed, off, n), None, validity)
     if t in (T.FIXED_SIZE_BINARY, T.DECIMAL):
         w = dt.byte_width
         data = np.frombuffer(bufs[1], dtype=np.uint8)[off * w:(off + n) * w]

@@ -110,6 +110,11 @@ class BaseIndex:
             labels = pa.array(values, type=self.get_index_array().type)
         except (pa.ArrowInvalid, pa.ArrowTypeError, TypeError, OverflowError):
             return self._positions_slow(values)
+        # a label the index type does not carry exactly (2.5 for an int index) matches nothing
+        conv = labels.to_pylist()
+        exact = [a == b or (a != a and b != b) for a, b in zip(conv, values)]
+        if not all(exact):
+            labels = pa.array([c if ok else None for c, ok in zip(conv, exact)], type=labels.type)
         col = ab.column_from_arrow("l", labels, self.device)
         nidx = self._persistent()
         if nidx is not None:
@@ -137,8 +142,10 @@ class _PersistentIndex(BaseIndex):
     """An index whose native structure (cylon/indexing/index.hpp) is built once, at
     construction (``set_index``), and reused by every lookup: Hash = sorted order images
     + an open-addressing table of the distinct values (one probe per label);
-    BinaryTree / BTree = the sorted images (binary search per label).  String indexes
-    fall back to the per-lookup join inside the native index."""
+    BinaryTree / BTree = the sorted images (binary search per label).  A string / binary
+    Hash index is persistent too (runs keyed by 64-bit hashes of the bytes, every candidate's
+    bytes verified against its label); string BinaryTree / BTree indexes use the per-lookup
+    join inside the native index."""
 
     def __init__(self, values, device: str = "cpu"):
         super().__init__(values, device)

@@ -173,6 +173,52 @@ def test_persistent_index_lookups(ctx, schema, kind):
     C.trace_enable(False)
 
 
+@pytest.mark.parametrize("kind", ["string", "nullable_string", "binary", "fixed_binary"])
+def test_persistent_string_hash_index(ctx, kind):
+    """A string / binary Hash index is built once (hash runs + byte verification on probe):
+    label order then row order, duplicates, misses, nulls never match, and 64-bit hash
+    collisions cannot merge distinct values (the probe compares bytes)."""
+    from cylon_amd._lib import C
+    from cylon_amd.indexing import IndexingSchema, build_index
+    rng = np.random.default_rng(4)
+    words = [f"w{int(x)}" for x in rng.integers(0, 300, 4000)]
+    if kind == "string":
+        arr = pa.array(words)
+    elif kind == "nullable_string":
+        arr = pa.array(words, mask=rng.random(4000) < 0.1)
+    elif kind == "binary":
+        arr = pa.array([w.encode() for w in words], pa.binary())
+    else:
+        arr = pa.array([w.encode().ljust(6, b"_") for w in words], pa.binary(6))
+    pyvals = arr.to_pylist()
+    C.trace_enable(True)
+    C.trace_reset()
+    idx = build_index(arr, IndexingSchema.HASH, ctx.device)
+    labels = [pyvals[3], "nope" if kind in ("string", "nullable_string") else b"nope__", pyvals[11], pyvals[3]]
+    labels = [l for l in labels if l is not None] or labels
+    for _ in range(3):
+        got = idx.positions_of_list(labels).tolist()
+    assert got == _loc_oracle(pyvals, labels)
+    assert idx.persistent_rows == sum(v is not None for v in pyvals)
+    assert dict(C.trace_counters()).get("index.built_rows", 0) == idx.persistent_rows
+    C.trace_enable(False)
+
+
+def test_index_labels_must_convert_exactly(ctx):
+    """A label that does not convert exactly to the index type matches nothing (2.5 is not 2)."""
+    from cylon_amd.indexing import IndexingSchema, build_index
+    arr = pa.array(np.array([1, 2, 3, 2, 127], dtype=np.int8))
+    for schema in ("HASH", "BTREE", "LINEAR"):
+        idx = build_index(arr, IndexingSchema[schema], ctx.device)
+        assert idx.positions_of_list([2.0]).tolist() == [1, 3]
+        assert idx.positions_of_list([2.5]).tolist() == []
+        assert idx.positions_of_list([383]).tolist() == []  # 383 = 127 mod 256
+    fidx = build_index(pa.array([0.5, 1.0, 2.0]), IndexingSchema.HASH, ctx.device)
+    assert fidx.positions_of_list([1]).tolist() == [1]
+    big = build_index(pa.array(np.array([2 ** 53], dtype=np.float64)), IndexingSchema.HASH, ctx.device)
+    assert big.positions_of_list([2 ** 53 + 1]).tolist() == []
+
+
 def test_native_loc_indexer_and_set_index(ctx):
     """C++ LocIndexer / ILocIndexer over a table whose index was set once (Set_Index)."""
     from cylon_amd._lib import C
