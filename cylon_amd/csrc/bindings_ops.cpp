@@ -73,6 +73,9 @@ void register_extended_ops(py::module &m) {
     return out;
   }, py::call_guard<py::gil_scoped_release>());
 
+  m.def("merge_sorted_runs", &ops::MergeSortedRuns, py::arg("runs"), py::arg("run_rows"), py::arg("col"),
+        py::arg("ascending") = true, rel);
+
   // ---- pinned, pipelined host -> device ingest (io/h2d.cpp); src = host address of nbytes
   m.def("h2d_copy", [](uintptr_t src, int64_t nbytes, at::Tensor dst, int threads) {
     CYLON_CHECK(dst.is_cuda() && dst.is_contiguous(), Code::Invalid, "h2d_copy: contiguous device tensor expected");

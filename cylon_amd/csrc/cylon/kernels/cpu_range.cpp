@@ -110,3 +110,20 @@ void splitter_partition(const uint64_t *const *images, const uint8_t *const *nul
 
 }  // namespace cpu
 }  // namespace cylon
+
+namespace cylon {
+namespace cpu {
+
+// CPU twin of merge.hip k_merge_pairs: stable merge, A first on ties
+void merge_sorted_pairs(const uint64_t *ak, const int64_t *ai, int64_t na, const uint64_t *bk, const int64_t *bi,
+                        int64_t nb, uint64_t *ok, int64_t *oi, void *) {
+  int64_t x = 0, y = 0, o = 0;
+  while (x < na || y < nb) {
+    const bool takea = x < na && (y >= nb || ak[x] <= bk[y]);
+    ok[o] = takea ? ak[x] : bk[y];
+    oi[o++] = takea ? ai[x++] : bi[y++];
+  }
+}
+
+}  // namespace cpu
+}  // namespace cylon

@@ -785,6 +785,65 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
   }
 }
 
+void RangeExchange(const TablePtr &t, const std::vector<int64_t> &bounds, int K,
+                   const std::function<void(int, int, const TablePtr &, const std::vector<int64_t> &)> &consume) {
+  auto ctx = t->GetContext();
+  const int W = ctx->GetWorldSize(), me = ctx->GetRank();
+  CYLON_CHECK(K >= 1 && (int64_t)bounds.size() == (int64_t)W * K + 1, Code::Invalid, "range exchange bounds");
+  for (const auto &c : t->columns())
+    CYLON_CHECK(!c.is_var(), Code::NotImplemented, "range exchange: fixed-width columns only");
+  const at::Device dev = t->device();
+  // descriptor: rows | nullable flag per column | rows per (destination, chunk)
+  std::vector<int64_t> desc{t->Rows()};
+  for (const auto &c : t->columns()) desc.push_back(c.nullable() ? 1 : 0);
+  for (int64_t i = 0; i < (int64_t)W * K; ++i) desc.push_back(bounds[i + 1] - bounds[i]);
+  const int64_t D = (int64_t)desc.size();
+  at::Tensor all;
+  {
+    CYLON_PHASE("shuffle.plan", dev);
+    all = ctx->GetCommunicator()->AllGather(at::tensor(desc, at::TensorOptions().dtype(at::kLong)).to(dev))
+              .to(at::kCPU)
+              .contiguous();
+  }
+  trace::add_counter("shuffle.plan_collectives", 1);
+  const int64_t *g = all.data_ptr<int64_t>();
+  const int nc = t->Columns();
+  std::vector<int64_t> nullable(nc, 0);
+  for (int r = 0; r < W; ++r)
+    for (int c = 0; c < nc; ++c) nullable[c] |= g[r * D + 1 + c];
+  auto cnt = [&](int from, int to, int k) { return g[(int64_t)from * D + 1 + nc + (int64_t)to * K + k]; };
+  std::vector<PendingTable> pend(K);
+  std::vector<std::vector<int64_t>> runs(K, std::vector<int64_t>(W));
+  {
+    CYLON_PHASE("shuffle.reorder+post", dev);
+    for (int k = 0; k < K; ++k) {
+      std::vector<int64_t> sc(W), rc(W);
+      std::vector<TablePtr> pieces;
+      for (int d = 0; d < W; ++d) {
+        sc[d] = cnt(me, d, k);
+        rc[d] = cnt(d, me, k);
+        runs[k][d] = rc[d];
+        pieces.push_back(Slice(t, bounds[(int64_t)d * K + k], sc[d]));
+      }
+      // K == 1: the destination ranges are already consecutive rows (no copy)
+      TablePtr send = K == 1 ? t : Merge(pieces);
+      pend[k] = AllToAllPost(send, sc, rc, nullable);
+      count_pending(pend[k]);
+    }
+  }
+  trace::add_counter("shuffle.chunks", K);
+  for (int k = 0; k < K; ++k) {
+    TablePtr got;
+    {
+      CYLON_PHASE("shuffle.wait", dev);
+      got = AllToAllFinish(pend[k]);
+    }
+    pend[k] = PendingTable();
+    trace::add_counter("shuffle.rows_out", got->Rows());
+    consume(k, K, got, runs[k]);
+  }
+}
+
 void ShufflePairPlanned(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,
                         const std::vector<int> &bcols,
                         const std::function<void(int, int, const TablePtr &, const TablePtr &)> &consume) {

@@ -132,6 +132,17 @@ void ShufflePairChunked(const TablePtr &a, const std::vector<int> &acols, const 
 void ShufflePairPlanned(const TablePtr &a, const std::vector<int> &acols, const TablePtr &b,
                         const std::vector<int> &bcols,
                         const std::function<void(int, int, const TablePtr &, const TablePtr &)> &consume);
+// Stable merge of consecutive sorted runs of `runs` (run_rows[r] rows each, in order) by column
+// `col` (pairwise merge-path rounds, kernels/merge.hip): the receive side of the pipelined sort.
+TablePtr MergeSortedRuns(const TablePtr &runs, const std::vector<int64_t> &run_rows, int col, bool asc);
+// Pipelined range exchange (distributed sort) of a table whose rows are ordered by destination
+// sub-range: bounds has W*K + 1 entries and rows [bounds[d*K + k], bounds[d*K + k + 1]) go to rank
+// d in chunk k.  One all-gather of (rows, nullability, sub-range counts) plans every chunk, all
+// chunks are posted at once (the communicator runs them in order) and consume(k, K, runs,
+// run_rows) receives chunk k -- the rows from every rank in rank order, run_rows[r] from rank r --
+// while the later chunks are still in flight.  Fixed-width columns only.
+void RangeExchange(const TablePtr &t, const std::vector<int64_t> &bounds, int K,
+                   const std::function<void(int, int, const TablePtr &, const std::vector<int64_t> &)> &consume);
 // single-table form (distributed group-by / unique): consume(k, K, t_k) per hash-disjoint chunk
 void ShufflePlanned(const TablePtr &t, const std::vector<int> &cols,
                     const std::function<void(int, int, const TablePtr &)> &consume);

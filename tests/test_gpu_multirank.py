@@ -230,25 +230,33 @@ def test_async_exchange_join_and_setops_on_device(chunks):
 def _dev_sort(ctx, case):
     import torch
     from cylon_amd import Table
+    from cylon_amd._lib import C
     rank = ctx.get_rank()
     g = torch.Generator(device="cuda").manual_seed(90 + rank)
     n = 200_000 + 30_000 * rank
-    if case == "wide":
+    if case == "wide_chunked":  # pipelined sort: 4 key sub-range chunks, merge-path merges on the device
+        ctx.add_config("sort_chunks", "4")
+    if case.startswith("wide"):
         k = torch.randint(-(1 << 62), 1 << 62, (n,), generator=g, device="cuda")
     else:  # one key everywhere
         k = torch.full((n,), 5, dtype=torch.int64, device="cuda")
     i = torch.arange(n, device="cuda") + 1_000_000 * rank
     t = Table.from_torch(ctx, {"k": k, "i": i})
-    s = t.distributed_sort("k", ascending=(case == "wide"))
-    return s.to_pandas(), t.to_pandas()
+    C.trace_enable(True)
+    C.trace_reset()
+    s = t.distributed_sort("k", ascending=case.startswith("wide"))
+    return s.to_pandas(), t.to_pandas(), dict(C.trace_counters())
 
 
-@pytest.mark.parametrize("case", ["wide", "one_key"])
+@pytest.mark.parametrize("case", ["wide", "wide_chunked", "one_key"])
 def test_distributed_sort_exact_splitters_on_device(case):
     res = run_distributed(_dev_sort, 2, case, device=DEV)
     allin = pd.concat([r[1] for r in res]).reset_index(drop=True)
     got = pd.concat([r[0] for r in res]).reset_index(drop=True)
-    exp = allin.sort_values("k", ascending=(case == "wide"), kind="mergesort").reset_index(drop=True)
+    for r in res:
+        assert r[2].get("sort.dist.pipelined", 0) == 1
+        assert r[2].get("shuffle.chunks", 0) == (4 if case == "wide_chunked" else 1)
+    exp = allin.sort_values("k", ascending=case.startswith("wide"), kind="mergesort").reset_index(drop=True)
     assert got["k"].tolist() == exp["k"].tolist() and got["i"].tolist() == exp["i"].tolist()
     loads = [len(r[0]) for r in res]
     assert max(loads) <= 1.5 * len(allin) / 2, loads

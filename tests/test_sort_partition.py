@@ -202,3 +202,60 @@ def test_verify_sort_config_cpu(ctx):
         ctx.add_config("verify_sort", "0")
         C.trace_enable(False)
     assert c.get("sort.verified", 0) == 2
+
+
+def _pipelined_sort_case(ctx, chunks, delay_us, asc):
+    from cylon_amd._lib import C
+    rank = ctx.get_rank()
+    if delay_us:
+        ctx._ctx.use_async_delay_transport(delay_us)
+    if chunks:
+        ctx.add_config("sort_chunks", str(chunks))
+    rng = np.random.default_rng(70 + rank)
+    n = 4000 + 700 * rank
+    a = rng.integers(-(1 << 40), 1 << 40, n, dtype=np.int64)
+    a[: n // 5] = 17  # a heavy tie: balance and stability come from the global row tie-break
+    df = pd.DataFrame({"a": a, "x": rng.standard_normal(n), "i": np.arange(n) + 100000 * rank})
+    C.trace_enable(True)
+    C.trace_reset()
+    s = Table.from_pandas(ctx, df).distributed_sort("a", ascending=asc)
+    return s.to_pandas(), df, dict(C.trace_counters())
+
+
+@pytest.mark.parametrize("world,chunks,delay_us,asc", [(3, 3, 0, True), (4, 1, 0, False), (2, 4, 300.0, True)])
+def test_pipelined_distributed_sort(world, chunks, delay_us, asc):
+    """Sort locally, split by exact (image, global row) splitters into contiguous ranges, exchange
+    K key sub-range chunks (one plan all-gather), merge each chunk's W sorted runs with the merge
+    path kernel: the result equals a stable sort of the rank-ordered concatenation, also over
+    the asynchronous delay transport (chunk k merges while chunk k+1 is in flight)."""
+    res = run_distributed(_pipelined_sort_case, world, chunks, delay_us, asc)
+    allin = pd.concat([r[1] for r in res]).reset_index(drop=True)
+    got = pd.concat([r[0] for r in res]).reset_index(drop=True)
+    exp = allin.sort_values("a", ascending=asc, kind="mergesort").reset_index(drop=True)
+    pd.testing.assert_frame_equal(got, exp, check_dtype=False)
+    for r in res:
+        c = r[2]
+        assert c.get("sort.dist.pipelined", 0) == 1
+        assert c.get("shuffle.chunks", 0) == chunks
+        assert c.get("shuffle.plan_collectives", 0) == 1
+        assert c.get("sort.dist.merge_rounds", 0) >= 1  # every chunk receives >= 2 non-empty runs here
+    loads = [len(r[0]) for r in res]
+    assert max(loads) <= 1.5 * len(allin) / world, loads
+
+
+@pytest.mark.parametrize("nruns", [1, 2, 3, 8])
+def test_merge_sorted_runs_stable(ctx, nruns):
+    """MergeSortedRuns (merge-path rounds) equals a stable sort of the concatenated runs:
+    equal keys keep run order, then row order; empty runs are skipped."""
+    from cylon_amd._lib import C
+    rng = np.random.default_rng(nruns)
+    sizes = [int(x) for x in rng.integers(0, 3000, nruns)]
+    if nruns > 2:
+        sizes[1] = 0
+    frames = [pd.DataFrame({"k": np.sort(rng.integers(-50, 50, s)), "src": np.full(s, r), "j": np.arange(s)})
+              for r, s in enumerate(sizes)]
+    allin = pd.concat(frames).reset_index(drop=True)
+    t = Table.from_pandas(ctx, allin)
+    got = t._wrap(C.merge_sorted_runs(t.native, sizes, 0, True)).to_pandas()
+    exp = allin.sort_values("k", kind="mergesort").reset_index(drop=True)
+    pd.testing.assert_frame_equal(got, exp, check_dtype=False)

@@ -44,27 +44,29 @@ def timed(fn, reps=3):
     return best * 1e3
 
 
-def sort_sim(W):
-    """Per-rank work of DistributedSort on W ranks: images + splitter partition + reorder (the
-    hash pid + partition-major reorder is the proxy: same scatter), the exchange of (W-1)/W of the
-    keys over W-1 links, then the local radix sort of the received rows (~rows/W)."""
+def sort_sim(W, K=4):
+    """Per-rank work of the pipelined DistributedSort on W ranks (ops/setops.cpp pipelined_sort):
+    the local radix sort of rows/W keys, the exchange of (W-1)/W of them over W-1 links in K key
+    sub-range chunks, and the merge of the W sorted runs each chunk brings (merge-path rounds).
+    Chunk k's merge overlaps chunk k+1's transfer, so the tail after the local sort is about
+    max(exchange, merge) + min(exchange, merge) / K instead of their sum."""
     n = rows // W
     g = torch.Generator(device="cuda").manual_seed(5)
     t = Table.from_torch(ctx, {"k": torch.randint(-(1 << 62), 1 << 62, (n,), generator=g, device="cuda")})
-
-    def part():
-        pid, _ = C.map_to_hash_partitions(t.native, [0], W)
-        return C.partition_reorder(t.native, pid, W)
-
-    tp = timed(part)
     ts = timed(lambda: t.sort("k"))
+    # what a rank receives: W sorted runs of ~n/W keys each (rank-ordered), merged into one
+    runs = [Table.from_torch(ctx, {"k": torch.sort(torch.randint(-(1 << 62), 1 << 62, (n // W,), generator=g,
+                                                                  device="cuda")).values}) for _ in range(W)]
+    got = Table.merge(runs)
+    tm = timed(lambda: C.merge_sorted_runs(got.native, [n // W] * W, 0, True))
     nbytes = n * 8 * (W - 1) / W
     txfer = nbytes / ((W - 1) * XGMI_GBPS * 1e9) * 1e3
-    est = tp + txfer + ts
-    print(f"SORT W={W} rows/rank={n}: partition {tp:.1f} ms, exchange {nbytes / 1e9:.2f} GB over {W - 1} links "
-          f"~{txfer:.1f} ms, local sort {ts:.1f} ms => estimate {est:.1f} ms ({rows / est * 1e3:.3g} rows/s/job)",
-          flush=True)
-    del t
+    serial = ts + txfer + tm
+    piped = ts + max(txfer, tm) + min(txfer, tm) / K
+    print(f"SORT W={W} rows/rank={n}: local sort {ts:.1f} ms, exchange {nbytes / 1e9:.2f} GB over {W - 1} links "
+          f"~{txfer:.1f} ms, merge of {W} runs {tm:.1f} ms => serial {serial:.1f} ms, pipelined (K={K}) "
+          f"{piped:.1f} ms ({rows / piped * 1e3:.3g} rows/s/job)", flush=True)
+    del t, runs, got
     torch.cuda.empty_cache()
 
 
