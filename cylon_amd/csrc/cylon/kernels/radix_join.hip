@@ -1420,7 +1420,8 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
                                                             int cap, const int64_t *__restrict__ out_offs, ColSet pc,
                                                             ColSet bs, BuildOut bo,
                                                             unsigned long long *__restrict__ cursor, int64_t out_cap,
-                                                            int *__restrict__ overflow) {
+                                                            int *__restrict__ overflow,
+                                                            unsigned long long *__restrict__ stamps) {
   // out_offs != nullptr: partition p's rows start at out_offs[p] (exact count kernel ran first).
   // out_offs == nullptr: fused count -- each partition claims its rows from *cursor with one
   // atomic after counting its matches (output partitions land in claim order); a claim past
@@ -1438,11 +1439,14 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
   uint16_t *perm = reinterpret_cast<uint16_t *>(area + 8 * (int64_t)cap);
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
+  int tix = -1;  // debug stamps (CYLON_RJ_STAMPS): block 0's partition count, RP_STAMP slots 0..5
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
     const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
     const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
     if (nr > cap && out_offs == nullptr && threadIdx.x == 0) atomicOr(overflow, 1);
     if (nr == 0 || nl == 0 || nr > cap) continue;
+    ++tix;
+    RP_STAMP(0);
     const int64_t obase = out_offs ? out_offs[p] : 0;
     // ---- phase A: probe rows of this wave's slice into VGkRJProbeRoundss (in flight during the build)
     const int64_t per = (nl + kRJWaves - 1) / kRJWaves;  // each wave owns a contiguous probe slice
@@ -1492,6 +1496,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
       }
     }
     __syncthreads();
+    RP_STAMP(1);
     uint32_t rk[kRJRowsPerThread];
 #pragma unroll
     for (int i = 0; i < kRJRowsPerThread; ++i)
@@ -1509,6 +1514,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
       }
     }
     __syncthreads();
+    RP_STAMP(2);
     // ---- phase C: count this wave's matches, slice offsets
     uint32_t c = 0;
 #pragma unroll
@@ -1533,6 +1539,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
       if (base < 0) continue;  // uniform: the block's claim did not fit
     }
     for (int w = 0; w < wave; ++w) base += wtot[w];
+    RP_STAMP(3);
     // ---- phase D: emit
     for (int u = 0; s0 + (int64_t)u * kWave < s1; ++u) {
       const int64_t l = s0 + (int64_t)u * kWave + lane;
@@ -1619,6 +1626,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
       }
       base += wsum;
     }
+    RP_STAMP(4);
   }
 }
 
@@ -1675,13 +1683,38 @@ void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t 
   hipStream_t s = as_stream(stream);
   // probe columns beyond 4 and staged build columns beyond 3 are loaded in place (slower, correct)
   unsigned long long *cur = reinterpret_cast<unsigned long long *>(cursor);
+  static const bool stamp = std::getenv("CYLON_RJ_STAMPS") != nullptr;  // debug: phase stamps to stderr
+  unsigned long long *st = nullptr;
+  if (stamp) {
+    HIP_CHECK(hipStreamSynchronize(s));
+    HIP_CHECK(hipMalloc(&st, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
+    HIP_CHECK(hipMemset(st, 0, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
+  }
   if (w8)
     hipLaunchKernelGGL((k_rj_write<4, 3, true>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys,
-                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow);
+                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st);
   else
     hipLaunchKernelGGL((k_rj_write<4, 3, false>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys,
-                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow);
+                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st);
   HIP_LAUNCH_CHECK();
+  if (st) {  // mean cycles per partition: load+stage, index build, count+claim, emit, then to the next
+    HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<unsigned long long> h(kRPStampTiles * kRPStampSlots);
+    HIP_CHECK(hipMemcpy(h.data(), st, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipFree(st));
+    double sum[5] = {0};
+    int np = 0;
+    for (int t = 1; t + 1 < kRPStampTiles; ++t) {
+      const unsigned long long *a = &h[t * kRPStampSlots], *b = &h[(t + 1) * kRPStampSlots];
+      if (b[0] == 0 || a[4] == 0) break;
+      for (int j = 1; j <= 4; ++j) sum[j - 1] += (double)(a[j] - a[j - 1]);
+      sum[4] += (double)(b[0] - a[0]);
+      ++np;
+    }
+    if (np)
+      std::fprintf(stderr, "rj_stamps partitions=%d total=%.0f | stage=%.0f index=%.0f count=%.0f emit=%.0f\n", np,
+                   sum[4] / np, sum[0] / np, sum[1] / np, sum[2] / np, sum[3] / np);
+  }
 }
 
 
