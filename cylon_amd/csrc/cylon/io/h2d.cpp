@@ -126,7 +126,7 @@ struct Ring {
   void *slot[kSlots] = {nullptr};
   hipEvent_t ev[kSlots] = {nullptr};
   bool used[kSlots] = {false};
-  hipEvent_t done = nullptr;
+  hipEvent_t done = nullptr, start = nullptr;
   hipStream_t stream = nullptr;
 };
 
@@ -159,10 +159,16 @@ void StagedH2D(const void *src, void *dst, size_t bytes, int device, int threads
       H2D_CHECK(hipEventCreateWithFlags(&r.ev[s], hipEventDisableTiming));
     }
     H2D_CHECK(hipEventCreateWithFlags(&r.done, hipEventDisableTiming));
+    H2D_CHECK(hipEventCreateWithFlags(&r.start, hipEventDisableTiming));
     H2D_CHECK(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
     r.ready = true;
   }
   const int parts = threads > 0 ? threads : pool().size() + 1;
+  // the DMAs are ordered after the work already queued on the consumer stream: a destination
+  // it is still filling or reading (a zero fill, memory the caching allocator just recycled)
+  const hipStream_t consumer = c10::hip::getCurrentHIPStream(device).stream();
+  H2D_CHECK(hipEventRecord(r.start, consumer));
+  H2D_CHECK(hipStreamWaitEvent(r.stream, r.start, 0));
   int64_t nchunks = 0;
   for (size_t off = 0; off < bytes; off += chunk, ++nchunks) {
     const int s = (int)(nchunks % kSlots);
@@ -175,7 +181,7 @@ void StagedH2D(const void *src, void *dst, size_t bytes, int device, int threads
   }
   // the consumer (the device's current stream) is ordered after the last DMA; the host is not
   H2D_CHECK(hipEventRecord(r.done, r.stream));
-  H2D_CHECK(hipStreamWaitEvent(c10::hip::getCurrentHIPStream(device).stream(), r.done, 0));
+  H2D_CHECK(hipStreamWaitEvent(consumer, r.done, 0));
   if (stats) {
     stats->bytes += (int64_t)bytes;
     stats->chunks += nchunks;

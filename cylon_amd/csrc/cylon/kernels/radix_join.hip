@@ -41,7 +41,7 @@ constexpr int kRPItems = 8;                      // rows per thread per tile
 constexpr int kRPTile = kRPThreads * kRPItems;   // 8192 rows
 constexpr int kRPMaxBuckets = 1024;
 constexpr int kRJMaxDigitBits = 10;
-constexpr int kRJRowArea = 155520;               // LDS bytes for the staged build rows (1 block per CU)
+constexpr int kRJRowArea = 154496;               // LDS bytes for the staged build rows (1 block per CU; 1 KB left for the emit owner map)
 constexpr int kRJMaxRows = 5120;                 // build rows per partition (5 per thread)
 constexpr int kRJThreads = 1024;
 constexpr int kRankBallot = 0, kRankBlockAtomic = 1, kRankWaveAtomic = 2;
@@ -1412,7 +1412,10 @@ struct BuildOut {               // build-side output columns
   int n;
 };
 
-template <int MAXP, int MAXB, bool W8>
+// OM: emit finds each output slot's probe lane through a per-wave LDS owner map (lanes write
+// their lane id into the slots of their matches) instead of a 6-step binary search over the
+// wave's match scan with cross-lane permutes (CYLON_RJ_OWNERMAP=1 selects it; A/B knob).
+template <int MAXP, int MAXB, bool W8, bool OM>
 __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__restrict__ pkeys,
                                                             const int64_t *__restrict__ poffs,
                                                             const int64_t *__restrict__ bkeys,
@@ -1435,6 +1438,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
   __shared__ __attribute__((aligned(16))) uint8_t area[kRJRowArea];
   __shared__ uint32_t wtot[kRJWaves];
   __shared__ int64_t sclaim;
+  __shared__ uint8_t ownmap[OM ? kRJWaves * kWave : 1];
   int64_t *skeys = reinterpret_cast<int64_t *>(area);
   uint16_t *perm = reinterpret_cast<uint16_t *>(area + 8 * (int64_t)cap);
   const int lane = lane_id();
@@ -1585,10 +1589,19 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
         const uint32_t so = t0 + lane;
         const bool act = so < wsum;
         int owner = 0;
+        if (OM) {
+          uint8_t *om = ownmap + wave * kWave;
+          const uint32_t e0 = excl > t0 ? excl : t0, e1 = excl + mc < t0 + kWave ? excl + mc : t0 + kWave;
+          __builtin_amdgcn_wave_barrier();  // the previous window's reads are done
+          for (uint32_t x = e0; x < e1; ++x) om[x - t0] = (uint8_t)lane;
+          __builtin_amdgcn_wave_barrier();
+          owner = act ? om[lane] : 0;
+        } else {
 #pragma unroll
-        for (int step = kWave / 2; step >= 1; step >>= 1) {
-          const uint32_t ic = __shfl(inc, owner + step - 1, kWave);
-          if (ic <= so) owner += step;
+          for (int step = kWave / 2; step >= 1; step >>= 1) {
+            const uint32_t ic = __shfl(inc, owner + step - 1, kWave);
+            if (ic <= so) owner += step;
+          }
         }
         const uint32_t j = so - __shfl(excl, owner, kWave);  // match rank inside the owner's bucket
         const int64_t ko = rj_shfl64(k, owner);
@@ -1690,12 +1703,17 @@ void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t 
     HIP_CHECK(hipMalloc(&st, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
     HIP_CHECK(hipMemset(st, 0, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
   }
-  if (w8)
-    hipLaunchKernelGGL((k_rj_write<4, 3, true>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys,
-                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st);
+  const char *om = std::getenv("CYLON_RJ_OWNERMAP");
+  const bool ownermap = om && om[0] == '1';
+  if (w8 && ownermap)
+    hipLaunchKernelGGL((k_rj_write<4, 3, true, true>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs,
+                       bkeys, boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st);
+  else if (w8)
+    hipLaunchKernelGGL((k_rj_write<4, 3, true, false>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs,
+                       bkeys, boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st);
   else
-    hipLaunchKernelGGL((k_rj_write<4, 3, false>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs, bkeys,
-                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st);
+    hipLaunchKernelGGL((k_rj_write<4, 3, false, false>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs,
+                       bkeys, boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st);
   HIP_LAUNCH_CHECK();
   if (st) {  // mean cycles per partition: load+stage, index build, count+claim, emit, then to the next
     HIP_CHECK(hipStreamSynchronize(s));

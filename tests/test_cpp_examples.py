@@ -212,6 +212,87 @@ def _check_examples(device, data_dir):
     assert got["loc_range"] == it.loc[labels[1]:labels[2]].row_count
 
 
+def _gen(seed, n, rng):
+    import pandas as pd
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    k = torch.randint(rng, (n,), generator=g, dtype=torch.long)
+    v = torch.rand(n, generator=g, dtype=torch.float64)
+    return pd.DataFrame({"k": k.numpy(), "v": v.numpy()})
+
+
+def _check_more_examples(device, data_dir):
+    """join (4 types x hash/sort + multi-index), scalar aggregates, in-memory datagen."""
+    import numpy as np
+    import pandas as pd
+    from cylon_amd import CylonContext
+    from cylon_amd.io import read_csv
+    ctx = CylonContext(device="cpu")
+    c1, c2 = (os.path.join(data_dir, "input", f) for f in ("csv1_0.csv", "csv2_0.csv"))
+    a, b = read_csv(ctx, c1).to_pandas(), read_csv(ctx, c2).to_pandas()
+    got = _run_example("join_example", device, c1, c2)
+    ka, kb = a.columns[0], b.columns[0]
+    for name, how in (("inner", "inner"), ("left", "left"), ("right", "right"), ("outer", "outer")):
+        want = len(a.merge(b, left_on=ka, right_on=kb, how=how))
+        assert got[f"{name}_hash"] == got[f"{name}_sort"] == want, (name, got)
+        assert got[f"{name}_algorithms_agree"] == 1
+    assert got["inner_multi_idx"] == len(a.merge(b, left_on=list(a.columns[:2]), right_on=list(b.columns[:2])))
+
+    got = _run_example("compute_example", device, c1)
+    assert got["rows"] == len(a)
+    for c, col in enumerate(a.columns):
+        if not np.issubdtype(a[col].dtype, np.number):
+            continue
+        assert got[f"col{c}_sum_x1000"] == int(round(a[col].sum() * 1000)), col
+        assert got[f"col{c}_count"] == int(a[col].count())
+        assert got[f"col{c}_min_x1000"] == int(round(a[col].min() * 1000))
+        assert got[f"col{c}_max_x1000"] == int(round(a[col].max() * 1000))
+        assert got[f"col{c}_minmax_consistent"] == 1
+
+    n = 20000
+    got = _run_example("datagen_join_example", device, str(n))
+    l, r = _gen(1000, n, 4 * n), _gen(1001, n, 4 * n)
+    assert got["join_rows"] == len(l.merge(r, on="k"))
+    assert got["union_rows"] == len(set(l.k) | set(r.k)) and got["intersect_rows"] == len(set(l.k) & set(r.k))
+    assert got["sorted_rows"] == n and got["sorted_ok"] == 1
+
+
+def test_cpp_more_examples_on_cpu(data_dir):
+    _check_more_examples("cpu", data_dir)
+
+
+@pytest.mark.gpu
+def test_cpp_more_examples_on_gpu(data_dir):
+    _check_more_examples("cuda:0", data_dir)
+
+
+def test_cpp_datagen_example_distributed_tcp():
+    """datagen_join_example as 3 native TCP ranks: per-rank results sum to the pandas totals."""
+    import socket
+    _ensure_built()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    n, W = 5000, 3
+    exe = os.path.join(ROOT, "examples", "cpp", "bin", "datagen_join_example")
+    procs = []
+    for r in range(W):
+        env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC")}
+        env.update(RANK=str(r), WORLD_SIZE=str(W), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([exe, "tcp", str(n)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                                      env=env))
+    res = [p.communicate(timeout=180) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [e[-1500:] for _, e in res]
+    outs = [dict((k, int(v)) for k, v in (line.split() for line in o.splitlines())) for o, _ in res]
+    import pandas as pd
+    L = pd.concat([_gen(1000 + 2 * r, n, 4 * n) for r in range(W)])
+    R = pd.concat([_gen(1001 + 2 * r, n, 4 * n) for r in range(W)])
+    assert sum(o["join_rows"] for o in outs) == len(L.merge(R, on="k"))
+    assert sum(o["union_rows"] for o in outs) == len(set(L.k) | set(R.k))
+    assert sum(o["intersect_rows"] for o in outs) == len(set(L.k) & set(R.k))
+    assert sum(o["sorted_rows"] for o in outs) == W * n and all(o["sorted_ok"] == 1 for o in outs)
+
+
 def test_cpp_reference_examples_on_cpu(data_dir):
     _check_examples("cpu", data_dir)
 

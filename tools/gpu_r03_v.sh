@@ -13,4 +13,7 @@ timeout -k 10 500 python tools/bench_suite.py --configs 2,4,5,6,7 --reps 3 > $O/
 timeout -k 10 300 python tools/rank_sim.py --sort 2000000000 2 4 8 > $O/rank_sim_sort.txt 2> $O/rank_sim_sort.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o join -- python3 bench.py --steps 1 --warmup 1 --no-phases > $O/prof.log 2>&1
 CYLON_RJ_STAMPS=1 timeout -k 10 200 python bench.py --steps 1 --warmup 1 --no-phases > $O/rj_stamps.json 2> $O/rj_stamps.err
+CYLON_RJ_OWNERMAP=1 CYLON_RJ_STAMPS=1 timeout -k 10 200 python bench.py --steps 1 --warmup 1 --no-phases > $O/rj_stamps_om.json 2> $O/rj_stamps_om.err
+CYLON_RJ_OWNERMAP=1 timeout -k 10 200 python bench.py --steps 20 --warmup 3 --verify > $O/bench_om.json 2> $O/bench_om.err
+timeout -k 10 200 python bench.py --steps 20 --warmup 3 > $O/bench_3.json 2> $O/bench_3.err
 echo done
