@@ -320,6 +320,7 @@ PYBIND11_MODULE(_C, m) {
   auto rel = py::call_guard<py::gil_scoped_release>();
   m.def("gather", &ops::Gather, rel);
   m.def("gather_nullable", &ops::GatherNullable, rel);
+  m.def("select_var", &ops::SelectVar, py::arg("a"), py::arg("b"), py::arg("cond"), rel);
   m.def("project", &ops::Project, rel);
   m.def("merge", &ops::Merge, rel);
   m.def("slice", &ops::Slice, rel);

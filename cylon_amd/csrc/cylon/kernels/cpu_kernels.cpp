@@ -185,6 +185,32 @@ void gather_columns(const ColView *in, const MutColView *out, int ncols, const i
   }
 }
 
+void select_var_lengths(const ColView &a, const ColView &b, int b_bcast, const uint8_t *cond, int64_t n,
+                        int64_t *out_lens, void *) {
+  for (int64_t i = 0; i < n; ++i) {
+    const bool from_a = cond == nullptr || cond[i] != 0;
+    const ColView &s = from_a ? a : b;
+    const int64_t j = from_a || !b_bcast ? i : 0;
+    out_lens[i] = s.offsets ? s.offsets[j + 1] - s.offsets[j] : 0;
+  }
+}
+
+void select_var_bytes(const ColView &a, const ColView &b, int b_bcast, const uint8_t *cond, int64_t n,
+                      const int64_t *out_off, uint8_t *out_bytes, uint8_t *out_valid, void *) {
+  for (int64_t i = 0; i < n; ++i) {
+    const bool from_a = cond == nullptr || cond[i] != 0;
+    const ColView &s = from_a ? a : b;
+    const int64_t j = from_a || !b_bcast ? i : 0;
+    uint8_t valid = 0;
+    if (s.offsets) {
+      const int64_t sb = s.offsets[j], len = s.offsets[j + 1] - sb;
+      if (len) std::memcpy(out_bytes + out_off[i], s.data + sb, len);
+      valid = s.valid ? s.valid[j] : 1;
+    }
+    if (out_valid) out_valid[i] = valid;
+  }
+}
+
 void gather_var_lengths(const ColView &in, const int64_t *idx, int64_t m, int64_t *out_lens, void *) {
   for (int64_t j = 0; j < m; ++j) {
     const int64_t s = idx[j];

@@ -24,6 +24,7 @@
 // Partitions whose build side exceeds the LDS capacity are reported; the
 // caller then falls back to the global-table join.
 #include <atomic>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -64,6 +65,12 @@ __device__ __forceinline__ uint32_t part_of(int64_t key, int bits) {
   return bits == 0 ? 0u : (uint32_t)(hashing::fmix64((uint64_t)key) >> (64 - bits));
 }
 
+__device__ __forceinline__ long long rj_shfl_xor64(long long x, int mask) {
+  const uint32_t lo = __shfl_xor((uint32_t)(uint64_t)x, mask, kWave);
+  const uint32_t hi = __shfl_xor((uint32_t)((uint64_t)x >> 32), mask, kWave);
+  return (long long)(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ uint64_t ld_elem(const uint8_t *src, int64_t i, int w) {
   switch (w) {
     case 1: return src[i];
@@ -98,14 +105,25 @@ __device__ __forceinline__ void stw(uint8_t *p, int64_t i, int w, uint64_t v) {
 // --------------------------------------------------------------------------
 // partition pass
 // --------------------------------------------------------------------------
-struct PartDigit {
-  const int64_t *keys;
+// NARROW (narrow-key join, join.cpp radix_join): the two relations' keys span < 2^32 values, so
+// a key's low 32 bits identify it; the partition hash is taken over those bits and column 0
+// (the key) leaves the pass as uint32 -- 4 B/row less in every later pass and in the join
+// kernels.  K = int64_t: the first pass reads the original keys; K = uint32_t: later passes.
+template <class K, bool NARROW>
+struct PartDigitT {
+  static constexpr bool kNarrow = NARROW;  // column 0 is stored as uint32
+  const K *keys;
   int bits;   // total partition bits
   int shift;  // digit = (part >> shift) & mask
   uint32_t mask;
-  __device__ __forceinline__ uint32_t of_key(int64_t k) const { return (part_of(k, bits) >> shift) & mask; }
-  __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key(keys[i]); }
+  __device__ __forceinline__ uint32_t of_key(int64_t k) const {
+    return (part_of(NARROW ? (int64_t)(uint32_t)(uint64_t)k : k, bits) >> shift) & mask;
+  }
+  __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key((int64_t)keys[i]); }
 };
+using PartDigit = PartDigitT<int64_t, false>;
+using PartDigitN64 = PartDigitT<int64_t, true>;   // first narrow pass: int64 keys in, uint32 out
+using PartDigitN32 = PartDigitT<uint32_t, true>;  // later narrow passes
 
 
 // Shuffle digit: the reference's partition of a single 8-byte integer key
@@ -113,6 +131,7 @@ struct PartDigit {
 // of two; partition.hip partition_f + hashing::partitioner), so one LDS-staged
 // pass produces the partition-major order of the whole table.
 struct ModDigit {
+  static constexpr bool kNarrow = false;
   const int64_t *keys;
   uint32_t nparts;
   __device__ __forceinline__ uint32_t of_key(int64_t k) const {
@@ -123,6 +142,7 @@ struct ModDigit {
 
 // Sort digit: bits [shift, shift + log2(mask+1)) of an order-preserving uint64 image (K6).
 struct ImageDigit {
+  static constexpr bool kNarrow = false;
   const int64_t *keys;
   int shift;
   uint32_t mask;
@@ -137,6 +157,7 @@ struct ImageDigit {
 // ((k ^ flip) - mn) >> rshift -- key ranges in key order -- and a pass's digit is
 // bits [shift, shift + log2(mask + 1)) of that partition id.
 struct RangeDigit {
+  static constexpr bool kNarrow = false;
   const int64_t *keys;
   uint64_t flip, mn;
   int rshift, shift;
@@ -166,6 +187,46 @@ __global__ __launch_bounds__(kRPThreads) void k_rp_hist(Digit digit, int64_t n, 
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       if (d[u] != 0xffffffffu) atomicAdd(&hist[d[u]], 1u);
+  }
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) bh[(int64_t)p * nblocks + blockIdx.x] = hist[p];
+}
+
+// k_rp_hist of a narrow-key join's first pass (low-32-bit digit) that also reduces the int64
+// keys' min and max into mm[0] / mm[1] (atomics, initialised by the caller): the join decides
+// from both relations' ranges whether the narrow passes apply, before the first pass runs.
+__global__ __launch_bounds__(kRPThreads) void k_rp_hist_minmax(PartDigitN64 digit, int64_t n, uint32_t nbuckets,
+                                                               int64_t rows_per_block, int64_t nblocks,
+                                                               int64_t *__restrict__ bh, long long *__restrict__ mm) {
+  __shared__ unsigned int hist[kRPMaxBuckets];
+  for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) hist[p] = 0;
+  __syncthreads();
+  const int64_t begin = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t end = (begin + rows_per_block < n) ? begin + rows_per_block : n;
+  long long lo = LLONG_MAX, hi = LLONG_MIN;
+  for (int64_t i0 = begin; i0 < end; i0 += 4 * kRPThreads) {
+    int64_t k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * kRPThreads + threadIdx.x;
+      k[u] = i < end ? digit.keys[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i0 + u * kRPThreads + threadIdx.x < end) {
+        atomicAdd(&hist[digit.of_key(k[u])], 1u);
+        lo = k[u] < lo ? k[u] : lo;
+        hi = k[u] > hi ? k[u] : hi;
+      }
+  }
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    const long long a = rj_shfl_xor64(lo, d), b = rj_shfl_xor64(hi, d);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  if (lane_id() == 0 && lo <= hi) {
+    atomicMin(&mm[0], lo);
+    atomicMax(&mm[1], hi);
   }
   __syncthreads();
   for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) bh[(int64_t)p * nblocks + blockIdx.x] = hist[p];
@@ -340,6 +401,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   constexpr int WAVES = THREADS / kWave;
   constexpr int TILE = THREADS * kRPItems;
   constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;  // buckets per thread in the offset scan
+  constexpr bool K4 = Digit::kNarrow;  // column 0 (the key) is stored as uint32
   static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 4 <= TILE * 8, "ranking scratch must fit the stage");
   static_assert(!LB || (THREADS >= kRPMaxBuckets && TILE == kRPTile), "lookback: one bucket a thread, 8192-row tiles");
   __shared__ int64_t running[kRPMaxBuckets];
@@ -504,9 +566,16 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       uint8_t *out = cols.out[c];
       const uint64_t x = c == 0 ? cols.key_xor : 0ull;
       if (LB && c + 1 == cols.n && threadIdx.x == 0) s_next = (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
+      const bool k4 = K4 && c == 0;  // narrow key: column 0 leaves as its low 32 bits
+      if (k4) {
 #pragma unroll
-      for (int k = 0; k < kRPItems; ++k)
-        if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
+        for (int k = 0; k < kRPItems; ++k)
+          if (pl[k] != 0xffffffffu) reinterpret_cast<uint32_t *>(st)[pl[k]] = (uint32_t)v[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < kRPItems; ++k)
+          if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
+      }
       __syncthreads();
       if (LB && c + 1 == cols.n) next = s_next;
       RP_STAMP(6 + 2 * c);
@@ -528,10 +597,18 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
           if (i < end) kv[k] = (uint64_t)digit.keys[i];
         }
       }
+      if (k4) {
 #pragma unroll
-      for (int q = 0; q < kRPItems; ++q) {
-        const int j = threadIdx.x + q * THREADS;
-        if (j < cnt) stw<W8>(out, dst[q], w, ldw<W8>(st, j, w));
+        for (int q = 0; q < kRPItems; ++q) {
+          const int j = threadIdx.x + q * THREADS;
+          if (j < cnt) reinterpret_cast<uint32_t *>(out)[dst[q]] = reinterpret_cast<const uint32_t *>(st)[j];
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < kRPItems; ++q) {
+          const int j = threadIdx.x + q * THREADS;
+          if (j < cnt) stw<W8>(out, dst[q], w, ldw<W8>(st, j, w));
+        }
       }
       __syncthreads();
       RP_STAMP(7 + 2 * c);
@@ -1052,6 +1129,7 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
   CYLON_CHECK(in[0] == reinterpret_cast<const uint8_t *>(dg.keys) && widths[0] == 8, Code::Invalid,
               "radix pass: column 0 must be the key");
+  static_assert(!Digit::kNarrow, "narrow-key passes launch through narrow_pass_launch");
   // key_xor rebuilds int64 keys from order images: only a sort's image digit may set it
   // (partition / mod / range digits store column 0 as read)
   CYLON_CHECK((key_xor == 0 || std::is_same<Digit, ImageDigit>::value), Code::Invalid,
@@ -1148,6 +1226,84 @@ void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, 
                    stable, lbws, lb_pass, lb_bits);
 }
 
+// ---- narrow-key join passes: the one-block-per-CU kernel (8192-row tiles, next-column prefetch)
+// for every column count; the first pass (int64 keys in, block-atomic ranking) may take its
+// scanned histogram from radix_narrow_prehist, later passes (uint32 keys) rank stably.
+static RPGeometry narrow_geometry(int64_t n) { return rp_geometry(n, 1024, 1); }
+
+void radix_narrow_prehist(const int64_t *keys, int64_t n, int total_bits, int digit_bits, int64_t *ws, int64_t *mm,
+                          void *stream) {
+  CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
+  hipStream_t s = as_stream(stream);
+  if (n == 0) return;
+  const RPGeometry g = narrow_geometry(n);
+  const uint32_t nb = 1u << digit_bits;
+  const int64_t m = g.nblocks * (int64_t)nb;
+  hipLaunchKernelGGL(k_rp_hist_minmax, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s,
+                     PartDigitN64{keys, total_bits, 0, nb - 1}, n, nb, g.rows_per_block, g.nblocks, ws,
+                     reinterpret_cast<long long *>(mm));
+  HIP_LAUNCH_CHECK();
+  exclusive_scan(ws, m, ws + m, ws + 2 * m + 1, stream);
+}
+
+template <class Digit>
+static void narrow_pass_launch(const Digit &dg, int64_t n, int digit_bits, const uint8_t *const *in,
+                               uint8_t *const *out, const int *widths, int ncols, int64_t *ws, hipStream_t s,
+                               bool stable, bool prescanned) {
+  static_assert(Digit::kNarrow, "narrow digits only");
+  if (n == 0) return;
+  CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
+  CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
+  CYLON_CHECK(in[0] == reinterpret_cast<const uint8_t *>(dg.keys) && widths[0] == 4, Code::Invalid,
+              "narrow radix pass: column 0 must be the key, stored as uint32");
+  const bool want_stable = stable;
+  const char *dbg = std::getenv("CYLON_RP_DEBUG_UNSTABLE");  // ranking-guard test knob (rows_pass_launch)
+  if (dbg && dbg[0] == '1') stable = false;
+  const RPGeometry g = narrow_geometry(n);
+  const uint32_t nb = 1u << digit_bits;
+  const int64_t m = g.nblocks * (int64_t)nb;
+  if (!prescanned) {
+    hipLaunchKernelGGL(k_rp_hist<Digit>, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, n, nb,
+                       g.rows_per_block, g.nblocks, ws);
+    HIP_LAUNCH_CHECK();
+    exclusive_scan(ws, m, ws + m, ws + 2 * m + 1, reinterpret_cast<void *>(s));
+  }
+  ColSet cs;
+  cs.n = ncols;
+  cs.key_xor = 0;
+  const char *gd = std::getenv("CYLON_RP_GUARD");
+  cs.check_order = want_stable && !(gd && gd[0] == '0') ? 1 : 0;
+  cs.order_bad = order_flag();
+  bool w8 = true;
+  for (int c = 0; c < kMaxFusedCols; ++c) {
+    cs.in[c] = c < ncols ? in[c] : nullptr;
+    cs.out[c] = c < ncols ? out[c] : nullptr;
+    cs.width[c] = c < ncols ? widths[c] : 8;
+    if (c > 0 && c < ncols) {
+      w8 &= widths[c] == 8;
+      CYLON_CHECK(in[c] != nullptr, Code::Invalid, "narrow radix pass: no generated columns");
+    }
+  }
+  if (!stable) rows_pass_kernel<Digit, 1024, kRankBlockAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, ws + m);
+  else if (rp_wave_atomic(s)) rows_pass_kernel<Digit, 1024, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, ws + m);
+  else rows_pass_kernel<Digit, 1024, kRankBallot>(w8, g, s, dg, digit_bits, nb, cs, n, ws + m);
+  HIP_LAUNCH_CHECK();
+}
+
+void radix_narrow_rows_pass(const void *keys, int key_bytes, int64_t n, int total_bits, int shift, int digit_bits,
+                            const uint8_t *const *in, uint8_t *const *out, const int *widths, int ncols, int64_t *ws,
+                            void *stream, bool stable, bool prescanned) {
+  CYLON_CHECK(key_bytes == 8 || key_bytes == 4, Code::Invalid, "narrow radix pass: key bytes " << key_bytes);
+  const uint32_t nb = 1u << digit_bits;
+  hipStream_t s = as_stream(stream);
+  if (key_bytes == 8)
+    narrow_pass_launch(PartDigitN64{reinterpret_cast<const int64_t *>(keys), total_bits, shift, nb - 1}, n, digit_bits,
+                       in, out, widths, ncols, ws, s, stable, prescanned);
+  else
+    narrow_pass_launch(PartDigitN32{reinterpret_cast<const uint32_t *>(keys), total_bits, shift, nb - 1}, n,
+                       digit_bits, in, out, widths, ncols, ws, s, stable, prescanned);
+}
+
 void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_bits, const uint8_t *const *in,
                           uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream,
                           uint64_t key_xor, uint64_t digit_flip, int64_t *lbws, int lb_pass, int lb_bits) {
@@ -1223,6 +1379,27 @@ void radix_part_offsets(const int64_t *keys, int64_t n, int bits, int64_t *offs,
   HIP_LAUNCH_CHECK();
 }
 
+// same over narrow-key partitions (uint32 keys, partition hash of the low 32 bits)
+__global__ void k_part_offsets_u32(const uint32_t *__restrict__ keys, int64_t n, int bits, int64_t nparts,
+                                   int64_t *__restrict__ offs) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= nparts; p += stride) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)part_of((int64_t)keys[mid], bits) < p) lo = mid + 1; else hi = mid;
+    }
+    offs[p] = lo;
+  }
+}
+
+void radix_narrow_part_offsets(const uint32_t *keys, int64_t n, int bits, int64_t *offs, void *stream) {
+  const int64_t np = int64_t(1) << bits;
+  hipLaunchKernelGGL(k_part_offsets_u32, dim3(grid_for(np + 1)), dim3(kBlock), 0, as_stream(stream), keys, n, bits,
+                     np, offs);
+  HIP_LAUNCH_CHECK();
+}
+
 __global__ void k_range_part_offsets(const int64_t *__restrict__ keys, int64_t n, uint64_t flip, uint64_t mn,
                                      int rshift, int64_t nparts, int64_t *__restrict__ offs) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -1259,8 +1436,8 @@ constexpr int kRJBuckets = 4096;
 // Build rows per partition that fit the LDS row area: key (8 B) + permutation
 // (2 B) + the staged build columns (widths w[q]; in[q] == nullptr marks the key
 // column itself, which is not staged twice).
-int64_t radix_join_capacity(const int *widths, const uint8_t *const *in, int n) {
-  int64_t row = 8 + 2;
+int64_t radix_join_capacity(const int *widths, const uint8_t *const *in, int n, int key_bytes) {
+  int64_t row = key_bytes + 2;
   for (int q = 0; q < n; ++q)
     if (in[q]) row += widths[q];
   int64_t cap = kRJRowArea / row;
@@ -1271,6 +1448,17 @@ int64_t radix_join_capacity(const int *widths, const uint8_t *const *in, int n) 
 __device__ __forceinline__ uint32_t rj_bucket(int64_t k) {
   return (uint32_t)hashing::fmix64((uint64_t)k) & (kRJBuckets - 1);
 }
+// narrow keys (low 32 bits): bucket from fmix32, independent of the partition's fmix64 bits
+__device__ __forceinline__ uint32_t rj_bucket(uint32_t k) { return hashing::fmix32(k) & (kRJBuckets - 1); }
+
+// output value of a join key: int64 keys as they are; narrow keys rebuilt from their low 32 bits
+// and the relations' minimum (every key lies in [kmin, kmin + 2^32))
+__device__ __forceinline__ int64_t rj_widen(int64_t k, int64_t) { return k; }
+__device__ __forceinline__ int64_t rj_widen(uint32_t k, int64_t kmin) {
+  return kmin + (int64_t)(uint32_t)(k - (uint32_t)(uint64_t)kmin);
+}
+__device__ __forceinline__ int64_t rj_shfl_key(int64_t x, int src);
+__device__ __forceinline__ uint32_t rj_shfl_key(uint32_t x, int src) { return __shfl(x, src, kWave); }
 
 // Build rows of one partition: thread t owns rows t + i * kRJThreads (cap <= kRJMaxRows).
 constexpr int kRJRowsPerThread = kRJMaxRows / kRJThreads;
@@ -1313,7 +1501,8 @@ __device__ __forceinline__ uint32_t rj_claim(uint16_t *bst, uint32_t b) {
   return (old >> sh) & 0xffffu;
 }
 
-__device__ __forceinline__ uint32_t rj_count(const uint16_t *bst, const int64_t *skeys, int64_t k) {
+template <class KT>
+__device__ __forceinline__ uint32_t rj_count(const uint16_t *bst, const KT *skeys, KT k) {
   const uint32_t b = rj_bucket(k);
   uint32_t c = 0;
   for (uint32_t i = bst[b], e = bst[b + 1]; i < e; ++i) c += (skeys[i] == k);
@@ -1328,15 +1517,16 @@ constexpr int kRCWaves = kRCThreads / kWave;
 constexpr int kRCRowsPerThread = kRJMaxRows / kRCThreads;
 static_assert(kRCRowsPerThread * kRCThreads == kRJMaxRows, "count rows per thread");
 
-__global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_rj_count(const int64_t *__restrict__ pkeys,
+template <class KT>
+__global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_rj_count(const KT *__restrict__ pkeys,
                                                       const int64_t *__restrict__ poffs,
-                                                      const int64_t *__restrict__ bkeys,
+                                                      const KT *__restrict__ bkeys,
                                                       const int64_t *__restrict__ boffs, int64_t nparts, int cap,
                                                       int64_t pstride, int64_t *__restrict__ counts, int *overflow) {
   // pstride > 1: only partitions 0, pstride, 2 pstride, ... are counted, into counts[p / pstride]
   // (the sampled output-size estimate of the fused write path)
   __shared__ __attribute__((aligned(16))) uint16_t bst[kRJBuckets + 8];
-  __shared__ int64_t skeys[kRJMaxRows];
+  __shared__ KT skeys[kRJMaxRows];
   __shared__ uint32_t wsum[kRCWaves];
   __shared__ unsigned long long csum[kRCWaves];
   const int64_t nsample = (nparts + pstride - 1) / pstride;
@@ -1373,14 +1563,14 @@ __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4)))
     for (int i = 0; i < kRCRowsPerThread; ++i) {
       const int r = threadIdx.x + i * kRCThreads;
       if (r < nr) {
-        const int64_t k = bkeys[rb + r];
+        const KT k = bkeys[rb + r];
         skeys[bst[rj_bucket(k)] + rk[i]] = k;
       }
     }
     __syncthreads();
     unsigned long long c = 0;
     for (int64_t l0 = threadIdx.x; l0 < nl; l0 += 4 * kRCThreads) {  // 4 probe loads in flight
-      int64_t pk[4];
+      KT pk[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (l0 + u * kRCThreads < nl) pk[u] = pkeys[lb + l0 + u * kRCThreads];
@@ -1404,6 +1594,7 @@ __device__ __forceinline__ int64_t rj_shfl64(int64_t x, int src) {
   const uint32_t hi = __shfl((uint32_t)((uint64_t)x >> 32), src, kWave);
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
+__device__ __forceinline__ int64_t rj_shfl_key(int64_t x, int src) { return rj_shfl64(x, src); }
 
 struct BuildOut {               // build-side output columns
   uint8_t *out[kMaxFusedCols];
@@ -1415,16 +1606,20 @@ struct BuildOut {               // build-side output columns
 // OM: emit finds each output slot's probe lane through a per-wave LDS owner map (lanes write
 // their lane id into the slots of their matches) instead of a 6-step binary search over the
 // wave's match scan with cross-lane permutes (CYLON_RJ_OWNERMAP=1 selects it; A/B knob).
-template <int MAXP, int MAXB, bool W8, bool OM>
-__global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__restrict__ pkeys,
+// KT: key type of the partitions (int64_t, or uint32_t low halves of a narrow-key join: kmin
+// rebuilds the output keys).  pkey: index of the probe column that IS the key (its value comes
+// from the probe key, not a second load; -1 none).
+template <int MAXP, int MAXB, bool W8, bool OM, class KT>
+__global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict__ pkeys,
                                                             const int64_t *__restrict__ poffs,
-                                                            const int64_t *__restrict__ bkeys,
+                                                            const KT *__restrict__ bkeys,
                                                             const int64_t *__restrict__ boffs, int64_t nparts,
                                                             int cap, const int64_t *__restrict__ out_offs, ColSet pc,
                                                             ColSet bs, BuildOut bo,
                                                             unsigned long long *__restrict__ cursor, int64_t out_cap,
                                                             int *__restrict__ overflow,
-                                                            unsigned long long *__restrict__ stamps) {
+                                                            unsigned long long *__restrict__ stamps, int64_t kmin,
+                                                            int pkey) {
   // out_offs != nullptr: partition p's rows start at out_offs[p] (exact count kernel ran first).
   // out_offs == nullptr: fused count -- each partition claims its rows from *cursor with one
   // atomic after counting its matches (output partitions land in claim order); a claim past
@@ -1439,8 +1634,8 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
   __shared__ uint32_t wtot[kRJWaves];
   __shared__ int64_t sclaim;
   __shared__ uint8_t ownmap[OM ? kRJWaves * kWave : 1];
-  int64_t *skeys = reinterpret_cast<int64_t *>(area);
-  uint16_t *perm = reinterpret_cast<uint16_t *>(area + 8 * (int64_t)cap);
+  KT *skeys = reinterpret_cast<KT *>(area);
+  uint16_t *perm = reinterpret_cast<uint16_t *>(area + sizeof(KT) * (int64_t)cap);
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
   int tix = -1;  // debug stamps (CYLON_RJ_STAMPS): block 0's partition count, RP_STAMP slots 0..5
@@ -1456,7 +1651,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
     const int64_t per = (nl + kRJWaves - 1) / kRJWaves;  // each wave owns a contiguous probe slice
     const int64_t s0 = lb + std::min<int64_t>(nl, wave * per);
     const int64_t s1 = lb + std::min<int64_t>(nl, (wave + 1) * per);
-    int64_t pk[kRJProbeRounds];
+    KT pk[kRJProbeRounds];
     uint64_t pv[kRJProbeRounds][MAXP];
 #pragma unroll
     for (int u = 0; u < kRJProbeRounds; ++u) {
@@ -1465,10 +1660,10 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
         pk[u] = pkeys[l];
 #pragma unroll
         for (int q = 0; q < MAXP; ++q)
-          if (q < pc.n) pv[u][q] = ldw<W8>(pc.in[q], l, pc.width[q]);
+          if (q < pc.n && q != pkey) pv[u][q] = ldw<W8>(pc.in[q], l, pc.width[q]);
       }
     }
-    int64_t bk[kRJRowsPerThread];
+    KT bk[kRJRowsPerThread];
 #pragma unroll
     for (int i = 0; i < kRJRowsPerThread; ++i) {
       const int r = threadIdx.x + i * kRJThreads;
@@ -1478,7 +1673,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
     __syncthreads();  // previous partition fully done with bst / area / wtot
     for (int s = threadIdx.x; s < kRJBuckets / 2; s += blockDim.x) reinterpret_cast<uint32_t *>(bst)[s] = 0;
     {  // payload columns, column by column (5 loads in flight per column)
-      int64_t off = 10 * (int64_t)cap;
+      int64_t off = (int64_t)(sizeof(KT) + 2) * cap;
 #pragma unroll
       for (int j = 0; j < MAXB; ++j) {
         if (j < bs.n) {
@@ -1548,7 +1743,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
     for (int u = 0; s0 + (int64_t)u * kWave < s1; ++u) {
       const int64_t l = s0 + (int64_t)u * kWave + lane;
       const bool active = l < s1;
-      int64_t k = 0;
+      KT k = 0;
       uint64_t v[MAXP] = {};
       if (u < kRJProbeRounds) {
 #pragma unroll
@@ -1562,7 +1757,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
         k = pkeys[l];
 #pragma unroll
         for (int q = 0; q < MAXP; ++q)
-          if (q < pc.n) v[q] = ldw<W8>(pc.in[q], l, pc.width[q]);
+          if (q < pc.n && q != pkey) v[q] = ldw<W8>(pc.in[q], l, pc.width[q]);
       }
       uint32_t i0 = 0, i1 = 0, mc = 0;
       if (active) {
@@ -1604,11 +1799,12 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
           }
         }
         const uint32_t j = so - __shfl(excl, owner, kWave);  // match rank inside the owner's bucket
-        const int64_t ko = rj_shfl64(k, owner);
+        const KT ko = rj_shfl_key(k, owner);
+        const uint64_t kw = (uint64_t)rj_widen(ko, kmin);
         const uint32_t b0 = __shfl(i0, owner, kWave), b1 = __shfl(i1, owner, kWave);
         uint64_t vo[MAXP];
 #pragma unroll
-        for (int q = 0; q < MAXP; ++q) vo[q] = (uint64_t)rj_shfl64((int64_t)v[q], owner);
+        for (int q = 0; q < MAXP; ++q) vo[q] = q == pkey ? kw : (uint64_t)rj_shfl64((int64_t)v[q], owner);
         if (act) {
           int r = 0;
           for (uint32_t i = b0, c = 0; i < b1; ++i) {
@@ -1625,16 +1821,17 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
             if (q < pc.n) stw<W8>(pc.out[q], o, pc.width[q], vo[q]);
           if (pc.n > MAXP) {
             const int64_t lo = s0 + (int64_t)u * kWave + owner;
-            for (int q = MAXP; q < pc.n; ++q) stw<W8>(pc.out[q], o, pc.width[q], ldw<W8>(pc.in[q], lo, pc.width[q]));
+            for (int q = MAXP; q < pc.n; ++q)
+              stw<W8>(pc.out[q], o, pc.width[q], q == pkey ? kw : ldw<W8>(pc.in[q], lo, pc.width[q]));
           }
 #pragma unroll
           for (int q = 0; q < MAXB + 1; ++q)
             if (q < bo.n)
               stw<W8>(bo.out[q], o, bo.width[q],
-                      bo.lds_off[q] < 0 ? (uint64_t)ko : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
+                      bo.lds_off[q] < 0 ? kw : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
           for (int q = MAXB + 1; q < bo.n; ++q)
             stw<W8>(bo.out[q], o, bo.width[q],
-                    bo.lds_off[q] < 0 ? (uint64_t)ko : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
+                    bo.lds_off[q] < 0 ? kw : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
         }
       }
       base += wsum;
@@ -1645,26 +1842,37 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
 
 static int rj_grid(int64_t nparts) { return (int)std::min<int64_t>(nparts, kNumCUs * 8); }
 
-void radix_join_count(const int64_t *pkeys, const int64_t *poffs, const int64_t *bkeys, const int64_t *boffs,
-                      int64_t nparts, int64_t cap, int64_t *counts, int *overflow, void *stream, int64_t pstride) {
+void radix_join_count(const void *pkeys, const int64_t *poffs, const void *bkeys, const int64_t *boffs,
+                      int64_t nparts, int64_t cap, int64_t *counts, int *overflow, void *stream, int64_t pstride,
+                      int key_bytes) {
   CYLON_CHECK(cap > 0 && cap <= kRJMaxRows, Code::Invalid, "radix join capacity " << cap);
   CYLON_CHECK(pstride >= 1, Code::Invalid, "partition stride " << pstride);
+  CYLON_CHECK(key_bytes == 8 || key_bytes == 4, Code::Invalid, "radix join key bytes " << key_bytes);
   hipStream_t s = as_stream(stream);
   HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
   const int64_t nsample = (nparts + pstride - 1) / pstride;
-  hipLaunchKernelGGL(k_rj_count, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(nsample, kNumCUs * 12))),
-                     dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap, pstride, counts, overflow);
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(nsample, kNumCUs * 12)));
+  if (key_bytes == 8)
+    hipLaunchKernelGGL(k_rj_count<int64_t>, grid, dim3(kRCThreads), 0, s, static_cast<const int64_t *>(pkeys), poffs,
+                       static_cast<const int64_t *>(bkeys), boffs, nparts, (int)cap, pstride, counts, overflow);
+  else
+    hipLaunchKernelGGL(k_rj_count<uint32_t>, grid, dim3(kRCThreads), 0, s, static_cast<const uint32_t *>(pkeys), poffs,
+                       static_cast<const uint32_t *>(bkeys), boffs, nparts, (int)cap, pstride, counts, overflow);
   HIP_LAUNCH_CHECK();
 }
 
-void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t *bkeys, const int64_t *boffs,
+void radix_join_write(const void *pkeys, const int64_t *poffs, const void *bkeys, const int64_t *boffs,
                       int64_t nparts, int64_t cap, const int64_t *out_offs, const uint8_t *const *pin,
                       uint8_t *const *pout, const int *pw, int npc, const uint8_t *const *bin, uint8_t *const *bout,
-                      const int *bw, int nbc, void *stream, int64_t *cursor, int64_t out_cap, int *overflow) {
+                      const int *bw, int nbc, void *stream, int64_t *cursor, int64_t out_cap, int *overflow,
+                      int key_bytes, int64_t kmin, int pkey) {
+  CYLON_CHECK(key_bytes == 8 || key_bytes == 4, Code::Invalid, "radix join key bytes " << key_bytes);
+  CYLON_CHECK(pkey >= -1 && pkey < npc, Code::Invalid, "radix join probe key column " << pkey);
   CYLON_CHECK(npc <= kMaxFusedCols && nbc <= kMaxFusedCols, Code::Invalid, "too many columns");
   CYLON_CHECK(out_offs != nullptr || (cursor != nullptr && overflow != nullptr), Code::Invalid,
               "radix join write: needs partition offsets or an output cursor");
-  CYLON_CHECK(cap > 0 && cap <= radix_join_capacity(bw, bin, nbc), Code::Invalid, "radix join capacity " << cap);
+  CYLON_CHECK(cap > 0 && cap <= radix_join_capacity(bw, bin, nbc, key_bytes), Code::Invalid,
+              "radix join capacity " << cap);
   ColSet pc, bs;
   BuildOut bo;
   pc.n = npc;
@@ -1684,7 +1892,7 @@ void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t 
     if (q < npc) w8 &= pw[q] == 8;
     if (q < nbc) w8 &= bw[q] == 8;
   }
-  int64_t off = 10 * cap;
+  int64_t off = (key_bytes + 2) * cap;
   for (int q = 0; q < nbc; ++q)
     if (bin[q]) {
       bo.lds_off[q] = (int)off;
@@ -1705,15 +1913,24 @@ void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t 
   }
   const char *om = std::getenv("CYLON_RJ_OWNERMAP");
   const bool ownermap = om && om[0] == '1';
-  if (w8 && ownermap)
-    hipLaunchKernelGGL((k_rj_write<4, 3, true, true>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs,
-                       bkeys, boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st);
+  const dim3 grid(rj_grid(nparts));
+  const int64_t *pk8 = static_cast<const int64_t *>(pkeys), *bk8 = static_cast<const int64_t *>(bkeys);
+  const uint32_t *pk4 = static_cast<const uint32_t *>(pkeys), *bk4 = static_cast<const uint32_t *>(bkeys);
+  if (key_bytes == 4 && w8)
+    hipLaunchKernelGGL((k_rj_write<4, 3, true, false, uint32_t>), grid, dim3(kRJThreads), 0, s, pk4, poffs, bk4, boffs,
+                       nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
+  else if (key_bytes == 4)
+    hipLaunchKernelGGL((k_rj_write<4, 3, false, false, uint32_t>), grid, dim3(kRJThreads), 0, s, pk4, poffs, bk4,
+                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
+  else if (w8 && ownermap)
+    hipLaunchKernelGGL((k_rj_write<4, 3, true, true, int64_t>), grid, dim3(kRJThreads), 0, s, pk8, poffs, bk8, boffs,
+                       nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
   else if (w8)
-    hipLaunchKernelGGL((k_rj_write<4, 3, true, false>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs,
-                       bkeys, boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st);
+    hipLaunchKernelGGL((k_rj_write<4, 3, true, false, int64_t>), grid, dim3(kRJThreads), 0, s, pk8, poffs, bk8, boffs,
+                       nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
   else
-    hipLaunchKernelGGL((k_rj_write<4, 3, false, false>), dim3(rj_grid(nparts)), dim3(kRJThreads), 0, s, pkeys, poffs,
-                       bkeys, boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st);
+    hipLaunchKernelGGL((k_rj_write<4, 3, false, false, int64_t>), grid, dim3(kRJThreads), 0, s, pk8, poffs, bk8,
+                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
   HIP_LAUNCH_CHECK();
   if (st) {  // mean cycles per partition: load+stage, index build, count+claim, emit, then to the next
     HIP_CHECK(hipStreamSynchronize(s));

@@ -178,7 +178,7 @@ static bool packs_validity(const TablePtr &t) {
 
 // Partition every column of t (+ validity bytes) by the top `bits` bits of fmix64(key).
 static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Tensor &keys, int bits,
-                                 const RangeSpec *range = nullptr) {
+                                 const RangeSpec *range = nullptr, at::Tensor *narrow_ws = nullptr) {
   std::vector<at::Tensor> cur{keys};
   std::vector<int> widths{8};
   std::vector<int> dslot(t->Columns(), -1), vslot(t->Columns(), -1);
@@ -208,7 +208,7 @@ static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Te
     return e && e[0] == '1';
   }();
   cur = RadixPartition(ex, std::move(cur), widths, bits, &offs, range, packs_validity(t) ? &packed : nullptr,
-                       range != nullptr || force_stable);
+                       range != nullptr || force_stable, narrow_ws);
   RadixSide s;
   s.keys = cur[0];
   s.offs = offs;
@@ -341,20 +341,49 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     if (col.type.width() == 8 && col.data.data_ptr() == (build_left ? lk : rk).data_ptr()) shape.in[q] = nullptr;
     if (col.nullable() && !packs_validity(bt)) ++q;  // packed validity words sit after the columns
   }
-  const int64_t cap = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size());
+  const int64_t cap8 = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size());
   // mean build rows per partition: 0.85 x capacity keeps the largest of ~1M uniform
   // partitions >8 sigma below the capacity (Poisson), and lets 1B rows use 19 bits
   // (passes of 10 + 9 bits; a 9-bit pass streams at ~5.5 TB/s, a 10-bit one ~3.9)
-  const int64_t target = std::max<int64_t>(1, cap * 85 / 100);
+  const int64_t target = std::max<int64_t>(1, cap8 * 85 / 100);
   int bits = 0;
   while ((nb >> bits) > target) ++bits;
   const int64_t nparts = int64_t(1) << bits;
   RadixSide L, R;
+  // Narrow keys: when the two relations' keys span < 2^32 values (one min/max reduction folded
+  // into the first pass's histogram kernel, then one host read), a key's low 32 bits identify
+  // it: the partition hash is taken over them and the key travels as uint32 through the passes
+  // and the join kernels (28 instead of 32 B/row for int64 key + 3 x 8 B payload), rebuilt as
+  // kmin + (low - (uint32)kmin) on output.  Measured SLOWER on MI355X and therefore opt-in
+  // (CYLON_RJ_NARROW=1; profiles/r03/narrow_keys_ab.txt): the 4-byte key column's scattered
+  // 64-B runs write no faster than 8-byte 128-B runs, so the second pass takes 19.8 instead of
+  // 17.9 ms and the write kernel 36.2 instead of 33.8 ms (headline 110-115 -> 119-121 ms).
+  int key_bytes = 8;
+  int64_t kmin = 0;
   {
     CYLON_PHASE("join.radix.partition", ex.device);
-    L = radix_partition(ex, left, lk, bits);
-    R = radix_partition(ex, right, rk, bits);
+    at::Tensor nws_l, nws_r;
+    const char *ne = std::getenv("CYLON_RJ_NARROW");  // read per join (tests toggle it)
+    const bool narrow_on = ne && ne[0] == '1';
+    if (narrow_on && bits > 0 && !hip::radix_lookback_enabled()) {
+      at::Tensor mm = at::empty({2}, ex.opts(at::kLong));
+      mm.select(0, 0).fill_(std::numeric_limits<int64_t>::max());
+      mm.select(0, 1).fill_(std::numeric_limits<int64_t>::min());
+      nws_l = RadixNarrowPrehist(ex, lk, bits, mm);
+      nws_r = RadixNarrowPrehist(ex, rk, bits, mm);
+      at::Tensor h = mm.cpu();
+      const int64_t lo = h[0].item<int64_t>(), hi = h[1].item<int64_t>();
+      if (lo <= hi && (uint64_t)hi - (uint64_t)lo < (uint64_t(1) << 32)) {
+        key_bytes = 4;
+        kmin = lo;
+        trace::add_counter("join.radix.narrow_keys", 1);
+      }
+    }
+    L = radix_partition(ex, left, lk, bits, nullptr, key_bytes == 4 ? &nws_l : nullptr);
+    R = radix_partition(ex, right, rk, bits, nullptr, key_bytes == 4 ? &nws_r : nullptr);
   }
+  const int64_t cap =
+      key_bytes == 8 ? cap8 : hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size(), key_bytes);
   RadixSide &B = build_left ? L : R;
   RadixSide &P = build_left ? R : L;
   // Output size.  Exact mode: a count kernel over every partition, a scan, then the write
@@ -382,8 +411,8 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   int64_t m = 0, alloc = 0;
   {
     CYLON_PHASE("join.radix.count", ex.device);
-    hip::radix_join_count(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
-                          nparts, cap, ptr<int64_t>(counts), overflow.data_ptr<int>(), ex.stream, stride);
+    hip::radix_join_count(P.keys.data_ptr(), ptr<int64_t>(P.offs), B.keys.data_ptr(), ptr<int64_t>(B.offs), nparts,
+                          cap, ptr<int64_t>(counts), overflow.data_ptr<int>(), ex.stream, stride, key_bytes);
     // the ranking guard of the stable (second and later) partition passes
     if (hip::rp_take_order_violation(ex.stream)) {
       trace::add_counter("join.radix.order_violation_fallback", 1);
@@ -442,13 +471,18 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   auto write = [&](int64_t rows, const int64_t *offs, int64_t *cursor) {
     RadixCols pc = build_left ? radix_cols(right, &R, &rcols, off, &rwords) : radix_cols(left, &L, &lcols, off, &lwords);
     RadixCols bc = build_left ? radix_cols(left, &L, &lcols, off, &lwords) : radix_cols(right, &R, &rcols, off, &rwords);
-    // probe-side columns are streamed from HBM: the key column is read from its partitioned array
+    // probe-side columns are streamed from HBM; the key column (in == nullptr) is written from
+    // the probe key the kernel already holds
+    int pkey = -1;
     for (size_t q = 0; q < pc.in.size(); ++q)
-      if (!pc.in[q]) pc.in[q] = reinterpret_cast<const uint8_t *>(P.keys.data_ptr());
-    hip::radix_join_write(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
-                          nparts, cap, offs, pc.in.data(), pc.out.data(), pc.w.data(), (int)pc.in.size(),
-                          bc.in.data(), bc.out.data(), bc.w.data(), (int)bc.in.size(), ex.stream, cursor, rows,
-                          overflow.data_ptr<int>());
+      if (!pc.in[q]) {
+        pc.in[q] = reinterpret_cast<const uint8_t *>(P.keys.data_ptr());
+        if (pkey < 0) pkey = (int)q;
+      }
+    hip::radix_join_write(P.keys.data_ptr(), ptr<int64_t>(P.offs), B.keys.data_ptr(), ptr<int64_t>(B.offs), nparts,
+                          cap, offs, pc.in.data(), pc.out.data(), pc.w.data(), (int)pc.in.size(), bc.in.data(),
+                          bc.out.data(), bc.w.data(), (int)bc.in.size(), ex.stream, cursor, rows,
+                          overflow.data_ptr<int>(), key_bytes, kmin, pkey);
   };
   if (stride == 1) {
     allocate(m);

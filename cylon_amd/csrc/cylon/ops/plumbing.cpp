@@ -28,6 +28,41 @@ static Column gather_var(const Exec &ex, const Column &c, const at::Tensor &idx,
   return Column(c.name, c.type, m, bytes, offs, valid);
 }
 
+// K15 var-width select (string / binary where and fill_null; kernels/select.hip): row i is a[i]
+// where cond[i], else b[i] (b one row long: broadcast; b undefined: null).  cond: bool or uint8
+// tensor of a's length on any device (undefined: always a).
+Column SelectVar(const Column &a, const std::optional<Column> &b, const at::Tensor &cond) {
+  CYLON_CHECK(a.is_var(), Code::TypeError, "select_var: column " << a.name << " is not variable width");
+  const int64_t n = a.length;
+  Exec ex(a.device());
+  if (b) {
+    CYLON_CHECK(b->is_var() && b->type.kind() == a.type.kind(), Code::TypeError,
+                "select_var: the other column must have the type of " << a.name);
+    CYLON_CHECK(b->length == n || b->length == 1, Code::Invalid,
+                "select_var: other has " << b->length << " rows, want " << n << " or 1");
+    CYLON_CHECK(b->device() == a.device(), Code::Invalid, "select_var: columns on different devices");
+  }
+  at::Tensor c;
+  if (cond.defined()) {
+    CYLON_CHECK(cond.numel() == n, Code::Invalid, "select_var: condition has " << cond.numel() << " rows, want " << n);
+    c = cond.to(ex.device, at::kByte).contiguous();
+  }
+  ColView av = a.view(), bv{};
+  const int bcast = b && b->length == 1 && n != 1 ? 1 : 0;
+  if (b) bv = b->view();
+  const uint8_t *cp = c.defined() ? ptr<uint8_t>(c) : nullptr;
+  at::Tensor lens = ex.empty_i64(n);
+  KCALL(ex, select_var_lengths, av, bv, bcast, cp, n, ptr<int64_t>(lens));
+  at::Tensor offs = exclusive_scan(ex, lens);
+  const int64_t total = read_i64(offs, n);
+  at::Tensor bytes = ex.empty_bytes(total);
+  const bool may_null = a.nullable() || !b || b->nullable();
+  at::Tensor valid = may_null ? ex.empty_u8(n) : at::Tensor();
+  KCALL(ex, select_var_bytes, av, bv, bcast, cp, n, ptr<int64_t>(offs), ptr<uint8_t>(bytes),
+        valid.defined() ? ptr<uint8_t>(valid) : nullptr);
+  return Column(a.name, a.type, n, bytes, offs, valid);
+}
+
 // Gather every column of a table with one fused launch per 16 fixed-width
 // columns; var-width columns take the two-pass path.
 static std::vector<Column> gather_columns(const std::vector<Column> &cols, const at::Tensor &idx, bool may_null) {

@@ -66,9 +66,32 @@ std::vector<at::Tensor> UnpackByteColumns(const Exec &ex, const BytePacking &bp,
   return out;
 }
 
+static int max_digit_bits() {  // digit bits per pass (<= 10); tuning knob
+  static const int v = [] {
+    const char *e = std::getenv("CYLON_RADIX_DIGIT_BITS");
+    return e ? std::max(1, std::min(10, std::atoi(e))) : 10;
+  }();
+  return v;
+}
+
+int RadixFirstDigitBits(int bits) {
+  const int npass = (bits + max_digit_bits() - 1) / max_digit_bits();
+  return npass ? (bits + npass - 1) / npass : 0;
+}
+
+at::Tensor RadixNarrowPrehist(const Exec &ex, const at::Tensor &keys, int bits, const at::Tensor &mm) {
+  const int db = RadixFirstDigitBits(bits);
+  const int64_t n = keys.numel();
+  at::Tensor ws = ex.empty_i64(hip::radix_rows_pass_workspace(n, db));
+  hip::radix_narrow_prehist(ptr<int64_t>(keys), n, bits, db, ptr<int64_t>(ws), ptr<int64_t>(mm), ex.stream);
+  return ws;
+}
+
 std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> cur, const std::vector<int> &widths,
                                        int bits, at::Tensor *offs, const RangeSpec *range,
-                                       std::vector<int> *keep_packed, bool stable) {
+                                       std::vector<int> *keep_packed, bool stable, at::Tensor *narrow_ws) {
+  const bool narrow = narrow_ws != nullptr;
+  CYLON_CHECK(!narrow || (!range && bits > 0), Code::Invalid, "RadixPartition: narrow keys need hash partitions");
   CYLON_CHECK(ex.gpu, Code::Invalid, "RadixPartition is a device path");
   CYLON_CHECK(!cur.empty() && cur.size() == widths.size() && widths[0] == 8, Code::Invalid,
               "RadixPartition: column 0 must be the int64 key");
@@ -80,10 +103,7 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
   // (16-B byte runs per pass instead of 128-B runs); packed: 30.2 ms.
   std::vector<int> pw = widths;
   const BytePacking bp = PackByteColumns(ex, cur, pw, n);
-  static const int max_db = [] {  // digit bits per pass (<= 10); tuning knob
-    const char *e = std::getenv("CYLON_RADIX_DIGIT_BITS");
-    return e ? std::max(1, std::min(10, std::atoi(e))) : 10;
-  }();
+  const int max_db = max_digit_bits();
   const int npass = (bits + max_db - 1) / max_db;
   std::vector<int> shifts, dbits;
   int lb_bits = 0;
@@ -96,7 +116,7 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
   }
   // chained-scan passes (kernels/radix_join.hip k_lb_hist): one read of the keys counts the
   // digits of every pass instead of a histogram kernel before each pass
-  const bool lbm = npass >= 2 && n > 0 && hip::radix_lookback_enabled();
+  const bool lbm = npass >= 2 && n > 0 && hip::radix_lookback_enabled() && !narrow;
   at::Tensor lbws;
   if (lbm) {
     lbws = ex.empty_i64(hip::radix_lb_workspace(n, lb_bits));
@@ -118,13 +138,22 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
     std::vector<at::Tensor> nxt;
     std::vector<const uint8_t *> in;
     std::vector<uint8_t *> out;
-    for (auto &x : cur) {
+    for (size_t c = 0; c < cur.size(); ++c) {
+      const at::Tensor &x = cur[c];
       // an undefined tensor is a row-id column: generated by the first pass (radix_rows_pass)
-      nxt.push_back(x.defined() ? at::empty_like(x) : ex.empty_i64(n));
+      nxt.push_back(narrow && c == 0 ? at::empty({n}, ex.opts(at::kInt))
+                                     : (x.defined() ? at::empty_like(x) : ex.empty_i64(n)));
       in.push_back(x.defined() ? reinterpret_cast<const uint8_t *>(x.data_ptr()) : nullptr);
       out.push_back(reinterpret_cast<uint8_t *>(nxt.back().data_ptr()));
     }
-    if (range)
+    if (narrow) {
+      CYLON_CHECK(ps > 0 || db == RadixFirstDigitBits(bits), Code::Invalid, "narrow prehist digit");
+      std::vector<int> nw = pw;
+      nw[0] = 4;
+      hip::radix_narrow_rows_pass(cur[0].data_ptr(), ps == 0 ? 8 : 4, n, bits, shift, db, in.data(), out.data(),
+                                  nw.data(), (int)cur.size(), ps == 0 ? ptr<int64_t>(*narrow_ws) : ptr<int64_t>(ws),
+                                  ex.stream, stable || ps > 0, ps == 0);
+    } else if (range)
       hip::radix_range_rows_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, range->flip, range->mn,
                                  range->rshift, shift, db, in.data(), out.data(), pw.data(), (int)cur.size(),
                                  ptr<int64_t>(ws), ex.stream, lbp, ps, lb_bits);
@@ -149,7 +178,10 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
   }
   *offs = ex.empty_i64((int64_t(1) << bits) + 1);
   if (keep_packed && !bp.active) keep_packed->clear();
-  if (range)
+  if (narrow)
+    hip::radix_narrow_part_offsets(reinterpret_cast<const uint32_t *>(cur[0].data_ptr()), n, bits,
+                                   ptr<int64_t>(*offs), ex.stream);
+  else if (range)
     hip::radix_range_part_offsets(ptr<int64_t>(cur[0]), n, range->flip, range->mn, range->rshift, bits,
                                   ptr<int64_t>(*offs), ex.stream);
   else

@@ -9,6 +9,7 @@
 #pragma once
 #include <functional>
 #include <memory>
+#include <optional>
 #include <string>
 #include <vector>
 
@@ -82,6 +83,8 @@ namespace ops {
 TablePtr Gather(const TablePtr &t, const at::Tensor &idx);  // idx int64, -1 -> null row
 TablePtr GatherNullable(const TablePtr &t, const at::Tensor &idx, bool may_null);
 Column GatherColumn(const Column &c, const at::Tensor &idx);
+// K15 string / binary select: row i = cond[i] ? a[i] : b[i] (b of one row: broadcast; no b: null)
+Column SelectVar(const Column &a, const std::optional<Column> &b, const at::Tensor &cond);
 TablePtr Project(const TablePtr &t, const std::vector<int> &cols);
 TablePtr Merge(const std::vector<TablePtr> &tables);  // vertical concat
 TablePtr Slice(const TablePtr &t, int64_t offset, int64_t length);

@@ -134,6 +134,32 @@ def is_null(table, invert: bool = False):
     return table._wrap(C.Table(table.native.context(), out))
 
 
+def _var_scalar(c, value, device):
+    """One-row device column of c's type holding value (None if value does not convert)."""
+    try:
+        arr = pa.array([value], type=ab.to_arrow_type(c.type))
+    except (pa.ArrowInvalid, pa.ArrowTypeError, TypeError, ValueError):
+        return None
+    return ab.column_from_arrow(c.name, arr, device)
+
+
+def _select_var(c, other, cond, device):
+    """K15 device select of a string / binary column (kernels/select.hip): cond ? c : other, where
+    other is None (null), a scalar (broadcast) or a column of c's type; None when other does not
+    fit (the caller then uses Arrow's host kernels)."""
+    if other is None:
+        b = None
+    elif isinstance(other, C.Column):
+        if not is_var(other) or other.type.type != c.type.type or other.length not in (1, c.length):
+            return None
+        b = other
+    else:
+        b = _var_scalar(c, other, device)
+        if b is None:
+            return None
+    return C.select_var(c, b, cond.to(torch.uint8))
+
+
 def fill_null(table, value):
     out = []
     for c in table.native.columns():
@@ -141,7 +167,9 @@ def fill_null(table, value):
             out.append(c)
             continue
         if is_var(c):
-            out.append(_from_arrow(c.name, pc.fill_null(_arrow_col(c), value), table.device))
+            res = _select_var(c, value, c.validity, table.device) if value is not None else c
+            out.append(res if res is not None else _from_arrow(c.name, pc.fill_null(_arrow_col(c), value),
+                                                               table.device))
             continue
         v = col_values(c)
         mask = col_valid(c)
@@ -165,9 +193,12 @@ def where(table, condition, other=None):
         if cvv is not None:
             cv = cv & cvv
         if is_var(c):
-            rhs = None if other is None else other
-            res = pc.if_else(pa.array(cv.cpu().numpy()), _arrow_col(c), rhs)
-            out.append(_from_arrow(c.name, res, table.device))
+            rhs = other.native.column(i) if isinstance(other, Table) else other
+            res = _select_var(c, rhs, cv, table.device)
+            if res is None:  # other of another type: Arrow's host if_else (casts / raises like pandas)
+                rhs = other.to_arrow().column(i) if isinstance(other, Table) else other
+                res = _from_arrow(c.name, pc.if_else(pa.array(cv.cpu().numpy()), _arrow_col(c), rhs), table.device)
+            out.append(res)
             continue
         v = col_values(c)
         valid = col_valid(c)

@@ -9,7 +9,7 @@ import pyarrow as pa
 import pytest
 import torch
 
-from cylon_amd import Table
+from cylon_amd import C, Table
 
 pytestmark = pytest.mark.gpu
 
@@ -366,3 +366,31 @@ def test_persistent_string_hash_index_on_device():
         pos.setdefault(v, []).append(i)
     exp = np.array([p for l in labels for p in pos.get(l, [])], dtype=np.int64)
     assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("n", [0, 1, 5000, 200_000])
+def test_string_select_kernel_matches_cpu(gpu_ctx, ctx, n):
+    """K15 select_var (kernels/select.hip: string where / fill_null) on the device against its CPU
+    twin and Arrow: per-row other, broadcast scalar, null other; rows up to ~3 KB exercise the
+    16-byte vector body with unaligned heads."""
+    import pyarrow.compute as pc
+    rng = np.random.default_rng(n + 1)
+    lens = rng.integers(0, 3000, n) if n else np.zeros(0, np.int64)
+    lens[::3] = rng.integers(0, 20, len(lens[::3]))
+    a = pa.array([None if i % 9 == 0 else "x" * int(lens[i]) + str(i) for i in range(n)], pa.string())
+    o = pa.array([None if i % 4 == 0 else "y%d" % i for i in range(n)], pa.string())
+    cond = rng.random(n) < 0.4
+    at = pa.table({"a": a, "o": o})
+    res = []
+    for cx in (gpu_ctx, ctx):
+        t = Table(at, cx)
+        cols = t.native.columns()
+        c = torch.from_numpy(cond)
+        outs = [C.select_var(cols[0], cols[1], c), C.select_var(cols[0], None, c)]
+        fill = t.fillna("F").to_arrow().column("a").combine_chunks()
+        res.append([t._wrap(C.Table(t.native.context(), [x])).to_arrow().column("a").combine_chunks() for x in outs]
+                   + [fill])
+    for g, h in zip(res[0], res[1]):
+        assert g.equals(h)
+    assert res[0][0].equals(pc.if_else(pa.array(cond, pa.bool_()), a, o))
+    assert res[0][2].equals(pc.fill_null(a, "F"))

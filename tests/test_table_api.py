@@ -6,10 +6,12 @@ import os
 import numpy as np
 import pandas as pd
 import pyarrow as pa
+import pyarrow.compute as pc
 import pytest
 import torch
 
 import cylon_amd as cy
+from cylon_amd import C
 from cylon_amd import CylonContext, DataFrame, JoinConfig, Series, Status, Table
 from cylon_amd.io import CSVReadOptions, CSVWriteOptions, read_csv, write_csv
 
@@ -226,3 +228,32 @@ def test_device_isin_strings_and_numeric_cast(ctx):
         Table(pa.table({"x": [1.5]}), ctx).astype("int64")
     with pytest.raises(Exception):
         t.astype({"i": "int8"})  # 300 out of range
+
+
+@pytest.mark.parametrize("typ", [pa.string(), pa.large_string(), pa.binary()])
+def test_string_fillna_where_select_kernel(ctx, typ):
+    """K15 string / binary where and fill_null run the native select kernels (select_var) and
+    match Arrow's if_else / fill_null: scalar fill, null `other`, column `other` (with nulls),
+    empty strings and rows longer than the 16-byte vector copy."""
+    rng = np.random.default_rng(4)
+    n = 3000
+
+    def val(i):
+        s = "" if i % 11 == 0 else ("abc%d" % i) * (1 + i % 37)
+        return s.encode() if typ == pa.binary() else s
+    a = pa.array([None if i % 7 == 0 else val(i) for i in range(n)], typ)
+    o = pa.array([None if i % 5 == 0 else val(i + 1) for i in range(n)], typ)
+    cond = rng.random(n) < 0.5
+    t = Table(pa.table({"s": a, "o": o}), ctx)
+    fill = b"FILL" if typ == pa.binary() else "FILL"
+    same = lambda got, ref: got.equals(ref.cast(got.type))  # noqa: E731  (large_string maps to string)
+    assert same(t.fillna(fill).to_arrow().column("s").combine_chunks(), pc.fill_null(a, fill))
+    m = Table(pa.table({"s": cond, "o": cond}), ctx)
+    got = t.where(m).to_arrow()
+    assert same(got.column("s").combine_chunks(), pc.if_else(pa.array(cond), a, None).cast(typ))
+    cols = t.native.columns()
+    sel = C.select_var(cols[0], cols[1], torch.from_numpy(cond))
+    ref = pc.if_else(pa.array(cond), a, o)
+    assert same(t._wrap(C.Table(t.native.context(), [sel])).to_arrow().column("s").combine_chunks(), ref)
+    with_scalar = t.where(m, fill).to_arrow().column("s").combine_chunks()
+    assert same(with_scalar, pc.if_else(pa.array(cond), a, pa.scalar(fill, typ)))
