@@ -345,8 +345,64 @@ __global__ __launch_bounds__(kRPThreads) void k_lb_scan(const unsigned long long
   if (p < nb) gstart[s * nb + p] = off + inc - c;
 }
 
+// LDS-DMA of `bytes` (a multiple of 4) contiguous global bytes into LDS at dst (16-byte aligned)
+// by the block's WAVES waves: 1 KB pieces with global_load_lds_dwordx4 (a wave-instruction lands
+// at its uniform base + lane * 16; the source may be only 8-byte aligned), the last < 16 bytes as
+// dwords.  No VGPRs hold the data.
+template <int WAVES>
+__device__ __forceinline__ void rj_dma_block(const uint8_t *src, int bytes, uint8_t *dst, int wave, int lane) {
+  const int nq = bytes >> 4;
+  for (int c0 = wave * kWave; c0 < nq; c0 += WAVES * kWave)
+    if (c0 + lane < nq)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + (int64_t)(c0 + lane) * 16),
+                                       (__attribute__((address_space(3))) void *)(dst + c0 * 16), 16, 0, 0);
+  const int t0 = nq << 2, nd = bytes >> 2;  // tail dwords (at most 3)
+  if (wave == WAVES - 1 && t0 + lane < nd)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + (int64_t)(t0 + lane) * 4),
+                                     (__attribute__((address_space(3))) void *)(dst + t0 * 4), 4, 0, 0);
+}
+
+// The same DMA issued from inline asm (the recipe of cdna_hip_programming.md §4): hipcc then keeps
+// no bookkeeping for it, so it does not drain it with vmcnt(0) before every later LDS access (it
+// cannot tell the DMA's destination from the ranking counters) -- the caller waits for it with an
+// explicit s_waitcnt before the buffer is read.  lds_base: the buffer's LDS byte address.
+template <int WAVES>
+__device__ __forceinline__ void rp_dma_asm(const uint8_t *src, int bytes, uint32_t lds_base, int wave, int lane) {
+  const int nq = bytes >> 4;
+  for (int c0 = wave * kWave; c0 < nq; c0 += WAVES * kWave) {
+    const uint32_t dst = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds_base + (uint32_t)c0 * 16u));
+    if (c0 + lane < nq) {
+      const uint8_t *g = src + (int64_t)(c0 + lane) * 16;
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(g), "s"(dst) : "memory");
+    }
+  }
+  const int t0 = nq << 2, nd = bytes >> 2;  // tail dwords (at most 3)
+  if (wave == WAVES - 1 && t0 + lane < nd) {
+    const uint32_t dst = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds_base + (uint32_t)t0 * 4u));
+    const uint8_t *g = src + (int64_t)(t0 + lane) * 4;
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(dst) : "memory");
+  }
+}
+
+// Block barrier.  RAW: LDS-only (lgkmcnt(0) + s_barrier) -- an LDS-DMA in flight stays in
+// flight (__syncthreads() waits vmcnt(0) while one is outstanding: cdna_hip_programming.md §5).
+template <bool RAW>
+__device__ __forceinline__ void rp_sync() {
+  if (RAW) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  } else {
+    __syncthreads();
+  }
+}
+
 // block-wide exclusive scan of one uint32 per thread (WAVES waves)
-template <int WAVES = kRPWaves>
+template <int WAVES = kRPWaves, bool RAW = false>
 __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) {
   const int lane = lane_id(), wave = threadIdx.x / kWave;
   uint32_t inc = c;
@@ -356,7 +412,7 @@ __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) 
     if (lane >= d) inc += t;
   }
   if (lane == kWave - 1) wsum[wave] = inc;
-  __syncthreads();
+  rp_sync<RAW>();
   uint32_t off = 0;
 #pragma unroll
   for (int w = 0; w < WAVES; ++w) off += (w < wave) ? wsum[w] : 0u;
@@ -394,7 +450,11 @@ constexpr int kRPStampTiles = 64, kRPStampSlots = 16;
 // 16-bit counters: stable exactly when one instruction's same-address atomics return in lane
 // order -- tools/lds_atomic_order.hip measures that on the device).
 // LB: lookback mode (tiles claimed from lb.ticket, offsets by decoupled lookback; bh_scan unused).
-template <class Digit, bool W8, int THREADS, int RANK, bool LB>
+// DMA1 (W8, >= 2 columns, column 1 read from memory): column 1 of the tile is fetched by LDS-DMA
+// into a second 64 KB buffer as soon as the tile's digits are known, so the load streams during the
+// ranking / scan / slot / destination phases (which move no bytes of their own) instead of behind
+// column 0's scatter; those phases then synchronise with LDS-only barriers.
+template <class Digit, bool W8, int THREADS, int RANK, bool LB, bool DMA1 = false>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_rows_pass(
     Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
     const int64_t *__restrict__ bh_scan, Lookback lb, unsigned long long *__restrict__ stamps) {
@@ -404,7 +464,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   constexpr bool K4 = Digit::kNarrow;  // column 0 (the key) is stored as uint32
   static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 4 <= TILE * 8, "ranking scratch must fit the stage");
   static_assert(!LB || (THREADS >= kRPMaxBuckets && TILE == kRPTile), "lookback: one bucket a thread, 8192-row tiles");
+  static_assert(!DMA1 || (W8 && !LB), "column-1 DMA: 8-byte columns, histogram mode");
   __shared__ int64_t running[kRPMaxBuckets];
+  __shared__ __attribute__((aligned(16))) uint64_t land[DMA1 ? TILE : 1];  // column 1 of the tile (DMA1)
   __shared__ uint32_t toff[kRPMaxBuckets + 1];
   __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16, sdig[TILE] u32}
   __shared__ uint32_t wsum[WAVES];
@@ -451,13 +513,19 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k)
       pl[k] = (wrow + k * kWave + lane < cnt) ? digit.of_key((int64_t)kv[k]) : 0xffffffffu;
+    // the digits consumed the prefetched keys (their loads are retired), so this DMA is the only
+    // vector-memory work in flight through the LDS-only barriers below
+    if (DMA1)
+      rp_dma_asm<WAVES>(cols.in[1] + tile * 8, cnt * 8,
+                        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint64_t *)(land),
+                        wave, lane);
     RP_STAMP(1);
     if (STABLE) {
       for (uint32_t q = threadIdx.x; q < WAVES * nbuckets; q += blockDim.x) wcnt[q] = 0;
     } else {
       for (uint32_t q = threadIdx.x; q < nbuckets; q += blockDim.x) bcnt[q] = 0;
     }
-    __syncthreads();  // also orders the previous tile's stage reads before the counters reuse it
+    rp_sync<DMA1>();  // also orders the previous tile's stage reads before the counters reuse it
     if (!STABLE) {
       // order inside a bucket's run is free (join partitions): one LDS atomic per row
       // replaces the nbits ballots of the stable match
@@ -491,7 +559,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       __builtin_amdgcn_wave_barrier();
       pl[k] = active ? (((base + rank) << 16) | p) : 0xffffffffu;
     }
-    __syncthreads();
+    rp_sync<DMA1>();
     RP_STAMP(2);
     {  // thread owns buckets [t*BPT, t*BPT+BPT): exclusive prefix over waves (in place), then a
        // block scan of the thread totals
@@ -516,7 +584,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         }
         total += run;
       }
-      const uint32_t ex = rp_block_exscan<WAVES>(total, wsum);
+      const uint32_t ex = rp_block_exscan<WAVES, DMA1>(total, wsum);
 #pragma unroll
       for (int i = 0; i < BPT; ++i) {
         const uint32_t p = threadIdx.x * BPT + i;
@@ -524,7 +592,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       }
       if (threadIdx.x == THREADS - 1) toff[nbuckets] = ex + total;
     }
-    __syncthreads();
+    rp_sync<DMA1>();
     RP_STAMP(3);
     // LB: this tile's bucket offsets from its predecessors (read by the dst phase): count published
     // before the slot phase, lookback after it.  nbuckets <= THREADS: one bucket a thread
@@ -539,7 +607,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       pl[k] = pos;
     }
     if (LB && threadIdx.x < nbuckets) running[threadIdx.x] = lb_exclusive(lb, nbuckets, tile / TILE, threadIdx.x, lbc);
-    __syncthreads();
+    rp_sync<DMA1>();
     RP_STAMP(4);
     int64_t dst[kRPItems];  // destination of sorted slot j = threadIdx.x + q * THREADS
 #pragma unroll
@@ -554,7 +622,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         }
       }
     }
-    __syncthreads();  // counters / digits dead: the union becomes the column stage
+    rp_sync<DMA1>();  // counters / digits dead: the union becomes the column stage
     RP_STAMP(5);
     // load column c+1 while column c streams out of the stage
     uint64_t v[kRPItems];
@@ -563,6 +631,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll 1
     for (int c = 0; c < cols.n; ++c) {  // column fields fetched once per column (scalar loads)
       const int w = cols.width[c];
+      if (DMA1 && c == 1) {  // column 1 landed by DMA (waited for at the end of column 0)
+#pragma unroll
+        for (int k = 0; k < kRPItems; ++k) v[k] = land[wrow + k * kWave + lane];
+      }
       uint8_t *out = cols.out[c];
       const uint64_t x = c == 0 ? cols.key_xor : 0ull;
       if (LB && c + 1 == cols.n && threadIdx.x == 0) s_next = (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
@@ -579,7 +651,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       __syncthreads();
       if (LB && c + 1 == cols.n) next = s_next;
       RP_STAMP(6 + 2 * c);
-      if (c + 1 < cols.n) {  // prefetch column c+1 of this tile
+      if (DMA1 && c == 0) {
+        // column 1 is in flight by DMA: nothing to prefetch behind column 0
+      } else if (c + 1 < cols.n) {  // prefetch column c+1 of this tile
         const uint8_t *in = cols.in[c + 1];
         const int w1 = cols.width[c + 1];
         if (in == nullptr) {  // row-id column: the pass generates it (no 8 B/row array to read)
@@ -610,6 +684,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
           if (j < cnt) stw<W8>(out, dst[q], w, ldw<W8>(st, j, w));
         }
       }
+      if (DMA1 && c == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // column 1 has landed
       __syncthreads();
       RP_STAMP(7 + 2 * c);
     }
@@ -985,6 +1060,18 @@ int64_t radix_rows_pass_workspace(int64_t n, int digit_bits) {  // covers both b
   return ws;
 }
 
+// Column-1 LDS-DMA of the one-block-per-CU pass (k_rows_pass DMA1): 8-byte columns, >= 2 of them,
+// column 1 read from memory.  Opt-in (CYLON_RP_DMA=1, read per launch): measured SLOWER on the
+// 1B x 1B join (profiles/r03/lds_dma_ab.txt: tile 82-86K -> 88-103K cycles).  hipcc's own
+// s_waitcnt vmcnt(0) before the kernel's register-spill reloads in the slot phase (it cannot count
+// the asm DMA) and the DMA issue behind the previous tile's outstanding scatter stores put the
+// transfer back on the critical path: the keys phase grows 1.4K -> 10K cycles, the slot phase
+// 2K -> 7K, while column 0's scatter shrinks only 16K -> 8-9K.
+static bool rp_dma1(bool w8, const ColSet &cs) {
+  const char *e = std::getenv("CYLON_RP_DMA");
+  return w8 && cs.n >= 2 && cs.in[1] != nullptr && e && e[0] == '1';
+}
+
 template <class Digit, int THREADS, int RANK, bool LB = false>
 static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit &dg, int digit_bits, uint32_t nb,
                              const ColSet &cs, int64_t n, const int64_t *bh_scan, const Lookback &lb = Lookback{}) {
@@ -995,7 +1082,16 @@ static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const 
     HIP_CHECK(hipMalloc(&st, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
     HIP_CHECK(hipMemset(st, 0, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
   }
-  if (w8)
+  bool launched = false;
+  if constexpr (THREADS == 1024 && !LB) {
+    if (rp_dma1(w8, cs)) {
+      hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS, RANK, LB, true>), dim3((unsigned)g.nblocks), dim3(THREADS),
+                         0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
+      launched = true;
+    }
+  }
+  if (launched) {
+  } else if (w8)
     hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS, RANK, LB>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s,
                        dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
   else
@@ -1609,7 +1705,13 @@ struct BuildOut {               // build-side output columns
 // KT: key type of the partitions (int64_t, or uint32_t low halves of a narrow-key join: kmin
 // rebuilds the output keys).  pkey: index of the probe column that IS the key (its value comes
 // from the probe key, not a second load; -1 none).
-template <int MAXP, int MAXB, bool W8, bool OM, class KT>
+// the write kernel's build staging: rj_dma_block over its 16 waves
+__device__ __forceinline__ void rj_dma(const uint8_t *src, int bytes, uint8_t *dst, int wave, int lane) {
+  rj_dma_block<kRJWaves>(src, bytes, dst, wave, lane);
+}
+
+// DMA: stage the build columns by LDS-DMA (needs W8) instead of register round trips per column.
+template <int MAXP, int MAXB, bool W8, bool OM, class KT, bool DMA>
 __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict__ pkeys,
                                                             const int64_t *__restrict__ poffs,
                                                             const KT *__restrict__ bkeys,
@@ -1664,15 +1766,33 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict
       }
     }
     KT bk[kRJRowsPerThread];
+    if (!DMA) {
 #pragma unroll
-    for (int i = 0; i < kRJRowsPerThread; ++i) {
-      const int r = threadIdx.x + i * kRJThreads;
-      if (r < nr) bk[i] = bkeys[rb + r];
+      for (int i = 0; i < kRJRowsPerThread; ++i) {
+        const int r = threadIdx.x + i * kRJThreads;
+        if (r < nr) bk[i] = bkeys[rb + r];
+      }
     }
     // ---- phase B: stage + index the build rows
     __syncthreads();  // previous partition fully done with bst / area / wtot
     for (int s = threadIdx.x; s < kRJBuckets / 2; s += blockDim.x) reinterpret_cast<uint32_t *>(bst)[s] = 0;
-    {  // payload columns, column by column (5 loads in flight per column)
+    if (DMA) {  // every build column in ONE round trip: the keys (raw order) into the key region,
+                // the payload columns into theirs; the loads hold no VGPRs
+      rj_dma(reinterpret_cast<const uint8_t *>(bkeys + rb), nr * (int)sizeof(KT), area, wave, lane);
+      int64_t off = (int64_t)(sizeof(KT) + 2) * cap;
+#pragma unroll
+      for (int j = 0; j < MAXB; ++j)
+        if (j < bs.n) {
+          rj_dma(bs.in[j] + rb * 8, nr * 8, area + off, wave, lane);
+          off += (int64_t)cap * 8;
+        }
+      for (int j = MAXB; j < bs.n; ++j) {  // rare: wide build rows
+        for (int r = threadIdx.x; r < nr; r += kRJThreads)
+          stw<true>(area + off, r, 8, ldw<true>(bs.in[j], rb + r, 8));
+        off += (int64_t)cap * 8;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {  // payload columns, column by column (5 loads in flight per column)
       int64_t off = (int64_t)(sizeof(KT) + 2) * cap;
 #pragma unroll
       for (int j = 0; j < MAXB; ++j) {
@@ -1695,6 +1815,13 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict
       }
     }
     __syncthreads();
+    if (DMA) {  // raw keys back from the key region (bucket placement overwrites it after the scan)
+#pragma unroll
+      for (int i = 0; i < kRJRowsPerThread; ++i) {
+        const int r = threadIdx.x + i * kRJThreads;
+        if (r < nr) bk[i] = skeys[r];
+      }
+    }
     RP_STAMP(1);
     uint32_t rk[kRJRowsPerThread];
 #pragma unroll
@@ -1916,20 +2043,29 @@ void radix_join_write(const void *pkeys, const int64_t *poffs, const void *bkeys
   const dim3 grid(rj_grid(nparts));
   const int64_t *pk8 = static_cast<const int64_t *>(pkeys), *bk8 = static_cast<const int64_t *>(bkeys);
   const uint32_t *pk4 = static_cast<const uint32_t *>(pkeys), *bk4 = static_cast<const uint32_t *>(bkeys);
-  if (key_bytes == 4 && w8)
-    hipLaunchKernelGGL((k_rj_write<4, 3, true, false, uint32_t>), grid, dim3(kRJThreads), 0, s, pk4, poffs, bk4, boffs,
+  // LDS-DMA build staging: write kernel 33.9 -> 32.9 ms per 1B x 1B join (profiles/r03/lds_dma_ab.txt)
+  const char *dm = std::getenv("CYLON_RJ_DMA");  // A/B knob: 0 = register staging
+  const bool dma = w8 && !(dm && dm[0] == '0');
+  if (key_bytes == 4 && dma)
+    hipLaunchKernelGGL((k_rj_write<4, 3, true, false, uint32_t, true>), grid, dim3(kRJThreads), 0, s, pk4, poffs, bk4,
+                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
+  else if (dma && !ownermap)
+    hipLaunchKernelGGL((k_rj_write<4, 3, true, false, int64_t, true>), grid, dim3(kRJThreads), 0, s, pk8, poffs, bk8,
+                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
+  else if (key_bytes == 4 && w8)
+    hipLaunchKernelGGL((k_rj_write<4, 3, true, false, uint32_t, false>), grid, dim3(kRJThreads), 0, s, pk4, poffs, bk4, boffs,
                        nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
   else if (key_bytes == 4)
-    hipLaunchKernelGGL((k_rj_write<4, 3, false, false, uint32_t>), grid, dim3(kRJThreads), 0, s, pk4, poffs, bk4,
+    hipLaunchKernelGGL((k_rj_write<4, 3, false, false, uint32_t, false>), grid, dim3(kRJThreads), 0, s, pk4, poffs, bk4,
                        boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
   else if (w8 && ownermap)
-    hipLaunchKernelGGL((k_rj_write<4, 3, true, true, int64_t>), grid, dim3(kRJThreads), 0, s, pk8, poffs, bk8, boffs,
+    hipLaunchKernelGGL((k_rj_write<4, 3, true, true, int64_t, false>), grid, dim3(kRJThreads), 0, s, pk8, poffs, bk8, boffs,
                        nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
   else if (w8)
-    hipLaunchKernelGGL((k_rj_write<4, 3, true, false, int64_t>), grid, dim3(kRJThreads), 0, s, pk8, poffs, bk8, boffs,
+    hipLaunchKernelGGL((k_rj_write<4, 3, true, false, int64_t, false>), grid, dim3(kRJThreads), 0, s, pk8, poffs, bk8, boffs,
                        nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
   else
-    hipLaunchKernelGGL((k_rj_write<4, 3, false, false, int64_t>), grid, dim3(kRJThreads), 0, s, pk8, poffs, bk8,
+    hipLaunchKernelGGL((k_rj_write<4, 3, false, false, int64_t, false>), grid, dim3(kRJThreads), 0, s, pk8, poffs, bk8,
                        boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
   HIP_LAUNCH_CHECK();
   if (st) {  // mean cycles per partition: load+stage, index build, count+claim, emit, then to the next
