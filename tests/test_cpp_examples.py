@@ -328,3 +328,67 @@ def test_cpp_examples_distributed_tcp(data_dir):
             else:
                 assert o["pipeline_matches_hash"] == 1 and o["group_sums_match_total"] == 1
         port += 1
+
+
+def _check_io_graph_examples(device, data_dir, out_dir):
+    """parquet_example (CSV -> Parquet -> device round trip, multi-file and column-subset reads,
+    join / union of the Parquet tables) and op_graph_example (DisJoinOP / DisUnionOp fed in
+    batches vs the one-shot operators), against pandas."""
+    import pandas as pd
+    c1, c2 = (os.path.join(data_dir, "input", f) for f in ("csv1_0.csv", "csv2_0.csv"))
+    l, r = pd.read_csv(c1), pd.read_csv(c2)
+    k = l.columns[0]
+    join_rows = len(l.merge(r, on=k))
+    union_rows = len(pd.concat([l, r]).drop_duplicates())
+    got = _run_example("parquet_example", device, c1, c2, str(out_dir))
+    assert got["left_rows"] == len(l) and got["right_rows"] == len(r) and got["roundtrip_equal"] == 1, got
+    assert got["multi_file_rows"] == len(l) + len(r) and got["subset_columns"] == 1, got
+    assert got["join_rows"] == join_rows and got["union_rows"] == union_rows, got
+    got = _run_example("op_graph_example", device, c1, c2, "4")
+    assert got["op_join_rows"] == got["direct_join_rows"] == join_rows, got
+    assert got["op_union_rows"] == got["direct_union_rows"] == union_rows, got
+
+
+def test_cpp_io_graph_examples_on_cpu(data_dir, tmp_path):
+    _check_io_graph_examples("cpu", data_dir, tmp_path)
+
+
+@pytest.mark.gpu
+def test_cpp_io_graph_examples_on_gpu(data_dir, tmp_path):
+    _check_io_graph_examples("cuda:0", data_dir, tmp_path)
+
+
+def test_cpp_io_graph_examples_distributed_tcp(data_dir, tmp_path):
+    """parquet_example and op_graph_example as 2 native TCP ranks (rank r reads csv{1,2}_r):
+    per-rank join / union rows of the streamed op graph equal the one-shot distributed operators',
+    and their sums equal pandas on the concatenated inputs."""
+    import socket
+    import pandas as pd
+    _ensure_built()
+    W = 2
+    files = [[os.path.join(data_dir, "input", f"csv{s}_{r}.csv") for s in (1, 2)] for r in range(W)]
+    L = pd.concat([pd.read_csv(f[0]) for f in files])
+    R = pd.concat([pd.read_csv(f[1]) for f in files])
+    k = L.columns[0]
+    for name, extra in (("parquet_example", [str(tmp_path)]), ("op_graph_example", ["3"])):
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        exe = os.path.join(ROOT, "examples", "cpp", "bin", name)
+        procs = []
+        for r in range(W):
+            env = {k2: v for k2, v in os.environ.items() if not k2.startswith("TORCHELASTIC")}
+            env.update(RANK=str(r), WORLD_SIZE=str(W), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([exe, "tcp", *files[r], *extra], stdout=subprocess.PIPE,
+                                          stderr=subprocess.PIPE, text=True, env=env))
+        res = [p.communicate(timeout=180) for p in procs]
+        assert all(p.returncode == 0 for p in procs), [e[-1500:] for _, e in res]
+        outs = [dict((a, int(b)) for a, b in (line.split() for line in o.splitlines())) for o, _ in res]
+        if name == "parquet_example":
+            assert all(o["roundtrip_equal"] == 1 for o in outs)
+            assert sum(o["join_rows"] for o in outs) == len(L.merge(R, on=k))
+            assert sum(o["union_rows"] for o in outs) == len(pd.concat([L, R]).drop_duplicates())
+        else:
+            assert all(o["op_join_rows"] == o["direct_join_rows"] and o["op_union_rows"] == o["direct_union_rows"]
+                       for o in outs), outs
+            assert sum(o["op_join_rows"] for o in outs) == len(L.merge(R, on=k))
