@@ -249,7 +249,38 @@ struct Lookback {
   unsigned long long *status;    // [tile][nbuckets]
   unsigned int *ticket;          // next tile to claim
   unsigned long long epoch;      // 1..63
+  // XCD-tile mode (XT): per-tile bucket offsets and one ticket per XCD (see k_rp_hist_tiles)
+  const uint32_t *xt_off;        // [tile][nbuckets] output row of the tile's first row of each bucket
+  unsigned int *xt_ticket;       // [8] next tile of each XCD's contiguous chunk
+  int64_t xt_tiles;              // tiles of the pass
 };
+
+// XCD-tile mode.  Histogram mode gives each block a contiguous chunk of rows, so the tiles of
+// one block write a bucket's consecutive runs ~34 us apart and the partial 128-B line at every
+// run boundary has left the XCD's 4 MB L2 before the next tile completes it (~20 % extra HBM
+// bytes, profiles/r03/pmc_join_1B_dma_vs_regstage.txt).  Here the tiles are split into 8
+// contiguous chunks, one per XCD, and the XCD's CUs claim its tiles IN ORDER from a per-XCD
+// ticket: at any moment an XCD's 32 CUs hold ~32 consecutive tiles, whose runs of each bucket
+// are adjacent in the output and are written within a few us of each other into the same L2.
+// Offsets are exact per tile (k_rp_hist_tiles + k_ts_*), so which CU takes a tile changes only
+// speed; a block whose own chunk is exhausted takes tiles from the other chunks.
+constexpr int kXcds = 8;
+__device__ __forceinline__ int xcc_id() {
+  int x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & (kXcds - 1);
+}
+// first row of the next tile this block processes, or n_rows when every chunk is exhausted
+__device__ __forceinline__ int64_t xt_claim(const Lookback &lb, int home, int64_t tile_rows, int64_t n_rows) {
+  for (int k = 0; k < kXcds; ++k) {
+    const int x = (home + k) & (kXcds - 1);
+    const int64_t lo = lb.xt_tiles * x / kXcds, hi = lb.xt_tiles * (x + 1) / kXcds;
+    if (lo >= hi) continue;
+    const int64_t j = (int64_t)atomicAdd(&lb.xt_ticket[x], 1u);
+    if (lo + j < hi) return (lo + j) * tile_rows;
+  }
+  return n_rows;
+}
 
 // Windowed lookback in two steps: lb_publish stores tile t's count of bucket p right after the
 // scan (successors can sum it while this tile ranks its slots); lb_exclusive then reads its
@@ -419,6 +450,86 @@ __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) 
   return off + inc - c;
 }
 
+// ---- XCD-tile mode (XT) offsets: per-tile bucket counts, then exact output rows per (tile, bucket)
+// th[t][p]: rows of bucket p in kRPTile-row tile t (uint16: a tile has <= 8192 rows)
+template <class Digit>
+__global__ __launch_bounds__(kRPThreads) void k_rp_hist_tiles(Digit digit, int64_t n, uint32_t nb, int64_t ntiles,
+                                                              uint16_t *__restrict__ th) {
+  __shared__ unsigned int hist[kRPMaxBuckets];
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (uint32_t p = threadIdx.x; p < nb; p += blockDim.x) hist[p] = 0;
+    __syncthreads();
+    uint32_t d[kRPItems];
+    const int64_t r0 = t * kRPTile;
+#pragma unroll
+    for (int u = 0; u < kRPItems; ++u) {
+      const int64_t i = r0 + u * kRPThreads + threadIdx.x;
+      d[u] = i < n ? digit(i) : 0xffffffffu;
+    }
+#pragma unroll
+    for (int u = 0; u < kRPItems; ++u)
+      if (d[u] != 0xffffffffu) atomicAdd(&hist[d[u]], 1u);
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < nb; p += blockDim.x) th[t * nb + p] = (uint16_t)hist[p];
+    __syncthreads();
+  }
+}
+
+constexpr int64_t kTsChunk = 512;  // tiles per chunk of the tile-offset scan
+
+// csum[c][p] = rows of bucket p in chunk c's tiles (one thread per bucket)
+__global__ void k_ts_chunk_sums(const uint16_t *__restrict__ th, uint32_t nb, int64_t ntiles,
+                                uint32_t *__restrict__ csum) {
+  const int64_t c = blockIdx.x, t0 = c * kTsChunk, t1 = t0 + kTsChunk < ntiles ? t0 + kTsChunk : ntiles;
+  const uint32_t p = threadIdx.x;
+  if (p >= nb) return;
+  uint32_t acc = 0;
+#pragma unroll 8
+  for (int64_t t = t0; t < t1; ++t) acc += th[t * nb + p];
+  csum[c * nb + p] = acc;
+}
+
+// cpre[c][p] = rows of bucket p in the chunks before c; bbase[p] = output row of bucket p's first
+// row (bucket-major order).  One block; each thread batches its chunk loads (independent addresses).
+__global__ __launch_bounds__(kRPThreads) void k_ts_chunk_prefix(const uint32_t *__restrict__ csum, uint32_t nb,
+                                                                int64_t nchunks, uint32_t *__restrict__ cpre,
+                                                                uint32_t *__restrict__ bbase) {
+  __shared__ uint32_t wsum[kRPWaves];
+  constexpr int B = 16;
+  const uint32_t p = threadIdx.x;
+  uint32_t acc = 0;
+  if (p < nb)
+    for (int64_t c0 = 0; c0 < nchunks; c0 += B) {
+      uint32_t x[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) x[u] = c0 + u < nchunks ? csum[(c0 + u) * nb + p] : 0u;
+#pragma unroll
+      for (int u = 0; u < B; ++u)
+        if (c0 + u < nchunks) {
+          cpre[(c0 + u) * nb + p] = acc;
+          acc += x[u];
+        }
+    }
+  const uint32_t base = rp_block_exscan<kRPWaves>(p < nb ? acc : 0u, wsum);
+  if (p < nb) bbase[p] = base;
+}
+
+// off[t][p] = output row of tile t's first row of bucket p
+__global__ void k_ts_offsets(const uint16_t *__restrict__ th, const uint32_t *__restrict__ cpre,
+                             const uint32_t *__restrict__ bbase, uint32_t nb, int64_t ntiles,
+                             uint32_t *__restrict__ off) {
+  const int64_t c = blockIdx.x, t0 = c * kTsChunk, t1 = t0 + kTsChunk < ntiles ? t0 + kTsChunk : ntiles;
+  const uint32_t p = threadIdx.x;
+  if (p >= nb) return;
+  uint32_t acc = cpre[c * nb + p] + bbase[p];
+#pragma unroll 8
+  for (int64_t t = t0; t < t1; ++t) {
+    off[t * nb + p] = acc;
+    acc += th[t * nb + p];
+  }
+}
+
+
 // LDS: running (8 KB) + toff (4 KB) + one 64 KB union that holds the per-wave
 // digit counters and the sorted-slot digits while ranking, then the column
 // stage (76 KB).  One 1024-thread block per CU (the ranking needs ~120 VGPRs);
@@ -436,7 +547,7 @@ __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) 
 constexpr int kRPStampTiles = 64, kRPStampSlots = 16;
 #define RP_STAMP(slot)                                                                               \
   do {                                                                                               \
-    if (stamps != nullptr && blockIdx.x == 0 && tix < kRPStampTiles && (slot) < kRPStampSlots) {     \
+    if (stamps != nullptr && blockIdx.x == 0 && tix >= 0 && tix < kRPStampTiles && (slot) < kRPStampSlots) { \
       unsigned long long t_;                                                                         \
       __builtin_amdgcn_sched_barrier(0);                                                             \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                    \
@@ -454,7 +565,7 @@ constexpr int kRPStampTiles = 64, kRPStampSlots = 16;
 // into a second 64 KB buffer as soon as the tile's digits are known, so the load streams during the
 // ranking / scan / slot / destination phases (which move no bytes of their own) instead of behind
 // column 0's scatter; those phases then synchronise with LDS-only barriers.
-template <class Digit, bool W8, int THREADS, int RANK, bool LB, bool DMA1 = false>
+template <class Digit, bool W8, int THREADS, int RANK, bool LB, bool DMA1 = false, bool XT = false>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_rows_pass(
     Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
     const int64_t *__restrict__ bh_scan, Lookback lb, unsigned long long *__restrict__ stamps) {
@@ -465,6 +576,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 4 <= TILE * 8, "ranking scratch must fit the stage");
   static_assert(!LB || (THREADS >= kRPMaxBuckets && TILE == kRPTile), "lookback: one bucket a thread, 8192-row tiles");
   static_assert(!DMA1 || (W8 && !LB), "column-1 DMA: 8-byte columns, histogram mode");
+  static_assert(!(LB && XT), "one tile schedule");
+  constexpr bool TICKET = LB || XT;  // tiles claimed one by one (not a contiguous chunk per block)
+  const int xhome = XT ? xcc_id() : 0;
   __shared__ int64_t running[kRPMaxBuckets];
   __shared__ __attribute__((aligned(16))) uint64_t land[DMA1 ? TILE : 1];  // column 1 of the tile (DMA1)
   __shared__ uint32_t toff[kRPMaxBuckets + 1];
@@ -482,8 +596,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 
   const int64_t b = blockIdx.x;
   int64_t begin, end;
-  if (LB) {
-    if (threadIdx.x == 0) s_next = (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
+  if (TICKET) {
+    if (threadIdx.x == 0) s_next = XT ? xt_claim(lb, xhome, TILE, n) : (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
     __syncthreads();
     begin = s_next;
     end = n;
@@ -509,6 +623,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     const int tix = (int)((tile - begin) / TILE);
     RP_STAMP(0);
     const int cnt = (int)((end - tile) < TILE ? (end - tile) : TILE);
+    // XT: this tile's bucket offsets (consumed after the slot phase; the load overlaps the ranking)
+    const uint32_t xoff = XT && threadIdx.x < nbuckets ? lb.xt_off[(tile / TILE) * nbuckets + threadIdx.x] : 0u;
     uint32_t pl[kRPItems];  // digit, then (in-wave rank << 16) | digit, then sorted slot; ~0 = inactive
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k)
@@ -607,6 +723,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       pl[k] = pos;
     }
     if (LB && threadIdx.x < nbuckets) running[threadIdx.x] = lb_exclusive(lb, nbuckets, tile / TILE, threadIdx.x, lbc);
+    if (XT && threadIdx.x < nbuckets) running[threadIdx.x] = xoff;
     rp_sync<DMA1>();
     RP_STAMP(4);
     int64_t dst[kRPItems];  // destination of sorted slot j = threadIdx.x + q * THREADS
@@ -637,7 +754,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       }
       uint8_t *out = cols.out[c];
       const uint64_t x = c == 0 ? cols.key_xor : 0ull;
-      if (LB && c + 1 == cols.n && threadIdx.x == 0) s_next = (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
+      if (TICKET && c + 1 == cols.n && threadIdx.x == 0)
+        s_next = XT ? xt_claim(lb, xhome, TILE, n) : (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
       const bool k4 = K4 && c == 0;  // narrow key: column 0 leaves as its low 32 bits
       if (k4) {
 #pragma unroll
@@ -649,7 +767,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
           if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
       }
       __syncthreads();
-      if (LB && c + 1 == cols.n) next = s_next;
+      if (TICKET && c + 1 == cols.n) next = s_next;
       RP_STAMP(6 + 2 * c);
       if (DMA1 && c == 0) {
         // column 1 is in flight by DMA: nothing to prefetch behind column 0
@@ -688,7 +806,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       __syncthreads();
       RP_STAMP(7 + 2 * c);
     }
-    if (!LB)
+    if (!TICKET)
       for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] += toff[p + 1] - toff[p];
   }
   if (order_bad) atomicOr(cols.order_bad, 1);
@@ -703,7 +821,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 //   * no cross-column / cross-tile prefetch (the second block hides the load latency);
 //   * the destination of sorted slot j is packed as (digit << 16 | j - toff[digit]) and
 //     completed from running[] in LDS at store time (8 VGPRs instead of 16).
-template <class Digit, bool W8, int RANK, bool LB>
+template <class Digit, bool W8, int RANK, bool LB, bool XT = false>
 __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_rows_pass_lean(
     Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
     const int64_t *__restrict__ bh_scan, Lookback lb) {
@@ -719,14 +837,17 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
   uint32_t *bcnt = reinterpret_cast<uint32_t *>(ustage);
   uint32_t *sdig = reinterpret_cast<uint32_t *>(wcnt + WAVES * kRPMaxBuckets);  // digit << 16 | input row
   uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
-  __shared__ int64_t s_next;  // LB: first row of the next claimed tile
+  __shared__ int64_t s_next;  // LB / XT: first row of the next claimed tile
   bool order_bad = false;
   (void)nbits;
+  static_assert(!(LB && XT), "one tile schedule");
+  constexpr bool TICKET = LB || XT;
+  const int xhome = XT ? xcc_id() : 0;
 
   const int64_t b = blockIdx.x;
   int64_t begin, end;
-  if (LB) {
-    if (threadIdx.x == 0) s_next = (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
+  if (TICKET) {
+    if (threadIdx.x == 0) s_next = XT ? xt_claim(lb, xhome, TILE, n) : (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
     __syncthreads();
     begin = s_next;
     end = n;
@@ -749,6 +870,8 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
     int tx = (int)threadIdx.x;
     asm volatile("" : "+v"(tx));
     const int lane = tx & (kWave - 1);
+    // XT: this tile's bucket offsets (stored to running[] after the slot phase)
+    const uint32_t xoff = XT && (uint32_t)tx < nbuckets ? lb.xt_off[(tile / TILE) * nbuckets + tx] : 0u;
     uint32_t pl[kRPItems];  // digit | in-tile rank << 16, then the sorted slot; ~0 = inactive
     const int64_t *kbase = digit.keys + tile + wrow;  // wave-uniform
     const int lim = cnt - wrow;                       // rows of this wave's slice that exist
@@ -823,6 +946,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
       pl[k] = pos;
     }
     if (LB && (uint32_t)tx < nbuckets) running[tx] = lb_exclusive(lb, nbuckets, tile / TILE, tx, lbc);
+    if (XT && (uint32_t)tx < nbuckets) running[tx] = xoff;
     __syncthreads();
     uint32_t dp[kRPItems];  // sorted slot j = tx + q * THREADS -> digit << 16 | offset in its run
 #pragma unroll
@@ -853,12 +977,13 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
         for (int k = 0; k < kRPItems; ++k) v[k] = (k * kWave + lane < lim) ? ldw<W8>(ibase, k * kWave + lane, w) : 0ull;
       }
       const uint64_t x = c == 0 ? cols.key_xor : 0ull;
-      if (LB && c + 1 == cols.n && tx == 0) s_next = (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
+      if (TICKET && c + 1 == cols.n && tx == 0)
+        s_next = XT ? xt_claim(lb, xhome, TILE, n) : (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
 #pragma unroll
       for (int k = 0; k < kRPItems; ++k)
         if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
       __syncthreads();
-      if (LB && c + 1 == cols.n) next = s_next;
+      if (TICKET && c + 1 == cols.n) next = s_next;
 #pragma unroll
       for (int q = 0; q < kRPItems; ++q) {
         const int j = tx + q * THREADS;
@@ -866,7 +991,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
       }
       __syncthreads();
     }
-    if (!LB)
+    if (!TICKET)
       for (uint32_t p = tx; p < nbuckets; p += THREADS) running[p] += toff[p + 1] - toff[p];
   }
   if (order_bad) atomicOr(cols.order_bad, 1);
@@ -1050,8 +1175,34 @@ static RPGeometry rp_geometry(int64_t n, int threads, int resident = 1) {
   return g;
 }
 
+// XCD-tile mode (k_rows_pass / k_rows_pass_lean XT), default on: 1B x 1B join 116-121 -> 102-103 ms,
+// passes 21 -> 15.5 ms, pass HBM traffic back to the column bytes (profiles/r03/xcd_tiles_ab.txt).
+// CYLON_RP_XT=0 returns to per-block contiguous chunks (read per call).
+static bool rp_xt() {
+  const char *e = std::getenv("CYLON_RP_XT");
+  return !(e && e[0] == '0');
+}
+
+struct XtLayout {  // int64-word offsets of the XT buffers in a pass workspace
+  int64_t ntiles, nchunks, th, off, csum, cpre, bbase, tickets, words;
+};
+static XtLayout xt_layout(int64_t n, uint32_t nb) {
+  XtLayout l;
+  l.ntiles = std::max<int64_t>(1, (n + kRPTile - 1) / kRPTile);
+  l.nchunks = (l.ntiles + kTsChunk - 1) / kTsChunk;
+  const int64_t cells = l.ntiles * nb, ccells = l.nchunks * nb;
+  l.th = 0;                                   // uint16 [ntiles][nb]
+  l.off = l.th + (cells * 2 + 7) / 8;         // uint32 [ntiles][nb]
+  l.csum = l.off + (cells * 4 + 7) / 8;       // uint32 [nchunks][nb]
+  l.cpre = l.csum + (ccells * 4 + 7) / 8;     // uint32 [nchunks][nb]
+  l.bbase = l.cpre + (ccells * 4 + 7) / 8;    // uint32 [nb]
+  l.tickets = l.bbase + (nb * 4 + 7) / 8;     // uint32 [kXcds]
+  l.words = l.tickets + kXcds;
+  return l;
+}
+
 int64_t radix_rows_pass_workspace(int64_t n, int digit_bits) {  // covers both block sizes and the lean pass
-  int64_t ws = 0;
+  int64_t ws = rp_xt() ? xt_layout(n, 1u << digit_bits).words : 0;
   for (int threads : {512, 1024, 2048}) {
     const int64_t m = (threads == 2048 ? rp_geometry(n, 1024, 2) : rp_geometry(n, threads)).nblocks *
                       (int64_t(1) << digit_bits);
@@ -1074,7 +1225,8 @@ static bool rp_dma1(bool w8, const ColSet &cs) {
 
 template <class Digit, int THREADS, int RANK, bool LB = false>
 static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit &dg, int digit_bits, uint32_t nb,
-                             const ColSet &cs, int64_t n, const int64_t *bh_scan, const Lookback &lb = Lookback{}) {
+                             const ColSet &cs, int64_t n, const int64_t *bh_scan, const Lookback &lb = Lookback{},
+                             bool xt = false) {
   static const bool stamp = std::getenv("CYLON_RP_STAMPS") != nullptr;  // debug: phase stamps to stderr
   unsigned long long *st = nullptr;
   if (stamp && !LB) {
@@ -1084,7 +1236,15 @@ static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const 
   }
   bool launched = false;
   if constexpr (THREADS == 1024 && !LB) {
-    if (rp_dma1(w8, cs)) {
+    if (xt) {
+      if (w8)
+        hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS, RANK, false, false, true>), dim3((unsigned)g.nblocks),
+                           dim3(THREADS), 0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
+      else
+        hipLaunchKernelGGL((k_rows_pass<Digit, false, THREADS, RANK, false, false, true>), dim3((unsigned)g.nblocks),
+                           dim3(THREADS), 0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
+      launched = true;
+    } else if (rp_dma1(w8, cs)) {
       hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS, RANK, LB, true>), dim3((unsigned)g.nblocks), dim3(THREADS),
                          0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
       launched = true;
@@ -1129,7 +1289,18 @@ static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const 
 
 template <class Digit, int RANK, bool LB>
 static void lean_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit &dg, int digit_bits, uint32_t nb,
-                        const ColSet &cs, int64_t n, const int64_t *bh_scan, const Lookback &lb) {
+                        const ColSet &cs, int64_t n, const int64_t *bh_scan, const Lookback &lb, bool xt = false) {
+  if constexpr (!LB) {
+    if (xt) {
+      if (w8)
+        hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, RANK, false, true>), dim3((unsigned)g.nblocks),
+                           dim3(kRPThreads), 0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
+      else
+        hipLaunchKernelGGL((k_rows_pass_lean<Digit, false, RANK, false, true>), dim3((unsigned)g.nblocks),
+                           dim3(kRPThreads), 0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
+      return;
+    }
+  }
   if (w8)
     hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, RANK, LB>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s,
                        dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
@@ -1249,7 +1420,31 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   RPGeometry g;
   const int64_t *bh_scan = nullptr;
   Lookback lb{};
-  if (lbm) {
+  const bool xt = !lbm && threads == 1024 && n < (int64_t(1) << 32) && rp_xt();
+  if (xt) {  // exact per-tile offsets, tiles claimed in order per XCD (see xt_claim)
+    const XtLayout L = xt_layout(n, nb);
+    uint16_t *th = reinterpret_cast<uint16_t *>(ws + L.th);
+    uint32_t *off = reinterpret_cast<uint32_t *>(ws + L.off);
+    uint32_t *csum = reinterpret_cast<uint32_t *>(ws + L.csum), *cpre = reinterpret_cast<uint32_t *>(ws + L.cpre);
+    unsigned *tk = reinterpret_cast<unsigned *>(ws + L.tickets);
+    HIP_CHECK(hipMemsetAsync(tk, 0, kXcds * sizeof(unsigned), s));
+    hipLaunchKernelGGL(k_rp_hist_tiles<Digit>, dim3((unsigned)std::min<int64_t>(L.ntiles, kNumCUs * 8)),
+                       dim3(kRPThreads), 0, s, dg, n, nb, L.ntiles, th);
+    HIP_LAUNCH_CHECK();
+    const unsigned bt = (unsigned)std::max<uint32_t>(kWave, (nb + kWave - 1) / kWave * kWave);
+    hipLaunchKernelGGL(k_ts_chunk_sums, dim3((unsigned)L.nchunks), dim3(bt), 0, s, th, nb, L.ntiles, csum);
+    HIP_LAUNCH_CHECK();
+    uint32_t *bbase = reinterpret_cast<uint32_t *>(ws + L.bbase);
+    hipLaunchKernelGGL(k_ts_chunk_prefix, dim3(1), dim3(kRPThreads), 0, s, csum, nb, L.nchunks, cpre, bbase);
+    HIP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_ts_offsets, dim3((unsigned)L.nchunks), dim3(bt), 0, s, th, cpre, bbase, nb, L.ntiles, off);
+    HIP_LAUNCH_CHECK();
+    lb.xt_off = off;
+    lb.xt_ticket = tk;
+    lb.xt_tiles = L.ntiles;
+    g.rows_per_block = kRPTile;
+    g.nblocks = std::min<int64_t>(L.ntiles, (int64_t)kNumCUs * (lean ? 2 : 1));  // persistent: all resident
+  } else if (lbm) {
     // status rows are 2^lb_bits wide; a pass with fewer bits indexes them with its own nb
     lb = lb_args(lbws, lb_pass, lb_bits);
     g.rows_per_block = kRPTile;
@@ -1289,8 +1484,8 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
       if (unstable) lean_kernel<Digit, R, true>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
       else lean_kernel<Digit, kRankWaveAtomic, true>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
     } else {
-      if (unstable) lean_kernel<Digit, R, false>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
-      else lean_kernel<Digit, kRankWaveAtomic, false>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
+      if (unstable) lean_kernel<Digit, R, false>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
+      else lean_kernel<Digit, kRankWaveAtomic, false>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
     }
     HIP_LAUNCH_CHECK();
     return;
@@ -1302,13 +1497,13 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
     else rows_pass_kernel<Digit, 1024, kRankBallot, true>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
   } else if (unstable) {
     constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankBallot;
-    if (big) rows_pass_kernel<Digit, 1024, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
+    if (big) rows_pass_kernel<Digit, 1024, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
     else rows_pass_kernel<Digit, 512, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
   } else if (wave_atomic) {
-    if (big) rows_pass_kernel<Digit, 1024, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
+    if (big) rows_pass_kernel<Digit, 1024, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
     else rows_pass_kernel<Digit, 512, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
   } else {
-    if (big) rows_pass_kernel<Digit, 1024, kRankBallot>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
+    if (big) rows_pass_kernel<Digit, 1024, kRankBallot>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
     else rows_pass_kernel<Digit, 512, kRankBallot>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
   }
   HIP_LAUNCH_CHECK();
