@@ -348,6 +348,8 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   const int64_t target = std::max<int64_t>(1, cap8 * 85 / 100);
   int bits = 0;
   while ((nb >> bits) > target) ++bits;
+  if (const char *xb = std::getenv("CYLON_RJ_EXTRA_BITS"))  // A/B knob: finer partitions
+    bits = std::min(bits + std::max(0, std::atoi(xb)), 2 * 10);
   const int64_t nparts = int64_t(1) << bits;
   RadixSide L, R;
   // Narrow keys: when the two relations' keys span < 2^32 values (one min/max reduction folded
