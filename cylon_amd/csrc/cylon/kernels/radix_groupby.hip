@@ -131,6 +131,13 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict
       if (threadIdx.x == 0) gcount[p] = 0;
       continue;
     }
+    if (rb > re || re > n || rb < 0) {  // corrupt partition offsets: report, touch nothing
+      if (threadIdx.x == 0) {
+        atomicOr(overflow, 8);
+        gcount[p] = 0;
+      }
+      continue;
+    }
     __syncthreads();  // previous partition done with the table
     for (int s = threadIdx.x; s <= S; s += blockDim.x) {
       tk[s] = kRGEmpty;
@@ -222,6 +229,10 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict
       if (!(occ >> q & 1u)) continue;
       const int s = threadIdx.x * kPer + q;
       const int64_t o = rb + pos++;
+      if (o >= re) {  // more groups than rows: report, write nothing
+        atomicOr(overflow, 16);
+        continue;
+      }
       okeys[o] = tk[s];
 #pragma unroll
       for (int j = 0; j < A; ++j)
@@ -229,7 +240,8 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict
     }
     if (threadIdx.x == 0) {
       const bool has_min = (bad & 2) != 0;
-      if (has_min) {
+      if (has_min && rb + tot >= re) atomicOr(overflow, 16);
+      if (has_min && rb + tot < re) {
         const int64_t o = rb + tot;
         okeys[o] = kRGEmpty;
         for (int j = 0; j < A; ++j)
@@ -257,7 +269,7 @@ int64_t distinct_estimate_workspace() { return kHllRegs; }
 
 void radix_groupby_agg(const int64_t *keys, const int64_t *offs, int64_t nparts, const RGAccDesc *acc, int nacc,
                        int64_t *okeys, uint64_t *oacc, int64_t n, int64_t *gcount, int *overflow, void *stream) {
-  CYLON_CHECK(nacc >= 0 && nacc <= 4, Code::Invalid, "radix group-by: at most 4 accumulators");
+  CYLON_CHECK(nacc >= 1 && nacc <= 4, Code::Invalid, "radix group-by: 1 to 4 accumulators");
   RGArgs a;
   a.nacc = nacc;
   for (int j = 0; j < 4; ++j) {
@@ -274,7 +286,10 @@ void radix_groupby_agg(const int64_t *keys, const int64_t *offs, int64_t nparts,
   if (nacc <= 1)
     hipLaunchKernelGGL((k_rg_agg<1, 4096>), dim3(grid), dim3(kRGThreads), 0, s, keys, offs, nparts, a, okeys, oacc,
                        n, gcount, overflow);
-  else if (nacc <= 3)
+  else if (nacc == 2)  // every accumulator slot of the table in use (A == nacc for each shape)
+    hipLaunchKernelGGL((k_rg_agg<2, 2048>), dim3(grid), dim3(kRGThreads), 0, s, keys, offs, nparts, a, okeys, oacc,
+                       n, gcount, overflow);
+  else if (nacc == 3)
     hipLaunchKernelGGL((k_rg_agg<3, 2048>), dim3(grid), dim3(kRGThreads), 0, s, keys, offs, nparts, a, okeys, oacc,
                        n, gcount, overflow);
   else

@@ -451,23 +451,26 @@ __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) 
 }
 
 // ---- XCD-tile mode (XT) offsets: per-tile bucket counts, then exact output rows per (tile, bucket)
-// th[t][p]: rows of bucket p in kRPTile-row tile t (uint16: a tile has <= 8192 rows)
+// th[t][p]: rows of bucket p in kRPTile-row tile t (uint16: a tile has <= 8192 rows).  512-thread
+// blocks (up to four per CU), 16 rows per thread with every key load issued before the first LDS
+// atomic: the kernel streams the keys at the CU's share of HBM instead of one round trip per tile.
+constexpr int kHTThreads = 512, kHTItems = kRPTile / kHTThreads;
 template <class Digit>
-__global__ __launch_bounds__(kRPThreads) void k_rp_hist_tiles(Digit digit, int64_t n, uint32_t nb, int64_t ntiles,
+__global__ __launch_bounds__(kHTThreads) void k_rp_hist_tiles(Digit digit, int64_t n, uint32_t nb, int64_t ntiles,
                                                               uint16_t *__restrict__ th) {
   __shared__ unsigned int hist[kRPMaxBuckets];
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    for (uint32_t p = threadIdx.x; p < nb; p += blockDim.x) hist[p] = 0;
-    __syncthreads();
-    uint32_t d[kRPItems];
     const int64_t r0 = t * kRPTile;
+    uint32_t d[kHTItems];
 #pragma unroll
-    for (int u = 0; u < kRPItems; ++u) {
-      const int64_t i = r0 + u * kRPThreads + threadIdx.x;
+    for (int u = 0; u < kHTItems; ++u) {
+      const int64_t i = r0 + u * kHTThreads + threadIdx.x;
       d[u] = i < n ? digit(i) : 0xffffffffu;
     }
+    for (uint32_t p = threadIdx.x; p < nb; p += blockDim.x) hist[p] = 0;
+    __syncthreads();
 #pragma unroll
-    for (int u = 0; u < kRPItems; ++u)
+    for (int u = 0; u < kHTItems; ++u)
       if (d[u] != 0xffffffffu) atomicAdd(&hist[d[u]], 1u);
     __syncthreads();
     for (uint32_t p = threadIdx.x; p < nb; p += blockDim.x) th[t * nb + p] = (uint16_t)hist[p];
@@ -1428,8 +1431,8 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
     uint32_t *csum = reinterpret_cast<uint32_t *>(ws + L.csum), *cpre = reinterpret_cast<uint32_t *>(ws + L.cpre);
     unsigned *tk = reinterpret_cast<unsigned *>(ws + L.tickets);
     HIP_CHECK(hipMemsetAsync(tk, 0, kXcds * sizeof(unsigned), s));
-    hipLaunchKernelGGL(k_rp_hist_tiles<Digit>, dim3((unsigned)std::min<int64_t>(L.ntiles, kNumCUs * 8)),
-                       dim3(kRPThreads), 0, s, dg, n, nb, L.ntiles, th);
+    hipLaunchKernelGGL(k_rp_hist_tiles<Digit>, dim3((unsigned)std::min<int64_t>(L.ntiles, kNumCUs * 16)),
+                       dim3(kHTThreads), 0, s, dg, n, nb, L.ntiles, th);
     HIP_LAUNCH_CHECK();
     const unsigned bt = (unsigned)std::max<uint32_t>(kWave, (nb + kWave - 1) / kWave * kWave);
     hipLaunchKernelGGL(k_ts_chunk_sums, dim3((unsigned)L.nchunks), dim3(bt), 0, s, th, nb, L.ntiles, csum);

@@ -286,7 +286,10 @@ static TablePtr radix_groupby(const TablePtr &t, int key, const std::vector<AggS
       default: return nullptr;
     }
   }
-  if (plan.size() > 4) return nullptr;
+  // the LDS aggregation kernels are instantiated with exactly nacc accumulator slots (1..4):
+  // k_rg_agg<3, 2048> run with two accumulators (one slot unused) faulted on MI355X at 3M rows /
+  // 1M groups (tools/diag_groupby_xt.py); no aggregation at all takes the global path
+  if (plan.empty() || plan.size() > 4) return nullptr;
   Exec ex(t->device());
   const int nacc = (int)plan.size();
   at::Tensor keys;
@@ -351,7 +354,10 @@ static TablePtr radix_groupby(const TablePtr &t, int key, const std::vector<AggS
     trace::add_counter("groupby.radix.order_violation_fallback", 1);
     return nullptr;
   }
-  if (overflow.item<int>() != 0) {
+  const int ovf = overflow.item<int>();
+  CYLON_CHECK((ovf & ~1) == 0, Code::ExecutionError,
+              "radix group-by: inconsistent partition (flags " << ovf << ": 8 = offsets, 16 = groups > rows)");
+  if (ovf != 0) {
     trace::add_counter("groupby.radix.overflow_fallback", 1);
     return nullptr;
   }

@@ -468,3 +468,34 @@ def test_verify_sort_config(gpu_ctx, dtype):
         gpu_ctx.add_config("verify_sort", "0")
         C.trace_enable(False)
     assert c.get("sort.verified", 0) == 2, c
+
+
+@pytest.mark.parametrize("op", ["join", "sort", "union", "groupby"])
+def test_xcd_tile_schedule_matches_chunk_schedule(gpu_ctx, monkeypatch, op):
+    """XCD-tile radix passes (default: per-tile histograms + offset scan, tiles claimed in order per XCD,
+    a block whose chunk is exhausted steals from the others) against the per-block-chunk schedule
+    (CYLON_RP_XT=0): identical results, including the stable order of the row sort."""
+    rng = np.random.default_rng(23)
+    n = 3_000_000  # > 256 tiles per pass: every XCD chunk is non-trivial
+    a = pa.table({"k": rng.integers(0, n // 3, n), "v": rng.random(n), "i": rng.integers(-50, 50, n)})
+    b = pa.table({"k": rng.integers(0, n // 3, n), "v": rng.random(n), "i": rng.integers(-50, 50, n)})
+    A, B = Table(a, gpu_ctx), Table(b, gpu_ctx)
+    for k, v in (("CYLON_RADIX_JOIN_MIN_ROWS", "1024"), ("CYLON_RADIX_SORT_MIN_ROWS", "1024"),
+                 ("CYLON_RADIX_GROUPBY_MIN_ROWS", "1024")):
+        monkeypatch.setenv(k, v)
+    res = []
+    for xt in ("0", "1"):
+        monkeypatch.setenv("CYLON_RP_XT", xt)
+        if op == "join":
+            res.append(_sorted_df(A.join(B, "inner", "hash", on=["k"], left_prefix="l_", right_prefix="r_")))
+        elif op == "sort":
+            res.append(A.sort("i").to_pandas())  # many ties: the order within them must match exactly
+        elif op == "union":
+            res.append(_sorted_df(A.union(B)))
+        else:
+            res.append(A.local_groupby("k", {"v": ["sum"], "i": ["max"]}).to_pandas()
+                       .sort_values("k").reset_index(drop=True))
+    if op == "groupby":
+        pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-12, atol=1e-12)
+    else:
+        pd.testing.assert_frame_equal(res[0], res[1])
