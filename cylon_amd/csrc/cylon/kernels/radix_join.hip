@@ -452,26 +452,32 @@ __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) 
 
 // ---- XCD-tile mode (XT) offsets: per-tile bucket counts, then exact output rows per (tile, bucket)
 // th[t][p]: rows of bucket p in kRPTile-row tile t (uint16: a tile has <= 8192 rows).  512-thread
-// blocks (up to four per CU), 16 rows per thread with every key load issued before the first LDS
-// atomic: the kernel streams the keys at the CU's share of HBM instead of one round trip per tile.
+// blocks (up to four per CU), 16 rows per thread; the next tile's digits are loaded while this
+// tile's LDS atomics and counter writes run, so the key stream never waits on the histogram.
 constexpr int kHTThreads = 512, kHTItems = kRPTile / kHTThreads;
+template <class Digit>
+__device__ __forceinline__ void ht_load(const Digit &digit, int64_t n, int64_t t, int64_t ntiles,
+                                        uint32_t (&d)[kHTItems]) {
+  const int64_t r0 = t * kRPTile;
+#pragma unroll
+  for (int u = 0; u < kHTItems; ++u) {
+    const int64_t i = r0 + u * kHTThreads + threadIdx.x;
+    d[u] = t < ntiles && i < n ? digit(i) : 0xffffffffu;
+  }
+}
 template <class Digit>
 __global__ __launch_bounds__(kHTThreads) void k_rp_hist_tiles(Digit digit, int64_t n, uint32_t nb, int64_t ntiles,
                                                               uint16_t *__restrict__ th) {
   __shared__ unsigned int hist[kRPMaxBuckets];
+  uint32_t d[kHTItems];
+  ht_load(digit, n, blockIdx.x, ntiles, d);
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int64_t r0 = t * kRPTile;
-    uint32_t d[kHTItems];
-#pragma unroll
-    for (int u = 0; u < kHTItems; ++u) {
-      const int64_t i = r0 + u * kHTThreads + threadIdx.x;
-      d[u] = i < n ? digit(i) : 0xffffffffu;
-    }
     for (uint32_t p = threadIdx.x; p < nb; p += blockDim.x) hist[p] = 0;
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < kHTItems; ++u)
       if (d[u] != 0xffffffffu) atomicAdd(&hist[d[u]], 1u);
+    ht_load(digit, n, t + gridDim.x, ntiles, d);  // next tile in flight during the flush
     __syncthreads();
     for (uint32_t p = threadIdx.x; p < nb; p += blockDim.x) th[t * nb + p] = (uint16_t)hist[p];
     __syncthreads();
