@@ -2050,7 +2050,14 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict
 #pragma unroll
     for (int u = 0; u < kRJProbeRounds; ++u)
       if (s0 + u * kWave + lane < s1) c += rj_count(bst, skeys, pk[u]);
-    for (int64_t l = s0 + kRJProbeRounds * kWave + lane; l < s1; l += kWave) c += rj_count(bst, skeys, pkeys[l]);
+    {  // later rounds' probe keys two rounds at a time (both loads in flight before either count)
+      int64_t l = s0 + kRJProbeRounds * kWave + lane;
+      for (; l + kWave < s1; l += 2 * kWave) {
+        const KT ka = pkeys[l], kb = pkeys[l + kWave];
+        c += rj_count(bst, skeys, ka) + rj_count(bst, skeys, kb);
+      }
+      if (l < s1) c += rj_count(bst, skeys, pkeys[l]);
+    }
     for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
     if (lane == 0) wtot[wave] = c;
     __syncthreads();
@@ -2070,25 +2077,30 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict
     }
     for (int w = 0; w < wave; ++w) base += wtot[w];
     RP_STAMP(3);
-    // ---- phase D: emit
+    // ---- phase D: emit.  Round u + 1's probe row is loaded while round u expands (kn / vn), so
+    // only the first round after the phase-A prefetch waits on memory.
+    static_assert(kRJProbeRounds == 1, "emit prefetch assumes one phase-A round");
+    KT kn = 0;
+    uint64_t vn[MAXP] = {};
     for (int u = 0; s0 + (int64_t)u * kWave < s1; ++u) {
       const int64_t l = s0 + (int64_t)u * kWave + lane;
       const bool active = l < s1;
       KT k = 0;
       uint64_t v[MAXP] = {};
-      if (u < kRJProbeRounds) {
+      if (u == 0) {
+        k = pk[0];
 #pragma unroll
-        for (int uu = 0; uu < kRJProbeRounds; ++uu)
-          if (uu == u) {
-            k = pk[uu];
+        for (int q = 0; q < MAXP; ++q) v[q] = pv[0][q];
+      } else {
+        k = kn;
 #pragma unroll
-            for (int q = 0; q < MAXP; ++q) v[q] = pv[uu][q];
-          }
-      } else if (active) {
-        k = pkeys[l];
+        for (int q = 0; q < MAXP; ++q) v[q] = vn[q];
+      }
+      if (l + kWave < s1) {  // prefetch round u + 1
+        kn = pkeys[l + kWave];
 #pragma unroll
         for (int q = 0; q < MAXP; ++q)
-          if (q < pc.n && q != pkey) v[q] = ldw<W8>(pc.in[q], l, pc.width[q]);
+          if (q < pc.n && q != pkey) vn[q] = ldw<W8>(pc.in[q], l + kWave, pc.width[q]);
       }
       uint32_t i0 = 0, i1 = 0, mc = 0;
       if (active) {
