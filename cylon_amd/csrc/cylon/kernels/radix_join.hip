@@ -1399,7 +1399,8 @@ static Lookback lb_args(int64_t *lbws, int pass, int max_digit_bits) {
 template <class Digit, bool CAN_UNSTABLE = std::is_same<Digit, PartDigit>::value>
 static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const uint8_t *const *in, uint8_t *const *out,
                              const int *widths, int ncols, int64_t *ws, void *stream, uint64_t key_xor = 0,
-                             bool stable = true, int64_t *lbws = nullptr, int lb_pass = 0, int lb_bits = 0) {
+                             bool stable = true, int64_t *lbws = nullptr, int lb_pass = 0, int lb_bits = 0,
+                             bool tiles_prescanned = false) {
   if (n == 0) return;
   CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
   CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
@@ -1430,6 +1431,7 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   const int64_t *bh_scan = nullptr;
   Lookback lb{};
   const bool xt = !lbm && threads == 1024 && n < (int64_t(1) << 32) && rp_xt();
+  if (!xt) tiles_prescanned = false;  // histogram mode counts its own blocks (the prescan is unused)
   if (xt) {  // exact per-tile offsets, tiles claimed in order per XCD (see xt_claim)
     const XtLayout L = xt_layout(n, nb);
     uint16_t *th = reinterpret_cast<uint16_t *>(ws + L.th);
@@ -1437,9 +1439,11 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
     uint32_t *csum = reinterpret_cast<uint32_t *>(ws + L.csum), *cpre = reinterpret_cast<uint32_t *>(ws + L.cpre);
     unsigned *tk = reinterpret_cast<unsigned *>(ws + L.tickets);
     HIP_CHECK(hipMemsetAsync(tk, 0, kXcds * sizeof(unsigned), s));
-    hipLaunchKernelGGL(k_rp_hist_tiles<Digit>, dim3((unsigned)std::min<int64_t>(L.ntiles, kNumCUs * 16)),
-                       dim3(kHTThreads), 0, s, dg, n, nb, L.ntiles, th);
-    HIP_LAUNCH_CHECK();
+    if (!tiles_prescanned) {  // else the caller already wrote th (radix_sort_prehist + fold)
+      hipLaunchKernelGGL(k_rp_hist_tiles<Digit>, dim3((unsigned)std::min<int64_t>(L.ntiles, kNumCUs * 16)),
+                         dim3(kHTThreads), 0, s, dg, n, nb, L.ntiles, th);
+      HIP_LAUNCH_CHECK();
+    }
     const unsigned bt = (unsigned)std::max<uint32_t>(kWave, (nb + kWave - 1) / kWave * kWave);
     hipLaunchKernelGGL(k_ts_chunk_sums, dim3((unsigned)L.nchunks), dim3(bt), 0, s, th, nb, L.ntiles, csum);
     HIP_LAUNCH_CHECK();
@@ -1606,10 +1610,96 @@ void radix_narrow_rows_pass(const void *keys, int key_bytes, int64_t n, int tota
 
 void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_bits, const uint8_t *const *in,
                           uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream,
-                          uint64_t key_xor, uint64_t digit_flip, int64_t *lbws, int lb_pass, int lb_bits) {
+                          uint64_t key_xor, uint64_t digit_flip, int64_t *lbws, int lb_pass, int lb_bits,
+                          bool tiles_prescanned) {
   const uint32_t nb = 1u << digit_bits;
   rows_pass_launch(ImageDigit{keys, shift, nb - 1, digit_flip}, n, digit_bits, in, out, widths, ncols, ws, stream,
-                   key_xor, true, lbws, lb_pass, lb_bits);
+                   key_xor, true, lbws, lb_pass, lb_bits, tiles_prescanned);
+}
+
+bool radix_xt_enabled() { return rp_xt(); }
+
+// ---- sort prologue: the keys' varying bits (OR ^ AND) and the first pass's per-tile histogram of
+// the order image's low 10 bits in ONE read of the keys (the separate reduction read them once more)
+constexpr int kSPBits = 10;
+__global__ __launch_bounds__(kHTThreads) void k_sort_prehist(const int64_t *__restrict__ keys, int64_t n,
+                                                             uint64_t flip, int64_t ntiles, uint16_t *__restrict__ th,
+                                                             unsigned long long *__restrict__ orand) {
+  constexpr uint32_t nb = 1u << kSPBits;
+  __shared__ unsigned int hist[nb];
+  uint64_t o = 0, a = ~0ull;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    uint64_t k[kHTItems];
+    const int64_t r0 = t * kRPTile;
+#pragma unroll
+    for (int u = 0; u < kHTItems; ++u) {
+      const int64_t i = r0 + u * kHTThreads + threadIdx.x;
+      k[u] = i < n ? (uint64_t)keys[i] : 0ull;
+    }
+    for (uint32_t p = threadIdx.x; p < nb; p += blockDim.x) hist[p] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kHTItems; ++u)
+      if (r0 + u * kHTThreads + threadIdx.x < n) {
+        o |= k[u];
+        a &= k[u];
+        atomicAdd(&hist[(uint32_t)((k[u] ^ flip) & (nb - 1))], 1u);
+      }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < nb; p += blockDim.x) th[t * nb + p] = (uint16_t)hist[p];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    o |= rj_shfl_xor64((long long)o, d);
+    a &= rj_shfl_xor64((long long)a, d);
+  }
+  if (lane_id() == 0) {
+    atomicOr(&orand[0], (unsigned long long)o);
+    atomicAnd(&orand[1], (unsigned long long)a);
+  }
+}
+
+// th[t][d] (2^db buckets) from the 10-bit histogram: digits that agree in their low db bits
+__global__ void k_sort_prehist_fold(const uint16_t *__restrict__ th10, int64_t ntiles, int db,
+                                    uint16_t *__restrict__ th) {
+  const uint32_t nb = 1u << db, groups = 1u << (kSPBits - db);
+  const int64_t cells = ntiles * nb, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < cells; c += stride) {
+    const int64_t t = c / nb;
+    const uint32_t d = (uint32_t)(c % nb);
+    uint32_t sum = 0;
+    for (uint32_t g = 0; g < groups; ++g) sum += th10[t * (1 << kSPBits) + d + (g << db)];
+    th[c] = (uint16_t)sum;
+  }
+}
+
+int64_t radix_sort_prehist_workspace(int64_t n) { return xt_layout(n, 1u << kSPBits).words + 2; }
+
+uint64_t radix_sort_prehist(const int64_t *keys, int64_t n, uint64_t flip, int64_t *pre_ws, void *stream) {
+  hipStream_t s = as_stream(stream);
+  const XtLayout L = xt_layout(n, 1u << kSPBits);
+  unsigned long long *orand = reinterpret_cast<unsigned long long *>(pre_ws + L.words);
+  const unsigned long long init[2] = {0ull, ~0ull};
+  HIP_CHECK(hipMemcpyAsync(orand, init, sizeof(init), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_sort_prehist, dim3((unsigned)std::min<int64_t>(L.ntiles, kNumCUs * 16)), dim3(kHTThreads), 0,
+                     s, keys, n, flip, L.ntiles, reinterpret_cast<uint16_t *>(pre_ws + L.th), orand);
+  HIP_LAUNCH_CHECK();
+  unsigned long long h[2];
+  HIP_CHECK(hipMemcpyAsync(h, orand, sizeof(h), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return n <= 1 ? 0ull : (uint64_t)(h[0] ^ h[1]);
+}
+
+void radix_sort_prehist_fold(const int64_t *pre_ws, int64_t n, int db, int64_t *ws, void *stream) {
+  CYLON_CHECK(db >= 1 && db <= kSPBits, Code::Invalid, "sort prehist fold: digit bits " << db);
+  const XtLayout P = xt_layout(n, 1u << kSPBits), L = xt_layout(n, 1u << db);
+  const uint16_t *th10 = reinterpret_cast<const uint16_t *>(pre_ws + P.th);
+  uint16_t *th = reinterpret_cast<uint16_t *>(ws + L.th);
+  const int64_t cells = L.ntiles * (int64_t(1) << db);
+  hipLaunchKernelGGL(k_sort_prehist_fold, dim3(grid_for(cells)), dim3(kBlock), 0, as_stream(stream), th10, L.ntiles,
+                     db, th);
+  HIP_LAUNCH_CHECK();
 }
 
 void radix_range_rows_pass(const int64_t *keys, int64_t n, uint64_t flip, uint64_t mn, int rshift, int shift,

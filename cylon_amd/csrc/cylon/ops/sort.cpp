@@ -156,9 +156,22 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
                       kc.data.element_size() == 8;
   at::Tensor img = raw_in ? kc.data : ex.empty_i64(n);
   at::Tensor ws2 = ex.empty_i64(2);
-  const uint64_t diff = hip::sort_keys_varying_bits(
-      kc.view(), n, !asc, raw_in ? nullptr : reinterpret_cast<uint64_t *>(ptr<int64_t>(img)), ptr<int64_t>(ws2),
-      ex.stream);
+  // raw 8-byte integer keys on the XCD-tile passes: one read gives the varying bits AND the first
+  // pass's per-tile histogram (bits [0, 10) of the image), folded below when the pass digit starts
+  // at bit 0 -- the separate reduction read every key once more (3.3 ms of a 2B-row sort)
+  const char *ph = std::getenv("CYLON_SORT_PREHIST");  // A/B knob: 0 = separate reduction + histogram
+  const bool prehist = raw_in && n > 0 && hip::radix_xt_enabled() && !hip::radix_lookback_enabled() &&
+                       !(ph && ph[0] == '0');
+  at::Tensor pre_ws;
+  uint64_t diff;
+  if (prehist) {
+    pre_ws = ex.empty_i64(hip::radix_sort_prehist_workspace(n));
+    diff = hip::radix_sort_prehist(ptr<int64_t>(kc.data), n, key_xor, ptr<int64_t>(pre_ws), ex.stream);
+  } else {
+    diff = hip::sort_keys_varying_bits(kc.view(), n, !asc,
+                                       raw_in ? nullptr : reinterpret_cast<uint64_t *>(ptr<int64_t>(img)),
+                                       ptr<int64_t>(ws2), ex.stream);
+  }
   std::vector<at::Tensor> cur{img};
   std::vector<int> widths{8};
   for (int ci = 0; ci < t->Columns(); ++ci) {
@@ -217,10 +230,13 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
       // raw_in: the first pass ranks key ^ key_xor and stores it (raw -> image); the last
       // pass XORs again (image -> raw); one pass does both (stores the raw key)
       const uint64_t flip = ps == 0 && raw_in ? key_xor : 0ull;
+      const bool pre = prehist && ps == 0 && shift == 0 && db <= 10 && !lbm;
+      if (pre) hip::radix_sort_prehist_fold(ptr<int64_t>(pre_ws), n, db, ptr<int64_t>(ws), ex.stream);
       hip::radix_sort_rows_pass(ptr<int64_t>(cur[0]), n, shift, db, in.data(), out.data(), widths.data(),
                                 (int)cur.size(), ptr<int64_t>(ws), ex.stream,
                                 flip ^ (ps + 1 == npass && key_in_last_pass ? key_xor : 0ull), flip,
-                                lbm ? ptr<int64_t>(lbws) : nullptr, ps, max_db);
+                                lbm ? ptr<int64_t>(lbws) : nullptr, ps, max_db, pre);
+      if (ps == 0) pre_ws = at::Tensor();  // 10-bit tile histogram consumed
       cur = std::move(nxt);
       shift += db;
     }
