@@ -105,25 +105,15 @@ __device__ __forceinline__ void stw(uint8_t *p, int64_t i, int w, uint64_t v) {
 // --------------------------------------------------------------------------
 // partition pass
 // --------------------------------------------------------------------------
-// NARROW (narrow-key join, join.cpp radix_join): the two relations' keys span < 2^32 values, so
-// a key's low 32 bits identify it; the partition hash is taken over those bits and column 0
-// (the key) leaves the pass as uint32 -- 4 B/row less in every later pass and in the join
-// kernels.  K = int64_t: the first pass reads the original keys; K = uint32_t: later passes.
-template <class K, bool NARROW>
-struct PartDigitT {
-  static constexpr bool kNarrow = NARROW;  // column 0 is stored as uint32
-  const K *keys;
+// Join digit: bits [shift, shift + log2(mask+1)) of the top `bits` bits of fmix64(key).
+struct PartDigit {
+  const int64_t *keys;
   int bits;   // total partition bits
   int shift;  // digit = (part >> shift) & mask
   uint32_t mask;
-  __device__ __forceinline__ uint32_t of_key(int64_t k) const {
-    return (part_of(NARROW ? (int64_t)(uint32_t)(uint64_t)k : k, bits) >> shift) & mask;
-  }
-  __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key((int64_t)keys[i]); }
+  __device__ __forceinline__ uint32_t of_key(int64_t k) const { return (part_of(k, bits) >> shift) & mask; }
+  __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key(keys[i]); }
 };
-using PartDigit = PartDigitT<int64_t, false>;
-using PartDigitN64 = PartDigitT<int64_t, true>;   // first narrow pass: int64 keys in, uint32 out
-using PartDigitN32 = PartDigitT<uint32_t, true>;  // later narrow passes
 
 
 // Shuffle digit: the reference's partition of a single 8-byte integer key
@@ -131,7 +121,6 @@ using PartDigitN32 = PartDigitT<uint32_t, true>;  // later narrow passes
 // of two; partition.hip partition_f + hashing::partitioner), so one LDS-staged
 // pass produces the partition-major order of the whole table.
 struct ModDigit {
-  static constexpr bool kNarrow = false;
   const int64_t *keys;
   uint32_t nparts;
   __device__ __forceinline__ uint32_t of_key(int64_t k) const {
@@ -142,7 +131,6 @@ struct ModDigit {
 
 // Sort digit: bits [shift, shift + log2(mask+1)) of an order-preserving uint64 image (K6).
 struct ImageDigit {
-  static constexpr bool kNarrow = false;
   const int64_t *keys;
   int shift;
   uint32_t mask;
@@ -157,7 +145,6 @@ struct ImageDigit {
 // ((k ^ flip) - mn) >> rshift -- key ranges in key order -- and a pass's digit is
 // bits [shift, shift + log2(mask + 1)) of that partition id.
 struct RangeDigit {
-  static constexpr bool kNarrow = false;
   const int64_t *keys;
   uint64_t flip, mn;
   int rshift, shift;
@@ -192,64 +179,8 @@ __global__ __launch_bounds__(kRPThreads) void k_rp_hist(Digit digit, int64_t n, 
   for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) bh[(int64_t)p * nblocks + blockIdx.x] = hist[p];
 }
 
-// k_rp_hist of a narrow-key join's first pass (low-32-bit digit) that also reduces the int64
-// keys' min and max into mm[0] / mm[1] (atomics, initialised by the caller): the join decides
-// from both relations' ranges whether the narrow passes apply, before the first pass runs.
-__global__ __launch_bounds__(kRPThreads) void k_rp_hist_minmax(PartDigitN64 digit, int64_t n, uint32_t nbuckets,
-                                                               int64_t rows_per_block, int64_t nblocks,
-                                                               int64_t *__restrict__ bh, long long *__restrict__ mm) {
-  __shared__ unsigned int hist[kRPMaxBuckets];
-  for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) hist[p] = 0;
-  __syncthreads();
-  const int64_t begin = (int64_t)blockIdx.x * rows_per_block;
-  const int64_t end = (begin + rows_per_block < n) ? begin + rows_per_block : n;
-  long long lo = LLONG_MAX, hi = LLONG_MIN;
-  for (int64_t i0 = begin; i0 < end; i0 += 4 * kRPThreads) {
-    int64_t k[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t i = i0 + u * kRPThreads + threadIdx.x;
-      k[u] = i < end ? digit.keys[i] : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (i0 + u * kRPThreads + threadIdx.x < end) {
-        atomicAdd(&hist[digit.of_key(k[u])], 1u);
-        lo = k[u] < lo ? k[u] : lo;
-        hi = k[u] > hi ? k[u] : hi;
-      }
-  }
-  for (int d = kWave / 2; d > 0; d >>= 1) {
-    const long long a = rj_shfl_xor64(lo, d), b = rj_shfl_xor64(hi, d);
-    lo = a < lo ? a : lo;
-    hi = b > hi ? b : hi;
-  }
-  if (lane_id() == 0 && lo <= hi) {
-    atomicMin(&mm[0], lo);
-    atomicMax(&mm[1], hi);
-  }
-  __syncthreads();
-  for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) bh[(int64_t)p * nblocks + blockIdx.x] = hist[p];
-}
-
-// Chained-scan passes (decoupled lookback).  Histogram mode runs k_rp_hist before every pass:
-// it re-reads the keys (8 B/row, 15 % of a key-only sort) to give each block's contiguous chunk
-// its bucket offsets.  Lookback mode counts every pass's digits ONCE (k_lb_hist: the counts of a
-// digit do not depend on the row order) and lets the pass kernel find a tile's offsets itself:
-// tiles are claimed in row order from a ticket counter; a tile publishes its per-bucket count,
-// then sums its predecessors' published counts back to the nearest tile that already published
-// an inclusive prefix, and publishes its own.  Status words are 64-bit (flag | pass epoch | rows)
-// relaxed agent-scope atomics: the value travels with its flag, so no fence is needed, and a
-// word left by an earlier pass of the same session (other epoch) reads as "not ready".
-constexpr int kLbMaxPasses = 8;
-constexpr unsigned long long kLbAgg = 1ull << 62, kLbPrefix = 2ull << 62, kLbValue = (1ull << 56) - 1;
-
-struct Lookback {
-  const int64_t *gstart;         // exclusive global start of every bucket of this pass
-  unsigned long long *status;    // [tile][nbuckets]
-  unsigned int *ticket;          // next tile to claim
-  unsigned long long epoch;      // 1..63
-  // XCD-tile mode (XT): per-tile bucket offsets and one ticket per XCD (see k_rp_hist_tiles)
+// Tile schedule of the XCD-tile passes: per-tile bucket offsets and one ticket per XCD.
+struct TileSched {
   const uint32_t *xt_off;        // [tile][nbuckets] output row of the tile's first row of each bucket
   unsigned int *xt_ticket;       // [8] next tile of each XCD's contiguous chunk
   int64_t xt_tiles;              // tiles of the pass
@@ -271,7 +202,7 @@ __device__ __forceinline__ int xcc_id() {
   return x & (kXcds - 1);
 }
 // first row of the next tile this block processes, or n_rows when every chunk is exhausted
-__device__ __forceinline__ int64_t xt_claim(const Lookback &lb, int home, int64_t tile_rows, int64_t n_rows) {
+__device__ __forceinline__ int64_t xt_claim(const TileSched &lb, int home, int64_t tile_rows, int64_t n_rows) {
   for (int k = 0; k < kXcds; ++k) {
     const int x = (home + k) & (kXcds - 1);
     const int64_t lo = lb.xt_tiles * x / kXcds, hi = lb.xt_tiles * (x + 1) / kXcds;
@@ -280,100 +211,6 @@ __device__ __forceinline__ int64_t xt_claim(const Lookback &lb, int home, int64_
     if (lo + j < hi) return (lo + j) * tile_rows;
   }
   return n_rows;
-}
-
-// Windowed lookback in two steps: lb_publish stores tile t's count of bucket p right after the
-// scan (successors can sum it while this tile ranks its slots); lb_exclusive then reads its
-// predecessors' words kLbWin at a time (independent loads, one round trip per window),
-// consumes them in order (waiting for any tile not ranked yet) until it meets an inclusive
-// prefix, publishes t's own prefix and returns the rows of bucket p in tiles < t plus the
-// bucket's global start.  One dependent load per predecessor cost the key-only sort ~50 % per
-// pass: hundreds of tiles are in flight, and the walk back to the nearest prefix is long.  The
-// window is not held across the slot phase (the loads' registers spill there).
-constexpr int kLbWin = 8;
-
-__device__ __forceinline__ unsigned long long lb_load(const unsigned long long *w) {
-  return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lb_store(unsigned long long *w, unsigned long long v) {
-  __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void lb_publish(const Lookback &lb, uint32_t nb, int64_t t, uint32_t p, uint32_t cnt) {
-  const unsigned long long tag = lb.epoch << 56;
-  if (t == 0) lb_store(lb.status + p, kLbPrefix | tag | (unsigned long long)(lb.gstart[p] + cnt));
-  else lb_store(lb.status + t * nb + p, kLbAgg | tag | cnt);
-}
-
-__device__ __forceinline__ int64_t lb_exclusive(const Lookback &lb, uint32_t nb, int64_t t, uint32_t p, uint32_t cnt) {
-  if (t == 0) return lb.gstart[p];
-  int64_t excl = 0;
-  for (int64_t j = t - 1;; j -= kLbWin) {
-    unsigned long long v[kLbWin];
-#pragma unroll
-    for (int w = 0; w < kLbWin; ++w) v[w] = j - w >= 0 ? lb_load(lb.status + (j - w) * nb + p) : 0ull;
-    bool found = false;
-#pragma unroll
-    for (int w = 0; w < kLbWin; ++w) {
-      if (found || j - w < 0) continue;  // tile 0 always holds a prefix: the walk ends there at the latest
-      unsigned long long x = v[w];
-      while (((x >> 56) & 63ull) != lb.epoch) {  // tile j - w not ranked yet (its block is running)
-        __builtin_amdgcn_s_sleep(1);
-        x = lb_load(lb.status + (j - w) * nb + p);
-      }
-      excl += (int64_t)(x & kLbValue);
-      found = (x & kLbPrefix) != 0;
-    }
-    if (found) break;
-  }
-  lb_store(lb.status + t * nb + p, kLbPrefix | (lb.epoch << 56) | (unsigned long long)(excl + cnt));
-  return excl;
-}
-
-template <class Digit>
-struct DigitSet {
-  Digit d[kLbMaxPasses];
-  int n;
-};
-
-// every pass's digit histogram in one read of the keys: hist[s][p] (u64, accumulated)
-template <class Digit>
-__global__ __launch_bounds__(kRPThreads) void k_lb_hist(DigitSet<Digit> ds, int64_t n, uint32_t nb,
-                                                        unsigned long long *__restrict__ gh) {
-  __shared__ unsigned int hist[kLbMaxPasses * kRPMaxBuckets];
-  for (uint32_t q = threadIdx.x; q < (uint32_t)ds.n * nb; q += blockDim.x) hist[q] = 0;
-  __syncthreads();
-  const int64_t *keys = ds.d[0].keys;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const int64_t k = keys[i];
-#pragma unroll
-    for (int s = 0; s < kLbMaxPasses; ++s)
-      if (s < ds.n) atomicAdd(&hist[s * nb + ds.d[s].of_key(k)], 1u);
-  }
-  __syncthreads();
-  for (uint32_t q = threadIdx.x; q < (uint32_t)ds.n * nb; q += blockDim.x)
-    if (hist[q]) atomicAdd(&gh[q], (unsigned long long)hist[q]);
-}
-
-// gstart[s][p] = exclusive scan of hist[s][.] (one block per pass)
-__global__ __launch_bounds__(kRPThreads) void k_lb_scan(const unsigned long long *__restrict__ gh, uint32_t nb,
-                                                        int64_t *__restrict__ gstart) {
-  __shared__ int64_t wsum[kRPWaves];
-  const int s = blockIdx.x, lane = lane_id(), wave = threadIdx.x / kWave;
-  const uint32_t p = threadIdx.x;
-  const int64_t c = p < nb ? (int64_t)gh[s * nb + p] : 0;
-  int64_t inc = c;
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const int64_t t = __shfl_up(inc, d, kWave);
-    if (lane >= d) inc += t;
-  }
-  if (lane == kWave - 1) wsum[wave] = inc;
-  __syncthreads();
-  int64_t off = 0;
-  for (int w = 0; w < wave; ++w) off += wsum[w];
-  if (p < nb) gstart[s * nb + p] = off + inc - c;
 }
 
 // LDS-DMA of `bytes` (a multiple of 4) contiguous global bytes into LDS at dst (16-byte aligned)
@@ -393,47 +230,8 @@ __device__ __forceinline__ void rj_dma_block(const uint8_t *src, int bytes, uint
                                      (__attribute__((address_space(3))) void *)(dst + t0 * 4), 4, 0, 0);
 }
 
-// The same DMA issued from inline asm (the recipe of cdna_hip_programming.md §4): hipcc then keeps
-// no bookkeeping for it, so it does not drain it with vmcnt(0) before every later LDS access (it
-// cannot tell the DMA's destination from the ranking counters) -- the caller waits for it with an
-// explicit s_waitcnt before the buffer is read.  lds_base: the buffer's LDS byte address.
-template <int WAVES>
-__device__ __forceinline__ void rp_dma_asm(const uint8_t *src, int bytes, uint32_t lds_base, int wave, int lane) {
-  const int nq = bytes >> 4;
-  for (int c0 = wave * kWave; c0 < nq; c0 += WAVES * kWave) {
-    const uint32_t dst = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds_base + (uint32_t)c0 * 16u));
-    if (c0 + lane < nq) {
-      const uint8_t *g = src + (int64_t)(c0 + lane) * 16;
-      unsigned keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(g), "s"(dst) : "memory");
-    }
-  }
-  const int t0 = nq << 2, nd = bytes >> 2;  // tail dwords (at most 3)
-  if (wave == WAVES - 1 && t0 + lane < nd) {
-    const uint32_t dst = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds_base + (uint32_t)t0 * 4u));
-    const uint8_t *g = src + (int64_t)(t0 + lane) * 4;
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(dst) : "memory");
-  }
-}
-
-// Block barrier.  RAW: LDS-only (lgkmcnt(0) + s_barrier) -- an LDS-DMA in flight stays in
-// flight (__syncthreads() waits vmcnt(0) while one is outstanding: cdna_hip_programming.md §5).
-template <bool RAW>
-__device__ __forceinline__ void rp_sync() {
-  if (RAW) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  } else {
-    __syncthreads();
-  }
-}
-
 // block-wide exclusive scan of one uint32 per thread (WAVES waves)
-template <int WAVES = kRPWaves, bool RAW = false>
+template <int WAVES = kRPWaves>
 __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) {
   const int lane = lane_id(), wave = threadIdx.x / kWave;
   uint32_t inc = c;
@@ -443,7 +241,7 @@ __device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) 
     if (lane >= d) inc += t;
   }
   if (lane == kWave - 1) wsum[wave] = inc;
-  rp_sync<RAW>();
+  __syncthreads();
   uint32_t off = 0;
 #pragma unroll
   for (int w = 0; w < WAVES; ++w) off += (w < wave) ? wsum[w] : 0u;
@@ -523,14 +321,16 @@ __global__ __launch_bounds__(kRPThreads) void k_ts_chunk_prefix(const uint32_t *
   if (p < nb) bbase[p] = base;
 }
 
-// off[t][p] = output row of tile t's first row of bucket p
+// off[t][p] = output row of tile t's first row of bucket p.  extra (optional, gapped layouts of the
+// planned shuffle): rows of free space placed before bucket p, so a bucket can be followed by a
+// receive region of the exchange (ops/shuffle.cpp planned_shuffle).
 __global__ void k_ts_offsets(const uint16_t *__restrict__ th, const uint32_t *__restrict__ cpre,
                              const uint32_t *__restrict__ bbase, uint32_t nb, int64_t ntiles,
-                             uint32_t *__restrict__ off) {
+                             uint32_t *__restrict__ off, const uint32_t *__restrict__ extra) {
   const int64_t c = blockIdx.x, t0 = c * kTsChunk, t1 = t0 + kTsChunk < ntiles ? t0 + kTsChunk : ntiles;
   const uint32_t p = threadIdx.x;
   if (p >= nb) return;
-  uint32_t acc = cpre[c * nb + p] + bbase[p];
+  uint32_t acc = cpre[c * nb + p] + bbase[p] + (extra != nullptr ? extra[p] : 0u);
 #pragma unroll 8
   for (int64_t t = t0; t < t1; ++t) {
     off[t * nb + p] = acc;
@@ -569,27 +369,18 @@ constexpr int kRPStampTiles = 64, kRPStampSlots = 16;
 // on block-wide counters: unstable), kRankWaveAtomic (LDS atomics on the wave's own packed
 // 16-bit counters: stable exactly when one instruction's same-address atomics return in lane
 // order -- tools/lds_atomic_order.hip measures that on the device).
-// LB: lookback mode (tiles claimed from lb.ticket, offsets by decoupled lookback; bh_scan unused).
-// DMA1 (W8, >= 2 columns, column 1 read from memory): column 1 of the tile is fetched by LDS-DMA
-// into a second 64 KB buffer as soon as the tile's digits are known, so the load streams during the
-// ranking / scan / slot / destination phases (which move no bytes of their own) instead of behind
-// column 0's scatter; those phases then synchronise with LDS-only barriers.
-template <class Digit, bool W8, int THREADS, int RANK, bool LB, bool DMA1 = false, bool XT = false>
+// XT: XCD-tile schedule (tiles claimed in order per XCD, exact per-tile bucket offsets in lb).
+template <class Digit, bool W8, int THREADS, int RANK, bool XT = false>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_rows_pass(
     Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
-    const int64_t *__restrict__ bh_scan, Lookback lb, unsigned long long *__restrict__ stamps) {
+    const int64_t *__restrict__ bh_scan, TileSched lb, unsigned long long *__restrict__ stamps) {
   constexpr int WAVES = THREADS / kWave;
   constexpr int TILE = THREADS * kRPItems;
   constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;  // buckets per thread in the offset scan
-  constexpr bool K4 = Digit::kNarrow;  // column 0 (the key) is stored as uint32
   static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 4 <= TILE * 8, "ranking scratch must fit the stage");
-  static_assert(!LB || (THREADS >= kRPMaxBuckets && TILE == kRPTile), "lookback: one bucket a thread, 8192-row tiles");
-  static_assert(!DMA1 || (W8 && !LB), "column-1 DMA: 8-byte columns, histogram mode");
-  static_assert(!(LB && XT), "one tile schedule");
-  constexpr bool TICKET = LB || XT;  // tiles claimed one by one (not a contiguous chunk per block)
+  constexpr bool TICKET = XT;  // tiles claimed one by one (not a contiguous chunk per block)
   const int xhome = XT ? xcc_id() : 0;
   __shared__ int64_t running[kRPMaxBuckets];
-  __shared__ __attribute__((aligned(16))) uint64_t land[DMA1 ? TILE : 1];  // column 1 of the tile (DMA1)
   __shared__ uint32_t toff[kRPMaxBuckets + 1];
   __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16, sdig[TILE] u32}
   __shared__ uint32_t wsum[WAVES];
@@ -600,13 +391,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   // sorted slot j -> digit << 16 | input row in the tile (the row feeds the ranking guard)
   uint32_t *sdig = reinterpret_cast<uint32_t *>(wcnt + WAVES * kRPMaxBuckets);
   uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
-  __shared__ int64_t s_next;  // LB: first row of the next claimed tile
+  __shared__ int64_t s_next;  // XT: first row of the next claimed tile
   bool order_bad = false;
 
   const int64_t b = blockIdx.x;
   int64_t begin, end;
   if (TICKET) {
-    if (threadIdx.x == 0) s_next = XT ? xt_claim(lb, xhome, TILE, n) : (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
+    if (threadIdx.x == 0) s_next = xt_claim(lb, xhome, TILE, n);
     __syncthreads();
     begin = s_next;
     end = n;
@@ -638,19 +429,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k)
       pl[k] = (wrow + k * kWave + lane < cnt) ? digit.of_key((int64_t)kv[k]) : 0xffffffffu;
-    // the digits consumed the prefetched keys (their loads are retired), so this DMA is the only
-    // vector-memory work in flight through the LDS-only barriers below
-    if (DMA1)
-      rp_dma_asm<WAVES>(cols.in[1] + tile * 8, cnt * 8,
-                        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint64_t *)(land),
-                        wave, lane);
     RP_STAMP(1);
     if (STABLE) {
       for (uint32_t q = threadIdx.x; q < WAVES * nbuckets; q += blockDim.x) wcnt[q] = 0;
     } else {
       for (uint32_t q = threadIdx.x; q < nbuckets; q += blockDim.x) bcnt[q] = 0;
     }
-    rp_sync<DMA1>();  // also orders the previous tile's stage reads before the counters reuse it
+    __syncthreads();  // also orders the previous tile's stage reads before the counters reuse it
     if (!STABLE) {
       // order inside a bucket's run is free (join partitions): one LDS atomic per row
       // replaces the nbits ballots of the stable match
@@ -684,7 +469,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       __builtin_amdgcn_wave_barrier();
       pl[k] = active ? (((base + rank) << 16) | p) : 0xffffffffu;
     }
-    rp_sync<DMA1>();
+    __syncthreads();
     RP_STAMP(2);
     {  // thread owns buckets [t*BPT, t*BPT+BPT): exclusive prefix over waves (in place), then a
        // block scan of the thread totals
@@ -709,7 +494,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         }
         total += run;
       }
-      const uint32_t ex = rp_block_exscan<WAVES, DMA1>(total, wsum);
+      const uint32_t ex = rp_block_exscan<WAVES>(total, wsum);
 #pragma unroll
       for (int i = 0; i < BPT; ++i) {
         const uint32_t p = threadIdx.x * BPT + i;
@@ -717,12 +502,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       }
       if (threadIdx.x == THREADS - 1) toff[nbuckets] = ex + total;
     }
-    rp_sync<DMA1>();
+    __syncthreads();
     RP_STAMP(3);
-    // LB: this tile's bucket offsets from its predecessors (read by the dst phase): count published
-    // before the slot phase, lookback after it.  nbuckets <= THREADS: one bucket a thread
-    const uint32_t lbc = LB && threadIdx.x < nbuckets ? toff[threadIdx.x + 1] - toff[threadIdx.x] : 0u;
-    if (LB && threadIdx.x < nbuckets) lb_publish(lb, nbuckets, tile / TILE, threadIdx.x, lbc);
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k) {
       if (pl[k] == 0xffffffffu) continue;
@@ -731,9 +512,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       sdig[pos] = (p << 16) | (uint32_t)(wrow + k * kWave + lane);
       pl[k] = pos;
     }
-    if (LB && threadIdx.x < nbuckets) running[threadIdx.x] = lb_exclusive(lb, nbuckets, tile / TILE, threadIdx.x, lbc);
     if (XT && threadIdx.x < nbuckets) running[threadIdx.x] = xoff;
-    rp_sync<DMA1>();
+    __syncthreads();
     RP_STAMP(4);
     int64_t dst[kRPItems];  // destination of sorted slot j = threadIdx.x + q * THREADS
 #pragma unroll
@@ -748,7 +528,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         }
       }
     }
-    rp_sync<DMA1>();  // counters / digits dead: the union becomes the column stage
+    __syncthreads();  // counters / digits dead: the union becomes the column stage
     RP_STAMP(5);
     // load column c+1 while column c streams out of the stage
     uint64_t v[kRPItems];
@@ -757,30 +537,16 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll 1
     for (int c = 0; c < cols.n; ++c) {  // column fields fetched once per column (scalar loads)
       const int w = cols.width[c];
-      if (DMA1 && c == 1) {  // column 1 landed by DMA (waited for at the end of column 0)
-#pragma unroll
-        for (int k = 0; k < kRPItems; ++k) v[k] = land[wrow + k * kWave + lane];
-      }
       uint8_t *out = cols.out[c];
       const uint64_t x = c == 0 ? cols.key_xor : 0ull;
-      if (TICKET && c + 1 == cols.n && threadIdx.x == 0)
-        s_next = XT ? xt_claim(lb, xhome, TILE, n) : (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
-      const bool k4 = K4 && c == 0;  // narrow key: column 0 leaves as its low 32 bits
-      if (k4) {
+      if (TICKET && c + 1 == cols.n && threadIdx.x == 0) s_next = xt_claim(lb, xhome, TILE, n);
 #pragma unroll
-        for (int k = 0; k < kRPItems; ++k)
-          if (pl[k] != 0xffffffffu) reinterpret_cast<uint32_t *>(st)[pl[k]] = (uint32_t)v[k];
-      } else {
-#pragma unroll
-        for (int k = 0; k < kRPItems; ++k)
-          if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
-      }
+      for (int k = 0; k < kRPItems; ++k)
+        if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
       __syncthreads();
       if (TICKET && c + 1 == cols.n) next = s_next;
       RP_STAMP(6 + 2 * c);
-      if (DMA1 && c == 0) {
-        // column 1 is in flight by DMA: nothing to prefetch behind column 0
-      } else if (c + 1 < cols.n) {  // prefetch column c+1 of this tile
+      if (c + 1 < cols.n) {  // prefetch column c+1 of this tile
         const uint8_t *in = cols.in[c + 1];
         const int w1 = cols.width[c + 1];
         if (in == nullptr) {  // row-id column: the pass generates it (no 8 B/row array to read)
@@ -798,20 +564,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
           if (i < end) kv[k] = (uint64_t)digit.keys[i];
         }
       }
-      if (k4) {
 #pragma unroll
-        for (int q = 0; q < kRPItems; ++q) {
-          const int j = threadIdx.x + q * THREADS;
-          if (j < cnt) reinterpret_cast<uint32_t *>(out)[dst[q]] = reinterpret_cast<const uint32_t *>(st)[j];
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < kRPItems; ++q) {
-          const int j = threadIdx.x + q * THREADS;
-          if (j < cnt) stw<W8>(out, dst[q], w, ldw<W8>(st, j, w));
-        }
+      for (int q = 0; q < kRPItems; ++q) {
+        const int j = threadIdx.x + q * THREADS;
+        if (j < cnt) stw<W8>(out, dst[q], w, ldw<W8>(st, j, w));
       }
-      if (DMA1 && c == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // column 1 has landed
       __syncthreads();
       RP_STAMP(7 + 2 * c);
     }
@@ -830,10 +587,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 //   * no cross-column / cross-tile prefetch (the second block hides the load latency);
 //   * the destination of sorted slot j is packed as (digit << 16 | j - toff[digit]) and
 //     completed from running[] in LDS at store time (8 VGPRs instead of 16).
-template <class Digit, bool W8, int RANK, bool LB, bool XT = false>
+template <class Digit, bool W8, int RANK, bool XT = false>
 __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_rows_pass_lean(
     Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
-    const int64_t *__restrict__ bh_scan, Lookback lb) {
+    const int64_t *__restrict__ bh_scan, TileSched lb) {
   constexpr int THREADS = kRPThreads, WAVES = THREADS / kWave, TILE = THREADS * kRPItems;
   constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;
   static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 4 <= TILE * 8, "ranking scratch must fit the stage");
@@ -846,17 +603,16 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
   uint32_t *bcnt = reinterpret_cast<uint32_t *>(ustage);
   uint32_t *sdig = reinterpret_cast<uint32_t *>(wcnt + WAVES * kRPMaxBuckets);  // digit << 16 | input row
   uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
-  __shared__ int64_t s_next;  // LB / XT: first row of the next claimed tile
+  __shared__ int64_t s_next;  // XT: first row of the next claimed tile
   bool order_bad = false;
   (void)nbits;
-  static_assert(!(LB && XT), "one tile schedule");
-  constexpr bool TICKET = LB || XT;
+  constexpr bool TICKET = XT;
   const int xhome = XT ? xcc_id() : 0;
 
   const int64_t b = blockIdx.x;
   int64_t begin, end;
   if (TICKET) {
-    if (threadIdx.x == 0) s_next = XT ? xt_claim(lb, xhome, TILE, n) : (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
+    if (threadIdx.x == 0) s_next = xt_claim(lb, xhome, TILE, n);
     __syncthreads();
     begin = s_next;
     end = n;
@@ -942,10 +698,6 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
       if (tx == THREADS - 1) toff[nbuckets] = ex + total;
     }
     __syncthreads();
-    // LB: this tile's bucket offsets (read by the column stores): count published before the slot
-    // phase, lookback after it.  nbuckets <= THREADS: one bucket a thread
-    const uint32_t lbc = LB && (uint32_t)tx < nbuckets ? toff[tx + 1] - toff[tx] : 0u;
-    if (LB && (uint32_t)tx < nbuckets) lb_publish(lb, nbuckets, tile / TILE, tx, lbc);
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k) {
       if (pl[k] == 0xffffffffu) continue;
@@ -954,7 +706,6 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
       sdig[pos] = (p << 16) | (uint32_t)(wrow + k * kWave + lane);
       pl[k] = pos;
     }
-    if (LB && (uint32_t)tx < nbuckets) running[tx] = lb_exclusive(lb, nbuckets, tile / TILE, tx, lbc);
     if (XT && (uint32_t)tx < nbuckets) running[tx] = xoff;
     __syncthreads();
     uint32_t dp[kRPItems];  // sorted slot j = tx + q * THREADS -> digit << 16 | offset in its run
@@ -986,8 +737,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
         for (int k = 0; k < kRPItems; ++k) v[k] = (k * kWave + lane < lim) ? ldw<W8>(ibase, k * kWave + lane, w) : 0ull;
       }
       const uint64_t x = c == 0 ? cols.key_xor : 0ull;
-      if (TICKET && c + 1 == cols.n && tx == 0)
-        s_next = XT ? xt_claim(lb, xhome, TILE, n) : (int64_t)atomicAdd(lb.ticket, 1u) * TILE;
+      if (TICKET && c + 1 == cols.n && tx == 0) s_next = xt_claim(lb, xhome, TILE, n);
 #pragma unroll
       for (int k = 0; k < kRPItems; ++k)
         if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
@@ -1220,52 +970,36 @@ int64_t radix_rows_pass_workspace(int64_t n, int digit_bits) {  // covers both b
   return ws;
 }
 
-// Column-1 LDS-DMA of the one-block-per-CU pass (k_rows_pass DMA1): 8-byte columns, >= 2 of them,
-// column 1 read from memory.  Opt-in (CYLON_RP_DMA=1, read per launch): measured SLOWER on the
-// 1B x 1B join (profiles/r03/lds_dma_ab.txt: tile 82-86K -> 88-103K cycles).  hipcc's own
-// s_waitcnt vmcnt(0) before the kernel's register-spill reloads in the slot phase (it cannot count
-// the asm DMA) and the DMA issue behind the previous tile's outstanding scatter stores put the
-// transfer back on the critical path: the keys phase grows 1.4K -> 10K cycles, the slot phase
-// 2K -> 7K, while column 0's scatter shrinks only 16K -> 8-9K.
-static bool rp_dma1(bool w8, const ColSet &cs) {
-  const char *e = std::getenv("CYLON_RP_DMA");
-  return w8 && cs.n >= 2 && cs.in[1] != nullptr && e && e[0] == '1';
-}
-
-template <class Digit, int THREADS, int RANK, bool LB = false>
+template <class Digit, int THREADS, int RANK>
 static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit &dg, int digit_bits, uint32_t nb,
-                             const ColSet &cs, int64_t n, const int64_t *bh_scan, const Lookback &lb = Lookback{},
+                             const ColSet &cs, int64_t n, const int64_t *bh_scan, const TileSched &lb = TileSched{},
                              bool xt = false) {
   static const bool stamp = std::getenv("CYLON_RP_STAMPS") != nullptr;  // debug: phase stamps to stderr
   unsigned long long *st = nullptr;
-  if (stamp && !LB) {
+  if (stamp) {
     HIP_CHECK(hipStreamSynchronize(s));
     HIP_CHECK(hipMalloc(&st, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
     HIP_CHECK(hipMemset(st, 0, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
   }
   bool launched = false;
-  if constexpr (THREADS == 1024 && !LB) {
+  if constexpr (THREADS == 1024) {
     if (xt) {
       if (w8)
-        hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS, RANK, false, false, true>), dim3((unsigned)g.nblocks),
-                           dim3(THREADS), 0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
+        hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS, RANK, true>), dim3((unsigned)g.nblocks), dim3(THREADS), 0,
+                           s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
       else
-        hipLaunchKernelGGL((k_rows_pass<Digit, false, THREADS, RANK, false, false, true>), dim3((unsigned)g.nblocks),
-                           dim3(THREADS), 0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
-      launched = true;
-    } else if (rp_dma1(w8, cs)) {
-      hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS, RANK, LB, true>), dim3((unsigned)g.nblocks), dim3(THREADS),
-                         0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
+        hipLaunchKernelGGL((k_rows_pass<Digit, false, THREADS, RANK, true>), dim3((unsigned)g.nblocks), dim3(THREADS), 0,
+                           s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
       launched = true;
     }
   }
   if (launched) {
   } else if (w8)
-    hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS, RANK, LB>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s,
-                       dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
+    hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS, RANK>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s, dg,
+                       digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
   else
-    hipLaunchKernelGGL((k_rows_pass<Digit, false, THREADS, RANK, LB>), dim3((unsigned)g.nblocks), dim3(THREADS), 0,
-                       s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
+    hipLaunchKernelGGL((k_rows_pass<Digit, false, THREADS, RANK>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s, dg,
+                       digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
   if (st) {
     HIP_CHECK(hipStreamSynchronize(s));
     std::vector<unsigned long long> h(kRPStampTiles * kRPStampSlots);
@@ -1296,124 +1030,43 @@ static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const 
   }
 }
 
-template <class Digit, int RANK, bool LB>
+template <class Digit, int RANK>
 static void lean_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit &dg, int digit_bits, uint32_t nb,
-                        const ColSet &cs, int64_t n, const int64_t *bh_scan, const Lookback &lb, bool xt = false) {
-  if constexpr (!LB) {
-    if (xt) {
-      if (w8)
-        hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, RANK, false, true>), dim3((unsigned)g.nblocks),
-                           dim3(kRPThreads), 0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
-      else
-        hipLaunchKernelGGL((k_rows_pass_lean<Digit, false, RANK, false, true>), dim3((unsigned)g.nblocks),
-                           dim3(kRPThreads), 0, s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
-      return;
-    }
+                        const ColSet &cs, int64_t n, const int64_t *bh_scan, const TileSched &lb, bool xt = false) {
+  if (xt) {
+    if (w8)
+      hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, RANK, true>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s,
+                         dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
+    else
+      hipLaunchKernelGGL((k_rows_pass_lean<Digit, false, RANK, true>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s,
+                         dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
+    return;
   }
   if (w8)
-    hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, RANK, LB>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s,
-                       dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
+    hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, RANK>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg,
+                       digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
   else
-    hipLaunchKernelGGL((k_rows_pass_lean<Digit, false, RANK, LB>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s,
-                       dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
-}
-
-// ---- lookback session workspace (int64 words):
-//   [hist u64: kLbMaxPasses x kRPMaxBuckets][gstart: same][tickets: kLbMaxPasses u32 (4 words)][status: tiles x 2^maxbits]
-constexpr int64_t kLbHistWords = (int64_t)kLbMaxPasses * kRPMaxBuckets;
-static int64_t lb_tiles(int64_t n) { return std::max<int64_t>(1, (n + kRPTile - 1) / kRPTile); }
-
-// Off by default: measured slower on MI355X (profiles/r03/lookback_ab.txt: 2B sort 99.3 -> 110.1 ms,
-// headline join 110.8 -> 118.6 ms).  Tiles claimed by ticket land in row order on whichever XCD
-// is free, so consecutive tiles' partial 128-B runs of one bucket are written from different
-// L2s instead of merging in one (the per-block chunks of histogram mode keep a bucket's
-// consecutive runs in one block, one L2), and every tile waits on agent-scope status words.
-// CYLON_RP_LOOKBACK=1 enables it.
-bool radix_lookback_enabled() {
-  const char *e = std::getenv("CYLON_RP_LOOKBACK");
-  return e && e[0] == '1';
-}
-
-int64_t radix_lb_workspace(int64_t n, int max_digit_bits) {
-  return 2 * kLbHistWords + kLbMaxPasses / 2 + lb_tiles(n) * (int64_t(1) << max_digit_bits);
-}
-
-template <class Digit>
-static void lb_prepare(const DigitSet<Digit> &ds, int64_t n, int max_digit_bits, int64_t *lbws, hipStream_t s) {
-  CYLON_CHECK(ds.n >= 1 && ds.n <= kLbMaxPasses, Code::Invalid, "lookback passes " << ds.n);
-  CYLON_CHECK(max_digit_bits >= 1 && max_digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << max_digit_bits);
-  const uint32_t nb = 1u << max_digit_bits;
-  // histograms, tickets and status words start at zero (epoch 0 is never a pass's tag)
-  HIP_CHECK(hipMemsetAsync(lbws, 0, sizeof(int64_t) * radix_lb_workspace(n, max_digit_bits), s));
-  if (n > 0) {
-    hipLaunchKernelGGL(k_lb_hist<Digit>, dim3(grid_for(n, kRPThreads * 8, kNumCUs * 2)), dim3(kRPThreads), 0, s, ds, n,
-                       nb, reinterpret_cast<unsigned long long *>(lbws));
-    HIP_LAUNCH_CHECK();
-  }
-  hipLaunchKernelGGL(k_lb_scan, dim3(ds.n), dim3(kRPThreads), 0, s, reinterpret_cast<unsigned long long *>(lbws), nb,
-                     lbws + kLbHistWords);
-  HIP_LAUNCH_CHECK();
-}
-
-// Every pass of one session uses the same bucket count (2^max_digit_bits histogram rows; a pass
-// with fewer digit bits leaves the upper rows empty).
-void radix_lb_prepare_part(const int64_t *keys, int64_t n, int total_bits, const int *shifts, const int *dbits,
-                           int npass, int max_digit_bits, int64_t *lbws, void *stream) {
-  DigitSet<PartDigit> ds{};
-  ds.n = npass;
-  for (int s = 0; s < npass; ++s) ds.d[s] = PartDigit{keys, total_bits, shifts[s], (1u << dbits[s]) - 1};
-  lb_prepare(ds, n, max_digit_bits, lbws, as_stream(stream));
-}
-
-void radix_lb_prepare_sort(const int64_t *keys, int64_t n, uint64_t flip, const int *shifts, const int *dbits,
-                           int npass, int max_digit_bits, int64_t *lbws, void *stream) {
-  DigitSet<ImageDigit> ds{};
-  ds.n = npass;
-  for (int s = 0; s < npass; ++s) ds.d[s] = ImageDigit{keys, shifts[s], (1u << dbits[s]) - 1, flip};
-  lb_prepare(ds, n, max_digit_bits, lbws, as_stream(stream));
-}
-
-void radix_lb_prepare_range(const int64_t *keys, int64_t n, uint64_t flip, uint64_t mn, int rshift, const int *shifts,
-                            const int *dbits, int npass, int max_digit_bits, int64_t *lbws, void *stream) {
-  DigitSet<RangeDigit> ds{};
-  ds.n = npass;
-  for (int s = 0; s < npass; ++s) ds.d[s] = RangeDigit{keys, flip, mn, rshift, shifts[s], (1u << dbits[s]) - 1};
-  lb_prepare(ds, n, max_digit_bits, lbws, as_stream(stream));
-}
-
-// pass `pass` of a lookback session: its gstart row, ticket and epoch
-static Lookback lb_args(int64_t *lbws, int pass, int max_digit_bits) {
-  Lookback lb;
-  lb.gstart = lbws + kLbHistWords + (int64_t)pass * (int64_t(1) << max_digit_bits);
-  lb.ticket = reinterpret_cast<unsigned int *>(lbws + 2 * kLbHistWords) + pass;
-  lb.status = reinterpret_cast<unsigned long long *>(lbws + 2 * kLbHistWords + kLbMaxPasses / 2);
-  lb.epoch = (unsigned long long)(pass + 1);
-  return lb;
+    hipLaunchKernelGGL((k_rows_pass_lean<Digit, false, RANK>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg,
+                       digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
 }
 
 // stable = false (join partitions only) ranks rows with LDS atomics: rows of one
 // bucket keep no particular order inside a tile's run.  Instantiated for PartDigit
 // only; every other digit (sort, shuffle, range join) needs the stable order.
-// lbws != nullptr: lookback mode, pass `lb_pass` of the session radix_lb_prepare_* set up with
-// `lb_bits` histogram bits (digit_bits <= lb_bits); ws is not used.
 template <class Digit, bool CAN_UNSTABLE = std::is_same<Digit, PartDigit>::value>
 static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const uint8_t *const *in, uint8_t *const *out,
                              const int *widths, int ncols, int64_t *ws, void *stream, uint64_t key_xor = 0,
-                             bool stable = true, int64_t *lbws = nullptr, int lb_pass = 0, int lb_bits = 0,
-                             bool tiles_prescanned = false) {
+                             bool stable = true, bool tiles_prescanned = false,
+                             const uint32_t *bucket_extra = nullptr) {
   if (n == 0) return;
   CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
   CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
   CYLON_CHECK(in[0] == reinterpret_cast<const uint8_t *>(dg.keys) && widths[0] == 8, Code::Invalid,
               "radix pass: column 0 must be the key");
-  static_assert(!Digit::kNarrow, "narrow-key passes launch through narrow_pass_launch");
   // key_xor rebuilds int64 keys from order images: only a sort's image digit may set it
   // (partition / mod / range digits store column 0 as read)
   CYLON_CHECK((key_xor == 0 || std::is_same<Digit, ImageDigit>::value), Code::Invalid,
               "radix pass: key_xor is only valid for order-image digits");
-  const bool lbm = lbws != nullptr;
-  CYLON_CHECK(!lbm || (lb_pass >= 0 && lb_pass < kLbMaxPasses && digit_bits <= lb_bits), Code::Invalid,
-              "radix pass: bad lookback pass " << lb_pass);
   hipStream_t s = as_stream(stream);
   const uint32_t nb = 1u << digit_bits;
   CYLON_CHECK(stable || CAN_UNSTABLE, Code::Invalid, "radix pass: only partition digits may rank unstably");
@@ -1424,13 +1077,13 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   if (CAN_UNSTABLE && dbg && dbg[0] == '1') stable = false;
   const bool unstable = CAN_UNSTABLE && !stable;
   const bool wave_atomic = !unstable && rp_wave_atomic(s);
-  // lookback tiles are 8192 rows: 1024-thread kernels only
-  const int threads = lbm ? 1024 : rp_threads(ncols, unstable || wave_atomic);
+  const int threads = rp_threads(ncols, unstable || wave_atomic);
   const bool lean = rp_lean(ncols) && (unstable || wave_atomic) && threads == 1024;
   RPGeometry g;
   const int64_t *bh_scan = nullptr;
-  Lookback lb{};
-  const bool xt = !lbm && threads == 1024 && n < (int64_t(1) << 32) && rp_xt();
+  TileSched lb{};
+  const bool xt = threads == 1024 && n < (int64_t(1) << 32) && rp_xt();
+  CYLON_CHECK(xt || bucket_extra == nullptr, Code::Invalid, "radix pass: gapped layouts need the XCD-tile schedule");
   if (!xt) tiles_prescanned = false;  // histogram mode counts its own blocks (the prescan is unused)
   if (xt) {  // exact per-tile offsets, tiles claimed in order per XCD (see xt_claim)
     const XtLayout L = xt_layout(n, nb);
@@ -1450,18 +1103,14 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
     uint32_t *bbase = reinterpret_cast<uint32_t *>(ws + L.bbase);
     hipLaunchKernelGGL(k_ts_chunk_prefix, dim3(1), dim3(kRPThreads), 0, s, csum, nb, L.nchunks, cpre, bbase);
     HIP_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ts_offsets, dim3((unsigned)L.nchunks), dim3(bt), 0, s, th, cpre, bbase, nb, L.ntiles, off);
+    hipLaunchKernelGGL(k_ts_offsets, dim3((unsigned)L.nchunks), dim3(bt), 0, s, th, cpre, bbase, nb, L.ntiles, off,
+                       bucket_extra);
     HIP_LAUNCH_CHECK();
     lb.xt_off = off;
     lb.xt_ticket = tk;
     lb.xt_tiles = L.ntiles;
     g.rows_per_block = kRPTile;
     g.nblocks = std::min<int64_t>(L.ntiles, (int64_t)kNumCUs * (lean ? 2 : 1));  // persistent: all resident
-  } else if (lbm) {
-    // status rows are 2^lb_bits wide; a pass with fewer bits indexes them with its own nb
-    lb = lb_args(lbws, lb_pass, lb_bits);
-    g.rows_per_block = kRPTile;
-    g.nblocks = std::min<int64_t>(lb_tiles(n), (int64_t)kNumCUs * (lean ? 2 : 1));  // persistent, tiles by ticket
   } else {
     g = rp_geometry(n, threads, lean ? 2 : 1);
     const int64_t m = g.nblocks * (int64_t)nb;
@@ -1493,22 +1142,12 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   const bool big = threads == 1024;
   if (lean) {
     constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankWaveAtomic;
-    if (lbm) {
-      if (unstable) lean_kernel<Digit, R, true>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
-      else lean_kernel<Digit, kRankWaveAtomic, true>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
-    } else {
-      if (unstable) lean_kernel<Digit, R, false>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
-      else lean_kernel<Digit, kRankWaveAtomic, false>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
-    }
+    if (unstable) lean_kernel<Digit, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
+    else lean_kernel<Digit, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
     HIP_LAUNCH_CHECK();
     return;
   }
-  if (lbm) {
-    constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankBallot;
-    if (unstable) rows_pass_kernel<Digit, 1024, R, true>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
-    else if (wave_atomic) rows_pass_kernel<Digit, 1024, kRankWaveAtomic, true>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
-    else rows_pass_kernel<Digit, 1024, kRankBallot, true>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb);
-  } else if (unstable) {
+  if (unstable) {
     constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankBallot;
     if (big) rows_pass_kernel<Digit, 1024, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
     else rows_pass_kernel<Digit, 512, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan);
@@ -1523,98 +1162,18 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
 }
 
 void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, int digit_bits, const uint8_t *const *in,
-                     uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream, bool stable,
-                     int64_t *lbws, int lb_pass, int lb_bits) {
+                     uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream, bool stable) {
   const uint32_t nb = 1u << digit_bits;
   rows_pass_launch(PartDigit{keys, total_bits, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws, stream, 0,
-                   stable, lbws, lb_pass, lb_bits);
-}
-
-// ---- narrow-key join passes: the one-block-per-CU kernel (8192-row tiles, next-column prefetch)
-// for every column count; the first pass (int64 keys in, block-atomic ranking) may take its
-// scanned histogram from radix_narrow_prehist, later passes (uint32 keys) rank stably.
-static RPGeometry narrow_geometry(int64_t n) { return rp_geometry(n, 1024, 1); }
-
-void radix_narrow_prehist(const int64_t *keys, int64_t n, int total_bits, int digit_bits, int64_t *ws, int64_t *mm,
-                          void *stream) {
-  CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
-  hipStream_t s = as_stream(stream);
-  if (n == 0) return;
-  const RPGeometry g = narrow_geometry(n);
-  const uint32_t nb = 1u << digit_bits;
-  const int64_t m = g.nblocks * (int64_t)nb;
-  hipLaunchKernelGGL(k_rp_hist_minmax, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s,
-                     PartDigitN64{keys, total_bits, 0, nb - 1}, n, nb, g.rows_per_block, g.nblocks, ws,
-                     reinterpret_cast<long long *>(mm));
-  HIP_LAUNCH_CHECK();
-  exclusive_scan(ws, m, ws + m, ws + 2 * m + 1, stream);
-}
-
-template <class Digit>
-static void narrow_pass_launch(const Digit &dg, int64_t n, int digit_bits, const uint8_t *const *in,
-                               uint8_t *const *out, const int *widths, int ncols, int64_t *ws, hipStream_t s,
-                               bool stable, bool prescanned) {
-  static_assert(Digit::kNarrow, "narrow digits only");
-  if (n == 0) return;
-  CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
-  CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
-  CYLON_CHECK(in[0] == reinterpret_cast<const uint8_t *>(dg.keys) && widths[0] == 4, Code::Invalid,
-              "narrow radix pass: column 0 must be the key, stored as uint32");
-  const bool want_stable = stable;
-  const char *dbg = std::getenv("CYLON_RP_DEBUG_UNSTABLE");  // ranking-guard test knob (rows_pass_launch)
-  if (dbg && dbg[0] == '1') stable = false;
-  const RPGeometry g = narrow_geometry(n);
-  const uint32_t nb = 1u << digit_bits;
-  const int64_t m = g.nblocks * (int64_t)nb;
-  if (!prescanned) {
-    hipLaunchKernelGGL(k_rp_hist<Digit>, dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s, dg, n, nb,
-                       g.rows_per_block, g.nblocks, ws);
-    HIP_LAUNCH_CHECK();
-    exclusive_scan(ws, m, ws + m, ws + 2 * m + 1, reinterpret_cast<void *>(s));
-  }
-  ColSet cs;
-  cs.n = ncols;
-  cs.key_xor = 0;
-  const char *gd = std::getenv("CYLON_RP_GUARD");
-  cs.check_order = want_stable && !(gd && gd[0] == '0') ? 1 : 0;
-  cs.order_bad = order_flag();
-  bool w8 = true;
-  for (int c = 0; c < kMaxFusedCols; ++c) {
-    cs.in[c] = c < ncols ? in[c] : nullptr;
-    cs.out[c] = c < ncols ? out[c] : nullptr;
-    cs.width[c] = c < ncols ? widths[c] : 8;
-    if (c > 0 && c < ncols) {
-      w8 &= widths[c] == 8;
-      CYLON_CHECK(in[c] != nullptr, Code::Invalid, "narrow radix pass: no generated columns");
-    }
-  }
-  if (!stable) rows_pass_kernel<Digit, 1024, kRankBlockAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, ws + m);
-  else if (rp_wave_atomic(s)) rows_pass_kernel<Digit, 1024, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, ws + m);
-  else rows_pass_kernel<Digit, 1024, kRankBallot>(w8, g, s, dg, digit_bits, nb, cs, n, ws + m);
-  HIP_LAUNCH_CHECK();
-}
-
-void radix_narrow_rows_pass(const void *keys, int key_bytes, int64_t n, int total_bits, int shift, int digit_bits,
-                            const uint8_t *const *in, uint8_t *const *out, const int *widths, int ncols, int64_t *ws,
-                            void *stream, bool stable, bool prescanned) {
-  CYLON_CHECK(key_bytes == 8 || key_bytes == 4, Code::Invalid, "narrow radix pass: key bytes " << key_bytes);
-  const uint32_t nb = 1u << digit_bits;
-  hipStream_t s = as_stream(stream);
-  if (key_bytes == 8)
-    narrow_pass_launch(PartDigitN64{reinterpret_cast<const int64_t *>(keys), total_bits, shift, nb - 1}, n, digit_bits,
-                       in, out, widths, ncols, ws, s, stable, prescanned);
-  else
-    narrow_pass_launch(PartDigitN32{reinterpret_cast<const uint32_t *>(keys), total_bits, shift, nb - 1}, n,
-                       digit_bits, in, out, widths, ncols, ws, s, stable, prescanned);
+                   stable);
 }
 
 void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_bits, const uint8_t *const *in,
                           uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream,
-                          uint64_t key_xor, uint64_t digit_flip, int64_t *lbws, int lb_pass, int lb_bits,
-                          bool tiles_prescanned) {
+                          uint64_t key_xor, uint64_t digit_flip, bool tiles_prescanned) {
   const uint32_t nb = 1u << digit_bits;
   rows_pass_launch(ImageDigit{keys, shift, nb - 1, digit_flip}, n, digit_bits, in, out, widths, ncols, ws, stream,
-                   key_xor, true, lbws, lb_pass, lb_bits, tiles_prescanned);
+                   key_xor, true, tiles_prescanned);
 }
 
 bool radix_xt_enabled() { return rp_xt(); }
@@ -1704,10 +1263,10 @@ void radix_sort_prehist_fold(const int64_t *pre_ws, int64_t n, int db, int64_t *
 
 void radix_range_rows_pass(const int64_t *keys, int64_t n, uint64_t flip, uint64_t mn, int rshift, int shift,
                            int digit_bits, const uint8_t *const *in, uint8_t *const *out, const int *widths, int ncols,
-                           int64_t *ws, void *stream, int64_t *lbws, int lb_pass, int lb_bits) {
+                           int64_t *ws, void *stream) {
   const uint32_t nb = 1u << digit_bits;
   rows_pass_launch(RangeDigit{keys, flip, mn, rshift, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws,
-                   stream, 0, true, lbws, lb_pass, lb_bits);
+                   stream, 0, true);
 }
 
 static int bits_for(uint32_t nparts) {
@@ -1724,6 +1283,20 @@ void radix_mod_rows_pass(const int64_t *keys, int64_t n, uint32_t nparts, const 
                          const int *widths, int ncols, int64_t *ws, void *stream) {
   CYLON_CHECK(nparts >= 1 && nparts <= (uint32_t)kRPMaxBuckets, Code::Invalid, "partition count " << nparts);
   rows_pass_launch(ModDigit{keys, nparts}, n, bits_for(nparts), in, out, widths, ncols, ws, stream);
+}
+
+// The same pass into a gapped layout: bucket p's rows start extra[p] rows further on (device
+// uint32[2^bits(nparts)], non-decreasing).  Only the XCD-tile schedule takes per-bucket bases: false
+// (nothing launched) when it cannot run (CYLON_RP_XT=0, ballot ranking, >= 2^32 output rows).
+bool radix_mod_rows_pass_gapped(const int64_t *keys, int64_t n, uint32_t nparts, const uint8_t *const *in,
+                                uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream,
+                                const uint32_t *extra, int64_t out_rows) {
+  CYLON_CHECK(nparts >= 1 && nparts <= (uint32_t)kRPMaxBuckets, Code::Invalid, "partition count " << nparts);
+  if (!rp_xt() || out_rows >= (int64_t(1) << 32) || n == 0) return false;
+  if (!rp_wave_atomic(as_stream(stream)) && rp_threads(ncols, false) != 1024) return false;
+  rows_pass_launch(ModDigit{keys, nparts}, n, bits_for(nparts), in, out, widths, ncols, ws, stream, 0, true, false,
+                   extra);
+  return true;
 }
 
 __global__ __launch_bounds__(kRPThreads) void k_mod_counts(ModDigit digit, int64_t n,
@@ -1769,27 +1342,6 @@ void radix_part_offsets(const int64_t *keys, int64_t n, int bits, int64_t *offs,
   HIP_LAUNCH_CHECK();
 }
 
-// same over narrow-key partitions (uint32 keys, partition hash of the low 32 bits)
-__global__ void k_part_offsets_u32(const uint32_t *__restrict__ keys, int64_t n, int bits, int64_t nparts,
-                                   int64_t *__restrict__ offs) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= nparts; p += stride) {
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if ((int64_t)part_of((int64_t)keys[mid], bits) < p) lo = mid + 1; else hi = mid;
-    }
-    offs[p] = lo;
-  }
-}
-
-void radix_narrow_part_offsets(const uint32_t *keys, int64_t n, int bits, int64_t *offs, void *stream) {
-  const int64_t np = int64_t(1) << bits;
-  hipLaunchKernelGGL(k_part_offsets_u32, dim3(grid_for(np + 1)), dim3(kBlock), 0, as_stream(stream), keys, n, bits,
-                     np, offs);
-  HIP_LAUNCH_CHECK();
-}
-
 __global__ void k_range_part_offsets(const int64_t *__restrict__ keys, int64_t n, uint64_t flip, uint64_t mn,
                                      int rshift, int64_t nparts, int64_t *__restrict__ offs) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -1825,9 +1377,9 @@ constexpr int kRJBuckets = 4096;
 
 // Build rows per partition that fit the LDS row area: key (8 B) + permutation
 // (2 B) + the staged build columns (widths w[q]; in[q] == nullptr marks the key
-// column itself, which is not staged twice).
-int64_t radix_join_capacity(const int *widths, const uint8_t *const *in, int n, int key_bytes) {
-  int64_t row = key_bytes + 2;
+// column itself, which is not staged twice) + a matched flag (build-preserving outer joins).
+int64_t radix_join_capacity(const int *widths, const uint8_t *const *in, int n, bool match_flags) {
+  int64_t row = 8 + 2 + (match_flags ? 1 : 0);
   for (int q = 0; q < n; ++q)
     if (in[q]) row += widths[q];
   int64_t cap = kRJRowArea / row;
@@ -1838,17 +1390,6 @@ int64_t radix_join_capacity(const int *widths, const uint8_t *const *in, int n, 
 __device__ __forceinline__ uint32_t rj_bucket(int64_t k) {
   return (uint32_t)hashing::fmix64((uint64_t)k) & (kRJBuckets - 1);
 }
-// narrow keys (low 32 bits): bucket from fmix32, independent of the partition's fmix64 bits
-__device__ __forceinline__ uint32_t rj_bucket(uint32_t k) { return hashing::fmix32(k) & (kRJBuckets - 1); }
-
-// output value of a join key: int64 keys as they are; narrow keys rebuilt from their low 32 bits
-// and the relations' minimum (every key lies in [kmin, kmin + 2^32))
-__device__ __forceinline__ int64_t rj_widen(int64_t k, int64_t) { return k; }
-__device__ __forceinline__ int64_t rj_widen(uint32_t k, int64_t kmin) {
-  return kmin + (int64_t)(uint32_t)(k - (uint32_t)(uint64_t)kmin);
-}
-__device__ __forceinline__ int64_t rj_shfl_key(int64_t x, int src);
-__device__ __forceinline__ uint32_t rj_shfl_key(uint32_t x, int src) { return __shfl(x, src, kWave); }
 
 // Build rows of one partition: thread t owns rows t + i * kRJThreads (cap <= kRJMaxRows).
 constexpr int kRJRowsPerThread = kRJMaxRows / kRJThreads;
@@ -1891,11 +1432,20 @@ __device__ __forceinline__ uint32_t rj_claim(uint16_t *bst, uint32_t b) {
   return (old >> sh) & 0xffffu;
 }
 
-template <class KT>
-__device__ __forceinline__ uint32_t rj_count(const uint16_t *bst, const KT *skeys, KT k) {
+// Outer joins (OJ bits): 1 = probe rows without a match are emitted once with a null build side,
+// 2 = build rows without a match are emitted after the partition's matches with a null probe side.
+constexpr int kOJProbe = 1, kOJBuild = 2;
+
+// matches of k in its bucket; OJ & 2: the matched build slots are flagged (plain byte stores of 1)
+template <int OJ>
+__device__ __forceinline__ uint32_t rj_count_mark(const uint16_t *bst, const int64_t *skeys, int64_t k, uint8_t *flg) {
   const uint32_t b = rj_bucket(k);
   uint32_t c = 0;
-  for (uint32_t i = bst[b], e = bst[b + 1]; i < e; ++i) c += (skeys[i] == k);
+  for (uint32_t i = bst[b], e = bst[b + 1]; i < e; ++i)
+    if (skeys[i] == k) {
+      ++c;
+      if (OJ & kOJBuild) flg[i] = 1;
+    }
   return c;
 }
 
@@ -1907,16 +1457,18 @@ constexpr int kRCWaves = kRCThreads / kWave;
 constexpr int kRCRowsPerThread = kRJMaxRows / kRCThreads;
 static_assert(kRCRowsPerThread * kRCThreads == kRJMaxRows, "count rows per thread");
 
-template <class KT>
-__global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_rj_count(const KT *__restrict__ pkeys,
-                                                      const int64_t *__restrict__ poffs,
-                                                      const KT *__restrict__ bkeys,
-                                                      const int64_t *__restrict__ boffs, int64_t nparts, int cap,
-                                                      int64_t pstride, int64_t *__restrict__ counts, int *overflow) {
+template <int OJ>
+__global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_rj_count(
+    const int64_t *__restrict__ pkeys, const int64_t *__restrict__ poffs, const int64_t *__restrict__ bkeys,
+    const int64_t *__restrict__ boffs, int64_t nparts, int cap, int64_t pstride, int64_t *__restrict__ counts,
+    int *overflow) {
+  using KT = int64_t;
   // pstride > 1: only partitions 0, pstride, 2 pstride, ... are counted, into counts[p / pstride]
-  // (the sampled output-size estimate of the fused write path)
+  // (the sampled output-size estimate of the fused write path).  Output rows per partition:
+  // matches, + unmatched probe rows (OJ & 1), + unmatched build rows (OJ & 2).
   __shared__ __attribute__((aligned(16))) uint16_t bst[kRJBuckets + 8];
   __shared__ KT skeys[kRJMaxRows];
+  __shared__ uint8_t flg[(OJ & kOJBuild) ? kRJMaxRows : 1];
   __shared__ uint32_t wsum[kRCWaves];
   __shared__ unsigned long long csum[kRCWaves];
   const int64_t nsample = (nparts + pstride - 1) / pstride;
@@ -1932,13 +1484,16 @@ __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4)))
       continue;
     }
     if (nr == 0 || nl == 0) {
-      if (threadIdx.x == 0) counts[ci] = 0;
+      if (threadIdx.x == 0)
+        counts[ci] = (nr == 0 && (OJ & kOJProbe) ? nl : 0) + (nl == 0 && (OJ & kOJBuild) ? nr : 0);
       continue;
     }
     // build keys are read twice (claim, then place): the second read hits L2 and the block
     // keeps only 16-bit ranks in registers (two 512-thread blocks per CU without spills)
-    __syncthreads();  // previous partition done with bst / skeys / csum
+    __syncthreads();  // previous partition done with bst / skeys / csum / flg
     for (int s = threadIdx.x; s < kRJBuckets / 2; s += blockDim.x) reinterpret_cast<uint32_t *>(bst)[s] = 0;
+    if (OJ & kOJBuild)
+      for (int i = threadIdx.x; i < nr; i += blockDim.x) flg[i] = 0;
     __syncthreads();
     uint32_t rk[kRCRowsPerThread];
 #pragma unroll
@@ -1966,7 +1521,14 @@ __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4)))
         if (l0 + u * kRCThreads < nl) pk[u] = pkeys[lb + l0 + u * kRCThreads];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (l0 + u * kRCThreads < nl) c += rj_count(bst, skeys, pk[u]);
+        if (l0 + u * kRCThreads < nl) {
+          const uint32_t mc = rj_count_mark<OJ>(bst, skeys, pk[u], flg);
+          c += (OJ & kOJProbe) && mc == 0 ? 1u : mc;
+        }
+    }
+    if (OJ & kOJBuild) {
+      __syncthreads();  // every probe has flagged its matches
+      for (int i = threadIdx.x; i < nr; i += blockDim.x) c += flg[i] ? 0u : 1u;
     }
     for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
     if (lane_id() == 0) csum[threadIdx.x / kWave] = c;
@@ -1991,31 +1553,33 @@ struct BuildOut {               // build-side output columns
   int width[kMaxFusedCols];
   int lds_off[kMaxFusedCols];   // byte offset of the staged column in the LDS row area, -1 = key
   int n;
+  int match_off;                // OJ & 2: byte offset of the build rows' matched flags in the row area
 };
 
-// OM: emit finds each output slot's probe lane through a per-wave LDS owner map (lanes write
-// their lane id into the slots of their matches) instead of a 6-step binary search over the
-// wave's match scan with cross-lane permutes (CYLON_RJ_OWNERMAP=1 selects it; A/B knob).
-// KT: key type of the partitions (int64_t, or uint32_t low halves of a narrow-key join: kmin
-// rebuilds the output keys).  pkey: index of the probe column that IS the key (its value comes
-// from the probe key, not a second load; -1 none).
+// Outer joins (OJ bits, see rj_count_mark): presence bytes (ppres / bpres: 1 = that side holds a
+// row) are written for the side(s) that can be null; the host turns them into the output
+// columns' validity (join.cpp radix_join).
+
 // the write kernel's build staging: rj_dma_block over its 16 waves
 __device__ __forceinline__ void rj_dma(const uint8_t *src, int bytes, uint8_t *dst, int wave, int lane) {
   rj_dma_block<kRJWaves>(src, bytes, dst, wave, lane);
 }
 
-// DMA: stage the build columns by LDS-DMA (needs W8) instead of register round trips per column.
-template <int MAXP, int MAXB, bool W8, bool OM, class KT, bool DMA>
-__global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict__ pkeys,
+// pkey: index of the probe column that IS the key (its value comes from the probe key, not a
+// second load; -1 none).  DMA: stage the build columns by LDS-DMA (needs W8) instead of register
+// round trips per column.
+template <int MAXP, int MAXB, bool W8, bool DMA, int OJ>
+__global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__restrict__ pkeys,
                                                             const int64_t *__restrict__ poffs,
-                                                            const KT *__restrict__ bkeys,
+                                                            const int64_t *__restrict__ bkeys,
                                                             const int64_t *__restrict__ boffs, int64_t nparts,
                                                             int cap, const int64_t *__restrict__ out_offs, ColSet pc,
                                                             ColSet bs, BuildOut bo,
                                                             unsigned long long *__restrict__ cursor, int64_t out_cap,
                                                             int *__restrict__ overflow,
-                                                            unsigned long long *__restrict__ stamps, int64_t kmin,
-                                                            int pkey) {
+                                                            unsigned long long *__restrict__ stamps, int pkey,
+                                                            uint8_t *__restrict__ ppres, uint8_t *__restrict__ bpres) {
+  using KT = int64_t;
   // out_offs != nullptr: partition p's rows start at out_offs[p] (exact count kernel ran first).
   // out_offs == nullptr: fused count -- each partition claims its rows from *cursor with one
   // atomic after counting its matches (output partitions land in claim order); a claim past
@@ -2024,14 +1588,15 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict
   // pc: probe columns (in -> out); bs: staged build columns (in, width), LDS
   // region j at 10*cap + sum of cap*width of the earlier ones; bo: build outputs.
   // Row area: keys in bucket order [0, 8 cap), permutation to the staged row
-  // [8 cap, 10 cap), payload columns in staged (original) row order.
+  // [8 cap, 10 cap), payload columns in staged (original) row order, then (OJ & 2) one matched
+  // flag per bucket slot.
   __shared__ __attribute__((aligned(16))) uint16_t bst[kRJBuckets + 8];
   __shared__ __attribute__((aligned(16))) uint8_t area[kRJRowArea];
   __shared__ uint32_t wtot[kRJWaves];
   __shared__ int64_t sclaim;
-  __shared__ uint8_t ownmap[OM ? kRJWaves * kWave : 1];
   KT *skeys = reinterpret_cast<KT *>(area);
   uint16_t *perm = reinterpret_cast<uint16_t *>(area + sizeof(KT) * (int64_t)cap);
+  uint8_t *flg = area + ((OJ & kOJBuild) ? bo.match_off : 0);
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
   int tix = -1;  // debug stamps (CYLON_RJ_STAMPS): block 0's partition count, RP_STAMP slots 0..5
@@ -2039,11 +1604,13 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict
     const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
     const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
     if (nr > cap && out_offs == nullptr && threadIdx.x == 0) atomicOr(overflow, 1);
-    if (nr == 0 || nl == 0 || nr > cap) continue;
+    // inner: both sides needed; outer: a preserved side alone still emits its rows
+    const bool live = (nr > 0 && nl > 0) || ((OJ & kOJProbe) && nl > 0) || ((OJ & kOJBuild) && nr > 0);
+    if (!live || nr > cap) continue;
     ++tix;
     RP_STAMP(0);
     const int64_t obase = out_offs ? out_offs[p] : 0;
-    // ---- phase A: probe rows of this wave's slice into VGkRJProbeRoundss (in flight during the build)
+    // ---- phase A: probe rows of this wave's slice into VGPRs (in flight during the build)
     const int64_t per = (nl + kRJWaves - 1) / kRJWaves;  // each wave owns a contiguous probe slice
     const int64_t s0 = lb + std::min<int64_t>(nl, wave * per);
     const int64_t s1 = lb + std::min<int64_t>(nl, (wave + 1) * per);
@@ -2070,6 +1637,8 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict
     // ---- phase B: stage + index the build rows
     __syncthreads();  // previous partition fully done with bst / area / wtot
     for (int s = threadIdx.x; s < kRJBuckets / 2; s += blockDim.x) reinterpret_cast<uint32_t *>(bst)[s] = 0;
+    if (OJ & kOJBuild)
+      for (int i = threadIdx.x; i < nr; i += blockDim.x) flg[i] = 0;
     if (DMA) {  // every build column in ONE round trip: the keys (raw order) into the key region,
                 // the payload columns into theirs; the loads hold no VGPRs
       rj_dma(reinterpret_cast<const uint8_t *>(bkeys + rb), nr * (int)sizeof(KT), area, wave, lane);
@@ -2135,26 +1704,40 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict
     }
     __syncthreads();
     RP_STAMP(2);
-    // ---- phase C: count this wave's matches, slice offsets
+    // ---- phase C: count this wave's output rows (matches; a lone row for an unmatched probe row
+    // of a probe-preserving join), flag matched build slots, slice offsets
+    auto emitted = [&](uint32_t mc) -> uint32_t { return (OJ & kOJProbe) ? (mc > 0u ? mc : 1u) : mc; };
     uint32_t c = 0;
 #pragma unroll
     for (int u = 0; u < kRJProbeRounds; ++u)
-      if (s0 + u * kWave + lane < s1) c += rj_count(bst, skeys, pk[u]);
+      if (s0 + u * kWave + lane < s1) c += emitted(rj_count_mark<OJ>(bst, skeys, pk[u], flg));
     {  // later rounds' probe keys two rounds at a time (both loads in flight before either count)
       int64_t l = s0 + kRJProbeRounds * kWave + lane;
       for (; l + kWave < s1; l += 2 * kWave) {
         const KT ka = pkeys[l], kb = pkeys[l + kWave];
-        c += rj_count(bst, skeys, ka) + rj_count(bst, skeys, kb);
+        c += emitted(rj_count_mark<OJ>(bst, skeys, ka, flg)) + emitted(rj_count_mark<OJ>(bst, skeys, kb, flg));
       }
-      if (l < s1) c += rj_count(bst, skeys, pkeys[l]);
+      if (l < s1) c += emitted(rj_count_mark<OJ>(bst, skeys, pkeys[l], flg));
     }
     for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
     if (lane == 0) wtot[wave] = c;
     __syncthreads();
+    // unmatched build rows (flags final after the barrier above): emitted after every match
+    uint32_t unm = 0;
+    if (OJ & kOJBuild) {
+      uint32_t u = 0;
+      for (int i = threadIdx.x; i < nr; i += blockDim.x) u += flg[i] ? 0u : 1u;
+      for (int d = kWave / 2; d > 0; d >>= 1) u += __shfl_xor(u, d, kWave);
+      __shared__ uint32_t usum[kRJWaves];
+      if (lane == 0) usum[wave] = u;
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < kRJWaves; ++w) unm += usum[w];
+    }
     int64_t base = obase;
     if (out_offs == nullptr) {
       if (threadIdx.x == 0) {
-        unsigned long long tot = 0;
+        unsigned long long tot = unm;
         for (int w = 0; w < kRJWaves; ++w) tot += wtot[w];
         const unsigned long long at = tot ? atomicAdd(cursor, tot) : 0ull;
         const bool fits = at + tot <= (unsigned long long)out_cap;
@@ -2165,6 +1748,9 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict
       base = sclaim;
       if (base < 0) continue;  // uniform: the block's claim did not fit
     }
+    int64_t ubase = base;  // first output row of the unmatched build rows
+#pragma unroll
+    for (int w = 0; w < kRJWaves; ++w) ubase += wtot[w];
     for (int w = 0; w < wave; ++w) base += wtot[w];
     RP_STAMP(3);
     // ---- phase D: emit.  Round u + 1's probe row is loaded while round u expands (kn / vn), so
@@ -2199,55 +1785,49 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict
         i1 = bst[b + 1];
         for (uint32_t i = i0; i < i1; ++i) mc += (skeys[i] == k);
       }
-      uint32_t inc = mc;  // wave inclusive scan of match counts
+      const uint32_t ec = active ? emitted(mc) : 0u;  // output rows of this probe row
+      uint32_t inc = ec;  // wave inclusive scan of output counts
 #pragma unroll
       for (int d = 1; d < kWave; d <<= 1) {
         const uint32_t x = __shfl_up(inc, d, kWave);
         if (lane >= d) inc += x;
       }
       const uint32_t wsum = __shfl(inc, kWave - 1, kWave);
-      const uint32_t excl = inc - mc;
+      const uint32_t excl = inc - ec;
       // Load-balanced expansion: lane t writes output rows base + t, base + 64 + t, ...
       // of this round, so every store covers a contiguous, fully active run of the
       // output column (a lane-per-probe-row loop over bucket entries would issue
       // sparse partial-line stores).  The producing probe lane ("owner") of row
-      // s is found by a binary search over the wave's inclusive match counts and
+      // s is found by a binary search over the wave's inclusive output counts and
       // its key / bucket / payload are read with cross-lane permutes.
       for (uint32_t t0 = 0; t0 < wsum; t0 += kWave) {
         const uint32_t so = t0 + lane;
         const bool act = so < wsum;
         int owner = 0;
-        if (OM) {
-          uint8_t *om = ownmap + wave * kWave;
-          const uint32_t e0 = excl > t0 ? excl : t0, e1 = excl + mc < t0 + kWave ? excl + mc : t0 + kWave;
-          __builtin_amdgcn_wave_barrier();  // the previous window's reads are done
-          for (uint32_t x = e0; x < e1; ++x) om[x - t0] = (uint8_t)lane;
-          __builtin_amdgcn_wave_barrier();
-          owner = act ? om[lane] : 0;
-        } else {
 #pragma unroll
-          for (int step = kWave / 2; step >= 1; step >>= 1) {
-            const uint32_t ic = __shfl(inc, owner + step - 1, kWave);
-            if (ic <= so) owner += step;
-          }
+        for (int step = kWave / 2; step >= 1; step >>= 1) {
+          const uint32_t ic = __shfl(inc, owner + step - 1, kWave);
+          if (ic <= so) owner += step;
         }
         const uint32_t j = so - __shfl(excl, owner, kWave);  // match rank inside the owner's bucket
         const KT ko = rj_shfl_key(k, owner);
-        const uint64_t kw = (uint64_t)rj_widen(ko, kmin);
+        const uint64_t kw = (uint64_t)ko;
         const uint32_t b0 = __shfl(i0, owner, kWave), b1 = __shfl(i1, owner, kWave);
+        const bool omatched = !(OJ & kOJProbe) || __shfl(mc, owner, kWave) > 0u;
         uint64_t vo[MAXP];
 #pragma unroll
         for (int q = 0; q < MAXP; ++q) vo[q] = q == pkey ? kw : (uint64_t)rj_shfl64((int64_t)v[q], owner);
         if (act) {
-          int r = 0;
-          for (uint32_t i = b0, c = 0; i < b1; ++i) {
-            if (skeys[i] != ko) continue;
-            if (c == j) {
-              r = perm[i];
-              break;
+          int r = -1;
+          if (omatched)
+            for (uint32_t i = b0, c = 0; i < b1; ++i) {
+              if (skeys[i] != ko) continue;
+              if (c == j) {
+                r = perm[i];
+                break;
+              }
+              ++c;
             }
-            ++c;
-          }
           const int64_t o = base + so;
 #pragma unroll
           for (int q = 0; q < MAXP; ++q)
@@ -2257,17 +1837,50 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict
             for (int q = MAXP; q < pc.n; ++q)
               stw<W8>(pc.out[q], o, pc.width[q], q == pkey ? kw : ldw<W8>(pc.in[q], lo, pc.width[q]));
           }
+          if ((OJ & kOJProbe) && r < 0) {  // unmatched probe row: build side null
 #pragma unroll
-          for (int q = 0; q < MAXB + 1; ++q)
-            if (q < bo.n)
+            for (int q = 0; q < MAXB + 1; ++q)
+              if (q < bo.n) stw<W8>(bo.out[q], o, bo.width[q], 0ull);
+            for (int q = MAXB + 1; q < bo.n; ++q) stw<W8>(bo.out[q], o, bo.width[q], 0ull);
+          } else {
+#pragma unroll
+            for (int q = 0; q < MAXB + 1; ++q)
+              if (q < bo.n)
+                stw<W8>(bo.out[q], o, bo.width[q],
+                        bo.lds_off[q] < 0 ? kw : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
+            for (int q = MAXB + 1; q < bo.n; ++q)
               stw<W8>(bo.out[q], o, bo.width[q],
                       bo.lds_off[q] < 0 ? kw : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
-          for (int q = MAXB + 1; q < bo.n; ++q)
-            stw<W8>(bo.out[q], o, bo.width[q],
-                    bo.lds_off[q] < 0 ? kw : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
+          }
+          if (OJ & kOJProbe) bpres[o] = r >= 0 ? 1 : 0;
+          if (OJ & kOJBuild) ppres[o] = 1;
         }
       }
       base += wsum;
+    }
+    if (OJ & kOJBuild) {  // ---- phase E: the unmatched build rows, in bucket-slot order
+      __syncthreads();  // every wave is done with wtot
+      int64_t at = ubase;
+      for (int i0 = 0; i0 < nr; i0 += kRJThreads) {
+        const int i = i0 + (int)threadIdx.x;
+        const uint32_t um = (i < nr && !flg[i]) ? 1u : 0u;
+        const uint32_t ex = rp_block_exscan<kRJWaves>(um, wtot);
+        uint32_t tot = 0;
+#pragma unroll
+        for (int w = 0; w < kRJWaves; ++w) tot += wtot[w];
+        if (um) {
+          const int64_t o = at + ex;
+          const int r = perm[i];
+          const uint64_t kw = (uint64_t)skeys[i];
+          for (int q = 0; q < pc.n; ++q) stw<W8>(pc.out[q], o, pc.width[q], q == pkey ? kw : 0ull);
+          for (int q = 0; q < bo.n; ++q)
+            stw<W8>(bo.out[q], o, bo.width[q], bo.lds_off[q] < 0 ? kw : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
+          ppres[o] = 0;
+          if (OJ & kOJProbe) bpres[o] = 1;
+        }
+        at += tot;
+        __syncthreads();  // wtot reused by the next round
+      }
     }
     RP_STAMP(4);
   }
@@ -2275,36 +1888,58 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const KT *__restrict
 
 static int rj_grid(int64_t nparts) { return (int)std::min<int64_t>(nparts, kNumCUs * 8); }
 
-void radix_join_count(const void *pkeys, const int64_t *poffs, const void *bkeys, const int64_t *boffs,
+void radix_join_count(const int64_t *pkeys, const int64_t *poffs, const int64_t *bkeys, const int64_t *boffs,
                       int64_t nparts, int64_t cap, int64_t *counts, int *overflow, void *stream, int64_t pstride,
-                      int key_bytes) {
+                      int outer) {
   CYLON_CHECK(cap > 0 && cap <= kRJMaxRows, Code::Invalid, "radix join capacity " << cap);
   CYLON_CHECK(pstride >= 1, Code::Invalid, "partition stride " << pstride);
-  CYLON_CHECK(key_bytes == 8 || key_bytes == 4, Code::Invalid, "radix join key bytes " << key_bytes);
+  CYLON_CHECK(outer >= 0 && outer <= 3, Code::Invalid, "radix join outer mode " << outer);
   hipStream_t s = as_stream(stream);
   HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
   const int64_t nsample = (nparts + pstride - 1) / pstride;
   const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(nsample, kNumCUs * 12)));
-  if (key_bytes == 8)
-    hipLaunchKernelGGL(k_rj_count<int64_t>, grid, dim3(kRCThreads), 0, s, static_cast<const int64_t *>(pkeys), poffs,
-                       static_cast<const int64_t *>(bkeys), boffs, nparts, (int)cap, pstride, counts, overflow);
-  else
-    hipLaunchKernelGGL(k_rj_count<uint32_t>, grid, dim3(kRCThreads), 0, s, static_cast<const uint32_t *>(pkeys), poffs,
-                       static_cast<const uint32_t *>(bkeys), boffs, nparts, (int)cap, pstride, counts, overflow);
+  switch (outer) {
+    case 0:
+      hipLaunchKernelGGL(k_rj_count<0>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
+                         pstride, counts, overflow);
+      break;
+    case 1:
+      hipLaunchKernelGGL(k_rj_count<1>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
+                         pstride, counts, overflow);
+      break;
+    case 2:
+      hipLaunchKernelGGL(k_rj_count<2>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
+                         pstride, counts, overflow);
+      break;
+    default:
+      hipLaunchKernelGGL(k_rj_count<3>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
+                         pstride, counts, overflow);
+  }
   HIP_LAUNCH_CHECK();
 }
 
-void radix_join_write(const void *pkeys, const int64_t *poffs, const void *bkeys, const int64_t *boffs,
+template <bool W8, bool DMA, int OJ>
+static void rj_write_launch(dim3 grid, hipStream_t s, const int64_t *pk, const int64_t *poffs, const int64_t *bk,
+                            const int64_t *boffs, int64_t nparts, int cap, const int64_t *out_offs, const ColSet &pc,
+                            const ColSet &bs, const BuildOut &bo, unsigned long long *cur, int64_t out_cap,
+                            int *overflow, unsigned long long *st, int pkey, uint8_t *ppres, uint8_t *bpres) {
+  hipLaunchKernelGGL((k_rj_write<4, 3, W8, DMA, OJ>), grid, dim3(kRJThreads), 0, s, pk, poffs, bk, boffs, nparts, cap,
+                     out_offs, pc, bs, bo, cur, out_cap, overflow, st, pkey, ppres, bpres);
+}
+
+void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t *bkeys, const int64_t *boffs,
                       int64_t nparts, int64_t cap, const int64_t *out_offs, const uint8_t *const *pin,
                       uint8_t *const *pout, const int *pw, int npc, const uint8_t *const *bin, uint8_t *const *bout,
-                      const int *bw, int nbc, void *stream, int64_t *cursor, int64_t out_cap, int *overflow,
-                      int key_bytes, int64_t kmin, int pkey) {
-  CYLON_CHECK(key_bytes == 8 || key_bytes == 4, Code::Invalid, "radix join key bytes " << key_bytes);
+                      const int *bw, int nbc, void *stream, int64_t *cursor, int64_t out_cap, int *overflow, int pkey,
+                      int outer, uint8_t *ppres, uint8_t *bpres) {
   CYLON_CHECK(pkey >= -1 && pkey < npc, Code::Invalid, "radix join probe key column " << pkey);
   CYLON_CHECK(npc <= kMaxFusedCols && nbc <= kMaxFusedCols, Code::Invalid, "too many columns");
   CYLON_CHECK(out_offs != nullptr || (cursor != nullptr && overflow != nullptr), Code::Invalid,
               "radix join write: needs partition offsets or an output cursor");
-  CYLON_CHECK(cap > 0 && cap <= radix_join_capacity(bw, bin, nbc, key_bytes), Code::Invalid,
+  CYLON_CHECK(outer >= 0 && outer <= 3, Code::Invalid, "radix join outer mode " << outer);
+  CYLON_CHECK(!(outer & kOJProbe) || bpres, Code::Invalid, "radix join: probe-preserving mode needs build presence");
+  CYLON_CHECK(!(outer & kOJBuild) || ppres, Code::Invalid, "radix join: build-preserving mode needs probe presence");
+  CYLON_CHECK(cap > 0 && cap <= radix_join_capacity(bw, bin, nbc, outer & kOJBuild), Code::Invalid,
               "radix join capacity " << cap);
   ColSet pc, bs;
   BuildOut bo;
@@ -2325,7 +1960,7 @@ void radix_join_write(const void *pkeys, const int64_t *poffs, const void *bkeys
     if (q < npc) w8 &= pw[q] == 8;
     if (q < nbc) w8 &= bw[q] == 8;
   }
-  int64_t off = (key_bytes + 2) * cap;
+  int64_t off = (8 + 2) * cap;
   for (int q = 0; q < nbc; ++q)
     if (bin[q]) {
       bo.lds_off[q] = (int)off;
@@ -2333,6 +1968,8 @@ void radix_join_write(const void *pkeys, const int64_t *poffs, const void *bkeys
       bs.in[bs.n] = bin[q];
       bs.width[bs.n++] = bw[q];
     }
+  bo.match_off = (int)off;
+  if (outer & kOJBuild) off += cap;
   CYLON_CHECK(off <= kRJRowArea, Code::Invalid, "radix join LDS rows " << off);
   hipStream_t s = as_stream(stream);
   // probe columns beyond 4 and staged build columns beyond 3 are loaded in place (slower, correct)
@@ -2344,35 +1981,29 @@ void radix_join_write(const void *pkeys, const int64_t *poffs, const void *bkeys
     HIP_CHECK(hipMalloc(&st, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
     HIP_CHECK(hipMemset(st, 0, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
   }
-  const char *om = std::getenv("CYLON_RJ_OWNERMAP");
-  const bool ownermap = om && om[0] == '1';
   const dim3 grid(rj_grid(nparts));
-  const int64_t *pk8 = static_cast<const int64_t *>(pkeys), *bk8 = static_cast<const int64_t *>(bkeys);
-  const uint32_t *pk4 = static_cast<const uint32_t *>(pkeys), *bk4 = static_cast<const uint32_t *>(bkeys);
   // LDS-DMA build staging: write kernel 33.9 -> 32.9 ms per 1B x 1B join (profiles/r03/lds_dma_ab.txt)
   const char *dm = std::getenv("CYLON_RJ_DMA");  // A/B knob: 0 = register staging
   const bool dma = w8 && !(dm && dm[0] == '0');
-  if (key_bytes == 4 && dma)
-    hipLaunchKernelGGL((k_rj_write<4, 3, true, false, uint32_t, true>), grid, dim3(kRJThreads), 0, s, pk4, poffs, bk4,
-                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
-  else if (dma && !ownermap)
-    hipLaunchKernelGGL((k_rj_write<4, 3, true, false, int64_t, true>), grid, dim3(kRJThreads), 0, s, pk8, poffs, bk8,
-                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
-  else if (key_bytes == 4 && w8)
-    hipLaunchKernelGGL((k_rj_write<4, 3, true, false, uint32_t, false>), grid, dim3(kRJThreads), 0, s, pk4, poffs, bk4, boffs,
-                       nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
-  else if (key_bytes == 4)
-    hipLaunchKernelGGL((k_rj_write<4, 3, false, false, uint32_t, false>), grid, dim3(kRJThreads), 0, s, pk4, poffs, bk4,
-                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
-  else if (w8 && ownermap)
-    hipLaunchKernelGGL((k_rj_write<4, 3, true, true, int64_t, false>), grid, dim3(kRJThreads), 0, s, pk8, poffs, bk8, boffs,
-                       nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
-  else if (w8)
-    hipLaunchKernelGGL((k_rj_write<4, 3, true, false, int64_t, false>), grid, dim3(kRJThreads), 0, s, pk8, poffs, bk8, boffs,
-                       nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
-  else
-    hipLaunchKernelGGL((k_rj_write<4, 3, false, false, int64_t, false>), grid, dim3(kRJThreads), 0, s, pk8, poffs, bk8,
-                       boffs, nparts, (int)cap, out_offs, pc, bs, bo, cur, out_cap, overflow, st, kmin, pkey);
+  const int ci = (int)cap;
+#define RJW(W8_, DMA_, OJ_)                                                                                        \
+  rj_write_launch<W8_, DMA_, OJ_>(grid, s, pkeys, poffs, bkeys, boffs, nparts, ci, out_offs, pc, bs, bo, cur, out_cap, \
+                                  overflow, st, pkey, ppres, bpres)
+  if (outer == 0) {
+    if (dma) RJW(true, true, 0);
+    else if (w8) RJW(true, false, 0);
+    else RJW(false, false, 0);
+  } else if (outer == 1) {
+    if (dma) RJW(true, true, 1);
+    else RJW(false, false, 1);
+  } else if (outer == 2) {
+    if (dma) RJW(true, true, 2);
+    else RJW(false, false, 2);
+  } else {
+    if (dma) RJW(true, true, 3);
+    else RJW(false, false, 3);
+  }
+#undef RJW
   HIP_LAUNCH_CHECK();
   if (st) {  // mean cycles per partition: load+stage, index build, count+claim, emit, then to the next
     HIP_CHECK(hipStreamSynchronize(s));

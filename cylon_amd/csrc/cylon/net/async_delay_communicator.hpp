@@ -33,6 +33,10 @@ class AsyncDelayCommunicator : public Communicator {
   std::pair<at::Tensor, std::shared_ptr<P2PRequest>> AllToAllVAsync(const at::Tensor &s,
                                                                     const std::vector<int64_t> &sc,
                                                                     const std::vector<int64_t> &rc) override;
+  std::shared_ptr<P2PRequest> AllToAllVSegmentsAsync(const at::Tensor &send, const std::vector<int64_t> &soff,
+                                                     const std::vector<int64_t> &scnt, const at::Tensor &recv,
+                                                     const std::vector<int64_t> &roff,
+                                                     const std::vector<int64_t> &rcnt) override;
   std::vector<int64_t> ExchangeCounts(const std::vector<int64_t> &c) override { return inner_->ExchangeCounts(c); }
   void AllReduce(at::Tensor &t, ReduceOp op) override { inner_->AllReduce(t, op); }
   at::Tensor AllGather(const at::Tensor &in) override { return inner_->AllGather(in); }
@@ -50,6 +54,7 @@ class AsyncDelayCommunicator : public Communicator {
   void *side_ = nullptr;  // hipStream_t, created on first use
   int side_dev_ = -1;
   int64_t posted_ = 0;
+  void *side_stream(int dev);
   std::shared_ptr<int64_t> in_flight_seen_ = std::make_shared<int64_t>(0);
 };
 

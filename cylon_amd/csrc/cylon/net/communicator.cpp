@@ -187,6 +187,39 @@ std::pair<at::Tensor, std::shared_ptr<P2PRequest>> Communicator::AllToAllVAsync(
   return {AllToAllV(send, sc, rc), std::make_shared<DoneRequest>()};
 }
 
+static void check_segments(int world, const at::Tensor &t, const std::vector<int64_t> &off,
+                           const std::vector<int64_t> &cnt, const char *what) {
+  CYLON_CHECK((int)off.size() == world && (int)cnt.size() == world, Code::Invalid,
+              what << " segments must have world-size entries");
+  const int64_t n = t.dim() == 0 ? 1 : t.size(0);
+  for (int r = 0; r < world; ++r)
+    CYLON_CHECK(cnt[r] >= 0 && off[r] >= 0 && off[r] + cnt[r] <= n, Code::Invalid,
+                what << " segment " << r << " [" << off[r] << ", +" << cnt[r] << ") outside " << n << " elements");
+}
+
+std::shared_ptr<P2PRequest> Communicator::AllToAllVSegmentsAsync(const at::Tensor &send,
+                                                                 const std::vector<int64_t> &soff,
+                                                                 const std::vector<int64_t> &scnt,
+                                                                 const at::Tensor &recv,
+                                                                 const std::vector<int64_t> &roff,
+                                                                 const std::vector<int64_t> &rcnt) {
+  const int w = GetWorldSize();
+  check_segments(w, send, soff, scnt, "send");
+  check_segments(w, recv, roff, rcnt, "receive");
+  std::vector<at::Tensor> pieces;
+  for (int r = 0; r < w; ++r) pieces.push_back(send.slice(0, soff[r], soff[r] + scnt[r]));
+  at::Tensor packed = at::cat(pieces);
+  auto posted = AllToAllVAsync(packed, scnt, rcnt);
+  posted.second->Wait();
+  const at::Tensor &got = posted.first;
+  int64_t at_ = 0;
+  for (int r = 0; r < w; ++r) {
+    if (rcnt[r]) recv.slice(0, roff[r], roff[r] + rcnt[r]).copy_(got.slice(0, at_, at_ + rcnt[r]));
+    at_ += rcnt[r];
+  }
+  return std::make_shared<DoneRequest>();
+}
+
 std::shared_ptr<P2PRequest> Communicator::ISend(const at::Tensor &, int, int) {
   CYLON_THROW(Code::NotImplemented, "point-to-point send needs a distributed communicator");
 }
@@ -284,6 +317,30 @@ std::pair<at::Tensor, std::shared_ptr<P2PRequest>> ProcessGroupCommunicator::All
   }
   // keep `in` alive until completion: c10d works hold their tensors
   return {user, std::make_shared<PGRequest>(work, out, at::Tensor(), type_ != CommType::RCCL)};
+}
+
+std::shared_ptr<P2PRequest> ProcessGroupCommunicator::AllToAllVSegmentsAsync(
+    const at::Tensor &send, const std::vector<int64_t> &soff, const std::vector<int64_t> &scnt,
+    const at::Tensor &recv, const std::vector<int64_t> &roff, const std::vector<int64_t> &rcnt) {
+  // gloo has no list all-to-all; a buffer off the communication device is staged anyway
+  if (type_ != CommType::RCCL || send.device() != device_ || recv.device() != device_)
+    return Communicator::AllToAllVSegmentsAsync(send, soff, scnt, recv, roff, rcnt);
+  check_segments(world_, send, soff, scnt, "send");
+  check_segments(world_, recv, roff, rcnt, "receive");
+  CYLON_CHECK(send.is_contiguous() && recv.is_contiguous() && send.scalar_type() == recv.scalar_type(),
+              Code::Invalid, "segment all-to-all: contiguous buffers of one dtype");
+  trace::add_counter("comm.alltoall_posted", 1);
+  at::Tensor s = send.scalar_type() == at::kBool ? send.view(at::kByte) : send;
+  at::Tensor d = recv.scalar_type() == at::kBool ? recv.view(at::kByte) : recv;
+  std::vector<at::Tensor> in, out;
+  for (int r = 0; r < world_; ++r) {
+    in.push_back(s.slice(0, soff[r], soff[r] + scnt[r]));
+    out.push_back(d.slice(0, roff[r], roff[r] + rcnt[r]));
+  }
+  // ProcessGroupNCCL::alltoall: grouped ncclSend / ncclRecv per peer on the communicator's
+  // stream, straight from and into the views (no staging buffer, no self copy for zero counts)
+  auto work = pg().alltoall(out, in);
+  return std::make_shared<PGRequest>(work, at::Tensor(), at::Tensor(), false);
 }
 
 std::shared_ptr<P2PRequest> ProcessGroupCommunicator::ISend(const at::Tensor &t, int dst, int tag) {

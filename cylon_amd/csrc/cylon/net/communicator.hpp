@@ -75,6 +75,15 @@ class Communicator {
   // Default: the blocking AllToAllV with an already completed request.
   virtual std::pair<at::Tensor, std::shared_ptr<P2PRequest>> AllToAllVAsync(
       const at::Tensor &send, const std::vector<int64_t> &send_counts, const std::vector<int64_t> &recv_counts);
+  // Posted all-to-all between caller-owned buffers at arbitrary per-peer offsets (elements along
+  // dim 0): send[soff[r] .. +scnt[r]) goes to rank r and rank r's piece lands in
+  // recv[roff[r] .. +rcnt[r]).  A zero count (e.g. this rank's own piece, kept in place by the
+  // planned shuffle) moves nothing.  RCCL: one grouped send/recv per peer straight between the
+  // buffers; default: a packed all-to-all plus copies, completed before returning.
+  virtual std::shared_ptr<P2PRequest> AllToAllVSegmentsAsync(const at::Tensor &send, const std::vector<int64_t> &soff,
+                                                             const std::vector<int64_t> &scnt, const at::Tensor &recv,
+                                                             const std::vector<int64_t> &roff,
+                                                             const std::vector<int64_t> &rcnt);
   // Exchange per-peer element counts (the size matrix row of this rank).
   virtual std::vector<int64_t> ExchangeCounts(const std::vector<int64_t> &send_counts) = 0;
   virtual void AllReduce(at::Tensor &t, ReduceOp op) = 0;
@@ -129,6 +138,13 @@ class FaultInjectionCommunicator : public Communicator {
     tick("AllToAllV");
     return inner_->AllToAllVAsync(s, sc, rc);
   }
+  std::shared_ptr<P2PRequest> AllToAllVSegmentsAsync(const at::Tensor &s, const std::vector<int64_t> &so,
+                                                     const std::vector<int64_t> &sc, const at::Tensor &r,
+                                                     const std::vector<int64_t> &ro,
+                                                     const std::vector<int64_t> &rc) override {
+    tick("AllToAllV");
+    return inner_->AllToAllVSegmentsAsync(s, so, sc, r, ro, rc);
+  }
   std::vector<int64_t> ExchangeCounts(const std::vector<int64_t> &c) override {
     tick("ExchangeCounts");
     return inner_->ExchangeCounts(c);
@@ -179,6 +195,10 @@ class ProcessGroupCommunicator : public Communicator {
   std::pair<at::Tensor, std::shared_ptr<P2PRequest>> AllToAllVAsync(
       const at::Tensor &send, const std::vector<int64_t> &send_counts,
       const std::vector<int64_t> &recv_counts) override;
+  std::shared_ptr<P2PRequest> AllToAllVSegmentsAsync(const at::Tensor &send, const std::vector<int64_t> &soff,
+                                                     const std::vector<int64_t> &scnt, const at::Tensor &recv,
+                                                     const std::vector<int64_t> &roff,
+                                                     const std::vector<int64_t> &rcnt) override;
   std::vector<int64_t> ExchangeCounts(const std::vector<int64_t> &send_counts) override;
   void AllReduce(at::Tensor &t, ReduceOp op) override;
   at::Tensor AllGather(const at::Tensor &in) override;

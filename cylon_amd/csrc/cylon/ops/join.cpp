@@ -178,7 +178,7 @@ static bool packs_validity(const TablePtr &t) {
 
 // Partition every column of t (+ validity bytes) by the top `bits` bits of fmix64(key).
 static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Tensor &keys, int bits,
-                                 const RangeSpec *range = nullptr, at::Tensor *narrow_ws = nullptr) {
+                                 const RangeSpec *range = nullptr) {
   std::vector<at::Tensor> cur{keys};
   std::vector<int> widths{8};
   std::vector<int> dslot(t->Columns(), -1), vslot(t->Columns(), -1);
@@ -208,7 +208,7 @@ static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Te
     return e && e[0] == '1';
   }();
   cur = RadixPartition(ex, std::move(cur), widths, bits, &offs, range, packs_validity(t) ? &packed : nullptr,
-                       range != nullptr || force_stable, narrow_ws);
+                       range != nullptr || force_stable);
   RadixSide s;
   s.keys = cur[0];
   s.offs = offs;
@@ -325,15 +325,44 @@ struct JoinSink {
   }
 };
 
+// Outer-join mode of the LDS join kernels (kernel_decls.inc radix_join_count): bit 0 = probe rows
+// without a match are output rows, bit 1 = build rows without a match are.
+static int outer_mode(JoinType jt, bool build_left) {
+  const bool lp = jt == JoinType::LEFT || jt == JoinType::FULL_OUTER;
+  const bool rp = jt == JoinType::RIGHT || jt == JoinType::FULL_OUTER;
+  return ((build_left ? rp : lp) ? 1 : 0) | ((build_left ? lp : rp) ? 2 : 0);
+}
+static bool left_may_null(JoinType jt) { return jt == JoinType::RIGHT || jt == JoinType::FULL_OUTER; }
+static bool right_may_null(JoinType jt) { return jt == JoinType::LEFT || jt == JoinType::FULL_OUTER; }
+
+// validity of the output columns of a side that can be null: the side's presence bytes, AND the
+// column's own validity where the input column was nullable
+static void apply_presence(std::vector<Column> &cols, const TablePtr &in, const at::Tensor &pres, int64_t off,
+                           int64_t m) {
+  if (m == 0) return;
+  at::Tensor p = pres.slice(0, 0, m);
+  for (int c = 0; c < in->Columns(); ++c) {
+    at::Tensor v = cols[c].validity.slice(0, off, off + m);
+    if (in->column(c).nullable()) v.mul_(p);
+    else v.copy_(p);
+  }
+}
+
 // Returns nullptr when a build partition overflows the LDS capacity (heavy key
-// skew / duplicates); the caller then runs the global-table join.  With a sink
-// the rows are written into the sink's columns and the sink's table is returned.
+// skew / duplicates); the caller then runs the global-table join.  With a sink the
+// rows are written into the sink's columns and the sink's table is returned.
+// Every column of both tables is fixed width (radix_eligible); lk / rk are the int64 join keys
+// (a key column itself, or the composite image of several key columns).  All four join types:
+// the kernels emit unmatched rows of the preserved side(s) with presence bytes (outer_mode).
 static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr &right, const at::Tensor &lk,
                            const at::Tensor &rk, const JoinConfig &cfg, JoinSink *sink = nullptr) {
   const int64_t nl = left->Rows(), nr = right->Rows();
   const bool build_left = nl < nr;
   const TablePtr &bt = build_left ? left : right;
   const int64_t nb = std::min(nl, nr);
+  const JoinType jt = cfg.GetType();
+  const int oj = outer_mode(jt, build_left);
+  const bool lnull = left_may_null(jt), rnull = right_may_null(jt);
   // LDS capacity from the build side's staged row width (key column counted once)
   RadixCols shape = radix_cols(bt, nullptr, nullptr);
   for (int c = 0, q = 0; c < bt->Columns(); ++c, ++q) {
@@ -341,51 +370,22 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     if (col.type.width() == 8 && col.data.data_ptr() == (build_left ? lk : rk).data_ptr()) shape.in[q] = nullptr;
     if (col.nullable() && !packs_validity(bt)) ++q;  // packed validity words sit after the columns
   }
-  const int64_t cap8 = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size());
+  const int64_t cap = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size(), (oj & 2) != 0);
   // mean build rows per partition: 0.85 x capacity keeps the largest of ~1M uniform
   // partitions >8 sigma below the capacity (Poisson), and lets 1B rows use 19 bits
   // (passes of 10 + 9 bits; a 9-bit pass streams at ~5.5 TB/s, a 10-bit one ~3.9)
-  const int64_t target = std::max<int64_t>(1, cap8 * 85 / 100);
+  const int64_t target = std::max<int64_t>(1, cap * 85 / 100);
   int bits = 0;
   while ((nb >> bits) > target) ++bits;
   if (const char *xb = std::getenv("CYLON_RJ_EXTRA_BITS"))  // A/B knob: finer partitions
     bits = std::min(bits + std::max(0, std::atoi(xb)), 2 * 10);
   const int64_t nparts = int64_t(1) << bits;
   RadixSide L, R;
-  // Narrow keys: when the two relations' keys span < 2^32 values (one min/max reduction folded
-  // into the first pass's histogram kernel, then one host read), a key's low 32 bits identify
-  // it: the partition hash is taken over them and the key travels as uint32 through the passes
-  // and the join kernels (28 instead of 32 B/row for int64 key + 3 x 8 B payload), rebuilt as
-  // kmin + (low - (uint32)kmin) on output.  Measured SLOWER on MI355X and therefore opt-in
-  // (CYLON_RJ_NARROW=1; profiles/r03/narrow_keys_ab.txt): the 4-byte key column's scattered
-  // 64-B runs write no faster than 8-byte 128-B runs, so the second pass takes 19.8 instead of
-  // 17.9 ms and the write kernel 36.2 instead of 33.8 ms (headline 110-115 -> 119-121 ms).
-  int key_bytes = 8;
-  int64_t kmin = 0;
   {
     CYLON_PHASE("join.radix.partition", ex.device);
-    at::Tensor nws_l, nws_r;
-    const char *ne = std::getenv("CYLON_RJ_NARROW");  // read per join (tests toggle it)
-    const bool narrow_on = ne && ne[0] == '1';
-    if (narrow_on && bits > 0 && !hip::radix_lookback_enabled()) {
-      at::Tensor mm = at::empty({2}, ex.opts(at::kLong));
-      mm.select(0, 0).fill_(std::numeric_limits<int64_t>::max());
-      mm.select(0, 1).fill_(std::numeric_limits<int64_t>::min());
-      nws_l = RadixNarrowPrehist(ex, lk, bits, mm);
-      nws_r = RadixNarrowPrehist(ex, rk, bits, mm);
-      at::Tensor h = mm.cpu();
-      const int64_t lo = h[0].item<int64_t>(), hi = h[1].item<int64_t>();
-      if (lo <= hi && (uint64_t)hi - (uint64_t)lo < (uint64_t(1) << 32)) {
-        key_bytes = 4;
-        kmin = lo;
-        trace::add_counter("join.radix.narrow_keys", 1);
-      }
-    }
-    L = radix_partition(ex, left, lk, bits, nullptr, key_bytes == 4 ? &nws_l : nullptr);
-    R = radix_partition(ex, right, rk, bits, nullptr, key_bytes == 4 ? &nws_r : nullptr);
+    L = radix_partition(ex, left, lk, bits);
+    R = radix_partition(ex, right, rk, bits);
   }
-  const int64_t cap =
-      key_bytes == 8 ? cap8 : hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size(), key_bytes);
   RadixSide &B = build_left ? L : R;
   RadixSide &P = build_left ? R : L;
   // Output size.  Exact mode: a count kernel over every partition, a scan, then the write
@@ -405,20 +405,36 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   const bool exact_count = ec && ec[0] == '1';
   const int64_t fused_min = fm ? std::atoll(fm) : 4096;
   const double est_scale = es ? std::atof(es) : 1.0;
-  const int64_t stride = exact_count || nparts < fused_min ? 1 : std::min<int64_t>(32, std::max<int64_t>(1, nparts / 64));
-  const int64_t nsample = (nparts + stride - 1) / stride;
-  at::Tensor counts = ex.empty_i64(nsample);
+  int64_t stride = exact_count || nparts < fused_min ? 1 : std::min<int64_t>(32, std::max<int64_t>(1, nparts / 64));
+  at::Tensor counts;
   at::Tensor overflow = at::empty({1}, ex.opts(at::kInt));
   at::Tensor out_offs;
   int64_t m = 0, alloc = 0;
   {
     CYLON_PHASE("join.radix.count", ex.device);
-    hip::radix_join_count(P.keys.data_ptr(), ptr<int64_t>(P.offs), B.keys.data_ptr(), ptr<int64_t>(B.offs), nparts,
-                          cap, ptr<int64_t>(counts), overflow.data_ptr<int>(), ex.stream, stride, key_bytes);
+    auto count = [&](int64_t st) {
+      counts = ex.empty_i64((nparts + st - 1) / st);
+      hip::radix_join_count(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
+                            nparts, cap, ptr<int64_t>(counts), overflow.data_ptr<int>(), ex.stream, st, oj);
+    };
+    count(stride);
     // the ranking guard of the stable (second and later) partition passes
     if (hip::rp_take_order_violation(ex.stream)) {
       trace::add_counter("join.radix.order_violation_fallback", 1);
       return nullptr;
+    }
+    if (stride > 1) {
+      // Skew check of the sample: extrapolating a hot key's partition 32x would over-allocate
+      // (ADVICE r03), so a sample whose largest partition output is far above its mean is
+      // counted exactly instead.
+      at::Tensor st = at::stack({counts.sum(), counts.max(), overflow.to(at::kLong)[0]}).cpu();
+      const int64_t ssum = st[0].item<int64_t>(), smax = st[1].item<int64_t>();
+      const int64_t nsample = counts.numel();
+      if (st[2].item<int64_t>() == 0 && smax > 16 * (ssum / std::max<int64_t>(1, nsample)) + 65536) {
+        trace::add_counter("join.radix.skewed_sample_exact_count", 1);
+        stride = 1;
+        count(1);
+      }
     }
     if (stride == 1) {
       out_offs = exclusive_scan(ex, counts);
@@ -435,7 +451,7 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
         trace::add_counter("join.radix.overflow_fallback", 1);
         return nullptr;
       }
-      const double est = (double)tail[0].item<int64_t>() * (double)nparts / (double)nsample;
+      const double est = (double)tail[0].item<int64_t>() * (double)nparts / (double)counts.numel();
       alloc = (int64_t)(est * 1.02 * est_scale) + (est_scale < 1.0 ? 0 : 65536);
       trace::add_counter("join.radix.estimated_rows", (int64_t)est);
     }
@@ -443,24 +459,29 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   CYLON_PHASE("join.radix.write", ex.device);
   std::vector<Column> lcols, rcols;
   std::vector<at::Tensor> lwords, rwords;
+  at::Tensor ppres, bpres;  // presence bytes of the probe / build side (outer joins)
   int64_t off = 0;
   auto allocate = [&](int64_t rows) {
     lcols.clear();
     rcols.clear();
     if (sink) {
-      std::vector<Column> proto;
+      std::vector<Column> proto;  // (the proto's validity only says whether the column is nullable)
       for (const auto &col : left->columns())
-        proto.emplace_back(cfg.GetLeftTablePrefix() + col.name, col.type, 0, col.data, at::Tensor(), col.validity);
+        proto.emplace_back(cfg.GetLeftTablePrefix() + col.name, col.type, 0, col.data, at::Tensor(),
+                           col.nullable() || lnull ? col.data : at::Tensor());
       for (const auto &col : right->columns())
-        proto.emplace_back(cfg.GetRightTablePrefix() + col.name, col.type, 0, col.data, at::Tensor(), col.validity);
+        proto.emplace_back(cfg.GetRightTablePrefix() + col.name, col.type, 0, col.data, at::Tensor(),
+                           col.nullable() || rnull ? col.data : at::Tensor());
       off = sink->reserve(ex, rows, proto);
       lcols.assign(sink->cols.begin(), sink->cols.begin() + left->Columns());
       rcols.assign(sink->cols.begin() + left->Columns(), sink->cols.end());
     } else {
       for (const auto &col : left->columns())
-        lcols.push_back(make_fixed_column(cfg.GetLeftTablePrefix() + col.name, col.type, rows, ex.device, col.nullable()));
+        lcols.push_back(make_fixed_column(cfg.GetLeftTablePrefix() + col.name, col.type, rows, ex.device,
+                                          col.nullable() || lnull));
       for (const auto &col : right->columns())
-        rcols.push_back(make_fixed_column(cfg.GetRightTablePrefix() + col.name, col.type, rows, ex.device, col.nullable()));
+        rcols.push_back(make_fixed_column(cfg.GetRightTablePrefix() + col.name, col.type, rows, ex.device,
+                                          col.nullable() || rnull));
     }
     auto word_outs = [&](const RadixSide &sd) {
       std::vector<at::Tensor> w;
@@ -469,6 +490,8 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     };
     lwords = word_outs(L);
     rwords = word_outs(R);
+    if (oj & 2) ppres = ex.empty_u8(std::max<int64_t>(rows, 1));
+    if (oj & 1) bpres = ex.empty_u8(std::max<int64_t>(rows, 1));
   };
   auto write = [&](int64_t rows, const int64_t *offs, int64_t *cursor) {
     RadixCols pc = build_left ? radix_cols(right, &R, &rcols, off, &rwords) : radix_cols(left, &L, &lcols, off, &lwords);
@@ -481,10 +504,11 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
         pc.in[q] = reinterpret_cast<const uint8_t *>(P.keys.data_ptr());
         if (pkey < 0) pkey = (int)q;
       }
-    hip::radix_join_write(P.keys.data_ptr(), ptr<int64_t>(P.offs), B.keys.data_ptr(), ptr<int64_t>(B.offs), nparts,
-                          cap, offs, pc.in.data(), pc.out.data(), pc.w.data(), (int)pc.in.size(), bc.in.data(),
-                          bc.out.data(), bc.w.data(), (int)bc.in.size(), ex.stream, cursor, rows,
-                          overflow.data_ptr<int>(), key_bytes, kmin, pkey);
+    hip::radix_join_write(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
+                          nparts, cap, offs, pc.in.data(), pc.out.data(), pc.w.data(), (int)pc.in.size(),
+                          bc.in.data(), bc.out.data(), bc.w.data(), (int)bc.in.size(), ex.stream, cursor, rows,
+                          overflow.data_ptr<int>(), pkey, oj, ppres.defined() ? ppres.data_ptr<uint8_t>() : nullptr,
+                          bpres.defined() ? bpres.data_ptr<uint8_t>() : nullptr);
   };
   if (stride == 1) {
     allocate(m);
@@ -522,8 +546,13 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   if (m > 0) {
     unpack_validity_words(ex, left, L, lwords, lcols, off, m);
     unpack_validity_words(ex, right, R, rwords, rcols, off, m);
+    // outer joins: the null side's validity from the presence bytes
+    const at::Tensor &lpres = build_left ? bpres : ppres, &rpres = build_left ? ppres : bpres;
+    if (lnull) apply_presence(lcols, left, lpres, off, m);
+    if (rnull) apply_presence(rcols, right, rpres, off, m);
   }
   trace::add_counter("join.radix.rows_out", m);
+  if (oj) trace::add_counter("join.radix.outer", oj);
   if (sink) return Table::Make(left->GetContext(), sink->cols);
   for (auto &c : rcols) lcols.push_back(std::move(c));
   return Table::Make(left->GetContext(), std::move(lcols));
@@ -746,12 +775,190 @@ static TablePtr range_join(const Exec &ex, const TablePtr &left, const TablePtr 
   return Table::Make(left->GetContext(), std::move(lcols));
 }
 
+// Keys of the LDS radix join (K5).  One simple key column: the column itself.  Several non-null
+// integer key columns: one EXACT composite -- each column's offset from its two-relation minimum,
+// packed into 63 bits when the spans fit -- or else a 64-bit row hash whose matches are verified
+// on the output (reference multi-key join: hash_join.cpp:92-186, TwoTableRowIndexHash).
+struct RadixKeys {
+  at::Tensor l, r;
+  bool ok = false, verify = false;
+};
+
+static bool int_key(const Column &c) {
+  return simple_key(c) && (c.type.kind() == ValueKind::SIGNED_INT ||
+                           (c.type.kind() == ValueKind::UNSIGNED_INT && c.type.width() < 8));
+}
+
+static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
+  const auto &lc = cfg.GetLeftColumnIdx();
+  const auto &rc = cfg.GetRightColumnIdx();
+  RadixKeys k;
+  if (lc.size() == 1) {
+    const Column &a = left->column(lc[0]), &b = right->column(rc[0]);
+    if (!(simple_key(a) && simple_key(b) && a.type == b.type)) return k;
+    k.l = encode_keys(ex, left, lc, true).keys;
+    k.r = encode_keys(ex, right, rc, true).keys;
+    k.ok = true;
+    return k;
+  }
+  for (size_t i = 0; i < lc.size(); ++i) {
+    const Column &a = left->column(lc[i]), &b = right->column(rc[i]);
+    if (!int_key(a) || !int_key(b) || !(a.type == b.type)) return k;
+  }
+  std::vector<at::Tensor> lk, rk, mm;
+  for (size_t i = 0; i < lc.size(); ++i) {
+    lk.push_back(encode_keys(ex, left, {lc[i]}, true).keys);
+    rk.push_back(encode_keys(ex, right, {rc[i]}, true).keys);
+    for (const at::Tensor &x : {lk.back(), rk.back()})
+      if (x.numel()) {
+        auto m2 = at::aminmax(x);
+        mm.push_back(std::get<0>(m2).reshape({1}));
+        mm.push_back(std::get<1>(m2).reshape({1}));
+      } else {
+        mm.push_back(at::full({1}, std::numeric_limits<int64_t>::max(), x.options()));
+        mm.push_back(at::full({1}, std::numeric_limits<int64_t>::min(), x.options()));
+      }
+  }
+  const std::vector<int64_t> h = to_host_vec(at::cat(mm));
+  std::vector<int64_t> lo(lc.size());
+  std::vector<int> nbits(lc.size());
+  int total = 0;
+  for (size_t i = 0; i < lc.size(); ++i) {
+    lo[i] = std::min(h[4 * i], h[4 * i + 2]);
+    const int64_t hi = std::max(h[4 * i + 1], h[4 * i + 3]);
+    const uint64_t span = hi >= lo[i] ? (uint64_t)hi - (uint64_t)lo[i] : 0;
+    int b = 0;
+    while (b < 64 && (span >> b) != 0) ++b;
+    nbits[i] = b;
+    total += b;
+  }
+  k.ok = true;
+  if (total <= 63) {  // exact: key i occupies its own bit range
+    auto pack = [&](const std::vector<at::Tensor> &ks) {
+      at::Tensor acc = at::zeros_like(ks[0]);
+      int sh = 0;
+      for (size_t i = ks.size(); i-- > 0;) {
+        acc.bitwise_or_(at::bitwise_left_shift(ks[i] - lo[i], sh));
+        sh += nbits[i];
+      }
+      return acc;
+    };
+    k.l = pack(lk);
+    k.r = pack(rk);
+    trace::add_counter("join.radix.composite_key", 1);
+    return k;
+  }
+  k.l = encode_keys(ex, left, lc, false).keys;  // row hash of the key columns
+  k.r = encode_keys(ex, right, rc, false).keys;
+  k.verify = true;
+  trace::add_counter("join.radix.hashed_key", 1);
+  return k;
+}
+
+// rows of a hashed-key radix join whose key columns differ (64-bit hash collisions); both sides
+// present rows only (outer rows carry one null side)
+static int64_t key_mismatches(const TablePtr &out, const JoinConfig &cfg, int nleft) {
+  const auto &lc = cfg.GetLeftColumnIdx();
+  const auto &rc = cfg.GetRightColumnIdx();
+  if (out->Rows() == 0) return 0;
+  at::Tensor bad;
+  for (size_t i = 0; i < lc.size(); ++i) {
+    const Column &a = out->column(lc[i]), &b = out->column(nleft + rc[i]);
+    at::Tensor ne = a.data.ne(b.data);
+    if (a.nullable()) ne.logical_and_(a.validity);
+    if (b.nullable()) ne.logical_and_(b.validity);
+    bad = bad.defined() ? bad.logical_or_(ne) : ne;
+  }
+  return bad.sum().item<int64_t>();
+}
+
+// LDS radix join of any large device join (every type, one or several keys, var-width payload
+// columns); nullptr when ineligible or when the kernels report an overflow / collision.  Tables
+// with string / binary / list columns join their fixed-width columns plus a row-number column,
+// and the var-width columns are gathered by those row numbers afterwards (two-pass offsets +
+// bytes gather, row -1 -> null).
+static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const TablePtr &right, const JoinConfig &cfg,
+                               JoinSink *sink) {
+  RadixKeys k = radix_keys(ex, left, right, cfg);
+  if (!k.ok) return nullptr;
+  auto has_var = [](const TablePtr &t) {
+    for (const auto &c : t->columns())
+      if (c.is_var() || c.type.kind() == ValueKind::FIXED_BYTES) return true;
+    return false;
+  };
+  const bool lvar = has_var(left), rvar = has_var(right);
+  // a chunked distributed join writes into its sink: fixed-width tables on exact keys only
+  if ((lvar || rvar || k.verify) && sink) return nullptr;
+  // proxy of a side with var-width columns: its fixed-width columns + the row number
+  static const std::string kRow = "__cylon_row";
+  auto proxy = [&](const TablePtr &t, std::vector<int> &fixed_pos) {
+    std::vector<Column> cols;
+    for (int c = 0; c < t->Columns(); ++c) {
+      const Column &col = t->column(c);
+      if (col.is_var() || col.type.kind() == ValueKind::FIXED_BYTES) continue;
+      fixed_pos.push_back(c);
+      cols.push_back(col);
+    }
+    cols.emplace_back(kRow, DataType(Type::INT64), t->Rows(), at::arange(t->Rows(), ex.opts(at::kLong)));
+    return Table::Make(t->GetContext(), std::move(cols));
+  };
+  std::vector<int> lfix, rfix;
+  TablePtr lp = lvar ? proxy(left, lfix) : left, rp = rvar ? proxy(right, rfix) : right;
+  if (!radix_eligible(lp) || !radix_eligible(rp)) return nullptr;
+  TablePtr out = radix_join(ex, lp, rp, k.l, k.r, cfg, sink);
+  if (!out) return nullptr;
+  if (k.verify) {
+    if (lvar || rvar) {  // key columns sit at other positions in a proxy: verify on the final table below
+    } else if (int64_t bad = key_mismatches(out, cfg, left->Columns())) {
+      trace::add_counter("join.radix.hash_collision_fallback", bad);
+      return nullptr;
+    }
+  }
+  if (!lvar && !rvar) return out;
+  const JoinType jt = cfg.GetType();
+  auto side = [&](const TablePtr &orig, bool var, const std::vector<int> &fix, int first, int np, bool may_null,
+                  const std::string &prefix) {
+    std::vector<Column> cols(orig->Columns());
+    if (!var) {
+      for (int c = 0; c < orig->Columns(); ++c) cols[c] = out->column(first + c);
+      return cols;
+    }
+    for (size_t j = 0; j < fix.size(); ++j) cols[fix[j]] = out->column(first + (int)j);
+    const Column &rid = out->column(first + np - 1);
+    at::Tensor idx = rid.nullable() ? at::where(rid.validity.to(at::kBool), rid.data, at::full({1}, -1, rid.data.options()))
+                                    : rid.data;
+    std::vector<Column> vcols;
+    std::vector<int> vpos;
+    for (int c = 0; c < orig->Columns(); ++c)
+      if (orig->column(c).is_var() || orig->column(c).type.kind() == ValueKind::FIXED_BYTES) {
+        vcols.push_back(orig->column(c));
+        vpos.push_back(c);
+      }
+    TablePtr g = GatherNullable(Table::Make(orig->GetContext(), vcols), idx.contiguous(), may_null);
+    for (size_t j = 0; j < vpos.size(); ++j) cols[vpos[j]] = g->column((int)j).with_name(prefix + g->column((int)j).name);
+    return cols;
+  };
+  std::vector<Column> all = side(left, lvar, lfix, 0, lp->Columns(), left_may_null(jt), cfg.GetLeftTablePrefix());
+  std::vector<Column> rc = side(right, rvar, rfix, lp->Columns(), rp->Columns(), right_may_null(jt),
+                                cfg.GetRightTablePrefix());
+  for (auto &c : rc) all.push_back(std::move(c));
+  TablePtr res = Table::Make(left->GetContext(), std::move(all));
+  trace::add_counter("join.radix.var_gather", 1);
+  if (k.verify)
+    if (int64_t bad = key_mismatches(res, cfg, left->Columns())) {
+      trace::add_counter("join.radix.hash_collision_fallback", bad);
+      return nullptr;
+    }
+  return res;
+}
+
 // Local join.  With a sink (chunked distributed join) the radix path writes into
 // the sink and nullptr is returned; other paths return their table.
 static TablePtr join_local(const TablePtr &left, const TablePtr &right, const JoinConfig &cfg, JoinSink *sink) {
-  if (left->device().is_cuda() && cfg.GetType() == JoinType::INNER && cfg.GetAlgorithm() == JoinAlgorithm::SORT &&
-      cfg.GetLeftColumnIdx().size() == 1 && std::min(left->Rows(), right->Rows()) >= radix_join_min_rows() &&
-      radix_eligible(left) && radix_eligible(right)) {
+  const bool big = left->device().is_cuda() && std::min(left->Rows(), right->Rows()) >= radix_join_min_rows();
+  const JoinType jt = cfg.GetType();
+  if (big && jt == JoinType::INNER && cfg.GetAlgorithm() == JoinAlgorithm::SORT &&
+      cfg.GetLeftColumnIdx().size() == 1 && radix_eligible(left) && radix_eligible(right)) {
     const Column &a = left->column(cfg.GetLeftColumnIdx()[0]);
     const Column &b = right->column(cfg.GetRightColumnIdx()[0]);
     if (simple_key(a) && simple_key(b) && a.type == b.type && a.type.kind() != ValueKind::FLOAT) {
@@ -761,23 +968,17 @@ static TablePtr join_local(const TablePtr &left, const TablePtr &right, const Jo
       return sorted_merge_join(ex, left, right, cfg);
     }
   }
-  if (left->device().is_cuda() && cfg.GetType() == JoinType::INNER && cfg.GetAlgorithm() == JoinAlgorithm::HASH &&
-      cfg.GetLeftColumnIdx().size() == 1 && std::min(left->Rows(), right->Rows()) >= radix_join_min_rows() &&
-      radix_eligible(left) && radix_eligible(right)) {
-    const Column &a = left->column(cfg.GetLeftColumnIdx()[0]);
-    const Column &b = right->column(cfg.GetRightColumnIdx()[0]);
-    if (simple_key(a) && simple_key(b) && a.type == b.type) {
-      Exec ex(left->device());
-      KeyEncoding lk = encode_keys(ex, left, cfg.GetLeftColumnIdx(), true);
-      KeyEncoding rk = encode_keys(ex, right, cfg.GetRightColumnIdx(), true);
-      if (TablePtr out = radix_join(ex, left, right, lk.keys, rk.keys, cfg, sink)) return sink ? nullptr : out;
-    }
+  // the LDS radix hash join: hash joins of every type, and sort-algorithm outer / multi-key
+  // joins (their output order is unspecified, docs/semantics.md)
+  if (big && (cfg.GetAlgorithm() == JoinAlgorithm::HASH || jt != JoinType::INNER ||
+              cfg.GetLeftColumnIdx().size() > 1)) {
+    Exec ex(left->device());
+    if (TablePtr out = radix_join_any(ex, left, right, cfg, sink)) return sink ? nullptr : out;
   }
   TablePtr l = left, r = right;
   auto idx = join_impl(left, right, cfg, true, &l, &r);
-  const JoinType jt = cfg.GetType();
-  const bool lnull = jt == JoinType::RIGHT || jt == JoinType::FULL_OUTER;
-  const bool rnull = jt == JoinType::LEFT || jt == JoinType::FULL_OUTER;
+  const bool lnull = left_may_null(jt);
+  const bool rnull = right_may_null(jt);
   CYLON_PHASE("join.materialize", l->device());
   TablePtr lo = GatherNullable(l, idx.first, lnull);
   TablePtr ro = GatherNullable(r, idx.second, rnull);

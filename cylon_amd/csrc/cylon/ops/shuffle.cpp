@@ -614,6 +614,226 @@ static at::Tensor counts_device(const TablePtr &t, const std::vector<int> &cols,
   return hash_pids_counts(t, cols, P).second;
 }
 
+
+// ---------------------------------------------------------------------------
+// Gapped exchange layout of one relation (planned_shuffle).  The sender's rows are laid out in
+// partition-major order (pid = chunk * W + rank, the reference's modulo partition refined into K
+// hash chunks) with, right after each chunk's OWN bucket, a receive region for the rows the other
+// ranks send this rank in that chunk:
+//   chunk k: [bucket (k,0)] ... [bucket (k,me)] [recv from 0 .. W-1, r != me] [bucket (k,me+1)] ...
+// so chunk k's input to the local operator is the contiguous range [own rows | received rows]:
+// the own partition never crosses the communicator (reference: table.cpp:89-106 keeps its piece
+// off MPI) and received rows land where the operator reads them (no concatenation copy).  The
+// reorder pass writes the gaps itself (kernels/radix_join.hip k_ts_offsets `extra`).  With
+// config shuffle_self_rccl=1 the own bucket is sent to this rank as well and chunk k's input is
+// its receive region alone (test knob: RCCL kernels run at world 1).
+// ---------------------------------------------------------------------------
+struct GapPlan {
+  int W = 1, K = 1, me = 0;
+  bool self_wire = false;
+  int64_t total = 0;                                     // rows of a layout column
+  std::vector<int64_t> bucket_base;                      // [W*K] first layout row of each partition
+  std::vector<uint32_t> extra;                           // [2^bits(W*K)] gap rows before each bucket
+  std::vector<int64_t> recv_base, recv_rows;             // [K] receive region of chunk k
+  std::vector<std::vector<int64_t>> send_off, send_cnt;  // [K][W] (layout rows)
+  std::vector<std::vector<int64_t>> recv_off, recv_cnt;  // [K][W]
+  std::vector<int64_t> in_off, in_rows;                  // [K] chunk k's input range
+};
+
+static GapPlan gap_plan(int W, int K, int me, bool self_wire, const std::function<int64_t(int, int, int)> &cnt,
+                        uint32_t P) {
+  GapPlan g;
+  g.W = W;
+  g.K = K;
+  g.me = me;
+  g.self_wire = self_wire;
+  uint32_t nbk = 1;
+  while (nbk < P) nbk <<= 1;
+  g.bucket_base.assign(P, 0);
+  g.extra.assign(std::max<uint32_t>(nbk, 2), 0);
+  g.recv_base.assign(K, 0);
+  g.recv_rows.assign(K, 0);
+  g.send_off.assign(K, std::vector<int64_t>(W, 0));
+  g.send_cnt = g.recv_off = g.recv_cnt = g.send_off;
+  g.in_off.assign(K, 0);
+  g.in_rows.assign(K, 0);
+  int64_t row = 0, own = 0;  // own: rows of the sender's buckets placed so far
+  for (int k = 0; k < K; ++k)
+    for (int r = 0; r < W; ++r) {
+      const uint32_t pid = (uint32_t)k * W + r;
+      g.bucket_base[pid] = row;
+      g.extra[pid] = (uint32_t)(row - own);
+      const int64_t c = cnt(k, me, r);
+      g.send_off[k][r] = row;
+      g.send_cnt[k][r] = (r == me && !self_wire) ? 0 : c;
+      row += c;
+      own += c;
+      if (r != me) continue;
+      g.recv_base[k] = row;
+      for (int src = 0; src < W; ++src) {
+        g.recv_off[k][src] = row;
+        g.recv_cnt[k][src] = (src == me && !self_wire) ? 0 : cnt(k, src, me);
+        row += g.recv_cnt[k][src];
+      }
+      g.recv_rows[k] = row - g.recv_base[k];
+      g.in_off[k] = self_wire ? g.recv_base[k] : g.bucket_base[pid];
+      g.in_rows[k] = g.recv_rows[k] + (self_wire ? 0 : c);
+    }
+  for (uint32_t p = P; p < (uint32_t)g.extra.size(); ++p) g.extra[p] = (uint32_t)(row - own);  // unused digits
+  g.total = row;
+  return g;
+}
+
+// ts[i] reordered into its gapped layout (columns of g.total rows; agreed-nullable columns get a
+// validity buffer whatever this rank holds).  Fast path: ONE LDS-staged mod-partition pass writes
+// the gaps itself; otherwise a partition-major reorder is copied bucket-range by bucket-range.
+static TablePtr layout_reorder(const TablePtr &t, const std::vector<int> &kcols, uint32_t P, const GapPlan &g,
+                               const std::vector<int64_t> &nullable, bool fast, bool *used_fast) {
+  Exec ex(t->device());
+  const int64_t n = t->Rows();
+  *used_fast = false;
+  if (fast && n > 0 && g.total < (int64_t(1) << 32)) {
+    const int key = kcols[0];
+    const Column &kc = t->column(key);
+    std::vector<at::Tensor> src{kc.data};
+    std::vector<int> widths{8};
+    std::vector<int> dslot(t->Columns(), 0), vslot(t->Columns(), -1);
+    for (int c = 0; c < t->Columns(); ++c) {
+      const Column &col = t->column(c);
+      if (c != key) {
+        dslot[c] = (int)src.size();
+        src.push_back(col.data);
+        widths.push_back(col.type.width());
+      }
+      if (col.nullable()) {
+        vslot[c] = (int)src.size();
+        src.push_back(col.validity);
+        widths.push_back(1);
+      }
+    }
+    const BytePacking bp = PackByteColumns(ex, src, widths, n);
+    std::vector<at::Tensor> out;
+    std::vector<const uint8_t *> in;
+    std::vector<uint8_t *> outp;
+    for (auto &x : src) {
+      out.push_back(at::empty({g.total}, x.options()));
+      in.push_back(reinterpret_cast<const uint8_t *>(x.data_ptr()));
+      outp.push_back(reinterpret_cast<uint8_t *>(out.back().data_ptr()));
+    }
+    at::Tensor ws = ex.empty_i64(hip::radix_mod_rows_pass_workspace(n, P));
+    at::Tensor extra = at::from_blob(const_cast<uint32_t *>(g.extra.data()), {(int64_t)g.extra.size()},
+                                     at::TensorOptions().dtype(at::kInt))
+                           .to(ex.device);
+    if (hip::radix_mod_rows_pass_gapped(reinterpret_cast<const int64_t *>(in[0]), n, P, in.data(), outp.data(),
+                                        widths.data(), (int)in.size(), ptr<int64_t>(ws), ex.stream,
+                                        reinterpret_cast<const uint32_t *>(ptr<int32_t>(extra)), g.total)) {
+      out = UnpackByteColumns(ex, bp, std::move(out), g.total);
+      std::vector<Column> cols;
+      for (int c = 0; c < t->Columns(); ++c) {
+        const Column &col = t->column(c);
+        at::Tensor v = vslot[c] >= 0 ? out[vslot[c]] : at::Tensor();
+        if (!v.defined() && nullable[c]) v = at::ones({g.total}, ex.opts(at::kByte));
+        cols.emplace_back(col.name, col.type, g.total, out[dslot[c]], at::Tensor(), v);
+      }
+      *used_fast = true;
+      trace::add_counter("shuffle.gapped_pass", 1);
+      return Table::Make(t->GetContext(), std::move(cols));
+    }
+  }
+  // partition-major reorder, then two range copies per chunk (buckets up to the own one, the rest)
+  trace::add_counter("shuffle.gapped_copy", 1);
+  std::pair<TablePtr, std::vector<int64_t>> ro =
+      fast ? std::make_pair(mod_reorder(t, kcols[0], P), std::vector<int64_t>())
+           : PartitionReorder(t, hash_pids(t, kcols, P), P);
+  std::vector<Column> cols;
+  for (int c = 0; c < t->Columns(); ++c) {
+    const Column &col = t->column(c);
+    Column o = make_fixed_column(col.name, col.type, g.total, ex.device, nullable[c] != 0);
+    if (o.nullable()) o.validity.fill_(1);
+    cols.push_back(std::move(o));
+  }
+  TablePtr lay = Table::Make(t->GetContext(), cols);
+  int64_t src_row = 0;
+  for (int k = 0; k < g.K; ++k)
+    for (int part = 0; part < 2; ++part) {
+      const int r0 = part == 0 ? 0 : g.me + 1, r1 = part == 0 ? g.me + 1 : g.W;
+      if (r0 >= r1) continue;
+      const int64_t dst = g.bucket_base[(size_t)k * g.W + r0];
+      int64_t len = 0;
+      for (int r = r0; r < r1; ++r) len += (r == g.me && !g.self_wire) ? g.in_rows[k] - g.recv_rows[k] : g.send_cnt[k][r];
+      if (len == 0) continue;
+      for (int c = 0; c < t->Columns(); ++c) {
+        Column d = lay->column(c).slice(dst, len);
+        Column sc = ro.first->column(c).slice(src_row, len);
+        d.data.copy_(sc.data);
+        if (d.nullable() && sc.nullable()) d.validity.copy_(sc.validity);
+      }
+      src_row += len;
+    }
+  return lay;
+}
+
+struct GapPending {
+  std::vector<std::shared_ptr<net::P2PRequest>> reqs;
+  std::vector<std::pair<int, at::Tensor>> widen;  // (column, received narrowed values of chunk k)
+};
+
+// posts chunk k of a gapped layout: one segment all-to-all per column buffer
+static GapPending post_gapped(const TablePtr &lay, const GapPlan &g, int k, const WirePlan &plan,
+                              const std::vector<at::Tensor> &wire, const std::vector<int64_t> &nullable) {
+  GapPending pd;
+  auto comm = lay->GetContext()->GetCommunicator();
+  int64_t moving = 0;
+  for (int r = 0; r < g.W; ++r) moving += g.send_cnt[k][r] + g.recv_cnt[k][r];
+  if (moving == 0) return pd;  // nothing crosses the wire in this chunk (world 1, own rows local)
+  Exec ex(lay->device());
+  auto scaled = [](std::vector<int64_t> v, int64_t per, int64_t minus) {
+    for (auto &x : v) x = (x - minus) * per;
+    return v;
+  };
+  for (int c = 0; c < lay->Columns(); ++c) {
+    const Column &col = lay->column(c);
+    const int64_t per = col.type.kind() == ValueKind::FIXED_BYTES ? col.type.width() : 1;
+    if (nullable[c])
+      pd.reqs.push_back(comm->AllToAllVSegmentsAsync(col.validity, g.send_off[k], g.send_cnt[k], col.validity,
+                                                     g.recv_off[k], g.recv_cnt[k]));
+    if (!plan.narrow.empty() && plan.narrow[c]) {
+      at::Tensor tmp = at::empty({std::max<int64_t>(g.recv_rows[k], 1)}, ex.opts(at::kInt));
+      pd.reqs.push_back(comm->AllToAllVSegmentsAsync(wire[c], g.send_off[k], g.send_cnt[k], tmp,
+                                                     scaled(g.recv_off[k], 1, g.recv_base[k]), g.recv_cnt[k]));
+      pd.widen.push_back({c, tmp});
+    } else {
+      pd.reqs.push_back(comm->AllToAllVSegmentsAsync(col.data, scaled(g.send_off[k], per, 0), scaled(g.send_cnt[k], per, 0),
+                                                     col.data, scaled(g.recv_off[k], per, 0),
+                                                     scaled(g.recv_cnt[k], per, 0)));
+    }
+  }
+  if (trace::enabled()) {
+    int64_t pending = 0;
+    for (auto &r : pd.reqs) pending += r->Test() ? 0 : 1;
+    trace::add_counter("shuffle.requests_posted", (int64_t)pd.reqs.size());
+    trace::add_counter("shuffle.requests_pending_after_post", pending);
+  }
+  return pd;
+}
+
+// waits for chunk k (stream waits on RCCL), widens narrowed columns into place, returns the input
+static TablePtr finish_gapped(const TablePtr &lay, const GapPlan &g, int k, GapPending &pd, const WirePlan &plan) {
+  int64_t in_flight = 0;
+  for (auto &r : pd.reqs) in_flight += r->Test() ? 0 : 1;
+  trace::add_counter("shuffle.requests_waited", (int64_t)pd.reqs.size());
+  trace::add_counter("shuffle.requests_in_flight_at_wait", in_flight);
+  for (auto &r : pd.reqs) r->Wait();
+  Exec ex(lay->device());
+  for (auto &w : pd.widen) {
+    const Column &col = lay->column(w.first);
+    if (g.recv_rows[k] > 0)
+      KCALL(ex, widen_u32, reinterpret_cast<const uint32_t *>(ptr<int32_t>(w.second)), g.recv_rows[k],
+            plan.base[w.first], ptr<int64_t>(col.data) + g.recv_base[k]);
+  }
+  return Slice(lay, g.in_off[k], g.in_rows[k]);
+}
+
 // ts: one or two tables (the binary operators shuffle both relations in one plan).
 static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<std::vector<int>> &tcols,
                             bool allow_chunks,
@@ -694,12 +914,19 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
   }
   const int64_t off_null = NT, off_mm = off_null + coff[NT], off_cnt = off_mm + 2 * (int64_t)cand.size();
   CYLON_CHECK(off_cnt + (int64_t)NT * P == D, Code::ExecutionError, "shuffle descriptor layout");
+  // own rows through the communicator as well (test knob: keeps the RCCL kernels running at world 1)
+  std::string sw = ctx->GetConfig("shuffle_self_rccl", "");
+  if (sw.empty())
+    if (const char *e = std::getenv("CYLON_SHUFFLE_SELF_RCCL")) sw = e;
+  const bool self_wire = sw == "1";
   int K = Kc;
   if (!forced) {  // chunked when every rank holds >= 2^24 rows of every table
     int64_t mn = std::numeric_limits<int64_t>::max();
     for (int r = 0; r < W; ++r)
       for (int i = 0; i < NT; ++i) mn = std::min(mn, g[r * D + i]);
     K = mn >= (int64_t(1) << 24) ? Kc : 1;
+    // nothing crosses the wire at world 1 (the own partition stays in place): no transfer to overlap
+    if (W == 1 && !self_wire) K = 1;
   }
   std::vector<int64_t> nullable(coff[NT], 0);
   for (int r = 0; r < W; ++r)
@@ -729,55 +956,66 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
     return s;
   };
   const uint32_t PK = (uint32_t)W * (uint32_t)K;
-  std::vector<TablePtr> wired(NT);
-  std::vector<std::vector<PendingTable>> pend(NT, std::vector<PendingTable>(K));
-  std::vector<std::vector<int64_t>> off(NT, std::vector<int64_t>(K + 1, 0));
+  if (PK == 1 && !self_wire) {  // world 1, one chunk: every row is already where it is consumed
+    trace::add_counter("shuffle.self_rows_kept_local", ts[0]->Rows() + (NT > 1 ? ts[1]->Rows() : 0));
+    trace::add_counter("shuffle.chunks", 1);
+    consume(0, 1, ts);
+    return;
+  }
+  std::vector<GapPlan> gp;
+  for (int i = 0; i < NT; ++i)
+    gp.push_back(gap_plan(W, K, me, self_wire, [&](int k, int from, int to) { return cnt(i, k, from, to); }, PK));
+  std::vector<TablePtr> lay(NT);
+  std::vector<std::vector<GapPending>> pend(NT, std::vector<GapPending>(K));
+  std::vector<std::vector<at::Tensor>> wire(NT);  // per column: narrowed send buffer (or undefined)
   auto post = [&](int side, int k) {
-    std::vector<int64_t> sc(W), rc(W);
-    int64_t tot = 0;
-    for (int r = 0; r < W; ++r) {
-      sc[r] = cnt(side, k, me, r);
-      rc[r] = cnt(side, k, r, me);
-      tot += sc[r];
-    }
-    off[side][k + 1] = off[side][k] + tot;
     const std::vector<int64_t> flags(nullable.begin() + coff[side], nullable.begin() + coff[side + 1]);
-    PendingTable pt = AllToAllPost(Slice(wired[side], off[side][k], tot), sc, rc, flags);
-    attach_plan(pt, ts[side], plans[side]);
-    count_pending(pt);
-    pend[side][k] = std::move(pt);
+    pend[side][k] = post_gapped(lay[side], gp[side], k, plans[side], wire[side], flags);
   };
   int nfast = 0;
   {
     CYLON_PHASE("shuffle.reorder+post", dev);
     for (int i = 0; i < NT; ++i) {  // table i's first chunk transfers while table i+1 is reordered
-      const bool f = K == Kc ? fast[i] : mod_pass_eligible(ts[i], tcols[i], PK);
-      nfast += f ? 1 : 0;
-      TablePtr ro = f ? mod_reorder(ts[i], tcols[i][0], PK) : PartitionReorder(ts[i], hash_pids(ts[i], tcols[i], PK), PK).first;
-      wired[i] = to_wire(ro, plans[i]);
+      const std::vector<int64_t> flags(nullable.begin() + coff[i], nullable.begin() + coff[i + 1]);
+      bool fastpath = false;
+      lay[i] = layout_reorder(ts[i], tcols[i], PK, gp[i], flags, K == Kc ? fast[i] : mod_pass_eligible(ts[i], tcols[i], PK),
+                              &fastpath);
+      nfast += fastpath ? 1 : 0;
+      wire[i].assign(ts[i]->Columns(), at::Tensor());
+      for (int c = 0; c < ts[i]->Columns(); ++c)
+        if (plans[i].narrow[c]) {
+          const Column &col = lay[i]->column(c);
+          Exec ex(dev);
+          wire[i][c] = at::empty({col.length}, ex.opts(at::kInt));
+          KCALL(ex, narrow_i64, ptr<int64_t>(col.data), col.length, plans[i].base[c],
+                reinterpret_cast<uint32_t *>(ptr<int32_t>(wire[i][c])));
+        }
       post(i, 0);
     }
     for (int k = 1; k < K; ++k)
       for (int i = 0; i < NT; ++i) post(i, k);
   }
-  int64_t rows_in = 0, bytes_in = 0;
+  int64_t rows_in = 0, bytes_in = 0, self_rows = 0;
   for (const TablePtr &t : ts) {
     rows_in += t->Rows();
     bytes_in += t->nbytes();
   }
+  for (int i = 0; i < NT; ++i)
+    for (int k = 0; k < K; ++k) self_rows += self_wire ? 0 : cnt(i, k, me, me);
   trace::add_counter("shuffle.fast_partition", nfast);
   trace::add_counter("shuffle.rows_in", rows_in);
   trace::add_counter("shuffle.bytes_in", bytes_in);
+  trace::add_counter("shuffle.self_rows_kept_local", self_rows);
   trace::add_counter("shuffle.chunks", K);
   for (int k = 0; k < K; ++k) {
     std::vector<TablePtr> got(NT);
     {
       CYLON_PHASE("shuffle.wait", dev);
-      for (int i = 0; i < NT; ++i) got[i] = AllToAllFinish(pend[i][k]);
+      for (int i = 0; i < NT; ++i) got[i] = finish_gapped(lay[i], gp[i], k, pend[i][k], plans[i]);
     }
     int64_t rows_out = 0;
     for (int i = 0; i < NT; ++i) {
-      pend[i][k] = PendingTable();
+      pend[i][k] = GapPending();
       rows_out += got[i]->Rows();
     }
     trace::add_counter("shuffle.rows_out", rows_out);

@@ -160,8 +160,7 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
   // pass's per-tile histogram (bits [0, 10) of the image), folded below when the pass digit starts
   // at bit 0 -- the separate reduction read every key once more (3.3 ms of a 2B-row sort)
   const char *ph = std::getenv("CYLON_SORT_PREHIST");  // A/B knob: 0 = separate reduction + histogram
-  const bool prehist = raw_in && n > 0 && hip::radix_xt_enabled() && !hip::radix_lookback_enabled() &&
-                       !(ph && ph[0] == '0');
+  const bool prehist = raw_in && n > 0 && hip::radix_xt_enabled() && !(ph && ph[0] == '0');
   at::Tensor pre_ws;
   uint64_t diff;
   if (prehist) {
@@ -203,19 +202,11 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
       max_db = std::max(max_db, db);
       sh += db;
     }
-    // chained-scan passes: every pass's digit counts from one read of the keys (pass 0's input,
-    // imaged by the same flip as pass 0's digit) instead of a histogram kernel per pass
-    const bool lbm = npass >= 2 && hip::radix_lookback_enabled();
-    at::Tensor ws, lbws;
-    if (lbm) {
-      lbws = ex.empty_i64(hip::radix_lb_workspace(n, max_db));
-      hip::radix_lb_prepare_sort(ptr<int64_t>(cur[0]), n, raw_in ? key_xor : 0ull, shifts.data(), dbits.data(), npass,
-                                 max_db, ptr<int64_t>(lbws), ex.stream);
-    }
+    at::Tensor ws;
     int shift = lo;
     for (int ps = 0; ps < npass; ++ps) {
       const int db = dbits[ps];
-      const int64_t wsn = lbm ? 1 : hip::radix_rows_pass_workspace(n, db);
+      const int64_t wsn = hip::radix_rows_pass_workspace(n, db);
       if (!ws.defined() || ws.numel() < wsn) ws = ex.empty_i64(wsn);
       std::vector<at::Tensor> nxt;
       std::vector<const uint8_t *> in;
@@ -230,12 +221,11 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
       // raw_in: the first pass ranks key ^ key_xor and stores it (raw -> image); the last
       // pass XORs again (image -> raw); one pass does both (stores the raw key)
       const uint64_t flip = ps == 0 && raw_in ? key_xor : 0ull;
-      const bool pre = prehist && ps == 0 && shift == 0 && db <= 10 && !lbm;
+      const bool pre = prehist && ps == 0 && shift == 0 && db <= 10;
       if (pre) hip::radix_sort_prehist_fold(ptr<int64_t>(pre_ws), n, db, ptr<int64_t>(ws), ex.stream);
       hip::radix_sort_rows_pass(ptr<int64_t>(cur[0]), n, shift, db, in.data(), out.data(), widths.data(),
                                 (int)cur.size(), ptr<int64_t>(ws), ex.stream,
-                                flip ^ (ps + 1 == npass && key_in_last_pass ? key_xor : 0ull), flip,
-                                lbm ? ptr<int64_t>(lbws) : nullptr, ps, max_db, pre);
+                                flip ^ (ps + 1 == npass && key_in_last_pass ? key_xor : 0ull), flip, pre);
       if (ps == 0) pre_ws = at::Tensor();  // 10-bit tile histogram consumed
       cur = std::move(nxt);
       shift += db;

@@ -66,18 +66,9 @@ struct RangeSpec {
 // keep_packed != nullptr: validity-style 1-byte columns that were packed 8 per 8-byte word
 // for the passes stay packed -- their slots come back undefined, the words are appended
 // to the result and *keep_packed lists the packed column indices in byte order.
-// narrow_ws != nullptr: narrow-key join passes (hash partitions only; kernel_decls.inc
-// radix_narrow_*): cols[0] (int64 keys whose two-relation range is < 2^32) leaves as uint32
-// (int32 tensor) and *narrow_ws holds the first pass's histogram from RadixNarrowPrehist.
 std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> cols, const std::vector<int> &widths,
                                        int bits, at::Tensor *offs, const RangeSpec *range = nullptr,
-                                       std::vector<int> *keep_packed = nullptr, bool stable = true,
-                                       at::Tensor *narrow_ws = nullptr);
-// First-pass histogram of a narrow-key join (returned workspace for RadixPartition's narrow_ws)
-// plus the keys' min / max folded into mm (int64[2], preset to INT64_MAX / INT64_MIN).
-at::Tensor RadixNarrowPrehist(const Exec &ex, const at::Tensor &keys, int bits, const at::Tensor &mm);
-// digit bits of the first LSD pass of a `bits`-bit radix partitioning
-int RadixFirstDigitBits(int bits);
+                                       std::vector<int> *keep_packed = nullptr, bool stable = true);
 
 // Row-moving passes (k_rows_pass) take their all-8-byte path only when every moved
 // column is 8 bytes wide; validity bytes beside 8-byte columns therefore travel packed

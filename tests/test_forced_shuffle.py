@@ -14,7 +14,7 @@ def _frame(df):
     return df.sort_values(list(df.columns), kind="mergesort").reset_index(drop=True)
 
 
-def _ops(ctx, chunks):
+def _ops(ctx, chunks, self_wire):
     from cylon_amd import CylonContext, Table
     from cylon_amd._lib import C
     rng = np.random.default_rng(1)
@@ -23,6 +23,7 @@ def _ops(ctx, chunks):
     b = pd.DataFrame({"k": rng.integers(0, 15_000, n), "v": rng.random(n), "s": [f"s{i % 17}" for i in range(n)]})
     local = CylonContext()
     res = {}
+    ctx.add_config("shuffle_self_rccl", "1" if self_wire else "0")
     for forced in (False, True):
         ctx.add_config("force_shuffle", "1" if forced else "0")
         ctx.add_config("shuffle_chunks", str(chunks))
@@ -43,13 +44,19 @@ def _ops(ctx, chunks):
     return res, ref
 
 
-@pytest.mark.parametrize("chunks", [1, 3])
-def test_force_shuffle_world1_matches_local(chunks):
-    res, ref = run_distributed(_ops, 1, chunks)[0]
+@pytest.mark.parametrize("chunks,self_wire", [(1, True), (3, True), (3, False)])
+def test_force_shuffle_world1_matches_local(chunks, self_wire):
+    """self_wire (config shuffle_self_rccl=1): the own partition goes through the communicator
+    too, so a world-1 context exercises the posted exchanges; without it the own rows stay in
+    place (reference table.cpp:89-106) and nothing is posted for the fixed-width operators."""
+    res, ref = run_distributed(_ops, 1, chunks, self_wire)[0]
     plain, pc = res[False]
     forced, fc = res[True]
     assert pc.get("shuffle.requests_waited", 0) == 0  # world-1 shortcut: no exchange
-    assert fc.get("shuffle.requests_waited", 0) > 0, fc  # forced: every op went through the exchange
+    if self_wire:
+        assert fc.get("shuffle.requests_waited", 0) > 0, fc  # forced: every op went through the exchange
+    else:
+        assert fc.get("shuffle.self_rows_kept_local", 0) > 0, fc
     if chunks > 1:
         assert fc.get("shuffle.chunks", 0) >= chunks and fc["shuffle.chunks"] % chunks == 0  # summed over ops
     pd.testing.assert_frame_equal(_frame(forced["join"]), _frame(ref), check_dtype=False)

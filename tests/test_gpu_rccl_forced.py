@@ -26,12 +26,15 @@ def _sorted_frame(df):
     return df.sort_values(list(df.columns), kind="mergesort").reset_index(drop=True)
 
 
-def _forced(ctx, chunks, n):
+def _forced(ctx, chunks, n, self_wire=True):
     import torch
     from cylon_amd import CylonContext, Table
     from cylon_amd._lib import C
     assert ctx.get_world_size() == 1 and ctx.on_gpu and ctx.is_distributed()
     ctx.add_config("force_shuffle", "1")
+    # the own partition normally stays in place (nothing to send at world 1); the knob routes it
+    # through RCCL so these tests keep driving real RCCL kernels on one GPU
+    ctx.add_config("shuffle_self_rccl", "1" if self_wire else "0")
     ctx.add_config("shuffle_chunks", str(chunks))
     cpu = CylonContext(device="cpu")
     g = torch.Generator(device="cuda").manual_seed(5)
@@ -65,9 +68,9 @@ def _forced(ctx, chunks, n):
     return out, join_counters, dict(C.trace_counters())
 
 
-@pytest.mark.parametrize("chunks", [1, 4])
-def test_forced_rccl_shuffle_matches_cpu_twin(chunks):
-    out, jc, oc = run_distributed(_forced, 1, chunks, 2_000_000, device="cuda:0", env=RCCL)[0]
+@pytest.mark.parametrize("chunks,self_wire", [(1, True), (4, True), (4, False)])
+def test_forced_rccl_shuffle_matches_cpu_twin(chunks, self_wire):
+    out, jc, oc = run_distributed(_forced, 1, chunks, 2_000_000, self_wire, device="cuda:0", env=RCCL)[0]
     for op, (got, exp) in out.items():
         assert len(got) == len(exp) > 0, op
         if op == "sort":  # globally ordered by (k, x); ties in any order
@@ -80,6 +83,11 @@ def test_forced_rccl_shuffle_matches_cpu_twin(chunks):
         else:
             got, exp = _sorted_frame(got), _sorted_frame(exp)
         pd.testing.assert_frame_equal(got, exp, check_dtype=False, obj=op)
+    if not self_wire:  # the own rows never left the layout: the join read them in place
+        assert jc.get("shuffle.self_rows_kept_local", 0) == 4_000_000, jc
+        assert jc.get("shuffle.requests_waited", 0) == 0, jc
+        assert jc.get("join.radix.rows_out", 0) == len(out["join"][0]), jc
+        return
     # the exchange ran through RCCL work handles: requests were posted, were still running on
     # the RCCL stream after posting (PGRequest::Test() == false: asynchronous to the host), and
     # were waited on by their consumers.  (Whether one is still running when its consumer

@@ -243,6 +243,41 @@ def test_pipelined_distributed_sort(world, chunks, delay_us, asc):
     assert max(loads) <= 1.5 * len(allin) / world, loads
 
 
+def _one_rank_nulls_case(ctx):
+    import pyarrow as pa
+    from cylon_amd._lib import C
+    rank = ctx.get_rank()
+    rng = np.random.default_rng(90 + rank)
+    n = 3000 + 500 * rank
+    a = rng.integers(-1000, 1000, n)
+    # only rank 1's key column carries a validity tensor (with nulls): every rank must still
+    # take the same sort path (the pipelined sort's eligibility is agreed across ranks)
+    arr = pa.array(a, mask=(rng.random(n) < 0.1)) if rank == 1 else pa.array(a)
+    t = Table(pa.table({"a": arr, "i": np.arange(n) + 100000 * rank}), ctx)
+    C.trace_enable(True)
+    C.trace_reset()
+    s = t.distributed_sort("a")
+    return s.to_pandas(), t.to_pandas(), dict(C.trace_counters())
+
+
+def test_distributed_sort_nulls_on_one_rank_only():
+    """a key column nullable on one rank only must not split the ranks between
+    the pipelined and the splitter sort (different collectives: a hang).  Result: globally sorted,
+    nulls last, every row once, and no rank took the pipelined path."""
+    res = run_distributed(_one_rank_nulls_case, 3)
+    allin = pd.concat([r[1] for r in res]).reset_index(drop=True)
+    got = pd.concat([r[0] for r in res]).reset_index(drop=True)
+    assert len(got) == len(allin)
+    assert sorted(got["i"].tolist()) == sorted(allin["i"].tolist())
+    keys = got["a"].tolist()
+    nn = [k for k in keys if not pd.isna(k)]
+    assert nn == sorted(nn)
+    first_null = next((j for j, k in enumerate(keys) if pd.isna(k)), len(keys))
+    assert all(pd.isna(k) for k in keys[first_null:])
+    for r in res:
+        assert r[2].get("sort.dist.pipelined", 0) == 0
+
+
 @pytest.mark.parametrize("nruns", [1, 2, 3, 8])
 def test_merge_sorted_runs_stable(ctx, nruns):
     """MergeSortedRuns (merge-path rounds) equals a stable sort of the concatenated runs:
