@@ -321,6 +321,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gather", &ops::Gather, rel);
   m.def("gather_nullable", &ops::GatherNullable, rel);
   m.def("select_var", &ops::SelectVar, py::arg("a"), py::arg("b"), py::arg("cond"), rel);
+  m.def("cast_string_to_number", &ops::CastStringToNumber, py::arg("col"), py::arg("target"), rel);
+  m.def("cast_integer_to_string", &ops::CastIntegerToString, py::arg("col"), py::arg("target"), rel);
   m.def("project", &ops::Project, rel);
   m.def("merge", &ops::Merge, rel);
   m.def("slice", &ops::Slice, rel);

@@ -2,6 +2,7 @@
 // order as the device versions; they run the engine on CPU tensors (gloo
 // tests, BASELINE config 1) and serve as the in-tree oracle for the GPU
 // numerics tests.
+#include "strparse.hpp"
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -183,6 +184,34 @@ void gather_columns(const ColView *in, const MutColView *out, int ncols, const i
       if (out[c].valid) out[c].valid[j] = (s < 0) ? 0 : (in[c].valid ? in[c].valid[s] : 1);
     }
   }
+}
+
+// K15 string <-> number casts (twins of strcast.hip; the parsers are shared in strparse.hpp)
+void str_to_i64(const ColView &c, int64_t n, int64_t *out, uint8_t *ok, void *) {
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t v = 0;
+    ok[i] = (!c.valid || c.valid[i]) ? strparse::sc_parse_i64(c.data + c.offsets[i], c.offsets[i + 1] - c.offsets[i], &v)
+                                     : 1;
+    out[i] = v;
+  }
+}
+
+void str_to_f64(const ColView &c, int64_t n, double *out, uint8_t *ok, void *) {
+  for (int64_t i = 0; i < n; ++i) {
+    double v = 0.0;
+    ok[i] = (!c.valid || c.valid[i]) ? strparse::sc_parse_f64(c.data + c.offsets[i], c.offsets[i + 1] - c.offsets[i], &v)
+                                     : 1;
+    out[i] = v;
+  }
+}
+
+void i64_to_str_lengths(const int64_t *v, const uint8_t *valid, int64_t n, int64_t *lens, void *) {
+  for (int64_t i = 0; i < n; ++i) lens[i] = (valid && !valid[i]) ? 0 : strparse::sc_i64_len(v[i]);
+}
+
+void i64_to_str_write(const int64_t *v, const uint8_t *valid, int64_t n, const int64_t *offs, uint8_t *bytes, void *) {
+  for (int64_t i = 0; i < n; ++i)
+    if (!valid || valid[i]) strparse::sc_i64_write(v[i], bytes + offs[i + 1]);
 }
 
 void select_var_lengths(const ColView &a, const ColView &b, int b_bcast, const uint8_t *cond, int64_t n,

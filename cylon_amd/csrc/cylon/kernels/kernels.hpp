@@ -61,8 +61,10 @@ constexpr int kMaxFusedCols = 16;  // columns handled by one multi-column launch
 struct RGAccDesc {
   const uint8_t *src;    // partitioned value column (nullptr: plain row count)
   const uint8_t *valid;  // partitioned validity bytes (nullptr: all valid)
-  int kind;              // 0 SUM_F64, 1 SUM_I64, 2 MIN (order image), 3 MAX (order image), 4 COUNT
+  int kind;              // 0 SUM_F64, 1 SUM_I64, 2 MIN (order image), 3 MAX (order image), 4 COUNT,
+                         // 5 M2 = sum of squared deviations from the group mean (VAR / STDDEV)
   int width, vkind;      // value width / ValueKind
+  int sum_acc, cnt_acc;  // M2: the SUM_F64 and COUNT accumulators of the same column (their mean)
 };
 
 enum AggOp : int {

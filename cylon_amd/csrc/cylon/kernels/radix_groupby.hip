@@ -86,11 +86,12 @@ double distinct_estimate(const int64_t *keys, int64_t n, uint32_t *regs, void *s
 }
 
 // accumulator kinds
-enum RGKind : int { RG_SUMF = 0, RG_SUMI = 1, RG_MIN = 2, RG_MAX = 3, RG_CNT = 4 };
+enum RGKind : int { RG_SUMF = 0, RG_SUMI = 1, RG_MIN = 2, RG_MAX = 3, RG_CNT = 4, RG_M2 = 5 };
 
 struct RGArgs {
   RGAccDesc acc[4];
   int nacc;
+  int has_m2;  // some accumulator is RG_M2: a second pass over the partition's rows
 };
 
 __device__ __forceinline__ uint64_t rg_img(uint64_t bits, int w, int kind) {
@@ -217,6 +218,7 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict
           case RG_SUMI: atomicAdd(t, (unsigned long long)extend_bits(vb[j], c.width, c.vkind)); break;
           case RG_MIN: atomicMin(t, (unsigned long long)rg_img(vb[j], c.width, c.vkind)); break;
           case RG_MAX: atomicMax(t, (unsigned long long)rg_img(vb[j], c.width, c.vkind)); break;
+          case RG_M2: break;  // second pass
           default: atomicAdd(t, 1ull);
         }
       }
@@ -229,6 +231,30 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict
         gcount[p] = 0;
       }
       continue;
+    }
+    if (a.has_m2) {
+      // VAR / STDDEV: squared deviations from the group mean, once every row's sum and count are
+      // in (the two-pass form of the global path, groupby.cpp kM2; the partition's rows are L2 hits)
+      for (int64_t r = rb + threadIdx.x; r < re; r += blockDim.x) {
+        const int64_t k = keys[r];
+        int slot = S;
+        if (k != kRGEmpty) {
+          uint32_t s = (uint32_t)hashing::fmix64((uint64_t)k) & (S - 1);
+          while (tk[s] != k) s = (s + 1) & (S - 1);  // present: inserted by the first pass
+          slot = (int)s;
+        }
+#pragma unroll
+        for (int j = 0; j < A; ++j) {
+          if (j >= a.nacc || a.acc[j].kind != RG_M2) continue;
+          const RGAccDesc &c = a.acc[j];
+          if (c.valid && !c.valid[r]) continue;
+          const double sum = __longlong_as_double((long long)ta[c.sum_acc][slot]);
+          const double cnt = (double)(long long)ta[c.cnt_acc][slot];
+          const double d = rg_double(load_bits(c.src, r, c.width), c.width, c.vkind) - sum / cnt;
+          atomicAdd(reinterpret_cast<double *>(&ta[j][slot]), d * d);
+        }
+      }
+      __syncthreads();
     }
     // compact occupied slots (+ slot S when the INT64_MIN key occurred) into the slab at rb
     constexpr int kPer = (S + kRGThreads - 1) / kRGThreads;
@@ -322,12 +348,22 @@ void radix_groupby_agg(const int64_t *keys, const int64_t *offs, int64_t nparts,
   CYLON_CHECK(nacc >= 1 && nacc <= 4, Code::Invalid, "radix group-by: 1 to 4 accumulators");
   RGArgs a;
   a.nacc = nacc;
+  a.has_m2 = 0;
   for (int j = 0; j < 4; ++j) {
     a.acc[j].src = j < nacc ? acc[j].src : nullptr;
     a.acc[j].valid = j < nacc ? acc[j].valid : nullptr;
     a.acc[j].kind = j < nacc ? acc[j].kind : RG_CNT;
     a.acc[j].width = j < nacc ? acc[j].width : 8;
     a.acc[j].vkind = j < nacc ? acc[j].vkind : 0;
+    a.acc[j].sum_acc = j < nacc ? acc[j].sum_acc : 0;
+    a.acc[j].cnt_acc = j < nacc ? acc[j].cnt_acc : 0;
+    if (j < nacc && acc[j].kind == RG_M2) {
+      CYLON_CHECK(acc[j].src && acc[j].sum_acc >= 0 && acc[j].sum_acc < nacc && acc[j].cnt_acc >= 0 &&
+                      acc[j].cnt_acc < nacc && acc[acc[j].sum_acc].kind == RG_SUMF &&
+                      acc[acc[j].cnt_acc].kind == RG_CNT,
+                  Code::Invalid, "radix group-by: M2 accumulator needs its column's sum and count");
+      a.has_m2 = 1;
+    }
   }
   hipStream_t s = as_stream(stream);
   HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));

@@ -237,25 +237,120 @@ static Column agg_column(const Exec &ex, const TablePtr &t, const GroupInfo &gi,
 }
 
 // ---------------------------------------------------------------------------
-// K8 LDS radix group-by (radix_groupby.hip): large inputs, one integer key,
-// SUM / COUNT / MIN / MAX / MEAN.  Groups come out in partition order (the
-// hash path's first-occurrence order is not kept; the reference's hash
-// group-by order is unspecified as well).  Returns nullptr when not eligible
-// or when a partition overflows its LDS table.
-// ---------------------------------------------------------------------------
+// K8 LDS radix group-by (radix_groupby.hip): large inputs; keys: one integer key, one float key
+// (canonical bits: -0.0 == +0.0, NaNs group together), or several non-null integer keys packed
+// into one exact 63-bit composite; SUM / COUNT / MIN / MAX / MEAN / VAR / STDDEV (M2 from a
+// second in-block pass over the partition's rows).  Groups come out in partition order (the
+// hash path's first-occurrence order is not kept; the reference's hash group-by order is
+// unspecified as well).  Returns nullptr when not eligible or when a partition overflows its
+// LDS table.  Reference: groupby/hash_groupby.cpp:92-201, compute/aggregate_kernels.hpp:92-263.
 static int64_t radix_groupby_min_rows() {
   const char *e = std::getenv("CYLON_RADIX_GROUPBY_MIN_ROWS");  // tuning / test knob
   return e ? std::atoll(e) : (int64_t(1) << 22);
 }
 
-static TablePtr radix_groupby(const TablePtr &t, int key, const std::vector<AggSpec> &aggs) {
+namespace {
+// the group key as one int64 per row, and its inverse for the output key columns
+struct GroupKey {
+  at::Tensor k;                 // int64 [n]
+  std::vector<int> cols;        // key columns
+  std::vector<int64_t> lo;      // composite: per-column minimum
+  std::vector<int> shift, bits; // composite: bit range of each column
+  bool composite = false, fbits = false;
+};
+}  // namespace
+
+static bool gb_int_key(const Column &c) {
+  return simple_key(c) && (c.type.kind() == ValueKind::SIGNED_INT ||
+                           (c.type.kind() == ValueKind::UNSIGNED_INT && c.type.width() < 8));
+}
+
+static bool group_key(const Exec &ex, const TablePtr &t, const std::vector<int> &keys, GroupKey &g) {
+  g.cols = keys;
+  const int64_t n = t->Rows();
+  if (keys.size() == 1) {
+    const Column &kc = t->column(keys[0]);
+    if (!simple_key(kc)) return false;
+    if (kc.type.kind() == ValueKind::SIGNED_INT || kc.type.kind() == ValueKind::UNSIGNED_INT) {
+      if (kc.type.width() == 8) {
+        g.k = kc.data.view(at::kLong);
+      } else {
+        g.k = ex.empty_i64(n);
+        hip::key64_from_column(kc.view(), n, ptr<int64_t>(g.k), ex.stream);
+      }
+      return true;
+    }
+    if (kc.type.kind() == ValueKind::FLOAT && (kc.type.width() == 8 || kc.type.width() == 4)) {
+      at::Tensor x = kc.data.to(at::kDouble);
+      x = at::where(x == 0, at::zeros_like(x), x);                                   // -0.0 -> +0.0
+      x = at::where(at::isnan(x), at::full_like(x, std::numeric_limits<double>::quiet_NaN()), x);
+      g.k = x.view(at::kLong).contiguous();
+      g.fbits = true;
+      return true;
+    }
+    return false;
+  }
+  std::vector<at::Tensor> ks, mm;
+  for (int c : keys) {
+    const Column &kc = t->column(c);
+    if (!gb_int_key(kc)) return false;
+    at::Tensor k = kc.type.width() == 8 ? kc.data.view(at::kLong) : ex.empty_i64(n);
+    if (kc.type.width() != 8) hip::key64_from_column(kc.view(), n, ptr<int64_t>(k), ex.stream);
+    ks.push_back(k);
+    auto m2 = at::aminmax(k);
+    mm.push_back(std::get<0>(m2).reshape({1}));
+    mm.push_back(std::get<1>(m2).reshape({1}));
+  }
+  const std::vector<int64_t> h = to_host_vec(at::cat(mm));
+  int total = 0;
+  g.lo.resize(keys.size());
+  g.bits.resize(keys.size());
+  g.shift.resize(keys.size());
+  for (size_t i = 0; i < keys.size(); ++i) {
+    g.lo[i] = h[2 * i];
+    const uint64_t span = (uint64_t)h[2 * i + 1] - (uint64_t)h[2 * i];
+    int b = 0;
+    while (b < 64 && (span >> b) != 0) ++b;
+    g.bits[i] = b;
+    total += b;
+  }
+  if (total > 63) return false;
+  g.k = at::zeros({n}, ex.opts(at::kLong));
+  for (size_t i = keys.size(), sh = 0; i-- > 0;) {
+    g.shift[i] = (int)sh;
+    g.k.bitwise_or_(at::bitwise_left_shift(ks[i] - g.lo[i], (int64_t)sh));
+    sh += g.bits[i];
+  }
+  g.composite = true;
+  return true;
+}
+
+// output key columns of the groups from their int64 keys
+static std::vector<Column> group_key_columns(const TablePtr &t, const GroupKey &g, const at::Tensor &gk) {
+  std::vector<Column> out;
+  const int64_t ng = gk.numel();
+  if (g.composite) {
+    for (size_t i = 0; i < g.cols.size(); ++i) {
+      const Column &kc = t->column(g.cols[i]);
+      const int64_t mask = g.bits[i] >= 63 ? std::numeric_limits<int64_t>::max() : (int64_t(1) << g.bits[i]) - 1;
+      at::Tensor v = at::bitwise_and(at::bitwise_right_shift(gk, (int64_t)g.shift[i]), mask) + g.lo[i];
+      out.emplace_back(kc.name, kc.type, ng, v.to(kc.data.scalar_type()).contiguous());
+    }
+    return out;
+  }
+  const Column &kc = t->column(g.cols[0]);
+  at::Tensor v = gk;
+  if (g.fbits) v = gk.view(at::kDouble).to(kc.data.scalar_type());
+  else if (kc.type.width() != 8) v = gk.to(kc.data.scalar_type());
+  out.emplace_back(kc.name, kc.type, ng, v.contiguous());
+  return out;
+}
+
+static TablePtr radix_groupby(const TablePtr &t, const std::vector<int> &keys, const std::vector<AggSpec> &aggs) {
   const int64_t n = t->Rows();
   if (!t->device().is_cuda() || n < radix_groupby_min_rows()) return nullptr;
-  const Column &kc = t->column(key);
-  if (!simple_key(kc) || (kc.type.kind() != ValueKind::SIGNED_INT && kc.type.kind() != ValueKind::UNSIGNED_INT))
-    return nullptr;
   struct Plan {
-    int col, kind;  // kind: 0 SUMF 1 SUMI 2 MIN 3 MAX 4 CNT
+    int col, kind;  // kind: 0 SUMF 1 SUMI 2 MIN 3 MAX 4 CNT 5 M2
   };
   std::vector<Plan> plan;
   auto need = [&](int col, int kind) {
@@ -265,7 +360,7 @@ static TablePtr radix_groupby(const TablePtr &t, int key, const std::vector<AggS
     return (int)plan.size() - 1;
   };
   struct Out {
-    int op, col, a, b;  // accumulator indices (b: count for MEAN / nullable MIN,MAX)
+    int op, col, a, b, c, ddof;  // accumulator indices (b: count for MEAN / VAR / nullable MIN,MAX; c: M2)
   };
   std::vector<Out> outs;
   for (const auto &a : aggs) {
@@ -276,40 +371,40 @@ static TablePtr radix_groupby(const TablePtr &t, int key, const std::vector<AggS
       return nullptr;
     const bool fl = c.type.kind() == ValueKind::FLOAT;
     switch (a.op) {
-      case AGG_SUM: outs.push_back({a.op, a.col, need(a.col, fl ? 0 : 1), -1}); break;
-      case AGG_COUNT: outs.push_back({a.op, a.col, need(a.col, 4), -1}); break;
+      case AGG_SUM: outs.push_back({a.op, a.col, need(a.col, fl ? 0 : 1), -1, -1, 0}); break;
+      case AGG_COUNT: outs.push_back({a.op, a.col, need(a.col, 4), -1, -1, 0}); break;
       case AGG_MIN:
       case AGG_MAX:
-        outs.push_back({a.op, a.col, need(a.col, a.op == AGG_MIN ? 2 : 3), c.nullable() ? need(a.col, 4) : -1});
+        outs.push_back({a.op, a.col, need(a.col, a.op == AGG_MIN ? 2 : 3), c.nullable() ? need(a.col, 4) : -1, -1, 0});
         break;
-      case AGG_MEAN: outs.push_back({a.op, a.col, need(a.col, 0), need(a.col, 4)}); break;
+      case AGG_MEAN: outs.push_back({a.op, a.col, need(a.col, 0), need(a.col, 4), -1, 0}); break;
+      case AGG_VAR:
+      case AGG_STDDEV: {
+        const int sa = need(a.col, 0), ca = need(a.col, 4);
+        outs.push_back({a.op, a.col, sa, ca, need(a.col, 5), a.ddof});
+        break;
+      }
       default: return nullptr;
     }
   }
-  // the LDS aggregation kernels are instantiated with exactly nacc accumulator slots (1..4):
-  // k_rg_agg<3, 2048> run with two accumulators (one slot unused) faulted on MI355X at 3M rows /
-  // 1M groups (tools/diag_groupby_xt.py); no aggregation at all takes the global path
+  // the LDS aggregation kernels are instantiated with exactly nacc accumulator slots (1..4)
   if (plan.empty() || plan.size() > 4) return nullptr;
   Exec ex(t->device());
+  GroupKey gkey;
+  if (!group_key(ex, t, keys, gkey)) return nullptr;
   const int nacc = (int)plan.size();
-  at::Tensor keys;
-  if (kc.type.width() == 8) {
-    keys = kc.data.view(at::kLong);
-  } else {
-    keys = ex.empty_i64(n);
-    hip::key64_from_column(kc.view(), n, ptr<int64_t>(keys), ex.stream);
-  }
+  const at::Tensor &kt = gkey.k;
   double est;
   {
     CYLON_PHASE("groupby.radix.estimate", ex.device);
     at::Tensor regs = at::empty({hip::distinct_estimate_workspace()}, ex.opts(at::kInt));
-    est = hip::distinct_estimate(ptr<int64_t>(keys), n, reinterpret_cast<uint32_t *>(ptr<int32_t>(regs)), ex.stream);
+    est = hip::distinct_estimate(ptr<int64_t>(kt), n, reinterpret_cast<uint32_t *>(ptr<int32_t>(regs)), ex.stream);
   }
   const double target = 0.6 * (double)hip::radix_groupby_slots(nacc);  // mean distinct keys per partition
   int bits = 0;
   while (bits < 24 && est * 1.05 / (double)(int64_t(1) << bits) > target) ++bits;
   // partition set: key, each used value column, its validity
-  std::vector<at::Tensor> cols{keys};
+  std::vector<at::Tensor> cols{kt};
   std::vector<int> widths{8};
   std::vector<int> dslot(t->Columns(), -1), vslot(t->Columns(), -1);
   for (const auto &pl : plan) {
@@ -341,6 +436,12 @@ static TablePtr radix_groupby(const TablePtr &t, int key, const std::vector<AggS
     desc[j].kind = plan[j].kind;
     desc[j].width = c.type.width();
     desc[j].vkind = static_cast<int>(c.type.kind());
+    desc[j].sum_acc = desc[j].cnt_acc = 0;
+    if (plan[j].kind == 5)
+      for (int q = 0; q < nacc; ++q) {
+        if (plan[q].col == plan[j].col && plan[q].kind == 0) desc[j].sum_acc = q;
+        if (plan[q].col == plan[j].col && plan[q].kind == 4) desc[j].cnt_acc = q;
+      }
   }
   at::Tensor okeys = ex.empty_i64(n), oacc = ex.empty_i64(std::max(1, nacc) * n), gcount = ex.empty_i64(nparts);
   at::Tensor overflow = at::empty({1}, ex.opts(at::kInt));
@@ -369,12 +470,9 @@ static TablePtr radix_groupby(const TablePtr &t, int key, const std::vector<AggS
                             reinterpret_cast<const uint64_t *>(ptr<int64_t>(oacc)), n, nacc, ptr<int64_t>(gkeys),
                             reinterpret_cast<uint64_t *>(ptr<int64_t>(gacc)), ng, ex.stream);
   trace::add_counter("groupby.radix.groups", ng);
+  if (gkey.composite) trace::add_counter("groupby.radix.composite_key", 1);
   auto plane = [&](int j) { return gacc.slice(0, j * ng, (j + 1) * ng); };
-  std::vector<Column> out;
-  {
-    at::Tensor kd = kc.type.width() == 8 ? gkeys : gkeys.to(kc.data.scalar_type());
-    out.emplace_back(kc.name, kc.type, ng, kd.contiguous());
-  }
+  std::vector<Column> out = group_key_columns(t, gkey, gkeys);
   for (const auto &o : outs) {
     const Column &c = t->column(o.col);
     const std::string name = std::string(AggPrefix(o.op)) + c.name;
@@ -397,6 +495,13 @@ static TablePtr radix_groupby(const TablePtr &t, int key, const std::vector<AggS
         out.push_back(double_col(name, s / cnt.to(at::kDouble), cnt > 0));
         break;
       }
+      case AGG_VAR:
+      case AGG_STDDEV: {
+        at::Tensor m2 = plane(o.c).view(at::kDouble), cnt = plane(o.b).to(at::kDouble);
+        at::Tensor var = m2 / (cnt - o.ddof);
+        out.push_back(double_col(name, o.op == AGG_VAR ? var : var.sqrt(), (cnt - o.ddof) > 0));
+        break;
+      }
     }
   }
   return Table::Make(t->GetContext(), std::move(out));
@@ -405,8 +510,8 @@ static TablePtr radix_groupby(const TablePtr &t, int key, const std::vector<AggS
 static TablePtr groupby_with(const TablePtr &t, const std::vector<int> &keys, const std::vector<AggSpec> &aggs,
                              bool presorted) {
   CYLON_CHECK(!keys.empty(), Code::Invalid, "group-by needs at least one key column");
-  if (!presorted && keys.size() == 1)
-    if (TablePtr r = radix_groupby(t, keys[0], aggs)) return r;
+  if (!presorted)
+    if (TablePtr r = radix_groupby(t, keys, aggs)) return r;
   Exec ex(t->device());
   GroupInfo gi;
   {

@@ -63,6 +63,66 @@ Column SelectVar(const Column &a, const std::optional<Column> &b, const at::Tens
   return Column(a.name, a.type, n, bytes, offs, valid);
 }
 
+std::optional<Column> CastStringToNumber(const Column &c, const DataType &target) {
+  CYLON_CHECK(c.type.type == Type::STRING || c.type.type == Type::BINARY, Code::TypeError,
+              "cast: column " << c.name << " is not a string column");
+  const ValueKind k = target.kind();
+  CYLON_CHECK(!target.is_variable_width() && (k == ValueKind::SIGNED_INT || k == ValueKind::UNSIGNED_INT ||
+                                              k == ValueKind::FLOAT) && target.type != Type::BOOL,
+              Code::TypeError, "cast: string -> " << target.ToString() << " is not a numeric cast");
+  Exec ex(c.device());
+  const int64_t n = c.length;
+  at::Tensor ok = ex.empty_u8(std::max<int64_t>(n, 1));
+  at::Tensor v;
+  const bool fl = k == ValueKind::FLOAT;
+  if (fl) {
+    v = at::empty({n}, ex.opts(at::kDouble));
+    KCALL(ex, str_to_f64, c.view(), n, ptr<double>(v), ptr<uint8_t>(ok));
+  } else {
+    v = ex.empty_i64(n);
+    KCALL(ex, str_to_i64, c.view(), n, ptr<int64_t>(v), ptr<uint8_t>(ok));
+  }
+  if (n) {
+    at::Tensor okn = ok.slice(0, 0, n);
+    const std::vector<int64_t> st = to_host_vec(at::stack({(okn == 0).sum(), (okn == 2).sum()}));
+    CYLON_CHECK(st[0] == 0, Code::Invalid, "cast: " << st[0] << " value(s) of column " << c.name
+                                                     << " do not parse as " << target.ToString());
+    if (st[1] != 0) return std::nullopt;  // host parser (hex integers, long or special floats)
+  }
+  at::Tensor live = c.nullable() ? v.masked_select(c.validity.to(at::kBool)) : v;
+  if (!fl && target.width() < 8 && live.numel()) {  // range check of the narrower integer
+    const std::vector<int64_t> mm = to_host_vec(at::stack({live.min(), live.max()}));
+    const int bits = 8 * target.width();
+    const int64_t lo = k == ValueKind::SIGNED_INT ? -(int64_t(1) << (bits - 1)) : 0;
+    const int64_t hi = k == ValueKind::SIGNED_INT ? (int64_t(1) << (bits - 1)) - 1 : (int64_t(1) << bits) - 1;
+    CYLON_CHECK(mm[0] >= lo && mm[1] <= hi, Code::Invalid,
+                "cast: integer value out of range for " << target.ToString() << " in column " << c.name);
+  }
+  if (!fl && k == ValueKind::UNSIGNED_INT && live.numel())
+    CYLON_CHECK(live.min().item<int64_t>() >= 0, Code::Invalid,
+                "cast: negative value for " << target.ToString() << " in column " << c.name);
+  at::Tensor out = v.to(storage_dtype(target)).contiguous();
+  return Column(c.name, target, n, out, at::Tensor(), c.validity);
+}
+
+Column CastIntegerToString(const Column &c, const DataType &target) {
+  CYLON_CHECK(target.type == Type::STRING, Code::TypeError, "cast: integer -> string only");
+  CYLON_CHECK(!c.is_var() && (c.type.kind() == ValueKind::SIGNED_INT || c.type.kind() == ValueKind::UNSIGNED_INT) &&
+                  c.type.type != Type::BOOL && !(c.type.kind() == ValueKind::UNSIGNED_INT && c.type.width() == 8) &&
+                  c.type.type >= Type::UINT8 && c.type.type <= Type::INT64,
+              Code::TypeError, "cast: " << c.type.ToString() << " -> string is not an integer cast");
+  Exec ex(c.device());
+  const int64_t n = c.length;
+  at::Tensor v = c.data.to(at::kLong).contiguous();
+  const uint8_t *valid = c.nullable() ? ptr<uint8_t>(c.validity) : nullptr;
+  at::Tensor lens = ex.empty_i64(n);
+  KCALL(ex, i64_to_str_lengths, ptr<int64_t>(v), valid, n, ptr<int64_t>(lens));
+  at::Tensor offs = exclusive_scan(ex, lens);
+  at::Tensor bytes = ex.empty_bytes(read_i64(offs, n));
+  KCALL(ex, i64_to_str_write, ptr<int64_t>(v), valid, n, ptr<int64_t>(offs), ptr<uint8_t>(bytes));
+  return Column(c.name, target, n, bytes, offs, c.validity);
+}
+
 // Gather every column of a table with one fused launch per 16 fixed-width
 // columns; var-width columns take the two-pass path.
 static std::vector<Column> gather_columns(const std::vector<Column> &cols, const at::Tensor &idx, bool may_null) {

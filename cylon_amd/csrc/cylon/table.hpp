@@ -85,6 +85,11 @@ TablePtr GatherNullable(const TablePtr &t, const at::Tensor &idx, bool may_null)
 Column GatherColumn(const Column &c, const at::Tensor &idx);
 // K15 string / binary select: row i = cond[i] ? a[i] : b[i] (b of one row: broadcast; no b: null)
 Column SelectVar(const Column &a, const std::optional<Column> &b, const at::Tensor &cond);
+// K15 casts between strings and numbers on the column's device (kernels/strcast.hip): string ->
+// integer / floating column, nullopt when a float needs the host's correctly rounded parser
+// (the caller then casts on the host); integer -> string.  Unparsable strings raise Invalid.
+std::optional<Column> CastStringToNumber(const Column &c, const DataType &target);
+Column CastIntegerToString(const Column &c, const DataType &target);
 TablePtr Project(const TablePtr &t, const std::vector<int> &cols);
 TablePtr Merge(const std::vector<TablePtr> &tables);  // vertical concat
 TablePtr Slice(const TablePtr &t, int64_t offset, int64_t length);

@@ -255,10 +255,20 @@ def _device_cast(c, target: pa.DataType, safe: bool):
     """Numeric -> numeric casts on the column's device (torch), with Arrow's safe-cast checks:
     float -> int must be integral and in range, int -> narrower int must be in range, int -> float
     must lie within the float's exact integer range (2^53 / 2^24).  uint64 sources go to Arrow."""
-    if is_var(c) or c.type.type == T.BOOL:
-        return None
     src = ab.to_arrow_type(c.type)
     num = lambda t: pa.types.is_integer(t) or pa.types.is_floating(t)  # noqa: E731
+    try:
+        # K15 string <-> number casts on the device (kernels/strcast.hip); None: the host parser
+        if is_var(c):
+            if pa.types.is_string(src) and num(target) and target != pa.float16():
+                return C.cast_string_to_number(c, ab.to_cylon_type(target))
+            return None
+        if pa.types.is_string(target) and pa.types.is_integer(src) and src != pa.uint64() and c.type.type != T.BOOL:
+            return C.cast_integer_to_string(c, ab.to_cylon_type(target))
+    except C.CylonError as e:
+        raise pa.ArrowInvalid(str(e)) from None
+    if c.type.type == T.BOOL:
+        return None
     if not (num(src) and num(target)) or target == pa.float16() or src == pa.float16():
         return None
     if src == pa.uint64():  # torch has no full uint64 min/max/compare support: Arrow's host kernels
@@ -291,8 +301,9 @@ def _device_cast(c, target: pa.DataType, safe: bool):
 
 
 def cast(table, dtype, safe: bool = True):
-    """astype: dtype may be a single type or {column: type}.  Numeric -> numeric casts run on the
-    table's device; everything else goes through Arrow's cast kernels on the host."""
+    """astype: dtype may be a single type or {column: type}.  Numeric -> numeric, string -> number
+    and integer -> string casts run on the table's device; everything else (float -> string,
+    dates, hex / special-value strings) goes through Arrow's cast kernels on the host."""
     from ..types import to_arrow
     cols = table.native.columns()
     targets = [dtype.get(c.name) if isinstance(dtype, dict) else dtype for c in cols]

@@ -196,52 +196,6 @@ def test_radix_join_matches_global_table_join(gpu_ctx, monkeypatch, case):
     pd.testing.assert_frame_equal(_sorted_df(got), _sorted_df(ref))
 
 
-@pytest.mark.parametrize("case", ["offset_edges", "sign_span", "wide_low32_collisions", "two_cols"])
-def test_radix_join_narrow_keys(gpu_ctx, monkeypatch, case):
-    """Narrow-key radix join: when both relations' keys span < 2^32 values the key travels as its
-    low 32 bits (partition hash over them, uint32 in the passes and LDS tables) and is rebuilt from
-    the minimum on output.  offset_edges: keys in [-2^40, -2^40 + 2^32) including both ends;
-    sign_span: keys around 0; wide_low32_collisions: keys k and k + 2^32 on the two sides share
-    their low 32 bits but differ -- the range test must refuse the narrow path and no such pair may
-    match; two_cols: key + one payload.  Checked against the global-table join."""
-    from cylon_amd._lib import C
-    rng = np.random.default_rng(17)
-    n = 400_000
-    if case == "offset_edges":
-        base = -(1 << 40)
-        kl = base + rng.integers(0, 1 << 32, n)
-        kr = np.concatenate([kl[: n // 2], base + rng.integers(0, 1 << 32, n - n // 2)])
-        kl[:2] = [base, base + (1 << 32) - 1]
-        kr[2:4] = [base, base + (1 << 32) - 1]
-    elif case == "sign_span":
-        kl = rng.integers(-300_000, 300_000, n)
-        kr = rng.integers(-300_000, 300_000, n)
-    elif case == "wide_low32_collisions":
-        kl = rng.integers(0, 300_000, n)
-        kr = kl + np.where(rng.random(n) < 0.5, 1 << 32, 0)
-    else:
-        kl = rng.integers(0, 300_000, n)
-        kr = rng.integers(0, 300_000, n)
-    a = {"k": kl} if case == "two_cols" else {"k": kl, "v": rng.random(n), "i": rng.integers(-9, 9, n)}
-    a["x"] = rng.random(n)
-    b = {"w": rng.random(n), "k": kr}
-    L, R = Table(pa.table(a), gpu_ctx), Table(pa.table(b), gpu_ctx)
-    on = dict(left_on=["k"], right_on=["k"], left_prefix="l_", right_prefix="r_")
-    monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", "1")
-    monkeypatch.setenv("CYLON_RJ_NARROW", "1")  # opt-in (measured slower: profiles/r03/narrow_keys_ab.txt)
-    C.trace_enable(True)
-    C.trace_reset()
-    got = L.join(R, "inner", "hash", **on)
-    c = dict(C.trace_counters())
-    C.trace_enable(False)
-    assert c.get("join.radix.rows_out", 0) == got.row_count, c  # the radix path ran
-    assert (c.get("join.radix.narrow_keys", 0) == 1) == (case != "wide_low32_collisions"), c
-    monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", str(1 << 62))
-    ref = L.join(R, "inner", "hash", **on)
-    assert got.row_count == ref.row_count > 0
-    pd.testing.assert_frame_equal(_sorted_df(got), _sorted_df(ref))
-
-
 @pytest.mark.parametrize("case", ["int64_many_groups", "int32_nullable", "few_groups", "min_key", "wide_aggs"])
 def test_radix_groupby_matches_global(gpu_ctx, monkeypatch, case):
     """K8 LDS radix group-by (HLL sizing, partitioned LDS aggregation) vs the global-table path."""

@@ -394,3 +394,23 @@ def test_string_select_kernel_matches_cpu(gpu_ctx, ctx, n):
         assert g.equals(h)
     assert res[0][0].equals(pc.if_else(pa.array(cond, pa.bool_()), a, o))
     assert res[0][2].equals(pc.fill_null(a, "F"))
+
+
+def test_string_number_casts_on_device(gpu_ctx):
+    """K15 astype string <-> number on the device (kernels/strcast.hip) against Arrow's host casts."""
+    import pyarrow.compute as pc
+    rng = np.random.default_rng(4)
+    n = 1_000_000
+    ints = rng.integers(-10**12, 10**12, n)
+    mask = rng.random(n) < 0.03
+    s_int = pa.array([str(x) for x in ints], mask=mask)
+    s_flt = pa.array([f"{x / 1000:.3f}" for x in ints], mask=mask)
+    t = Table(pa.table({"i": s_int, "f": s_flt, "x": pa.array(ints, mask=mask)}), gpu_ctx)
+    c = t.native.columns()
+    from cylon_amd.data import compute as cp
+    assert all(cp._device_cast(col, typ, True) is not None
+               for col, typ in zip(c, (pa.int64(), pa.float64(), pa.string())))  # the device path runs
+    out = t.astype({"i": pa.int64(), "f": pa.float64(), "x": pa.string()}).to_arrow()
+    assert out.column("i").to_pylist() == pc.cast(s_int, pa.int64()).to_pylist()
+    assert out.column("f").to_pylist() == pc.cast(s_flt, pa.float64()).to_pylist()
+    assert out.column("x").to_pylist() == pc.cast(pa.array(ints, mask=mask), pa.string()).to_pylist()

@@ -123,3 +123,56 @@ def test_radix_join_hot_key_sample_is_counted_exactly(gpu_ctx, monkeypatch):
     assert got.row_count == exp
     if c.get("join.radix.estimated_rows"):  # the fused estimate was used: it must not be inflated
         assert c["join.radix.estimated_rows"] < 3 * exp, c
+
+
+# ---- LDS radix group-by (kernels/radix_groupby.hip) beyond one integer key + SUM/COUNT/MIN/MAX/MEAN
+def _groupby_both(T, keys, aggs, monkeypatch):
+    res, counters = [], []
+    for thr in ("1", str(1 << 62)):  # radix path, then the global-table path
+        monkeypatch.setenv("CYLON_RADIX_GROUPBY_MIN_ROWS", thr)
+        C.trace_enable(True)
+        C.trace_reset()
+        df = T.local_groupby(keys, aggs).to_pandas()
+        counters.append(dict(C.trace_counters()))
+        C.trace_enable(False)
+        res.append(df.sort_values(keys).reset_index(drop=True))
+    return res, counters
+
+
+@pytest.mark.parametrize("case", ["var_std", "two_keys", "float_key", "two_keys_var"])
+def test_radix_groupby_extended(gpu_ctx, monkeypatch, case):
+    """VAR / STDDEV through the M2 accumulator (second in-block pass over a partition's rows), two
+    integer keys through an exact composite key, a float key through canonical bits -- against
+    the global-table path."""
+    rng = np.random.default_rng(12)
+    n = 600_000
+    t = pa.table({"k": rng.integers(0, 50_000, n), "g": rng.integers(-4, 4, n).astype(np.int16),
+                  "x": pa.array(rng.standard_normal(n) + 100.0, mask=rng.random(n) < 0.05),
+                  "f": np.round(rng.standard_normal(n), 1)})
+    T = Table(t, gpu_ctx)
+    keys, aggs = {"var_std": (["k"], {"x": ["sum", "mean", "std"]}),
+                  "two_keys": (["k", "g"], {"x": ["sum", "max"], "f": ["count"]}),
+                  "float_key": (["f"], {"x": ["sum", "min"], "k": ["max"]}),
+                  "two_keys_var": (["k", "g"], {"x": ["var", "mean"]})}[case]
+    res, cnt = _groupby_both(T, keys, aggs, monkeypatch)
+    assert cnt[0].get("groupby.radix.groups", 0) == len(res[0]), cnt[0]
+    if len(keys) > 1:
+        assert cnt[0].get("groupby.radix.composite_key", 0) == 1, cnt[0]
+    pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-8, atol=1e-8)
+
+
+@pytest.mark.parametrize("nacc,wide", [(2, False), (2, True), (3, False)])
+def test_radix_groupby_3m_rows_1m_groups(gpu_ctx, monkeypatch, nacc, wide):
+    """The round-3 fault shape: 3M rows / ~1M groups with two accumulators run in the three-slot
+    <3, 2048> LDS table (CYLON_RG_WIDE=1), next to the exact two-slot table and three accumulators
+    (which use <3, 2048> anyway)."""
+    rng = np.random.default_rng(23)
+    n = 3_000_000
+    t = pa.table({"k": rng.integers(0, n // 3, n), "v": rng.random(n), "i": rng.integers(-50, 50, n)})
+    T = Table(t, gpu_ctx)
+    aggs = {2: {"v": ["sum"], "i": ["max"]}, 3: {"v": ["sum", "max"], "i": ["max"]}}[nacc]
+    if wide:
+        monkeypatch.setenv("CYLON_RG_WIDE", "1")
+    res, cnt = _groupby_both(T, ["k"], aggs, monkeypatch)
+    assert cnt[0].get("groupby.radix.groups", 0) == len(res[0]) > 900_000, cnt[0]
+    pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-9, atol=1e-9)

@@ -100,3 +100,62 @@ def test_memory_pool_accounting(ctx):
     assert p.bytes_allocated() == 0 and p.max_memory() == 32000
     ctx.set_memory_pool(p)
     assert ctx.memory_stats()["pool_max_memory"] == 32000
+
+
+# ---- K15 string <-> number casts (kernels/strcast.hip; CPU twin here, GPU in test_gpu_ops.py)
+def _cast_cases():
+    import pyarrow as pa
+    return [
+        (["1", "-25", None, "007", "-0", "9223372036854775807", "-9223372036854775808"], pa.int64()),
+        (["12", None, "-128", "127"], pa.int8()),
+        (["1.5", ".5", "5.", "+1e3", "1E-3", None, "-0", "123456789.125", "0.1", "1e22", "3.14159"], pa.float64()),
+        (["0.1", "2.5e-3", "7"], pa.float32()),
+        (["inf", "1.5", "nan", "1e400", "0.12345678901234567890123"], pa.float64()),  # host parser
+        (["0x10", "5"], pa.int64()),  # hex: host parser
+    ]
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_string_to_number_cast_matches_arrow(ctx, case):
+    import math
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    from cylon_amd import Table
+    vals, typ = _cast_cases()[case]
+    arr = pa.array(vals, pa.string())
+    got = Table(pa.table({"s": arr}), ctx).astype({"s": typ}).to_arrow().column(0).to_pylist()
+    exp = pc.cast(arr, typ).to_pylist()
+    assert len(got) == len(exp)
+    for g, e in zip(got, exp):
+        if e is None or g is None:
+            assert g is None and e is None
+        elif isinstance(e, float) and math.isnan(e):
+            assert math.isnan(g)
+        else:
+            assert g == e and (not isinstance(e, float) or math.copysign(1, g) == math.copysign(1, e)), (g, e)
+
+
+@pytest.mark.parametrize("bad,typ", [("+5", "int64"), ("1_000", "int64"), ("", "int64"), (" 1", "int64"),
+                                     ("300", "int8"), ("-1", "uint8"), (".", "float64"), ("1e", "float64"),
+                                     ("e5", "float64"), ("1.5x", "float64")])
+def test_string_to_number_cast_rejects_like_arrow(ctx, bad, typ):
+    import pyarrow as pa
+    from cylon_amd import Table
+    with pytest.raises(pa.ArrowInvalid):
+        pa.compute.cast(pa.array([bad]), getattr(pa, typ)())
+    with pytest.raises(pa.ArrowInvalid):
+        Table(pa.table({"s": pa.array(["1", bad])}), ctx).astype({"s": getattr(pa, typ)()})
+
+
+@pytest.mark.parametrize("typ", ["int64", "int32", "int8", "uint16", "uint32"])
+def test_integer_to_string_cast_matches_arrow(ctx, typ):
+    import numpy as np
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    from cylon_amd import Table
+    info = np.iinfo(typ)
+    rng = np.random.default_rng(1)
+    v = list(rng.integers(info.min, info.max, 200, dtype=typ, endpoint=True)) + [info.min, info.max, 0]
+    arr = pa.array(v, getattr(pa, typ)(), mask=np.arange(len(v)) % 17 == 3)
+    got = Table(pa.table({"x": arr}), ctx).astype({"x": pa.string()}).to_arrow().column(0)
+    assert got.to_pylist() == pc.cast(arr, pa.string()).to_pylist()
