@@ -163,8 +163,7 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict
     for (int s = threadIdx.x; s <= S; s += blockDim.x) {
       tk[s] = kRGEmpty;
 #pragma unroll
-      for (int j = 0; j < A; ++j)
-        if (j < a.nacc) ta[j][s] = rg_init(a.acc[j].kind);
+      for (int j = 0; j < A; ++j) ta[j][s] = rg_init(a.acc[j].kind);
     }
     if (threadIdx.x == 0) bad = 0;
     __syncthreads();
@@ -176,8 +175,7 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict
       const int64_t k = keys[r];
       uint64_t vb[A];
 #pragma unroll
-      for (int j = 0; j < A; ++j)
-        if (j < a.nacc && a.acc[j].src) vb[j] = load_bits(a.acc[j].src, r, a.acc[j].width);
+      for (int j = 0; j < A; ++j) vb[j] = load_bits(a.acc[j].src, r, a.acc[j].width);
       int slot = S;
       if (k != kRGEmpty) {
         uint32_t s = (uint32_t)hashing::fmix64((uint64_t)k) & (S - 1);
@@ -209,7 +207,6 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict
       }
 #pragma unroll
       for (int j = 0; j < A; ++j) {
-        if (j >= a.nacc) continue;
         const RGAccDesc &c = a.acc[j];
         if (c.valid && !c.valid[r]) continue;
         unsigned long long *t = &ta[j][slot];
@@ -245,7 +242,7 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict
         }
 #pragma unroll
         for (int j = 0; j < A; ++j) {
-          if (j >= a.nacc || a.acc[j].kind != RG_M2) continue;
+          if (a.acc[j].kind != RG_M2) continue;
           const RGAccDesc &c = a.acc[j];
           if (c.valid && !c.valid[r]) continue;
           const double sum = __longlong_as_double((long long)ta[c.sum_acc][slot]);
@@ -293,14 +290,13 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict
       }
       okeys[o] = tk[s];
 #pragma unroll
-      for (int j = 0; j < A; ++j)
-        if (j < a.nacc) {
-          if (DBG && (int64_t)j * n + o >= (int64_t)a.nacc * n) {
-            rg_dbg(dbg, 4, p, o, rb, re, j, s);
-            continue;
-          }
-          oacc[(int64_t)j * n + o] = ta[j][s];
+      for (int j = 0; j < A; ++j) {
+        if (DBG && (int64_t)j * n + o >= (int64_t)A * n) {
+          rg_dbg(dbg, 4, p, o, rb, re, j, s);
+          continue;
         }
+        oacc[(int64_t)j * n + o] = ta[j][s];
+      }
     }
     if (threadIdx.x == 0) {
       const bool has_min = (bad & 2) != 0;
@@ -308,8 +304,7 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict
       if (has_min && rb + tot < re) {
         const int64_t o = rb + tot;
         okeys[o] = kRGEmpty;
-        for (int j = 0; j < A; ++j)
-          if (j < a.nacc) oacc[(int64_t)j * n + o] = ta[j][S];
+        for (int j = 0; j < A; ++j) oacc[(int64_t)j * n + o] = ta[j][S];
       }
       gcount[p] = tot + (has_min ? 1 : 0);
     }
@@ -343,21 +338,37 @@ static void rg_launch(int grid, hipStream_t s, const int64_t *keys, const int64_
                        oacc, n, gcount, overflow, nullptr);
 }
 
+// Accumulator planes (oacc holds planes * n words): nacc, or 3 for two accumulators under the
+// CYLON_RG_WIDE=1 diagnostic (a dummy count fills the third slot of the <3, 2048> table).
+int radix_groupby_planes(int nacc) {
+  const char *we = std::getenv("CYLON_RG_WIDE");
+  return (we && we[0] == '1' && nacc == 2) ? 3 : nacc;
+}
+
+// Every accumulator slot of a table instance is live: A == planes, and a padded slot is a real
+// count (src = the keys) writing its own plane.  Round 3 ran two accumulators in the <3, 2048>
+// table and guarded the idle slot with `j < nacc`; hipcc (ROCm 7.2, gfx950) materialised that
+// uniform guard as a lane mask inside the table-init loop, whose last trip (slot S of S + 1)
+// runs with one lane active, and reused the mask for the compaction stores under another EXEC:
+// the idle slot's store to oacc[2n + o] then executed past the 2n-word allocation
+// (profiles/r04/rg_agg_fault_isa.txt).  Without runtime slot guards nothing can mis-evaluate.
 void radix_groupby_agg(const int64_t *keys, const int64_t *offs, int64_t nparts, const RGAccDesc *acc, int nacc,
                        int64_t *okeys, uint64_t *oacc, int64_t n, int64_t *gcount, int *overflow, void *stream) {
   CYLON_CHECK(nacc >= 1 && nacc <= 4, Code::Invalid, "radix group-by: 1 to 4 accumulators");
+  const int A = radix_groupby_planes(nacc);
   RGArgs a;
-  a.nacc = nacc;
+  a.nacc = A;
   a.has_m2 = 0;
   for (int j = 0; j < 4; ++j) {
-    a.acc[j].src = j < nacc ? acc[j].src : nullptr;
-    a.acc[j].valid = j < nacc ? acc[j].valid : nullptr;
-    a.acc[j].kind = j < nacc ? acc[j].kind : RG_CNT;
-    a.acc[j].width = j < nacc ? acc[j].width : 8;
-    a.acc[j].vkind = j < nacc ? acc[j].vkind : 0;
-    a.acc[j].sum_acc = j < nacc ? acc[j].sum_acc : 0;
-    a.acc[j].cnt_acc = j < nacc ? acc[j].cnt_acc : 0;
-    if (j < nacc && acc[j].kind == RG_M2) {
+    const bool real = j < nacc;
+    a.acc[j].src = real && acc[j].src ? acc[j].src : reinterpret_cast<const uint8_t *>(keys);
+    a.acc[j].valid = real ? acc[j].valid : nullptr;
+    a.acc[j].kind = real ? acc[j].kind : RG_CNT;
+    a.acc[j].width = real && acc[j].src ? acc[j].width : 8;
+    a.acc[j].vkind = real ? acc[j].vkind : 0;
+    a.acc[j].sum_acc = real ? acc[j].sum_acc : 0;
+    a.acc[j].cnt_acc = real ? acc[j].cnt_acc : 0;
+    if (real && acc[j].kind == RG_M2) {
       CYLON_CHECK(acc[j].src && acc[j].sum_acc >= 0 && acc[j].sum_acc < nacc && acc[j].cnt_acc >= 0 &&
                       acc[j].cnt_acc < nacc && acc[acc[j].sum_acc].kind == RG_SUMF &&
                       acc[acc[j].cnt_acc].kind == RG_CNT,
@@ -368,29 +379,27 @@ void radix_groupby_agg(const int64_t *keys, const int64_t *offs, int64_t nparts,
   hipStream_t s = as_stream(stream);
   HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
   const int grid = (int)std::min<int64_t>(nparts, kNumCUs * 4);
-  // diagnostics (tools/diag_groupby_xt.py, tests): CYLON_RG_WIDE=1 runs two accumulators in the
-  // three-slot <3, 2048> table (the shape that faulted in round 3), CYLON_RG_DEBUG=1 the
-  // bounds-checked instantiation that records instead of faulting
-  const char *we = std::getenv("CYLON_RG_WIDE");
+  // CYLON_RG_DEBUG=1: the bounds-checked instantiation that records instead of faulting
   const char *de = std::getenv("CYLON_RG_DEBUG");
-  const bool wide = we && we[0] == '1' && nacc == 2;
   long long *dbg = nullptr;
   if (de && de[0] == '1') {
     HIP_CHECK(hipMallocAsync(reinterpret_cast<void **>(&dbg), 8 * sizeof(long long), s));
     HIP_CHECK(hipMemsetAsync(dbg, 0, 8 * sizeof(long long), s));
   }
-  if (nacc <= 1) rg_launch<1, 4096>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow, dbg);
-  else if (nacc == 2 && !wide) rg_launch<2, 2048>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow, dbg);
-  else if (nacc <= 3) rg_launch<3, 2048>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow, dbg);
-  else rg_launch<4, 1024>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow, dbg);
+  switch (A) {
+    case 1: rg_launch<1, 4096>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow, dbg); break;
+    case 2: rg_launch<2, 2048>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow, dbg); break;
+    case 3: rg_launch<3, 2048>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow, dbg); break;
+    default: rg_launch<4, 1024>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow, dbg);
+  }
   HIP_LAUNCH_CHECK();
   if (dbg) {
     long long h[8];
     HIP_CHECK(hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     HIP_CHECK(hipFreeAsync(dbg, s));
-    std::fprintf(stderr, "rg_debug nacc=%d wide=%d nparts=%lld n=%lld violations=%lld site=%lld p=%lld idx=%lld "
-                 "rb=%lld re=%lld j=%lld slot=%lld\n", nacc, (int)wide, (long long)nparts, (long long)n, h[0], h[1],
+    std::fprintf(stderr, "rg_debug nacc=%d planes=%d nparts=%lld n=%lld violations=%lld site=%lld p=%lld idx=%lld "
+                 "rb=%lld re=%lld j=%lld slot=%lld\n", nacc, A, (long long)nparts, (long long)n, h[0], h[1],
                  h[2], h[3], h[4], h[5], h[6], h[7]);
     CYLON_CHECK(h[0] == 0, Code::ExecutionError, "radix group-by debug: " << h[0] << " out-of-range accesses (site "
                                                                            << h[1] << ")");

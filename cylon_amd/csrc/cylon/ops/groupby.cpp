@@ -443,7 +443,8 @@ static TablePtr radix_groupby(const TablePtr &t, const std::vector<int> &keys, c
         if (plan[q].col == plan[j].col && plan[q].kind == 4) desc[j].cnt_acc = q;
       }
   }
-  at::Tensor okeys = ex.empty_i64(n), oacc = ex.empty_i64(std::max(1, nacc) * n), gcount = ex.empty_i64(nparts);
+  at::Tensor okeys = ex.empty_i64(n), oacc = ex.empty_i64(hip::radix_groupby_planes(nacc) * n),
+             gcount = ex.empty_i64(nparts);
   at::Tensor overflow = at::empty({1}, ex.opts(at::kInt));
   {
     CYLON_PHASE("groupby.radix.aggregate", ex.device);

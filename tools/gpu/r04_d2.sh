@@ -3,7 +3,7 @@
 # rehearsal (bench --verify, distributed group-by and sort), then the k_rg_agg diagnosis.
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/r04d
+O=gpurun_out/r04e
 mkdir -p $O
 export TMPDIR=/tmp
 CYLON_SHUFFLE_CHUNKS=4 CYLON_SHUFFLE_SELF_RCCL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_selfrccl -o selfrccl -- python3 bench.py --force-shuffle --steps 1 --warmup 1 --no-phases > $O/prof_selfrccl.log 2>&1
