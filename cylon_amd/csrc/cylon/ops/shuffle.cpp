@@ -983,12 +983,17 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
       nfast += fastpath ? 1 : 0;
       wire[i].assign(ts[i]->Columns(), at::Tensor());
       for (int c = 0; c < ts[i]->Columns(); ++c)
-        if (plans[i].narrow[c]) {
+        if (plans[i].narrow[c]) {  // narrowed copies of the rows that are sent (not the own rows)
           const Column &col = lay[i]->column(c);
           Exec ex(dev);
           wire[i][c] = at::empty({col.length}, ex.opts(at::kInt));
-          KCALL(ex, narrow_i64, ptr<int64_t>(col.data), col.length, plans[i].base[c],
-                reinterpret_cast<uint32_t *>(ptr<int32_t>(wire[i][c])));
+          for (int k = 0; k < K; ++k)
+            for (int r = 0; r < W; ++r)
+              if (const int64_t cnt_kr = gp[i].send_cnt[k][r]) {
+                const int64_t o = gp[i].send_off[k][r];
+                KCALL(ex, narrow_i64, ptr<int64_t>(col.data) + o, cnt_kr, plans[i].base[c],
+                      reinterpret_cast<uint32_t *>(ptr<int32_t>(wire[i][c])) + o);
+              }
         }
       post(i, 0);
     }

@@ -247,3 +247,58 @@ def test_dis_join_op_streaming_rounds():
         c = r[3]
         # left: 5 rounds (rank 0's batches), right: 3 rounds -- identical on both ranks
         assert c.get("graph.alltoall.rounds") == 8, c
+
+
+def _eight_rank_ops(ctx):
+    """One rank of the 8-rank rehearsal: chunked planned joins (inner, left) with the gapped
+    exchange layout, a two-key join, a distributed group-by and a distributed sort."""
+    import numpy as np
+    import pandas as pd
+    from cylon_amd import Table
+    from cylon_amd._lib import C
+    rank = ctx.get_rank()
+    rng = np.random.default_rng(800 + rank)
+    n = 3000 + 250 * rank
+    a = pd.DataFrame({"k": rng.integers(0, 9000, n), "g": rng.integers(0, 3, n), "v": rng.random(n)})
+    b = pd.DataFrame({"k": rng.integers(0, 9000, n), "g": rng.integers(0, 3, n), "w": rng.random(n)})
+    ctx.add_config("shuffle_chunks", "3")
+    ta, tb = Table.from_pandas(ctx, a), Table.from_pandas(ctx, b)
+    C.trace_enable(True)
+    C.trace_reset()
+    out = {"inner": ta.distributed_join(tb, "inner", "hash", on=["k"], left_prefix="l_", right_prefix="r_"),
+           "left": ta.distributed_join(tb, "left", "hash", on=["k"], left_prefix="l_", right_prefix="r_"),
+           "two": ta.distributed_join(tb, "inner", "hash", on=["k", "g"], left_prefix="l_", right_prefix="r_")}
+    counters = dict(C.trace_counters())
+    out["gb"] = ta.groupby("k", {"v": ["sum", "count"]})
+    out["sort"] = ta.distributed_sort("k")
+    return {k: v.to_pandas() for k, v in out.items()}, a, b, counters
+
+
+def test_eight_rank_distributed_rehearsal():
+    """8 ranks over gloo (the driver's 8-GPU shape on CPUs): every rank's results together equal
+    pandas on the concatenated inputs; the own partition of each chunk stays in place."""
+    import pandas as pd
+    from dist_utils import run_distributed
+    res = run_distributed(_eight_rank_ops, 8)
+    A = pd.concat([r[1] for r in res]).reset_index(drop=True)
+    B = pd.concat([r[2] for r in res]).reset_index(drop=True)
+
+    def canon(df):
+        df = df[sorted(df.columns)]
+        return df.sort_values(list(df.columns), kind="mergesort", na_position="last").reset_index(drop=True)
+
+    la, rb = A.add_prefix("l_"), B.add_prefix("r_")
+    exp_inner = la.merge(rb, left_on="l_k", right_on="r_k")
+    exp_left = la.merge(rb, left_on="l_k", right_on="r_k", how="left")
+    exp_two = la.merge(rb, left_on=["l_k", "l_g"], right_on=["r_k", "r_g"])
+    for name, exp in (("inner", exp_inner), ("left", exp_left), ("two", exp_two)):
+        got = pd.concat([r[0][name] for r in res])
+        pd.testing.assert_frame_equal(canon(got), canon(exp), check_dtype=False, obj=name)
+    gb = pd.concat([r[0]["gb"] for r in res]).sort_values("k").reset_index(drop=True)
+    eg = A.groupby("k")["v"].agg(["sum", "count"]).reset_index()
+    assert gb["k"].tolist() == eg["k"].tolist() and gb["count_v"].tolist() == eg["count"].tolist()
+    srt = pd.concat([r[0]["sort"] for r in res])["k"].tolist()
+    assert srt == sorted(A["k"].tolist())
+    for r in res:
+        assert r[3].get("shuffle.self_rows_kept_local", 0) > 0, r[3]
+        assert r[3].get("shuffle.plan_collectives", 0) == 3, r[3]

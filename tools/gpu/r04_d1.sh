@@ -12,5 +12,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 > $O/bench_1.json 2> $O/bench_1.err
 timeout -k 10 300 python bench.py --force-shuffle --steps 10 --warmup 3 > $O/bench_forced_k1.json 2> $O/bench_forced_k1.err
 CYLON_SHUFFLE_CHUNKS=4 timeout -k 10 300 python bench.py --force-shuffle --steps 10 --warmup 3 --verify > $O/bench_forced_k4.json 2> $O/bench_forced_k4.err
-CYLON_SHUFFLE_CHUNKS=4 CYLON_SHUFFLE_SELF_RCCL=1 timeout -k 10 300 python bench.py --force-shuffle --steps 10 --warmup 3 > $O/bench_forced_k4_selfrccl.json 2> $O/bench_forced_k4_selfrccl.err
+CYLON_SHUFFLE_CHUNKS=4 CYLON_SHUFFLE_SELF_RCCL=1 timeout -k 10 300 python bench.py --force-shuffle --rows 500000000 --steps 10 --warmup 3 > $O/bench_forced_k4_selfrccl_500m.json 2> $O/bench_forced_k4_selfrccl.err
 echo done

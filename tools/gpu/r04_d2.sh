@@ -6,7 +6,10 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/r04e
 mkdir -p $O
 export TMPDIR=/tmp
-CYLON_SHUFFLE_CHUNKS=4 CYLON_SHUFFLE_SELF_RCCL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_selfrccl -o selfrccl -- python3 bench.py --force-shuffle --steps 1 --warmup 1 --no-phases > $O/prof_selfrccl.log 2>&1
+CYLON_SHUFFLE_CHUNKS=4 CYLON_SHUFFLE_SELF_RCCL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_selfrccl -o selfrccl -- python3 bench.py --force-shuffle --rows 500000000 --steps 1 --warmup 1 --no-phases > $O/prof_selfrccl.log 2>&1
+CYLON_SHUFFLE_CHUNKS=4 CYLON_SHUFFLE_SELF_RCCL=1 timeout -k 10 300 python bench.py --force-shuffle --rows 500000000 --steps 10 --warmup 3 > $O/bench_forced_k4_selfrccl_500m.json 2> $O/bench_forced_k4_selfrccl.err
+CYLON_SHUFFLE_CHUNKS=4 timeout -k 10 300 python bench.py --force-shuffle --steps 10 --warmup 3 > $O/bench_forced_k4.json 2> $O/bench_forced_k4.err
+CYLON_SHUFFLE_CHUNKS=4 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_k4 -o k4 -- python3 bench.py --force-shuffle --steps 1 --warmup 1 --no-phases > $O/prof_k4.log 2>&1
 timeout -k 10 300 python tools/join_types_probe.py 100000000 3 inner,left,right,outer,inner2 > $O/jt_100m.jsonl 2> $O/jt_100m.err
 timeout -k 10 500 python tools/join_types_probe.py 1000000000 2 inner,left,outer,inner2 > $O/jt_1b.jsonl 2> $O/jt_1b.err
 CYLON_BENCH_BACKEND=gloo-gpu timeout -k 10 400 python bench.py --gpus 8 --rows 40000000 --steps 2 --warmup 1 --verify > $O/bench_multirank_8.json 2> $O/bench_multirank_8.err
