@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--key-ratio", type=float, default=0.99)
     p.add_argument("--no-phases", action="store_true", help="skip the traced per-phase step after the timed region")
     p.add_argument("--verify", action="store_true", help="check the last output against torch (outside the timing)")
+    p.add_argument("--sync-steps", action="store_true",
+                   help="diagnostic: synchronise the device after every timed step (host never runs ahead)")
     p.add_argument("--force-shuffle", action="store_true",
                    help="with --gpus 1: run a world-1 RCCL context through the full shuffle + exchange path "
                         "(config force_shuffle=1) instead of the local join")
@@ -191,14 +193,24 @@ def main():
         out = None
     ctx.barrier()
     sync()
+    alloc0 = torch.cuda.memory_stats() if torch.cuda.is_available() else {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = None  # the previous output is released before the next join allocates
         out = step()
+        if args.sync_steps:
+            sync()
     sync()
     ctx.barrier()
     elapsed = time.perf_counter() - t0
     out_rows = out.row_count if out is not None else 0
+    # caching-allocator activity inside the timed region: a retry frees every cached block
+    # (device synchronise + hipFree) and mallocs again -- the cost of running at the memory limit
+    alloc1 = torch.cuda.memory_stats() if torch.cuda.is_available() else {}
+    allocator = {"alloc_retries": int(alloc1.get("num_alloc_retries", 0) - alloc0.get("num_alloc_retries", 0)),
+                 "device_mallocs": int(alloc1.get("num_device_alloc", 0) - alloc0.get("num_device_alloc", 0)),
+                 "device_frees": int(alloc1.get("num_device_free", 0) - alloc0.get("num_device_free", 0)),
+                 "peak_reserved_gb": round(alloc1.get("reserved_bytes.all.peak", 0) / 2**30, 1)}
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
@@ -263,6 +275,9 @@ def main():
             rec["phases_ms_max_over_ranks"] = phases
         if verify is not None:
             rec["verify"] = verify
+        rec["allocator_timed_region"] = allocator
+        if args.sync_steps:
+            rec["sync_steps"] = True
         if args.force_shuffle:
             rec["force_shuffle"] = True
         if counters:

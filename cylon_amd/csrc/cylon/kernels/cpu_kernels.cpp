@@ -271,6 +271,28 @@ void key64_from_column(const ColView &col, int64_t n, int64_t *out, void *) {
   for (int64_t i = 0; i < n; ++i) out[i] = extend_bits(load_bits(col.data, i, col.width), col.width, col.kind);
 }
 
+void composite_key_pack(const ColView *cols, int nk, const int64_t *lo, const int *shift, int64_t n, int64_t *out,
+                        void *) {
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t acc = 0;
+    for (int k = 0; k < nk; ++k)
+      acc |= (uint64_t)(extend_bits(load_bits(cols[k].data, i, cols[k].width), cols[k].width, cols[k].kind) - lo[k])
+             << shift[k];
+    out[i] = (int64_t)acc;
+  }
+}
+
+void composite_key_unpack(const int64_t *key, int64_t n, int nk, const int64_t *lo, const int *shift, const int *bits,
+                          const MutColView *out, void *) {
+  for (int k = 0; k < nk; ++k) {
+    const uint64_t mask = bits[k] >= 64 ? ~0ull : ((1ull << bits[k]) - 1);
+    for (int64_t i = 0; i < n; ++i) {
+      const uint64_t x = (uint64_t)lo[k] + (((uint64_t)key[i] >> shift[k]) & mask);
+      std::memcpy(out[k].data + i * out[k].width, &x, out[k].width);  // little endian: the low bytes
+    }
+  }
+}
+
 void hash_table_init(HashSlot *table, int64_t tsize, void *) {
   for (int64_t i = 0; i < tsize; ++i) {
     table[i].key = 0;

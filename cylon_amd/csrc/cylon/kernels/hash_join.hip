@@ -291,6 +291,87 @@ void key64_from_column(const ColView &col, int64_t n, int64_t *out, void *stream
   HIP_LAUNCH_CHECK();
 }
 
+// K5 exact composite key of several integer key columns (ops/join.cpp radix_keys): one pass reads
+// every key column at its own width and writes the packed int64 -- the LDS radix join then moves
+// ONE 8-byte key instead of the image plus each key column; unpack rebuilds the key columns of the
+// join output from the composite the kernel wrote (one read, one write per key column).
+struct CompositeSpec {
+  ColView c[kMaxCompositeKeys];
+  MutColView o[kMaxCompositeKeys];
+  int64_t lo[kMaxCompositeKeys];
+  uint64_t mask[kMaxCompositeKeys];
+  int shift[kMaxCompositeKeys];
+};
+
+template <int NK>
+__global__ void k_composite_pack(CompositeSpec s, int64_t n, int64_t *__restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+      acc |= (uint64_t)(extend_bits(load_bits(s.c[k].data, i, s.c[k].width), s.c[k].width, s.c[k].kind) - s.lo[k])
+             << s.shift[k];
+    out[i] = (int64_t)acc;
+  }
+}
+
+template <int NK>
+__global__ void k_composite_unpack(CompositeSpec s, int64_t n, const int64_t *__restrict__ key) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t v = (uint64_t)key[i];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const uint64_t x = (uint64_t)s.lo[k] + ((v >> s.shift[k]) & s.mask[k]);
+      switch (s.o[k].width) {
+        case 1: s.o[k].data[i] = (uint8_t)x; break;
+        case 2: reinterpret_cast<uint16_t *>(s.o[k].data)[i] = (uint16_t)x; break;
+        case 4: reinterpret_cast<uint32_t *>(s.o[k].data)[i] = (uint32_t)x; break;
+        default: reinterpret_cast<uint64_t *>(s.o[k].data)[i] = x; break;
+      }
+    }
+  }
+}
+
+static CompositeSpec composite_spec(int nk, const int64_t *lo, const int *shift, const int *bits) {
+  CYLON_CHECK(nk >= 1 && nk <= kMaxCompositeKeys, Code::Invalid, "composite key of " << nk << " columns");
+  CompositeSpec s;
+  for (int k = 0; k < nk; ++k) {
+    s.lo[k] = lo[k];
+    s.shift[k] = shift[k];
+    s.mask[k] = bits ? (bits[k] >= 64 ? ~0ull : ((1ull << bits[k]) - 1)) : 0;
+  }
+  return s;
+}
+
+#define CYLON_NK_SWITCH(nk, KERNEL, ...)                                                                     \
+  switch (nk) {                                                                                              \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                                               \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;                                               \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break;                                               \
+    default: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                                              \
+  }
+
+void composite_key_pack(const ColView *cols, int nk, const int64_t *lo, const int *shift, int64_t n, int64_t *out,
+                        void *stream) {
+  if (n == 0) return;
+  CompositeSpec s = composite_spec(nk, lo, shift, nullptr);
+  for (int k = 0; k < nk; ++k) s.c[k] = cols[k];
+  CYLON_NK_SWITCH(nk, k_composite_pack, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), s, n, out);
+  HIP_LAUNCH_CHECK();
+}
+
+void composite_key_unpack(const int64_t *key, int64_t n, int nk, const int64_t *lo, const int *shift, const int *bits,
+                          const MutColView *out, void *stream) {
+  if (n == 0) return;
+  CompositeSpec s = composite_spec(nk, lo, shift, bits);
+  for (int k = 0; k < nk; ++k) s.o[k] = out[k];
+  CYLON_NK_SWITCH(nk, k_composite_unpack, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), s, n, key);
+  HIP_LAUNCH_CHECK();
+}
+#undef CYLON_NK_SWITCH
+
 __device__ __forceinline__ bool value_equal(const ColView &a, int64_t i, const ColView &b, int64_t j) {
   const bool va = a.valid == nullptr || a.valid[i] != 0;
   const bool vb = b.valid == nullptr || b.valid[j] != 0;

@@ -54,6 +54,7 @@ struct HashTableRef {
 };
 
 constexpr int kMaxFusedCols = 16;  // columns handled by one multi-column launch
+constexpr int kMaxCompositeKeys = 4;  // key columns of one composite join / group-by key
 
 // Aggregation op ids, numerically identical to the reference
 // (cpp/src/cylon/compute/aggregate_kernels.hpp:40-50).

@@ -16,6 +16,7 @@
 //   3. outer completion: matched flags (mark_indices) + compaction of the
 //      unmatched rows of the preserved side(s), appended with -1 partners.
 //   4. materialisation: one fused gather launch per side (K4).
+#include <algorithm>
 #include <cstdlib>
 #include <limits>
 
@@ -336,12 +337,17 @@ static bool left_may_null(JoinType jt) { return jt == JoinType::RIGHT || jt == J
 static bool right_may_null(JoinType jt) { return jt == JoinType::LEFT || jt == JoinType::FULL_OUTER; }
 
 // validity of the output columns of a side that can be null: the side's presence bytes, AND the
-// column's own validity where the input column was nullable
+// column's own validity where the input column was nullable.  Without a sink the columns of a
+// non-nullable input share the presence bytes as their validity (no per-column copy: a 1B-row
+// FULL OUTER join would otherwise hold 8 more bytes per output row); a sink's columns own theirs.
 static void apply_presence(std::vector<Column> &cols, const TablePtr &in, const at::Tensor &pres, int64_t off,
-                           int64_t m) {
-  if (m == 0) return;
+                           int64_t m, bool share) {
   at::Tensor p = pres.slice(0, 0, m);
   for (int c = 0; c < in->Columns(); ++c) {
+    if (share && !in->column(c).nullable()) {
+      cols[c].validity = p;
+      continue;
+    }
     at::Tensor v = cols[c].validity.slice(0, off, off + m);
     if (in->column(c).nullable()) v.mul_(p);
     else v.copy_(p);
@@ -476,12 +482,12 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
       lcols.assign(sink->cols.begin(), sink->cols.begin() + left->Columns());
       rcols.assign(sink->cols.begin() + left->Columns(), sink->cols.end());
     } else {
-      for (const auto &col : left->columns())
+      for (const auto &col : left->columns())  // (null-side validity: apply_presence)
         lcols.push_back(make_fixed_column(cfg.GetLeftTablePrefix() + col.name, col.type, rows, ex.device,
-                                          col.nullable() || lnull));
+                                          col.nullable()));
       for (const auto &col : right->columns())
         rcols.push_back(make_fixed_column(cfg.GetRightTablePrefix() + col.name, col.type, rows, ex.device,
-                                          col.nullable() || rnull));
+                                          col.nullable()));
     }
     auto word_outs = [&](const RadixSide &sd) {
       std::vector<at::Tensor> w;
@@ -546,10 +552,11 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   if (m > 0) {
     unpack_validity_words(ex, left, L, lwords, lcols, off, m);
     unpack_validity_words(ex, right, R, rwords, rcols, off, m);
-    // outer joins: the null side's validity from the presence bytes
+  }
+  {  // outer joins: the null side's validity from the presence bytes
     const at::Tensor &lpres = build_left ? bpres : ppres, &rpres = build_left ? ppres : bpres;
-    if (lnull) apply_presence(lcols, left, lpres, off, m);
-    if (rnull) apply_presence(rcols, right, rpres, off, m);
+    if (lnull) apply_presence(lcols, left, lpres, off, m, sink == nullptr);
+    if (rnull) apply_presence(rcols, right, rpres, off, m, sink == nullptr);
   }
   trace::add_counter("join.radix.rows_out", m);
   if (oj) trace::add_counter("join.radix.outer", oj);
@@ -782,6 +789,9 @@ static TablePtr range_join(const Exec &ex, const TablePtr &left, const TablePtr 
 struct RadixKeys {
   at::Tensor l, r;
   bool ok = false, verify = false;
+  bool composite = false;  // l / r are exact composites: key column i = lo[i] + ((key >> shift[i]) & 2^bits[i]-1)
+  std::vector<int64_t> lo;
+  std::vector<int> shift, bits;
 };
 
 static bool int_key(const Column &c) {
@@ -801,52 +811,62 @@ static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr
     k.ok = true;
     return k;
   }
+  bool packable = lc.size() <= (size_t)kMaxCompositeKeys;
   for (size_t i = 0; i < lc.size(); ++i) {
     const Column &a = left->column(lc[i]), &b = right->column(rc[i]);
-    if (!int_key(a) || !int_key(b) || !(a.type == b.type)) return k;
-  }
-  std::vector<at::Tensor> lk, rk, mm;
-  for (size_t i = 0; i < lc.size(); ++i) {
-    lk.push_back(encode_keys(ex, left, {lc[i]}, true).keys);
-    rk.push_back(encode_keys(ex, right, {rc[i]}, true).keys);
-    for (const at::Tensor &x : {lk.back(), rk.back()})
-      if (x.numel()) {
-        auto m2 = at::aminmax(x);
-        mm.push_back(std::get<0>(m2).reshape({1}));
-        mm.push_back(std::get<1>(m2).reshape({1}));
-      } else {
-        mm.push_back(at::full({1}, std::numeric_limits<int64_t>::max(), x.options()));
-        mm.push_back(at::full({1}, std::numeric_limits<int64_t>::min(), x.options()));
-      }
-  }
-  const std::vector<int64_t> h = to_host_vec(at::cat(mm));
-  std::vector<int64_t> lo(lc.size());
-  std::vector<int> nbits(lc.size());
-  int total = 0;
-  for (size_t i = 0; i < lc.size(); ++i) {
-    lo[i] = std::min(h[4 * i], h[4 * i + 2]);
-    const int64_t hi = std::max(h[4 * i + 1], h[4 * i + 3]);
-    const uint64_t span = hi >= lo[i] ? (uint64_t)hi - (uint64_t)lo[i] : 0;
-    int b = 0;
-    while (b < 64 && (span >> b) != 0) ++b;
-    nbits[i] = b;
-    total += b;
+    if (!simple_key(a) || !simple_key(b) || !(a.type == b.type)) return k;
+    packable = packable && int_key(a);
   }
   k.ok = true;
-  if (total <= 63) {  // exact: key i occupies its own bit range
-    auto pack = [&](const std::vector<at::Tensor> &ks) {
-      at::Tensor acc = at::zeros_like(ks[0]);
-      int sh = 0;
-      for (size_t i = ks.size(); i-- > 0;) {
-        acc.bitwise_or_(at::bitwise_left_shift(ks[i] - lo[i], sh));
-        sh += nbits[i];
-      }
-      return acc;
+  if (packable) {
+    // per-key span over both relations (signed / byte storage: min / max of the column itself,
+    // wider unsigned storage through its 64-bit image)
+    auto span_of = [&](const Column &c, const TablePtr &t, int col) -> at::Tensor {
+      if (c.data.numel() == 0)
+        return at::tensor({std::numeric_limits<int64_t>::max(), std::numeric_limits<int64_t>::min()},
+                          ex.opts(at::kLong));
+      const bool direct = c.type.kind() == ValueKind::SIGNED_INT || c.type.width() == 1;
+      at::Tensor x = direct ? c.data : encode_keys(ex, t, {col}, true).keys;
+      auto m2 = at::aminmax(x);
+      return at::stack({std::get<0>(m2).to(at::kLong), std::get<1>(m2).to(at::kLong)});
     };
-    k.l = pack(lk);
-    k.r = pack(rk);
-    trace::add_counter("join.radix.composite_key", 1);
-    return k;
+    std::vector<at::Tensor> mm;
+    for (size_t i = 0; i < lc.size(); ++i) {
+      mm.push_back(span_of(left->column(lc[i]), left, lc[i]));
+      mm.push_back(span_of(right->column(rc[i]), right, rc[i]));
+    }
+    const std::vector<int64_t> h = to_host_vec(at::cat(mm));
+    const size_t nk = lc.size();
+    k.lo.resize(nk);
+    k.bits.resize(nk);
+    k.shift.resize(nk);
+    int total = 0;
+    for (size_t i = 0; i < nk; ++i) {
+      k.lo[i] = std::min(h[4 * i], h[4 * i + 2]);
+      const int64_t hi = std::max(h[4 * i + 1], h[4 * i + 3]);
+      const uint64_t span = hi >= k.lo[i] ? (uint64_t)hi - (uint64_t)k.lo[i] : 0;
+      int b = 0;
+      while (b < 64 && (span >> b) != 0) ++b;
+      k.bits[i] = b;
+      total += b;
+    }
+    if (total <= 63) {  // exact: key i occupies its own bit range (the last key the lowest bits)
+      for (size_t i = nk, sh = 0; i-- > 0;) {
+        k.shift[i] = (int)sh;
+        sh += k.bits[i];
+      }
+      auto pack = [&](const TablePtr &t, const std::vector<int> &cols) {
+        std::vector<ColView> v = views(t, cols);
+        at::Tensor out = ex.empty_i64(t->Rows());
+        KCALL(ex, composite_key_pack, v.data(), (int)nk, k.lo.data(), k.shift.data(), t->Rows(), ptr<int64_t>(out));
+        return out;
+      };
+      k.l = pack(left, lc);
+      k.r = pack(right, rc);
+      k.composite = true;
+      trace::add_counter("join.radix.composite_key", 1);
+      return k;
+    }
   }
   k.l = encode_keys(ex, left, lc, false).keys;  // row hash of the key columns
   k.r = encode_keys(ex, right, rc, false).keys;
@@ -876,61 +896,90 @@ static int64_t key_mismatches(const TablePtr &out, const JoinConfig &cfg, int nl
 // columns); nullptr when ineligible or when the kernels report an overflow / collision.  Tables
 // with string / binary / list columns join their fixed-width columns plus a row-number column,
 // and the var-width columns are gathered by those row numbers afterwards (two-pass offsets +
-// bytes gather, row -1 -> null).
+// bytes gather, row -1 -> null).  Exact composite keys (no sink): the proxy tables carry the
+// composite in place of the key columns, so the passes and the write kernel move one 8-byte key
+// (as in the one-key join), and composite_key_unpack rebuilds the key columns of the output.
 static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const TablePtr &right, const JoinConfig &cfg,
                                JoinSink *sink) {
   RadixKeys k = radix_keys(ex, left, right, cfg);
   if (!k.ok) return nullptr;
-  auto has_var = [](const TablePtr &t) {
+  auto var_col = [](const Column &c) { return c.is_var() || c.type.kind() == ValueKind::FIXED_BYTES; };
+  auto has_var = [&](const TablePtr &t) {
     for (const auto &c : t->columns())
-      if (c.is_var() || c.type.kind() == ValueKind::FIXED_BYTES) return true;
+      if (var_col(c)) return true;
     return false;
   };
   const bool lvar = has_var(left), rvar = has_var(right);
   // a chunked distributed join writes into its sink: fixed-width tables on exact keys only
   if ((lvar || rvar || k.verify) && sink) return nullptr;
-  // proxy of a side with var-width columns: its fixed-width columns + the row number
-  static const std::string kRow = "__cylon_row";
-  auto proxy = [&](const TablePtr &t, std::vector<int> &fixed_pos) {
+  const bool ckey = k.composite && !sink;
+  const auto &lc = cfg.GetLeftColumnIdx();
+  const auto &rc = cfg.GetRightColumnIdx();
+  // proxy of a side: [composite key] + its fixed-width non-key columns [+ the row number];
+  // pos[c] = proxy column of the side's column c (-1: rebuilt from the key or gathered)
+  static const std::string kRow = "__cylon_row", kKey = "__cylon_key";
+  auto proxy = [&](const TablePtr &t, bool var, const std::vector<int> &keys, const at::Tensor &img,
+                   std::vector<int> &pos) {
+    pos.assign(t->Columns(), -1);
     std::vector<Column> cols;
+    if (ckey) cols.emplace_back(kKey, DataType(Type::INT64), t->Rows(), img);
     for (int c = 0; c < t->Columns(); ++c) {
       const Column &col = t->column(c);
-      if (col.is_var() || col.type.kind() == ValueKind::FIXED_BYTES) continue;
-      fixed_pos.push_back(c);
+      if (var_col(col) || (ckey && std::find(keys.begin(), keys.end(), c) != keys.end())) continue;
+      pos[c] = (int)cols.size();
       cols.push_back(col);
     }
-    cols.emplace_back(kRow, DataType(Type::INT64), t->Rows(), at::arange(t->Rows(), ex.opts(at::kLong)));
+    if (var) cols.emplace_back(kRow, DataType(Type::INT64), t->Rows(), at::arange(t->Rows(), ex.opts(at::kLong)));
     return Table::Make(t->GetContext(), std::move(cols));
   };
-  std::vector<int> lfix, rfix;
-  TablePtr lp = lvar ? proxy(left, lfix) : left, rp = rvar ? proxy(right, rfix) : right;
+  std::vector<int> lpos, rpos;
+  const bool lpx = lvar || ckey, rpx = rvar || ckey;
+  TablePtr lp = lpx ? proxy(left, lvar, lc, k.l, lpos) : left, rp = rpx ? proxy(right, rvar, rc, k.r, rpos) : right;
   if (!radix_eligible(lp) || !radix_eligible(rp)) return nullptr;
   TablePtr out = radix_join(ex, lp, rp, k.l, k.r, cfg, sink);
   if (!out) return nullptr;
-  if (k.verify) {
-    if (lvar || rvar) {  // key columns sit at other positions in a proxy: verify on the final table below
-    } else if (int64_t bad = key_mismatches(out, cfg, left->Columns())) {
+  if (k.verify && !lvar && !rvar)
+    if (int64_t bad = key_mismatches(out, cfg, left->Columns())) {
       trace::add_counter("join.radix.hash_collision_fallback", bad);
       return nullptr;
     }
-  }
-  if (!lvar && !rvar) return out;
+  if (!lpx && !rpx) return out;
   const JoinType jt = cfg.GetType();
-  auto side = [&](const TablePtr &orig, bool var, const std::vector<int> &fix, int first, int np, bool may_null,
-                  const std::string &prefix) {
+  auto side = [&](const TablePtr &orig, bool px, bool var, const std::vector<int> &pos, const std::vector<int> &keys,
+                  int first, int np, bool may_null, const std::string &prefix) {
     std::vector<Column> cols(orig->Columns());
-    if (!var) {
+    if (!px) {
       for (int c = 0; c < orig->Columns(); ++c) cols[c] = out->column(first + c);
       return cols;
     }
-    for (size_t j = 0; j < fix.size(); ++j) cols[fix[j]] = out->column(first + (int)j);
+    for (int c = 0; c < orig->Columns(); ++c)
+      if (pos[c] >= 0) cols[c] = out->column(first + pos[c]);
+    if (ckey) {  // the key columns from the composite (its validity: the side's presence)
+      const Column &img = out->column(first);
+      std::vector<MutColView> mv;
+      for (size_t i = 0; i < keys.size(); ++i) {
+        const Column &kc = orig->column(keys[i]);
+        Column o = make_fixed_column(prefix + kc.name, kc.type, img.length, ex.device, false);
+        o.validity = img.validity;
+        MutColView v;
+        v.data = reinterpret_cast<uint8_t *>(ptr<uint8_t>(o.data.view(at::kByte)));
+        v.width = kc.type.width();
+        v.kind = static_cast<int>(kc.type.kind());
+        mv.push_back(v);
+        cols[keys[i]] = std::move(o);
+      }
+      KCALL(ex, composite_key_unpack, ptr<int64_t>(img.data), img.length, (int)keys.size(), k.lo.data(),
+            k.shift.data(), k.bits.data(), mv.data());
+      trace::add_counter("join.radix.composite_unpacked", (int64_t)keys.size());
+    }
+    if (!var) return cols;
     const Column &rid = out->column(first + np - 1);
     at::Tensor idx = rid.nullable() ? at::where(rid.validity.to(at::kBool), rid.data, at::full({1}, -1, rid.data.options()))
                                     : rid.data;
     std::vector<Column> vcols;
     std::vector<int> vpos;
     for (int c = 0; c < orig->Columns(); ++c)
-      if (orig->column(c).is_var() || orig->column(c).type.kind() == ValueKind::FIXED_BYTES) {
+      if (var_col(orig->column(c))) {
         vcols.push_back(orig->column(c));
         vpos.push_back(c);
       }
@@ -938,12 +987,12 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
     for (size_t j = 0; j < vpos.size(); ++j) cols[vpos[j]] = g->column((int)j).with_name(prefix + g->column((int)j).name);
     return cols;
   };
-  std::vector<Column> all = side(left, lvar, lfix, 0, lp->Columns(), left_may_null(jt), cfg.GetLeftTablePrefix());
-  std::vector<Column> rc = side(right, rvar, rfix, lp->Columns(), rp->Columns(), right_may_null(jt),
-                                cfg.GetRightTablePrefix());
-  for (auto &c : rc) all.push_back(std::move(c));
+  std::vector<Column> all = side(left, lpx, lvar, lpos, lc, 0, lp->Columns(), left_may_null(jt), cfg.GetLeftTablePrefix());
+  std::vector<Column> rcols = side(right, rpx, rvar, rpos, rc, lp->Columns(), rp->Columns(), right_may_null(jt),
+                                   cfg.GetRightTablePrefix());
+  for (auto &c : rcols) all.push_back(std::move(c));
   TablePtr res = Table::Make(left->GetContext(), std::move(all));
-  trace::add_counter("join.radix.var_gather", 1);
+  if (lvar || rvar) trace::add_counter("join.radix.var_gather", 1);
   if (k.verify)
     if (int64_t bad = key_mismatches(res, cfg, left->Columns())) {
       trace::add_counter("join.radix.hash_collision_fallback", bad);

@@ -48,8 +48,10 @@ def test_radix_outer_join_matches_cpu(gpu_ctx, ctx, monkeypatch, how, left_small
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
 
 
-@pytest.mark.parametrize("how", ["inner", "outer"])
+@pytest.mark.parametrize("how", ["inner", "left", "outer"])
 def test_radix_join_composite_two_keys(gpu_ctx, ctx, monkeypatch, how):
+    """Two int keys -> one exact composite (composite_key_pack); the proxy tables carry it in place
+    of the key columns and composite_key_unpack rebuilds them (null where the side is absent)."""
     rng = np.random.default_rng(6)
     n = 400_000
     a = pa.table({"k": rng.integers(0, 200_000, n), "g": rng.integers(-3, 3, n).astype(np.int32),
@@ -57,7 +59,28 @@ def test_radix_join_composite_two_keys(gpu_ctx, ctx, monkeypatch, how):
     b = pa.table({"k": rng.integers(0, 200_000, n), "g": rng.integers(-3, 3, n).astype(np.int32),
                   "w": rng.random(n)})
     got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["k", "g"], monkeypatch)
-    assert c.get("join.radix.composite_key", 0) == 1, c
+    assert c.get("join.radix.composite_key", 0) == 1 and c.get("join.radix.composite_unpacked", 0) == 4, c
+    assert list(got.columns) == list(exp.columns)
+    pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
+
+
+def test_radix_join_composite_mixed_widths_var_payload(gpu_ctx, ctx, monkeypatch):
+    """Three keys of widths 8 / 4 / 1 (signed, signed, unsigned) with negative minima, keys not
+    leading the column order, and a string payload (composite proxy + row-number gather)."""
+    rng = np.random.default_rng(16)
+    n = 300_000
+    def mk(seed_off, tag):
+        r = np.random.default_rng(60 + seed_off)
+        return pa.table({"s": [f"{tag}{x}" for x in r.integers(0, 500, n)],
+                         "k": r.integers(-(1 << 40), -(1 << 40) + 90_000, n),
+                         "x": r.random(n),
+                         "h": r.integers(-70_000, -69_990, n).astype(np.int32),
+                         "u": r.integers(250, 256, n).astype(np.uint8)})
+    a, b = mk(0, "a"), mk(1, "b")
+    got, exp, c = _join(gpu_ctx, ctx, a, b, "left", ["k", "h", "u"], monkeypatch)
+    assert c.get("join.radix.composite_key", 0) == 1 and c.get("join.radix.var_gather", 0) == 1, c
+    assert list(got.columns) == list(exp.columns)
+    assert len(exp) > n
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
 
 

@@ -38,7 +38,10 @@ tables = {}
 for t in types:
     two = t.endswith("2")
     if two not in tables:
+        tables.clear()  # one table pair resident at a time (1B x 1B: 64-80 GB per pair)
+        torch.cuda.empty_cache()
         tables[two] = (side("a", two), side("b", two))
+    torch.cuda.empty_cache()  # each type starts from the same allocator state
     L, R = tables[two]
     how = {"inner": "inner", "left": "left", "right": "right", "outer": "outer"}[t.rstrip("2")]
     on = [0, 1] if two else [0]
@@ -57,6 +60,7 @@ for t in types:
         torch.cuda.synchronize()
         ts.append(1000 * (time.perf_counter() - t0))
         del out
+    torch.cuda.reset_peak_memory_stats()
     C.trace_enable(True)
     C.trace_reset()
     out = run()
@@ -65,4 +69,5 @@ for t in types:
     C.trace_enable(False)
     del out
     print(json.dumps({"type": t, "rows_per_side": n, "ms": round(statistics.median(ts), 3),
-                      "all_ms": [round(x, 2) for x in ts], "out_rows": rows, "counters": cnt}), flush=True)
+                      "all_ms": [round(x, 2) for x in ts], "out_rows": rows,
+                      "peak_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1), "counters": cnt}), flush=True)
