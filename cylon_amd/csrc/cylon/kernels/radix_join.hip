@@ -59,6 +59,18 @@ struct ColSet {
   // instruction's same-address LDS atomics in lane order -- sets *order_bad.
   int check_order;
   int *order_bad;
+  // Next-digit side output (LSD sort): as column 0 is stored at row r, nd_out[r] = (stored >>
+  // nd_shift) & nd_mask -- the NEXT pass's digit, so that pass's per-tile histogram reads 2 bytes
+  // per row instead of the 8-byte key (nullptr: off)
+  uint16_t *nd_out;
+  int nd_shift;
+  uint32_t nd_mask;
+};
+
+// Digit read from a next-digit array written by the previous pass (histogram kernels only)
+struct NdDigit {
+  const uint16_t *d;
+  __device__ __forceinline__ uint32_t operator()(int64_t i) const { return d[i]; }
 };
 
 __device__ __forceinline__ uint32_t part_of(int64_t key, int bits) {
@@ -184,6 +196,17 @@ struct TileSched {
   const uint32_t *xt_off;        // [tile][nbuckets] output row of the tile's first row of each bucket
   unsigned int *xt_ticket;       // [8] next tile of each XCD's contiguous chunk
   int64_t xt_tiles;              // tiles of the pass
+  // slot mode (the MSD second pass of a join partition, k_rows_pass<..., SLOT>): the input is the
+  // first pass's bucket-major output; a tile never straddles an input bucket, and input bucket b's
+  // rows go to output slots b * nbuckets + d of sl_slot rows each (claimed with one atomic per
+  // (tile, digit) -- no histogram pass); a run that does not fit goes to the trash rows after the
+  // last slot and raises sl_overflow (the caller repartitions exactly)
+  const uint32_t *sl_tpre = nullptr;   // [nb1 + 1] first tile of each input bucket (exclusive scan)
+  const uint32_t *sl_bbase = nullptr;  // [nb1] first input row of each input bucket
+  unsigned int *sl_cursor = nullptr;   // [nb1 * nbuckets] rows claimed in each output slot
+  unsigned int *sl_overflow = nullptr;
+  int64_t sl_slot = 0;                 // rows per output slot
+  int sl_nb1 = 0;                      // input buckets (<= 1023)
 };
 
 // XCD-tile mode.  Histogram mode gives each block a contiguous chunk of rows, so the tiles of
@@ -201,6 +224,16 @@ __device__ __forceinline__ int xcc_id() {
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
   return x & (kXcds - 1);
 }
+// slot mode: input bucket of tile t (tp: LDS copy of sl_tpre; the last bucket whose first tile <= t)
+__device__ __forceinline__ int sl_bucket(const uint32_t *tp, int nb1, int64_t t) {
+  int lo = 0, hi = nb1 - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((int64_t)tp[mid] <= t) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
 // first row of the next tile this block processes, or n_rows when every chunk is exhausted
 __device__ __forceinline__ int64_t xt_claim(const TileSched &lb, int home, int64_t tile_rows, int64_t n_rows) {
   for (int k = 0; k < kXcds; ++k) {
@@ -370,7 +403,8 @@ constexpr int kRPStampTiles = 64, kRPStampSlots = 16;
 // 16-bit counters: stable exactly when one instruction's same-address atomics return in lane
 // order -- tools/lds_atomic_order.hip measures that on the device).
 // XT: XCD-tile schedule (tiles claimed in order per XCD, exact per-tile bucket offsets in lb).
-template <class Digit, bool W8, int THREADS, int RANK, bool XT = false>
+// SLOT: slot mode (TileSched): tiles of one input bucket each, per-(tile, digit) slot claims.
+template <class Digit, bool W8, int THREADS, int RANK, bool XT = false, bool SLOT = false>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_rows_pass(
     Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
     const int64_t *__restrict__ bh_scan, TileSched lb, unsigned long long *__restrict__ stamps) {
@@ -378,8 +412,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   constexpr int TILE = THREADS * kRPItems;
   constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;  // buckets per thread in the offset scan
   static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 4 <= TILE * 8, "ranking scratch must fit the stage");
-  constexpr bool TICKET = XT;  // tiles claimed one by one (not a contiguous chunk per block)
-  const int xhome = XT ? xcc_id() : 0;
+  constexpr bool TICKET = XT || SLOT;  // tiles claimed one by one (not a contiguous chunk per block)
+  static_assert(!(XT && SLOT), "one tile schedule");
+  static_assert(!SLOT || RANK == kRankBlockAtomic, "slot mode ranks with block atomics (counts in bcnt)");
+  const int xhome = TICKET ? xcc_id() : 0;
   __shared__ int64_t running[kRPMaxBuckets];
   __shared__ uint32_t toff[kRPMaxBuckets + 1];
   __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16, sdig[TILE] u32}
@@ -392,11 +428,57 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   uint32_t *sdig = reinterpret_cast<uint32_t *>(wcnt + WAVES * kRPMaxBuckets);
   uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
   __shared__ int64_t s_next;  // XT: first row of the next claimed tile
+  // SLOT: end row / input bucket of the current ([par]) and the next ([par ^ 1]) tile, in LDS
+  // rather than registers (the classic pass already runs at the 128-VGPR budget)
+  __shared__ int64_t s_tend[2];
+  __shared__ int s_tb[2];
+  int par = 0;
   bool order_bad = false;
+  // SLOT: the input buckets' first tiles (upper half of running[]: digits <= 512) and first rows
+  // (sbb) in LDS; tiles are dealt statically -- XCD x (= blockIdx % 8, the dispatcher's round
+  // robin) owns the tiles of input buckets [x nb1 / 8, (x + 1) nb1 / 8), its j-th block takes
+  // every nblk-th of them -- so taking the next tile is a few LDS reads (no atomic, no global load
+  // on the barrier path), and an XCD's CUs still work on adjacent tiles of the same buckets.
+  uint32_t *tp = reinterpret_cast<uint32_t *>(running + kRPMaxBuckets / 2);
+  __shared__ uint32_t sbb[SLOT ? kRPMaxBuckets : 1];
+  __shared__ int64_t s_tix, s_thi;  // SLOT (thread 0): this block's next tile index, its XCD's end
+  auto sl_take = [&](int slot) {    // thread 0: take the next tile, resolve its rows and bucket
+    const int64_t t = s_tix;
+    if (t >= s_thi) {
+      s_next = n;
+      s_tend[slot] = n;
+      s_tb[slot] = 0;
+      return;
+    }
+    s_tix = t + ((int64_t)gridDim.x - (blockIdx.x & (kXcds - 1)) + kXcds - 1) / kXcds;
+    const int bk = sl_bucket(tp, lb.sl_nb1, t);
+    const int64_t bend = bk + 1 < lb.sl_nb1 ? (int64_t)sbb[bk + 1] : n;
+    const int64_t r0 = (int64_t)sbb[bk] + (t - (int64_t)tp[bk]) * TILE;
+    s_next = r0;
+    s_tend[slot] = r0 + TILE < bend ? r0 + TILE : bend;
+    s_tb[slot] = bk;
+  };
 
   const int64_t b = blockIdx.x;
   int64_t begin, end;
-  if (TICKET) {
+  if (SLOT) {
+    for (int i = threadIdx.x; i < lb.sl_nb1; i += THREADS) {
+      tp[i] = lb.sl_tpre[i];
+      sbb[i] = lb.sl_bbase[i];
+    }
+    if (threadIdx.x == 0) {
+      const int x = blockIdx.x & (kXcds - 1);
+      const int b0 = lb.sl_nb1 * x / kXcds, b1 = lb.sl_nb1 * (x + 1) / kXcds;
+      const uint32_t ttot = lb.sl_tpre[lb.sl_nb1];
+      s_tix = (int64_t)(b0 < lb.sl_nb1 ? lb.sl_tpre[b0] : ttot) + blockIdx.x / kXcds;
+      s_thi = b1 < lb.sl_nb1 ? lb.sl_tpre[b1] : ttot;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) sl_take(0);
+    __syncthreads();
+    begin = s_next;
+    end = n;
+  } else if (TICKET) {
     if (threadIdx.x == 0) s_next = xt_claim(lb, xhome, TILE, n);
     __syncthreads();
     begin = s_next;
@@ -416,13 +498,15 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
   for (int k = 0; k < kRPItems; ++k) {
     const int64_t i = begin + wrow + k * kWave + lane;
-    if (i < end) kv[k] = (uint64_t)digit.keys[i];
+    if (i < (SLOT ? s_tend[0] : end)) kv[k] = (uint64_t)digit.keys[i];
   }
   for (int64_t tile = begin, next = 0; tile < end; tile = next) {
     next = tile + TILE;
     const int tix = (int)((tile - begin) / TILE);
     RP_STAMP(0);
-    const int cnt = (int)((end - tile) < TILE ? (end - tile) : TILE);
+    const int cnt = SLOT ? (int)(s_tend[par] - tile) : (int)((end - tile) < TILE ? (end - tile) : TILE);
+    // SLOT: claim the next tile now, where few registers are live (read after this tile's barriers)
+    if (SLOT && threadIdx.x == 0) sl_take(par ^ 1);
     // XT: this tile's bucket offsets (consumed after the slot phase; the load overlaps the ranking)
     const uint32_t xoff = XT && threadIdx.x < nbuckets ? lb.xt_off[(tile / TILE) * nbuckets + threadIdx.x] : 0u;
     uint32_t pl[kRPItems];  // digit, then (in-wave rank << 16) | digit, then sorted slot; ~0 = inactive
@@ -471,6 +555,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     __syncthreads();
     RP_STAMP(2);
+    // SLOT: claim this tile's run in every output slot it feeds as soon as the counts exist (the
+    // atomics' latency hides behind the scan and the slot phase)
+    uint32_t sl_c = 0, sl_base = 0;
+    if (SLOT && threadIdx.x < nbuckets) {
+      sl_c = STABLE ? 0u : bcnt[threadIdx.x];
+      if (sl_c) sl_base = atomicAdd(&lb.sl_cursor[(int64_t)s_tb[par] * nbuckets + threadIdx.x], sl_c);
+    }
     {  // thread owns buckets [t*BPT, t*BPT+BPT): exclusive prefix over waves (in place), then a
        // block scan of the thread totals
       uint32_t loc[BPT];
@@ -513,6 +604,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       pl[k] = pos;
     }
     if (XT && threadIdx.x < nbuckets) running[threadIdx.x] = xoff;
+    if (SLOT && threadIdx.x < nbuckets) {
+      const bool fits = (int64_t)sl_base + sl_c <= lb.sl_slot;
+      if (sl_c && !fits) atomicOr(lb.sl_overflow, 1u);
+      running[threadIdx.x] = fits ? ((int64_t)s_tb[par] * nbuckets + threadIdx.x) * lb.sl_slot + sl_base
+                                  : (int64_t)lb.sl_nb1 * nbuckets * lb.sl_slot;  // the trash rows
+    }
     __syncthreads();
     RP_STAMP(4);
     int64_t dst[kRPItems];  // destination of sorted slot j = threadIdx.x + q * THREADS
@@ -539,7 +636,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       const int w = cols.width[c];
       uint8_t *out = cols.out[c];
       const uint64_t x = c == 0 ? cols.key_xor : 0ull;
-      if (TICKET && c + 1 == cols.n && threadIdx.x == 0) s_next = xt_claim(lb, xhome, TILE, n);
+      if (TICKET && c + 1 == cols.n && threadIdx.x == 0) {
+        if (!SLOT) s_next = xt_claim(lb, xhome, TILE, n);
+      }
 #pragma unroll
       for (int k = 0; k < kRPItems; ++k)
         if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
@@ -561,19 +660,32 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
         for (int k = 0; k < kRPItems; ++k) {
           const int64_t i = next + wrow + k * kWave + lane;
-          if (i < end) kv[k] = (uint64_t)digit.keys[i];
+          if (i < (SLOT ? s_tend[par ^ 1] : end)) kv[k] = (uint64_t)digit.keys[i];
         }
       }
+      if (c == 0 && cols.nd_out != nullptr) {
 #pragma unroll
-      for (int q = 0; q < kRPItems; ++q) {
-        const int j = threadIdx.x + q * THREADS;
-        if (j < cnt) stw<W8>(out, dst[q], w, ldw<W8>(st, j, w));
+        for (int q = 0; q < kRPItems; ++q) {
+          const int j = threadIdx.x + q * THREADS;
+          if (j < cnt) {
+            const uint64_t kv0 = ldw<W8>(st, j, w);
+            stw<W8>(out, dst[q], w, kv0);
+            cols.nd_out[dst[q]] = (uint16_t)((kv0 >> cols.nd_shift) & cols.nd_mask);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < kRPItems; ++q) {
+          const int j = threadIdx.x + q * THREADS;
+          if (j < cnt) stw<W8>(out, dst[q], w, ldw<W8>(st, j, w));
+        }
       }
       __syncthreads();
       RP_STAMP(7 + 2 * c);
     }
     if (!TICKET)
       for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] += toff[p + 1] - toff[p];
+    if (SLOT) par ^= 1;
   }
   if (order_bad) atomicOr(cols.order_bad, 1);
 }
@@ -743,10 +855,23 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
         if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
       __syncthreads();
       if (TICKET && c + 1 == cols.n) next = s_next;
+      if (c == 0 && cols.nd_out != nullptr) {
 #pragma unroll
-      for (int q = 0; q < kRPItems; ++q) {
-        const int j = tx + q * THREADS;
-        if (j < cnt) stw<W8>(out, running[dp[q] >> 16] + (int64_t)(dp[q] & 0xffffu), w, ldw<W8>(st, j, w));
+        for (int q = 0; q < kRPItems; ++q) {
+          const int j = tx + q * THREADS;
+          if (j < cnt) {
+            const int64_t o = running[dp[q] >> 16] + (int64_t)(dp[q] & 0xffffu);
+            const uint64_t kv0 = ldw<W8>(st, j, w);
+            stw<W8>(out, o, w, kv0);
+            cols.nd_out[o] = (uint16_t)((kv0 >> cols.nd_shift) & cols.nd_mask);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < kRPItems; ++q) {
+          const int j = tx + q * THREADS;
+          if (j < cnt) stw<W8>(out, running[dp[q] >> 16] + (int64_t)(dp[q] & 0xffffu), w, ldw<W8>(st, j, w));
+        }
       }
       __syncthreads();
     }
@@ -1057,7 +1182,8 @@ template <class Digit, bool CAN_UNSTABLE = std::is_same<Digit, PartDigit>::value
 static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const uint8_t *const *in, uint8_t *const *out,
                              const int *widths, int ncols, int64_t *ws, void *stream, uint64_t key_xor = 0,
                              bool stable = true, bool tiles_prescanned = false,
-                             const uint32_t *bucket_extra = nullptr) {
+                             const uint32_t *bucket_extra = nullptr, const uint16_t *nd_in = nullptr,
+                             uint16_t *nd_out = nullptr, int nd_shift = 0, uint32_t nd_mask = 0) {
   if (n == 0) return;
   CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
   CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
@@ -1085,6 +1211,7 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   const bool xt = threads == 1024 && n < (int64_t(1) << 32) && rp_xt();
   CYLON_CHECK(xt || bucket_extra == nullptr, Code::Invalid, "radix pass: gapped layouts need the XCD-tile schedule");
   if (!xt) tiles_prescanned = false;  // histogram mode counts its own blocks (the prescan is unused)
+  if (!xt) nd_in = nullptr;            // ... and reads the keys (the previous pass's digits go unused)
   if (xt) {  // exact per-tile offsets, tiles claimed in order per XCD (see xt_claim)
     const XtLayout L = xt_layout(n, nb);
     uint16_t *th = reinterpret_cast<uint16_t *>(ws + L.th);
@@ -1092,7 +1219,11 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
     uint32_t *csum = reinterpret_cast<uint32_t *>(ws + L.csum), *cpre = reinterpret_cast<uint32_t *>(ws + L.cpre);
     unsigned *tk = reinterpret_cast<unsigned *>(ws + L.tickets);
     HIP_CHECK(hipMemsetAsync(tk, 0, kXcds * sizeof(unsigned), s));
-    if (!tiles_prescanned) {  // else the caller already wrote th (radix_sort_prehist + fold)
+    if (!tiles_prescanned && nd_in != nullptr) {  // the previous pass wrote this pass's digits
+      hipLaunchKernelGGL(k_rp_hist_tiles<NdDigit>, dim3((unsigned)std::min<int64_t>(L.ntiles, kNumCUs * 16)),
+                         dim3(kHTThreads), 0, s, NdDigit{nd_in}, n, nb, L.ntiles, th);
+      HIP_LAUNCH_CHECK();
+    } else if (!tiles_prescanned) {  // else the caller already wrote th (radix_sort_prehist + fold)
       hipLaunchKernelGGL(k_rp_hist_tiles<Digit>, dim3((unsigned)std::min<int64_t>(L.ntiles, kNumCUs * 16)),
                          dim3(kHTThreads), 0, s, dg, n, nb, L.ntiles, th);
       HIP_LAUNCH_CHECK();
@@ -1125,6 +1256,9 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   ColSet cs;
   cs.n = ncols;
   cs.key_xor = key_xor;
+  cs.nd_out = nd_out;
+  cs.nd_shift = nd_shift;
+  cs.nd_mask = nd_mask;
   const char *gd = std::getenv("CYLON_RP_GUARD");  // A/B knob: 0 disables the ranking guard
   cs.check_order = want_stable && !(gd && gd[0] == '0') ? 1 : 0;
   cs.order_bad = order_flag();
@@ -1170,10 +1304,110 @@ void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, 
 
 void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_bits, const uint8_t *const *in,
                           uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream,
-                          uint64_t key_xor, uint64_t digit_flip, bool tiles_prescanned) {
+                          uint64_t key_xor, uint64_t digit_flip, bool tiles_prescanned, const uint16_t *nd_in,
+                          uint16_t *nd_out, int nd_shift, int nd_bits) {
   const uint32_t nb = 1u << digit_bits;
+  // (the digits come from column 0 as stored: images on every pass but a last one that restores keys)
+  CYLON_CHECK(nd_out == nullptr || (nd_bits >= 1 && nd_bits <= 16), Code::Invalid,
+              "sort pass: next-digit output of " << nd_bits << " bits");
   rows_pass_launch(ImageDigit{keys, shift, nb - 1, digit_flip}, n, digit_bits, in, out, widths, ncols, ws, stream,
-                   key_xor, true, tiles_prescanned);
+                   key_xor, true, tiles_prescanned, nullptr, nd_in, nd_out, nd_shift,
+                   nd_out ? (1u << nd_bits) - 1u : 0u);
+}
+
+// ---- slot mode (the MSD second pass of a join partition; TileSched)
+// tpre[b] = first tile of input bucket b (exclusive scan of its tile count), tpre[nb1] = all tiles
+__global__ __launch_bounds__(kRPThreads) void k_sl_tiles(const uint32_t *__restrict__ bbase, int nb1, int64_t n,
+                                                         uint32_t *__restrict__ tpre) {
+  __shared__ uint32_t wsum[kRPWaves];
+  const int b = threadIdx.x;
+  uint32_t t = 0;
+  if (b < nb1) {
+    const int64_t e = b + 1 < nb1 ? (int64_t)bbase[b + 1] : n;
+    t = (uint32_t)((e - (int64_t)bbase[b] + kRPTile - 1) / kRPTile);
+  }
+  const uint32_t ex = rp_block_exscan<kRPWaves>(t, wsum);
+  if (b < nb1) tpre[b] = ex;
+  if (b == nb1 - 1) tpre[nb1] = ex + t;
+}
+
+// rows in each slot (a slot that overflowed reports its capacity; the caller discards the result)
+__global__ void k_sl_counts(const unsigned int *__restrict__ cursor, int64_t nslots, int64_t slot,
+                            int64_t *__restrict__ counts) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += stride)
+    counts[i] = (int64_t)cursor[i] < slot ? (int64_t)cursor[i] : slot;
+}
+
+bool radix_slot_eligible(int64_t n, int ncols, int first_bits, int second_bits) {
+  return rp_xt() && n > 0 && n < (int64_t(1) << 32) && rp_threads(ncols, true) == 1024 && first_bits >= 1 &&
+         first_bits <= kRJMaxDigitBits && second_bits >= 1 && (1 << second_bits) <= kRPMaxBuckets / 2;
+}
+
+int64_t radix_slot_tile_rows() { return kRPTile; }
+
+int64_t radix_slot_workspace(int first_bits, int second_bits) {  // int64 words
+  const int64_t u32 = ((int64_t(1) << first_bits) + 1) + kXcds + 1 + (int64_t(1) << (first_bits + second_bits));
+  return (u32 + 1) / 2;
+}
+
+void radix_slot_rows_pass(const int64_t *keys, int64_t n, int total_bits, int first_bits, int second_bits,
+                          const uint8_t *const *in, uint8_t *const *out, const int *widths, int ncols,
+                          const int64_t *first_ws, int64_t slot, int64_t *ws, int64_t *counts, unsigned int *overflow,
+                          void *stream) {
+  CYLON_CHECK(radix_slot_eligible(n, ncols, first_bits, second_bits), Code::Invalid, "slot pass not eligible");
+  CYLON_CHECK(in[0] == reinterpret_cast<const uint8_t *>(keys) && widths[0] == 8, Code::Invalid,
+              "slot pass: column 0 must be the key");
+  CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols && slot > 0, Code::Invalid, "slot pass arguments");
+  hipStream_t s = as_stream(stream);
+  const int nb1 = 1 << first_bits;
+  const uint32_t nb = 1u << second_bits;
+  const int64_t nslots = int64_t(nb1) * nb;
+  // the first pass (XT, radix_rows_pass) left its bucket bases in its workspace
+  const uint32_t *bbase = reinterpret_cast<const uint32_t *>(first_ws + xt_layout(n, (uint32_t)nb1).bbase);
+  uint32_t *w32 = reinterpret_cast<uint32_t *>(ws);
+  uint32_t *tpre = w32;
+  unsigned int *cursor = w32 + nb1 + 1 + kXcds + 1;
+  HIP_CHECK(hipMemsetAsync(cursor, 0, sizeof(uint32_t) * nslots, s));
+  hipLaunchKernelGGL(k_sl_tiles, dim3(1), dim3(kRPThreads), 0, s, bbase, nb1, n, tpre);
+  HIP_LAUNCH_CHECK();
+  TileSched lb{};
+  lb.sl_tpre = tpre;
+  lb.sl_bbase = bbase;
+  lb.sl_cursor = cursor;
+  lb.sl_overflow = overflow;
+  lb.sl_slot = slot;
+  lb.sl_nb1 = nb1;
+  ColSet cs;
+  cs.n = ncols;
+  cs.key_xor = 0;
+  cs.check_order = 0;  // MSD: the order inside a slot is free
+  cs.order_bad = order_flag();
+  cs.nd_out = nullptr;
+  cs.nd_shift = 0;
+  cs.nd_mask = 0;
+  bool w8 = true;
+  for (int c = 0; c < kMaxFusedCols; ++c) {
+    cs.in[c] = c < ncols ? in[c] : nullptr;
+    cs.out[c] = c < ncols ? out[c] : nullptr;
+    cs.width[c] = c < ncols ? widths[c] : 8;
+    if (c < ncols) {
+      w8 &= widths[c] == 8;
+      CYLON_CHECK(in[c] != nullptr, Code::Invalid, "slot pass: every column is read (row ids come from pass 1)");
+    }
+  }
+  const PartDigit dg{keys, total_bits, 0, nb - 1};
+  // every XCD needs at least one block: its input buckets' tiles are dealt to its own blocks only
+  const int64_t nblocks = std::max<int64_t>(kXcds, std::min<int64_t>((n + kRPTile - 1) / kRPTile + nb1, kNumCUs));
+  if (w8)
+    hipLaunchKernelGGL((k_rows_pass<PartDigit, true, 1024, kRankBlockAtomic, false, true>), dim3((unsigned)nblocks),
+                       dim3(1024), 0, s, dg, second_bits, nb, cs, n, (int64_t)kRPTile, nblocks, nullptr, lb, nullptr);
+  else
+    hipLaunchKernelGGL((k_rows_pass<PartDigit, false, 1024, kRankBlockAtomic, false, true>), dim3((unsigned)nblocks),
+                       dim3(1024), 0, s, dg, second_bits, nb, cs, n, (int64_t)kRPTile, nblocks, nullptr, lb, nullptr);
+  HIP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_sl_counts, dim3(grid_for(nslots)), dim3(kBlock), 0, s, cursor, nslots, slot, counts);
+  HIP_LAUNCH_CHECK();
 }
 
 bool radix_xt_enabled() { return rp_xt(); }
@@ -1457,11 +1691,23 @@ constexpr int kRCWaves = kRCThreads / kWave;
 constexpr int kRCRowsPerThread = kRJMaxRows / kRCThreads;
 static_assert(kRCRowsPerThread * kRCThreads == kRJMaxRows, "count rows per thread");
 
+// rows of partition p: offs[p] .. offs[p + 1] (exact passes), or slot-mode partitions (slot > 0:
+// radix_slot_rows_pass) at p * slot holding offs[p] rows
+__device__ __forceinline__ void part_span(const int64_t *offs, int64_t slot, int64_t p, int64_t &b, int64_t &n) {
+  if (slot > 0) {
+    b = p * slot;
+    n = offs[p];
+  } else {
+    b = offs[p];
+    n = offs[p + 1] - b;
+  }
+}
+
 template <int OJ>
 __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_rj_count(
     const int64_t *__restrict__ pkeys, const int64_t *__restrict__ poffs, const int64_t *__restrict__ bkeys,
     const int64_t *__restrict__ boffs, int64_t nparts, int cap, int64_t pstride, int64_t *__restrict__ counts,
-    int *overflow) {
+    int *overflow, int64_t pslot, int64_t bslot) {
   using KT = int64_t;
   // pstride > 1: only partitions 0, pstride, 2 pstride, ... are counted, into counts[p / pstride]
   // (the sampled output-size estimate of the fused write path).  Output rows per partition:
@@ -1474,8 +1720,9 @@ __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4)))
   const int64_t nsample = (nparts + pstride - 1) / pstride;
   for (int64_t ci = blockIdx.x; ci < nsample; ci += gridDim.x) {
     const int64_t p = ci * pstride;
-    const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
-    const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
+    int64_t rb, nr, lb, nl;
+    part_span(boffs, bslot, p, rb, nr);
+    part_span(poffs, pslot, p, lb, nl);
     if (nr > cap) {  // uniform branch: whole block
       if (threadIdx.x == 0) {
         atomicOr(overflow, 1);
@@ -1578,7 +1825,8 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
                                                             unsigned long long *__restrict__ cursor, int64_t out_cap,
                                                             int *__restrict__ overflow,
                                                             unsigned long long *__restrict__ stamps, int pkey,
-                                                            uint8_t *__restrict__ ppres, uint8_t *__restrict__ bpres) {
+                                                            uint8_t *__restrict__ ppres, uint8_t *__restrict__ bpres,
+                                                            int64_t pslot, int64_t bslot) {
   using KT = int64_t;
   // out_offs != nullptr: partition p's rows start at out_offs[p] (exact count kernel ran first).
   // out_offs == nullptr: fused count -- each partition claims its rows from *cursor with one
@@ -1601,8 +1849,9 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
   const int wave = threadIdx.x / kWave;
   int tix = -1;  // debug stamps (CYLON_RJ_STAMPS): block 0's partition count, RP_STAMP slots 0..5
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
-    const int64_t rb = boffs[p], nr = boffs[p + 1] - rb;
-    const int64_t lb = poffs[p], nl = poffs[p + 1] - lb;
+    int64_t rb, nr, lb, nl;
+    part_span(boffs, bslot, p, rb, nr);
+    part_span(poffs, pslot, p, lb, nl);
     if (nr > cap && out_offs == nullptr && threadIdx.x == 0) atomicOr(overflow, 1);
     // inner: both sides needed; outer: a preserved side alone still emits its rows
     const bool live = (nr > 0 && nl > 0) || ((OJ & kOJProbe) && nl > 0) || ((OJ & kOJBuild) && nr > 0);
@@ -1890,7 +2139,7 @@ static int rj_grid(int64_t nparts) { return (int)std::min<int64_t>(nparts, kNumC
 
 void radix_join_count(const int64_t *pkeys, const int64_t *poffs, const int64_t *bkeys, const int64_t *boffs,
                       int64_t nparts, int64_t cap, int64_t *counts, int *overflow, void *stream, int64_t pstride,
-                      int outer) {
+                      int outer, int64_t pslot, int64_t bslot) {
   CYLON_CHECK(cap > 0 && cap <= kRJMaxRows, Code::Invalid, "radix join capacity " << cap);
   CYLON_CHECK(pstride >= 1, Code::Invalid, "partition stride " << pstride);
   CYLON_CHECK(outer >= 0 && outer <= 3, Code::Invalid, "radix join outer mode " << outer);
@@ -1901,19 +2150,19 @@ void radix_join_count(const int64_t *pkeys, const int64_t *poffs, const int64_t 
   switch (outer) {
     case 0:
       hipLaunchKernelGGL(k_rj_count<0>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
-                         pstride, counts, overflow);
+                         pstride, counts, overflow, pslot, bslot);
       break;
     case 1:
       hipLaunchKernelGGL(k_rj_count<1>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
-                         pstride, counts, overflow);
+                         pstride, counts, overflow, pslot, bslot);
       break;
     case 2:
       hipLaunchKernelGGL(k_rj_count<2>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
-                         pstride, counts, overflow);
+                         pstride, counts, overflow, pslot, bslot);
       break;
     default:
       hipLaunchKernelGGL(k_rj_count<3>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
-                         pstride, counts, overflow);
+                         pstride, counts, overflow, pslot, bslot);
   }
   HIP_LAUNCH_CHECK();
 }
@@ -1922,16 +2171,17 @@ template <bool W8, bool DMA, int OJ>
 static void rj_write_launch(dim3 grid, hipStream_t s, const int64_t *pk, const int64_t *poffs, const int64_t *bk,
                             const int64_t *boffs, int64_t nparts, int cap, const int64_t *out_offs, const ColSet &pc,
                             const ColSet &bs, const BuildOut &bo, unsigned long long *cur, int64_t out_cap,
-                            int *overflow, unsigned long long *st, int pkey, uint8_t *ppres, uint8_t *bpres) {
+                            int *overflow, unsigned long long *st, int pkey, uint8_t *ppres, uint8_t *bpres,
+                            int64_t pslot, int64_t bslot) {
   hipLaunchKernelGGL((k_rj_write<4, 3, W8, DMA, OJ>), grid, dim3(kRJThreads), 0, s, pk, poffs, bk, boffs, nparts, cap,
-                     out_offs, pc, bs, bo, cur, out_cap, overflow, st, pkey, ppres, bpres);
+                     out_offs, pc, bs, bo, cur, out_cap, overflow, st, pkey, ppres, bpres, pslot, bslot);
 }
 
 void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t *bkeys, const int64_t *boffs,
                       int64_t nparts, int64_t cap, const int64_t *out_offs, const uint8_t *const *pin,
                       uint8_t *const *pout, const int *pw, int npc, const uint8_t *const *bin, uint8_t *const *bout,
                       const int *bw, int nbc, void *stream, int64_t *cursor, int64_t out_cap, int *overflow, int pkey,
-                      int outer, uint8_t *ppres, uint8_t *bpres) {
+                      int outer, uint8_t *ppres, uint8_t *bpres, int64_t pslot, int64_t bslot) {
   CYLON_CHECK(pkey >= -1 && pkey < npc, Code::Invalid, "radix join probe key column " << pkey);
   CYLON_CHECK(npc <= kMaxFusedCols && nbc <= kMaxFusedCols, Code::Invalid, "too many columns");
   CYLON_CHECK(out_offs != nullptr || (cursor != nullptr && overflow != nullptr), Code::Invalid,
@@ -1988,7 +2238,7 @@ void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t 
   const int ci = (int)cap;
 #define RJW(W8_, DMA_, OJ_)                                                                                        \
   rj_write_launch<W8_, DMA_, OJ_>(grid, s, pkeys, poffs, bkeys, boffs, nparts, ci, out_offs, pc, bs, bo, cur, out_cap, \
-                                  overflow, st, pkey, ppres, bpres)
+                                  overflow, st, pkey, ppres, bpres, pslot, bslot)
   if (outer == 0) {
     if (dma) RJW(true, true, 0);
     else if (w8) RJW(true, false, 0);

@@ -17,6 +17,7 @@
 //      unmatched rows of the preserved side(s), appended with -1 partners.
 //   4. materialisation: one fused gather launch per side (K4).
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <limits>
 
@@ -157,7 +158,9 @@ static bool radix_eligible(const TablePtr &t) {
 }
 
 struct RadixSide {
-  at::Tensor keys, offs;
+  at::Tensor keys, offs;  // offs: partition offsets [2^bits + 1], or (slot > 0) rows per partition
+  int64_t slot = 0;       // slot mode: partition p's rows start at p * slot (RadixPartitionSlotted)
+  at::Tensor overflow;    // slot mode: int32 device flag, set when a partition outgrew its slot
   std::vector<at::Tensor> data, valid;  // per table column (valid undefined if not nullable or packed)
   std::vector<bool> is_key;             // data[c] is the (partitioned) key array itself
   // validity bytes kept packed 8 per 8-byte word (radix.cpp): vpos[c] = byte position of
@@ -178,8 +181,9 @@ static bool packs_validity(const TablePtr &t) {
 }
 
 // Partition every column of t (+ validity bytes) by the top `bits` bits of fmix64(key).
+// slot > 0: try the slot-mode (histogram-free MSD) partition first
 static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Tensor &keys, int bits,
-                                 const RangeSpec *range = nullptr) {
+                                 const RangeSpec *range = nullptr, int64_t slot = 0) {
   std::vector<at::Tensor> cur{keys};
   std::vector<int> widths{8};
   std::vector<int> dslot(t->Columns(), -1), vslot(t->Columns(), -1);
@@ -208,9 +212,18 @@ static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Te
     const char *e = std::getenv("CYLON_RP_STABLE");
     return e && e[0] == '1';
   }();
-  cur = RadixPartition(ex, std::move(cur), widths, bits, &offs, range, packs_validity(t) ? &packed : nullptr,
-                       range != nullptr || force_stable);
   RadixSide s;
+  std::vector<at::Tensor> sl;
+  if (slot > 0 && !range && !force_stable)
+    sl = RadixPartitionSlotted(ex, cur, widths, bits, slot, &offs, &s.overflow,
+                               packs_validity(t) ? &packed : nullptr);
+  if (!sl.empty()) {
+    cur = std::move(sl);
+    s.slot = slot;
+  } else {
+    cur = RadixPartition(ex, std::move(cur), widths, bits, &offs, range, packs_validity(t) ? &packed : nullptr,
+                         range != nullptr || force_stable);
+  }
   s.keys = cur[0];
   s.offs = offs;
   for (size_t w = nslots; w < cur.size(); ++w) s.vwords.push_back(cur[w]);
@@ -377,20 +390,45 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     if (col.nullable() && !packs_validity(bt)) ++q;  // packed validity words sit after the columns
   }
   const int64_t cap = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size(), (oj & 2) != 0);
-  // mean build rows per partition: 0.85 x capacity keeps the largest of ~1M uniform
-  // partitions >8 sigma below the capacity (Poisson), and lets 1B rows use 19 bits
-  // (passes of 10 + 9 bits; a 9-bit pass streams at ~5.5 TB/s, a 10-bit one ~3.9)
-  const int64_t target = std::max<int64_t>(1, cap * 85 / 100);
+  // fewest partition bits whose mean build partition sits 8 Poisson sigma (+16 rows) below the
+  // LDS capacity: the largest of ~2^18 uniform partitions then fits with ~1e-10 failure odds (an
+  // overflow only sends the join to the exact / global path).  1B rows: 18 bits -- two 9-bit
+  // passes -- for inner joins (cap 4544) and build-preserving outer joins (cap 4408) alike.
+  auto fits = [&](int64_t mean) { return (double)mean + 8.0 * std::sqrt((double)mean) + 16.0 <= (double)cap; };
   int bits = 0;
-  while ((nb >> bits) > target) ++bits;
+  while (bits < 24 && !fits((nb + (int64_t(1) << bits) - 1) >> bits)) ++bits;
   if (const char *xb = std::getenv("CYLON_RJ_EXTRA_BITS"))  // A/B knob: finer partitions
     bits = std::min(bits + std::max(0, std::atoi(xb)), 2 * 10);
   const int64_t nparts = int64_t(1) << bits;
+  // Slot mode for two-pass partitions (>= 11 bits): the second pass claims fixed-size partition
+  // slots (mean + 8 sigma + 64 rows) instead of reading the keys once more for exact offsets
+  // (k_rp_hist_tiles + scans + k_part_offsets, ~2 ms per 1B-row side).  A partition beyond its
+  // slot (skewed keys) sends that side through the exact passes.  Knob: CYLON_RJ_SLOT=0.
+  const char *se = std::getenv("CYLON_RJ_SLOT");
+  const bool slot_on = !(se && se[0] == '0');
+  auto slot_of = [&](int64_t rows) -> int64_t {
+    if (!slot_on || bits < 11) return 0;
+    const double mean = (double)rows / (double)nparts;
+    return ((int64_t)(mean + 8.0 * std::sqrt(mean) + 64.0) + 7) & ~int64_t(7);
+  };
   RadixSide L, R;
   {
     CYLON_PHASE("join.radix.partition", ex.device);
-    L = radix_partition(ex, left, lk, bits);
-    R = radix_partition(ex, right, rk, bits);
+    L = radix_partition(ex, left, lk, bits, nullptr, slot_of(nl));
+    R = radix_partition(ex, right, rk, bits, nullptr, slot_of(nr));
+    if (L.slot || R.slot) {  // a side whose partition outgrew a slot is partitioned exactly
+      at::Tensor f = at::stack({L.slot ? L.overflow[0] : at::zeros({}, ex.opts(at::kInt)),
+                                R.slot ? R.overflow[0] : at::zeros({}, ex.opts(at::kInt))}).cpu();
+      if (f[0].item<int>()) {
+        trace::add_counter("join.radix.slot_overflow", 1);
+        L = radix_partition(ex, left, lk, bits);
+      }
+      if (f[1].item<int>()) {
+        trace::add_counter("join.radix.slot_overflow", 1);
+        R = radix_partition(ex, right, rk, bits);
+      }
+      trace::add_counter("join.radix.slot_sides", (L.slot ? 1 : 0) + (R.slot ? 1 : 0));
+    }
   }
   RadixSide &B = build_left ? L : R;
   RadixSide &P = build_left ? R : L;
@@ -421,7 +459,8 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     auto count = [&](int64_t st) {
       counts = ex.empty_i64((nparts + st - 1) / st);
       hip::radix_join_count(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
-                            nparts, cap, ptr<int64_t>(counts), overflow.data_ptr<int>(), ex.stream, st, oj);
+                            nparts, cap, ptr<int64_t>(counts), overflow.data_ptr<int>(), ex.stream, st, oj, P.slot,
+                            B.slot);
     };
     count(stride);
     // the ranking guard of the stable (second and later) partition passes
@@ -514,7 +553,7 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
                           nparts, cap, offs, pc.in.data(), pc.out.data(), pc.w.data(), (int)pc.in.size(),
                           bc.in.data(), bc.out.data(), bc.w.data(), (int)bc.in.size(), ex.stream, cursor, rows,
                           overflow.data_ptr<int>(), pkey, oj, ppres.defined() ? ppres.data_ptr<uint8_t>() : nullptr,
-                          bpres.defined() ? bpres.data_ptr<uint8_t>() : nullptr);
+                          bpres.defined() ? bpres.data_ptr<uint8_t>() : nullptr, P.slot, B.slot);
   };
   if (stride == 1) {
     allocate(m);

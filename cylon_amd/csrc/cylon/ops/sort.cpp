@@ -203,6 +203,11 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
       sh += db;
     }
     at::Tensor ws;
+    // each pass but the last writes the next pass's digits (2 B/row) as it stores the keys: the
+    // next pass's tile histogram then reads those instead of the 8-byte keys (XCD-tile passes)
+    const char *nde = std::getenv("CYLON_SORT_NEXT_DIGITS");  // A/B knob: 0 = histograms read the keys
+    const bool nd_on = hip::radix_xt_enabled() && npass > 1 && !(nde && nde[0] == '0');
+    at::Tensor nd = nd_on ? at::empty({n}, ex.opts(at::kShort)) : at::Tensor();
     int shift = lo;
     for (int ps = 0; ps < npass; ++ps) {
       const int db = dbits[ps];
@@ -223,9 +228,12 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
       const uint64_t flip = ps == 0 && raw_in ? key_xor : 0ull;
       const bool pre = prehist && ps == 0 && shift == 0 && db <= 10;
       if (pre) hip::radix_sort_prehist_fold(ptr<int64_t>(pre_ws), n, db, ptr<int64_t>(ws), ex.stream);
+      uint16_t *ndp = nd_on ? reinterpret_cast<uint16_t *>(nd.data_ptr()) : nullptr;
       hip::radix_sort_rows_pass(ptr<int64_t>(cur[0]), n, shift, db, in.data(), out.data(), widths.data(),
                                 (int)cur.size(), ptr<int64_t>(ws), ex.stream,
-                                flip ^ (ps + 1 == npass && key_in_last_pass ? key_xor : 0ull), flip, pre);
+                                flip ^ (ps + 1 == npass && key_in_last_pass ? key_xor : 0ull), flip, pre,
+                                ps > 0 ? ndp : nullptr, ps + 1 < npass ? ndp : nullptr, shift + db,
+                                ps + 1 < npass ? dbits[ps + 1] : 0);
       if (ps == 0) pre_ws = at::Tensor();  // 10-bit tile histogram consumed
       cur = std::move(nxt);
       shift += db;

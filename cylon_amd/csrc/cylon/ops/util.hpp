@@ -70,6 +70,16 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
                                        int bits, at::Tensor *offs, const RangeSpec *range = nullptr,
                                        std::vector<int> *keep_packed = nullptr, bool stable = true);
 
+// Hash-join partition in slot mode (MSD, two passes, no histogram before the second pass; see
+// kernel_decls.inc radix_slot_rows_pass): partition p holds (*counts)[p] rows at row p * slot.
+// Returns an empty vector (nothing launched) when the shape is not eligible; *overflow (int32
+// device flag) is set when a partition did not fit its slot -- the result is then unusable and
+// the caller partitions exactly instead.  keep_packed as for RadixPartition.
+std::vector<at::Tensor> RadixPartitionSlotted(const Exec &ex, std::vector<at::Tensor> cols,
+                                              const std::vector<int> &widths, int bits, int64_t slot,
+                                              at::Tensor *counts, at::Tensor *overflow,
+                                              std::vector<int> *keep_packed = nullptr);
+
 // Row-moving passes (k_rows_pass) take their all-8-byte path only when every moved
 // column is 8 bytes wide; validity bytes beside 8-byte columns therefore travel packed
 // 8 per 8-byte word (bitmap.hip pack_byte_columns).  PackByteColumns rewrites

@@ -384,6 +384,7 @@ def test_radix_join_ranking_guard_falls_back(gpu_ctx, monkeypatch, count_mode):
     L, R = Table(a, gpu_ctx), Table(b, gpu_ctx)
     on = dict(left_on=["k"], right_on=["k"], left_prefix="l_", right_prefix="r_")
     monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", "1024")
+    monkeypatch.setenv("CYLON_RJ_SLOT", "0")  # the guard watches the exact LSD passes (slot mode has no stable pass)
     if count_mode == "fused":
         monkeypatch.setenv("CYLON_RJ_FUSED_MIN_PARTS", "64")
     else:

@@ -148,6 +148,39 @@ def test_radix_join_hot_key_sample_is_counted_exactly(gpu_ctx, monkeypatch):
         assert c["join.radix.estimated_rows"] < 3 * exp, c
 
 
+# ---- slot-mode partitions (radix_slot_rows_pass): MSD second pass into fixed-size partition slots
+@pytest.mark.parametrize("how", ["inner", "left", "outer"])
+def test_radix_join_slot_partitions_match_cpu(gpu_ctx, ctx, monkeypatch, how):
+    """CYLON_RJ_EXTRA_BITS=4 gives 2^12+ partitions at 1M rows, so both sides take the two-pass
+    slot mode (high digit with exact offsets, then the low digit into slots without a histogram);
+    nullable payloads travel as packed validity words through the slots."""
+    monkeypatch.setenv("CYLON_RJ_EXTRA_BITS", "4")
+    rng = np.random.default_rng(31)
+    nl, nr = 1_000_000, 1_200_000
+    a = pa.table({"k": rng.integers(0, 1_500_000, nl), "v": rng.random(nl),
+                  "i": pa.array(rng.integers(-9, 9, nl), mask=rng.random(nl) < 0.1)})
+    b = pa.table({"k": rng.integers(0, 1_500_000, nr), "w": rng.random(nr)})
+    got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["k"], monkeypatch)
+    assert c.get("join.radix.slot_sides", 0) == 2 and c.get("join.radix.slot_overflow", 0) == 0, c
+    assert c["join.radix.rows_out"] == len(exp)
+    pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
+
+
+def test_radix_join_slot_overflow_repartitions_exactly(gpu_ctx, ctx, monkeypatch):
+    """A hot probe key fills one partition far beyond its slot: that side is partitioned again
+    with exact offsets (join.radix.slot_overflow) and the result is unchanged."""
+    monkeypatch.setenv("CYLON_RJ_EXTRA_BITS", "4")
+    rng = np.random.default_rng(32)
+    nl, nr = 800_000, 1_000_000
+    kr = rng.integers(0, 1_000_000, nr)
+    kr[: 20_000] = 4242  # one partition receives 20k extra probe rows (slot ~ 400)
+    a = pa.table({"k": rng.integers(0, 1_000_000, nl), "v": rng.random(nl)})
+    b = pa.table({"k": kr, "w": rng.random(nr)})
+    got, exp, c = _join(gpu_ctx, ctx, a, b, "inner", ["k"], monkeypatch)
+    assert c.get("join.radix.slot_overflow", 0) >= 1, c
+    pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
+
+
 # ---- LDS radix group-by (kernels/radix_groupby.hip) beyond one integer key + SUM/COUNT/MIN/MAX/MEAN
 def _groupby_both(T, keys, aggs, monkeypatch):
     res, counters = [], []
