@@ -196,18 +196,30 @@ struct TileSched {
   const uint32_t *xt_off;        // [tile][nbuckets] output row of the tile's first row of each bucket
   unsigned int *xt_ticket;       // [8] next tile of each XCD's contiguous chunk
   int64_t xt_tiles;              // tiles of the pass
-  // slot mode (the MSD second pass of a join partition, k_rows_pass<..., SLOT>): the input is the
-  // first pass's bucket-major output; a tile never straddles an input bucket, and input bucket b's
-  // rows go to output slots b * nbuckets + d of sl_slot rows each (claimed with one atomic per
-  // (tile, digit) -- no histogram pass); a run that does not fit goes to the trash rows after the
-  // last slot and raises sl_overflow (the caller repartitions exactly)
-  const uint32_t *sl_tpre = nullptr;   // [nb1 + 1] first tile of each input bucket (exclusive scan)
-  const uint32_t *sl_bbase = nullptr;  // [nb1] first input row of each input bucket
-  unsigned int *sl_cursor = nullptr;   // [nb1 * nbuckets] rows claimed in each output slot
+  // slot mode (k_rows_pass<..., SLOT>, the histogram-free passes of a join partition): the input
+  // is a list of row segments [ss[g], se[g]); a tile never straddles a segment, and digit d of
+  // segment g goes to output slot (g >> sl_gshift) * nbuckets * sl_B + d * sl_B + (g & sl_gmask)
+  // of sl_slot rows (claimed with one atomic per (tile, digit)); a run that does not fit goes to
+  // the trash rows after the last slot and raises sl_overflow (the caller repartitions exactly).
+  // XCD x (blockIdx % 8) owns segments [x S / 8, (x + 1) S / 8).
+  //   first pass over a table: S = 8 chunks of n / 8 rows, slot = d * 8 + g (one slot per
+  //     (bucket, XCD): every slot is filled from ONE XCD's L2);
+  //   second pass: S = 8 * nb1 slots of that pass (or nb1 exact buckets), slot = (g >> 3) * nb + d.
+  const uint32_t *sl_tpre = nullptr;  // [S + 1] first tile of each segment (exclusive scan)
+  const uint32_t *sl_ss = nullptr;    // [S] first row of each segment
+  const uint32_t *sl_se = nullptr;    // [S] end row of each segment
+  unsigned int *sl_cursor = nullptr;  // [nslots] rows claimed in each output slot
   unsigned int *sl_overflow = nullptr;
-  int64_t sl_slot = 0;                 // rows per output slot
-  int sl_nb1 = 0;                      // input buckets (<= 1023)
+  int64_t sl_slot = 0;                // rows per output slot
+  int64_t sl_nslots = 0;              // output slots (the trash rows start at sl_nslots * sl_slot)
+  int sl_nseg = 0;                    // S <= kSlotMaxSeg
+  int sl_gshift = 0, sl_gmask = 0, sl_B = 1;
+  // debug instance (CYLON_SLOT_DEBUG=1): rows of the input / output arrays; an access outside them is
+  // skipped, counted in sl_dbg[0] and printed (first few)
+  int64_t sl_in_rows = 0, sl_out_rows = 0;
+  unsigned int *sl_dbg = nullptr;
 };
+constexpr int kSlotMaxSeg = 4096;
 
 // XCD-tile mode.  Histogram mode gives each block a contiguous chunk of rows, so the tiles of
 // one block write a bucket's consecutive runs ~34 us apart and the partial 128-B line at every
@@ -225,7 +237,7 @@ __device__ __forceinline__ int xcc_id() {
   return x & (kXcds - 1);
 }
 // slot mode: input bucket of tile t (tp: LDS copy of sl_tpre; the last bucket whose first tile <= t)
-__device__ __forceinline__ int sl_bucket(const uint32_t *tp, int nb1, int64_t t) {
+__device__ __forceinline__ int sl_segment(const uint32_t *tp, int nb1, int64_t t) {
   int lo = 0, hi = nb1 - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -404,7 +416,8 @@ constexpr int kRPStampTiles = 64, kRPStampSlots = 16;
 // order -- tools/lds_atomic_order.hip measures that on the device).
 // XT: XCD-tile schedule (tiles claimed in order per XCD, exact per-tile bucket offsets in lb).
 // SLOT: slot mode (TileSched): tiles of one input bucket each, per-(tile, digit) slot claims.
-template <class Digit, bool W8, int THREADS, int RANK, bool XT = false, bool SLOT = false>
+// SDBG: bounds-checked slot instance (tools / CYLON_SLOT_DEBUG=1).
+template <class Digit, bool W8, int THREADS, int RANK, bool XT = false, bool SLOT = false, bool SDBG = false>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_rows_pass(
     Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
     const int64_t *__restrict__ bh_scan, TileSched lb, unsigned long long *__restrict__ stamps) {
@@ -434,50 +447,56 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   __shared__ int s_tb[2];
   int par = 0;
   bool order_bad = false;
-  // SLOT: the input buckets' first tiles (upper half of running[]: digits <= 512) and first rows
-  // (sbb) in LDS; tiles are dealt statically -- XCD x (= blockIdx % 8, the dispatcher's round
-  // robin) owns the tiles of input buckets [x nb1 / 8, (x + 1) nb1 / 8), its j-th block takes
-  // every nblk-th of them -- so taking the next tile is a few LDS reads (no atomic, no global load
-  // on the barrier path), and an XCD's CUs still work on adjacent tiles of the same buckets.
-  uint32_t *tp = reinterpret_cast<uint32_t *>(running + kRPMaxBuckets / 2);
-  __shared__ uint32_t sbb[SLOT ? kRPMaxBuckets : 1];
+  // SLOT: the segments' first tiles / first rows / end rows in LDS; tiles are dealt statically --
+  // XCD x (= blockIdx % 8, the dispatcher's round robin) owns the tiles of its segments, its j-th
+  // block takes every nblk-th of them -- so taking the next tile is a few LDS reads (no atomic, no
+  // global load on the barrier path), and an XCD's CUs work on adjacent tiles of the same segment.
+  __shared__ uint32_t tp[SLOT ? kSlotMaxSeg : 1], sss[SLOT ? kSlotMaxSeg : 1], sse[SLOT ? kSlotMaxSeg : 1];
   __shared__ int64_t s_tix, s_thi;  // SLOT (thread 0): this block's next tile index, its XCD's end
-  auto sl_take = [&](int slot) {    // thread 0: take the next tile, resolve its rows and bucket
+  auto sl_take = [&](int slot) {    // thread 0: take the next tile, resolve its rows and slot base
     const int64_t t = s_tix;
-    if (t >= s_thi) {
-      s_next = n;
-      s_tend[slot] = n;
+    if (t >= s_thi) {  // none left (slot-mode inputs may have rows beyond n: a sentinel, not n; row
+                       // arithmetic on it must not overflow)
+      s_next = INT64_MAX / 4;
+      s_tend[slot] = 0;
       s_tb[slot] = 0;
       return;
     }
     s_tix = t + ((int64_t)gridDim.x - (blockIdx.x & (kXcds - 1)) + kXcds - 1) / kXcds;
-    const int bk = sl_bucket(tp, lb.sl_nb1, t);
-    const int64_t bend = bk + 1 < lb.sl_nb1 ? (int64_t)sbb[bk + 1] : n;
-    const int64_t r0 = (int64_t)sbb[bk] + (t - (int64_t)tp[bk]) * TILE;
+    const int g = sl_segment(tp, lb.sl_nseg, t);
+    const int64_t gend = (int64_t)sse[g];
+    const int64_t r0 = (int64_t)sss[g] + (t - (int64_t)tp[g]) * TILE;
     s_next = r0;
-    s_tend[slot] = r0 + TILE < bend ? r0 + TILE : bend;
-    s_tb[slot] = bk;
+    s_tend[slot] = r0 + TILE < gend ? r0 + TILE : gend;
+    if (SDBG && (r0 < 0 || s_tend[slot] > lb.sl_in_rows || g < 0 || g >= lb.sl_nseg)) {
+      if (atomicAdd(lb.sl_dbg, 1u) < 8u)
+        printf("slot dbg: block %d tile %lld seg %d rows [%lld, %lld) in_rows %lld\n", (int)blockIdx.x, (long long)t, g,
+               (long long)r0, (long long)s_tend[slot], (long long)lb.sl_in_rows);
+      s_tend[slot] = r0;  // empty tile
+    }
+    // digit d of this tile goes to slot s_tb + d * sl_B
+    s_tb[slot] = (g >> lb.sl_gshift) * (int)nbuckets * lb.sl_B + (g & lb.sl_gmask);
   };
 
   const int64_t b = blockIdx.x;
   int64_t begin, end;
   if (SLOT) {
-    for (int i = threadIdx.x; i < lb.sl_nb1; i += THREADS) {
+    for (int i = threadIdx.x; i < lb.sl_nseg; i += THREADS) {
       tp[i] = lb.sl_tpre[i];
-      sbb[i] = lb.sl_bbase[i];
+      sss[i] = lb.sl_ss[i];
+      sse[i] = lb.sl_se[i];
     }
     if (threadIdx.x == 0) {
       const int x = blockIdx.x & (kXcds - 1);
-      const int b0 = lb.sl_nb1 * x / kXcds, b1 = lb.sl_nb1 * (x + 1) / kXcds;
-      const uint32_t ttot = lb.sl_tpre[lb.sl_nb1];
-      s_tix = (int64_t)(b0 < lb.sl_nb1 ? lb.sl_tpre[b0] : ttot) + blockIdx.x / kXcds;
-      s_thi = b1 < lb.sl_nb1 ? lb.sl_tpre[b1] : ttot;
+      const int g0 = lb.sl_nseg * x / kXcds, g1 = lb.sl_nseg * (x + 1) / kXcds;
+      s_tix = (int64_t)lb.sl_tpre[g0] + blockIdx.x / kXcds;
+      s_thi = lb.sl_tpre[g1];
     }
     __syncthreads();
     if (threadIdx.x == 0) sl_take(0);
     __syncthreads();
     begin = s_next;
-    end = n;
+    end = INT64_MAX / 4;  // the loop runs until sl_take reports no tile
   } else if (TICKET) {
     if (threadIdx.x == 0) s_next = xt_claim(lb, xhome, TILE, n);
     __syncthreads();
@@ -560,7 +579,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     uint32_t sl_c = 0, sl_base = 0;
     if (SLOT && threadIdx.x < nbuckets) {
       sl_c = STABLE ? 0u : bcnt[threadIdx.x];
-      if (sl_c) sl_base = atomicAdd(&lb.sl_cursor[(int64_t)s_tb[par] * nbuckets + threadIdx.x], sl_c);
+      if (SDBG && sl_c && ((int64_t)s_tb[par] + (int64_t)threadIdx.x * lb.sl_B >= lb.sl_nslots || s_tb[par] < 0)) {
+        if (atomicAdd(lb.sl_dbg, 1u) < 8u)
+          printf("slot dbg: block %d cursor index %lld of %lld\n", (int)blockIdx.x,
+                 (long long)((int64_t)s_tb[par] + (int64_t)threadIdx.x * lb.sl_B), (long long)lb.sl_nslots);
+        sl_c = 0;
+      }
+      if (sl_c) sl_base = atomicAdd(&lb.sl_cursor[(int64_t)s_tb[par] + (int64_t)threadIdx.x * lb.sl_B], sl_c);
     }
     {  // thread owns buckets [t*BPT, t*BPT+BPT): exclusive prefix over waves (in place), then a
        // block scan of the thread totals
@@ -607,8 +632,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     if (SLOT && threadIdx.x < nbuckets) {
       const bool fits = (int64_t)sl_base + sl_c <= lb.sl_slot;
       if (sl_c && !fits) atomicOr(lb.sl_overflow, 1u);
-      running[threadIdx.x] = fits ? ((int64_t)s_tb[par] * nbuckets + threadIdx.x) * lb.sl_slot + sl_base
-                                  : (int64_t)lb.sl_nb1 * nbuckets * lb.sl_slot;  // the trash rows
+      running[threadIdx.x] = fits ? ((int64_t)s_tb[par] + (int64_t)threadIdx.x * lb.sl_B) * lb.sl_slot + sl_base
+                                  : lb.sl_nslots * lb.sl_slot;  // the trash rows
     }
     __syncthreads();
     RP_STAMP(4);
@@ -619,6 +644,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       if (j < cnt) {
         const uint32_t e = sdig[j], p = e >> 16;
         dst[q] = running[p] + (j - (int64_t)toff[p]);
+        if (SDBG && (dst[q] < 0 || dst[q] >= lb.sl_out_rows || p >= nbuckets)) {
+          if (atomicAdd(lb.sl_dbg, 1u) < 8u)
+            printf("slot dbg: block %d tile %lld slot j %d digit %u dst %lld out_rows %lld cnt %d\n", (int)blockIdx.x,
+                   (long long)tile, j, p, (long long)dst[q], (long long)lb.sl_out_rows, cnt);
+          dst[q] = lb.sl_nslots * lb.sl_slot;  // the trash rows
+        }
         if (cols.check_order && j > 0) {  // same bucket as the previous slot: input order kept?
           const uint32_t f = sdig[j - 1];
           order_bad |= (f >> 16) == p && f > e;
@@ -1315,20 +1346,52 @@ void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_b
                    nd_out ? (1u << nd_bits) - 1u : 0u);
 }
 
-// ---- slot mode (the MSD second pass of a join partition; TileSched)
-// tpre[b] = first tile of input bucket b (exclusive scan of its tile count), tpre[nb1] = all tiles
-__global__ __launch_bounds__(kRPThreads) void k_sl_tiles(const uint32_t *__restrict__ bbase, int nb1, int64_t n,
-                                                         uint32_t *__restrict__ tpre) {
+// ---- slot mode (the histogram-free passes of a join partition; TileSched)
+// Segment list of a slot pass and the tile prefix over it (one block; S <= kSlotMaxSeg):
+//   src 0: the table itself, 8 chunks [n g / 8, n (g + 1) / 8)
+//   src 1: the exact buckets of an XT pass (bucket bases in its workspace: bbase)
+//   src 2: the slots of a previous slot pass (slot g at g * pslot, pcnt[g] rows)
+// (SRC is a template parameter: with a runtime source the compiler merged the bbase / pcnt branches
+// and loaded through the null pointer of the unused one -- the fault of gpurun_out/r04j)
+template <int SRC>
+__global__ __launch_bounds__(kRPThreads) void k_sl_segments(int S, int64_t n, const uint32_t *__restrict__ bbase,
+                                                            const int64_t *__restrict__ pcnt, int64_t pslot,
+                                                            uint32_t *__restrict__ ss, uint32_t *__restrict__ se,
+                                                            uint32_t *__restrict__ tpre) {
   __shared__ uint32_t wsum[kRPWaves];
-  const int b = threadIdx.x;
-  uint32_t t = 0;
-  if (b < nb1) {
-    const int64_t e = b + 1 < nb1 ? (int64_t)bbase[b + 1] : n;
-    t = (uint32_t)((e - (int64_t)bbase[b] + kRPTile - 1) / kRPTile);
+  constexpr int PER = kSlotMaxSeg / kRPThreads;
+  uint32_t tiles[PER];
+  uint32_t tot = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int g = threadIdx.x * PER + i;
+    tiles[i] = 0;
+    if (g < S) {
+      int64_t a, e;
+      if constexpr (SRC == 0) {
+        a = n * g / S;
+        e = n * (g + 1) / S;
+      } else if constexpr (SRC == 1) {
+        a = bbase[g];
+        e = g + 1 < S ? (int64_t)bbase[g + 1] : n;
+      } else {
+        a = (int64_t)g * pslot;
+        e = a + (pcnt[g] < pslot ? pcnt[g] : pslot);
+      }
+      ss[g] = (uint32_t)a;
+      se[g] = (uint32_t)e;
+      tiles[i] = (uint32_t)((e - a + kRPTile - 1) / kRPTile);
+    }
+    tot += tiles[i];
   }
-  const uint32_t ex = rp_block_exscan<kRPWaves>(t, wsum);
-  if (b < nb1) tpre[b] = ex;
-  if (b == nb1 - 1) tpre[nb1] = ex + t;
+  uint32_t ex = rp_block_exscan<kRPWaves>(tot, wsum);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int g = threadIdx.x * PER + i;
+    if (g < S) tpre[g] = ex;
+    ex += tiles[i];
+  }
+  if (threadIdx.x == kRPThreads - 1) tpre[S] = ex;
 }
 
 // rows in each slot (a slot that overflowed reports its capacity; the caller discards the result)
@@ -1339,49 +1402,109 @@ __global__ void k_sl_counts(const unsigned int *__restrict__ cursor, int64_t nsl
     counts[i] = (int64_t)cursor[i] < slot ? (int64_t)cursor[i] : slot;
 }
 
-bool radix_slot_eligible(int64_t n, int ncols, int first_bits, int second_bits) {
-  return rp_xt() && n > 0 && n < (int64_t(1) << 32) && rp_threads(ncols, true) == 1024 && first_bits >= 1 &&
-         first_bits <= kRJMaxDigitBits && second_bits >= 1 && (1 << second_bits) <= kRPMaxBuckets / 2;
-}
-
 int64_t radix_slot_tile_rows() { return kRPTile; }
 
-int64_t radix_slot_workspace(int first_bits, int second_bits) {  // int64 words
-  const int64_t u32 = ((int64_t(1) << first_bits) + 1) + kXcds + 1 + (int64_t(1) << (first_bits + second_bits));
+bool radix_slot_eligible(int64_t n, int ncols, int first_bits, int second_bits) {
+  return rp_xt() && n > 0 && rp_threads(ncols, true) == 1024 && first_bits >= 1 && first_bits <= kRJMaxDigitBits &&
+         second_bits >= 1 && second_bits <= kRJMaxDigitBits && (int64_t(kXcds) << first_bits) * 2 < (int64_t(1) << 32) &&
+         n < (int64_t(1) << 31);
+}
+
+bool radix_slot_first_pass_ok(int first_bits) { return (kXcds << first_bits) <= kSlotMaxSeg; }
+
+int64_t radix_slot_workspace(int first_bits, int second_bits) {  // int64 words: segments + cursors
+  const int64_t segs = std::max<int64_t>(kXcds << first_bits, int64_t(1) << first_bits);
+  const int64_t u32 = 3 * (segs + 1) + (int64_t(kXcds) << first_bits) + (int64_t(1) << (first_bits + second_bits));
   return (u32 + 1) / 2;
 }
 
-void radix_slot_rows_pass(const int64_t *keys, int64_t n, int total_bits, int first_bits, int second_bits,
-                          const uint8_t *const *in, uint8_t *const *out, const int *widths, int ncols,
-                          const int64_t *first_ws, int64_t slot, int64_t *ws, int64_t *counts, unsigned int *overflow,
-                          void *stream) {
-  CYLON_CHECK(radix_slot_eligible(n, ncols, first_bits, second_bits), Code::Invalid, "slot pass not eligible");
-  CYLON_CHECK(in[0] == reinterpret_cast<const uint8_t *>(keys) && widths[0] == 8, Code::Invalid,
+static void slot_pass(const PartDigit &dg, int64_t n, int digit_bits, const uint8_t *const *in, uint8_t *const *out,
+                      const int *widths, int ncols, int src, int S, const uint32_t *bbase, const int64_t *pcnt,
+                      int64_t pslot, int gshift, int gmask, int B, int64_t nslots, int64_t slot, int64_t *ws,
+                      int64_t *counts, unsigned int *overflow, hipStream_t s, int64_t in_rows) {
+  CYLON_CHECK(S >= 1 && S <= kSlotMaxSeg && ncols >= 1 && ncols <= kMaxFusedCols && slot > 0, Code::Invalid,
+              "slot pass arguments");
+  CYLON_CHECK(in[0] == reinterpret_cast<const uint8_t *>(dg.keys) && widths[0] == 8, Code::Invalid,
               "slot pass: column 0 must be the key");
-  CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols && slot > 0, Code::Invalid, "slot pass arguments");
-  hipStream_t s = as_stream(stream);
-  const int nb1 = 1 << first_bits;
-  const uint32_t nb = 1u << second_bits;
-  const int64_t nslots = int64_t(nb1) * nb;
-  // the first pass (XT, radix_rows_pass) left its bucket bases in its workspace
-  const uint32_t *bbase = reinterpret_cast<const uint32_t *>(first_ws + xt_layout(n, (uint32_t)nb1).bbase);
+  CYLON_CHECK(nslots * slot + kRPTile < (int64_t(1) << 32), Code::Invalid, "slot pass: output rows beyond 2^32");
+  const uint32_t nb = 1u << digit_bits;
   uint32_t *w32 = reinterpret_cast<uint32_t *>(ws);
-  uint32_t *tpre = w32;
-  unsigned int *cursor = w32 + nb1 + 1 + kXcds + 1;
+  uint32_t *ss = w32, *se = ss + S, *tpre = se + S;
+  unsigned int *cursor = tpre + S + 1;
+  static const bool dbg = [] {
+    const char *e = std::getenv("CYLON_SLOT_DEBUG");
+    return e && e[0] == '1';
+  }();
+  auto dsync = [&](const char *what) {  // debug: every step synchronised and checked on its own
+    if (!dbg) return;
+    const hipError_t e1 = hipStreamSynchronize(s), e2 = hipGetLastError();
+    std::fprintf(stderr, "slot dbg: src %d after %s: %s / %s\n", src, what, hipGetErrorString(e1), hipGetErrorString(e2));
+  };
+  if (dbg) {
+    std::fprintf(stderr, "slot dbg: src %d S %d n %lld nslots %lld slot %lld pslot %lld ws %p cursor %p bbase %p pcnt %p "
+                 "in_rows %lld ncols %d\n", src, S, (long long)n, (long long)nslots, (long long)slot, (long long)pslot,
+                 (void *)ws, (void *)cursor, (const void *)bbase, (const void *)pcnt, (long long)in_rows, ncols);
+    if (src == 2) {
+      dsync("entry");
+      std::vector<int64_t> hc(S);
+      HIP_CHECK(hipMemcpy(hc.data(), pcnt, sizeof(int64_t) * S, hipMemcpyDeviceToHost));
+      int64_t mn = INT64_MAX, mx = INT64_MIN, sum = 0;
+      for (int64_t v : hc) {
+        mn = std::min(mn, v);
+        mx = std::max(mx, v);
+        sum += v;
+      }
+      std::fprintf(stderr, "slot dbg: previous counts min %lld max %lld sum %lld\n", (long long)mn, (long long)mx,
+                   (long long)sum);
+    }
+  }
   HIP_CHECK(hipMemsetAsync(cursor, 0, sizeof(uint32_t) * nslots, s));
-  hipLaunchKernelGGL(k_sl_tiles, dim3(1), dim3(kRPThreads), 0, s, bbase, nb1, n, tpre);
+  dsync("cursor memset");
+  CYLON_CHECK((src == 0) || (src == 1 && bbase) || (src == 2 && pcnt), Code::Invalid, "slot pass source " << src);
+  if (src == 0)
+    hipLaunchKernelGGL(k_sl_segments<0>, dim3(1), dim3(kRPThreads), 0, s, S, n, bbase, pcnt, pslot, ss, se, tpre);
+  else if (src == 1)
+    hipLaunchKernelGGL(k_sl_segments<1>, dim3(1), dim3(kRPThreads), 0, s, S, n, bbase, pcnt, pslot, ss, se, tpre);
+  else
+    hipLaunchKernelGGL(k_sl_segments<2>, dim3(1), dim3(kRPThreads), 0, s, S, n, bbase, pcnt, pslot, ss, se, tpre);
+  dsync("k_sl_segments");
   HIP_LAUNCH_CHECK();
   TileSched lb{};
   lb.sl_tpre = tpre;
-  lb.sl_bbase = bbase;
+  lb.sl_ss = ss;
+  lb.sl_se = se;
   lb.sl_cursor = cursor;
   lb.sl_overflow = overflow;
   lb.sl_slot = slot;
-  lb.sl_nb1 = nb1;
+  lb.sl_nslots = nslots;
+  lb.sl_nseg = S;
+  lb.sl_gshift = gshift;
+  lb.sl_gmask = gmask;
+  lb.sl_B = B;
+  lb.sl_in_rows = in_rows;
+  lb.sl_out_rows = nslots * slot + kRPTile;
+  static unsigned int *dbg_count = nullptr;
+  if (dbg) {
+    if (!dbg_count) HIP_CHECK(hipMalloc(&dbg_count, sizeof(unsigned int)));
+    HIP_CHECK(hipMemsetAsync(dbg_count, 0, sizeof(unsigned int), s));
+    lb.sl_dbg = dbg_count;
+    // host check of the segment table
+    HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<uint32_t> h(3 * S + 1);
+    HIP_CHECK(hipMemcpy(h.data(), ss, sizeof(uint32_t) * (3 * S + 1), hipMemcpyDeviceToHost));
+    int64_t bad = 0, rows = 0;
+    for (int g = 0; g < S; ++g) {
+      const int64_t a = h[g], e = h[S + g], t0 = h[2 * S + g], t1 = h[2 * S + g + 1];
+      rows += e - a;
+      if (a > e || e > in_rows || t1 - t0 != (e - a + kRPTile - 1) / kRPTile) ++bad;
+    }
+    std::fprintf(stderr, "slot dbg: pass src %d S %d n %lld rows in segments %lld in_rows %lld tiles %u bad %lld grid?\n", src,
+                 S, (long long)n, (long long)rows, (long long)in_rows, h[3 * S], (long long)bad);
+  }
   ColSet cs;
   cs.n = ncols;
   cs.key_xor = 0;
-  cs.check_order = 0;  // MSD: the order inside a slot is free
+  cs.check_order = 0;  // the order inside a slot is free
   cs.order_bad = order_flag();
   cs.nd_out = nullptr;
   cs.nd_shift = 0;
@@ -1393,21 +1516,62 @@ void radix_slot_rows_pass(const int64_t *keys, int64_t n, int total_bits, int fi
     cs.width[c] = c < ncols ? widths[c] : 8;
     if (c < ncols) {
       w8 &= widths[c] == 8;
-      CYLON_CHECK(in[c] != nullptr, Code::Invalid, "slot pass: every column is read (row ids come from pass 1)");
+      CYLON_CHECK(in[c] != nullptr, Code::Invalid, "slot pass: every column is read");
     }
   }
-  const PartDigit dg{keys, total_bits, 0, nb - 1};
-  // every XCD needs at least one block: its input buckets' tiles are dealt to its own blocks only
-  const int64_t nblocks = std::max<int64_t>(kXcds, std::min<int64_t>((n + kRPTile - 1) / kRPTile + nb1, kNumCUs));
-  if (w8)
+  // every XCD needs at least one block: its segments' tiles are dealt to its own blocks only
+  const int64_t nblocks = std::max<int64_t>(kXcds, std::min<int64_t>((n + kRPTile - 1) / kRPTile + S, kNumCUs));
+  if (dbg && w8)
+    hipLaunchKernelGGL((k_rows_pass<PartDigit, true, 1024, kRankBlockAtomic, false, true, true>),
+                       dim3((unsigned)nblocks), dim3(1024), 0, s, dg, digit_bits, nb, cs, n, (int64_t)kRPTile, nblocks,
+                       nullptr, lb, nullptr);
+  else if (w8)
     hipLaunchKernelGGL((k_rows_pass<PartDigit, true, 1024, kRankBlockAtomic, false, true>), dim3((unsigned)nblocks),
-                       dim3(1024), 0, s, dg, second_bits, nb, cs, n, (int64_t)kRPTile, nblocks, nullptr, lb, nullptr);
+                       dim3(1024), 0, s, dg, digit_bits, nb, cs, n, (int64_t)kRPTile, nblocks, nullptr, lb, nullptr);
   else
     hipLaunchKernelGGL((k_rows_pass<PartDigit, false, 1024, kRankBlockAtomic, false, true>), dim3((unsigned)nblocks),
-                       dim3(1024), 0, s, dg, second_bits, nb, cs, n, (int64_t)kRPTile, nblocks, nullptr, lb, nullptr);
+                       dim3(1024), 0, s, dg, digit_bits, nb, cs, n, (int64_t)kRPTile, nblocks, nullptr, lb, nullptr);
   HIP_LAUNCH_CHECK();
+  if (dbg) {
+    unsigned int h = 0;
+    HIP_CHECK(hipMemcpyAsync(&h, dbg_count, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    std::fprintf(stderr, "slot dbg: pass src %d done, %u bad accesses, grid %lld\n", src, h, (long long)nblocks);
+  }
   hipLaunchKernelGGL(k_sl_counts, dim3(grid_for(nslots)), dim3(kBlock), 0, s, cursor, nslots, slot, counts);
+  dsync("k_sl_counts");
   HIP_LAUNCH_CHECK();
+}
+
+void radix_slot_first_pass(const int64_t *keys, int64_t n, int total_bits, int first_bits, int second_bits,
+                           const uint8_t *const *in, uint8_t *const *out, const int *widths, int ncols, int64_t slot,
+                           int64_t *ws, int64_t *counts, unsigned int *overflow, void *stream) {
+  CYLON_CHECK(radix_slot_eligible(n, ncols, first_bits, second_bits) && radix_slot_first_pass_ok(first_bits),
+              Code::Invalid, "slot first pass not eligible");
+  const int nb1 = 1 << first_bits;
+  // the high digit; slot d * 8 + x holds bucket d's rows from XCD x's chunk of the table
+  slot_pass(PartDigit{keys, total_bits, second_bits, (uint32_t)nb1 - 1}, n, first_bits, in, out, widths, ncols, 0,
+            kXcds, nullptr, nullptr, 0, 3, kXcds - 1, kXcds, int64_t(kXcds) * nb1, slot, ws, counts, overflow,
+            as_stream(stream), n);
+}
+
+void radix_slot_rows_pass(const int64_t *keys, int64_t n, int total_bits, int first_bits, int second_bits,
+                          const uint8_t *const *in, uint8_t *const *out, const int *widths, int ncols,
+                          const int64_t *first_ws, const int64_t *first_counts, int64_t first_slot, int64_t slot,
+                          int64_t *ws, int64_t *counts, unsigned int *overflow, void *stream) {
+  CYLON_CHECK(radix_slot_eligible(n, ncols, first_bits, second_bits), Code::Invalid, "slot pass not eligible");
+  const int nb1 = 1 << first_bits;
+  const int64_t nslots = int64_t(nb1) << second_bits;
+  const PartDigit dg{keys, total_bits, 0, (1u << second_bits) - 1};
+  if (first_counts != nullptr) {  // after a slot first pass: segment g = slot g (bucket g >> 3)
+    slot_pass(dg, n, second_bits, in, out, widths, ncols, 2, kXcds * nb1, nullptr, first_counts, first_slot, 3, 0, 1,
+              nslots, slot, ws, counts, overflow, as_stream(stream), int64_t(kXcds) * nb1 * first_slot + kRPTile);
+  } else {  // after an XT first pass: segment g = exact bucket g (bases in its workspace)
+    CYLON_CHECK(nb1 <= kSlotMaxSeg, Code::Invalid, "slot pass: too many input buckets");
+    const uint32_t *bbase = reinterpret_cast<const uint32_t *>(first_ws + xt_layout(n, (uint32_t)nb1).bbase);
+    slot_pass(dg, n, second_bits, in, out, widths, ncols, 1, nb1, bbase, nullptr, 0, 0, 0, 1, nslots, slot, ws,
+              counts, overflow, as_stream(stream), n);
+  }
 }
 
 bool radix_xt_enabled() { return rp_xt(); }
