@@ -443,7 +443,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   __shared__ int64_t s_next;  // XT: first row of the next claimed tile
   // SLOT: end row / input bucket of the current ([par]) and the next ([par ^ 1]) tile, in LDS
   // rather than registers (the classic pass already runs at the 128-VGPR budget)
-  __shared__ int64_t s_tend[2];
+  __shared__ int64_t s_tend[2], s_tr0[2];
   __shared__ int s_tb[2];
   int par = 0;
   bool order_bad = false;
@@ -457,7 +457,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     const int64_t t = s_tix;
     if (t >= s_thi) {  // none left (slot-mode inputs may have rows beyond n: a sentinel, not n; row
                        // arithmetic on it must not overflow)
-      s_next = INT64_MAX / 4;
+      s_tr0[slot] = INT64_MAX / 4;
       s_tend[slot] = 0;
       s_tb[slot] = 0;
       return;
@@ -466,7 +466,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     const int g = sl_segment(tp, lb.sl_nseg, t);
     const int64_t gend = (int64_t)sse[g];
     const int64_t r0 = (int64_t)sss[g] + (t - (int64_t)tp[g]) * TILE;
-    s_next = r0;
+    s_tr0[slot] = r0;
     s_tend[slot] = r0 + TILE < gend ? r0 + TILE : gend;
     if (SDBG && (r0 < 0 || s_tend[slot] > lb.sl_in_rows || g < 0 || g >= lb.sl_nseg)) {
       if (atomicAdd(lb.sl_dbg, 1u) < 8u)
@@ -493,9 +493,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       s_thi = lb.sl_tpre[g1];
     }
     __syncthreads();
-    if (threadIdx.x == 0) sl_take(0);
+    if (threadIdx.x == 0) {  // the first two tiles; later claims run at the end of a tile, two ahead
+      sl_take(0);
+      sl_take(1);
+    }
     __syncthreads();
-    begin = s_next;
+    begin = s_tr0[0];
     end = INT64_MAX / 4;  // the loop runs until sl_take reports no tile
   } else if (TICKET) {
     if (threadIdx.x == 0) s_next = xt_claim(lb, xhome, TILE, n);
@@ -524,8 +527,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     const int tix = (int)((tile - begin) / TILE);
     RP_STAMP(0);
     const int cnt = SLOT ? (int)(s_tend[par] - tile) : (int)((end - tile) < TILE ? (end - tile) : TILE);
-    // SLOT: claim the next tile now, where few registers are live (read after this tile's barriers)
-    if (SLOT && threadIdx.x == 0) sl_take(par ^ 1);
     // XT: this tile's bucket offsets (consumed after the slot phase; the load overlaps the ranking)
     const uint32_t xoff = XT && threadIdx.x < nbuckets ? lb.xt_off[(tile / TILE) * nbuckets + threadIdx.x] : 0u;
     uint32_t pl[kRPItems];  // digit, then (in-wave rank << 16) | digit, then sorted slot; ~0 = inactive
@@ -637,18 +638,27 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     __syncthreads();
     RP_STAMP(4);
-    int64_t dst[kRPItems];  // destination of sorted slot j = threadIdx.x + q * THREADS
+    // destination of sorted slot j = threadIdx.x + q * THREADS.  SLOT: packed as digit << 16 | offset
+    // in its run and completed from running[] (LDS) at each store -- 8 VGPRs instead of 16 in the
+    // instance that also carries the slot bookkeeping (the trick of the lean kernel)
+    using DstT = typename std::conditional<SLOT, uint32_t, int64_t>::type;
+    DstT dst[kRPItems];
+#define RP_DEST(q) (SLOT ? running[(uint32_t)dst[q] >> 16] + (int64_t)((uint32_t)dst[q] & 0xffffu) : (int64_t)dst[q])
 #pragma unroll
     for (int q = 0; q < kRPItems; ++q) {
       const int j = threadIdx.x + q * THREADS;
       if (j < cnt) {
         const uint32_t e = sdig[j], p = e >> 16;
-        dst[q] = running[p] + (j - (int64_t)toff[p]);
-        if (SDBG && (dst[q] < 0 || dst[q] >= lb.sl_out_rows || p >= nbuckets)) {
-          if (atomicAdd(lb.sl_dbg, 1u) < 8u)
-            printf("slot dbg: block %d tile %lld slot j %d digit %u dst %lld out_rows %lld cnt %d\n", (int)blockIdx.x,
-                   (long long)tile, j, p, (long long)dst[q], (long long)lb.sl_out_rows, cnt);
-          dst[q] = lb.sl_nslots * lb.sl_slot;  // the trash rows
+        if constexpr (SLOT) dst[q] = (p << 16) | (uint32_t)(j - (int)toff[p]);
+        else dst[q] = running[p] + (j - (int64_t)toff[p]);
+        if (SDBG) {
+          const int64_t d = running[p] + (j - (int64_t)toff[p]);
+          if (d < 0 || d + kRPTile > lb.sl_out_rows + kRPTile || p >= nbuckets) {
+            if (atomicAdd(lb.sl_dbg, 1u) < 8u)
+              printf("slot dbg: block %d tile %lld slot j %d digit %u dst %lld out_rows %lld cnt %d\n",
+                     (int)blockIdx.x, (long long)tile, j, p, (long long)d, (long long)lb.sl_out_rows, cnt);
+            if (d < 0 || d >= lb.sl_out_rows) atomicOr(lb.sl_overflow, 1u);
+          }
         }
         if (cols.check_order && j > 0) {  // same bucket as the previous slot: input order kept?
           const uint32_t f = sdig[j - 1];
@@ -674,7 +684,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       for (int k = 0; k < kRPItems; ++k)
         if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
       __syncthreads();
-      if (TICKET && c + 1 == cols.n) next = s_next;
+      if (TICKET && c + 1 == cols.n) next = SLOT ? s_tr0[par ^ 1] : s_next;
       RP_STAMP(6 + 2 * c);
       if (c + 1 < cols.n) {  // prefetch column c+1 of this tile
         const uint8_t *in = cols.in[c + 1];
@@ -694,29 +704,36 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
           if (i < (SLOT ? s_tend[par ^ 1] : end)) kv[k] = (uint64_t)digit.keys[i];
         }
       }
-      if (c == 0 && cols.nd_out != nullptr) {
+      if (std::is_same<Digit, ImageDigit>::value && c == 0 && cols.nd_out != nullptr) {  // sorts only
 #pragma unroll
         for (int q = 0; q < kRPItems; ++q) {
           const int j = threadIdx.x + q * THREADS;
           if (j < cnt) {
             const uint64_t kv0 = ldw<W8>(st, j, w);
-            stw<W8>(out, dst[q], w, kv0);
-            cols.nd_out[dst[q]] = (uint16_t)((kv0 >> cols.nd_shift) & cols.nd_mask);
+            const int64_t o = RP_DEST(q);
+            stw<W8>(out, o, w, kv0);
+            cols.nd_out[o] = (uint16_t)((kv0 >> cols.nd_shift) & cols.nd_mask);
           }
         }
       } else {
 #pragma unroll
         for (int q = 0; q < kRPItems; ++q) {
           const int j = threadIdx.x + q * THREADS;
-          if (j < cnt) stw<W8>(out, dst[q], w, ldw<W8>(st, j, w));
+          if (j < cnt) stw<W8>(out, RP_DEST(q), w, ldw<W8>(st, j, w));
         }
       }
       __syncthreads();
       RP_STAMP(7 + 2 * c);
     }
+#undef RP_DEST
     if (!TICKET)
       for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) running[p] += toff[p + 1] - toff[p];
-    if (SLOT) par ^= 1;
+    if (SLOT) {
+      par ^= 1;
+      // the tile after the next one, into the slot of the tile just finished: claimed here, where
+      // only the next tile's keys are live (its rows are read two tiles' barriers later)
+      if (threadIdx.x == 0) sl_take(par ^ 1);
+    }
   }
   if (order_bad) atomicOr(cols.order_bad, 1);
 }
@@ -886,7 +903,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
         if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
       __syncthreads();
       if (TICKET && c + 1 == cols.n) next = s_next;
-      if (c == 0 && cols.nd_out != nullptr) {
+      if (std::is_same<Digit, ImageDigit>::value && c == 0 && cols.nd_out != nullptr) {  // sorts only
 #pragma unroll
         for (int q = 0; q < kRPItems; ++q) {
           const int j = tx + q * THREADS;

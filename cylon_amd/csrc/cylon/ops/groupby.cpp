@@ -13,6 +13,7 @@
 //   * output names carry a single prefix (the reference double-prefixes in
 //     its two-phase path);
 //   * COUNT counts non-null values (identical to the reference on non-null data).
+#include <algorithm>
 #include <cstdlib>
 #include <limits>
 
@@ -509,10 +510,75 @@ static TablePtr radix_groupby(const TablePtr &t, const std::vector<int> &keys, c
 }
 
 static TablePtr groupby_with(const TablePtr &t, const std::vector<int> &keys, const std::vector<AggSpec> &aggs,
+                             bool presorted);
+
+// NUNIQUE on the LDS radix path, composed from radix group-bys: the other aggregates of the keys
+// (one radix group-by), and per NUNIQUE column x the distinct (keys, x) pairs with x non-null (a
+// radix group-by on keys + x) counted per key (a group-by of those pairs); a LEFT join of the first
+// result with each count table on the keys puts them side by side (a group whose x is all null
+// counts 0).  Output order: join order (group-by order is unspecified, docs/semantics.md).
+static TablePtr radix_groupby_nunique(const TablePtr &t, const std::vector<int> &keys,
+                                      const std::vector<AggSpec> &aggs) {
+  if (!t->device().is_cuda() || t->Rows() < radix_groupby_min_rows()) return nullptr;
+  std::vector<AggSpec> rest;
+  std::vector<int> nucols;
+  for (const auto &a : aggs) {
+    if (a.op != AGG_NUNIQUE) {
+      rest.push_back(a);
+    } else if (std::find(nucols.begin(), nucols.end(), a.col) == nucols.end()) {
+      if (std::find(keys.begin(), keys.end(), a.col) != keys.end()) return nullptr;  // (nunique of a key: 1)
+      nucols.push_back(a.col);
+    }
+  }
+  if (nucols.empty()) return nullptr;
+  for (int k : keys)
+    if (t->column(k).nullable() || t->column(k).is_var()) return nullptr;
+  const int nk = (int)keys.size();
+  const bool count_only = rest.empty();  // (a COUNT of the first key carries the groups, then dropped)
+  TablePtr base = radix_groupby(t, keys, count_only ? std::vector<AggSpec>{AggSpec{keys[0], AGG_COUNT}} : rest);
+  if (!base) return nullptr;
+  std::vector<int> kidx(nk);
+  for (int i = 0; i < nk; ++i) kidx[i] = i;
+  TablePtr cur = base;  // columns: keys, rest aggregates, then one (keys, count) block per joined column
+  std::vector<int> nupos;  // column of cur holding the count of nucols[i]
+  for (int x : nucols) {
+    std::vector<int> pc(keys);
+    pc.push_back(x);
+    TablePtr pairs = Project(t, pc);
+    if (t->column(x).nullable()) pairs = FilterByMask(pairs, t->column(x).validity);
+    std::vector<int> pk(kidx);
+    pk.push_back(nk);
+    TablePtr distinct = groupby_with(pairs, pk, {AggSpec{nk, AGG_COUNT}}, false);
+    TablePtr counts = groupby_with(Project(distinct, kidx), kidx, {AggSpec{0, AGG_COUNT}}, false);
+    const int width = cur->Columns();
+    cur = Join(cur, counts, join::config::JoinConfig::LeftJoin(kidx, kidx, join::config::HASH));
+    nupos.push_back(width + nk);
+  }
+  trace::add_counter("groupby.radix.nunique_columns", (int64_t)nucols.size());
+  std::vector<Column> out;
+  for (int i = 0; i < nk; ++i) out.push_back(cur->column(i).with_name(t->column(keys[i]).name));
+  int ri = 0;
+  for (const auto &a : aggs) {
+    if (a.op != AGG_NUNIQUE) {
+      out.push_back(cur->column(nk + ri++));
+      continue;
+    }
+    const size_t j = std::find(nucols.begin(), nucols.end(), a.col) - nucols.begin();
+    Column c = cur->column(nupos[j]);
+    at::Tensor v = c.nullable() ? c.data.masked_fill(c.validity == 0, 0) : c.data;
+    out.emplace_back(std::string(AggPrefix(AGG_NUNIQUE)) + t->column(a.col).name, DataType(Type::INT64), c.length,
+                     v.contiguous());
+  }
+  return Table::Make(t->GetContext(), std::move(out));
+}
+
+static TablePtr groupby_with(const TablePtr &t, const std::vector<int> &keys, const std::vector<AggSpec> &aggs,
                              bool presorted) {
   CYLON_CHECK(!keys.empty(), Code::Invalid, "group-by needs at least one key column");
-  if (!presorted)
+  if (!presorted) {
     if (TablePtr r = radix_groupby(t, keys, aggs)) return r;
+    if (TablePtr r = radix_groupby_nunique(t, keys, aggs)) return r;
+  }
   Exec ex(t->device());
   GroupInfo gi;
   {

@@ -217,6 +217,27 @@ def test_radix_groupby_extended(gpu_ctx, monkeypatch, case):
     pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-8, atol=1e-8)
 
 
+@pytest.mark.parametrize("case", ["with_sum", "alone", "two_keys"])
+def test_radix_groupby_nunique(gpu_ctx, monkeypatch, case):
+    """NUNIQUE on the radix path: distinct (keys, x) pairs by a radix group-by, counted per key, LEFT
+    joined to the other aggregates (a group whose x is all null counts 0) -- against the global path."""
+    rng = np.random.default_rng(13)
+    n = 600_000
+    k = rng.integers(0, 40_000, n)
+    g = rng.integers(0, 6, n).astype(np.int32)
+    gmask = (rng.random(n) < 0.1) | (k % 997 == 0)  # nulls, and some groups with every value null
+    t = pa.table({"k": k, "h": rng.integers(-2, 2, n).astype(np.int16), "g": pa.array(g, mask=gmask),
+                  "x": rng.random(n)})
+    T = Table(t, gpu_ctx)
+    keys, aggs = {"with_sum": (["k"], {"g": ["nunique"], "x": ["sum", "max"]}),
+                  "alone": (["k"], {"g": "nunique"}),
+                  "two_keys": (["k", "h"], {"x": ["mean"], "g": ["nunique"]})}[case]
+    res, cnt = _groupby_both(T, keys, aggs, monkeypatch)
+    assert cnt[0].get("groupby.radix.nunique_columns", 0) == 1, cnt[0]
+    assert list(res[0].columns) == list(res[1].columns)
+    pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-9, atol=1e-9, check_dtype=False)
+
+
 @pytest.mark.parametrize("nacc,wide", [(2, False), (2, True), (3, False)])
 def test_radix_groupby_3m_rows_1m_groups(gpu_ctx, monkeypatch, nacc, wide):
     """The round-3 fault shape: 3M rows / ~1M groups with two accumulators run in the three-slot
