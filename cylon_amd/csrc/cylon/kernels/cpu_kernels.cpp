@@ -293,6 +293,18 @@ void composite_key_unpack(const int64_t *key, int64_t n, int nk, const int64_t *
   }
 }
 
+void float_key_bits(const ColView &c, int64_t n, int64_t *out, void *) {
+  for (int64_t i = 0; i < n; ++i) {
+    double v = c.width == 8 ? reinterpret_cast<const double *>(c.data)[i]
+                            : (double)reinterpret_cast<const float *>(c.data)[i];
+    if (v == 0.0) v = 0.0;
+    int64_t b;
+    std::memcpy(&b, &v, 8);
+    if (v != v) b = 0x7ff8000000000000ll;
+    out[i] = b;
+  }
+}
+
 void hash_table_init(HashSlot *table, int64_t tsize, void *) {
   for (int64_t i = 0; i < tsize; ++i) {
     table[i].key = 0;

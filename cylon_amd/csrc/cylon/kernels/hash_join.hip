@@ -372,6 +372,27 @@ void composite_key_unpack(const int64_t *key, int64_t n, int nk, const int64_t *
 }
 #undef CYLON_NK_SWITCH
 
+// K8 float group key: the float64 image's bits with -0.0 -> +0.0 and every NaN -> one quiet NaN
+// (float32 widened first), one read and one write (the torch where/isnan chain took ~5 passes)
+__global__ void k_float_key_bits(ColView c, int64_t n, int64_t *__restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    double v = c.width == 8 ? reinterpret_cast<const double *>(c.data)[i]
+                            : (double)reinterpret_cast<const float *>(c.data)[i];
+    if (v == 0.0) v = 0.0;
+    int64_t b = __double_as_longlong(v);
+    if (v != v) b = 0x7ff8000000000000ll;
+    out[i] = b;
+  }
+}
+
+void float_key_bits(const ColView &c, int64_t n, int64_t *out, void *stream) {
+  if (n == 0) return;
+  CYLON_CHECK(c.width == 8 || c.width == 4, Code::Invalid, "float key of width " << c.width);
+  hipLaunchKernelGGL(k_float_key_bits, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), c, n, out);
+  HIP_LAUNCH_CHECK();
+}
+
 __device__ __forceinline__ bool value_equal(const ColView &a, int64_t i, const ColView &b, int64_t j) {
   const bool va = a.valid == nullptr || a.valid[i] != 0;
   const bool vb = b.valid == nullptr || b.valid[j] != 0;

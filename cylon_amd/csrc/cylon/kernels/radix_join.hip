@@ -641,15 +641,19 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     // destination of sorted slot j = threadIdx.x + q * THREADS.  SLOT: packed as digit << 16 | offset
     // in its run and completed from running[] (LDS) at each store -- 8 VGPRs instead of 16 in the
     // instance that also carries the slot bookkeeping (the trick of the lean kernel)
-    using DstT = typename std::conditional<SLOT, uint32_t, int64_t>::type;
+    // (SLOT could pack them as digit << 16 | offset and complete them from running[] at each store --
+    // 8 fewer VGPRs -- but the dependent LDS read per store measured slower: r04m, 17.3 vs 14.3 ms)
+    constexpr bool PACKDST = false;
+    using DstT = typename std::conditional<SLOT && PACKDST, uint32_t, int64_t>::type;
     DstT dst[kRPItems];
-#define RP_DEST(q) (SLOT ? running[(uint32_t)dst[q] >> 16] + (int64_t)((uint32_t)dst[q] & 0xffffu) : (int64_t)dst[q])
+#define RP_DEST(q) \
+  ((SLOT && PACKDST) ? running[(uint32_t)dst[q] >> 16] + (int64_t)((uint32_t)dst[q] & 0xffffu) : (int64_t)dst[q])
 #pragma unroll
     for (int q = 0; q < kRPItems; ++q) {
       const int j = threadIdx.x + q * THREADS;
       if (j < cnt) {
         const uint32_t e = sdig[j], p = e >> 16;
-        if constexpr (SLOT) dst[q] = (p << 16) | (uint32_t)(j - (int)toff[p]);
+        if constexpr (SLOT && PACKDST) dst[q] = (p << 16) | (uint32_t)(j - (int)toff[p]);
         else dst[q] = running[p] + (j - (int64_t)toff[p]);
         if (SDBG) {
           const int64_t d = running[p] + (j - (int64_t)toff[p]);

@@ -282,25 +282,25 @@ static bool group_key(const Exec &ex, const TablePtr &t, const std::vector<int> 
       return true;
     }
     if (kc.type.kind() == ValueKind::FLOAT && (kc.type.width() == 8 || kc.type.width() == 4)) {
-      at::Tensor x = kc.data.to(at::kDouble);
-      x = at::where(x == 0, at::zeros_like(x), x);                                   // -0.0 -> +0.0
-      x = at::where(at::isnan(x), at::full_like(x, std::numeric_limits<double>::quiet_NaN()), x);
-      g.k = x.view(at::kLong).contiguous();
+      g.k = ex.empty_i64(n);  // -0.0 -> +0.0, NaNs -> one quiet NaN: one fused pass
+      KCALL(ex, float_key_bits, kc.view(), n, ptr<int64_t>(g.k));
       g.fbits = true;
       return true;
     }
     return false;
   }
-  std::vector<at::Tensor> ks, mm;
+  std::vector<at::Tensor> mm;
+  if ((int)keys.size() > kMaxCompositeKeys) return false;
   for (int c : keys) {
     const Column &kc = t->column(c);
     if (!gb_int_key(kc)) return false;
-    at::Tensor k = kc.type.width() == 8 ? kc.data.view(at::kLong) : ex.empty_i64(n);
-    if (kc.type.width() != 8) hip::key64_from_column(kc.view(), n, ptr<int64_t>(k), ex.stream);
-    ks.push_back(k);
+    // span: min / max of the column itself (signed or byte storage), else of its 64-bit image
+    const bool direct = kc.type.kind() == ValueKind::SIGNED_INT || kc.type.width() == 1;
+    at::Tensor k = direct ? kc.data : ex.empty_i64(n);
+    if (!direct) hip::key64_from_column(kc.view(), n, ptr<int64_t>(k), ex.stream);
     auto m2 = at::aminmax(k);
-    mm.push_back(std::get<0>(m2).reshape({1}));
-    mm.push_back(std::get<1>(m2).reshape({1}));
+    mm.push_back(std::get<0>(m2).to(at::kLong).reshape({1}));
+    mm.push_back(std::get<1>(m2).to(at::kLong).reshape({1}));
   }
   const std::vector<int64_t> h = to_host_vec(at::cat(mm));
   int total = 0;
@@ -316,12 +316,14 @@ static bool group_key(const Exec &ex, const TablePtr &t, const std::vector<int> 
     total += b;
   }
   if (total > 63) return false;
-  g.k = at::zeros({n}, ex.opts(at::kLong));
   for (size_t i = keys.size(), sh = 0; i-- > 0;) {
     g.shift[i] = (int)sh;
-    g.k.bitwise_or_(at::bitwise_left_shift(ks[i] - g.lo[i], (int64_t)sh));
     sh += g.bits[i];
   }
+  // one fused pass (composite_key_pack: each key column read once at its own width)
+  g.k = ex.empty_i64(n);
+  std::vector<ColView> v = views(t, keys);
+  KCALL(ex, composite_key_pack, v.data(), (int)keys.size(), g.lo.data(), g.shift.data(), n, ptr<int64_t>(g.k));
   g.composite = true;
   return true;
 }

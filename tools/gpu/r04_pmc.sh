@@ -21,5 +21,5 @@ pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE TCC_EA0_WRREQ_64B_sum
 pass tcc TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum
-for k in "k_rows_pass<cylon::hip::PartDigit, true, 1024, 1" "k_rows_pass<cylon::hip::PartDigit, true, 1024, 2" k_rj_count k_rj_write k_rp_hist_tiles; do python3 $R/tools/pmc_summary.py $O/sq $O/fetch $O/write $O/tcc "$k"; done > $O/summary.txt 2>&1
+for k in "k_rows_pass<cylon::hip::PartDigit, true, 1024, 1, false, true" "k_rows_pass<cylon::hip::PartDigit, true, 1024, 1, true" "k_rows_pass<cylon::hip::PartDigit, true, 1024, 2" k_rj_count k_rj_write k_rp_hist_tiles k_sl_segments; do python3 $R/tools/pmc_summary.py $O/sq $O/fetch $O/write $O/tcc "$k"; done > $O/summary.txt 2>&1
 echo pmc done

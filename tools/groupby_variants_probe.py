@@ -2,7 +2,8 @@
 values) with richer aggregations and keys:
   sum        {"x": "sum"}                         (the config-4 baseline)
   sum_mean_std {"x": ["sum", "mean", "std"]}      (M2 accumulator: a second in-block pass)
-  two_keys   keys (g, h) with h in [0, 4)         (exact composite key), {"x": "sum"}
+  two_keys   keys (g // 4, g % 4): the same 10M groups as two key columns (exact composite), {"x": "sum"}
+  two_keys_4x keys (g, h) with h in [0, 4): 4x the groups (40M), {"x": "sum"}
   float_key  key = g as float64                   (canonical bits), {"x": "sum"}
 
 usage: python tools/groupby_variants_probe.py [rows] [groups] [reps] [variants, comma separated]
@@ -22,18 +23,22 @@ from cylon_amd._lib import C  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000_000
 groups = int(sys.argv[2]) if len(sys.argv) > 2 else 10_000_000
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
-variants = (sys.argv[4] if len(sys.argv) > 4 else "sum,sum_mean_std,two_keys,float_key").split(",")
+variants = (sys.argv[4] if len(sys.argv) > 4 else "sum,sum_mean_std,two_keys,two_keys_4x,float_key").split(",")
 ctx = CylonContext(device="cuda:0")
 g = torch.Generator(device="cuda").manual_seed(4)
 cols = {"g": torch.randint(0, groups, (n,), generator=g, device="cuda"),
         "x": torch.rand(n, generator=g, device="cuda", dtype=torch.float64)}
 if "two_keys" in variants:
+    cols["g1"] = cols["g"] // 4
+    cols["g2"] = cols["g"] % 4
+if "two_keys_4x" in variants:
     cols["h"] = torch.randint(0, 4, (n,), generator=g, device="cuda")
 if "float_key" in variants:
     cols["f"] = cols["g"].to(torch.float64)
 t = Table.from_torch(ctx, cols)
 spec = {"sum": (["g"], {"x": "sum"}), "sum_mean_std": (["g"], {"x": ["sum", "mean", "std"]}),
-        "two_keys": (["g", "h"], {"x": "sum"}), "float_key": (["f"], {"x": "sum"})}
+        "two_keys": (["g1", "g2"], {"x": "sum"}), "two_keys_4x": (["g", "h"], {"x": "sum"}),
+        "float_key": (["f"], {"x": "sum"})}
 for v in variants:
     keys, aggs = spec[v]
     torch.cuda.empty_cache()
