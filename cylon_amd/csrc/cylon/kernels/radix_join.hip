@@ -202,8 +202,9 @@ struct TileSched {
   // of sl_slot rows (claimed with one atomic per (tile, digit)); a run that does not fit goes to
   // the trash rows after the last slot and raises sl_overflow (the caller repartitions exactly).
   // XCD x (blockIdx % 8) owns segments [x S / 8, (x + 1) S / 8).
-  //   first pass over a table: S = 8 chunks of n / 8 rows, slot = d * 8 + g (one slot per
-  //     (bucket, XCD): every slot is filled from ONE XCD's L2);
+  //   first pass over a table: S = 8 chunks of n / 8 rows, slot = g * nb + d (one slot per
+  //     (XCD, bucket): every slot is filled from ONE XCD's L2, and XCD-major cursors keep each
+  //     XCD's claim atomics on cache lines of its own);
   //   second pass: S = 8 * nb1 slots of that pass (or nb1 exact buckets), slot = (g >> 3) * nb + d.
   const uint32_t *sl_tpre = nullptr;  // [S + 1] first tile of each segment (exclusive scan)
   const uint32_t *sl_ss = nullptr;    // [S] first row of each segment
@@ -1395,9 +1396,10 @@ __global__ __launch_bounds__(kRPThreads) void k_sl_segments(int S, int64_t n, co
       } else if constexpr (SRC == 1) {
         a = bbase[g];
         e = g + 1 < S ? (int64_t)bbase[g + 1] : n;
-      } else {
-        a = (int64_t)g * pslot;
-        e = a + (pcnt[g] < pslot ? pcnt[g] : pslot);
+      } else {  // segment g = (bucket g >> 3, XCD g & 7) is first-pass slot (g & 7) * (S / 8) + (g >> 3)
+        const int64_t sl = (int64_t)(g & (kXcds - 1)) * (S / kXcds) + (g >> 3);
+        a = sl * pslot;
+        e = a + (pcnt[sl] < pslot ? pcnt[sl] : pslot);
       }
       ss[g] = (uint32_t)a;
       se[g] = (uint32_t)e;
@@ -1570,10 +1572,11 @@ void radix_slot_first_pass(const int64_t *keys, int64_t n, int total_bits, int f
   CYLON_CHECK(radix_slot_eligible(n, ncols, first_bits, second_bits) && radix_slot_first_pass_ok(first_bits),
               Code::Invalid, "slot first pass not eligible");
   const int nb1 = 1 << first_bits;
-  // the high digit; slot d * 8 + x holds bucket d's rows from XCD x's chunk of the table
+  // the high digit; slot x * 2^first_bits + d holds bucket d's rows from XCD x's chunk of the table
+  // (XCD-major: the cursors one XCD claims from share cache lines only with each other -- the
+  // bucket-major order d * 8 + x put 8 XCDs' atomics on every line)
   slot_pass(PartDigit{keys, total_bits, second_bits, (uint32_t)nb1 - 1}, n, first_bits, in, out, widths, ncols, 0,
-            kXcds, nullptr, nullptr, 0, 3, kXcds - 1, kXcds, int64_t(kXcds) * nb1, slot, ws, counts, overflow,
-            as_stream(stream), n);
+            kXcds, nullptr, nullptr, 0, 0, 0, 1, int64_t(kXcds) * nb1, slot, ws, counts, overflow, as_stream(stream), n);
 }
 
 void radix_slot_rows_pass(const int64_t *keys, int64_t n, int total_bits, int first_bits, int second_bits,
@@ -1584,7 +1587,7 @@ void radix_slot_rows_pass(const int64_t *keys, int64_t n, int total_bits, int fi
   const int nb1 = 1 << first_bits;
   const int64_t nslots = int64_t(nb1) << second_bits;
   const PartDigit dg{keys, total_bits, 0, (1u << second_bits) - 1};
-  if (first_counts != nullptr) {  // after a slot first pass: segment g = slot g (bucket g >> 3)
+  if (first_counts != nullptr) {  // after a slot first pass: segment g = (bucket g >> 3, XCD g & 7)
     slot_pass(dg, n, second_bits, in, out, widths, ncols, 2, kXcds * nb1, nullptr, first_counts, first_slot, 3, 0, 1,
               nslots, slot, ws, counts, overflow, as_stream(stream), int64_t(kXcds) * nb1 * first_slot + kRPTile);
   } else {  // after an XT first pass: segment g = exact bucket g (bases in its workspace)
