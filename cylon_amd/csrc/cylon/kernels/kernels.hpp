@@ -56,6 +56,17 @@ struct HashTableRef {
 constexpr int kMaxFusedCols = 16;  // columns handled by one multi-column launch
 constexpr int kMaxCompositeKeys = 4;  // key columns of one composite join / group-by key
 
+// buffers of one look-back LSD sort pass (radix_sort_lb_args; radix_join.hip "look-back sort passes")
+struct SortLbArgs {
+  const uint32_t *plan_in;  // this pass's chunk plan (nullptr: exact per-tile offsets)
+  uint32_t *plan_out;       // the next pass's plan, counted by this pass (nullptr: last pass)
+  uint32_t *state;          // [tile][nb] look-back words
+  int64_t state_words;
+  uint32_t *gcnt;           // [block][8][nbn] counts
+  int64_t gcnt_words;
+  unsigned int *err;        // look-back wait timed out
+};
+
 // Aggregation op ids, numerically identical to the reference
 // (cpp/src/cylon/compute/aggregate_kernels.hpp:40-50).
 // one accumulator of the LDS radix group-by (radix_groupby.hip)

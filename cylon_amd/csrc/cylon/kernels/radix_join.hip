@@ -65,6 +65,7 @@ struct ColSet {
   uint16_t *nd_out;
   int nd_shift;
   uint32_t nd_mask;
+  uint64_t nd_sub;  // the sort's ImageDigit::sub
 };
 
 // Digit read from a next-digit array written by the previous pass (histogram kernels only)
@@ -141,14 +142,17 @@ struct ModDigit {
   __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key(keys[i]); }
 };
 
-// Sort digit: bits [shift, shift + log2(mask+1)) of an order-preserving uint64 image (K6).
+// Sort digit: bits [shift, shift + log2(mask+1)) of an order-preserving uint64 image (K6), less
+// the smallest image (sub): keys spanning less than their varying bits need fewer digit bits
+// (uniform keys in [-2^62, 2^62) vary in all 64 bits but span 63: 7 x 9-bit digits, not 10 + 6 x 9)
 struct ImageDigit {
   const int64_t *keys;
   int shift;
   uint32_t mask;
   uint64_t flip;  // image = key ^ flip (0 once column 0 holds images)
+  uint64_t sub;
   __device__ __forceinline__ uint32_t of_key(int64_t k) const {
-    return (uint32_t)(((uint64_t)k ^ flip) >> shift) & mask;
+    return (uint32_t)((((uint64_t)k ^ flip) - sub) >> shift) & mask;
   }
   __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key(keys[i]); }
 };
@@ -219,8 +223,37 @@ struct TileSched {
   // skipped, counted in sl_dbg[0] and printed (first few)
   int64_t sl_in_rows = 0, sl_out_rows = 0;
   unsigned int *sl_dbg = nullptr;
+  // look-back sort passes (k_rows_pass_lean<..., LBM>, see "look-back sort passes" below)
+  const uint32_t *lb_plan = nullptr;  // in: chunk rows / tiles / bases of this pass (LBM & 2)
+  uint32_t *lb_state = nullptr;       // in: [tile][nb] flag | value + 1 words, zeroed
+  unsigned int *lb_err = nullptr;     // in: set when a look-back wait timed out
+  uint32_t *lb_gcnt = nullptr;        // out: [block][8][nbn] (chunk, next digit) counts (LBM & 1)
+  int lb_xshift = 0;                  // out: next pass's chunk = this pass's digit >> lb_xshift
+  // in: chunk x only on XCD x, look-back words stored without write-through (they stay in that
+  // XCD's L2, where its CUs' L1-bypassing loads find them); CYLON_SORT_LB_LOCAL=1
+  int lb_local = 0;
 };
 constexpr int kSlotMaxSeg = 4096;
+
+// ---- look-back sort passes (LSD sort of 1-2 all-8-byte columns; CYLON_SORT_LOOKBACK=0 disables)
+// The exact XT pass needs every tile's digit counts before it starts (k_rp_hist_tiles over the
+// previous pass's next-digit array + k_ts_* scans: ~1 ms, and writing that 2-byte array ~2 ms, of
+// every 2B-row pass).  Here instead:
+//   * the input is split into 8 chunks by the top 3 bits of the PREVIOUS pass's digit (contiguous:
+//     that pass left the rows in that order), chunk x claimed tile by tile in order by XCD x;
+//   * the previous pass counted, per (chunk, this pass's digit), the rows it stored (LDS counters,
+//     flushed to per-block global rows) -> per-(chunk, digit) output bases (k_lb_plan);
+//   * inside a chunk a tile's offset is the sum of its predecessors' digit counts, found by a
+//     decoupled look-back: each tile publishes its counts (AGGREGATE) right after ranking, then walks
+//     back over its predecessors' words until an INCLUSIVE prefix, and publishes its own.
+// A word is 0 (not yet), value + 1 (aggregate) or 2^31 | value + 1 (inclusive prefix): flag and
+// value travel in one 32-bit agent-scope atomic store / load, so no fence orders them.  Tiles are
+// claimed in order per chunk, so a tile waits only on tiles already claimed by running blocks; a
+// wait that exceeds kLbSpinLimit polls (never expected) sets lb_err and the sort falls back.
+constexpr int kLbChunks = 8, kLbMaxBuckets = 512;
+constexpr int kLbCnt = 0, kLbC = kLbChunks * kLbMaxBuckets, kLbTP = kLbC + 16, kLbBase = kLbTP + 16,
+              kLbTickets = kLbBase + kLbChunks * kLbMaxBuckets, kLbPlanWords = kLbTickets + 16;
+constexpr int kLbSpinLimit = 1 << 20, kLbWindow = 4;
 
 // XCD-tile mode.  Histogram mode gives each block a contiguous chunk of rows, so the tiles of
 // one block write a bucket's consecutive runs ~34 us apart and the partial 128-B line at every
@@ -257,6 +290,35 @@ __device__ __forceinline__ int64_t xt_claim(const TileSched &lb, int home, int64
     if (lo + j < hi) return (lo + j) * tile_rows;
   }
   return n_rows;
+}
+
+// look-back passes: first row of the next tile of chunk home (else of another chunk), or n_rows
+__device__ __forceinline__ int64_t lb_claim(const TileSched &lb, const uint32_t *sC, const uint32_t *sTP, int home,
+                                            int64_t tile_rows, int64_t n_rows) {
+  for (int k = 0; k < (lb.lb_local ? 1 : kXcds); ++k) {
+    const int x = (home + k) & (kXcds - 1);
+    const uint32_t T = sTP[x + 1] - sTP[x];
+    if (T == 0) continue;
+    const uint32_t j = atomicAdd(&lb.xt_ticket[x], 1u);
+    if (j < T) return (int64_t)sC[x] + (int64_t)j * tile_rows;
+  }
+  return n_rows;
+}
+
+// look-back counting: add the packed 16-bit LDS counters to the block's global row g and clear them
+// (every thread of the block calls it)
+template <int THREADS>
+__device__ __forceinline__ void lb_flush(uint32_t *lc, uint32_t *g, uint32_t lwords) {
+  __syncthreads();
+  for (uint32_t w = threadIdx.x; w < lwords; w += THREADS) {
+    const uint32_t v = lc[w];
+    if (v) {
+      g[2 * w] += v & 0xffffu;
+      g[2 * w + 1] += v >> 16;
+    }
+    lc[w] = 0;
+  }
+  __syncthreads();
 }
 
 // LDS-DMA of `bytes` (a multiple of 4) contiguous global bytes into LDS at dst (16-byte aligned)
@@ -717,7 +779,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             const uint64_t kv0 = ldw<W8>(st, j, w);
             const int64_t o = RP_DEST(q);
             stw<W8>(out, o, w, kv0);
-            cols.nd_out[o] = (uint16_t)((kv0 >> cols.nd_shift) & cols.nd_mask);
+            cols.nd_out[o] = (uint16_t)(((kv0 - cols.nd_sub) >> cols.nd_shift) & cols.nd_mask);
           }
         }
       } else {
@@ -752,32 +814,50 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 //   * no cross-column / cross-tile prefetch (the second block hides the load latency);
 //   * the destination of sorted slot j is packed as (digit << 16 | j - toff[digit]) and
 //     completed from running[] in LDS at store time (8 VGPRs instead of 16).
-template <class Digit, bool W8, int RANK, bool XT = false>
+// LBM (sorts, XT only): bit 1 = offsets by look-back (lb_plan / lb_state), bit 0 = count the
+// (chunk, next digit) pairs for the next look-back pass (lb_gcnt); both limit digits to 9 bits.
+template <class Digit, bool W8, int RANK, bool XT = false, int LBM = 0>
 __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_rows_pass_lean(
     Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
     const int64_t *__restrict__ bh_scan, TileSched lb) {
   constexpr int THREADS = kRPThreads, WAVES = THREADS / kWave, TILE = THREADS * kRPItems;
-  constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;
-  static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 4 <= TILE * 8, "ranking scratch must fit the stage");
-  __shared__ int64_t running[kRPMaxBuckets];
-  __shared__ uint32_t toff[kRPMaxBuckets + 1];
+  constexpr bool LBIN = (LBM & 2) != 0, CNT = (LBM & 1) != 0;
+  static_assert(LBM == 0 || (XT && std::is_same<Digit, ImageDigit>::value), "look-back passes are XT sort passes");
+  constexpr int MAXB = LBM ? kLbMaxBuckets : kRPMaxBuckets;
+  constexpr int BPT = (MAXB + THREADS - 1) / THREADS;
+  static_assert(WAVES * MAXB * 2 + TILE * 4 <= TILE * 8, "ranking scratch must fit the stage");
+  __shared__ int64_t running[MAXB];
+  __shared__ uint32_t toff[MAXB + 1];
   __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16 or bcnt[nb] u32, sdig[TILE] u16}
   __shared__ uint32_t wsum[WAVES];
+  // look-back: chunk first rows / first tiles; counting: packed 16-bit (chunk, next digit) counters
+  __shared__ uint32_t s_C[LBIN ? kLbChunks + 1 : 1], s_TP[LBIN ? kLbChunks + 1 : 1];
+  __shared__ uint32_t lcnt[CNT ? kLbChunks * kLbMaxBuckets / 2 : 1];
   constexpr bool STABLE = RANK != kRankBlockAtomic;
   uint16_t *wcnt = reinterpret_cast<uint16_t *>(ustage);
   uint32_t *bcnt = reinterpret_cast<uint32_t *>(ustage);
-  uint32_t *sdig = reinterpret_cast<uint32_t *>(wcnt + WAVES * kRPMaxBuckets);  // digit << 16 | input row
+  uint32_t *sdig = reinterpret_cast<uint32_t *>(wcnt + WAVES * MAXB);  // digit << 16 | input row
   uint8_t *st = reinterpret_cast<uint8_t *>(ustage);
   __shared__ int64_t s_next;  // XT: first row of the next claimed tile
   bool order_bad = false;
   (void)nbits;
   constexpr bool TICKET = XT;
   const int xhome = XT ? xcc_id() : 0;
+  const uint32_t nbn = cols.nd_mask + 1u;               // counting: next pass's buckets
+  const uint32_t lwords = CNT ? kLbChunks * nbn / 2 : 0;  // counting: LDS words in use
+  int since_flush = 0;
 
   const int64_t b = blockIdx.x;
   int64_t begin, end;
+  if (CNT)
+    for (uint32_t w = threadIdx.x; w < lwords; w += THREADS) lcnt[w] = 0;
+  if (LBIN && threadIdx.x <= kLbChunks) {
+    s_C[threadIdx.x] = lb.lb_plan[kLbC + threadIdx.x];
+    s_TP[threadIdx.x] = lb.lb_plan[kLbTP + threadIdx.x];
+  }
   if (TICKET) {
-    if (threadIdx.x == 0) s_next = xt_claim(lb, xhome, TILE, n);
+    if (LBIN) __syncthreads();
+    if (threadIdx.x == 0) s_next = LBIN ? lb_claim(lb, s_C, s_TP, xhome, TILE, n) : xt_claim(lb, xhome, TILE, n);
     __syncthreads();
     begin = s_next;
     end = n;
@@ -794,14 +874,20 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
 
   for (int64_t tile = begin, next = 0; tile < end; tile = next) {
     next = tile + TILE;
-    const int cnt = (int)((end - tile) < TILE ? (end - tile) : TILE);
+    // look-back: the tile's chunk (uniform) and its index in the chunk
+    int cx = 0;
+    if (LBIN)
+      while (cx + 1 < kLbChunks && (int64_t)s_C[cx + 1] <= tile) ++cx;
+    const int64_t ck = LBIN ? (tile - (int64_t)s_C[cx]) / TILE : 0;
+    const int64_t tend = LBIN ? (int64_t)s_C[cx + 1] : end;
+    const int cnt = (int)((tend - tile) < TILE ? (tend - tile) : TILE);
     // per-thread constants are recomputed every tile from an opaque copy of the thread id:
     // hoisted out of the tile loop they outlive the 64-VGPR budget and spill
     int tx = (int)threadIdx.x;
     asm volatile("" : "+v"(tx));
     const int lane = tx & (kWave - 1);
     // XT: this tile's bucket offsets (stored to running[] after the slot phase)
-    const uint32_t xoff = XT && (uint32_t)tx < nbuckets ? lb.xt_off[(tile / TILE) * nbuckets + tx] : 0u;
+    const uint32_t xoff = XT && !LBIN && (uint32_t)tx < nbuckets ? lb.xt_off[(tile / TILE) * nbuckets + tx] : 0u;
     uint32_t pl[kRPItems];  // digit | in-tile rank << 16, then the sorted slot; ~0 = inactive
     const int64_t *kbase = digit.keys + tile + wrow;  // wave-uniform
     const int lim = cnt - wrow;                       // rows of this wave's slice that exist
@@ -863,6 +949,14 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
       if (tx == THREADS - 1) toff[nbuckets] = ex + total;
     }
     __syncthreads();
+    const int64_t lgid = LBIN ? (int64_t)s_TP[cx] + ck : 0;  // look-back: the tile's state row
+    if (LBIN && (uint32_t)tx < nbuckets) {  // publish this tile's counts (the chunk's first: its prefix)
+      const uint32_t v = (ck == 0 ? 0x80000000u : 0u) | (toff[tx + 1] - toff[tx] + 1u);
+      if (lb.lb_local)
+        __hip_atomic_store(&lb.lb_state[lgid * nbuckets + tx], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      else
+        __hip_atomic_store(&lb.lb_state[lgid * nbuckets + tx], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k) {
       if (pl[k] == 0xffffffffu) continue;
@@ -871,7 +965,53 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
       sdig[pos] = (p << 16) | (uint32_t)(wrow + k * kWave + lane);
       pl[k] = pos;
     }
-    if (XT && (uint32_t)tx < nbuckets) running[tx] = xoff;
+    if (LBIN && (uint32_t)tx < nbuckets) {  // look back over the chunk's earlier tiles
+      const uint32_t own = toff[tx + 1] - toff[tx];
+      uint32_t excl = 0;
+      if (ck > 0) {
+        // windowed walk: the next kLbWindow predecessors' words are loaded together (one round trip
+        // per window instead of per tile; a walk is a few tiles long: those claimed just before)
+        const int64_t lo = (int64_t)s_TP[cx];  // the chunk's first tile (always an inclusive prefix)
+        int64_t j = lgid - 1;
+        for (int spin = 0;;) {
+          uint32_t w[kLbWindow];
+#pragma unroll
+          for (int i = 0; i < kLbWindow; ++i)
+            w[i] = j - i >= lo ? __hip_atomic_load(&lb.lb_state[(j - i) * nbuckets + tx], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                               : 0u;
+          int used = 0;
+          bool done = false;
+#pragma unroll
+          for (int i = 0; i < kLbWindow; ++i) {
+            if (done || used < i || w[i] == 0u) continue;  // stop at the first word not yet published
+            excl += (w[i] & 0x7fffffffu) - 1u;
+            used = i + 1;
+            done = (w[i] & 0x80000000u) != 0u;
+          }
+          if (done) break;
+          j -= used;
+          if (used == 0) {  // the nearest predecessor has not published yet
+            __builtin_amdgcn_s_sleep(1);
+            // give up after kLbSpinLimit polls, or at once after any other wait gave up (the result
+            // is discarded then, so the grid only has to drain)
+            if (++spin > kLbSpinLimit ||
+                ((spin & 255) == 0 && __hip_atomic_load(lb.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+              atomicOr(lb.lb_err, 1u);
+              break;
+            }
+          }
+        }
+        if (lb.lb_local)
+          __hip_atomic_store(&lb.lb_state[lgid * nbuckets + tx], 0x80000000u | (excl + own + 1u), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+          __hip_atomic_store(&lb.lb_state[lgid * nbuckets + tx], 0x80000000u | (excl + own + 1u), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+      running[tx] = (int64_t)lb.lb_plan[kLbBase + cx * nbuckets + tx] + excl;
+    }
+    if (XT && !LBIN && (uint32_t)tx < nbuckets) running[tx] = xoff;
     __syncthreads();
     uint32_t dp[kRPItems];  // sorted slot j = tx + q * THREADS -> digit << 16 | offset in its run
 #pragma unroll
@@ -902,13 +1042,28 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
         for (int k = 0; k < kRPItems; ++k) v[k] = (k * kWave + lane < lim) ? ldw<W8>(ibase, k * kWave + lane, w) : 0ull;
       }
       const uint64_t x = c == 0 ? cols.key_xor : 0ull;
-      if (TICKET && c + 1 == cols.n && tx == 0) s_next = xt_claim(lb, xhome, TILE, n);
+      if (TICKET && c + 1 == cols.n && tx == 0)
+        s_next = LBIN ? lb_claim(lb, s_C, s_TP, xhome, TILE, n) : xt_claim(lb, xhome, TILE, n);
 #pragma unroll
       for (int k = 0; k < kRPItems; ++k)
         if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
       __syncthreads();
       if (TICKET && c + 1 == cols.n) next = s_next;
-      if (std::is_same<Digit, ImageDigit>::value && c == 0 && cols.nd_out != nullptr) {  // sorts only
+      if (CNT && c == 0) {  // count (chunk of the next pass, next digit) as the keys are stored
+        const int xsh = lb.lb_xshift;
+#pragma unroll
+        for (int q = 0; q < kRPItems; ++q) {
+          const int j = tx + q * THREADS;
+          if (j < cnt) {
+            const uint32_t p = dp[q] >> 16;
+            const int64_t o = running[p] + (int64_t)(dp[q] & 0xffffu);
+            const uint64_t kv0 = ldw<W8>(st, j, w);
+            stw<W8>(out, o, w, kv0);
+            const uint32_t cell = (p >> xsh) * nbn + (uint32_t)(((kv0 - cols.nd_sub) >> cols.nd_shift) & cols.nd_mask);
+            atomicAdd(&lcnt[cell >> 1], 1u << ((cell & 1u) << 4));
+          }
+        }
+      } else if (std::is_same<Digit, ImageDigit>::value && c == 0 && cols.nd_out != nullptr) {  // sorts only
 #pragma unroll
         for (int q = 0; q < kRPItems; ++q) {
           const int j = tx + q * THREADS;
@@ -916,7 +1071,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
             const int64_t o = running[dp[q] >> 16] + (int64_t)(dp[q] & 0xffffu);
             const uint64_t kv0 = ldw<W8>(st, j, w);
             stw<W8>(out, o, w, kv0);
-            cols.nd_out[o] = (uint16_t)((kv0 >> cols.nd_shift) & cols.nd_mask);
+            cols.nd_out[o] = (uint16_t)(((kv0 - cols.nd_sub) >> cols.nd_shift) & cols.nd_mask);
           }
         }
       } else {
@@ -930,7 +1085,12 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
     }
     if (!TICKET)
       for (uint32_t p = tx; p < nbuckets; p += THREADS) running[p] += toff[p + 1] - toff[p];
+    if (CNT && ++since_flush == 7) {  // 7 tiles x 8192 rows fit a 16-bit counter
+      lb_flush<THREADS>(lcnt, lb.lb_gcnt + (int64_t)blockIdx.x * (2 * lwords), lwords);
+      since_flush = 0;
+    }
   }
+  if (CNT && since_flush > 0) lb_flush<THREADS>(lcnt, lb.lb_gcnt + (int64_t)blockIdx.x * (2 * lwords), lwords);
   if (order_bad) atomicOr(cols.order_bad, 1);
 }
 
@@ -1210,7 +1370,24 @@ static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const 
 
 template <class Digit, int RANK>
 static void lean_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit &dg, int digit_bits, uint32_t nb,
-                        const ColSet &cs, int64_t n, const int64_t *bh_scan, const TileSched &lb, bool xt = false) {
+                        const ColSet &cs, int64_t n, const int64_t *bh_scan, const TileSched &lb, bool xt = false,
+                        int lbm = 0) {
+  if (lbm) {  // look-back sort passes: XT, all columns 8 bytes wide (checked by the caller)
+    if constexpr (std::is_same<Digit, ImageDigit>::value && RANK == kRankWaveAtomic) {
+      const dim3 gr((unsigned)g.nblocks), bl(kRPThreads);
+      if (lbm == 1)
+        hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, RANK, true, 1>), gr, bl, 0, s, dg, digit_bits, nb, cs, n,
+                           g.rows_per_block, g.nblocks, bh_scan, lb);
+      else if (lbm == 2)
+        hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, RANK, true, 2>), gr, bl, 0, s, dg, digit_bits, nb, cs, n,
+                           g.rows_per_block, g.nblocks, bh_scan, lb);
+      else
+        hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, RANK, true, 3>), gr, bl, 0, s, dg, digit_bits, nb, cs, n,
+                           g.rows_per_block, g.nblocks, bh_scan, lb);
+      return;
+    }
+    CYLON_THROW(Code::Invalid, "look-back pass: sort digits with stable wave ranking only");
+  }
   if (xt) {
     if (w8)
       hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, RANK, true>), dim3((unsigned)g.nblocks), dim3(kRPThreads), 0, s,
@@ -1228,6 +1405,71 @@ static void lean_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit
                        digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
 }
 
+// ---- look-back sort passes, host side (see "look-back sort passes")
+// cnt[c] += gcnt[b][c] over a slice of the blocks (grid: cells / 256 x kLbReduceSlices)
+constexpr int kLbReduceSlices = 32;
+__global__ __launch_bounds__(256) void k_lb_reduce(const uint32_t *__restrict__ gcnt, int64_t nblk, int cells,
+                                                   uint32_t *__restrict__ cnt) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cells) return;
+  const int64_t b0 = nblk * blockIdx.y / kLbReduceSlices, b1 = nblk * (blockIdx.y + 1) / kLbReduceSlices;
+  uint32_t acc = 0;
+  for (int64_t b = b0; b < b1; ++b) acc += gcnt[b * cells + c];
+  if (acc) atomicAdd(&cnt[c], acc);
+}
+
+// plan of a look-back pass from its (chunk, digit) counts: chunk first rows C, first tiles TP
+// (tiles never straddle chunks) and bases[x][d] = rows of digits < d + rows of digit d in chunks < x
+__global__ __launch_bounds__(kLbMaxBuckets) void k_lb_plan(uint32_t *__restrict__ plan, uint32_t nb) {
+  __shared__ uint32_t wsum[kLbMaxBuckets / kWave];
+  __shared__ uint32_t csz[kLbChunks];
+  const uint32_t d = threadIdx.x;
+  if (d < kLbChunks) csz[d] = 0;
+  uint32_t c[kLbChunks], tot = 0;
+#pragma unroll
+  for (int x = 0; x < kLbChunks; ++x) {
+    c[x] = d < nb ? plan[kLbCnt + x * nb + d] : 0u;
+    tot += c[x];
+  }
+  __syncthreads();
+  uint32_t run = rp_block_exscan<kLbMaxBuckets / kWave>(tot, wsum);
+#pragma unroll
+  for (int x = 0; x < kLbChunks; ++x) {
+    if (d < nb) plan[kLbBase + x * nb + d] = run;
+    run += c[x];
+    if (c[x]) atomicAdd(&csz[x], c[x]);
+  }
+  __syncthreads();
+  if (d == 0) {
+    uint32_t r = 0, t = 0;
+    for (int x = 0; x < kLbChunks; ++x) {
+      plan[kLbC + x] = r;
+      plan[kLbTP + x] = t;
+      r += csz[x];
+      t += (csz[x] + kRPTile - 1) / kRPTile;
+    }
+    plan[kLbC + kLbChunks] = r;
+    plan[kLbTP + kLbChunks] = t;
+  }
+}
+
+// local look-back mode: every chunk's tiles were claimed (XCD x had blocks), else err |= 2
+__global__ void k_lb_check(const uint32_t *__restrict__ plan, unsigned int *err) {
+  const int x = threadIdx.x;
+  if (x < kLbChunks && plan[kLbTickets + x] < plan[kLbTP + x + 1] - plan[kLbTP + x]) atomicOr(err, 2u);
+}
+
+static void lb_plan_next(const SortLbArgs *lba, int64_t nblk, uint32_t nbn, int64_t n, hipStream_t s) {
+  const int cells = kLbChunks * (int)nbn;
+  HIP_CHECK(hipMemsetAsync(lba->plan_out + kLbCnt, 0, sizeof(uint32_t) * cells, s));
+  hipLaunchKernelGGL(k_lb_reduce, dim3((unsigned)((cells + 255) / 256), kLbReduceSlices), dim3(256), 0, s, lba->gcnt,
+                     nblk, cells, lba->plan_out + kLbCnt);
+  HIP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_lb_plan, dim3(1), dim3(kLbMaxBuckets), 0, s, lba->plan_out, nbn);
+  HIP_LAUNCH_CHECK();
+  (void)n;
+}
+
 // stable = false (join partitions only) ranks rows with LDS atomics: rows of one
 // bucket keep no particular order inside a tile's run.  Instantiated for PartDigit
 // only; every other digit (sort, shuffle, range join) needs the stable order.
@@ -1236,7 +1478,8 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
                              const int *widths, int ncols, int64_t *ws, void *stream, uint64_t key_xor = 0,
                              bool stable = true, bool tiles_prescanned = false,
                              const uint32_t *bucket_extra = nullptr, const uint16_t *nd_in = nullptr,
-                             uint16_t *nd_out = nullptr, int nd_shift = 0, uint32_t nd_mask = 0) {
+                             uint16_t *nd_out = nullptr, int nd_shift = 0, uint32_t nd_mask = 0,
+                             uint64_t nd_sub = 0, const SortLbArgs *lba = nullptr) {
   if (n == 0) return;
   CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
   CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
@@ -1263,9 +1506,30 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   TileSched lb{};
   const bool xt = threads == 1024 && n < (int64_t(1) << 32) && rp_xt();
   CYLON_CHECK(xt || bucket_extra == nullptr, Code::Invalid, "radix pass: gapped layouts need the XCD-tile schedule");
+  const bool lbin = lba && lba->plan_in, lbcnt = lba && lba->plan_out;
+  if (lbin || lbcnt) {
+    bool w8all = true;
+    for (int c = 0; c < ncols; ++c) w8all &= widths[c] == 8;
+    CYLON_CHECK(xt && lean && !unstable && wave_atomic && w8all && nb <= (uint32_t)kLbMaxBuckets &&
+                    n < (int64_t(1) << 31) - 2 && (!lbcnt || (digit_bits >= 3 && nd_mask + 1 <= (uint32_t)kLbMaxBuckets)),
+                Code::Invalid, "look-back sort pass not eligible");
+  }
   if (!xt) tiles_prescanned = false;  // histogram mode counts its own blocks (the prescan is unused)
   if (!xt) nd_in = nullptr;            // ... and reads the keys (the previous pass's digits go unused)
-  if (xt) {  // exact per-tile offsets, tiles claimed in order per XCD (see xt_claim)
+  if (xt && lbin) {  // look-back offsets: the previous pass planned the chunks (see k_lb_plan)
+    const int64_t ntiles = (n + kRPTile - 1) / kRPTile;
+    HIP_CHECK(hipMemsetAsync(const_cast<uint32_t *>(lba->plan_in) + kLbTickets, 0, kXcds * sizeof(uint32_t), s));
+    CYLON_CHECK((ntiles + kLbChunks) * nb <= lba->state_words, Code::Invalid, "look-back state too small");
+    HIP_CHECK(hipMemsetAsync(lba->state, 0, sizeof(uint32_t) * (ntiles + kLbChunks) * nb, s));
+    lb.lb_plan = lba->plan_in;
+    lb.lb_state = lba->state;
+    lb.lb_err = lba->err;
+    lb.xt_ticket = const_cast<uint32_t *>(lba->plan_in) + kLbTickets;
+    const char *lc = std::getenv("CYLON_SORT_LB_LOCAL");  // experiment knob, read per pass
+    lb.lb_local = lc && lc[0] == '1';
+    g.rows_per_block = kRPTile;
+    g.nblocks = std::min<int64_t>(ntiles + kLbChunks, (int64_t)kNumCUs * 2);
+  } else if (xt) {  // exact per-tile offsets, tiles claimed in order per XCD (see xt_claim)
     const XtLayout L = xt_layout(n, nb);
     uint16_t *th = reinterpret_cast<uint16_t *>(ws + L.th);
     uint32_t *off = reinterpret_cast<uint32_t *>(ws + L.off);
@@ -1312,6 +1576,7 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   cs.nd_out = nd_out;
   cs.nd_shift = nd_shift;
   cs.nd_mask = nd_mask;
+  cs.nd_sub = nd_sub;
   const char *gd = std::getenv("CYLON_RP_GUARD");  // A/B knob: 0 disables the ranking guard
   cs.check_order = want_stable && !(gd && gd[0] == '0') ? 1 : 0;
   cs.order_bad = order_flag();
@@ -1327,11 +1592,24 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
                 "radix pass: a generated row-id column must be an 8-byte payload column");
   }
   const bool big = threads == 1024;
+  if (lbcnt) {  // per-block (chunk, next digit) rows, summed into the next pass's plan below
+    const int64_t words = g.nblocks * kLbChunks * (int64_t)(nd_mask + 1);
+    CYLON_CHECK(words <= lba->gcnt_words, Code::Invalid, "look-back counters too small");
+    HIP_CHECK(hipMemsetAsync(lba->gcnt, 0, sizeof(uint32_t) * words, s));
+    lb.lb_gcnt = lba->gcnt;
+    lb.lb_xshift = digit_bits - 3;
+  }
   if (lean) {
     constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankWaveAtomic;
+    const int lbm = (lbin ? 2 : 0) | (lbcnt ? 1 : 0);
     if (unstable) lean_kernel<Digit, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
-    else lean_kernel<Digit, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
+    else lean_kernel<Digit, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt, lbm);
     HIP_LAUNCH_CHECK();
+    if (lbin && lb.lb_local) {
+      hipLaunchKernelGGL(k_lb_check, dim3(1), dim3(kWave), 0, s, lba->plan_in, lba->err);
+      HIP_LAUNCH_CHECK();
+    }
+    if (lbcnt) lb_plan_next(lba, g.nblocks, nd_mask + 1, n, s);
     return;
   }
   if (unstable) {
@@ -1358,14 +1636,57 @@ void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, 
 void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_bits, const uint8_t *const *in,
                           uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream,
                           uint64_t key_xor, uint64_t digit_flip, bool tiles_prescanned, const uint16_t *nd_in,
-                          uint16_t *nd_out, int nd_shift, int nd_bits) {
+                          uint16_t *nd_out, int nd_shift, int nd_bits, uint64_t sub, const SortLbArgs *lb) {
   const uint32_t nb = 1u << digit_bits;
+  CYLON_CHECK(!(lb && lb->plan_out) || (nd_out == nullptr && nd_bits >= 1 && nd_bits <= 9), Code::Invalid,
+              "look-back counting pass: next digit of " << nd_bits << " bits");
   // (the digits come from column 0 as stored: images on every pass but a last one that restores keys)
   CYLON_CHECK(nd_out == nullptr || (nd_bits >= 1 && nd_bits <= 16), Code::Invalid,
               "sort pass: next-digit output of " << nd_bits << " bits");
-  rows_pass_launch(ImageDigit{keys, shift, nb - 1, digit_flip}, n, digit_bits, in, out, widths, ncols, ws, stream,
-                   key_xor, true, tiles_prescanned, nullptr, nd_in, nd_out, nd_shift,
-                   nd_out ? (1u << nd_bits) - 1u : 0u);
+  rows_pass_launch(ImageDigit{keys, shift, nb - 1, digit_flip, sub}, n, digit_bits, in, out, widths, ncols, ws,
+                   stream, key_xor, true, tiles_prescanned, nullptr, lb && lb->plan_in ? nullptr : nd_in, nd_out,
+                   nd_shift, nd_out || (lb && lb->plan_out) ? (1u << nd_bits) - 1u : 0u, sub, lb);
+}
+
+bool radix_sort_lb_eligible(int64_t n, int ncols, const int *widths, const int *dbits, int npass, void *stream) {
+  const char *e = std::getenv("CYLON_SORT_LOOKBACK");  // A/B knob: 0 = exact per-tile histogram passes
+  if ((e && e[0] == '0') || !rp_xt() || npass < 2 || n < 1 || n >= (int64_t(1) << 31) - 2) return false;
+  if (rp_threads(ncols, true) != 1024 || !rp_lean(ncols) || !rp_wave_atomic(as_stream(stream))) return false;
+  for (int c = 0; c < ncols; ++c)
+    if (widths[c] != 8) return false;
+  for (int p = 0; p < npass; ++p)
+    if (dbits[p] < 3 || dbits[p] > 9) return false;
+  return true;
+}
+
+static int64_t lb_state_words(int64_t n) { return ((n + kRPTile - 1) / kRPTile + kLbChunks) * kLbMaxBuckets; }
+static int64_t lb_gcnt_words() { return int64_t(2) * kNumCUs * kLbChunks * kLbMaxBuckets; }
+
+int64_t radix_sort_lb_workspace(int64_t n) {
+  const int64_t u32 = 2 * (int64_t)kLbPlanWords + 16 + lb_state_words(n) + lb_gcnt_words();
+  return (u32 + 1) / 2;
+}
+
+SortLbArgs radix_sort_lb_args(int64_t *ws, int64_t n, int pass, int npass, void *stream) {
+  uint32_t *w = reinterpret_cast<uint32_t *>(ws);
+  SortLbArgs a{};
+  a.err = w + 2 * kLbPlanWords;
+  a.state = a.err + 16;
+  a.state_words = lb_state_words(n);
+  a.gcnt = a.state + a.state_words;
+  a.gcnt_words = lb_gcnt_words();
+  if (pass == 0) HIP_CHECK(hipMemsetAsync(a.err, 0, sizeof(uint32_t), as_stream(stream)));
+  a.plan_in = pass > 0 ? w + ((pass - 1) & 1) * kLbPlanWords : nullptr;
+  a.plan_out = pass + 1 < npass ? w + (pass & 1) * kLbPlanWords : nullptr;
+  return a;
+}
+
+bool radix_sort_lb_failed(const int64_t *ws, void *stream) {
+  unsigned h = 0;
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(ws);
+  HIP_CHECK(hipMemcpyAsync(&h, w + 2 * kLbPlanWords, sizeof(h), hipMemcpyDeviceToHost, as_stream(stream)));
+  HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
+  return h != 0;
 }
 
 // ---- slot mode (the histogram-free passes of a join partition; TileSched)
@@ -1532,6 +1853,7 @@ static void slot_pass(const PartDigit &dg, int64_t n, int digit_bits, const uint
   cs.nd_out = nullptr;
   cs.nd_shift = 0;
   cs.nd_mask = 0;
+  cs.nd_sub = 0;
   bool w8 = true;
   for (int c = 0; c < kMaxFusedCols; ++c) {
     cs.in[c] = c < ncols ? in[c] : nullptr;
@@ -1600,15 +1922,16 @@ void radix_slot_rows_pass(const int64_t *keys, int64_t n, int total_bits, int fi
 
 bool radix_xt_enabled() { return rp_xt(); }
 
-// ---- sort prologue: the keys' varying bits (OR ^ AND) and the first pass's per-tile histogram of
-// the order image's low 10 bits in ONE read of the keys (the separate reduction read them once more)
+// ---- sort prologue: the keys' varying bits (OR ^ AND), the images' min and max, and the first
+// pass's per-tile histogram of the order image's low 10 bits in ONE read of the keys (the separate
+// reduction read them once more)
 constexpr int kSPBits = 10;
 __global__ __launch_bounds__(kHTThreads) void k_sort_prehist(const int64_t *__restrict__ keys, int64_t n,
                                                              uint64_t flip, int64_t ntiles, uint16_t *__restrict__ th,
                                                              unsigned long long *__restrict__ orand) {
   constexpr uint32_t nb = 1u << kSPBits;
   __shared__ unsigned int hist[nb];
-  uint64_t o = 0, a = ~0ull;
+  uint64_t o = 0, a = ~0ull, mn = ~0ull, mx = 0;
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     uint64_t k[kHTItems];
     const int64_t r0 = t * kRPTile;
@@ -1624,7 +1947,10 @@ __global__ __launch_bounds__(kHTThreads) void k_sort_prehist(const int64_t *__re
       if (r0 + u * kHTThreads + threadIdx.x < n) {
         o |= k[u];
         a &= k[u];
-        atomicAdd(&hist[(uint32_t)((k[u] ^ flip) & (nb - 1))], 1u);
+        const uint64_t im = k[u] ^ flip;
+        mn = im < mn ? im : mn;
+        mx = im > mx ? im : mx;
+        atomicAdd(&hist[(uint32_t)(im & (nb - 1))], 1u);
       }
     __syncthreads();
     for (uint32_t p = threadIdx.x; p < nb; p += blockDim.x) th[t * nb + p] = (uint16_t)hist[p];
@@ -1634,15 +1960,21 @@ __global__ __launch_bounds__(kHTThreads) void k_sort_prehist(const int64_t *__re
   for (int d = kWave / 2; d > 0; d >>= 1) {
     o |= rj_shfl_xor64((long long)o, d);
     a &= rj_shfl_xor64((long long)a, d);
+    const uint64_t m0 = (uint64_t)rj_shfl_xor64((long long)mn, d), m1 = (uint64_t)rj_shfl_xor64((long long)mx, d);
+    mn = m0 < mn ? m0 : mn;
+    mx = m1 > mx ? m1 : mx;
   }
   if (lane_id() == 0) {
     atomicOr(&orand[0], (unsigned long long)o);
     atomicAnd(&orand[1], (unsigned long long)a);
+    atomicMin(&orand[2], (unsigned long long)mn);
+    atomicMax(&orand[3], (unsigned long long)mx);
   }
 }
 
-// th[t][d] (2^db buckets) from the 10-bit histogram: digits that agree in their low db bits
-__global__ void k_sort_prehist_fold(const uint16_t *__restrict__ th10, int64_t ntiles, int db,
+// th[t][d] (2^db buckets) from the 10-bit histogram of the images: the low db bits of image - sub
+// are d exactly when the image's are (d + sub) mod 2^db (rot = sub mod 2^db)
+__global__ void k_sort_prehist_fold(const uint16_t *__restrict__ th10, int64_t ntiles, int db, uint32_t rot,
                                     uint16_t *__restrict__ th) {
   const uint32_t nb = 1u << db, groups = 1u << (kSPBits - db);
   const int64_t cells = ntiles * nb, stride = (int64_t)gridDim.x * blockDim.x;
@@ -1650,36 +1982,40 @@ __global__ void k_sort_prehist_fold(const uint16_t *__restrict__ th10, int64_t n
     const int64_t t = c / nb;
     const uint32_t d = (uint32_t)(c % nb);
     uint32_t sum = 0;
-    for (uint32_t g = 0; g < groups; ++g) sum += th10[t * (1 << kSPBits) + d + (g << db)];
+    const uint32_t v = (d + rot) & (nb - 1);
+    for (uint32_t g = 0; g < groups; ++g) sum += th10[t * (1 << kSPBits) + v + (g << db)];
     th[c] = (uint16_t)sum;
   }
 }
 
-int64_t radix_sort_prehist_workspace(int64_t n) { return xt_layout(n, 1u << kSPBits).words + 2; }
+int64_t radix_sort_prehist_workspace(int64_t n) { return xt_layout(n, 1u << kSPBits).words + 4; }
 
-uint64_t radix_sort_prehist(const int64_t *keys, int64_t n, uint64_t flip, int64_t *pre_ws, void *stream) {
+uint64_t radix_sort_prehist(const int64_t *keys, int64_t n, uint64_t flip, int64_t *pre_ws, void *stream,
+                            uint64_t *img_min, uint64_t *img_max) {
   hipStream_t s = as_stream(stream);
   const XtLayout L = xt_layout(n, 1u << kSPBits);
   unsigned long long *orand = reinterpret_cast<unsigned long long *>(pre_ws + L.words);
-  const unsigned long long init[2] = {0ull, ~0ull};
+  const unsigned long long init[4] = {0ull, ~0ull, ~0ull, 0ull};
   HIP_CHECK(hipMemcpyAsync(orand, init, sizeof(init), hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_sort_prehist, dim3((unsigned)std::min<int64_t>(L.ntiles, kNumCUs * 16)), dim3(kHTThreads), 0,
                      s, keys, n, flip, L.ntiles, reinterpret_cast<uint16_t *>(pre_ws + L.th), orand);
   HIP_LAUNCH_CHECK();
-  unsigned long long h[2];
+  unsigned long long h[4];
   HIP_CHECK(hipMemcpyAsync(h, orand, sizeof(h), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
+  if (img_min) *img_min = h[2];
+  if (img_max) *img_max = h[3];
   return n <= 1 ? 0ull : (uint64_t)(h[0] ^ h[1]);
 }
 
-void radix_sort_prehist_fold(const int64_t *pre_ws, int64_t n, int db, int64_t *ws, void *stream) {
+void radix_sort_prehist_fold(const int64_t *pre_ws, int64_t n, int db, int64_t *ws, void *stream, uint64_t sub) {
   CYLON_CHECK(db >= 1 && db <= kSPBits, Code::Invalid, "sort prehist fold: digit bits " << db);
   const XtLayout P = xt_layout(n, 1u << kSPBits), L = xt_layout(n, 1u << db);
   const uint16_t *th10 = reinterpret_cast<const uint16_t *>(pre_ws + P.th);
   uint16_t *th = reinterpret_cast<uint16_t *>(ws + L.th);
   const int64_t cells = L.ntiles * (int64_t(1) << db);
   hipLaunchKernelGGL(k_sort_prehist_fold, dim3(grid_for(cells)), dim3(kBlock), 0, as_stream(stream), th10, L.ntiles,
-                     db, th);
+                     db, (uint32_t)(sub & ((1u << db) - 1)), th);
   HIP_LAUNCH_CHECK();
 }
 

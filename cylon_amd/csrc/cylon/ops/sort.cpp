@@ -162,10 +162,11 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
   const char *ph = std::getenv("CYLON_SORT_PREHIST");  // A/B knob: 0 = separate reduction + histogram
   const bool prehist = raw_in && n > 0 && hip::radix_xt_enabled() && !(ph && ph[0] == '0');
   at::Tensor pre_ws;
-  uint64_t diff;
+  uint64_t diff, img_min = 0, img_max = 0;
   if (prehist) {
     pre_ws = ex.empty_i64(hip::radix_sort_prehist_workspace(n));
-    diff = hip::radix_sort_prehist(ptr<int64_t>(kc.data), n, key_xor, ptr<int64_t>(pre_ws), ex.stream);
+    diff = hip::radix_sort_prehist(ptr<int64_t>(kc.data), n, key_xor, ptr<int64_t>(pre_ws), ex.stream, &img_min,
+                                   &img_max);
   } else {
     diff = hip::sort_keys_varying_bits(kc.view(), n, !asc,
                                        raw_in ? nullptr : reinterpret_cast<uint64_t *>(ptr<int64_t>(img)),
@@ -191,7 +192,20 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
   BytePacking bp;
   if (diff != 0) bp = PackByteColumns(ex, cur, widths, n);
   if (diff != 0) {
-    const int lo = __builtin_ctzll(diff), hi = 64 - __builtin_clzll(diff);
+    const int lo = __builtin_ctzll(diff);
+    int hi = 64 - __builtin_clzll(diff);
+    // digits of image - min when the keys span fewer bits than vary (every image agrees with the
+    // minimum below bit lo, so image - min keeps those bits zero); knob CYLON_SORT_SUB_MIN=0
+    const char *sm = std::getenv("CYLON_SORT_SUB_MIN");
+    uint64_t sub = 0;
+    if (prehist && img_max > img_min && !(sm && sm[0] == '0')) {
+      const int hr = 64 - __builtin_clzll(img_max - img_min);
+      if (hr < hi) {
+        sub = img_min;
+        hi = hr;
+        trace::add_counter("sort.radix.sub_min", 1);
+      }
+    }
     const int npass = (hi - lo + 9) / 10;
     std::vector<int> shifts, dbits;
     int max_db = 0;
@@ -206,8 +220,12 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
     // each pass but the last writes the next pass's digits (2 B/row) as it stores the keys: the
     // next pass's tile histogram then reads those instead of the 8-byte keys (XCD-tile passes)
     const char *nde = std::getenv("CYLON_SORT_NEXT_DIGITS");  // A/B knob: 0 = histograms read the keys
-    const bool nd_on = hip::radix_xt_enabled() && npass > 1 && !(nde && nde[0] == '0');
+    // look-back passes (1-2 all-8-byte columns): no tile histograms and no next-digit array at all
+    const bool lb_on = hip::radix_sort_lb_eligible(n, (int)cur.size(), widths.data(), dbits.data(), npass, ex.stream);
+    const bool nd_on = !lb_on && hip::radix_xt_enabled() && npass > 1 && !(nde && nde[0] == '0');
     at::Tensor nd = nd_on ? at::empty({n}, ex.opts(at::kShort)) : at::Tensor();
+    at::Tensor lbws = lb_on ? ex.empty_i64(hip::radix_sort_lb_workspace(n)) : at::Tensor();
+    if (lb_on) trace::add_counter("sort.radix.lookback", 1);
     int shift = lo;
     for (int ps = 0; ps < npass; ++ps) {
       const int db = dbits[ps];
@@ -227,18 +245,25 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
       // pass XORs again (image -> raw); one pass does both (stores the raw key)
       const uint64_t flip = ps == 0 && raw_in ? key_xor : 0ull;
       const bool pre = prehist && ps == 0 && shift == 0 && db <= 10;
-      if (pre) hip::radix_sort_prehist_fold(ptr<int64_t>(pre_ws), n, db, ptr<int64_t>(ws), ex.stream);
+      if (pre) hip::radix_sort_prehist_fold(ptr<int64_t>(pre_ws), n, db, ptr<int64_t>(ws), ex.stream, sub);
       uint16_t *ndp = nd_on ? reinterpret_cast<uint16_t *>(nd.data_ptr()) : nullptr;
+      SortLbArgs lba{};
+      if (lb_on) lba = hip::radix_sort_lb_args(ptr<int64_t>(lbws), n, ps, npass, ex.stream);
       hip::radix_sort_rows_pass(ptr<int64_t>(cur[0]), n, shift, db, in.data(), out.data(), widths.data(),
                                 (int)cur.size(), ptr<int64_t>(ws), ex.stream,
                                 flip ^ (ps + 1 == npass && key_in_last_pass ? key_xor : 0ull), flip, pre,
                                 ps > 0 ? ndp : nullptr, ps + 1 < npass ? ndp : nullptr, shift + db,
-                                ps + 1 < npass ? dbits[ps + 1] : 0);
+                                ps + 1 < npass ? dbits[ps + 1] : 0, sub, lb_on ? &lba : nullptr);
       if (ps == 0) pre_ws = at::Tensor();  // 10-bit tile histogram consumed
       cur = std::move(nxt);
       shift += db;
     }
     cur = UnpackByteColumns(ex, bp, std::move(cur), n);
+    if (lb_on && hip::radix_sort_lb_failed(ptr<int64_t>(lbws), ex.stream)) {  // never expected
+      trace::add_counter("sort.radix.lookback_timeout_fallback", 1);
+      hip::rp_take_order_violation(ex.stream);
+      return nullptr;
+    }
     if (hip::rp_take_order_violation(ex.stream)) {  // ranking guard: index sort instead
       trace::add_counter("sort.radix.order_violation_fallback", 1);
       return nullptr;

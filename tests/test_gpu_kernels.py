@@ -163,6 +163,40 @@ def test_radix_sort_large_int64(gpu_ctx):
     assert torch.equal(s, torch.sort(k).values)
 
 
+@pytest.mark.parametrize("case", ["uniform63", "small_range_ties", "skewed", "desc", "one_chunk"])
+def test_lookback_sort_passes_match_stable_torch_sort(gpu_ctx, monkeypatch, case):
+    """Look-back LSD passes (2 all-8-byte columns: key + payload; chunk plans counted by the previous
+    pass, offsets from a decoupled look-back) vs torch's stable sort; payload order = stability."""
+    n = 5_000_000
+    g = torch.Generator(device="cuda").manual_seed(21)
+    if case in ("uniform63", "desc"):
+        k = torch.randint(-2**62, 2**62, (n,), generator=g, device="cuda")
+    elif case == "small_range_ties":
+        k = torch.randint(-3000, 3000, (n,), generator=g, device="cuda") * 977
+    elif case == "skewed":  # 90 % one key: one chunk / one digit holds most rows (36 bits: 4 x 9-bit digits)
+        k = torch.randint(0, 1 << 36, (n,), generator=g, device="cuda")
+        k[torch.rand(n, generator=g, device="cuda") < 0.9] = 123456789
+    else:  # 3 x 8-bit digits, the first one < 32: every row lands in chunk 0 of the second pass
+        a = torch.randint(0, 32, (n,), generator=g, device="cuda")
+        b = torch.randint(0, 1 << 16, (n,), generator=g, device="cuda")
+        k = ((a | (b << 8)) << 3) + (1 << 50)
+    v = torch.arange(n, device="cuda")
+    t = Table.from_torch(gpu_ctx, {"k": k, "v": v})
+    asc = case != "desc"
+    monkeypatch.setenv("CYLON_RADIX_SORT_MIN_ROWS", "1")
+    C.trace_enable(True)
+    C.trace_reset()
+    out = t.sort("k", ascending=asc).to_torch()
+    torch.cuda.synchronize()
+    c = dict(C.trace_counters())
+    C.trace_enable(False)
+    assert c.get("sort.radix.lookback", 0) == 1, c
+    assert c.get("sort.radix.lookback_timeout_fallback", 0) == 0, c
+    ref_k, idx = torch.sort(k, stable=True, descending=not asc)
+    assert torch.equal(out["k"], ref_k)
+    assert torch.equal(out["v"], v[idx])
+
+
 def _sorted_df(t):
     df = t.to_pandas()
     return df.sort_values(list(df.columns), kind="stable").reset_index(drop=True)
@@ -222,7 +256,7 @@ def test_radix_groupby_matches_global(gpu_ctx, monkeypatch, case):
 
 
 @pytest.mark.parametrize("dtype", ["int64", "float64", "int32", "uint16", "float32", "uint64", "int64_full",
-                                   "int64_equal"])
+                                   "int64_equal", "int64_offset", "int64_offset_odd"])
 @pytest.mark.parametrize("asc", [True, False])
 def test_radix_row_sort_matches_index_sort(gpu_ctx, monkeypatch, dtype, asc):
     """Row-moving LSD sort (all columns through LDS-staged passes) vs index sort + gather; stable on ties.
@@ -239,6 +273,10 @@ def test_radix_row_sort_matches_index_sort(gpu_ctx, monkeypatch, dtype, asc):
         k[4:2000] = k[2000:3996]  # ties
     elif dtype == "int64_equal":
         k = np.full(n, -77, dtype=np.int64)
+    elif dtype == "int64_offset":  # far from zero, low 3 bits constant: digits of image - min from bit 3
+        k = 10**15 + 8 * rng.integers(0, 100_000, n, dtype=np.int64)
+    elif dtype == "int64_offset_odd":  # digits of image - min from bit 0 (the prologue histogram rotated)
+        k = -(10**15) + 12345 + rng.integers(0, 3_000_000, n, dtype=np.int64)
     elif dtype.startswith("float"):
         k = rng.standard_normal(n).astype(dtype)
         k[::101] = np.nan
