@@ -229,9 +229,6 @@ struct TileSched {
   unsigned int *lb_err = nullptr;     // in: set when a look-back wait timed out
   uint32_t *lb_gcnt = nullptr;        // out: [block][8][nbn] (chunk, next digit) counts (LBM & 1)
   int lb_xshift = 0;                  // out: next pass's chunk = this pass's digit >> lb_xshift
-  // in: chunk x only on XCD x, look-back words stored without write-through (they stay in that
-  // XCD's L2, where its CUs' L1-bypassing loads find them); CYLON_SORT_LB_LOCAL=1
-  int lb_local = 0;
 };
 constexpr int kSlotMaxSeg = 4096;
 
@@ -251,7 +248,13 @@ constexpr int kSlotMaxSeg = 4096;
 // claimed in order per chunk, so a tile waits only on tiles already claimed by running blocks; a
 // wait that exceeds kLbSpinLimit polls (never expected) sets lb_err and the sort falls back.
 constexpr int kLbChunks = 8, kLbMaxBuckets = 512;
-constexpr int kLbCnt = 0, kLbC = kLbChunks * kLbMaxBuckets, kLbTP = kLbC + 16, kLbBase = kLbTP + 16,
+// plan[kLbLocal] = 1: chunk x runs only on XCD x and the look-back words are stored without
+// write-through, so they stay in that XCD's L2 where its CUs' L1-bypassing loads find them (a
+// round trip to L2 instead of HBM; 2B-row sort 92.8 -> 83.8 ms, profiles/r04/sort_lookback_ab.txt);
+// 0: any XCD takes a chunk's tiles once its own are done and the words are written through.  The
+// plan chooses local when no chunk exceeds 1.5x the mean (CYLON_SORT_LB_LOCAL=0/1 forces it).
+constexpr int kLbCnt = 0, kLbC = kLbChunks * kLbMaxBuckets, kLbTP = kLbC + 16, kLbLocal = kLbTP + 12,
+              kLbBase = kLbTP + 16,
               kLbTickets = kLbBase + kLbChunks * kLbMaxBuckets, kLbPlanWords = kLbTickets + 16;
 constexpr int kLbSpinLimit = 1 << 20, kLbWindow = 4;
 
@@ -295,7 +298,8 @@ __device__ __forceinline__ int64_t xt_claim(const TileSched &lb, int home, int64
 // look-back passes: first row of the next tile of chunk home (else of another chunk), or n_rows
 __device__ __forceinline__ int64_t lb_claim(const TileSched &lb, const uint32_t *sC, const uint32_t *sTP, int home,
                                             int64_t tile_rows, int64_t n_rows) {
-  for (int k = 0; k < (lb.lb_local ? 1 : kXcds); ++k) {
+  const bool local = sTP[kLbChunks + 1] != 0;  // s_TP[9]: the plan's local flag
+  for (int k = 0; k < (local ? 1 : kXcds); ++k) {
     const int x = (home + k) & (kXcds - 1);
     const uint32_t T = sTP[x + 1] - sTP[x];
     if (T == 0) continue;
@@ -831,7 +835,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
   __shared__ uint64_t ustage[TILE];  // column stage | {wcnt[WAVES][nb] u16 or bcnt[nb] u32, sdig[TILE] u16}
   __shared__ uint32_t wsum[WAVES];
   // look-back: chunk first rows / first tiles; counting: packed 16-bit (chunk, next digit) counters
-  __shared__ uint32_t s_C[LBIN ? kLbChunks + 1 : 1], s_TP[LBIN ? kLbChunks + 1 : 1];
+  __shared__ uint32_t s_C[LBIN ? kLbChunks + 1 : 1], s_TP[LBIN ? kLbChunks + 2 : 1];  // s_TP[9] = local flag
   __shared__ uint32_t lcnt[CNT ? kLbChunks * kLbMaxBuckets / 2 : 1];
   constexpr bool STABLE = RANK != kRankBlockAtomic;
   uint16_t *wcnt = reinterpret_cast<uint16_t *>(ustage);
@@ -855,6 +859,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
     s_C[threadIdx.x] = lb.lb_plan[kLbC + threadIdx.x];
     s_TP[threadIdx.x] = lb.lb_plan[kLbTP + threadIdx.x];
   }
+  if (LBIN && threadIdx.x == kLbChunks + 1) s_TP[kLbChunks + 1] = lb.lb_plan[kLbLocal];
   if (TICKET) {
     if (LBIN) __syncthreads();
     if (threadIdx.x == 0) s_next = LBIN ? lb_claim(lb, s_C, s_TP, xhome, TILE, n) : xt_claim(lb, xhome, TILE, n);
@@ -952,7 +957,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
     const int64_t lgid = LBIN ? (int64_t)s_TP[cx] + ck : 0;  // look-back: the tile's state row
     if (LBIN && (uint32_t)tx < nbuckets) {  // publish this tile's counts (the chunk's first: its prefix)
       const uint32_t v = (ck == 0 ? 0x80000000u : 0u) | (toff[tx + 1] - toff[tx] + 1u);
-      if (lb.lb_local)
+      if (s_TP[kLbChunks + 1])
         __hip_atomic_store(&lb.lb_state[lgid * nbuckets + tx], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       else
         __hip_atomic_store(&lb.lb_state[lgid * nbuckets + tx], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1002,7 +1007,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
             }
           }
         }
-        if (lb.lb_local)
+        if (s_TP[kLbChunks + 1])
           __hip_atomic_store(&lb.lb_state[lgid * nbuckets + tx], 0x80000000u | (excl + own + 1u), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
         else
@@ -1420,7 +1425,7 @@ __global__ __launch_bounds__(256) void k_lb_reduce(const uint32_t *__restrict__ 
 
 // plan of a look-back pass from its (chunk, digit) counts: chunk first rows C, first tiles TP
 // (tiles never straddle chunks) and bases[x][d] = rows of digits < d + rows of digit d in chunks < x
-__global__ __launch_bounds__(kLbMaxBuckets) void k_lb_plan(uint32_t *__restrict__ plan, uint32_t nb) {
+__global__ __launch_bounds__(kLbMaxBuckets) void k_lb_plan(uint32_t *__restrict__ plan, uint32_t nb, int local_mode) {
   __shared__ uint32_t wsum[kLbMaxBuckets / kWave];
   __shared__ uint32_t csz[kLbChunks];
   const uint32_t d = threadIdx.x;
@@ -1450,6 +1455,9 @@ __global__ __launch_bounds__(kLbMaxBuckets) void k_lb_plan(uint32_t *__restrict_
     }
     plan[kLbC + kLbChunks] = r;
     plan[kLbTP + kLbChunks] = t;
+    uint32_t mx = 0;
+    for (int x = 0; x < kLbChunks; ++x) mx = csz[x] > mx ? csz[x] : mx;
+    plan[kLbLocal] = local_mode >= 0 ? (uint32_t)local_mode : (uint64_t)mx * kLbChunks * 2 <= (uint64_t)r * 3 ? 1u : 0u;
   }
 }
 
@@ -1465,7 +1473,9 @@ static void lb_plan_next(const SortLbArgs *lba, int64_t nblk, uint32_t nbn, int6
   hipLaunchKernelGGL(k_lb_reduce, dim3((unsigned)((cells + 255) / 256), kLbReduceSlices), dim3(256), 0, s, lba->gcnt,
                      nblk, cells, lba->plan_out + kLbCnt);
   HIP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_lb_plan, dim3(1), dim3(kLbMaxBuckets), 0, s, lba->plan_out, nbn);
+  const char *lc = std::getenv("CYLON_SORT_LB_LOCAL");  // 0 / 1 force the chunk mode (default: by balance)
+  const int local_mode = lc && (lc[0] == '0' || lc[0] == '1') ? lc[0] - '0' : -1;
+  hipLaunchKernelGGL(k_lb_plan, dim3(1), dim3(kLbMaxBuckets), 0, s, lba->plan_out, nbn, local_mode);
   HIP_LAUNCH_CHECK();
   (void)n;
 }
@@ -1525,8 +1535,6 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
     lb.lb_state = lba->state;
     lb.lb_err = lba->err;
     lb.xt_ticket = const_cast<uint32_t *>(lba->plan_in) + kLbTickets;
-    const char *lc = std::getenv("CYLON_SORT_LB_LOCAL");  // experiment knob, read per pass
-    lb.lb_local = lc && lc[0] == '1';
     g.rows_per_block = kRPTile;
     g.nblocks = std::min<int64_t>(ntiles + kLbChunks, (int64_t)kNumCUs * 2);
   } else if (xt) {  // exact per-tile offsets, tiles claimed in order per XCD (see xt_claim)
@@ -1605,7 +1613,7 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
     if (unstable) lean_kernel<Digit, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
     else lean_kernel<Digit, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt, lbm);
     HIP_LAUNCH_CHECK();
-    if (lbin && lb.lb_local) {
+    if (lbin) {  // local chunks: XCD x had blocks
       hipLaunchKernelGGL(k_lb_check, dim3(1), dim3(kWave), 0, s, lba->plan_in, lba->err);
       HIP_LAUNCH_CHECK();
     }

@@ -163,13 +163,18 @@ def test_radix_sort_large_int64(gpu_ctx):
     assert torch.equal(s, torch.sort(k).values)
 
 
-@pytest.mark.parametrize("case", ["uniform63", "small_range_ties", "skewed", "desc", "one_chunk"])
+@pytest.mark.parametrize("case", ["uniform63", "uniform63_global", "small_range_ties", "skewed", "desc",
+                                  "one_chunk"])
 def test_lookback_sort_passes_match_stable_torch_sort(gpu_ctx, monkeypatch, case):
     """Look-back LSD passes (2 all-8-byte columns: key + payload; chunk plans counted by the previous
-    pass, offsets from a decoupled look-back) vs torch's stable sort; payload order = stability."""
+    pass, offsets from a decoupled look-back) vs torch's stable sort; payload order = stability.
+    Balanced chunks run XCD-local (look-back words in one L2), skewed ones (and uniform63_global,
+    forced) let every XCD take any chunk's tiles with written-through words."""
     n = 5_000_000
     g = torch.Generator(device="cuda").manual_seed(21)
-    if case in ("uniform63", "desc"):
+    if case == "uniform63_global":
+        monkeypatch.setenv("CYLON_SORT_LB_LOCAL", "0")
+    if case in ("uniform63", "uniform63_global", "desc"):
         k = torch.randint(-2**62, 2**62, (n,), generator=g, device="cuda")
     elif case == "small_range_ties":
         k = torch.randint(-3000, 3000, (n,), generator=g, device="cuda") * 977
