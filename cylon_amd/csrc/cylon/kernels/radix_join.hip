@@ -1047,13 +1047,14 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
         for (int k = 0; k < kRPItems; ++k) v[k] = (k * kWave + lane < lim) ? ldw<W8>(ibase, k * kWave + lane, w) : 0ull;
       }
       const uint64_t x = c == 0 ? cols.key_xor : 0ull;
-      if (TICKET && c + 1 == cols.n && tx == 0)
-        s_next = LBIN ? lb_claim(lb, s_C, s_TP, xhome, TILE, n) : xt_claim(lb, xhome, TILE, n);
+      // look-back passes claim their next tile only once this one is written (below): a tile claimed
+      // ahead would publish its counts a whole tile later and stall its successors' look-back
+      if (TICKET && !LBIN && c + 1 == cols.n && tx == 0) s_next = xt_claim(lb, xhome, TILE, n);
 #pragma unroll
       for (int k = 0; k < kRPItems; ++k)
         if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
       __syncthreads();
-      if (TICKET && c + 1 == cols.n) next = s_next;
+      if (TICKET && !LBIN && c + 1 == cols.n) next = s_next;
       if (CNT && c == 0) {  // count (chunk of the next pass, next digit) as the keys are stored
         const int xsh = lb.lb_xshift;
 #pragma unroll
@@ -1090,6 +1091,11 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
     }
     if (!TICKET)
       for (uint32_t p = tx; p < nbuckets; p += THREADS) running[p] += toff[p + 1] - toff[p];
+    if (LBIN) {  // (the column loop ended with a barrier)
+      if (tx == 0) s_next = lb_claim(lb, s_C, s_TP, xhome, TILE, n);
+      __syncthreads();
+      next = s_next;
+    }
     if (CNT && ++since_flush == 7) {  // 7 tiles x 8192 rows fit a 16-bit counter
       lb_flush<THREADS>(lcnt, lb.lb_gcnt + (int64_t)blockIdx.x * (2 * lwords), lwords);
       since_flush = 0;
