@@ -970,52 +970,6 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
       sdig[pos] = (p << 16) | (uint32_t)(wrow + k * kWave + lane);
       pl[k] = pos;
     }
-    if (LBIN && (uint32_t)tx < nbuckets) {  // look back over the chunk's earlier tiles
-      const uint32_t own = toff[tx + 1] - toff[tx];
-      uint32_t excl = 0;
-      if (ck > 0) {
-        // windowed walk: the next kLbWindow predecessors' words are loaded together (one round trip
-        // per window instead of per tile; a walk is a few tiles long: those claimed just before)
-        const int64_t lo = (int64_t)s_TP[cx];  // the chunk's first tile (always an inclusive prefix)
-        int64_t j = lgid - 1;
-        for (int spin = 0;;) {
-          uint32_t w[kLbWindow];
-#pragma unroll
-          for (int i = 0; i < kLbWindow; ++i)
-            w[i] = j - i >= lo ? __hip_atomic_load(&lb.lb_state[(j - i) * nbuckets + tx], __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT)
-                               : 0u;
-          int used = 0;
-          bool done = false;
-#pragma unroll
-          for (int i = 0; i < kLbWindow; ++i) {
-            if (done || used < i || w[i] == 0u) continue;  // stop at the first word not yet published
-            excl += (w[i] & 0x7fffffffu) - 1u;
-            used = i + 1;
-            done = (w[i] & 0x80000000u) != 0u;
-          }
-          if (done) break;
-          j -= used;
-          if (used == 0) {  // the nearest predecessor has not published yet
-            __builtin_amdgcn_s_sleep(1);
-            // give up after kLbSpinLimit polls, or at once after any other wait gave up (the result
-            // is discarded then, so the grid only has to drain)
-            if (++spin > kLbSpinLimit ||
-                ((spin & 255) == 0 && __hip_atomic_load(lb.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-              atomicOr(lb.lb_err, 1u);
-              break;
-            }
-          }
-        }
-        if (s_TP[kLbChunks + 1])
-          __hip_atomic_store(&lb.lb_state[lgid * nbuckets + tx], 0x80000000u | (excl + own + 1u), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-        else
-          __hip_atomic_store(&lb.lb_state[lgid * nbuckets + tx], 0x80000000u | (excl + own + 1u), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      }
-      running[tx] = (int64_t)lb.lb_plan[kLbBase + cx * nbuckets + tx] + excl;
-    }
     if (XT && !LBIN && (uint32_t)tx < nbuckets) running[tx] = xoff;
     __syncthreads();
     uint32_t dp[kRPItems];  // sorted slot j = tx + q * THREADS -> digit << 16 | offset in its run
@@ -1055,6 +1009,55 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
         if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
       __syncthreads();
       if (TICKET && !LBIN && c + 1 == cols.n) next = s_next;
+      // look back over the chunk's earlier tiles only now that the keys are staged: the predecessors
+      // have had this tile's ranking AND staging time to publish their prefixes (fewer round trips)
+      if (LBIN && c == 0 && (uint32_t)tx < nbuckets) {
+        const uint32_t own = toff[tx + 1] - toff[tx];
+        uint32_t excl = 0;
+        if (ck > 0) {
+          // windowed walk: the next kLbWindow predecessors' words are loaded together (one round trip
+          // per window instead of per tile; a walk is a few tiles long: those claimed just before)
+          const int64_t lo = (int64_t)s_TP[cx];  // the chunk's first tile (always an inclusive prefix)
+          int64_t j = lgid - 1;
+          for (int spin = 0;;) {
+            uint32_t w[kLbWindow];
+#pragma unroll
+            for (int i = 0; i < kLbWindow; ++i)
+              w[i] = j - i >= lo ? __hip_atomic_load(&lb.lb_state[(j - i) * nbuckets + tx], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)
+                                 : 0u;
+            int used = 0;
+            bool done = false;
+#pragma unroll
+            for (int i = 0; i < kLbWindow; ++i) {
+              if (done || used < i || w[i] == 0u) continue;  // stop at the first word not yet published
+              excl += (w[i] & 0x7fffffffu) - 1u;
+              used = i + 1;
+              done = (w[i] & 0x80000000u) != 0u;
+            }
+            if (done) break;
+            j -= used;
+            if (used == 0) {  // the nearest predecessor has not published yet
+              __builtin_amdgcn_s_sleep(1);
+              // give up after kLbSpinLimit polls, or at once after any other wait gave up (the result
+              // is discarded then, so the grid only has to drain)
+              if (++spin > kLbSpinLimit ||
+                  ((spin & 255) == 0 && __hip_atomic_load(lb.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                atomicOr(lb.lb_err, 1u);
+                break;
+              }
+            }
+          }
+          if (s_TP[kLbChunks + 1])
+            __hip_atomic_store(&lb.lb_state[lgid * nbuckets + tx], 0x80000000u | (excl + own + 1u), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          else
+            __hip_atomic_store(&lb.lb_state[lgid * nbuckets + tx], 0x80000000u | (excl + own + 1u), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        running[tx] = (int64_t)lb.lb_plan[kLbBase + cx * nbuckets + tx] + excl;
+      }
+      if (LBIN && c == 0) __syncthreads();
       if (CNT && c == 0) {  // count (chunk of the next pass, next digit) as the keys are stored
         const int xsh = lb.lb_xshift;
 #pragma unroll
