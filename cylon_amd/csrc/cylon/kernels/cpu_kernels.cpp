@@ -272,22 +272,26 @@ void key64_from_column(const ColView &col, int64_t n, int64_t *out, void *) {
 }
 
 void composite_key_pack(const ColView *cols, int nk, const int64_t *lo, const int *shift, int64_t n, int64_t *out,
-                        void *) {
+                        const int64_t *ncode, void *) {
   for (int64_t i = 0; i < n; ++i) {
     uint64_t acc = 0;
-    for (int k = 0; k < nk; ++k)
-      acc |= (uint64_t)(extend_bits(load_bits(cols[k].data, i, cols[k].width), cols[k].width, cols[k].kind) - lo[k])
-             << shift[k];
+    for (int k = 0; k < nk; ++k) {
+      uint64_t f = (uint64_t)(extend_bits(load_bits(cols[k].data, i, cols[k].width), cols[k].width, cols[k].kind) - lo[k]);
+      if (ncode && ncode[k] >= 0 && cols[k].valid && !cols[k].valid[i]) f = (uint64_t)ncode[k];
+      acc |= f << shift[k];
+    }
     out[i] = (int64_t)acc;
   }
 }
 
 void composite_key_unpack(const int64_t *key, int64_t n, int nk, const int64_t *lo, const int *shift, const int *bits,
-                          const MutColView *out, void *) {
+                          const MutColView *out, const int64_t *ncode, void *) {
   for (int k = 0; k < nk; ++k) {
     const uint64_t mask = bits[k] >= 64 ? ~0ull : ((1ull << bits[k]) - 1);
     for (int64_t i = 0; i < n; ++i) {
-      const uint64_t x = (uint64_t)lo[k] + (((uint64_t)key[i] >> shift[k]) & mask);
+      const uint64_t f = ((uint64_t)key[i] >> shift[k]) & mask;
+      if (ncode && ncode[k] >= 0 && f == (uint64_t)ncode[k] && out[k].valid) out[k].valid[i] = 0;
+      const uint64_t x = (uint64_t)lo[k] + f;
       std::memcpy(out[k].data + i * out[k].width, &x, out[k].width);  // little endian: the low bytes
     }
   }

@@ -300,6 +300,7 @@ struct CompositeSpec {
   MutColView o[kMaxCompositeKeys];
   int64_t lo[kMaxCompositeKeys];
   uint64_t mask[kMaxCompositeKeys];
+  int64_t ncode[kMaxCompositeKeys];  // field value of a null (-1: the column has no nulls)
   int shift[kMaxCompositeKeys];
 };
 
@@ -309,9 +310,11 @@ __global__ void k_composite_pack(CompositeSpec s, int64_t n, int64_t *__restrict
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     uint64_t acc = 0;
 #pragma unroll
-    for (int k = 0; k < NK; ++k)
-      acc |= (uint64_t)(extend_bits(load_bits(s.c[k].data, i, s.c[k].width), s.c[k].width, s.c[k].kind) - s.lo[k])
-             << s.shift[k];
+    for (int k = 0; k < NK; ++k) {
+      uint64_t f = (uint64_t)(extend_bits(load_bits(s.c[k].data, i, s.c[k].width), s.c[k].width, s.c[k].kind) - s.lo[k]);
+      if (s.ncode[k] >= 0 && s.c[k].valid && !s.c[k].valid[i]) f = (uint64_t)s.ncode[k];
+      acc |= f << s.shift[k];
+    }
     out[i] = (int64_t)acc;
   }
 }
@@ -323,7 +326,9 @@ __global__ void k_composite_unpack(CompositeSpec s, int64_t n, const int64_t *__
     const uint64_t v = (uint64_t)key[i];
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
-      const uint64_t x = (uint64_t)s.lo[k] + ((v >> s.shift[k]) & s.mask[k]);
+      const uint64_t f = (v >> s.shift[k]) & s.mask[k];
+      if (s.ncode[k] >= 0 && f == (uint64_t)s.ncode[k] && s.o[k].valid) s.o[k].valid[i] = 0;
+      const uint64_t x = (uint64_t)s.lo[k] + f;
       switch (s.o[k].width) {
         case 1: s.o[k].data[i] = (uint8_t)x; break;
         case 2: reinterpret_cast<uint16_t *>(s.o[k].data)[i] = (uint16_t)x; break;
@@ -334,11 +339,13 @@ __global__ void k_composite_unpack(CompositeSpec s, int64_t n, const int64_t *__
   }
 }
 
-static CompositeSpec composite_spec(int nk, const int64_t *lo, const int *shift, const int *bits) {
+static CompositeSpec composite_spec(int nk, const int64_t *lo, const int *shift, const int *bits,
+                                    const int64_t *ncode) {
   CYLON_CHECK(nk >= 1 && nk <= kMaxCompositeKeys, Code::Invalid, "composite key of " << nk << " columns");
   CompositeSpec s;
   for (int k = 0; k < nk; ++k) {
     s.lo[k] = lo[k];
+    s.ncode[k] = ncode ? ncode[k] : -1;
     s.shift[k] = shift[k];
     s.mask[k] = bits ? (bits[k] >= 64 ? ~0ull : ((1ull << bits[k]) - 1)) : 0;
   }
@@ -354,18 +361,18 @@ static CompositeSpec composite_spec(int nk, const int64_t *lo, const int *shift,
   }
 
 void composite_key_pack(const ColView *cols, int nk, const int64_t *lo, const int *shift, int64_t n, int64_t *out,
-                        void *stream) {
+                        const int64_t *ncode, void *stream) {
   if (n == 0) return;
-  CompositeSpec s = composite_spec(nk, lo, shift, nullptr);
+  CompositeSpec s = composite_spec(nk, lo, shift, nullptr, ncode);
   for (int k = 0; k < nk; ++k) s.c[k] = cols[k];
   CYLON_NK_SWITCH(nk, k_composite_pack, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), s, n, out);
   HIP_LAUNCH_CHECK();
 }
 
 void composite_key_unpack(const int64_t *key, int64_t n, int nk, const int64_t *lo, const int *shift, const int *bits,
-                          const MutColView *out, void *stream) {
+                          const MutColView *out, const int64_t *ncode, void *stream) {
   if (n == 0) return;
-  CompositeSpec s = composite_spec(nk, lo, shift, bits);
+  CompositeSpec s = composite_spec(nk, lo, shift, bits, ncode);
   for (int k = 0; k < nk; ++k) s.o[k] = out[k];
   CYLON_NK_SWITCH(nk, k_composite_unpack, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), s, n, key);
   HIP_LAUNCH_CHECK();

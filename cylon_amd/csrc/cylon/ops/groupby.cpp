@@ -258,6 +258,8 @@ struct GroupKey {
   std::vector<int64_t> lo;      // composite: per-column minimum
   std::vector<int> shift, bits; // composite: bit range of each column
   bool composite = false, fbits = false;
+  bool null_group = false;  // nullable single integer key: null rows carry null_key (no valid key has it)
+  int64_t null_key = 0;
 };
 }  // namespace
 
@@ -271,13 +273,29 @@ static bool group_key(const Exec &ex, const TablePtr &t, const std::vector<int> 
   const int64_t n = t->Rows();
   if (keys.size() == 1) {
     const Column &kc = t->column(keys[0]);
-    if (!simple_key(kc)) return false;
-    if (kc.type.kind() == ValueKind::SIGNED_INT || kc.type.kind() == ValueKind::UNSIGNED_INT) {
+    const bool int_key = kc.type.kind() == ValueKind::SIGNED_INT || kc.type.kind() == ValueKind::UNSIGNED_INT;
+    // a nullable integer key: its null rows form one group (as on the global path) under a key value
+    // no valid row has -- one below the smallest valid key, or one above the largest
+    const bool nullable_int = int_key && kc.nullable() && !kc.is_var() && kc.type.width() <= 8 &&
+                              kc.data.element_size() == kc.type.width();
+    if (!simple_key(kc) && !nullable_int) return false;
+    if (int_key) {
       if (kc.type.width() == 8) {
         g.k = kc.data.view(at::kLong);
       } else {
         g.k = ex.empty_i64(n);
         hip::key64_from_column(kc.view(), n, ptr<int64_t>(g.k), ex.stream);
+      }
+      if (nullable_int) {
+        const at::Tensor valid = kc.validity.slice(0, 0, n).ne(0);
+        const at::Tensor lim = at::cat({at::where(valid, g.k, std::numeric_limits<int64_t>::max()).min().reshape({1}),
+                                        at::where(valid, g.k, std::numeric_limits<int64_t>::min()).max().reshape({1})});
+        const std::vector<int64_t> h = to_host_vec(lim);
+        if (h[0] > std::numeric_limits<int64_t>::min()) g.null_key = h[0] - 1;
+        else if (h[1] < std::numeric_limits<int64_t>::max()) g.null_key = h[1] + 1;
+        else return false;  // every int64 value is a key: no free value for the null group
+        g.k = at::where(valid, g.k, g.null_key);
+        g.null_group = true;
       }
       return true;
     }
@@ -323,7 +341,8 @@ static bool group_key(const Exec &ex, const TablePtr &t, const std::vector<int> 
   // one fused pass (composite_key_pack: each key column read once at its own width)
   g.k = ex.empty_i64(n);
   std::vector<ColView> v = views(t, keys);
-  KCALL(ex, composite_key_pack, v.data(), (int)keys.size(), g.lo.data(), g.shift.data(), n, ptr<int64_t>(g.k));
+  KCALL(ex, composite_key_pack, v.data(), (int)keys.size(), g.lo.data(), g.shift.data(), n, ptr<int64_t>(g.k),
+        nullptr);
   g.composite = true;
   return true;
 }
@@ -345,7 +364,12 @@ static std::vector<Column> group_key_columns(const TablePtr &t, const GroupKey &
   at::Tensor v = gk;
   if (g.fbits) v = gk.view(at::kDouble).to(kc.data.scalar_type());
   else if (kc.type.width() != 8) v = gk.to(kc.data.scalar_type());
-  out.emplace_back(kc.name, kc.type, ng, v.contiguous());
+  at::Tensor valid;
+  if (g.null_group) {  // the null group's key slot: value unspecified, validity 0
+    valid = gk.ne(g.null_key).to(at::kByte);
+    v = at::where(valid.to(at::kBool), v, at::zeros({1}, v.options()));
+  }
+  out.emplace_back(kc.name, kc.type, ng, v.contiguous(), at::Tensor(), valid);
   return out;
 }
 

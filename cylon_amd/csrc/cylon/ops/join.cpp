@@ -831,11 +831,21 @@ struct RadixKeys {
   bool composite = false;  // l / r are exact composites: key column i = lo[i] + ((key >> shift[i]) & 2^bits[i]-1)
   std::vector<int64_t> lo;
   std::vector<int> shift, bits;
+  std::vector<int64_t> ncode;  // composite: field value of a null in key i (-1: no nulls on either side)
+  bool nulls = false;
 };
 
 static bool int_key(const Column &c) {
   return simple_key(c) && (c.type.kind() == ValueKind::SIGNED_INT ||
                            (c.type.kind() == ValueKind::UNSIGNED_INT && c.type.width() < 8));
+}
+
+// an integer key column that may hold nulls (fixed width <= 8, dense storage): packable into an exact
+// composite with one field value reserved for null, so nulls match nulls (docs/semantics.md)
+static bool nullable_int_key(const Column &c) {
+  return c.nullable() && !c.is_var() && c.type.kind() != ValueKind::FIXED_BYTES && c.type.width() <= 8 &&
+         c.data.element_size() == c.type.width() &&
+         (c.type.kind() == ValueKind::SIGNED_INT || (c.type.kind() == ValueKind::UNSIGNED_INT && c.type.width() < 8));
 }
 
 static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
@@ -844,18 +854,23 @@ static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr
   RadixKeys k;
   if (lc.size() == 1) {
     const Column &a = left->column(lc[0]), &b = right->column(rc[0]);
-    if (!(simple_key(a) && simple_key(b) && a.type == b.type)) return k;
-    k.l = encode_keys(ex, left, lc, true).keys;
-    k.r = encode_keys(ex, right, rc, true).keys;
-    k.ok = true;
-    return k;
+    if (simple_key(a) && simple_key(b) && a.type == b.type) {
+      k.l = encode_keys(ex, left, lc, true).keys;
+      k.r = encode_keys(ex, right, rc, true).keys;
+      k.ok = true;
+      return k;
+    }
   }
   bool packable = lc.size() <= (size_t)kMaxCompositeKeys;
   for (size_t i = 0; i < lc.size(); ++i) {
     const Column &a = left->column(lc[i]), &b = right->column(rc[i]);
-    if (!simple_key(a) || !simple_key(b) || !(a.type == b.type)) return k;
-    packable = packable && int_key(a);
+    if (!(a.type == b.type)) return k;
+    const bool na = nullable_int_key(a), nb = nullable_int_key(b);
+    if ((!simple_key(a) && !na) || (!simple_key(b) && !nb)) return k;
+    k.nulls = k.nulls || na || nb;
+    packable = packable && (int_key(a) || na) && (int_key(b) || nb);
   }
+  if (k.nulls && !packable) return k;  // nullable keys only as an exact composite
   k.ok = true;
   if (packable) {
     // per-key span over both relations (signed / byte storage: min / max of the column itself,
@@ -864,6 +879,13 @@ static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr
       if (c.data.numel() == 0)
         return at::tensor({std::numeric_limits<int64_t>::max(), std::numeric_limits<int64_t>::min()},
                           ex.opts(at::kLong));
+      if (c.nullable()) {  // over the valid rows only (all null: an empty span)
+        at::Tensor x = ex.empty_i64(t->Rows());
+        hip::key64_from_column(c.view(), t->Rows(), ptr<int64_t>(x), ex.stream);
+        const at::Tensor valid = c.validity.slice(0, 0, t->Rows()).ne(0);
+        return at::stack({at::where(valid, x, std::numeric_limits<int64_t>::max()).min(),
+                          at::where(valid, x, std::numeric_limits<int64_t>::min()).max()});
+      }
       const bool direct = c.type.kind() == ValueKind::SIGNED_INT || c.type.width() == 1;
       at::Tensor x = direct ? c.data : encode_keys(ex, t, {col}, true).keys;
       auto m2 = at::aminmax(x);
@@ -879,16 +901,24 @@ static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr
     k.lo.resize(nk);
     k.bits.resize(nk);
     k.shift.resize(nk);
+    k.ncode.assign(nk, -1);
     int total = 0;
     for (size_t i = 0; i < nk; ++i) {
       k.lo[i] = std::min(h[4 * i], h[4 * i + 2]);
       const int64_t hi = std::max(h[4 * i + 1], h[4 * i + 3]);
-      const uint64_t span = hi >= k.lo[i] ? (uint64_t)hi - (uint64_t)k.lo[i] : 0;
+      if (hi < k.lo[i]) k.lo[i] = 0;  // no valid key on either side
+      uint64_t span = hi >= k.lo[i] ? (uint64_t)hi - (uint64_t)k.lo[i] : 0;
+      if (left->column(lc[i]).nullable() || right->column(rc[i]).nullable()) {
+        if (span >= (uint64_t)std::numeric_limits<int64_t>::max()) return k.ok = false, k;  // no free field value
+        k.ncode[i] = (int64_t)span + 1;  // one past the largest valid field
+        span += 1;
+      }
       int b = 0;
       while (b < 64 && (span >> b) != 0) ++b;
       k.bits[i] = b;
       total += b;
     }
+    if (total > 63 && k.nulls) return k.ok = false, k;  // nullable keys only as an exact composite
     if (total <= 63) {  // exact: key i occupies its own bit range (the last key the lowest bits)
       for (size_t i = nk, sh = 0; i-- > 0;) {
         k.shift[i] = (int)sh;
@@ -897,7 +927,8 @@ static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr
       auto pack = [&](const TablePtr &t, const std::vector<int> &cols) {
         std::vector<ColView> v = views(t, cols);
         at::Tensor out = ex.empty_i64(t->Rows());
-        KCALL(ex, composite_key_pack, v.data(), (int)nk, k.lo.data(), k.shift.data(), t->Rows(), ptr<int64_t>(out));
+        KCALL(ex, composite_key_pack, v.data(), (int)nk, k.lo.data(), k.shift.data(), t->Rows(), ptr<int64_t>(out),
+              k.nulls ? k.ncode.data() : nullptr);
         return out;
       };
       k.l = pack(left, lc);
@@ -1001,6 +1032,10 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
         Column o = make_fixed_column(prefix + kc.name, kc.type, img.length, ex.device, false);
         o.validity = img.validity;
         MutColView v;
+        if (k.ncode[i] >= 0) {  // nulls come back where the field holds the null code (own validity)
+          o.validity = img.validity.defined() ? img.validity.clone() : at::ones({img.length}, ex.opts(at::kByte));
+          v.valid = img.length ? o.validity.data_ptr<uint8_t>() : nullptr;
+        }
         v.data = reinterpret_cast<uint8_t *>(ptr<uint8_t>(o.data.view(at::kByte)));
         v.width = kc.type.width();
         v.kind = static_cast<int>(kc.type.kind());
@@ -1008,7 +1043,7 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
         cols[keys[i]] = std::move(o);
       }
       KCALL(ex, composite_key_unpack, ptr<int64_t>(img.data), img.length, (int)keys.size(), k.lo.data(),
-            k.shift.data(), k.bits.data(), mv.data());
+            k.shift.data(), k.bits.data(), mv.data(), k.nulls ? k.ncode.data() : nullptr);
       trace::add_counter("join.radix.composite_unpacked", (int64_t)keys.size());
     }
     if (!var) return cols;

@@ -235,19 +235,23 @@ def test_radix_join_matches_global_table_join(gpu_ctx, monkeypatch, case):
     pd.testing.assert_frame_equal(_sorted_df(got), _sorted_df(ref))
 
 
-@pytest.mark.parametrize("case", ["int64_many_groups", "int32_nullable", "few_groups", "min_key", "wide_aggs"])
+@pytest.mark.parametrize("case", ["int64_many_groups", "int32_nullable", "few_groups", "min_key", "wide_aggs",
+                                  "null_keys", "null_keys_int16"])
 def test_radix_groupby_matches_global(gpu_ctx, monkeypatch, case):
     """K8 LDS radix group-by (HLL sizing, partitioned LDS aggregation) vs the global-table path."""
     rng = np.random.default_rng(5)
     n = 400_000
     groups = {"int64_many_groups": 150_000, "int32_nullable": 20_000, "few_groups": 7, "min_key": 5000,
-              "wide_aggs": 3000}[case]
+              "wide_aggs": 3000, "null_keys": 40_000, "null_keys_int16": 300}[case]
     k = rng.integers(-groups, groups, n)
     if case == "min_key":
         k[::97] = np.iinfo(np.int64).min
-    kt = pa.int32() if case == "int32_nullable" else pa.int64()
+    kt = {"int32_nullable": pa.int32(), "null_keys_int16": pa.int16()}.get(case, pa.int64())
     fmask = rng.random(n) < 0.1 if case == "int32_nullable" else None
-    t = pa.table({"k": pa.array(k, kt), "f": pa.array(rng.standard_normal(n), mask=fmask),
+    kmask = rng.random(n) < 0.05 if case.startswith("null_keys") else None  # null keys: one group
+    if case == "null_keys":
+        k[:3] = [np.iinfo(np.int64).min, 7, 0]  # the null group goes above the max (INT64_MIN is a key)
+    t = pa.table({"k": pa.array(k, kt, mask=kmask), "f": pa.array(rng.standard_normal(n), mask=fmask),
                   "i": pa.array(rng.integers(-1000, 1000, n), pa.int32())})
     T = Table(t, gpu_ctx)
     aggs = {"f": ["sum", "count", "min", "max", "mean"], "i": ["sum", "min"]} if case == "wide_aggs" else \
@@ -255,7 +259,13 @@ def test_radix_groupby_matches_global(gpu_ctx, monkeypatch, case):
     res = []
     for thr in ("1", str(1 << 62)):
         monkeypatch.setenv("CYLON_RADIX_GROUPBY_MIN_ROWS", thr)
+        C.trace_enable(True)
+        C.trace_reset()
         df = T.local_groupby("k", aggs).to_pandas()
+        c = dict(C.trace_counters())
+        C.trace_enable(False)
+        if thr == "1" and case.startswith("null_keys"):
+            assert c.get("groupby.radix.groups", 0) > 0, c  # the radix path took the nullable key
         res.append(df.sort_values("k").reset_index(drop=True))
     pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-9, atol=1e-9)
 

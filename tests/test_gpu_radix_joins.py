@@ -49,6 +49,35 @@ def test_radix_outer_join_matches_cpu(gpu_ctx, ctx, monkeypatch, how, left_small
 
 
 @pytest.mark.parametrize("how", ["inner", "left", "outer"])
+@pytest.mark.parametrize("nkeys", [1, 2])
+def test_radix_join_nullable_int_keys(gpu_ctx, ctx, monkeypatch, how, nkeys):
+    """Nullable integer keys join on the radix path as an exact composite whose null code (one past
+    the largest valid field) makes nulls match nulls, as on the CPU twin (docs/semantics.md); the
+    unpacked key columns come back null there."""
+    rng = np.random.default_rng(16)
+    n = 300_000
+
+    def side(seed_off):
+        k = rng.integers(-50_000, 150_000, n)
+        km = np.zeros(n, bool)
+        km[rng.choice(n, 40, replace=False)] = True  # 40 null keys a side: 1600 null-null rows
+        cols = {"k": pa.array(k, mask=km)}
+        if nkeys == 2:
+            g = rng.integers(0, 4, n).astype(np.int16)
+            gm = np.zeros(n, bool)
+            gm[rng.choice(n, 25, replace=False)] = True
+            cols["g"] = pa.array(g, mask=gm)
+        cols["v" if seed_off == 0 else "w"] = rng.random(n)
+        return pa.table(cols)
+
+    a, b = side(0), side(1)
+    got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["k", "g"][:nkeys], monkeypatch)
+    assert c.get("join.radix.composite_key", 0) == 1, c
+    assert list(got.columns) == list(exp.columns)
+    pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
+
+
+@pytest.mark.parametrize("how", ["inner", "left", "outer"])
 def test_radix_join_composite_two_keys(gpu_ctx, ctx, monkeypatch, how):
     """Two int keys -> one exact composite (composite_key_pack); the proxy tables carry it in place
     of the key columns and composite_key_unpack rebuilds them (null where the side is absent)."""
