@@ -260,6 +260,7 @@ struct GroupKey {
   bool composite = false, fbits = false;
   bool null_group = false;  // nullable single integer key: null rows carry null_key (no valid key has it)
   int64_t null_key = 0;
+  std::vector<int64_t> ncode;  // composite: field value of a null in key i (-1: the column has no nulls)
 };
 }  // namespace
 
@@ -309,9 +310,23 @@ static bool group_key(const Exec &ex, const TablePtr &t, const std::vector<int> 
   }
   std::vector<at::Tensor> mm;
   if ((int)keys.size() > kMaxCompositeKeys) return false;
+  bool any_null = false;
   for (int c : keys) {
     const Column &kc = t->column(c);
-    if (!gb_int_key(kc)) return false;
+    const bool nullable_int = kc.nullable() && !kc.is_var() && kc.type.width() <= 8 &&
+                              kc.data.element_size() == kc.type.width() &&
+                              (kc.type.kind() == ValueKind::SIGNED_INT ||
+                               (kc.type.kind() == ValueKind::UNSIGNED_INT && kc.type.width() < 8));
+    if (!gb_int_key(kc) && !nullable_int) return false;
+    if (nullable_int) {  // span over the valid rows (a null takes the field value one past it)
+      any_null = true;
+      at::Tensor k = ex.empty_i64(n);
+      hip::key64_from_column(kc.view(), n, ptr<int64_t>(k), ex.stream);
+      const at::Tensor valid = kc.validity.slice(0, 0, n).ne(0);
+      mm.push_back(at::where(valid, k, std::numeric_limits<int64_t>::max()).min().reshape({1}));
+      mm.push_back(at::where(valid, k, std::numeric_limits<int64_t>::min()).max().reshape({1}));
+      continue;
+    }
     // span: min / max of the column itself (signed or byte storage), else of its 64-bit image
     const bool direct = kc.type.kind() == ValueKind::SIGNED_INT || kc.type.width() == 1;
     at::Tensor k = direct ? kc.data : ex.empty_i64(n);
@@ -325,9 +340,16 @@ static bool group_key(const Exec &ex, const TablePtr &t, const std::vector<int> 
   g.lo.resize(keys.size());
   g.bits.resize(keys.size());
   g.shift.resize(keys.size());
+  g.ncode.assign(keys.size(), -1);
   for (size_t i = 0; i < keys.size(); ++i) {
     g.lo[i] = h[2 * i];
-    const uint64_t span = (uint64_t)h[2 * i + 1] - (uint64_t)h[2 * i];
+    if (h[2 * i + 1] < h[2 * i]) g.lo[i] = 0;  // every key of the column null
+    uint64_t span = h[2 * i + 1] >= h[2 * i] ? (uint64_t)h[2 * i + 1] - (uint64_t)h[2 * i] : 0;
+    if (t->column(keys[i]).nullable()) {
+      if (span >= (uint64_t)std::numeric_limits<int64_t>::max()) return false;
+      g.ncode[i] = (int64_t)span + 1;
+      span += 1;
+    }
     int b = 0;
     while (b < 64 && (span >> b) != 0) ++b;
     g.bits[i] = b;
@@ -342,7 +364,7 @@ static bool group_key(const Exec &ex, const TablePtr &t, const std::vector<int> 
   g.k = ex.empty_i64(n);
   std::vector<ColView> v = views(t, keys);
   KCALL(ex, composite_key_pack, v.data(), (int)keys.size(), g.lo.data(), g.shift.data(), n, ptr<int64_t>(g.k),
-        nullptr);
+        any_null ? g.ncode.data() : nullptr);
   g.composite = true;
   return true;
 }
@@ -355,8 +377,13 @@ static std::vector<Column> group_key_columns(const TablePtr &t, const GroupKey &
     for (size_t i = 0; i < g.cols.size(); ++i) {
       const Column &kc = t->column(g.cols[i]);
       const int64_t mask = g.bits[i] >= 63 ? std::numeric_limits<int64_t>::max() : (int64_t(1) << g.bits[i]) - 1;
-      at::Tensor v = at::bitwise_and(at::bitwise_right_shift(gk, (int64_t)g.shift[i]), mask) + g.lo[i];
-      out.emplace_back(kc.name, kc.type, ng, v.to(kc.data.scalar_type()).contiguous());
+      const at::Tensor f = at::bitwise_and(at::bitwise_right_shift(gk, (int64_t)g.shift[i]), mask);
+      at::Tensor v = f + g.lo[i], valid;
+      if (g.ncode[i] >= 0) {  // the null code: a null key, value unspecified
+        valid = f.ne(g.ncode[i]).to(at::kByte);
+        v = at::where(valid.to(at::kBool), v, at::zeros({1}, v.options()));
+      }
+      out.emplace_back(kc.name, kc.type, ng, v.to(kc.data.scalar_type()).contiguous(), at::Tensor(), valid);
     }
     return out;
   }

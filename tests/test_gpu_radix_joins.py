@@ -224,21 +224,24 @@ def _groupby_both(T, keys, aggs, monkeypatch):
     return res, counters
 
 
-@pytest.mark.parametrize("case", ["var_std", "two_keys", "float_key", "two_keys_var"])
+@pytest.mark.parametrize("case", ["var_std", "two_keys", "float_key", "two_keys_var", "two_keys_nulls"])
 def test_radix_groupby_extended(gpu_ctx, monkeypatch, case):
     """VAR / STDDEV through the M2 accumulator (second in-block pass over a partition's rows), two
     integer keys through an exact composite key, a float key through canonical bits -- against
     the global-table path."""
     rng = np.random.default_rng(12)
     n = 600_000
-    t = pa.table({"k": rng.integers(0, 50_000, n), "g": rng.integers(-4, 4, n).astype(np.int16),
+    nulls = case == "two_keys_nulls"  # nullable keys: a null code per key field of the composite
+    t = pa.table({"k": pa.array(rng.integers(0, 50_000, n), mask=(rng.random(n) < 0.01) if nulls else None),
+                  "g": pa.array(rng.integers(-4, 4, n).astype(np.int16), mask=(rng.random(n) < 0.02) if nulls else None),
                   "x": pa.array(rng.standard_normal(n) + 100.0, mask=rng.random(n) < 0.05),
                   "f": np.round(rng.standard_normal(n), 1)})
     T = Table(t, gpu_ctx)
     keys, aggs = {"var_std": (["k"], {"x": ["sum", "mean", "std"]}),
                   "two_keys": (["k", "g"], {"x": ["sum", "max"], "f": ["count"]}),
                   "float_key": (["f"], {"x": ["sum", "min"], "k": ["max"]}),
-                  "two_keys_var": (["k", "g"], {"x": ["var", "mean"]})}[case]
+                  "two_keys_var": (["k", "g"], {"x": ["var", "mean"]}),
+                  "two_keys_nulls": (["k", "g"], {"x": ["sum", "count"], "f": ["max"]})}[case]
     res, cnt = _groupby_both(T, keys, aggs, monkeypatch)
     assert cnt[0].get("groupby.radix.groups", 0) == len(res[0]), cnt[0]
     if len(keys) > 1:
