@@ -3,7 +3,7 @@
 # command twice and once with --verify, config 4/5 suite numbers.
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/r04final
+O=gpurun_out/${R04_FINAL_DIR:-r04final}
 mkdir -p $O
 export TMPDIR=/tmp
 . tools/gpu/lib.sh
