@@ -126,6 +126,10 @@ struct PartDigit {
   uint32_t mask;
   __device__ __forceinline__ uint32_t of_key(int64_t k) const { return (part_of(k, bits) >> shift) & mask; }
   __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key(keys[i]); }
+  // look-back counting: the next pass's digit of a stored key
+  __device__ __forceinline__ uint32_t next_of(uint64_t stored, int nshift, uint32_t nmask, uint64_t) const {
+    return (part_of((int64_t)stored, bits) >> nshift) & nmask;
+  }
 };
 
 
@@ -155,6 +159,10 @@ struct ImageDigit {
     return (uint32_t)((((uint64_t)k ^ flip) - sub) >> shift) & mask;
   }
   __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key(keys[i]); }
+  // look-back counting: the next pass's digit of a stored image
+  __device__ __forceinline__ uint32_t next_of(uint64_t stored, int nshift, uint32_t nmask, uint64_t nsub) const {
+    return (uint32_t)((stored - nsub) >> nshift) & nmask;
+  }
 };
 
 // Order-preserving range digit (K7 range join): the partition of key k is
@@ -826,7 +834,8 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
     const int64_t *__restrict__ bh_scan, TileSched lb) {
   constexpr int THREADS = kRPThreads, WAVES = THREADS / kWave, TILE = THREADS * kRPItems;
   constexpr bool LBIN = (LBM & 2) != 0, CNT = (LBM & 1) != 0;
-  static_assert(LBM == 0 || (XT && std::is_same<Digit, ImageDigit>::value), "look-back passes are XT sort passes");
+  static_assert(LBM == 0 || (XT && (std::is_same<Digit, ImageDigit>::value || std::is_same<Digit, PartDigit>::value)),
+                "look-back passes are XT sort / hash-partition passes");
   constexpr int MAXB = LBM ? kLbMaxBuckets : kRPMaxBuckets;
   constexpr int BPT = (MAXB + THREADS - 1) / THREADS;
   static_assert(WAVES * MAXB * 2 + TILE * 4 <= TILE * 8, "ranking scratch must fit the stage");
@@ -1068,7 +1077,9 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
             const int64_t o = running[p] + (int64_t)(dp[q] & 0xffffu);
             const uint64_t kv0 = ldw<W8>(st, j, w);
             stw<W8>(out, o, w, kv0);
-            const uint32_t cell = (p >> xsh) * nbn + (uint32_t)(((kv0 - cols.nd_sub) >> cols.nd_shift) & cols.nd_mask);
+            uint32_t nd = 0;
+            if constexpr (LBM != 0) nd = digit.next_of(kv0, cols.nd_shift, cols.nd_mask, cols.nd_sub);
+            const uint32_t cell = (p >> xsh) * nbn + nd;
             atomicAdd(&lcnt[cell >> 1], 1u << ((cell & 1u) << 4));
           }
         }
@@ -1387,7 +1398,8 @@ static void lean_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit
                         const ColSet &cs, int64_t n, const int64_t *bh_scan, const TileSched &lb, bool xt = false,
                         int lbm = 0) {
   if (lbm) {  // look-back sort passes: XT, all columns 8 bytes wide (checked by the caller)
-    if constexpr (std::is_same<Digit, ImageDigit>::value && RANK == kRankWaveAtomic) {
+    if constexpr ((std::is_same<Digit, ImageDigit>::value || std::is_same<Digit, PartDigit>::value) &&
+                  RANK == kRankWaveAtomic) {
       const dim3 gr((unsigned)g.nblocks), bl(kRPThreads);
       if (lbm == 1)
         hipLaunchKernelGGL((k_rows_pass_lean<Digit, true, RANK, true, 1>), gr, bl, 0, s, dg, digit_bits, nb, cs, n,
@@ -1400,7 +1412,7 @@ static void lean_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit
                            g.rows_per_block, g.nblocks, bh_scan, lb);
       return;
     }
-    CYLON_THROW(Code::Invalid, "look-back pass: sort digits with stable wave ranking only");
+    CYLON_THROW(Code::Invalid, "look-back pass: sort / partition digits with stable wave ranking only");
   }
   if (xt) {
     if (w8)
@@ -1644,10 +1656,14 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
 }
 
 void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, int digit_bits, const uint8_t *const *in,
-                     uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream, bool stable) {
+                     uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream, bool stable,
+                     const SortLbArgs *lb, int nd_bits) {
   const uint32_t nb = 1u << digit_bits;
+  CYLON_CHECK(!(lb && lb->plan_out) || (nd_bits >= 1 && nd_bits <= 9 && stable), Code::Invalid,
+              "look-back counting partition pass: next digit of " << nd_bits << " bits");
   rows_pass_launch(PartDigit{keys, total_bits, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws, stream, 0,
-                   stable);
+                   stable, false, nullptr, nullptr, nullptr, shift + digit_bits,
+                   lb && lb->plan_out ? (1u << nd_bits) - 1u : 0u, 0, lb);
 }
 
 void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_bits, const uint8_t *const *in,

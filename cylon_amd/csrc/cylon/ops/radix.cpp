@@ -5,6 +5,7 @@
 #include <cstdlib>
 
 #include "util.hpp"
+#include "../trace.hpp"
 
 namespace cylon {
 namespace ops {
@@ -67,14 +68,13 @@ std::vector<at::Tensor> UnpackByteColumns(const Exec &ex, const BytePacking &bp,
   return out;
 }
 
-static int max_digit_bits() {  // digit bits per pass (<= 10); tuning knob
-  static const int v = [] {
-    const char *e = std::getenv("CYLON_RADIX_DIGIT_BITS");
-    return e ? std::max(1, std::min(10, std::atoi(e))) : 10;
-  }();
-  return v;
+static int max_digit_bits() {  // digit bits per pass (<= 10); tuning / test knob, read per call
+  const char *e = std::getenv("CYLON_RADIX_DIGIT_BITS");
+  return e ? std::max(1, std::min(10, std::atoi(e))) : 10;
 }
 
+
+static thread_local bool tl_partition_lb_off = false;  // set while a look-back fallback repartitions
 
 std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> cur, const std::vector<int> &widths,
                                        int bits, at::Tensor *offs, const RangeSpec *range,
@@ -86,6 +86,14 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
   for (size_t c = 1; c < cur.size(); ++c)
     CYLON_CHECK(cur[c].defined() || (widths[c] == 8 && !range), Code::Invalid,
                 "RadixPartition: only 8-byte hash-partition columns may be generated row ids");
+  // look-back passes (stable hash partitions of 1-2 all-8-byte columns, as for the sort): the first
+  // pass counts (chunk, next digit) and the later ones take their offsets by look-back, without a
+  // tile histogram (1B-row group-by 24.2 / 25.3 -> 23.3 / 24.0 ms, profiles/r04/partition_lookback_ab.txt).
+  // CYLON_PARTITION_LOOKBACK=0 returns to the exact tile histograms.
+  const char *plb = std::getenv("CYLON_PARTITION_LOOKBACK");
+  const char *dbu = std::getenv("CYLON_RP_DEBUG_UNSTABLE");
+  const bool lb_want = !range && stable && !tl_partition_lb_off && !(plb && plb[0] == '0') && !(dbu && dbu[0] == '1');
+  const std::vector<at::Tensor> orig = lb_want ? cur : std::vector<at::Tensor>();  // for the (never seen) fallback
   // Nullable payloads made a 200M join 24.8 -> 47.8 ms with unpacked validity bytes
   // (16-B byte runs per pass instead of 128-B runs); packed: 30.2 ms.
   std::vector<int> pw = widths;
@@ -94,8 +102,17 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
   const int npass = (bits + max_db - 1) / max_db;
   int shift = 0;
   at::Tensor ws;
+  std::vector<int> dbits;
+  for (int ps = 0, sh = 0; ps < npass; ++ps) {
+    dbits.push_back((bits - sh + (npass - ps) - 1) / (npass - ps));
+    sh += dbits.back();
+  }
+  const bool lb_on = lb_want && hip::radix_sort_lb_eligible(n, (int)cur.size(), pw.data(), dbits.data(), npass,
+                                                            ex.stream);
+  at::Tensor lbws = lb_on ? ex.empty_i64(hip::radix_sort_lb_workspace(n)) : at::Tensor();
+  if (lb_on) trace::add_counter("partition.radix.lookback", 1);
   for (int ps = 0; ps < npass; ++ps) {
-    const int db = (bits - shift + (npass - ps) - 1) / (npass - ps);
+    const int db = dbits[ps];
     const int64_t wsn = hip::radix_rows_pass_workspace(n, db);
     if (!ws.defined() || ws.numel() < wsn) ws = ex.empty_i64(wsn);
     std::vector<at::Tensor> nxt;
@@ -112,12 +129,24 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
       hip::radix_range_rows_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, range->flip, range->mn,
                                  range->rshift, shift, db, in.data(), out.data(), pw.data(), (int)cur.size(),
                                  ptr<int64_t>(ws), ex.stream);
-    else
+    else {
+      SortLbArgs lba{};
+      if (lb_on) lba = hip::radix_sort_lb_args(ptr<int64_t>(lbws), n, ps, npass, ex.stream);
       hip::radix_rows_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, bits, shift, db, in.data(),
                            out.data(), pw.data(), (int)cur.size(), ptr<int64_t>(ws), ex.stream,
-                           stable || ps > 0);  // LSD: every pass after the first keeps the order it receives
+                           stable || ps > 0,  // LSD: every pass after the first keeps the order it receives
+                           lb_on ? &lba : nullptr, ps + 1 < npass ? dbits[ps + 1] : 0);
+    }
     cur = std::move(nxt);
     shift += db;
+  }
+  if (lb_on && hip::radix_sort_lb_failed(ptr<int64_t>(lbws), ex.stream)) {  // a look-back wait gave up
+    trace::add_counter("partition.radix.lookback_timeout_fallback", 1);
+    cur.clear();
+    tl_partition_lb_off = true;  // the exact passes, once
+    std::vector<at::Tensor> r = RadixPartition(ex, orig, widths, bits, offs, range, keep_packed, stable);
+    tl_partition_lb_off = false;
+    return r;
   }
   for (auto &x : cur)  // no pass ran (bits == 0): row ids are still to be made
     if (!x.defined()) x = at::arange(n, ex.opts(at::kLong));

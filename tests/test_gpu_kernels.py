@@ -202,6 +202,39 @@ def test_lookback_sort_passes_match_stable_torch_sort(gpu_ctx, monkeypatch, case
     assert torch.equal(out["v"], v[idx])
 
 
+@pytest.mark.parametrize("op", ["groupby", "unique", "union"])
+def test_partition_lookback_passes_match_exact(gpu_ctx, monkeypatch, op):
+    """Look-back passes of the stable two-pass hash partitions (group-by, set ops): 5-bit digits force
+    two passes on a small table; the result equals the exact-histogram passes (CYLON_PARTITION_LOOKBACK=0)."""
+    n = 3_000_000
+    g = torch.Generator(device="cuda").manual_seed(23)
+    k = torch.randint(0, 400_000, (n,), generator=g, device="cuda")
+    x = torch.randint(0, 3, (n,), generator=g, device="cuda").to(torch.float64)
+    t = Table.from_torch(gpu_ctx, {"k": k, "x": x})
+    t2 = Table.from_torch(gpu_ctx, {"k": k[: n // 2] + 7, "x": x[: n // 2]})
+    monkeypatch.setenv("CYLON_RADIX_DIGIT_BITS", "5")
+    monkeypatch.setenv("CYLON_RADIX_GROUPBY_MIN_ROWS", "1")
+    monkeypatch.setenv("CYLON_RADIX_SETOP_MIN_ROWS", "1")
+    res = []
+    for lb in ("1", "0"):
+        monkeypatch.setenv("CYLON_PARTITION_LOOKBACK", lb)
+        C.trace_enable(True)
+        C.trace_reset()
+        if op == "groupby":
+            df = t.local_groupby("k", {"x": ["sum", "count"]}).to_pandas().sort_values("k")
+        elif op == "unique":
+            df = t.unique().to_pandas().sort_values(["k", "x"])
+        else:
+            df = t.union(t2).to_pandas().sort_values(["k", "x"])
+        c = dict(C.trace_counters())
+        C.trace_enable(False)
+        if lb == "1":
+            assert c.get("partition.radix.lookback", 0) >= 1, c
+            assert c.get("partition.radix.lookback_timeout_fallback", 0) == 0, c
+        res.append(df.reset_index(drop=True))
+    pd.testing.assert_frame_equal(res[0], res[1])
+
+
 def _sorted_df(t):
     df = t.to_pandas()
     return df.sort_values(list(df.columns), kind="stable").reset_index(drop=True)
