@@ -11,7 +11,8 @@ RCCL + local device hash join + materialisation of all 8 output columns).
 metric value = (|L| + |R|) / step time, whole job.
 
 Usage:
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--algorithm hash|sort] [--verify]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--algorithm hash|sort]
+                  [--how inner|left|right|outer] [--no-verify]
 
 With --gpus N > 1 and no torchrun environment, bench.py starts
 `torch.distributed.run --nproc-per-node N` on itself as a child process (one
@@ -19,10 +20,12 @@ rank per GPU, RCCL), the way the reference's run_dist_scaling.py:115-154 starts
 `mpirun -np w`; the parent never touches the GPU.  Under an outer torchrun,
 WORLD_SIZE must equal --gpus (a mismatch exits non-zero).
 
-After the timed region one extra traced step reports per-phase milliseconds
-(max over ranks; not part of the metric), and --verify checks the last timed
-step's output against an independent torch computation of the same join
-(key-count and payload-sum identities, see verify_join).
+After the timed region the last timed step's output is checked against an
+independent torch computation of the same join (key-count and payload-sum
+identities, see verify_join; --no-verify skips it), and one extra traced step
+reports per-phase milliseconds (max over ranks; not part of the metric).  At
+N > 1 every rank reports its device, PCI bus id and the process group's world
+size into the JSON line ("ranks"), so the record names the GPUs the ranks ran on.
 """
 import argparse
 import json
@@ -48,7 +51,9 @@ def parse():
     p.add_argument("--algorithm", default="hash", choices=["hash", "sort"])
     p.add_argument("--key-ratio", type=float, default=0.99)
     p.add_argument("--no-phases", action="store_true", help="skip the traced per-phase step after the timed region")
-    p.add_argument("--verify", action="store_true", help="check the last output against torch (outside the timing)")
+    p.add_argument("--how", default="inner", choices=["inner", "left", "right", "outer"])
+    p.add_argument("--verify", action="store_true", help="(default) check the last output against torch, untimed")
+    p.add_argument("--no-verify", action="store_true", help="skip the output check")
     p.add_argument("--sync-steps", action="store_true",
                    help="diagnostic: synchronise the device after every timed step (host never runs ahead)")
     p.add_argument("--force-shuffle", action="store_true",
@@ -140,35 +145,84 @@ def max_over_ranks(ctx, d: dict) -> dict:
     return out
 
 
-def verify_join(ctx, left, right, out, key_range) -> dict:
-    """Independent check of an inner join output by per-key identities (torch bincount over the
-    global key range, all-reduced over ranks):
-      rows        = sum_k cL(k) cR(k)
-      sum l_k     = sum_k k cL(k) cR(k)      (and l_k == r_k row by row)
-      sum l_v0    = sum_k SL(k) cR(k)         SL = per-key sum of left v0
-      sum r_v0    = sum_k cL(k) SR(k)"""
-    lt, rt, ot = left.to_torch(), right.to_torch(), out.to_torch()
+def verify_join(ctx, left, right, out, key_range, how="inner") -> dict:
+    """Independent check of a join output by per-key identities (torch bincount over the global
+    key range, all-reduced over ranks; reference join/join_utils.cpp:126-181 for the outer rows):
+      rows          = sum_k cL(k) cR(k)  [+ sum_k cL(k) [cR(k) = 0] (left, outer)]
+                                         [+ sum_k cR(k) [cL(k) = 0] (right, outer)]
+      null l / r    = the unmatched right / left rows above, and their payload bytes are zero
+      sum l_k       = sum over rows with a left side of their key  (l_k == r_k where both exist)
+      sum l_v0      = sum_k SL(k) max(cR(k), [left kept])      SL = per-key sum of left v0
+      sum r_v0      = sum_k SR(k) max(cL(k), [right kept])"""
+    lt, rt = left.to_torch(), right.to_torch()
+    ocols = {c.name: c for c in out.native.columns()}
     dev = lt["k"].device
-    cL = torch.bincount(lt["k"], minlength=key_range).to(torch.float64)
-    cR = torch.bincount(rt["k"], minlength=key_range).to(torch.float64)
+    f64 = torch.float64
+    cL = torch.bincount(lt["k"], minlength=key_range).to(f64)
+    cR = torch.bincount(rt["k"], minlength=key_range).to(f64)
     SL = torch.bincount(lt["k"], weights=lt["v0"], minlength=key_range)
     SR = torch.bincount(rt["k"], weights=rt["v0"], minlength=key_range)
     for t in (cL, cR, SL, SR):
         if ctx.get_world_size() > 1:
             t.copy_(ctx.allreduce(t, "sum"))
-    keys = torch.arange(key_range, device=dev, dtype=torch.float64)
-    expect = torch.stack([(cL * cR).sum(), (keys * cL * cR).sum(), (SL * cR).sum(), (cL * SR).sum()])
-    del cL, cR, SL, SR, keys
-    mism = (ot["l_k"] != ot["r_k"]).sum().to(torch.float64)
-    got = torch.stack([torch.tensor(float(out.row_count), dtype=torch.float64, device=dev),
-                       ot["l_k"].to(torch.float64).sum(), ot["l_v0"].sum(), ot["r_v0"].sum(), mism])
+    keep_l = how in ("left", "outer")
+    keep_r = how in ("right", "outer")
+    keys = torch.arange(key_range, device=dev, dtype=f64)
+    zl, zr = (cR == 0).to(f64), (cL == 0).to(f64)
+    inner = (cL * cR).sum()
+    un_l = (cL * zl).sum() if keep_l else torch.zeros((), dtype=f64, device=dev)
+    un_r = (cR * zr).sum() if keep_r else torch.zeros((), dtype=f64, device=dev)
+    lk_rows = cL * (cR + zl) if keep_l else cL * cR  # output rows holding a left key, per key
+    expect = torch.stack([inner + un_l + un_r, un_r, un_l, (keys * lk_rows).sum(),
+                          (SL * (cR + zl) if keep_l else SL * cR).sum(), (SR * (cL + zr) if keep_r else SR * cL).sum()])
+    del cL, cR, SL, SR, keys, zl, zr, lk_rows
+
+    def col(name):
+        c = ocols[name]
+        v = c.validity
+        return c.data, (torch.ones(c.data.shape[0], dtype=torch.bool, device=dev) if v is None else v.to(torch.bool))
+    lkd, lkv = col("l_k")
+    rkd, rkv = col("r_k")
+    lvd, lvv = col("l_v0")
+    rvd, rvv = col("r_v0")
+    both = lkv & rkv
+    mism = ((lkd != rkd) & both).sum().to(f64)
+    null_payload = (lvd.abs() * (~lvv)).sum() + (rvd.abs() * (~rvv)).sum()  # null slots hold zeros
+    got = torch.stack([torch.tensor(float(out.row_count), dtype=f64, device=dev), (~lkv).sum().to(f64),
+                       (~rkv).sum().to(f64), (lkd.to(f64) * lkv).sum(), (lvd * lvv).sum(), (rvd * rvv).sum(), mism,
+                       null_payload.to(f64)])
     if ctx.get_world_size() > 1:
         got = ctx.allreduce(got, "sum")
     e, g = expect.cpu().tolist(), got.cpu().tolist()
-    rel = [abs(a - b) / max(abs(a), 1.0) for a, b in zip(e, g[:4])]
-    ok = g[0] == e[0] and g[4] == 0 and rel[1] < 1e-12 and rel[2] < 1e-9 and rel[3] < 1e-9
-    return {"ok": bool(ok), "rows": int(g[0]), "expected_rows": int(e[0]), "key_mismatch_rows": int(g[4]),
-            "rel_err_sum_k": rel[1], "rel_err_sum_l_v0": rel[2], "rel_err_sum_r_v0": rel[3]}
+    rel = [abs(a - b) / max(abs(a), 1.0) for a, b in zip(e, g[:6])]
+    ok = g[0] == e[0] and g[1] == e[1] and g[2] == e[2] and g[6] == 0 and g[7] == 0 and rel[3] < 1e-12 and \
+        rel[4] < 1e-9 and rel[5] < 1e-9
+    return {"ok": bool(ok), "how": how, "rows": int(g[0]), "expected_rows": int(e[0]),
+            "null_left_rows": int(g[1]), "expected_null_left_rows": int(e[1]),
+            "null_right_rows": int(g[2]), "expected_null_right_rows": int(e[2]),
+            "key_mismatch_rows": int(g[6]), "null_payload_abs_sum": g[7],
+            "rel_err_sum_k": rel[3], "rel_err_sum_l_v0": rel[4], "rel_err_sum_r_v0": rel[5]}
+
+
+def rank_record(ctx) -> list:
+    """[{rank, device, pci_bus_id, world_size}] of every rank (all-gathered; rank 0 prints it)."""
+    import torch.distributed as dist
+    rec = {"rank": ctx.get_rank(), "world_size_pg": dist.get_world_size() if dist.is_initialized() else 1,
+           "backend": dist.get_backend() if dist.is_initialized() else None}
+    if torch.cuda.is_available():
+        d = torch.cuda.current_device()
+        props = torch.cuda.get_device_properties(d)
+        rec.update({"device": d, "name": props.name,
+                    "pci_bus_id": f"{getattr(props, 'pci_domain_id', 0):04x}:{getattr(props, 'pci_bus_id', 0):02x}:"
+                                  f"{getattr(props, 'pci_device_id', 0):02x}",
+                    "uuid": str(getattr(props, "uuid", ""))})
+    else:
+        rec["device"] = "cpu"
+    if ctx.get_world_size() == 1:
+        return [rec]
+    allv = [None] * ctx.get_world_size()
+    dist.all_gather_object(allv, rec)
+    return allv
 
 
 def main():
@@ -185,7 +239,7 @@ def main():
     sync()
 
     def step():
-        return left.distributed_join(right, "inner", args.algorithm, on=[0], left_prefix="l_", right_prefix="r_")
+        return left.distributed_join(right, args.how, args.algorithm, on=[0], left_prefix="l_", right_prefix="r_")
 
     out = None
     for _ in range(args.warmup):
@@ -221,9 +275,10 @@ def main():
     elapsed = float(t.item())
 
     verify = None
-    if args.verify and out is not None:
-        verify = verify_join(ctx, left, right, out, key_range)
+    if not args.no_verify and out is not None:
+        verify = verify_join(ctx, left, right, out, key_range, args.how)
     out = None
+    ranks = rank_record(ctx)
 
     phases = None
     counters = {}
@@ -248,7 +303,8 @@ def main():
     value = rows_in / (ms_per_step / 1000.0)
     if rank == 0:
         rec = {
-            "metric": "rows/sec distributed inner-join, 1B×1B int64 keys, at 1/2/4/8 MI355X",
+            "metric": ("rows/sec distributed inner-join, 1B×1B int64 keys, at 1/2/4/8 MI355X" if args.how == "inner"
+                       else f"rows/sec distributed {args.how}-join, 1B×1B int64 keys (not the headline)"),
             "value": value,
             "unit": "rows/s",
             "n_gpus": n,
@@ -261,7 +317,7 @@ def main():
             "dtype": "int64 keys / float64 payload",
             "data": "synthetic (device-generated; keys uniform in [0, 0.99*rows), reference run_dist_scaling shape)",
             "config": {
-                "model": f"distributed inner join ({args.algorithm}), int64 key + {args.payload_cols} float64 cols",
+                "model": f"distributed {args.how} join ({args.algorithm}), int64 key + {args.payload_cols} float64 cols",
                 "global_batch": args.rows,
                 "seq_len": 1 + args.payload_cols,
                 "parallelism": (f"dp{n} (hash shuffle over {'RCCL' if os.environ.get('CYLON_BENCH_BACKEND', '') == '' else os.environ['CYLON_BENCH_BACKEND']})"
@@ -275,6 +331,7 @@ def main():
             rec["phases_ms_max_over_ranks"] = phases
         if verify is not None:
             rec["verify"] = verify
+        rec["ranks"] = ranks
         rec["allocator_timed_region"] = allocator
         if args.sync_steps:
             rec["sync_steps"] = True

@@ -12,6 +12,7 @@
 #include "cylon/indexing/index.hpp"
 #include "cylon/io/device_interop.hpp"
 #include "cylon/io/h2d.hpp"
+#include "cylon/knobs.hpp"
 #include "cylon/ops/api_ext.hpp"
 #include "cylon/ops/graph.hpp"
 #include "cylon/ops/relational.hpp"
@@ -40,7 +41,12 @@ void register_extended_ops(py::module &m) {
   m.def("index_lookup", &ops::IndexLookup, py::arg("ctx"), py::arg("index"), py::arg("labels"), rel);
 
   // ---- device self-check behind the radix passes' wave-atomic stable ranking (radix_join.hip)
-  m.def("rp_reset_lane_order", []() { hip::rp_reset_lane_order(); });
+  m.def("rp_set_ranking", [](int mode) { hip::rp_set_ranking(mode); });
+  m.def("knob_registry", []() {  // (name without CYLON_, group, effect) of every native knob
+    std::vector<std::tuple<std::string, std::string, std::string>> r;
+    for (const auto &k : knobs::Registry()) r.emplace_back(k.name, k.group, k.effect);
+    return r;
+  });
   m.def("rp_take_order_violation", [](const std::string &device) {
     ops::Exec ex{at::Device(device)};
     CYLON_CHECK(ex.gpu, Code::Invalid, "rp_take_order_violation needs a GPU device");

@@ -1,6 +1,7 @@
 // L0/L2 core objects: DataType, Column, Table, CylonContext.
 // Reference: cpp/src/cylon/data_types.hpp, column.cpp, table.cpp:1-61 (ctor),
 // ctx/cylon_context.cpp:25-108.
+#include "cylon/knobs.hpp"
 #include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPGuard.h>
 
@@ -245,9 +246,7 @@ int CylonContext::GetWorldSize() const { return distributed_ ? communicator_->Ge
 bool CylonContext::ShuffleRequired() const {
   if (!distributed_) return false;
   if (GetWorldSize() > 1) return true;
-  std::string v = GetConfig("force_shuffle", "");
-  if (v.empty())
-    if (const char *e = std::getenv("CYLON_FORCE_SHUFFLE")) v = e;
+  const std::string v = knobs::ConfigOr(GetConfig("force_shuffle", ""), "FORCE_SHUFFLE");
   return v == "1" || v == "true";
 }
 

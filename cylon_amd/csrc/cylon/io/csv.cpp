@@ -1,5 +1,6 @@
 // Native CSV reader / writer (C25): see csv.hpp.
 #include "csv.hpp"
+#include "cylon/trace.hpp"
 
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -334,8 +335,7 @@ TablePtr ReadCSV(const std::shared_ptr<CylonContext> &ctx, const std::string &pa
   }
   std::vector<std::vector<std::pair<size_t, size_t>>> lines(T);
   auto tick = [t0 = std::chrono::steady_clock::now()](const char *what) {
-    static const bool on = std::getenv("CYLON_CSV_TIMING") != nullptr;
-    if (on)
+    if (trace::log_level() >= 3)
       std::fprintf(stderr, "[csv] %-10s %.3f ms\n", what,
                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   };

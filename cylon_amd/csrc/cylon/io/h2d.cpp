@@ -1,4 +1,5 @@
 // Pinned, pipelined host -> device ingest (see h2d.hpp).
+#include "cylon/knobs.hpp"
 #include "h2d.hpp"
 
 #include <hip/hip_runtime.h>
@@ -108,8 +109,7 @@ class CopyPool {
 };
 
 int default_threads() {
-  const char *e = std::getenv("CYLON_H2D_THREADS");
-  if (e) return std::max(1, std::atoi(e));
+  if (const int64_t t = knobs::Int("H2D_THREADS", 0)) return (int)std::max<int64_t>(1, t);
   const unsigned hc = std::thread::hardware_concurrency();
   return (int)std::max(1u, std::min(8u, hc ? hc / 2 : 1u));
 }
@@ -139,8 +139,7 @@ Ring &ring(int device) {
 
 size_t StagedH2DChunkBytes() {
   static const size_t b = [] {
-    const char *e = std::getenv("CYLON_H2D_CHUNK_MB");
-    const long mb = e ? std::max(1L, std::atol(e)) : 32L;
+    const long mb = (long)std::max<int64_t>(1, knobs::Int("H2D_CHUNK_MB", 32));
     return (size_t)mb << 20;
   }();
   return b;

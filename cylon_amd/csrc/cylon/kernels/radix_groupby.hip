@@ -119,28 +119,11 @@ __device__ __forceinline__ double rg_double(uint64_t b, int w, int kind) {
 
 __device__ __forceinline__ uint64_t rg_init(int kind) { return kind == RG_MIN ? ~0ull : 0ull; }
 
-// Debug instantiation (DBG, CYLON_RG_DEBUG=1): every global index is checked against the sizes
-// the host allocated before the access is made; a violation is recorded in dbg[0..7] = {count,
-// site, partition, index, rb, re, j, slot} and the access is skipped instead of faulting.
-__device__ __forceinline__ void rg_dbg(long long *dbg, int site, int64_t p, int64_t idx, int64_t rb, int64_t re,
-                                       int j, int slot) {
-  if (atomicAdd(reinterpret_cast<unsigned long long *>(dbg), 1ull) == 0ull) {
-    dbg[1] = site;
-    dbg[2] = p;
-    dbg[3] = idx;
-    dbg[4] = rb;
-    dbg[5] = re;
-    dbg[6] = j;
-    dbg[7] = slot;
-  }
-}
-
-template <int A, int S, bool DBG = false>
+template <int A, int S>
 __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict__ keys,
                                                        const int64_t *__restrict__ offs, int64_t nparts, RGArgs a,
                                                        int64_t *__restrict__ okeys, uint64_t *__restrict__ oacc,
-                                                       int64_t n, int64_t *__restrict__ gcount, int *overflow,
-                                                       long long *__restrict__ dbg = nullptr) {
+                                                       int64_t n, int64_t *__restrict__ gcount, int *overflow) {
   __shared__ int64_t tk[S + 1];
   __shared__ unsigned long long ta[A][S + 1];
   __shared__ uint32_t wsum[kRGWaves];
@@ -168,10 +151,6 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict
     if (threadIdx.x == 0) bad = 0;
     __syncthreads();
     for (int64_t r = rb + threadIdx.x; r < re; r += blockDim.x) {
-      if (DBG && (r < 0 || r >= n)) {
-        rg_dbg(dbg, 1, p, r, rb, re, -1, -1);
-        continue;
-      }
       const int64_t k = keys[r];
       uint64_t vb[A];
 #pragma unroll
@@ -201,10 +180,6 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict
         }
         slot = (int)s;
       }  // else: the INT64_MIN key accumulates into slot S
-      if (DBG && (slot < 0 || slot > S)) {
-        rg_dbg(dbg, 2, p, r, rb, re, -1, slot);
-        continue;
-      }
 #pragma unroll
       for (int j = 0; j < A; ++j) {
         const RGAccDesc &c = a.acc[j];
@@ -284,17 +259,9 @@ __global__ __launch_bounds__(kRGThreads) void k_rg_agg(const int64_t *__restrict
         atomicOr(overflow, 16);
         continue;
       }
-      if (DBG && (o < 0 || o >= n || s >= S)) {
-        rg_dbg(dbg, 3, p, o, rb, re, -1, s);
-        continue;
-      }
       okeys[o] = tk[s];
 #pragma unroll
       for (int j = 0; j < A; ++j) {
-        if (DBG && (int64_t)j * n + o >= (int64_t)A * n) {
-          rg_dbg(dbg, 4, p, o, rb, re, j, s);
-          continue;
-        }
         oacc[(int64_t)j * n + o] = ta[j][s];
       }
     }
@@ -328,22 +295,13 @@ int64_t distinct_estimate_workspace() { return kHllRegs; }
 
 template <int A, int S>
 static void rg_launch(int grid, hipStream_t s, const int64_t *keys, const int64_t *offs, int64_t nparts,
-                      const RGArgs &a, int64_t *okeys, uint64_t *oacc, int64_t n, int64_t *gcount, int *overflow,
-                      long long *dbg) {
-  if (dbg)
-    hipLaunchKernelGGL((k_rg_agg<A, S, true>), dim3(grid), dim3(kRGThreads), 0, s, keys, offs, nparts, a, okeys, oacc,
-                       n, gcount, overflow, dbg);
-  else
-    hipLaunchKernelGGL((k_rg_agg<A, S, false>), dim3(grid), dim3(kRGThreads), 0, s, keys, offs, nparts, a, okeys,
-                       oacc, n, gcount, overflow, nullptr);
+                      const RGArgs &a, int64_t *okeys, uint64_t *oacc, int64_t n, int64_t *gcount, int *overflow) {
+  hipLaunchKernelGGL((k_rg_agg<A, S>), dim3(grid), dim3(kRGThreads), 0, s, keys, offs, nparts, a, okeys, oacc, n,
+                     gcount, overflow);
 }
 
-// Accumulator planes (oacc holds planes * n words): nacc, or 3 for two accumulators under the
-// CYLON_RG_WIDE=1 diagnostic (a dummy count fills the third slot of the <3, 2048> table).
-int radix_groupby_planes(int nacc) {
-  const char *we = std::getenv("CYLON_RG_WIDE");
-  return (we && we[0] == '1' && nacc == 2) ? 3 : nacc;
-}
+// Accumulator planes (oacc holds planes * n words)
+int radix_groupby_planes(int nacc) { return nacc; }
 
 // Every accumulator slot of a table instance is live: A == planes, and a padded slot is a real
 // count (src = the keys) writing its own plane.  Round 3 ran two accumulators in the <3, 2048>
@@ -379,31 +337,13 @@ void radix_groupby_agg(const int64_t *keys, const int64_t *offs, int64_t nparts,
   hipStream_t s = as_stream(stream);
   HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
   const int grid = (int)std::min<int64_t>(nparts, kNumCUs * 4);
-  // CYLON_RG_DEBUG=1: the bounds-checked instantiation that records instead of faulting
-  const char *de = std::getenv("CYLON_RG_DEBUG");
-  long long *dbg = nullptr;
-  if (de && de[0] == '1') {
-    HIP_CHECK(hipMallocAsync(reinterpret_cast<void **>(&dbg), 8 * sizeof(long long), s));
-    HIP_CHECK(hipMemsetAsync(dbg, 0, 8 * sizeof(long long), s));
-  }
   switch (A) {
-    case 1: rg_launch<1, 4096>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow, dbg); break;
-    case 2: rg_launch<2, 2048>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow, dbg); break;
-    case 3: rg_launch<3, 2048>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow, dbg); break;
-    default: rg_launch<4, 1024>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow, dbg);
+    case 1: rg_launch<1, 4096>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow); break;
+    case 2: rg_launch<2, 2048>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow); break;
+    case 3: rg_launch<3, 2048>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow); break;
+    default: rg_launch<4, 1024>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow);
   }
   HIP_LAUNCH_CHECK();
-  if (dbg) {
-    long long h[8];
-    HIP_CHECK(hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    HIP_CHECK(hipFreeAsync(dbg, s));
-    std::fprintf(stderr, "rg_debug nacc=%d planes=%d nparts=%lld n=%lld violations=%lld site=%lld p=%lld idx=%lld "
-                 "rb=%lld re=%lld j=%lld slot=%lld\n", nacc, A, (long long)nparts, (long long)n, h[0], h[1],
-                 h[2], h[3], h[4], h[5], h[6], h[7]);
-    CYLON_CHECK(h[0] == 0, Code::ExecutionError, "radix group-by debug: " << h[0] << " out-of-range accesses (site "
-                                                                           << h[1] << ")");
-  }
 }
 
 int64_t radix_groupby_slots(int nacc) { return nacc <= 1 ? 4096 : (nacc <= 3 ? 2048 : 1024); }

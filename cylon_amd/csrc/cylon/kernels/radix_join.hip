@@ -23,6 +23,7 @@
 //      owns a contiguous slice of the probe rows (wave-level scans only).
 // Partitions whose build side exceeds the LDS capacity are reported; the
 // caller then falls back to the global-table join.
+#include "cylon/knobs.hpp"
 #include <atomic>
 #include <climits>
 #include <cstdio>
@@ -227,10 +228,6 @@ struct TileSched {
   int64_t sl_nslots = 0;              // output slots (the trash rows start at sl_nslots * sl_slot)
   int sl_nseg = 0;                    // S <= kSlotMaxSeg
   int sl_gshift = 0, sl_gmask = 0, sl_B = 1;
-  // debug instance (CYLON_SLOT_DEBUG=1): rows of the input / output arrays; an access outside them is
-  // skipped, counted in sl_dbg[0] and printed (first few)
-  int64_t sl_in_rows = 0, sl_out_rows = 0;
-  unsigned int *sl_dbg = nullptr;
   // look-back sort passes (k_rows_pass_lean<..., LBM>, see "look-back sort passes" below)
   const uint32_t *lb_plan = nullptr;  // in: chunk rows / tiles / bases of this pass (LBM & 2)
   uint32_t *lb_state = nullptr;       // in: [tile][nb] flag | value + 1 words, zeroed
@@ -260,7 +257,7 @@ constexpr int kLbChunks = 8, kLbMaxBuckets = 512;
 // write-through, so they stay in that XCD's L2 where its CUs' L1-bypassing loads find them (a
 // round trip to L2 instead of HBM; 2B-row sort 92.8 -> 83.8 ms, profiles/r04/sort_lookback_ab.txt);
 // 0: any XCD takes a chunk's tiles once its own are done and the words are written through.  The
-// plan chooses local when no chunk exceeds 1.5x the mean (CYLON_SORT_LB_LOCAL=0/1 forces it).
+// plan chooses local when no chunk exceeds 1.5x the mean.
 constexpr int kLbCnt = 0, kLbC = kLbChunks * kLbMaxBuckets, kLbTP = kLbC + 16, kLbLocal = kLbTP + 12,
               kLbBase = kLbTP + 16,
               kLbTickets = kLbBase + kLbChunks * kLbMaxBuckets, kLbPlanWords = kLbTickets + 16;
@@ -471,19 +468,6 @@ __global__ void k_ts_offsets(const uint16_t *__restrict__ th, const uint32_t *__
 // with vmcnt(0) for all outstanding loads AND stores: gfx9 counts both on one
 // counter).  Issuing several columns' loads per wait instead (more VGPRs, fewer
 // waves) measured slower -- profiles/rows_pass_experiments_r02.txt.
-// Debug phase stamps (CYLON_RP_STAMPS=1, rows_pass_launch): wave 0 of block 0 records the
-// shader clock at each phase boundary of its first kRPStampTiles tiles; nullptr otherwise.
-constexpr int kRPStampTiles = 64, kRPStampSlots = 16;
-#define RP_STAMP(slot)                                                                               \
-  do {                                                                                               \
-    if (stamps != nullptr && blockIdx.x == 0 && tix >= 0 && tix < kRPStampTiles && (slot) < kRPStampSlots) { \
-      unsigned long long t_;                                                                         \
-      __builtin_amdgcn_sched_barrier(0);                                                             \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                    \
-      __builtin_amdgcn_sched_barrier(0);                                                             \
-      if (threadIdx.x == 0) stamps[tix * kRPStampSlots + (slot)] = t_;                               \
-    }                                                                                                \
-  } while (0)
 
 // RANK: kRankBallot (stable wave64 ballot match), kRankBlockAtomic (one LDS atomic per row
 // on block-wide counters: unstable), kRankWaveAtomic (LDS atomics on the wave's own packed
@@ -491,11 +475,10 @@ constexpr int kRPStampTiles = 64, kRPStampSlots = 16;
 // order -- tools/lds_atomic_order.hip measures that on the device).
 // XT: XCD-tile schedule (tiles claimed in order per XCD, exact per-tile bucket offsets in lb).
 // SLOT: slot mode (TileSched): tiles of one input bucket each, per-(tile, digit) slot claims.
-// SDBG: bounds-checked slot instance (tools / CYLON_SLOT_DEBUG=1).
-template <class Digit, bool W8, int THREADS, int RANK, bool XT = false, bool SLOT = false, bool SDBG = false>
+template <class Digit, bool W8, int THREADS, int RANK, bool XT = false, bool SLOT = false>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_rows_pass(
     Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
-    const int64_t *__restrict__ bh_scan, TileSched lb, unsigned long long *__restrict__ stamps) {
+    const int64_t *__restrict__ bh_scan, TileSched lb) {
   constexpr int WAVES = THREADS / kWave;
   constexpr int TILE = THREADS * kRPItems;
   constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;  // buckets per thread in the offset scan
@@ -543,12 +526,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     const int64_t r0 = (int64_t)sss[g] + (t - (int64_t)tp[g]) * TILE;
     s_tr0[slot] = r0;
     s_tend[slot] = r0 + TILE < gend ? r0 + TILE : gend;
-    if (SDBG && (r0 < 0 || s_tend[slot] > lb.sl_in_rows || g < 0 || g >= lb.sl_nseg)) {
-      if (atomicAdd(lb.sl_dbg, 1u) < 8u)
-        printf("slot dbg: block %d tile %lld seg %d rows [%lld, %lld) in_rows %lld\n", (int)blockIdx.x, (long long)t, g,
-               (long long)r0, (long long)s_tend[slot], (long long)lb.sl_in_rows);
-      s_tend[slot] = r0;  // empty tile
-    }
     // digit d of this tile goes to slot s_tb + d * sl_B
     s_tb[slot] = (g >> lb.sl_gshift) * (int)nbuckets * lb.sl_B + (g & lb.sl_gmask);
   };
@@ -599,8 +576,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   }
   for (int64_t tile = begin, next = 0; tile < end; tile = next) {
     next = tile + TILE;
-    const int tix = (int)((tile - begin) / TILE);
-    RP_STAMP(0);
     const int cnt = SLOT ? (int)(s_tend[par] - tile) : (int)((end - tile) < TILE ? (end - tile) : TILE);
     // XT: this tile's bucket offsets (consumed after the slot phase; the load overlaps the ranking)
     const uint32_t xoff = XT && threadIdx.x < nbuckets ? lb.xt_off[(tile / TILE) * nbuckets + threadIdx.x] : 0u;
@@ -608,7 +583,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k)
       pl[k] = (wrow + k * kWave + lane < cnt) ? digit.of_key((int64_t)kv[k]) : 0xffffffffu;
-    RP_STAMP(1);
     if (STABLE) {
       for (uint32_t q = threadIdx.x; q < WAVES * nbuckets; q += blockDim.x) wcnt[q] = 0;
     } else {
@@ -649,18 +623,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       pl[k] = active ? (((base + rank) << 16) | p) : 0xffffffffu;
     }
     __syncthreads();
-    RP_STAMP(2);
     // SLOT: claim this tile's run in every output slot it feeds as soon as the counts exist (the
     // atomics' latency hides behind the scan and the slot phase)
     uint32_t sl_c = 0, sl_base = 0;
     if (SLOT && threadIdx.x < nbuckets) {
       sl_c = STABLE ? 0u : bcnt[threadIdx.x];
-      if (SDBG && sl_c && ((int64_t)s_tb[par] + (int64_t)threadIdx.x * lb.sl_B >= lb.sl_nslots || s_tb[par] < 0)) {
-        if (atomicAdd(lb.sl_dbg, 1u) < 8u)
-          printf("slot dbg: block %d cursor index %lld of %lld\n", (int)blockIdx.x,
-                 (long long)((int64_t)s_tb[par] + (int64_t)threadIdx.x * lb.sl_B), (long long)lb.sl_nslots);
-        sl_c = 0;
-      }
       if (sl_c) sl_base = atomicAdd(&lb.sl_cursor[(int64_t)s_tb[par] + (int64_t)threadIdx.x * lb.sl_B], sl_c);
     }
     {  // thread owns buckets [t*BPT, t*BPT+BPT): exclusive prefix over waves (in place), then a
@@ -695,7 +662,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       if (threadIdx.x == THREADS - 1) toff[nbuckets] = ex + total;
     }
     __syncthreads();
-    RP_STAMP(3);
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k) {
       if (pl[k] == 0xffffffffu) continue;
@@ -712,7 +678,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
                                   : lb.sl_nslots * lb.sl_slot;  // the trash rows
     }
     __syncthreads();
-    RP_STAMP(4);
     // destination of sorted slot j = threadIdx.x + q * THREADS.  SLOT: packed as digit << 16 | offset
     // in its run and completed from running[] (LDS) at each store -- 8 VGPRs instead of 16 in the
     // instance that also carries the slot bookkeeping (the trick of the lean kernel)
@@ -730,15 +695,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         const uint32_t e = sdig[j], p = e >> 16;
         if constexpr (SLOT && PACKDST) dst[q] = (p << 16) | (uint32_t)(j - (int)toff[p]);
         else dst[q] = running[p] + (j - (int64_t)toff[p]);
-        if (SDBG) {
-          const int64_t d = running[p] + (j - (int64_t)toff[p]);
-          if (d < 0 || d + kRPTile > lb.sl_out_rows + kRPTile || p >= nbuckets) {
-            if (atomicAdd(lb.sl_dbg, 1u) < 8u)
-              printf("slot dbg: block %d tile %lld slot j %d digit %u dst %lld out_rows %lld cnt %d\n",
-                     (int)blockIdx.x, (long long)tile, j, p, (long long)d, (long long)lb.sl_out_rows, cnt);
-            if (d < 0 || d >= lb.sl_out_rows) atomicOr(lb.sl_overflow, 1u);
-          }
-        }
         if (cols.check_order && j > 0) {  // same bucket as the previous slot: input order kept?
           const uint32_t f = sdig[j - 1];
           order_bad |= (f >> 16) == p && f > e;
@@ -746,7 +702,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       }
     }
     __syncthreads();  // counters / digits dead: the union becomes the column stage
-    RP_STAMP(5);
     // load column c+1 while column c streams out of the stage
     uint64_t v[kRPItems];
 #pragma unroll
@@ -764,7 +719,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
       __syncthreads();
       if (TICKET && c + 1 == cols.n) next = SLOT ? s_tr0[par ^ 1] : s_next;
-      RP_STAMP(6 + 2 * c);
       if (c + 1 < cols.n) {  // prefetch column c+1 of this tile
         const uint8_t *in = cols.in[c + 1];
         const int w1 = cols.width[c + 1];
@@ -802,7 +756,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         }
       }
       __syncthreads();
-      RP_STAMP(7 + 2 * c);
     }
 #undef RP_DEST
     if (!TICKET)
@@ -1129,15 +1082,8 @@ struct RPGeometry {
 // (profiles/rank_variants_r02.txt).  With the ballot ranking, two 512-thread blocks per CU
 // (4096-row tiles) interleave one block's ranking with the other's memory traffic, which
 // pays for 1-2 column passes (2B sort 137 -> 120 ms) but not for wide rows
-// (profiles/rows_pass_experiments_r02.txt).  CYLON_RP_THREADS=512|1024 forces one.
-static int rp_threads(int ncols, bool cheap_rank) {
-  static const int forced = [] {
-    const char *e = std::getenv("CYLON_RP_THREADS");
-    const int t = e ? std::atoi(e) : 0;
-    return t == 512 || t == 1024 ? t : 0;
-  }();
-  return forced ? forced : (ncols <= 2 && !cheap_rank ? 512 : 1024);
-}
+// (profiles/rows_pass_experiments_r02.txt).
+static int rp_threads(int ncols, bool cheap_rank) { return ncols <= 2 && !cheap_rank ? 512 : 1024; }
 
 // Self-check of kRankWaveAtomic's precondition: every lane of a wave adds 1 to a
 // pseudo-random packed 16-bit counter of the wave's own row (bucket ranges of 2 ... 1024,
@@ -1210,7 +1156,7 @@ int64_t lds_lane_order_violations(int blocks, int rounds, void *stream) {
 // self-check (run once per device, at context creation -- CylonContext::Init calls
 // lds_lane_order_ok -- not inside a pass), else ballots.  A stability violation seen by a
 // pass's ranking guard (rp_take_order_violation) switches the device to ballots for the rest
-// of the process.  CYLON_RP_RANK=wave|ballot forces one.
+// of the process.  rp_set_ranking (tests) forces one.
 static std::atomic<int> g_lane_ok[64];  // 0 unknown, 1 ok, 2 not ok
 
 static int current_device() {
@@ -1220,12 +1166,6 @@ static int current_device() {
 }
 
 bool lds_lane_order_ok(void *stream) {
-  static const int forced = [] {
-    const char *e = std::getenv("CYLON_RP_RANK");
-    if (!e) return -1;
-    return std::string(e) == "wave" ? 1 : (std::string(e) == "ballot" ? 0 : -1);
-  }();
-  if (forced >= 0) return forced == 1;
   std::atomic<int> &st = g_lane_ok[current_device()];
   int v = st.load();
   if (v == 0) {
@@ -1254,8 +1194,9 @@ static int *order_flag() {
   return f;
 }
 
-void rp_reset_lane_order() {  // forget every device's ranking verdict (tests): re-probe on next use
-  for (auto &v : g_lane_ok) v.store(0);
+// tests: 0 = forget every device's ranking verdict (re-probe on next use), 1 = wave-atomic, 2 = ballots
+void rp_set_ranking(int mode) {
+  for (auto &v : g_lane_ok) v.store(mode == 1 ? 1 : (mode == 2 ? 2 : 0));
 }
 
 bool rp_take_order_violation(void *stream) {
@@ -1277,13 +1218,8 @@ static bool rp_wave_atomic(hipStream_t s) { return lds_lane_order_ok(reinterpret
 // lean wins for passes that move 1-2 columns (2B-row sort 107.5 -> 99.2 ms, 1B group-by 27.6 ->
 // 25.0 ms; its two blocks overlap each other's ranking and barriers) and loses for the 4-column
 // join passes (17.9 -> 20.0 ms per pass: without the classic kernel's next-column prefetch each
-// column's load latency is exposed).  CYLON_RP_KERNEL=lean|classic forces one (read per launch).
-static bool rp_lean(int ncols) {
-  const char *e = std::getenv("CYLON_RP_KERNEL");
-  if (e && std::string(e) == "lean") return true;
-  if (e && std::string(e) == "classic") return false;
-  return ncols <= 2;
-}
+// column's load latency is exposed).
+static bool rp_lean(int ncols) { return ncols <= 2; }
 
 // resident: blocks per CU that run at once (lean pass: 2 x 1024 threads)
 static RPGeometry rp_geometry(int64_t n, int threads, int resident = 1) {
@@ -1299,11 +1235,8 @@ static RPGeometry rp_geometry(int64_t n, int threads, int resident = 1) {
 
 // XCD-tile mode (k_rows_pass / k_rows_pass_lean XT), default on: 1B x 1B join 116-121 -> 102-103 ms,
 // passes 21 -> 15.5 ms, pass HBM traffic back to the column bytes (profiles/r03/xcd_tiles_ab.txt).
-// CYLON_RP_XT=0 returns to per-block contiguous chunks (read per call).
-static bool rp_xt() {
-  const char *e = std::getenv("CYLON_RP_XT");
-  return !(e && e[0] == '0');
-}
+// The per-block-chunk schedule (histogram mode) remains for 512-thread ballot passes and n >= 2^32.
+static bool rp_xt() { return true; }
 
 struct XtLayout {  // int64-word offsets of the XT buffers in a pass workspace
   int64_t ntiles, nchunks, th, off, csum, cpre, bbase, tickets, words;
@@ -1337,60 +1270,25 @@ template <class Digit, int THREADS, int RANK>
 static void rows_pass_kernel(bool w8, const RPGeometry &g, hipStream_t s, const Digit &dg, int digit_bits, uint32_t nb,
                              const ColSet &cs, int64_t n, const int64_t *bh_scan, const TileSched &lb = TileSched{},
                              bool xt = false) {
-  static const bool stamp = std::getenv("CYLON_RP_STAMPS") != nullptr;  // debug: phase stamps to stderr
-  unsigned long long *st = nullptr;
-  if (stamp) {
-    HIP_CHECK(hipStreamSynchronize(s));
-    HIP_CHECK(hipMalloc(&st, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
-    HIP_CHECK(hipMemset(st, 0, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
-  }
   bool launched = false;
   if constexpr (THREADS == 1024) {
     if (xt) {
       if (w8)
         hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS, RANK, true>), dim3((unsigned)g.nblocks), dim3(THREADS), 0,
-                           s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
+                           s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
       else
         hipLaunchKernelGGL((k_rows_pass<Digit, false, THREADS, RANK, true>), dim3((unsigned)g.nblocks), dim3(THREADS), 0,
-                           s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
+                           s, dg, digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
       launched = true;
     }
   }
   if (launched) {
   } else if (w8)
     hipLaunchKernelGGL((k_rows_pass<Digit, true, THREADS, RANK>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s, dg,
-                       digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
+                       digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
   else
     hipLaunchKernelGGL((k_rows_pass<Digit, false, THREADS, RANK>), dim3((unsigned)g.nblocks), dim3(THREADS), 0, s, dg,
-                       digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb, st);
-  if (st) {
-    HIP_CHECK(hipStreamSynchronize(s));
-    std::vector<unsigned long long> h(kRPStampTiles * kRPStampSlots);
-    HIP_CHECK(hipMemcpy(h.data(), st, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost));
-    HIP_CHECK(hipFree(st));
-    // mean cycles of each phase over the full tiles after the first (tile i: slot j - slot j-1,
-    // slot 0 of tile i+1 closes the last column)
-    const int last = 7 + 2 * (cs.n - 1);
-    double sum[kRPStampSlots] = {0};
-    int tiles = 0;
-    for (int t = 1; t + 1 < kRPStampTiles; ++t) {
-      if (h[(t + 1) * kRPStampSlots] == 0) break;
-      for (int j = 1; j <= last && j < kRPStampSlots; ++j)
-        sum[j] += (double)(h[t * kRPStampSlots + j] - h[t * kRPStampSlots + j - 1]);
-      sum[0] += (double)(h[(t + 1) * kRPStampSlots] - h[t * kRPStampSlots]);
-      ++tiles;
-    }
-    if (tiles > 0) {
-      std::fprintf(stderr, "rp_stamps threads=%d stable=%d ncols=%d bits=%d tiles=%d tile_total=%.0f |", THREADS,
-                   RANK, cs.n, digit_bits, tiles, sum[0] / tiles);
-      static const char *names[] = {"", "keys", "rank", "scan", "slot", "dst"};
-      for (int j = 1; j <= last && j < kRPStampSlots; ++j) {
-        if (j <= 5) std::fprintf(stderr, " %s=%.0f", names[j], sum[j] / tiles);
-        else std::fprintf(stderr, " c%d_%s=%.0f", (j - 6) / 2, (j % 2 == 0) ? "stage" : "scatter", sum[j] / tiles);
-      }
-      std::fprintf(stderr, "\n");
-    }
-  }
+                       digit_bits, nb, cs, n, g.rows_per_block, g.nblocks, bh_scan, lb);
 }
 
 template <class Digit, int RANK>
@@ -1446,7 +1344,7 @@ __global__ __launch_bounds__(256) void k_lb_reduce(const uint32_t *__restrict__ 
 
 // plan of a look-back pass from its (chunk, digit) counts: chunk first rows C, first tiles TP
 // (tiles never straddle chunks) and bases[x][d] = rows of digits < d + rows of digit d in chunks < x
-__global__ __launch_bounds__(kLbMaxBuckets) void k_lb_plan(uint32_t *__restrict__ plan, uint32_t nb, int local_mode) {
+__global__ __launch_bounds__(kLbMaxBuckets) void k_lb_plan(uint32_t *__restrict__ plan, uint32_t nb) {
   __shared__ uint32_t wsum[kLbMaxBuckets / kWave];
   __shared__ uint32_t csz[kLbChunks];
   const uint32_t d = threadIdx.x;
@@ -1478,7 +1376,7 @@ __global__ __launch_bounds__(kLbMaxBuckets) void k_lb_plan(uint32_t *__restrict_
     plan[kLbTP + kLbChunks] = t;
     uint32_t mx = 0;
     for (int x = 0; x < kLbChunks; ++x) mx = csz[x] > mx ? csz[x] : mx;
-    plan[kLbLocal] = local_mode >= 0 ? (uint32_t)local_mode : (uint64_t)mx * kLbChunks * 2 <= (uint64_t)r * 3 ? 1u : 0u;
+    plan[kLbLocal] = (uint64_t)mx * kLbChunks * 2 <= (uint64_t)r * 3 ? 1u : 0u;
   }
 }
 
@@ -1494,9 +1392,7 @@ static void lb_plan_next(const SortLbArgs *lba, int64_t nblk, uint32_t nbn, int6
   hipLaunchKernelGGL(k_lb_reduce, dim3((unsigned)((cells + 255) / 256), kLbReduceSlices), dim3(256), 0, s, lba->gcnt,
                      nblk, cells, lba->plan_out + kLbCnt);
   HIP_LAUNCH_CHECK();
-  const char *lc = std::getenv("CYLON_SORT_LB_LOCAL");  // 0 / 1 force the chunk mode (default: by balance)
-  const int local_mode = lc && (lc[0] == '0' || lc[0] == '1') ? lc[0] - '0' : -1;
-  hipLaunchKernelGGL(k_lb_plan, dim3(1), dim3(kLbMaxBuckets), 0, s, lba->plan_out, nbn, local_mode);
+  hipLaunchKernelGGL(k_lb_plan, dim3(1), dim3(kLbMaxBuckets), 0, s, lba->plan_out, nbn);
   HIP_LAUNCH_CHECK();
   (void)n;
 }
@@ -1526,8 +1422,7 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   // test knob: every partition pass ranks unstably, so LSD passes after the first scramble the
   // order they received -- rows end in wrong partitions and the join's ranking guard must fire
   const bool want_stable = stable;  // the ranking guard checks what the caller asked for
-  const char *dbg = std::getenv("CYLON_RP_DEBUG_UNSTABLE");
-  if (CAN_UNSTABLE && dbg && dbg[0] == '1') stable = false;
+  if (CAN_UNSTABLE && knobs::Flag("RP_DEBUG_UNSTABLE", false)) stable = false;
   const bool unstable = CAN_UNSTABLE && !stable;
   const bool wave_atomic = !unstable && rp_wave_atomic(s);
   const int threads = rp_threads(ncols, unstable || wave_atomic);
@@ -1606,8 +1501,7 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   cs.nd_shift = nd_shift;
   cs.nd_mask = nd_mask;
   cs.nd_sub = nd_sub;
-  const char *gd = std::getenv("CYLON_RP_GUARD");  // A/B knob: 0 disables the ranking guard
-  cs.check_order = want_stable && !(gd && gd[0] == '0') ? 1 : 0;
+  cs.check_order = want_stable ? 1 : 0;
   cs.order_bad = order_flag();
   for (int c = 0; c < kMaxFusedCols; ++c) {
     cs.in[c] = c < ncols ? in[c] : nullptr;
@@ -1682,8 +1576,7 @@ void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_b
 }
 
 bool radix_sort_lb_eligible(int64_t n, int ncols, const int *widths, const int *dbits, int npass, void *stream) {
-  const char *e = std::getenv("CYLON_SORT_LOOKBACK");  // A/B knob: 0 = exact per-tile histogram passes
-  if ((e && e[0] == '0') || !rp_xt() || npass < 2 || n < 1 || n >= (int64_t(1) << 31) - 2) return false;
+  if (!knobs::Flag("SORT_LOOKBACK", true) || !rp_xt() || npass < 2 || n < 1 || n >= (int64_t(1) << 31) - 2) return false;
   if (rp_threads(ncols, true) != 1024 || !rp_lean(ncols) || !rp_wave_atomic(as_stream(stream))) return false;
   for (int c = 0; c < ncols; ++c)
     if (widths[c] != 8) return false;
@@ -1798,7 +1691,7 @@ int64_t radix_slot_workspace(int first_bits, int second_bits) {  // int64 words:
 static void slot_pass(const PartDigit &dg, int64_t n, int digit_bits, const uint8_t *const *in, uint8_t *const *out,
                       const int *widths, int ncols, int src, int S, const uint32_t *bbase, const int64_t *pcnt,
                       int64_t pslot, int gshift, int gmask, int B, int64_t nslots, int64_t slot, int64_t *ws,
-                      int64_t *counts, unsigned int *overflow, hipStream_t s, int64_t in_rows) {
+                      int64_t *counts, unsigned int *overflow, hipStream_t s) {
   CYLON_CHECK(S >= 1 && S <= kSlotMaxSeg && ncols >= 1 && ncols <= kMaxFusedCols && slot > 0, Code::Invalid,
               "slot pass arguments");
   CYLON_CHECK(in[0] == reinterpret_cast<const uint8_t *>(dg.keys) && widths[0] == 8, Code::Invalid,
@@ -1808,35 +1701,7 @@ static void slot_pass(const PartDigit &dg, int64_t n, int digit_bits, const uint
   uint32_t *w32 = reinterpret_cast<uint32_t *>(ws);
   uint32_t *ss = w32, *se = ss + S, *tpre = se + S;
   unsigned int *cursor = tpre + S + 1;
-  static const bool dbg = [] {
-    const char *e = std::getenv("CYLON_SLOT_DEBUG");
-    return e && e[0] == '1';
-  }();
-  auto dsync = [&](const char *what) {  // debug: every step synchronised and checked on its own
-    if (!dbg) return;
-    const hipError_t e1 = hipStreamSynchronize(s), e2 = hipGetLastError();
-    std::fprintf(stderr, "slot dbg: src %d after %s: %s / %s\n", src, what, hipGetErrorString(e1), hipGetErrorString(e2));
-  };
-  if (dbg) {
-    std::fprintf(stderr, "slot dbg: src %d S %d n %lld nslots %lld slot %lld pslot %lld ws %p cursor %p bbase %p pcnt %p "
-                 "in_rows %lld ncols %d\n", src, S, (long long)n, (long long)nslots, (long long)slot, (long long)pslot,
-                 (void *)ws, (void *)cursor, (const void *)bbase, (const void *)pcnt, (long long)in_rows, ncols);
-    if (src == 2) {
-      dsync("entry");
-      std::vector<int64_t> hc(S);
-      HIP_CHECK(hipMemcpy(hc.data(), pcnt, sizeof(int64_t) * S, hipMemcpyDeviceToHost));
-      int64_t mn = INT64_MAX, mx = INT64_MIN, sum = 0;
-      for (int64_t v : hc) {
-        mn = std::min(mn, v);
-        mx = std::max(mx, v);
-        sum += v;
-      }
-      std::fprintf(stderr, "slot dbg: previous counts min %lld max %lld sum %lld\n", (long long)mn, (long long)mx,
-                   (long long)sum);
-    }
-  }
   HIP_CHECK(hipMemsetAsync(cursor, 0, sizeof(uint32_t) * nslots, s));
-  dsync("cursor memset");
   CYLON_CHECK((src == 0) || (src == 1 && bbase) || (src == 2 && pcnt), Code::Invalid, "slot pass source " << src);
   if (src == 0)
     hipLaunchKernelGGL(k_sl_segments<0>, dim3(1), dim3(kRPThreads), 0, s, S, n, bbase, pcnt, pslot, ss, se, tpre);
@@ -1844,7 +1709,6 @@ static void slot_pass(const PartDigit &dg, int64_t n, int digit_bits, const uint
     hipLaunchKernelGGL(k_sl_segments<1>, dim3(1), dim3(kRPThreads), 0, s, S, n, bbase, pcnt, pslot, ss, se, tpre);
   else
     hipLaunchKernelGGL(k_sl_segments<2>, dim3(1), dim3(kRPThreads), 0, s, S, n, bbase, pcnt, pslot, ss, se, tpre);
-  dsync("k_sl_segments");
   HIP_LAUNCH_CHECK();
   TileSched lb{};
   lb.sl_tpre = tpre;
@@ -1858,26 +1722,6 @@ static void slot_pass(const PartDigit &dg, int64_t n, int digit_bits, const uint
   lb.sl_gshift = gshift;
   lb.sl_gmask = gmask;
   lb.sl_B = B;
-  lb.sl_in_rows = in_rows;
-  lb.sl_out_rows = nslots * slot + kRPTile;
-  static unsigned int *dbg_count = nullptr;
-  if (dbg) {
-    if (!dbg_count) HIP_CHECK(hipMalloc(&dbg_count, sizeof(unsigned int)));
-    HIP_CHECK(hipMemsetAsync(dbg_count, 0, sizeof(unsigned int), s));
-    lb.sl_dbg = dbg_count;
-    // host check of the segment table
-    HIP_CHECK(hipStreamSynchronize(s));
-    std::vector<uint32_t> h(3 * S + 1);
-    HIP_CHECK(hipMemcpy(h.data(), ss, sizeof(uint32_t) * (3 * S + 1), hipMemcpyDeviceToHost));
-    int64_t bad = 0, rows = 0;
-    for (int g = 0; g < S; ++g) {
-      const int64_t a = h[g], e = h[S + g], t0 = h[2 * S + g], t1 = h[2 * S + g + 1];
-      rows += e - a;
-      if (a > e || e > in_rows || t1 - t0 != (e - a + kRPTile - 1) / kRPTile) ++bad;
-    }
-    std::fprintf(stderr, "slot dbg: pass src %d S %d n %lld rows in segments %lld in_rows %lld tiles %u bad %lld grid?\n", src,
-                 S, (long long)n, (long long)rows, (long long)in_rows, h[3 * S], (long long)bad);
-  }
   ColSet cs;
   cs.n = ncols;
   cs.key_xor = 0;
@@ -1899,25 +1743,14 @@ static void slot_pass(const PartDigit &dg, int64_t n, int digit_bits, const uint
   }
   // every XCD needs at least one block: its segments' tiles are dealt to its own blocks only
   const int64_t nblocks = std::max<int64_t>(kXcds, std::min<int64_t>((n + kRPTile - 1) / kRPTile + S, kNumCUs));
-  if (dbg && w8)
-    hipLaunchKernelGGL((k_rows_pass<PartDigit, true, 1024, kRankBlockAtomic, false, true, true>),
-                       dim3((unsigned)nblocks), dim3(1024), 0, s, dg, digit_bits, nb, cs, n, (int64_t)kRPTile, nblocks,
-                       nullptr, lb, nullptr);
-  else if (w8)
+  if (w8)
     hipLaunchKernelGGL((k_rows_pass<PartDigit, true, 1024, kRankBlockAtomic, false, true>), dim3((unsigned)nblocks),
-                       dim3(1024), 0, s, dg, digit_bits, nb, cs, n, (int64_t)kRPTile, nblocks, nullptr, lb, nullptr);
+                       dim3(1024), 0, s, dg, digit_bits, nb, cs, n, (int64_t)kRPTile, nblocks, nullptr, lb);
   else
     hipLaunchKernelGGL((k_rows_pass<PartDigit, false, 1024, kRankBlockAtomic, false, true>), dim3((unsigned)nblocks),
-                       dim3(1024), 0, s, dg, digit_bits, nb, cs, n, (int64_t)kRPTile, nblocks, nullptr, lb, nullptr);
+                       dim3(1024), 0, s, dg, digit_bits, nb, cs, n, (int64_t)kRPTile, nblocks, nullptr, lb);
   HIP_LAUNCH_CHECK();
-  if (dbg) {
-    unsigned int h = 0;
-    HIP_CHECK(hipMemcpyAsync(&h, dbg_count, sizeof(h), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    std::fprintf(stderr, "slot dbg: pass src %d done, %u bad accesses, grid %lld\n", src, h, (long long)nblocks);
-  }
   hipLaunchKernelGGL(k_sl_counts, dim3(grid_for(nslots)), dim3(kBlock), 0, s, cursor, nslots, slot, counts);
-  dsync("k_sl_counts");
   HIP_LAUNCH_CHECK();
 }
 
@@ -1931,7 +1764,7 @@ void radix_slot_first_pass(const int64_t *keys, int64_t n, int total_bits, int f
   // (XCD-major: the cursors one XCD claims from share cache lines only with each other -- the
   // bucket-major order d * 8 + x put 8 XCDs' atomics on every line)
   slot_pass(PartDigit{keys, total_bits, second_bits, (uint32_t)nb1 - 1}, n, first_bits, in, out, widths, ncols, 0,
-            kXcds, nullptr, nullptr, 0, 0, 0, 1, int64_t(kXcds) * nb1, slot, ws, counts, overflow, as_stream(stream), n);
+            kXcds, nullptr, nullptr, 0, 0, 0, 1, int64_t(kXcds) * nb1, slot, ws, counts, overflow, as_stream(stream));
 }
 
 void radix_slot_rows_pass(const int64_t *keys, int64_t n, int total_bits, int first_bits, int second_bits,
@@ -1944,16 +1777,15 @@ void radix_slot_rows_pass(const int64_t *keys, int64_t n, int total_bits, int fi
   const PartDigit dg{keys, total_bits, 0, (1u << second_bits) - 1};
   if (first_counts != nullptr) {  // after a slot first pass: segment g = (bucket g >> 3, XCD g & 7)
     slot_pass(dg, n, second_bits, in, out, widths, ncols, 2, kXcds * nb1, nullptr, first_counts, first_slot, 3, 0, 1,
-              nslots, slot, ws, counts, overflow, as_stream(stream), int64_t(kXcds) * nb1 * first_slot + kRPTile);
+              nslots, slot, ws, counts, overflow, as_stream(stream));
   } else {  // after an XT first pass: segment g = exact bucket g (bases in its workspace)
     CYLON_CHECK(nb1 <= kSlotMaxSeg, Code::Invalid, "slot pass: too many input buckets");
     const uint32_t *bbase = reinterpret_cast<const uint32_t *>(first_ws + xt_layout(n, (uint32_t)nb1).bbase);
     slot_pass(dg, n, second_bits, in, out, widths, ncols, 1, nb1, bbase, nullptr, 0, 0, 0, 1, nslots, slot, ws,
-              counts, overflow, as_stream(stream), n);
+              counts, overflow, as_stream(stream));
   }
 }
 
-bool radix_xt_enabled() { return rp_xt(); }
 
 // ---- sort prologue: the keys' varying bits (OR ^ AND), the images' min and max, and the first
 // pass's per-tile histogram of the order image's low 10 bits in ONE read of the keys (the separate
@@ -2264,22 +2096,42 @@ template <int OJ>
 __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_rj_count(
     const int64_t *__restrict__ pkeys, const int64_t *__restrict__ poffs, const int64_t *__restrict__ bkeys,
     const int64_t *__restrict__ boffs, int64_t nparts, int cap, int64_t pstride, int64_t *__restrict__ counts,
-    int *overflow, int64_t pslot, int64_t bslot) {
+    int *overflow, int64_t pslot, int64_t bslot, const int64_t *__restrict__ items, int64_t nitems,
+    const uint8_t *__restrict__ skip) {
   using KT = int64_t;
   // pstride > 1: only partitions 0, pstride, 2 pstride, ... are counted, into counts[p / pstride]
   // (the sampled output-size estimate of the fused write path).  Output rows per partition:
-  // matches, + unmatched probe rows (OJ & 1), + unmatched build rows (OJ & 2).
+  // matches, + unmatched probe rows (OJ & 1), + unmatched build rows (OJ & 2).  items != nullptr:
+  // counts[i] = output rows of split item i (its deferred sides' unmatched rows excluded); skip[p]:
+  // partition p is covered by items (counts 0, never an LDS overflow).
   __shared__ __attribute__((aligned(16))) uint16_t bst[kRJBuckets + 8];
   __shared__ KT skeys[kRJMaxRows];
   __shared__ uint8_t flg[(OJ & kOJBuild) ? kRJMaxRows : 1];
   __shared__ uint32_t wsum[kRCWaves];
   __shared__ unsigned long long csum[kRCWaves];
-  const int64_t nsample = (nparts + pstride - 1) / pstride;
+  const int64_t nsample = items ? nitems : (nparts + pstride - 1) / pstride;
   for (int64_t ci = blockIdx.x; ci < nsample; ci += gridDim.x) {
-    const int64_t p = ci * pstride;
     int64_t rb, nr, lb, nl;
-    part_span(boffs, bslot, p, rb, nr);
-    part_span(poffs, pslot, p, lb, nl);
+    int iflags = 0;
+    if (items) {
+      const int64_t *it = items + ci * kRJItemWords;
+      lb = it[0];
+      nl = it[1];
+      rb = it[2];
+      nr = it[3];
+      iflags = (int)it[4];
+    } else {
+      const int64_t p = ci * pstride;
+      if (skip && skip[p]) {
+        if (threadIdx.x == 0) counts[ci] = 0;
+        continue;
+      }
+      part_span(boffs, bslot, p, rb, nr);
+      part_span(poffs, pslot, p, lb, nl);
+    }
+    // unmatched rows of a side count here unless the item defers them (emitted by emission items)
+    const bool pun = (OJ & kOJProbe) && !(iflags & kRJItemPDefer);
+    const bool bun = (OJ & kOJBuild) && !(iflags & kRJItemBDefer);
     if (nr > cap) {  // uniform branch: whole block
       if (threadIdx.x == 0) {
         atomicOr(overflow, 1);
@@ -2289,7 +2141,7 @@ __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4)))
     }
     if (nr == 0 || nl == 0) {
       if (threadIdx.x == 0)
-        counts[ci] = (nr == 0 && (OJ & kOJProbe) ? nl : 0) + (nl == 0 && (OJ & kOJBuild) ? nr : 0);
+        counts[ci] = (nr == 0 && pun ? nl : 0) + (nl == 0 && bun ? nr : 0);
       continue;
     }
     // build keys are read twice (claim, then place): the second read hits L2 and the block
@@ -2327,10 +2179,10 @@ __global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4)))
       for (int u = 0; u < 4; ++u)
         if (l0 + u * kRCThreads < nl) {
           const uint32_t mc = rj_count_mark<OJ>(bst, skeys, pk[u], flg);
-          c += (OJ & kOJProbe) && mc == 0 ? 1u : mc;
+          c += pun && mc == 0 ? 1u : mc;
         }
     }
-    if (OJ & kOJBuild) {
+    if ((OJ & kOJBuild) && bun) {  // uniform branch
       __syncthreads();  // every probe has flagged its matches
       for (int i = threadIdx.x; i < nr; i += blockDim.x) c += flg[i] ? 0u : 1u;
     }
@@ -2381,9 +2233,13 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
                                                             ColSet bs, BuildOut bo,
                                                             unsigned long long *__restrict__ cursor, int64_t out_cap,
                                                             int *__restrict__ overflow,
-                                                            unsigned long long *__restrict__ stamps, int pkey,
+                                                            int pkey,
                                                             uint8_t *__restrict__ ppres, uint8_t *__restrict__ bpres,
-                                                            int64_t pslot, int64_t bslot) {
+                                                            int64_t pslot, int64_t bslot,
+                                                            const int64_t *__restrict__ items, int64_t nitems,
+                                                            const uint8_t *__restrict__ skip,
+                                                            uint8_t *__restrict__ gprobe,
+                                                            uint8_t *__restrict__ gbuild) {
   using KT = int64_t;
   // out_offs != nullptr: partition p's rows start at out_offs[p] (exact count kernel ran first).
   // out_offs == nullptr: fused count -- each partition claims its rows from *cursor with one
@@ -2404,18 +2260,31 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
   uint8_t *flg = area + ((OJ & kOJBuild) ? bo.match_off : 0);
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
-  int tix = -1;  // debug stamps (CYLON_RJ_STAMPS): block 0's partition count, RP_STAMP slots 0..5
-  for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
-    int64_t rb, nr, lb, nl;
-    part_span(boffs, bslot, p, rb, nr);
-    part_span(poffs, pslot, p, lb, nl);
+  // work w < nitems: split item w (heaviest first: they lead the grid-stride order); else partition
+  // w - nitems unless skip marks it as covered by items.  Items run in cursor mode only.
+  for (int64_t w = blockIdx.x; w < nitems + nparts; w += gridDim.x) {
+    int64_t rb, nr, lb, nl, p = -1;
+    int iflags = 0;
+    if (w < nitems) {
+      const int64_t *it = items + w * kRJItemWords;
+      lb = it[0];
+      nl = it[1];
+      rb = it[2];
+      nr = it[3];
+      iflags = (int)it[4];
+    } else {
+      p = w - nitems;
+      if (skip && skip[p]) continue;
+      part_span(boffs, bslot, p, rb, nr);
+      part_span(poffs, pslot, p, lb, nl);
+    }
+    const bool pdefer = (iflags & kRJItemPDefer) != 0, bdefer = (iflags & kRJItemBDefer) != 0;
+    const bool pemit = (iflags & kRJItemPEmit) != 0, bemit = (iflags & kRJItemBEmit) != 0;
     if (nr > cap && out_offs == nullptr && threadIdx.x == 0) atomicOr(overflow, 1);
     // inner: both sides needed; outer: a preserved side alone still emits its rows
     const bool live = (nr > 0 && nl > 0) || ((OJ & kOJProbe) && nl > 0) || ((OJ & kOJBuild) && nr > 0);
     if (!live || nr > cap) continue;
-    ++tix;
-    RP_STAMP(0);
-    const int64_t obase = out_offs ? out_offs[p] : 0;
+    const int64_t obase = out_offs && p >= 0 ? out_offs[p] : 0;
     // ---- phase A: probe rows of this wave's slice into VGPRs (in flight during the build)
     const int64_t per = (nl + kRJWaves - 1) / kRJWaves;  // each wave owns a contiguous probe slice
     const int64_t s0 = lb + std::min<int64_t>(nl, wave * per);
@@ -2491,7 +2360,6 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
         if (r < nr) bk[i] = skeys[r];
       }
     }
-    RP_STAMP(1);
     uint32_t rk[kRJRowsPerThread];
 #pragma unroll
     for (int i = 0; i < kRJRowsPerThread; ++i)
@@ -2506,31 +2374,44 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
         const uint32_t pos = bst[rj_bucket(bk[i])] + rk[i];
         skeys[pos] = bk[i];
         perm[pos] = (uint16_t)r;
+        if ((OJ & kOJBuild) && bemit) flg[pos] = gbuild[rb + r];  // matched by an earlier item
       }
     }
     __syncthreads();
-    RP_STAMP(2);
     // ---- phase C: count this wave's output rows (matches; a lone row for an unmatched probe row
     // of a probe-preserving join), flag matched build slots, slice offsets
-    auto emitted = [&](uint32_t mc) -> uint32_t { return (OJ & kOJProbe) ? (mc > 0u ? mc : 1u) : mc; };
+    // (a deferring item emits no lone probe rows; an emission item skips rows an earlier item matched)
+    auto emitted = [&](uint32_t mc) -> uint32_t { return (OJ & kOJProbe) && !pdefer ? (mc > 0u ? mc : 1u) : mc; };
+    auto plive = [&](int64_t l) -> bool { return !pemit || gprobe[l] == 0; };
+    // output rows of probe row l (key k); a deferring item records the row's match here, before the
+    // output claim (a claim that does not fit must still leave the flags of an exact rerun's count)
+    auto count_row = [&](int64_t l, KT k) -> uint32_t {
+      const uint32_t mc = rj_count_mark<OJ>(bst, skeys, k, flg);
+      if ((OJ & kOJProbe) && pdefer && mc) gprobe[l] = 1;
+      return plive(l) ? emitted(mc) : 0u;
+    };
     uint32_t c = 0;
 #pragma unroll
     for (int u = 0; u < kRJProbeRounds; ++u)
-      if (s0 + u * kWave + lane < s1) c += emitted(rj_count_mark<OJ>(bst, skeys, pk[u], flg));
+      if (s0 + u * kWave + lane < s1) c += count_row(s0 + u * kWave + lane, pk[u]);
     {  // later rounds' probe keys two rounds at a time (both loads in flight before either count)
       int64_t l = s0 + kRJProbeRounds * kWave + lane;
       for (; l + kWave < s1; l += 2 * kWave) {
         const KT ka = pkeys[l], kb = pkeys[l + kWave];
-        c += emitted(rj_count_mark<OJ>(bst, skeys, ka, flg)) + emitted(rj_count_mark<OJ>(bst, skeys, kb, flg));
+        c += count_row(l, ka) + count_row(l + kWave, kb);
       }
-      if (l < s1) c += emitted(rj_count_mark<OJ>(bst, skeys, pkeys[l], flg));
+      if (l < s1) c += count_row(l, pkeys[l]);
     }
     for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
     if (lane == 0) wtot[wave] = c;
     __syncthreads();
-    // unmatched build rows (flags final after the barrier above): emitted after every match
+    // unmatched build rows (flags final after the barrier above): emitted after every match, or
+    // recorded for a later emission item (bdefer)
     uint32_t unm = 0;
-    if (OJ & kOJBuild) {
+    if ((OJ & kOJBuild) && bdefer) {
+      for (int i = threadIdx.x; i < nr; i += blockDim.x)
+        if (flg[i]) gbuild[rb + perm[i]] = 1;
+    } else if (OJ & kOJBuild) {
       uint32_t u = 0;
       for (int i = threadIdx.x; i < nr; i += blockDim.x) u += flg[i] ? 0u : 1u;
       for (int d = kWave / 2; d > 0; d >>= 1) u += __shfl_xor(u, d, kWave);
@@ -2558,7 +2439,6 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
 #pragma unroll
     for (int w = 0; w < kRJWaves; ++w) ubase += wtot[w];
     for (int w = 0; w < wave; ++w) base += wtot[w];
-    RP_STAMP(3);
     // ---- phase D: emit.  Round u + 1's probe row is loaded while round u expands (kn / vn), so
     // only the first round after the phase-A prefetch waits on memory.
     static_assert(kRJProbeRounds == 1, "emit prefetch assumes one phase-A round");
@@ -2566,7 +2446,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
     uint64_t vn[MAXP] = {};
     for (int u = 0; s0 + (int64_t)u * kWave < s1; ++u) {
       const int64_t l = s0 + (int64_t)u * kWave + lane;
-      const bool active = l < s1;
+      const bool active = l < s1 && plive(l);
       KT k = 0;
       uint64_t v[MAXP] = {};
       if (u == 0) {
@@ -2584,12 +2464,20 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
         for (int q = 0; q < MAXP; ++q)
           if (q < pc.n && q != pkey) vn[q] = ldw<W8>(pc.in[q], l + kWave, pc.width[q]);
       }
-      uint32_t i0 = 0, i1 = 0, mc = 0;
+      // i0: the first match (scans for match rank j start there); pure: the matches are adjacent, so
+      // match j is slot i0 + j (a hot key's chunk fills its bucket: no O(mc^2) rank scans)
+      uint32_t i0 = 0, i1 = 0, mc = 0, pure = 0;
       if (active) {
         const uint32_t b = rj_bucket(k);
-        i0 = bst[b];
         i1 = bst[b + 1];
-        for (uint32_t i = i0; i < i1; ++i) mc += (skeys[i] == k);
+        uint32_t last = 0;
+        for (uint32_t i = bst[b]; i < i1; ++i)
+          if (skeys[i] == k) {
+            if (mc == 0) i0 = i;
+            last = i;
+            ++mc;
+          }
+        pure = mc > 0 && last - i0 + 1 == mc;
       }
       const uint32_t ec = active ? emitted(mc) : 0u;  // output rows of this probe row
       uint32_t inc = ec;  // wave inclusive scan of output counts
@@ -2619,13 +2507,16 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
         const KT ko = rj_shfl_key(k, owner);
         const uint64_t kw = (uint64_t)ko;
         const uint32_t b0 = __shfl(i0, owner, kWave), b1 = __shfl(i1, owner, kWave);
+        const bool opure = __shfl(pure, owner, kWave) != 0u;
         const bool omatched = !(OJ & kOJProbe) || __shfl(mc, owner, kWave) > 0u;
         uint64_t vo[MAXP];
 #pragma unroll
         for (int q = 0; q < MAXP; ++q) vo[q] = q == pkey ? kw : (uint64_t)rj_shfl64((int64_t)v[q], owner);
         if (act) {
           int r = -1;
-          if (omatched)
+          if (omatched && opure)
+            r = perm[b0 + j];
+          else if (omatched)
             for (uint32_t i = b0, c = 0; i < b1; ++i) {
               if (skeys[i] != ko) continue;
               if (c == j) {
@@ -2664,7 +2555,7 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
       }
       base += wsum;
     }
-    if (OJ & kOJBuild) {  // ---- phase E: the unmatched build rows, in bucket-slot order
+    if ((OJ & kOJBuild) && !bdefer) {  // ---- phase E: the unmatched build rows, in bucket-slot order
       __syncthreads();  // every wave is done with wtot
       int64_t at = ubase;
       for (int i0 = 0; i0 < nr; i0 += kRJThreads) {
@@ -2688,7 +2579,6 @@ __global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__res
         __syncthreads();  // wtot reused by the next round
       }
     }
-    RP_STAMP(4);
   }
 }
 
@@ -2696,30 +2586,34 @@ static int rj_grid(int64_t nparts) { return (int)std::min<int64_t>(nparts, kNumC
 
 void radix_join_count(const int64_t *pkeys, const int64_t *poffs, const int64_t *bkeys, const int64_t *boffs,
                       int64_t nparts, int64_t cap, int64_t *counts, int *overflow, void *stream, int64_t pstride,
-                      int outer, int64_t pslot, int64_t bslot) {
+                      int outer, int64_t pslot, int64_t bslot, const RJSplit *split) {
   CYLON_CHECK(cap > 0 && cap <= kRJMaxRows, Code::Invalid, "radix join capacity " << cap);
   CYLON_CHECK(pstride >= 1, Code::Invalid, "partition stride " << pstride);
   CYLON_CHECK(outer >= 0 && outer <= 3, Code::Invalid, "radix join outer mode " << outer);
   hipStream_t s = as_stream(stream);
   HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
-  const int64_t nsample = (nparts + pstride - 1) / pstride;
+  const int64_t *items = split ? split->items : nullptr;
+  const int64_t nitems = items ? split->nitems : 0;
+  const uint8_t *skip = split ? split->skip : nullptr;
+  const int64_t nsample = items ? nitems : (nparts + pstride - 1) / pstride;
+  if (nsample == 0) return;
   const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(nsample, kNumCUs * 12)));
   switch (outer) {
     case 0:
       hipLaunchKernelGGL(k_rj_count<0>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
-                         pstride, counts, overflow, pslot, bslot);
+                         pstride, counts, overflow, pslot, bslot, items, nitems, skip);
       break;
     case 1:
       hipLaunchKernelGGL(k_rj_count<1>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
-                         pstride, counts, overflow, pslot, bslot);
+                         pstride, counts, overflow, pslot, bslot, items, nitems, skip);
       break;
     case 2:
       hipLaunchKernelGGL(k_rj_count<2>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
-                         pstride, counts, overflow, pslot, bslot);
+                         pstride, counts, overflow, pslot, bslot, items, nitems, skip);
       break;
     default:
       hipLaunchKernelGGL(k_rj_count<3>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
-                         pstride, counts, overflow, pslot, bslot);
+                         pstride, counts, overflow, pslot, bslot, items, nitems, skip);
   }
   HIP_LAUNCH_CHECK();
 }
@@ -2728,17 +2622,19 @@ template <bool W8, bool DMA, int OJ>
 static void rj_write_launch(dim3 grid, hipStream_t s, const int64_t *pk, const int64_t *poffs, const int64_t *bk,
                             const int64_t *boffs, int64_t nparts, int cap, const int64_t *out_offs, const ColSet &pc,
                             const ColSet &bs, const BuildOut &bo, unsigned long long *cur, int64_t out_cap,
-                            int *overflow, unsigned long long *st, int pkey, uint8_t *ppres, uint8_t *bpres,
-                            int64_t pslot, int64_t bslot) {
+                            int *overflow, int pkey, uint8_t *ppres, uint8_t *bpres,
+                            int64_t pslot, int64_t bslot, const RJSplit &sp) {
   hipLaunchKernelGGL((k_rj_write<4, 3, W8, DMA, OJ>), grid, dim3(kRJThreads), 0, s, pk, poffs, bk, boffs, nparts, cap,
-                     out_offs, pc, bs, bo, cur, out_cap, overflow, st, pkey, ppres, bpres, pslot, bslot);
+                     out_offs, pc, bs, bo, cur, out_cap, overflow, pkey, ppres, bpres, pslot, bslot, sp.items, sp.nitems,
+                     sp.skip, sp.gprobe, sp.gbuild);
 }
 
 void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t *bkeys, const int64_t *boffs,
                       int64_t nparts, int64_t cap, const int64_t *out_offs, const uint8_t *const *pin,
                       uint8_t *const *pout, const int *pw, int npc, const uint8_t *const *bin, uint8_t *const *bout,
                       const int *bw, int nbc, void *stream, int64_t *cursor, int64_t out_cap, int *overflow, int pkey,
-                      int outer, uint8_t *ppres, uint8_t *bpres, int64_t pslot, int64_t bslot) {
+                      int outer, uint8_t *ppres, uint8_t *bpres, int64_t pslot, int64_t bslot,
+                      const RJSplit *split) {
   CYLON_CHECK(pkey >= -1 && pkey < npc, Code::Invalid, "radix join probe key column " << pkey);
   CYLON_CHECK(npc <= kMaxFusedCols && nbc <= kMaxFusedCols, Code::Invalid, "too many columns");
   CYLON_CHECK(out_offs != nullptr || (cursor != nullptr && overflow != nullptr), Code::Invalid,
@@ -2746,6 +2642,10 @@ void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t 
   CYLON_CHECK(outer >= 0 && outer <= 3, Code::Invalid, "radix join outer mode " << outer);
   CYLON_CHECK(!(outer & kOJProbe) || bpres, Code::Invalid, "radix join: probe-preserving mode needs build presence");
   CYLON_CHECK(!(outer & kOJBuild) || ppres, Code::Invalid, "radix join: build-preserving mode needs probe presence");
+  const RJSplit sp = split ? *split : RJSplit{};
+  CYLON_CHECK(sp.nitems == 0 || (out_offs == nullptr && sp.items), Code::Invalid,
+              "radix join write: split items need the cursor mode");
+  if (sp.nitems + nparts == 0) return;
   CYLON_CHECK(cap > 0 && cap <= radix_join_capacity(bw, bin, nbc, outer & kOJBuild), Code::Invalid,
               "radix join capacity " << cap);
   ColSet pc, bs;
@@ -2781,21 +2681,13 @@ void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t 
   hipStream_t s = as_stream(stream);
   // probe columns beyond 4 and staged build columns beyond 3 are loaded in place (slower, correct)
   unsigned long long *cur = reinterpret_cast<unsigned long long *>(cursor);
-  static const bool stamp = std::getenv("CYLON_RJ_STAMPS") != nullptr;  // debug: phase stamps to stderr
-  unsigned long long *st = nullptr;
-  if (stamp) {
-    HIP_CHECK(hipStreamSynchronize(s));
-    HIP_CHECK(hipMalloc(&st, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
-    HIP_CHECK(hipMemset(st, 0, sizeof(unsigned long long) * kRPStampTiles * kRPStampSlots));
-  }
-  const dim3 grid(rj_grid(nparts));
+  const dim3 grid(rj_grid(nparts + sp.nitems));
   // LDS-DMA build staging: write kernel 33.9 -> 32.9 ms per 1B x 1B join (profiles/r03/lds_dma_ab.txt)
-  const char *dm = std::getenv("CYLON_RJ_DMA");  // A/B knob: 0 = register staging
-  const bool dma = w8 && !(dm && dm[0] == '0');
+  const bool dma = w8;
   const int ci = (int)cap;
 #define RJW(W8_, DMA_, OJ_)                                                                                        \
   rj_write_launch<W8_, DMA_, OJ_>(grid, s, pkeys, poffs, bkeys, boffs, nparts, ci, out_offs, pc, bs, bo, cur, out_cap, \
-                                  overflow, st, pkey, ppres, bpres, pslot, bslot)
+                                  overflow, pkey, ppres, bpres, pslot, bslot, sp)
   if (outer == 0) {
     if (dma) RJW(true, true, 0);
     else if (w8) RJW(true, false, 0);
@@ -2812,24 +2704,6 @@ void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t 
   }
 #undef RJW
   HIP_LAUNCH_CHECK();
-  if (st) {  // mean cycles per partition: load+stage, index build, count+claim, emit, then to the next
-    HIP_CHECK(hipStreamSynchronize(s));
-    std::vector<unsigned long long> h(kRPStampTiles * kRPStampSlots);
-    HIP_CHECK(hipMemcpy(h.data(), st, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost));
-    HIP_CHECK(hipFree(st));
-    double sum[5] = {0};
-    int np = 0;
-    for (int t = 1; t + 1 < kRPStampTiles; ++t) {
-      const unsigned long long *a = &h[t * kRPStampSlots], *b = &h[(t + 1) * kRPStampSlots];
-      if (b[0] == 0 || a[4] == 0) break;
-      for (int j = 1; j <= 4; ++j) sum[j - 1] += (double)(a[j] - a[j - 1]);
-      sum[4] += (double)(b[0] - a[0]);
-      ++np;
-    }
-    if (np)
-      std::fprintf(stderr, "rj_stamps partitions=%d total=%.0f | stage=%.0f index=%.0f count=%.0f emit=%.0f\n", np,
-                   sum[4] / np, sum[0] / np, sum[1] / np, sum[2] / np, sum[3] / np);
-  }
 }
 
 

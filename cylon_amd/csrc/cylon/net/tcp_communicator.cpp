@@ -1,4 +1,5 @@
 // Full-mesh TCP communicator (see tcp_communicator.hpp).
+#include "cylon/knobs.hpp"
 #include "tcp_communicator.hpp"
 
 #include <arpa/inet.h>
@@ -55,7 +56,7 @@ void tune(int fd) {
 // address other ranks can reach this one at: the local end of a (UDP, unsent)
 // connection towards the rendezvous host, i.e. the interface that routes there
 std::string local_address(const std::string &master) {
-  if (const char *h = std::getenv("CYLON_TCP_HOST")) return h;
+  if (const char *h = knobs::Get("TCP_HOST")) return h;
   if (master.empty() || master == "127.0.0.1" || master == "localhost") return "127.0.0.1";
   addrinfo hints{}, *res = nullptr;
   hints.ai_family = AF_INET;

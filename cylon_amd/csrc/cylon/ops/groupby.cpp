@@ -13,6 +13,7 @@
 //   * output names carry a single prefix (the reference double-prefixes in
 //     its two-phase path);
 //   * COUNT counts non-null values (identical to the reference on non-null data).
+#include "cylon/knobs.hpp"
 #include <algorithm>
 #include <cstdlib>
 #include <limits>
@@ -246,8 +247,7 @@ static Column agg_column(const Exec &ex, const TablePtr &t, const GroupInfo &gi,
 // unspecified as well).  Returns nullptr when not eligible or when a partition overflows its
 // LDS table.  Reference: groupby/hash_groupby.cpp:92-201, compute/aggregate_kernels.hpp:92-263.
 static int64_t radix_groupby_min_rows() {
-  const char *e = std::getenv("CYLON_RADIX_GROUPBY_MIN_ROWS");  // tuning / test knob
-  return e ? std::atoll(e) : (int64_t(1) << 22);
+  return knobs::Int("RADIX_GROUPBY_MIN_ROWS", int64_t(1) << 22);
 }
 
 namespace {

@@ -16,7 +16,9 @@
 //   3. outer completion: matched flags (mark_indices) + compaction of the
 //      unmatched rows of the preserved side(s), appended with -1 partners.
 //   4. materialisation: one fused gather launch per side (K4).
+#include "cylon/knobs.hpp"
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdlib>
 #include <limits>
@@ -72,11 +74,33 @@ static constexpr int64_t kSortedBuildRows = int64_t(1) << 20;
 static constexpr int64_t kEmitProbeRows = int64_t(1) << 22;
 
 // inner-join index pairs on int64 keys via the K5 hash table (build = smaller side)
+// Global-table hash join (the path of joins the LDS radix join does not take).  Clustering-free
+// directory: the build keys are sorted once, and the open-addressing table holds each DISTINCT key
+// once with its head index h; key k's build rows are perm[hstart[h], hstart[h + 1]).  A hot key is
+// one slot, so no probe ever walks through its duplicates (a row-per-slot linear-probing multimap
+// puts a hot key's duplicates into every nearby key's probe path: primary clustering that grows
+// with the hot run's length).  Probes find <= 1 directory entry; the (probe, head) pairs are then
+// expanded into (probe, build row) pairs in probe-row order.  Reference: the unordered_multimap of
+// join/hash_join.cpp:255-298.
 static std::pair<at::Tensor, at::Tensor> hash_join_pairs(const Exec &ex, const at::Tensor &lk, const at::Tensor &rk) {
   const bool build_left = lk.numel() < rk.numel();
-  const at::Tensor &bk = build_left ? lk : rk;
+  const at::Tensor &bk0 = build_left ? lk : rk;
   const at::Tensor &pk = build_left ? rk : lk;
-  const int64_t nb = bk.numel(), np = pk.numel();
+  const int64_t nb0 = bk0.numel(), np = pk.numel();
+  at::Tensor sk, perm, hstart;
+  {
+    CYLON_PHASE("join.build.directory", ex.device);
+    auto sr = at::sort(bk0);
+    sk = std::get<0>(sr);
+    perm = std::get<1>(sr);
+    at::Tensor head = at::ones({nb0}, ex.opts(at::kBool));
+    if (nb0 > 1) head.slice(0, 1, nb0).copy_(sk.slice(0, 1, nb0) != sk.slice(0, 0, nb0 - 1));
+    at::Tensor hpos = head.nonzero().flatten();
+    sk = sk.index_select(0, hpos);  // distinct keys, ascending
+    hstart = at::cat({hpos, at::full({1}, nb0, ex.opts(at::kLong))});
+  }
+  const at::Tensor &bk = sk;
+  const int64_t nb = bk.numel();
   const int64_t cap = next_pow2(std::max<int64_t>(2 * nb, 64));
   const int shift = 64 - __builtin_ctzll((unsigned long long)cap);
   at::Tensor table;
@@ -96,10 +120,10 @@ static std::pair<at::Tensor, at::Tensor> hash_join_pairs(const Exec &ex, const a
     table = at::empty({t.tsize * 2}, ex.opts(at::kLong));  // HashSlot = 2 x int64
     t.slots = reinterpret_cast<HashSlot *>(table.data_ptr());
     KCALL(ex, hash_table_init, t.slots, t.tsize);
-    const at::Tensor &sk = which ? kb : ka;
-    const at::Tensor &sr = which ? vb : va;
+    const at::Tensor &sk2 = which ? kb : ka;
+    const at::Tensor &sr2 = which ? vb : va;
     const at::Tensor &pm = which ? ka : kb;
-    KCALL(ex, hash_table_place, reinterpret_cast<const uint64_t *>(ptr<int64_t>(sk)), ptr<int64_t>(sr),
+    KCALL(ex, hash_table_place, reinterpret_cast<const uint64_t *>(ptr<int64_t>(sk2)), ptr<int64_t>(sr2),
           ptr<int64_t>(pm), nb, t);
   } else {
     table = at::empty({cap * 2}, ex.opts(at::kLong));
@@ -107,28 +131,47 @@ static std::pair<at::Tensor, at::Tensor> hash_join_pairs(const Exec &ex, const a
     KCALL(ex, hash_table_init, t.slots, cap);
     KCALL(ex, hash_build, ptr<int64_t>(bk), nb, t);
   }
+  // (probe row, head) pairs: at most one per probe row
+  at::Tensor po, ho;
   if (ex.gpu && np >= kEmitProbeRows) {
     CYLON_PHASE("join.probe.emit", ex.device);
-    // single-pass probe into an over-allocated pair buffer; exact two-pass fallback on overflow
-    const int64_t capacity = np + np / 4 + 4096;
-    at::Tensor po = ex.empty_i64(capacity), bo = ex.empty_i64(capacity), cnt = ex.empty_i64(1);
+    const int64_t capacity = np + 4096;
+    po = ex.empty_i64(capacity);
+    ho = ex.empty_i64(capacity);
+    at::Tensor cnt = ex.empty_i64(1);
     KCALL(ex, hash_probe_emit, ptr<int64_t>(pk), np, t, capacity, ptr<int64_t>(cnt), ptr<int64_t>(po),
-          ptr<int64_t>(bo));
+          ptr<int64_t>(ho));
     const int64_t m = read_i64(cnt, 0);
-    if (m <= capacity) {
-      po = po.slice(0, 0, m);
-      bo = bo.slice(0, 0, m);
-      return build_left ? std::make_pair(bo, po) : std::make_pair(po, bo);
+    CYLON_CHECK(m <= np, Code::ExecutionError, "directory probe: " << m << " matches for " << np << " probe rows");
+    po = po.slice(0, 0, m);
+    ho = ho.slice(0, 0, m);
+  } else {
+    CYLON_PHASE("join.probe.twopass", ex.device);
+    at::Tensor counts = ex.empty_i64(np);
+    KCALL(ex, hash_probe_count, ptr<int64_t>(pk), np, t, ptr<int64_t>(counts));
+    at::Tensor offs = exclusive_scan(ex, counts);
+    counts = at::Tensor();
+    const int64_t m = read_i64(offs, np);
+    po = ex.empty_i64(m);
+    ho = ex.empty_i64(m);
+    KCALL(ex, hash_probe_write, ptr<int64_t>(pk), np, t, ptr<int64_t>(offs), ptr<int64_t>(po), ptr<int64_t>(ho));
+  }
+  table = at::Tensor();
+  at::Tensor bo;
+  {
+    CYLON_PHASE("join.probe.expand", ex.device);
+    at::Tensor first = hstart.index_select(0, ho);
+    at::Tensor cnt = hstart.index_select(0, ho + 1) - first;
+    const int64_t m = po.numel() ? cnt.sum().item<int64_t>() : 0;
+    if (m != po.numel()) {  // some key has duplicates: repeat each pair over its key's rows
+      at::Tensor excl = cnt.cumsum(0) - cnt;
+      po = po.repeat_interleave(cnt, 0, m);
+      at::Tensor pos = (first - excl).repeat_interleave(cnt, 0, m) + at::arange(m, ex.opts(at::kLong));
+      bo = perm.index_select(0, pos);
+    } else {
+      bo = perm.index_select(0, first);
     }
   }
-  CYLON_PHASE("join.probe.twopass", ex.device);
-  at::Tensor counts = ex.empty_i64(np);
-  KCALL(ex, hash_probe_count, ptr<int64_t>(pk), np, t, ptr<int64_t>(counts));
-  at::Tensor offs = exclusive_scan(ex, counts);
-  counts = at::Tensor();
-  const int64_t m = read_i64(offs, np);
-  at::Tensor po = ex.empty_i64(m), bo = ex.empty_i64(m);
-  KCALL(ex, hash_probe_write, ptr<int64_t>(pk), np, t, ptr<int64_t>(offs), ptr<int64_t>(po), ptr<int64_t>(bo));
   return build_left ? std::make_pair(bo, po) : std::make_pair(po, bo);
 }
 
@@ -139,8 +182,7 @@ static std::pair<at::Tensor, at::Tensor> hash_join_pairs(const Exec &ex, const a
 // exact key where every column is fixed width <= 8 bytes.
 // ---------------------------------------------------------------------------
 static int64_t radix_join_min_rows() {
-  const char *e = std::getenv("CYLON_RADIX_JOIN_MIN_ROWS");  // tuning / test knob
-  return e ? std::atoll(e) : (int64_t(1) << 22);
+  return knobs::Int("RADIX_JOIN_MIN_ROWS", int64_t(1) << 22);
 }
 
 static constexpr int64_t kRadixRowsPerPart = 4096;  // avg build rows per partition (LDS table: 6144 max)
@@ -168,6 +210,14 @@ struct RadixSide {
   std::vector<int> vpos;
   std::vector<at::Tensor> vwords;
 };
+
+// rows of each partition / its first row in the partitioned arrays (slot mode: p * slot)
+static at::Tensor part_counts(const RadixSide &s, int64_t nparts) {
+  return s.slot ? s.offs.slice(0, 0, nparts) : s.offs.slice(0, 1, nparts + 1) - s.offs.slice(0, 0, nparts);
+}
+static at::Tensor part_starts(const RadixSide &s, int64_t nparts) {
+  return s.slot ? at::arange(nparts, s.offs.options()) * s.slot : s.offs.slice(0, 0, nparts);
+}
 
 // the partition / write kernels move validity packed when every data column is 8 bytes wide
 // (the all-8-byte kernel variants; byte runs of 1-byte validity columns cost 2x)
@@ -206,15 +256,10 @@ static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Te
   const size_t nslots = cur.size();
   std::vector<int> packed;
   // hash partitions: the LDS join ignores row order inside a partition, so the first LSD pass
-  // ranks with LDS atomics (later passes must keep its order; CYLON_RP_STABLE=1 restores the
-  // stable ballot ranking everywhere for A/B runs)
-  static const bool force_stable = [] {
-    const char *e = std::getenv("CYLON_RP_STABLE");
-    return e && e[0] == '1';
-  }();
+  // ranks with LDS atomics (later passes must keep its order)
   RadixSide s;
   std::vector<at::Tensor> sl;
-  if (slot > 0 && !range && !force_stable)
+  if (slot > 0 && !range)
     sl = RadixPartitionSlotted(ex, cur, widths, bits, slot, &offs, &s.overflow,
                                packs_validity(t) ? &packed : nullptr);
   if (!sl.empty()) {
@@ -222,7 +267,7 @@ static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Te
     s.slot = slot;
   } else {
     cur = RadixPartition(ex, std::move(cur), widths, bits, &offs, range, packs_validity(t) ? &packed : nullptr,
-                         range != nullptr || force_stable);
+                         range != nullptr);
   }
   s.keys = cur[0];
   s.offs = offs;
@@ -397,15 +442,14 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   auto fits = [&](int64_t mean) { return (double)mean + 8.0 * std::sqrt((double)mean) + 16.0 <= (double)cap; };
   int bits = 0;
   while (bits < 24 && !fits((nb + (int64_t(1) << bits) - 1) >> bits)) ++bits;
-  if (const char *xb = std::getenv("CYLON_RJ_EXTRA_BITS"))  // A/B knob: finer partitions
-    bits = std::min(bits + std::max(0, std::atoi(xb)), 2 * 10);
+  if (const int64_t xb = knobs::Int("RJ_EXTRA_BITS", 0))  // test knob: finer partitions
+    bits = std::min(bits + (int)std::max<int64_t>(0, xb), 2 * 10);
   const int64_t nparts = int64_t(1) << bits;
   // Slot mode for two-pass partitions (>= 11 bits): the second pass claims fixed-size partition
   // slots (mean + 8 sigma + 64 rows) instead of reading the keys once more for exact offsets
   // (k_rp_hist_tiles + scans + k_part_offsets, ~2 ms per 1B-row side).  A partition beyond its
-  // slot (skewed keys) sends that side through the exact passes.  Knob: CYLON_RJ_SLOT=0.
-  const char *se = std::getenv("CYLON_RJ_SLOT");
-  const bool slot_on = !(se && se[0] == '0');
+  // slot (skewed keys) sends that side through the exact passes.  Test knob: CYLON_RJ_SLOT=0.
+  const bool slot_on = knobs::Flag("RJ_SLOT", true);
   auto slot_of = [&](int64_t rows) -> int64_t {
     if (!slot_on || bits < 11) return 0;
     const double mean = (double)rows / (double)nparts;
@@ -432,6 +476,81 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   }
   RadixSide &B = build_left ? L : R;
   RadixSide &P = build_left ? R : L;
+  // Skewed partitions are handled per partition, not per join: a partition whose build side exceeds
+  // the LDS capacity or whose probe side is hot (> 2 probe chunks) is skipped by the partition loop
+  // and covered by split work items (kernel_decls.inc RJSplit): build chunks of <= cap rows x probe
+  // chunks of pch rows, so a hot key costs its own rows, never the whole join (reference: one
+  // unordered_multimap, join/hash_join.cpp:255-298).
+  const int64_t np_rows = build_left ? nr : nl;
+  const int64_t pch = std::max<int64_t>(int64_t(1) << 15, 8 * ((np_rows + nparts - 1) / nparts));
+  const int64_t split_rows = std::max<int64_t>(8, std::min<int64_t>(cap, knobs::Int("RJ_SPLIT_ROWS", cap)));
+  at::Tensor bcnt = part_counts(B, nparts), pcnt = part_counts(P, nparts);
+  at::Tensor heavy = at::logical_or(bcnt > split_rows, pcnt > 2 * pch);
+  at::Tensor skip = heavy.to(at::kByte);
+  const int64_t nheavy = heavy.sum().item<int64_t>();
+  std::vector<int64_t> items, emits;  // kRJItemWords per item
+  int64_t emit_bound = 0;
+  if (nheavy > 0) {
+    at::Tensor hidx = heavy.nonzero().flatten();
+    at::Tensor info = at::stack({part_starts(P, nparts).index_select(0, hidx), pcnt.index_select(0, hidx),
+                                 part_starts(B, nparts).index_select(0, hidx), bcnt.index_select(0, hidx)},
+                                1)
+                          .cpu()
+                          .contiguous();
+    const int64_t *h = info.data_ptr<int64_t>();
+    std::vector<std::array<int64_t, hip::kRJItemWords>> work;
+    for (int64_t i = 0; i < nheavy; ++i) {
+      const int64_t lb0 = h[4 * i], nl0 = h[4 * i + 1], rb0 = h[4 * i + 2], nr0 = h[4 * i + 3];
+      const int64_t nbc = std::max<int64_t>(1, (nr0 + split_rows - 1) / split_rows);
+      const int64_t npc = nl0 > 2 * pch ? (nl0 + pch - 1) / pch : 1;
+      // a side split into several items learns "unmatched" only from all of them: deferred
+      const bool pdef = (oj & 1) && nbc > 1, bdef = (oj & 2) && npc > 1;
+      const int64_t fl = (pdef ? hip::kRJItemPDefer : 0) | (bdef ? hip::kRJItemBDefer : 0);
+      for (int64_t bc = 0; bc < nbc; ++bc)
+        for (int64_t pc = 0; pc < npc; ++pc) {
+          const int64_t b0 = nr0 * bc / nbc, b1 = nr0 * (bc + 1) / nbc, p0 = nl0 * pc / npc, p1 = nl0 * (pc + 1) / npc;
+          if (b1 > b0 || p1 > p0) work.push_back({lb0 + p0, p1 - p0, rb0 + b0, b1 - b0, fl});
+        }
+      if (pdef) {
+        for (int64_t pc = 0; pc < npc; ++pc)
+          emits.insert(emits.end(), {lb0 + nl0 * pc / npc, nl0 * (pc + 1) / npc - nl0 * pc / npc, 0, 0,
+                                     (int64_t)hip::kRJItemPEmit});
+        emit_bound += nl0;
+      }
+      if (bdef) {
+        for (int64_t bc = 0; bc < nbc; ++bc)
+          emits.insert(emits.end(), {0, 0, rb0 + nr0 * bc / nbc, nr0 * (bc + 1) / nbc - nr0 * bc / nbc,
+                                     (int64_t)hip::kRJItemBEmit});
+        emit_bound += nr0;
+      }
+    }
+    // heaviest items first: they lead the write kernel's grid-stride order
+    std::stable_sort(work.begin(), work.end(), [](const auto &a, const auto &b) {
+      return a[1] * std::max<int64_t>(1, a[3]) > b[1] * std::max<int64_t>(1, b[3]);
+    });
+    for (const auto &w : work) items.insert(items.end(), w.begin(), w.end());
+    trace::add_counter("join.radix.split_partitions", nheavy);
+    trace::add_counter("join.radix.split_items", (int64_t)work.size());
+  }
+  const int64_t nitems = (int64_t)items.size() / hip::kRJItemWords, nemits = (int64_t)emits.size() / hip::kRJItemWords;
+  at::Tensor items_d = nitems ? at::tensor(items, at::TensorOptions().dtype(at::kLong)).to(ex.device) : at::Tensor();
+  at::Tensor emits_d = nemits ? at::tensor(emits, at::TensorOptions().dtype(at::kLong)).to(ex.device) : at::Tensor();
+  at::Tensor gprobe, gbuild;  // matched flags of the deferred sides (per partitioned row)
+  for (int64_t i = 0; i < nitems; ++i) {
+    const int64_t f = items[i * hip::kRJItemWords + 4];
+    if ((f & hip::kRJItemPDefer) && !gprobe.defined()) gprobe = at::zeros({std::max<int64_t>(1, P.keys.numel())}, ex.opts(at::kByte));
+    if ((f & hip::kRJItemBDefer) && !gbuild.defined()) gbuild = at::zeros({std::max<int64_t>(1, B.keys.numel())}, ex.opts(at::kByte));
+  }
+  hip::RJSplit split_main, split_emit;
+  split_main.skip = nheavy ? skip.data_ptr<uint8_t>() : nullptr;
+  split_main.items = nitems ? ptr<int64_t>(items_d) : nullptr;
+  split_main.nitems = nitems;
+  split_main.gprobe = gprobe.defined() ? gprobe.data_ptr<uint8_t>() : nullptr;
+  split_main.gbuild = gbuild.defined() ? gbuild.data_ptr<uint8_t>() : nullptr;
+  split_emit = split_main;
+  split_emit.skip = nullptr;
+  split_emit.items = nemits ? ptr<int64_t>(emits_d) : nullptr;
+  split_emit.nitems = nemits;
   // Output size.  Exact mode: a count kernel over every partition, a scan, then the write
   // kernel at the scanned offsets.  Fused mode (default): the count kernel runs on every
   // 32nd partition only, the output is allocated for the extrapolated size + 2 % (partitions
@@ -443,11 +562,9 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   // test / A-B knobs: CYLON_RJ_EXACT_COUNT=1 (count kernel over every partition),
   // CYLON_RJ_FUSED_MIN_PARTS (default 4096), CYLON_RJ_ESTIMATE_SCALE (scales the estimate: < 1
   // forces the exact rerun)
-  const char *ec = std::getenv("CYLON_RJ_EXACT_COUNT");
-  const char *fm = std::getenv("CYLON_RJ_FUSED_MIN_PARTS");
-  const char *es = std::getenv("CYLON_RJ_ESTIMATE_SCALE");
-  const bool exact_count = ec && ec[0] == '1';
-  const int64_t fused_min = fm ? std::atoll(fm) : 4096;
+  const bool exact_count = knobs::Flag("RJ_EXACT_COUNT", false);
+  const int64_t fused_min = knobs::Int("RJ_FUSED_MIN_PARTS", 4096);
+  const char *es = knobs::Get("RJ_ESTIMATE_SCALE");
   const double est_scale = es ? std::atof(es) : 1.0;
   int64_t stride = exact_count || nparts < fused_min ? 1 : std::min<int64_t>(32, std::max<int64_t>(1, nparts / 64));
   at::Tensor counts;
@@ -456,11 +573,13 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   int64_t m = 0, alloc = 0;
   {
     CYLON_PHASE("join.radix.count", ex.device);
+    hip::RJSplit skip_only;  // the partition count skips split partitions (items are counted below)
+    skip_only.skip = split_main.skip;
     auto count = [&](int64_t st) {
       counts = ex.empty_i64((nparts + st - 1) / st);
       hip::radix_join_count(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
                             nparts, cap, ptr<int64_t>(counts), overflow.data_ptr<int>(), ex.stream, st, oj, P.slot,
-                            B.slot);
+                            B.slot, &skip_only);
     };
     count(stride);
     // the ranking guard of the stable (second and later) partition passes
@@ -499,6 +618,18 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
       const double est = (double)tail[0].item<int64_t>() * (double)nparts / (double)counts.numel();
       alloc = (int64_t)(est * 1.02 * est_scale) + (est_scale < 1.0 ? 0 : 65536);
       trace::add_counter("join.radix.estimated_rows", (int64_t)est);
+    }
+    if (nitems > 0) {  // split items: counted exactly (their deferred rows bounded), cursor mode
+      at::Tensor ic = ex.empty_i64(nitems);
+      hip::RJSplit only = split_main;
+      only.skip = nullptr;
+      hip::radix_join_count(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
+                            0, cap, ptr<int64_t>(ic), overflow.data_ptr<int>(), ex.stream, 1, oj, P.slot, B.slot,
+                            &only);
+      const int64_t exact_items = ic.sum().item<int64_t>();
+      alloc = (stride == 1 ? m : alloc) + exact_items + emit_bound;
+      stride = 2;  // (cursor mode below)
+      out_offs = at::Tensor();
     }
   }
   CYLON_PHASE("join.radix.write", ex.device);
@@ -553,7 +684,13 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
                           nparts, cap, offs, pc.in.data(), pc.out.data(), pc.w.data(), (int)pc.in.size(),
                           bc.in.data(), bc.out.data(), bc.w.data(), (int)bc.in.size(), ex.stream, cursor, rows,
                           overflow.data_ptr<int>(), pkey, oj, ppres.defined() ? ppres.data_ptr<uint8_t>() : nullptr,
-                          bpres.defined() ? bpres.data_ptr<uint8_t>() : nullptr, P.slot, B.slot);
+                          bpres.defined() ? bpres.data_ptr<uint8_t>() : nullptr, P.slot, B.slot, &split_main);
+    if (nemits > 0)  // the deferred sides' unmatched rows, after every item recorded its matches
+      hip::radix_join_write(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
+                            0, cap, nullptr, pc.in.data(), pc.out.data(), pc.w.data(), (int)pc.in.size(),
+                            bc.in.data(), bc.out.data(), bc.w.data(), (int)bc.in.size(), ex.stream, cursor, rows,
+                            overflow.data_ptr<int>(), pkey, oj, ppres.defined() ? ppres.data_ptr<uint8_t>() : nullptr,
+                            bpres.defined() ? bpres.data_ptr<uint8_t>() : nullptr, P.slot, B.slot, &split_emit);
   };
   if (stride == 1) {
     allocate(m);
@@ -576,6 +713,8 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
       if (sink) sink->size = off;
       cursor.zero_();
       overflow.zero_();
+      if (gprobe.defined()) gprobe.zero_();
+      if (gbuild.defined()) gbuild.zero_();
       allocate(m);
       write(m, nullptr, ptr<int64_t>(cursor));
       CYLON_CHECK(at::cat({cursor, overflow.to(at::kLong)}).cpu().equal(at::tensor({m, (int64_t)0})),
@@ -737,8 +876,7 @@ static TablePtr sorted_merge_join(const Exec &ex, const TablePtr &left, const Ta
 // Returns nullptr when the keys are too sparse for 12-bit partitions or a
 // partition overflows (skew): the caller then runs sorted_merge_join.
 static bool range_join_enabled() {
-  const char *e = std::getenv("CYLON_RANGE_JOIN");  // test / tuning knob: 0 = sort-merge path only
-  return !(e && e[0] == '0');
+  return knobs::Flag("RANGE_JOIN", true);  // test knob: 0 = sort-merge path only
 }
 
 static TablePtr range_join(const Exec &ex, const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
@@ -753,10 +891,7 @@ static TablePtr range_join(const Exec &ex, const TablePtr &left, const TablePtr 
   int span_bits = 0;
   while (span_bits < 64 && (span >> span_bits) != 0) ++span_bits;
   // ~half the LDS capacity per side and partition on average: far below the cap for uniform keys
-  static const int64_t target = [] {  // tuning knob
-    const char *e = std::getenv("CYLON_RANGE_JOIN_TARGET");
-    return e ? std::max<int64_t>(1, std::atoll(e)) : hip::range_join_max_rows() / 2;
-  }();
+  const int64_t target = hip::range_join_max_rows() / 2;
   int bits = 0;
   while ((std::max(nl, nr) >> bits) > target) ++bits;
   // sparse keys: up to 16x more (smaller) partitions than the row count asks for keep

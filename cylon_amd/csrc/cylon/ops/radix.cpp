@@ -1,5 +1,6 @@
 // Shared radix partitioning driver for the LDS radix join and group-by
 // (kernels: radix_join.hip k_rp_hist / k_rows_pass / k_part_offsets).
+#include "cylon/knobs.hpp"
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -22,11 +23,7 @@ BytePacking PackByteColumns(const Exec &ex, std::vector<at::Tensor> &cur, std::v
       others8 &= widths[i] == 8;
     }
   }
-  static const bool enabled = [] {  // A/B knob (tools/nullable_probe.py)
-    const char *e = std::getenv("CYLON_PACK_VALIDITY");
-    return !(e && e[0] == '0');
-  }();
-  bp.active = enabled && !bp.byte_idx.empty() && others8 && n > 0;
+  bp.active = !bp.byte_idx.empty() && others8 && n > 0;
   if (!bp.active) return bp;
   const int k = (int)bp.byte_idx.size(), nw = bp.words();
   std::vector<const uint8_t *> src;
@@ -68,10 +65,6 @@ std::vector<at::Tensor> UnpackByteColumns(const Exec &ex, const BytePacking &bp,
   return out;
 }
 
-static int max_digit_bits() {  // digit bits per pass (<= 10); tuning / test knob, read per call
-  const char *e = std::getenv("CYLON_RADIX_DIGIT_BITS");
-  return e ? std::max(1, std::min(10, std::atoi(e))) : 10;
-}
 
 
 static thread_local bool tl_partition_lb_off = false;  // set while a look-back fallback repartitions
@@ -89,16 +82,15 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
   // look-back passes (stable hash partitions of 1-2 all-8-byte columns, as for the sort): the first
   // pass counts (chunk, next digit) and the later ones take their offsets by look-back, without a
   // tile histogram (1B-row group-by 24.2 / 25.3 -> 23.3 / 24.0 ms, profiles/r04/partition_lookback_ab.txt).
-  // CYLON_PARTITION_LOOKBACK=0 returns to the exact tile histograms.
-  const char *plb = std::getenv("CYLON_PARTITION_LOOKBACK");
-  const char *dbu = std::getenv("CYLON_RP_DEBUG_UNSTABLE");
-  const bool lb_want = !range && stable && !tl_partition_lb_off && !(plb && plb[0] == '0') && !(dbu && dbu[0] == '1');
+  // Test knob CYLON_PARTITION_LOOKBACK=0 returns to the exact tile histograms.
+  const bool lb_want = !range && stable && !tl_partition_lb_off && knobs::Flag("PARTITION_LOOKBACK", true) &&
+                       !knobs::Flag("RP_DEBUG_UNSTABLE", false);
   const std::vector<at::Tensor> orig = lb_want ? cur : std::vector<at::Tensor>();  // for the (never seen) fallback
   // Nullable payloads made a 200M join 24.8 -> 47.8 ms with unpacked validity bytes
   // (16-B byte runs per pass instead of 128-B runs); packed: 30.2 ms.
   std::vector<int> pw = widths;
   const BytePacking bp = PackByteColumns(ex, cur, pw, n);
-  const int max_db = max_digit_bits();
+  const int max_db = 10;  // digit bits per pass
   const int npass = (bits + max_db - 1) / max_db;
   int shift = 0;
   at::Tensor ws;
@@ -178,7 +170,7 @@ std::vector<at::Tensor> RadixPartitionSlotted(const Exec &ex, std::vector<at::Te
   const int64_t n = cur[0].numel();
   // second (low) digit <= 9 bits, first (high) digit <= 10 bits: 11 .. 19 partition bits
   const int db2 = std::min(9, bits / 2), db1 = bits - db2;
-  if (bits < 2 || db1 > 10 || max_digit_bits() < 10) return {};
+  if (bits < 2 || db1 > 10) return {};
   // (the block size of the unstable pass does not depend on the column count)
   if (!hip::radix_slot_eligible(n, (int)cur.size(), db1, db2)) return {};
   std::vector<int> pw = widths;

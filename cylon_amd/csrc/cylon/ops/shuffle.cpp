@@ -5,6 +5,7 @@
 // shuffle_table_by_hashing), arrow/arrow_all_to_all.cpp (per-buffer header +
 // payload protocol).  Partition -> rank mapping is identical: partition i goes
 // to rank i when P == world, else to rank i*world/P (table.cpp:89-106).
+#include "cylon/knobs.hpp"
 #include <limits>
 
 #include "util.hpp"
@@ -156,9 +157,7 @@ static std::vector<WirePlan> plan_wire(const std::vector<TablePtr> &ts) {
     plans[i].base.assign(ts[i]->Columns(), 0);
   }
   auto ctx = ts[0]->GetContext();
-  std::string v = ctx->GetConfig("shuffle_narrow", "");
-  if (v.empty())
-    if (const char *e = std::getenv("CYLON_SHUFFLE_NARROW")) v = e;
+  const std::string v = knobs::ConfigOr(ctx->GetConfig("shuffle_narrow", ""), "SHUFFLE_NARROW");
   if (v == "0") return plans;
   std::vector<std::pair<size_t, int>> cand;
   for (size_t i = 0; i < ts.size(); ++i)
@@ -461,9 +460,7 @@ int ShuffleChunks(const TablePtr &a, const TablePtr &b) {
   for (const TablePtr &t : {a, b})
     for (const auto &c : t->columns())
       if (c.is_var()) return 1;
-  std::string v = ctx->GetConfig("shuffle_chunks", "");
-  if (v.empty())
-    if (const char *e = std::getenv("CYLON_SHUFFLE_CHUNKS")) v = e;
+  const std::string v = knobs::ConfigOr(ctx->GetConfig("shuffle_chunks", ""), "SHUFFLE_CHUNKS");
   if (!v.empty()) return std::max(1, std::min(64, std::atoi(v.c_str())));
   if (!a->device().is_cuda() || !ctx->ShuffleRequired()) return 1;
   at::Tensor rows = at::tensor({std::min(a->Rows(), b->Rows())}, at::TensorOptions().dtype(at::kLong)).to(a->device());
@@ -638,6 +635,7 @@ struct GapPlan {
   std::vector<std::vector<int64_t>> send_off, send_cnt;  // [K][W] (layout rows)
   std::vector<std::vector<int64_t>> recv_off, recv_cnt;  // [K][W]
   std::vector<int64_t> in_off, in_rows;                  // [K] chunk k's input range
+  std::vector<int64_t> wire_rows;                        // [K] rows ANY rank puts on the wire in chunk k
 };
 
 static GapPlan gap_plan(int W, int K, int me, bool self_wire, const std::function<int64_t(int, int, int)> &cnt,
@@ -657,6 +655,13 @@ static GapPlan gap_plan(int W, int K, int me, bool self_wire, const std::functio
   g.send_cnt = g.recv_off = g.recv_cnt = g.send_off;
   g.in_off.assign(K, 0);
   g.in_rows.assign(K, 0);
+  // the skip-the-collective decision must be the same on every rank: computed from the
+  // whole gathered count matrix, not from this rank's own sends and receives
+  g.wire_rows.assign(K, 0);
+  for (int k = 0; k < K; ++k)
+    for (int from = 0; from < W; ++from)
+      for (int to = 0; to < W; ++to)
+        if (from != to || self_wire) g.wire_rows[k] += cnt(k, from, to);
   int64_t row = 0, own = 0;  // own: rows of the sender's buckets placed so far
   for (int k = 0; k < K; ++k)
     for (int r = 0; r < W; ++r) {
@@ -783,9 +788,9 @@ static GapPending post_gapped(const TablePtr &lay, const GapPlan &g, int k, cons
                               const std::vector<at::Tensor> &wire, const std::vector<int64_t> &nullable) {
   GapPending pd;
   auto comm = lay->GetContext()->GetCommunicator();
-  int64_t moving = 0;
-  for (int r = 0; r < g.W; ++r) moving += g.send_cnt[k][r] + g.recv_cnt[k][r];
-  if (moving == 0) return pd;  // nothing crosses the wire in this chunk (world 1, own rows local)
+  // nothing crosses the wire in chunk k on ANY rank (world 1 with the own rows local): every rank
+  // skips the collectives together; otherwise every rank posts, with zero counts where it is idle
+  if (g.wire_rows[k] == 0) return pd;
   Exec ex(lay->device());
   auto scaled = [](std::vector<int64_t> v, int64_t per, int64_t minus) {
     for (auto &x : v) x = (x - minus) * per;
@@ -857,9 +862,7 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
     return;
   }
   const int W = ctx->GetWorldSize(), me = ctx->GetRank();
-  std::string v = ctx->GetConfig("shuffle_chunks", "");
-  if (v.empty())
-    if (const char *e = std::getenv("CYLON_SHUFFLE_CHUNKS")) v = e;
+  const std::string v = knobs::ConfigOr(ctx->GetConfig("shuffle_chunks", ""), "SHUFFLE_CHUNKS");
   const int forced = !allow_chunks ? 1 : (v.empty() ? 0 : std::max(1, std::min(64, std::atoi(v.c_str()))));
   // 8 chunks on the device: the first chunk's exchange (the only one with no join to hide behind)
   // is 1/8 of the traffic; the self-wire trace overlaps 82.5 % of the RCCL time at 8 chunks vs
@@ -876,9 +879,7 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
     for (const auto &c : t->columns()) nflags.push_back(c.nullable() ? 1 : 0);
   parts.push_back(at::tensor(rows, at::TensorOptions().dtype(at::kLong)).to(dev));
   parts.push_back(at::tensor(nflags, at::TensorOptions().dtype(at::kLong)).to(dev));
-  std::string nv = ctx->GetConfig("shuffle_narrow", "");
-  if (nv.empty())
-    if (const char *e = std::getenv("CYLON_SHUFFLE_NARROW")) nv = e;
+  const std::string nv = knobs::ConfigOr(ctx->GetConfig("shuffle_narrow", ""), "SHUFFLE_NARROW");
   std::vector<std::pair<int, int>> cand;  // (table, column) narrowable on the wire
   if (nv != "0")
     for (int side = 0; side < NT; ++side)
@@ -918,9 +919,7 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
   const int64_t off_null = NT, off_mm = off_null + coff[NT], off_cnt = off_mm + 2 * (int64_t)cand.size();
   CYLON_CHECK(off_cnt + (int64_t)NT * P == D, Code::ExecutionError, "shuffle descriptor layout");
   // own rows through the communicator as well (test knob: keeps the RCCL kernels running at world 1)
-  std::string sw = ctx->GetConfig("shuffle_self_rccl", "");
-  if (sw.empty())
-    if (const char *e = std::getenv("CYLON_SHUFFLE_SELF_RCCL")) sw = e;
+  const std::string sw = knobs::ConfigOr(ctx->GetConfig("shuffle_self_rccl", ""), "SHUFFLE_SELF_RCCL");
   const bool self_wire = sw == "1";
   int K = Kc;
   if (!forced) {  // chunked when every rank holds >= 2^24 rows of every table

@@ -8,6 +8,7 @@
 // Strings sort by stable passes over their length and then their 8-byte
 // big-endian chunks from the last chunk to the first, which yields byte-wise
 // lexicographic order.
+#include "cylon/knobs.hpp"
 #include <limits>
 #include <cstdlib>
 
@@ -127,8 +128,7 @@ at::Tensor SortIndices(const TablePtr &t, const std::vector<int> &cols, const st
 // afterwards (~50 G random accesses/s, profiles/membench.txt).  Constant
 // leading/trailing bits of the image are skipped (OR ^ AND reduction).
 static int64_t radix_sort_min_rows() {
-  const char *e = std::getenv("CYLON_RADIX_SORT_MIN_ROWS");  // tuning / test knob
-  return e ? std::atoll(e) : (int64_t(1) << 22);
+  return knobs::Int("RADIX_SORT_MIN_ROWS", int64_t(1) << 22);
 }
 
 static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
@@ -159,8 +159,7 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
   // raw 8-byte integer keys on the XCD-tile passes: one read gives the varying bits AND the first
   // pass's per-tile histogram (bits [0, 10) of the image), folded below when the pass digit starts
   // at bit 0 -- the separate reduction read every key once more (3.3 ms of a 2B-row sort)
-  const char *ph = std::getenv("CYLON_SORT_PREHIST");  // A/B knob: 0 = separate reduction + histogram
-  const bool prehist = raw_in && n > 0 && hip::radix_xt_enabled() && !(ph && ph[0] == '0');
+  const bool prehist = raw_in && n > 0;
   at::Tensor pre_ws;
   uint64_t diff, img_min = 0, img_max = 0;
   if (prehist) {
@@ -195,10 +194,9 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
     const int lo = __builtin_ctzll(diff);
     int hi = 64 - __builtin_clzll(diff);
     // digits of image - min when the keys span fewer bits than vary (every image agrees with the
-    // minimum below bit lo, so image - min keeps those bits zero); knob CYLON_SORT_SUB_MIN=0
-    const char *sm = std::getenv("CYLON_SORT_SUB_MIN");
+    // minimum below bit lo, so image - min keeps those bits zero)
     uint64_t sub = 0;
-    if (prehist && img_max > img_min && !(sm && sm[0] == '0')) {
+    if (prehist && img_max > img_min) {
       const int hr = 64 - __builtin_clzll(img_max - img_min);
       if (hr < hi) {
         sub = img_min;
@@ -219,10 +217,9 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
     at::Tensor ws;
     // each pass but the last writes the next pass's digits (2 B/row) as it stores the keys: the
     // next pass's tile histogram then reads those instead of the 8-byte keys (XCD-tile passes)
-    const char *nde = std::getenv("CYLON_SORT_NEXT_DIGITS");  // A/B knob: 0 = histograms read the keys
     // look-back passes (1-2 all-8-byte columns): no tile histograms and no next-digit array at all
     const bool lb_on = hip::radix_sort_lb_eligible(n, (int)cur.size(), widths.data(), dbits.data(), npass, ex.stream);
-    const bool nd_on = !lb_on && hip::radix_xt_enabled() && npass > 1 && !(nde && nde[0] == '0');
+    const bool nd_on = !lb_on && npass > 1;
     at::Tensor nd = nd_on ? at::empty({n}, ex.opts(at::kShort)) : at::Tensor();
     at::Tensor lbws = lb_on ? ex.empty_i64(hip::radix_sort_lb_workspace(n)) : at::Tensor();
     if (lb_on) trace::add_counter("sort.radix.lookback", 1);
@@ -301,9 +298,7 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
 // order images checks that the result is non-decreasing in the requested order
 static void verify_sorted(const TablePtr &out, int col, bool asc) {
   auto ctx = out->GetContext();
-  std::string v = ctx->GetConfig("verify_sort", "");
-  if (v.empty())
-    if (const char *e = std::getenv("CYLON_VERIFY_SORT")) v = e;
+  const std::string v = knobs::ConfigOr(ctx->GetConfig("verify_sort", ""), "VERIFY_SORT");
   if (v != "1" || out->Rows() < 2) return;
   Exec ex(out->device());
   const Column &c = out->column(col);

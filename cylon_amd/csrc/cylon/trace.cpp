@@ -1,4 +1,5 @@
 // Tracing / counters / logging implementation (see trace.hpp).
+#include "cylon/knobs.hpp"
 #include "trace.hpp"
 
 #include <hip/hip_runtime_api.h>
@@ -44,7 +45,7 @@ int64_t now_ns() {
 bool enabled() {
   int e = g_enabled.load();
   if (e < 0) {
-    const char *v = std::getenv("CYLON_TRACE");
+    const char *v = knobs::Get("TRACE");
     e = (v && v[0] && v[0] != '0') ? 1 : 0;
     g_enabled.store(e);
   }
@@ -54,10 +55,7 @@ bool enabled() {
 void set_enabled(bool on) { g_enabled.store(on ? 1 : 0); }
 
 int log_level() {
-  static int lvl = [] {
-    const char *v = std::getenv("CYLON_LOG_LEVEL");
-    return v ? std::atoi(v) : 1;
-  }();
+  static int lvl = (int)knobs::Int("LOG_LEVEL", 1);
   return lvl;
 }
 

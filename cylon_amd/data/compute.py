@@ -260,7 +260,8 @@ def _device_cast(c, target: pa.DataType, safe: bool):
     try:
         # K15 string <-> number casts on the device (kernels/strcast.hip); None: the host parser
         if is_var(c):
-            if pa.types.is_string(src) and num(target) and target != pa.float16():
+            # uint64 targets: the device parser reads int64, Arrow's host cast takes the full range
+            if pa.types.is_string(src) and num(target) and target not in (pa.float16(), pa.uint64()):
                 return C.cast_string_to_number(c, ab.to_cylon_type(target))
             return None
         if pa.types.is_string(target) and pa.types.is_integer(src) and src != pa.uint64() and c.type.type != T.BOOL:

@@ -23,4 +23,6 @@ def rows_from_argv(default: int) -> int:
 
 def report(name: str, value) -> None:
     """One "name value" line per result (tests/test_python_examples.py parses them)."""
-    print(f"{name} {value}", flush=True)
+    # one write per line: ranks share the pipe, and print's separate end="\n" write could interleave
+    sys.stdout.write(f"{name} {value}\n")
+    sys.stdout.flush()

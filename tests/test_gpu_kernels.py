@@ -32,28 +32,22 @@ def test_lds_atomics_return_in_lane_order(gpu_ctx):
     assert C.lds_lane_order_violations("cuda:0", 256, 4096) == 0
 
 
-@pytest.mark.parametrize("rank", ["wave", "ballot"])
-def test_radix_sort_stable_under_both_rankings(gpu_ctx, rank):
-    """The row-moving sort (stable LSD passes) under each stable ranking method, in a child
-    process (the choice is fixed per process): ties keep their input order."""
-    import os
-    import subprocess
-    import sys
-    code = (
-        "import numpy as np, pyarrow as pa\n"
-        "from cylon_amd import CylonContext, Table\n"
-        "ctx = CylonContext(config=None, distributed=False, device='cuda:0')\n"
-        "rng = np.random.default_rng(3)\n"
-        "n = 400_000\n"
-        "k = rng.integers(-300, 300, n)\n"
-        "t = Table(pa.table({'k': k, 'p': np.arange(n)}), ctx)\n"
-        "s = t.sort('k').to_pandas()\n"
-        "ref = np.lexsort((np.arange(n), k))\n"
-        "assert np.array_equal(s['p'].to_numpy(), ref), 'unstable'\n"
-        "print('ok')\n")
-    env = dict(os.environ, CYLON_RP_RANK=rank, CYLON_RADIX_SORT_MIN_ROWS="1")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]
+@pytest.mark.parametrize("rank", [1, 2])
+def test_radix_sort_stable_under_both_rankings(gpu_ctx, monkeypatch, rank):
+    """The row-moving sort (stable LSD passes) under each stable ranking method (1 = wave-atomic,
+    2 = ballots, forced with rp_set_ranking; 0 re-probes the device afterwards): ties keep their
+    input order."""
+    rng = np.random.default_rng(3)
+    n = 400_000
+    k = rng.integers(-300, 300, n)
+    t = Table(pa.table({"k": k, "p": np.arange(n)}), gpu_ctx)
+    monkeypatch.setenv("CYLON_RADIX_SORT_MIN_ROWS", "1")
+    C.rp_set_ranking(rank)
+    try:
+        s = t.sort("k").to_pandas()
+    finally:
+        C.rp_set_ranking(0)
+    assert np.array_equal(s["p"].to_numpy(), np.lexsort((np.arange(n), k))), "unstable"
 
 
 @pytest.mark.parametrize("nparts", [1, 2, 3, 4, 7, 8, 64, 1000])
@@ -163,18 +157,15 @@ def test_radix_sort_large_int64(gpu_ctx):
     assert torch.equal(s, torch.sort(k).values)
 
 
-@pytest.mark.parametrize("case", ["uniform63", "uniform63_global", "small_range_ties", "skewed", "desc",
-                                  "one_chunk"])
+@pytest.mark.parametrize("case", ["uniform63", "small_range_ties", "skewed", "desc", "one_chunk"])
 def test_lookback_sort_passes_match_stable_torch_sort(gpu_ctx, monkeypatch, case):
     """Look-back LSD passes (2 all-8-byte columns: key + payload; chunk plans counted by the previous
     pass, offsets from a decoupled look-back) vs torch's stable sort; payload order = stability.
-    Balanced chunks run XCD-local (look-back words in one L2), skewed ones (and uniform63_global,
-    forced) let every XCD take any chunk's tiles with written-through words."""
+    Balanced chunks run XCD-local (look-back words in one L2), skewed ones (
+    90 % one key) let every XCD take any chunk's tiles with written-through words."""
     n = 5_000_000
     g = torch.Generator(device="cuda").manual_seed(21)
-    if case == "uniform63_global":
-        monkeypatch.setenv("CYLON_SORT_LB_LOCAL", "0")
-    if case in ("uniform63", "uniform63_global", "desc"):
+    if case in ("uniform63", "desc"):
         k = torch.randint(-2**62, 2**62, (n,), generator=g, device="cuda")
     elif case == "small_range_ties":
         k = torch.randint(-3000, 3000, (n,), generator=g, device="cuda") * 977
@@ -204,15 +195,15 @@ def test_lookback_sort_passes_match_stable_torch_sort(gpu_ctx, monkeypatch, case
 
 @pytest.mark.parametrize("op", ["groupby", "unique", "union"])
 def test_partition_lookback_passes_match_exact(gpu_ctx, monkeypatch, op):
-    """Look-back passes of the stable two-pass hash partitions (group-by, set ops): 5-bit digits force
-    two passes on a small table; the result equals the exact-histogram passes (CYLON_PARTITION_LOOKBACK=0)."""
-    n = 3_000_000
+    """Look-back passes of the stable two-pass hash partitions (group-by, set ops): 12M rows need more
+    than 10 partition bits, i.e. two passes; the result equals the exact-histogram passes
+    (CYLON_PARTITION_LOOKBACK=0)."""
+    n = 12_000_000
     g = torch.Generator(device="cuda").manual_seed(23)
-    k = torch.randint(0, 400_000, (n,), generator=g, device="cuda")
+    k = torch.randint(0, 1_600_000, (n,), generator=g, device="cuda")
     x = torch.randint(0, 3, (n,), generator=g, device="cuda").to(torch.float64)
     t = Table.from_torch(gpu_ctx, {"k": k, "x": x})
     t2 = Table.from_torch(gpu_ctx, {"k": k[: n // 2] + 7, "x": x[: n // 2]})
-    monkeypatch.setenv("CYLON_RADIX_DIGIT_BITS", "5")
     monkeypatch.setenv("CYLON_RADIX_GROUPBY_MIN_ROWS", "1")
     monkeypatch.setenv("CYLON_RADIX_SETOP_MIN_ROWS", "1")
     res = []
@@ -484,7 +475,7 @@ def test_radix_join_ranking_guard_falls_back(gpu_ctx, monkeypatch, count_mode):
     c = dict(C.trace_counters())
     C.trace_enable(False)
     monkeypatch.delenv("CYLON_RP_DEBUG_UNSTABLE")
-    C.rp_reset_lane_order()  # the guard switched the device to ballot ranking: probe again
+    C.rp_set_ranking(0)  # the guard switched the device to ballot ranking: probe again
     assert c.get("join.radix.order_violation_fallback", 0) == 1, c
     assert got.row_count == ref.row_count
     pd.testing.assert_frame_equal(_sorted_df(got), _sorted_df(ref))
@@ -513,9 +504,10 @@ def test_verify_sort_config(gpu_ctx, dtype):
 
 @pytest.mark.parametrize("op", ["join", "sort", "union", "groupby"])
 def test_xcd_tile_schedule_matches_chunk_schedule(gpu_ctx, monkeypatch, op):
-    """XCD-tile radix passes (default: per-tile histograms + offset scan, tiles claimed in order per XCD,
-    a block whose chunk is exhausted steals from the others) against the per-block-chunk schedule
-    (CYLON_RP_XT=0): identical results, including the stable order of the row sort."""
+    """XCD-tile radix passes (wave-atomic ranking: per-tile histograms or look-back offsets, tiles
+    claimed in order per XCD) against the per-block-chunk histogram schedule the ballot ranking runs
+    for 1-2 column passes (rp_set_ranking(2): 512-thread blocks): identical results, including the
+    stable order of the row sort."""
     rng = np.random.default_rng(23)
     n = 3_000_000  # > 256 tiles per pass: every XCD chunk is non-trivial
     a = pa.table({"k": rng.integers(0, n // 3, n), "v": rng.random(n), "i": rng.integers(-50, 50, n)})
@@ -525,8 +517,8 @@ def test_xcd_tile_schedule_matches_chunk_schedule(gpu_ctx, monkeypatch, op):
                  ("CYLON_RADIX_GROUPBY_MIN_ROWS", "1024")):
         monkeypatch.setenv(k, v)
     res = []
-    for xt in ("0", "1"):
-        monkeypatch.setenv("CYLON_RP_XT", xt)
+    for mode in (2, 1):
+        C.rp_set_ranking(mode)
         if op == "join":
             res.append(_sorted_df(A.join(B, "inner", "hash", on=["k"], left_prefix="l_", right_prefix="r_")))
         elif op == "sort":
@@ -536,6 +528,7 @@ def test_xcd_tile_schedule_matches_chunk_schedule(gpu_ctx, monkeypatch, op):
         else:
             res.append(A.local_groupby("k", {"v": ["sum"], "i": ["max"]}).to_pandas()
                        .sort_values("k").reset_index(drop=True))
+    C.rp_set_ranking(0)
     if op == "groupby":
         pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-12, atol=1e-12)
     else:

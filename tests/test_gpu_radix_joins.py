@@ -270,18 +270,63 @@ def test_radix_groupby_nunique(gpu_ctx, monkeypatch, case):
     pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-9, atol=1e-9, check_dtype=False)
 
 
-@pytest.mark.parametrize("nacc,wide", [(2, False), (2, True), (3, False)])
-def test_radix_groupby_3m_rows_1m_groups(gpu_ctx, monkeypatch, nacc, wide):
-    """The round-3 fault shape: 3M rows / ~1M groups with two accumulators run in the three-slot
-    <3, 2048> LDS table (CYLON_RG_WIDE=1), next to the exact two-slot table and three accumulators
-    (which use <3, 2048> anyway)."""
+@pytest.mark.parametrize("nacc", [2, 3])
+def test_radix_groupby_3m_rows_1m_groups(gpu_ctx, monkeypatch, nacc):
+    """The round-3 fault shape: 3M rows / ~1M groups with two and three accumulators (the <2, 2048>
+    and <3, 2048> LDS tables)."""
     rng = np.random.default_rng(23)
     n = 3_000_000
     t = pa.table({"k": rng.integers(0, n // 3, n), "v": rng.random(n), "i": rng.integers(-50, 50, n)})
     T = Table(t, gpu_ctx)
     aggs = {2: {"v": ["sum"], "i": ["max"]}, 3: {"v": ["sum", "max"], "i": ["max"]}}[nacc]
-    if wide:
-        monkeypatch.setenv("CYLON_RG_WIDE", "1")
     res, cnt = _groupby_both(T, ["k"], aggs, monkeypatch)
     assert cnt[0].get("groupby.radix.groups", 0) == len(res[0]) > 900_000, cnt[0]
     pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-9, atol=1e-9)
+
+
+def _zipf_ranks(rng, n, s, key_range):
+    u = rng.random(n)
+    r = np.floor(np.maximum(u, 1e-300) ** (-1.0 / (s - 1.0)))
+    r = np.minimum(r, 2.0**62).astype(np.int64) % key_range
+    return (r * 0x9E3779B1) % key_range
+
+
+@pytest.mark.parametrize("how", ["inner", "left", "right", "outer"])
+@pytest.mark.parametrize("shape", ["hotbuild", "zipfprobe"])
+def test_radix_join_skewed_partitions_split(gpu_ctx, ctx, monkeypatch, how, shape):
+    """Skew is handled per partition (kernel_decls.inc RJSplit): hot build keys beyond the LDS
+    capacity are joined in build chunks, a hot probe partition in probe chunks; the rest of the join
+    stays on the per-partition path and nothing falls back to the global table.  Outer joins defer a
+    split side's unmatched rows to emission items.  Against the CPU twin at 2M x 2M."""
+    rng = np.random.default_rng(41)
+    n = 2_000_000
+    kr = int(0.99 * n)
+    lk = rng.integers(0, kr, n)
+    rk = rng.integers(0, kr, n)
+    if shape == "hotbuild":  # right = build side (equal sizes): 8 hot keys x 6k duplicates
+        pos = rng.choice(n, 8 * 6000, replace=False)
+        rk[pos] = np.repeat(np.arange(8) * (kr // 8) + 3, 6000)
+    else:  # probe (left) keys Zipf(1.1): the hottest key holds ~6.7 % of the rows
+        lk = _zipf_ranks(rng, n, 1.1, kr)
+    a = pa.table({"k": lk, "v": rng.random(n)})
+    b = pa.table({"k": rk, "w": rng.random(n), "i": pa.array(rng.integers(-5, 5, n), mask=rng.random(n) < 0.05)})
+    got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["k"], monkeypatch)
+    assert c.get("join.radix.split_partitions", 0) > 0, c
+    assert c.get("join.radix.overflow_fallback", 0) == 0, c
+    assert c["join.radix.rows_out"] == len(exp)
+    pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
+
+
+@pytest.mark.parametrize("how", ["inner", "left", "right", "outer"])
+def test_radix_join_forced_small_build_chunks(gpu_ctx, ctx, monkeypatch, how):
+    """CYLON_RJ_SPLIT_ROWS=64 splits every partition with more than 64 build rows into 64-row build
+    chunks: most partitions run as items, both outer sides deferred (many chunks per partition)."""
+    rng = np.random.default_rng(43)
+    nl, nr = 400_000, 300_000
+    a = pa.table({"k": rng.integers(0, 200_000, nl), "v": rng.random(nl)})
+    b = pa.table({"k": rng.integers(0, 200_000, nr), "w": rng.random(nr)})
+    monkeypatch.setenv("CYLON_RJ_SPLIT_ROWS", "64")
+    got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["k"], monkeypatch)
+    assert c.get("join.radix.split_items", 0) > 100, c
+    assert c["join.radix.rows_out"] == len(exp)
+    pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)

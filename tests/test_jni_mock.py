@@ -32,6 +32,8 @@ def _build(tmp_path):
 
 
 @pytest.mark.skipif(not os.path.exists(SO), reason="native core library not built")
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "java", "src", "main", "native", "cylon_jni.cpp")),
+                    reason="java sources not in this snapshot (.gpurunignore leaves ./java off the GPU box)")
 def test_jni_layer_through_mock_jnienv(ctx, tmp_path):
     exe = _build(tmp_path)
     a, b = os.path.join(DATA, "csv1_0.csv"), os.path.join(DATA, "csv2_0.csv")

@@ -216,3 +216,28 @@ def test_distributed_join_narrowed_wire(chunks):
     assert len(got) == len(ref) > 0
     assert _canon(got) == _canon(ref[got.columns])
     assert all(r[3] == 3 for r in res)  # l.k, l.z, r.k (l.w spans > 2^32)
+
+
+@pytest.mark.parametrize("how", JOIN_TYPES)
+def test_global_hash_join_hot_keys_directory(ctx, how):
+    """The global-table join's directory holds each distinct build key once (ops/join.cpp
+    hash_join_pairs): hot keys with thousands of duplicates on both sides, next to unique keys."""
+    from cylon_amd._lib import C
+    rng = np.random.default_rng(9)
+    n = 20_000
+    ka = rng.integers(0, 5_000, n)
+    kb = rng.integers(0, 5_000, n)
+    ka[rng.random(n) < 0.02] = 77  # ~400 x ~3000 rows of key 77
+    kb[rng.random(n) < 0.15] = 77
+    kb[rng.random(n) < 0.05] = -3  # only on the build side
+    a = pd.DataFrame({"k": ka, "v": rng.random(n)})
+    b = pd.DataFrame({"k": kb[: n // 2], "w": rng.random(n // 2)})
+    C.trace_enable(True)
+    C.trace_reset()
+    out = Table.from_pandas(ctx, a).join(Table.from_pandas(ctx, b), how, "hash", on=["k"], left_prefix="l_",
+                                         right_prefix="r_").to_pandas()
+    c = dict(C.trace_counters())
+    C.trace_enable(False)
+    ref = _oracle(a, b, how, ["k"], ["k"])
+    assert len(out) == len(ref)
+    assert _canon(out) == _canon(ref[out.columns])

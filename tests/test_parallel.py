@@ -185,11 +185,14 @@ def test_bench_contract_multirank_cpu_rehearsal():
               "vs_baseline", "dtype", "data", "config"):
         assert k in rec
     assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["config"]["output_rows"] > 0
+    # self-validating multi-rank record: verified by default, one entry per rank with its world size
+    assert rec["verify"]["ok"] and rec["verify"]["rows"] == rec["config"]["output_rows"]
+    assert [r["rank"] for r in rec["ranks"]] == [0, 1] and all(r["world_size_pg"] == 2 for r in rec["ranks"])
 
 
 def test_bench_self_launch_four_ranks_cpu():
     """bench.py --gpus 4 with no torchrun environment starts 4 ranks itself (child torchrun) and
-    reports n_gpus == 4, per-phase timings and a passing --verify; a WORLD_SIZE that disagrees
+    reports n_gpus == 4, per-phase timings and a passing verify of a FULL OUTER join; a WORLD_SIZE that disagrees
     with --gpus exits non-zero (reference launch: cpp/src/experiments/run_dist_scaling.py:115-154)."""
     import json
     import os
@@ -199,7 +202,7 @@ def test_bench_self_launch_four_ranks_cpu():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["CYLON_BENCH_BACKEND"] = "gloo"
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4", "--steps", "2",
-                          "--warmup", "1", "--rows", "80000", "--verify"],
+                          "--warmup", "1", "--rows", "80000", "--how", "outer"],
                          capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert out.returncode == 0 and len(lines) == 1, out.stderr[-2000:]
@@ -302,3 +305,47 @@ def test_eight_rank_distributed_rehearsal():
     for r in res:
         assert r[3].get("shuffle.self_rows_kept_local", 0) > 0, r[3]
         assert r[3].get("shuffle.plan_collectives", 0) == 3, r[3]
+
+
+def _idle_rank_ops(ctx, chunks):
+    """Rank 2 holds empty tables and no key of ranks 0 / 1 hashes to it: in every chunk its own
+    sends and receives are all zero while the other ranks exchange (the collective
+    must still be posted on every rank, or the busy ranks block)."""
+    from cylon_amd import CylonContext
+    from cylon_amd._lib import C
+    rank, world = ctx.get_rank(), ctx.get_world_size()
+    ctx.add_config("shuffle_chunks", str(chunks))
+    # keys whose planned-shuffle partition (hash % (world * chunks)) maps to rank 0 or 1
+    local = CylonContext()
+    cand = Table.from_pandas(local, pd.DataFrame({"k": np.arange(600, dtype=np.int64)}))
+    parts = cand.hash_partition(["k"], world * chunks)
+    keys = np.concatenate([t.to_pandas()["k"].to_numpy() for p, t in enumerate(parts) if p % world != 2])
+    rng = np.random.default_rng(rank)
+    n = 0 if rank == 2 else 300
+    a = pd.DataFrame({"k": rng.choice(keys, n).astype(np.int64), "v": rng.random(n)})
+    b = pd.DataFrame({"k": rng.choice(keys, n).astype(np.int64), "w": rng.random(n)})
+    C.trace_enable(True)
+    C.trace_reset()
+    ta, tb = Table.from_pandas(ctx, a), Table.from_pandas(ctx, b)
+    out = {"join": ta.distributed_join(tb, "inner", "hash", on=["k"], left_prefix="l_", right_prefix="r_"),
+           "union": ta[["k"]].distributed_union(tb[["k"]]),
+           "gb": ta.groupby("k", {"v": ["sum"]})}
+    counters = dict(C.trace_counters())
+    C.trace_enable(False)
+    return {k: v.to_pandas() for k, v in out.items()}, a, b, counters
+
+
+@pytest.mark.parametrize("chunks", [1, 2])
+def test_idle_rank_still_posts_collectives(chunks):
+    res = run_distributed(_idle_rank_ops, 3, chunks, timeout=120.0)
+    A = pd.concat([r[1] for r in res]).reset_index(drop=True)
+    B = pd.concat([r[2] for r in res]).reset_index(drop=True)
+    assert len(res[2][0]["join"]) == 0 and len(res[2][0]["union"]) == 0  # rank 2 stayed idle
+    exp = A.add_prefix("l_").merge(B.add_prefix("r_"), left_on="l_k", right_on="r_k")
+    got = pd.concat([r[0]["join"] for r in res])
+    assert _rows(got[sorted(got.columns)]) == _rows(exp[sorted(exp.columns)])
+    un = sorted(pd.concat([r[0]["union"] for r in res])["k"].tolist())
+    assert un == sorted(set(A["k"]) | set(B["k"]))
+    gb = pd.concat([r[0]["gb"] for r in res]).sort_values("k")
+    assert gb["k"].tolist() == sorted(set(A["k"]))
+    assert all(r[3].get("shuffle.plan_collectives", 0) >= 1 for r in res)

@@ -159,3 +159,21 @@ def test_integer_to_string_cast_matches_arrow(ctx, typ):
     arr = pa.array(v, getattr(pa, typ)(), mask=np.arange(len(v)) % 17 == 3)
     got = Table(pa.table({"x": arr}), ctx).astype({"x": pa.string()}).to_arrow().column(0)
     assert got.to_pylist() == pc.cast(arr, pa.string()).to_pylist()
+
+
+def test_knob_registry_matches_docs():
+    """docs/knobs.md lists exactly the knobs of the native registry (knobs.cpp), and no native source
+    reads a CYLON_* variable around the registry."""
+    import glob
+    import re
+    from cylon_amd._lib import C
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    reg = {f"CYLON_{name}" for name, _, _ in C.knob_registry()}
+    doc = open(os.path.join(root, "docs", "knobs.md")).read()
+    tables = doc[doc.index("## Runtime"):]  # the tables (the intro names deleted knobs)
+    assert set(re.findall(r"`(CYLON_[A-Z0-9_]+)`", tables)) == reg
+    srcs = glob.glob(os.path.join(root, "cylon_amd", "csrc", "**", "*.cpp"), recursive=True) + \
+        glob.glob(os.path.join(root, "cylon_amd", "csrc", "**", "*.hip"), recursive=True)
+    offenders = [p for p in srcs if 'getenv("CYLON_' in open(p).read() and not p.endswith("knobs.cpp")]
+    assert offenders == []
+    assert len(reg) <= 25

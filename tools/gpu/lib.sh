@@ -12,7 +12,7 @@ step() {
   # a GPU memory fault surfaces as a Python exception (rc 1): treat it like a crash
   if grep -qE "illegal memory access|MEMORY_APERTURE_VIOLATION|Memory access fault|HSA_STATUS_ERROR" "$O/$name.out" "$O/$name.err" 2>/dev/null; then
     echo "stopping after $name (GPU fault reported)" | tee -a "$O/steps.txt"
-    exit 3
+    exit 97
   fi
   if [ "$rc" -ge 124 ]; then
     echo "stopping after $name (rc=$rc)" | tee -a "$O/steps.txt"
