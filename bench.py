@@ -146,36 +146,40 @@ def max_over_ranks(ctx, d: dict) -> dict:
 
 
 def verify_join(ctx, left, right, out, key_range, how="inner") -> dict:
-    """Independent check of a join output by per-key identities (torch bincount over the global
-    key range, all-reduced over ranks; reference join/join_utils.cpp:126-181 for the outer rows):
-      rows          = sum_k cL(k) cR(k)  [+ sum_k cL(k) [cR(k) = 0] (left, outer)]
-                                         [+ sum_k cR(k) [cL(k) = 0] (right, outer)]
-      null l / r    = the unmatched right / left rows above, and their payload bytes are zero
-      sum l_k       = sum over rows with a left side of their key  (l_k == r_k where both exist)
-      sum l_v0      = sum_k SL(k) max(cR(k), [left kept])      SL = per-key sum of left v0
-      sum r_v0      = sum_k SR(k) max(cL(k), [right kept])"""
+    """Independent check of a join output by per-key identities (global key counts cL / cR by torch
+    bincount, all-reduced over ranks; per-row gathers of them, no weighted histogram -- a float64
+    atomic histogram serialises on a hot key; reference join/join_utils.cpp:126-181 for outer rows):
+      rows        = sum_k cL(k) cR(k)  [+ sum_k cL(k) [cR(k) = 0] (left, outer)]
+                                       [+ sum_k cR(k) [cL(k) = 0] (right, outer)]
+      null l / r  = the unmatched right / left rows above, and their payload bytes are zero
+      sum l_k     = sum over left rows i of k_i * (cR(k_i) [+ [cR(k_i) = 0]])  (l_k == r_k where both exist)
+      sum l_v0    = sum over left rows i of v_i * (cR(k_i) [+ [cR(k_i) = 0]])
+      sum r_v0    = sum over right rows j of w_j * (cL(k_j) [+ [cL(k_j) = 0]])"""
     lt, rt = left.to_torch(), right.to_torch()
     ocols = {c.name: c for c in out.native.columns()}
     dev = lt["k"].device
     f64 = torch.float64
-    cL = torch.bincount(lt["k"], minlength=key_range).to(f64)
-    cR = torch.bincount(rt["k"], minlength=key_range).to(f64)
-    SL = torch.bincount(lt["k"], weights=lt["v0"], minlength=key_range)
-    SR = torch.bincount(rt["k"], weights=rt["v0"], minlength=key_range)
-    for t in (cL, cR, SL, SR):
-        if ctx.get_world_size() > 1:
-            t.copy_(ctx.allreduce(t, "sum"))
+    cL = torch.bincount(lt["k"], minlength=key_range)
+    cR = torch.bincount(rt["k"], minlength=key_range)
+    if ctx.get_world_size() > 1:
+        cL.copy_(ctx.allreduce(cL, "sum"))
+        cR.copy_(ctx.allreduce(cR, "sum"))
     keep_l = how in ("left", "outer")
     keep_r = how in ("right", "outer")
-    keys = torch.arange(key_range, device=dev, dtype=f64)
-    zl, zr = (cR == 0).to(f64), (cL == 0).to(f64)
-    inner = (cL * cR).sum()
-    un_l = (cL * zl).sum() if keep_l else torch.zeros((), dtype=f64, device=dev)
-    un_r = (cR * zr).sum() if keep_r else torch.zeros((), dtype=f64, device=dev)
-    lk_rows = cL * (cR + zl) if keep_l else cL * cR  # output rows holding a left key, per key
-    expect = torch.stack([inner + un_l + un_r, un_r, un_l, (keys * lk_rows).sum(),
-                          (SL * (cR + zl) if keep_l else SL * cR).sum(), (SR * (cL + zr) if keep_r else SR * cL).sum()])
-    del cL, cR, SL, SR, keys, zl, zr, lk_rows
+    inner = (cL.to(f64) * cR.to(f64)).sum()
+    un_l = (cL * (cR == 0)).sum().to(f64) if keep_l else torch.zeros((), dtype=f64, device=dev)
+    un_r = (cR * (cL == 0)).sum().to(f64) if keep_r else torch.zeros((), dtype=f64, device=dev)
+
+    def mult(c_other, keys, keep):  # output rows of each input row
+        m = c_other.index_select(0, keys)
+        return (m + (m == 0)).to(f64) if keep else m.to(f64)
+    ml = mult(cR, lt["k"], keep_l)
+    mr = mult(cL, rt["k"], keep_r)
+    part = torch.stack([(lt["k"].to(f64) * ml).sum(), (lt["v0"] * ml).sum(), (rt["v0"] * mr).sum()])
+    del ml, mr, cL, cR
+    if ctx.get_world_size() > 1:
+        part = ctx.allreduce(part, "sum")
+    expect = torch.cat([torch.stack([inner + un_l + un_r, un_r, un_l]), part])
 
     def col(name):
         c = ocols[name]

@@ -23,98 +23,10 @@
 //      owns a contiguous slice of the probe rows (wave-level scans only).
 // Partitions whose build side exceeds the LDS capacity are reported; the
 // caller then falls back to the global-table join.
-#include "cylon/knobs.hpp"
-#include <atomic>
-#include <climits>
-#include <cstdio>
-#include <cstdlib>
-#include <string>
-#include <type_traits>
-#include <vector>
-
-#include "stable_rank.hpp"
+#include "radix_common.hpp"
 
 namespace cylon {
 namespace hip {
-
-constexpr int kRPThreads = 1024;                 // partition pass block (16 waves)
-constexpr int kRPWaves = kRPThreads / kWave;
-constexpr int kRPItems = 8;                      // rows per thread per tile
-constexpr int kRPTile = kRPThreads * kRPItems;   // 8192 rows
-constexpr int kRPMaxBuckets = 1024;
-constexpr int kRJMaxDigitBits = 10;
-constexpr int kRJRowArea = 154496;               // LDS bytes for the staged build rows (1 block per CU; 1 KB left for the emit owner map)
-constexpr int kRJMaxRows = 5120;                 // build rows per partition (5 per thread)
-constexpr int kRJThreads = 1024;
-constexpr int kRankBallot = 0, kRankBlockAtomic = 1, kRankWaveAtomic = 2;
-constexpr int kRJWaves = kRJThreads / kWave;
-
-struct ColSet {
-  const uint8_t *in[kMaxFusedCols];
-  uint8_t *out[kMaxFusedCols];
-  int width[kMaxFusedCols];
-  int n;
-  uint64_t key_xor;  // XORed into column 0 as it is stored (a sort's last pass rebuilds int64 keys from images)
-  // Ranking guard (passes that must be stable): inside every bucket run of the sorted tile the
-  // input rows must ascend; a violation -- the wave-atomic ranking relies on gfx950 returning one
-  // instruction's same-address LDS atomics in lane order -- sets *order_bad.
-  int check_order;
-  int *order_bad;
-  // Next-digit side output (LSD sort): as column 0 is stored at row r, nd_out[r] = (stored >>
-  // nd_shift) & nd_mask -- the NEXT pass's digit, so that pass's per-tile histogram reads 2 bytes
-  // per row instead of the 8-byte key (nullptr: off)
-  uint16_t *nd_out;
-  int nd_shift;
-  uint32_t nd_mask;
-  uint64_t nd_sub;  // the sort's ImageDigit::sub
-};
-
-// Digit read from a next-digit array written by the previous pass (histogram kernels only)
-struct NdDigit {
-  const uint16_t *d;
-  __device__ __forceinline__ uint32_t operator()(int64_t i) const { return d[i]; }
-};
-
-__device__ __forceinline__ uint32_t part_of(int64_t key, int bits) {
-  return bits == 0 ? 0u : (uint32_t)(hashing::fmix64((uint64_t)key) >> (64 - bits));
-}
-
-__device__ __forceinline__ long long rj_shfl_xor64(long long x, int mask) {
-  const uint32_t lo = __shfl_xor((uint32_t)(uint64_t)x, mask, kWave);
-  const uint32_t hi = __shfl_xor((uint32_t)((uint64_t)x >> 32), mask, kWave);
-  return (long long)(((uint64_t)hi << 32) | lo);
-}
-
-__device__ __forceinline__ uint64_t ld_elem(const uint8_t *src, int64_t i, int w) {
-  switch (w) {
-    case 1: return src[i];
-    case 2: return reinterpret_cast<const uint16_t *>(src)[i];
-    case 4: return reinterpret_cast<const uint32_t *>(src)[i];
-    default: return reinterpret_cast<const uint64_t *>(src)[i];
-  }
-}
-
-__device__ __forceinline__ void st_elem(uint8_t *dst, int64_t i, int w, uint64_t v) {
-  switch (w) {
-    case 1: dst[i] = (uint8_t)v; break;
-    case 2: reinterpret_cast<uint16_t *>(dst)[i] = (uint16_t)v; break;
-    case 4: reinterpret_cast<uint32_t *>(dst)[i] = (uint32_t)v; break;
-    default: reinterpret_cast<uint64_t *>(dst)[i] = v;
-  }
-}
-
-// Column loops below are unrolled to compile-time bounds with `q < n` guards, so
-// every ColSet field is a statically indexed kernel argument (SGPRs, loaded
-// once); a runtime-indexed field would be re-fetched with a dependent scalar
-// load per element.  W8 = every column 8 bytes wide (no width dispatch).
-template <bool W8>
-__device__ __forceinline__ uint64_t ldw(const uint8_t *p, int64_t i, int w) {
-  return W8 ? reinterpret_cast<const uint64_t *>(p)[i] : ld_elem(p, i, w);
-}
-template <bool W8>
-__device__ __forceinline__ void stw(uint8_t *p, int64_t i, int w, uint64_t v) {
-  if (W8) reinterpret_cast<uint64_t *>(p)[i] = v; else st_elem(p, i, w, v);
-}
 
 // --------------------------------------------------------------------------
 // partition pass
@@ -125,6 +37,7 @@ struct PartDigit {
   int bits;   // total partition bits
   int shift;  // digit = (part >> shift) & mask
   uint32_t mask;
+  CYLON_DIGIT_COMMON
   __device__ __forceinline__ uint32_t of_key(int64_t k) const { return (part_of(k, bits) >> shift) & mask; }
   __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key(keys[i]); }
   // look-back counting: the next pass's digit of a stored key
@@ -134,6 +47,37 @@ struct PartDigit {
 };
 
 
+// Narrowed join digit (join partitions of int64 keys): every key of a join lies in [base, base + 2^32)
+// with base = (left key 0) - 2^31 (checked on the fly; a key outside sets *bad and the join
+// repartitions without narrowing), so column 0 travels as the uint32 offset key - base -- 4 B/row
+// less in every pass write, in the second pass's reads and in the join kernel's reads -- and the
+// partition is the top bits of fmix32(offset) (a bijection: equal offsets <=> equal keys).
+struct PartDigitN {
+  static constexpr bool kNarrow = true;
+  const void *keys;          // int64 keys (first pass) or uint32 offsets (later passes)
+  int kin4;                  // keys holds uint32 offsets
+  const int64_t *base_src;   // base = base_src[0] - 2^31, read by init()
+  unsigned int *bad;         // set when a key lies outside [base, base + 2^32)
+  int bits;                  // total partition bits
+  int shift;                 // digit = (part >> shift) & mask
+  uint32_t mask;
+  int64_t base;
+  __device__ __forceinline__ void init() { base = (int64_t)((uint64_t)base_src[0] - (uint64_t(1) << 31)); }
+  __device__ __forceinline__ uint64_t key_at(int64_t i) const {
+    return kin4 ? (uint64_t)reinterpret_cast<const uint32_t *>(keys)[i]
+                : (uint64_t)reinterpret_cast<const int64_t *>(keys)[i];
+  }
+  __device__ __forceinline__ uint64_t narrow(uint64_t kv) const {
+    return kin4 ? (kv & 0xffffffffull) : ((kv - (uint64_t)base) & 0xffffffffull);
+  }
+  __device__ __forceinline__ bool too_wide(uint64_t kv) const { return !kin4 && (kv - (uint64_t)base) > 0xffffffffull; }
+  __device__ __forceinline__ void report_bad() const { atomicOr(bad, 1u); }
+  __device__ __forceinline__ uint32_t of_key(int64_t k) const {
+    return bits == 0 ? 0u : ((hashing::fmix32((uint32_t)narrow((uint64_t)k)) >> (32 - bits)) >> shift) & mask;
+  }
+  __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key((int64_t)key_at(i)); }
+};
+
 // Shuffle digit: the reference's partition of a single 8-byte integer key
 // (ModuloPartitionKernel: h = (uint32)key, pid = h % P, or h & (P-1) for powers
 // of two; partition.hip partition_f + hashing::partitioner), so one LDS-staged
@@ -141,6 +85,7 @@ struct PartDigit {
 struct ModDigit {
   const int64_t *keys;
   uint32_t nparts;
+  CYLON_DIGIT_COMMON
   __device__ __forceinline__ uint32_t of_key(int64_t k) const {
     return hashing::partitioner((uint32_t)(uint64_t)k, nparts);
   }
@@ -156,6 +101,7 @@ struct ImageDigit {
   uint32_t mask;
   uint64_t flip;  // image = key ^ flip (0 once column 0 holds images)
   uint64_t sub;
+  CYLON_DIGIT_COMMON
   __device__ __forceinline__ uint32_t of_key(int64_t k) const {
     return (uint32_t)((((uint64_t)k ^ flip) - sub) >> shift) & mask;
   }
@@ -174,6 +120,7 @@ struct RangeDigit {
   uint64_t flip, mn;
   int rshift, shift;
   uint32_t mask;
+  CYLON_DIGIT_COMMON
   __device__ __forceinline__ uint32_t of_key(int64_t k) const {
     return (uint32_t)((((uint64_t)k ^ flip) - mn) >> (rshift + shift)) & mask;
   }
@@ -181,9 +128,11 @@ struct RangeDigit {
 };
 
 template <class Digit>
-__global__ __launch_bounds__(kRPThreads) void k_rp_hist(Digit digit, int64_t n, uint32_t nbuckets,
+__global__ __launch_bounds__(kRPThreads) void k_rp_hist(Digit digit0, int64_t n, uint32_t nbuckets,
                                                         int64_t rows_per_block, int64_t nblocks,
                                                         int64_t *__restrict__ bh) {
+  Digit digit = digit0;
+  digit.init();
   __shared__ unsigned int hist[kRPMaxBuckets];
   for (uint32_t p = threadIdx.x; p < nbuckets; p += blockDim.x) hist[p] = 0;
   __syncthreads();
@@ -272,12 +221,6 @@ constexpr int kLbSpinLimit = 1 << 20, kLbWindow = 4;
 // are adjacent in the output and are written within a few us of each other into the same L2.
 // Offsets are exact per tile (k_rp_hist_tiles + k_ts_*), so which CU takes a tile changes only
 // speed; a block whose own chunk is exhausted takes tiles from the other chunks.
-constexpr int kXcds = 8;
-__device__ __forceinline__ int xcc_id() {
-  int x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-  return x & (kXcds - 1);
-}
 // slot mode: input bucket of tile t (tp: LDS copy of sl_tpre; the last bucket whose first tile <= t)
 __device__ __forceinline__ int sl_segment(const uint32_t *tp, int nb1, int64_t t) {
   int lo = 0, hi = nb1 - 1;
@@ -330,40 +273,7 @@ __device__ __forceinline__ void lb_flush(uint32_t *lc, uint32_t *g, uint32_t lwo
   __syncthreads();
 }
 
-// LDS-DMA of `bytes` (a multiple of 4) contiguous global bytes into LDS at dst (16-byte aligned)
-// by the block's WAVES waves: 1 KB pieces with global_load_lds_dwordx4 (a wave-instruction lands
-// at its uniform base + lane * 16; the source may be only 8-byte aligned), the last < 16 bytes as
-// dwords.  No VGPRs hold the data.
-template <int WAVES>
-__device__ __forceinline__ void rj_dma_block(const uint8_t *src, int bytes, uint8_t *dst, int wave, int lane) {
-  const int nq = bytes >> 4;
-  for (int c0 = wave * kWave; c0 < nq; c0 += WAVES * kWave)
-    if (c0 + lane < nq)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + (int64_t)(c0 + lane) * 16),
-                                       (__attribute__((address_space(3))) void *)(dst + c0 * 16), 16, 0, 0);
-  const int t0 = nq << 2, nd = bytes >> 2;  // tail dwords (at most 3)
-  if (wave == WAVES - 1 && t0 + lane < nd)
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + (int64_t)(t0 + lane) * 4),
-                                     (__attribute__((address_space(3))) void *)(dst + t0 * 4), 4, 0, 0);
-}
 
-// block-wide exclusive scan of one uint32 per thread (WAVES waves)
-template <int WAVES = kRPWaves>
-__device__ __forceinline__ uint32_t rp_block_exscan(uint32_t c, uint32_t *wsum) {
-  const int lane = lane_id(), wave = threadIdx.x / kWave;
-  uint32_t inc = c;
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const uint32_t t = __shfl_up(inc, d, kWave);
-    if (lane >= d) inc += t;
-  }
-  if (lane == kWave - 1) wsum[wave] = inc;
-  __syncthreads();
-  uint32_t off = 0;
-#pragma unroll
-  for (int w = 0; w < WAVES; ++w) off += (w < wave) ? wsum[w] : 0u;
-  return off + inc - c;
-}
 
 // ---- XCD-tile mode (XT) offsets: per-tile bucket counts, then exact output rows per (tile, bucket)
 // th[t][p]: rows of bucket p in kRPTile-row tile t (uint16: a tile has <= 8192 rows).  512-thread
@@ -381,8 +291,10 @@ __device__ __forceinline__ void ht_load(const Digit &digit, int64_t n, int64_t t
   }
 }
 template <class Digit>
-__global__ __launch_bounds__(kHTThreads) void k_rp_hist_tiles(Digit digit, int64_t n, uint32_t nb, int64_t ntiles,
+__global__ __launch_bounds__(kHTThreads) void k_rp_hist_tiles(Digit digit0, int64_t n, uint32_t nb, int64_t ntiles,
                                                               uint16_t *__restrict__ th) {
+  Digit digit = digit0;
+  digit.init();
   __shared__ unsigned int hist[kRPMaxBuckets];
   uint32_t d[kHTItems];
   ht_load(digit, n, blockIdx.x, ntiles, d);
@@ -477,11 +389,14 @@ __global__ void k_ts_offsets(const uint16_t *__restrict__ th, const uint32_t *__
 // SLOT: slot mode (TileSched): tiles of one input bucket each, per-(tile, digit) slot claims.
 template <class Digit, bool W8, int THREADS, int RANK, bool XT = false, bool SLOT = false>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_rows_pass(
-    Digit digit, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
+    Digit digit0, int nbits, uint32_t nbuckets, ColSet cols, int64_t n, int64_t rows_per_block, int64_t nblocks,
     const int64_t *__restrict__ bh_scan, TileSched lb) {
   constexpr int WAVES = THREADS / kWave;
   constexpr int TILE = THREADS * kRPItems;
   constexpr int BPT = (kRPMaxBuckets + THREADS - 1) / THREADS;  // buckets per thread in the offset scan
+  Digit digit = digit0;
+  digit.init();
+  bool narrow_bad = false;  // PartDigitN: a key outside the uint32 offset range
   static_assert(WAVES * kRPMaxBuckets * 2 + TILE * 4 <= TILE * 8, "ranking scratch must fit the stage");
   constexpr bool TICKET = XT || SLOT;  // tiles claimed one by one (not a contiguous chunk per block)
   static_assert(!(XT && SLOT), "one tile schedule");
@@ -572,7 +487,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
   for (int k = 0; k < kRPItems; ++k) {
     const int64_t i = begin + wrow + k * kWave + lane;
-    if (i < (SLOT ? s_tend[0] : end)) kv[k] = (uint64_t)digit.keys[i];
+    if (i < (SLOT ? s_tend[0] : end)) kv[k] = digit.key_at(i);
   }
   for (int64_t tile = begin, next = 0; tile < end; tile = next) {
     next = tile + TILE;
@@ -581,8 +496,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     const uint32_t xoff = XT && threadIdx.x < nbuckets ? lb.xt_off[(tile / TILE) * nbuckets + threadIdx.x] : 0u;
     uint32_t pl[kRPItems];  // digit, then (in-wave rank << 16) | digit, then sorted slot; ~0 = inactive
 #pragma unroll
-    for (int k = 0; k < kRPItems; ++k)
-      pl[k] = (wrow + k * kWave + lane < cnt) ? digit.of_key((int64_t)kv[k]) : 0xffffffffu;
+    for (int k = 0; k < kRPItems; ++k) {
+      const bool act = wrow + k * kWave + lane < cnt;
+      pl[k] = act ? digit.of_key((int64_t)kv[k]) : 0xffffffffu;
+      if (Digit::kNarrow) narrow_bad |= act && digit.too_wide(kv[k]);
+    }
     if (STABLE) {
       for (uint32_t q = threadIdx.x; q < WAVES * nbuckets; q += blockDim.x) wcnt[q] = 0;
     } else {
@@ -714,9 +632,16 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       if (TICKET && c + 1 == cols.n && threadIdx.x == 0) {
         if (!SLOT) s_next = xt_claim(lb, xhome, TILE, n);
       }
+      const bool n4 = Digit::kNarrow && c == 0;  // column 0 as the uint32 offset
+      if (n4) {
 #pragma unroll
-      for (int k = 0; k < kRPItems; ++k)
-        if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
+        for (int k = 0; k < kRPItems; ++k)
+          if (pl[k] != 0xffffffffu) stw<false>(st, pl[k], 4, digit.narrow(v[k]));
+      } else {
+#pragma unroll
+        for (int k = 0; k < kRPItems; ++k)
+          if (pl[k] != 0xffffffffu) stw<W8>(st, pl[k], w, v[k] ^ x);
+      }
       __syncthreads();
       if (TICKET && c + 1 == cols.n) next = SLOT ? s_tr0[par ^ 1] : s_next;
       if (c + 1 < cols.n) {  // prefetch column c+1 of this tile
@@ -734,7 +659,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
         for (int k = 0; k < kRPItems; ++k) {
           const int64_t i = next + wrow + k * kWave + lane;
-          if (i < (SLOT ? s_tend[par ^ 1] : end)) kv[k] = (uint64_t)digit.keys[i];
+          if (i < (SLOT ? s_tend[par ^ 1] : end)) kv[k] = digit.key_at(i);
         }
       }
       if (std::is_same<Digit, ImageDigit>::value && c == 0 && cols.nd_out != nullptr) {  // sorts only
@@ -747,6 +672,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             stw<W8>(out, o, w, kv0);
             cols.nd_out[o] = (uint16_t)(((kv0 - cols.nd_sub) >> cols.nd_shift) & cols.nd_mask);
           }
+        }
+      } else if (n4) {
+#pragma unroll
+        for (int q = 0; q < kRPItems; ++q) {
+          const int j = threadIdx.x + q * THREADS;
+          if (j < cnt) stw<false>(out, RP_DEST(q), 4, ldw<false>(st, j, 4));
         }
       } else {
 #pragma unroll
@@ -768,6 +699,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
   }
   if (order_bad) atomicOr(cols.order_bad, 1);
+  if (Digit::kNarrow && narrow_bad) digit.report_bad();
 }
 
 // Register-lean pass: the same tile algorithm (8192-row tiles, LDS-atomic ranking, one
@@ -1400,7 +1332,17 @@ static void lb_plan_next(const SortLbArgs *lba, int64_t nblk, uint32_t nbn, int6
 // stable = false (join partitions only) ranks rows with LDS atomics: rows of one
 // bucket keep no particular order inside a tile's run.  Instantiated for PartDigit
 // only; every other digit (sort, shuffle, range join) needs the stable order.
-template <class Digit, bool CAN_UNSTABLE = std::is_same<Digit, PartDigit>::value>
+// column 0 of a pass input: the int64 key, or (narrowed join passes after the first) uint32 offsets
+template <class Digit>
+static bool key_column_ok(const Digit &dg, const uint8_t *const *in, const int *widths) {
+  if constexpr (Digit::kNarrow)
+    return in[0] == reinterpret_cast<const uint8_t *>(dg.keys) && widths[0] == (dg.kin4 ? 4 : 8);
+  else
+    return in[0] == reinterpret_cast<const uint8_t *>(dg.keys) && widths[0] == 8;
+}
+
+template <class Digit,
+          bool CAN_UNSTABLE = std::is_same<Digit, PartDigit>::value || std::is_same<Digit, PartDigitN>::value>
 static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const uint8_t *const *in, uint8_t *const *out,
                              const int *widths, int ncols, int64_t *ws, void *stream, uint64_t key_xor = 0,
                              bool stable = true, bool tiles_prescanned = false,
@@ -1410,8 +1352,7 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   if (n == 0) return;
   CYLON_CHECK(digit_bits >= 1 && digit_bits <= kRJMaxDigitBits, Code::Invalid, "digit bits " << digit_bits);
   CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "bad column count " << ncols);
-  CYLON_CHECK(in[0] == reinterpret_cast<const uint8_t *>(dg.keys) && widths[0] == 8, Code::Invalid,
-              "radix pass: column 0 must be the key");
+  CYLON_CHECK(key_column_ok(dg, in, widths), Code::Invalid, "radix pass: column 0 must be the key");
   // key_xor rebuilds int64 keys from order images: only a sort's image digit may set it
   // (partition / mod / range digits store column 0 as read)
   CYLON_CHECK((key_xor == 0 || std::is_same<Digit, ImageDigit>::value), Code::Invalid,
@@ -1426,7 +1367,7 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
   const bool unstable = CAN_UNSTABLE && !stable;
   const bool wave_atomic = !unstable && rp_wave_atomic(s);
   const int threads = rp_threads(ncols, unstable || wave_atomic);
-  const bool lean = rp_lean(ncols) && (unstable || wave_atomic) && threads == 1024;
+  const bool lean = !Digit::kNarrow && rp_lean(ncols) && (unstable || wave_atomic) && threads == 1024;
   RPGeometry g;
   const int64_t *bh_scan = nullptr;
   TileSched lb{};
@@ -1508,9 +1449,9 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
     cs.out[c] = c < ncols ? out[c] : nullptr;
     cs.width[c] = c < ncols ? widths[c] : 8;
   }
-  bool w8 = true;
+  bool w8 = true;  // (a narrowed column 0 is stored as 4 bytes by its own path)
   for (int c = 0; c < ncols; ++c) {
-    w8 &= widths[c] == 8;
+    w8 &= widths[c] == 8 || (Digit::kNarrow && c == 0);
     CYLON_CHECK(in[c] != nullptr || (c > 0 && widths[c] == 8), Code::Invalid,
                 "radix pass: a generated row-id column must be an 8-byte payload column");
   }
@@ -1523,10 +1464,12 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
     lb.lb_xshift = digit_bits - 3;
   }
   if (lean) {
-    constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankWaveAtomic;
-    const int lbm = (lbin ? 2 : 0) | (lbcnt ? 1 : 0);
-    if (unstable) lean_kernel<Digit, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
-    else lean_kernel<Digit, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt, lbm);
+    if constexpr (!Digit::kNarrow) {
+      constexpr int R = CAN_UNSTABLE ? kRankBlockAtomic : kRankWaveAtomic;
+      const int lbm = (lbin ? 2 : 0) | (lbcnt ? 1 : 0);
+      if (unstable) lean_kernel<Digit, R>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt);
+      else lean_kernel<Digit, kRankWaveAtomic>(w8, g, s, dg, digit_bits, nb, cs, n, bh_scan, lb, xt, lbm);
+    }
     HIP_LAUNCH_CHECK();
     if (lbin) {  // local chunks: XCD x had blocks
       hipLaunchKernelGGL(k_lb_check, dim3(1), dim3(kWave), 0, s, lba->plan_in, lba->err);
@@ -1551,8 +1494,14 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
 
 void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, int digit_bits, const uint8_t *const *in,
                      uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream, bool stable,
-                     const SortLbArgs *lb, int nd_bits) {
+                     const SortLbArgs *lb, int nd_bits, const NarrowKeys *nk) {
   const uint32_t nb = 1u << digit_bits;
+  if (nk && nk->base_src) {  // narrowed join partition pass (no look-back counting)
+    CYLON_CHECK(!(lb && (lb->plan_in || lb->plan_out)), Code::Invalid, "narrowed pass: no look-back");
+    rows_pass_launch(PartDigitN{keys, nk->kin4, nk->base_src, nk->bad, total_bits, shift, nb - 1, 0}, n, digit_bits, in,
+                     out, widths, ncols, ws, stream, 0, stable);
+    return;
+  }
   CYLON_CHECK(!(lb && lb->plan_out) || (nd_bits >= 1 && nd_bits <= 9 && stable), Code::Invalid,
               "look-back counting partition pass: next digit of " << nd_bits << " bits");
   rows_pass_launch(PartDigit{keys, total_bits, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws, stream, 0,
@@ -1688,14 +1637,14 @@ int64_t radix_slot_workspace(int first_bits, int second_bits) {  // int64 words:
   return (u32 + 1) / 2;
 }
 
-static void slot_pass(const PartDigit &dg, int64_t n, int digit_bits, const uint8_t *const *in, uint8_t *const *out,
+template <class Digit>
+static void slot_pass(const Digit &dg, int64_t n, int digit_bits, const uint8_t *const *in, uint8_t *const *out,
                       const int *widths, int ncols, int src, int S, const uint32_t *bbase, const int64_t *pcnt,
                       int64_t pslot, int gshift, int gmask, int B, int64_t nslots, int64_t slot, int64_t *ws,
                       int64_t *counts, unsigned int *overflow, hipStream_t s) {
   CYLON_CHECK(S >= 1 && S <= kSlotMaxSeg && ncols >= 1 && ncols <= kMaxFusedCols && slot > 0, Code::Invalid,
               "slot pass arguments");
-  CYLON_CHECK(in[0] == reinterpret_cast<const uint8_t *>(dg.keys) && widths[0] == 8, Code::Invalid,
-              "slot pass: column 0 must be the key");
+  CYLON_CHECK(key_column_ok(dg, in, widths), Code::Invalid, "slot pass: column 0 must be the key");
   CYLON_CHECK(nslots * slot + kRPTile < (int64_t(1) << 32), Code::Invalid, "slot pass: output rows beyond 2^32");
   const uint32_t nb = 1u << digit_bits;
   uint32_t *w32 = reinterpret_cast<uint32_t *>(ws);
@@ -1737,17 +1686,17 @@ static void slot_pass(const PartDigit &dg, int64_t n, int digit_bits, const uint
     cs.out[c] = c < ncols ? out[c] : nullptr;
     cs.width[c] = c < ncols ? widths[c] : 8;
     if (c < ncols) {
-      w8 &= widths[c] == 8;
+      w8 &= widths[c] == 8 || (Digit::kNarrow && c == 0);
       CYLON_CHECK(in[c] != nullptr, Code::Invalid, "slot pass: every column is read");
     }
   }
   // every XCD needs at least one block: its segments' tiles are dealt to its own blocks only
   const int64_t nblocks = std::max<int64_t>(kXcds, std::min<int64_t>((n + kRPTile - 1) / kRPTile + S, kNumCUs));
   if (w8)
-    hipLaunchKernelGGL((k_rows_pass<PartDigit, true, 1024, kRankBlockAtomic, false, true>), dim3((unsigned)nblocks),
+    hipLaunchKernelGGL((k_rows_pass<Digit, true, 1024, kRankBlockAtomic, false, true>), dim3((unsigned)nblocks),
                        dim3(1024), 0, s, dg, digit_bits, nb, cs, n, (int64_t)kRPTile, nblocks, nullptr, lb);
   else
-    hipLaunchKernelGGL((k_rows_pass<PartDigit, false, 1024, kRankBlockAtomic, false, true>), dim3((unsigned)nblocks),
+    hipLaunchKernelGGL((k_rows_pass<Digit, false, 1024, kRankBlockAtomic, false, true>), dim3((unsigned)nblocks),
                        dim3(1024), 0, s, dg, digit_bits, nb, cs, n, (int64_t)kRPTile, nblocks, nullptr, lb);
   HIP_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_sl_counts, dim3(grid_for(nslots)), dim3(kBlock), 0, s, cursor, nslots, slot, counts);
@@ -1756,25 +1705,50 @@ static void slot_pass(const PartDigit &dg, int64_t n, int digit_bits, const uint
 
 void radix_slot_first_pass(const int64_t *keys, int64_t n, int total_bits, int first_bits, int second_bits,
                            const uint8_t *const *in, uint8_t *const *out, const int *widths, int ncols, int64_t slot,
-                           int64_t *ws, int64_t *counts, unsigned int *overflow, void *stream) {
+                           int64_t *ws, int64_t *counts, unsigned int *overflow, void *stream, const NarrowKeys *nk) {
   CYLON_CHECK(radix_slot_eligible(n, ncols, first_bits, second_bits) && radix_slot_first_pass_ok(first_bits),
               Code::Invalid, "slot first pass not eligible");
   const int nb1 = 1 << first_bits;
   // the high digit; slot x * 2^first_bits + d holds bucket d's rows from XCD x's chunk of the table
   // (XCD-major: the cursors one XCD claims from share cache lines only with each other -- the
   // bucket-major order d * 8 + x put 8 XCDs' atomics on every line)
-  slot_pass(PartDigit{keys, total_bits, second_bits, (uint32_t)nb1 - 1}, n, first_bits, in, out, widths, ncols, 0,
-            kXcds, nullptr, nullptr, 0, 0, 0, 1, int64_t(kXcds) * nb1, slot, ws, counts, overflow, as_stream(stream));
+  if (nk && nk->base_src)
+    slot_pass(PartDigitN{keys, nk->kin4, nk->base_src, nk->bad, total_bits, second_bits, (uint32_t)nb1 - 1, 0}, n,
+              first_bits, in, out, widths, ncols, 0, kXcds, nullptr, nullptr, 0, 0, 0, 1, int64_t(kXcds) * nb1, slot, ws,
+              counts, overflow, as_stream(stream));
+  else
+    slot_pass(PartDigit{keys, total_bits, second_bits, (uint32_t)nb1 - 1}, n, first_bits, in, out, widths, ncols, 0,
+              kXcds, nullptr, nullptr, 0, 0, 0, 1, int64_t(kXcds) * nb1, slot, ws, counts, overflow, as_stream(stream));
 }
+
+template <class Digit>
+static void slot_rows_pass(const Digit &dg, int64_t n, int first_bits, int second_bits, const uint8_t *const *in,
+                           uint8_t *const *out, const int *widths, int ncols, const int64_t *first_ws,
+                           const int64_t *first_counts, int64_t first_slot, int64_t slot, int64_t *ws, int64_t *counts,
+                           unsigned int *overflow, void *stream);
 
 void radix_slot_rows_pass(const int64_t *keys, int64_t n, int total_bits, int first_bits, int second_bits,
                           const uint8_t *const *in, uint8_t *const *out, const int *widths, int ncols,
                           const int64_t *first_ws, const int64_t *first_counts, int64_t first_slot, int64_t slot,
-                          int64_t *ws, int64_t *counts, unsigned int *overflow, void *stream) {
+                          int64_t *ws, int64_t *counts, unsigned int *overflow, void *stream, const NarrowKeys *nk) {
+  if (nk && nk->base_src) {
+    slot_rows_pass(PartDigitN{keys, nk->kin4, nk->base_src, nk->bad, total_bits, 0, (1u << second_bits) - 1, 0}, n,
+                   first_bits, second_bits, in, out, widths, ncols, first_ws, first_counts, first_slot, slot, ws, counts,
+                   overflow, stream);
+  } else {
+    slot_rows_pass(PartDigit{keys, total_bits, 0, (1u << second_bits) - 1}, n, first_bits, second_bits, in, out,
+                   widths, ncols, first_ws, first_counts, first_slot, slot, ws, counts, overflow, stream);
+  }
+}
+
+template <class Digit>
+static void slot_rows_pass(const Digit &dg, int64_t n, int first_bits, int second_bits, const uint8_t *const *in,
+                           uint8_t *const *out, const int *widths, int ncols, const int64_t *first_ws,
+                           const int64_t *first_counts, int64_t first_slot, int64_t slot, int64_t *ws, int64_t *counts,
+                           unsigned int *overflow, void *stream) {
   CYLON_CHECK(radix_slot_eligible(n, ncols, first_bits, second_bits), Code::Invalid, "slot pass not eligible");
   const int nb1 = 1 << first_bits;
   const int64_t nslots = int64_t(nb1) << second_bits;
-  const PartDigit dg{keys, total_bits, 0, (1u << second_bits) - 1};
   if (first_counts != nullptr) {  // after a slot first pass: segment g = (bucket g >> 3, XCD g & 7)
     slot_pass(dg, n, second_bits, in, out, widths, ncols, 2, kXcds * nb1, nullptr, first_counts, first_slot, 3, 0, 1,
               nslots, slot, ws, counts, overflow, as_stream(stream));
@@ -1958,6 +1932,28 @@ __global__ void k_part_offsets(const int64_t *__restrict__ keys, int64_t n, int 
   }
 }
 
+// narrowed join keys (PartDigitN): partition = top bits of fmix32(offset)
+__global__ void k_part_offsets32(const uint32_t *__restrict__ keys, int64_t n, int bits, int64_t nparts,
+                                 int64_t *__restrict__ offs) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= nparts; p += stride) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)(hashing::fmix32(keys[mid]) >> (32 - bits)) < p) lo = mid + 1; else hi = mid;
+    }
+    offs[p] = lo;
+  }
+}
+
+void radix_part_offsets32(const uint32_t *keys, int64_t n, int bits, int64_t *offs, void *stream) {
+  CYLON_CHECK(bits >= 1 && bits <= 31, Code::Invalid, "narrowed partition bits " << bits);
+  const int64_t np = int64_t(1) << bits;
+  hipLaunchKernelGGL(k_part_offsets32, dim3(grid_for(np + 1)), dim3(kBlock), 0, as_stream(stream), keys, n, bits, np,
+                     offs);
+  HIP_LAUNCH_CHECK();
+}
+
 void radix_part_offsets(const int64_t *keys, int64_t n, int bits, int64_t *offs, void *stream) {
   const int64_t np = int64_t(1) << bits;
   hipLaunchKernelGGL(k_part_offsets, dim3(grid_for(np + 1)), dim3(kBlock), 0, as_stream(stream), keys, n, bits, np,
@@ -1983,1025 +1979,6 @@ void radix_range_part_offsets(const int64_t *keys, int64_t n, uint64_t flip, uin
   const int64_t np = int64_t(1) << bits;
   hipLaunchKernelGGL(k_range_part_offsets, dim3(grid_for(np + 1)), dim3(kBlock), 0, as_stream(stream), keys, n, flip,
                      mn, rshift, np, offs);
-  HIP_LAUNCH_CHECK();
-}
-
-// --------------------------------------------------------------------------
-// per-partition LDS join
-// --------------------------------------------------------------------------
-// The build rows of a partition are indexed by a bucketed (CSR) hash in LDS:
-// 2048 buckets by the low bits of fmix64(key) (independent of the partition
-// bits, which are the top bits), bucket starts as uint16, the keys stored in
-// bucket order and a uint16 permutation back to the staged row.  A probe scans
-// exactly its bucket (mean occupancy < 1): no clustering, no tombstones, and a
-// lane's loop length is its bucket's size.  Built with one LDS atomic per row
-// (16-bit counters packed in pairs), a block scan and one scatter.
-constexpr int kRJBuckets = 4096;
-
-// Build rows per partition that fit the LDS row area: key (8 B) + permutation
-// (2 B) + the staged build columns (widths w[q]; in[q] == nullptr marks the key
-// column itself, which is not staged twice) + a matched flag (build-preserving outer joins).
-int64_t radix_join_capacity(const int *widths, const uint8_t *const *in, int n, bool match_flags) {
-  int64_t row = 8 + 2 + (match_flags ? 1 : 0);
-  for (int q = 0; q < n; ++q)
-    if (in[q]) row += widths[q];
-  int64_t cap = kRJRowArea / row;
-  cap = std::min<int64_t>(cap, kRJMaxRows);
-  return cap & ~int64_t(7);  // multiple of 8: every column region stays 8-byte aligned
-}
-
-__device__ __forceinline__ uint32_t rj_bucket(int64_t k) {
-  return (uint32_t)hashing::fmix64((uint64_t)k) & (kRJBuckets - 1);
-}
-
-// Build rows of one partition: thread t owns rows t + i * kRJThreads (cap <= kRJMaxRows).
-constexpr int kRJRowsPerThread = kRJMaxRows / kRJThreads;
-static_assert(kRJRowsPerThread * kRJThreads == kRJMaxRows, "build rows per thread");
-constexpr int kRJProbeRounds = 1;  // probe rounds of 64 rows per wave prefetched into VGPRs
-
-// bst[0..kRJBuckets) holds per-bucket counts on entry (exclusive starts on exit), bst[kRJBuckets] = total
-template <int THREADS = kRJThreads>
-__device__ __forceinline__ void rj_scan_buckets(uint16_t *bst, uint32_t *wsum) {
-  constexpr int BPT = kRJBuckets / THREADS;
-  const int lane = lane_id(), wave = threadIdx.x / kWave;
-  uint32_t c[BPT], t = 0;
-#pragma unroll
-  for (int j = 0; j < BPT; ++j) {
-    c[j] = bst[threadIdx.x * BPT + j];
-    t += c[j];
-  }
-  uint32_t inc = t;
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const uint32_t x = __shfl_up(inc, d, kWave);
-    if (lane >= d) inc += x;
-  }
-  if (lane == kWave - 1) wsum[wave] = inc;
-  __syncthreads();
-  uint32_t off = inc - t;
-  for (int w = 0; w < wave; ++w) off += wsum[w];
-#pragma unroll
-  for (int j = 0; j < BPT; ++j) {
-    bst[threadIdx.x * BPT + j] = (uint16_t)off;
-    off += c[j];
-  }
-  if (threadIdx.x == THREADS - 1) bst[kRJBuckets] = (uint16_t)off;
-}
-
-// count one bucket's rank for a new row: 16-bit counters packed in pairs
-__device__ __forceinline__ uint32_t rj_claim(uint16_t *bst, uint32_t b) {
-  const uint32_t sh = (b & 1u) * 16u;
-  const uint32_t old = atomicAdd(reinterpret_cast<uint32_t *>(bst) + (b >> 1), 1u << sh);
-  return (old >> sh) & 0xffffu;
-}
-
-// Outer joins (OJ bits): 1 = probe rows without a match are emitted once with a null build side,
-// 2 = build rows without a match are emitted after the partition's matches with a null probe side.
-constexpr int kOJProbe = 1, kOJBuild = 2;
-
-// matches of k in its bucket; OJ & 2: the matched build slots are flagged (plain byte stores of 1)
-template <int OJ>
-__device__ __forceinline__ uint32_t rj_count_mark(const uint16_t *bst, const int64_t *skeys, int64_t k, uint8_t *flg) {
-  const uint32_t b = rj_bucket(k);
-  uint32_t c = 0;
-  for (uint32_t i = bst[b], e = bst[b + 1]; i < e; ++i)
-    if (skeys[i] == k) {
-      ++c;
-      if (OJ & kOJBuild) flg[i] = 1;
-    }
-  return c;
-}
-
-// Count kernel block: 512 threads (10 build + 10 probe keys per thread) so two or three
-// blocks share a CU (48 KB LDS each) and one block's key loads overlap another's probing;
-// the 1024-thread version ran one latency-bound block per CU (128 VGPRs).
-constexpr int kRCThreads = 512;
-constexpr int kRCWaves = kRCThreads / kWave;
-constexpr int kRCRowsPerThread = kRJMaxRows / kRCThreads;
-static_assert(kRCRowsPerThread * kRCThreads == kRJMaxRows, "count rows per thread");
-
-// rows of partition p: offs[p] .. offs[p + 1] (exact passes), or slot-mode partitions (slot > 0:
-// radix_slot_rows_pass) at p * slot holding offs[p] rows
-__device__ __forceinline__ void part_span(const int64_t *offs, int64_t slot, int64_t p, int64_t &b, int64_t &n) {
-  if (slot > 0) {
-    b = p * slot;
-    n = offs[p];
-  } else {
-    b = offs[p];
-    n = offs[p + 1] - b;
-  }
-}
-
-template <int OJ>
-__global__ __launch_bounds__(kRCThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_rj_count(
-    const int64_t *__restrict__ pkeys, const int64_t *__restrict__ poffs, const int64_t *__restrict__ bkeys,
-    const int64_t *__restrict__ boffs, int64_t nparts, int cap, int64_t pstride, int64_t *__restrict__ counts,
-    int *overflow, int64_t pslot, int64_t bslot, const int64_t *__restrict__ items, int64_t nitems,
-    const uint8_t *__restrict__ skip) {
-  using KT = int64_t;
-  // pstride > 1: only partitions 0, pstride, 2 pstride, ... are counted, into counts[p / pstride]
-  // (the sampled output-size estimate of the fused write path).  Output rows per partition:
-  // matches, + unmatched probe rows (OJ & 1), + unmatched build rows (OJ & 2).  items != nullptr:
-  // counts[i] = output rows of split item i (its deferred sides' unmatched rows excluded); skip[p]:
-  // partition p is covered by items (counts 0, never an LDS overflow).
-  __shared__ __attribute__((aligned(16))) uint16_t bst[kRJBuckets + 8];
-  __shared__ KT skeys[kRJMaxRows];
-  __shared__ uint8_t flg[(OJ & kOJBuild) ? kRJMaxRows : 1];
-  __shared__ uint32_t wsum[kRCWaves];
-  __shared__ unsigned long long csum[kRCWaves];
-  const int64_t nsample = items ? nitems : (nparts + pstride - 1) / pstride;
-  for (int64_t ci = blockIdx.x; ci < nsample; ci += gridDim.x) {
-    int64_t rb, nr, lb, nl;
-    int iflags = 0;
-    if (items) {
-      const int64_t *it = items + ci * kRJItemWords;
-      lb = it[0];
-      nl = it[1];
-      rb = it[2];
-      nr = it[3];
-      iflags = (int)it[4];
-    } else {
-      const int64_t p = ci * pstride;
-      if (skip && skip[p]) {
-        if (threadIdx.x == 0) counts[ci] = 0;
-        continue;
-      }
-      part_span(boffs, bslot, p, rb, nr);
-      part_span(poffs, pslot, p, lb, nl);
-    }
-    // unmatched rows of a side count here unless the item defers them (emitted by emission items)
-    const bool pun = (OJ & kOJProbe) && !(iflags & kRJItemPDefer);
-    const bool bun = (OJ & kOJBuild) && !(iflags & kRJItemBDefer);
-    if (nr > cap) {  // uniform branch: whole block
-      if (threadIdx.x == 0) {
-        atomicOr(overflow, 1);
-        counts[ci] = 0;
-      }
-      continue;
-    }
-    if (nr == 0 || nl == 0) {
-      if (threadIdx.x == 0)
-        counts[ci] = (nr == 0 && pun ? nl : 0) + (nl == 0 && bun ? nr : 0);
-      continue;
-    }
-    // build keys are read twice (claim, then place): the second read hits L2 and the block
-    // keeps only 16-bit ranks in registers (two 512-thread blocks per CU without spills)
-    __syncthreads();  // previous partition done with bst / skeys / csum / flg
-    for (int s = threadIdx.x; s < kRJBuckets / 2; s += blockDim.x) reinterpret_cast<uint32_t *>(bst)[s] = 0;
-    if (OJ & kOJBuild)
-      for (int i = threadIdx.x; i < nr; i += blockDim.x) flg[i] = 0;
-    __syncthreads();
-    uint32_t rk[kRCRowsPerThread];
-#pragma unroll
-    for (int i = 0; i < kRCRowsPerThread; ++i) {
-      const int r = threadIdx.x + i * kRCThreads;
-      if (r < nr) rk[i] = rj_claim(bst, rj_bucket(bkeys[rb + r]));
-    }
-    __syncthreads();
-    rj_scan_buckets<kRCThreads>(bst, wsum);
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kRCRowsPerThread; ++i) {
-      const int r = threadIdx.x + i * kRCThreads;
-      if (r < nr) {
-        const KT k = bkeys[rb + r];
-        skeys[bst[rj_bucket(k)] + rk[i]] = k;
-      }
-    }
-    __syncthreads();
-    unsigned long long c = 0;
-    for (int64_t l0 = threadIdx.x; l0 < nl; l0 += 4 * kRCThreads) {  // 4 probe loads in flight
-      KT pk[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (l0 + u * kRCThreads < nl) pk[u] = pkeys[lb + l0 + u * kRCThreads];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (l0 + u * kRCThreads < nl) {
-          const uint32_t mc = rj_count_mark<OJ>(bst, skeys, pk[u], flg);
-          c += pun && mc == 0 ? 1u : mc;
-        }
-    }
-    if ((OJ & kOJBuild) && bun) {  // uniform branch
-      __syncthreads();  // every probe has flagged its matches
-      for (int i = threadIdx.x; i < nr; i += blockDim.x) c += flg[i] ? 0u : 1u;
-    }
-    for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
-    if (lane_id() == 0) csum[threadIdx.x / kWave] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned long long tot = 0;
-      for (int w = 0; w < kRCWaves; ++w) tot += csum[w];
-      counts[ci] = (int64_t)tot;
-    }
-  }
-}
-
-__device__ __forceinline__ int64_t rj_shfl64(int64_t x, int src) {
-  const uint32_t lo = __shfl((uint32_t)(uint64_t)x, src, kWave);
-  const uint32_t hi = __shfl((uint32_t)((uint64_t)x >> 32), src, kWave);
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-__device__ __forceinline__ int64_t rj_shfl_key(int64_t x, int src) { return rj_shfl64(x, src); }
-
-struct BuildOut {               // build-side output columns
-  uint8_t *out[kMaxFusedCols];
-  int width[kMaxFusedCols];
-  int lds_off[kMaxFusedCols];   // byte offset of the staged column in the LDS row area, -1 = key
-  int n;
-  int match_off;                // OJ & 2: byte offset of the build rows' matched flags in the row area
-};
-
-// Outer joins (OJ bits, see rj_count_mark): presence bytes (ppres / bpres: 1 = that side holds a
-// row) are written for the side(s) that can be null; the host turns them into the output
-// columns' validity (join.cpp radix_join).
-
-// the write kernel's build staging: rj_dma_block over its 16 waves
-__device__ __forceinline__ void rj_dma(const uint8_t *src, int bytes, uint8_t *dst, int wave, int lane) {
-  rj_dma_block<kRJWaves>(src, bytes, dst, wave, lane);
-}
-
-// pkey: index of the probe column that IS the key (its value comes from the probe key, not a
-// second load; -1 none).  DMA: stage the build columns by LDS-DMA (needs W8) instead of register
-// round trips per column.
-template <int MAXP, int MAXB, bool W8, bool DMA, int OJ>
-__global__ __launch_bounds__(kRJThreads, 4) void k_rj_write(const int64_t *__restrict__ pkeys,
-                                                            const int64_t *__restrict__ poffs,
-                                                            const int64_t *__restrict__ bkeys,
-                                                            const int64_t *__restrict__ boffs, int64_t nparts,
-                                                            int cap, const int64_t *__restrict__ out_offs, ColSet pc,
-                                                            ColSet bs, BuildOut bo,
-                                                            unsigned long long *__restrict__ cursor, int64_t out_cap,
-                                                            int *__restrict__ overflow,
-                                                            int pkey,
-                                                            uint8_t *__restrict__ ppres, uint8_t *__restrict__ bpres,
-                                                            int64_t pslot, int64_t bslot,
-                                                            const int64_t *__restrict__ items, int64_t nitems,
-                                                            const uint8_t *__restrict__ skip,
-                                                            uint8_t *__restrict__ gprobe,
-                                                            uint8_t *__restrict__ gbuild) {
-  using KT = int64_t;
-  // out_offs != nullptr: partition p's rows start at out_offs[p] (exact count kernel ran first).
-  // out_offs == nullptr: fused count -- each partition claims its rows from *cursor with one
-  // atomic after counting its matches (output partitions land in claim order); a claim past
-  // out_cap sets overflow bit 2 and writes nothing (the cursor still totals the rows needed),
-  // a build side beyond the LDS capacity sets bit 1.
-  // pc: probe columns (in -> out); bs: staged build columns (in, width), LDS
-  // region j at 10*cap + sum of cap*width of the earlier ones; bo: build outputs.
-  // Row area: keys in bucket order [0, 8 cap), permutation to the staged row
-  // [8 cap, 10 cap), payload columns in staged (original) row order, then (OJ & 2) one matched
-  // flag per bucket slot.
-  __shared__ __attribute__((aligned(16))) uint16_t bst[kRJBuckets + 8];
-  __shared__ __attribute__((aligned(16))) uint8_t area[kRJRowArea];
-  __shared__ uint32_t wtot[kRJWaves];
-  __shared__ int64_t sclaim;
-  KT *skeys = reinterpret_cast<KT *>(area);
-  uint16_t *perm = reinterpret_cast<uint16_t *>(area + sizeof(KT) * (int64_t)cap);
-  uint8_t *flg = area + ((OJ & kOJBuild) ? bo.match_off : 0);
-  const int lane = lane_id();
-  const int wave = threadIdx.x / kWave;
-  // work w < nitems: split item w (heaviest first: they lead the grid-stride order); else partition
-  // w - nitems unless skip marks it as covered by items.  Items run in cursor mode only.
-  for (int64_t w = blockIdx.x; w < nitems + nparts; w += gridDim.x) {
-    int64_t rb, nr, lb, nl, p = -1;
-    int iflags = 0;
-    if (w < nitems) {
-      const int64_t *it = items + w * kRJItemWords;
-      lb = it[0];
-      nl = it[1];
-      rb = it[2];
-      nr = it[3];
-      iflags = (int)it[4];
-    } else {
-      p = w - nitems;
-      if (skip && skip[p]) continue;
-      part_span(boffs, bslot, p, rb, nr);
-      part_span(poffs, pslot, p, lb, nl);
-    }
-    const bool pdefer = (iflags & kRJItemPDefer) != 0, bdefer = (iflags & kRJItemBDefer) != 0;
-    const bool pemit = (iflags & kRJItemPEmit) != 0, bemit = (iflags & kRJItemBEmit) != 0;
-    if (nr > cap && out_offs == nullptr && threadIdx.x == 0) atomicOr(overflow, 1);
-    // inner: both sides needed; outer: a preserved side alone still emits its rows
-    const bool live = (nr > 0 && nl > 0) || ((OJ & kOJProbe) && nl > 0) || ((OJ & kOJBuild) && nr > 0);
-    if (!live || nr > cap) continue;
-    const int64_t obase = out_offs && p >= 0 ? out_offs[p] : 0;
-    // ---- phase A: probe rows of this wave's slice into VGPRs (in flight during the build)
-    const int64_t per = (nl + kRJWaves - 1) / kRJWaves;  // each wave owns a contiguous probe slice
-    const int64_t s0 = lb + std::min<int64_t>(nl, wave * per);
-    const int64_t s1 = lb + std::min<int64_t>(nl, (wave + 1) * per);
-    KT pk[kRJProbeRounds];
-    uint64_t pv[kRJProbeRounds][MAXP];
-#pragma unroll
-    for (int u = 0; u < kRJProbeRounds; ++u) {
-      const int64_t l = s0 + u * kWave + lane;
-      if (l < s1) {
-        pk[u] = pkeys[l];
-#pragma unroll
-        for (int q = 0; q < MAXP; ++q)
-          if (q < pc.n && q != pkey) pv[u][q] = ldw<W8>(pc.in[q], l, pc.width[q]);
-      }
-    }
-    KT bk[kRJRowsPerThread];
-    if (!DMA) {
-#pragma unroll
-      for (int i = 0; i < kRJRowsPerThread; ++i) {
-        const int r = threadIdx.x + i * kRJThreads;
-        if (r < nr) bk[i] = bkeys[rb + r];
-      }
-    }
-    // ---- phase B: stage + index the build rows
-    __syncthreads();  // previous partition fully done with bst / area / wtot
-    for (int s = threadIdx.x; s < kRJBuckets / 2; s += blockDim.x) reinterpret_cast<uint32_t *>(bst)[s] = 0;
-    if (OJ & kOJBuild)
-      for (int i = threadIdx.x; i < nr; i += blockDim.x) flg[i] = 0;
-    if (DMA) {  // every build column in ONE round trip: the keys (raw order) into the key region,
-                // the payload columns into theirs; the loads hold no VGPRs
-      rj_dma(reinterpret_cast<const uint8_t *>(bkeys + rb), nr * (int)sizeof(KT), area, wave, lane);
-      int64_t off = (int64_t)(sizeof(KT) + 2) * cap;
-#pragma unroll
-      for (int j = 0; j < MAXB; ++j)
-        if (j < bs.n) {
-          rj_dma(bs.in[j] + rb * 8, nr * 8, area + off, wave, lane);
-          off += (int64_t)cap * 8;
-        }
-      for (int j = MAXB; j < bs.n; ++j) {  // rare: wide build rows
-        for (int r = threadIdx.x; r < nr; r += kRJThreads)
-          stw<true>(area + off, r, 8, ldw<true>(bs.in[j], rb + r, 8));
-        off += (int64_t)cap * 8;
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {  // payload columns, column by column (5 loads in flight per column)
-      int64_t off = (int64_t)(sizeof(KT) + 2) * cap;
-#pragma unroll
-      for (int j = 0; j < MAXB; ++j) {
-        if (j < bs.n) {
-          uint64_t x[kRJRowsPerThread];
-#pragma unroll
-          for (int i = 0; i < kRJRowsPerThread; ++i)
-            if (threadIdx.x + i * kRJThreads < nr) x[i] = ldw<W8>(bs.in[j], rb + threadIdx.x + i * kRJThreads, bs.width[j]);
-#pragma unroll
-          for (int i = 0; i < kRJRowsPerThread; ++i)
-            if (threadIdx.x + i * kRJThreads < nr) stw<W8>(area + off, threadIdx.x + i * kRJThreads, bs.width[j], x[i]);
-          off += (int64_t)cap * bs.width[j];
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      for (int j = MAXB; j < bs.n; ++j) {  // rare: wide build rows
-        for (int r = threadIdx.x; r < nr; r += kRJThreads)
-          stw<W8>(area + off, r, bs.width[j], ldw<W8>(bs.in[j], rb + r, bs.width[j]));
-        off += (int64_t)cap * bs.width[j];
-      }
-    }
-    __syncthreads();
-    if (DMA) {  // raw keys back from the key region (bucket placement overwrites it after the scan)
-#pragma unroll
-      for (int i = 0; i < kRJRowsPerThread; ++i) {
-        const int r = threadIdx.x + i * kRJThreads;
-        if (r < nr) bk[i] = skeys[r];
-      }
-    }
-    uint32_t rk[kRJRowsPerThread];
-#pragma unroll
-    for (int i = 0; i < kRJRowsPerThread; ++i)
-      if (threadIdx.x + i * kRJThreads < nr) rk[i] = rj_claim(bst, rj_bucket(bk[i]));
-    __syncthreads();
-    rj_scan_buckets(bst, wtot);
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kRJRowsPerThread; ++i) {
-      const int r = threadIdx.x + i * kRJThreads;
-      if (r < nr) {
-        const uint32_t pos = bst[rj_bucket(bk[i])] + rk[i];
-        skeys[pos] = bk[i];
-        perm[pos] = (uint16_t)r;
-        if ((OJ & kOJBuild) && bemit) flg[pos] = gbuild[rb + r];  // matched by an earlier item
-      }
-    }
-    __syncthreads();
-    // ---- phase C: count this wave's output rows (matches; a lone row for an unmatched probe row
-    // of a probe-preserving join), flag matched build slots, slice offsets
-    // (a deferring item emits no lone probe rows; an emission item skips rows an earlier item matched)
-    auto emitted = [&](uint32_t mc) -> uint32_t { return (OJ & kOJProbe) && !pdefer ? (mc > 0u ? mc : 1u) : mc; };
-    auto plive = [&](int64_t l) -> bool { return !pemit || gprobe[l] == 0; };
-    // output rows of probe row l (key k); a deferring item records the row's match here, before the
-    // output claim (a claim that does not fit must still leave the flags of an exact rerun's count)
-    auto count_row = [&](int64_t l, KT k) -> uint32_t {
-      const uint32_t mc = rj_count_mark<OJ>(bst, skeys, k, flg);
-      if ((OJ & kOJProbe) && pdefer && mc) gprobe[l] = 1;
-      return plive(l) ? emitted(mc) : 0u;
-    };
-    uint32_t c = 0;
-#pragma unroll
-    for (int u = 0; u < kRJProbeRounds; ++u)
-      if (s0 + u * kWave + lane < s1) c += count_row(s0 + u * kWave + lane, pk[u]);
-    {  // later rounds' probe keys two rounds at a time (both loads in flight before either count)
-      int64_t l = s0 + kRJProbeRounds * kWave + lane;
-      for (; l + kWave < s1; l += 2 * kWave) {
-        const KT ka = pkeys[l], kb = pkeys[l + kWave];
-        c += count_row(l, ka) + count_row(l + kWave, kb);
-      }
-      if (l < s1) c += count_row(l, pkeys[l]);
-    }
-    for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
-    if (lane == 0) wtot[wave] = c;
-    __syncthreads();
-    // unmatched build rows (flags final after the barrier above): emitted after every match, or
-    // recorded for a later emission item (bdefer)
-    uint32_t unm = 0;
-    if ((OJ & kOJBuild) && bdefer) {
-      for (int i = threadIdx.x; i < nr; i += blockDim.x)
-        if (flg[i]) gbuild[rb + perm[i]] = 1;
-    } else if (OJ & kOJBuild) {
-      uint32_t u = 0;
-      for (int i = threadIdx.x; i < nr; i += blockDim.x) u += flg[i] ? 0u : 1u;
-      for (int d = kWave / 2; d > 0; d >>= 1) u += __shfl_xor(u, d, kWave);
-      __shared__ uint32_t usum[kRJWaves];
-      if (lane == 0) usum[wave] = u;
-      __syncthreads();
-#pragma unroll
-      for (int w = 0; w < kRJWaves; ++w) unm += usum[w];
-    }
-    int64_t base = obase;
-    if (out_offs == nullptr) {
-      if (threadIdx.x == 0) {
-        unsigned long long tot = unm;
-        for (int w = 0; w < kRJWaves; ++w) tot += wtot[w];
-        const unsigned long long at = tot ? atomicAdd(cursor, tot) : 0ull;
-        const bool fits = at + tot <= (unsigned long long)out_cap;
-        if (!fits) atomicOr(overflow, 2);
-        sclaim = fits ? (int64_t)at : -1;
-      }
-      __syncthreads();
-      base = sclaim;
-      if (base < 0) continue;  // uniform: the block's claim did not fit
-    }
-    int64_t ubase = base;  // first output row of the unmatched build rows
-#pragma unroll
-    for (int w = 0; w < kRJWaves; ++w) ubase += wtot[w];
-    for (int w = 0; w < wave; ++w) base += wtot[w];
-    // ---- phase D: emit.  Round u + 1's probe row is loaded while round u expands (kn / vn), so
-    // only the first round after the phase-A prefetch waits on memory.
-    static_assert(kRJProbeRounds == 1, "emit prefetch assumes one phase-A round");
-    KT kn = 0;
-    uint64_t vn[MAXP] = {};
-    for (int u = 0; s0 + (int64_t)u * kWave < s1; ++u) {
-      const int64_t l = s0 + (int64_t)u * kWave + lane;
-      const bool active = l < s1 && plive(l);
-      KT k = 0;
-      uint64_t v[MAXP] = {};
-      if (u == 0) {
-        k = pk[0];
-#pragma unroll
-        for (int q = 0; q < MAXP; ++q) v[q] = pv[0][q];
-      } else {
-        k = kn;
-#pragma unroll
-        for (int q = 0; q < MAXP; ++q) v[q] = vn[q];
-      }
-      if (l + kWave < s1) {  // prefetch round u + 1
-        kn = pkeys[l + kWave];
-#pragma unroll
-        for (int q = 0; q < MAXP; ++q)
-          if (q < pc.n && q != pkey) vn[q] = ldw<W8>(pc.in[q], l + kWave, pc.width[q]);
-      }
-      // i0: the first match (scans for match rank j start there); pure: the matches are adjacent, so
-      // match j is slot i0 + j (a hot key's chunk fills its bucket: no O(mc^2) rank scans)
-      uint32_t i0 = 0, i1 = 0, mc = 0, pure = 0;
-      if (active) {
-        const uint32_t b = rj_bucket(k);
-        i1 = bst[b + 1];
-        uint32_t last = 0;
-        for (uint32_t i = bst[b]; i < i1; ++i)
-          if (skeys[i] == k) {
-            if (mc == 0) i0 = i;
-            last = i;
-            ++mc;
-          }
-        pure = mc > 0 && last - i0 + 1 == mc;
-      }
-      const uint32_t ec = active ? emitted(mc) : 0u;  // output rows of this probe row
-      uint32_t inc = ec;  // wave inclusive scan of output counts
-#pragma unroll
-      for (int d = 1; d < kWave; d <<= 1) {
-        const uint32_t x = __shfl_up(inc, d, kWave);
-        if (lane >= d) inc += x;
-      }
-      const uint32_t wsum = __shfl(inc, kWave - 1, kWave);
-      const uint32_t excl = inc - ec;
-      // Load-balanced expansion: lane t writes output rows base + t, base + 64 + t, ...
-      // of this round, so every store covers a contiguous, fully active run of the
-      // output column (a lane-per-probe-row loop over bucket entries would issue
-      // sparse partial-line stores).  The producing probe lane ("owner") of row
-      // s is found by a binary search over the wave's inclusive output counts and
-      // its key / bucket / payload are read with cross-lane permutes.
-      for (uint32_t t0 = 0; t0 < wsum; t0 += kWave) {
-        const uint32_t so = t0 + lane;
-        const bool act = so < wsum;
-        int owner = 0;
-#pragma unroll
-        for (int step = kWave / 2; step >= 1; step >>= 1) {
-          const uint32_t ic = __shfl(inc, owner + step - 1, kWave);
-          if (ic <= so) owner += step;
-        }
-        const uint32_t j = so - __shfl(excl, owner, kWave);  // match rank inside the owner's bucket
-        const KT ko = rj_shfl_key(k, owner);
-        const uint64_t kw = (uint64_t)ko;
-        const uint32_t b0 = __shfl(i0, owner, kWave), b1 = __shfl(i1, owner, kWave);
-        const bool opure = __shfl(pure, owner, kWave) != 0u;
-        const bool omatched = !(OJ & kOJProbe) || __shfl(mc, owner, kWave) > 0u;
-        uint64_t vo[MAXP];
-#pragma unroll
-        for (int q = 0; q < MAXP; ++q) vo[q] = q == pkey ? kw : (uint64_t)rj_shfl64((int64_t)v[q], owner);
-        if (act) {
-          int r = -1;
-          if (omatched && opure)
-            r = perm[b0 + j];
-          else if (omatched)
-            for (uint32_t i = b0, c = 0; i < b1; ++i) {
-              if (skeys[i] != ko) continue;
-              if (c == j) {
-                r = perm[i];
-                break;
-              }
-              ++c;
-            }
-          const int64_t o = base + so;
-#pragma unroll
-          for (int q = 0; q < MAXP; ++q)
-            if (q < pc.n) stw<W8>(pc.out[q], o, pc.width[q], vo[q]);
-          if (pc.n > MAXP) {
-            const int64_t lo = s0 + (int64_t)u * kWave + owner;
-            for (int q = MAXP; q < pc.n; ++q)
-              stw<W8>(pc.out[q], o, pc.width[q], q == pkey ? kw : ldw<W8>(pc.in[q], lo, pc.width[q]));
-          }
-          if ((OJ & kOJProbe) && r < 0) {  // unmatched probe row: build side null
-#pragma unroll
-            for (int q = 0; q < MAXB + 1; ++q)
-              if (q < bo.n) stw<W8>(bo.out[q], o, bo.width[q], 0ull);
-            for (int q = MAXB + 1; q < bo.n; ++q) stw<W8>(bo.out[q], o, bo.width[q], 0ull);
-          } else {
-#pragma unroll
-            for (int q = 0; q < MAXB + 1; ++q)
-              if (q < bo.n)
-                stw<W8>(bo.out[q], o, bo.width[q],
-                        bo.lds_off[q] < 0 ? kw : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
-            for (int q = MAXB + 1; q < bo.n; ++q)
-              stw<W8>(bo.out[q], o, bo.width[q],
-                      bo.lds_off[q] < 0 ? kw : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
-          }
-          if (OJ & kOJProbe) bpres[o] = r >= 0 ? 1 : 0;
-          if (OJ & kOJBuild) ppres[o] = 1;
-        }
-      }
-      base += wsum;
-    }
-    if ((OJ & kOJBuild) && !bdefer) {  // ---- phase E: the unmatched build rows, in bucket-slot order
-      __syncthreads();  // every wave is done with wtot
-      int64_t at = ubase;
-      for (int i0 = 0; i0 < nr; i0 += kRJThreads) {
-        const int i = i0 + (int)threadIdx.x;
-        const uint32_t um = (i < nr && !flg[i]) ? 1u : 0u;
-        const uint32_t ex = rp_block_exscan<kRJWaves>(um, wtot);
-        uint32_t tot = 0;
-#pragma unroll
-        for (int w = 0; w < kRJWaves; ++w) tot += wtot[w];
-        if (um) {
-          const int64_t o = at + ex;
-          const int r = perm[i];
-          const uint64_t kw = (uint64_t)skeys[i];
-          for (int q = 0; q < pc.n; ++q) stw<W8>(pc.out[q], o, pc.width[q], q == pkey ? kw : 0ull);
-          for (int q = 0; q < bo.n; ++q)
-            stw<W8>(bo.out[q], o, bo.width[q], bo.lds_off[q] < 0 ? kw : ldw<W8>(area + bo.lds_off[q], r, bo.width[q]));
-          ppres[o] = 0;
-          if (OJ & kOJProbe) bpres[o] = 1;
-        }
-        at += tot;
-        __syncthreads();  // wtot reused by the next round
-      }
-    }
-  }
-}
-
-static int rj_grid(int64_t nparts) { return (int)std::min<int64_t>(nparts, kNumCUs * 8); }
-
-void radix_join_count(const int64_t *pkeys, const int64_t *poffs, const int64_t *bkeys, const int64_t *boffs,
-                      int64_t nparts, int64_t cap, int64_t *counts, int *overflow, void *stream, int64_t pstride,
-                      int outer, int64_t pslot, int64_t bslot, const RJSplit *split) {
-  CYLON_CHECK(cap > 0 && cap <= kRJMaxRows, Code::Invalid, "radix join capacity " << cap);
-  CYLON_CHECK(pstride >= 1, Code::Invalid, "partition stride " << pstride);
-  CYLON_CHECK(outer >= 0 && outer <= 3, Code::Invalid, "radix join outer mode " << outer);
-  hipStream_t s = as_stream(stream);
-  HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
-  const int64_t *items = split ? split->items : nullptr;
-  const int64_t nitems = items ? split->nitems : 0;
-  const uint8_t *skip = split ? split->skip : nullptr;
-  const int64_t nsample = items ? nitems : (nparts + pstride - 1) / pstride;
-  if (nsample == 0) return;
-  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(nsample, kNumCUs * 12)));
-  switch (outer) {
-    case 0:
-      hipLaunchKernelGGL(k_rj_count<0>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
-                         pstride, counts, overflow, pslot, bslot, items, nitems, skip);
-      break;
-    case 1:
-      hipLaunchKernelGGL(k_rj_count<1>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
-                         pstride, counts, overflow, pslot, bslot, items, nitems, skip);
-      break;
-    case 2:
-      hipLaunchKernelGGL(k_rj_count<2>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
-                         pstride, counts, overflow, pslot, bslot, items, nitems, skip);
-      break;
-    default:
-      hipLaunchKernelGGL(k_rj_count<3>, grid, dim3(kRCThreads), 0, s, pkeys, poffs, bkeys, boffs, nparts, (int)cap,
-                         pstride, counts, overflow, pslot, bslot, items, nitems, skip);
-  }
-  HIP_LAUNCH_CHECK();
-}
-
-template <bool W8, bool DMA, int OJ>
-static void rj_write_launch(dim3 grid, hipStream_t s, const int64_t *pk, const int64_t *poffs, const int64_t *bk,
-                            const int64_t *boffs, int64_t nparts, int cap, const int64_t *out_offs, const ColSet &pc,
-                            const ColSet &bs, const BuildOut &bo, unsigned long long *cur, int64_t out_cap,
-                            int *overflow, int pkey, uint8_t *ppres, uint8_t *bpres,
-                            int64_t pslot, int64_t bslot, const RJSplit &sp) {
-  hipLaunchKernelGGL((k_rj_write<4, 3, W8, DMA, OJ>), grid, dim3(kRJThreads), 0, s, pk, poffs, bk, boffs, nparts, cap,
-                     out_offs, pc, bs, bo, cur, out_cap, overflow, pkey, ppres, bpres, pslot, bslot, sp.items, sp.nitems,
-                     sp.skip, sp.gprobe, sp.gbuild);
-}
-
-void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t *bkeys, const int64_t *boffs,
-                      int64_t nparts, int64_t cap, const int64_t *out_offs, const uint8_t *const *pin,
-                      uint8_t *const *pout, const int *pw, int npc, const uint8_t *const *bin, uint8_t *const *bout,
-                      const int *bw, int nbc, void *stream, int64_t *cursor, int64_t out_cap, int *overflow, int pkey,
-                      int outer, uint8_t *ppres, uint8_t *bpres, int64_t pslot, int64_t bslot,
-                      const RJSplit *split) {
-  CYLON_CHECK(pkey >= -1 && pkey < npc, Code::Invalid, "radix join probe key column " << pkey);
-  CYLON_CHECK(npc <= kMaxFusedCols && nbc <= kMaxFusedCols, Code::Invalid, "too many columns");
-  CYLON_CHECK(out_offs != nullptr || (cursor != nullptr && overflow != nullptr), Code::Invalid,
-              "radix join write: needs partition offsets or an output cursor");
-  CYLON_CHECK(outer >= 0 && outer <= 3, Code::Invalid, "radix join outer mode " << outer);
-  CYLON_CHECK(!(outer & kOJProbe) || bpres, Code::Invalid, "radix join: probe-preserving mode needs build presence");
-  CYLON_CHECK(!(outer & kOJBuild) || ppres, Code::Invalid, "radix join: build-preserving mode needs probe presence");
-  const RJSplit sp = split ? *split : RJSplit{};
-  CYLON_CHECK(sp.nitems == 0 || (out_offs == nullptr && sp.items), Code::Invalid,
-              "radix join write: split items need the cursor mode");
-  if (sp.nitems + nparts == 0) return;
-  CYLON_CHECK(cap > 0 && cap <= radix_join_capacity(bw, bin, nbc, outer & kOJBuild), Code::Invalid,
-              "radix join capacity " << cap);
-  ColSet pc, bs;
-  BuildOut bo;
-  pc.n = npc;
-  bs.n = 0;
-  bo.n = nbc;
-  bool w8 = true;
-  for (int q = 0; q < kMaxFusedCols; ++q) {
-    pc.in[q] = q < npc ? pin[q] : nullptr;
-    pc.out[q] = q < npc ? pout[q] : nullptr;
-    pc.width[q] = q < npc ? pw[q] : 8;
-    bs.in[q] = nullptr;
-    bs.out[q] = nullptr;
-    bs.width[q] = 8;
-    bo.out[q] = q < nbc ? bout[q] : nullptr;
-    bo.width[q] = q < nbc ? bw[q] : 8;
-    bo.lds_off[q] = -1;
-    if (q < npc) w8 &= pw[q] == 8;
-    if (q < nbc) w8 &= bw[q] == 8;
-  }
-  int64_t off = (8 + 2) * cap;
-  for (int q = 0; q < nbc; ++q)
-    if (bin[q]) {
-      bo.lds_off[q] = (int)off;
-      off += cap * bw[q];
-      bs.in[bs.n] = bin[q];
-      bs.width[bs.n++] = bw[q];
-    }
-  bo.match_off = (int)off;
-  if (outer & kOJBuild) off += cap;
-  CYLON_CHECK(off <= kRJRowArea, Code::Invalid, "radix join LDS rows " << off);
-  hipStream_t s = as_stream(stream);
-  // probe columns beyond 4 and staged build columns beyond 3 are loaded in place (slower, correct)
-  unsigned long long *cur = reinterpret_cast<unsigned long long *>(cursor);
-  const dim3 grid(rj_grid(nparts + sp.nitems));
-  // LDS-DMA build staging: write kernel 33.9 -> 32.9 ms per 1B x 1B join (profiles/r03/lds_dma_ab.txt)
-  const bool dma = w8;
-  const int ci = (int)cap;
-#define RJW(W8_, DMA_, OJ_)                                                                                        \
-  rj_write_launch<W8_, DMA_, OJ_>(grid, s, pkeys, poffs, bkeys, boffs, nparts, ci, out_offs, pc, bs, bo, cur, out_cap, \
-                                  overflow, pkey, ppres, bpres, pslot, bslot, sp)
-  if (outer == 0) {
-    if (dma) RJW(true, true, 0);
-    else if (w8) RJW(true, false, 0);
-    else RJW(false, false, 0);
-  } else if (outer == 1) {
-    if (dma) RJW(true, true, 1);
-    else RJW(false, false, 1);
-  } else if (outer == 2) {
-    if (dma) RJW(true, true, 2);
-    else RJW(false, false, 2);
-  } else {
-    if (dma) RJW(true, true, 3);
-    else RJW(false, false, 3);
-  }
-#undef RJW
-  HIP_LAUNCH_CHECK();
-}
-
-
-// --------------------------------------------------------------------------
-// K7 range join: sort-algorithm inner join on range partitions
-// --------------------------------------------------------------------------
-// Both relations are partitioned by RangeDigit into key ranges of 2^rshift
-// values (rshift <= 12), so inside a partition the low rshift bits of
-// (key ^ flip) - mn are an exact key offset.  Per partition one workgroup
-// counts both sides by key offset in LDS (4096 buckets), scans the counts into
-// CSR starts and output offsets, scatters each side's row numbers into key
-// order (uint16 permutations), and then emits output rows slot-major: output
-// row t of the partition finds its key by a binary search over the output
-// offsets and its (left, right) pair as (idx / |R_v|, idx % |R_v|).  The output
-// is therefore ordered by key (partitions are key ranges in order), with no key
-// comparisons at all and every output column written as contiguous runs.
-constexpr int kRGThreads = 1024;
-constexpr int kRGMaxRows = 8192;  // rows per side per partition (uint16 permutations)
-constexpr int kRGBuckets = 4096;
-constexpr int kRGBucketsPerThread = kRGBuckets / kRGThreads;
-
-int64_t range_join_max_rows() { return kRGMaxRows; }
-int range_join_max_shift() { return 12; }
-
-constexpr int kRGRowsPerThread = kRGMaxRows / kRGThreads;
-
-// Low 32 bits of a partition's keys (all the bucket needs: the offset is taken
-// mod 2^rshift) held in registers, kRGRowsPerThread per thread; loaded for the
-// next partition while the current one is processed.
-struct RGKeys {
-  int64_t b = 0, n = 0;
-  uint32_t k[kRGRowsPerThread];
-};
-
-__device__ __forceinline__ void rg_load(const int64_t *__restrict__ keys, const int64_t *__restrict__ offs, int64_t p,
-                                        RGKeys &s) {
-  s.b = offs[p];
-  s.n = offs[p + 1] - s.b;
-  const uint32_t *k32 = reinterpret_cast<const uint32_t *>(keys);
-#pragma unroll
-  for (int i = 0; i < kRGRowsPerThread; ++i) {
-    const int64_t r = threadIdx.x + i * kRGThreads;
-    if (r < s.n && r < kRGMaxRows) s.k[i] = k32[2 * (s.b + r)];  // little endian: low half
-  }
-}
-
-__device__ __forceinline__ uint32_t rg_bucket32(uint32_t k, uint32_t flip, uint32_t mn, uint32_t bmask) {
-  return ((k ^ flip) - mn) & bmask;
-}
-
-__global__ __launch_bounds__(kRGThreads) void k_rg_count(const int64_t *__restrict__ lkeys,
-                                                         const int64_t *__restrict__ loffs,
-                                                         const int64_t *__restrict__ rkeys,
-                                                         const int64_t *__restrict__ roffs, int64_t nparts,
-                                                         uint64_t flip, uint64_t mn, uint32_t bmask,
-                                                         int64_t *__restrict__ counts, int *overflow) {
-  __shared__ uint32_t hl[kRGBuckets], hr[kRGBuckets];
-  __shared__ unsigned long long wsum[kRGThreads / kWave];
-  const uint32_t nb = bmask + 1, f32 = (uint32_t)flip, m32 = (uint32_t)mn;
-  RGKeys nl_, nr_;
-  if ((int64_t)blockIdx.x < nparts) {
-    rg_load(lkeys, loffs, blockIdx.x, nl_);
-    rg_load(rkeys, roffs, blockIdx.x, nr_);
-  }
-  for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
-    const RGKeys L = nl_, R = nr_;
-    if (p + gridDim.x < nparts) {  // next partition's keys in flight during this one
-      rg_load(lkeys, loffs, p + gridDim.x, nl_);
-      rg_load(rkeys, roffs, p + gridDim.x, nr_);
-    }
-    if (L.n > kRGMaxRows || R.n > kRGMaxRows) {  // uniform branch
-      if (threadIdx.x == 0) {
-        atomicOr(overflow, 1);
-        counts[p] = 0;
-      }
-      continue;
-    }
-    if (L.n == 0 || R.n == 0) {
-      if (threadIdx.x == 0) counts[p] = 0;
-      continue;
-    }
-    __syncthreads();  // previous partition done with hl / hr / wsum
-    for (uint32_t v = threadIdx.x; v < nb; v += kRGThreads) hl[v] = hr[v] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kRGRowsPerThread; ++i) {
-      const int64_t r = threadIdx.x + i * kRGThreads;
-      if (r < L.n) atomicAdd(&hl[rg_bucket32(L.k[i], f32, m32, bmask)], 1u);
-      if (r < R.n) atomicAdd(&hr[rg_bucket32(R.k[i], f32, m32, bmask)], 1u);
-    }
-    __syncthreads();
-    unsigned long long c = 0;
-    for (uint32_t v = threadIdx.x; v < nb; v += kRGThreads) c += (unsigned long long)hl[v] * hr[v];
-    for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
-    if (lane_id() == 0) wsum[threadIdx.x / kWave] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned long long t = 0;
-      for (int w = 0; w < kRGThreads / kWave; ++w) t += wsum[w];
-      counts[p] = (int64_t)t;
-    }
-  }
-}
-
-// exclusive scan of a[0..nb) in place (a[nb] = total), kRGBucketsPerThread values per thread
-template <class T>
-__device__ __forceinline__ void rg_scan(T *a, uint32_t nb, T *wtot) {
-  const int lane = lane_id(), wave = threadIdx.x / kWave;
-  T c[kRGBucketsPerThread], t = 0;
-#pragma unroll
-  for (int j = 0; j < kRGBucketsPerThread; ++j) {
-    const uint32_t v = threadIdx.x * kRGBucketsPerThread + j;
-    c[j] = v < nb ? a[v] : T(0);
-    t += c[j];
-  }
-  T inc = t;
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const T x = __shfl_up(inc, d, kWave);
-    if (lane >= d) inc += x;
-  }
-  if (lane == kWave - 1) wtot[wave] = inc;
-  __syncthreads();
-  T off = inc - t;
-  for (int w = 0; w < wave; ++w) off += wtot[w];
-  T total = 0;
-  for (int w = 0; w < kRGThreads / kWave; ++w) total += wtot[w];
-#pragma unroll
-  for (int j = 0; j < kRGBucketsPerThread; ++j) {
-    const uint32_t v = threadIdx.x * kRGBucketsPerThread + j;
-    if (v < nb) a[v] = off;
-    off += c[j];
-  }
-  if (threadIdx.x == 0) a[nb] = total;
-}
-
-constexpr int kRGEmit = 4;  // output rows per thread per emit chunk (4096 per chunk)
-
-// stream one column of a partition side into the LDS stage (coalesced), then write
-// the chunk's output rows from it: an output row's payload is a random row of the
-// partition, so gathering it straight from global memory would pull a whole cache
-// line through L2 -> L1 per 8-byte value (the first version of this kernel was
-// bound by exactly that).
-template <bool W8>
-__device__ __forceinline__ void rg_emit_column(uint8_t *stage, const uint8_t *in, int64_t base, int64_t rows,
-                                               uint8_t *out, int w, int64_t obase, uint32_t c0, uint32_t total,
-                                               const uint16_t *pos) {
-  __syncthreads();  // stage free
-  for (int64_t r0 = 0; r0 < rows; r0 += 4 * kRGThreads) {  // four loads in flight per thread
-    uint64_t x[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t r = r0 + u * kRGThreads + threadIdx.x;
-      if (r < rows) x[u] = ldw<W8>(in, base + r, w);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t r = r0 + u * kRGThreads + threadIdx.x;
-      if (r < rows) stw<W8>(stage, r, w, x[u]);
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int e = 0; e < kRGEmit; ++e) {
-    const uint32_t t = c0 + e * kRGThreads + threadIdx.x;
-    if (t < total) stw<W8>(out, obase + t, w, ldw<W8>(stage, pos[e], w));
-  }
-}
-
-template <bool W8>
-__global__ __launch_bounds__(kRGThreads) void k_rg_write(const int64_t *__restrict__ lkeys,
-                                                         const int64_t *__restrict__ loffs,
-                                                         const int64_t *__restrict__ rkeys,
-                                                         const int64_t *__restrict__ roffs, int64_t nparts,
-                                                         uint64_t flip, uint64_t mn, uint32_t bmask,
-                                                         const int64_t *__restrict__ out_offs, ColSet lc, ColSet rc) {
-  __shared__ uint32_t ls[kRGBuckets + 1], rs[kRGBuckets + 1], oo[kRGBuckets + 1];
-  __shared__ uint16_t pl[kRGMaxRows], pr[kRGMaxRows];
-  __shared__ uint64_t stage64[kRGMaxRows];  // scatter cursors, then one payload column at a time
-  __shared__ uint32_t wtot[3][kRGThreads / kWave];
-  uint8_t *stage = reinterpret_cast<uint8_t *>(stage64);
-  uint32_t *lcur = reinterpret_cast<uint32_t *>(stage64), *rcur = lcur + kRGBuckets;
-  static_assert(2 * kRGBuckets * sizeof(uint32_t) <= kRGMaxRows * sizeof(uint64_t), "cursors fit the stage");
-  const uint32_t nb = bmask + 1, f32 = (uint32_t)flip, m32 = (uint32_t)mn;
-  RGKeys nl_, nr_;
-  if ((int64_t)blockIdx.x < nparts) {
-    rg_load(lkeys, loffs, blockIdx.x, nl_);
-    rg_load(rkeys, roffs, blockIdx.x, nr_);
-  }
-  for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
-    const RGKeys L = nl_, R = nr_;
-    if (p + gridDim.x < nparts) {  // next partition's keys in flight during this one
-      rg_load(lkeys, loffs, p + gridDim.x, nl_);
-      rg_load(rkeys, roffs, p + gridDim.x, nr_);
-    }
-    const int64_t lb = L.b, nl = L.n, rb = R.b, nr = R.n;
-    if (nl == 0 || nr == 0 || nl > kRGMaxRows || nr > kRGMaxRows) continue;
-    const int64_t obase = out_offs[p];
-    __syncthreads();  // previous partition fully done with the LDS arrays
-    for (uint32_t v = threadIdx.x; v < nb; v += kRGThreads) ls[v] = rs[v] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kRGRowsPerThread; ++i) {
-      const int64_t r = threadIdx.x + i * kRGThreads;
-      if (r < nl) atomicAdd(&ls[rg_bucket32(L.k[i], f32, m32, bmask)], 1u);
-      if (r < nr) atomicAdd(&rs[rg_bucket32(R.k[i], f32, m32, bmask)], 1u);
-    }
-    __syncthreads();
-    for (uint32_t v = threadIdx.x; v < nb; v += kRGThreads) oo[v] = ls[v] * rs[v];
-    __syncthreads();
-    rg_scan(ls, nb, wtot[0]);
-    rg_scan(rs, nb, wtot[1]);
-    rg_scan(oo, nb, wtot[2]);
-    __syncthreads();
-    for (uint32_t v = threadIdx.x; v < nb; v += kRGThreads) {
-      lcur[v] = ls[v];
-      rcur[v] = rs[v];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kRGRowsPerThread; ++i) {
-      const int64_t r = threadIdx.x + i * kRGThreads;
-      if (r < nl) pl[atomicAdd(&lcur[rg_bucket32(L.k[i], f32, m32, bmask)], 1u)] = (uint16_t)r;
-      if (r < nr) pr[atomicAdd(&rcur[rg_bucket32(R.k[i], f32, m32, bmask)], 1u)] = (uint16_t)r;
-    }
-    __syncthreads();
-    const uint32_t total = oo[nb];
-    for (uint32_t c0 = 0; c0 < total; c0 += kRGEmit * kRGThreads) {
-      uint16_t lp[kRGEmit], rp[kRGEmit];  // partition rows of this thread's output rows
-#pragma unroll
-      for (int e = 0; e < kRGEmit; ++e) {
-        const uint32_t t = c0 + e * kRGThreads + threadIdx.x;
-        lp[e] = rp[e] = 0;
-        if (t < total) {
-          uint32_t lo = 0, hi = nb;  // largest v with oo[v] <= t (always a non-empty key)
-          while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (oo[mid] <= t) lo = mid; else hi = mid;
-          }
-          const uint32_t idx = t - oo[lo], cr = rs[lo + 1] - rs[lo];
-          const uint32_t li = idx / cr, ri = idx - li * cr;
-          lp[e] = pl[ls[lo] + li];
-          rp[e] = pr[rs[lo] + ri];
-        }
-      }
-#pragma unroll 1
-      for (int q = 0; q < lc.n; ++q)
-        rg_emit_column<W8>(stage, lc.in[q], lb, nl, lc.out[q], lc.width[q], obase, c0, total, lp);
-#pragma unroll 1
-      for (int q = 0; q < rc.n; ++q)
-        rg_emit_column<W8>(stage, rc.in[q], rb, nr, rc.out[q], rc.width[q], obase, c0, total, rp);
-    }
-  }
-}
-
-static int rg_grid(int64_t nparts) { return (int)std::min<int64_t>(nparts, kNumCUs * 4); }
-
-void range_join_count(const int64_t *lkeys, const int64_t *loffs, const int64_t *rkeys, const int64_t *roffs,
-                      int64_t nparts, uint64_t flip, uint64_t mn, int rshift, int64_t *counts, int *overflow,
-                      void *stream) {
-  CYLON_CHECK(rshift >= 0 && rshift <= 12, Code::Invalid, "range join key bits per partition " << rshift);
-  hipStream_t s = as_stream(stream);
-  HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
-  if (nparts == 0) return;
-  hipLaunchKernelGGL(k_rg_count, dim3(rg_grid(nparts)), dim3(kRGThreads), 0, s, lkeys, loffs, rkeys, roffs, nparts,
-                     flip, mn, (uint32_t)((1u << rshift) - 1), counts, overflow);
-  HIP_LAUNCH_CHECK();
-}
-
-void range_join_write(const int64_t *lkeys, const int64_t *loffs, const int64_t *rkeys, const int64_t *roffs,
-                      int64_t nparts, uint64_t flip, uint64_t mn, int rshift, const int64_t *out_offs,
-                      const uint8_t *const *lin, uint8_t *const *lout, const int *lw, int nlc,
-                      const uint8_t *const *rin, uint8_t *const *rout, const int *rw, int nrc, void *stream) {
-  CYLON_CHECK(rshift >= 0 && rshift <= 12, Code::Invalid, "range join key bits per partition " << rshift);
-  CYLON_CHECK(nlc <= kMaxFusedCols && nrc <= kMaxFusedCols, Code::Invalid, "too many columns");
-  if (nparts == 0) return;
-  ColSet lc, rc;
-  lc.n = nlc;
-  rc.n = nrc;
-  bool w8 = true;
-  for (int q = 0; q < kMaxFusedCols; ++q) {
-    lc.in[q] = q < nlc ? lin[q] : nullptr;
-    lc.out[q] = q < nlc ? lout[q] : nullptr;
-    lc.width[q] = q < nlc ? lw[q] : 8;
-    rc.in[q] = q < nrc ? rin[q] : nullptr;
-    rc.out[q] = q < nrc ? rout[q] : nullptr;
-    rc.width[q] = q < nrc ? rw[q] : 8;
-    if (q < nlc) w8 &= lw[q] == 8;
-    if (q < nrc) w8 &= rw[q] == 8;
-  }
-  const uint32_t bmask = (uint32_t)((1u << rshift) - 1);
-  hipStream_t s = as_stream(stream);
-  if (w8)
-    hipLaunchKernelGGL(k_rg_write<true>, dim3(rg_grid(nparts)), dim3(kRGThreads), 0, s, lkeys, loffs, rkeys, roffs,
-                       nparts, flip, mn, bmask, out_offs, lc, rc);
-  else
-    hipLaunchKernelGGL(k_rg_write<false>, dim3(rg_grid(nparts)), dim3(kRGThreads), 0, s, lkeys, loffs, rkeys, roffs,
-                       nparts, flip, mn, bmask, out_offs, lc, rc);
   HIP_LAUNCH_CHECK();
 }
 

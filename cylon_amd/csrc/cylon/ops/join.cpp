@@ -211,6 +211,9 @@ struct RadixSide {
   std::vector<at::Tensor> vwords;
 };
 
+// partitioned key array (int64, or uint32 offsets when narrowed) as the kernels' pointer
+static const int64_t *kptr(const at::Tensor &k) { return reinterpret_cast<const int64_t *>(k.data_ptr()); }
+
 // rows of each partition / its first row in the partitioned arrays (slot mode: p * slot)
 static at::Tensor part_counts(const RadixSide &s, int64_t nparts) {
   return s.slot ? s.offs.slice(0, 0, nparts) : s.offs.slice(0, 1, nparts + 1) - s.offs.slice(0, 0, nparts);
@@ -233,7 +236,8 @@ static bool packs_validity(const TablePtr &t) {
 // Partition every column of t (+ validity bytes) by the top `bits` bits of fmix64(key).
 // slot > 0: try the slot-mode (histogram-free MSD) partition first
 static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Tensor &keys, int bits,
-                                 const RangeSpec *range = nullptr, int64_t slot = 0) {
+                                 const RangeSpec *range = nullptr, int64_t slot = 0,
+                                 const hip::NarrowKeys *nk = nullptr) {
   std::vector<at::Tensor> cur{keys};
   std::vector<int> widths{8};
   std::vector<int> dslot(t->Columns(), -1), vslot(t->Columns(), -1);
@@ -261,13 +265,13 @@ static RadixSide radix_partition(const Exec &ex, const TablePtr &t, const at::Te
   std::vector<at::Tensor> sl;
   if (slot > 0 && !range)
     sl = RadixPartitionSlotted(ex, cur, widths, bits, slot, &offs, &s.overflow,
-                               packs_validity(t) ? &packed : nullptr);
+                               packs_validity(t) ? &packed : nullptr, nk);
   if (!sl.empty()) {
     cur = std::move(sl);
     s.slot = slot;
   } else {
     cur = RadixPartition(ex, std::move(cur), widths, bits, &offs, range, packs_validity(t) ? &packed : nullptr,
-                         range != nullptr);
+                         range != nullptr, nk);
   }
   s.keys = cur[0];
   s.offs = offs;
@@ -434,7 +438,28 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     if (col.type.width() == 8 && col.data.data_ptr() == (build_left ? lk : rk).data_ptr()) shape.in[q] = nullptr;
     if (col.nullable() && !packs_validity(bt)) ++q;  // packed validity words sit after the columns
   }
-  const int64_t cap = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size(), (oj & 2) != 0);
+  // Narrowed keys (kernel_decls.inc NarrowKeys): when each side's join key is its own int64 column,
+  // the partitions carry it as a uint32 offset from base = (left key 0) - 2^31 -- 4 B/row less in
+  // every pass write, the second pass's reads and the join kernel's reads (the headline's 1B x 1B
+  // join: 16 of 128 bytes moved per row and side).  A key outside [base, base + 2^32) is detected
+  // by the first pass, and the join repartitions without narrowing.
+  auto own_key_column = [](const TablePtr &t, const at::Tensor &k) {
+    int hits = 0;
+    for (const auto &c : t->columns())
+      hits += c.type.width() == 8 && c.data.data_ptr() == k.data_ptr() &&
+              (c.type.kind() == ValueKind::SIGNED_INT || c.type.kind() == ValueKind::UNSIGNED_INT);
+    return hits == 1;
+  };
+  bool narrow = nl > 0 && nr > 0 && lk.scalar_type() == at::kLong && rk.scalar_type() == at::kLong &&
+                own_key_column(left, lk) && own_key_column(right, rk);
+  at::Tensor narrow_bad = narrow ? at::zeros({1}, ex.opts(at::kInt)) : at::Tensor();
+  hip::NarrowKeys nk;
+  if (narrow) {
+    nk.base_src = ptr<int64_t>(lk);
+    nk.bad = reinterpret_cast<unsigned int *>(narrow_bad.data_ptr<int>());
+  }
+  int64_t cap = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size(), (oj & 2) != 0,
+                                         narrow ? 4 : 8);
   // fewest partition bits whose mean build partition sits 8 Poisson sigma (+16 rows) below the
   // LDS capacity: the largest of ~2^18 uniform partitions then fits with ~1e-10 failure odds (an
   // overflow only sends the join to the exact / global path).  1B rows: 18 bits -- two 9-bit
@@ -458,24 +483,38 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   RadixSide L, R;
   {
     CYLON_PHASE("join.radix.partition", ex.device);
-    L = radix_partition(ex, left, lk, bits, nullptr, slot_of(nl));
-    R = radix_partition(ex, right, rk, bits, nullptr, slot_of(nr));
-    if (L.slot || R.slot) {  // a side whose partition outgrew a slot is partitioned exactly
-      at::Tensor f = at::stack({L.slot ? L.overflow[0] : at::zeros({}, ex.opts(at::kInt)),
-                                R.slot ? R.overflow[0] : at::zeros({}, ex.opts(at::kInt))}).cpu();
+    const hip::NarrowKeys *nkp = narrow ? &nk : nullptr;
+    L = radix_partition(ex, left, lk, bits, nullptr, slot_of(nl), nkp);
+    R = radix_partition(ex, right, rk, bits, nullptr, slot_of(nr), nkp);
+    if (L.slot || R.slot || narrow) {  // a side whose partition outgrew a slot is partitioned exactly
+      at::Tensor z = at::zeros({}, ex.opts(at::kInt));
+      at::Tensor f = at::stack({L.slot ? L.overflow[0] : z, R.slot ? R.overflow[0] : z,
+                                narrow ? narrow_bad[0] : z}).cpu();
+      if (f[2].item<int>()) {  // a key outside the uint32 offset range: both sides as int64 keys
+        trace::add_counter("join.radix.narrow_fallback", 1);
+        narrow = false;  // (8-byte keys: the smaller LDS capacity; fuller partitions become split items)
+        cap = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size(), (oj & 2) != 0, 8);
+        L = radix_partition(ex, left, lk, bits, nullptr, slot_of(nl));
+        R = radix_partition(ex, right, rk, bits, nullptr, slot_of(nr));
+        if (L.slot || R.slot)
+          f = at::stack({L.slot ? L.overflow[0] : z, R.slot ? R.overflow[0] : z, z}).cpu();
+      }
+      nkp = narrow ? &nk : nullptr;
       if (f[0].item<int>()) {
         trace::add_counter("join.radix.slot_overflow", 1);
-        L = radix_partition(ex, left, lk, bits);
+        L = radix_partition(ex, left, lk, bits, nullptr, 0, nkp);
       }
       if (f[1].item<int>()) {
         trace::add_counter("join.radix.slot_overflow", 1);
-        R = radix_partition(ex, right, rk, bits);
+        R = radix_partition(ex, right, rk, bits, nullptr, 0, nkp);
       }
       trace::add_counter("join.radix.slot_sides", (L.slot ? 1 : 0) + (R.slot ? 1 : 0));
+      if (narrow) trace::add_counter("join.radix.narrow_keys", 1);
     }
   }
   RadixSide &B = build_left ? L : R;
   RadixSide &P = build_left ? R : L;
+  const int64_t *nbase = narrow ? ptr<int64_t>(lk) : nullptr;  // the join kernels' narrowed-key base
   // Skewed partitions are handled per partition, not per join: a partition whose build side exceeds
   // the LDS capacity or whose probe side is hot (> 2 probe chunks) is skipped by the partition loop
   // and covered by split work items (kernel_decls.inc RJSplit): build chunks of <= cap rows x probe
@@ -486,8 +525,14 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   const int64_t split_rows = std::max<int64_t>(8, std::min<int64_t>(cap, knobs::Int("RJ_SPLIT_ROWS", cap)));
   at::Tensor bcnt = part_counts(B, nparts), pcnt = part_counts(P, nparts);
   at::Tensor heavy = at::logical_or(bcnt > split_rows, pcnt > 2 * pch);
-  at::Tensor skip = heavy.to(at::kByte);
-  const int64_t nheavy = heavy.sum().item<int64_t>();
+  // hot-ish partitions (far above the mean, not split) are counted exactly instead of sampled: a
+  // sample that misses them under-estimates the output and costs a second write (skip = 2)
+  const int64_t bmean = ((build_left ? nl : nr) + nparts - 1) / nparts;
+  at::Tensor mid = at::logical_and(heavy.logical_not(),
+                                   at::logical_or(pcnt > 4 * (np_rows + nparts - 1) / nparts + 1024, bcnt > 4 * bmean + 1024));
+  at::Tensor skip = heavy.to(at::kByte), skip_sample = at::logical_or(heavy, mid).to(at::kByte);
+  at::Tensor hm = at::stack({heavy.sum(), mid.sum()}).cpu();
+  const int64_t nheavy = hm[0].item<int64_t>(), nmid = hm[1].item<int64_t>();
   std::vector<int64_t> items, emits;  // kRJItemWords per item
   int64_t emit_bound = 0;
   if (nheavy > 0) {
@@ -543,6 +588,16 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   }
   hip::RJSplit split_main, split_emit;
   split_main.skip = nheavy ? skip.data_ptr<uint8_t>() : nullptr;
+  at::Tensor mid_items;  // count-only items of the skip = 2 partitions
+  if (nmid > 0) {
+    at::Tensor midx = mid.nonzero().flatten();
+    mid_items = at::stack({part_starts(P, nparts).index_select(0, midx), pcnt.index_select(0, midx),
+                           part_starts(B, nparts).index_select(0, midx), bcnt.index_select(0, midx),
+                           at::zeros({nmid}, ex.opts(at::kLong))},
+                          1)
+                    .contiguous();
+    trace::add_counter("join.radix.exact_counted_partitions", nmid);
+  }
   split_main.items = nitems ? ptr<int64_t>(items_d) : nullptr;
   split_main.nitems = nitems;
   split_main.gprobe = gprobe.defined() ? gprobe.data_ptr<uint8_t>() : nullptr;
@@ -573,13 +628,15 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   int64_t m = 0, alloc = 0;
   {
     CYLON_PHASE("join.radix.count", ex.device);
-    hip::RJSplit skip_only;  // the partition count skips split partitions (items are counted below)
-    skip_only.skip = split_main.skip;
+    // the partition count skips split partitions (items are counted below); the sampled count also
+    // the hot-ish ones (counted exactly below)
+    hip::RJSplit skip_only;
     auto count = [&](int64_t st) {
+      skip_only.skip = st > 1 && nmid ? skip_sample.data_ptr<uint8_t>() : split_main.skip;
       counts = ex.empty_i64((nparts + st - 1) / st);
-      hip::radix_join_count(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
+      hip::radix_join_count(kptr(P.keys), ptr<int64_t>(P.offs), kptr(B.keys), ptr<int64_t>(B.offs),
                             nparts, cap, ptr<int64_t>(counts), overflow.data_ptr<int>(), ex.stream, st, oj, P.slot,
-                            B.slot, &skip_only);
+                            B.slot, &skip_only, nbase);
     };
     count(stride);
     // the ranking guard of the stable (second and later) partition passes
@@ -616,16 +673,29 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
         return nullptr;
       }
       const double est = (double)tail[0].item<int64_t>() * (double)nparts / (double)counts.numel();
-      alloc = (int64_t)(est * 1.02 * est_scale) + (est_scale < 1.0 ? 0 : 65536);
+      // skewed inputs (split or exactly counted partitions exist): the sampled rest still holds
+      // moderately hot keys, so its estimate gets 10 % slack instead of 2 % (memory, not a rewrite)
+      const double slack = nheavy + nmid > 0 ? 1.10 : 1.02;
+      alloc = (int64_t)(est * slack * est_scale) + (est_scale < 1.0 ? 0 : 65536);
       trace::add_counter("join.radix.estimated_rows", (int64_t)est);
+    }
+    if (nmid > 0 && stride > 1) {  // the partitions left out of the sample, counted exactly
+      at::Tensor mc = ex.empty_i64(nmid);
+      hip::RJSplit only;
+      only.items = ptr<int64_t>(mid_items);
+      only.nitems = nmid;
+      hip::radix_join_count(kptr(P.keys), ptr<int64_t>(P.offs), kptr(B.keys), ptr<int64_t>(B.offs),
+                            0, cap, ptr<int64_t>(mc), overflow.data_ptr<int>(), ex.stream, 1, oj, P.slot, B.slot,
+                            &only, nbase);
+      alloc += mc.sum().item<int64_t>();
     }
     if (nitems > 0) {  // split items: counted exactly (their deferred rows bounded), cursor mode
       at::Tensor ic = ex.empty_i64(nitems);
       hip::RJSplit only = split_main;
       only.skip = nullptr;
-      hip::radix_join_count(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
+      hip::radix_join_count(kptr(P.keys), ptr<int64_t>(P.offs), kptr(B.keys), ptr<int64_t>(B.offs),
                             0, cap, ptr<int64_t>(ic), overflow.data_ptr<int>(), ex.stream, 1, oj, P.slot, B.slot,
-                            &only);
+                            &only, nbase);
       const int64_t exact_items = ic.sum().item<int64_t>();
       alloc = (stride == 1 ? m : alloc) + exact_items + emit_bound;
       stride = 2;  // (cursor mode below)
@@ -680,17 +750,17 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
         pc.in[q] = reinterpret_cast<const uint8_t *>(P.keys.data_ptr());
         if (pkey < 0) pkey = (int)q;
       }
-    hip::radix_join_write(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
+    hip::radix_join_write(kptr(P.keys), ptr<int64_t>(P.offs), kptr(B.keys), ptr<int64_t>(B.offs),
                           nparts, cap, offs, pc.in.data(), pc.out.data(), pc.w.data(), (int)pc.in.size(),
                           bc.in.data(), bc.out.data(), bc.w.data(), (int)bc.in.size(), ex.stream, cursor, rows,
                           overflow.data_ptr<int>(), pkey, oj, ppres.defined() ? ppres.data_ptr<uint8_t>() : nullptr,
-                          bpres.defined() ? bpres.data_ptr<uint8_t>() : nullptr, P.slot, B.slot, &split_main);
+                          bpres.defined() ? bpres.data_ptr<uint8_t>() : nullptr, P.slot, B.slot, &split_main, nbase);
     if (nemits > 0)  // the deferred sides' unmatched rows, after every item recorded its matches
-      hip::radix_join_write(ptr<int64_t>(P.keys), ptr<int64_t>(P.offs), ptr<int64_t>(B.keys), ptr<int64_t>(B.offs),
+      hip::radix_join_write(kptr(P.keys), ptr<int64_t>(P.offs), kptr(B.keys), ptr<int64_t>(B.offs),
                             0, cap, nullptr, pc.in.data(), pc.out.data(), pc.w.data(), (int)pc.in.size(),
                             bc.in.data(), bc.out.data(), bc.w.data(), (int)bc.in.size(), ex.stream, cursor, rows,
                             overflow.data_ptr<int>(), pkey, oj, ppres.defined() ? ppres.data_ptr<uint8_t>() : nullptr,
-                            bpres.defined() ? bpres.data_ptr<uint8_t>() : nullptr, P.slot, B.slot, &split_emit);
+                            bpres.defined() ? bpres.data_ptr<uint8_t>() : nullptr, P.slot, B.slot, &split_emit, nbase);
   };
   if (stride == 1) {
     allocate(m);
@@ -997,13 +1067,19 @@ static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr
     }
   }
   bool packable = lc.size() <= (size_t)kMaxCompositeKeys;
+  // non-null string / binary / fixed-size binary key columns join through the verified row hash
+  // (their bytes travel as gathered var-width columns; reference arrow_partition_kernels.cpp:243-305)
+  auto hashed_ok = [](const Column &c) {
+    return !c.nullable() && (c.is_var() || c.type.kind() == ValueKind::FIXED_BYTES);
+  };
   for (size_t i = 0; i < lc.size(); ++i) {
     const Column &a = left->column(lc[i]), &b = right->column(rc[i]);
     if (!(a.type == b.type)) return k;
     const bool na = nullable_int_key(a), nb = nullable_int_key(b);
-    if ((!simple_key(a) && !na) || (!simple_key(b) && !nb)) return k;
+    if ((!simple_key(a) && !na && !hashed_ok(a)) || (!simple_key(b) && !nb && !hashed_ok(b))) return k;
     k.nulls = k.nulls || na || nb;
     packable = packable && (int_key(a) || na) && (int_key(b) || nb);
+    if (hashed_ok(a)) trace::add_counter("join.radix.var_key", 1);
   }
   if (k.nulls && !packable) return k;  // nullable keys only as an exact composite
   k.ok = true;
@@ -1081,18 +1157,26 @@ static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr
 }
 
 // rows of a hashed-key radix join whose key columns differ (64-bit hash collisions); both sides
-// present rows only (outer rows carry one null side)
+// present rows only (outer rows carry one null side).  Row-wise equality of every key type
+// (strings / binary byte-wise) by the rows_equal kernel.
 static int64_t key_mismatches(const TablePtr &out, const JoinConfig &cfg, int nleft) {
   const auto &lc = cfg.GetLeftColumnIdx();
   const auto &rc = cfg.GetRightColumnIdx();
-  if (out->Rows() == 0) return 0;
-  at::Tensor bad;
-  for (size_t i = 0; i < lc.size(); ++i) {
+  const int64_t m = out->Rows();
+  if (m == 0) return 0;
+  Exec ex(out->device());
+  std::vector<int> lcols(lc.begin(), lc.end()), rcols;
+  for (int c : rc) rcols.push_back(nleft + c);
+  std::vector<ColView> lv = views(out, lcols), rv = views(out, rcols);
+  at::Tensor idx = at::arange(m, ex.opts(at::kLong));
+  at::Tensor eq = ex.empty_u8(m);
+  KCALL(ex, rows_equal, lv.data(), rv.data(), (int)lv.size(), ptr<int64_t>(idx), ptr<int64_t>(idx), m,
+        ptr<uint8_t>(eq));
+  at::Tensor bad = eq.eq(0);
+  for (size_t i = 0; i < lc.size(); ++i) {  // compare where both sides hold a row
     const Column &a = out->column(lc[i]), &b = out->column(nleft + rc[i]);
-    at::Tensor ne = a.data.ne(b.data);
-    if (a.nullable()) ne.logical_and_(a.validity);
-    if (b.nullable()) ne.logical_and_(b.validity);
-    bad = bad.defined() ? bad.logical_or_(ne) : ne;
+    if (a.nullable()) bad.logical_and_(a.validity.slice(0, 0, m));
+    if (b.nullable()) bad.logical_and_(b.validity.slice(0, 0, m));
   }
   return bad.sum().item<int64_t>();
 }

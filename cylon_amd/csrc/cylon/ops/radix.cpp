@@ -71,7 +71,7 @@ static thread_local bool tl_partition_lb_off = false;  // set while a look-back 
 
 std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> cur, const std::vector<int> &widths,
                                        int bits, at::Tensor *offs, const RangeSpec *range,
-                                       std::vector<int> *keep_packed, bool stable) {
+                                       std::vector<int> *keep_packed, bool stable, const hip::NarrowKeys *nk) {
   CYLON_CHECK(ex.gpu, Code::Invalid, "RadixPartition is a device path");
   CYLON_CHECK(!cur.empty() && cur.size() == widths.size() && widths[0] == 8, Code::Invalid,
               "RadixPartition: column 0 must be the int64 key");
@@ -83,7 +83,9 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
   // pass counts (chunk, next digit) and the later ones take their offsets by look-back, without a
   // tile histogram (1B-row group-by 24.2 / 25.3 -> 23.3 / 24.0 ms, profiles/r04/partition_lookback_ab.txt).
   // Test knob CYLON_PARTITION_LOOKBACK=0 returns to the exact tile histograms.
-  const bool lb_want = !range && stable && !tl_partition_lb_off && knobs::Flag("PARTITION_LOOKBACK", true) &&
+  if (nk && !nk->base_src) nk = nullptr;
+  CYLON_CHECK(!(nk && range), Code::Invalid, "RadixPartition: narrowed keys are hash partitions");
+  const bool lb_want = !range && !nk && stable && !tl_partition_lb_off && knobs::Flag("PARTITION_LOOKBACK", true) &&
                        !knobs::Flag("RP_DEBUG_UNSTABLE", false);
   const std::vector<at::Tensor> orig = lb_want ? cur : std::vector<at::Tensor>();  // for the (never seen) fallback
   // Nullable payloads made a 200M join 24.8 -> 47.8 ms with unpacked validity bytes
@@ -110,10 +112,12 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
     std::vector<at::Tensor> nxt;
     std::vector<const uint8_t *> in;
     std::vector<uint8_t *> out;
+    std::vector<int> pwp = pw;  // narrowed keys: column 0 is 4 bytes wide after the first pass
+    if (nk && ps > 0) pwp[0] = 4;
     for (size_t c = 0; c < cur.size(); ++c) {
       const at::Tensor &x = cur[c];
       // an undefined tensor is a row-id column: generated by the first pass (radix_rows_pass)
-      nxt.push_back(x.defined() ? at::empty_like(x) : ex.empty_i64(n));
+      nxt.push_back(nk && c == 0 ? at::empty({n}, ex.opts(at::kInt)) : (x.defined() ? at::empty_like(x) : ex.empty_i64(n)));
       in.push_back(x.defined() ? reinterpret_cast<const uint8_t *>(x.data_ptr()) : nullptr);
       out.push_back(reinterpret_cast<uint8_t *>(nxt.back().data_ptr()));
     }
@@ -124,10 +128,15 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
     else {
       SortLbArgs lba{};
       if (lb_on) lba = hip::radix_sort_lb_args(ptr<int64_t>(lbws), n, ps, npass, ex.stream);
+      hip::NarrowKeys nkp;
+      if (nk) {
+        nkp = *nk;
+        nkp.kin4 = ps > 0;
+      }
       hip::radix_rows_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, bits, shift, db, in.data(),
-                           out.data(), pw.data(), (int)cur.size(), ptr<int64_t>(ws), ex.stream,
+                           out.data(), pwp.data(), (int)cur.size(), ptr<int64_t>(ws), ex.stream,
                            stable || ps > 0,  // LSD: every pass after the first keeps the order it receives
-                           lb_on ? &lba : nullptr, ps + 1 < npass ? dbits[ps + 1] : 0);
+                           lb_on ? &lba : nullptr, ps + 1 < npass ? dbits[ps + 1] : 0, nk ? &nkp : nullptr);
     }
     cur = std::move(nxt);
     shift += db;
@@ -156,6 +165,9 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
   if (range)
     hip::radix_range_part_offsets(ptr<int64_t>(cur[0]), n, range->flip, range->mn, range->rshift, bits,
                                   ptr<int64_t>(*offs), ex.stream);
+  else if (nk && npass > 0)
+    hip::radix_part_offsets32(reinterpret_cast<const uint32_t *>(cur[0].data_ptr()), n, bits, ptr<int64_t>(*offs),
+                              ex.stream);
   else
     hip::radix_part_offsets(ptr<int64_t>(cur[0]), n, bits, ptr<int64_t>(*offs), ex.stream);
   return cur;
@@ -164,7 +176,8 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
 std::vector<at::Tensor> RadixPartitionSlotted(const Exec &ex, std::vector<at::Tensor> cur,
                                               const std::vector<int> &widths, int bits, int64_t slot,
                                               at::Tensor *counts, at::Tensor *overflow,
-                                              std::vector<int> *keep_packed) {
+                                              std::vector<int> *keep_packed, const hip::NarrowKeys *nk) {
+  if (nk && !nk->base_src) nk = nullptr;
   CYLON_CHECK(ex.gpu && !cur.empty() && cur.size() == widths.size() && widths[0] == 8 && slot > 0, Code::Invalid,
               "RadixPartitionSlotted arguments");
   const int64_t n = cur[0].numel();
@@ -192,7 +205,8 @@ std::vector<at::Tensor> RadixPartitionSlotted(const Exec &ex, std::vector<at::Te
   std::vector<const uint8_t *> in;
   std::vector<uint8_t *> out;
   for (const at::Tensor &x : cur) {
-    mid.push_back(x.defined() ? at::empty({rows1}, x.options()) : ex.empty_i64(rows1));
+    mid.push_back(nk && mid.empty() ? at::empty({rows1}, ex.opts(at::kInt))
+                                    : (x.defined() ? at::empty({rows1}, x.options()) : ex.empty_i64(rows1)));
     in.push_back(x.defined() ? reinterpret_cast<const uint8_t *>(x.data_ptr()) : nullptr);
     out.push_back(reinterpret_cast<uint8_t *>(mid.back().data_ptr()));
   }
@@ -204,10 +218,10 @@ std::vector<at::Tensor> RadixPartitionSlotted(const Exec &ex, std::vector<at::Te
       }
     hip::radix_slot_first_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, bits, db1, db2, in.data(),
                                out.data(), pw.data(), (int)cur.size(), s1, ptr<int64_t>(ws1), ptr<int64_t>(cnt1), ovf,
-                               ex.stream);
+                               ex.stream, nk);
   } else {
     hip::radix_rows_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, bits, db2, db1, in.data(),
-                         out.data(), pw.data(), (int)cur.size(), ptr<int64_t>(ws1), ex.stream, false);
+                         out.data(), pw.data(), (int)cur.size(), ptr<int64_t>(ws1), ex.stream, false, nullptr, 0, nk);
   }
   cur.clear();
   // pass 2: the low digit inside each first-pass bucket, into the partition slots
@@ -223,10 +237,17 @@ std::vector<at::Tensor> RadixPartitionSlotted(const Exec &ex, std::vector<at::Te
   }
   at::Tensor ws2 = ex.empty_i64(hip::radix_slot_workspace(db1, db2));
   *counts = ex.empty_i64(nparts);
+  hip::NarrowKeys nk2;
+  std::vector<int> pw2 = pw;
+  if (nk) {
+    nk2 = *nk;
+    nk2.kin4 = 1;
+    pw2[0] = 4;
+  }
   hip::radix_slot_rows_pass(reinterpret_cast<const int64_t *>(mid[0].data_ptr()), n, bits, db1, db2, in.data(),
-                            out.data(), pw.data(), (int)mid.size(), ptr<int64_t>(ws1),
+                            out.data(), pw2.data(), (int)mid.size(), ptr<int64_t>(ws1),
                             slot1 ? ptr<int64_t>(cnt1) : nullptr, s1, slot, ptr<int64_t>(ws2), ptr<int64_t>(*counts),
-                            ovf, ex.stream);
+                            ovf, ex.stream, nk ? &nk2 : nullptr);
   mid.clear();
   if (bp.active && keep_packed) {
     std::vector<at::Tensor> res(bp.keep_idx.size() + bp.byte_idx.size());

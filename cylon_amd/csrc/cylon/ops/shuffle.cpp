@@ -693,7 +693,8 @@ static GapPlan gap_plan(int W, int K, int me, bool self_wire, const std::functio
 // validity buffer whatever this rank holds).  Fast path: ONE LDS-staged mod-partition pass writes
 // the gaps itself; otherwise a partition-major reorder is copied bucket-range by bucket-range.
 static TablePtr layout_reorder(const TablePtr &t, const std::vector<int> &kcols, uint32_t P, const GapPlan &g,
-                               const std::vector<int64_t> &nullable, bool fast, bool *used_fast) {
+                               const std::vector<int64_t> &nullable, bool fast, bool *used_fast,
+                               const at::Tensor &pid_pre = at::Tensor()) {
   Exec ex(t->device());
   const int64_t n = t->Rows();
   *used_fast = false;
@@ -749,7 +750,7 @@ static TablePtr layout_reorder(const TablePtr &t, const std::vector<int> &kcols,
   trace::add_counter("shuffle.gapped_copy", 1);
   std::pair<TablePtr, std::vector<int64_t>> ro =
       fast ? std::make_pair(mod_reorder(t, kcols[0], P), std::vector<int64_t>())
-           : PartitionReorder(t, hash_pids(t, kcols, P), P);
+           : PartitionReorder(t, pid_pre.defined() ? pid_pre : hash_pids(t, kcols, P), P);
   std::vector<Column> cols;
   for (int c = 0; c < t->Columns(); ++c) {
     const Column &col = t->column(c);
@@ -785,7 +786,8 @@ struct GapPending {
 
 // posts chunk k of a gapped layout: one segment all-to-all per column buffer
 static GapPending post_gapped(const TablePtr &lay, const GapPlan &g, int k, const WirePlan &plan,
-                              const std::vector<at::Tensor> &wire, const std::vector<int64_t> &nullable) {
+                              const std::vector<at::Tensor> &wire, const std::vector<int64_t> &nullable,
+                              int skip_col = -1) {
   GapPending pd;
   auto comm = lay->GetContext()->GetCommunicator();
   // nothing crosses the wire in chunk k on ANY rank (world 1 with the own rows local): every rank
@@ -797,6 +799,7 @@ static GapPending post_gapped(const TablePtr &lay, const GapPlan &g, int k, cons
     return v;
   };
   for (int c = 0; c < lay->Columns(); ++c) {
+    if (c == skip_col) continue;  // (a proxy's source-row column is used by the sender only)
     const Column &col = lay->column(c);
     const int64_t per = col.type.kind() == ValueKind::FIXED_BYTES ? col.type.width() : 1;
     if (nullable[c])
@@ -849,17 +852,42 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
     consume(0, 1, ts);
     return;
   }
-  bool var = false;
-  for (const TablePtr &t : ts)
-    for (const auto &c : t->columns()) var |= c.is_var();
-  if (var) {  // strings: byte counts per column need their own exchange
-    if (NT == 2) {
-      auto lr = ShufflePair(ts[0], tcols[0], ts[1], tcols[1]);
-      consume(0, 1, {lr.first, lr.second});
-    } else {
-      consume(0, 1, {Shuffle(ts[0], tcols[0])});
+  // Var-width (string / binary) columns: the planned exchange moves a fixed-width PROXY of the table
+  // -- var column c replaced by its int64 lengths (with c's validity), plus a source-row column used
+  // only on the sending side -- and each var column's bytes in a gapped byte layout of its own
+  // (same partition order, receive regions sized by per-partition byte counts that travel in the
+  // one descriptor), posted per chunk like the rows.  Chunk k's var column is its received bytes
+  // with offsets from the chunk's lengths.  Reference: arrow_all_to_all.cpp (lengths + bytes).
+  struct VarSpec {
+    std::vector<int> vcols;  // var-width column indices
+    int rid = -1;            // proxy column of the source row
+    TablePtr orig;
+    at::Tensor pid;          // partition ids of the original rows (W * Kc partitions)
+  };
+  std::vector<VarSpec> vs(NT);
+  std::vector<TablePtr> tsp(ts);  // the tables as exchanged (proxies for var-width tables)
+  int nvar = 0;
+  for (int i = 0; i < NT; ++i) {
+    for (int c = 0; c < ts[i]->Columns(); ++c)
+      if (ts[i]->column(c).is_var()) vs[i].vcols.push_back(c);
+    if (vs[i].vcols.empty()) continue;
+    nvar += (int)vs[i].vcols.size();
+    vs[i].orig = ts[i];
+    Exec ex(ts[i]->device());
+    const int64_t n = ts[i]->Rows();
+    std::vector<Column> pc;
+    for (int c = 0; c < ts[i]->Columns(); ++c) {
+      const Column &col = ts[i]->column(c);
+      if (!col.is_var()) {
+        pc.push_back(col);
+        continue;
+      }
+      at::Tensor lens = col.offsets.slice(0, 1, n + 1) - col.offsets.slice(0, 0, n);
+      pc.emplace_back(col.name, DataType(Type::INT64), n, lens.contiguous(), at::Tensor(), col.validity);
     }
-    return;
+    vs[i].rid = (int)pc.size();
+    pc.emplace_back("__cylon_row", DataType(Type::INT64), n, at::arange(n, ex.opts(at::kLong)));
+    tsp[i] = Table::Make(ts[i]->GetContext(), std::move(pc));
   }
   const int W = ctx->GetWorldSize(), me = ctx->GetRank();
   const std::string v = knobs::ConfigOr(ctx->GetConfig("shuffle_chunks", ""), "SHUFFLE_CHUNKS");
@@ -874,8 +902,8 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
   // ---- the descriptor (assembled on the device: no sync before the all-gather)
   std::vector<at::Tensor> parts;
   std::vector<int64_t> rows, nflags;
-  for (const TablePtr &t : ts) rows.push_back(t->Rows());
-  for (const TablePtr &t : ts)
+  for (const TablePtr &t : tsp) rows.push_back(t->Rows());
+  for (const TablePtr &t : tsp)
     for (const auto &c : t->columns()) nflags.push_back(c.nullable() ? 1 : 0);
   parts.push_back(at::tensor(rows, at::TensorOptions().dtype(at::kLong)).to(dev));
   parts.push_back(at::tensor(nflags, at::TensorOptions().dtype(at::kLong)).to(dev));
@@ -883,10 +911,10 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
   std::vector<std::pair<int, int>> cand;  // (table, column) narrowable on the wire
   if (nv != "0")
     for (int side = 0; side < NT; ++side)
-      for (int c = 0; c < ts[side]->Columns(); ++c)
-        if (narrow_candidate(ts[side]->column(c))) cand.push_back({side, c});
+      for (int c = 0; c < tsp[side]->Columns(); ++c)
+        if (c != vs[side].rid && narrow_candidate(tsp[side]->column(c))) cand.push_back({side, c});
   for (auto &sc : cand) {
-    const Column &c = ts[sc.first]->column(sc.second);
+    const Column &c = tsp[sc.first]->column(sc.second);
     if (c.length == 0) {
       parts.push_back(at::tensor({std::numeric_limits<int64_t>::max(), std::numeric_limits<int64_t>::min()}, lopt));
     } else {
@@ -895,13 +923,28 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
     }
   }
   std::vector<bool> fast(NT);
+  std::vector<at::Tensor> vbytes;  // per var column: bytes per partition
   {
     CYLON_PHASE("shuffle.partition", dev);
     for (int i = 0; i < NT; ++i) {
-      fast[i] = mod_pass_eligible(ts[i], tcols[i], P);
-      parts.push_back(counts_device(ts[i], tcols[i], P, fast[i]));
+      fast[i] = vs[i].vcols.empty() && mod_pass_eligible(ts[i], tcols[i], P);
+      if (vs[i].vcols.empty()) {
+        parts.push_back(counts_device(ts[i], tcols[i], P, fast[i]));
+        continue;
+      }
+      auto pc = hash_pids_counts(ts[i], tcols[i], P);  // the ORIGINAL key columns (a var key hashes its bytes)
+      vs[i].pid = pc.first;
+      parts.push_back(pc.second);
+      const at::Tensor pid64 = pc.first.to(at::kLong);
+      for (int c : vs[i].vcols) {
+        const Column &col = ts[i]->column(c);
+        const int64_t n = ts[i]->Rows();
+        at::Tensor lens = col.offsets.slice(0, 1, n + 1) - col.offsets.slice(0, 0, n);
+        vbytes.push_back(at::zeros({(int64_t)P}, lens.options()).index_add_(0, pid64, lens));
+      }
     }
   }
+  for (auto &b : vbytes) parts.push_back(b);
   at::Tensor desc = at::cat(parts);
   const int64_t D = desc.numel();
   at::Tensor all;
@@ -913,11 +956,12 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
   const int64_t *g = all.data_ptr<int64_t>();  // W x D
   std::vector<int> ncols(NT), coff(NT + 1, 0);
   for (int i = 0; i < NT; ++i) {
-    ncols[i] = ts[i]->Columns();
+    ncols[i] = tsp[i]->Columns();
     coff[i + 1] = coff[i] + ncols[i];
   }
   const int64_t off_null = NT, off_mm = off_null + coff[NT], off_cnt = off_mm + 2 * (int64_t)cand.size();
-  CYLON_CHECK(off_cnt + (int64_t)NT * P == D, Code::ExecutionError, "shuffle descriptor layout");
+  const int64_t off_vb = off_cnt + (int64_t)NT * P;  // then P byte counts per var column
+  CYLON_CHECK(off_vb + (int64_t)nvar * P == D, Code::ExecutionError, "shuffle descriptor layout");
   // own rows through the communicator as well (test knob: keeps the RCCL kernels running at world 1)
   const std::string sw = knobs::ConfigOr(ctx->GetConfig("shuffle_self_rccl", ""), "SHUFFLE_SELF_RCCL");
   const bool self_wire = sw == "1";
@@ -957,6 +1001,14 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
     for (int q = 0; q < Kc; ++q) s += c[(int64_t)q * W + to];
     return s;
   };
+  // bytes of var column v (global index over the tables' var columns) this rank sends / receives
+  auto cntb = [&](int v, int k, int from, int to) -> int64_t {
+    const int64_t *c = g + (int64_t)from * D + off_vb + (int64_t)v * P;
+    if (K == Kc) return c[(int64_t)k * W + to];
+    int64_t s = 0;
+    for (int q = 0; q < Kc; ++q) s += c[(int64_t)q * W + to];
+    return s;
+  };
   const uint32_t PK = (uint32_t)W * (uint32_t)K;
   if (PK == 1 && !self_wire) {  // world 1, one chunk: every row is already where it is consumed
     trace::add_counter("shuffle.self_rows_kept_local", ts[0]->Rows() + (NT > 1 ? ts[1]->Rows() : 0));
@@ -967,12 +1019,28 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
   std::vector<GapPlan> gp;
   for (int i = 0; i < NT; ++i)
     gp.push_back(gap_plan(W, K, me, self_wire, [&](int k, int from, int to) { return cnt(i, k, from, to); }, PK));
+  // per var column: its gapped byte layout (plan in bytes) and the byte buffer
+  std::vector<GapPlan> gpb;
+  std::vector<at::Tensor> vbuf;
+  std::vector<int> vfirst(NT, 0);  // first global var index of table i
+  for (int i = 0, v = 0; i < NT; ++i) {
+    vfirst[i] = v;
+    for (size_t j = 0; j < vs[i].vcols.size(); ++j, ++v)
+      gpb.push_back(gap_plan(W, K, me, self_wire, [&, v](int k, int from, int to) { return cntb(v, k, from, to); }, PK));
+  }
+  vbuf.resize(gpb.size());
   std::vector<TablePtr> lay(NT);
   std::vector<std::vector<GapPending>> pend(NT, std::vector<GapPending>(K));
   std::vector<std::vector<at::Tensor>> wire(NT);  // per column: narrowed send buffer (or undefined)
   auto post = [&](int side, int k) {
     const std::vector<int64_t> flags(nullable.begin() + coff[side], nullable.begin() + coff[side + 1]);
-    pend[side][k] = post_gapped(lay[side], gp[side], k, plans[side], wire[side], flags);
+    pend[side][k] = post_gapped(lay[side], gp[side], k, plans[side], wire[side], flags, vs[side].rid);
+    for (size_t j = 0; j < vs[side].vcols.size(); ++j) {  // the var columns' bytes of chunk k
+      const int v = vfirst[side] + (int)j;
+      if (gpb[v].wire_rows[k] == 0) continue;  // (agreed on every rank)
+      pend[side][k].reqs.push_back(ctx->GetCommunicator()->AllToAllVSegmentsAsync(
+          vbuf[v], gpb[v].send_off[k], gpb[v].send_cnt[k], vbuf[v], gpb[v].recv_off[k], gpb[v].recv_cnt[k]));
+    }
   };
   int nfast = 0;
   {
@@ -980,11 +1048,41 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
     for (int i = 0; i < NT; ++i) {  // table i's first chunk transfers while table i+1 is reordered
       const std::vector<int64_t> flags(nullable.begin() + coff[i], nullable.begin() + coff[i + 1]);
       bool fastpath = false;
-      lay[i] = layout_reorder(ts[i], tcols[i], PK, gp[i], flags, K == Kc ? fast[i] : mod_pass_eligible(ts[i], tcols[i], PK),
-                              &fastpath);
+      const bool var_t = !vs[i].vcols.empty();
+      lay[i] = layout_reorder(tsp[i], tcols[i], PK, gp[i], flags,
+                              !var_t && (K == Kc ? fast[i] : mod_pass_eligible(ts[i], tcols[i], PK)), &fastpath,
+                              var_t ? (K == Kc ? vs[i].pid : hash_pids(ts[i], tcols[i], PK)) : at::Tensor());
       nfast += fastpath ? 1 : 0;
-      wire[i].assign(ts[i]->Columns(), at::Tensor());
-      for (int c = 0; c < ts[i]->Columns(); ++c)
+      if (var_t) {  // each var column's bytes, gathered in the layout's bucket order into its byte layout
+        Exec ex(dev);
+        std::vector<at::Tensor> idxs;
+        const at::Tensor &rid = lay[i]->column(vs[i].rid).data;
+        for (int k = 0; k < K; ++k)
+          for (int r = 0; r < W; ++r)
+            if (const int64_t nr = cnt(i, k, me, r)) {
+              const int64_t b0 = gp[i].bucket_base[(size_t)k * W + r];
+              idxs.push_back(rid.slice(0, b0, b0 + nr));
+            }
+        const at::Tensor idx = idxs.empty() ? ex.empty_i64(0) : at::cat(idxs);
+        for (size_t j = 0; j < vs[i].vcols.size(); ++j) {
+          const int v = vfirst[i] + (int)j;
+          const Column &vc = vs[i].orig->column(vs[i].vcols[j]);
+          const TablePtr gt = Gather(Table::Make(ctx, {Column(vc.name, vc.type, vc.length, vc.data, vc.offsets)}), idx);
+          const at::Tensor &gb = gt->column(0).data;
+          vbuf[v] = at::empty({std::max<int64_t>(gpb[v].total, 1)}, ex.opts(at::kByte));
+          int64_t cur = 0;
+          for (int k = 0; k < K; ++k)
+            for (int r = 0; r < W; ++r)
+              if (const int64_t nb = cntb(v, k, me, r)) {
+                const int64_t b0 = gpb[v].bucket_base[(size_t)k * W + r];
+                vbuf[v].slice(0, b0, b0 + nb).copy_(gb.slice(0, cur, cur + nb));
+                cur += nb;
+              }
+        }
+        trace::add_counter("shuffle.var_columns_planned", (int64_t)vs[i].vcols.size());
+      }
+      wire[i].assign(tsp[i]->Columns(), at::Tensor());
+      for (int c = 0; c < tsp[i]->Columns(); ++c)
         if (plans[i].narrow[c]) {  // narrowed copies of the rows that are sent (not the own rows)
           const Column &col = lay[i]->column(c);
           Exec ex(dev);
@@ -1024,6 +1122,23 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
     for (int i = 0; i < NT; ++i) {
       pend[i][k] = GapPending();
       rows_out += got[i]->Rows();
+      if (vs[i].vcols.empty()) continue;
+      // back to the original schema: lengths -> offsets over the chunk's bytes, source rows dropped
+      Exec ex(dev);
+      std::vector<Column> oc;
+      for (int c = 0, j = 0; c < vs[i].orig->Columns(); ++c) {
+        const Column &pcol = got[i]->column(c);
+        if (j < (int)vs[i].vcols.size() && vs[i].vcols[j] == c) {
+          const GapPlan &gb = gpb[vfirst[i] + j];
+          at::Tensor offs = exclusive_scan(ex, pcol.data.contiguous());
+          at::Tensor bytes = vbuf[vfirst[i] + j].slice(0, gb.in_off[k], gb.in_off[k] + gb.in_rows[k]);
+          oc.emplace_back(pcol.name, vs[i].orig->column(c).type, pcol.length, bytes, offs, pcol.validity);
+          ++j;
+        } else {
+          oc.push_back(pcol);
+        }
+      }
+      got[i] = Table::Make(ctx, std::move(oc));
     }
     trace::add_counter("shuffle.rows_out", rows_out);
     consume(k, K, got);

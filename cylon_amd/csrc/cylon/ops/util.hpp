@@ -68,7 +68,8 @@ struct RangeSpec {
 // to the result and *keep_packed lists the packed column indices in byte order.
 std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> cols, const std::vector<int> &widths,
                                        int bits, at::Tensor *offs, const RangeSpec *range = nullptr,
-                                       std::vector<int> *keep_packed = nullptr, bool stable = true);
+                                       std::vector<int> *keep_packed = nullptr, bool stable = true,
+                                       const hip::NarrowKeys *nk = nullptr);
 
 // Hash-join partition in slot mode (MSD, two passes, no histogram before the second pass; see
 // kernel_decls.inc radix_slot_rows_pass): partition p holds (*counts)[p] rows at row p * slot.
@@ -78,7 +79,8 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
 std::vector<at::Tensor> RadixPartitionSlotted(const Exec &ex, std::vector<at::Tensor> cols,
                                               const std::vector<int> &widths, int bits, int64_t slot,
                                               at::Tensor *counts, at::Tensor *overflow,
-                                              std::vector<int> *keep_packed = nullptr);
+                                              std::vector<int> *keep_packed = nullptr,
+                                              const hip::NarrowKeys *nk = nullptr);
 
 // Row-moving passes (k_rows_pass) take their all-8-byte path only when every moved
 // column is 8 bytes wide; validity bytes beside 8-byte columns therefore travel packed

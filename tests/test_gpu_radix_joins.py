@@ -212,6 +212,9 @@ def test_radix_join_slot_overflow_repartitions_exactly(gpu_ctx, ctx, monkeypatch
 
 # ---- LDS radix group-by (kernels/radix_groupby.hip) beyond one integer key + SUM/COUNT/MIN/MAX/MEAN
 def _groupby_both(T, keys, aggs, monkeypatch):
+    """[radix path, GPU global-table path] results and counters; both are also checked against the
+    CPU twin of the group-by (kernels/cpu_groupby.cpp, an independent implementation), so an
+    encoding bug shared by the two GPU paths (composite key, float canonical bits, null code) fails."""
     res, counters = [], []
     for thr in ("1", str(1 << 62)):  # radix path, then the global-table path
         monkeypatch.setenv("CYLON_RADIX_GROUPBY_MIN_ROWS", thr)
@@ -221,6 +224,9 @@ def _groupby_both(T, keys, aggs, monkeypatch):
         counters.append(dict(C.trace_counters()))
         C.trace_enable(False)
         res.append(df.sort_values(keys).reset_index(drop=True))
+    cpu = T.to_cpu().local_groupby(keys, aggs).to_pandas().sort_values(keys).reset_index(drop=True)
+    assert list(cpu.columns) == list(res[0].columns)
+    pd.testing.assert_frame_equal(res[0], cpu, check_exact=False, rtol=1e-8, atol=1e-8, check_dtype=False)
     return res, counters
 
 
@@ -328,5 +334,55 @@ def test_radix_join_forced_small_build_chunks(gpu_ctx, ctx, monkeypatch, how):
     monkeypatch.setenv("CYLON_RJ_SPLIT_ROWS", "64")
     got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["k"], monkeypatch)
     assert c.get("join.radix.split_items", 0) > 100, c
+    assert c["join.radix.rows_out"] == len(exp)
+    pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
+
+
+@pytest.mark.parametrize("case", ["narrow_far_from_zero", "wide_fallback", "uint64_top"])
+@pytest.mark.parametrize("how", ["inner", "outer"])
+def test_radix_join_narrowed_keys(gpu_ctx, ctx, monkeypatch, case, how):
+    """Narrowed partition keys (kernel_decls.inc NarrowKeys): keys within 2^31 of the left table's
+    first key travel as uint32 offsets (also far from zero, and for uint64 keys near 2^64); keys
+    spanning more than 2^32 are detected by the first pass and joined as int64 keys."""
+    rng = np.random.default_rng(47)
+    n = 1_500_000
+    if case == "narrow_far_from_zero":
+        lo, span, typ = -(1 << 62), 1 << 30, pa.int64()
+    elif case == "wide_fallback":
+        lo, span, typ = -(1 << 40), 1 << 41, pa.int64()
+    else:
+        lo, span, typ = (1 << 63) + (1 << 62), 1 << 29, pa.uint64()
+    ka = rng.integers(0, span // 2, n).astype(np.uint64) * 2 + np.uint64(lo % (1 << 64))
+    kb = rng.integers(0, span // 2, n).astype(np.uint64) * 2 + np.uint64(lo % (1 << 64))
+    kb[: n // 3] = ka[rng.integers(0, n, n // 3)]  # plenty of matches
+    if typ == pa.int64():
+        ka, kb = ka.view(np.int64), kb.view(np.int64)
+    a = pa.table({"k": pa.array(ka, typ), "v": rng.random(n)})
+    b = pa.table({"k": pa.array(kb, typ), "w": rng.random(n)})
+    got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["k"], monkeypatch)
+    if case == "wide_fallback":
+        assert c.get("join.radix.narrow_fallback", 0) == 1, c
+    elif case == "narrow_far_from_zero":
+        assert c.get("join.radix.narrow_keys", 0) == 1 and c.get("join.radix.narrow_fallback", 0) == 0, c
+    # (uint64 keys join through their 64-bit image, which is not the column itself: not narrowed)
+    assert c["join.radix.rows_out"] == len(exp)
+    pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
+
+
+@pytest.mark.parametrize("how", ["inner", "left", "outer"])
+@pytest.mark.parametrize("keys", [["s"], ["s", "k"]])
+def test_radix_join_string_keys(gpu_ctx, ctx, monkeypatch, how, keys):
+    """String keys on the LDS radix path: the row hash of the key columns is partitioned and matched
+    in LDS, the key bytes are gathered by row number and every output row's keys are compared with
+    rows_equal (a 64-bit collision would fall back).  Against the CPU twin."""
+    rng = np.random.default_rng(53)
+    n = 1_200_000
+    ids_a = rng.integers(0, 900_000, n)
+    ids_b = rng.integers(0, 900_000, n)
+    a = pa.table({"s": pa.array([f"key-{x:09d}" for x in ids_a]), "k": ids_a % 7, "v": rng.random(n)})
+    b = pa.table({"s": pa.array([f"key-{x:09d}" for x in ids_b]), "k": ids_b % 7, "w": rng.random(n)})
+    got, exp, c = _join(gpu_ctx, ctx, a, b, how, keys, monkeypatch)
+    assert c.get("join.radix.var_key", 0) >= 1 and c.get("join.radix.hashed_key", 0) == 1, c
+    assert c.get("join.radix.hash_collision_fallback", 0) == 0, c
     assert c["join.radix.rows_out"] == len(exp)
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)

@@ -349,3 +349,52 @@ def test_idle_rank_still_posts_collectives(chunks):
     gb = pd.concat([r[0]["gb"] for r in res]).sort_values("k")
     assert gb["k"].tolist() == sorted(set(A["k"]))
     assert all(r[3].get("shuffle.plan_collectives", 0) >= 1 for r in res)
+
+
+def _string_join_chunks(ctx, chunks, n):
+    """String key + string payload through the planned, chunked exchange (var columns as lengths in
+    the gapped row layout and bytes in their own gapped byte layouts)."""
+    from cylon_amd import Table
+    from cylon_amd._lib import C
+    rank = ctx.get_rank()
+    rng = np.random.default_rng(70 + rank)
+    ka, kb = rng.integers(0, n, n), rng.integers(0, n, n)
+    a = pd.DataFrame({"s": [f"id{x:07d}" for x in ka], "x": rng.integers(-9, 9, n),
+                      "p": [("p" * int(x % 5)) + str(x) for x in ka]})
+    b = pd.DataFrame({"s": [f"id{x:07d}" for x in kb], "v": rng.random(n)})
+    ta, tb = Table.from_pandas(ctx, a), Table.from_pandas(ctx, b)
+    ctx.add_config("shuffle_chunks", str(chunks))
+    C.trace_enable(True)
+    C.trace_reset()
+    out = {"join": ta.distributed_join(tb, "inner", "hash", on=["s"], left_prefix="l_", right_prefix="r_"),
+           "left": ta.distributed_join(tb, "left", "hash", on=["s"], left_prefix="l_", right_prefix="r_"),
+           "union": ta[["s"]].distributed_union(tb[["s"]])}
+    counters = dict(C.trace_counters())
+    C.trace_enable(False)
+    return {k: v.to_pandas() for k, v in out.items()}, a, b, counters
+
+
+def _check_string_join(res, chunks):
+    A = pd.concat([r[1] for r in res]).reset_index(drop=True)
+    B = pd.concat([r[2] for r in res]).reset_index(drop=True)
+    la, rb = A.add_prefix("l_"), B.add_prefix("r_")
+    for how in ("join", "left"):
+        got = pd.concat([r[0][how] for r in res])
+        exp = la.merge(rb, left_on="l_s", right_on="r_s", how="inner" if how == "join" else "left")
+        cols = sorted(got.columns)
+        key = lambda df: sorted(map(lambda t: tuple("~nan" if (x is None or (isinstance(x, float) and x != x)) else x
+                                                    for x in t), df[cols].itertuples(index=False)), key=str)
+        assert len(got) == len(exp) and key(got) == key(exp), how
+    un = sorted(pd.concat([r[0]["union"] for r in res])["s"].tolist())
+    assert un == sorted(set(A["s"]) | set(B["s"]))
+    for r in res:
+        assert r[3].get("shuffle.var_columns_planned", 0) > 0, r[3]
+        assert r[3].get("shuffle.chunks", 0) == 3 * chunks, r[3]  # three operators, each chunked
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 3), (3, 2)])
+def test_planned_shuffle_var_width_chunked(world, chunks):
+    """Tables with string columns take the planned, chunked exchange (not the unplanned ShufflePair):
+    a string-key join, a LEFT join and a union, against pandas on the gathered inputs."""
+    res = run_distributed(_string_join_chunks, world, chunks, 3_000, timeout=200.0)
+    _check_string_join(res, chunks)

@@ -1,0 +1,91 @@
+"""String-key join on the LDS radix path vs the int64-key join of the same shape (VERDICT r04 "do
+this" 5): N x N rows, 16-byte string keys ("k" + 15 decimal digits of an int key uniform in
+[0, 0.99 N)) + 3 float64 payload columns, all generated in HBM.
+
+usage: python tools/string_join_probe.py <rows per side> [reps]
+Prints one JSON line per key type: median ms, output rows, join.* counters, and (string run) the
+output's key-equality / row-count check against the int64 run."""
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from cylon_amd import CylonContext, Table  # noqa: E402
+from cylon_amd._lib import C  # noqa: E402
+from cylon_amd.types import DataType, Type  # noqa: E402
+
+
+def string_column(name, ints):
+    """16-byte ASCII keys 'k' + 15 zero-padded digits of ints (device)."""
+    n = ints.numel()
+    digits = torch.empty((n, 15), dtype=torch.uint8, device=ints.device)
+    x = ints.clone()
+    for d in range(14, -1, -1):
+        digits[:, d] = (x % 10 + 48).to(torch.uint8)
+        x //= 10
+    b = torch.cat([torch.full((n, 1), ord("k"), dtype=torch.uint8, device=ints.device), digits], 1).reshape(-1)
+    offs = torch.arange(0, 16 * n + 1, 16, dtype=torch.int64, device=ints.device)
+    return C.Column(name, DataType(Type.STRING), n, b, offs)
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 200_000_000
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    ctx = CylonContext(device="cuda:0")
+    kr = int(0.99 * n)
+    res = {}
+    for kind in ("int64", "string"):
+        torch.cuda.empty_cache()
+        g = torch.Generator(device="cuda").manual_seed(0)  # the same keys for both runs
+        sides = []
+        for _ in range(2):
+            k = torch.randint(0, kr, (n,), generator=g, device="cuda")
+            vals = {f"v{i}": torch.rand(n, generator=g, device="cuda", dtype=torch.float64) for i in range(3)}
+            t = Table.from_torch(ctx, {"k": k, **vals})
+            if kind == "string":
+                cols = [string_column("k", k)] + [c for c in t.native.columns()[1:]]
+                t = Table(context=ctx, _native=C.Table(ctx._ctx, cols))
+            del k
+            sides.append(t)
+        L, R = sides
+
+        def run():
+            return L.join(R, "inner", "hash", on=["k"], left_prefix="l_", right_prefix="r_")
+
+        out = run()
+        rows = out.row_count
+        del out
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = run()
+            torch.cuda.synchronize()
+            ts.append(1000 * (time.perf_counter() - t0))
+            del out
+        C.trace_enable(True)
+        C.trace_reset()
+        out = run()
+        torch.cuda.synchronize()
+        cnt = {k: v for k, v in dict(C.trace_counters()).items() if k.startswith("join.")}
+        C.trace_enable(False)
+        rec = {"key": kind, "rows_per_side": n, "ms": round(statistics.median(ts), 3),
+               "all_ms": [round(x, 2) for x in ts], "out_rows": rows, "counters": cnt}
+        if kind == "string":  # the key bytes of both sides are equal row by row (also checked by the join)
+            lk, rk = out.native.columns()[0], out.native.columns()[4]
+            rec["key_bytes_equal"] = bool(torch.equal(lk.data, rk.data) and torch.equal(lk.offsets, rk.offsets))
+            rec["rows_equal_int64_run"] = rows == res["int64"]["out_rows"]
+        del out, L, R, sides
+        res[kind] = rec
+        print(json.dumps(rec), flush=True)
+    print(json.dumps({"string_over_int64": round(res["string"]["ms"] / res["int64"]["ms"], 3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
