@@ -3,6 +3,7 @@
 // ctx/cylon_context.cpp:25-108.
 #include "cylon/knobs.hpp"
 #include <c10/hip/HIPCachingAllocator.h>
+#include <hip/hip_runtime_api.h>
 #include <c10/hip/HIPGuard.h>
 
 #include <cstdlib>
@@ -281,6 +282,18 @@ std::shared_ptr<MemoryPool> CylonContext::GetMemoryPool() {
   std::lock_guard<std::mutex> lk(mu_);
   if (!pool_ || pool_->device() != device_) pool_ = DefaultMemoryPool(device_);
   return pool_;
+}
+
+int64_t CylonContext::DeviceHeadroom() const {
+  if (!device_.is_cuda()) return 0;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+  auto stats = c10::hip::HIPCachingAllocator::getDeviceStats(device_.index());
+  const size_t agg = static_cast<size_t>(c10::CachingAllocator::StatType::AGGREGATE);
+  int64_t h = (int64_t)free_b + stats.reserved_bytes[agg].current - stats.allocated_bytes[agg].current;
+  const std::string cap = GetConfig("memory_budget_mb", "");
+  if (!cap.empty()) h = std::min<int64_t>(h, std::atoll(cap.c_str()) << 20);
+  return h;
 }
 
 int64_t CylonContext::MaxMemory() const {

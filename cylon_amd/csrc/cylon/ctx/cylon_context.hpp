@@ -61,6 +61,9 @@ class CylonContext {
 
   // HBM pool statistics (bytes) from the HIP caching allocator; 0 on CPU.
   int64_t BytesAllocated() const;
+  // bytes the device can still hand out: free HBM + the caching allocator's cached, unused blocks
+  // (config "memory_budget_mb" caps it; 0 on the CPU = unbounded)
+  int64_t DeviceHeadroom() const;
   int64_t MaxMemory() const;
 
   // C2: the context's memory pool (default: DeviceMemoryPool / HostMemoryPool

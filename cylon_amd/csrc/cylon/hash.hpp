@@ -36,6 +36,23 @@ CYLON_HD uint64_t fmix64(uint64_t k) {
   return k;
 }
 
+// 64-bit hash of a byte string (join / set-op keys of string, binary and fixed-size binary columns):
+// a chain of fmix64 bijections over the little-endian 8-byte words, seeded with the length.  Two
+// 32-bit murmur3 hashes with different seeds (round 4) are correlated on short keys: a 200M x 200M
+// join on 16-byte keys saw 3 false matches, ~2^11 more than 64 independent bits give.
+CYLON_HD uint64_t bytes_hash64(const uint8_t *p, int64_t len) {
+  uint64_t h = 0x9E3779B97F4A7C15ULL ^ (uint64_t)len;
+  int64_t i = 0;
+  for (; i + 8 <= len; i += 8) {
+    uint64_t w = 0;
+    for (int b = 0; b < 8; ++b) w |= (uint64_t)p[i + b] << (8 * b);
+    h = fmix64(h ^ w) + 0x632BE59BD9B4E019ULL;
+  }
+  uint64_t w = 0;
+  for (int b = 0; i + b < len; ++b) w |= (uint64_t)p[i + b] << (8 * b);
+  return fmix64(h ^ w ^ ((uint64_t)len << 56));
+}
+
 CYLON_HD uint32_t murmur_mix_k1(uint32_t k1) {
   k1 *= 0xcc9e2d51u;
   k1 = rotl32(k1, 15);

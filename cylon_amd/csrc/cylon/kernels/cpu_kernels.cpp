@@ -71,14 +71,10 @@ inline uint64_t value_hash64(const ColView &c, int64_t i) {
   if (c.valid != nullptr && c.valid[i] == 0) return 0x5bd1e9955bd1e995ULL;
   if (c.kind == static_cast<int>(ValueKind::VAR_BYTES)) {
     const int64_t b = c.offsets[i], e = c.offsets[i + 1];
-    const uint32_t h1 = hashing::murmur3_32(c.data + b, e - b, 0u);
-    const uint32_t h2 = hashing::murmur3_32(c.data + b, e - b, 0x9747b28cu);
-    return ((uint64_t)h1 << 32) ^ h2 ^ (uint64_t)(e - b);
+    return hashing::bytes_hash64(c.data + b, e - b);
   }
   if (c.kind == static_cast<int>(ValueKind::FIXED_BYTES)) {
-    const uint32_t h1 = hashing::murmur3_32(c.data + i * (int64_t)c.width, c.width, 0u);
-    const uint32_t h2 = hashing::murmur3_32(c.data + i * (int64_t)c.width, c.width, 0x9747b28cu);
-    return ((uint64_t)h1 << 32) ^ h2;
+    return hashing::bytes_hash64(c.data + i * (int64_t)c.width, c.width);
   }
   return hashing::fmix64((uint64_t)extend_bits(load_bits(c.data, i, c.width), c.width, c.kind));
 }
@@ -247,7 +243,7 @@ void gather_var_lengths(const ColView &in, const int64_t *idx, int64_t m, int64_
   }
 }
 
-void gather_var_bytes(const ColView &in, const int64_t *idx, int64_t m, const int64_t *out_off,
+void gather_var_bytes(const ColView &in, const int64_t *idx, int64_t m, const int64_t *out_off, int64_t,
                       uint8_t *out_bytes, uint8_t *out_valid, void *) {
   for (int64_t j = 0; j < m; ++j) {
     const int64_t s = idx[j];

@@ -601,8 +601,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
     // instance that also carries the slot bookkeeping (the trick of the lean kernel)
     // (SLOT could pack them as digit << 16 | offset and complete them from running[] at each store --
     // 8 fewer VGPRs -- but the dependent LDS read per store measured slower: r04m, 17.3 vs 14.3 ms)
+    // SLOT: destinations as uint32 rows (slot layouts stay below 2^32 rows, radix_slot_eligible):
+    // 8 fewer VGPRs in a kernel that runs at the 128-VGPR limit
     constexpr bool PACKDST = false;
-    using DstT = typename std::conditional<SLOT && PACKDST, uint32_t, int64_t>::type;
+    using DstT = typename std::conditional<SLOT, uint32_t, int64_t>::type;
     DstT dst[kRPItems];
 #define RP_DEST(q) \
   ((SLOT && PACKDST) ? running[(uint32_t)dst[q] >> 16] + (int64_t)((uint32_t)dst[q] & 0xffffu) : (int64_t)dst[q])
@@ -612,7 +614,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
       if (j < cnt) {
         const uint32_t e = sdig[j], p = e >> 16;
         if constexpr (SLOT && PACKDST) dst[q] = (p << 16) | (uint32_t)(j - (int)toff[p]);
-        else dst[q] = running[p] + (j - (int64_t)toff[p]);
+        else dst[q] = (DstT)(running[p] + (j - (int64_t)toff[p]));
         if (cols.check_order && j > 0) {  // same bucket as the previous slot: input order kept?
           const uint32_t f = sdig[j - 1];
           order_bad |= (f >> 16) == p && f > e;

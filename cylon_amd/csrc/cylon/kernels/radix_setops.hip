@@ -52,14 +52,10 @@ __device__ __forceinline__ uint64_t so_value_hash(const ColView &c, int64_t i) {
   if (c.valid != nullptr && c.valid[i] == 0) return 0x5bd1e9955bd1e995ULL;
   if (c.kind == static_cast<int>(ValueKind::VAR_BYTES)) {
     const int64_t b = c.offsets[i], e = c.offsets[i + 1];
-    const uint32_t h1 = hashing::murmur3_32(c.data + b, e - b, 0u);
-    const uint32_t h2 = hashing::murmur3_32(c.data + b, e - b, 0x9747b28cu);
-    return ((uint64_t)h1 << 32) ^ h2 ^ (uint64_t)(e - b);
+    return hashing::bytes_hash64(c.data + b, e - b);
   }
   if (c.kind == static_cast<int>(ValueKind::FIXED_BYTES)) {
-    const uint32_t h1 = hashing::murmur3_32(c.data + i * (int64_t)c.width, c.width, 0u);
-    const uint32_t h2 = hashing::murmur3_32(c.data + i * (int64_t)c.width, c.width, 0x9747b28cu);
-    return ((uint64_t)h1 << 32) ^ h2;
+    return hashing::bytes_hash64(c.data + i * (int64_t)c.width, c.width);
   }
   uint64_t bits = (uint64_t)extend_bits(load_bits(c.data, i, c.width), c.width, c.kind);
   if (c.kind == static_cast<int>(ValueKind::FLOAT)) {

@@ -44,14 +44,17 @@ __device__ __forceinline__ int64_t block_exclusive_scan(int64_t v, int64_t *lds_
   return wave_off + inc - v;
 }
 
+// Tile loads are wave-coalesced: element base + k * kBlock + t (the sum does not care about order);
+// the scan stages its tile through LDS (one pad element per 16, so the per-thread runs of 16 read
+// back without bank conflicts) and scans 16 consecutive elements per thread.
 __global__ __launch_bounds__(kBlock) void k_block_sums(const int64_t *__restrict__ in, int64_t n,
                                                        int64_t *__restrict__ sums) {
   __shared__ int64_t lds[kBlock / kWave];
-  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + threadIdx.x;
   int64_t s = 0;
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
-    const int64_t i = base + k;
+    const int64_t i = base + (int64_t)k * kBlock;
     if (i < n) s += in[i];
   }
   int64_t tot;
@@ -59,28 +62,42 @@ __global__ __launch_bounds__(kBlock) void k_block_sums(const int64_t *__restrict
   if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
 
+__device__ __forceinline__ int scan_pad(int i) { return i + (i >> 4); }
+
 __global__ __launch_bounds__(kBlock) void k_block_scan(const int64_t *__restrict__ in, int64_t n,
                                                        const int64_t *__restrict__ offs,
                                                        int64_t *__restrict__ out) {
   __shared__ int64_t lds[kBlock / kWave];
-  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  __shared__ int64_t tile[kScanTile + kScanTile / 16];
+  const int64_t t0 = (int64_t)blockIdx.x * kScanTile;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int e = k * kBlock + threadIdx.x;
+    tile[scan_pad(e)] = (t0 + e < n) ? in[t0 + e] : 0;
+  }
+  __syncthreads();
   int64_t v[kScanItems];
   int64_t s = 0;
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
-    const int64_t i = base + k;
-    v[k] = (i < n) ? in[i] : 0;
+    v[k] = tile[scan_pad(threadIdx.x * kScanItems + k)];
     s += v[k];
   }
   int64_t tot;
   int64_t run = block_exclusive_scan(s, lds, &tot) + (offs ? offs[blockIdx.x] : 0);
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
-    const int64_t i = base + k;
-    if (i < n) out[i] = run;
+    tile[scan_pad(threadIdx.x * kScanItems + k)] = run;
     run += v[k];
   }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int e = k * kBlock + threadIdx.x;
+    if (t0 + e < n) out[t0 + e] = tile[scan_pad(e)];
+  }
   // out[n] = grand total, written by the thread owning element n-1
+  const int64_t base = t0 + (int64_t)threadIdx.x * kScanItems;
   if (n > 0 && base <= n - 1 && n - 1 < base + kScanItems) out[n] = run;
 }
 

@@ -469,6 +469,12 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   while (bits < 24 && !fits((nb + (int64_t(1) << bits) - 1) >> bits)) ++bits;
   if (const int64_t xb = knobs::Int("RJ_EXTRA_BITS", 0))  // test knob: finer partitions
     bits = std::min(bits + (int)std::max<int64_t>(0, xb), 2 * 10);
+  if (narrow && bits == 0) {  // one partition: no pass runs, so nothing would narrow the keys
+    narrow = false;
+    nk = hip::NarrowKeys();
+    cap = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size(), (oj & 2) != 0, 8);
+    while (bits < 24 && !fits((nb + (int64_t(1) << bits) - 1) >> bits)) ++bits;
+  }
   const int64_t nparts = int64_t(1) << bits;
   // Slot mode for two-pass partitions (>= 11 bits): the second pass claims fixed-size partition
   // slots (mean + 8 sigma + 64 rows) instead of reading the keys once more for exact offsets
@@ -1156,14 +1162,15 @@ static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr
   return k;
 }
 
-// rows of a hashed-key radix join whose key columns differ (64-bit hash collisions); both sides
-// present rows only (outer rows carry one null side).  Row-wise equality of every key type
-// (strings / binary byte-wise) by the rows_equal kernel.
-static int64_t key_mismatches(const TablePtr &out, const JoinConfig &cfg, int nleft) {
+// Rows of a hashed-key radix join whose key columns differ (64-bit key-hash collisions), as a bool
+// mask, or an undefined tensor when there are none.  Rows where both sides are present only (outer
+// rows carry one null side); row-wise equality of every key type (strings / binary byte-wise) by
+// the rows_equal kernel.
+static at::Tensor key_mismatches(const TablePtr &out, const JoinConfig &cfg, int nleft) {
   const auto &lc = cfg.GetLeftColumnIdx();
   const auto &rc = cfg.GetRightColumnIdx();
   const int64_t m = out->Rows();
-  if (m == 0) return 0;
+  if (m == 0) return at::Tensor();
   Exec ex(out->device());
   std::vector<int> lcols(lc.begin(), lc.end()), rcols;
   for (int c : rc) rcols.push_back(nleft + c);
@@ -1178,7 +1185,96 @@ static int64_t key_mismatches(const TablePtr &out, const JoinConfig &cfg, int nl
     if (a.nullable()) bad.logical_and_(a.validity.slice(0, 0, m));
     if (b.nullable()) bad.logical_and_(b.validity.slice(0, 0, m));
   }
-  return bad.sum().item<int64_t>();
+  return bad.any().item<bool>() ? bad : at::Tensor();
+}
+
+// A collision pairs rows whose keys differ: an inner join drops those rows; any other join type
+// redoes the join on the exact path (nullptr), since a falsely matched row may owe an unmatched one.
+static TablePtr drop_false_matches(const TablePtr &out, const JoinConfig &cfg, int nleft) {
+  at::Tensor bad = key_mismatches(out, cfg, nleft);
+  if (!bad.defined()) return out;
+  const int64_t n = bad.sum().item<int64_t>();
+  if (cfg.GetType() != JoinType::INNER) {
+    trace::add_counter("join.radix.hash_collision_fallback", n);
+    return nullptr;
+  }
+  trace::add_counter("join.radix.hash_collision_dropped", n);
+  return FilterByMask(out, bad.logical_not());
+}
+
+// ---------------------------------------------------------------------------
+// Bounded memory.  radix_join's working set -- both sides' partitioned copies (the
+// second pass's slots) plus the first pass's transient copy of one side -- and its output are sized
+// against the device headroom (free HBM + the caching allocator's cached blocks; config
+// "memory_budget_mb" caps it).  When they do not fit, the join runs in C key-hash chunks: rows whose
+// multiplicative key hash falls in chunk c are gathered from both sides, partitioned and joined into
+// ONE output sink allocated for the whole result, so the peak is inputs + output + ~1/C of the
+// working set (plus the chunk copies) instead of inputs + output + the whole working set.  The
+// output size is estimated from an exactly joined 1/1024 key-hash sample when it matters.
+// Reference: the retain=false release of shuffled inputs, table.cpp:150-155.
+// ---------------------------------------------------------------------------
+static int64_t radix_row_bytes(const TablePtr &t) {
+  int64_t b = 0;
+  for (const auto &c : t->columns()) b += c.type.width() + (c.nullable() ? 1 : 0);
+  return std::max<int64_t>(b, 8);
+}
+
+static at::Tensor key_chunk_ids(const at::Tensor &k, int64_t C) {  // independent of fmix64 / fmix32 bits
+  at::Tensor h = k * (int64_t)0x9E3779B97F4A7C15ull;
+  return at::bitwise_and(at::bitwise_right_shift(h, 32), 0x7fffffff).remainder(C);
+}
+
+static int radix_join_chunks(const Exec &ex, const TablePtr &l, const TablePtr &r, const at::Tensor &lk,
+                             const at::Tensor &rk) {
+  if (!ex.gpu) return 1;
+  const int64_t head = l->GetContext()->DeviceHeadroom();
+  if (head <= 0) return 1;
+  const int64_t nl = l->Rows(), nr = r->Rows();
+  const int64_t bl = radix_row_bytes(l) * nl, br = radix_row_bytes(r) * nr;
+  const int64_t work = (int64_t)(1.17 * (double)(bl + br)) + (int64_t)(1.03 * (double)std::max(bl, br));
+  const int64_t out_row = radix_row_bytes(l) + radix_row_bytes(r);
+  const double budget = 0.92 * (double)head;
+  // one output row per row of the larger side, with room to spare: no estimate needed
+  if ((double)work + 1.5 * (double)(std::max(nl, nr) * out_row) <= budget) return 1;
+  int64_t est = 0;
+  {  // exact join of a 1/1024 hash sample of both key sets, scaled up
+    at::Tensor sl = at::bitwise_and(at::bitwise_right_shift(lk * (int64_t)0x632BE59BD9B4E019ll, 40), 1023).eq(0);
+    at::Tensor sr = at::bitwise_and(at::bitwise_right_shift(rk * (int64_t)0x632BE59BD9B4E019ll, 40), 1023).eq(0);
+    auto pr = hash_join_pairs(ex, lk.masked_select(sl), rk.masked_select(sr));
+    est = (int64_t)(1.1 * 1024.0 * (double)pr.first.numel()) + 65536;
+  }
+  const double out_bytes = (double)est * (double)out_row;
+  if ((double)work + out_bytes <= budget) return 1;
+  const double room = budget - out_bytes;
+  const int C = room <= 0 ? 64 : (int)std::min<double>(64.0, std::ceil((double)(work + bl + br) / room));
+  trace::add_counter("join.radix.memory_chunks", C);
+  trace::add_counter("join.radix.estimated_output_rows", est);
+  return std::max(C, 2);
+}
+
+// the radix join in C key-hash chunks into one sink (see above); nullptr if a chunk's radix join fails
+static TablePtr radix_join_chunked(const Exec &ex, const TablePtr &l, const TablePtr &r, const at::Tensor &lk,
+                                   const at::Tensor &rk, const JoinConfig &cfg, int C) {
+  auto key_col = [](const TablePtr &t, const at::Tensor &k) {
+    for (int c = 0; c < t->Columns(); ++c)
+      if (t->column(c).data.defined() && t->column(c).data.data_ptr() == k.data_ptr()) return c;
+    return -1;
+  };
+  const int lkc = key_col(l, lk), rkc = key_col(r, rk);
+  const at::Tensor cl = key_chunk_ids(lk, C), cr = key_chunk_ids(rk, C);
+  JoinSink sink;
+  sink.chunks_total = C;
+  for (int c = 0; c < C; ++c) {
+    at::Tensor il = cl.eq(c).nonzero().flatten(), ir = cr.eq(c).nonzero().flatten();
+    TablePtr lc = Gather(l, il), rc = Gather(r, ir);
+    const at::Tensor lkc_t = lkc >= 0 ? lc->column(lkc).data : lk.index_select(0, il);
+    const at::Tensor rkc_t = rkc >= 0 ? rc->column(rkc).data : rk.index_select(0, ir);
+    il = at::Tensor();
+    ir = at::Tensor();
+    if (!radix_join(ex, lc, rc, lkc_t, rkc_t, cfg, &sink)) return nullptr;
+    ++sink.chunks_done;
+  }
+  return sink.finish(l->GetContext());
 }
 
 // LDS radix join of any large device join (every type, one or several keys, var-width payload
@@ -1225,13 +1321,11 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
   const bool lpx = lvar || ckey, rpx = rvar || ckey;
   TablePtr lp = lpx ? proxy(left, lvar, lc, k.l, lpos) : left, rp = rpx ? proxy(right, rvar, rc, k.r, rpos) : right;
   if (!radix_eligible(lp) || !radix_eligible(rp)) return nullptr;
-  TablePtr out = radix_join(ex, lp, rp, k.l, k.r, cfg, sink);
+  const int mchunks = sink ? 1 : radix_join_chunks(ex, lp, rp, k.l, k.r);
+  TablePtr out = mchunks > 1 ? radix_join_chunked(ex, lp, rp, k.l, k.r, cfg, mchunks)
+                             : radix_join(ex, lp, rp, k.l, k.r, cfg, sink);
   if (!out) return nullptr;
-  if (k.verify && !lvar && !rvar)
-    if (int64_t bad = key_mismatches(out, cfg, left->Columns())) {
-      trace::add_counter("join.radix.hash_collision_fallback", bad);
-      return nullptr;
-    }
+  if (k.verify && !lvar && !rvar) return drop_false_matches(out, cfg, left->Columns());
   if (!lpx && !rpx) return out;
   const JoinType jt = cfg.GetType();
   auto side = [&](const TablePtr &orig, bool px, bool var, const std::vector<int> &pos, const std::vector<int> &keys,
@@ -1286,12 +1380,7 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
   for (auto &c : rcols) all.push_back(std::move(c));
   TablePtr res = Table::Make(left->GetContext(), std::move(all));
   if (lvar || rvar) trace::add_counter("join.radix.var_gather", 1);
-  if (k.verify)
-    if (int64_t bad = key_mismatches(res, cfg, left->Columns())) {
-      trace::add_counter("join.radix.hash_collision_fallback", bad);
-      return nullptr;
-    }
-  return res;
+  return k.verify ? drop_false_matches(res, cfg, left->Columns()) : res;
 }
 
 // Local join.  With a sink (chunked distributed join) the radix path writes into

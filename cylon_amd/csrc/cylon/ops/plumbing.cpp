@@ -23,7 +23,7 @@ static Column gather_var(const Exec &ex, const Column &c, const at::Tensor &idx,
   at::Tensor bytes = ex.empty_bytes(total);
   at::Tensor valid;
   if (c.nullable() || may_null) valid = ex.empty_u8(m);
-  KCALL(ex, gather_var_bytes, in, ptr<int64_t>(idx), m, ptr<int64_t>(offs), ptr<uint8_t>(bytes),
+  KCALL(ex, gather_var_bytes, in, ptr<int64_t>(idx), m, ptr<int64_t>(offs), total, ptr<uint8_t>(bytes),
         valid.defined() ? ptr<uint8_t>(valid) : nullptr);
   return Column(c.name, c.type, m, bytes, offs, valid);
 }

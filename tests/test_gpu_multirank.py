@@ -136,7 +136,7 @@ def _join_edge_cases(ctx, case):
     rank = ctx.get_rank()
     g = torch.Generator(device="cuda").manual_seed(50 + rank)
     n = 40_000
-    if case == "skew":  # one hot key on the (smaller) build side overflows the LDS capacity -> fallback
+    if case == "skew":  # one hot key on the (smaller) build side overflows the LDS capacity -> split items
         k = torch.randint(0, 5000, (n,), generator=g, device="cuda")
         m = n // 4
         kb = torch.where(torch.rand(m, generator=g, device="cuda") < 0.3, torch.zeros(m, dtype=torch.int64, device="cuda"),
@@ -169,8 +169,9 @@ def test_chunked_join_edge_cases_on_device(case):
     ref = a.add_prefix("l_").merge(b.add_prefix("r_"), left_on="l_k", right_on="r_k")
     assert len(got) == len(ref)
     assert _canon(got[sorted(got.columns)]) == _canon(ref[sorted(got.columns)])
-    if case == "skew":
-        assert any(r[3].get("join.radix.overflow_fallback", 0) > 0 for r in res)
+    if case == "skew":  # the hot key's partition runs as split work items (no global-table fallback)
+        assert any(r[3].get("join.radix.split_partitions", 0) > 0 for r in res)
+        assert all(r[3].get("join.radix.overflow_fallback", 0) == 0 for r in res)
 
 
 # ---------------------------------------------------------------------------

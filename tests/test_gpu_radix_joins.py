@@ -386,3 +386,22 @@ def test_radix_join_string_keys(gpu_ctx, ctx, monkeypatch, how, keys):
     assert c.get("join.radix.hash_collision_fallback", 0) == 0, c
     assert c["join.radix.rows_out"] == len(exp)
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
+
+
+@pytest.mark.parametrize("how", ["inner", "left", "outer"])
+def test_radix_join_memory_bounded_chunks(gpu_ctx, ctx, monkeypatch, how):
+    """Bounded memory: with a device budget (config memory_budget_mb) below the join's working set
+    + output, the radix join runs in key-hash chunks into one output sink (join.radix.memory_chunks)
+    and gives the CPU twin's result."""
+    rng = np.random.default_rng(59)
+    n = 3_000_000
+    a = pa.table({"k": rng.integers(0, 2_000_000, n), "v": rng.random(n)})
+    b = pa.table({"k": rng.integers(0, 2_000_000, n), "w": rng.random(n), "i": rng.integers(-5, 5, n)})
+    gpu_ctx.add_config("memory_budget_mb", "220")
+    try:
+        got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["k"], monkeypatch)
+    finally:
+        gpu_ctx.add_config("memory_budget_mb", "")
+    assert c.get("join.radix.memory_chunks", 0) >= 2, c
+    assert len(got) == len(exp)
+    pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
