@@ -268,7 +268,8 @@ def main():
     allocator = {"alloc_retries": int(alloc1.get("num_alloc_retries", 0) - alloc0.get("num_alloc_retries", 0)),
                  "device_mallocs": int(alloc1.get("num_device_alloc", 0) - alloc0.get("num_device_alloc", 0)),
                  "device_frees": int(alloc1.get("num_device_free", 0) - alloc0.get("num_device_free", 0)),
-                 "peak_reserved_gb": round(alloc1.get("reserved_bytes.all.peak", 0) / 2**30, 1)}
+                 "peak_reserved_gb": round(alloc1.get("reserved_bytes.all.peak", 0) / 2**30, 1),
+                 "peak_allocated_gb": round(alloc1.get("allocated_bytes.all.peak", 0) / 2**30, 1)}
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:

@@ -42,6 +42,7 @@ void register_extended_ops(py::module &m) {
 
   // ---- device self-check behind the radix passes' wave-atomic stable ranking (radix_join.hip)
   m.def("rp_set_ranking", [](int mode) { hip::rp_set_ranking(mode); });
+  m.def("partition_digit_bits", [](int bits) { ops::SetPartitionDigitBits(bits); });
   m.def("knob_registry", []() {  // (name without CYLON_, group, effect) of every native knob
     std::vector<std::tuple<std::string, std::string, std::string>> r;
     for (const auto &k : knobs::Registry()) r.emplace_back(k.name, k.group, k.effect);

@@ -1,6 +1,7 @@
 // L0/L2 core objects: DataType, Column, Table, CylonContext.
 // Reference: cpp/src/cylon/data_types.hpp, column.cpp, table.cpp:1-61 (ctor),
 // ctx/cylon_context.cpp:25-108.
+#include <mutex>
 #include "cylon/knobs.hpp"
 #include <c10/hip/HIPCachingAllocator.h>
 #include <hip/hip_runtime_api.h>
@@ -196,10 +197,14 @@ TablePtr Table::to(at::Device dev) const {
 CylonContext::CylonContext(bool distributed) : distributed_(distributed) {}
 
 // GPU contexts run the radix passes' lane-order self-check once per device here, so that
-// no pass allocates or synchronises for it (and stream capture of a pass stays possible)
+// no pass allocates or synchronises for it (and stream capture of a pass stays possible), and
+// load every kernel code object (a first launch inside a pipelined join blocked the host for up to
+// 40 ms while its transfers ran without compute to overlap)
 static void warm_device(const at::Device &device) {
   if (!device.is_cuda()) return;
   c10::hip::HIPGuard guard(device.index());
+  static std::once_flag loaded[64];
+  std::call_once(loaded[device.index() & 63], [] { hip::preload_device_code(); });
   hip::lds_lane_order_ok(reinterpret_cast<void *>(c10::hip::getCurrentHIPStream(device.index()).stream()));
 }
 

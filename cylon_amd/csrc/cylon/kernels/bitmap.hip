@@ -110,5 +110,8 @@ void unpack_byte_columns(const uint64_t *const *words, int k, int64_t n, uint8_t
   HIP_LAUNCH_CHECK();
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_bitmap() { preload_code(reinterpret_cast<const void *>(&k_pack_validity)); }
+
 }  // namespace hip
 }  // namespace cylon

@@ -68,5 +68,8 @@ void batched_copy(const void *const *src, void *const *dst, const int64_t *bytes
   }
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_copy() { preload_code(reinterpret_cast<const void *>(&k_batched_copy)); }
+
 }  // namespace hip
 }  // namespace cylon

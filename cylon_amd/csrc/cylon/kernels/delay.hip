@@ -21,5 +21,8 @@ void spin_delay_us(double us, void *stream) {
   HIP_LAUNCH_CHECK();
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_delay() { preload_code(reinterpret_cast<const void *>(&k_spin_delay)); }
+
 }  // namespace hip
 }  // namespace cylon

@@ -34,6 +34,12 @@ inline int grid_for(int64_t n, int64_t per_block = kBlock, int64_t cap = kMaxGri
 
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
+// load the code object holding fn now (HIP loads a code object lazily, on its first launch)
+inline void preload_code(const void *fn) {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, fn);
+}
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ uint64_t lanemask_lt() {

@@ -415,5 +415,8 @@ void group_quantile(const ColView &v, const int64_t *perm, const int64_t *offs, 
   HIP_LAUNCH_CHECK();
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_groupby() { preload_code(reinterpret_cast<const void *>(&k_group_insert)); }
+
 }  // namespace hip
 }  // namespace cylon

@@ -466,5 +466,8 @@ void radix_partition_ids(const int64_t *keys, int64_t n, int bits, uint32_t *pid
   HIP_LAUNCH_CHECK();
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_hash_join() { preload_code(reinterpret_cast<const void *>(&k_table_init)); }
+
 }  // namespace hip
 }  // namespace cylon

@@ -173,5 +173,8 @@ void index_verify_bytes(const ColView &col, const ColView &labels, const int64_t
   HIP_LAUNCH_CHECK();
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_index() { preload_code(reinterpret_cast<const void *>(&k_index_bounds)); }
+
 }  // namespace hip
 }  // namespace cylon

@@ -761,5 +761,8 @@ void radix_join_write(const int64_t *pkeys, const int64_t *poffs, const int64_t 
 }
 
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_lds_join() { preload_code(reinterpret_cast<const void *>(&(k_rj_count<0, false>))); }
+
 }  // namespace hip
 }  // namespace cylon

@@ -99,5 +99,8 @@ void merge_sorted_pairs(const uint64_t *ak, const int64_t *ai, int64_t na, const
   HIP_LAUNCH_CHECK();
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_merge() { preload_code(reinterpret_cast<const void *>(&k_merge_pairs)); }
+
 }  // namespace hip
 }  // namespace cylon

@@ -397,5 +397,8 @@ void widen_u32(const uint32_t *in, int64_t n, int64_t base, int64_t *out, void *
   HIP_LAUNCH_CHECK();
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_partition() { preload_code(reinterpret_cast<const void *>(&k_row_partition_hash)); }
+
 }  // namespace hip
 }  // namespace cylon

@@ -357,5 +357,8 @@ void radix_groupby_pack(const int64_t *offs, const int64_t *goff, int64_t nparts
   HIP_LAUNCH_CHECK();
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_radix_groupby() { preload_code(reinterpret_cast<const void *>(&k_hll)); }
+
 }  // namespace hip
 }  // namespace cylon

@@ -112,6 +112,10 @@ struct ImageDigit {
   }
 };
 
+// digits whose pass can write the next pass's digit of every stored key (ColSet::nd_out)
+template <class Digit>
+constexpr bool kNdDigit = std::is_same<Digit, ImageDigit>::value || std::is_same<Digit, PartDigit>::value;
+
 // Order-preserving range digit (K7 range join): the partition of key k is
 // ((k ^ flip) - mn) >> rshift -- key ranges in key order -- and a pass's digit is
 // bits [shift, shift + log2(mask + 1)) of that partition id.
@@ -664,7 +668,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
           if (i < (SLOT ? s_tend[par ^ 1] : end)) kv[k] = digit.key_at(i);
         }
       }
-      if (std::is_same<Digit, ImageDigit>::value && c == 0 && cols.nd_out != nullptr) {  // sorts only
+      if (kNdDigit<Digit> && c == 0 && cols.nd_out != nullptr) {  // sorts, stable hash partitions
 #pragma unroll
         for (int q = 0; q < kRPItems; ++q) {
           const int j = threadIdx.x + q * THREADS;
@@ -672,7 +676,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
             const uint64_t kv0 = ldw<W8>(st, j, w);
             const int64_t o = RP_DEST(q);
             stw<W8>(out, o, w, kv0);
-            cols.nd_out[o] = (uint16_t)(((kv0 - cols.nd_sub) >> cols.nd_shift) & cols.nd_mask);
+            if constexpr (kNdDigit<Digit>)
+              cols.nd_out[o] = (uint16_t)digit.next_of(kv0, cols.nd_shift, cols.nd_mask, cols.nd_sub);
           }
         }
       } else if (n4) {
@@ -970,7 +975,7 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
             atomicAdd(&lcnt[cell >> 1], 1u << ((cell & 1u) << 4));
           }
         }
-      } else if (std::is_same<Digit, ImageDigit>::value && c == 0 && cols.nd_out != nullptr) {  // sorts only
+      } else if (kNdDigit<Digit> && c == 0 && cols.nd_out != nullptr) {  // sorts, stable hash partitions
 #pragma unroll
         for (int q = 0; q < kRPItems; ++q) {
           const int j = tx + q * THREADS;
@@ -978,7 +983,8 @@ __global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(8)))
             const int64_t o = running[dp[q] >> 16] + (int64_t)(dp[q] & 0xffffu);
             const uint64_t kv0 = ldw<W8>(st, j, w);
             stw<W8>(out, o, w, kv0);
-            cols.nd_out[o] = (uint16_t)(((kv0 - cols.nd_sub) >> cols.nd_shift) & cols.nd_mask);
+            if constexpr (kNdDigit<Digit>)
+              cols.nd_out[o] = (uint16_t)digit.next_of(kv0, cols.nd_shift, cols.nd_mask, cols.nd_sub);
           }
         }
       } else {
@@ -1496,7 +1502,8 @@ static void rows_pass_launch(const Digit &dg, int64_t n, int digit_bits, const u
 
 void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, int digit_bits, const uint8_t *const *in,
                      uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream, bool stable,
-                     const SortLbArgs *lb, int nd_bits, const NarrowKeys *nk) {
+                     const SortLbArgs *lb, int nd_bits, const NarrowKeys *nk, bool tiles_prescanned,
+                     const uint16_t *nd_in, uint16_t *nd_out) {
   const uint32_t nb = 1u << digit_bits;
   if (nk && nk->base_src) {  // narrowed join partition pass (no look-back counting)
     CYLON_CHECK(!(lb && (lb->plan_in || lb->plan_out)), Code::Invalid, "narrowed pass: no look-back");
@@ -1504,12 +1511,15 @@ void radix_rows_pass(const int64_t *keys, int64_t n, int total_bits, int shift, 
                      out, widths, ncols, ws, stream, 0, stable);
     return;
   }
-  CYLON_CHECK(!(lb && lb->plan_out) || (nd_bits >= 1 && nd_bits <= 9 && stable), Code::Invalid,
+  CYLON_CHECK(!(lb && lb->plan_out) || (nd_bits >= 1 && nd_bits <= 9 && stable && !nd_out), Code::Invalid,
               "look-back counting partition pass: next digit of " << nd_bits << " bits");
+  CYLON_CHECK(!nd_out || (nd_bits >= 1 && nd_bits <= 16), Code::Invalid, "partition pass: next-digit output");
   rows_pass_launch(PartDigit{keys, total_bits, shift, nb - 1}, n, digit_bits, in, out, widths, ncols, ws, stream, 0,
-                   stable, false, nullptr, nullptr, nullptr, shift + digit_bits,
-                   lb && lb->plan_out ? (1u << nd_bits) - 1u : 0u, 0, lb);
+                   stable, tiles_prescanned, nullptr, lb && lb->plan_in ? nullptr : nd_in, nd_out, shift + digit_bits,
+                   (lb && lb->plan_out) || nd_out ? (1u << nd_bits) - 1u : 0u, 0, lb);
 }
+
+int64_t radix_rows_pass_th_offset(int64_t n, int digit_bits) { return xt_layout(n, 1u << digit_bits).th; }
 
 void radix_sort_rows_pass(const int64_t *keys, int64_t n, int shift, int digit_bits, const uint8_t *const *in,
                           uint8_t *const *out, const int *widths, int ncols, int64_t *ws, void *stream,
@@ -1643,7 +1653,7 @@ template <class Digit>
 static void slot_pass(const Digit &dg, int64_t n, int digit_bits, const uint8_t *const *in, uint8_t *const *out,
                       const int *widths, int ncols, int src, int S, const uint32_t *bbase, const int64_t *pcnt,
                       int64_t pslot, int gshift, int gmask, int B, int64_t nslots, int64_t slot, int64_t *ws,
-                      int64_t *counts, unsigned int *overflow, hipStream_t s) {
+                      int64_t *counts, unsigned int *overflow, hipStream_t s, uint64_t key_xor = 0) {
   CYLON_CHECK(S >= 1 && S <= kSlotMaxSeg && ncols >= 1 && ncols <= kMaxFusedCols && slot > 0, Code::Invalid,
               "slot pass arguments");
   CYLON_CHECK(key_column_ok(dg, in, widths), Code::Invalid, "slot pass: column 0 must be the key");
@@ -1675,7 +1685,7 @@ static void slot_pass(const Digit &dg, int64_t n, int digit_bits, const uint8_t 
   lb.sl_B = B;
   ColSet cs;
   cs.n = ncols;
-  cs.key_xor = 0;
+  cs.key_xor = key_xor;  // (a sort's first MSD pass stores order images)
   cs.check_order = 0;  // the order inside a slot is free
   cs.order_bad = order_flag();
   cs.nd_out = nullptr;
@@ -1762,6 +1772,42 @@ static void slot_rows_pass(const Digit &dg, int64_t n, int first_bits, int secon
   }
 }
 
+// MSD passes of a keys-only sort (seg_sort.hip sorts each final partition in LDS): the first takes
+// bits [hr - db1, hr) of image - sub from the raw keys and stores the images (key ^ key_xor) -- into
+// (XCD, bucket) slots when 8 x 2^db1 segments fit the second pass's table (slot > 0), else exactly
+// (XCD-tile pass: bucket bases in ws) -- the second bits [hr - db1 - db2, hr - db1) into slots.
+// Partitions come out in key order.
+void radix_sort_msd_first_pass(const int64_t *keys, int64_t n, int hr, int db1, int db2, uint64_t key_xor,
+                               uint64_t sub, int64_t *out, int64_t slot, int64_t *ws, int64_t *counts,
+                               unsigned int *overflow, void *stream) {
+  CYLON_CHECK(radix_slot_eligible(n, 1, db1, db2) && hr >= db1 + db2 && hr <= 64 &&
+                  (slot == 0 || radix_slot_first_pass_ok(db1)),
+              Code::Invalid, "MSD sort pass not eligible");
+  const int nb1 = 1 << db1;
+  const uint8_t *in[1] = {reinterpret_cast<const uint8_t *>(keys)};
+  uint8_t *o[1] = {reinterpret_cast<uint8_t *>(out)};
+  const int w[1] = {8};
+  const ImageDigit dg{keys, hr - db1, (uint32_t)nb1 - 1, key_xor, sub};
+  if (slot > 0)
+    slot_pass(dg, n, db1, in, o, w, 1, 0, kXcds, nullptr, nullptr, 0, 0, 0, 1, int64_t(kXcds) * nb1, slot, ws, counts,
+              overflow, as_stream(stream), key_xor);
+  else {  // (the second pass reads the bucket bases of an XCD-tile pass: wave-atomic ranking, 1024 threads)
+    CYLON_CHECK(rp_xt() && rp_wave_atomic(as_stream(stream)), Code::Invalid, "MSD sort: exact first pass needs XT");
+    rows_pass_launch(dg, n, db1, in, o, w, 1, ws, stream, key_xor);
+  }
+}
+
+void radix_sort_msd_second_pass(const int64_t *images, int64_t n, int hr, int db1, int db2, uint64_t sub,
+                                const int64_t *first_ws, const int64_t *first_counts, int64_t first_slot, int64_t *out,
+                                int64_t slot, int64_t *ws, int64_t *counts, unsigned int *overflow, void *stream) {
+  CYLON_CHECK(hr >= db1 + db2 && hr <= 64 && (first_counts != nullptr || first_ws != nullptr), Code::Invalid,
+              "MSD sort pass digits");
+  const uint8_t *in[1] = {reinterpret_cast<const uint8_t *>(images)};
+  uint8_t *o[1] = {reinterpret_cast<uint8_t *>(out)};
+  const int w[1] = {8};
+  slot_rows_pass(ImageDigit{images, hr - db1 - db2, (1u << db2) - 1, 0, sub}, n, db1, db2, in, o, w, 1, first_ws,
+                 first_counts, first_slot, slot, ws, counts, overflow, stream);
+}
 
 // ---- sort prologue: the keys' varying bits (OR ^ AND), the images' min and max, and the first
 // pass's per-tile histogram of the order image's low 10 bits in ONE read of the keys (the separate
@@ -1983,6 +2029,9 @@ void radix_range_part_offsets(const int64_t *keys, int64_t n, uint64_t flip, uin
                      mn, rshift, np, offs);
   HIP_LAUNCH_CHECK();
 }
+
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_radix_join() { preload_code(reinterpret_cast<const void *>(&k_sl_counts)); }
 
 }  // namespace hip
 }  // namespace cylon

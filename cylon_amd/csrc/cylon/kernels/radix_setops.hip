@@ -6,7 +6,7 @@
 // :923-999 (Unique keep first / last over a column subset).
 //
 // MI355X design (no sort, no global hash table):
-//   1. k_so_hash: one pass per table writes a 64-bit row hash (NaN / -0.0 /
+//   1. k_so_hash_tiles: one pass over L ++ R writes a 64-bit row hash (NaN / -0.0 /
 //      null canonicalised so that equal rows hash equal) and the global row id
 //      (left rows 0..nl-1, right rows nl..n-1).
 //   2. the (hash, row id) pairs are radix-partitioned by the top bits of
@@ -68,26 +68,113 @@ __device__ __forceinline__ uint64_t so_value_hash(const ColView &c, int64_t i) {
   return hashing::fmix64(bits);
 }
 
-__global__ void k_so_hash(SOColSet cols, int ncols, int64_t n, int64_t base, uint64_t *__restrict__ h,
-                          int64_t *__restrict__ rowid) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    uint64_t x = 0x84222325cbf29ce4ULL;
-    for (int c = 0; c < ncols; ++c) x = hashing::combine64(x, so_value_hash(cols.c[c], i));
-    h[base + i] = x | 1ull;  // 0 marks an empty LDS slot
-    if (rowid != nullptr) rowid[base + i] = base + i;  // null: the partition pass generates row ids
+// Row hash of the concatenated L ++ R rows with the first partition pass's tile histogram (the
+// prehist of ops/radix.cpp RadixPartition): 8192-row tiles (the XCD-tile passes' kRPTile), 16 rows
+// per thread.  Every column of a row is loaded before any is hashed -- the per-column loop of
+// k_so_hash waited one memory latency per column (4 per row: 1B-row union side 11.2 ms, 3.6 TB/s).
+constexpr int kSHThreads = 512, kSHTile = 8192, kSHItems = kSHTile / kSHThreads;
+
+// NC >= ncols columns held per row; the column sets live in device memory (cols[0] = L, cols[1] = R):
+// their fields are wave-uniform scalar loads, and neither set is copied into registers or scratch
+template <int NC>
+__device__ __forceinline__ uint64_t so_row_hash(const SOColSet *__restrict__ S, int ncols, int64_t i) {
+  uint64_t raw[NC];
+  uint8_t vb[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    raw[c] = 0;
+    vb[c] = 1;
+    if (c < ncols) {
+      const ColView &col = S->c[c];
+      if (col.kind != static_cast<int>(ValueKind::VAR_BYTES) && col.kind != static_cast<int>(ValueKind::FIXED_BYTES))
+        raw[c] = load_bits(col.data, i, col.width);
+      if (col.valid != nullptr) vb[c] = col.valid[i];
+    }
+  }
+  uint64_t x = 0x84222325cbf29ce4ULL;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (c < ncols) {
+      const ColView &col = S->c[c];
+      uint64_t hv;
+      if (vb[c] == 0) {
+        hv = 0x5bd1e9955bd1e995ULL;
+      } else if (col.kind == static_cast<int>(ValueKind::VAR_BYTES) ||
+                 col.kind == static_cast<int>(ValueKind::FIXED_BYTES)) {
+        hv = so_value_hash(col, i);
+      } else {
+        uint64_t bits = (uint64_t)extend_bits(raw[c], col.width, col.kind);
+        if (col.kind == static_cast<int>(ValueKind::FLOAT)) {
+          bool nan = false;
+          if (col.width == 8) nan = __longlong_as_double((long long)bits) != __longlong_as_double((long long)bits);
+          else if (col.width == 4) nan = __int_as_float((int)bits) != __int_as_float((int)bits);
+          else if (col.width == 2) nan = ((bits & 0x7c00u) == 0x7c00u) && (bits & 0x3ffu);
+          if (nan) bits = 0x7ff8000000000000ull;
+        }
+        hv = hashing::fmix64(bits);
+      }
+      x = hashing::combine64(x, hv);
+    }
+  }
+  return x | 1ull;  // 0 marks an empty LDS slot
+}
+
+template <int NC>
+__global__ __launch_bounds__(kSHThreads) void k_so_hash_tiles(const SOColSet *__restrict__ cols, int ncols, int64_t nl,
+                                                              int64_t n, uint64_t *__restrict__ h, int bits,
+                                                              uint32_t dmask, int64_t ntiles,
+                                                              uint16_t *__restrict__ th) {
+  __shared__ uint32_t hist[1024];
+  const uint32_t nb = dmask + 1u;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (uint32_t p = threadIdx.x; p < nb; p += kSHThreads) hist[p] = 0u;
+    __syncthreads();
+    const int64_t r0 = t * kSHTile;
+    for (int u = 0; u < kSHItems; ++u) {
+      const int64_t i = r0 + u * kSHThreads + threadIdx.x;
+      if (i < n) {
+        const bool left = i < nl;
+        const uint64_t x = so_row_hash<NC>(cols + (left ? 0 : 1), ncols, left ? i : i - nl);
+        h[i] = x;
+        if (th != nullptr) atomicAdd(&hist[(uint32_t)(hashing::fmix64(x) >> (64 - bits)) & dmask], 1u);
+      }
+    }
+    __syncthreads();
+    if (th != nullptr)
+      for (uint32_t p = threadIdx.x; p < nb; p += kSHThreads) th[t * nb + p] = (uint16_t)hist[p];
+    __syncthreads();
   }
 }
 
-void setop_row_hash(const ColView *cols, int ncols, int64_t n, int64_t base, uint64_t *h, int64_t *rowid,
-                    void *stream) {
+void setop_row_hash_tiles(const ColView *lcols, const ColView *rcols, int ncols, int64_t nl, int64_t n, uint64_t *h,
+                          int bits, int digit_bits, uint16_t *th, void *colsets, void *stream) {
   if (n == 0) return;
-  CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols, Code::Invalid, "set operation over " << ncols << " columns");
-  SOColSet s;
-  for (int c = 0; c < ncols; ++c) s.c[c] = cols[c];
-  hipLaunchKernelGGL(k_so_hash, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), s, ncols, n, base, h, rowid);
+  CYLON_CHECK(ncols >= 1 && ncols <= kMaxFusedCols && digit_bits >= 1 && digit_bits <= 10 && bits >= digit_bits &&
+                  bits <= 64,
+              Code::Invalid, "row hash tiles: " << ncols << " columns, digit " << digit_bits << " of " << bits);
+  SOColSet hs[2];
+  for (int c = 0; c < ncols; ++c) {
+    hs[0].c[c] = lcols[c];
+    hs[1].c[c] = rcols ? rcols[c] : lcols[c];
+  }
+  hipStream_t s = as_stream(stream);
+  HIP_CHECK(hipMemcpyAsync(colsets, hs, sizeof(hs), hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipStreamSynchronize(s));  // (hs is pageable host memory on this stack frame)
+  const SOColSet *d = reinterpret_cast<const SOColSet *>(colsets);
+  const int64_t ntiles = (n + kSHTile - 1) / kSHTile;
+  const int grid = (int)std::min<int64_t>(ntiles, (int64_t)kNumCUs * 4);
+  const uint32_t dm = (1u << digit_bits) - 1u;
+  if (ncols <= 4)
+    hipLaunchKernelGGL(k_so_hash_tiles<4>, dim3(grid), dim3(kSHThreads), 0, s, d, ncols, nl, n, h, bits, dm, ntiles, th);
+  else if (ncols <= 8)
+    hipLaunchKernelGGL(k_so_hash_tiles<8>, dim3(grid), dim3(kSHThreads), 0, s, d, ncols, nl, n, h, bits, dm, ntiles, th);
+  else
+    hipLaunchKernelGGL(k_so_hash_tiles<kMaxFusedCols>, dim3(grid), dim3(kSHThreads), 0, s, d, ncols, nl, n, h, bits, dm,
+                       ntiles, th);
   HIP_LAUNCH_CHECK();
 }
+
+int64_t setop_colsets_bytes() { return (int64_t)(2 * sizeof(SOColSet)); }
 
 int64_t setop_rows_per_part() { return kSORowsPerPart; }
 
@@ -293,6 +380,9 @@ void setop_dedup(const uint64_t *ph, const int64_t *prow, const int64_t *offs, i
                      keep_last ? 1 : 0, L, R, ncols, mask, reinterpret_cast<unsigned long long *>(exc), bad);
   HIP_LAUNCH_CHECK();
 }
+
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_radix_setops() { preload_code(reinterpret_cast<const void *>(&k_so_hash_tiles<4>)); }
 
 }  // namespace hip
 }  // namespace cylon

@@ -192,5 +192,8 @@ void splitter_partition(const uint64_t *const *images, const uint8_t *const *nul
   HIP_LAUNCH_CHECK();
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_range() { preload_code(reinterpret_cast<const void *>(&k_range_minmax)); }
+
 }  // namespace hip
 }  // namespace cylon

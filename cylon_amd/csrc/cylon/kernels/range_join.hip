@@ -302,5 +302,8 @@ void range_join_write(const int64_t *lkeys, const int64_t *loffs, const int64_t 
   HIP_LAUNCH_CHECK();
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_range_join() { preload_code(reinterpret_cast<const void *>(&k_rg_count)); }
+
 }  // namespace hip
 }  // namespace cylon

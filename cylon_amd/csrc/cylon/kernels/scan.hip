@@ -317,5 +317,52 @@ void mark_indices(const int64_t *idx, int64_t m, uint8_t *flags, void *stream) {
   HIP_LAUNCH_CHECK();
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_scan() { preload_code(reinterpret_cast<const void *>(&k_block_sums)); }
+
+void preload_bitmap();
+void preload_copy();
+void preload_delay();
+void preload_groupby();
+void preload_hash_join();
+void preload_index();
+void preload_lds_join();
+void preload_merge();
+void preload_partition();
+void preload_radix_groupby();
+void preload_radix_join();
+void preload_radix_setops();
+void preload_range();
+void preload_range_join();
+void preload_seg_sort();
+void preload_select();
+void preload_sort();
+void preload_strcast();
+
+// Every kernel file's code object, once per process and device (HIP loads a code object on the first
+// launch from it: inside a pipelined join that stalled the host for up to 40 ms while the posted
+// transfers ran with nothing to overlap, profiles/r05/first_step_overlap.txt)
+void preload_device_code() {
+  preload_bitmap();
+  preload_copy();
+  preload_delay();
+  preload_groupby();
+  preload_hash_join();
+  preload_index();
+  preload_lds_join();
+  preload_merge();
+  preload_partition();
+  preload_radix_groupby();
+  preload_radix_join();
+  preload_radix_setops();
+  preload_range();
+  preload_range_join();
+  preload_scan();
+  preload_seg_sort();
+  preload_select();
+  preload_sort();
+  preload_strcast();
+}
+
 }  // namespace hip
 }  // namespace cylon

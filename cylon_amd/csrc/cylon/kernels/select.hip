@@ -80,5 +80,8 @@ void select_var_bytes(const ColView &a, const ColView &b, int b_bcast, const uin
   HIP_LAUNCH_CHECK();
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_select() { preload_code(reinterpret_cast<const void *>(&k_select_var_lengths)); }
+
 }  // namespace hip
 }  // namespace cylon

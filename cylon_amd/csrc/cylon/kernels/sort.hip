@@ -381,5 +381,8 @@ void sort_string_chunk_keys(const ColView &col, const int64_t *perm, int64_t n, 
   HIP_LAUNCH_CHECK();
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_sort() { preload_code(reinterpret_cast<const void *>(&k_sort_keys)); }
+
 }  // namespace hip
 }  // namespace cylon

@@ -85,5 +85,8 @@ void i64_to_str_write(const int64_t *v, const uint8_t *valid, int64_t n, const i
   HIP_LAUNCH_CHECK();
 }
 
+// this file's code object is loaded at context creation (preload_device_code), not on first use
+void preload_strcast() { preload_code(reinterpret_cast<const void *>(&k_str_to_i64)); }
+
 }  // namespace hip
 }  // namespace cylon

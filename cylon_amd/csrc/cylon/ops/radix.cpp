@@ -5,6 +5,8 @@
 #include <cmath>
 #include <cstdlib>
 
+#include <atomic>
+
 #include "util.hpp"
 #include "../trace.hpp"
 
@@ -68,10 +70,14 @@ std::vector<at::Tensor> UnpackByteColumns(const Exec &ex, const BytePacking &bp,
 
 
 static thread_local bool tl_partition_lb_off = false;  // set while a look-back fallback repartitions
+static std::atomic<int> g_max_digit_bits{10};  // A/B hook (SetPartitionDigitBits): digit bits per pass
+
+void SetPartitionDigitBits(int bits) { g_max_digit_bits.store(bits >= 3 && bits <= 10 ? bits : 10); }
 
 std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> cur, const std::vector<int> &widths,
                                        int bits, at::Tensor *offs, const RangeSpec *range,
-                                       std::vector<int> *keep_packed, bool stable, const hip::NarrowKeys *nk) {
+                                       std::vector<int> *keep_packed, bool stable, const hip::NarrowKeys *nk,
+                                       const PrehistFn *prehist) {
   CYLON_CHECK(ex.gpu, Code::Invalid, "RadixPartition is a device path");
   CYLON_CHECK(!cur.empty() && cur.size() == widths.size() && widths[0] == 8, Code::Invalid,
               "RadixPartition: column 0 must be the int64 key");
@@ -92,7 +98,7 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
   // (16-B byte runs per pass instead of 128-B runs); packed: 30.2 ms.
   std::vector<int> pw = widths;
   const BytePacking bp = PackByteColumns(ex, cur, pw, n);
-  const int max_db = 10;  // digit bits per pass
+  const int max_db = g_max_digit_bits.load();  // digit bits per pass
   const int npass = (bits + max_db - 1) / max_db;
   int shift = 0;
   at::Tensor ws;
@@ -105,10 +111,18 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
                                                             ex.stream);
   at::Tensor lbws = lb_on ? ex.empty_i64(hip::radix_sort_lb_workspace(n)) : at::Tensor();
   if (lb_on) trace::add_counter("partition.radix.lookback", 1);
+  // exact XCD-tile passes after the first: the previous pass writes every stored key's next digit
+  // (2 B/row), so this pass's tile histogram reads 2 bytes per row instead of the 8-byte key
+  const bool nd_on = !range && !nk && !lb_on && npass > 1;
+  at::Tensor nd = nd_on ? at::empty({n}, ex.opts(at::kShort)) : at::Tensor();
+  uint16_t *ndp = nd_on ? reinterpret_cast<uint16_t *>(nd.data_ptr()) : nullptr;
   for (int ps = 0; ps < npass; ++ps) {
     const int db = dbits[ps];
     const int64_t wsn = hip::radix_rows_pass_workspace(n, db);
     if (!ws.defined() || ws.numel() < wsn) ws = ex.empty_i64(wsn);
+    // the caller's producer kernel (a row hash) already counted the first pass's tile digits
+    const bool pre = ps == 0 && prehist && !range && !nk;
+    if (pre) (*prehist)(ptr<int64_t>(ws) + hip::radix_rows_pass_th_offset(n, db), db);
     std::vector<at::Tensor> nxt;
     std::vector<const uint8_t *> in;
     std::vector<uint8_t *> out;
@@ -136,7 +150,8 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
       hip::radix_rows_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, bits, shift, db, in.data(),
                            out.data(), pwp.data(), (int)cur.size(), ptr<int64_t>(ws), ex.stream,
                            stable || ps > 0,  // LSD: every pass after the first keeps the order it receives
-                           lb_on ? &lba : nullptr, ps + 1 < npass ? dbits[ps + 1] : 0, nk ? &nkp : nullptr);
+                           lb_on ? &lba : nullptr, ps + 1 < npass ? dbits[ps + 1] : 0, nk ? &nkp : nullptr, pre,
+                           nd_on && ps > 0 ? ndp : nullptr, nd_on && ps + 1 < npass ? ndp : nullptr);
     }
     cur = std::move(nxt);
     shift += db;

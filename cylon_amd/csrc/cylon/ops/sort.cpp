@@ -12,6 +12,9 @@
 #include <limits>
 #include <cstdlib>
 
+#include <atomic>
+#include <cmath>
+
 #include "util.hpp"
 #include "../trace.hpp"
 
@@ -127,8 +130,59 @@ at::Tensor SortIndices(const TablePtr &t, const std::vector<int> &cols, const st
 // instead of sorting (image, row) pairs and gathering each column at random
 // afterwards (~50 G random accesses/s, profiles/membench.txt).  Constant
 // leading/trailing bits of the image are skipped (OR ^ AND reduction).
+static std::atomic<bool> g_msd_sort{true};  // A/B hook (SetMsdSort)
+void SetMsdSort(bool on) { g_msd_sort.store(on); }
+static bool msd_sort_on() { return g_msd_sort.load(); }
+
 static int64_t radix_sort_min_rows() {
   return knobs::Int("RADIX_SORT_MIN_ROWS", int64_t(1) << 22);
+}
+
+// Keys-only sorts of 8-byte integers (a one-column table): two MSD slot passes over the top digits
+// of image - min, then one LDS sort of every final partition by the bits below them
+// (kernels/seg_sort.hip): the keys cross HBM three times instead of once per 9-bit LSD pass (seven
+// for keys spanning 63 bits).  Every partition must fit the LDS (slot <= seg_sort_capacity()); keys
+// whose top digits are skewed overflow a slot, and the LSD passes sort instead (nullptr).
+static TablePtr radix_sort_keys_msd(const Exec &ex, const TablePtr &t, const Column &kc, uint64_t key_xor,
+                                    uint64_t img_min, uint64_t img_max) {
+  const int64_t n = t->Rows();
+  if (img_max <= img_min || !hip::lds_lane_order_ok(ex.stream)) return nullptr;
+  const int hr = 64 - __builtin_clzll(img_max - img_min);
+  auto slot_for = [](double mean) { return ((int64_t)(mean + 8.0 * std::sqrt(mean) + 64.0) + 7) & ~int64_t(7); };
+  const int64_t cap = hip::seg_sort_capacity();
+  int bits = 11;
+  while (bits < 19 && slot_for((double)n / (double)(int64_t(1) << bits)) > cap) ++bits;
+  const int64_t slot = slot_for((double)n / (double)(int64_t(1) << bits));
+  const int db2 = std::min(9, bits / 2), db1 = bits - db2;
+  if (slot > cap || bits > hr || !hip::radix_slot_eligible(n, 1, db1, db2)) return nullptr;
+  CYLON_PHASE("sort.radix_msd", ex.device);
+  const int64_t nb1 = int64_t(1) << db1, nparts = int64_t(1) << bits, tail = hip::radix_slot_tile_rows();
+  // first pass into (XCD, bucket) slots when the second pass's segment table holds 8 x 2^db1 of them,
+  // else exact (2B keys: 19 bits = 10 + 9)
+  const bool slot1 = hip::radix_slot_first_pass_ok(db1);
+  const int64_t s1 = slot1 ? slot_for((double)n / (double)(8 * nb1)) : 0;
+  at::Tensor ovf = at::zeros({1}, ex.opts(at::kInt));
+  unsigned int *ov = reinterpret_cast<unsigned int *>(ovf.data_ptr<int>());
+  at::Tensor mid = ex.empty_i64(slot1 ? 8 * nb1 * s1 + tail : n), cnt1 = slot1 ? ex.empty_i64(8 * nb1) : at::Tensor();
+  at::Tensor ws = ex.empty_i64(slot1 ? hip::radix_slot_workspace(db1, db2) : hip::radix_rows_pass_workspace(n, db1));
+  hip::radix_sort_msd_first_pass(ptr<int64_t>(kc.data), n, hr, db1, db2, key_xor, img_min, ptr<int64_t>(mid), s1,
+                                 ptr<int64_t>(ws), slot1 ? ptr<int64_t>(cnt1) : nullptr, ov, ex.stream);
+  at::Tensor fin = ex.empty_i64(nparts * slot + tail), counts = ex.empty_i64(nparts);
+  at::Tensor ws2 = ex.empty_i64(hip::radix_slot_workspace(db1, db2));
+  hip::radix_sort_msd_second_pass(ptr<int64_t>(mid), n, hr, db1, db2, img_min, ptr<int64_t>(ws),
+                                  slot1 ? ptr<int64_t>(cnt1) : nullptr, s1, ptr<int64_t>(fin), slot, ptr<int64_t>(ws2),
+                                  ptr<int64_t>(counts), ov, ex.stream);
+  mid = at::Tensor();
+  if (ovf.item<int>() != 0) {  // a partition outgrew its slot: skewed top digits
+    trace::add_counter("sort.radix.msd_slot_overflow", 1);
+    return nullptr;
+  }
+  at::Tensor offs = exclusive_scan(ex, counts);
+  at::Tensor out = at::empty_like(kc.data);
+  hip::seg_sort_local(ptr<int64_t>(fin), ptr<int64_t>(counts), slot, nparts, ptr<int64_t>(offs), img_min, hr - bits,
+                      key_xor, ptr<int64_t>(out), ex.stream);
+  trace::add_counter("sort.radix.msd", 1);
+  return Table::Make(t->GetContext(), {Column(kc.name, kc.type, n, out)});
 }
 
 static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
@@ -171,6 +225,8 @@ static TablePtr radix_sort_table(const TablePtr &t, int col, bool asc) {
                                        raw_in ? nullptr : reinterpret_cast<uint64_t *>(ptr<int64_t>(img)),
                                        ptr<int64_t>(ws2), ex.stream);
   }
+  if (prehist && diff != 0 && t->Columns() == 1 && key_from_image && msd_sort_on())
+    if (TablePtr r = radix_sort_keys_msd(ex, t, kc, key_xor, img_min, img_max)) return r;
   std::vector<at::Tensor> cur{img};
   std::vector<int> widths{8};
   for (int ci = 0; ci < t->Columns(); ++ci) {

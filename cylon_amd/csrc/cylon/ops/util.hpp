@@ -3,6 +3,7 @@
 // allocator (stream ordered, so scratch tensors may be released as soon as the
 // launches that use them are enqueued).
 #pragma once
+#include <functional>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/hip/HIPGuard.h>
@@ -66,10 +67,14 @@ struct RangeSpec {
 // keep_packed != nullptr: validity-style 1-byte columns that were packed 8 per 8-byte word
 // for the passes stay packed -- their slots come back undefined, the words are appended
 // to the result and *keep_packed lists the packed column indices in byte order.
+// prehist (stable hash partitions): called before the first pass with the address of that pass's
+// per-tile digit counts in its workspace and the pass's digit bits; it must fill column 0 (the keys)
+// and those counts (radix_setops.hip setop_row_hash_tiles), which the first pass then does not recount.
+using PrehistFn = std::function<void(int64_t *tile_counts, int digit_bits)>;
 std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> cols, const std::vector<int> &widths,
                                        int bits, at::Tensor *offs, const RangeSpec *range = nullptr,
                                        std::vector<int> *keep_packed = nullptr, bool stable = true,
-                                       const hip::NarrowKeys *nk = nullptr);
+                                       const hip::NarrowKeys *nk = nullptr, const PrehistFn *prehist = nullptr);
 
 // Hash-join partition in slot mode (MSD, two passes, no histogram before the second pass; see
 // kernel_decls.inc radix_slot_rows_pass): partition p holds (*counts)[p] rows at row p * slot.

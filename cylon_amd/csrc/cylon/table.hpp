@@ -163,6 +163,8 @@ std::pair<at::Tensor, at::Tensor> JoinIndices(const TablePtr &left, const TableP
                                               const join::config::JoinConfig &cfg);
 // C27/K16: index row positions matching each label, grouped by label order then row order
 at::Tensor IndexLookup(const std::shared_ptr<CylonContext> &ctx, const Column &index, const Column &labels);
+// A/B hook of the stable hash partitions (ops/radix.cpp): digit bits per pass, 3..10 (default 10)
+void SetPartitionDigitBits(int bits);
 
 // grouping = true: only equal values must end adjacent (list columns then sort by their bytes)
 at::Tensor SortIndices(const TablePtr &t, const std::vector<int> &cols, const std::vector<bool> &ascending,

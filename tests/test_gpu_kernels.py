@@ -193,6 +193,48 @@ def test_lookback_sort_passes_match_stable_torch_sort(gpu_ctx, monkeypatch, case
     assert torch.equal(out["v"], v[idx])
 
 
+@pytest.mark.parametrize("case", ["uniform63", "desc", "ties", "uint64", "skewed", "narrow_span"])
+def test_msd_keys_only_sort_matches_torch(gpu_ctx, monkeypatch, case):
+    """Keys-only int sorts: two MSD slot passes + the LDS segment sort (kernels/seg_sort.hip) vs
+    torch.sort.  Skewed top digits overflow a slot and the LSD passes sort instead; a span narrower
+    than the MSD digits never takes the MSD path."""
+    n = 6_000_000
+    g = torch.Generator(device="cuda").manual_seed(23)
+    dt = torch.int64
+    if case in ("uniform63", "desc"):
+        k = torch.randint(-2**62, 2**62, (n,), generator=g, device="cuda")
+    elif case == "ties":  # ~600k distinct keys spread over 30 bits: runs of ~10 equal keys
+        k = torch.randint(-300000, 300000, (n,), generator=g, device="cuda") * 977
+    elif case == "uint64":
+        k = torch.randint(0, 2**63 - 1, (n,), generator=g, device="cuda").to(torch.uint64)
+        dt = torch.uint64
+    elif case == "skewed":  # 90 % one key: its partition outgrows every slot
+        k = torch.randint(0, 1 << 40, (n,), generator=g, device="cuda")
+        k[torch.rand(n, generator=g, device="cuda") < 0.9] = 123456789
+    else:  # keys in [0, 1024): 10 varying bits, fewer than the 11 MSD bits
+        k = torch.randint(0, 1024, (n,), generator=g, device="cuda")
+    t = Table.from_torch(gpu_ctx, {"k": k})
+    asc = case != "desc"
+    monkeypatch.setenv("CYLON_RADIX_SORT_MIN_ROWS", "1")
+    C.trace_enable(True)
+    C.trace_reset()
+    out = t.sort("k", ascending=asc).to_torch()["k"]
+    torch.cuda.synchronize()
+    c = dict(C.trace_counters())
+    C.trace_enable(False)
+    if dt == torch.uint64:  # torch sorts uint64 as unsigned only via int64 + bias
+        ref = (torch.sort(k.view(torch.int64) ^ (-(2**63)))[0] ^ (-(2**63))).view(torch.uint64)
+        assert torch.equal(out.view(torch.int64), ref.view(torch.int64))
+    else:
+        assert torch.equal(out, torch.sort(k, descending=not asc).values)
+    if case == "skewed":
+        assert c.get("sort.radix.msd_slot_overflow", 0) == 1 and c.get("sort.radix.msd", 0) == 0, c
+    elif case == "narrow_span":
+        assert c.get("sort.radix.msd", 0) == 0, c
+    else:
+        assert c.get("sort.radix.msd", 0) == 1, c
+
+
 @pytest.mark.parametrize("op", ["groupby", "unique", "union"])
 def test_partition_lookback_passes_match_exact(gpu_ctx, monkeypatch, op):
     """Look-back passes of the stable two-pass hash partitions (group-by, set ops): 12M rows need more

@@ -373,8 +373,9 @@ def test_radix_join_narrowed_keys(gpu_ctx, ctx, monkeypatch, case, how):
 @pytest.mark.parametrize("keys", [["s"], ["s", "k"]])
 def test_radix_join_string_keys(gpu_ctx, ctx, monkeypatch, how, keys):
     """String keys on the LDS radix path: the row hash of the key columns is partitioned and matched
-    in LDS, the key bytes are gathered by row number and every output row's keys are compared with
-    rows_equal (a 64-bit collision would fall back).  Against the CPU twin."""
+    in LDS; the fixed-length (13-byte) key strings travel as two int64 word columns (no gather by row
+    number) and every output row's key words are compared (a 64-bit collision would be dropped /
+    fall back).  Against the CPU twin."""
     rng = np.random.default_rng(53)
     n = 1_200_000
     ids_a = rng.integers(0, 900_000, n)
@@ -384,6 +385,7 @@ def test_radix_join_string_keys(gpu_ctx, ctx, monkeypatch, how, keys):
     got, exp, c = _join(gpu_ctx, ctx, a, b, how, keys, monkeypatch)
     assert c.get("join.radix.var_key", 0) >= 1 and c.get("join.radix.hashed_key", 0) == 1, c
     assert c.get("join.radix.hash_collision_fallback", 0) == 0, c
+    assert c.get("join.radix.word_columns", 0) == 2 and c.get("join.radix.var_gather", 0) == 0, c
     assert c["join.radix.rows_out"] == len(exp)
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
 

@@ -25,4 +25,6 @@ pass tcc TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum
 for k in "k_rows_pass<cylon::hip::PartDigitN" k_rj_count k_rj_write k_sl_segments; do
   python3 $R/tools/pmc_summary.py $O/sq $O/sq2 $O/fetch $O/write $O/tcc "$k"
 done > $O/summary.txt 2>&1
+# the raw per-pass CSVs are large: only the summary and the logs travel back
+rm -rf $O/sq $O/sq2 $O/fetch $O/write $O/tcc
 echo pmc done
