@@ -238,6 +238,7 @@ PYBIND11_MODULE(_C, m) {
                     const at::Device device = parse_device(dev);
                     const at::Device comm_device = ct == net::CommType::RCCL ? device : at::Device(at::kCPU);
                     auto comm = std::make_shared<net::ProcessGroupCommunicator>(pg, ct, comm_device);
+                    comm->WarmUp();
                     return CylonContext::InitDistributed(comm, device);
                   }, py::call_guard<py::gil_scoped_release>())
       .def_static("init_native",

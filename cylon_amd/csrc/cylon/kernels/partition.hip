@@ -338,6 +338,133 @@ void gather_var_bytes(const ColView &in, const int64_t *idx, int64_t m, const in
 }
 
 // ---------------------------------------------------------------------------
+// fixed-length strings <-> int64 word columns (ops/join.cpp: strings of L bytes travel through the
+// radix join as ceil(L / 8) words); one row per thread, 8-byte accesses when L % 8 == 0
+// ---------------------------------------------------------------------------
+constexpr int kMaxWords = 8;
+struct WordPtrs {
+  int64_t *w[kMaxWords];
+};
+struct ConstWordPtrs {
+  const int64_t *w[kMaxWords];
+};
+
+__global__ void k_bytes_to_words(const uint8_t *__restrict__ bytes, int64_t n, int L, int W, int aligned8,
+                                 WordPtrs out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint8_t *src = bytes + i * L;
+    if (aligned8) {
+      const uint64_t *s8 = reinterpret_cast<const uint64_t *>(src);
+      for (int j = 0; j < W; ++j) out.w[j][i] = (int64_t)s8[j];
+    } else {
+      for (int j = 0; j < W; ++j) {
+        uint64_t v = 0;
+        for (int b = 0; b < 8 && 8 * j + b < L; ++b) v |= (uint64_t)src[8 * j + b] << (8 * b);
+        out.w[j][i] = (int64_t)v;
+      }
+    }
+  }
+}
+
+__global__ void k_words_to_bytes(ConstWordPtrs in, int64_t n, int L, int W, int aligned8,
+                                 uint8_t *__restrict__ bytes) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint8_t *dst = bytes + i * L;
+    if (aligned8) {
+      uint64_t *d8 = reinterpret_cast<uint64_t *>(dst);
+      for (int j = 0; j < W; ++j) d8[j] = (uint64_t)in.w[j][i];
+    } else {
+      for (int j = 0; j < W; ++j) {
+        const uint64_t v = (uint64_t)in.w[j][i];
+        for (int b = 0; b < 8 && 8 * j + b < L; ++b) dst[8 * j + b] = (uint8_t)(v >> (8 * b));
+      }
+    }
+  }
+}
+
+// bad[i] = 1 where both rows are present and any word differs
+__global__ void k_words_mismatch(ConstWordPtrs a, ConstWordPtrs b, int W, const uint8_t *__restrict__ va,
+                                 const uint8_t *__restrict__ vb, int64_t n, uint8_t *__restrict__ bad) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    bool diff = false;
+    for (int j = 0; j < W; ++j) diff |= a.w[j][i] != b.w[j][i];
+    if (va && !va[i]) diff = false;
+    if (vb && !vb[i]) diff = false;
+    bad[i] = diff ? 1 : 0;
+  }
+}
+
+// mm[0] = min, mm[1] = max of the row lengths offs[i + 1] - offs[i] (mm preset to {~0, 0})
+__global__ void k_len_minmax(const int64_t *__restrict__ offs, int64_t n, unsigned long long *mm) {
+  unsigned long long lo = ~0ull, hi = 0ull;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const unsigned long long l = (unsigned long long)(offs[i + 1] - offs[i]);
+    lo = l < lo ? l : lo;
+    hi = l > hi ? l : hi;
+  }
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    const unsigned long long a = __shfl_xor(lo, d, kWave), b = __shfl_xor(hi, d, kWave);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  if (lane_id() == 0) {
+    atomicMin(&mm[0], lo);
+    atomicMax(&mm[1], hi);
+  }
+}
+
+void var_len_minmax(const int64_t *offs, int64_t n, int64_t *mm, void *stream) {
+  hipStream_t s = as_stream(stream);
+  HIP_CHECK(hipMemsetAsync(mm, 0xff, sizeof(int64_t), s));  // min: all ones
+  HIP_CHECK(hipMemsetAsync(mm + 1, 0, sizeof(int64_t), s));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_len_minmax, dim3(grid_for(n)), dim3(kBlock), 0, s, offs, n,
+                       reinterpret_cast<unsigned long long *>(mm));
+    HIP_LAUNCH_CHECK();
+  }
+}
+
+void bytes_to_words(const uint8_t *bytes, int64_t n, int L, int64_t *const *words, void *stream) {
+  const int W = (L + 7) / 8;
+  CYLON_CHECK(L >= 1 && W <= kMaxWords, Code::Invalid, "string words: length " << L);
+  if (n == 0) return;
+  WordPtrs o{};
+  for (int j = 0; j < W; ++j) o.w[j] = words[j];
+  const int al = (L & 7) == 0 && (reinterpret_cast<uintptr_t>(bytes) & 7) == 0;  // 8-byte accesses
+  hipLaunchKernelGGL(k_bytes_to_words, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), bytes, n, L, W, al, o);
+  HIP_LAUNCH_CHECK();
+}
+
+void words_to_bytes(const int64_t *const *words, int64_t n, int L, uint8_t *bytes, void *stream) {
+  const int W = (L + 7) / 8;
+  CYLON_CHECK(L >= 1 && W <= kMaxWords, Code::Invalid, "string words: length " << L);
+  if (n == 0) return;
+  ConstWordPtrs in{};
+  for (int j = 0; j < W; ++j) in.w[j] = words[j];
+  const int al = (L & 7) == 0 && (reinterpret_cast<uintptr_t>(bytes) & 7) == 0;
+  hipLaunchKernelGGL(k_words_to_bytes, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), in, n, L, W, al, bytes);
+  HIP_LAUNCH_CHECK();
+}
+
+void words_mismatch(const int64_t *const *a, const int64_t *const *b, int W, const uint8_t *va, const uint8_t *vb,
+                    int64_t n, uint8_t *bad, void *stream) {
+  CYLON_CHECK(W >= 1 && W <= kMaxWords, Code::Invalid, "string words: " << W);
+  if (n == 0) return;
+  ConstWordPtrs pa{}, pb{};
+  for (int j = 0; j < W; ++j) {
+    pa.w[j] = a[j];
+    pb.w[j] = b[j];
+  }
+  hipLaunchKernelGGL(k_words_mismatch, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), pa, pb, W, va, vb, n,
+                     bad);
+  HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------
 // shuffle wire narrowing (int64 <-> uint32 offsets from a global base): two
 // rows per thread with 16-byte accesses of the wide side when aligned
 // ---------------------------------------------------------------------------

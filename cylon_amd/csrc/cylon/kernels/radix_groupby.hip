@@ -88,8 +88,9 @@ double distinct_estimate(const int64_t *keys, int64_t n, uint32_t *regs, void *s
 // accumulator kinds
 enum RGKind : int { RG_SUMF = 0, RG_SUMI = 1, RG_MIN = 2, RG_MAX = 3, RG_CNT = 4, RG_M2 = 5 };
 
+constexpr int kRGMaxAcc = 8;
 struct RGArgs {
-  RGAccDesc acc[4];
+  RGAccDesc acc[kRGMaxAcc];
   int nacc;
   int has_m2;  // some accumulator is RG_M2: a second pass over the partition's rows
 };
@@ -300,8 +301,9 @@ static void rg_launch(int grid, hipStream_t s, const int64_t *keys, const int64_
                      gcount, overflow);
 }
 
-// Accumulator planes (oacc holds planes * n words)
-int radix_groupby_planes(int nacc) { return nacc; }
+// Accumulator planes (oacc holds planes * n words): 1-4 accumulators use their own table instance,
+// 5-8 the 8-plane one (idle planes are real counts of their own)
+int radix_groupby_planes(int nacc) { return nacc <= 4 ? nacc : kRGMaxAcc; }
 
 // Every accumulator slot of a table instance is live: A == planes, and a padded slot is a real
 // count (src = the keys) writing its own plane.  Round 3 ran two accumulators in the <3, 2048>
@@ -312,12 +314,12 @@ int radix_groupby_planes(int nacc) { return nacc; }
 // (profiles/r04/rg_agg_fault_isa.txt).  Without runtime slot guards nothing can mis-evaluate.
 void radix_groupby_agg(const int64_t *keys, const int64_t *offs, int64_t nparts, const RGAccDesc *acc, int nacc,
                        int64_t *okeys, uint64_t *oacc, int64_t n, int64_t *gcount, int *overflow, void *stream) {
-  CYLON_CHECK(nacc >= 1 && nacc <= 4, Code::Invalid, "radix group-by: 1 to 4 accumulators");
+  CYLON_CHECK(nacc >= 1 && nacc <= kRGMaxAcc, Code::Invalid, "radix group-by: 1 to 8 accumulators");
   const int A = radix_groupby_planes(nacc);
   RGArgs a;
   a.nacc = A;
   a.has_m2 = 0;
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < kRGMaxAcc; ++j) {
     const bool real = j < nacc;
     a.acc[j].src = real && acc[j].src ? acc[j].src : reinterpret_cast<const uint8_t *>(keys);
     a.acc[j].valid = real ? acc[j].valid : nullptr;
@@ -341,12 +343,13 @@ void radix_groupby_agg(const int64_t *keys, const int64_t *offs, int64_t nparts,
     case 1: rg_launch<1, 4096>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow); break;
     case 2: rg_launch<2, 2048>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow); break;
     case 3: rg_launch<3, 2048>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow); break;
-    default: rg_launch<4, 1024>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow);
+    case 4: rg_launch<4, 1024>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow); break;
+    default: rg_launch<kRGMaxAcc, 1024>(grid, s, keys, offs, nparts, a, okeys, oacc, n, gcount, overflow);
   }
   HIP_LAUNCH_CHECK();
 }
 
-int64_t radix_groupby_slots(int nacc) { return nacc <= 1 ? 4096 : (nacc <= 3 ? 2048 : 1024); }
+int64_t radix_groupby_slots(int nacc) { return nacc <= 1 ? 4096 : (nacc <= 3 ? 2048 : 1024); }  // (5-8: 1024)
 
 void radix_groupby_pack(const int64_t *offs, const int64_t *goff, int64_t nparts, const int64_t *okeys,
                         const uint64_t *oacc, int64_t n, int nacc, int64_t *keys_out, uint64_t *acc_out,

@@ -76,7 +76,9 @@ constexpr int kSHThreads = 512, kSHTile = 8192, kSHItems = kSHTile / kSHThreads;
 
 // NC >= ncols columns held per row; the column sets live in device memory (cols[0] = L, cols[1] = R):
 // their fields are wave-uniform scalar loads, and neither set is copied into registers or scratch
-template <int NC>
+// W8: every column is a non-null 8-byte number -- one unconditional 8-byte load per column, all in
+// flight together (the width switch of load_bits put a wait for each load at its join point)
+template <int NC, bool W8>
 __device__ __forceinline__ uint64_t so_row_hash(const SOColSet *__restrict__ S, int ncols, int64_t i) {
   uint64_t raw[NC];
   uint8_t vb[NC];
@@ -86,9 +88,14 @@ __device__ __forceinline__ uint64_t so_row_hash(const SOColSet *__restrict__ S, 
     vb[c] = 1;
     if (c < ncols) {
       const ColView &col = S->c[c];
-      if (col.kind != static_cast<int>(ValueKind::VAR_BYTES) && col.kind != static_cast<int>(ValueKind::FIXED_BYTES))
-        raw[c] = load_bits(col.data, i, col.width);
-      if (col.valid != nullptr) vb[c] = col.valid[i];
+      if (W8) {
+        raw[c] = reinterpret_cast<const uint64_t *>(col.data)[i];
+      } else {
+        if (col.kind != static_cast<int>(ValueKind::VAR_BYTES) &&
+            col.kind != static_cast<int>(ValueKind::FIXED_BYTES))
+          raw[c] = load_bits(col.data, i, col.width);
+        if (col.valid != nullptr) vb[c] = col.valid[i];
+      }
     }
   }
   uint64_t x = 0x84222325cbf29ce4ULL;
@@ -97,10 +104,10 @@ __device__ __forceinline__ uint64_t so_row_hash(const SOColSet *__restrict__ S, 
     if (c < ncols) {
       const ColView &col = S->c[c];
       uint64_t hv;
-      if (vb[c] == 0) {
+      if (!W8 && vb[c] == 0) {
         hv = 0x5bd1e9955bd1e995ULL;
-      } else if (col.kind == static_cast<int>(ValueKind::VAR_BYTES) ||
-                 col.kind == static_cast<int>(ValueKind::FIXED_BYTES)) {
+      } else if (!W8 && (col.kind == static_cast<int>(ValueKind::VAR_BYTES) ||
+                         col.kind == static_cast<int>(ValueKind::FIXED_BYTES))) {
         hv = so_value_hash(col, i);
       } else {
         uint64_t bits = (uint64_t)extend_bits(raw[c], col.width, col.kind);
@@ -119,7 +126,7 @@ __device__ __forceinline__ uint64_t so_row_hash(const SOColSet *__restrict__ S, 
   return x | 1ull;  // 0 marks an empty LDS slot
 }
 
-template <int NC>
+template <int NC, bool W8>
 __global__ __launch_bounds__(kSHThreads) void k_so_hash_tiles(const SOColSet *__restrict__ cols, int ncols, int64_t nl,
                                                               int64_t n, uint64_t *__restrict__ h, int bits,
                                                               uint32_t dmask, int64_t ntiles,
@@ -130,13 +137,69 @@ __global__ __launch_bounds__(kSHThreads) void k_so_hash_tiles(const SOColSet *__
     for (uint32_t p = threadIdx.x; p < nb; p += kSHThreads) hist[p] = 0u;
     __syncthreads();
     const int64_t r0 = t * kSHTile;
-    for (int u = 0; u < kSHItems; ++u) {
-      const int64_t i = r0 + u * kSHThreads + threadIdx.x;
-      if (i < n) {
-        const bool left = i < nl;
-        const uint64_t x = so_row_hash<NC>(cols + (left ? 0 : 1), ncols, left ? i : i - nl);
-        h[i] = x;
-        if (th != nullptr) atomicAdd(&hist[(uint32_t)(hashing::fmix64(x) >> (64 - bits)) & dmask], 1u);
+    // a tile wholly on one side reads that side's column set through a block-uniform pointer (scalar
+    // loads); only the tile holding row nl chooses per row
+    const int side = r0 + kSHTile <= nl ? 0 : (r0 >= nl ? 1 : 2);
+    auto one = [&](int64_t i, const SOColSet *S, int64_t j) {
+      const uint64_t x = so_row_hash<NC, W8>(S, ncols, j);
+      h[i] = x;
+      if (th != nullptr) atomicAdd(&hist[(uint32_t)(hashing::fmix64(x) >> (64 - bits)) & dmask], 1u);
+    };
+    if (W8 && side < 2) {
+      // 8-byte columns of one side: the column pointers / kinds are block-uniform; four rows' loads of
+      // every column are issued before any of them is hashed (one memory latency per four rows)
+      const SOColSet *S = cols + side;
+      const int64_t jo = side ? nl : 0;
+      const uint64_t *cp[NC];
+      int kind[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        cp[c] = c < ncols ? reinterpret_cast<const uint64_t *>(S->c[c].data) : nullptr;
+        kind[c] = c < ncols ? S->c[c].kind : 0;
+      }
+      constexpr int B = 4;
+      for (int u0 = 0; u0 < kSHItems; u0 += B) {
+        uint64_t raw[B][NC];
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          const int64_t i = r0 + (u0 + q) * kSHThreads + threadIdx.x;
+#pragma unroll
+          for (int c = 0; c < NC; ++c) raw[q][c] = (c < ncols && i < n) ? cp[c][i - jo] : 0ull;
+        }
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          const int64_t i = r0 + (u0 + q) * kSHThreads + threadIdx.x;
+          if (i >= n) continue;
+          uint64_t x = 0x84222325cbf29ce4ULL;
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            if (c >= ncols) continue;
+            uint64_t b = raw[q][c];
+            if (kind[c] == static_cast<int>(ValueKind::FLOAT) &&
+                __longlong_as_double((long long)b) != __longlong_as_double((long long)b))
+              b = 0x7ff8000000000000ull;
+            x = hashing::combine64(x, hashing::fmix64(b));
+          }
+          x |= 1ull;
+          h[i] = x;
+          if (th != nullptr) atomicAdd(&hist[(uint32_t)(hashing::fmix64(x) >> (64 - bits)) & dmask], 1u);
+        }
+      }
+    } else if (side == 0) {
+      for (int u = 0; u < kSHItems; ++u) {
+        const int64_t i = r0 + u * kSHThreads + threadIdx.x;
+        if (i < n) one(i, cols, i);
+      }
+    } else if (side == 1) {
+      for (int u = 0; u < kSHItems; ++u) {
+        const int64_t i = r0 + u * kSHThreads + threadIdx.x;
+        if (i < n) one(i, cols + 1, i - nl);
+      }
+    } else {
+      for (int u = 0; u < kSHItems; ++u) {
+        const int64_t i = r0 + u * kSHThreads + threadIdx.x;
+        if (i < n && i < nl) one(i, cols, i);
+        if (i < n && i >= nl) one(i, cols + 1, i - nl);
       }
     }
     __syncthreads();
@@ -164,13 +227,26 @@ void setop_row_hash_tiles(const ColView *lcols, const ColView *rcols, int ncols,
   const int64_t ntiles = (n + kSHTile - 1) / kSHTile;
   const int grid = (int)std::min<int64_t>(ntiles, (int64_t)kNumCUs * 4);
   const uint32_t dm = (1u << digit_bits) - 1u;
-  if (ncols <= 4)
-    hipLaunchKernelGGL(k_so_hash_tiles<4>, dim3(grid), dim3(kSHThreads), 0, s, d, ncols, nl, n, h, bits, dm, ntiles, th);
-  else if (ncols <= 8)
-    hipLaunchKernelGGL(k_so_hash_tiles<8>, dim3(grid), dim3(kSHThreads), 0, s, d, ncols, nl, n, h, bits, dm, ntiles, th);
-  else
-    hipLaunchKernelGGL(k_so_hash_tiles<kMaxFusedCols>, dim3(grid), dim3(kSHThreads), 0, s, d, ncols, nl, n, h, bits, dm,
+  bool w8 = true;
+  for (int c = 0; c < ncols; ++c)
+    for (const SOColSet &x : hs)
+      w8 &= x.c[c].width == 8 && x.c[c].valid == nullptr && x.c[c].kind != static_cast<int>(ValueKind::VAR_BYTES) &&
+            x.c[c].kind != static_cast<int>(ValueKind::FIXED_BYTES);
+  if (w8 && ncols <= 4)
+    hipLaunchKernelGGL((k_so_hash_tiles<4, true>), dim3(grid), dim3(kSHThreads), 0, s, d, ncols, nl, n, h, bits, dm,
                        ntiles, th);
+  else if (w8 && ncols <= 8)
+    hipLaunchKernelGGL((k_so_hash_tiles<8, true>), dim3(grid), dim3(kSHThreads), 0, s, d, ncols, nl, n, h, bits, dm,
+                       ntiles, th);
+  else if (ncols <= 4)
+    hipLaunchKernelGGL((k_so_hash_tiles<4, false>), dim3(grid), dim3(kSHThreads), 0, s, d, ncols, nl, n, h, bits, dm,
+                       ntiles, th);
+  else if (ncols <= 8)
+    hipLaunchKernelGGL((k_so_hash_tiles<8, false>), dim3(grid), dim3(kSHThreads), 0, s, d, ncols, nl, n, h, bits, dm,
+                       ntiles, th);
+  else
+    hipLaunchKernelGGL((k_so_hash_tiles<kMaxFusedCols, false>), dim3(grid), dim3(kSHThreads), 0, s, d, ncols, nl, n, h,
+                       bits, dm, ntiles, th);
   HIP_LAUNCH_CHECK();
 }
 
@@ -382,7 +458,7 @@ void setop_dedup(const uint64_t *ph, const int64_t *prow, const int64_t *offs, i
 }
 
 // this file's code object is loaded at context creation (preload_device_code), not on first use
-void preload_radix_setops() { preload_code(reinterpret_cast<const void *>(&k_so_hash_tiles<4>)); }
+void preload_radix_setops() { preload_code(reinterpret_cast<const void *>(&k_so_hash_tiles<4, true>)); }
 
 }  // namespace hip
 }  // namespace cylon

@@ -70,10 +70,11 @@ __device__ __forceinline__ void seg_round(const SegRank &R, uint64_t *buf, const
   __syncthreads();
 }
 
-// A partition's keys are uniform over its local bits in the common case: ONE round on the top <= 9
-// local bits leaves buckets of a few keys (mean c / 512), which thread d then insertion-sorts in
-// place (buckets of <= kSegRun keys).  A partition with a larger bucket (clustered low bits) is
-// sorted by full LSD rounds over all its local bits instead.
+// A partition's keys are uniform over its local bits in the common case: two stable rounds on the
+// top <= 18 local bits (lower digit first) leave buckets of a few keys (mean c / 512) already
+// ordered by their next 9 bits, which thread d then insertion-sorts in place (buckets of <= kSegRun
+// keys).  A partition with a larger bucket (clustered low bits) is sorted by full LSD rounds over
+// all its local bits instead.
 constexpr int kSegRun = 48;
 
 __global__ __launch_bounds__(kSegThreads, 2) void k_seg_sort(const uint64_t *__restrict__ in,
@@ -103,6 +104,18 @@ __global__ __launch_bounds__(kSegThreads, 2) void k_seg_sort(const uint64_t *__r
       k[i] = r < c ? src[r] : 0ull;
     }
     if (topb > 0) {
+      if (local_bits > kSegBits) {  // the 9 bits below the top ones first (LSD), then the top ones:
+        // buckets then hold keys already ordered by their next 9 bits, so the insertion sort below
+        // mostly compares (a single round left ~7.5 unordered keys per bucket: the wave's largest
+        // bucket, ~17 keys, cost ~150 LDS steps)
+        const int lb = local_bits - kSegBits < kSegBits ? local_bits - kSegBits : kSegBits;
+        seg_round(R, buf, k, c, rbase, wave, sub, local_bits - kSegBits - lb, (1u << lb) - 1u);
+#pragma unroll
+        for (int i = 0; i < kSegItems; ++i) {
+          const int r = rbase + i * kWave;
+          if (r < c) k[i] = buf[r];
+        }
+      }
       seg_round(R, buf, k, c, rbase, wave, sub, local_bits - topb, (1u << topb) - 1u);
       if (threadIdx.x == 0) smax = 0u;
       __syncthreads();
@@ -114,8 +127,8 @@ __global__ __launch_bounds__(kSegThreads, 2) void k_seg_sort(const uint64_t *__r
       }
       if (lane == 0) atomicMax(&smax, m);
       __syncthreads();
-      if (local_bits <= kSegBits) {
-        // the round sorted every local bit
+      if (local_bits <= 2 * kSegBits) {
+        // the rounds sorted every local bit
       } else if (smax <= (uint32_t)kSegRun) {
         const uint32_t b = toff[threadIdx.x], e = b + run;
         for (uint32_t i = b + 1; i < e; ++i) {  // images compare as unsigned integers

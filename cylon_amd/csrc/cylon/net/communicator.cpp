@@ -72,6 +72,21 @@ ProcessGroupCommunicator::~ProcessGroupCommunicator() = default;
 
 void ProcessGroupCommunicator::Finalize() { pg_.reset(); }
 
+void ProcessGroupCommunicator::WarmUp() {
+  if (type_ != CommType::RCCL || !device_.is_cuda()) return;
+  constexpr int64_t kBytes = int64_t(4) << 20;  // per peer: large enough to use the p2p channels
+  at::Tensor s = at::zeros({world_ * kBytes}, at::TensorOptions().dtype(at::kByte).device(device_));
+  at::Tensor r = at::empty_like(s);
+  std::vector<at::Tensor> in, out;
+  for (int p = 0; p < world_; ++p) {
+    in.push_back(s.slice(0, p * kBytes, (p + 1) * kBytes));
+    out.push_back(r.slice(0, p * kBytes, (p + 1) * kBytes));
+  }
+  wait_work(pg().alltoall(out, in));
+  r.sum().item<int64_t>();  // (completes on the host: the connections exist from here on)
+  trace::add_counter("comm.warmup", 1);
+}
+
 c10d::ProcessGroup &ProcessGroupCommunicator::pg() const {
   CYLON_CHECK(pg_, Code::Invalid, "communicator used after finalize()");
   return *pg_;

@@ -208,6 +208,10 @@ class ProcessGroupCommunicator : public Communicator {
   // drops the ProcessGroup reference, so that torch.distributed.destroy_process_group()
   // tears the group down deterministically (not at interpreter exit)
   void Finalize() override;
+  // RCCL: one grouped send / receive with every peer (and self) at context creation, so the first
+  // shuffle of a job does not pay the communicator's lazy p2p connection setup while its transfers
+  // should be overlapping compute (the first step's overlap, profiles/r05/first_step_overlap.txt)
+  void WarmUp();
   at::Device comm_device() const { return device_; }
 
  private:

@@ -441,8 +441,8 @@ static TablePtr radix_groupby(const TablePtr &t, const std::vector<int> &keys, c
       default: return nullptr;
     }
   }
-  // the LDS aggregation kernels are instantiated with exactly nacc accumulator slots (1..4)
-  if (plan.empty() || plan.size() > 4) return nullptr;
+  // the LDS aggregation kernels are instantiated with 1, 2, 3, 4 or 8 accumulator planes
+  if (plan.empty() || plan.size() > 8) return nullptr;
   Exec ex(t->device());
   GroupKey gkey;
   if (!group_key(ex, t, keys, gkey)) return nullptr;

@@ -1281,36 +1281,38 @@ static TablePtr radix_join_chunked(const Exec &ex, const TablePtr &l, const Tabl
 // as ceil(L / 8) int64 word columns -- moved by the partition passes and the write kernel like any
 // payload -- instead of a row number and a gather by it afterwards (random reads at ~50 G accesses/s:
 // a 200M x 200M join on 16-byte string keys spent 26 of its 62 ms gathering, profiles/r05).
-static int64_t fixed_var_len(const Column &c) {  // L, or -1
+static int64_t fixed_var_len(const Exec &ex, const Column &c) {  // L, or -1
   if (c.nullable() || !(c.type.type == Type::STRING || c.type.type == Type::BINARY) || c.length == 0) return -1;
-  at::Tensor o = c.offsets.slice(0, 0, c.length + 1);
-  at::Tensor d = o.slice(0, 1, c.length + 1) - o.slice(0, 0, c.length);
-  at::Tensor mm = at::stack({d.min(), d.max()}).cpu();
-  const int64_t lo = mm[0].item<int64_t>(), hi = mm[1].item<int64_t>();
+  at::Tensor mm = ex.empty_i64(2);
+  hip::var_len_minmax(ptr<int64_t>(c.offsets), c.length, ptr<int64_t>(mm), ex.stream);
+  at::Tensor h = mm.cpu();
+  const int64_t lo = h[0].item<int64_t>(), hi = h[1].item<int64_t>();
   return lo == hi && lo > 0 && lo <= 64 ? lo : -1;
 }
 
-static std::vector<at::Tensor> var_to_words(const Column &c, int64_t L) {
+static std::vector<at::Tensor> var_to_words(const Exec &ex, const Column &c, int64_t L) {
   const int64_t n = c.length, W = (L + 7) / 8;
   const int64_t o0 = c.offsets.slice(0, 0, 1).cpu().item<int64_t>();
-  at::Tensor m = c.data.view(at::kByte).slice(0, o0, o0 + n * L).view({n, L});
-  if (8 * W != L) m = at::constant_pad_nd(m, {0, 8 * W - L}, 0);
-  at::Tensor w = m.contiguous().view(at::kLong);  // [n, W]
   std::vector<at::Tensor> out;
-  for (int64_t j = 0; j < W; ++j) out.push_back(w.select(1, j).contiguous());
+  std::vector<int64_t *> wp;
+  for (int64_t j = 0; j < W; ++j) {
+    out.push_back(ex.empty_i64(n));
+    wp.push_back(ptr<int64_t>(out.back()));
+  }
+  hip::bytes_to_words(ptr<uint8_t>(c.data) + o0, n, (int)L, wp.data(), ex.stream);
   return out;
 }
 
-static Column words_to_var(const std::string &name, const DataType &type, const std::vector<Column> &wc, int64_t L) {
-  const int64_t m = wc[0].length, W = (int64_t)wc.size();
-  std::vector<at::Tensor> ws;
-  for (const auto &c : wc) ws.push_back(c.data.slice(0, 0, m));
-  at::Tensor b = at::stack(ws, 1).view(at::kByte).view({m, 8 * W});  // [m, 8 W]
-  if (8 * W != L) b = b.slice(1, 0, L);
-  at::Tensor bytes = b.contiguous().view({m * L});
-  at::Tensor offs = at::arange(0, (m + 1) * L, L, wc[0].data.options().dtype(at::kLong));
+static Column words_to_var(const Exec &ex, const std::string &name, const DataType &type,
+                           const std::vector<Column> &wc, int64_t L) {
+  const int64_t m = wc[0].length;
+  std::vector<const int64_t *> wp;
+  for (const auto &c : wc) wp.push_back(ptr<int64_t>(c.data));
+  at::Tensor bytes = ex.empty_bytes(std::max<int64_t>(1, m * L));
+  hip::words_to_bytes(wp.data(), m, (int)L, ptr<uint8_t>(bytes), ex.stream);
+  at::Tensor offs = at::arange(0, (m + 1) * L, L, ex.opts(at::kLong));
   // (a null row of an outer join keeps L zero bytes under its null: Arrow allows any length there)
-  return Column(name, type, m, bytes, offs, wc[0].validity);
+  return Column(name, type, m, bytes.slice(0, 0, m * L), offs, wc[0].validity);
 }
 
 // LDS radix join of any large device join (every type, one or several keys, var-width payload
@@ -1352,14 +1354,14 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
       const Column &col = t->column(c);
       if (ckey && std::find(keys.begin(), keys.end(), c) != keys.end()) continue;
       if (var_col(col)) {
-        const int64_t L = fixed_var_len(col);
+        const int64_t L = fixed_var_len(ex, col);
         if (L < 0) {
           var = true;
           continue;
         }
         wlen[c] = L;
         pos[c] = (int)cols.size();
-        std::vector<at::Tensor> w = var_to_words(col, L);
+        std::vector<at::Tensor> w = var_to_words(ex, col, L);
         for (size_t j = 0; j < w.size(); ++j)
           cols.emplace_back("__cylon_w" + std::to_string(c) + "_" + std::to_string(j), DataType(Type::INT64),
                             t->Rows(), w[j]);
@@ -1404,7 +1406,7 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
         const int64_t L = wlen[c];
         std::vector<Column> wc;
         for (int64_t j = 0; j < (L + 7) / 8; ++j) wc.push_back(out->column(first + pos[c] + (int)j));
-        cols[c] = words_to_var(prefix + orig->column(c).name, orig->column(c).type, wc, L);
+        cols[c] = words_to_var(ex, prefix + orig->column(c).name, orig->column(c).type, wc, L);
       } else {
         cols[c] = out->column(first + pos[c]);
       }
@@ -1460,17 +1462,21 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
   if (!words) return drop_false_matches(res, cfg, left->Columns());
   const int64_t m = out->Rows();
   if (m == 0) return res;
-  at::Tensor bad = at::zeros({m}, ex.opts(at::kBool));
+  std::vector<const int64_t *> aw, bw;
   const int rfirst = lp->Columns();
   for (size_t i = 0; i < lc.size(); ++i)
-    for (int64_t j = 0; j < (lwlen[lc[i]] + 7) / 8; ++j)
-      bad.logical_or_(out->column(lpos[lc[i]] + (int)j).data.slice(0, 0, m) !=
-                      out->column(rfirst + rpos[rc[i]] + (int)j).data.slice(0, 0, m));
+    for (int64_t j = 0; j < (lwlen[lc[i]] + 7) / 8; ++j) {
+      aw.push_back(ptr<int64_t>(out->column(lpos[lc[i]] + (int)j).data));
+      bw.push_back(ptr<int64_t>(out->column(rfirst + rpos[rc[i]] + (int)j).data));
+    }
+  if (aw.size() > 8) return drop_false_matches(res, cfg, left->Columns());
   const Column &lw = out->column(lpos[lc[0]]), &rw = out->column(rfirst + rpos[rc[0]]);
-  if (lw.nullable()) bad.logical_and_(lw.validity.slice(0, 0, m).to(at::kBool));  // both sides present only
-  if (rw.nullable()) bad.logical_and_(rw.validity.slice(0, 0, m).to(at::kBool));
-  if (!bad.any().item<bool>()) return res;
-  const int64_t nbad = bad.sum().item<int64_t>();
+  at::Tensor badb = ex.empty_u8(m);  // both sides present and some key word differs
+  hip::words_mismatch(aw.data(), bw.data(), (int)aw.size(), lw.nullable() ? ptr<uint8_t>(lw.validity) : nullptr,
+                      rw.nullable() ? ptr<uint8_t>(rw.validity) : nullptr, m, ptr<uint8_t>(badb), ex.stream);
+  const int64_t nbad = badb.sum(at::kLong).item<int64_t>();
+  if (nbad == 0) return res;
+  at::Tensor bad = badb.to(at::kBool);
   if (jt != JoinType::INNER) {
     trace::add_counter("join.radix.hash_collision_fallback", nbad);
     return nullptr;

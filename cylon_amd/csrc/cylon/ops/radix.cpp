@@ -216,14 +216,30 @@ std::vector<at::Tensor> RadixPartitionSlotted(const Exec &ex, std::vector<at::Te
   at::Tensor cnt1 = slot1 ? ex.empty_i64(8 * nb1) : at::Tensor();
   *overflow = at::zeros({1}, ex.opts(at::kInt));
   unsigned int *ovf = reinterpret_cast<unsigned int *>(overflow->data_ptr<int>());
+  // The first pass's output (freed when the second pass is done) is ONE allocation carved into its
+  // columns: the caching allocator then splits that cached block for the join's output columns.
+  // Column-sized blocks were each ~1 % smaller than an output column (slot padding 1.6 % vs the
+  // output estimate's 2 % slack), so the 1B x 1B join's output reserved 25 GB of fresh memory next to
+  // 28 GB of unusable cached blocks (peak reserved 207 GB for 181 GB allocated).
   std::vector<at::Tensor> mid;
   std::vector<const uint8_t *> in;
   std::vector<uint8_t *> out;
-  for (const at::Tensor &x : cur) {
-    mid.push_back(nk && mid.empty() ? at::empty({rows1}, ex.opts(at::kInt))
-                                    : (x.defined() ? at::empty({rows1}, x.options()) : ex.empty_i64(rows1)));
-    in.push_back(x.defined() ? reinterpret_cast<const uint8_t *>(x.data_ptr()) : nullptr);
-    out.push_back(reinterpret_cast<uint8_t *>(mid.back().data_ptr()));
+  {
+    std::vector<at::ScalarType> dt;
+    std::vector<int64_t> at_byte;
+    int64_t total = 0;
+    for (const at::Tensor &x : cur) {
+      dt.push_back(nk && dt.empty() ? at::kInt : (x.defined() ? x.scalar_type() : at::kLong));
+      at_byte.push_back(total);
+      total += (rows1 * (int64_t)c10::elementSize(dt.back()) + 255) & ~int64_t(255);
+    }
+    at::Tensor block = ex.empty_bytes(total);
+    for (size_t c = 0; c < cur.size(); ++c) {
+      const int64_t es = (int64_t)c10::elementSize(dt[c]);
+      mid.push_back(block.slice(0, at_byte[c], at_byte[c] + rows1 * es).view(dt[c]));
+      in.push_back(cur[c].defined() ? reinterpret_cast<const uint8_t *>(cur[c].data_ptr()) : nullptr);
+      out.push_back(reinterpret_cast<uint8_t *>(mid.back().data_ptr()));
+    }
   }
   if (slot1) {
     for (size_t c = 0; c < cur.size(); ++c)  // (the slot pass reads every column: row ids made here)

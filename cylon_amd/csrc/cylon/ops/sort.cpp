@@ -148,11 +148,15 @@ static TablePtr radix_sort_keys_msd(const Exec &ex, const TablePtr &t, const Col
   const int64_t n = t->Rows();
   if (img_max <= img_min || !hip::lds_lane_order_ok(ex.stream)) return nullptr;
   const int hr = 64 - __builtin_clzll(img_max - img_min);
+  // the keys fill [0, span) of the digits' [0, 2^hr): a bucket of an occupied range holds 1 / fill
+  // times the mean (keys in [-3e6, 3e6) x 977 span 33 bits at fill 0.68)
+  const double fill = std::max(0.5, (double)(img_max - img_min) / std::ldexp(1.0, hr));
   auto slot_for = [](double mean) { return ((int64_t)(mean + 8.0 * std::sqrt(mean) + 64.0) + 7) & ~int64_t(7); };
   const int64_t cap = hip::seg_sort_capacity();
+  auto mean_of = [&](int64_t buckets) { return (double)n / ((double)buckets * fill); };
   int bits = 11;
-  while (bits < 19 && slot_for((double)n / (double)(int64_t(1) << bits)) > cap) ++bits;
-  const int64_t slot = slot_for((double)n / (double)(int64_t(1) << bits));
+  while (bits < 19 && slot_for(mean_of(int64_t(1) << bits)) > cap) ++bits;
+  const int64_t slot = slot_for(mean_of(int64_t(1) << bits));
   const int db2 = std::min(9, bits / 2), db1 = bits - db2;
   if (slot > cap || bits > hr || !hip::radix_slot_eligible(n, 1, db1, db2)) return nullptr;
   CYLON_PHASE("sort.radix_msd", ex.device);
@@ -160,7 +164,7 @@ static TablePtr radix_sort_keys_msd(const Exec &ex, const TablePtr &t, const Col
   // first pass into (XCD, bucket) slots when the second pass's segment table holds 8 x 2^db1 of them,
   // else exact (2B keys: 19 bits = 10 + 9)
   const bool slot1 = hip::radix_slot_first_pass_ok(db1);
-  const int64_t s1 = slot1 ? slot_for((double)n / (double)(8 * nb1)) : 0;
+  const int64_t s1 = slot1 ? slot_for(mean_of(8 * nb1)) : 0;
   at::Tensor ovf = at::zeros({1}, ex.opts(at::kInt));
   unsigned int *ov = reinterpret_cast<unsigned int *>(ovf.data_ptr<int>());
   at::Tensor mid = ex.empty_i64(slot1 ? 8 * nb1 * s1 + tail : n), cnt1 = slot1 ? ex.empty_i64(8 * nb1) : at::Tensor();

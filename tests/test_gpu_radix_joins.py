@@ -230,6 +230,22 @@ def _groupby_both(T, keys, aggs, monkeypatch):
     return res, counters
 
 
+@pytest.mark.parametrize("case", ["six_planes", "eight_planes"])
+def test_radix_groupby_many_accumulators(gpu_ctx, monkeypatch, case):
+    """5-8 accumulator planes (the 8-plane LDS table; idle planes are counts of their own): sums,
+    means, min / max and VAR / STD over three columns -- against the CPU twin and the global path."""
+    rng = np.random.default_rng(14)
+    n = 500_000
+    t = pa.table({"k": rng.integers(0, 40_000, n), "x": rng.standard_normal(n) * 10.0,
+                  "y": pa.array(rng.integers(-1000, 1000, n), mask=rng.random(n) < 0.03),
+                  "z": rng.random(n)})
+    T = Table(t, gpu_ctx)
+    aggs = ({"x": ["sum", "var"], "y": ["max", "mean"]} if case == "six_planes"
+            else {"x": ["std", "min"], "y": ["mean", "max"], "z": ["sum"]})
+    res, cnt = _groupby_both(T, ["k"], aggs, monkeypatch)
+    assert cnt[0].get("groupby.radix.groups", 0) == len(res[0]), cnt[0]
+
+
 @pytest.mark.parametrize("case", ["var_std", "two_keys", "float_key", "two_keys_var", "two_keys_nulls"])
 def test_radix_groupby_extended(gpu_ctx, monkeypatch, case):
     """VAR / STDDEV through the M2 accumulator (second in-block pass over a partition's rows), two

@@ -2,7 +2,7 @@
 host was inside while the compute stream sat idle (the first-step overlap question: transfers in
 flight, no compute kernel to overlap them with).
 
-  python tools/api_gap_report.py <results.db> [transfer substring, default rcclGenericKernel] [steps]
+  python tools/api_gap_report.py <results.db> [transfer substring, default rcclGenericKernel] [steps] [skip]
 
 Steps are found as in overlap_report.py (transfer kernels split into `steps` equal groups).  For
 every step: the HIP API calls by total time, the longest single calls, and every gap > 2 ms
@@ -20,6 +20,7 @@ def main():
     db = sys.argv[1]
     pat = sys.argv[2] if len(sys.argv) > 2 else "rcclGenericKernel"
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    skip = int(sys.argv[4]) if len(sys.argv) > 4 else 0  # leading transfers (the context's warm-up exchange)
     c = sqlite3.connect(db)
     ks = c.execute("select name, start, end from kernels order by start").fetchall()
     api = c.execute("select name, start, end from regions order by start").fetchall()
@@ -30,7 +31,7 @@ def main():
         print("no kernels")
         return
     t0 = ks[0][1]
-    xfer = [k for k in ks if pat in (k[0] or "")]
+    xfer = [k for k in ks if pat in (k[0] or "")][skip:]
     work = [k for k in ks if pat not in (k[0] or "") and "rocclr" not in (k[0] or "")]
     per = max(1, len(xfer) // steps)
     print(f"{len(ks)} kernels, {len(api)} HIP API calls, {len(xfer)} transfer kernels ({pat})")

@@ -1,7 +1,9 @@
 """Overlap of transfer kernels with compute kernels in a rocprofv3 kernel trace (results.db):
 for every transfer-kernel interval, the compute kernels that ran while it was in flight.
 
-  python tools/overlap_report.py <results.db> [transfer substring, default k_spin_delay] [steps]
+  python tools/overlap_report.py <results.db> [transfer substring, default k_spin_delay] [steps] [skip]
+
+skip: leading transfer kernels to ignore (1 for a distributed context's RCCL warm-up exchange).
 
 steps: the trace holds that many equal steps (e.g. 2 for --warmup 1 --steps 1): the transfers are
 split into that many consecutive groups and each group's overlap is reported (the first step also
@@ -18,12 +20,12 @@ def short(n):
     return (n or "?").split("(")[0].replace("void ", "").replace("cylon::hip::", "")[:48]
 
 
-def report(db, pat="k_spin_delay", steps=1):
+def report(db, pat="k_spin_delay", steps=1, skip=0):
     c = sqlite3.connect(db)
     cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
     name = "kernel_name" if "kernel_name" in cols else "name"
     rows = c.execute(f"select {name}, start, end from kernels order by start").fetchall()
-    xfer = [(n, s, e) for n, s, e in rows if pat in (n or "")]
+    xfer = [(n, s, e) for n, s, e in rows if pat in (n or "")][skip:]  # skip: the context's warm-up exchange
     work = [(n, s, e) for n, s, e in rows if pat not in (n or "") and "rocclr" not in (n or "")]
     out = [f"{len(xfer)} transfer kernels ({pat}), {len(work)} compute kernels"]
     total_ov = 0
@@ -51,4 +53,4 @@ def report(db, pat="k_spin_delay", steps=1):
 
 if __name__ == "__main__":
     print(report(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "k_spin_delay",
-                 int(sys.argv[3]) if len(sys.argv) > 3 else 1))
+                 int(sys.argv[3]) if len(sys.argv) > 3 else 1, int(sys.argv[4]) if len(sys.argv) > 4 else 0))
