@@ -1772,6 +1772,33 @@ static void slot_rows_pass(const Digit &dg, int64_t n, int first_bits, int secon
   }
 }
 
+// ---- sampled partition histogram (join slot-mode decision): hist[part] += 1 for keys i = k * stride
+template <class Digit>
+__global__ void k_part_sample(Digit dg, int64_t n, int64_t stride, uint32_t *__restrict__ hist) {
+  dg.init();
+  const int64_t m = (n + stride - 1) / stride;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += step)
+    atomicAdd(&hist[dg(k * stride)], 1u);
+}
+
+void radix_part_sample(const int64_t *keys, int64_t n, int bits, int64_t stride, uint32_t *hist,
+                       const NarrowKeys *nk, void *stream) {
+  CYLON_CHECK(bits >= 1 && bits <= 24 && stride >= 1, Code::Invalid, "partition sample: " << bits << " bits");
+  hipStream_t s = as_stream(stream);
+  HIP_CHECK(hipMemsetAsync(hist, 0, sizeof(uint32_t) << bits, s));
+  const int64_t m = (n + stride - 1) / stride;
+  if (m == 0) return;
+  const uint32_t mask = (uint32_t)((int64_t(1) << bits) - 1);
+  if (nk && nk->base_src)
+    hipLaunchKernelGGL(k_part_sample<PartDigitN>, dim3(grid_for(m)), dim3(kBlock), 0, s,
+                       PartDigitN{keys, 0, nk->base_src, nk->bad, bits, 0, mask, 0}, n, stride, hist);
+  else
+    hipLaunchKernelGGL(k_part_sample<PartDigit>, dim3(grid_for(m)), dim3(kBlock), 0, s,
+                       PartDigit{keys, bits, 0, mask}, n, stride, hist);
+  HIP_LAUNCH_CHECK();
+}
+
 // MSD passes of a keys-only sort (seg_sort.hip sorts each final partition in LDS): the first takes
 // bits [hr - db1, hr) of image - sub from the raw keys and stores the images (key ^ key_xor) -- into
 // (XCD, bucket) slots when 8 x 2^db1 segments fit the second pass's table (slot > 0), else exactly

@@ -490,8 +490,32 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   {
     CYLON_PHASE("join.radix.partition", ex.device);
     const hip::NarrowKeys *nkp = narrow ? &nk : nullptr;
-    L = radix_partition(ex, left, lk, bits, nullptr, slot_of(nl), nkp);
-    R = radix_partition(ex, right, rk, bits, nullptr, slot_of(nr), nkp);
+    // A side with a hot partition would overflow a slot and repartition exactly after both slot
+    // passes (1B x 1B with 16 build keys x 200k duplicates: +48 ms): a histogram of ~4M sampled keys
+    // (every stride-th) finds a partition far above the mean first, and that side starts exact.
+    int64_t sl = slot_of(nl), sr = slot_of(nr);
+    if ((sl || sr) && std::max(nl, nr) >= (int64_t(1) << 24)) {
+      auto sample = [&](const at::Tensor &k, int64_t rows, at::Tensor &h, int64_t &stride) {
+        stride = std::max<int64_t>(1, rows >> 22);
+        h = at::empty({nparts}, ex.opts(at::kInt));
+        hip::radix_part_sample(ptr<int64_t>(k), rows, bits, stride, reinterpret_cast<uint32_t *>(h.data_ptr<int>()),
+                               nkp, ex.stream);
+      };
+      at::Tensor hl, hr;
+      int64_t stl = 1, str = 1;
+      sample(lk, nl, hl, stl);
+      sample(rk, nr, hr, str);
+      at::Tensor mx = at::stack({hl.max(), hr.max()}).cpu();
+      auto hot = [&](int64_t m, int64_t rows, int64_t stride) {
+        const double mean = (double)((rows + stride - 1) / stride) / (double)nparts;
+        return (double)m > 4.0 * mean + 32.0;
+      };
+      if (sl && hot(mx[0].item<int>(), nl, stl)) sl = 0;
+      if (sr && hot(mx[1].item<int>(), nr, str)) sr = 0;
+      if (!sl || !sr) trace::add_counter("join.radix.sampled_skew_sides", (sl ? 0 : 1) + (sr ? 0 : 1));
+    }
+    L = radix_partition(ex, left, lk, bits, nullptr, sl, nkp);
+    R = radix_partition(ex, right, rk, bits, nullptr, sr, nkp);
     if (L.slot || R.slot || narrow) {  // a side whose partition outgrew a slot is partitioned exactly
       at::Tensor z = at::zeros({}, ex.opts(at::kInt));
       at::Tensor f = at::stack({L.slot ? L.overflow[0] : z, R.slot ? R.overflow[0] : z,
