@@ -200,11 +200,30 @@ CylonContext::CylonContext(bool distributed) : distributed_(distributed) {}
 // no pass allocates or synchronises for it (and stream capture of a pass stays possible), and
 // load every kernel code object (a first launch inside a pipelined join blocked the host for up to
 // 40 ms while its transfers ran without compute to overlap)
+// PyTorch's own device kernels are loaded on first launch too (an 11 ms stall before the first
+// compare_scalar of a pipelined join's first step): the ATen ops of the operator layer's host logic
+// run once on a few rows here
+static void warm_aten(const at::Device &device) {
+  const auto o = at::TensorOptions().device(device);
+  at::Tensor a = at::arange(4096, o.dtype(at::kLong)), b = a.flip(0);
+  at::Tensor m = a > 7, e = a.eq(b), l = at::logical_or(m, e).logical_and(a < 4000).logical_not();
+  at::Tensor u8 = m.to(at::kByte), i32 = a.to(at::kInt), f = a.to(at::kDouble);
+  at::Tensor idx = m.nonzero().flatten();
+  at::Tensor g = a.index_select(0, idx), w = at::where(m, a, b);
+  at::Tensor st = at::stack({a.sum(), a.max(), a.min(), u8.sum(at::kLong), l.any().to(at::kLong), i32.max().to(at::kLong),
+                             g.sum(), w.max(), f.sum().to(at::kLong), at::cat({a, b}).sum(), a.cumsum(0)[4095],
+                             (a * 3 + b).sum(), at::bincount(i32.remainder(17)).sum()});
+  (void)st.cpu();
+}
+
 static void warm_device(const at::Device &device) {
   if (!device.is_cuda()) return;
   c10::hip::HIPGuard guard(device.index());
   static std::once_flag loaded[64];
-  std::call_once(loaded[device.index() & 63], [] { hip::preload_device_code(); });
+  std::call_once(loaded[device.index() & 63], [&device] {
+    hip::preload_device_code();
+    warm_aten(device);
+  });
   hip::lds_lane_order_ok(reinterpret_cast<void *>(c10::hip::getCurrentHIPStream(device.index()).stream()));
 }
 

@@ -72,8 +72,9 @@ struct PartDigitN {
   }
   __device__ __forceinline__ bool too_wide(uint64_t kv) const { return !kin4 && (kv - (uint64_t)base) > 0xffffffffull; }
   __device__ __forceinline__ void report_bad() const { atomicOr(bad, 1u); }
-  __device__ __forceinline__ uint32_t of_key(int64_t k) const {
-    return bits == 0 ? 0u : ((hashing::fmix32((uint32_t)narrow((uint64_t)k)) >> (32 - bits)) >> shift) & mask;
+  __device__ __forceinline__ uint32_t of_key(int64_t k) const { return of_offset((uint32_t)narrow((uint64_t)k)); }
+  __device__ __forceinline__ uint32_t of_offset(uint32_t off) const {
+    return bits == 0 ? 0u : ((hashing::fmix32(off) >> (32 - bits)) >> shift) & mask;
   }
   __device__ __forceinline__ uint32_t operator()(int64_t i) const { return of_key((int64_t)key_at(i)); }
 };
@@ -487,11 +488,23 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
   uint16_t *mycnt = wcnt + wave * nbuckets;
   const int wrow = wave * kWave * kRPItems;
 
-  uint64_t kv[kRPItems];  // keys of the current tile (column 0)
+  // keys of the current tile (column 0); narrowed digits hold the uint32 offset from the load on
+  // (8 fewer VGPRs in a kernel that spills at the 128-VGPR limit)
+  using KVT = typename std::conditional<Digit::kNarrow, uint32_t, uint64_t>::type;
+  KVT kv[kRPItems];
+  auto load_key = [&](int64_t i) -> KVT {
+    const uint64_t raw = digit.key_at(i);
+    if constexpr (Digit::kNarrow) {
+      narrow_bad |= digit.too_wide(raw);
+      return (KVT)digit.narrow(raw);
+    } else {
+      return (KVT)raw;
+    }
+  };
 #pragma unroll
   for (int k = 0; k < kRPItems; ++k) {
     const int64_t i = begin + wrow + k * kWave + lane;
-    if (i < (SLOT ? s_tend[0] : end)) kv[k] = digit.key_at(i);
+    if (i < (SLOT ? s_tend[0] : end)) kv[k] = load_key(i);
   }
   for (int64_t tile = begin, next = 0; tile < end; tile = next) {
     next = tile + TILE;
@@ -502,8 +515,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
     for (int k = 0; k < kRPItems; ++k) {
       const bool act = wrow + k * kWave + lane < cnt;
-      pl[k] = act ? digit.of_key((int64_t)kv[k]) : 0xffffffffu;
-      if (Digit::kNarrow) narrow_bad |= act && digit.too_wide(kv[k]);
+      if constexpr (Digit::kNarrow) pl[k] = act ? digit.of_offset(kv[k]) : 0xffffffffu;
+      else pl[k] = act ? digit.of_key((int64_t)kv[k]) : 0xffffffffu;
     }
     if (STABLE) {
       for (uint32_t q = threadIdx.x; q < WAVES * nbuckets; q += blockDim.x) wcnt[q] = 0;
@@ -639,10 +652,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
         if (!SLOT) s_next = xt_claim(lb, xhome, TILE, n);
       }
       const bool n4 = Digit::kNarrow && c == 0;  // column 0 as the uint32 offset
-      if (n4) {
+      if (n4) {  // (v holds the narrowed offsets already)
 #pragma unroll
         for (int k = 0; k < kRPItems; ++k)
-          if (pl[k] != 0xffffffffu) stw<false>(st, pl[k], 4, digit.narrow(v[k]));
+          if (pl[k] != 0xffffffffu) stw<false>(st, pl[k], 4, v[k] & 0xffffffffull);
       } else {
 #pragma unroll
         for (int k = 0; k < kRPItems; ++k)
@@ -665,7 +678,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
         for (int k = 0; k < kRPItems; ++k) {
           const int64_t i = next + wrow + k * kWave + lane;
-          if (i < (SLOT ? s_tend[par ^ 1] : end)) kv[k] = digit.key_at(i);
+          if (i < (SLOT ? s_tend[par ^ 1] : end)) kv[k] = load_key(i);
         }
       }
       if (kNdDigit<Digit> && c == 0 && cols.nd_out != nullptr) {  // sorts, stable hash partitions
