@@ -491,12 +491,12 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     CYLON_PHASE("join.radix.partition", ex.device);
     const hip::NarrowKeys *nkp = narrow ? &nk : nullptr;
     // A side with a hot partition would overflow a slot and repartition exactly after both slot
-    // passes (1B x 1B with 16 build keys x 200k duplicates: +48 ms): a histogram of ~4M sampled keys
+    // passes (1B x 1B with 16 build keys x 200k duplicates: +48 ms): a histogram of ~1M sampled keys
     // (every stride-th) finds a partition far above the mean first, and that side starts exact.
     int64_t sl = slot_of(nl), sr = slot_of(nr);
     if ((sl || sr) && std::max(nl, nr) >= (int64_t(1) << 24)) {
       auto sample = [&](const at::Tensor &k, int64_t rows, at::Tensor &h, int64_t &stride) {
-        stride = std::max<int64_t>(1, rows >> 22);
+        stride = std::max<int64_t>(1, rows >> 20);
         h = at::empty({nparts}, ex.opts(at::kInt));
         hip::radix_part_sample(ptr<int64_t>(k), rows, bits, stride, reinterpret_cast<uint32_t *>(h.data_ptr<int>()),
                                nkp, ex.stream);
