@@ -341,7 +341,7 @@ __device__ __forceinline__ void so_load(const uint64_t *__restrict__ ph, const i
 // held in registers (8 per thread) and the next partition's are loaded while this
 // one is deduplicated, so the global latency hides behind the LDS work of the two
 // phases (rows beyond 8192 in a skewed partition are streamed from global).
-__global__ __launch_bounds__(kSOThreads) void k_so_dedup(const uint64_t *__restrict__ ph,
+__global__ __launch_bounds__(kSOThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_so_dedup(const uint64_t *__restrict__ ph,
                                                          const int64_t *__restrict__ prow,
                                                          const int64_t *__restrict__ offs, int64_t nparts,
                                                          int64_t nl, int op, int keep_last, SOColSet L, SOColSet R,
