@@ -545,6 +545,26 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   RadixSide &B = build_left ? L : R;
   RadixSide &P = build_left ? R : L;
   const int64_t *nbase = narrow ? ptr<int64_t>(lk) : nullptr;  // the join kernels' narrowed-key base
+  // Inner joins keyed on one integer column per side (the partitioned key itself, same type, no
+  // nulls): the two key values of every output row are equal, so the build side's output key
+  // column is the probe side's -- one buffer behind both (columns are immutable): 8 B/row less
+  // written and allocated (1B x 1B: 8 GB).  A/B knob: CYLON_RJ_SHARE_KEY=0.
+  auto key_col = [](const TablePtr &t, const at::Tensor &k) {
+    int idx = -1, hits = 0;
+    for (int c = 0; c < t->Columns(); ++c) {
+      const Column &col = t->column(c);
+      if (col.type.width() == 8 && col.data.data_ptr() == k.data_ptr() && !col.nullable() &&
+          (col.type.kind() == ValueKind::SIGNED_INT || col.type.kind() == ValueKind::UNSIGNED_INT)) {
+        idx = c;
+        ++hits;
+      }
+    }
+    return hits == 1 ? idx : -1;
+  };
+  const int kl = key_col(left, lk), kr = key_col(right, rk);
+  const bool share_key = oj == 0 && !sink && kl >= 0 && kr >= 0 && left->column(kl).type == right->column(kr).type &&
+                         knobs::Flag("RJ_SHARE_KEY", true);
+  const int bkc = build_left ? kl : kr;  // the build side's key column (not written when shared)
   // Skewed partitions are handled per partition, not per join: a partition whose build side exceeds
   // the LDS capacity or whose probe side is hot (> 2 probe chunks) is skipped by the partition loop
   // and covered by split work items (kernel_decls.inc RJSplit): build chunks of <= cap rows x probe
@@ -752,12 +772,18 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
       lcols.assign(sink->cols.begin(), sink->cols.begin() + left->Columns());
       rcols.assign(sink->cols.begin() + left->Columns(), sink->cols.end());
     } else {
-      for (const auto &col : left->columns())  // (null-side validity: apply_presence)
-        lcols.push_back(make_fixed_column(cfg.GetLeftTablePrefix() + col.name, col.type, rows, ex.device,
-                                          col.nullable()));
-      for (const auto &col : right->columns())
-        rcols.push_back(make_fixed_column(cfg.GetRightTablePrefix() + col.name, col.type, rows, ex.device,
-                                          col.nullable()));
+      for (int c = 0; c < left->Columns(); ++c) {  // (null-side validity: apply_presence)
+        const Column &col = left->column(c);
+        const bool shared = share_key && build_left && c == bkc;
+        lcols.push_back(make_fixed_column(cfg.GetLeftTablePrefix() + col.name, col.type, shared ? 0 : rows,
+                                          ex.device, col.nullable()));
+      }
+      for (int c = 0; c < right->Columns(); ++c) {
+        const Column &col = right->column(c);
+        const bool shared = share_key && !build_left && c == bkc;
+        rcols.push_back(make_fixed_column(cfg.GetRightTablePrefix() + col.name, col.type, shared ? 0 : rows,
+                                          ex.device, col.nullable()));
+      }
     }
     auto word_outs = [&](const RadixSide &sd) {
       std::vector<at::Tensor> w;
@@ -772,6 +798,13 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   auto write = [&](int64_t rows, const int64_t *offs, int64_t *cursor) {
     RadixCols pc = build_left ? radix_cols(right, &R, &rcols, off, &rwords) : radix_cols(left, &L, &lcols, off, &lwords);
     RadixCols bc = build_left ? radix_cols(left, &L, &lcols, off, &lwords) : radix_cols(right, &R, &rcols, off, &rwords);
+    if (share_key) {  // the build key column's entry (after any unpacked validity entries before it)
+      int q = 0;
+      for (int c = 0; c < bkc; ++c) q += 1 + (bt->column(c).nullable() && B.vwords.empty());
+      bc.in.erase(bc.in.begin() + q);
+      bc.out.erase(bc.out.begin() + q);
+      bc.w.erase(bc.w.begin() + q);
+    }
     // probe-side columns are streamed from HBM; the key column (in == nullptr) is written from
     // the probe key the kernel already holds
     int pkey = -1;
@@ -823,9 +856,18 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
       sink->size = off + m;  // give back the estimate's slack
     }
     if (!sink) {
-      for (auto &c : lcols) c = c.slice(0, m);
-      for (auto &c : rcols) c = c.slice(0, m);
+      for (auto &c : lcols)
+        if (c.length > 0) c = c.slice(0, m);
+      for (auto &c : rcols)
+        if (c.length > 0) c = c.slice(0, m);
     }
+  }
+  if (share_key) {
+    Column &dst = build_left ? lcols[kl] : rcols[kr];
+    const Column &src = build_left ? rcols[kr] : lcols[kl];
+    dst.data = src.data;
+    dst.length = src.length;
+    trace::add_counter("join.radix.shared_key_column", 1);
   }
   if (m > 0) {
     unpack_validity_words(ex, left, L, lwords, lcols, off, m);

@@ -133,7 +133,8 @@ class Table(PandasOpsMixin):
         return Table(context=ctx, _native=C.import_device_table(ctx._ctx, caps[0], caps[1]))
 
     def to_torch(self) -> Dict[str, torch.Tensor]:
-        """Columns as device tensors (zero-copy, fixed width columns only)."""
+        """Columns as device tensors (zero-copy, fixed width columns only).  Columns may share a
+        buffer (an inner join's two key columns, docs/semantics.md): clone before in-place writes."""
         out = {}
         for c in self._t.columns():
             if c.offsets is not None:

@@ -210,6 +210,26 @@ def test_radix_join_slot_overflow_repartitions_exactly(gpu_ctx, ctx, monkeypatch
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
 
 
+@pytest.mark.parametrize("left_small", [True, False])
+@pytest.mark.parametrize("share", ["1", "0"])
+def test_radix_inner_join_shared_key_column(gpu_ctx, ctx, monkeypatch, left_small, share):
+    """Inner joins on one integer key column per side write the probe side's key column once and
+    give the build side's output key column the same buffer (join.radix.shared_key_column); the
+    key sits behind a nullable payload column so the build column list's index shift is exercised.
+    CYLON_RJ_SHARE_KEY=0 writes both columns; the results are equal either way."""
+    monkeypatch.setenv("CYLON_RJ_SHARE_KEY", share)
+    rng = np.random.default_rng(41)
+    nl, nr = (300_000, 500_000) if left_small else (500_000, 300_000)
+    a = pa.table({"i": pa.array(rng.integers(-9, 9, nl), mask=rng.random(nl) < 0.1),
+                  "k": rng.integers(0, 600_000, nl), "v": rng.random(nl)})
+    b = pa.table({"w": rng.random(nr), "k": rng.integers(0, 600_000, nr)})
+    got, exp, c = _join(gpu_ctx, ctx, a, b, "inner", ["k"], monkeypatch)
+    assert c.get("join.radix.shared_key_column", 0) == (1 if share == "1" else 0), c
+    assert c["join.radix.rows_out"] == len(exp)
+    assert (got["l_k"].to_numpy() == got["r_k"].to_numpy()).all()
+    pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
+
+
 # ---- LDS radix group-by (kernels/radix_groupby.hip) beyond one integer key + SUM/COUNT/MIN/MAX/MEAN
 def _groupby_both(T, keys, aggs, monkeypatch):
     """[radix path, GPU global-table path] results and counters; both are also checked against the
