@@ -386,15 +386,21 @@ __global__ void k_words_to_bytes(ConstWordPtrs in, int64_t n, int L, int W, int 
 
 // bad[i] = 1 where both rows are present and any word differs
 __global__ void k_words_mismatch(ConstWordPtrs a, ConstWordPtrs b, int W, const uint8_t *__restrict__ va,
-                                 const uint8_t *__restrict__ vb, int64_t n, uint8_t *__restrict__ bad) {
+                                 const uint8_t *__restrict__ vb, int64_t n, uint8_t *__restrict__ bad,
+                                 unsigned long long *nbad) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  unsigned long long c = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     bool diff = false;
     for (int j = 0; j < W; ++j) diff |= a.w[j][i] != b.w[j][i];
     if (va && !va[i]) diff = false;
     if (vb && !vb[i]) diff = false;
     bad[i] = diff ? 1 : 0;
+    c += diff ? 1ull : 0ull;
   }
+  // the count rides along (no separate reduction over the flags): one atomic per wave that saw a row
+  for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0 && c) atomicAdd(nbad, c);
 }
 
 // mm[0] = min, mm[1] = max of the row lengths offs[i + 1] - offs[i] (mm preset to {~0, 0})
@@ -451,8 +457,9 @@ void words_to_bytes(const int64_t *const *words, int64_t n, int L, uint8_t *byte
 }
 
 void words_mismatch(const int64_t *const *a, const int64_t *const *b, int W, const uint8_t *va, const uint8_t *vb,
-                    int64_t n, uint8_t *bad, void *stream) {
+                    int64_t n, uint8_t *bad, int64_t *nbad, void *stream) {
   CYLON_CHECK(W >= 1 && W <= kMaxWords, Code::Invalid, "string words: " << W);
+  HIP_CHECK(hipMemsetAsync(nbad, 0, sizeof(int64_t), as_stream(stream)));
   if (n == 0) return;
   ConstWordPtrs pa{}, pb{};
   for (int j = 0; j < W; ++j) {
@@ -460,7 +467,7 @@ void words_mismatch(const int64_t *const *a, const int64_t *const *b, int W, con
     pb.w[j] = b[j];
   }
   hipLaunchKernelGGL(k_words_mismatch, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), pa, pb, W, va, vb, n,
-                     bad);
+                     bad, reinterpret_cast<unsigned long long *>(nbad));
   HIP_LAUNCH_CHECK();
 }
 

@@ -1459,15 +1459,23 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
   if (k.verify && !lvar && !rvar) return drop_false_matches(out, cfg, left->Columns());
   if (!lpx && !rpx) return out;
   const JoinType jt = cfg.GetType();
+  // Inner join on one fixed-length string key per side (same type and length, no nulls): the key
+  // words are verified equal row by row below, so the right output key column is the left one's
+  // bytes and offsets (one words -> bytes conversion; CYLON_RJ_SHARE_KEY=0 converts both).
+  const bool share_skey = jt == JoinType::INNER && k.verify && lc.size() == 1 && lpx && rpx && lwlen[lc[0]] > 0 &&
+                          lwlen[lc[0]] == rwlen[rc[0]] && left->column(lc[0]).type == right->column(rc[0]).type &&
+                          !left->column(lc[0]).nullable() && !right->column(rc[0]).nullable() &&
+                          knobs::Flag("RJ_SHARE_KEY", true);
   auto side = [&](const TablePtr &orig, bool px, bool var, const std::vector<int> &pos, const std::vector<int64_t> &wlen,
-                  const std::vector<int> &keys, int first, int np, bool may_null, const std::string &prefix) {
+                  const std::vector<int> &keys, int first, int np, bool may_null, const std::string &prefix,
+                  int skip_col) {
     std::vector<Column> cols(orig->Columns());
     if (!px) {
       for (int c = 0; c < orig->Columns(); ++c) cols[c] = out->column(first + c);
       return cols;
     }
     for (int c = 0; c < orig->Columns(); ++c) {
-      if (pos[c] < 0) continue;
+      if (pos[c] < 0 || c == skip_col) continue;
       if (wlen[c] > 0) {  // a fixed-length string from its word columns
         const int64_t L = wlen[c];
         std::vector<Column> wc;
@@ -1515,9 +1523,13 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
     return cols;
   };
   std::vector<Column> all = side(left, lpx, lgather, lpos, lwlen, lc, 0, lp->Columns(), left_may_null(jt),
-                                cfg.GetLeftTablePrefix());
+                                cfg.GetLeftTablePrefix(), -1);
   std::vector<Column> rcols = side(right, rpx, rgather, rpos, rwlen, rc, lp->Columns(), rp->Columns(),
-                                   right_may_null(jt), cfg.GetRightTablePrefix());
+                                   right_may_null(jt), cfg.GetRightTablePrefix(), share_skey ? rc[0] : -1);
+  if (share_skey) {
+    rcols[rc[0]] = all[lc[0]].with_name(cfg.GetRightTablePrefix() + right->column(rc[0]).name);
+    trace::add_counter("join.radix.shared_key_column", 1);
+  }
   for (auto &c : rcols) all.push_back(std::move(c));
   TablePtr res = Table::Make(left->GetContext(), std::move(all));
   if (lgather || rgather) trace::add_counter("join.radix.var_gather", 1);
@@ -1538,9 +1550,11 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
   if (aw.size() > 8) return drop_false_matches(res, cfg, left->Columns());
   const Column &lw = out->column(lpos[lc[0]]), &rw = out->column(rfirst + rpos[rc[0]]);
   at::Tensor badb = ex.empty_u8(m);  // both sides present and some key word differs
+  at::Tensor nbadd = ex.empty_i64(1);
   hip::words_mismatch(aw.data(), bw.data(), (int)aw.size(), lw.nullable() ? ptr<uint8_t>(lw.validity) : nullptr,
-                      rw.nullable() ? ptr<uint8_t>(rw.validity) : nullptr, m, ptr<uint8_t>(badb), ex.stream);
-  const int64_t nbad = badb.sum(at::kLong).item<int64_t>();
+                      rw.nullable() ? ptr<uint8_t>(rw.validity) : nullptr, m, ptr<uint8_t>(badb), ptr<int64_t>(nbadd),
+                      ex.stream);
+  const int64_t nbad = nbadd.item<int64_t>();
   if (nbad == 0) return res;
   at::Tensor bad = badb.to(at::kBool);
   if (jt != JoinType::INNER) {

@@ -412,6 +412,7 @@ def test_radix_join_string_keys(gpu_ctx, ctx, monkeypatch, how, keys):
     in LDS; the fixed-length (13-byte) key strings travel as two int64 word columns (no gather by row
     number) and every output row's key words are compared (a 64-bit collision would be dropped /
     fall back).  Against the CPU twin."""
+    monkeypatch.setenv("CYLON_RJ_SHARE_KEY", "1")
     rng = np.random.default_rng(53)
     n = 1_200_000
     ids_a = rng.integers(0, 900_000, n)
@@ -422,6 +423,8 @@ def test_radix_join_string_keys(gpu_ctx, ctx, monkeypatch, how, keys):
     assert c.get("join.radix.var_key", 0) >= 1 and c.get("join.radix.hashed_key", 0) == 1, c
     assert c.get("join.radix.hash_collision_fallback", 0) == 0, c
     assert c.get("join.radix.word_columns", 0) == 2 and c.get("join.radix.var_gather", 0) == 0, c
+    # inner on the string alone: the right key column is the verified left one's buffers
+    assert c.get("join.radix.shared_key_column", 0) == (1 if how == "inner" and keys == ["s"] else 0), c
     assert c["join.radix.rows_out"] == len(exp)
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
 
