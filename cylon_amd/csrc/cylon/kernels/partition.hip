@@ -349,21 +349,27 @@ struct ConstWordPtrs {
   const int64_t *w[kMaxWords];
 };
 
+// hash (optional): the key row hash of a one-string-column key, hashing::combine64(seed,
+// bytes_hash64(row)) as k_row_hash64 computes it, from the words in registers (bytes_hash64 folds
+// the same little-endian words, the last one zero-padded) -- no second read of the bytes
 __global__ void k_bytes_to_words(const uint8_t *__restrict__ bytes, int64_t n, int L, int W, int aligned8,
-                                 WordPtrs out) {
+                                 WordPtrs out, uint64_t *__restrict__ hash) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint8_t *src = bytes + i * L;
-    if (aligned8) {
-      const uint64_t *s8 = reinterpret_cast<const uint64_t *>(src);
-      for (int j = 0; j < W; ++j) out.w[j][i] = (int64_t)s8[j];
-    } else {
-      for (int j = 0; j < W; ++j) {
-        uint64_t v = 0;
+    uint64_t h = 0x9E3779B97F4A7C15ULL ^ (uint64_t)L, tail = 0;
+    for (int j = 0; j < W; ++j) {
+      uint64_t v = 0;
+      if (aligned8) {
+        v = reinterpret_cast<const uint64_t *>(src)[j];
+      } else {
         for (int b = 0; b < 8 && 8 * j + b < L; ++b) v |= (uint64_t)src[8 * j + b] << (8 * b);
-        out.w[j][i] = (int64_t)v;
       }
+      out.w[j][i] = (int64_t)v;
+      if (8 * (j + 1) <= L) h = hashing::fmix64(h ^ v) + 0x632BE59BD9B4E019ULL;
+      else tail = v;
     }
+    if (hash) hash[i] = hashing::combine64(0x84222325cbf29ce4ULL, hashing::fmix64(h ^ tail ^ ((uint64_t)L << 56)));
   }
 }
 
@@ -434,14 +440,15 @@ void var_len_minmax(const int64_t *offs, int64_t n, int64_t *mm, void *stream) {
   }
 }
 
-void bytes_to_words(const uint8_t *bytes, int64_t n, int L, int64_t *const *words, void *stream) {
+void bytes_to_words(const uint8_t *bytes, int64_t n, int L, int64_t *const *words, void *stream, uint64_t *hash) {
   const int W = (L + 7) / 8;
   CYLON_CHECK(L >= 1 && W <= kMaxWords, Code::Invalid, "string words: length " << L);
   if (n == 0) return;
   WordPtrs o{};
   for (int j = 0; j < W; ++j) o.w[j] = words[j];
   const int al = (L & 7) == 0 && (reinterpret_cast<uintptr_t>(bytes) & 7) == 0;  // 8-byte accesses
-  hipLaunchKernelGGL(k_bytes_to_words, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), bytes, n, L, W, al, o);
+  hipLaunchKernelGGL(k_bytes_to_words, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), bytes, n, L, W, al, o,
+                     hash);
   HIP_LAUNCH_CHECK();
 }
 

@@ -1110,7 +1110,13 @@ struct RadixKeys {
   std::vector<int> shift, bits;
   std::vector<int64_t> ncode;  // composite: field value of a null in key i (-1: no nulls on either side)
   bool nulls = false;
+  // one fixed-length string key per side: its word columns, written by the read that hashed it
+  std::vector<at::Tensor> lwords, rwords;
+  int64_t wlen = -1;
 };
+
+static int64_t fixed_var_len(const Exec &ex, const Column &c);
+static std::vector<at::Tensor> var_to_words(const Exec &ex, const Column &c, int64_t L, at::Tensor *hash = nullptr);
 
 static bool int_key(const Column &c) {
   return simple_key(c) && (c.type.kind() == ValueKind::SIGNED_INT ||
@@ -1125,7 +1131,8 @@ static bool nullable_int_key(const Column &c) {
          (c.type.kind() == ValueKind::SIGNED_INT || (c.type.kind() == ValueKind::UNSIGNED_INT && c.type.width() < 8));
 }
 
-static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr &right, const JoinConfig &cfg) {
+static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr &right, const JoinConfig &cfg,
+                            bool words_ok) {
   const auto &lc = cfg.GetLeftColumnIdx();
   const auto &rc = cfg.GetRightColumnIdx();
   RadixKeys k;
@@ -1221,9 +1228,21 @@ static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr
       return k;
     }
   }
+  k.verify = true;
+  if (words_ok && lc.size() == 1 && left->device().is_cuda()) {
+    // one fixed-length string key per side: the word columns the radix join carries and the row hash
+    // come out of one read of the bytes (the proxies below take the words)
+    const int64_t L = fixed_var_len(ex, left->column(lc[0]));
+    if (L > 0 && fixed_var_len(ex, right->column(rc[0])) == L) {
+      k.wlen = L;
+      k.lwords = var_to_words(ex, left->column(lc[0]), L, &k.l);
+      k.rwords = var_to_words(ex, right->column(rc[0]), L, &k.r);
+      trace::add_counter("join.radix.hashed_key", 1);
+      return k;
+    }
+  }
   k.l = encode_keys(ex, left, lc, false).keys;  // row hash of the key columns
   k.r = encode_keys(ex, right, rc, false).keys;
-  k.verify = true;
   trace::add_counter("join.radix.hashed_key", 1);
   return k;
 }
@@ -1356,8 +1375,9 @@ static int64_t fixed_var_len(const Exec &ex, const Column &c) {  // L, or -1
   return lo == hi && lo > 0 && lo <= 64 ? lo : -1;
 }
 
-static std::vector<at::Tensor> var_to_words(const Exec &ex, const Column &c, int64_t L) {
+static std::vector<at::Tensor> var_to_words(const Exec &ex, const Column &c, int64_t L, at::Tensor *hash) {
   const int64_t n = c.length, W = (L + 7) / 8;
+  if (hash) *hash = ex.empty_i64(n);
   const int64_t o0 = c.offsets.slice(0, 0, 1).cpu().item<int64_t>();
   std::vector<at::Tensor> out;
   std::vector<int64_t *> wp;
@@ -1365,7 +1385,8 @@ static std::vector<at::Tensor> var_to_words(const Exec &ex, const Column &c, int
     out.push_back(ex.empty_i64(n));
     wp.push_back(ptr<int64_t>(out.back()));
   }
-  hip::bytes_to_words(ptr<uint8_t>(c.data) + o0, n, (int)L, wp.data(), ex.stream);
+  hip::bytes_to_words(ptr<uint8_t>(c.data) + o0, n, (int)L, wp.data(), ex.stream,
+                      hash ? reinterpret_cast<uint64_t *>(ptr<int64_t>(*hash)) : nullptr);
   return out;
 }
 
@@ -1390,7 +1411,7 @@ static Column words_to_var(const Exec &ex, const std::string &name, const DataTy
 // (as in the one-key join), and composite_key_unpack rebuilds the key columns of the output.
 static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const TablePtr &right, const JoinConfig &cfg,
                                JoinSink *sink) {
-  RadixKeys k = radix_keys(ex, left, right, cfg);
+  RadixKeys k = radix_keys(ex, left, right, cfg, sink == nullptr);  // (a sink takes no var-width keys)
   if (!k.ok) return nullptr;
   auto var_col = [](const Column &c) { return c.is_var() || c.type.kind() == ValueKind::FIXED_BYTES; };
   auto has_var = [&](const TablePtr &t) {
@@ -1410,7 +1431,7 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
   // wlen[c] = L of a column carried as words (from proxy column pos[c]), else -1
   static const std::string kRow = "__cylon_row", kKey = "__cylon_key";
   auto proxy = [&](const TablePtr &t, bool &var, const std::vector<int> &keys, const at::Tensor &img,
-                   std::vector<int> &pos, std::vector<int64_t> &wlen) {
+                   std::vector<int> &pos, std::vector<int64_t> &wlen, const std::vector<at::Tensor> &kwords) {
     pos.assign(t->Columns(), -1);
     wlen.assign(t->Columns(), -1);
     std::vector<Column> cols;
@@ -1420,14 +1441,15 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
       const Column &col = t->column(c);
       if (ckey && std::find(keys.begin(), keys.end(), c) != keys.end()) continue;
       if (var_col(col)) {
-        const int64_t L = fixed_var_len(ex, col);
+        const bool kw = !kwords.empty() && c == keys[0];  // the key's words from radix_keys
+        const int64_t L = kw ? k.wlen : fixed_var_len(ex, col);
         if (L < 0) {
           var = true;
           continue;
         }
         wlen[c] = L;
         pos[c] = (int)cols.size();
-        std::vector<at::Tensor> w = var_to_words(ex, col, L);
+        std::vector<at::Tensor> w = kw ? kwords : var_to_words(ex, col, L);
         for (size_t j = 0; j < w.size(); ++j)
           cols.emplace_back("__cylon_w" + std::to_string(c) + "_" + std::to_string(j), DataType(Type::INT64),
                             t->Rows(), w[j]);
@@ -1443,8 +1465,8 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
   std::vector<int64_t> lwlen, rwlen;
   const bool lpx = lvar || ckey, rpx = rvar || ckey;
   bool lgather = false, rgather = false;  // var-width columns gathered by row number after the join
-  TablePtr lp = lpx ? proxy(left, lgather, lc, k.l, lpos, lwlen) : left;
-  TablePtr rp = rpx ? proxy(right, rgather, rc, k.r, rpos, rwlen) : right;
+  TablePtr lp = lpx ? proxy(left, lgather, lc, k.l, lpos, lwlen, k.lwords) : left;
+  TablePtr rp = rpx ? proxy(right, rgather, rc, k.r, rpos, rwlen, k.rwords) : right;
   if (lpx || rpx) {
     int64_t nw = 0;
     for (int64_t L : lwlen) nw += L > 0;
