@@ -36,6 +36,23 @@ CYLON_HD uint64_t fmix64(uint64_t k) {
   return k;
 }
 
+// inverse of fmix64: x ^= x >> 33 undoes itself (shift >= 32), the multipliers are odd (inverses mod 2^64)
+CYLON_HD uint64_t fmix64_inv(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0x9cb4b2f8129337dbULL;
+  k ^= k >> 33;
+  k *= 0x4f74430c22a54005ULL;
+  k ^= k >> 33;
+  return k;
+}
+
+// Invertible key of a fixed-length string of L bytes held as W = ceil(L / 8) little-endian words:
+// h = fmix64(w0 ^ g), g a chain over L and words 1..W-1.  For fixed g, w0 -> h is a bijection, so
+// (h, w1..w_{W-1}) determines the string: the join carries h as its key in place of w0
+// (w0 = fmix64_inv(h) ^ g), and equal h + equal w1.. means equal strings.
+CYLON_HD uint64_t word_key_seed(int64_t len) { return 0x9E3779B97F4A7C15ULL ^ (uint64_t)len; }
+CYLON_HD uint64_t word_key_step(uint64_t g, uint64_t w) { return fmix64(g ^ w) + 0x632BE59BD9B4E019ULL; }
+
 // 64-bit hash of a byte string (join / set-op keys of string, binary and fixed-size binary columns):
 // a chain of fmix64 bijections over the little-endian 8-byte words, seeded with the length.  Two
 // 32-bit murmur3 hashes with different seeds (round 4) are correlated on short keys: a 200M x 200M

@@ -349,15 +349,16 @@ struct ConstWordPtrs {
   const int64_t *w[kMaxWords];
 };
 
-// hash (optional): the key row hash of a one-string-column key, hashing::combine64(seed,
+// hash (optional), inv = 0: the key row hash of a one-string-column key, hashing::combine64(seed,
 // bytes_hash64(row)) as k_row_hash64 computes it, from the words in registers (bytes_hash64 folds
-// the same little-endian words, the last one zero-padded) -- no second read of the bytes
+// the same little-endian words, the last one zero-padded) -- no second read of the bytes.
+// inv = 1: hash = the invertible word key (hash.hpp word_key_*) and word 0 is not written.
 __global__ void k_bytes_to_words(const uint8_t *__restrict__ bytes, int64_t n, int L, int W, int aligned8,
-                                 WordPtrs out, uint64_t *__restrict__ hash) {
+                                 WordPtrs out, uint64_t *__restrict__ hash, int inv) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint8_t *src = bytes + i * L;
-    uint64_t h = 0x9E3779B97F4A7C15ULL ^ (uint64_t)L, tail = 0;
+    uint64_t h = hashing::word_key_seed(L), tail = 0, w0 = 0;
     for (int j = 0; j < W; ++j) {
       uint64_t v = 0;
       if (aligned8) {
@@ -365,28 +366,44 @@ __global__ void k_bytes_to_words(const uint8_t *__restrict__ bytes, int64_t n, i
       } else {
         for (int b = 0; b < 8 && 8 * j + b < L; ++b) v |= (uint64_t)src[8 * j + b] << (8 * b);
       }
+      if (inv) {
+        if (j == 0) {
+          w0 = v;
+        } else {
+          out.w[j][i] = (int64_t)v;
+          h = hashing::word_key_step(h, v);
+        }
+        continue;
+      }
       out.w[j][i] = (int64_t)v;
-      if (8 * (j + 1) <= L) h = hashing::fmix64(h ^ v) + 0x632BE59BD9B4E019ULL;
+      if (8 * (j + 1) <= L) h = hashing::word_key_step(h, v);
       else tail = v;
     }
-    if (hash) hash[i] = hashing::combine64(0x84222325cbf29ce4ULL, hashing::fmix64(h ^ tail ^ ((uint64_t)L << 56)));
+    if (inv) hash[i] = hashing::fmix64(w0 ^ h);
+    else if (hash) hash[i] = hashing::combine64(0x84222325cbf29ce4ULL, hashing::fmix64(h ^ tail ^ ((uint64_t)L << 56)));
   }
 }
 
+// hash (optional): word 0 comes from the invertible word key, w0 = fmix64_inv(hash) ^ g(words 1..)
 __global__ void k_words_to_bytes(ConstWordPtrs in, int64_t n, int L, int W, int aligned8,
-                                 uint8_t *__restrict__ bytes) {
+                                 uint8_t *__restrict__ bytes, const uint64_t *__restrict__ hash) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     uint8_t *dst = bytes + i * L;
-    if (aligned8) {
-      uint64_t *d8 = reinterpret_cast<uint64_t *>(dst);
-      for (int j = 0; j < W; ++j) d8[j] = (uint64_t)in.w[j][i];
-    } else {
-      for (int j = 0; j < W; ++j) {
-        const uint64_t v = (uint64_t)in.w[j][i];
+    auto put = [&](int j, uint64_t v) {
+      if (aligned8) {
+        reinterpret_cast<uint64_t *>(dst)[j] = v;
+      } else {
         for (int b = 0; b < 8 && 8 * j + b < L; ++b) dst[8 * j + b] = (uint8_t)(v >> (8 * b));
       }
+    };
+    uint64_t g = hashing::word_key_seed(L);
+    for (int j = hash ? 1 : 0; j < W; ++j) {
+      const uint64_t v = (uint64_t)in.w[j][i];
+      if (hash) g = hashing::word_key_step(g, v);
+      put(j, v);
     }
+    if (hash) put(0, hashing::fmix64_inv(hash[i]) ^ g);
   }
 }
 
@@ -440,26 +457,30 @@ void var_len_minmax(const int64_t *offs, int64_t n, int64_t *mm, void *stream) {
   }
 }
 
-void bytes_to_words(const uint8_t *bytes, int64_t n, int L, int64_t *const *words, void *stream, uint64_t *hash) {
+void bytes_to_words(const uint8_t *bytes, int64_t n, int L, int64_t *const *words, void *stream, uint64_t *hash,
+                    bool inv) {
   const int W = (L + 7) / 8;
   CYLON_CHECK(L >= 1 && W <= kMaxWords, Code::Invalid, "string words: length " << L);
+  CYLON_CHECK(!inv || hash, Code::Invalid, "string words: the invertible key needs its output");
   if (n == 0) return;
   WordPtrs o{};
-  for (int j = 0; j < W; ++j) o.w[j] = words[j];
+  for (int j = inv ? 1 : 0; j < W; ++j) o.w[j] = words[j];
   const int al = (L & 7) == 0 && (reinterpret_cast<uintptr_t>(bytes) & 7) == 0;  // 8-byte accesses
   hipLaunchKernelGGL(k_bytes_to_words, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), bytes, n, L, W, al, o,
-                     hash);
+                     hash, inv ? 1 : 0);
   HIP_LAUNCH_CHECK();
 }
 
-void words_to_bytes(const int64_t *const *words, int64_t n, int L, uint8_t *bytes, void *stream) {
+void words_to_bytes(const int64_t *const *words, int64_t n, int L, uint8_t *bytes, void *stream,
+                    const uint64_t *hash) {
   const int W = (L + 7) / 8;
   CYLON_CHECK(L >= 1 && W <= kMaxWords, Code::Invalid, "string words: length " << L);
   if (n == 0) return;
   ConstWordPtrs in{};
-  for (int j = 0; j < W; ++j) in.w[j] = words[j];
+  for (int j = hash ? 1 : 0; j < W; ++j) in.w[j] = words[j];
   const int al = (L & 7) == 0 && (reinterpret_cast<uintptr_t>(bytes) & 7) == 0;
-  hipLaunchKernelGGL(k_words_to_bytes, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), in, n, L, W, al, bytes);
+  hipLaunchKernelGGL(k_words_to_bytes, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), in, n, L, W, al, bytes,
+                     hash);
   HIP_LAUNCH_CHECK();
 }
 

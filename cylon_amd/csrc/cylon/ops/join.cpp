@@ -423,7 +423,8 @@ static void apply_presence(std::vector<Column> &cols, const TablePtr &in, const 
 // (a key column itself, or the composite image of several key columns).  All four join types:
 // the kernels emit unmatched rows of the preserved side(s) with presence bytes (outer_mode).
 static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr &right, const at::Tensor &lk,
-                           const at::Tensor &rk, const JoinConfig &cfg, JoinSink *sink = nullptr) {
+                           const at::Tensor &rk, const JoinConfig &cfg, JoinSink *sink = nullptr,
+                           bool hashed_key = false) {
   const int64_t nl = left->Rows(), nr = right->Rows();
   const bool build_left = nl < nr;
   const TablePtr &bt = build_left ? left : right;
@@ -450,7 +451,8 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
               (c.type.kind() == ValueKind::SIGNED_INT || c.type.kind() == ValueKind::UNSIGNED_INT);
     return hits == 1;
   };
-  bool narrow = nl > 0 && nr > 0 && lk.scalar_type() == at::kLong && rk.scalar_type() == at::kLong &&
+  // (a hashed key -- the invertible string word key a proxy carries as a column -- never fits 32 bits)
+  bool narrow = !hashed_key && nl > 0 && nr > 0 && lk.scalar_type() == at::kLong && rk.scalar_type() == at::kLong &&
                 own_key_column(left, lk) && own_key_column(right, rk);
   at::Tensor narrow_bad = narrow ? at::zeros({1}, ex.opts(at::kInt)) : at::Tensor();
   hip::NarrowKeys nk;
@@ -1110,13 +1112,16 @@ struct RadixKeys {
   std::vector<int> shift, bits;
   std::vector<int64_t> ncode;  // composite: field value of a null in key i (-1: no nulls on either side)
   bool nulls = false;
-  // one fixed-length string key per side: its word columns, written by the read that hashed it
+  // one fixed-length string key per side: l / r are its invertible word keys (hash.hpp word_key_*,
+  // carried by the proxies as a column in place of word 0) and lwords / rwords its words 1..W-1,
+  // all from one read of the bytes
   std::vector<at::Tensor> lwords, rwords;
   int64_t wlen = -1;
 };
 
 static int64_t fixed_var_len(const Exec &ex, const Column &c);
-static std::vector<at::Tensor> var_to_words(const Exec &ex, const Column &c, int64_t L, at::Tensor *hash = nullptr);
+static std::vector<at::Tensor> var_to_words(const Exec &ex, const Column &c, int64_t L, at::Tensor *hash = nullptr,
+                                            bool inv = false);
 
 static bool int_key(const Column &c) {
   return simple_key(c) && (c.type.kind() == ValueKind::SIGNED_INT ||
@@ -1235,8 +1240,8 @@ static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr
     const int64_t L = fixed_var_len(ex, left->column(lc[0]));
     if (L > 0 && fixed_var_len(ex, right->column(rc[0])) == L) {
       k.wlen = L;
-      k.lwords = var_to_words(ex, left->column(lc[0]), L, &k.l);
-      k.rwords = var_to_words(ex, right->column(rc[0]), L, &k.r);
+      k.lwords = var_to_words(ex, left->column(lc[0]), L, &k.l, true);
+      k.rwords = var_to_words(ex, right->column(rc[0]), L, &k.r, true);
       trace::add_counter("join.radix.hashed_key", 1);
       return k;
     }
@@ -1339,7 +1344,7 @@ static int radix_join_chunks(const Exec &ex, const TablePtr &l, const TablePtr &
 
 // the radix join in C key-hash chunks into one sink (see above); nullptr if a chunk's radix join fails
 static TablePtr radix_join_chunked(const Exec &ex, const TablePtr &l, const TablePtr &r, const at::Tensor &lk,
-                                   const at::Tensor &rk, const JoinConfig &cfg, int C) {
+                                   const at::Tensor &rk, const JoinConfig &cfg, int C, bool hashed_key = false) {
   auto key_col = [](const TablePtr &t, const at::Tensor &k) {
     for (int c = 0; c < t->Columns(); ++c)
       if (t->column(c).data.defined() && t->column(c).data.data_ptr() == k.data_ptr()) return c;
@@ -1356,7 +1361,7 @@ static TablePtr radix_join_chunked(const Exec &ex, const TablePtr &l, const Tabl
     const at::Tensor rkc_t = rkc >= 0 ? rc->column(rkc).data : rk.index_select(0, ir);
     il = at::Tensor();
     ir = at::Tensor();
-    if (!radix_join(ex, lc, rc, lkc_t, rkc_t, cfg, &sink)) return nullptr;
+    if (!radix_join(ex, lc, rc, lkc_t, rkc_t, cfg, &sink, hashed_key)) return nullptr;
     ++sink.chunks_done;
   }
   return sink.finish(l->GetContext());
@@ -1375,28 +1380,32 @@ static int64_t fixed_var_len(const Exec &ex, const Column &c) {  // L, or -1
   return lo == hi && lo > 0 && lo <= 64 ? lo : -1;
 }
 
-static std::vector<at::Tensor> var_to_words(const Exec &ex, const Column &c, int64_t L, at::Tensor *hash) {
+// words 0..W-1 (inv: words 1..W-1, *hash = the invertible word key that stands in for word 0)
+static std::vector<at::Tensor> var_to_words(const Exec &ex, const Column &c, int64_t L, at::Tensor *hash, bool inv) {
   const int64_t n = c.length, W = (L + 7) / 8;
   if (hash) *hash = ex.empty_i64(n);
   const int64_t o0 = c.offsets.slice(0, 0, 1).cpu().item<int64_t>();
   std::vector<at::Tensor> out;
   std::vector<int64_t *> wp;
-  for (int64_t j = 0; j < W; ++j) {
+  if (inv) wp.push_back(nullptr);
+  for (int64_t j = inv ? 1 : 0; j < W; ++j) {
     out.push_back(ex.empty_i64(n));
     wp.push_back(ptr<int64_t>(out.back()));
   }
   hip::bytes_to_words(ptr<uint8_t>(c.data) + o0, n, (int)L, wp.data(), ex.stream,
-                      hash ? reinterpret_cast<uint64_t *>(ptr<int64_t>(*hash)) : nullptr);
+                      hash ? reinterpret_cast<uint64_t *>(ptr<int64_t>(*hash)) : nullptr, inv);
   return out;
 }
 
+// wc = the word columns 0..W-1 (inv: wc[0] = the invertible word key, wc[1..] = words 1..W-1)
 static Column words_to_var(const Exec &ex, const std::string &name, const DataType &type,
-                           const std::vector<Column> &wc, int64_t L) {
+                           const std::vector<Column> &wc, int64_t L, bool inv = false) {
   const int64_t m = wc[0].length;
   std::vector<const int64_t *> wp;
   for (const auto &c : wc) wp.push_back(ptr<int64_t>(c.data));
   at::Tensor bytes = ex.empty_bytes(std::max<int64_t>(1, m * L));
-  hip::words_to_bytes(wp.data(), m, (int)L, ptr<uint8_t>(bytes), ex.stream);
+  hip::words_to_bytes(wp.data(), m, (int)L, ptr<uint8_t>(bytes), ex.stream,
+                      inv ? reinterpret_cast<const uint64_t *>(wp[0]) : nullptr);
   at::Tensor offs = at::arange(0, (m + 1) * L, L, ex.opts(at::kLong));
   // (a null row of an outer join keeps L zero bytes under its null: Arrow allows any length there)
   return Column(name, type, m, bytes.slice(0, 0, m * L), offs, wc[0].validity);
@@ -1441,7 +1450,7 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
       const Column &col = t->column(c);
       if (ckey && std::find(keys.begin(), keys.end(), c) != keys.end()) continue;
       if (var_col(col)) {
-        const bool kw = !kwords.empty() && c == keys[0];  // the key's words from radix_keys
+        const bool kw = k.wlen > 0 && c == keys[0];  // the key's word key + words from radix_keys
         const int64_t L = kw ? k.wlen : fixed_var_len(ex, col);
         if (L < 0) {
           var = true;
@@ -1449,10 +1458,12 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
         }
         wlen[c] = L;
         pos[c] = (int)cols.size();
+        // the key's word key is the join key itself (no pass moves it twice), then words 1..W-1
+        if (kw) cols.emplace_back("__cylon_wk" + std::to_string(c), DataType(Type::INT64), t->Rows(), img);
         std::vector<at::Tensor> w = kw ? kwords : var_to_words(ex, col, L);
         for (size_t j = 0; j < w.size(); ++j)
-          cols.emplace_back("__cylon_w" + std::to_string(c) + "_" + std::to_string(j), DataType(Type::INT64),
-                            t->Rows(), w[j]);
+          cols.emplace_back("__cylon_w" + std::to_string(c) + "_" + std::to_string(j + (kw ? 1 : 0)),
+                            DataType(Type::INT64), t->Rows(), w[j]);
         continue;
       }
       pos[c] = (int)cols.size();
@@ -1475,8 +1486,8 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
   }
   if (!radix_eligible(lp) || !radix_eligible(rp)) return nullptr;
   const int mchunks = sink ? 1 : radix_join_chunks(ex, lp, rp, k.l, k.r);
-  TablePtr out = mchunks > 1 ? radix_join_chunked(ex, lp, rp, k.l, k.r, cfg, mchunks)
-                             : radix_join(ex, lp, rp, k.l, k.r, cfg, sink);
+  TablePtr out = mchunks > 1 ? radix_join_chunked(ex, lp, rp, k.l, k.r, cfg, mchunks, k.verify)
+                             : radix_join(ex, lp, rp, k.l, k.r, cfg, sink, k.verify);
   if (!out) return nullptr;
   if (k.verify && !lvar && !rvar) return drop_false_matches(out, cfg, left->Columns());
   if (!lpx && !rpx) return out;
@@ -1502,7 +1513,8 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
         const int64_t L = wlen[c];
         std::vector<Column> wc;
         for (int64_t j = 0; j < (L + 7) / 8; ++j) wc.push_back(out->column(first + pos[c] + (int)j));
-        cols[c] = words_to_var(ex, prefix + orig->column(c).name, orig->column(c).type, wc, L);
+        cols[c] = words_to_var(ex, prefix + orig->column(c).name, orig->column(c).type, wc, L,
+                               k.wlen > 0 && c == keys[0]);
       } else {
         cols[c] = out->column(first + pos[c]);
       }
@@ -1564,11 +1576,13 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
   if (m == 0) return res;
   std::vector<const int64_t *> aw, bw;
   const int rfirst = lp->Columns();
+  // (a word-key column: the key words 1..W-1 -- equal word keys were matched, so word 0 is equal too)
   for (size_t i = 0; i < lc.size(); ++i)
-    for (int64_t j = 0; j < (lwlen[lc[i]] + 7) / 8; ++j) {
+    for (int64_t j = k.wlen > 0 ? 1 : 0; j < (lwlen[lc[i]] + 7) / 8; ++j) {
       aw.push_back(ptr<int64_t>(out->column(lpos[lc[i]] + (int)j).data));
       bw.push_back(ptr<int64_t>(out->column(rfirst + rpos[rc[i]] + (int)j).data));
     }
+  if (aw.empty()) return res;  // an L <= 8 word key is the string itself: no false matches
   if (aw.size() > 8) return drop_false_matches(res, cfg, left->Columns());
   const Column &lw = out->column(lpos[lc[0]]), &rw = out->column(rfirst + rpos[rc[0]]);
   at::Tensor badb = ex.empty_u8(m);  // both sides present and some key word differs

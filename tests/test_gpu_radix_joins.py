@@ -423,8 +423,30 @@ def test_radix_join_string_keys(gpu_ctx, ctx, monkeypatch, how, keys):
     assert c.get("join.radix.var_key", 0) >= 1 and c.get("join.radix.hashed_key", 0) == 1, c
     assert c.get("join.radix.hash_collision_fallback", 0) == 0, c
     assert c.get("join.radix.word_columns", 0) == 2 and c.get("join.radix.var_gather", 0) == 0, c
-    # inner on the string alone: the right key column is the verified left one's buffers
-    assert c.get("join.radix.shared_key_column", 0) == (1 if how == "inner" and keys == ["s"] else 0), c
+    # inner on the string alone: the build side's word-key column is the probe side's (radix_join)
+    # and the right key column is the verified left one's buffers
+    assert c.get("join.radix.shared_key_column", 0) == (2 if how == "inner" and keys == ["s"] else 0), c
+    assert c["join.radix.rows_out"] == len(exp)
+    pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
+
+
+@pytest.mark.parametrize("how", ["inner", "outer"])
+@pytest.mark.parametrize("fmt", ["s{:06d}", "key-{:020d}", "key-{:011d}/bin"])
+def test_radix_join_string_word_key(gpu_ctx, ctx, monkeypatch, how, fmt):
+    """One fixed-length string key per side joins on its invertible word key (hash.hpp word_key_*):
+    7-byte strings (one word: the key IS the string, no verification), 24 bytes (three aligned
+    words: word 0 rebuilt from the key after the join) and 19-byte binary (unaligned tail word).
+    Output key bytes must round-trip exactly.  Against the CPU twin."""
+    rng = np.random.default_rng(61)
+    n = 1_000_000
+    ids_a, ids_b = rng.integers(0, 800_000, n), rng.integers(0, 800_000, n)
+    enc = (lambda v: [fmt.format(x).encode() for x in v]) if fmt.endswith("/bin") else \
+        (lambda v: [fmt.format(x) for x in v])
+    a = pa.table({"s": pa.array(enc(ids_a)), "v": rng.random(n)})
+    b = pa.table({"s": pa.array(enc(ids_b)), "w": rng.random(n)})
+    got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["s"], monkeypatch)
+    assert c.get("join.radix.hashed_key", 0) == 1 and c.get("join.radix.var_gather", 0) == 0, c
+    assert c.get("join.radix.narrow_fallback", 0) == 0 and c.get("join.radix.hash_collision_fallback", 0) == 0, c
     assert c["join.radix.rows_out"] == len(exp)
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
 
