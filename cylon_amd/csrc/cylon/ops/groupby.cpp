@@ -258,6 +258,10 @@ struct GroupKey {
   std::vector<int64_t> lo;      // composite: per-column minimum
   std::vector<int> shift, bits; // composite: bit range of each column
   bool composite = false, fbits = false;
+  // one fixed-length string key (wlen = L bytes): k is its invertible word key (hash.hpp word_key_*),
+  // wmin / wmax the accumulators of MIN / MAX of its words 1..W-1 (equal in every group: exact)
+  int64_t wlen = -1;
+  std::vector<int> wmin, wmax;
   bool null_group = false;  // nullable single integer key: null rows carry null_key (no valid key has it)
   int64_t null_key = 0;
   std::vector<int64_t> ncode;  // composite: field value of a null in key i (-1: the column has no nulls)
@@ -400,9 +404,48 @@ static std::vector<Column> group_key_columns(const TablePtr &t, const GroupKey &
   return out;
 }
 
-static TablePtr radix_groupby(const TablePtr &t, const std::vector<int> &keys, const std::vector<AggSpec> &aggs) {
-  const int64_t n = t->Rows();
-  if (!t->device().is_cuda() || n < radix_groupby_min_rows()) return nullptr;
+// L when every row of c (a non-null string / binary column) holds L <= 64 bytes, else -1
+static int64_t fixed_string_len(const Exec &ex, const Column &c) {
+  if (c.nullable() || !(c.type.type == Type::STRING || c.type.type == Type::BINARY) || c.length == 0) return -1;
+  at::Tensor mm = ex.empty_i64(2);
+  hip::var_len_minmax(ptr<int64_t>(c.offsets), c.length, ptr<int64_t>(mm), ex.stream);
+  const std::vector<int64_t> h = to_host_vec(mm);
+  return h[0] == h[1] && h[0] > 0 && h[0] <= 64 ? h[0] : -1;
+}
+
+static TablePtr radix_groupby(const TablePtr &tin, const std::vector<int> &keys, const std::vector<AggSpec> &aggs) {
+  const int64_t n = tin->Rows();
+  if (!tin->device().is_cuda() || n < radix_groupby_min_rows()) return nullptr;
+  // A fixed-length string key groups by its invertible word key h (ops/join.cpp uses the same key):
+  // equal h + equal words 1..W-1 means equal strings, so the words ride along as MIN and MAX
+  // accumulators and the result is exact when MIN == MAX in every group (else: the exact path).
+  // The output key bytes are rebuilt from h and the MIN words.
+  TablePtr t = tin;
+  GroupKey gkey;
+  int wfirst = -1;  // column of word 1 in the augmented table
+  at::Tensor wk;
+  if (keys.size() == 1 && tin->column(keys[0]).is_var()) {
+    const Column &kc = tin->column(keys[0]);
+    Exec ex0(tin->device());
+    const int64_t L = fixed_string_len(ex0, kc);
+    if (L < 0) return nullptr;
+    const int64_t W = (L + 7) / 8;
+    const int64_t o0 = read_i64(kc.offsets, 0);
+    wk = ex0.empty_i64(n);
+    std::vector<Column> cols = tin->columns();
+    std::vector<int64_t *> wp{nullptr};
+    wfirst = (int)cols.size();
+    for (int64_t j = 1; j < W; ++j) {
+      cols.emplace_back("__gw" + std::to_string(j), DataType(Type::INT64), n, ex0.empty_i64(n));
+      wp.push_back(ptr<int64_t>(cols.back().data));
+    }
+    hip::bytes_to_words(ptr<uint8_t>(kc.data) + o0, n, (int)L, wp.data(), ex0.stream,
+                        reinterpret_cast<uint64_t *>(ptr<int64_t>(wk)), true);
+    t = Table::Make(tin->GetContext(), std::move(cols));
+    gkey.wlen = L;
+    gkey.cols = keys;
+    gkey.k = wk;
+  }
   struct Plan {
     int col, kind;  // kind: 0 SUMF 1 SUMI 2 MIN 3 MAX 4 CNT 5 M2
   };
@@ -441,11 +484,16 @@ static TablePtr radix_groupby(const TablePtr &t, const std::vector<int> &keys, c
       default: return nullptr;
     }
   }
+  if (gkey.wlen > 0) {
+    for (int c = wfirst; c < t->Columns(); ++c) {
+      gkey.wmin.push_back(need(c, 2));
+      gkey.wmax.push_back(need(c, 3));
+    }
+  }
   // the LDS aggregation kernels are instantiated with 1, 2, 3, 4 or 8 accumulator planes
   if (plan.empty() || plan.size() > 8) return nullptr;
   Exec ex(t->device());
-  GroupKey gkey;
-  if (!group_key(ex, t, keys, gkey)) return nullptr;
+  if (gkey.wlen < 0 && !group_key(ex, t, keys, gkey)) return nullptr;
   const int nacc = (int)plan.size();
   const at::Tensor &kt = gkey.k;
   double est;
@@ -527,7 +575,33 @@ static TablePtr radix_groupby(const TablePtr &t, const std::vector<int> &keys, c
   trace::add_counter("groupby.radix.groups", ng);
   if (gkey.composite) trace::add_counter("groupby.radix.composite_key", 1);
   auto plane = [&](int j) { return gacc.slice(0, j * ng, (j + 1) * ng); };
-  std::vector<Column> out = group_key_columns(t, gkey, gkeys);
+  std::vector<Column> out;
+  if (gkey.wlen > 0) {
+    if (!gkey.wmin.empty()) {  // exact iff every group's words 1..W-1 agree (a 64-bit h collision: not)
+      std::vector<at::Tensor> ne;
+      for (size_t j = 0; j < gkey.wmin.size(); ++j) ne.push_back(plane(gkey.wmin[j]).ne(plane(gkey.wmax[j])).any());
+      if (at::stack(ne).any().item<bool>()) {
+        trace::add_counter("groupby.radix.word_key_collision_fallback", 1);
+        return nullptr;
+      }
+    }
+    const Column &kc = t->column(keys[0]);
+    const int64_t L = gkey.wlen;
+    std::vector<at::Tensor> wcols;  // the words from the MIN planes (which hold order images)
+    std::vector<const int64_t *> wp{nullptr};
+    for (size_t j = 0; j < gkey.wmin.size(); ++j) {
+      wcols.push_back(minmax_col(ex, "", t->column(wfirst + (int)j), plane(gkey.wmin[j]).contiguous(), at::Tensor()).data);
+      wp.push_back(ptr<int64_t>(wcols.back()));
+    }
+    at::Tensor bytes = ex.empty_bytes(std::max<int64_t>(1, ng * L));
+    if (ng > 0)
+      hip::words_to_bytes(wp.data(), ng, (int)L, ptr<uint8_t>(bytes), ex.stream,
+                          reinterpret_cast<const uint64_t *>(ptr<int64_t>(gkeys)));
+    out.emplace_back(kc.name, kc.type, ng, bytes.slice(0, 0, ng * L), at::arange(0, (ng + 1) * L, L, ex.opts(at::kLong)));
+    trace::add_counter("groupby.radix.word_key", 1);
+  } else {
+    out = group_key_columns(t, gkey, gkeys);
+  }
   for (const auto &o : outs) {
     const Column &c = t->column(o.col);
     const std::string name = std::string(AggPrefix(o.op)) + c.name;

@@ -291,6 +291,23 @@ def test_radix_groupby_extended(gpu_ctx, monkeypatch, case):
     pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-8, atol=1e-8)
 
 
+@pytest.mark.parametrize("fmt", ["s{:06d}", "key-{:09d}", "key-{:020d}", "key-{:011d}/bin"])
+def test_radix_groupby_string_word_key(gpu_ctx, monkeypatch, fmt):
+    """A fixed-length string key groups on the LDS radix path by its invertible word key: words
+    1..W-1 ride along as MIN / MAX accumulators (equal in every group = exact), and the output key
+    bytes are rebuilt from the key and the MIN words.  7 bytes (one word), 13 (unaligned), 24
+    (three aligned words) and 19-byte binary; against the global path and the CPU twin."""
+    rng = np.random.default_rng(14)
+    n = 600_000
+    ids = rng.integers(0, 40_000, n)
+    vals = [fmt.format(x).encode() for x in ids] if fmt.endswith("/bin") else [fmt.format(x) for x in ids]
+    t = pa.table({"s": pa.array(vals), "x": rng.standard_normal(n), "k": rng.integers(-50, 50, n)})
+    res, cnt = _groupby_both(Table(t, gpu_ctx), ["s"], {"x": ["sum", "mean"], "k": ["max"]}, monkeypatch)
+    assert cnt[0].get("groupby.radix.word_key", 0) == 1, cnt[0]
+    assert cnt[0].get("groupby.radix.groups", 0) == len(res[0]) == len(np.unique(ids)), cnt[0]
+    pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-8, atol=1e-8)
+
+
 @pytest.mark.parametrize("case", ["with_sum", "alone", "two_keys"])
 def test_radix_groupby_nunique(gpu_ctx, monkeypatch, case):
     """NUNIQUE on the radix path: distinct (keys, x) pairs by a radix group-by, counted per key, LEFT
