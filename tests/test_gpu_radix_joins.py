@@ -485,3 +485,23 @@ def test_radix_join_memory_bounded_chunks(gpu_ctx, ctx, monkeypatch, how):
     assert c.get("join.radix.memory_chunks", 0) >= 2, c
     assert len(got) == len(exp)
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
+
+
+@pytest.mark.parametrize("how", ["inner", "outer"])
+def test_radix_join_memory_bounded_chunks_string_key(gpu_ctx, ctx, monkeypatch, how):
+    """Bounded memory with a 16-byte string key: the key-hash chunks split the proxies (word key +
+    word 1 + payload) and each chunk joins into the sink without narrowing the word key."""
+    rng = np.random.default_rng(67)
+    n = 2_000_000
+    ids_a, ids_b = rng.integers(0, 1_500_000, n), rng.integers(0, 1_500_000, n)
+    a = pa.table({"s": pa.array([f"k{x:015d}" for x in ids_a]), "v": rng.random(n)})
+    b = pa.table({"s": pa.array([f"k{x:015d}" for x in ids_b]), "w": rng.random(n)})
+    gpu_ctx.add_config("memory_budget_mb", "150")
+    try:
+        got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["s"], monkeypatch)
+    finally:
+        gpu_ctx.add_config("memory_budget_mb", "")
+    assert c.get("join.radix.memory_chunks", 0) >= 2, c
+    assert c.get("join.radix.narrow_fallback", 0) == 0, c
+    assert len(got) == len(exp)
+    pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
