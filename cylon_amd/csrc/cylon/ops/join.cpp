@@ -1235,8 +1235,8 @@ static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr
   }
   k.verify = true;
   if (words_ok && lc.size() == 1 && left->device().is_cuda()) {
-    // one fixed-length string key per side: the word columns the radix join carries and the row hash
-    // come out of one read of the bytes (the proxies below take the words)
+    // one fixed-length string key per side: its invertible word key (the join key, standing in for
+    // word 0) and words 1..W-1 come out of one read of the bytes (the proxies below carry them)
     const int64_t L = fixed_var_len(ex, left->column(lc[0]));
     if (L > 0 && fixed_var_len(ex, right->column(rc[0])) == L) {
       k.wlen = L;
