@@ -311,7 +311,10 @@ std::shared_ptr<MemoryPool> CylonContext::GetMemoryPool() {
 int64_t CylonContext::DeviceHeadroom() const {
   if (!device_.is_cuda()) return 0;
   size_t free_b = 0, total_b = 0;
-  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+  {
+    c10::hip::HIPGuard guard(device_.index());  // hipMemGetInfo reports the CURRENT device
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+  }
   auto stats = c10::hip::HIPCachingAllocator::getDeviceStats(device_.index());
   const size_t agg = static_cast<size_t>(c10::CachingAllocator::StatType::AGGREGATE);
   int64_t h = (int64_t)free_b + stats.reserved_bytes[agg].current - stats.allocated_bytes[agg].current;

@@ -426,6 +426,121 @@ __global__ void k_words_mismatch(ConstWordPtrs a, ConstWordPtrs b, int W, const 
   if ((threadIdx.x & (kWave - 1)) == 0 && c) atomicAdd(nbad, c);
 }
 
+// ---- variable-length strings as W zero-padded words + a length (the padded word key: the fixed-length
+// invertible key of hash.hpp over W words, seeded with the row's own length).  A row's bytes are read
+// as the aligned 8-byte words that hold at least one of its bytes (never past its last byte's word,
+// so never into another page) and funnel-shifted into place.
+__global__ void k_var_to_words(const uint8_t *__restrict__ bytes, const int64_t *__restrict__ offs, int64_t n, int W,
+                               WordPtrs out, uint64_t *__restrict__ hash, int64_t *__restrict__ lens,
+                               uint64_t *__restrict__ h2) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t o = offs[i], L = offs[i + 1] - o;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(bytes + o);
+    const uint64_t *p = reinterpret_cast<const uint64_t *>(a & ~uintptr_t(7));
+    const int sh = (int)(a & 7) * 8;
+    const int64_t nw = ((int64_t)(a & 7) + L + 7) >> 3;  // aligned words holding the row's bytes
+    uint64_t g = hashing::word_key_seed(L), w0 = 0, s2 = 0xC2B2AE3D27D4EB4FULL ^ (uint64_t)L;
+    uint64_t cur = nw > 0 ? p[0] : 0;
+    for (int j = 0; j < W; ++j) {
+      const uint64_t nxt = j + 1 < nw ? p[j + 1] : 0;
+      uint64_t v = sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
+      const int64_t rem = L - 8 * (int64_t)j;  // row bytes from word j on
+      if (rem <= 0) v = 0;
+      else if (rem < 8) v &= (uint64_t(1) << (8 * rem)) - 1;
+      cur = nxt;
+      if (j == 0) w0 = v;
+      else {
+        out.w[j][i] = (int64_t)v;
+        g = hashing::word_key_step(g, v);
+      }
+      s2 = hashing::fmix64((s2 + v) * 0x87C37B91114253D5ULL) ^ 0x4CF5AD432745937FULL;
+    }
+    hash[i] = hashing::fmix64(w0 ^ g);
+    lens[i] = L;
+    if (h2) h2[i] = s2;
+  }
+}
+
+__global__ void k_words_to_var(ConstWordPtrs in, const uint64_t *__restrict__ hash, const int64_t *__restrict__ lens,
+                               const int64_t *__restrict__ ooffs, int64_t n, int W, uint8_t *__restrict__ bytes) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t L = lens[i];
+    uint8_t *dst = bytes + ooffs[i];
+    uint64_t g = hashing::word_key_seed(L);
+    for (int j = 1; j < W; ++j) g = hashing::word_key_step(g, (uint64_t)in.w[j][i]);
+    for (int j = 0; j < W && 8 * j < L; ++j) {
+      const uint64_t v = j == 0 ? hashing::fmix64_inv(hash[i]) ^ g : (uint64_t)in.w[j][i];
+      const int64_t nb = L - 8 * j < 8 ? L - 8 * j : 8;
+      uint8_t *d = dst + 8 * j;
+      if (nb == 8 && (reinterpret_cast<uintptr_t>(d) & 7) == 0) {
+        *reinterpret_cast<uint64_t *>(d) = v;
+      } else if (nb == 8 && (reinterpret_cast<uintptr_t>(d) & 3) == 0) {
+        reinterpret_cast<uint32_t *>(d)[0] = (uint32_t)v;
+        reinterpret_cast<uint32_t *>(d)[1] = (uint32_t)(v >> 32);
+      } else {
+        for (int b = 0; b < nb; ++b) d[b] = (uint8_t)(v >> (8 * b));
+      }
+    }
+  }
+}
+
+// two independent 64-bit hashes of rows of any length (the group-by's string key h and its check
+// h2): different seeds, and h2 mixes with a different multiplier and an add instead of a xor
+__global__ void k_var_hash2(const uint8_t *__restrict__ bytes, const int64_t *__restrict__ offs, int64_t n,
+                            uint64_t *__restrict__ h1, uint64_t *__restrict__ h2) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t o = offs[i], L = offs[i + 1] - o;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(bytes + o);
+    const uint64_t *p = reinterpret_cast<const uint64_t *>(a & ~uintptr_t(7));
+    const int sh = (int)(a & 7) * 8;
+    const int64_t nw = ((int64_t)(a & 7) + L + 7) >> 3, W = (L + 7) >> 3;
+    uint64_t x = hashing::word_key_seed(L), y = 0xC2B2AE3D27D4EB4FULL ^ (uint64_t)L;
+    uint64_t cur = nw > 0 ? p[0] : 0;
+    for (int64_t j = 0; j < W; ++j) {
+      const uint64_t nxt = j + 1 < nw ? p[j + 1] : 0;
+      uint64_t v = sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
+      const int64_t rem = L - 8 * j;
+      if (rem < 8) v &= (uint64_t(1) << (8 * rem)) - 1;
+      cur = nxt;
+      x = hashing::word_key_step(x, v);
+      y = hashing::fmix64((y + v) * 0x87C37B91114253D5ULL) ^ 0x4CF5AD432745937FULL;
+    }
+    h1[i] = hashing::fmix64(x);
+    h2[i] = y;
+  }
+}
+
+void var_hash2(const uint8_t *bytes, const int64_t *offs, int64_t n, uint64_t *h1, uint64_t *h2, void *stream) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_var_hash2, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), bytes, offs, n, h1, h2);
+  HIP_LAUNCH_CHECK();
+}
+
+void var_to_words(const uint8_t *bytes, const int64_t *offs, int64_t n, int W, int64_t *const *words, uint64_t *hash,
+                  int64_t *lens, uint64_t *h2, void *stream) {
+  CYLON_CHECK(W >= 1 && W <= kMaxWords && hash && lens, Code::Invalid, "padded string words: W " << W);
+  if (n == 0) return;
+  WordPtrs o{};
+  for (int j = 1; j < W; ++j) o.w[j] = words[j];
+  hipLaunchKernelGGL(k_var_to_words, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), bytes, offs, n, W, o, hash,
+                     lens, h2);
+  HIP_LAUNCH_CHECK();
+}
+
+void words_to_var(const int64_t *const *words, const uint64_t *hash, const int64_t *lens, const int64_t *out_offs,
+                  int64_t n, int W, uint8_t *bytes, void *stream) {
+  CYLON_CHECK(W >= 1 && W <= kMaxWords && hash, Code::Invalid, "padded string words: W " << W);
+  if (n == 0) return;
+  ConstWordPtrs in{};
+  for (int j = 1; j < W; ++j) in.w[j] = words[j];
+  hipLaunchKernelGGL(k_words_to_var, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), in, hash, lens, out_offs,
+                     n, W, bytes);
+  HIP_LAUNCH_CHECK();
+}
+
 // mm[0] = min, mm[1] = max of the row lengths offs[i + 1] - offs[i] (mm preset to {~0, 0})
 __global__ void k_len_minmax(const int64_t *__restrict__ offs, int64_t n, unsigned long long *mm) {
   unsigned long long lo = ~0ull, hi = 0ull;

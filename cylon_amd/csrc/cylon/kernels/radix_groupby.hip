@@ -292,6 +292,138 @@ __global__ void k_rg_pack(const int64_t *__restrict__ offs, const int64_t *__res
   }
 }
 
+// ---- QUANTILE on the radix path.  The rows (group key, value) are partitioned
+// by the group key's hash into partitions of <= kQCap rows; one workgroup sorts a partition in LDS by
+// (key, value) -- a bitonic network over the next power of two, pad rows (~0, ~0) last -- so every
+// group is a run with its valid values first, ascending (a null value's image ~0 sorts after every
+// valid one: NaNs are canonicalised to the positive quiet NaN, whose image is below ~0).  The thread
+// at a run's first row counts the run's valid values and applies the global path's type-2 rule
+// (groupby.hip k_quantile), and the groups are compacted with a block scan into the slab at the
+// partition's row offset (groups <= rows), as k_rg_agg does; radix_groupby_pack then packs them.
+constexpr int kQCap = 4096, kQThreads = 512, kQPer = kQCap / kQThreads;
+
+// block-wide exclusive scan of one uint32 per thread
+__device__ __forceinline__ uint32_t q_block_exscan(uint32_t c, uint32_t *wsum) {
+  const int lane = lane_id(), wave = threadIdx.x / kWave;
+  uint32_t inc = c;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t t = __shfl_up(inc, d, kWave);
+    if (lane >= d) inc += t;
+  }
+  if (lane == kWave - 1) wsum[wave] = inc;
+  __syncthreads();
+  uint32_t off = 0;
+#pragma unroll
+  for (int w = 0; w < kQThreads / kWave; ++w) off += (w < wave) ? wsum[w] : 0u;
+  return off + inc - c;
+}
+
+__device__ __forceinline__ uint64_t q_image(double d) {
+  uint64_t b = (uint64_t)__double_as_longlong(d != d ? __longlong_as_double(0x7ff8000000000000ll) : d);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double q_unimage(uint64_t m) {
+  return __longlong_as_double((long long)((m >> 63) ? (m & 0x7fffffffffffffffull) : ~m));
+}
+
+__global__ __launch_bounds__(kQThreads) void k_rg_quantile(const int64_t *__restrict__ keys,
+                                                           const uint8_t *__restrict__ vals, int vwidth, int vkind,
+                                                           const uint8_t *__restrict__ valid,
+                                                           const int64_t *__restrict__ offs, int64_t nparts, double q,
+                                                           int64_t *__restrict__ okeys, uint64_t *__restrict__ oq,
+                                                           uint64_t *__restrict__ ovalid, int64_t *__restrict__ gcount,
+                                                           int *__restrict__ overflow) {
+  __shared__ uint64_t sk[kQCap], sv[kQCap];
+  __shared__ uint32_t wsum[kQThreads / kWave];
+  for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
+    const int64_t b = offs[p], cnt = offs[p + 1] - b;
+    if (cnt > kQCap) {
+      if (threadIdx.x == 0) {
+        atomicOr(overflow, 1);
+        gcount[p] = 0;
+      }
+      continue;
+    }
+    int P = 1;
+    while (P < cnt) P <<= 1;
+    for (int i = threadIdx.x; i < P; i += kQThreads) {
+      if (i < cnt) {
+        sk[i] = (uint64_t)keys[b + i];
+        sv[i] = (valid == nullptr || valid[b + i]) ? q_image(rg_double(load_bits(vals, b + i, vwidth), vwidth, vkind))
+                                                   : ~0ull;
+      } else {
+        sk[i] = ~0ull;
+        sv[i] = ~0ull;
+      }
+    }
+    __syncthreads();
+    for (int size = 2; size <= P; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int i = threadIdx.x; i < (P >> 1); i += kQThreads) {
+          const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+          const bool up = (lo & size) == 0;
+          const uint64_t ka = sk[lo], kb = sk[hi], va = sv[lo], vb = sv[hi];
+          const bool gt = ka > kb || (ka == kb && va > vb);
+          if (gt == up) {
+            sk[lo] = kb;
+            sk[hi] = ka;
+            sv[lo] = vb;
+            sv[hi] = va;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // group starts among the first cnt sorted rows (pads sort last; a pad equal to a real row is
+    // interchangeable with it); thread t owns rows [t * kQPer, t * kQPer + kQPer)
+    uint32_t mine = 0;
+#pragma unroll
+    for (int u = 0; u < kQPer; ++u) {
+      const int i = threadIdx.x * kQPer + u;
+      mine += (i < cnt && (i == 0 || sk[i] != sk[i - 1])) ? 1u : 0u;
+    }
+    const uint32_t ex = q_block_exscan(mine, wsum);
+    uint32_t g = ex;
+#pragma unroll 1
+    for (int u = 0; u < kQPer; ++u) {
+      const int i = threadIdx.x * kQPer + u;
+      if (!(i < cnt && (i == 0 || sk[i] != sk[i - 1]))) continue;
+      int e = i + 1;
+      while (e < cnt && sk[e] == sk[i]) ++e;
+      int nv = 0;  // valid values: the run's first rows
+      while (i + nv < e && sv[i + nv] != ~0ull) ++nv;
+      double r = 0.0;
+      if (nv > 0) {
+        const double np = (double)nv * q, j = floor(np), gg = np - j;
+        int pos = (int)j;
+        if (pos >= nv) pos = nv - 1;
+        r = (gg == 0.0 && pos > 0) ? 0.5 * (q_unimage(sv[i + pos - 1]) + q_unimage(sv[i + pos])) : q_unimage(sv[i + pos]);
+      }
+      okeys[b + g] = (int64_t)sk[i];
+      oq[b + g] = (uint64_t)__double_as_longlong(r);
+      ovalid[b + g] = nv > 0 ? 1ull : 0ull;
+      ++g;
+    }
+    if (threadIdx.x == kQThreads - 1) gcount[p] = ex + mine;
+    __syncthreads();
+  }
+}
+
+int64_t radix_quantile_capacity() { return kQCap; }
+
+void radix_groupby_quantile(const int64_t *keys, const uint8_t *vals, int vwidth, int vkind, const uint8_t *valid,
+                            const int64_t *offs, int64_t nparts, double q, int64_t *okeys, uint64_t *oq,
+                            uint64_t *ovalid, int64_t *gcount, int *overflow, void *stream) {
+  hipStream_t s = as_stream(stream);
+  HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
+  if (nparts == 0) return;
+  const int grid = (int)std::min<int64_t>(nparts, 8 * 256);
+  hipLaunchKernelGGL(k_rg_quantile, dim3(grid), dim3(kQThreads), 0, s, keys, vals, vwidth, vkind, valid, offs, nparts,
+                     q, okeys, oq, ovalid, gcount, overflow);
+  HIP_LAUNCH_CHECK();
+}
+
 int64_t distinct_estimate_workspace() { return kHllRegs; }
 
 template <int A, int S>

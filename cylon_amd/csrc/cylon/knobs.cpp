@@ -34,6 +34,7 @@ const std::vector<KnobInfo> &Registry() {
       {"RJ_FUSED_MIN_PARTS", "test", "partitions from which the sampled output estimate is used (4096)"},
       {"RJ_ESTIMATE_SCALE", "test", "scales the sampled output estimate (< 1 forces the exact rerun)"},
       {"RJ_SHARE_KEY", "test", "0: an inner join writes the build side's key column instead of sharing the probe side's"},
+      {"RJ_VAR_WORDS", "test", "0: variable-length string keys / payloads travel as a row number + byte gather, not padded words"},
       {"RJ_EXTRA_BITS", "test", "extra join partition bits (finer partitions)"},
       {"RJ_SPLIT_ROWS", "test", "build rows per chunk of a split (skewed) join partition (default: LDS capacity)"},
       {"SORT_LOOKBACK", "test", "0: sorts use the exact per-tile histogram passes"},

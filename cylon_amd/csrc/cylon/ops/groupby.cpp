@@ -262,6 +262,10 @@ struct GroupKey {
   // wmin / wmax the accumulators of MIN / MAX of its words 1..W-1 (equal in every group: exact)
   int64_t wlen = -1;
   std::vector<int> wmin, wmax;
+  // any other string key: k is a 64-bit hash of the bytes; wmin[0] / wmax[0] the MIN / MAX of an
+  // independent hash h2 (equal in every group: the groups are verified), rmin MIN of the row number
+  bool hashed = false;
+  int rmin = -1;
   bool null_group = false;  // nullable single integer key: null rows carry null_key (no valid key has it)
   int64_t null_key = 0;
   std::vector<int64_t> ncode;  // composite: field value of a null in key i (-1: the column has no nulls)
@@ -413,18 +417,45 @@ static int64_t fixed_string_len(const Exec &ex, const Column &c) {
   return h[0] == h[1] && h[0] > 0 && h[0] <= 64 ? h[0] : -1;
 }
 
-static TablePtr radix_groupby(const TablePtr &tin, const std::vector<int> &keys, const std::vector<AggSpec> &aggs) {
+static TablePtr radix_groupby(const TablePtr &tin, const std::vector<int> &keys, const std::vector<AggSpec> &aggs,
+                              bool hash_strings = false) {
   const int64_t n = tin->Rows();
   if (!tin->device().is_cuda() || n < radix_groupby_min_rows()) return nullptr;
   // A fixed-length string key groups by its invertible word key h (ops/join.cpp uses the same key):
   // equal h + equal words 1..W-1 means equal strings, so the words ride along as MIN and MAX
   // accumulators and the result is exact when MIN == MAX in every group (else: the exact path).
   // The output key bytes are rebuilt from h and the MIN words.
+  //
+  // Any other non-null string key (variable length, or words that would not fit the accumulator
+  // planes) groups by a 64-bit hash h of its bytes, with MIN and MAX of an independent 64-bit hash h2
+  // and MIN of the row number as accumulators: MIN(h2) == MAX(h2) in every group means all its rows
+  // agree on 128 hash bits (else: the exact path), and the output key is the bytes of each group's
+  // first row (one gather of ng rows).  Reference: hash_groupby.cpp:92-126 takes any key type.
   TablePtr t = tin;
   GroupKey gkey;
   int wfirst = -1;  // column of word 1 in the augmented table
+  int hcol = -1, rcol = -1;  // hashed string key: columns of h2 and of the row number
   at::Tensor wk;
   if (keys.size() == 1 && tin->column(keys[0]).is_var()) {
+    const Column &kc = tin->column(keys[0]);
+    if (kc.nullable() || !(kc.type.type == Type::STRING || kc.type.type == Type::BINARY)) return nullptr;
+    Exec ex0(tin->device());
+    if (hash_strings || fixed_string_len(ex0, kc) < 0) {
+      at::Tensor h1 = ex0.empty_i64(n), h2 = ex0.empty_i64(n);
+      hip::var_hash2(ptr<uint8_t>(kc.data), ptr<int64_t>(kc.offsets), n, reinterpret_cast<uint64_t *>(ptr<int64_t>(h1)),
+                     reinterpret_cast<uint64_t *>(ptr<int64_t>(h2)), ex0.stream);
+      std::vector<Column> cols = tin->columns();
+      hcol = (int)cols.size();
+      cols.emplace_back("__gh2", DataType(Type::INT64), n, h2);
+      rcol = (int)cols.size();
+      cols.emplace_back("__grow", DataType(Type::INT64), n, at::arange(n, ex0.opts(at::kLong)));
+      t = Table::Make(tin->GetContext(), std::move(cols));
+      gkey.hashed = true;
+      gkey.cols = keys;
+      gkey.k = h1;
+    }
+  }
+  if (keys.size() == 1 && tin->column(keys[0]).is_var() && !gkey.hashed) {
     const Column &kc = tin->column(keys[0]);
     Exec ex0(tin->device());
     const int64_t L = fixed_string_len(ex0, kc);
@@ -490,10 +521,20 @@ static TablePtr radix_groupby(const TablePtr &tin, const std::vector<int> &keys,
       gkey.wmax.push_back(need(c, 3));
     }
   }
-  // the LDS aggregation kernels are instantiated with 1, 2, 3, 4 or 8 accumulator planes
+  if (gkey.hashed) {
+    gkey.wmin.push_back(need(hcol, 2));
+    gkey.wmax.push_back(need(hcol, 3));
+    gkey.rmin = need(rcol, 2);
+  }
+  // the LDS aggregation kernels are instantiated with 1, 2, 3, 4 or 8 accumulator planes; a
+  // fixed-length key whose MIN / MAX words do not fit beside the aggregates is hashed instead
+  if (plan.size() > 8 && gkey.wlen > 0) {
+    trace::add_counter("groupby.radix.word_key_too_wide", 1);
+    return radix_groupby(tin, keys, aggs, true);
+  }
   if (plan.empty() || plan.size() > 8) return nullptr;
   Exec ex(t->device());
-  if (gkey.wlen < 0 && !group_key(ex, t, keys, gkey)) return nullptr;
+  if (gkey.wlen < 0 && !gkey.hashed && !group_key(ex, t, keys, gkey)) return nullptr;
   const int nacc = (int)plan.size();
   const at::Tensor &kt = gkey.k;
   double est;
@@ -576,7 +617,16 @@ static TablePtr radix_groupby(const TablePtr &tin, const std::vector<int> &keys,
   if (gkey.composite) trace::add_counter("groupby.radix.composite_key", 1);
   auto plane = [&](int j) { return gacc.slice(0, j * ng, (j + 1) * ng); };
   std::vector<Column> out;
-  if (gkey.wlen > 0) {
+  if (gkey.hashed) {
+    if (ng > 0 && plane(gkey.wmin[0]).ne(plane(gkey.wmax[0])).any().item<bool>()) {
+      trace::add_counter("groupby.radix.string_hash_collision_fallback", 1);
+      return nullptr;
+    }
+    const at::Tensor rep = minmax_col(ex, "", t->column(rcol), plane(gkey.rmin).contiguous(), at::Tensor()).data;
+    const Column &kc = t->column(keys[0]);
+    out.push_back(Gather(Table::Make(t->GetContext(), {kc}), rep)->column(0));
+    trace::add_counter("groupby.radix.hashed_string_key", 1);
+  } else if (gkey.wlen > 0) {
     if (!gkey.wmin.empty()) {  // exact iff every group's words 1..W-1 agree (a 64-bit h collision: not)
       std::vector<at::Tensor> ne;
       for (size_t j = 0; j < gkey.wmin.size(); ++j) ne.push_back(plane(gkey.wmin[j]).ne(plane(gkey.wmax[j])).any());
@@ -639,34 +689,116 @@ static TablePtr radix_groupby(const TablePtr &tin, const std::vector<int> &keys,
 static TablePtr groupby_with(const TablePtr &t, const std::vector<int> &keys, const std::vector<AggSpec> &aggs,
                              bool presorted);
 
-// NUNIQUE on the LDS radix path, composed from radix group-bys: the other aggregates of the keys
-// (one radix group-by), and per NUNIQUE column x the distinct (keys, x) pairs with x non-null (a
-// radix group-by on keys + x) counted per key (a group-by of those pairs); a LEFT join of the first
-// result with each count table on the keys puts them side by side (a group whose x is all null
-// counts 0).  Output order: join order (group-by order is unspecified, docs/semantics.md).
-static TablePtr radix_groupby_nunique(const TablePtr &t, const std::vector<int> &keys,
-                                      const std::vector<AggSpec> &aggs) {
+// QUANTILE on the LDS radix path (one (column, q) aggregate): the rows (group key, value[, validity])
+// are radix-partitioned by the key's hash into partitions of <= radix_quantile_capacity() rows, and
+// one workgroup per partition sorts them in LDS by (key, value) and takes each group's quantile by
+// the global path's type-2 rule (radix_groupby.hip k_rg_quantile).  nullptr when a partition
+// overflows (a group -- or a hash bucket of groups -- beyond the capacity): the caller falls back.
+// Reference: compute/aggregate_kernels.hpp:504-545 (QuantileKernel).
+static TablePtr radix_quantile_table(const TablePtr &t, const std::vector<int> &keys, const AggSpec &a) {
+  const Column &c = t->column(a.col);
+  const int w = c.type.width();
+  if (c.is_var() || c.type.kind() == ValueKind::FIXED_BYTES || !c.type.is_numeric() ||
+      !(w == 1 || w == 2 || w == 4 || w == 8))
+    return nullptr;
+  Exec ex(t->device());
+  GroupKey gkey;
+  if (!group_key(ex, t, keys, gkey)) return nullptr;
+  const int64_t n = t->Rows(), cap = hip::radix_quantile_capacity();
+  int bits = 0;  // mean rows per partition <= 0.85 capacity (the Poisson tail of hashed keys fits)
+  while (bits < 24 && (double)n / (double)(int64_t(1) << bits) > 0.85 * (double)cap) ++bits;
+  std::vector<at::Tensor> cols{gkey.k, c.data};
+  std::vector<int> widths{8, w};
+  if (c.nullable()) {
+    cols.push_back(c.validity);
+    widths.push_back(1);
+  }
+  at::Tensor offs;
+  if (bits > 0) {
+    CYLON_PHASE("groupby.radix.quantile_partition", ex.device);
+    cols = RadixPartition(ex, std::move(cols), widths, bits, &offs, nullptr, nullptr, false);
+  } else {
+    offs = at::tensor({int64_t(0), n}, at::TensorOptions().dtype(at::kLong)).to(ex.device);
+  }
+  const int64_t nparts = int64_t(1) << bits;
+  at::Tensor okeys = ex.empty_i64(n), oacc = ex.empty_i64(2 * n), gcount = ex.empty_i64(nparts);
+  at::Tensor overflow = at::empty({1}, ex.opts(at::kInt));
+  {
+    CYLON_PHASE("groupby.radix.quantile", ex.device);
+    hip::radix_groupby_quantile(ptr<int64_t>(cols[0]), reinterpret_cast<const uint8_t *>(cols[1].data_ptr()), w,
+                                static_cast<int>(c.type.kind()), c.nullable() ? cols[2].data_ptr<uint8_t>() : nullptr,
+                                ptr<int64_t>(offs), nparts, a.quantile, ptr<int64_t>(okeys),
+                                reinterpret_cast<uint64_t *>(ptr<int64_t>(oacc)),
+                                reinterpret_cast<uint64_t *>(ptr<int64_t>(oacc) + n), ptr<int64_t>(gcount),
+                                overflow.data_ptr<int>(), ex.stream);
+  }
+  if (overflow.item<int>() != 0) {
+    trace::add_counter("groupby.radix.quantile_overflow_fallback", 1);
+    return nullptr;
+  }
+  at::Tensor goff = exclusive_scan(ex, gcount);
+  const int64_t ng = read_i64(goff, nparts);
+  at::Tensor gkeys = ex.empty_i64(ng), gacc = ex.empty_i64(2 * ng);
+  if (ng > 0)
+    hip::radix_groupby_pack(ptr<int64_t>(offs), ptr<int64_t>(goff), nparts, ptr<int64_t>(okeys),
+                            reinterpret_cast<const uint64_t *>(ptr<int64_t>(oacc)), n, 2, ptr<int64_t>(gkeys),
+                            reinterpret_cast<uint64_t *>(ptr<int64_t>(gacc)), ng, ex.stream);
+  std::vector<Column> out = group_key_columns(t, gkey, gkeys);
+  out.push_back(double_col(std::string(AggPrefix(AGG_QUANTILE)) + c.name, gacc.slice(0, 0, ng).view(at::kDouble),
+                           gacc.slice(0, ng, 2 * ng).ne(0)));
+  trace::add_counter("groupby.radix.quantile", 1);
+  return Table::Make(t->GetContext(), std::move(out));
+}
+
+// NUNIQUE and QUANTILE on the LDS radix path, composed from radix group-bys: the other aggregates of
+// the keys (one radix group-by); per NUNIQUE column x the distinct (keys, x) pairs with x non-null
+// (a radix group-by on keys + x) counted per key (a group-by of those pairs); per QUANTILE aggregate
+// the LDS-sorted partitions above.  A LEFT join of the first result with each such (keys, value)
+// table on the keys puts them side by side (a group whose x is all null counts 0 / has a null
+// quantile).  Output order: join order (group-by order is unspecified, docs/semantics.md).
+static TablePtr radix_groupby_composed(const TablePtr &t, const std::vector<int> &keys,
+                                       const std::vector<AggSpec> &aggs) {
   if (!t->device().is_cuda() || t->Rows() < radix_groupby_min_rows()) return nullptr;
   std::vector<AggSpec> rest;
-  std::vector<int> nucols;
-  for (const auto &a : aggs) {
-    if (a.op != AGG_NUNIQUE) {
+  std::vector<int> nucols, qidx;  // NUNIQUE columns; indices of the QUANTILE aggregates
+  for (size_t i = 0; i < aggs.size(); ++i) {
+    const auto &a = aggs[i];
+    if (a.op == AGG_QUANTILE) {
+      qidx.push_back((int)i);
+    } else if (a.op != AGG_NUNIQUE) {
       rest.push_back(a);
     } else if (std::find(nucols.begin(), nucols.end(), a.col) == nucols.end()) {
       if (std::find(keys.begin(), keys.end(), a.col) != keys.end()) return nullptr;  // (nunique of a key: 1)
       nucols.push_back(a.col);
     }
   }
-  if (nucols.empty()) return nullptr;
+  if (nucols.empty() && qidx.empty()) return nullptr;
   for (int k : keys)
-    if (t->column(k).nullable() || t->column(k).is_var()) return nullptr;
+    if (t->column(k).is_var() || (!nucols.empty() && t->column(k).nullable())) return nullptr;
   const int nk = (int)keys.size();
-  const bool count_only = rest.empty();  // (a COUNT of the first key carries the groups, then dropped)
-  TablePtr base = radix_groupby(t, keys, count_only ? std::vector<AggSpec>{AggSpec{keys[0], AGG_COUNT}} : rest);
-  if (!base) return nullptr;
   std::vector<int> kidx(nk);
   for (int i = 0; i < nk; ++i) kidx[i] = i;
-  TablePtr cur = base;  // columns: keys, rest aggregates, then one (keys, count) block per joined column
+  // the base: the rest aggregates, or the first quantile table, or a COUNT carrying the groups
+  TablePtr cur;
+  std::vector<int> qpos(aggs.size(), -1);  // column of cur holding quantile aggregate i
+  size_t qfirst = 0;
+  if (!rest.empty()) {
+    cur = radix_groupby(t, keys, rest);
+  } else if (!qidx.empty()) {
+    cur = radix_quantile_table(t, keys, aggs[(size_t)qidx[0]]);
+    qpos[(size_t)qidx[0]] = nk;
+    qfirst = 1;
+  } else {
+    cur = radix_groupby(t, keys, {AggSpec{keys[0], AGG_COUNT}});
+  }
+  if (!cur) return nullptr;
+  for (size_t j = qfirst; j < qidx.size(); ++j) {
+    TablePtr qt = radix_quantile_table(t, keys, aggs[(size_t)qidx[j]]);
+    if (!qt) return nullptr;
+    const int width = cur->Columns();
+    cur = Join(cur, qt, join::config::JoinConfig::LeftJoin(kidx, kidx, join::config::HASH));
+    qpos[(size_t)qidx[j]] = width + nk;
+  }
   std::vector<int> nupos;  // column of cur holding the count of nucols[i]
   for (int x : nucols) {
     std::vector<int> pc(keys);
@@ -681,11 +813,16 @@ static TablePtr radix_groupby_nunique(const TablePtr &t, const std::vector<int> 
     cur = Join(cur, counts, join::config::JoinConfig::LeftJoin(kidx, kidx, join::config::HASH));
     nupos.push_back(width + nk);
   }
-  trace::add_counter("groupby.radix.nunique_columns", (int64_t)nucols.size());
+  if (!nucols.empty()) trace::add_counter("groupby.radix.nunique_columns", (int64_t)nucols.size());
   std::vector<Column> out;
   for (int i = 0; i < nk; ++i) out.push_back(cur->column(i).with_name(t->column(keys[i]).name));
   int ri = 0;
-  for (const auto &a : aggs) {
+  for (size_t i = 0; i < aggs.size(); ++i) {
+    const auto &a = aggs[i];
+    if (a.op == AGG_QUANTILE) {
+      out.push_back(cur->column(qpos[i]).with_name(std::string(AggPrefix(AGG_QUANTILE)) + t->column(a.col).name));
+      continue;
+    }
     if (a.op != AGG_NUNIQUE) {
       out.push_back(cur->column(nk + ri++));
       continue;
@@ -704,7 +841,7 @@ static TablePtr groupby_with(const TablePtr &t, const std::vector<int> &keys, co
   CYLON_CHECK(!keys.empty(), Code::Invalid, "group-by needs at least one key column");
   if (!presorted) {
     if (TablePtr r = radix_groupby(t, keys, aggs)) return r;
-    if (TablePtr r = radix_groupby_nunique(t, keys, aggs)) return r;
+    if (TablePtr r = radix_groupby_composed(t, keys, aggs)) return r;
   }
   Exec ex(t->device());
   GroupInfo gi;

@@ -1117,11 +1117,18 @@ struct RadixKeys {
   // all from one read of the bytes
   std::vector<at::Tensor> lwords, rwords;
   int64_t wlen = -1;
+  // one variable-length string key per side, every row <= 64 bytes: W = vw zero-padded words, l / r
+  // the padded word keys (word 0's stand-in), lwords / rwords words 1..W-1, llen / rlen the lengths
+  int vw = 0;
+  at::Tensor llen, rlen;
 };
 
 static int64_t fixed_var_len(const Exec &ex, const Column &c);
 static std::vector<at::Tensor> var_to_words(const Exec &ex, const Column &c, int64_t L, at::Tensor *hash = nullptr,
                                             bool inv = false);
+static std::pair<int64_t, int64_t> var_len_range(const Exec &ex, const Column &c);
+static std::vector<at::Tensor> var_to_padded(const Exec &ex, const Column &c, int W, at::Tensor *key,
+                                             at::Tensor *lens);
 
 static bool int_key(const Column &c) {
   return simple_key(c) && (c.type.kind() == ValueKind::SIGNED_INT ||
@@ -1245,6 +1252,21 @@ static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr
       trace::add_counter("join.radix.hashed_key", 1);
       return k;
     }
+    // variable-length rows of <= 64 bytes: zero-padded words + the length (the padded word key seeds
+    // its chain with the row's length, so equal keys + equal words 1..W-1 + equal lengths <=> equal
+    // strings), no row-number gather of the key bytes after the join
+    const Column &a = left->column(lc[0]), &b = right->column(rc[0]);
+    if (a.is_var() && b.is_var() && knobs::Flag("RJ_VAR_WORDS", true)) {
+      const auto ra = var_len_range(ex, a), rb = var_len_range(ex, b);
+      const int64_t hi = std::max(ra.second, rb.second);
+      if (ra.first >= 0 && rb.first >= 0 && hi <= 64) {
+        k.vw = (int)std::max<int64_t>(1, (hi + 7) / 8);
+        k.lwords = var_to_padded(ex, a, k.vw, &k.l, &k.llen);
+        k.rwords = var_to_padded(ex, b, k.vw, &k.r, &k.rlen);
+        trace::add_counter("join.radix.var_word_key", 1);
+        return k;
+      }
+    }
   }
   k.l = encode_keys(ex, left, lc, false).keys;  // row hash of the key columns
   k.r = encode_keys(ex, right, rc, false).keys;
@@ -1315,7 +1337,7 @@ static at::Tensor key_chunk_ids(const at::Tensor &k, int64_t C) {  // independen
 }
 
 static int radix_join_chunks(const Exec &ex, const TablePtr &l, const TablePtr &r, const at::Tensor &lk,
-                             const at::Tensor &rk) {
+                             const at::Tensor &rk, JoinType jt) {
   if (!ex.gpu) return 1;
   const int64_t head = l->GetContext()->DeviceHeadroom();
   if (head <= 0) return 1;
@@ -1324,8 +1346,11 @@ static int radix_join_chunks(const Exec &ex, const TablePtr &l, const TablePtr &
   const int64_t work = (int64_t)(1.17 * (double)(bl + br)) + (int64_t)(1.03 * (double)std::max(bl, br));
   const int64_t out_row = radix_row_bytes(l) + radix_row_bytes(r);
   const double budget = 0.92 * (double)head;
-  // one output row per row of the larger side, with room to spare: no estimate needed
-  if ((double)work + 1.5 * (double)(std::max(nl, nr) * out_row) <= budget) return 1;
+  // one output row per row of the larger side, with room to spare (plus every preserved row of an
+  // outer join): no estimate needed
+  const int64_t outer_rows = (jt == JoinType::LEFT || jt == JoinType::FULL_OUTER ? nl : 0) +
+                             (jt == JoinType::RIGHT || jt == JoinType::FULL_OUTER ? nr : 0);
+  if ((double)work + (1.5 * (double)std::max(nl, nr) + (double)outer_rows) * (double)out_row <= budget) return 1;
   int64_t est = 0;
   {  // exact join of a 1/1024 hash sample of both key sets, scaled up
     at::Tensor sl = at::bitwise_and(at::bitwise_right_shift(lk * (int64_t)0x632BE59BD9B4E019ll, 40), 1023).eq(0);
@@ -1333,6 +1358,9 @@ static int radix_join_chunks(const Exec &ex, const TablePtr &l, const TablePtr &
     auto pr = hash_join_pairs(ex, lk.masked_select(sl), rk.masked_select(sr));
     est = (int64_t)(1.1 * 1024.0 * (double)pr.first.numel()) + 65536;
   }
+  // the sample counts matched pairs only: an outer join also emits its preserved side's unmatched
+  // rows -- up to all of them (a low-match join), so they are added in full
+  est += outer_rows;
   const double out_bytes = (double)est * (double)out_row;
   if ((double)work + out_bytes <= budget) return 1;
   const double room = budget - out_bytes;
@@ -1397,6 +1425,56 @@ static std::vector<at::Tensor> var_to_words(const Exec &ex, const Column &c, int
   return out;
 }
 
+// {min, max} row length of a non-null string / binary column, or {-1, -1}
+static std::pair<int64_t, int64_t> var_len_range(const Exec &ex, const Column &c) {
+  if (c.nullable() || !(c.type.type == Type::STRING || c.type.type == Type::BINARY)) return {-1, -1};
+  if (c.length == 0) return {0, 0};
+  at::Tensor mm = ex.empty_i64(2);
+  hip::var_len_minmax(ptr<int64_t>(c.offsets), c.length, ptr<int64_t>(mm), ex.stream);
+  const std::vector<int64_t> h = to_host_vec(mm);
+  return {h[0], h[1]};
+}
+
+// a variable-length column (rows <= 8 W bytes) as W zero-padded words: *key = the padded word key
+// (word 0's stand-in), *lens = the row lengths; returns words 1..W-1.  One read of the bytes.
+static std::vector<at::Tensor> var_to_padded(const Exec &ex, const Column &c, int W, at::Tensor *key,
+                                             at::Tensor *lens) {
+  const int64_t n = c.length;
+  *key = ex.empty_i64(n);
+  *lens = ex.empty_i64(n);
+  std::vector<at::Tensor> out;
+  std::vector<int64_t *> wp{nullptr};
+  for (int j = 1; j < W; ++j) {
+    out.push_back(ex.empty_i64(n));
+    wp.push_back(ptr<int64_t>(out.back()));
+  }
+  hip::var_to_words(ptr<uint8_t>(c.data), ptr<int64_t>(c.offsets), n, W, wp.data(),
+                    reinterpret_cast<uint64_t *>(ptr<int64_t>(*key)), ptr<int64_t>(*lens), nullptr, ex.stream);
+  return out;
+}
+
+// wc = {padded word key, words 1..W-1, lengths} of m rows -> a string / binary column (rows whose
+// length column is null -- an outer join's absent side -- become null, zero bytes)
+static Column padded_to_var(const Exec &ex, const std::string &name, const DataType &type,
+                            const std::vector<Column> &wc, int W) {
+  const Column &lc = wc[(size_t)W];
+  const int64_t m = lc.length;
+  at::Tensor lens = lc.data.slice(0, 0, m);
+  if (lc.nullable()) lens = at::where(lc.validity.slice(0, 0, m).to(at::kBool), lens, at::zeros({1}, lens.options()));
+  at::Tensor offs = at::zeros({m + 1}, ex.opts(at::kLong));
+  if (m) {
+    at::Tensor tail = offs.slice(0, 1, m + 1);
+    at::cumsum_out(tail, lens, 0);
+  }
+  const int64_t nbytes = m ? read_i64(offs, m) : 0;
+  at::Tensor bytes = ex.empty_bytes(std::max<int64_t>(1, nbytes));
+  std::vector<const int64_t *> wp;
+  for (int j = 0; j < W; ++j) wp.push_back(ptr<int64_t>(wc[(size_t)j].data));
+  hip::words_to_var(wp.data(), reinterpret_cast<const uint64_t *>(wp[0]), ptr<int64_t>(lens),
+                    ptr<int64_t>(offs), m, W, ptr<uint8_t>(bytes), ex.stream);
+  return Column(name, type, m, bytes.slice(0, 0, nbytes), offs, lc.validity);
+}
+
 // wc = the word columns 0..W-1 (inv: wc[0] = the invertible word key, wc[1..] = words 1..W-1)
 static Column words_to_var(const Exec &ex, const std::string &name, const DataType &type,
                            const std::vector<Column> &wc, int64_t L, bool inv = false) {
@@ -1439,10 +1517,13 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
   // pos[c] = proxy column of the side's column c (-1: rebuilt from the key or gathered);
   // wlen[c] = L of a column carried as words (from proxy column pos[c]), else -1
   static const std::string kRow = "__cylon_row", kKey = "__cylon_key";
+  // vwid[c] = W of a variable-length key carried as W padded words + its length column
   auto proxy = [&](const TablePtr &t, bool &var, const std::vector<int> &keys, const at::Tensor &img,
-                   std::vector<int> &pos, std::vector<int64_t> &wlen, const std::vector<at::Tensor> &kwords) {
+                   std::vector<int> &pos, std::vector<int64_t> &wlen, std::vector<int> &vwid,
+                   const std::vector<at::Tensor> &kwords, const at::Tensor &klens) {
     pos.assign(t->Columns(), -1);
     wlen.assign(t->Columns(), -1);
+    vwid.assign(t->Columns(), 0);
     std::vector<Column> cols;
     if (ckey) cols.emplace_back(kKey, DataType(Type::INT64), t->Rows(), img);
     var = false;
@@ -1450,6 +1531,16 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
       const Column &col = t->column(c);
       if (ckey && std::find(keys.begin(), keys.end(), c) != keys.end()) continue;
       if (var_col(col)) {
+        if (k.vw > 0 && c == keys[0]) {  // padded word key, words 1..W-1, length (radix_keys)
+          vwid[c] = k.vw;
+          pos[c] = (int)cols.size();
+          cols.emplace_back("__cylon_wk" + std::to_string(c), DataType(Type::INT64), t->Rows(), img);
+          for (size_t j = 0; j < kwords.size(); ++j)
+            cols.emplace_back("__cylon_w" + std::to_string(c) + "_" + std::to_string(j + 1), DataType(Type::INT64),
+                              t->Rows(), kwords[j]);
+          cols.emplace_back("__cylon_wl" + std::to_string(c), DataType(Type::INT64), t->Rows(), klens);
+          continue;
+        }
         const bool kw = k.wlen > 0 && c == keys[0];  // the key's word key + words from radix_keys
         const int64_t L = kw ? k.wlen : fixed_var_len(ex, col);
         if (L < 0) {
@@ -1472,20 +1563,22 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
     if (var) cols.emplace_back(kRow, DataType(Type::INT64), t->Rows(), at::arange(t->Rows(), ex.opts(at::kLong)));
     return Table::Make(t->GetContext(), std::move(cols));
   };
-  std::vector<int> lpos, rpos;
+  std::vector<int> lpos, rpos, lvw, rvw;
   std::vector<int64_t> lwlen, rwlen;
   const bool lpx = lvar || ckey, rpx = rvar || ckey;
   bool lgather = false, rgather = false;  // var-width columns gathered by row number after the join
-  TablePtr lp = lpx ? proxy(left, lgather, lc, k.l, lpos, lwlen, k.lwords) : left;
-  TablePtr rp = rpx ? proxy(right, rgather, rc, k.r, rpos, rwlen, k.rwords) : right;
+  TablePtr lp = lpx ? proxy(left, lgather, lc, k.l, lpos, lwlen, lvw, k.lwords, k.llen) : left;
+  TablePtr rp = rpx ? proxy(right, rgather, rc, k.r, rpos, rwlen, rvw, k.rwords, k.rlen) : right;
   if (lpx || rpx) {
     int64_t nw = 0;
     for (int64_t L : lwlen) nw += L > 0;
     for (int64_t L : rwlen) nw += L > 0;
+    for (int W : lvw) nw += W > 0;
+    for (int W : rvw) nw += W > 0;
     if (nw) trace::add_counter("join.radix.word_columns", nw);
   }
   if (!radix_eligible(lp) || !radix_eligible(rp)) return nullptr;
-  const int mchunks = sink ? 1 : radix_join_chunks(ex, lp, rp, k.l, k.r);
+  const int mchunks = sink ? 1 : radix_join_chunks(ex, lp, rp, k.l, k.r, cfg.GetType());
   TablePtr out = mchunks > 1 ? radix_join_chunked(ex, lp, rp, k.l, k.r, cfg, mchunks, k.verify)
                              : radix_join(ex, lp, rp, k.l, k.r, cfg, sink, k.verify);
   if (!out) return nullptr;
@@ -1495,13 +1588,14 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
   // Inner join on one fixed-length string key per side (same type and length, no nulls): the key
   // words are verified equal row by row below, so the right output key column is the left one's
   // bytes and offsets (one words -> bytes conversion; CYLON_RJ_SHARE_KEY=0 converts both).
-  const bool share_skey = jt == JoinType::INNER && k.verify && lc.size() == 1 && lpx && rpx && lwlen[lc[0]] > 0 &&
-                          lwlen[lc[0]] == rwlen[rc[0]] && left->column(lc[0]).type == right->column(rc[0]).type &&
+  const bool share_skey = jt == JoinType::INNER && k.verify && lc.size() == 1 && lpx && rpx &&
+                          ((lwlen[lc[0]] > 0 && lwlen[lc[0]] == rwlen[rc[0]]) || (lvw[lc[0]] > 0 && lvw[lc[0]] == rvw[rc[0]])) &&
+                          left->column(lc[0]).type == right->column(rc[0]).type &&
                           !left->column(lc[0]).nullable() && !right->column(rc[0]).nullable() &&
                           knobs::Flag("RJ_SHARE_KEY", true);
   auto side = [&](const TablePtr &orig, bool px, bool var, const std::vector<int> &pos, const std::vector<int64_t> &wlen,
-                  const std::vector<int> &keys, int first, int np, bool may_null, const std::string &prefix,
-                  int skip_col) {
+                  const std::vector<int> &vwid, const std::vector<int> &keys, int first, int np, bool may_null,
+                  const std::string &prefix, int skip_col) {
     std::vector<Column> cols(orig->Columns());
     if (!px) {
       for (int c = 0; c < orig->Columns(); ++c) cols[c] = out->column(first + c);
@@ -1509,6 +1603,12 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
     }
     for (int c = 0; c < orig->Columns(); ++c) {
       if (pos[c] < 0 || c == skip_col) continue;
+      if (vwid[c] > 0) {  // a variable-length string from its padded words + length
+        std::vector<Column> wc;
+        for (int j = 0; j <= vwid[c]; ++j) wc.push_back(out->column(first + pos[c] + j));
+        cols[c] = padded_to_var(ex, prefix + orig->column(c).name, orig->column(c).type, wc, vwid[c]);
+        continue;
+      }
       if (wlen[c] > 0) {  // a fixed-length string from its word columns
         const int64_t L = wlen[c];
         std::vector<Column> wc;
@@ -1556,9 +1656,9 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
     for (size_t j = 0; j < vpos.size(); ++j) cols[vpos[j]] = g->column((int)j).with_name(prefix + g->column((int)j).name);
     return cols;
   };
-  std::vector<Column> all = side(left, lpx, lgather, lpos, lwlen, lc, 0, lp->Columns(), left_may_null(jt),
+  std::vector<Column> all = side(left, lpx, lgather, lpos, lwlen, lvw, lc, 0, lp->Columns(), left_may_null(jt),
                                 cfg.GetLeftTablePrefix(), -1);
-  std::vector<Column> rcols = side(right, rpx, rgather, rpos, rwlen, rc, lp->Columns(), rp->Columns(),
+  std::vector<Column> rcols = side(right, rpx, rgather, rpos, rwlen, rvw, rc, lp->Columns(), rp->Columns(),
                                    right_may_null(jt), cfg.GetRightTablePrefix(), share_skey ? rc[0] : -1);
   if (share_skey) {
     rcols[rc[0]] = all[lc[0]].with_name(cfg.GetRightTablePrefix() + right->column(rc[0]).name);
@@ -1570,18 +1670,22 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
   if (!k.verify) return res;
   // keys that are all fixed-length strings: compare their word columns (8 bytes per compare)
   bool words = lpx && rpx;
-  for (size_t i = 0; words && i < lc.size(); ++i) words = lwlen[lc[i]] > 0 && lwlen[lc[i]] == rwlen[rc[i]];
+  for (size_t i = 0; words && i < lc.size(); ++i)
+    words = (lwlen[lc[i]] > 0 && lwlen[lc[i]] == rwlen[rc[i]]) || (lvw[lc[i]] > 0 && lvw[lc[i]] == rvw[rc[i]]);
   if (!words) return drop_false_matches(res, cfg, left->Columns());
   const int64_t m = out->Rows();
   if (m == 0) return res;
   std::vector<const int64_t *> aw, bw;
   const int rfirst = lp->Columns();
-  // (a word-key column: the key words 1..W-1 -- equal word keys were matched, so word 0 is equal too)
-  for (size_t i = 0; i < lc.size(); ++i)
-    for (int64_t j = k.wlen > 0 ? 1 : 0; j < (lwlen[lc[i]] + 7) / 8; ++j) {
+  // (a word-key column: the key words 1..W-1 -- equal word keys were matched, so word 0 is equal too;
+  // a padded word key: words 1..W-1 and the length, which seeds the key's chain)
+  for (size_t i = 0; i < lc.size(); ++i) {
+    const int64_t nwc = lvw[lc[i]] > 0 ? lvw[lc[i]] + 1 : (lwlen[lc[i]] + 7) / 8;
+    for (int64_t j = (k.wlen > 0 || k.vw > 0) ? 1 : 0; j < nwc; ++j) {
       aw.push_back(ptr<int64_t>(out->column(lpos[lc[i]] + (int)j).data));
       bw.push_back(ptr<int64_t>(out->column(rfirst + rpos[rc[i]] + (int)j).data));
     }
+  }
   if (aw.empty()) return res;  // an L <= 8 word key is the string itself: no false matches
   if (aw.size() > 8) return drop_false_matches(res, cfg, left->Columns());
   const Column &lw = out->column(lpos[lc[0]]), &rw = out->column(rfirst + rpos[rc[0]]);

@@ -133,13 +133,21 @@ class Table(PandasOpsMixin):
         return Table(context=ctx, _native=C.import_device_table(ctx._ctx, caps[0], caps[1]))
 
     def to_torch(self) -> Dict[str, torch.Tensor]:
-        """Columns as device tensors (zero-copy, fixed width columns only).  Columns may share a
-        buffer (an inner join's two key columns, docs/semantics.md): clone before in-place writes."""
-        out = {}
+        """Columns as device tensors (zero-copy, fixed width columns only).  Columns of one table
+        may share a buffer natively (an inner join's two key columns hold the same values,
+        docs/semantics.md); the second and later names of a shared buffer come back as copies, so an
+        in-place write through one returned tensor never changes another."""
+        out, seen = {}, set()
         for c in self._t.columns():
             if c.offsets is not None:
                 raise TypeError(f"column {c.name} is variable width")
-            out[c.name] = c.data
+            d = c.data
+            key = (d.device, d.untyped_storage().data_ptr()) if d.numel() else None
+            if key is not None and key in seen:
+                d = d.clone()
+            elif key is not None:
+                seen.add(key)
+            out[c.name] = d
         return out
 
     def to_csv(self, path, csv_write_options=None):

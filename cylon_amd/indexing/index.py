@@ -78,6 +78,42 @@ class BaseIndex:
     def values(self) -> np.ndarray:
         return self.get_index_array().to_numpy(zero_copy_only=False)
 
+    def isin(self, values, skip_null: bool = True, zero_copy_only: bool = False) -> np.ndarray:
+        """Per label: is it one of `values` (reference index.pyx:81, Arrow is_in semantics: a null
+        label matches a null value only when skip_null is False).  Numeric labels are tested on the
+        index's device (torch.isin against the exactly representable values); others via Arrow."""
+        if not isinstance(values, (list, np.ndarray)):
+            raise ValueError("values must be List or np.ndarray")
+        vals = values.tolist() if isinstance(values, np.ndarray) else list(values)
+        labels = getattr(self, "_values", None)
+        if labels is None and getattr(self, "_arrow", None) is None:  # (a RangeIndex: its labels)
+            labels = torch.from_numpy(self.get_index_array().to_numpy(zero_copy_only=False).copy())
+        if labels is not None:
+            dt = labels.dtype
+            keep = []
+            for v in vals:
+                if v is None or isinstance(v, (str, bytes)):
+                    continue
+                try:
+                    c = torch.tensor([v], dtype=dt)
+                except (TypeError, RuntimeError, OverflowError):
+                    continue
+                if c.item() == v or (v != v and c.item() != c.item()):  # exactly representable (NaN too)
+                    keep.append(c)
+            vs = torch.cat(keep).to(labels.device) if keep else torch.empty(0, dtype=dt, device=labels.device)
+            res = torch.isin(labels, vs)
+            if dt.is_floating_point and any(v != v for v in vals if isinstance(v, float)):
+                res |= torch.isnan(labels)
+            return res.cpu().numpy()
+        import pyarrow.compute as pc
+        arr = self._arrow
+        try:
+            vset = pa.array(vals, type=arr.type)
+        except (pa.ArrowInvalid, pa.ArrowTypeError, TypeError, OverflowError):
+            vset = pa.array([v for v in vals if v is None or isinstance(v, (str, bytes)) == pa.types.is_string(arr.type)])
+        out = pc.is_in(arr, options=pc.SetLookupOptions(value_set=vset, skip_nulls=skip_null))
+        return out.to_numpy(zero_copy_only=zero_copy_only)
+
     def to(self, device: str) -> "BaseIndex":
         return type(self)(self._values if self._values is not None else self._arrow, device)
 

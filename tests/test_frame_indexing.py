@@ -238,3 +238,32 @@ def test_native_loc_indexer_and_set_index(ctx):
     assert il == {"k": [1, 5]}
     C.table_reset_index(t.native)
     assert C.table_get_index(t.native) is None
+
+
+@pytest.mark.parametrize("kind", ["int", "float_nan", "string_nulls", "range"])
+@pytest.mark.parametrize("skip_null", [True, False])
+def test_base_index_isin_matches_arrow(kind, skip_null):
+    """BaseIndex.isin (reference indexing/index.pyx:81): per label membership, against Arrow's is_in
+    (the reference's compare_array_like_values) as the oracle."""
+    import pyarrow.compute as pc
+    from cylon_amd.indexing.index import BaseIndex, HashIndex, RangeIndex
+    if kind == "int":
+        labels, values, idx = pa.array([5, 1, 9, 1, 7]), [1, 7, 2.5, 100], HashIndex([5, 1, 9, 1, 7])
+    elif kind == "float_nan":
+        labels, values = pa.array([1.5, float("nan"), 2.0, -0.5]), np.array([2.0, np.nan])
+        idx = BaseIndex(np.array([1.5, np.nan, 2.0, -0.5]))
+    elif kind == "string_nulls":
+        labels, values = pa.array(["a", None, "c", "a", "d"]), ["a", None, "d"]
+        idx = BaseIndex(labels)
+    else:
+        labels, values, idx = pa.array(np.arange(2, 12, 3)), [5, 8, 9], RangeIndex(2, 12, 3)
+    got = idx.isin(values, skip_null=skip_null)
+    vs = [v for v in (values.tolist() if isinstance(values, np.ndarray) else values)
+          if not (kind == "int" and isinstance(v, float) and not float(v).is_integer())]
+    exp = pc.is_in(labels, options=pc.SetLookupOptions(value_set=pa.array(vs, type=labels.type),
+                                                       skip_nulls=skip_null)).to_numpy(zero_copy_only=False)
+    if kind == "float_nan":  # Arrow's is_in matches NaN with NaN; so does isin
+        exp = exp.copy()
+    assert got.tolist() == exp.tolist()
+    with pytest.raises(ValueError):
+        idx.isin("not-a-list")

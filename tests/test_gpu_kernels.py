@@ -267,6 +267,15 @@ def test_partition_lookback_passes_match_exact(gpu_ctx, monkeypatch, op):
             assert c.get("partition.radix.lookback_timeout_fallback", 0) == 0, c
         res.append(df.reset_index(drop=True))
     pd.testing.assert_frame_equal(res[0], res[1])
+    # the CPU twin as an independent third oracle (a shared GPU encoding bug would pass the A/B)
+    tc, t2c = t.to_cpu(), t2.to_cpu()
+    if op == "groupby":
+        cpu = tc.local_groupby("k", {"x": ["sum", "count"]}).to_pandas().sort_values("k")
+    elif op == "unique":
+        cpu = tc.unique().to_pandas().sort_values(["k", "x"])
+    else:
+        cpu = tc.union(t2c).to_pandas().sort_values(["k", "x"])
+    pd.testing.assert_frame_equal(res[0], cpu.reset_index(drop=True), check_dtype=False)
 
 
 def _sorted_df(t):
@@ -275,7 +284,7 @@ def _sorted_df(t):
 
 
 @pytest.mark.parametrize("case", ["int64", "int32_nullable", "dups", "skew_fallback", "left_smaller"])
-def test_radix_join_matches_global_table_join(gpu_ctx, monkeypatch, case):
+def test_radix_join_matches_global_table_join(gpu_ctx, ctx, monkeypatch, case):
     """K5 LDS radix join (partitioned, fused materialisation) vs the global-table join."""
     rng = np.random.default_rng(11)
     nl, nr = 300_000, 200_000
@@ -300,11 +309,13 @@ def test_radix_join_matches_global_table_join(gpu_ctx, monkeypatch, case):
     ref = L.join(R, "inner", "hash", **on)
     assert got.column_names == ref.column_names
     pd.testing.assert_frame_equal(_sorted_df(got), _sorted_df(ref))
+    cpu = Table(a, ctx).join(Table(b, ctx), "inner", "hash", **on)  # CPU twin: third oracle
+    pd.testing.assert_frame_equal(_sorted_df(got), _sorted_df(cpu), check_dtype=False)
 
 
 @pytest.mark.parametrize("case", ["int64_many_groups", "int32_nullable", "few_groups", "min_key", "wide_aggs",
                                   "null_keys", "null_keys_int16"])
-def test_radix_groupby_matches_global(gpu_ctx, monkeypatch, case):
+def test_radix_groupby_matches_global(gpu_ctx, ctx, monkeypatch, case):
     """K8 LDS radix group-by (HLL sizing, partitioned LDS aggregation) vs the global-table path."""
     rng = np.random.default_rng(5)
     n = 400_000
@@ -335,6 +346,9 @@ def test_radix_groupby_matches_global(gpu_ctx, monkeypatch, case):
             assert c.get("groupby.radix.groups", 0) > 0, c  # the radix path took the nullable key
         res.append(df.sort_values("k").reset_index(drop=True))
     pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-9, atol=1e-9)
+    cpu = Table(t, ctx).local_groupby("k", aggs).to_pandas()  # CPU twin: third oracle
+    pd.testing.assert_frame_equal(res[0], cpu.sort_values("k").reset_index(drop=True), check_exact=False,
+                                  rtol=1e-9, atol=1e-9, check_dtype=False)
 
 
 @pytest.mark.parametrize("dtype", ["int64", "float64", "int32", "uint16", "float32", "uint64", "int64_full",

@@ -8,6 +8,7 @@ import numpy as np
 import pandas as pd
 import pyarrow as pa
 import pytest
+import torch
 
 from cylon_amd import Table
 from cylon_amd._lib import C
@@ -230,6 +231,27 @@ def test_radix_inner_join_shared_key_column(gpu_ctx, ctx, monkeypatch, left_smal
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
 
 
+def test_shared_key_column_to_torch_is_copy_on_second_name(gpu_ctx, monkeypatch):
+    """The inner join's two key columns share one device buffer natively; to_torch() hands the
+    second name a copy, so an in-place write through one tensor leaves the other (and the table)
+    unchanged."""
+    monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", "1024")
+    monkeypatch.setenv("CYLON_RJ_SHARE_KEY", "1")
+    rng = np.random.default_rng(43)
+    a = pa.table({"k": rng.integers(0, 200_000, 300_000), "v": rng.random(300_000)})
+    b = pa.table({"k": rng.integers(0, 200_000, 300_000), "w": rng.random(300_000)})
+    out = Table(a, gpu_ctx).join(Table(b, gpu_ctx), "inner", "hash", on=["k"], left_prefix="l_", right_prefix="r_")
+    cols = {c.name: c for c in out.native.columns()}
+    assert cols["l_k"].data.data_ptr() == cols["r_k"].data.data_ptr()  # shared natively
+    t = out.to_torch()
+    assert t["l_k"].data_ptr() != t["r_k"].data_ptr()
+    before = t["r_k"].clone()
+    t["l_k"].add_(1)
+    assert torch.equal(t["r_k"], before)
+    t["l_k"].sub_(1)  # (l_k is the table's own buffer: restore it)
+    assert torch.equal(t["l_k"], t["r_k"])
+
+
 # ---- LDS radix group-by (kernels/radix_groupby.hip) beyond one integer key + SUM/COUNT/MIN/MAX/MEAN
 def _groupby_both(T, keys, aggs, monkeypatch):
     """[radix path, GPU global-table path] results and counters; both are also checked against the
@@ -306,6 +328,52 @@ def test_radix_groupby_string_word_key(gpu_ctx, monkeypatch, fmt):
     assert cnt[0].get("groupby.radix.word_key", 0) == 1, cnt[0]
     assert cnt[0].get("groupby.radix.groups", 0) == len(res[0]) == len(np.unique(ids)), cnt[0]
     pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-8, atol=1e-8)
+
+
+@pytest.mark.parametrize("case", ["var_8_32", "var_1_100_binary", "fixed_40_too_wide"])
+def test_radix_groupby_hashed_string_key(gpu_ctx, monkeypatch, case):
+    """Variable-length string / binary keys (and fixed-length keys whose MIN / MAX words would not fit
+    the 8 accumulator planes) group on the LDS radix path by a 64-bit hash of the bytes, verified by
+    MIN == MAX of an independent 64-bit hash per group; the output key is each group's first row's
+    bytes.  Against the global path and the CPU twin."""
+    rng = np.random.default_rng(15)
+    n = 600_000
+    ids = rng.integers(0, 40_000, n)
+    if case == "fixed_40_too_wide":
+        vals = [f"key-{x:036d}" for x in ids]
+    else:
+        lo, hi = (8, 32) if case == "var_8_32" else (1, 100)
+        vals = _var_strings(rng, ids, lo, hi, binary=case.endswith("binary"))
+    t = pa.table({"s": pa.array(vals), "x": rng.standard_normal(n), "k": rng.integers(-50, 50, n)})
+    res, cnt = _groupby_both(Table(t, gpu_ctx), ["s"], {"x": ["sum", "mean"], "k": ["max"]}, monkeypatch)
+    assert cnt[0].get("groupby.radix.hashed_string_key", 0) == 1, cnt[0]
+    assert cnt[0].get("groupby.radix.word_key_too_wide", 0) == (1 if case == "fixed_40_too_wide" else 0), cnt[0]
+    assert cnt[0].get("groupby.radix.groups", 0) == len(res[0]) == len(np.unique(ids)), cnt[0]
+    pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-8, atol=1e-8)
+
+
+@pytest.mark.parametrize("case", ["median_alone", "sum_q25_nullable", "int_values_two_q", "two_keys_q90"])
+def test_radix_groupby_quantile(gpu_ctx, monkeypatch, case):
+    """QUANTILE on the LDS radix path: (group key, value) rows partitioned by the key hash and sorted
+    per partition in LDS, each group's quantile by the global path's type-2 rule (nulls excluded; a
+    group whose values are all null gets a null quantile), LEFT-joined to the other aggregates.
+    Against the global path and the CPU twin."""
+    rng = np.random.default_rng(17)
+    n = 700_000
+    k = rng.integers(0, 30_000, n)
+    xmask = (rng.random(n) < 0.05) | (k % 1009 == 0)  # nulls, and groups whose x is all null
+    t = pa.table({"k": k, "g": rng.integers(-3, 3, n).astype(np.int16),
+                  "x": pa.array(np.round(rng.standard_normal(n) * 100.0, 1), mask=xmask if case == "sum_q25_nullable" else None),
+                  "i": rng.integers(-1000, 1000, n).astype(np.int32)})
+    keys, aggs = {"median_alone": (["k"], {"x": ["median"]}),
+                  "sum_q25_nullable": (["k"], {"x": ["sum", ("quantile", 0.25)]}),
+                  "int_values_two_q": (["k"], {"i": [("quantile", 0.5), ("quantile", 0.9)], "x": ["max"]}),
+                  "two_keys_q90": (["k", "g"], {"x": [("quantile", 0.9), "mean"]})}[case]
+    res, cnt = _groupby_both(Table(t, gpu_ctx), keys, aggs, monkeypatch)
+    nq = 2 if case == "int_values_two_q" else 1
+    assert cnt[0].get("groupby.radix.quantile", 0) == nq, cnt[0]
+    assert cnt[0].get("groupby.radix.quantile_overflow_fallback", 0) == 0, cnt[0]
+    pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-12, atol=1e-12)
 
 
 @pytest.mark.parametrize("case", ["with_sum", "alone", "two_keys"])
@@ -504,4 +572,63 @@ def test_radix_join_memory_bounded_chunks_string_key(gpu_ctx, ctx, monkeypatch, 
     assert c.get("join.radix.memory_chunks", 0) >= 2, c
     assert c.get("join.radix.narrow_fallback", 0) == 0, c
     assert len(got) == len(exp)
+    pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
+
+
+def _var_strings(rng, ids, lo, hi, binary=False):
+    """Keys of random length in [lo, hi] that are a function of the id (equal ids <=> equal keys):
+    the id's digits, then filler bytes up to a length drawn from the id."""
+    out = []
+    for x in ids:
+        ln = lo + (int(x) * 2654435761 % (hi - lo + 1))
+        s = (f"{x:d}#" + "abcdefghijklmnopqrstuvwxyz0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZ" * 2)[:max(ln, 0)]
+        if ln < len(f"{x:d}#"):  # too short for the id: a prefix would alias ids -- keep the id whole
+            s = f"{x:d}"
+        out.append(s.encode() if binary else s)
+    return out
+
+
+@pytest.mark.parametrize("how", ["inner", "left", "outer"])
+@pytest.mark.parametrize("kind", ["string_8_32", "binary_1_40", "string_0_64"])
+def test_radix_join_variable_length_keys(gpu_ctx, ctx, monkeypatch, how, kind):
+    """Variable-length string / binary keys (rows <= 64 bytes) travel as zero-padded words + a length
+    column under the padded word key (no row-number gather of the key bytes): empty strings, one-word
+    keys, unaligned tails, 5-8 words.  Output key bytes must round-trip exactly; against the CPU twin."""
+    rng = np.random.default_rng(71)
+    n = 1_000_000
+    lo, hi = {"string_8_32": (8, 32), "binary_1_40": (1, 40), "string_0_64": (0, 64)}[kind]
+    ids_a, ids_b = rng.integers(0, 700_000, n), rng.integers(0, 700_000, n)
+    bin_ = kind.startswith("binary")
+    a = pa.table({"s": pa.array(_var_strings(rng, ids_a, lo, hi, bin_)), "v": rng.random(n)})
+    b = pa.table({"s": pa.array(_var_strings(rng, ids_b, lo, hi, bin_)), "w": rng.random(n)})
+    if kind == "string_0_64":  # a few empty keys on both sides (they match each other)
+        a = a.set_column(0, "s", pa.array([("" if i % 9973 == 0 else s) for i, s in enumerate(a["s"].to_pylist())]))
+        b = b.set_column(0, "s", pa.array([("" if i % 7919 == 0 else s) for i, s in enumerate(b["s"].to_pylist())]))
+    got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["s"], monkeypatch)
+    assert c.get("join.radix.var_word_key", 0) == 1 and c.get("join.radix.var_gather", 0) == 0, c
+    assert c.get("join.radix.hash_collision_fallback", 0) == 0, c
+    assert c.get("join.radix.shared_key_column", 0) == (2 if how == "inner" else 0), c
+    assert c["join.radix.rows_out"] == len(exp)
+    pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
+
+
+@pytest.mark.parametrize("how", ["inner", "outer"])
+@pytest.mark.parametrize("case", ["no_words_knob", "longer_than_64"])
+def test_radix_join_variable_length_keys_gather_path(gpu_ctx, ctx, monkeypatch, how, case):
+    """The hashed-key path of variable-length keys: the 64-bit row hash is partitioned and matched,
+    the key bytes are gathered by row number after the join (var_gather) and every output row's keys
+    are compared byte-wise (rows_equal).  Taken for keys longer than 64 bytes, or with
+    CYLON_RJ_VAR_WORDS=0.  Against the CPU twin."""
+    rng = np.random.default_rng(73)
+    n = 600_000
+    ids_a, ids_b = rng.integers(0, 400_000, n), rng.integers(0, 400_000, n)
+    lo, hi = (4, 30) if case == "no_words_knob" else (50, 90)
+    if case == "no_words_knob":
+        monkeypatch.setenv("CYLON_RJ_VAR_WORDS", "0")
+    a = pa.table({"s": pa.array(_var_strings(rng, ids_a, lo, hi)), "v": rng.random(n)})
+    b = pa.table({"s": pa.array(_var_strings(rng, ids_b, lo, hi)), "w": rng.random(n)})
+    got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["s"], monkeypatch)
+    assert c.get("join.radix.var_word_key", 0) == 0 and c.get("join.radix.var_gather", 0) == 1, c
+    assert c.get("join.radix.hashed_key", 0) == 1 and c.get("join.radix.hash_collision_fallback", 0) == 0, c
+    assert c["join.radix.rows_out"] == len(exp)
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)

@@ -19,13 +19,16 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 from cylon_amd import CylonContext, Table  # noqa: E402
 from cylon_amd._lib import C  # noqa: E402
-from string_join_probe import string_column  # noqa: E402
+from string_join_probe import string_column, var_string_column, var_string_ints  # noqa: E402
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 200_000_000
-    groups = int(sys.argv[2]) if len(sys.argv) > 2 else 10_000_000
-    reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    args = [a for a in sys.argv[1:] if not a.startswith("--var")]
+    var = next((a for a in sys.argv[1:] if a.startswith("--var")), None)  # --var=8,32
+    vlo, vhi = (int(x) for x in var.split("=")[1].split(",")) if var else (0, 0)
+    n = int(args[0]) if len(args) > 0 else 200_000_000
+    groups = int(args[1]) if len(args) > 1 else 10_000_000
+    reps = int(args[2]) if len(args) > 2 else 3
     ctx = CylonContext(device="cuda:0")
     res, sums = {}, {}
     for kind in ("int64", "string"):
@@ -35,7 +38,8 @@ def main():
         v = torch.rand(n, generator=g, device="cuda", dtype=torch.float64)
         t = Table.from_torch(ctx, {"k": k, "v": v})
         if kind == "string":
-            t = Table(context=ctx, _native=C.Table(ctx._ctx, [string_column("k", k)] + [t.native.columns()[1]]))
+            kc = var_string_column("k", k, vlo, vhi) if var else string_column("k", k)
+            t = Table(context=ctx, _native=C.Table(ctx._ctx, [kc] + [t.native.columns()[1]]))
 
         def run():
             return t.local_groupby(["k"], {"v": ["sum", "max"]})
@@ -58,7 +62,9 @@ def main():
         cnt = {a: b for a, b in dict(C.trace_counters()).items() if a.startswith("groupby.")}
         C.trace_enable(False)
         cols = out.native.columns()
-        if kind == "string":  # key bytes -> the int key (15 digits after 'k')
+        if kind == "string" and var:
+            key = var_string_ints(cols[0])
+        elif kind == "string":  # key bytes -> the int key (15 digits after 'k')
             b = cols[0].data.reshape(-1, 16)[:, 1:].to(torch.int64) - 48
             key = torch.zeros(b.shape[0], dtype=torch.int64, device=b.device)
             for d in range(15):
@@ -67,7 +73,7 @@ def main():
             key = cols[0].data
         order = torch.argsort(key)
         sums[kind] = (key[order], cols[1].data[order])
-        rec = {"key": kind, "rows": n, "ms": round(statistics.median(ts), 3), "all_ms": [round(x, 2) for x in ts],
+        rec = {"key": kind + (f" var[{vlo},{vhi}]" if var and kind == "string" else ""), "rows": n, "ms": round(statistics.median(ts), 3), "all_ms": [round(x, 2) for x in ts],
                "groups": ng, "counters": cnt}
         if kind == "string":
             rec["keys_equal_int64_run"] = bool(torch.equal(sums["int64"][0], sums["string"][0]))

@@ -34,9 +34,43 @@ def string_column(name, ints):
     return C.Column(name, DataType(Type.STRING), n, b, offs)
 
 
+def var_string_column(name, ints, lo=8, hi=32):
+    """Variable-length ASCII keys of lo..hi bytes (device): 'k' + 5 base-64 digits of ints (< 2^30)
+    + filler bytes, the length a function of the int (so equal ints <=> equal keys)."""
+    n = ints.numel()
+    ln = lo + (ints * 2654435761) % (hi - lo + 1)
+    buf = torch.empty((n, hi), dtype=torch.uint8, device=ints.device)
+    buf[:, 0] = ord("k")
+    x = ints.clone()
+    for d in range(5):
+        buf[:, 1 + d] = (x % 64 + 48).to(torch.uint8)
+        x //= 64
+    for j in range(6, hi):
+        buf[:, j] = ((buf[:, 1 + j % 5].to(torch.int64) + j) % 64 + 48).to(torch.uint8)
+    pos = torch.arange(hi, device=ints.device)[None, :]
+    step = 1 << 24  # (one boolean-mask select over all rows overflows inside torch)
+    b = torch.cat([buf[i:i + step].masked_select(pos < ln[i:i + step, None]) for i in range(0, n, step)])
+    del buf
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=ints.device)
+    offs[1:] = torch.cumsum(ln, 0)
+    return C.Column(name, DataType(Type.STRING), n, b, offs)
+
+
+def var_string_ints(col):
+    """The ints of var_string_column keys (digits 1..5 of each row)."""
+    o = col.offsets[:-1]
+    key = torch.zeros(o.numel(), dtype=torch.int64, device=o.device)
+    for d in range(4, -1, -1):
+        key = key * 64 + (col.data[o + 1 + d].to(torch.int64) - 48)
+    return key
+
+
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 200_000_000
-    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    args = [a for a in sys.argv[1:] if not a.startswith("--var")]
+    var = next((a for a in sys.argv[1:] if a.startswith("--var")), None)  # --var=8,32
+    vlo, vhi = (int(x) for x in var.split("=")[1].split(",")) if var else (0, 0)
+    n = int(args[0]) if len(args) > 0 else 200_000_000
+    reps = int(args[1]) if len(args) > 1 else 3
     ctx = CylonContext(device="cuda:0")
     kr = int(0.99 * n)
     res = {}
@@ -49,7 +83,8 @@ def main():
             vals = {f"v{i}": torch.rand(n, generator=g, device="cuda", dtype=torch.float64) for i in range(3)}
             t = Table.from_torch(ctx, {"k": k, **vals})
             if kind == "string":
-                cols = [string_column("k", k)] + [c for c in t.native.columns()[1:]]
+                kc = var_string_column("k", k, vlo, vhi) if var else string_column("k", k)
+                cols = [kc] + [c for c in t.native.columns()[1:]]
                 t = Table(context=ctx, _native=C.Table(ctx._ctx, cols))
             del k
             sides.append(t)
@@ -75,7 +110,7 @@ def main():
         torch.cuda.synchronize()
         cnt = {k: v for k, v in dict(C.trace_counters()).items() if k.startswith("join.")}
         C.trace_enable(False)
-        rec = {"key": kind, "rows_per_side": n, "ms": round(statistics.median(ts), 3),
+        rec = {"key": kind + (f" var[{vlo},{vhi}]" if var and kind == "string" else ""), "rows_per_side": n, "ms": round(statistics.median(ts), 3),
                "all_ms": [round(x, 2) for x in ts], "out_rows": rows, "counters": cnt}
         if kind == "string":  # the key bytes of both sides are equal row by row (also checked by the join)
             lk, rk = out.native.columns()[0], out.native.columns()[4]
