@@ -155,8 +155,13 @@ def verify_join(ctx, left, right, out, key_range, how="inner") -> dict:
       sum l_k     = sum over left rows i of k_i * (cR(k_i) [+ [cR(k_i) = 0]])  (l_k == r_k where both exist)
       sum l_v0    = sum over left rows i of v_i * (cR(k_i) [+ [cR(k_i) = 0]])
       sum r_v0    = sum over right rows j of w_j * (cL(k_j) [+ [cL(k_j) = 0]])"""
+    return verify_join_against(ctx, out, join_expectation(ctx, left, right, key_range, how), how)
+
+
+def join_expectation(ctx, left, right, key_range, how="inner"):
+    """The verify_join identities' expected values, from the inputs alone (so a caller can take them
+    before a retain = false join releases its inputs)."""
     lt, rt = left.to_torch(), right.to_torch()
-    ocols = {c.name: c for c in out.native.columns()}
     dev = lt["k"].device
     f64 = torch.float64
     cL = torch.bincount(lt["k"], minlength=key_range)
@@ -179,7 +184,13 @@ def verify_join(ctx, left, right, out, key_range, how="inner") -> dict:
     del ml, mr, cL, cR
     if ctx.get_world_size() > 1:
         part = ctx.allreduce(part, "sum")
-    expect = torch.cat([torch.stack([inner + un_l + un_r, un_r, un_l]), part])
+    return torch.cat([torch.stack([inner + un_l + un_r, un_r, un_l]), part])
+
+
+def verify_join_against(ctx, out, expect, how="inner") -> dict:
+    ocols = {c.name: c for c in out.native.columns()}
+    dev = expect.device
+    f64 = torch.float64
 
     def col(name):
         c = ocols[name]

@@ -182,6 +182,17 @@ int64_t Table::nbytes() const {
   return b;
 }
 
+void Table::ReleaseIfNotRetained() {
+  if (retain_) return;
+  for (auto &c : columns_) {
+    c.data = at::empty({0}, c.data.options());
+    if (c.validity.defined()) c.validity = at::empty({0}, c.validity.options());
+    if (c.offsets.defined()) c.offsets = at::zeros({1}, c.offsets.options());
+    c.length = 0;
+  }
+  rows_ = 0;
+}
+
 TablePtr Table::to(at::Device dev) const {
   std::vector<Column> cols;
   cols.reserve(columns_.size());

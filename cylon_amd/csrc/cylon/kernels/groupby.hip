@@ -396,11 +396,11 @@ __global__ void k_quantile(const ColView v, const int64_t *__restrict__ perm, co
     }
     const double np = (double)cnt * q;
     const double j = floor(np);
-    const double gg = np - j;
+    const bool whole = np == j;  // (a comparison: `np - j == 0` may be contracted into fma(cnt, q, -j))
     int64_t pos = (int64_t)j;
     if (pos >= cnt) pos = cnt - 1;
     double r;
-    if (gg == 0.0 && pos > 0) r = 0.5 * (as_double(v, perm[b + pos - 1]) + as_double(v, perm[b + pos]));
+    if (whole && pos > 0) r = 0.5 * (as_double(v, perm[b + pos - 1]) + as_double(v, perm[b + pos]));
     else r = as_double(v, perm[b + pos]);
     out[g] = r;
     valid[g] = 1;

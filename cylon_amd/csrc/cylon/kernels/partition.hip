@@ -430,24 +430,35 @@ __global__ void k_words_mismatch(ConstWordPtrs a, ConstWordPtrs b, int W, const 
 // invertible key of hash.hpp over W words, seeded with the row's own length).  A row's bytes are read
 // as the aligned 8-byte words that hold at least one of its bytes (never past its last byte's word,
 // so never into another page) and funnel-shifted into place.
+// Text mode (text = 1: no row holds a zero byte -- *nul reports one if it does): the key is seeded
+// with 0 instead of the length, which the zero padding then encodes (the string ends at the first
+// zero byte), so no length column travels; words_to_var recomputes the lengths from the words.
+__device__ __forceinline__ bool has_zero_byte(uint64_t v) {
+  return ((v - 0x0101010101010101ull) & ~v & 0x8080808080808080ull) != 0;
+}
+
 __global__ void k_var_to_words(const uint8_t *__restrict__ bytes, const int64_t *__restrict__ offs, int64_t n, int W,
                                WordPtrs out, uint64_t *__restrict__ hash, int64_t *__restrict__ lens,
-                               uint64_t *__restrict__ h2) {
+                               uint64_t *__restrict__ h2, int text, unsigned int *__restrict__ nul) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  bool anynul = false;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const int64_t o = offs[i], L = offs[i + 1] - o;
     const uintptr_t a = reinterpret_cast<uintptr_t>(bytes + o);
     const uint64_t *p = reinterpret_cast<const uint64_t *>(a & ~uintptr_t(7));
     const int sh = (int)(a & 7) * 8;
     const int64_t nw = ((int64_t)(a & 7) + L + 7) >> 3;  // aligned words holding the row's bytes
-    uint64_t g = hashing::word_key_seed(L), w0 = 0, s2 = 0xC2B2AE3D27D4EB4FULL ^ (uint64_t)L;
+    uint64_t g = hashing::word_key_seed(text ? 0 : L), w0 = 0, s2 = 0xC2B2AE3D27D4EB4FULL ^ (uint64_t)L;
     uint64_t cur = nw > 0 ? p[0] : 0;
     for (int j = 0; j < W; ++j) {
       const uint64_t nxt = j + 1 < nw ? p[j + 1] : 0;
       uint64_t v = sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
       const int64_t rem = L - 8 * (int64_t)j;  // row bytes from word j on
-      if (rem <= 0) v = 0;
-      else if (rem < 8) v &= (uint64_t(1) << (8 * rem)) - 1;
+      uint64_t keep = ~0ull;
+      if (rem <= 0) keep = 0;
+      else if (rem < 8) keep = (uint64_t(1) << (8 * rem)) - 1;
+      v &= keep;
+      if (nul && rem > 0) anynul |= has_zero_byte(v | ~keep);
       cur = nxt;
       if (j == 0) w0 = v;
       else {
@@ -457,31 +468,107 @@ __global__ void k_var_to_words(const uint8_t *__restrict__ bytes, const int64_t 
       s2 = hashing::fmix64((s2 + v) * 0x87C37B91114253D5ULL) ^ 0x4CF5AD432745937FULL;
     }
     hash[i] = hashing::fmix64(w0 ^ g);
-    lens[i] = L;
+    if (lens) lens[i] = L;
     if (h2) h2[i] = s2;
+  }
+  if (anynul) atomicOr(nul, 1u);
+}
+
+// text mode: row lengths from the words (the first zero byte; w0 rebuilt from the key)
+__global__ void k_padded_text_lens(ConstWordPtrs in, const uint64_t *__restrict__ hash, int64_t n, int W,
+                                   int64_t *__restrict__ lens) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint64_t w[kMaxWords];
+    uint64_t g = hashing::word_key_seed(0);
+#pragma unroll
+    for (int j = 1; j < kMaxWords; ++j) {
+      w[j] = j < W ? (uint64_t)in.w[j][i] : 0;
+      if (j < W) g = hashing::word_key_step(g, w[j]);
+    }
+    w[0] = hashing::fmix64_inv(hash[i]) ^ g;
+    int64_t L = 8 * W;
+    bool found = false;
+#pragma unroll
+    for (int j = 0; j < kMaxWords; ++j) {
+      if (j >= W || found) continue;
+      const uint64_t z = (w[j] - 0x0101010101010101ull) & ~w[j] & 0x8080808080808080ull;
+      if (z) {  // (the lowest flagged byte is exact: the first zero byte)
+        L = 8 * j + (__ffsll((long long)z) - 1) / 8;
+        found = true;
+      }
+    }
+    lens[i] = L;
   }
 }
 
+// nb <= 8 bytes of v at d with the widest naturally aligned stores
+__device__ __forceinline__ void put_bytes(uint8_t *d, uint64_t v, int nb) {
+  while (nb > 0) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(d);
+    if ((a & 7) == 0 && nb == 8) {
+      *reinterpret_cast<uint64_t *>(d) = v;
+      return;
+    }
+    if ((a & 3) == 0 && nb >= 4) {
+      *reinterpret_cast<uint32_t *>(d) = (uint32_t)v;
+      d += 4;
+      v >>= 32;
+      nb -= 4;
+    } else if ((a & 1) == 0 && nb >= 2) {
+      *reinterpret_cast<uint16_t *>(d) = (uint16_t)v;
+      d += 2;
+      v >>= 16;
+      nb -= 2;
+    } else {
+      *d = (uint8_t)v;
+      ++d;
+      v >>= 8;
+      --nb;
+    }
+  }
+}
+
+// A row of L bytes at dst (any alignment): the head up to dst's next 8-byte boundary, then aligned
+// 8-byte stores of the words funnel-shifted by the head length, then the tail -- ~L / 8 + 4 stores
+// instead of L byte stores (neighbouring rows share the head / tail words: no wider stores there).
 __global__ void k_words_to_var(ConstWordPtrs in, const uint64_t *__restrict__ hash, const int64_t *__restrict__ lens,
-                               const int64_t *__restrict__ ooffs, int64_t n, int W, uint8_t *__restrict__ bytes) {
+                               const int64_t *__restrict__ ooffs, int64_t n, int W, int text,
+                               uint8_t *__restrict__ bytes) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const int64_t L = lens[i];
+    if (L <= 0) continue;
     uint8_t *dst = bytes + ooffs[i];
-    uint64_t g = hashing::word_key_seed(L);
-    for (int j = 1; j < W; ++j) g = hashing::word_key_step(g, (uint64_t)in.w[j][i]);
-    for (int j = 0; j < W && 8 * j < L; ++j) {
-      const uint64_t v = j == 0 ? hashing::fmix64_inv(hash[i]) ^ g : (uint64_t)in.w[j][i];
-      const int64_t nb = L - 8 * j < 8 ? L - 8 * j : 8;
-      uint8_t *d = dst + 8 * j;
-      if (nb == 8 && (reinterpret_cast<uintptr_t>(d) & 7) == 0) {
-        *reinterpret_cast<uint64_t *>(d) = v;
-      } else if (nb == 8 && (reinterpret_cast<uintptr_t>(d) & 3) == 0) {
-        reinterpret_cast<uint32_t *>(d)[0] = (uint32_t)v;
-        reinterpret_cast<uint32_t *>(d)[1] = (uint32_t)(v >> 32);
-      } else {
-        for (int b = 0; b < nb; ++b) d[b] = (uint8_t)(v >> (8 * b));
-      }
+    uint64_t w[kMaxWords + 1];
+    uint64_t g = hashing::word_key_seed(text ? 0 : L);
+#pragma unroll
+    for (int j = 1; j < kMaxWords; ++j) {
+      w[j] = j < W ? (uint64_t)in.w[j][i] : 0;
+      if (j < W) g = hashing::word_key_step(g, w[j]);
+    }
+    w[kMaxWords] = 0;
+    w[0] = hashing::fmix64_inv(hash[i]) ^ g;
+    const int h = (int)((8 - (reinterpret_cast<uintptr_t>(dst) & 7)) & 7);  // head bytes
+    if (L <= h) {
+      put_bytes(dst, w[0], (int)L);
+      continue;
+    }
+    if (h) put_bytes(dst, w[0], h);
+    const int64_t body = (L - h) >> 3;  // aligned 8-byte chunks
+#pragma unroll
+    for (int k = 0; k < kMaxWords; ++k) {
+      if (k >= body) break;
+      const uint64_t c = h ? (w[k] >> (8 * h)) | (w[k + 1] << (64 - 8 * h)) : w[k];
+      *reinterpret_cast<uint64_t *>(dst + h + 8 * k) = c;
+    }
+    const int tail = (int)((L - h) & 7);
+    if (tail) {
+      uint64_t c = 0;
+#pragma unroll
+      for (int k = 0; k < kMaxWords; ++k)
+        if (k == body) c = h ? (w[k] >> (8 * h)) | (w[k + 1] << (64 - 8 * h)) : w[k];
+      put_bytes(dst + h + 8 * body, c, tail);
     }
   }
 }
@@ -520,24 +607,34 @@ void var_hash2(const uint8_t *bytes, const int64_t *offs, int64_t n, uint64_t *h
 }
 
 void var_to_words(const uint8_t *bytes, const int64_t *offs, int64_t n, int W, int64_t *const *words, uint64_t *hash,
-                  int64_t *lens, uint64_t *h2, void *stream) {
-  CYLON_CHECK(W >= 1 && W <= kMaxWords && hash && lens, Code::Invalid, "padded string words: W " << W);
+                  int64_t *lens, uint64_t *h2, void *stream, bool text, unsigned int *nul) {
+  CYLON_CHECK(W >= 1 && W <= kMaxWords && hash && (lens || text), Code::Invalid, "padded string words: W " << W);
   if (n == 0) return;
   WordPtrs o{};
   for (int j = 1; j < W; ++j) o.w[j] = words[j];
   hipLaunchKernelGGL(k_var_to_words, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), bytes, offs, n, W, o, hash,
-                     lens, h2);
+                     lens, h2, text ? 1 : 0, nul);
+  HIP_LAUNCH_CHECK();
+}
+
+void padded_text_lens(const int64_t *const *words, const uint64_t *hash, int64_t n, int W, int64_t *lens,
+                      void *stream) {
+  CYLON_CHECK(W >= 1 && W <= kMaxWords && hash, Code::Invalid, "padded string words: W " << W);
+  if (n == 0) return;
+  ConstWordPtrs in{};
+  for (int j = 1; j < W; ++j) in.w[j] = words[j];
+  hipLaunchKernelGGL(k_padded_text_lens, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), in, hash, n, W, lens);
   HIP_LAUNCH_CHECK();
 }
 
 void words_to_var(const int64_t *const *words, const uint64_t *hash, const int64_t *lens, const int64_t *out_offs,
-                  int64_t n, int W, uint8_t *bytes, void *stream) {
+                  int64_t n, int W, uint8_t *bytes, void *stream, bool text) {
   CYLON_CHECK(W >= 1 && W <= kMaxWords && hash, Code::Invalid, "padded string words: W " << W);
   if (n == 0) return;
   ConstWordPtrs in{};
   for (int j = 1; j < W; ++j) in.w[j] = words[j];
   hipLaunchKernelGGL(k_words_to_var, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), in, hash, lens, out_offs,
-                     n, W, bytes);
+                     n, W, text ? 1 : 0, bytes);
   HIP_LAUNCH_CHECK();
 }
 

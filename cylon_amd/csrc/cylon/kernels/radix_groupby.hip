@@ -293,14 +293,22 @@ __global__ void k_rg_pack(const int64_t *__restrict__ offs, const int64_t *__res
 }
 
 // ---- QUANTILE on the radix path.  The rows (group key, value) are partitioned
-// by the group key's hash into partitions of <= kQCap rows; one workgroup sorts a partition in LDS by
-// (key, value) -- a bitonic network over the next power of two, pad rows (~0, ~0) last -- so every
-// group is a run with its valid values first, ascending (a null value's image ~0 sorts after every
-// valid one: NaNs are canonicalised to the positive quiet NaN, whose image is below ~0).  The thread
-// at a run's first row counts the run's valid values and applies the global path's type-2 rule
-// (groupby.hip k_quantile), and the groups are compacted with a block scan into the slab at the
-// partition's row offset (groups <= rows), as k_rg_agg does; radix_groupby_pack then packs them.
-constexpr int kQCap = 4096, kQThreads = 512, kQPer = kQCap / kQThreads;
+// by the group key's hash into partitions of <= kQCap rows (whole groups); one workgroup per
+// partition then SELECTS each group's order statistics instead of sorting:
+//   1. each thread holds 8 rows in registers; the next kQBBits bits of fmix64(key) (below the
+//      partition bits) pick a local bucket: LDS atomics count them and give each row its slot in
+//      the bucket, a block scan places the buckets, and the rows land in LDS in bucket order -- a
+//      bucket holds one group (rarely a few: ~10 groups per partition over 2048 buckets);
+//   2. every row ranks itself inside its group by one pass over its bucket -- rank = rows of the
+//      same key with a smaller (value, slot), nv = the group's valid values -- lanes of one bucket
+//      read the same LDS words (broadcasts);
+//   3. the row whose rank is the type-2 position (global path k_quantile: np = nv q, j = floor(np),
+//      pos = min(j, nv - 1), the mean with rank pos - 1 when np is whole) writes the group, the
+//      group's first row when every value is null; a block scan of those writers gives the slab
+//      slots (groups <= rows, as k_rg_agg) and radix_groupby_pack packs the slabs.
+// Nulls rank after every value (excluded, as the global path does).  Values compare as
+// order-preserving images of their doubles (NaN canonicalised).
+constexpr int kQCap = 4096, kQThreads = 512, kQPer = kQCap / kQThreads, kQBBits = 11, kQBuckets = 1 << kQBBits;
 
 // block-wide exclusive scan of one uint32 per thread
 __device__ __forceinline__ uint32_t q_block_exscan(uint32_t c, uint32_t *wsum) {
@@ -330,12 +338,17 @@ __device__ __forceinline__ double q_unimage(uint64_t m) {
 __global__ __launch_bounds__(kQThreads) void k_rg_quantile(const int64_t *__restrict__ keys,
                                                            const uint8_t *__restrict__ vals, int vwidth, int vkind,
                                                            const uint8_t *__restrict__ valid,
-                                                           const int64_t *__restrict__ offs, int64_t nparts, double q,
-                                                           int64_t *__restrict__ okeys, uint64_t *__restrict__ oq,
-                                                           uint64_t *__restrict__ ovalid, int64_t *__restrict__ gcount,
-                                                           int *__restrict__ overflow) {
-  __shared__ uint64_t sk[kQCap], sv[kQCap];
+                                                           const int64_t *__restrict__ offs, int64_t nparts, int bits,
+                                                           double q, int64_t *__restrict__ okeys,
+                                                           uint64_t *__restrict__ oq, uint64_t *__restrict__ ovalid,
+                                                           int64_t *__restrict__ gcount, int *__restrict__ overflow) {
+  __shared__ int64_t sk[kQCap];           // rows in bucket order: key
+  __shared__ uint64_t sv[kQCap];          //                       value image (~0: null)
+  __shared__ uint16_t sb[kQCap];          //                       bucket
+  __shared__ uint32_t bcnt[kQBuckets];    // rows per bucket, then the bucket's first slot
+  __shared__ double wv[kQCap];            // a writer row's quantile (at its slot)
   __shared__ uint32_t wsum[kQThreads / kWave];
+  const int shift = 64 - bits - kQBBits;  // bucket bits just below the partition bits
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
     const int64_t b = offs[p], cnt = offs[p + 1] - b;
     if (cnt > kQCap) {
@@ -345,67 +358,104 @@ __global__ __launch_bounds__(kQThreads) void k_rg_quantile(const int64_t *__rest
       }
       continue;
     }
-    int P = 1;
-    while (P < cnt) P <<= 1;
-    for (int i = threadIdx.x; i < P; i += kQThreads) {
+    for (int i = threadIdx.x; i < kQBuckets; i += kQThreads) bcnt[i] = 0;
+    __syncthreads();
+    int64_t rk[kQPer];
+    uint64_t rv[kQPer];
+    uint32_t rbk[kQPer];  // bucket << 16 | slot in the bucket (~0: no row)
+#pragma unroll
+    for (int u = 0; u < kQPer; ++u) {
+      const int i = u * kQThreads + threadIdx.x;
+      rbk[u] = 0xffffffffu;
       if (i < cnt) {
-        sk[i] = (uint64_t)keys[b + i];
-        sv[i] = (valid == nullptr || valid[b + i]) ? q_image(rg_double(load_bits(vals, b + i, vwidth), vwidth, vkind))
+        rk[u] = keys[b + i];
+        rv[u] = (valid == nullptr || valid[b + i]) ? q_image(rg_double(load_bits(vals, b + i, vwidth), vwidth, vkind))
                                                    : ~0ull;
-      } else {
-        sk[i] = ~0ull;
-        sv[i] = ~0ull;
+        const uint32_t bk = shift >= 0 ? (uint32_t)(hashing::fmix64((uint64_t)rk[u]) >> shift) & (kQBuckets - 1)
+                                       : (uint32_t)hashing::fmix64((uint64_t)rk[u]) & (kQBuckets - 1);
+        rbk[u] = bk << 16 | atomicAdd(&bcnt[bk], 1u);
       }
     }
     __syncthreads();
-    for (int size = 2; size <= P; size <<= 1) {
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        for (int i = threadIdx.x; i < (P >> 1); i += kQThreads) {
-          const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
-          const bool up = (lo & size) == 0;
-          const uint64_t ka = sk[lo], kb = sk[hi], va = sv[lo], vb = sv[hi];
-          const bool gt = ka > kb || (ka == kb && va > vb);
-          if (gt == up) {
-            sk[lo] = kb;
-            sk[hi] = ka;
-            sv[lo] = vb;
-            sv[hi] = va;
-          }
-        }
-        __syncthreads();
+    {  // bucket first slots (exclusive scan; kQBuckets / kQThreads buckets per thread)
+      constexpr int BPT = kQBuckets / kQThreads;
+      uint32_t c[BPT], tot = 0;
+#pragma unroll
+      for (int j = 0; j < BPT; ++j) {
+        c[j] = bcnt[threadIdx.x * BPT + j];
+        tot += c[j];
+      }
+      uint32_t ex = q_block_exscan(tot, wsum);
+#pragma unroll
+      for (int j = 0; j < BPT; ++j) {
+        bcnt[threadIdx.x * BPT + j] = ex;
+        ex += c[j];
       }
     }
-    // group starts among the first cnt sorted rows (pads sort last; a pad equal to a real row is
-    // interchangeable with it); thread t owns rows [t * kQPer, t * kQPer + kQPer)
-    uint32_t mine = 0;
+    __syncthreads();
 #pragma unroll
-    for (int u = 0; u < kQPer; ++u) {
-      const int i = threadIdx.x * kQPer + u;
-      mine += (i < cnt && (i == 0 || sk[i] != sk[i - 1])) ? 1u : 0u;
-    }
-    const uint32_t ex = q_block_exscan(mine, wsum);
-    uint32_t g = ex;
+    for (int u = 0; u < kQPer; ++u)
+      if (rbk[u] != 0xffffffffu) {
+        const uint32_t bk = rbk[u] >> 16, pos = bcnt[bk] + (rbk[u] & 0xffffu);
+        sk[pos] = rk[u];
+        sv[pos] = rv[u];
+        sb[pos] = (uint16_t)bk;
+      }
+    __syncthreads();
+    // rank every row in its group (one pass over its bucket); the writer rows of each group
+    uint32_t wmask = 0;  // 2 bits per row: 1 = writes a null quantile, 3 = a valid one
 #pragma unroll 1
     for (int u = 0; u < kQPer; ++u) {
-      const int i = threadIdx.x * kQPer + u;
-      if (!(i < cnt && (i == 0 || sk[i] != sk[i - 1]))) continue;
-      int e = i + 1;
-      while (e < cnt && sk[e] == sk[i]) ++e;
-      int nv = 0;  // valid values: the run's first rows
-      while (i + nv < e && sv[i + nv] != ~0ull) ++nv;
-      double r = 0.0;
-      if (nv > 0) {
-        const double np = (double)nv * q, j = floor(np), gg = np - j;
-        int pos = (int)j;
-        if (pos >= nv) pos = nv - 1;
-        r = (gg == 0.0 && pos > 0) ? 0.5 * (q_unimage(sv[i + pos - 1]) + q_unimage(sv[i + pos])) : q_unimage(sv[i + pos]);
+      const int i = u * kQThreads + threadIdx.x;  // slot in bucket order
+      if (i >= cnt) continue;
+      const int64_t k = sk[i];
+      const uint64_t v = sv[i];
+      const uint32_t bk = sb[i];
+      const int e0 = (int)bcnt[bk], e1 = bk + 1 < (uint32_t)kQBuckets ? (int)bcnt[bk + 1] : (int)cnt;
+      int rank = 0, nv = 0, lead = 1;  // lead: no earlier row of this key
+      uint64_t below = 0;              // (the largest valid value ranked just below, for a whole np)
+      bool has_below = false;
+      for (int j = e0; j < e1; ++j) {
+        if (sk[j] != k) continue;
+        const uint64_t vj = sv[j];
+        if (j < i) lead = 0;
+        if (vj != ~0ull) ++nv;
+        if (vj < v || (vj == v && j < i)) {
+          ++rank;
+          if (vj != ~0ull && (!has_below || vj >= below)) {
+            below = vj;
+            has_below = true;
+          }
+        }
       }
-      okeys[b + g] = (int64_t)sk[i];
-      oq[b + g] = (uint64_t)__double_as_longlong(r);
-      ovalid[b + g] = nv > 0 ? 1ull : 0ull;
+      if (nv == 0) {  // every value of the group is null: its first row writes a null quantile
+        if (lead) {
+          wmask |= 1u << (2 * u);
+          wv[i] = 0.0;
+        }
+        continue;
+      }
+      if (v == ~0ull) continue;
+      const double np = (double)nv * q, jf = floor(np);
+      const bool whole = np == jf;  // (a comparison: `np - j == 0` is contracted into an fma)
+      int pos = (int)jf;
+      if (pos >= nv) pos = nv - 1;
+      if (rank != pos) continue;
+      wmask |= 3u << (2 * u);  // a valid quantile
+      wv[i] = (whole && pos > 0) ? 0.5 * (q_unimage(below) + q_unimage(v)) : q_unimage(v);
+    }
+    uint32_t g = q_block_exscan((uint32_t)__popc(wmask & 0x5555u), wsum);
+#pragma unroll 1
+    for (int u = 0; u < kQPer; ++u) {
+      const int i = u * kQThreads + threadIdx.x;
+      const uint32_t f = (wmask >> (2 * u)) & 3u;
+      if (!f) continue;
+      okeys[b + g] = sk[i];
+      oq[b + g] = (uint64_t)__double_as_longlong(wv[i]);
+      ovalid[b + g] = f == 3 ? 1ull : 0ull;
       ++g;
     }
-    if (threadIdx.x == kQThreads - 1) gcount[p] = ex + mine;
+    if (threadIdx.x == kQThreads - 1) gcount[p] = g;
     __syncthreads();
   }
 }
@@ -413,14 +463,14 @@ __global__ __launch_bounds__(kQThreads) void k_rg_quantile(const int64_t *__rest
 int64_t radix_quantile_capacity() { return kQCap; }
 
 void radix_groupby_quantile(const int64_t *keys, const uint8_t *vals, int vwidth, int vkind, const uint8_t *valid,
-                            const int64_t *offs, int64_t nparts, double q, int64_t *okeys, uint64_t *oq,
+                            const int64_t *offs, int64_t nparts, int bits, double q, int64_t *okeys, uint64_t *oq,
                             uint64_t *ovalid, int64_t *gcount, int *overflow, void *stream) {
   hipStream_t s = as_stream(stream);
   HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
   if (nparts == 0) return;
   const int grid = (int)std::min<int64_t>(nparts, 8 * 256);
   hipLaunchKernelGGL(k_rg_quantile, dim3(grid), dim3(kQThreads), 0, s, keys, vals, vwidth, vkind, valid, offs, nparts,
-                     q, okeys, oq, ovalid, gcount, overflow);
+                     bits, q, okeys, oq, ovalid, gcount, overflow);
   HIP_LAUNCH_CHECK();
 }
 

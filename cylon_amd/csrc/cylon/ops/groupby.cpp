@@ -695,6 +695,9 @@ static TablePtr groupby_with(const TablePtr &t, const std::vector<int> &keys, co
 // the global path's type-2 rule (radix_groupby.hip k_rg_quantile).  nullptr when a partition
 // overflows (a group -- or a hash bucket of groups -- beyond the capacity): the caller falls back.
 // Reference: compute/aggregate_kernels.hpp:504-545 (QuantileKernel).
+static TablePtr radix_quantile_bits(const TablePtr &t, const std::vector<int> &keys, const AggSpec &a, const GroupKey &gkey,
+                                    int bits, const Column &c, int w);
+
 static TablePtr radix_quantile_table(const TablePtr &t, const std::vector<int> &keys, const AggSpec &a) {
   const Column &c = t->column(a.col);
   const int w = c.type.width();
@@ -705,8 +708,32 @@ static TablePtr radix_quantile_table(const TablePtr &t, const std::vector<int> &
   GroupKey gkey;
   if (!group_key(ex, t, keys, gkey)) return nullptr;
   const int64_t n = t->Rows(), cap = hip::radix_quantile_capacity();
-  int bits = 0;  // mean rows per partition <= 0.85 capacity (the Poisson tail of hashed keys fits)
-  while (bits < 24 && (double)n / (double)(int64_t(1) << bits) > 0.85 * (double)cap) ++bits;
+  // A partition holds Poisson(groups / P) whole groups of ~n / groups rows each, so its row count
+  // varies with the group size: P comes from the distinct-key estimate (HyperLogLog), with the
+  // groups' Poisson tail (6 sigma) inside the capacity -- 1B rows / 10M groups: 20 bits (two passes),
+  // where a row-count rule (1907-row mean) overflowed.  Groups larger than half the capacity: global path.
+  double groups;
+  {
+    at::Tensor regs = at::empty({hip::distinct_estimate_workspace()}, ex.opts(at::kInt));
+    groups = std::max(1.0, hip::distinct_estimate(ptr<int64_t>(gkey.k), n, reinterpret_cast<uint32_t *>(ptr<int32_t>(regs)),
+                                                  ex.stream));
+  }
+  const double grp_rows = (double)n / groups;
+  if (grp_rows > 0.5 * (double)cap) return nullptr;
+  auto fits = [&](int b) {
+    const double lam = groups / (double)(int64_t(1) << b);
+    return (double)n / (double)(int64_t(1) << b) <= 0.85 * (double)cap &&
+           grp_rows * (lam + 6.0 * std::sqrt(lam) + 2.0) <= (double)cap;
+  };
+  int bits = 0;
+  while (bits < 24 && !fits(bits)) ++bits;
+  return radix_quantile_bits(t, keys, a, gkey, bits, c, w);
+}
+
+static TablePtr radix_quantile_bits(const TablePtr &t, const std::vector<int> &keys, const AggSpec &a, const GroupKey &gkey,
+                                    int bits, const Column &c, int w) {
+  Exec ex(t->device());
+  const int64_t n = t->Rows();
   std::vector<at::Tensor> cols{gkey.k, c.data};
   std::vector<int> widths{8, w};
   if (c.nullable()) {
@@ -727,12 +754,17 @@ static TablePtr radix_quantile_table(const TablePtr &t, const std::vector<int> &
     CYLON_PHASE("groupby.radix.quantile", ex.device);
     hip::radix_groupby_quantile(ptr<int64_t>(cols[0]), reinterpret_cast<const uint8_t *>(cols[1].data_ptr()), w,
                                 static_cast<int>(c.type.kind()), c.nullable() ? cols[2].data_ptr<uint8_t>() : nullptr,
-                                ptr<int64_t>(offs), nparts, a.quantile, ptr<int64_t>(okeys),
+                                ptr<int64_t>(offs), nparts, bits, a.quantile, ptr<int64_t>(okeys),
                                 reinterpret_cast<uint64_t *>(ptr<int64_t>(oacc)),
                                 reinterpret_cast<uint64_t *>(ptr<int64_t>(oacc) + n), ptr<int64_t>(gcount),
                                 overflow.data_ptr<int>(), ex.stream);
   }
-  if (overflow.item<int>() != 0) {
+  if (overflow.item<int>() != 0) {  // a partition beyond the LDS capacity: finer partitions, once
+    if (bits <= 22) {
+      trace::add_counter("groupby.radix.quantile_overflow_retry", 1);
+      cols.clear();
+      return radix_quantile_bits(t, keys, a, gkey, bits + 2, c, w);
+    }
     trace::add_counter("groupby.radix.quantile_overflow_fallback", 1);
     return nullptr;
   }

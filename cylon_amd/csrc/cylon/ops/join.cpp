@@ -422,9 +422,8 @@ static void apply_presence(std::vector<Column> &cols, const TablePtr &in, const 
 // Every column of both tables is fixed width (radix_eligible); lk / rk are the int64 join keys
 // (a key column itself, or the composite image of several key columns).  All four join types:
 // the kernels emit unmatched rows of the preserved side(s) with presence bytes (outer_mode).
-static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr &right, const at::Tensor &lk,
-                           const at::Tensor &rk, const JoinConfig &cfg, JoinSink *sink = nullptr,
-                           bool hashed_key = false) {
+static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr &right, at::Tensor lk, at::Tensor rk,
+                           const JoinConfig &cfg, JoinSink *sink = nullptr, bool hashed_key = false) {
   const int64_t nl = left->Rows(), nr = right->Rows();
   const bool build_left = nl < nr;
   const TablePtr &bt = build_left ? left : right;
@@ -455,9 +454,11 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   bool narrow = !hashed_key && nl > 0 && nr > 0 && lk.scalar_type() == at::kLong && rk.scalar_type() == at::kLong &&
                 own_key_column(left, lk) && own_key_column(right, rk);
   at::Tensor narrow_bad = narrow ? at::zeros({1}, ex.opts(at::kInt)) : at::Tensor();
+  // the narrowing base's source (left key 0), its own copy: a released input's key column goes away
+  const at::Tensor base_src = narrow ? lk.slice(0, 0, 1).clone() : at::Tensor();
   hip::NarrowKeys nk;
   if (narrow) {
-    nk.base_src = ptr<int64_t>(lk);
+    nk.base_src = ptr<int64_t>(base_src);
     nk.bad = reinterpret_cast<unsigned int *>(narrow_bad.data_ptr<int>());
   }
   int64_t cap = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size(), (oj & 2) != 0,
@@ -488,6 +489,37 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     const double mean = (double)rows / (double)nparts;
     return ((int64_t)(mean + 8.0 * std::sqrt(mean) + 64.0) + 7) & ~int64_t(7);
   };
+  auto key_col = [](const TablePtr &t, const at::Tensor &k) {
+    int idx = -1, hits = 0;
+    for (int c = 0; c < t->Columns(); ++c) {
+      const Column &col = t->column(c);
+      if (col.type.width() == 8 && col.data.data_ptr() == k.data_ptr() && !col.nullable() &&
+          (col.type.kind() == ValueKind::SIGNED_INT || col.type.kind() == ValueKind::UNSIGNED_INT)) {
+        idx = c;
+        ++hits;
+      }
+    }
+    return hits == 1 ? idx : -1;
+  };
+  const int kl = key_col(left, lk), kr = key_col(right, rk);
+  // retain = false (reference table.cpp:150-154): an input is released as soon as nothing can need
+  // it again -- its own passes fit their slots and no key of either side leaves the narrowed range
+  // (else it would be repartitioned from the input) -- so its buffers are free before the other
+  // side's passes and the output allocation (1B x 1B: ~64 GB lower peak).  Only the sink-less join
+  // on partitions that can always complete releases (no global-table fallback needs the input later).
+  const bool rel_l = !left->IsRetain() && !sink, rel_r = !right->IsRetain() && !sink;
+  bool released_l = false, released_r = false;
+  at::Tensor r_outside;  // narrowed keys: right keys outside [base, base + 2^32) (checked before releasing left)
+  if (rel_l && narrow) {
+    auto mm = at::aminmax(rk);
+    const at::Tensor base = base_src - (int64_t(1) << 31);
+    r_outside = at::logical_or(std::get<0>(mm) < base, (std::get<1>(mm) - base) > (int64_t)0xffffffffll).to(at::kInt);
+  }
+  auto release = [&](const TablePtr &t, at::Tensor &key) {
+    t->ReleaseIfNotRetained();
+    key = at::Tensor();
+    trace::add_counter("join.radix.released_inputs", 1);
+  };
   RadixSide L, R;
   {
     CYLON_PHASE("join.radix.partition", ex.device);
@@ -517,7 +549,24 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
       if (!sl || !sr) trace::add_counter("join.radix.sampled_skew_sides", (sl ? 0 : 1) + (sr ? 0 : 1));
     }
     L = radix_partition(ex, left, lk, bits, nullptr, sl, nkp);
+    if (rel_l) {
+      at::Tensor z = at::zeros({1}, ex.opts(at::kInt));
+      const int bad = at::cat({L.slot ? L.overflow.slice(0, 0, 1) : z, narrow ? narrow_bad : z,
+                               r_outside.defined() ? r_outside.reshape({1}) : z}).sum().item<int>();
+      if (bad == 0) {
+        release(left, lk);
+        released_l = true;
+      }
+    }
     R = radix_partition(ex, right, rk, bits, nullptr, sr, nkp);
+    if (rel_r) {
+      at::Tensor z = at::zeros({1}, ex.opts(at::kInt));
+      const int bad = at::cat({R.slot ? R.overflow.slice(0, 0, 1) : z, narrow ? narrow_bad : z}).sum().item<int>();
+      if (bad == 0) {
+        release(right, rk);
+        released_r = true;
+      }
+    }
     if (L.slot || R.slot || narrow) {  // a side whose partition outgrew a slot is partitioned exactly
       at::Tensor z = at::zeros({}, ex.opts(at::kInt));
       at::Tensor f = at::stack({L.slot ? L.overflow[0] : z, R.slot ? R.overflow[0] : z,
@@ -546,24 +595,18 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   }
   RadixSide &B = build_left ? L : R;
   RadixSide &P = build_left ? R : L;
-  const int64_t *nbase = narrow ? ptr<int64_t>(lk) : nullptr;  // the join kernels' narrowed-key base
+  const int64_t *nbase = narrow ? ptr<int64_t>(base_src) : nullptr;  // the join kernels' narrowed-key base
+  // (a released input can no longer feed a fallback: the remaining failure exits raise instead)
+  const bool released = released_l || released_r;
+  auto fail = [&](const char *why) -> TablePtr {
+    CYLON_CHECK(!released, Code::ExecutionError,
+                "radix join with a released (retain = false) input could not complete: " << why);
+    return nullptr;
+  };
   // Inner joins keyed on one integer column per side (the partitioned key itself, same type, no
   // nulls): the two key values of every output row are equal, so the build side's output key
   // column is the probe side's -- one buffer behind both (columns are immutable): 8 B/row less
   // written and allocated (1B x 1B: 8 GB).  A/B knob: CYLON_RJ_SHARE_KEY=0.
-  auto key_col = [](const TablePtr &t, const at::Tensor &k) {
-    int idx = -1, hits = 0;
-    for (int c = 0; c < t->Columns(); ++c) {
-      const Column &col = t->column(c);
-      if (col.type.width() == 8 && col.data.data_ptr() == k.data_ptr() && !col.nullable() &&
-          (col.type.kind() == ValueKind::SIGNED_INT || col.type.kind() == ValueKind::UNSIGNED_INT)) {
-        idx = c;
-        ++hits;
-      }
-    }
-    return hits == 1 ? idx : -1;
-  };
-  const int kl = key_col(left, lk), kr = key_col(right, rk);
   const bool share_key = oj == 0 && !sink && kl >= 0 && kr >= 0 && left->column(kl).type == right->column(kr).type &&
                          knobs::Flag("RJ_SHARE_KEY", true);
   const int bkc = build_left ? kl : kr;  // the build side's key column (not written when shared)
@@ -694,7 +737,7 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     // the ranking guard of the stable (second and later) partition passes
     if (hip::rp_take_order_violation(ex.stream)) {
       trace::add_counter("join.radix.order_violation_fallback", 1);
-      return nullptr;
+      return fail("order violation");
     }
     if (stride > 1) {
       // Skew check of the sample: extrapolating a hot key's partition 32x would over-allocate
@@ -715,14 +758,14 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
       m = tail[0].item<int64_t>();
       if (tail[1].item<int64_t>() != 0) {
         trace::add_counter("join.radix.overflow_fallback", 1);
-        return nullptr;
+        return fail("overflow");
       }
       alloc = m;
     } else {
       at::Tensor tail = at::stack({counts.sum(), overflow.to(at::kLong)[0]}).cpu();
       if (tail[1].item<int64_t>() != 0) {  // a sampled partition already overflows the LDS (or is misplaced)
         trace::add_counter("join.radix.overflow_fallback", 1);
-        return nullptr;
+        return fail("overflow");
       }
       const double est = (double)tail[0].item<int64_t>() * (double)nparts / (double)counts.numel();
       // skewed inputs (split or exactly counted partitions exist): the sampled rest still holds
@@ -841,7 +884,7 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     if (flags & 1) {  // a build partition beyond the LDS capacity: global-table join instead
       if (sink) sink->size = off;
       trace::add_counter("join.radix.overflow_fallback", 1);
-      return nullptr;
+      return fail("overflow");
     }
     if (flags & 2) {  // the estimate was short: write again into an exact allocation
       trace::add_counter("join.radix.estimate_rerun", 1);
@@ -1121,6 +1164,7 @@ struct RadixKeys {
   // the padded word keys (word 0's stand-in), lwords / rwords words 1..W-1, llen / rlen the lengths
   int vw = 0;
   at::Tensor llen, rlen;
+  bool vtext = false;  // text mode (no zero bytes on either side): no length columns (partition.hip)
 };
 
 static int64_t fixed_var_len(const Exec &ex, const Column &c);
@@ -1128,7 +1172,7 @@ static std::vector<at::Tensor> var_to_words(const Exec &ex, const Column &c, int
                                             bool inv = false);
 static std::pair<int64_t, int64_t> var_len_range(const Exec &ex, const Column &c);
 static std::vector<at::Tensor> var_to_padded(const Exec &ex, const Column &c, int W, at::Tensor *key,
-                                             at::Tensor *lens);
+                                             at::Tensor *lens, unsigned int *nul = nullptr);
 
 static bool int_key(const Column &c) {
   return simple_key(c) && (c.type.kind() == ValueKind::SIGNED_INT ||
@@ -1261,9 +1305,18 @@ static RadixKeys radix_keys(const Exec &ex, const TablePtr &left, const TablePtr
       const int64_t hi = std::max(ra.second, rb.second);
       if (ra.first >= 0 && rb.first >= 0 && hi <= 64) {
         k.vw = (int)std::max<int64_t>(1, (hi + 7) / 8);
-        k.lwords = var_to_padded(ex, a, k.vw, &k.l, &k.llen);
-        k.rwords = var_to_padded(ex, b, k.vw, &k.r, &k.rlen);
-        trace::add_counter("join.radix.var_word_key", 1);
+        // text mode first (no zero byte in any row: the padding encodes the length, no length
+        // column travels); a zero byte on either side redoes both sides with lengths
+        at::Tensor nul = at::zeros({1}, ex.opts(at::kInt));
+        unsigned int *np = reinterpret_cast<unsigned int *>(nul.data_ptr<int>());
+        k.lwords = var_to_padded(ex, a, k.vw, &k.l, nullptr, np);
+        k.rwords = var_to_padded(ex, b, k.vw, &k.r, nullptr, np);
+        k.vtext = nul.item<int>() == 0;
+        if (!k.vtext) {
+          k.lwords = var_to_padded(ex, a, k.vw, &k.l, &k.llen);
+          k.rwords = var_to_padded(ex, b, k.vw, &k.r, &k.rlen);
+        }
+        trace::add_counter(k.vtext ? "join.radix.var_word_key_text" : "join.radix.var_word_key", 1);
         return k;
       }
     }
@@ -1379,6 +1432,70 @@ static TablePtr radix_join_chunked(const Exec &ex, const TablePtr &l, const Tabl
     return -1;
   };
   const int lkc = key_col(l, lk), rkc = key_col(r, rk);
+  // retain = false on both inputs: one chunk-major pass per side (radix.cpp RadixChunkPartition: every
+  // column, chunk = the LOW bits of fmix64(key)) whose input is released right after it, so each chunk
+  // is a contiguous slice and the inputs are read once -- instead of a chunk-id filter + row gather
+  // per chunk, whose gathers touch nearly every cache line of the inputs C times
+  if (!l->IsRetain() && !r->IsRetain() && C <= 1024) {
+    int cbits = 1;  // (twice the chunks the retained-input budget asks for: the copies and the output
+    while ((1 << cbits) < 2 * C) ++cbits;  // hold ~inputs + output, so each chunk's working set must be small)
+    const int64_t C2 = int64_t(1) << cbits;
+    auto chunk_major = [&](const TablePtr &t, const at::Tensor &k, int kc, at::Tensor &kout, std::vector<int64_t> &offs) {
+      std::vector<at::Tensor> cur{k};
+      std::vector<int> widths{8}, dpos(t->Columns(), -1), vpos(t->Columns(), -1);
+      for (int c = 0; c < t->Columns(); ++c) {
+        const Column &col = t->column(c);
+        if (c == kc) {
+          dpos[c] = 0;
+        } else {
+          dpos[c] = (int)cur.size();
+          cur.push_back(col.data);
+          widths.push_back(col.type.width());
+        }
+        if (col.nullable()) {
+          vpos[c] = (int)cur.size();
+          cur.push_back(col.validity);
+          widths.push_back(1);
+        }
+      }
+      at::Tensor o;
+      std::vector<at::Tensor> out = RadixChunkPartition(ex, std::move(cur), widths, cbits, &o);
+      offs = to_host_vec(o);
+      std::vector<Column> cols;
+      for (int c = 0; c < t->Columns(); ++c) {
+        const Column &col = t->column(c);
+        at::Tensor d = out[dpos[c]];
+        if (c == kc && d.scalar_type() != col.data.scalar_type()) d = d.view(col.data.scalar_type());
+        cols.emplace_back(col.name, col.type, t->Rows(), d, at::Tensor(), vpos[c] >= 0 ? out[vpos[c]] : at::Tensor());
+      }
+      kout = out[0];
+      TablePtr res = Table::Make(t->GetContext(), std::move(cols));
+      t->ReleaseIfNotRetained();
+      trace::add_counter("join.radix.released_inputs", 1);
+      return res;
+    };
+    at::Tensor lkp, rkp;
+    std::vector<int64_t> lo, ro;
+    TablePtr lp = chunk_major(l, lk, lkc, lkp, lo);
+    TablePtr rp = chunk_major(r, rk, rkc, rkp, ro);
+    trace::add_counter("join.radix.chunk_pass", 2);
+    JoinSink sink;
+    sink.chunks_total = (int)C2;
+    auto slice_tab = [&](const TablePtr &t, int64_t a, int64_t b) {
+      std::vector<Column> cols;
+      for (const auto &c : t->columns()) cols.push_back(c.slice(a, b - a));
+      return Table::Make(t->GetContext(), std::move(cols));
+    };
+    for (int64_t c = 0; c < C2; ++c) {
+      TablePtr lc = slice_tab(lp, lo[c], lo[c + 1]), rc = slice_tab(rp, ro[c], ro[c + 1]);
+      const at::Tensor lkc_t = lkc >= 0 ? lc->column(lkc).data.view(at::kLong) : lkp.slice(0, lo[c], lo[c + 1]);
+      const at::Tensor rkc_t = rkc >= 0 ? rc->column(rkc).data.view(at::kLong) : rkp.slice(0, ro[c], ro[c + 1]);
+      CYLON_CHECK(radix_join(ex, lc, rc, lkc_t, rkc_t, cfg, &sink, hashed_key), Code::ExecutionError,
+                  "radix join of a chunk of released (retain = false) inputs did not complete");
+      ++sink.chunks_done;
+    }
+    return sink.finish(l->GetContext());
+  }
   const at::Tensor cl = key_chunk_ids(lk, C), cr = key_chunk_ids(rk, C);
   JoinSink sink;
   sink.chunks_total = C;
@@ -1438,10 +1555,10 @@ static std::pair<int64_t, int64_t> var_len_range(const Exec &ex, const Column &c
 // a variable-length column (rows <= 8 W bytes) as W zero-padded words: *key = the padded word key
 // (word 0's stand-in), *lens = the row lengths; returns words 1..W-1.  One read of the bytes.
 static std::vector<at::Tensor> var_to_padded(const Exec &ex, const Column &c, int W, at::Tensor *key,
-                                             at::Tensor *lens) {
+                                             at::Tensor *lens, unsigned int *nul) {
   const int64_t n = c.length;
   *key = ex.empty_i64(n);
-  *lens = ex.empty_i64(n);
+  if (lens) *lens = ex.empty_i64(n);
   std::vector<at::Tensor> out;
   std::vector<int64_t *> wp{nullptr};
   for (int j = 1; j < W; ++j) {
@@ -1449,18 +1566,28 @@ static std::vector<at::Tensor> var_to_padded(const Exec &ex, const Column &c, in
     wp.push_back(ptr<int64_t>(out.back()));
   }
   hip::var_to_words(ptr<uint8_t>(c.data), ptr<int64_t>(c.offsets), n, W, wp.data(),
-                    reinterpret_cast<uint64_t *>(ptr<int64_t>(*key)), ptr<int64_t>(*lens), nullptr, ex.stream);
+                    reinterpret_cast<uint64_t *>(ptr<int64_t>(*key)), lens ? ptr<int64_t>(*lens) : nullptr, nullptr,
+                    ex.stream, lens == nullptr, nul);
   return out;
 }
 
-// wc = {padded word key, words 1..W-1, lengths} of m rows -> a string / binary column (rows whose
-// length column is null -- an outer join's absent side -- become null, zero bytes)
+// wc = {padded word key, words 1..W-1[, lengths]} of m rows -> a string / binary column (rows whose
+// key column is null -- an outer join's absent side -- become null, zero bytes).  Text mode (no
+// length column): the lengths come from the words.
 static Column padded_to_var(const Exec &ex, const std::string &name, const DataType &type,
-                            const std::vector<Column> &wc, int W) {
-  const Column &lc = wc[(size_t)W];
-  const int64_t m = lc.length;
-  at::Tensor lens = lc.data.slice(0, 0, m);
-  if (lc.nullable()) lens = at::where(lc.validity.slice(0, 0, m).to(at::kBool), lens, at::zeros({1}, lens.options()));
+                            const std::vector<Column> &wc, int W, bool text) {
+  const Column &kc = wc[0];
+  const int64_t m = kc.length;
+  at::Tensor lens;
+  if (text) {
+    lens = ex.empty_i64(std::max<int64_t>(m, 1)).slice(0, 0, m);
+    std::vector<const int64_t *> wp;
+    for (int j = 0; j < W; ++j) wp.push_back(ptr<int64_t>(wc[(size_t)j].data));
+    hip::padded_text_lens(wp.data(), reinterpret_cast<const uint64_t *>(wp[0]), m, W, ptr<int64_t>(lens), ex.stream);
+  } else {
+    lens = wc[(size_t)W].data.slice(0, 0, m);
+  }
+  if (kc.nullable()) lens = at::where(kc.validity.slice(0, 0, m).to(at::kBool), lens, at::zeros({1}, lens.options()));
   at::Tensor offs = at::zeros({m + 1}, ex.opts(at::kLong));
   if (m) {
     at::Tensor tail = offs.slice(0, 1, m + 1);
@@ -1471,8 +1598,8 @@ static Column padded_to_var(const Exec &ex, const std::string &name, const DataT
   std::vector<const int64_t *> wp;
   for (int j = 0; j < W; ++j) wp.push_back(ptr<int64_t>(wc[(size_t)j].data));
   hip::words_to_var(wp.data(), reinterpret_cast<const uint64_t *>(wp[0]), ptr<int64_t>(lens),
-                    ptr<int64_t>(offs), m, W, ptr<uint8_t>(bytes), ex.stream);
-  return Column(name, type, m, bytes.slice(0, 0, nbytes), offs, lc.validity);
+                    ptr<int64_t>(offs), m, W, ptr<uint8_t>(bytes), ex.stream, text);
+  return Column(name, type, m, bytes.slice(0, 0, nbytes), offs, kc.validity);
 }
 
 // wc = the word columns 0..W-1 (inv: wc[0] = the invertible word key, wc[1..] = words 1..W-1)
@@ -1538,7 +1665,7 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
           for (size_t j = 0; j < kwords.size(); ++j)
             cols.emplace_back("__cylon_w" + std::to_string(c) + "_" + std::to_string(j + 1), DataType(Type::INT64),
                               t->Rows(), kwords[j]);
-          cols.emplace_back("__cylon_wl" + std::to_string(c), DataType(Type::INT64), t->Rows(), klens);
+          if (!k.vtext) cols.emplace_back("__cylon_wl" + std::to_string(c), DataType(Type::INT64), t->Rows(), klens);
           continue;
         }
         const bool kw = k.wlen > 0 && c == keys[0];  // the key's word key + words from radix_keys
@@ -1580,7 +1707,7 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
   if (!radix_eligible(lp) || !radix_eligible(rp)) return nullptr;
   const int mchunks = sink ? 1 : radix_join_chunks(ex, lp, rp, k.l, k.r, cfg.GetType());
   TablePtr out = mchunks > 1 ? radix_join_chunked(ex, lp, rp, k.l, k.r, cfg, mchunks, k.verify)
-                             : radix_join(ex, lp, rp, k.l, k.r, cfg, sink, k.verify);
+                             : radix_join(ex, lp, rp, std::move(k.l), std::move(k.r), cfg, sink, k.verify);
   if (!out) return nullptr;
   if (k.verify && !lvar && !rvar) return drop_false_matches(out, cfg, left->Columns());
   if (!lpx && !rpx) return out;
@@ -1605,8 +1732,8 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
       if (pos[c] < 0 || c == skip_col) continue;
       if (vwid[c] > 0) {  // a variable-length string from its padded words + length
         std::vector<Column> wc;
-        for (int j = 0; j <= vwid[c]; ++j) wc.push_back(out->column(first + pos[c] + j));
-        cols[c] = padded_to_var(ex, prefix + orig->column(c).name, orig->column(c).type, wc, vwid[c]);
+        for (int j = 0; j < vwid[c] + (k.vtext ? 0 : 1); ++j) wc.push_back(out->column(first + pos[c] + j));
+        cols[c] = padded_to_var(ex, prefix + orig->column(c).name, orig->column(c).type, wc, vwid[c], k.vtext);
         continue;
       }
       if (wlen[c] > 0) {  // a fixed-length string from its word columns
@@ -1680,7 +1807,7 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
   // (a word-key column: the key words 1..W-1 -- equal word keys were matched, so word 0 is equal too;
   // a padded word key: words 1..W-1 and the length, which seeds the key's chain)
   for (size_t i = 0; i < lc.size(); ++i) {
-    const int64_t nwc = lvw[lc[i]] > 0 ? lvw[lc[i]] + 1 : (lwlen[lc[i]] + 7) / 8;
+    const int64_t nwc = lvw[lc[i]] > 0 ? lvw[lc[i]] + (k.vtext ? 0 : 1) : (lwlen[lc[i]] + 7) / 8;
     for (int64_t j = (k.wlen > 0 || k.vw > 0) ? 1 : 0; j < nwc; ++j) {
       aw.push_back(ptr<int64_t>(out->column(lpos[lc[i]] + (int)j).data));
       bw.push_back(ptr<int64_t>(out->column(rfirst + rpos[rc[i]] + (int)j).data));

@@ -188,6 +188,30 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
   return cur;
 }
 
+std::vector<at::Tensor> RadixChunkPartition(const Exec &ex, std::vector<at::Tensor> cur, const std::vector<int> &widths,
+                                            int cbits, at::Tensor *offs) {
+  CYLON_CHECK(ex.gpu && !cur.empty() && cur.size() == widths.size() && widths[0] == 8, Code::Invalid,
+              "RadixChunkPartition arguments");
+  const int64_t n = cur[0].numel();
+  std::vector<int> pw = widths;
+  const BytePacking bp = PackByteColumns(ex, cur, pw, n);
+  CYLON_CHECK(cur.size() <= 16, Code::Invalid, "RadixChunkPartition: " << cur.size() << " columns in one pass");
+  at::Tensor ws = ex.empty_i64(hip::radix_rows_pass_workspace(n, cbits));
+  std::vector<at::Tensor> nxt;
+  std::vector<const uint8_t *> in;
+  std::vector<uint8_t *> out;
+  for (const auto &x : cur) {
+    nxt.push_back(at::empty_like(x));
+    in.push_back(reinterpret_cast<const uint8_t *>(x.data_ptr()));
+    out.push_back(reinterpret_cast<uint8_t *>(nxt.back().data_ptr()));
+  }
+  *offs = ex.empty_i64((int64_t(1) << cbits) + 1);
+  hip::radix_chunk_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, cbits, in.data(), out.data(),
+                        pw.data(), (int)cur.size(), ptr<int64_t>(ws), ptr<int64_t>(*offs), ex.stream);
+  cur.clear();
+  return UnpackByteColumns(ex, bp, std::move(nxt), n);
+}
+
 std::vector<at::Tensor> RadixPartitionSlotted(const Exec &ex, std::vector<at::Tensor> cur,
                                               const std::vector<int> &widths, int bits, int64_t slot,
                                               at::Tensor *counts, at::Tensor *overflow,

@@ -76,6 +76,12 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
                                        std::vector<int> *keep_packed = nullptr, bool stable = true,
                                        const hip::NarrowKeys *nk = nullptr, const PrehistFn *prehist = nullptr);
 
+// Chunk-major order of a table for the bounded-memory join: one exact pass of every column by the
+// LOW cbits bits of fmix64(column 0 = the int64 key) (independent of the join partition's top bits);
+// *offs (2^cbits + 1 rows) = each chunk's first row.  Validity bytes travel packed as for RadixPartition.
+std::vector<at::Tensor> RadixChunkPartition(const Exec &ex, std::vector<at::Tensor> cols, const std::vector<int> &widths,
+                                            int cbits, at::Tensor *offs);
+
 // Hash-join partition in slot mode (MSD, two passes, no histogram before the second pass; see
 // kernel_decls.inc radix_slot_rows_pass): partition p holds (*counts)[p] rows at row p * slot.
 // Returns an empty vector (nothing launched) when the shape is not eligible; *overflow (int32

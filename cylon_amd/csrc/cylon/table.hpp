@@ -49,6 +49,11 @@ class Table {
     columns_.clear();
     rows_ = 0;
   }
+  // retain = false (reference table.cpp:150-154, :358-362): an operator that has consumed this
+  // table's rows drops its buffers early, so the memory returns to the allocator while the operator
+  // still runs.  The columns keep their name, type and nullability, with 0 rows (the table is
+  // empty afterwards).  A no-op for retained tables.
+  void ReleaseIfNotRetained();
 
   // total bytes of all buffers
   int64_t nbytes() const;

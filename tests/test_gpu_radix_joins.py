@@ -537,20 +537,35 @@ def test_radix_join_string_word_key(gpu_ctx, ctx, monkeypatch, how, fmt):
 
 
 @pytest.mark.parametrize("how", ["inner", "left", "outer"])
-def test_radix_join_memory_bounded_chunks(gpu_ctx, ctx, monkeypatch, how):
+@pytest.mark.parametrize("retain", [True, False])
+def test_radix_join_memory_bounded_chunks(gpu_ctx, ctx, monkeypatch, how, retain):
     """Bounded memory: with a device budget (config memory_budget_mb) below the join's working set
     + output, the radix join runs in key-hash chunks into one output sink (join.radix.memory_chunks)
-    and gives the CPU twin's result."""
+    and gives the CPU twin's result.  retain = false: one chunk-major pass per side (the input is
+    released after it) makes every chunk a contiguous slice (join.radix.chunk_pass)."""
     rng = np.random.default_rng(59)
     n = 3_000_000
-    a = pa.table({"k": rng.integers(0, 2_000_000, n), "v": rng.random(n)})
+    a = pa.table({"k": rng.integers(0, 2_000_000, n), "v": rng.random(n),
+                  "u": pa.array(rng.integers(-9, 9, n), mask=rng.random(n) < 0.1)})
     b = pa.table({"k": rng.integers(0, 2_000_000, n), "w": rng.random(n), "i": rng.integers(-5, 5, n)})
     gpu_ctx.add_config("memory_budget_mb", "220")
+    monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", "1024")
+    kw = dict(left_on=["k"], right_on=["k"], left_prefix="l_", right_prefix="r_")
     try:
-        got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["k"], monkeypatch)
+        L, R = Table(a, gpu_ctx), Table(b, gpu_ctx)
+        L.retain_memory(retain)
+        R.retain_memory(retain)
+        C.trace_enable(True)
+        C.trace_reset()
+        got = L.join(R, how, "hash", **kw).to_pandas()
+        c = dict(C.trace_counters())
+        C.trace_enable(False)
     finally:
         gpu_ctx.add_config("memory_budget_mb", "")
+    exp = Table(a, ctx).join(Table(b, ctx), how, "hash", **kw).to_pandas()
     assert c.get("join.radix.memory_chunks", 0) >= 2, c
+    assert c.get("join.radix.chunk_pass", 0) == (0 if retain else 2), c
+    assert (L.row_count, R.row_count) == ((n, n) if retain else (0, 0))
     assert len(got) == len(exp)
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
 
@@ -604,8 +619,14 @@ def test_radix_join_variable_length_keys(gpu_ctx, ctx, monkeypatch, how, kind):
     if kind == "string_0_64":  # a few empty keys on both sides (they match each other)
         a = a.set_column(0, "s", pa.array([("" if i % 9973 == 0 else s) for i, s in enumerate(a["s"].to_pylist())]))
         b = b.set_column(0, "s", pa.array([("" if i % 7919 == 0 else s) for i, s in enumerate(b["s"].to_pylist())]))
+    if bin_:  # zero bytes inside keys (a trailing one too): the length column must travel
+        fix = (lambda x: x[:2] + b"\x00" + x[2:] if x[:1] in (b"1", b"2") else (x + b"\x00" if x[:1] == b"3" else x))
+        a = a.set_column(0, "s", pa.array([fix(x) for x in a["s"].to_pylist()]))
+        b = b.set_column(0, "s", pa.array([fix(x) for x in b["s"].to_pylist()]))
     got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["s"], monkeypatch)
-    assert c.get("join.radix.var_word_key", 0) == 1 and c.get("join.radix.var_gather", 0) == 0, c
+    # text keys (no zero byte): the padding encodes the length (text mode); binary keys carry it
+    mode = "join.radix.var_word_key" if bin_ else "join.radix.var_word_key_text"
+    assert c.get(mode, 0) == 1 and c.get("join.radix.var_gather", 0) == 0, c
     assert c.get("join.radix.hash_collision_fallback", 0) == 0, c
     assert c.get("join.radix.shared_key_column", 0) == (2 if how == "inner" else 0), c
     assert c["join.radix.rows_out"] == len(exp)
@@ -628,7 +649,54 @@ def test_radix_join_variable_length_keys_gather_path(gpu_ctx, ctx, monkeypatch, 
     a = pa.table({"s": pa.array(_var_strings(rng, ids_a, lo, hi)), "v": rng.random(n)})
     b = pa.table({"s": pa.array(_var_strings(rng, ids_b, lo, hi)), "w": rng.random(n)})
     got, exp, c = _join(gpu_ctx, ctx, a, b, how, ["s"], monkeypatch)
-    assert c.get("join.radix.var_word_key", 0) == 0 and c.get("join.radix.var_gather", 0) == 1, c
+    assert c.get("join.radix.var_word_key", 0) == 0 and c.get("join.radix.var_word_key_text", 0) == 0, c
+    assert c.get("join.radix.var_gather", 0) == 1, c
     assert c.get("join.radix.hashed_key", 0) == 1 and c.get("join.radix.hash_collision_fallback", 0) == 0, c
     assert c["join.radix.rows_out"] == len(exp)
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
+
+
+@pytest.mark.parametrize("how", ["inner", "left"])
+def test_radix_join_retain_false_releases_inputs(gpu_ctx, monkeypatch, how):
+    """retain = false (reference table.cpp:150-154): each input's buffers are released as soon as
+    its partition passes fit (the other side's passes and the output then reuse the memory), so the
+    join's peak allocation drops by about the inputs' size; the inputs are empty afterwards and the
+    result equals the retained join's."""
+    n = 20_000_000
+
+    def run(retain):
+        g = torch.Generator(device="cuda").manual_seed(3)
+        sides = []
+        for _ in range(2):
+            cols = {"k": torch.randint(0, int(0.99 * n), (n,), generator=g, device="cuda")}
+            for i in range(3):
+                cols[f"v{i}"] = torch.rand(n, generator=g, device="cuda", dtype=torch.float64)
+            t = Table.from_torch(gpu_ctx, cols)
+            del cols
+            t.retain_memory(retain)
+            sides.append(t)
+        L, R = sides
+        del sides
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        base = torch.cuda.memory_allocated()
+        torch.cuda.reset_peak_memory_stats()
+        C.trace_enable(True)
+        C.trace_reset()
+        out = L.join(R, how, "hash", on=["k"], left_prefix="l_", right_prefix="r_")
+        torch.cuda.synchronize()
+        c = dict(C.trace_counters())
+        C.trace_enable(False)
+        peak = torch.cuda.max_memory_allocated() - base
+        t = out.to_torch()
+        sums = {name: float(x.double().sum()) for name, x in t.items() if not name.startswith("r_v")}
+        sums["rows"] = out.row_count
+        return sums, peak, c, (L.row_count, R.row_count)
+
+    kept, peak_kept, c_kept, rows_kept = run(True)
+    rel, peak_rel, c_rel, rows_rel = run(False)
+    assert c_kept.get("join.radix.released_inputs", 0) == 0 and rows_kept == (n, n)
+    assert c_rel.get("join.radix.released_inputs", 0) == 2 and rows_rel == (0, 0), c_rel
+    assert rel == kept
+    input_bytes = 2 * n * 32
+    assert peak_kept - peak_rel >= 0.5 * input_bytes, (peak_kept, peak_rel)
