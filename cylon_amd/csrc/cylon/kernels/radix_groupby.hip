@@ -335,20 +335,28 @@ __device__ __forceinline__ double q_unimage(uint64_t m) {
   return __longlong_as_double((long long)((m >> 63) ? (m & 0x7fffffffffffffffull) : ~m));
 }
 
-__global__ __launch_bounds__(kQThreads) void k_rg_quantile(const int64_t *__restrict__ keys,
-                                                           const uint8_t *__restrict__ vals, int vwidth, int vkind,
-                                                           const uint8_t *__restrict__ valid,
-                                                           const int64_t *__restrict__ offs, int64_t nparts, int bits,
-                                                           double q, int64_t *__restrict__ okeys,
-                                                           uint64_t *__restrict__ oq, uint64_t *__restrict__ ovalid,
-                                                           int64_t *__restrict__ gcount, int *__restrict__ overflow) {
-  __shared__ int64_t sk[kQCap];           // rows in bucket order: key
-  __shared__ uint64_t sv[kQCap];          //                       value image (~0: null)
-  __shared__ uint16_t sb[kQCap];          //                       bucket
-  __shared__ uint32_t bcnt[kQBuckets];    // rows per bucket, then the bucket's first slot
-  __shared__ double wv[kQCap];            // a writer row's quantile (at its slot)
+struct alignas(16) QKV {  // one row of a partition in LDS: group key, value image (~0: null)
+  int64_t k;
+  uint64_t v;
+};
+
+// 72 KB of LDS (rows as 16-byte (key, value) pairs read with one ds_read_b128, bucket counters) and
+// the writers' quantiles in registers: two blocks per CU, so one block's rank loop runs while the
+// other loads or places its partition.  The rank loop reads four rows per round before comparing
+// any of them (four LDS round trips in flight instead of one per row: the loop is latency-bound).
+__global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_rg_quantile(
+    const int64_t *__restrict__ keys, const uint8_t *__restrict__ vals, int vwidth, int vkind,
+    const uint8_t *__restrict__ valid, const int64_t *__restrict__ offs, int64_t nparts, int bits, double q,
+    int64_t *__restrict__ okeys, uint64_t *__restrict__ oq, uint64_t *__restrict__ ovalid,
+    int64_t *__restrict__ gcount, int *__restrict__ overflow) {
+  __shared__ QKV skv[kQCap];            // rows in bucket order
+  __shared__ uint32_t bcnt[kQBuckets];  // rows per bucket, then the bucket's first slot
   __shared__ uint32_t wsum[kQThreads / kWave];
   const int shift = 64 - bits - kQBBits;  // bucket bits just below the partition bits
+  auto bucket_of = [&](int64_t k) -> uint32_t {
+    const uint64_t h = hashing::fmix64((uint64_t)k);
+    return shift >= 0 ? (uint32_t)(h >> shift) & (kQBuckets - 1) : (uint32_t)h & (kQBuckets - 1);
+  };
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
     const int64_t b = offs[p], cnt = offs[p + 1] - b;
     if (cnt > kQCap) {
@@ -360,19 +368,15 @@ __global__ __launch_bounds__(kQThreads) void k_rg_quantile(const int64_t *__rest
     }
     for (int i = threadIdx.x; i < kQBuckets; i += kQThreads) bcnt[i] = 0;
     __syncthreads();
-    int64_t rk[kQPer];
-    uint64_t rv[kQPer];
+    // bucket slots from the keys; the rows are read again (L2-resident: the partition was just
+    // read) when they are placed, instead of holding 8 keys + values per thread across the scan
     uint32_t rbk[kQPer];  // bucket << 16 | slot in the bucket (~0: no row)
 #pragma unroll
     for (int u = 0; u < kQPer; ++u) {
       const int i = u * kQThreads + threadIdx.x;
       rbk[u] = 0xffffffffu;
       if (i < cnt) {
-        rk[u] = keys[b + i];
-        rv[u] = (valid == nullptr || valid[b + i]) ? q_image(rg_double(load_bits(vals, b + i, vwidth), vwidth, vkind))
-                                                   : ~0ull;
-        const uint32_t bk = shift >= 0 ? (uint32_t)(hashing::fmix64((uint64_t)rk[u]) >> shift) & (kQBuckets - 1)
-                                       : (uint32_t)hashing::fmix64((uint64_t)rk[u]) & (kQBuckets - 1);
+        const uint32_t bk = bucket_of(keys[b + i]);
         rbk[u] = bk << 16 | atomicAdd(&bcnt[bk], 1u);
       }
     }
@@ -396,43 +400,49 @@ __global__ __launch_bounds__(kQThreads) void k_rg_quantile(const int64_t *__rest
 #pragma unroll
     for (int u = 0; u < kQPer; ++u)
       if (rbk[u] != 0xffffffffu) {
+        const int i = u * kQThreads + threadIdx.x;
         const uint32_t bk = rbk[u] >> 16, pos = bcnt[bk] + (rbk[u] & 0xffffu);
-        sk[pos] = rk[u];
-        sv[pos] = rv[u];
-        sb[pos] = (uint16_t)bk;
+        const uint64_t v = (valid == nullptr || valid[b + i])
+                               ? q_image(rg_double(load_bits(vals, b + i, vwidth), vwidth, vkind))
+                               : ~0ull;
+        skv[pos] = QKV{keys[b + i], v};
       }
     __syncthreads();
-    // rank every row in its group (one pass over its bucket); the writer rows of each group
+    // rank every row in its group (one pass over its bucket); the writer rows of each group park
+    // their quantile in the ovalid slab at their own slot (read back by the same thread below)
     uint32_t wmask = 0;  // 2 bits per row: 1 = writes a null quantile, 3 = a valid one
 #pragma unroll 1
     for (int u = 0; u < kQPer; ++u) {
       const int i = u * kQThreads + threadIdx.x;  // slot in bucket order
-      if (i >= cnt) continue;
-      const int64_t k = sk[i];
-      const uint64_t v = sv[i];
-      const uint32_t bk = sb[i];
+      if (i >= cnt) break;
+      const QKV me = skv[i];
+      const int64_t k = me.k;
+      const uint64_t v = me.v;
+      const uint32_t bk = bucket_of(k);
       const int e0 = (int)bcnt[bk], e1 = bk + 1 < (uint32_t)kQBuckets ? (int)bcnt[bk + 1] : (int)cnt;
       int rank = 0, nv = 0, lead = 1;  // lead: no earlier row of this key
-      uint64_t below = 0;              // (the largest valid value ranked just below, for a whole np)
-      bool has_below = false;
-      for (int j = e0; j < e1; ++j) {
-        if (sk[j] != k) continue;
-        const uint64_t vj = sv[j];
-        if (j < i) lead = 0;
-        if (vj != ~0ull) ++nv;
-        if (vj < v || (vj == v && j < i)) {
-          ++rank;
-          if (vj != ~0ull && (!has_below || vj >= below)) {
-            below = vj;
-            has_below = true;
+      uint64_t below = 0;              // the largest valid value ranked just below (0: none -- every
+                                       // valid image is > 0, the null image ~0 the largest)
+#pragma unroll 1
+      for (int j = e0; j < e1; j += 4) {
+        QKV r[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) r[t] = j + t < e1 ? skv[j + t] : QKV{k ^ 1, 0};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (r[t].k != k) continue;
+          const int jj = j + t;
+          const uint64_t vj = r[t].v;
+          lead &= jj >= i;
+          nv += vj != ~0ull;
+          if (vj < v || (vj == v && jj < i)) {
+            ++rank;
+            if (vj != ~0ull && vj > below) below = vj;
           }
         }
       }
       if (nv == 0) {  // every value of the group is null: its first row writes a null quantile
-        if (lead) {
-          wmask |= 1u << (2 * u);
-          wv[i] = 0.0;
-        }
+        if (lead) wmask |= 1u << (2 * u);
         continue;
       }
       if (v == ~0ull) continue;
@@ -442,16 +452,22 @@ __global__ __launch_bounds__(kQThreads) void k_rg_quantile(const int64_t *__rest
       if (pos >= nv) pos = nv - 1;
       if (rank != pos) continue;
       wmask |= 3u << (2 * u);  // a valid quantile
-      wv[i] = (whole && pos > 0) ? 0.5 * (q_unimage(below) + q_unimage(v)) : q_unimage(v);
+      const double qv = (whole && pos > 0) ? 0.5 * (q_unimage(below) + q_unimage(v)) : q_unimage(v);
+      ovalid[b + i] = (uint64_t)__double_as_longlong(qv);
     }
     uint32_t g = q_block_exscan((uint32_t)__popc(wmask & 0x5555u), wsum);
-#pragma unroll 1
+    uint64_t wq[kQPer];
+#pragma unroll
+    for (int u = 0; u < kQPer; ++u)
+      wq[u] = ((wmask >> (2 * u)) & 3u) == 3u ? ovalid[b + u * kQThreads + threadIdx.x] : 0ull;
+    __syncthreads();  // every parked quantile read before the compacted writes overwrite the slab
+#pragma unroll
     for (int u = 0; u < kQPer; ++u) {
       const int i = u * kQThreads + threadIdx.x;
       const uint32_t f = (wmask >> (2 * u)) & 3u;
       if (!f) continue;
-      okeys[b + g] = sk[i];
-      oq[b + g] = (uint64_t)__double_as_longlong(wv[i]);
+      okeys[b + g] = skv[i].k;
+      oq[b + g] = wq[u];
       ovalid[b + g] = f == 3 ? 1ull : 0ull;
       ++g;
     }
@@ -468,7 +484,7 @@ void radix_groupby_quantile(const int64_t *keys, const uint8_t *vals, int vwidth
   hipStream_t s = as_stream(stream);
   HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
   if (nparts == 0) return;
-  const int grid = (int)std::min<int64_t>(nparts, 8 * 256);
+  const int grid = (int)std::min<int64_t>(nparts, 16 * 256);
   hipLaunchKernelGGL(k_rg_quantile, dim3(grid), dim3(kQThreads), 0, s, keys, vals, vwidth, vkind, valid, offs, nparts,
                      bits, q, okeys, oq, ovalid, gcount, overflow);
   HIP_LAUNCH_CHECK();

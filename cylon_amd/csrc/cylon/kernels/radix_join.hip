@@ -2279,25 +2279,72 @@ bool radix_mod_rows_pass_gapped(const int64_t *keys, int64_t n, uint32_t nparts,
   return true;
 }
 
+// Shuffle descriptor counts: rows per modulo partition, and (minmax != nullptr) the key column's
+// min / max from the same read of the keys -- the wire narrowing's range (ops/shuffle.cpp
+// planned_shuffle), which otherwise costs a second full read of the key column (aminmax).
 __global__ __launch_bounds__(kRPThreads) void k_mod_counts(ModDigit digit, int64_t n,
-                                                           unsigned long long *__restrict__ counts) {
+                                                           unsigned long long *__restrict__ counts,
+                                                           long long *__restrict__ minmax) {
   __shared__ unsigned int hist[kRPMaxBuckets];
+  __shared__ long long wmin[kRPWaves], wmax[kRPWaves];
   for (uint32_t p = threadIdx.x; p < digit.nparts; p += blockDim.x) hist[p] = 0;
   __syncthreads();
+  long long lo = LLONG_MAX, hi = LLONG_MIN;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) atomicAdd(&hist[digit(i)], 1u);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t k = digit.keys[i];
+    atomicAdd(&hist[digit.of_key(k)], 1u);
+    lo = k < lo ? k : lo;
+    hi = k > hi ? k : hi;
+  }
+  if (minmax != nullptr) {  // wave64 butterfly, then one global atomic pair per block
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      const long long a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+      lo = a < lo ? a : lo;
+      hi = b > hi ? b : hi;
+    }
+    const int w = threadIdx.x / kWave;
+    if (lane_id() == 0) {
+      wmin[w] = lo;
+      wmax[w] = hi;
+    }
+  }
   __syncthreads();
   for (uint32_t p = threadIdx.x; p < digit.nparts; p += blockDim.x)
     if (hist[p]) atomicAdd(&counts[p], (unsigned long long)hist[p]);
+  if (minmax != nullptr && threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x / kWave); ++w) {
+      lo = wmin[w] < lo ? wmin[w] : lo;
+      hi = wmax[w] > hi ? wmax[w] : hi;
+    }
+    lo = wmin[0] < lo ? wmin[0] : lo;
+    hi = wmax[0] > hi ? wmax[0] : hi;
+    atomicMin(&minmax[0], lo);
+    atomicMax(&minmax[1], hi);
+  }
 }
 
-void mod_partition_counts(const int64_t *keys, int64_t n, uint32_t nparts, int64_t *counts, void *stream) {
+__global__ void k_minmax_init(long long *minmax) {
+  if (threadIdx.x == 0) {
+    minmax[0] = LLONG_MAX;
+    minmax[1] = LLONG_MIN;
+  }
+}
+
+void mod_partition_counts(const int64_t *keys, int64_t n, uint32_t nparts, int64_t *counts, void *stream,
+                          int64_t *minmax) {
   CYLON_CHECK(nparts >= 1 && nparts <= (uint32_t)kRPMaxBuckets, Code::Invalid, "partition count " << nparts);
   hipStream_t s = as_stream(stream);
   HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int64_t) * nparts, s));
+  long long *mm = reinterpret_cast<long long *>(minmax);
+  if (mm != nullptr) {
+    hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(kWave), 0, s, mm);
+    HIP_LAUNCH_CHECK();
+  }
   if (n == 0) return;
   hipLaunchKernelGGL(k_mod_counts, dim3(grid_for(n, kRPThreads, kNumCUs * 2)), dim3(kRPThreads), 0, s,
-                     ModDigit{keys, nparts}, n, reinterpret_cast<unsigned long long *>(counts));
+                     ModDigit{keys, nparts}, n, reinterpret_cast<unsigned long long *>(counts), mm);
   HIP_LAUNCH_CHECK();
 }
 

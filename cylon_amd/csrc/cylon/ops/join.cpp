@@ -88,6 +88,7 @@ static std::pair<at::Tensor, at::Tensor> hash_join_pairs(const Exec &ex, const a
   const at::Tensor &pk = build_left ? rk : lk;
   const int64_t nb0 = bk0.numel(), np = pk.numel();
   at::Tensor sk, perm, hstart;
+  bool distinct = false;
   {
     CYLON_PHASE("join.build.directory", ex.device);
     auto sr = at::sort(bk0);
@@ -95,9 +96,14 @@ static std::pair<at::Tensor, at::Tensor> hash_join_pairs(const Exec &ex, const a
     perm = std::get<1>(sr);
     at::Tensor head = at::ones({nb0}, ex.opts(at::kBool));
     if (nb0 > 1) head.slice(0, 1, nb0).copy_(sk.slice(0, 1, nb0) != sk.slice(0, 0, nb0 - 1));
-    at::Tensor hpos = head.nonzero().flatten();
-    sk = sk.index_select(0, hpos);  // distinct keys, ascending
-    hstart = at::cat({hpos, at::full({1}, nb0, ex.opts(at::kLong))});
+    // distinct build keys (the common case): the sorted keys ARE the directory and
+    // every head is its own row -- no compaction, and the expansion below is one gather
+    distinct = nb0 == 0 || head.all().item<bool>();
+    if (!distinct) {
+      at::Tensor hpos = head.nonzero().flatten();
+      sk = sk.index_select(0, hpos);  // distinct keys, ascending
+      hstart = at::cat({hpos, at::full({1}, nb0, ex.opts(at::kLong))});
+    }
   }
   const at::Tensor &bk = sk;
   const int64_t nb = bk.numel();
@@ -160,6 +166,8 @@ static std::pair<at::Tensor, at::Tensor> hash_join_pairs(const Exec &ex, const a
   at::Tensor bo;
   {
     CYLON_PHASE("join.probe.expand", ex.device);
+    if (distinct) return build_left ? std::make_pair(perm.index_select(0, ho), po)
+                                    : std::make_pair(po, perm.index_select(0, ho));
     at::Tensor first = hstart.index_select(0, ho);
     at::Tensor cnt = hstart.index_select(0, ho + 1) - first;
     const int64_t m = po.numel() ? cnt.sum().item<int64_t>() : 0;
@@ -739,14 +747,17 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
       trace::add_counter("join.radix.order_violation_fallback", 1);
       return fail("order violation");
     }
+    int64_t ssum = 0, sover = 0;  // the sample's total and overflow flag (one read for both uses)
     if (stride > 1) {
       // Skew check of the sample: extrapolating a hot key's partition 32x would over-allocate
       // (ADVICE r03), so a sample whose largest partition output is far above its mean is
       // counted exactly instead.
       at::Tensor st = at::stack({counts.sum(), counts.max(), overflow.to(at::kLong)[0]}).cpu();
-      const int64_t ssum = st[0].item<int64_t>(), smax = st[1].item<int64_t>();
+      ssum = st[0].item<int64_t>();
+      sover = st[2].item<int64_t>();
+      const int64_t smax = st[1].item<int64_t>();
       const int64_t nsample = counts.numel();
-      if (st[2].item<int64_t>() == 0 && smax > 16 * (ssum / std::max<int64_t>(1, nsample)) + 65536) {
+      if (sover == 0 && smax > 16 * (ssum / std::max<int64_t>(1, nsample)) + 65536) {
         trace::add_counter("join.radix.skewed_sample_exact_count", 1);
         stride = 1;
         count(1);
@@ -762,12 +773,11 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
       }
       alloc = m;
     } else {
-      at::Tensor tail = at::stack({counts.sum(), overflow.to(at::kLong)[0]}).cpu();
-      if (tail[1].item<int64_t>() != 0) {  // a sampled partition already overflows the LDS (or is misplaced)
+      if (sover != 0) {  // a sampled partition already overflows the LDS (or is misplaced)
         trace::add_counter("join.radix.overflow_fallback", 1);
         return fail("overflow");
       }
-      const double est = (double)tail[0].item<int64_t>() * (double)nparts / (double)counts.numel();
+      const double est = (double)ssum * (double)nparts / (double)counts.numel();
       // skewed inputs (split or exactly counted partitions exist): the sampled rest still holds
       // moderately hot keys, so its estimate gets 10 % slack instead of 2 % (memory, not a rewrite)
       const double slack = nheavy + nmid > 0 ? 1.10 : 1.02;

@@ -913,28 +913,30 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
     for (int side = 0; side < NT; ++side)
       for (int c = 0; c < tsp[side]->Columns(); ++c)
         if (c != vs[side].rid && narrow_candidate(tsp[side]->column(c))) cand.push_back({side, c});
-  for (auto &sc : cand) {
-    const Column &c = tsp[sc.first]->column(sc.second);
-    if (c.length == 0) {
-      parts.push_back(at::tensor({std::numeric_limits<int64_t>::max(), std::numeric_limits<int64_t>::min()}, lopt));
-    } else {
-      auto mm = at::aminmax(c.data.slice(0, 0, c.length));
-      parts.push_back(at::stack({std::get<0>(mm), std::get<1>(mm)}));
-    }
-  }
   std::vector<bool> fast(NT);
   std::vector<at::Tensor> vbytes;  // per var column: bytes per partition
+  std::vector<at::Tensor> counts(NT), key_mm(NT);  // key_mm: the fast count kernel's key min / max
   {
     CYLON_PHASE("shuffle.partition", dev);
     for (int i = 0; i < NT; ++i) {
       fast[i] = vs[i].vcols.empty() && mod_pass_eligible(ts[i], tcols[i], P);
       if (vs[i].vcols.empty()) {
-        parts.push_back(counts_device(ts[i], tcols[i], P, fast[i]));
+        if (fast[i]) {  // counts and, for a narrowable key, its range from ONE read of the keys
+          Exec ex(dev);
+          counts[i] = ex.empty_i64(P);
+          const bool kmm = std::find(cand.begin(), cand.end(), std::make_pair(i, tcols[i][0])) != cand.end();
+          if (kmm) key_mm[i] = ex.empty_i64(2);
+          hip::mod_partition_counts(reinterpret_cast<const int64_t *>(ts[i]->column(tcols[i][0]).data.data_ptr()),
+                                    ts[i]->Rows(), P, ptr<int64_t>(counts[i]), ex.stream,
+                                    kmm ? ptr<int64_t>(key_mm[i]) : nullptr);
+        } else {
+          counts[i] = counts_device(ts[i], tcols[i], P, false);
+        }
         continue;
       }
       auto pc = hash_pids_counts(ts[i], tcols[i], P);  // the ORIGINAL key columns (a var key hashes its bytes)
       vs[i].pid = pc.first;
-      parts.push_back(pc.second);
+      counts[i] = pc.second;
       const at::Tensor pid64 = pc.first.to(at::kLong);
       for (int c : vs[i].vcols) {
         const Column &col = ts[i]->column(c);
@@ -944,6 +946,19 @@ static void planned_shuffle(const std::vector<TablePtr> &ts, const std::vector<s
       }
     }
   }
+  for (auto &sc : cand) {
+    const Column &c = tsp[sc.first]->column(sc.second);
+    if (c.length == 0) {
+      parts.push_back(at::tensor({std::numeric_limits<int64_t>::max(), std::numeric_limits<int64_t>::min()}, lopt));
+    } else if (key_mm[sc.first].defined() && sc.second == tcols[sc.first][0]) {
+      parts.push_back(key_mm[sc.first]);
+      trace::add_counter("shuffle.fused_key_minmax", 1);
+    } else {
+      auto mm = at::aminmax(c.data.slice(0, 0, c.length));
+      parts.push_back(at::stack({std::get<0>(mm), std::get<1>(mm)}));
+    }
+  }
+  for (auto &cn : counts) parts.push_back(cn);
   for (auto &b : vbytes) parts.push_back(b);
   at::Tensor desc = at::cat(parts);
   const int64_t D = desc.numel();
