@@ -193,6 +193,16 @@ void Table::ReleaseIfNotRetained() {
   rows_ = 0;
 }
 
+void Table::ReleaseBufferIfNotRetained(int c, bool validity) {
+  if (retain_ || c < 0 || c >= (int)columns_.size()) return;
+  Column &col = columns_[(size_t)c];
+  if (validity) {
+    if (col.validity.defined()) col.validity = at::empty({0}, col.validity.options());
+  } else {
+    col.data = at::empty({0}, col.data.options());
+  }
+}
+
 TablePtr Table::to(at::Device dev) const {
   std::vector<Column> cols;
   cols.reserve(columns_.size());

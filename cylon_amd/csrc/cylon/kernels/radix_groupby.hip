@@ -309,6 +309,7 @@ __global__ void k_rg_pack(const int64_t *__restrict__ offs, const int64_t *__res
 // Nulls rank after every value (excluded, as the global path does).  Values compare as
 // order-preserving images of their doubles (NaN canonicalised).
 constexpr int kQCap = 4096, kQThreads = 512, kQPer = kQCap / kQThreads, kQBBits = 11, kQBuckets = 1 << kQBBits;
+constexpr int kQWaveRows = 128;  // buckets one wave sorts in registers (2 rows per lane)
 
 // block-wide exclusive scan of one uint32 per thread
 __device__ __forceinline__ uint32_t q_block_exscan(uint32_t c, uint32_t *wsum) {
@@ -340,18 +341,201 @@ struct alignas(16) QKV {  // one row of a partition in LDS: group key, value ima
   uint64_t v;
 };
 
-// 72 KB of LDS (rows as 16-byte (key, value) pairs read with one ds_read_b128, bucket counters) and
-// the writers' quantiles in registers: two blocks per CU, so one block's rank loop runs while the
-// other loads or places its partition.  The rank loop reads four rows per round before comparing
-// any of them (four LDS round trips in flight instead of one per row: the loop is latency-bound).
+__device__ __forceinline__ bool q_less(int64_t ak, uint64_t av, int64_t bk, uint64_t bv) {
+  return ak != bk ? ak < bk : av < bv;
+}
+
+// Bitonic sort of 64 * S (key, value) rows held by one wave, element e = s * 64 + lane in slot s of
+// lane `lane`: distances < 64 exchange through cross-lane shuffles, distance >= 64 inside the lane.
+// Fully unrolled (constant shuffle distances and direction masks): the rolled form measured 89 vs
+// 77 ms per 1B-row call, although unrolled the compiler spills lane masks through v_readlane.
+template <int S>
+__device__ __forceinline__ void q_wave_bitonic(int64_t (&k)[S], uint64_t (&v)[S]) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int kk = 2; kk <= 64 * S; kk <<= 1) {
+#pragma unroll
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {
+        const int js = j >> 6;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          if (s & js) continue;  // the pair (s, s | js), handled from its lower slot
+          const int t = s | js;
+          const bool asc = ((s * 64 + lane) & kk) == 0;
+          if (q_less(k[t], v[t], k[s], v[s]) == asc) {
+            const int64_t tk = k[s];
+            const uint64_t tv = v[s];
+            k[s] = k[t];
+            v[s] = v[t];
+            k[t] = tk;
+            v[t] = tv;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const int64_t ok = __shfl_xor((long long)k[s], j);
+          const uint64_t ov = (uint64_t)__shfl_xor((unsigned long long)v[s], j);
+          const bool asc = ((s * 64 + lane) & kk) == 0, lower = (lane & j) == 0;
+          const bool take = lower == asc ? q_less(ok, ov, k[s], v[s]) : q_less(k[s], v[s], ok, ov);
+          if (take) {
+            k[s] = ok;
+            v[s] = ov;
+          }
+        }
+      }
+    }
+  }
+}
+
+// Output of one group (a writer row): its slot comes from the partition's LDS counter, so the
+// groups of a partition come out in no fixed order (group-by order is unspecified).  FUSE: the
+// valid values' sum, count, min and max go to the four fz planes at the same slot.
+template <bool FUSE>
+__device__ __forceinline__ void q_emit(unsigned int *nout, int64_t *okeys, uint64_t *oq, uint64_t *ovalid,
+                                       uint64_t *fz, int64_t n, int64_t b, int64_t key, bool has, double qv,
+                                       double sum, int64_t cnt, double mn, double mx) {
+  const int64_t g = b + (int64_t)atomicAdd(nout, 1u);
+  okeys[g] = key;
+  oq[g] = has ? (uint64_t)__double_as_longlong(qv) : 0ull;
+  ovalid[g] = has ? 1ull : 0ull;
+  if constexpr (FUSE) {
+    fz[g] = (uint64_t)__double_as_longlong(sum);
+    fz[n + g] = (uint64_t)cnt;
+    fz[2 * n + g] = has ? (uint64_t)__double_as_longlong(mn) : 0ull;
+    fz[3 * n + g] = has ? (uint64_t)__double_as_longlong(mx) : 0ull;
+  }
+}
+
+// One wave ranks one bucket of sz <= 64 * S rows (slots [e0, e0 + sz) of skv): sort by (key, value)
+// -- pads (the bucket's largest key, the null image) sort after every real row and tie only with
+// that key's null rows, whose content they share -- then each group's rows are contiguous with its
+// valid values first in value order, so the type-2 position is index arithmetic.  The sorted rows go
+// back to skv, and each group's LAST valid row (its first row when every value is null) emits the
+// group: the quantile rows are read back from skv at start + pos (and pos - 1); FUSE: the sum from a
+// segmented wave scan, min / max the first / last valid values.
+template <int S, bool FUSE>
+__device__ __forceinline__ void q_rank_bucket(QKV *skv, int e0, int sz, double q, unsigned int *nout, int64_t *okeys,
+                                              uint64_t *oq, uint64_t *ovalid, uint64_t *fz, int64_t n, int64_t b) {
+  const int lane = lane_id();
+  int64_t k[S];
+  uint64_t v[S];
+  int64_t kmax = INT64_MIN;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int e = s * 64 + lane;
+    if (e < sz) {
+      const QKV r = skv[e0 + e];
+      k[s] = r.k;
+      v[s] = r.v;
+      kmax = r.k > kmax ? r.k : kmax;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t x = __shfl_xor((long long)kmax, o);
+    kmax = x > kmax ? x : kmax;
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    if (s * 64 + lane >= sz) {
+      k[s] = kmax;
+      v[s] = ~0ull;
+    }
+  q_wave_bitonic<S>(k, v);
+  bool head[S], last_valid[S];
+  int start[S];
+  double sum[S];
+  int carry = 0;
+  double scarry = 0.0;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    int64_t pk = __shfl_up((long long)k[s], 1), nk = __shfl_down((long long)k[s], 1);
+    uint64_t nvv = (uint64_t)__shfl_down((unsigned long long)v[s], 1);
+    if (s > 0) {
+      const int64_t lk = __shfl((long long)k[s - 1], 63);
+      if (lane == 0) pk = lk;
+    }
+    if (s + 1 < S) {
+      const int64_t fk = __shfl((long long)k[s + 1], 0);
+      const uint64_t fv = (uint64_t)__shfl((unsigned long long)v[s + 1], 0);
+      if (lane == 63) {
+        nk = fk;
+        nvv = fv;
+      }
+    }
+    const int e = s * 64 + lane;
+    head[s] = e == 0 || k[s] != pk;
+    last_valid[s] = v[s] != ~0ull && (e == 64 * S - 1 || nk != k[s] || nvv == ~0ull);
+    int st = head[s] ? e : 0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int x = __shfl_up(st, d);
+      if (lane >= d) st = x > st ? x : st;
+    }
+    st = st > carry ? st : carry;
+    start[s] = st;
+    carry = __shfl(st, 63);
+    if constexpr (FUSE) {  // segmented inclusive sum of the valid values (nulls and pads add 0)
+      double x = v[s] != ~0ull ? q_unimage(v[s]) : 0.0;
+      bool f = head[s];
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const double y = __shfl_up(x, d);
+        const int g = __shfl_up((int)f, d);
+        if (lane >= d && !f) {
+          x += y;
+          f = g != 0;
+        }
+      }
+      if (!f) x += scarry;
+      sum[s] = x;
+      scarry = __shfl(x, 63);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    if (s * 64 + lane < sz) skv[e0 + s * 64 + lane] = QKV{k[s], v[s]};
+  __builtin_amdgcn_wave_barrier();  // (one wave's LDS writes complete in order before its reads)
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int e = s * 64 + lane;
+    if (e >= sz) continue;
+    if (head[s] && v[s] == ~0ull) {  // every value of the group is null (valid values sort first)
+      q_emit<FUSE>(nout, okeys, oq, ovalid, fz, n, b, k[s], false, 0.0, 0.0, 0, 0.0, 0.0);
+      continue;
+    }
+    if (!last_valid[s]) continue;
+    const int nv = e - start[s] + 1;
+    const double np = (double)nv * q, jf = floor(np);
+    const bool whole = np == jf;
+    int pos = (int)jf;
+    if (pos >= nv) pos = nv - 1;
+    const double at = q_unimage(skv[e0 + start[s] + pos].v);
+    const double qv = (whole && pos > 0) ? 0.5 * (q_unimage(skv[e0 + start[s] + pos - 1].v) + at) : at;
+    double mn = 0.0;
+    if constexpr (FUSE) mn = q_unimage(skv[e0 + start[s]].v);
+    q_emit<FUSE>(nout, okeys, oq, ovalid, fz, n, b, k[s], true, qv, FUSE ? sum[s] : 0.0, nv, mn, q_unimage(v[s]));
+  }
+}
+
+// 72 KB of LDS (the partition's rows as 16-byte (key, value) pairs, bucket counters): two blocks per
+// CU.  Per partition: the rows are read ONCE from HBM into LDS (input order, bucket counts by LDS
+// atomics), moved to bucket order inside LDS, ranked (a wave per bucket of <= kQWaveRows rows; every
+// row of a larger bucket counts its rank over the bucket), and each group is written by one row at
+// a slot from an LDS counter -- one HBM round trip and six barriers per partition.
+template <bool FUSE>
 __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_rg_quantile(
     const int64_t *__restrict__ keys, const uint8_t *__restrict__ vals, int vwidth, int vkind,
     const uint8_t *__restrict__ valid, const int64_t *__restrict__ offs, int64_t nparts, int bits, double q,
     int64_t *__restrict__ okeys, uint64_t *__restrict__ oq, uint64_t *__restrict__ ovalid,
-    int64_t *__restrict__ gcount, int *__restrict__ overflow) {
-  __shared__ QKV skv[kQCap];            // rows in bucket order
+    uint64_t *__restrict__ fz, int64_t n, int64_t *__restrict__ gcount, int *__restrict__ overflow) {
+  __shared__ QKV skv[kQCap];            // rows (input order, then bucket order)
   __shared__ uint32_t bcnt[kQBuckets];  // rows per bucket, then the bucket's first slot
   __shared__ uint32_t wsum[kQThreads / kWave];
+  __shared__ unsigned int s_nout;       // groups emitted by this partition
+  __shared__ uint16_t sbl[kQBuckets];   // the partition's buckets of <= kQWaveRows rows, compacted
   const int shift = 64 - bits - kQBBits;  // bucket bits just below the partition bits
   auto bucket_of = [&](int64_t k) -> uint32_t {
     const uint64_t h = hashing::fmix64((uint64_t)k);
@@ -367,16 +551,20 @@ __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       continue;
     }
     for (int i = threadIdx.x; i < kQBuckets; i += kQThreads) bcnt[i] = 0;
+    if (threadIdx.x == 0) s_nout = 0;
     __syncthreads();
-    // bucket slots from the keys; the rows are read again (L2-resident: the partition was just
-    // read) when they are placed, instead of holding 8 keys + values per thread across the scan
     uint32_t rbk[kQPer];  // bucket << 16 | slot in the bucket (~0: no row)
 #pragma unroll
     for (int u = 0; u < kQPer; ++u) {
       const int i = u * kQThreads + threadIdx.x;
       rbk[u] = 0xffffffffu;
       if (i < cnt) {
-        const uint32_t bk = bucket_of(keys[b + i]);
+        const int64_t kk = keys[b + i];
+        const uint64_t vv = (valid == nullptr || valid[b + i])
+                                ? q_image(rg_double(load_bits(vals, b + i, vwidth), vwidth, vkind))
+                                : ~0ull;
+        skv[i] = QKV{kk, vv};
+        const uint32_t bk = bucket_of(kk);
         rbk[u] = bk << 16 | atomicAdd(&bcnt[bk], 1u);
       }
     }
@@ -396,21 +584,57 @@ __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         ex += c[j];
       }
     }
-    __syncthreads();
+    {  // input order -> bucket order, inside LDS
+      QKV r[kQPer];
 #pragma unroll
-    for (int u = 0; u < kQPer; ++u)
-      if (rbk[u] != 0xffffffffu) {
-        const int i = u * kQThreads + threadIdx.x;
-        const uint32_t bk = rbk[u] >> 16, pos = bcnt[bk] + (rbk[u] & 0xffffu);
-        const uint64_t v = (valid == nullptr || valid[b + i])
-                               ? q_image(rg_double(load_bits(vals, b + i, vwidth), vwidth, vkind))
-                               : ~0ull;
-        skv[pos] = QKV{keys[b + i], v};
-      }
+      for (int u = 0; u < kQPer; ++u)
+        if (rbk[u] != 0xffffffffu) r[u] = skv[u * kQThreads + threadIdx.x];
+      __syncthreads();  // (also orders the scan's bcnt writes before the reads below)
+#pragma unroll
+      for (int u = 0; u < kQPer; ++u)
+        if (rbk[u] != 0xffffffffu) skv[bcnt[rbk[u] >> 16] + (rbk[u] & 0xffffu)] = r[u];
+    }
     __syncthreads();
-    // rank every row in its group (one pass over its bucket); the writer rows of each group park
-    // their quantile in the ovalid slab at their own slot (read back by the same thread below)
-    uint32_t wmask = 0;  // 2 bits per row: 1 = writes a null quantile, 3 = a valid one
+    // buckets of <= kQWaveRows rows (nearly all: a bucket holds one group, rarely a few): one wave
+    // sorts each.  The non-empty ones are listed first (ballots + a block scan over the waves) and
+    // dealt round-robin, so every wave sorts ~(buckets / 8) of them: a partition's ~10 groups per 8
+    // waves, instead of whichever waves' bucket ranges they hash into (PMC: 75 % of wave cycles
+    // waiting, mostly at the barrier behind the busiest wave)
+    const int wave = threadIdx.x / kWave, lane = lane_id();
+    {
+      constexpr int PER = kQBuckets / (kQThreads / kWave);  // buckets a wave lists
+      uint64_t mk[PER / kWave];
+      uint32_t mine = 0;
+#pragma unroll
+      for (int c = 0; c < PER / kWave; ++c) {
+        const int bk = wave * PER + c * kWave + lane;
+        const int szl = (bk + 1 < kQBuckets ? (int)bcnt[bk + 1] : (int)cnt) - (int)bcnt[bk];
+        mk[c] = __ballot(szl > 0 && szl <= kQWaveRows);
+        mine += (uint32_t)__popcll(mk[c]);
+      }
+      if (lane == 0) wsum[wave] = mine;
+      __syncthreads();
+      uint32_t at = 0, tot = 0;
+#pragma unroll
+      for (int w = 0; w < kQThreads / kWave; ++w) {
+        at += w < wave ? wsum[w] : 0u;
+        tot += wsum[w];
+      }
+#pragma unroll
+      for (int c = 0; c < PER / kWave; ++c) {
+        if ((mk[c] >> lane) & 1ull) sbl[at + (uint32_t)__popcll(mk[c] & lanemask_lt())] = (uint16_t)(wave * PER + c * kWave + lane);
+        at += (uint32_t)__popcll(mk[c]);
+      }
+      __syncthreads();
+      for (uint32_t j = wave; j < tot; j += kQThreads / kWave) {
+        const int bk = sbl[j];
+        const int e0 = (int)bcnt[bk], sz = (bk + 1 < kQBuckets ? (int)bcnt[bk + 1] : (int)cnt) - e0;
+        if (sz <= 64) q_rank_bucket<1, FUSE>(skv, e0, sz, q, &s_nout, okeys, oq, ovalid, fz, n, b);
+        else q_rank_bucket<2, FUSE>(skv, e0, sz, q, &s_nout, okeys, oq, ovalid, fz, n, b);
+      }
+    }
+    // rows of larger buckets (never touched by the wave phase): every row counts its rank over its
+    // bucket; the row at the type-2 position emits the group
 #pragma unroll 1
     for (int u = 0; u < kQPer; ++u) {
       const int i = u * kQThreads + threadIdx.x;  // slot in bucket order
@@ -420,9 +644,12 @@ __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       const uint64_t v = me.v;
       const uint32_t bk = bucket_of(k);
       const int e0 = (int)bcnt[bk], e1 = bk + 1 < (uint32_t)kQBuckets ? (int)bcnt[bk + 1] : (int)cnt;
+      if (e1 - e0 <= kQWaveRows) continue;
       int rank = 0, nv = 0, lead = 1;  // lead: no earlier row of this key
       uint64_t below = 0;              // the largest valid value ranked just below (0: none -- every
                                        // valid image is > 0, the null image ~0 the largest)
+      double gsum = 0.0;               // FUSE: the group's valid sum / smallest / largest image
+      uint64_t gmin = ~0ull, gmax = 0;
 #pragma unroll 1
       for (int j = e0; j < e1; j += 4) {
         QKV r[4];
@@ -435,14 +662,21 @@ __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(4))) 
           const uint64_t vj = r[t].v;
           lead &= jj >= i;
           nv += vj != ~0ull;
+          if constexpr (FUSE) {
+            if (vj != ~0ull) {
+              gsum += q_unimage(vj);
+              gmin = vj < gmin ? vj : gmin;
+              gmax = vj > gmax ? vj : gmax;
+            }
+          }
           if (vj < v || (vj == v && jj < i)) {
             ++rank;
             if (vj != ~0ull && vj > below) below = vj;
           }
         }
       }
-      if (nv == 0) {  // every value of the group is null: its first row writes a null quantile
-        if (lead) wmask |= 1u << (2 * u);
+      if (nv == 0) {  // every value of the group is null: its first row emits a null quantile
+        if (lead) q_emit<FUSE>(&s_nout, okeys, oq, ovalid, fz, n, b, k, false, 0.0, 0.0, 0, 0.0, 0.0);
         continue;
       }
       if (v == ~0ull) continue;
@@ -451,28 +685,12 @@ __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       int pos = (int)jf;
       if (pos >= nv) pos = nv - 1;
       if (rank != pos) continue;
-      wmask |= 3u << (2 * u);  // a valid quantile
       const double qv = (whole && pos > 0) ? 0.5 * (q_unimage(below) + q_unimage(v)) : q_unimage(v);
-      ovalid[b + i] = (uint64_t)__double_as_longlong(qv);
+      q_emit<FUSE>(&s_nout, okeys, oq, ovalid, fz, n, b, k, true, qv, gsum, nv, q_unimage(gmin), q_unimage(gmax));
     }
-    uint32_t g = q_block_exscan((uint32_t)__popc(wmask & 0x5555u), wsum);
-    uint64_t wq[kQPer];
-#pragma unroll
-    for (int u = 0; u < kQPer; ++u)
-      wq[u] = ((wmask >> (2 * u)) & 3u) == 3u ? ovalid[b + u * kQThreads + threadIdx.x] : 0ull;
-    __syncthreads();  // every parked quantile read before the compacted writes overwrite the slab
-#pragma unroll
-    for (int u = 0; u < kQPer; ++u) {
-      const int i = u * kQThreads + threadIdx.x;
-      const uint32_t f = (wmask >> (2 * u)) & 3u;
-      if (!f) continue;
-      okeys[b + g] = skv[i].k;
-      oq[b + g] = wq[u];
-      ovalid[b + g] = f == 3 ? 1ull : 0ull;
-      ++g;
-    }
-    if (threadIdx.x == kQThreads - 1) gcount[p] = g;
     __syncthreads();
+    if (threadIdx.x == 0) gcount[p] = s_nout;
+    __syncthreads();  // (s_nout and skv are reused by the next partition)
   }
 }
 
@@ -480,13 +698,18 @@ int64_t radix_quantile_capacity() { return kQCap; }
 
 void radix_groupby_quantile(const int64_t *keys, const uint8_t *vals, int vwidth, int vkind, const uint8_t *valid,
                             const int64_t *offs, int64_t nparts, int bits, double q, int64_t *okeys, uint64_t *oq,
-                            uint64_t *ovalid, int64_t *gcount, int *overflow, void *stream) {
+                            uint64_t *ovalid, int64_t *gcount, int *overflow, void *stream, uint64_t *fused,
+                            int64_t n) {
   hipStream_t s = as_stream(stream);
   HIP_CHECK(hipMemsetAsync(overflow, 0, sizeof(int), s));
   if (nparts == 0) return;
   const int grid = (int)std::min<int64_t>(nparts, 16 * 256);
-  hipLaunchKernelGGL(k_rg_quantile, dim3(grid), dim3(kQThreads), 0, s, keys, vals, vwidth, vkind, valid, offs, nparts,
-                     bits, q, okeys, oq, ovalid, gcount, overflow);
+  if (fused)
+    hipLaunchKernelGGL(k_rg_quantile<true>, dim3(grid), dim3(kQThreads), 0, s, keys, vals, vwidth, vkind, valid, offs,
+                       nparts, bits, q, okeys, oq, ovalid, fused, n, gcount, overflow);
+  else
+    hipLaunchKernelGGL(k_rg_quantile<false>, dim3(grid), dim3(kQThreads), 0, s, keys, vals, vwidth, vkind, valid, offs,
+                       nparts, bits, q, okeys, oq, ovalid, fused, n, gcount, overflow);
   HIP_LAUNCH_CHECK();
 }
 

@@ -1164,6 +1164,11 @@ bool rp_take_order_violation(void *stream) {
   }
   return h != 0;
 }
+int *rp_order_flag() { return order_flag(); }
+void rp_note_order_violation(void *stream) {
+  HIP_CHECK(hipMemsetAsync(order_flag(), 0, sizeof(int), as_stream(stream)));
+  g_lane_ok[current_device()].store(2);
+}
 static bool rp_wave_atomic(hipStream_t s) { return lds_lane_order_ok(reinterpret_cast<void *>(s)); }
 
 // Pass kernel: "lean" (two register-lean blocks per CU) or "classic" (one block per CU with
@@ -2080,6 +2085,23 @@ static void slot_rows_pass(const Digit &dg, int64_t n, int first_bits, int secon
   }
 }
 
+// Second pass of a bounded-memory join chunk (ops/join.cpp radix_join_chunked): the input is the
+// chunk's rows of an exact narrowed first pass -- nseg consecutive first-pass buckets, bucket g
+// starting at row bbase[g] (relative to the chunk) -- and digit d = the low second_bits bits of the
+// total_bits partition id goes to slot g * 2^second_bits + d, so the chunk's partitions come out
+// in partition order.
+void radix_slot_segment_pass(const uint32_t *keys, int64_t n, int total_bits, int second_bits, const uint8_t *const *in,
+                             uint8_t *const *out, const int *widths, int ncols, const uint32_t *bbase, int nseg,
+                             int64_t slot, int64_t *ws, int64_t *counts, unsigned int *overflow, void *stream,
+                             const NarrowKeys *nk) {
+  CYLON_CHECK(nk && nk->base_src && nseg >= 1 && nseg <= kSlotMaxSeg && n > 0 && n < (int64_t(1) << 31),
+              Code::Invalid, "segment slot pass arguments");
+  const int64_t nslots = int64_t(nseg) << second_bits;
+  slot_pass(PartDigitN{keys, 1, nk->base_src, nk->bad, total_bits, 0, (1u << second_bits) - 1, 0}, n, second_bits,
+            in, out, widths, ncols, 1, nseg, bbase, nullptr, 0, 0, 0, 1, nslots, slot, ws, counts, overflow,
+            as_stream(stream));
+}
+
 // ---- sampled partition histogram (join slot-mode decision): hist[part] += 1 for keys i = k * stride
 template <class Digit>
 __global__ void k_part_sample(Digit dg, int64_t n, int64_t stride, uint32_t *__restrict__ hist) {
@@ -2408,10 +2430,13 @@ __global__ void k_low_chunk_offsets(const int64_t *__restrict__ keys, int64_t n,
 }
 
 void radix_chunk_pass(const int64_t *keys, int64_t n, int cbits, const uint8_t *const *in, uint8_t *const *out,
-                      const int *widths, int ncols, int64_t *ws, int64_t *offs, void *stream) {
+                      const int *widths, int ncols, int64_t *ws, int64_t *offs, void *stream, bool stable) {
   CYLON_CHECK(cbits >= 1 && cbits <= kRJMaxDigitBits, Code::Invalid, "chunk pass bits " << cbits);
   const uint32_t nb = 1u << cbits;
-  rows_pass_launch(PartDigit{keys, 64, 0, nb - 1}, n, cbits, in, out, widths, ncols, ws, stream, 0, false);
+  // stable: exact per-tile offsets AND a stable in-tile rank, so every pass over the same keys moves
+  // row i to the same place (column groups of one table, moved by separate passes)
+  rows_pass_launch(PartDigit{keys, 64, 0, nb - 1}, n, cbits, in, out, widths, ncols, ws, stream, 0, stable);
+  if (offs == nullptr) return;
   // (column 0 of the output: the keys in chunk-major order)
   hipLaunchKernelGGL(k_low_chunk_offsets, dim3(grid_for((int64_t)nb + 1)), dim3(kBlock), 0, as_stream(stream),
                      reinterpret_cast<const int64_t *>(out[0]), n, nb - 1, (int64_t)nb, offs);

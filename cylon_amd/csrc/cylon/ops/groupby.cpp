@@ -696,9 +696,13 @@ static TablePtr groupby_with(const TablePtr &t, const std::vector<int> &keys, co
 // overflows (a group -- or a hash bucket of groups -- beyond the capacity): the caller falls back.
 // Reference: compute/aggregate_kernels.hpp:504-545 (QuantileKernel).
 static TablePtr radix_quantile_bits(const TablePtr &t, const std::vector<int> &keys, const AggSpec &a, const GroupKey &gkey,
-                                    int bits, const Column &c, int w);
+                                    int bits, const Column &c, int w, const std::vector<AggSpec> *fuse);
 
-static TablePtr radix_quantile_table(const TablePtr &t, const std::vector<int> &keys, const AggSpec &a) {
+// fuse (optional): SUM / COUNT / MEAN / MIN / MAX aggregates of the quantile's own float64 column,
+// computed by the quantile kernel from the same sorted rows (no second group-by and no join); their
+// columns follow the quantile column in `fuse` order.
+static TablePtr radix_quantile_table(const TablePtr &t, const std::vector<int> &keys, const AggSpec &a,
+                                     const std::vector<AggSpec> *fuse = nullptr) {
   const Column &c = t->column(a.col);
   const int w = c.type.width();
   if (c.is_var() || c.type.kind() == ValueKind::FIXED_BYTES || !c.type.is_numeric() ||
@@ -727,11 +731,11 @@ static TablePtr radix_quantile_table(const TablePtr &t, const std::vector<int> &
   };
   int bits = 0;
   while (bits < 24 && !fits(bits)) ++bits;
-  return radix_quantile_bits(t, keys, a, gkey, bits, c, w);
+  return radix_quantile_bits(t, keys, a, gkey, bits, c, w, fuse);
 }
 
 static TablePtr radix_quantile_bits(const TablePtr &t, const std::vector<int> &keys, const AggSpec &a, const GroupKey &gkey,
-                                    int bits, const Column &c, int w) {
+                                    int bits, const Column &c, int w, const std::vector<AggSpec> *fuse) {
   Exec ex(t->device());
   const int64_t n = t->Rows();
   std::vector<at::Tensor> cols{gkey.k, c.data};
@@ -748,7 +752,8 @@ static TablePtr radix_quantile_bits(const TablePtr &t, const std::vector<int> &k
     offs = at::tensor({int64_t(0), n}, at::TensorOptions().dtype(at::kLong)).to(ex.device);
   }
   const int64_t nparts = int64_t(1) << bits;
-  at::Tensor okeys = ex.empty_i64(n), oacc = ex.empty_i64(2 * n), gcount = ex.empty_i64(nparts);
+  const int planes = fuse ? 6 : 2;  // quantile, validity [, sum, count, min, max]
+  at::Tensor okeys = ex.empty_i64(n), oacc = ex.empty_i64(planes * n), gcount = ex.empty_i64(nparts);
   at::Tensor overflow = at::empty({1}, ex.opts(at::kInt));
   {
     CYLON_PHASE("groupby.radix.quantile", ex.device);
@@ -757,27 +762,43 @@ static TablePtr radix_quantile_bits(const TablePtr &t, const std::vector<int> &k
                                 ptr<int64_t>(offs), nparts, bits, a.quantile, ptr<int64_t>(okeys),
                                 reinterpret_cast<uint64_t *>(ptr<int64_t>(oacc)),
                                 reinterpret_cast<uint64_t *>(ptr<int64_t>(oacc) + n), ptr<int64_t>(gcount),
-                                overflow.data_ptr<int>(), ex.stream);
+                                overflow.data_ptr<int>(), ex.stream,
+                                fuse ? reinterpret_cast<uint64_t *>(ptr<int64_t>(oacc) + 2 * n) : nullptr, n);
   }
   if (overflow.item<int>() != 0) {  // a partition beyond the LDS capacity: finer partitions, once
     if (bits <= 22) {
       trace::add_counter("groupby.radix.quantile_overflow_retry", 1);
       cols.clear();
-      return radix_quantile_bits(t, keys, a, gkey, bits + 2, c, w);
+      return radix_quantile_bits(t, keys, a, gkey, bits + 2, c, w, fuse);
     }
     trace::add_counter("groupby.radix.quantile_overflow_fallback", 1);
     return nullptr;
   }
   at::Tensor goff = exclusive_scan(ex, gcount);
   const int64_t ng = read_i64(goff, nparts);
-  at::Tensor gkeys = ex.empty_i64(ng), gacc = ex.empty_i64(2 * ng);
+  at::Tensor gkeys = ex.empty_i64(ng), gacc = ex.empty_i64(planes * ng);
   if (ng > 0)
     hip::radix_groupby_pack(ptr<int64_t>(offs), ptr<int64_t>(goff), nparts, ptr<int64_t>(okeys),
-                            reinterpret_cast<const uint64_t *>(ptr<int64_t>(oacc)), n, 2, ptr<int64_t>(gkeys),
+                            reinterpret_cast<const uint64_t *>(ptr<int64_t>(oacc)), n, planes, ptr<int64_t>(gkeys),
                             reinterpret_cast<uint64_t *>(ptr<int64_t>(gacc)), ng, ex.stream);
   std::vector<Column> out = group_key_columns(t, gkey, gkeys);
-  out.push_back(double_col(std::string(AggPrefix(AGG_QUANTILE)) + c.name, gacc.slice(0, 0, ng).view(at::kDouble),
-                           gacc.slice(0, ng, 2 * ng).ne(0)));
+  auto plane = [&](int j) { return gacc.slice(0, j * ng, (j + 1) * ng); };
+  out.push_back(double_col(std::string(AggPrefix(AGG_QUANTILE)) + c.name, plane(0).view(at::kDouble), plane(1).ne(0)));
+  if (fuse) {
+    const at::Tensor cnt = plane(3), some = cnt > 0;
+    for (const AggSpec &f : *fuse) {
+      const std::string name = std::string(AggPrefix(f.op)) + c.name;
+      switch (f.op) {
+        case AGG_SUM: out.push_back(double_col(name, plane(2).view(at::kDouble))); break;
+        case AGG_COUNT: out.push_back(long_col(name, cnt)); break;
+        case AGG_MEAN: out.push_back(double_col(name, plane(2).view(at::kDouble) / cnt.to(at::kDouble), some)); break;
+        case AGG_MIN: out.push_back(double_col(name, plane(4).view(at::kDouble), c.nullable() ? some : at::Tensor())); break;
+        case AGG_MAX: out.push_back(double_col(name, plane(5).view(at::kDouble), c.nullable() ? some : at::Tensor())); break;
+        default: CYLON_THROW(Code::Invalid, "fused quantile aggregate " << f.op);
+      }
+    }
+    trace::add_counter("groupby.radix.quantile_fused_aggs", (int64_t)fuse->size());
+  }
   trace::add_counter("groupby.radix.quantile", 1);
   return Table::Make(t->GetContext(), std::move(out));
 }
@@ -807,6 +828,28 @@ static TablePtr radix_groupby_composed(const TablePtr &t, const std::vector<int>
   if (nucols.empty() && qidx.empty()) return nullptr;
   for (int k : keys)
     if (t->column(k).is_var() || (!nucols.empty() && t->column(k).nullable())) return nullptr;
+  // one QUANTILE of a float64 column whose other aggregates are SUM / COUNT / MEAN / MIN / MAX of the
+  // same column: the quantile kernel computes them all from its sorted rows (one partition of
+  // (key, value), no second group-by, no join) -- the {sum, quantile} shape of the config-4 bench
+  if (qidx.size() == 1 && nucols.empty() && !rest.empty()) {
+    const int qc = aggs[(size_t)qidx[0]].col;
+    bool fusable = t->column(qc).type.type == Type::DOUBLE;
+    for (const auto &r : rest)
+      fusable &= r.col == qc && (r.op == AGG_SUM || r.op == AGG_COUNT || r.op == AGG_MEAN || r.op == AGG_MIN ||
+                                 r.op == AGG_MAX);
+    if (fusable) {
+      TablePtr ft = radix_quantile_table(t, keys, aggs[(size_t)qidx[0]], &rest);
+      if (ft) {
+        const int nk = (int)keys.size();
+        std::vector<Column> out;
+        for (int i = 0; i < nk; ++i) out.push_back(ft->column(i).with_name(t->column(keys[i]).name));
+        int ri = 0;
+        for (size_t i = 0; i < aggs.size(); ++i)
+          out.push_back(ft->column(aggs[i].op == AGG_QUANTILE ? nk : nk + 1 + ri++));
+        return Table::Make(t->GetContext(), std::move(out));
+      }
+    }
+  }
   const int nk = (int)keys.size();
   std::vector<int> kidx(nk);
   for (int i = 0; i < nk; ++i) kidx[i] = i;

@@ -349,6 +349,14 @@ static void unpack_validity_words(const Exec &ex, const TablePtr &t, const Radix
   hip::unpack_byte_columns(wp.data(), (int)dst.size(), m, dst.data(), ex.stream);
 }
 
+// A bounded-memory join chunk partitioned outside radix_join (radix_join_chunked): both sides'
+// partitions (narrowed keys), the chunk's partition bits and the narrowing base's source.
+struct PrePartition {
+  RadixSide L, R;
+  int bits = 0;
+  at::Tensor base_src;
+};
+
 // Output accumulator of a chunked (pipelined) distributed join.  The radix join
 // writes every chunk's rows straight into one set of output columns at the
 // running row offset (capacity sized from the first chunk's output for all
@@ -359,6 +367,10 @@ struct JoinSink {
   std::vector<Column> cols;  // left columns ++ right columns, `cap` rows each
   int64_t size = 0, cap = 0;
   int chunks_total = 1, chunks_done = 0;
+  // the radix join's sampled skew check before its slot passes (off for the bounded-memory chunks:
+  // a skewed chunk still completes -- an overflowing slot repartitions that side exactly)
+  bool sample_skew = true;
+  const PrePartition *pre = nullptr;  // this chunk arrives partitioned (radix_join skips its passes)
   std::vector<TablePtr> tables;
 
   // room for m more rows; returns the row offset to write at
@@ -439,11 +451,14 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   const JoinType jt = cfg.GetType();
   const int oj = outer_mode(jt, build_left);
   const bool lnull = left_may_null(jt), rnull = right_may_null(jt);
+  const PrePartition *pre = sink ? sink->pre : nullptr;  // (tables: schema only, partitions in pre)
   // LDS capacity from the build side's staged row width (key column counted once)
   RadixCols shape = radix_cols(bt, nullptr, nullptr);
   for (int c = 0, q = 0; c < bt->Columns(); ++c, ++q) {
     const Column &col = bt->column(c);
-    if (col.type.width() == 8 && col.data.data_ptr() == (build_left ? lk : rk).data_ptr()) shape.in[q] = nullptr;
+    const bool is_key = pre ? (build_left ? pre->L : pre->R).is_key[(size_t)c]
+                            : col.type.width() == 8 && col.data.data_ptr() == (build_left ? lk : rk).data_ptr();
+    if (is_key) shape.in[q] = nullptr;
     if (col.nullable() && !packs_validity(bt)) ++q;  // packed validity words sit after the columns
   }
   // Narrowed keys (kernel_decls.inc NarrowKeys): when each side's join key is its own int64 column,
@@ -459,11 +474,11 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     return hits == 1;
   };
   // (a hashed key -- the invertible string word key a proxy carries as a column -- never fits 32 bits)
-  bool narrow = !hashed_key && nl > 0 && nr > 0 && lk.scalar_type() == at::kLong && rk.scalar_type() == at::kLong &&
-                own_key_column(left, lk) && own_key_column(right, rk);
+  bool narrow = pre != nullptr || (!hashed_key && nl > 0 && nr > 0 && lk.scalar_type() == at::kLong &&
+                                   rk.scalar_type() == at::kLong && own_key_column(left, lk) && own_key_column(right, rk));
   at::Tensor narrow_bad = narrow ? at::zeros({1}, ex.opts(at::kInt)) : at::Tensor();
   // the narrowing base's source (left key 0), its own copy: a released input's key column goes away
-  const at::Tensor base_src = narrow ? lk.slice(0, 0, 1).clone() : at::Tensor();
+  const at::Tensor base_src = pre ? pre->base_src : narrow ? lk.slice(0, 0, 1).clone() : at::Tensor();
   hip::NarrowKeys nk;
   if (narrow) {
     nk.base_src = ptr<int64_t>(base_src);
@@ -480,7 +495,8 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   while (bits < 24 && !fits((nb + (int64_t(1) << bits) - 1) >> bits)) ++bits;
   if (const int64_t xb = knobs::Int("RJ_EXTRA_BITS", 0))  // test knob: finer partitions
     bits = std::min(bits + (int)std::max<int64_t>(0, xb), 2 * 10);
-  if (narrow && bits == 0) {  // one partition: no pass runs, so nothing would narrow the keys
+  if (pre) bits = pre->bits;
+  if (narrow && bits == 0 && !pre) {  // one partition: no pass runs, so nothing would narrow the keys
     narrow = false;
     nk = hip::NarrowKeys();
     cap = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size(), (oj & 2) != 0, 8);
@@ -509,7 +525,7 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     }
     return hits == 1 ? idx : -1;
   };
-  const int kl = key_col(left, lk), kr = key_col(right, rk);
+  const int kl = pre ? -1 : key_col(left, lk), kr = pre ? -1 : key_col(right, rk);
   // retain = false (reference table.cpp:150-154): an input is released as soon as nothing can need
   // it again -- its own passes fit their slots and no key of either side leaves the narrowed range
   // (else it would be repartitioned from the input) -- so its buffers are free before the other
@@ -528,15 +544,45 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     key = at::Tensor();
     trace::add_counter("join.radix.released_inputs", 1);
   };
+  // Skewed partitions are handled per partition, not per join: a partition whose build side exceeds
+  // the LDS capacity or whose probe side is hot (> 2 probe chunks) is skipped by the partition loop
+  // and covered by split work items (kernel_decls.inc RJSplit): build chunks of <= cap rows x probe
+  // chunks of pch rows, so a hot key costs its own rows, never the whole join (reference: one
+  // unordered_multimap, join/hash_join.cpp:255-298).
+  const int64_t np_rows = build_left ? nr : nl;
+  const int64_t pch = std::max<int64_t>(int64_t(1) << 15, 8 * ((np_rows + nparts - 1) / nparts));
+  const int64_t bmean = ((build_left ? nl : nr) + nparts - 1) / nparts;
+  struct SkewMasks {
+    at::Tensor bcnt, pcnt, heavy, mid, sums;  // sums: [heavy partitions, mid partitions] (device)
+    int64_t cap = 0;
+  };
+  auto skew_masks = [&](const RadixSide &Bs, const RadixSide &Ps, int64_t cp) {
+    SkewMasks k;
+    k.cap = cp;
+    const int64_t split_rows = std::max<int64_t>(8, std::min<int64_t>(cp, knobs::Int("RJ_SPLIT_ROWS", cp)));
+    k.bcnt = part_counts(Bs, nparts);
+    k.pcnt = part_counts(Ps, nparts);
+    k.heavy = at::logical_or(k.bcnt > split_rows, k.pcnt > 2 * pch);
+    // hot-ish partitions (far above the mean, not split) are counted exactly instead of sampled: a
+    // sample that misses them under-estimates the output and costs a second write (skip = 2)
+    k.mid = at::logical_and(k.heavy.logical_not(),
+                            at::logical_or(k.pcnt > 4 * (np_rows + nparts - 1) / nparts + 1024, k.bcnt > 4 * bmean + 1024));
+    k.sums = at::stack({k.heavy.sum(), k.mid.sum()});
+    return k;
+  };
+  SkewMasks sk;  // computed with the partition flags' read when no side is repartitioned
   RadixSide L, R;
-  {
+  if (pre) {
+    L = pre->L;
+    R = pre->R;
+  } else {
     CYLON_PHASE("join.radix.partition", ex.device);
     const hip::NarrowKeys *nkp = narrow ? &nk : nullptr;
     // A side with a hot partition would overflow a slot and repartition exactly after both slot
     // passes (1B x 1B with 16 build keys x 200k duplicates: +48 ms): a histogram of ~1M sampled keys
     // (every stride-th) finds a partition far above the mean first, and that side starts exact.
     int64_t sl = slot_of(nl), sr = slot_of(nr);
-    if ((sl || sr) && std::max(nl, nr) >= (int64_t(1) << 24)) {
+    if ((sl || sr) && std::max(nl, nr) >= (int64_t(1) << 24) && (!sink || sink->sample_skew)) {
       auto sample = [&](const at::Tensor &k, int64_t rows, at::Tensor &h, int64_t &stride) {
         stride = std::max<int64_t>(1, rows >> 20);
         h = at::empty({nparts}, ex.opts(at::kInt));
@@ -577,26 +623,35 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     }
     if (L.slot || R.slot || narrow) {  // a side whose partition outgrew a slot is partitioned exactly
       at::Tensor z = at::zeros({}, ex.opts(at::kInt));
-      at::Tensor f = at::stack({L.slot ? L.overflow[0] : z, R.slot ? R.overflow[0] : z,
-                                narrow ? narrow_bad[0] : z}).cpu();
-      if (f[2].item<int>()) {  // a key outside the uint32 offset range: both sides as int64 keys
+      // the skew masks of the partitions as they stand ride in the same copy (used when no side is
+      // repartitioned below: one host sync instead of two)
+      sk = skew_masks(build_left ? L : R, build_left ? R : L, cap);
+      at::Tensor f = at::cat({at::stack({L.slot ? L.overflow[0] : z, R.slot ? R.overflow[0] : z,
+                                         narrow ? narrow_bad[0] : z}).to(at::kLong),
+                              sk.sums}).cpu();
+      bool redo = f[2].item<int64_t>() != 0;
+      if (redo) {  // a key outside the uint32 offset range: both sides as int64 keys
         trace::add_counter("join.radix.narrow_fallback", 1);
         narrow = false;  // (8-byte keys: the smaller LDS capacity; fuller partitions become split items)
         cap = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size(), (oj & 2) != 0, 8);
         L = radix_partition(ex, left, lk, bits, nullptr, slot_of(nl));
         R = radix_partition(ex, right, rk, bits, nullptr, slot_of(nr));
         if (L.slot || R.slot)
-          f = at::stack({L.slot ? L.overflow[0] : z, R.slot ? R.overflow[0] : z, z}).cpu();
+          f = at::stack({L.slot ? L.overflow[0] : z, R.slot ? R.overflow[0] : z, z}).to(at::kLong).cpu();
       }
       nkp = narrow ? &nk : nullptr;
-      if (f[0].item<int>()) {
+      if (f[0].item<int64_t>()) {
         trace::add_counter("join.radix.slot_overflow", 1);
         L = radix_partition(ex, left, lk, bits, nullptr, 0, nkp);
+        redo = true;
       }
-      if (f[1].item<int>()) {
+      if (f[1].item<int64_t>()) {
         trace::add_counter("join.radix.slot_overflow", 1);
         R = radix_partition(ex, right, rk, bits, nullptr, 0, nkp);
+        redo = true;
       }
+      if (redo) sk = SkewMasks();
+      else sk.sums = f.slice(0, 3, 5);  // (host copy of the sums)
       trace::add_counter("join.radix.slot_sides", (L.slot ? 1 : 0) + (R.slot ? 1 : 0));
       if (narrow) trace::add_counter("join.radix.narrow_keys", 1);
     }
@@ -618,23 +673,11 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   const bool share_key = oj == 0 && !sink && kl >= 0 && kr >= 0 && left->column(kl).type == right->column(kr).type &&
                          knobs::Flag("RJ_SHARE_KEY", true);
   const int bkc = build_left ? kl : kr;  // the build side's key column (not written when shared)
-  // Skewed partitions are handled per partition, not per join: a partition whose build side exceeds
-  // the LDS capacity or whose probe side is hot (> 2 probe chunks) is skipped by the partition loop
-  // and covered by split work items (kernel_decls.inc RJSplit): build chunks of <= cap rows x probe
-  // chunks of pch rows, so a hot key costs its own rows, never the whole join (reference: one
-  // unordered_multimap, join/hash_join.cpp:255-298).
-  const int64_t np_rows = build_left ? nr : nl;
-  const int64_t pch = std::max<int64_t>(int64_t(1) << 15, 8 * ((np_rows + nparts - 1) / nparts));
   const int64_t split_rows = std::max<int64_t>(8, std::min<int64_t>(cap, knobs::Int("RJ_SPLIT_ROWS", cap)));
-  at::Tensor bcnt = part_counts(B, nparts), pcnt = part_counts(P, nparts);
-  at::Tensor heavy = at::logical_or(bcnt > split_rows, pcnt > 2 * pch);
-  // hot-ish partitions (far above the mean, not split) are counted exactly instead of sampled: a
-  // sample that misses them under-estimates the output and costs a second write (skip = 2)
-  const int64_t bmean = ((build_left ? nl : nr) + nparts - 1) / nparts;
-  at::Tensor mid = at::logical_and(heavy.logical_not(),
-                                   at::logical_or(pcnt > 4 * (np_rows + nparts - 1) / nparts + 1024, bcnt > 4 * bmean + 1024));
+  if (!sk.heavy.defined() || sk.cap != cap) sk = skew_masks(B, P, cap);
+  const at::Tensor &bcnt = sk.bcnt, &pcnt = sk.pcnt, &heavy = sk.heavy, &mid = sk.mid;
   at::Tensor skip = heavy.to(at::kByte), skip_sample = at::logical_or(heavy, mid).to(at::kByte);
-  at::Tensor hm = at::stack({heavy.sum(), mid.sum()}).cpu();
+  const at::Tensor hm = sk.sums.is_cuda() ? sk.sums.cpu() : sk.sums;
   const int64_t nheavy = hm[0].item<int64_t>(), nmid = hm[1].item<int64_t>();
   std::vector<int64_t> items, emits;  // kRJItemWords per item
   int64_t emit_bound = 0;
@@ -742,17 +785,22 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
                             B.slot, &skip_only, nbase);
     };
     count(stride);
-    // the ranking guard of the stable (second and later) partition passes
-    if (hip::rp_take_order_violation(ex.stream)) {
+    // the ranking guard of the stable (second and later) partition passes: its device flag travels
+    // in the same copy as the count results (one host sync instead of two)
+    const at::Tensor oflag = at::from_blob(hip::rp_order_flag(), {1}, ex.opts(at::kInt)).to(at::kLong);
+    auto order_violation = [&](int64_t flag) {
+      if (!flag) return false;
+      hip::rp_note_order_violation(ex.stream);
       trace::add_counter("join.radix.order_violation_fallback", 1);
-      return fail("order violation");
-    }
+      return true;
+    };
     int64_t ssum = 0, sover = 0;  // the sample's total and overflow flag (one read for both uses)
     if (stride > 1) {
       // Skew check of the sample: extrapolating a hot key's partition 32x would over-allocate
       // (ADVICE r03), so a sample whose largest partition output is far above its mean is
       // counted exactly instead.
-      at::Tensor st = at::stack({counts.sum(), counts.max(), overflow.to(at::kLong)[0]}).cpu();
+      at::Tensor st = at::stack({counts.sum(), counts.max(), overflow.to(at::kLong)[0], oflag[0]}).cpu();
+      if (order_violation(st[3].item<int64_t>())) return fail("order violation");
       ssum = st[0].item<int64_t>();
       sover = st[2].item<int64_t>();
       const int64_t smax = st[1].item<int64_t>();
@@ -765,7 +813,8 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
     }
     if (stride == 1) {
       out_offs = exclusive_scan(ex, counts);
-      at::Tensor tail = at::cat({out_offs.slice(0, nparts, nparts + 1), overflow.to(at::kLong)}).cpu();
+      at::Tensor tail = at::cat({out_offs.slice(0, nparts, nparts + 1), overflow.to(at::kLong), oflag}).cpu();
+      if (order_violation(tail[2].item<int64_t>())) return fail("order violation");
       m = tail[0].item<int64_t>();
       if (tail[1].item<int64_t>() != 0) {
         trace::add_counter("join.radix.overflow_fallback", 1);
@@ -1433,6 +1482,240 @@ static int radix_join_chunks(const Exec &ex, const TablePtr &l, const TablePtr &
   return std::max(C, 2);
 }
 
+// Bounded memory with retain = false and an int64 key column per side: the chunk pass IS the join's
+// first radix pass -- every column moved once by the HIGH db1 bits of the narrowed partition hash
+// (exact, so each first-level bucket is a contiguous row range; column groups with stable passes as
+// in the chunk-major path, releasing each group's input buffers) -- and chunk c is a range of
+// consecutive first-level buckets.  Per chunk only the slot second pass runs (radix_slot_segment_pass
+// over its buckets) and radix_join joins the prepartitioned chunk into the sink (JoinSink::pre):
+// the rows cross HBM in two passes, as in the unbounded join, instead of three (chunk-major pass +
+// the chunk's own two passes).  nullptr when not applicable (the caller takes the chunk-major path).
+static TablePtr radix_join_first_pass_chunks(const Exec &ex, const TablePtr &l, const TablePtr &r, const at::Tensor &lk,
+                                             const at::Tensor &rk, int lkc, int rkc, const JoinConfig &cfg, int C,
+                                             bool hashed_key) {
+  if (l->IsRetain() || r->IsRetain() || hashed_key || lkc < 0 || rkc < 0 || lk.scalar_type() != at::kLong ||
+      rk.scalar_type() != at::kLong || !knobs::Flag("RJ_FIRST_PASS_CHUNKS", true))
+    return nullptr;
+  // (nullable columns take the chunk-major path: radix_join sizes the LDS rows for packed validity
+  // words, which these partitions do not carry)
+  for (const TablePtr &t : {l, r})
+    for (const auto &c : t->columns())
+      if (c.is_var() || c.type.width() > 8 || c.nullable()) return nullptr;
+  const int64_t nl = l->Rows(), nr = r->Rows();
+  if (nl < (int64_t(1) << 20) || nr < (int64_t(1) << 20)) return nullptr;
+  // the narrowed-key range, checked before anything is released: [base, base + 2^32), base = (left
+  // key 0) - 2^31, as in radix_join
+  const at::Tensor base_src = lk.slice(0, 0, 1).clone();
+  {
+    auto ml = at::aminmax(lk), mr = at::aminmax(rk);
+    const at::Tensor h = at::stack({std::get<0>(ml), std::get<1>(ml), std::get<0>(mr), std::get<1>(mr), base_src[0]}).cpu();
+    const int64_t base = h[4].item<int64_t>() - (int64_t(1) << 31);
+    for (int i = 0; i < 4; ++i) {
+      const int64_t v = h[i].item<int64_t>();
+      if (v < base || (uint64_t)(v - base) > 0xffffffffull) return nullptr;
+    }
+  }
+  // partition bits as radix_join chooses them for the whole join (narrowed keys)
+  const bool build_left = nl < nr;
+  const TablePtr &bt = build_left ? l : r;
+  const int bkc = build_left ? lkc : rkc;
+  const int oj = outer_mode(cfg.GetType(), build_left);
+  RadixCols shape = radix_cols(bt, nullptr, nullptr);
+  for (int c = 0, q = 0; c < bt->Columns(); ++c, ++q) {
+    if (c == bkc) shape.in[q] = nullptr;
+    if (bt->column(c).nullable() && !packs_validity(bt)) ++q;
+  }
+  const int64_t cap = hip::radix_join_capacity(shape.w.data(), shape.in.data(), (int)shape.w.size(), (oj & 2) != 0, 4);
+  const int64_t nb = std::min(nl, nr);
+  auto fits = [&](int64_t mean) { return (double)mean + 8.0 * std::sqrt((double)mean) + 16.0 <= (double)cap; };
+  int bits = 0;
+  while (bits < 24 && !fits((nb + (int64_t(1) << bits) - 1) >> bits)) ++bits;
+  const int db2 = std::min(9, bits / 2), db1 = bits - db2;
+  if (bits < 11 || db1 > 10) return nullptr;
+  int cbits = 1;  // chunks: twice what the retained-input budget asks for, as the chunk-major path
+  while ((1 << cbits) < 2 * C) ++cbits;
+  cbits = std::min(cbits, db1);
+  const int gbits = db1 - cbits;  // first-level buckets per chunk: 2^gbits
+  if ((1 << gbits) > 4096) return nullptr;
+  at::Tensor narrow_bad = at::zeros({1}, ex.opts(at::kInt));
+  hip::NarrowKeys nk;
+  nk.base_src = ptr<int64_t>(base_src);
+  nk.bad = reinterpret_cast<unsigned int *>(narrow_bad.data_ptr<int>());
+  // ---- first pass of each side, column group by column group
+  struct First {
+    at::Tensor keys;                     // uint32 offsets, first-level bucket order
+    std::vector<at::Tensor> data, valid;  // per column (data of the key column: undefined)
+    std::vector<int64_t> boff;            // 2^db1 + 1 bucket starts
+    int64_t n = 0;
+  };
+  auto first_pass = [&](const TablePtr &t, const at::Tensor &k, int kc) {
+    First f;
+    f.n = t->Rows();
+    f.data.resize((size_t)t->Columns());
+    f.valid.resize((size_t)t->Columns());
+    std::vector<std::pair<int, bool>> ent;
+    for (int c = 0; c < t->Columns(); ++c) {
+      if (c != kc) ent.push_back({c, false});
+      if (t->column(c).nullable()) ent.push_back({c, true});
+    }
+    constexpr size_t kGroup = 3;
+    const size_t ngroups = std::max<size_t>(1, (ent.size() + kGroup - 1) / kGroup);
+    const bool stable = ngroups > 1;
+    f.keys = at::empty({f.n}, ex.opts(at::kInt));
+    at::Tensor ws = ex.empty_i64(hip::radix_rows_pass_workspace(f.n, db1));
+    for (size_t g = 0; g < ngroups; ++g) {
+      const size_t e0 = ent.size() * g / ngroups, e1 = ent.size() * (g + 1) / ngroups;
+      std::vector<const uint8_t *> in{reinterpret_cast<const uint8_t *>(k.data_ptr())};
+      std::vector<uint8_t *> out{reinterpret_cast<uint8_t *>(f.keys.data_ptr())};
+      std::vector<int> widths{8};
+      for (size_t e = e0; e < e1; ++e) {
+        const Column &col = t->column(ent[e].first);
+        const at::Tensor &src = ent[e].second ? col.validity : col.data;
+        at::Tensor dst = at::empty_like(src);
+        in.push_back(reinterpret_cast<const uint8_t *>(src.data_ptr()));
+        out.push_back(reinterpret_cast<uint8_t *>(dst.data_ptr()));
+        widths.push_back(ent[e].second ? 1 : col.type.width());
+        (ent[e].second ? f.valid : f.data)[(size_t)ent[e].first] = dst;
+      }
+      hip::radix_rows_pass(reinterpret_cast<const int64_t *>(k.data_ptr()), f.n, bits, db2, db1, in.data(), out.data(),
+                           widths.data(), (int)in.size(), ptr<int64_t>(ws), ex.stream, stable, nullptr, 0, &nk);
+      if (stable)
+        for (size_t e = e0; e < e1; ++e) t->ReleaseBufferIfNotRetained(ent[e].first, ent[e].second);
+    }
+    at::Tensor offs = ex.empty_i64((int64_t(1) << db1) + 1);
+    hip::radix_part_offsets32(reinterpret_cast<const uint32_t *>(f.keys.data_ptr()), f.n, db1, ptr<int64_t>(offs),
+                              ex.stream);
+    f.boff = to_host_vec(offs);
+    return f;
+  };
+  First fl = first_pass(l, lk, lkc);
+  l->ReleaseIfNotRetained();
+  First fr = first_pass(r, rk, rkc);
+  r->ReleaseIfNotRetained();
+  trace::add_counter("join.radix.released_inputs", 2);
+  trace::add_counter("join.radix.first_pass_chunks", int64_t(1) << cbits);
+  CYLON_CHECK(narrow_bad.item<int>() == 0, Code::ExecutionError, "first-pass chunks: a key left the narrowed range");
+  // schema tables of a chunk (names, types, nullability; the data lives in the partitions)
+  auto schema = [&](const TablePtr &t, int64_t rows) {
+    std::vector<Column> cols;
+    for (const auto &c : t->columns())
+      cols.emplace_back(c.name, c.type, rows, at::empty({0}, c.data.options()), at::Tensor(),
+                        c.nullable() ? at::empty({0}, ex.opts(at::kByte)) : at::Tensor());
+    return Table::Make(t->GetContext(), std::move(cols));
+  };
+  const int64_t nparts = int64_t(1) << bits;
+  auto slot_of = [&](int64_t rows) {
+    const double mean = (double)rows / (double)nparts;
+    return ((int64_t)(mean + 8.0 * std::sqrt(mean) + 64.0) + 7) & ~int64_t(7);
+  };
+  // second pass of one side's chunk [b0, b1) of first-level buckets -> its RadixSide
+  auto second_pass = [&](const TablePtr &t, const First &f, int kc, int64_t b0, int64_t b1, int64_t slot) {
+    const int64_t r0 = f.boff[(size_t)b0], r1 = f.boff[(size_t)b1], n = r1 - r0;
+    const int nseg = (int)(b1 - b0);
+    const int64_t nslots = int64_t(nseg) << db2;
+    RadixSide s;
+    std::vector<const uint8_t *> in{reinterpret_cast<const uint8_t *>(ptr<int32_t>(f.keys) + r0)};
+    std::vector<int> widths{4};
+    std::vector<std::pair<int, bool>> ent;
+    for (int c = 0; c < t->Columns(); ++c) {
+      if (c != kc) ent.push_back({c, false});
+      if (t->column(c).nullable()) ent.push_back({c, true});
+    }
+    for (const auto &e : ent) {
+      const at::Tensor &src = e.second ? f.valid[(size_t)e.first] : f.data[(size_t)e.first];
+      const int w = e.second ? 1 : t->column(e.first).type.width();
+      in.push_back(reinterpret_cast<const uint8_t *>(src.data_ptr()) + r0 * w);
+      widths.push_back(w);
+    }
+    s.data.assign((size_t)t->Columns(), at::Tensor());
+    s.valid.assign((size_t)t->Columns(), at::Tensor());
+    s.is_key.assign((size_t)t->Columns(), false);
+    s.vpos.assign((size_t)t->Columns(), -1);
+    if (n == 0) {  // (an empty chunk side: empty partitions)
+      s.keys = at::empty({0}, ex.opts(at::kInt));
+      s.offs = at::zeros({nslots}, ex.opts(at::kLong));
+      s.slot = 1;
+      s.overflow = at::zeros({1}, ex.opts(at::kInt));
+      for (int c = 0; c < t->Columns(); ++c) {
+        s.is_key[(size_t)c] = c == kc;
+        s.data[(size_t)c] = c == kc ? s.keys : at::empty({0}, t->column(c).data.options());
+        if (t->column(c).nullable()) s.valid[(size_t)c] = at::empty({0}, ex.opts(at::kByte));
+      }
+      return s;
+    }
+    const at::Tensor bb = (at::from_blob(const_cast<int64_t *>(f.boff.data()) + b0, {nseg}, at::TensorOptions().dtype(at::kLong)).clone() - r0)
+                              .to(at::kInt)
+                              .to(ex.device);
+    const int64_t rows = nslots * slot + hip::radix_slot_tile_rows();
+    std::vector<at::Tensor> fin;
+    std::vector<uint8_t *> out;
+    fin.push_back(at::empty({rows}, ex.opts(at::kInt)));
+    out.push_back(reinterpret_cast<uint8_t *>(fin.back().data_ptr()));
+    for (const auto &e : ent) {
+      const at::Tensor &src = e.second ? f.valid[(size_t)e.first] : f.data[(size_t)e.first];
+      fin.push_back(at::empty({rows}, src.options()));
+      out.push_back(reinterpret_cast<uint8_t *>(fin.back().data_ptr()));
+    }
+    int fbits = 0;
+    while ((1 << fbits) < nseg) ++fbits;
+    at::Tensor ws = ex.empty_i64(hip::radix_slot_workspace(std::max(1, fbits), db2));
+    s.offs = ex.empty_i64(nslots);
+    s.overflow = at::zeros({1}, ex.opts(at::kInt));
+    hip::NarrowKeys nk2 = nk;
+    nk2.kin4 = 1;
+    hip::radix_slot_segment_pass(reinterpret_cast<const uint32_t *>(ptr<int32_t>(f.keys) + r0), n, bits, db2, in.data(),
+                                 out.data(), widths.data(), (int)in.size(),
+                                 reinterpret_cast<const uint32_t *>(bb.data_ptr<int>()), nseg, slot, ptr<int64_t>(ws),
+                                 ptr<int64_t>(s.offs), reinterpret_cast<unsigned int *>(s.overflow.data_ptr<int>()),
+                                 ex.stream, &nk2);
+    s.slot = slot;
+    s.keys = fin[0];
+    for (int c = 0; c < t->Columns(); ++c) {
+      s.is_key[(size_t)c] = c == kc;
+      if (c == kc) s.data[(size_t)c] = s.keys;
+    }
+    for (size_t j = 0; j < ent.size(); ++j) (ent[j].second ? s.valid : s.data)[(size_t)ent[j].first] = fin[1 + j];
+    return s;
+  };
+  JoinSink sink;
+  sink.chunks_total = 1 << cbits;
+  sink.sample_skew = false;
+  const int64_t ls = slot_of(nl), rs = slot_of(nr);
+  for (int64_t c = 0; c < (int64_t(1) << cbits); ++c) {
+    const int64_t b0 = c << gbits, b1 = (c + 1) << gbits;
+    PrePartition pp;
+    pp.bits = gbits + db2;
+    pp.base_src = base_src;
+    int64_t lslot = ls, rslot = rs;
+    for (int attempt = 0;; ++attempt) {
+      pp.L = second_pass(l, fl, lkc, b0, b1, lslot);
+      pp.R = second_pass(r, fr, rkc, b0, b1, rslot);
+      const at::Tensor ov = at::cat({pp.L.overflow, pp.R.overflow}).cpu();
+      const bool lo = ov[0].item<int>() != 0, ro = ov[1].item<int>() != 0;
+      if (!lo && !ro) break;
+      // a partition beyond its slot (skewed keys): that side again with slots as large as the chunk's
+      // largest first-level bucket (which bounds every partition of the chunk)
+      CYLON_CHECK(attempt == 0, Code::ExecutionError, "first-pass chunks: slot overflow after resizing");
+      trace::add_counter("join.radix.slot_overflow", 1);
+      auto widest = [&](const First &f) {
+        int64_t m = 0;
+        for (int64_t b = b0; b < b1; ++b) m = std::max(m, f.boff[(size_t)b + 1] - f.boff[(size_t)b]);
+        return (m + 7) & ~int64_t(7);
+      };
+      if (lo) lslot = widest(fl);
+      if (ro) rslot = widest(fr);
+    }
+    sink.pre = &pp;
+    const TablePtr ls_t = schema(l, pp.L.keys.numel() ? fl.boff[(size_t)b1] - fl.boff[(size_t)b0] : 0);
+    const TablePtr rs_t = schema(r, pp.R.keys.numel() ? fr.boff[(size_t)b1] - fr.boff[(size_t)b0] : 0);
+    CYLON_CHECK(radix_join(ex, ls_t, rs_t, pp.L.keys, pp.R.keys, cfg, &sink), Code::ExecutionError,
+                "radix join of a first-pass chunk of released (retain = false) inputs did not complete");
+    sink.pre = nullptr;
+    ++sink.chunks_done;
+  }
+  return sink.finish(l->GetContext());
+}
+
 // the radix join in C key-hash chunks into one sink (see above); nullptr if a chunk's radix join fails
 static TablePtr radix_join_chunked(const Exec &ex, const TablePtr &l, const TablePtr &r, const at::Tensor &lk,
                                    const at::Tensor &rk, const JoinConfig &cfg, int C, bool hashed_key = false) {
@@ -1442,6 +1725,7 @@ static TablePtr radix_join_chunked(const Exec &ex, const TablePtr &l, const Tabl
     return -1;
   };
   const int lkc = key_col(l, lk), rkc = key_col(r, rk);
+  if (TablePtr t = radix_join_first_pass_chunks(ex, l, r, lk, rk, lkc, rkc, cfg, C, hashed_key)) return t;
   // retain = false on both inputs: one chunk-major pass per side (radix.cpp RadixChunkPartition: every
   // column, chunk = the LOW bits of fmix64(key)) whose input is released right after it, so each chunk
   // is a contiguous slice and the inputs are read once -- instead of a chunk-id filter + row gather
@@ -1450,38 +1734,51 @@ static TablePtr radix_join_chunked(const Exec &ex, const TablePtr &l, const Tabl
     int cbits = 1;  // (twice the chunks the retained-input budget asks for: the copies and the output
     while ((1 << cbits) < 2 * C) ++cbits;  // hold ~inputs + output, so each chunk's working set must be small)
     const int64_t C2 = int64_t(1) << cbits;
+    // Column groups: a pass moves the key plus <= kGroup other buffers, and the group's input buffers
+    // are released before the next group's pass, so the side's copy reuses its own input's memory
+    // (peak: the inputs + one group's copies, not the inputs + a whole second copy).  With several
+    // groups the passes rank stably (exact tile offsets, stable in-tile order): every group's rows
+    // land where the first group's did, the later passes rewriting the same keys in place.
+    constexpr size_t kGroup = 3;
     auto chunk_major = [&](const TablePtr &t, const at::Tensor &k, int kc, at::Tensor &kout, std::vector<int64_t> &offs) {
-      std::vector<at::Tensor> cur{k};
-      std::vector<int> widths{8}, dpos(t->Columns(), -1), vpos(t->Columns(), -1);
+      std::vector<std::pair<int, bool>> ent;  // (column, validity?) of every buffer that moves with the key
       for (int c = 0; c < t->Columns(); ++c) {
-        const Column &col = t->column(c);
-        if (c == kc) {
-          dpos[c] = 0;
-        } else {
-          dpos[c] = (int)cur.size();
-          cur.push_back(col.data);
-          widths.push_back(col.type.width());
+        if (c != kc) ent.push_back({c, false});
+        if (t->column(c).nullable()) ent.push_back({c, true});
+      }
+      const size_t ngroups = std::max<size_t>(1, (ent.size() + kGroup - 1) / kGroup);
+      const bool stable = ngroups > 1;
+      std::vector<at::Tensor> dout(t->Columns()), vout(t->Columns());
+      at::Tensor o;
+      for (size_t g = 0; g < ngroups; ++g) {
+        const size_t e0 = ent.size() * g / ngroups, e1 = ent.size() * (g + 1) / ngroups;
+        std::vector<at::Tensor> sub{k};
+        std::vector<int> widths{8};
+        for (size_t e = e0; e < e1; ++e) {
+          const Column &col = t->column(ent[e].first);
+          sub.push_back(ent[e].second ? col.validity : col.data);
+          widths.push_back(ent[e].second ? 1 : col.type.width());
         }
-        if (col.nullable()) {
-          vpos[c] = (int)cur.size();
-          cur.push_back(col.validity);
-          widths.push_back(1);
+        std::vector<at::Tensor> res =
+            RadixChunkPartition(ex, std::move(sub), widths, cbits, g == 0 ? &o : nullptr, g == 0 ? nullptr : &kout, stable);
+        if (g == 0) kout = res[0];
+        for (size_t e = e0; e < e1; ++e) {
+          (ent[e].second ? vout : dout)[(size_t)ent[e].first] = res[1 + e - e0];
+          if (stable) t->ReleaseBufferIfNotRetained(ent[e].first, ent[e].second);
         }
       }
-      at::Tensor o;
-      std::vector<at::Tensor> out = RadixChunkPartition(ex, std::move(cur), widths, cbits, &o);
       offs = to_host_vec(o);
       std::vector<Column> cols;
       for (int c = 0; c < t->Columns(); ++c) {
         const Column &col = t->column(c);
-        at::Tensor d = out[dpos[c]];
+        at::Tensor d = c == kc ? kout : dout[(size_t)c];
         if (c == kc && d.scalar_type() != col.data.scalar_type()) d = d.view(col.data.scalar_type());
-        cols.emplace_back(col.name, col.type, t->Rows(), d, at::Tensor(), vpos[c] >= 0 ? out[vpos[c]] : at::Tensor());
+        cols.emplace_back(col.name, col.type, kout.numel(), d, at::Tensor(), vout[(size_t)c]);
       }
-      kout = out[0];
       TablePtr res = Table::Make(t->GetContext(), std::move(cols));
       t->ReleaseIfNotRetained();
       trace::add_counter("join.radix.released_inputs", 1);
+      if (stable) trace::add_counter("join.radix.chunk_pass_groups", (int64_t)ngroups);
       return res;
     };
     at::Tensor lkp, rkp;
@@ -1491,6 +1788,7 @@ static TablePtr radix_join_chunked(const Exec &ex, const TablePtr &l, const Tabl
     trace::add_counter("join.radix.chunk_pass", 2);
     JoinSink sink;
     sink.chunks_total = (int)C2;
+    sink.sample_skew = false;
     auto slice_tab = [&](const TablePtr &t, int64_t a, int64_t b) {
       std::vector<Column> cols;
       for (const auto &c : t->columns()) cols.push_back(c.slice(a, b - a));

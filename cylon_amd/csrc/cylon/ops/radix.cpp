@@ -189,10 +189,11 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
 }
 
 std::vector<at::Tensor> RadixChunkPartition(const Exec &ex, std::vector<at::Tensor> cur, const std::vector<int> &widths,
-                                            int cbits, at::Tensor *offs) {
+                                            int cbits, at::Tensor *offs, const at::Tensor *key_into, bool stable) {
   CYLON_CHECK(ex.gpu && !cur.empty() && cur.size() == widths.size() && widths[0] == 8, Code::Invalid,
               "RadixChunkPartition arguments");
   const int64_t n = cur[0].numel();
+  CYLON_CHECK(!key_into || key_into->numel() == n, Code::Invalid, "RadixChunkPartition: key output size");
   std::vector<int> pw = widths;
   const BytePacking bp = PackByteColumns(ex, cur, pw, n);
   CYLON_CHECK(cur.size() <= 16, Code::Invalid, "RadixChunkPartition: " << cur.size() << " columns in one pass");
@@ -200,14 +201,15 @@ std::vector<at::Tensor> RadixChunkPartition(const Exec &ex, std::vector<at::Tens
   std::vector<at::Tensor> nxt;
   std::vector<const uint8_t *> in;
   std::vector<uint8_t *> out;
-  for (const auto &x : cur) {
-    nxt.push_back(at::empty_like(x));
-    in.push_back(reinterpret_cast<const uint8_t *>(x.data_ptr()));
+  for (size_t c = 0; c < cur.size(); ++c) {
+    nxt.push_back(c == 0 && key_into ? *key_into : at::empty_like(cur[c]));
+    in.push_back(reinterpret_cast<const uint8_t *>(cur[c].data_ptr()));
     out.push_back(reinterpret_cast<uint8_t *>(nxt.back().data_ptr()));
   }
-  *offs = ex.empty_i64((int64_t(1) << cbits) + 1);
+  if (offs) *offs = ex.empty_i64((int64_t(1) << cbits) + 1);
   hip::radix_chunk_pass(reinterpret_cast<const int64_t *>(cur[0].data_ptr()), n, cbits, in.data(), out.data(),
-                        pw.data(), (int)cur.size(), ptr<int64_t>(ws), ptr<int64_t>(*offs), ex.stream);
+                        pw.data(), (int)cur.size(), ptr<int64_t>(ws), offs ? ptr<int64_t>(*offs) : nullptr, ex.stream,
+                        stable);
   cur.clear();
   return UnpackByteColumns(ex, bp, std::move(nxt), n);
 }

@@ -79,8 +79,12 @@ std::vector<at::Tensor> RadixPartition(const Exec &ex, std::vector<at::Tensor> c
 // Chunk-major order of a table for the bounded-memory join: one exact pass of every column by the
 // LOW cbits bits of fmix64(column 0 = the int64 key) (independent of the join partition's top bits);
 // *offs (2^cbits + 1 rows) = each chunk's first row.  Validity bytes travel packed as for RadixPartition.
+// key_into: write column 0 into this existing array (a later column group of the same table: the
+// stable pass puts the keys exactly where the first group's pass did); offs may then be nullptr.
+// stable: every pass over the same keys produces the same row order (column groups).
 std::vector<at::Tensor> RadixChunkPartition(const Exec &ex, std::vector<at::Tensor> cols, const std::vector<int> &widths,
-                                            int cbits, at::Tensor *offs);
+                                            int cbits, at::Tensor *offs, const at::Tensor *key_into = nullptr,
+                                            bool stable = false);
 
 // Hash-join partition in slot mode (MSD, two passes, no histogram before the second pass; see
 // kernel_decls.inc radix_slot_rows_pass): partition p holds (*counts)[p] rows at row p * slot.

@@ -54,6 +54,9 @@ class Table {
   // still runs.  The columns keep their name, type and nullability, with 0 rows (the table is
   // empty afterwards).  A no-op for retained tables.
   void ReleaseIfNotRetained();
+  // retain = false: drop one buffer of column c (its data, or its validity) while an operator that
+  // consumes the table column group by column group still runs; ReleaseIfNotRetained() finishes.
+  void ReleaseBufferIfNotRetained(int c, bool validity);
 
   // total bytes of all buffers
   int64_t nbytes() const;
