@@ -389,6 +389,42 @@ __device__ __forceinline__ void q_wave_bitonic(int64_t (&k)[S], uint64_t (&v)[S]
   }
 }
 
+// The single-group case of q_wave_bitonic (every row of the bucket has the same key -- nearly every
+// bucket): values only, one 64-bit compare and two shuffles per element and stage instead of two
+// compares and four shuffles.
+template <int S>
+__device__ __forceinline__ void q_wave_bitonic_v(uint64_t (&v)[S]) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int kk = 2; kk <= 64 * S; kk <<= 1) {
+#pragma unroll
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {
+        const int js = j >> 6;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          if (s & js) continue;
+          const int t = s | js;
+          const bool asc = ((s * 64 + lane) & kk) == 0;
+          if ((v[t] < v[s]) == asc) {
+            const uint64_t tv = v[s];
+            v[s] = v[t];
+            v[t] = tv;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const uint64_t ov = (uint64_t)__shfl_xor((unsigned long long)v[s], j);
+          const bool asc = ((s * 64 + lane) & kk) == 0, lower = (lane & j) == 0;
+          const uint64_t lo = ov < v[s] ? ov : v[s], hi = ov < v[s] ? v[s] : ov;
+          v[s] = lower == asc ? lo : hi;
+        }
+      }
+    }
+  }
+}
+
 // Output of one group (a writer row): its slot comes from the partition's LDS counter, so the
 // groups of a partition come out in no fixed order (group-by order is unspecified).  FUSE: the
 // valid values' sum, count, min and max go to the four fz planes at the same slot.
@@ -432,10 +468,15 @@ __device__ __forceinline__ void q_rank_bucket(QKV *skv, int e0, int sz, double q
       kmax = r.k > kmax ? r.k : kmax;
     }
   }
+  int64_t kmin = INT64_MAX;
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    if (s * 64 + lane < sz) kmin = k[s] < kmin ? k[s] : kmin;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const int64_t x = __shfl_xor((long long)kmax, o);
+    const int64_t x = __shfl_xor((long long)kmax, o), y = __shfl_xor((long long)kmin, o);
     kmax = x > kmax ? x : kmax;
+    kmin = y < kmin ? y : kmin;
   }
 #pragma unroll
   for (int s = 0; s < S; ++s)
@@ -443,6 +484,40 @@ __device__ __forceinline__ void q_rank_bucket(QKV *skv, int e0, int sz, double q
       k[s] = kmax;
       v[s] = ~0ull;
     }
+  if (kmin == kmax) {  // one group: sort the values only; valid values first, nulls and pads after
+    q_wave_bitonic_v<S>(v);
+    int nv = 0;
+    double sum = 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const bool ok = v[s] != ~0ull;
+      nv += __popcll(__ballot(ok));
+      if constexpr (FUSE) sum += ok ? q_unimage(v[s]) : 0.0;
+    }
+    if constexpr (FUSE) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      if (s * 64 + lane < sz) skv[e0 + s * 64 + lane] = QKV{kmax, v[s]};
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {  // the group's row
+      if (nv == 0) {
+        q_emit<FUSE>(nout, okeys, oq, ovalid, fz, n, b, kmax, false, 0.0, 0.0, 0, 0.0, 0.0);
+      } else {
+        const double np = (double)nv * q, jf = floor(np);
+        const bool whole = np == jf;
+        int pos = (int)jf;
+        if (pos >= nv) pos = nv - 1;
+        const double at = q_unimage(skv[e0 + pos].v);
+        const double qv = (whole && pos > 0) ? 0.5 * (q_unimage(skv[e0 + pos - 1].v) + at) : at;
+        q_emit<FUSE>(nout, okeys, oq, ovalid, fz, n, b, kmax, true, qv, sum, nv, q_unimage(skv[e0].v),
+                     q_unimage(skv[e0 + nv - 1].v));
+      }
+    }
+    return;
+  }
   q_wave_bitonic<S>(k, v);
   bool head[S], last_valid[S];
   int start[S];

@@ -1530,6 +1530,8 @@ static TablePtr radix_join_first_pass_chunks(const Exec &ex, const TablePtr &l, 
   auto fits = [&](int64_t mean) { return (double)mean + 8.0 * std::sqrt((double)mean) + 16.0 <= (double)cap; };
   int bits = 0;
   while (bits < 24 && !fits((nb + (int64_t(1) << bits) - 1) >> bits)) ++bits;
+  if (const int64_t xb = knobs::Int("RJ_EXTRA_BITS", 0))  // test knob: finer partitions (as radix_join)
+    bits = std::min(bits + (int)std::max<int64_t>(0, xb), 2 * 10);
   const int db2 = std::min(9, bits / 2), db1 = bits - db2;
   if (bits < 11 || db1 > 10) return nullptr;
   int cbits = 1;  // chunks: twice what the retained-input budget asks for, as the chunk-major path

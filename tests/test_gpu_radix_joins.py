@@ -598,6 +598,7 @@ def test_radix_join_memory_bounded_first_pass_chunks(gpu_ctx, ctx, monkeypatch, 
     gpu_ctx.add_config("memory_budget_mb", "260")
     monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", "1024")
     monkeypatch.setenv("CYLON_RJ_FIRST_PASS_CHUNKS", "1" if first_pass else "0")
+    monkeypatch.setenv("CYLON_RJ_EXTRA_BITS", "2")  # 12 partition bits: two levels at 3M rows
     kw = dict(left_on=["k"], right_on=["k"], left_prefix="l_", right_prefix="r_")
     try:
         L, R = Table(a, gpu_ctx), Table(b, gpu_ctx)

@@ -1,0 +1,13 @@
+# round 6: bounded-memory join whose chunks are ranges of the join's own first radix pass
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${RUN:-r06o}
+mkdir -p $O
+. tools/gpu/lib.sh
+step newtests 900 python -u -m pytest tests/test_gpu_radix_joins.py -x -q --timeout 300 --timeout-method thread -k "memory_bounded or retain"
+step bounded6 900 python tools/retain_probe.py --rows 1000000000 --payload-cols 6 --steps 3 --warmup 3 --retain 0
+step bounded6_old 900 env CYLON_RJ_FIRST_PASS_CHUNKS=0 python tools/retain_probe.py --rows 1000000000 --payload-cols 6 --steps 3 --warmup 3 --retain 0
+tail -3 $O/newtests.out
+grep -h summary $O/bounded6.out $O/bounded6_old.out | cut -c1-400
+grep -h '"step": 5' $O/bounded6.out | cut -c1-900
