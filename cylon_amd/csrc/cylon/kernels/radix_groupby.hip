@@ -341,6 +341,27 @@ struct alignas(16) QKV {  // one row of a partition in LDS: group key, value ima
   uint64_t v;
 };
 
+// lane ^ j exchange of a 64-bit value: ds_swizzle (bit mode, xor mask j within 32-lane halves; no
+// address VGPR) for j <= 16, ds_bpermute (__shfl_xor) across the halves for j = 32.  j is a constant
+// after the bitonic loops unroll.
+template <int J>
+__device__ __forceinline__ uint32_t q_swz(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (J << 10) | 0x1F);
+}
+__device__ __forceinline__ uint64_t q_xor64(uint64_t v, int j) {
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  uint32_t a, b;
+  switch (j) {
+    case 1: a = q_swz<1>(lo); b = q_swz<1>(hi); break;
+    case 2: a = q_swz<2>(lo); b = q_swz<2>(hi); break;
+    case 4: a = q_swz<4>(lo); b = q_swz<4>(hi); break;
+    case 8: a = q_swz<8>(lo); b = q_swz<8>(hi); break;
+    case 16: a = q_swz<16>(lo); b = q_swz<16>(hi); break;
+    default: return (uint64_t)__shfl_xor((unsigned long long)v, j);
+  }
+  return (uint64_t)a | ((uint64_t)b << 32);
+}
+
 __device__ __forceinline__ bool q_less(int64_t ak, uint64_t av, int64_t bk, uint64_t bv) {
   return ak != bk ? ak < bk : av < bv;
 }
@@ -375,8 +396,8 @@ __device__ __forceinline__ void q_wave_bitonic(int64_t (&k)[S], uint64_t (&v)[S]
       } else {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-          const int64_t ok = __shfl_xor((long long)k[s], j);
-          const uint64_t ov = (uint64_t)__shfl_xor((unsigned long long)v[s], j);
+          const int64_t ok = (int64_t)q_xor64((uint64_t)k[s], j);
+          const uint64_t ov = q_xor64(v[s], j);
           const bool asc = ((s * 64 + lane) & kk) == 0, lower = (lane & j) == 0;
           const bool take = lower == asc ? q_less(ok, ov, k[s], v[s]) : q_less(k[s], v[s], ok, ov);
           if (take) {
@@ -415,7 +436,7 @@ __device__ __forceinline__ void q_wave_bitonic_v(uint64_t (&v)[S]) {
       } else {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-          const uint64_t ov = (uint64_t)__shfl_xor((unsigned long long)v[s], j);
+          const uint64_t ov = q_xor64(v[s], j);
           const bool asc = ((s * 64 + lane) & kk) == 0, lower = (lane & j) == 0;
           const uint64_t lo = ov < v[s] ? ov : v[s], hi = ov < v[s] ? v[s] : ov;
           v[s] = lower == asc ? lo : hi;
