@@ -576,7 +576,7 @@ __global__ void k_words_to_var(ConstWordPtrs in, const uint64_t *__restrict__ ha
 // two independent 64-bit hashes of rows of any length (the group-by's string key h and its check
 // h2): different seeds, and h2 mixes with a different multiplier and an add instead of a xor
 __global__ void k_var_hash2(const uint8_t *__restrict__ bytes, const int64_t *__restrict__ offs, int64_t n,
-                            uint64_t *__restrict__ h1, uint64_t *__restrict__ h2) {
+                            uint64_t *__restrict__ h1, uint64_t *__restrict__ h2, int pack_row) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const int64_t o = offs[i], L = offs[i + 1] - o;
@@ -596,13 +596,16 @@ __global__ void k_var_hash2(const uint8_t *__restrict__ bytes, const int64_t *__
       y = hashing::fmix64((y + v) * 0x87C37B91114253D5ULL) ^ 0x4CF5AD432745937FULL;
     }
     h1[i] = hashing::fmix64(x);
-    h2[i] = y;
+    h2[i] = pack_row ? (y & 0xFFFFFFFF00000000ull) | (uint64_t)i : y;
   }
 }
 
-void var_hash2(const uint8_t *bytes, const int64_t *offs, int64_t n, uint64_t *h1, uint64_t *h2, void *stream) {
+void var_hash2(const uint8_t *bytes, const int64_t *offs, int64_t n, uint64_t *h1, uint64_t *h2, void *stream,
+               bool pack_row) {
+  CYLON_CHECK(!pack_row || n <= (int64_t(1) << 32), Code::Invalid, "var_hash2: row numbers beyond 32 bits");
   if (n == 0) return;
-  hipLaunchKernelGGL(k_var_hash2, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), bytes, offs, n, h1, h2);
+  hipLaunchKernelGGL(k_var_hash2, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), bytes, offs, n, h1, h2,
+                     pack_row ? 1 : 0);
   HIP_LAUNCH_CHECK();
 }
 

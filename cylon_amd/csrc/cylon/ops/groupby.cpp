@@ -427,28 +427,30 @@ static TablePtr radix_groupby(const TablePtr &tin, const std::vector<int> &keys,
   // The output key bytes are rebuilt from h and the MIN words.
   //
   // Any other non-null string key (variable length, or words that would not fit the accumulator
-  // planes) groups by a 64-bit hash h of its bytes, with MIN and MAX of an independent 64-bit hash h2
-  // and MIN of the row number as accumulators: MIN(h2) == MAX(h2) in every group means all its rows
-  // agree on 128 hash bits (else: the exact path), and the output key is the bytes of each group's
-  // first row (one gather of ng rows).  Reference: hash_groupby.cpp:92-126 takes any key type.
+  // planes) groups by a 64-bit hash h of its bytes, with MIN and MAX of one packed column -- the high
+  // 32 bits of an independent hash h2 above the row number -- as accumulators: equal high halves of
+  // MIN and MAX in every group mean all its rows agree on 96 hash bits (else: the exact path), and
+  // the output key is the bytes of the row in MIN's low half (one gather of ng rows).  Reference:
+  // hash_groupby.cpp:92-126 takes any key type.
   TablePtr t = tin;
   GroupKey gkey;
   int wfirst = -1;  // column of word 1 in the augmented table
-  int hcol = -1, rcol = -1;  // hashed string key: columns of h2 and of the row number
+  int hcol = -1;  // hashed string key: column of (h2 high half << 32 | row)
   at::Tensor wk;
   if (keys.size() == 1 && tin->column(keys[0]).is_var()) {
     const Column &kc = tin->column(keys[0]);
     if (kc.nullable() || !(kc.type.type == Type::STRING || kc.type.type == Type::BINARY)) return nullptr;
     Exec ex0(tin->device());
-    if (hash_strings || fixed_string_len(ex0, kc) < 0) {
+    if ((hash_strings || fixed_string_len(ex0, kc) < 0) && n <= (int64_t(1) << 32)) {
+      // one column, (high 32 bits of h2) << 32 | row: MIN and MAX of it verify the group (equal high
+      // halves: every row agrees on 64 + 32 hash bits) and MIN's low half is a representative row --
+      // 8 B/row through the passes and one accumulator plane fewer than h2 + a row-number column
       at::Tensor h1 = ex0.empty_i64(n), h2 = ex0.empty_i64(n);
       hip::var_hash2(ptr<uint8_t>(kc.data), ptr<int64_t>(kc.offsets), n, reinterpret_cast<uint64_t *>(ptr<int64_t>(h1)),
-                     reinterpret_cast<uint64_t *>(ptr<int64_t>(h2)), ex0.stream);
+                     reinterpret_cast<uint64_t *>(ptr<int64_t>(h2)), ex0.stream, true);
       std::vector<Column> cols = tin->columns();
       hcol = (int)cols.size();
-      cols.emplace_back("__gh2", DataType(Type::INT64), n, h2);
-      rcol = (int)cols.size();
-      cols.emplace_back("__grow", DataType(Type::INT64), n, at::arange(n, ex0.opts(at::kLong)));
+      cols.emplace_back("__gh2row", DataType(Type::INT64), n, h2);
       t = Table::Make(tin->GetContext(), std::move(cols));
       gkey.hashed = true;
       gkey.cols = keys;
@@ -524,7 +526,7 @@ static TablePtr radix_groupby(const TablePtr &tin, const std::vector<int> &keys,
   if (gkey.hashed) {
     gkey.wmin.push_back(need(hcol, 2));
     gkey.wmax.push_back(need(hcol, 3));
-    gkey.rmin = need(rcol, 2);
+    gkey.rmin = gkey.wmin.back();  // (its low 32 bits: the row)
   }
   // the LDS aggregation kernels are instantiated with 1, 2, 3, 4 or 8 accumulator planes; a
   // fixed-length key whose MIN / MAX words do not fit beside the aggregates is hashed instead
@@ -618,11 +620,13 @@ static TablePtr radix_groupby(const TablePtr &tin, const std::vector<int> &keys,
   auto plane = [&](int j) { return gacc.slice(0, j * ng, (j + 1) * ng); };
   std::vector<Column> out;
   if (gkey.hashed) {
-    if (ng > 0 && plane(gkey.wmin[0]).ne(plane(gkey.wmax[0])).any().item<bool>()) {
+    const at::Tensor mn = minmax_col(ex, "", t->column(hcol), plane(gkey.wmin[0]).contiguous(), at::Tensor()).data;
+    const at::Tensor mx = minmax_col(ex, "", t->column(hcol), plane(gkey.wmax[0]).contiguous(), at::Tensor()).data;
+    if (ng > 0 && at::bitwise_right_shift(mn, 32).ne(at::bitwise_right_shift(mx, 32)).any().item<bool>()) {
       trace::add_counter("groupby.radix.string_hash_collision_fallback", 1);
       return nullptr;
     }
-    const at::Tensor rep = minmax_col(ex, "", t->column(rcol), plane(gkey.rmin).contiguous(), at::Tensor()).data;
+    const at::Tensor rep = at::bitwise_and(mn, 0xffffffffll);
     const Column &kc = t->column(keys[0]);
     out.push_back(Gather(Table::Make(t->GetContext(), {kc}), rep)->column(0));
     trace::add_counter("groupby.radix.hashed_string_key", 1);

@@ -18,6 +18,7 @@
 //   4. materialisation: one fused gather launch per side (K4).
 #include "cylon/knobs.hpp"
 #include <algorithm>
+#include <optional>
 #include <array>
 #include <cmath>
 #include <cstdlib>
@@ -1935,6 +1936,8 @@ static Column words_to_var(const Exec &ex, const std::string &name, const DataTy
 // (as in the one-key join), and composite_key_unpack rebuilds the key columns of the output.
 static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const TablePtr &right, const JoinConfig &cfg,
                                JoinSink *sink) {
+  std::optional<trace::Phase> keys_phase;
+  keys_phase.emplace("join.radix.keys", ex.device);  // key encoding + proxies (ends before the join)
   RadixKeys k = radix_keys(ex, left, right, cfg, sink == nullptr);  // (a sink takes no var-width keys)
   if (!k.ok) return nullptr;
   auto var_col = [](const Column &c) { return c.is_var() || c.type.kind() == ValueKind::FIXED_BYTES; };
@@ -2015,12 +2018,14 @@ static TablePtr radix_join_any(const Exec &ex, const TablePtr &left, const Table
     if (nw) trace::add_counter("join.radix.word_columns", nw);
   }
   if (!radix_eligible(lp) || !radix_eligible(rp)) return nullptr;
+  keys_phase.reset();
   const int mchunks = sink ? 1 : radix_join_chunks(ex, lp, rp, k.l, k.r, cfg.GetType());
   TablePtr out = mchunks > 1 ? radix_join_chunked(ex, lp, rp, k.l, k.r, cfg, mchunks, k.verify)
                              : radix_join(ex, lp, rp, std::move(k.l), std::move(k.r), cfg, sink, k.verify);
   if (!out) return nullptr;
   if (k.verify && !lvar && !rvar) return drop_false_matches(out, cfg, left->Columns());
   if (!lpx && !rpx) return out;
+  CYLON_PHASE("join.radix.rebuild", ex.device);  // word / proxy columns back to the output columns
   const JoinType jt = cfg.GetType();
   // Inner join on one fixed-length string key per side (same type and length, no nulls): the key
   // words are verified equal row by row below, so the right output key column is the left one's

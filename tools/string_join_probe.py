@@ -109,9 +109,10 @@ def main():
         out = run()
         torch.cuda.synchronize()
         cnt = {k: v for k, v in dict(C.trace_counters()).items() if k.startswith("join.")}
+        phases = {k: round(v[0], 3) for k, v in dict(C.trace_phases()).items()}
         C.trace_enable(False)
         rec = {"key": kind + (f" var[{vlo},{vhi}]" if var and kind == "string" else ""), "rows_per_side": n, "ms": round(statistics.median(ts), 3),
-               "all_ms": [round(x, 2) for x in ts], "out_rows": rows, "counters": cnt}
+               "all_ms": [round(x, 2) for x in ts], "out_rows": rows, "counters": cnt, "phases_ms": phases}
         if kind == "string":  # the key bytes of both sides are equal row by row (also checked by the join)
             lk, rk = out.native.columns()[0], out.native.columns()[4]
             rec["key_bytes_equal"] = bool(torch.equal(lk.data, rk.data) and torch.equal(lk.offsets, rk.offsets))
