@@ -1594,281 +1594,6 @@ bool radix_sort_lb_failed(const int64_t *ws, void *stream) {
   return h != 0;
 }
 
-// ---- pipelined slot pass (keep HBM busy through the ranking).  k_rows_pass<...,
-// SLOT> ranks a tile (digits, LDS atomics, the slot claims, a block scan, the sorted-slot table, the
-// destinations: ~13 % of a tile's cycles, profiles/r03/lds_dma_ab.txt) while no column moves.  Here
-// tile t+1 is ranked INSIDE tile t's column loop, one step per barrier phase the column loop has
-// anyway, so the ranking's LDS / ALU work and its global claim atomics run while tile t's loads and
-// stores are in flight:
-//   column c, phase A: column c of tile t goes into the stage in INPUT row order (linear, no bank
-//     conflicts);  ranking step: c = 0 zeroes the counters, c = 1 ranks t+1 (LDS atomics on the
-//     keys loaded in phase B of c = 0), c = 2 finishes the scan (slot bases, run offsets);
-//   column c, phase B: column c + 1 of tile t is loaded (c = 0: also tile t+1's keys), and sorted
-//     slot j of tile t stores stage[srow[j]] at dst[j] (a gather from the stage instead of the
-//     classic kernel's scatter into it);  ranking step: c = 1 claims t+1's runs in their output
-//     slots and scans the counts per wave, c = 2 writes t+1's sorted-slot rows and digits;
-//   after the loop: tile t+1's destinations (the only step without memory traffic in flight).
-// Sorted-slot rows are double buffered (srow[2]); the segment first rows / ends are read from global
-// memory by the one thread that takes tiles (LDS keeps the tile prefix only): 140 KB of LDS.  Same
-// registers as the classic kernel (dst of t, keys and ranks of t+1, one column in flight).  Needs
-// >= 3 columns (the three ranking steps ride on columns 0-2).
-template <class Digit, bool W8>
-__global__ __launch_bounds__(kRPThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_slot_pass_pipe(
-    Digit digit0, uint32_t nbuckets, ColSet cols, TileSched lb) {
-  constexpr int THREADS = kRPThreads, WAVES = THREADS / kWave, IT = kRPItems, TILE = THREADS * IT;
-  static_assert(TILE <= 65536, "sorted-slot rows are 16-bit");
-  Digit digit = digit0;
-  digit.init();
-  bool narrow_bad = false;
-  __shared__ uint64_t st[TILE];                  // column stage, input row order
-  __shared__ uint16_t srow[2][TILE];             // sorted slot -> input row (tile t, tile t+1)
-  __shared__ uint16_t sdg[TILE];                 // sorted slot -> digit (tile t+1)
-  __shared__ uint32_t bcnt[kRPMaxBuckets], toff[kRPMaxBuckets + 1], run[kRPMaxBuckets];
-  __shared__ uint32_t wsum[WAVES];
-  __shared__ uint32_t tp[kSlotMaxSeg];
-  __shared__ int64_t s_tend[3], s_tr0[3];
-  __shared__ int s_tb[3];
-  __shared__ int64_t s_tix, s_thi;
-  __shared__ int s_seg;  // thread 0: segment of the last tile taken (tiles are taken in increasing order)
-  constexpr int64_t kNone = INT64_MAX / 4;
-  // Taking a tile (thread 0) is split in two: take_issue finds the block's next tile and its segment
-  // g (LDS) and LOADS the segment's first / end rows (global: LDS holds the tile prefix only);
-  // take_finish writes the ring entry one barrier phase later, when the loads have long arrived --
-  // thread 0 never stalls its wave, and with it a barrier of the whole block, on those loads.
-  int64_t tk_t = -1, tk_ss = 0, tk_se = 0;
-  int tk_g = 0, tk_e = 0;
-  auto take_issue = [&](int e) {
-    tk_e = e;
-    tk_t = s_tix;
-    if (tk_t >= s_thi) {
-      tk_t = -1;
-      return;
-    }
-    s_tix = tk_t + ((int64_t)gridDim.x - (blockIdx.x & (kXcds - 1)) + kXcds - 1) / kXcds;
-    int g = s_seg;
-    while (g + 1 < lb.sl_nseg && (int64_t)tp[g + 1] <= tk_t) ++g;
-    s_seg = g;
-    tk_g = g;
-    tk_ss = (int64_t)lb.sl_ss[g];
-    tk_se = (int64_t)lb.sl_se[g];
-  };
-  auto take_finish = [&]() {
-    const int e = tk_e;
-    if (tk_t < 0) {
-      s_tr0[e] = kNone;
-      s_tend[e] = 0;
-      s_tb[e] = 0;
-      return;
-    }
-    const int64_t r0 = tk_ss + (tk_t - (int64_t)tp[tk_g]) * TILE;
-    s_tr0[e] = r0;
-    s_tend[e] = r0 + TILE < tk_se ? r0 + TILE : tk_se;
-    s_tb[e] = (tk_g >> lb.sl_gshift) * (int)nbuckets * lb.sl_B + (tk_g & lb.sl_gmask);
-  };
-  auto take = [&](int e) {
-    take_issue(e);
-    take_finish();
-  };
-  for (int i = threadIdx.x; i < lb.sl_nseg; i += THREADS) tp[i] = lb.sl_tpre[i];
-  if (threadIdx.x == 0) {
-    const int x = blockIdx.x & (kXcds - 1);
-    const int g0 = lb.sl_nseg * x / kXcds, g1 = lb.sl_nseg * (x + 1) / kXcds;
-    s_tix = (int64_t)lb.sl_tpre[g0] + blockIdx.x / kXcds;
-    s_thi = lb.sl_tpre[g1];
-    s_seg = g0;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    take(0);
-    take(1);
-  }
-  __syncthreads();
-  const int wave = threadIdx.x / kWave, lane = lane_id();
-  const int wrow = wave * kWave * IT;
-  using KVT = typename std::conditional<Digit::kNarrow, uint32_t, uint64_t>::type;
-  auto load_key = [&](int64_t i) -> KVT {
-    const uint64_t raw = digit.key_at(i);
-    if constexpr (Digit::kNarrow) {
-      narrow_bad |= digit.too_wide(raw);
-      return (KVT)digit.narrow(raw);
-    } else {
-      return (KVT)raw;
-    }
-  };
-  auto digit_of = [&](KVT k) -> uint32_t {
-    if constexpr (Digit::kNarrow) return digit.of_offset(k);
-    else return digit.of_key((int64_t)k);
-  };
-  KVT kv[IT];     // keys of the tile being ranked
-  uint32_t pl[IT];  // its digits | in-bucket rank << 16 (~0: no row)
-  uint32_t dst[IT];  // tile t: output row of sorted slot threadIdx.x + q * THREADS
-  uint64_t v[IT];    // the column in flight (tile t)
-  // ranking steps of the tile in ring entry e (rows [r0, r0 + cnt)) into srow[b]
-  uint32_t sl_c = 0, sl_base = 0, incl = 0;  // (threads < nbuckets) count, claimed base, inclusive wave scan
-  auto rank_zero = [&]() {
-    for (uint32_t p = threadIdx.x; p < nbuckets; p += THREADS) bcnt[p] = 0;
-  };
-  auto rank_atomics = [&](int cnt) {
-#pragma unroll
-    for (int k = 0; k < IT; ++k) {
-      const bool act = wrow + k * kWave + lane < cnt;
-      pl[k] = act ? digit_of(kv[k]) : 0xffffffffu;
-      if (act) pl[k] |= atomicAdd(&bcnt[pl[k]], 1u) << 16;
-    }
-  };
-  auto rank_claim_scan = [&](int e) {  // (after a barrier) claims + per-wave inclusive scan of the counts
-    sl_c = threadIdx.x < nbuckets ? bcnt[threadIdx.x] : 0u;
-    sl_base = 0;
-    if (sl_c) sl_base = atomicAdd(&lb.sl_cursor[(int64_t)s_tb[e] + (int64_t)threadIdx.x * lb.sl_B], sl_c);
-    incl = sl_c;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-      const uint32_t t = __shfl_up(incl, d, kWave);
-      if (lane >= d) incl += t;
-    }
-    if (lane == kWave - 1) wsum[wave] = incl;
-  };
-  auto rank_offsets = [&](int e) {  // (after a barrier) run offsets and slot bases
-    uint32_t off = 0;
-#pragma unroll
-    for (int w = 0; w < WAVES; ++w) off += (w < wave) ? wsum[w] : 0u;
-    if (threadIdx.x < nbuckets) {
-      toff[threadIdx.x] = off + incl - sl_c;
-      const bool fits = (int64_t)sl_base + sl_c <= lb.sl_slot;
-      if (sl_c && !fits) atomicOr(lb.sl_overflow, 1u);
-      run[threadIdx.x] = fits ? (uint32_t)(((int64_t)s_tb[e] + (int64_t)threadIdx.x * lb.sl_B) * lb.sl_slot + sl_base)
-                              : (uint32_t)(lb.sl_nslots * lb.sl_slot);  // the trash rows
-    }
-    if (threadIdx.x == THREADS - 1) toff[nbuckets] = off + incl;
-  };
-  auto rank_slots = [&](int b) {  // (after a barrier) sorted-slot rows and digits
-#pragma unroll
-    for (int k = 0; k < IT; ++k)
-      if (pl[k] != 0xffffffffu) {
-        const uint32_t p = pl[k] & 0xffffu, pos = toff[p] + (pl[k] >> 16);
-        srow[b][pos] = (uint16_t)(wrow + k * kWave + lane);
-        sdg[pos] = (uint16_t)p;
-      }
-  };
-  auto rank_dst = [&](int cnt) {  // (after a barrier) destinations of the sorted slots
-#pragma unroll
-    for (int q = 0; q < IT; ++q) {
-      const int j = threadIdx.x + q * THREADS;
-      if (j < cnt) {
-        const uint32_t p = sdg[j];
-        dst[q] = run[p] + (uint32_t)(j - (int)toff[p]);
-      }
-    }
-  };
-  // ---- prologue: tile 0 ranked alone
-  int cur = 0, buf = 0;
-  {
-    const int64_t r0 = s_tr0[0];
-    const int cnt = r0 < kNone ? (int)(s_tend[0] - r0) : 0;
-#pragma unroll
-    for (int k = 0; k < IT; ++k) {
-      const int64_t i = r0 + wrow + k * kWave + lane;
-      if (wrow + k * kWave + lane < cnt) kv[k] = load_key(i);
-    }
-    rank_zero();
-    __syncthreads();
-    rank_atomics(cnt);
-    __syncthreads();
-    rank_claim_scan(0);
-    __syncthreads();
-    rank_offsets(0);
-    __syncthreads();
-    rank_slots(0);
-    __syncthreads();
-    rank_dst(cnt);
-#pragma unroll
-    for (int k = 0; k < IT; ++k) v[k] = (uint64_t)kv[k];
-  }
-  bool first = true;
-  while (s_tr0[cur] < kNone) {
-    const int nx = cur == 2 ? 0 : cur + 1;
-    const int64_t tile = s_tr0[cur];
-    const int cnt = (int)(s_tend[cur] - tile);
-    // tile t+1's ring entry is complete only after phase A of column 0 (take_finish), except for
-    // tile 1, which the prologue took whole
-    bool more = first && s_tr0[nx] < kNone;
-    int64_t nr0 = 0;
-    int ncnt = 0;
-#pragma unroll 1
-    for (int c = 0; c < cols.n; ++c) {
-      const int w = cols.width[c];
-      const bool n4 = Digit::kNarrow && c == 0;  // column 0 as the uint32 offset
-      uint8_t *out = cols.out[c];
-      // phase A: column c of tile t into the stage, input row order
-      uint8_t *stb = reinterpret_cast<uint8_t *>(st);
-      if (n4) {
-#pragma unroll
-        for (int k = 0; k < IT; ++k)
-          if (wrow + k * kWave + lane < cnt) stw<false>(stb, wrow + k * kWave + lane, 4, v[k] & 0xffffffffull);
-      } else {
-#pragma unroll
-        for (int k = 0; k < IT; ++k)
-          if (wrow + k * kWave + lane < cnt) stw<W8>(stb, wrow + k * kWave + lane, w, v[k]);
-      }
-      if (c == 0) {
-        rank_zero();
-        if (!first && threadIdx.x == 0) take_finish();
-      } else if (more) {
-        if (c == 1) rank_atomics(ncnt);
-        else if (c == 2) rank_offsets(nx);
-      }
-      __syncthreads();
-      if (c == 0) {
-        more = s_tr0[nx] < kNone;
-        nr0 = s_tr0[nx];
-        ncnt = more ? (int)(s_tend[nx] - nr0) : 0;
-      }
-      // phase B: column c + 1 in flight (c = 0: also tile t+1's keys), tile t's sorted slots stored
-      if (c + 1 < cols.n) {
-        const uint8_t *in = cols.in[c + 1];
-        const int w1 = cols.width[c + 1];
-#pragma unroll
-        for (int k = 0; k < IT; ++k)
-          if (wrow + k * kWave + lane < cnt) v[k] = ldw<W8>(in, tile + wrow + k * kWave + lane, w1);
-      }
-      if (c == 0 && more) {
-#pragma unroll
-        for (int k = 0; k < IT; ++k)
-          if (wrow + k * kWave + lane < ncnt) kv[k] = load_key(nr0 + wrow + k * kWave + lane);
-      }
-      if (n4) {
-#pragma unroll
-        for (int q = 0; q < IT; ++q) {
-          const int j = threadIdx.x + q * THREADS;
-          if (j < cnt) stw<false>(out, (int64_t)dst[q], 4, ldw<false>(stb, srow[buf][j], 4));
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < IT; ++q) {
-          const int j = threadIdx.x + q * THREADS;
-          if (j < cnt) stw<W8>(out, (int64_t)dst[q], w, ldw<W8>(stb, srow[buf][j], w));
-        }
-      }
-      if (more) {
-        if (c == 1) rank_claim_scan(nx);
-        else if (c == 2) rank_slots(buf ^ 1);
-      }
-      __syncthreads();
-    }
-    // tile t+1: destinations; its keys are the next column 0; the tile after it is taken
-    if (more) {
-      rank_dst(ncnt);
-#pragma unroll
-      for (int k = 0; k < IT; ++k) v[k] = (uint64_t)kv[k];
-    }
-    if (threadIdx.x == 0) take_issue(nx == 2 ? 0 : nx + 1);  // (the entry of tile t-1, free now)
-    __syncthreads();
-    cur = nx;
-    buf ^= 1;
-    first = false;
-  }
-  if (Digit::kNarrow && narrow_bad) digit.report_bad();
-}
 
 // ---- slot mode (the histogram-free passes of a join partition; TileSched)
 // Segment list of a slot pass and the tile prefix over it (one block; S <= kSlotMaxSeg):
@@ -1998,25 +1723,9 @@ static void slot_pass(const Digit &dg, int64_t n, int digit_bits, const uint8_t 
   }
   // every XCD needs at least one block: its segments' tiles are dealt to its own blocks only
   const int64_t nblocks = std::max<int64_t>(kXcds, std::min<int64_t>((n + kRPTile - 1) / kRPTile + S, kNumCUs));
-  // join partitions of >= 3 columns: the pipelined pass (ranking under the column traffic) when
-  // CYLON_RJ_PIPE=1.  Off by default: same-box A/B at 1B x 1B, 85.25 / 85.55 ms pipelined vs 85.50 /
-  // 85.00 ms classic (profiles/r06/pipelined_pass_ab.txt) -- hiding the ranking gains nothing, so the
-  // pass is bound by its memory traffic (partial-line writes), not by the ranking's ALU / LDS phases
-  constexpr bool kPipeDigit = std::is_same<Digit, PartDigit>::value || std::is_same<Digit, PartDigitN>::value;
-  if constexpr (kPipeDigit) {
-    if (ncols >= 3 && key_xor == 0 && knobs::Flag("RJ_PIPE", false)) {
-      if (w8)
-        hipLaunchKernelGGL((k_slot_pass_pipe<Digit, true>), dim3((unsigned)nblocks), dim3(kRPThreads), 0, s, dg, nb, cs,
-                           lb);
-      else
-        hipLaunchKernelGGL((k_slot_pass_pipe<Digit, false>), dim3((unsigned)nblocks), dim3(kRPThreads), 0, s, dg, nb, cs,
-                           lb);
-      HIP_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_sl_counts, dim3(grid_for(nslots)), dim3(kBlock), 0, s, cursor, nslots, slot, counts);
-      HIP_LAUNCH_CHECK();
-      return;
-    }
-  }
+  // (a pipelined variant that ranked tile t+1 under tile t's column traffic measured no gain --
+  // 85.25 / 85.55 vs 85.50 / 85.00 ms at 1B x 1B, profiles/r06/pipelined_pass_ab.txt -- and was removed:
+  // the passes are bound by their partial-line write traffic, not by the ranking phases)
   if (w8)
     hipLaunchKernelGGL((k_rows_pass<Digit, true, 1024, kRankBlockAtomic, false, true>), dim3((unsigned)nblocks),
                        dim3(1024), 0, s, dg, digit_bits, nb, cs, n, (int64_t)kRPTile, nblocks, nullptr, lb);

@@ -31,7 +31,6 @@ const std::vector<KnobInfo> &Registry() {
       // test forcing of fallback paths that the defaults rarely take
       {"RJ_SLOT", "test", "0: join partitions by the exact LSD passes instead of slot mode"},
       {"RJ_FIRST_PASS_CHUNKS", "test", "0: bounded-memory joins of released int64-key inputs take the chunk-major pass instead of chunking the join's first radix pass"},
-      {"RJ_PIPE", "test", "1: join slot passes rank each tile under the previous tile's column traffic (pipelined kernel; no gain measured)"},
       {"RJ_EXACT_COUNT", "test", "1: the join counts every partition (no sampled output estimate)"},
       {"RJ_FUSED_MIN_PARTS", "test", "partitions from which the sampled output estimate is used (4096)"},
       {"RJ_ESTIMATE_SCALE", "test", "scales the sampled output estimate (< 1 forces the exact rerun)"},
