@@ -356,6 +356,9 @@ struct PrePartition {
   RadixSide L, R;
   int bits = 0;
   at::Tensor base_src;
+  // set by radix_join (nothing written) when a side's slot pass overflowed: the flags ride with
+  // radix_join's first host read instead of a read of their own
+  mutable bool overflowed = false, overflow_l = false, overflow_r = false;
 };
 
 // Output accumulator of a chunked (pipelined) distributed join.  The radix join
@@ -678,7 +681,18 @@ static TablePtr radix_join(const Exec &ex, const TablePtr &left, const TablePtr 
   if (!sk.heavy.defined() || sk.cap != cap) sk = skew_masks(B, P, cap);
   const at::Tensor &bcnt = sk.bcnt, &pcnt = sk.pcnt, &heavy = sk.heavy, &mid = sk.mid;
   at::Tensor skip = heavy.to(at::kByte), skip_sample = at::logical_or(heavy, mid).to(at::kByte);
-  const at::Tensor hm = sk.sums.is_cuda() ? sk.sums.cpu() : sk.sums;
+  at::Tensor hm;
+  if (pre) {  // the prepartitioned sides' slot overflow flags in the same copy
+    hm = at::cat({sk.sums.to(at::kLong), pre->L.overflow.to(at::kLong), pre->R.overflow.to(at::kLong)}).cpu();
+    pre->overflow_l = hm[2].item<int64_t>() != 0;
+    pre->overflow_r = hm[3].item<int64_t>() != 0;
+    if (pre->overflow_l || pre->overflow_r) {
+      pre->overflowed = true;
+      return nullptr;
+    }
+  } else {
+    hm = sk.sums.is_cuda() ? sk.sums.cpu() : sk.sums;
+  }
   const int64_t nheavy = hm[0].item<int64_t>(), nmid = hm[1].item<int64_t>();
   std::vector<int64_t> items, emits;  // kRJItemWords per item
   int64_t emit_bound = 0;
@@ -1549,6 +1563,7 @@ static TablePtr radix_join_first_pass_chunks(const Exec &ex, const TablePtr &l, 
     at::Tensor keys;                     // uint32 offsets, first-level bucket order
     std::vector<at::Tensor> data, valid;  // per column (data of the key column: undefined)
     std::vector<int64_t> boff;            // 2^db1 + 1 bucket starts
+    at::Tensor boff_dev;                  // the same on the device
     int64_t n = 0;
   };
   auto first_pass = [&](const TablePtr &t, const at::Tensor &k, int kc) {
@@ -1589,6 +1604,7 @@ static TablePtr radix_join_first_pass_chunks(const Exec &ex, const TablePtr &l, 
     hip::radix_part_offsets32(reinterpret_cast<const uint32_t *>(f.keys.data_ptr()), f.n, db1, ptr<int64_t>(offs),
                               ex.stream);
     f.boff = to_host_vec(offs);
+    f.boff_dev = offs;
     return f;
   };
   First fl = first_pass(l, lk, lkc);
@@ -1646,9 +1662,7 @@ static TablePtr radix_join_first_pass_chunks(const Exec &ex, const TablePtr &l, 
       }
       return s;
     }
-    const at::Tensor bb = (at::from_blob(const_cast<int64_t *>(f.boff.data()) + b0, {nseg}, at::TensorOptions().dtype(at::kLong)).clone() - r0)
-                              .to(at::kInt)
-                              .to(ex.device);
+    const at::Tensor bb = (f.boff_dev.slice(0, b0, b1) - r0).to(at::kInt);  // (device: no host copy per chunk)
     const int64_t rows = nslots * slot + hip::radix_slot_tile_rows();
     std::vector<at::Tensor> fin;
     std::vector<uint8_t *> out;
@@ -1690,30 +1704,30 @@ static TablePtr radix_join_first_pass_chunks(const Exec &ex, const TablePtr &l, 
     pp.bits = gbits + db2;
     pp.base_src = base_src;
     int64_t lslot = ls, rslot = rs;
+    const TablePtr ls_t = schema(l, fl.boff[(size_t)b1] - fl.boff[(size_t)b0]);
+    const TablePtr rs_t = schema(r, fr.boff[(size_t)b1] - fr.boff[(size_t)b0]);
     for (int attempt = 0;; ++attempt) {
       pp.L = second_pass(l, fl, lkc, b0, b1, lslot);
       pp.R = second_pass(r, fr, rkc, b0, b1, rslot);
-      const at::Tensor ov = at::cat({pp.L.overflow, pp.R.overflow}).cpu();
-      const bool lo = ov[0].item<int>() != 0, ro = ov[1].item<int>() != 0;
-      if (!lo && !ro) break;
-      // a partition beyond its slot (skewed keys): that side again with slots as large as the chunk's
-      // largest first-level bucket (which bounds every partition of the chunk)
-      CYLON_CHECK(attempt == 0, Code::ExecutionError, "first-pass chunks: slot overflow after resizing");
+      pp.overflowed = false;
+      sink.pre = &pp;
+      const bool done = radix_join(ex, ls_t, rs_t, pp.L.keys, pp.R.keys, cfg, &sink) != nullptr;
+      sink.pre = nullptr;
+      if (done) break;
+      CYLON_CHECK(pp.overflowed && attempt == 0, Code::ExecutionError,
+                  "radix join of a first-pass chunk of released (retain = false) inputs did not complete");
+      // a partition beyond its slot (skewed keys; radix_join saw the flags and wrote nothing): the
+      // overflowing side again with slots as large as the chunk's largest first-level bucket (which
+      // bounds every partition of the chunk)
       trace::add_counter("join.radix.slot_overflow", 1);
       auto widest = [&](const First &f) {
         int64_t m = 0;
         for (int64_t b = b0; b < b1; ++b) m = std::max(m, f.boff[(size_t)b + 1] - f.boff[(size_t)b]);
         return (m + 7) & ~int64_t(7);
       };
-      if (lo) lslot = widest(fl);
-      if (ro) rslot = widest(fr);
+      if (pp.overflow_l) lslot = std::max<int64_t>(lslot, widest(fl));
+      if (pp.overflow_r) rslot = std::max<int64_t>(rslot, widest(fr));
     }
-    sink.pre = &pp;
-    const TablePtr ls_t = schema(l, pp.L.keys.numel() ? fl.boff[(size_t)b1] - fl.boff[(size_t)b0] : 0);
-    const TablePtr rs_t = schema(r, pp.R.keys.numel() ? fr.boff[(size_t)b1] - fr.boff[(size_t)b0] : 0);
-    CYLON_CHECK(radix_join(ex, ls_t, rs_t, pp.L.keys, pp.R.keys, cfg, &sink), Code::ExecutionError,
-                "radix join of a first-pass chunk of released (retain = false) inputs did not complete");
-    sink.pre = nullptr;
     ++sink.chunks_done;
   }
   return sink.finish(l->GetContext());
@@ -1899,11 +1913,8 @@ static Column padded_to_var(const Exec &ex, const std::string &name, const DataT
     lens = wc[(size_t)W].data.slice(0, 0, m);
   }
   if (kc.nullable()) lens = at::where(kc.validity.slice(0, 0, m).to(at::kBool), lens, at::zeros({1}, lens.options()));
-  at::Tensor offs = at::zeros({m + 1}, ex.opts(at::kLong));
-  if (m) {
-    at::Tensor tail = offs.slice(0, 1, m + 1);
-    at::cumsum_out(tail, lens, 0);
-  }
+  // offsets = the device exclusive scan of the lengths (offs[m] = total): no zero fill + ATen cumsum
+  at::Tensor offs = m ? exclusive_scan(ex, lens.contiguous()) : at::zeros({1}, ex.opts(at::kLong));
   const int64_t nbytes = m ? read_i64(offs, m) : 0;
   at::Tensor bytes = ex.empty_bytes(std::max<int64_t>(1, nbytes));
   std::vector<const int64_t *> wp;

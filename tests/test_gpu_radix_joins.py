@@ -583,18 +583,24 @@ def test_radix_join_memory_bounded_chunks(gpu_ctx, ctx, monkeypatch, how, retain
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
 
 
-@pytest.mark.parametrize("how", ["inner", "left", "outer"])
-@pytest.mark.parametrize("first_pass", [True, False])
-def test_radix_join_memory_bounded_first_pass_chunks(gpu_ctx, ctx, monkeypatch, how, first_pass):
+@pytest.mark.parametrize("how,first_pass,skew", [("inner", True, False), ("left", True, False), ("outer", True, False),
+                                                  ("inner", False, False), ("left", False, False), ("outer", False, False),
+                                                  ("inner", True, True), ("outer", True, True)])
+def test_radix_join_memory_bounded_first_pass_chunks(gpu_ctx, ctx, monkeypatch, how, first_pass, skew):
     """Bounded memory, retain = false, non-nullable int64-key tables: the chunks are ranges of the join's
     own first radix pass (join.radix.first_pass_chunks; per chunk only the second pass + the LDS join,
     into one sink) -- or, with CYLON_RJ_FIRST_PASS_CHUNKS=0, the chunk-major pass.  Both equal the CPU
     twin; a wide side moves in stable column groups."""
     rng = np.random.default_rng(61)
     n = 3_000_000
-    a = pa.table({"k": rng.integers(0, 2_000_000, n), "v": rng.random(n), "x": rng.random(n),
+    ka = rng.integers(0, 2_000_000, n)
+    kb = rng.integers(0, 2_000_000, n)
+    if skew:  # one hot key: its partition outgrows its slot in the second pass (widened, then split items)
+        ka[rng.random(n) < 0.002] = 777  # ~6000 rows against a ~1000-row slot
+        kb[:20] = 777
+    a = pa.table({"k": ka, "v": rng.random(n), "x": rng.random(n),
                   "y": rng.integers(-7, 7, n).astype(np.int32), "z": rng.random(n)})
-    b = pa.table({"k": rng.integers(0, 2_000_000, n), "w": rng.random(n), "i": rng.integers(-5, 5, n)})
+    b = pa.table({"k": kb, "w": rng.random(n), "i": rng.integers(-5, 5, n)})
     gpu_ctx.add_config("memory_budget_mb", "260")
     monkeypatch.setenv("CYLON_RADIX_JOIN_MIN_ROWS", "1024")
     monkeypatch.setenv("CYLON_RJ_FIRST_PASS_CHUNKS", "1" if first_pass else "0")
@@ -615,6 +621,8 @@ def test_radix_join_memory_bounded_first_pass_chunks(gpu_ctx, ctx, monkeypatch, 
     assert c.get("join.radix.memory_chunks", 0) >= 2, c
     assert (c.get("join.radix.first_pass_chunks", 0) >= 2) == first_pass, c
     assert c.get("join.radix.chunk_pass", 0) == (0 if first_pass else 2), c
+    if skew and first_pass:
+        assert c.get("join.radix.slot_overflow", 0) >= 1, c
     assert (L.row_count, R.row_count) == (0, 0)
     assert len(got) == len(exp)
     pd.testing.assert_frame_equal(_canon(got), _canon(exp), check_dtype=False)
