@@ -341,21 +341,27 @@ struct alignas(16) QKV {  // one row of a partition in LDS: group key, value ima
   uint64_t v;
 };
 
-// lane ^ j exchange of a 64-bit value: ds_swizzle (bit mode, xor mask j within 32-lane halves; no
-// address VGPR) for j <= 16, ds_bpermute (__shfl_xor) across the halves for j = 32.  j is a constant
-// after the bitonic loops unroll.
+// lane ^ j exchange of a 64-bit value: DPP lane permutes (VALU source modifiers, no LDS round trip)
+// where one exists -- quad_perm [1,0,3,2] / [2,3,0,1] for j = 1 / 2, row_ror:8 for j = 8 --, ds_swizzle
+// (bit mode, xor mask j within 32-lane halves; no address VGPR) for j = 4, 16, ds_bpermute (__shfl_xor)
+// across the halves for j = 32.  j is a constant after the bitonic loops unroll; every lane of the wave
+// is active in the sorts (pads fill the bucket), so no DPP source lane is disabled.
 template <int J>
 __device__ __forceinline__ uint32_t q_swz(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (J << 10) | 0x1F);
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t q_dpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
 }
 __device__ __forceinline__ uint64_t q_xor64(uint64_t v, int j) {
   const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
   uint32_t a, b;
   switch (j) {
-    case 1: a = q_swz<1>(lo); b = q_swz<1>(hi); break;
-    case 2: a = q_swz<2>(lo); b = q_swz<2>(hi); break;
+    case 1: a = q_dpp<0xB1>(lo); b = q_dpp<0xB1>(hi); break;    // quad_perm [1,0,3,2]
+    case 2: a = q_dpp<0x4E>(lo); b = q_dpp<0x4E>(hi); break;    // quad_perm [2,3,0,1]
     case 4: a = q_swz<4>(lo); b = q_swz<4>(hi); break;
-    case 8: a = q_swz<8>(lo); b = q_swz<8>(hi); break;
+    case 8: a = q_dpp<0x128>(lo); b = q_dpp<0x128>(hi); break;  // row_ror:8 = lane ^ 8 in a row
     case 16: a = q_swz<16>(lo); b = q_swz<16>(hi); break;
     default: return (uint64_t)__shfl_xor((unsigned long long)v, j);
   }
@@ -410,42 +416,6 @@ __device__ __forceinline__ void q_wave_bitonic(int64_t (&k)[S], uint64_t (&v)[S]
   }
 }
 
-// The single-group case of q_wave_bitonic (every row of the bucket has the same key -- nearly every
-// bucket): values only, one 64-bit compare and two shuffles per element and stage instead of two
-// compares and four shuffles.
-template <int S>
-__device__ __forceinline__ void q_wave_bitonic_v(uint64_t (&v)[S]) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int kk = 2; kk <= 64 * S; kk <<= 1) {
-#pragma unroll
-    for (int j = kk >> 1; j > 0; j >>= 1) {
-      if (j >= 64) {
-        const int js = j >> 6;
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-          if (s & js) continue;
-          const int t = s | js;
-          const bool asc = ((s * 64 + lane) & kk) == 0;
-          if ((v[t] < v[s]) == asc) {
-            const uint64_t tv = v[s];
-            v[s] = v[t];
-            v[t] = tv;
-          }
-        }
-      } else {
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-          const uint64_t ov = q_xor64(v[s], j);
-          const bool asc = ((s * 64 + lane) & kk) == 0, lower = (lane & j) == 0;
-          const uint64_t lo = ov < v[s] ? ov : v[s], hi = ov < v[s] ? v[s] : ov;
-          v[s] = lower == asc ? lo : hi;
-        }
-      }
-    }
-  }
-}
-
 // Output of one group (a writer row): its slot comes from the partition's LDS counter, so the
 // groups of a partition come out in no fixed order (group-by order is unspecified).  FUSE: the
 // valid values' sum, count, min and max go to the four fz planes at the same slot.
@@ -465,7 +435,74 @@ __device__ __forceinline__ void q_emit(unsigned int *nout, int64_t *okeys, uint6
   }
 }
 
-// One wave ranks one bucket of sz <= 64 * S rows (slots [e0, e0 + sz) of skv): sort by (key, value)
+// Wave-uniform copy of a value every lane holds (readfirstlane of both halves): keeps the select's
+// loop counters and branches scalar.
+__device__ __forceinline__ uint64_t q_uniform64(uint64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+// One word (W = 1: high 32 bits, 0: low) of the wave radix select below: per bit, the candidates
+// with a 0 there (a ballot per slot) keep the order statistic if more than k of them remain, else
+// the 1s do with k reduced; stops once one candidate is left.  Bits, counts and masks are scalar.
+template <int S, int W>
+__device__ __forceinline__ void q_select_word(const uint64_t (&v)[S], uint64_t (&A)[S], uint32_t &k, uint32_t &na,
+                                              int top) {
+  for (int bit = top; bit >= 0 && na > 1; --bit) {
+    const uint32_t m = 1u << bit;
+    uint64_t z[S];
+    uint32_t c = 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const uint32_t w = W ? (uint32_t)(v[s] >> 32) : (uint32_t)v[s];
+      z[s] = __ballot((w & m) == 0u) & A[s];
+      c += (uint32_t)__popcll(z[s]);
+    }
+    if (k < c) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) A[s] = z[s];
+      na = c;
+    } else {
+#pragma unroll
+      for (int s = 0; s < S; ++s) A[s] &= ~z[s];
+      k -= c;
+      na -= c;
+    }
+  }
+}
+
+// The k-th smallest (0-based, k < nv) of the wave's valid values (v != the null image ~0; pads are
+// ~0 too) by an MSB-first radix select over ballots, starting at hb, the highest bit in which the
+// valid values' min and max differ (every valid value shares the bits above it).  Replaces the
+// bitonic sort of a single-key bucket: ~10-20 scalar-heavy bit steps instead of 28 exchange stages.
+template <int S>
+__device__ __forceinline__ uint64_t q_wave_select(const uint64_t (&v)[S], uint32_t k, uint32_t nv, int hb) {
+  uint64_t A[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) A[s] = __ballot(v[s] != ~0ull);
+  uint32_t na = nv;
+  if (hb >= 32) q_select_word<S, 1>(v, A, k, na, hb - 32);
+  q_select_word<S, 0>(v, A, k, na, hb >= 32 ? 31 : hb);
+  // one candidate left, or several equal ones (all bits from hb down decided): the first of them
+  uint64_t r = 0;
+  bool found = false;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (!found && A[s] != 0ull) {
+      const int l = __builtin_ctzll(A[s]);
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v[s], l);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v[s] >> 32), l);
+      r = (uint64_t)lo | ((uint64_t)hi << 32);
+      found = true;
+    }
+  }
+  return r;
+}
+
+// One wave ranks one bucket of sz <= 64 * S rows (slots [e0, e0 + sz) of skv).  A bucket of one key
+// (nearly all) takes its order statistics by q_wave_select, min / max / sum by wave reductions, and
+// lane 0 emits it.  Otherwise: sort by (key, value)
 // -- pads (the bucket's largest key, the null image) sort after every real row and tie only with
 // that key's null rows, whose content they share -- then each group's rows are contiguous with its
 // valid values first in value order, so the type-2 position is index arithmetic.  The sorted rows go
@@ -505,37 +542,64 @@ __device__ __forceinline__ void q_rank_bucket(QKV *skv, int e0, int sz, double q
       k[s] = kmax;
       v[s] = ~0ull;
     }
-  if (kmin == kmax) {  // one group: sort the values only; valid values first, nulls and pads after
-    q_wave_bitonic_v<S>(v);
-    int nv = 0;
+  if (kmin == kmax) {  // one group (nearly every bucket): order statistics by a wave radix select
+    uint32_t nv = 0;
     double sum = 0.0;
+    uint64_t mn = ~0ull, mx = 0;  // smallest / largest valid image (every valid image is > 0)
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const bool ok = v[s] != ~0ull;
-      nv += __popcll(__ballot(ok));
+      nv += (uint32_t)__popcll(__ballot(ok));
       if constexpr (FUSE) sum += ok ? q_unimage(v[s]) : 0.0;
-    }
-    if constexpr (FUSE) {
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-    }
-#pragma unroll
-    for (int s = 0; s < S; ++s)
-      if (s * 64 + lane < sz) skv[e0 + s * 64 + lane] = QKV{kmax, v[s]};
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {  // the group's row
-      if (nv == 0) {
-        q_emit<FUSE>(nout, okeys, oq, ovalid, fz, n, b, kmax, false, 0.0, 0.0, 0, 0.0, 0.0);
-      } else {
-        const double np = (double)nv * q, jf = floor(np);
-        const bool whole = np == jf;
-        int pos = (int)jf;
-        if (pos >= nv) pos = nv - 1;
-        const double at = q_unimage(skv[e0 + pos].v);
-        const double qv = (whole && pos > 0) ? 0.5 * (q_unimage(skv[e0 + pos - 1].v) + at) : at;
-        q_emit<FUSE>(nout, okeys, oq, ovalid, fz, n, b, kmax, true, qv, sum, nv, q_unimage(skv[e0].v),
-                     q_unimage(skv[e0 + nv - 1].v));
+      if (ok) {
+        mn = v[s] < mn ? v[s] : mn;
+        mx = v[s] > mx ? v[s] : mx;
       }
+    }
+#pragma unroll
+    for (int j = 1; j < 64; j <<= 1) {
+      const uint64_t a = q_xor64(mn, j), c = q_xor64(mx, j);
+      mn = a < mn ? a : mn;
+      mx = c > mx ? c : mx;
+      if constexpr (FUSE) sum += __shfl_xor(sum, j);
+    }
+    if (nv == 0) {
+      if (lane == 0) q_emit<FUSE>(nout, okeys, oq, ovalid, fz, n, b, kmax, false, 0.0, 0.0, 0, 0.0, 0.0);
+      return;
+    }
+    mn = q_uniform64(mn);
+    mx = q_uniform64(mx);
+    const double np = (double)nv * q, jf = floor(np);
+    const bool whole = np == jf;
+    int pos = (int)jf;
+    if (pos >= (int)nv) pos = (int)nv - 1;
+    pos = __builtin_amdgcn_readfirstlane(pos);
+    uint64_t at = mn, below = mn;
+    if (mn != mx) {
+      at = q_wave_select<S>(v, (uint32_t)pos, nv, 63 - __builtin_clzll(mn ^ mx));
+      below = at;
+      if (whole && pos > 0) {  // the (pos - 1)-th: the largest value below `at`, unless `at` repeats
+        uint32_t cl = 0;
+        uint64_t bm = 0;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const bool lt = v[s] < at;  // (nulls and pads, ~0, never are)
+          cl += (uint32_t)__popcll(__ballot(lt));
+          if (lt) bm = v[s] > bm ? v[s] : bm;
+        }
+        if (cl >= (uint32_t)pos) {
+#pragma unroll
+          for (int j = 1; j < 64; j <<= 1) {
+            const uint64_t a = q_xor64(bm, j);
+            bm = a > bm ? a : bm;
+          }
+          below = q_uniform64(bm);
+        }
+      }
+    }
+    if (lane == 0) {  // the group's row
+      const double qv = (whole && pos > 0) ? 0.5 * (q_unimage(below) + q_unimage(at)) : q_unimage(at);
+      q_emit<FUSE>(nout, okeys, oq, ovalid, fz, n, b, kmax, true, qv, sum, (int64_t)nv, q_unimage(mn), q_unimage(mx));
     }
     return;
   }
@@ -632,6 +696,7 @@ __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(4))) 
   __shared__ uint32_t wsum[kQThreads / kWave];
   __shared__ unsigned int s_nout;       // groups emitted by this partition
   __shared__ uint16_t sbl[kQBuckets];   // the partition's buckets of <= kQWaveRows rows, compacted
+  __shared__ int s_big;                 // the partition has a bucket of > kQWaveRows rows
   const int shift = 64 - bits - kQBBits;  // bucket bits just below the partition bits
   auto bucket_of = [&](int64_t k) -> uint32_t {
     const uint64_t h = hashing::fmix64((uint64_t)k);
@@ -647,21 +712,58 @@ __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       continue;
     }
     for (int i = threadIdx.x; i < kQBuckets; i += kQThreads) bcnt[i] = 0;
-    if (threadIdx.x == 0) s_nout = 0;
+    if (threadIdx.x == 0) {
+      s_nout = 0;
+      s_big = 0;
+    }
     __syncthreads();
     uint32_t rbk[kQPer];  // bucket << 16 | slot in the bucket (~0: no row)
 #pragma unroll
-    for (int u = 0; u < kQPer; ++u) {
-      const int i = u * kQThreads + threadIdx.x;
-      rbk[u] = 0xffffffffu;
-      if (i < cnt) {
-        const int64_t kk = keys[b + i];
-        const uint64_t vv = (valid == nullptr || valid[b + i])
-                                ? q_image(rg_double(load_bits(vals, b + i, vwidth), vwidth, vkind))
-                                : ~0ull;
-        skv[i] = QKV{kk, vv};
-        const uint32_t bk = bucket_of(kk);
-        rbk[u] = bk << 16 | atomicAdd(&bcnt[bk], 1u);
+    for (int u = 0; u < kQPer; ++u) rbk[u] = 0xffffffffu;
+    if (vwidth == 8) {
+      // 8-byte values (float64 / int64): two rows per thread per batch, every key, value and
+      // validity load of the batch issued before any is used (the value is loaded whether or not
+      // the row is null), so a typical partition (<= 1024 rows) costs one HBM latency, not a
+      // chain of dependent ones per row round
+      const uint64_t *v8 = reinterpret_cast<const uint64_t *>(vals);
+#pragma unroll
+      for (int u0 = 0; u0 < kQPer; u0 += 2) {
+        int64_t kk[2];
+        uint64_t raw[2];
+        bool ok[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int i = (u0 + t) * kQThreads + threadIdx.x;
+          if (i < cnt) {
+            kk[t] = keys[b + i];
+            raw[t] = v8[b + i];
+            ok[t] = valid == nullptr || valid[b + i];
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int i = (u0 + t) * kQThreads + threadIdx.x;
+          if (i < cnt) {
+            skv[i] = QKV{kk[t], ok[t] ? q_image(rg_double(raw[t], 8, vkind)) : ~0ull};
+            const uint32_t bk = bucket_of(kk[t]);
+            rbk[u0 + t] = bk << 16 | atomicAdd(&bcnt[bk], 1u);
+          }
+        }
+        if ((u0 + 2) * kQThreads >= cnt) break;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kQPer; ++u) {
+        const int i = u * kQThreads + threadIdx.x;
+        if (i < cnt) {
+          const int64_t kk = keys[b + i];
+          const uint64_t vv = (valid == nullptr || valid[b + i])
+                                  ? q_image(rg_double(load_bits(vals, b + i, vwidth), vwidth, vkind))
+                                  : ~0ull;
+          skv[i] = QKV{kk, vv};
+          const uint32_t bk = bucket_of(kk);
+          rbk[u] = bk << 16 | atomicAdd(&bcnt[bk], 1u);
+        }
       }
     }
     __syncthreads();
@@ -701,14 +803,17 @@ __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       constexpr int PER = kQBuckets / (kQThreads / kWave);  // buckets a wave lists
       uint64_t mk[PER / kWave];
       uint32_t mine = 0;
+      bool big = false;
 #pragma unroll
       for (int c = 0; c < PER / kWave; ++c) {
         const int bk = wave * PER + c * kWave + lane;
         const int szl = (bk + 1 < kQBuckets ? (int)bcnt[bk + 1] : (int)cnt) - (int)bcnt[bk];
         mk[c] = __ballot(szl > 0 && szl <= kQWaveRows);
         mine += (uint32_t)__popcll(mk[c]);
+        big |= szl > kQWaveRows;
       }
       if (lane == 0) wsum[wave] = mine;
+      if (big) s_big = 1;
       __syncthreads();
       uint32_t at = 0, tot = 0;
 #pragma unroll
@@ -730,9 +835,10 @@ __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       }
     }
     // rows of larger buckets (never touched by the wave phase): every row counts its rank over its
-    // bucket; the row at the type-2 position emits the group
+    // bucket; the row at the type-2 position emits the group.  Skipped (block-uniform s_big, written
+    // before the listing's barriers) when the partition has none -- nearly always.
 #pragma unroll 1
-    for (int u = 0; u < kQPer; ++u) {
+    for (int u = 0; u < (s_big ? kQPer : 0); ++u) {
       const int i = u * kQThreads + threadIdx.x;  // slot in bucket order
       if (i >= cnt) break;
       const QKV me = skv[i];
