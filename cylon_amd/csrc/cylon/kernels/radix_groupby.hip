@@ -515,7 +515,6 @@ __device__ __forceinline__ void q_rank_bucket(QKV *skv, int e0, int sz, double q
   const int lane = lane_id();
   int64_t k[S];
   uint64_t v[S];
-  int64_t kmax = INT64_MIN;
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int e = s * 64 + lane;
@@ -523,26 +522,19 @@ __device__ __forceinline__ void q_rank_bucket(QKV *skv, int e0, int sz, double q
       const QKV r = skv[e0 + e];
       k[s] = r.k;
       v[s] = r.v;
-      kmax = r.k > kmax ? r.k : kmax;
     }
   }
-  int64_t kmin = INT64_MAX;
+  // one key?  Row 0 always exists (sz >= 1): one compare per row and a ballot against its key
+  const int64_t k0 = (int64_t)q_uniform64((uint64_t)k[0]);
+  bool other = false;
 #pragma unroll
   for (int s = 0; s < S; ++s)
-    if (s * 64 + lane < sz) kmin = k[s] < kmin ? k[s] : kmin;
+    if (s * 64 + lane < sz) other |= k[s] != k0;
+  if (__ballot(other) == 0ull) {  // one group (nearly every bucket): order statistics by a wave radix select
+    const int64_t kmax = k0;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const int64_t x = __shfl_xor((long long)kmax, o), y = __shfl_xor((long long)kmin, o);
-    kmax = x > kmax ? x : kmax;
-    kmin = y < kmin ? y : kmin;
-  }
-#pragma unroll
-  for (int s = 0; s < S; ++s)
-    if (s * 64 + lane >= sz) {
-      k[s] = kmax;
-      v[s] = ~0ull;
-    }
-  if (kmin == kmax) {  // one group (nearly every bucket): order statistics by a wave radix select
+    for (int s = 0; s < S; ++s)
+      if (s * 64 + lane >= sz) v[s] = ~0ull;
     uint32_t nv = 0;
     double sum = 0.0;
     uint64_t mn = ~0ull, mx = 0;  // smallest / largest valid image (every valid image is > 0)
@@ -561,7 +553,7 @@ __device__ __forceinline__ void q_rank_bucket(QKV *skv, int e0, int sz, double q
       const uint64_t a = q_xor64(mn, j), c = q_xor64(mx, j);
       mn = a < mn ? a : mn;
       mx = c > mx ? c : mx;
-      if constexpr (FUSE) sum += __shfl_xor(sum, j);
+      if constexpr (FUSE) sum += __longlong_as_double((long long)q_xor64((uint64_t)__double_as_longlong(sum), j));
     }
     if (nv == 0) {
       if (lane == 0) q_emit<FUSE>(nout, okeys, oq, ovalid, fz, n, b, kmax, false, 0.0, 0.0, 0, 0.0, 0.0);
@@ -603,6 +595,21 @@ __device__ __forceinline__ void q_rank_bucket(QKV *skv, int e0, int sz, double q
     }
     return;
   }
+  int64_t kmax = INT64_MIN;  // pads take the bucket's largest key
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    if (s * 64 + lane < sz) kmax = k[s] > kmax ? k[s] : kmax;
+#pragma unroll
+  for (int j = 1; j < 64; j <<= 1) {
+    const int64_t x = (int64_t)q_xor64((uint64_t)kmax, j);
+    kmax = x > kmax ? x : kmax;
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    if (s * 64 + lane >= sz) {
+      k[s] = kmax;
+      v[s] = ~0ull;
+    }
   q_wave_bitonic<S>(k, v);
   bool head[S], last_valid[S];
   int start[S];
@@ -697,10 +704,13 @@ __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(4))) 
   __shared__ unsigned int s_nout;       // groups emitted by this partition
   __shared__ uint16_t sbl[kQBuckets];   // the partition's buckets of <= kQWaveRows rows, compacted
   __shared__ int s_big;                 // the partition has a bucket of > kQWaveRows rows
-  const int shift = 64 - bits - kQBBits;  // bucket bits just below the partition bits
-  auto bucket_of = [&](int64_t k) -> uint32_t {
-    const uint64_t h = hashing::fmix64((uint64_t)k);
-    return shift >= 0 ? (uint32_t)(h >> shift) & (kQBuckets - 1) : (uint32_t)h & (kQBuckets - 1);
+  // bucket of a key inside its partition: a Fibonacci hash of the key's folded halves (one 32-bit
+  // multiply, not a second fmix64 per row; the partition itself came from the fmix64 bits, so the
+  // two are independent).  Keys that share a bucket take the mixed (key, value) path, still exact.
+  (void)bits;
+  auto bucket_of = [](int64_t k) -> uint32_t {
+    const uint32_t f = (uint32_t)(uint64_t)k ^ (uint32_t)((uint64_t)k >> 32);
+    return (f * 0x9E3779B1u) >> (32 - kQBBits);
   };
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
     const int64_t b = offs[p], cnt = offs[p + 1] - b;
