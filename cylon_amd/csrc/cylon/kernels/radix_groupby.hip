@@ -294,18 +294,18 @@ __global__ void k_rg_pack(const int64_t *__restrict__ offs, const int64_t *__res
 
 // ---- QUANTILE on the radix path.  The rows (group key, value) are partitioned
 // by the group key's hash into partitions of <= kQCap rows (whole groups); one workgroup per
-// partition then SELECTS each group's order statistics instead of sorting:
-//   1. each thread holds 8 rows in registers; the next kQBBits bits of fmix64(key) (below the
-//      partition bits) pick a local bucket: LDS atomics count them and give each row its slot in
-//      the bucket, a block scan places the buckets, and the rows land in LDS in bucket order -- a
-//      bucket holds one group (rarely a few: ~10 groups per partition over 2048 buckets);
-//   2. every row ranks itself inside its group by one pass over its bucket -- rank = rows of the
-//      same key with a smaller (value, slot), nv = the group's valid values -- lanes of one bucket
-//      read the same LDS words (broadcasts);
-//   3. the row whose rank is the type-2 position (global path k_quantile: np = nv q, j = floor(np),
-//      pos = min(j, nv - 1), the mean with rank pos - 1 when np is whole) writes the group, the
-//      group's first row when every value is null; a block scan of those writers gives the slab
-//      slots (groups <= rows, as k_rg_agg) and radix_groupby_pack packs the slabs.
+// partition then takes each group's order statistics:
+//   1. the partition's rows are read once from HBM into LDS; a Fibonacci hash of the key picks one
+//      of kQBuckets local buckets (LDS atomics count them, a block scan places them) and the rows
+//      are moved to bucket order inside LDS -- a bucket holds one group (rarely a few: ~10 groups
+//      per partition);
+//   2. the non-empty buckets of <= kQWaveRows rows are dealt round-robin to the block's waves: a
+//      one-key bucket takes the type-2 order statistics by a wave radix select over ballots
+//      (q_wave_select), a mixed bucket is sorted by (key, value) in registers (q_wave_bitonic);
+//      rows of larger buckets count their rank over the bucket;
+//   3. the type-2 position (global path k_quantile: np = nv q, j = floor(np), pos = min(j, nv - 1),
+//      the mean with the (pos - 1)-th when np is whole) is written per group at a slot from an LDS
+//      counter (gcount per partition; radix_groupby_pack packs the slabs).
 // Nulls rank after every value (excluded, as the global path does).  Values compare as
 // order-preserving images of their doubles (NaN canonicalised).
 constexpr int kQCap = 4096, kQThreads = 512, kQPer = kQCap / kQThreads, kQBBits = 11, kQBuckets = 1 << kQBBits;
