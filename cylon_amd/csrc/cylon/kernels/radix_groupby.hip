@@ -712,21 +712,23 @@ __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     const uint32_t f = (uint32_t)(uint64_t)k ^ (uint32_t)((uint64_t)k >> 32);
     return (f * 0x9E3779B1u) >> (32 - kQBBits);
   };
+  // the bucket counters and flags start zeroed; every partition zeroes them again for the next one
+  // before its trailing barrier (no barrier of its own for the reset)
+  for (int i = threadIdx.x; i < kQBuckets; i += kQThreads) bcnt[i] = 0;
+  if (threadIdx.x == 0) {
+    s_nout = 0;
+    s_big = 0;
+  }
+  __syncthreads();
   for (int64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
     const int64_t b = offs[p], cnt = offs[p + 1] - b;
-    if (cnt > kQCap) {
+    if (cnt > kQCap) {  // (block-uniform: the LDS state stays zeroed)
       if (threadIdx.x == 0) {
         atomicOr(overflow, 1);
         gcount[p] = 0;
       }
       continue;
     }
-    for (int i = threadIdx.x; i < kQBuckets; i += kQThreads) bcnt[i] = 0;
-    if (threadIdx.x == 0) {
-      s_nout = 0;
-      s_big = 0;
-    }
-    __syncthreads();
     uint32_t rbk[kQPer];  // bucket << 16 | slot in the bucket (~0: no row)
 #pragma unroll
     for (int u = 0; u < kQPer; ++u) rbk[u] = 0xffffffffu;
@@ -900,9 +902,14 @@ __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       const double qv = (whole && pos > 0) ? 0.5 * (q_unimage(below) + q_unimage(v)) : q_unimage(v);
       q_emit<FUSE>(&s_nout, okeys, oq, ovalid, fz, n, b, k, true, qv, gsum, nv, q_unimage(gmin), q_unimage(gmax));
     }
-    __syncthreads();
-    if (threadIdx.x == 0) gcount[p] = s_nout;
-    __syncthreads();  // (s_nout and skv are reused by the next partition)
+    __syncthreads();  // every read of bcnt / skv / s_nout of this partition is done
+    for (int i = threadIdx.x; i < kQBuckets; i += kQThreads) bcnt[i] = 0;
+    if (threadIdx.x == 0) {
+      gcount[p] = s_nout;
+      s_nout = 0;
+      s_big = 0;
+    }
+    __syncthreads();  // (zeroed state and skv reused by the next partition)
   }
 }
 

@@ -382,7 +382,15 @@ def test_radix_groupby_quantile(gpu_ctx, monkeypatch, case):
     # SUM / COUNT / MEAN / MIN / MAX of the quantile's own float64 column come from the quantile kernel
     fused = {"sum_q25_nullable": 1, "two_keys_q90": 1, "mixed_group_sizes": 5}.get(case, 0)
     assert cnt[0].get("groupby.radix.quantile_fused_aggs", 0) == fused, cnt[0]
-    pd.testing.assert_frame_equal(res[0], res[1], check_exact=False, rtol=1e-12, atol=1e-12)
+    # quantiles, min / max / count are order statistics and counts: equal to 1e-12.  Sums and means
+    # add a group's values in an order that differs between the paths (and, for groups counted by
+    # LDS atomics, between runs): ~230 values of magnitude <= ~500 that cancel to ~0.4 can differ by
+    # a few 1e-12 absolute, so those columns get an absolute tolerance of 1e-8
+    summed = [c for c in res[0].columns if c.startswith(("sum_", "mean_"))]
+    pd.testing.assert_frame_equal(res[0].drop(columns=summed), res[1].drop(columns=summed), check_exact=False,
+                                  rtol=1e-12, atol=1e-12)
+    if summed:
+        pd.testing.assert_frame_equal(res[0][summed], res[1][summed], check_exact=False, rtol=1e-12, atol=1e-8)
 
 
 @pytest.mark.parametrize("case", ["with_sum", "alone", "two_keys"])
